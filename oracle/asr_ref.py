@@ -1,0 +1,236 @@
+"""torch-CPU restatement of the hybrid CTC/attention training math (oracle; test infra only).
+
+Pure functions over a parameter dict keyed by the REFERENCE's state_dict names,
+so fixtures recorded from the reference load directly.  Gradients come from
+torch autograd on CPU.  Every function cites the reference lines it restates.
+Nothing here is imported by the product package.
+"""
+import numpy as np
+import torch
+
+from . import ctc_ref
+
+
+# ---------------------------------------------------------------------------
+# LSTM direction with packed-sequence semantics (rnn.py:166-172, 218-224, 343-390)
+# ---------------------------------------------------------------------------
+def lstm_direction(x, lens, w_ih, w_hh, b_ih, b_hh, reverse):
+    """x: [B, T, Din] (sorted desc by lens).  Gate order i, f, g, o; h0 = c0 = 0
+    (rnn.py:499-536).  The reverse direction starts at each utterance's own last
+    frame; outputs beyond the length are zero (pack/pad_packed semantics)."""
+    B, T, _ = x.shape
+    H = w_hh.shape[1]
+    gx = torch.matmul(x, w_ih.t()) + b_ih + b_hh            # [B, T, 4H]
+    h = x.new_zeros(B, H)
+    c = x.new_zeros(B, H)
+    outs = [None] * T
+    lens_t = torch.as_tensor(np.asarray(lens), dtype=torch.long)
+    order = range(T - 1, -1, -1) if reverse else range(T)
+    for t in order:
+        g = gx[:, t] + h @ w_hh.t()
+        i, f, gg, o = g.split(H, dim=1)
+        c_new = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(gg)
+        h_new = torch.sigmoid(o) * torch.tanh(c_new)
+        act = (lens_t > t).to(x.dtype).unsqueeze(1)
+        h = h_new * act
+        c = c_new * act
+        outs[t] = h
+    return torch.stack(outs, dim=1)
+
+
+def blstm_encoder(p, prefix, cfg, xs, x_lens):
+    """RNNEncoder.forward (rnn.py:284-487) for rnn_type='lstm', bidirectional,
+    subsample_type 'drop', no projection / residual / conv (dropout = 0).
+
+    Returns (out [B, T', 2H], out_lens np.int32 [B], perm np.int64 [B])."""
+    x_lens = np.asarray(x_lens)
+    perm = np.argsort(-x_lens, kind='stable')                 # rnn.py:319-326
+    xs = xs[torch.as_tensor(perm)]
+    lens = x_lens[perm].astype(np.int64)
+    n_layers = cfg['num_layers']
+    sub = cfg.get('subsample_list') or [False] * n_layers
+    fast = sum(sub) == 0
+    for l in range(n_layers):
+        if fast:   # one multi-layer nn.LSTM: lstm.weight_ih_l{l}{_reverse}
+            names = [prefix + 'lstm.%s_l%d%s' % (n, l, s) for s in ('', '_reverse')
+                     for n in ('weight_ih', 'weight_hh', 'bias_ih', 'bias_hh')]
+        else:      # per-layer nn.LSTM: lstm_l{l}.weight_ih_l0{_reverse}
+            names = [prefix + 'lstm_l%d.%s_l0%s' % (l, n, s) for s in ('', '_reverse')
+                     for n in ('weight_ih', 'weight_hh', 'bias_ih', 'bias_hh')]
+        T_out = int(lens.max())                              # pad_packed -> max len
+        xs = xs[:, :T_out]
+        fw = lstm_direction(xs, lens, *[p[n] for n in names[:4]], reverse=False)
+        bw = lstm_direction(xs, lens, *[p[n] for n in names[4:]], reverse=True)
+        xs = torch.cat([fw, bw], dim=2)
+        if not fast and l != n_layers - 1 and sub[l]:
+            xs = xs[:, 1::2]                                  # rnn.py:415-419
+            lens = np.full(len(lens), xs.shape[1], np.int64)  # quirk rnn.py:435-439
+    return xs, lens.astype(np.int32), perm.astype(np.int64)
+
+
+def linear_nd(p, name, x):
+    """LinearND (linear.py:32-47): affine on the last dim (dropout = 0)."""
+    y = torch.matmul(x, p[name + '.fc.weight'].t())
+    b = p.get(name + '.fc.bias')
+    return y if b is None else y + b
+
+
+# ---------------------------------------------------------------------------
+# CTC (warp-ctc contract, ctc.py:30-66) as an autograd function over float64
+# ---------------------------------------------------------------------------
+class _CTCOracle(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels_flat, label_lens, act_lens):
+        costs, grads = ctc_ref.ctc_batch(logits.detach().numpy(), labels_flat, label_lens,
+                                         act_lens, time_major=False)
+        ctx.save_for_backward(torch.from_numpy(grads).to(logits.dtype))
+        return torch.tensor(costs.sum(), dtype=logits.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        grads, = ctx.saved_tensors
+        return grads * g, None, None, None
+
+
+def ctc_sum(logits, labels_flat, label_lens, act_lens):
+    return _CTCOracle.apply(logits, labels_flat, label_lens, act_lens)
+
+
+def _concat_labels(ys, y_lens):
+    """_concatenate_labels (ctc.py:532-549)."""
+    return np.concatenate([ys[b, :y_lens[b]] for b in range(len(y_lens))]).astype(np.int64)
+
+
+def ls_xent(logits, lens, ls_prob, size_average):
+    """cross_entropy_label_smoothing (criterion.py:51-80)."""
+    B, _, V = logits.shape
+    lp = torch.log_softmax(logits, dim=-1)
+    tot = sum((-(ls_prob / V) * lp[b, :int(lens[b])]).sum() for b in range(B))
+    return tot / B if size_average else tot
+
+
+def ctc_model_loss(p, cfg, xs, ys, x_lens, y_lens):
+    """CTC.forward (ctc.py:272-342).  xs numpy [B,T,F]; ys numpy [B,L] pad -1."""
+    xs_t = torch.from_numpy(np.asarray(xs, np.float32))
+    out, out_lens, perm = blstm_encoder(p, 'encoder.', cfg, xs_t, x_lens)
+    h = out
+    for i in range(len(cfg.get('fc_list', []))):
+        h = linear_nd(p, 'fc_%d' % i, h)
+    logits = linear_nd(p, 'fc_out', h)
+    if cfg.get('logits_temperature', 1) != 1:
+        logits = logits / cfg['logits_temperature']
+    ys_s = (np.asarray(ys) + 1)[perm]                       # ctc.py:300,310-312
+    yl_s = np.asarray(y_lens)[perm]
+    B = xs.shape[0]
+    loss = ctc_sum(logits, _concat_labels(ys_s, yl_s), yl_s, out_lens) / B
+    ls = cfg.get('label_smoothing_prob', 0)
+    if ls > 0:
+        loss = loss * (1 - ls) + ls_xent(logits, out_lens, ls, False) / B
+    return loss, logits, out_lens, perm
+
+
+# ---------------------------------------------------------------------------
+# Location attention (attention_layer.py:74-98, 155-177, 214-251)
+# ---------------------------------------------------------------------------
+def location_attention(p, prefix, enc_out, enc_out_a, x_lens, dec_out, aw_prev,
+                       sharpening=1.0, sigmoid_smoothing=False):
+    """enc_out [B,T,E], enc_out_a [B,T,A], dec_out [B,D], aw_prev [B,T].
+    Returns ctx [B,E], aw [B,T]."""
+    B, T, _ = enc_out.shape
+    w = p[prefix + 'conv_head0.weight']                      # [C, 1, 1, K]
+    C, K = w.shape[0], w.shape[3]
+    f = torch.nn.functional.conv1d(aw_prev.unsqueeze(1), w.view(C, 1, K), padding=K // 2)
+    f = f.transpose(1, 2)                                    # [B, T, C]
+    pre = (enc_out_a + (dec_out @ p[prefix + 'W_dec_head0.fc.weight'].t()).unsqueeze(1)
+           + f @ p[prefix + 'W_conv_head0.fc.weight'].t())
+    e = (torch.tanh(pre) @ p[prefix + 'V_head0.fc.weight'].t()).squeeze(2)
+    mask = (torch.arange(T).unsqueeze(0) < torch.as_tensor(np.asarray(x_lens)).unsqueeze(1))
+    e = e * mask.to(e.dtype)                                 # multiplicative mask :216-225
+    e = e * sharpening
+    aw = torch.sigmoid(e) if sigmoid_smoothing else torch.softmax(e, dim=-1)
+    ctx = (enc_out * aw.unsqueeze(2)).sum(1)
+    return ctx, aw
+
+
+def lstm_cell(p, name, x, h, c):
+    """nn.LSTMCell (rnn_decoder.py:48,84-88)."""
+    g = (x @ p[name + '.weight_ih'].t() + p[name + '.bias_ih']
+         + h @ p[name + '.weight_hh'].t() + p[name + '.bias_hh'])
+    H = h.shape[1]
+    i, f, gg, o = g.split(H, dim=1)
+    c = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(gg)
+    return torch.sigmoid(o) * torch.tanh(c), c
+
+
+def attention_model_loss(p, cfg, xs, ys, x_lens, y_lens):
+    """AttentionSeq2seq.forward (attention_seq2seq.py:422-562) for the
+    bahdanau order, location attention, 1 head, LSTM decoder, forward
+    direction only (backward_loss_weight = 0), ss_prob = 0, dropout = 0."""
+    xs_t = torch.from_numpy(np.asarray(xs, np.float32))
+    enc_cfg = dict(num_layers=cfg['encoder_num_layers'], subsample_list=cfg['subsample_list'])
+    enc_out, enc_lens, perm = blstm_encoder(p, 'encoder.', enc_cfg, xs_t, x_lens)
+    B, T, E = enc_out.shape
+    V = cfg['num_classes'] + 1
+    eos = cfg['num_classes']
+    ys = np.asarray(ys)
+    y_lens = np.asarray(y_lens)
+    Lp = ys.shape[1]
+    ys_in = np.full((B, Lp + 1), eos, np.int64)              # :458-473
+    ys_out = np.full((B, Lp + 1), -1, np.int64)
+    for b in range(B):
+        ys_in[b, 1:y_lens[b] + 1] = ys[b, :y_lens[b]]
+        ys_out[b, :y_lens[b]] = ys[b, :y_lens[b]]
+        ys_out[b, y_lens[b]] = eos
+    ys_in, ys_out, yl = ys_in[perm], ys_out[perm], y_lens[perm]
+
+    D = cfg['decoder_num_units']
+    pre = 'attend_0_fwd.'
+    enc_out_a = linear_nd(p, pre + 'W_enc_head0', enc_out)  # :735-739
+    init = cfg.get('init_dec_state', 'first')
+    c = enc_out.new_zeros(B, D)
+    if init == 'zero':
+        h = enc_out.new_zeros(B, D)
+    else:                                                    # :831-857
+        src = {'mean': enc_out.mean(1), 'final': enc_out[:, -1], 'first': enc_out[:, 0]}[init]
+        h = torch.tanh(linear_nd(p, 'W_dec_init_0_fwd', src))
+    dec_out = h
+    aw = enc_out.new_zeros(B, T)
+    ctx = enc_out.new_zeros(B, E)
+    if cfg.get('label_smoothing_prob', 0) > 0:               # Embedding_LS (linear.py:80-116)
+        emb_w = p['embed_0.embed.fc.weight'].t()             # [V, emb]
+    else:                                                    # Embedding, padding_idx=-1
+        emb_w = p['embed_0.embed.weight']
+    ys_emb = emb_w[torch.as_tensor(ys_in)]                   # [B, L+1, emb]
+    logits = []
+    for t in range(Lp + 1):                                  # :742-793
+        if t > 0:
+            dec_in = torch.cat([ys_emb[:, t], ctx], dim=-1)
+            h, c = lstm_cell(p, 'decoder_0_fwd.lstm_l0', dec_in, h, c)
+            dec_out = h
+        ctx, aw = location_attention(p, pre, enc_out, enc_out_a, enc_lens, dec_out, aw,
+                                     cfg.get('sharpening_factor', 1),
+                                     cfg.get('sigmoid_smoothing', False))
+        z = torch.tanh(linear_nd(p, 'W_d_0_fwd', dec_out) + linear_nd(p, 'W_c_0_fwd', ctx))
+        logits.append(linear_nd(p, 'fc_0_fwd', z))
+    logits = torch.stack(logits, 1)                          # [B, L+1, V]
+    if cfg.get('logits_temperature', 1) != 1:
+        logits = logits / cfg['logits_temperature']
+    tgt = torch.as_tensor(ys_out.reshape(-1))
+    loss = torch.nn.functional.cross_entropy(logits.reshape(-1, V), tgt, ignore_index=-1,
+                                             reduction='sum') / B
+    ls = cfg.get('label_smoothing_prob', 0)
+    if ls > 0:
+        loss = loss * (1 - ls) + ls_xent(logits, yl + 1, ls, True)
+    loss = loss * (1 - cfg.get('backward_loss_weight', 0))
+    lam = cfg.get('ctc_loss_weight', 0)
+    if lam > 0:                                              # :534-549, :609-653
+        lg = linear_nd(p, 'fc_ctc_0', enc_out)
+        lab = _concat_labels(np.asarray(ys)[perm] + 1, yl)
+        loss = loss + ctc_sum(lg, lab, yl, enc_lens) / B * lam
+    return loss
+
+
+def embedding_padding_row(cfg):
+    """nn.Embedding(padding_idx=-1) in linear.py:63-64 zeroes the gradient of
+    row num_classes (= <sos>/<eos>); the oracle applies it post-backward."""
+    return cfg['num_classes']

@@ -1,0 +1,332 @@
+#!/usr/bin/env python
+"""Generate the golden vectors under tests/golden/ from the REFERENCE itself.
+
+Runs only in the build container (it imports /root/reference, which does not
+exist on the GPU box).  The outputs are small .npz fixtures: inputs, the
+reference's state_dict, and the reference's outputs / gradients.  Nothing from
+the reference's source is stored -- only numbers.
+
+The reference (torch-0.3 era code) needs a few harness-only shims to run on
+torch 2.10 (SURVEY.md §8c "What makes the full hot path run here"):
+
+  1. ``warpctc_pytorch`` is absent (external, unpinned SeanNaren/warp-ctc).  A
+     stand-in module fills ``grads``/``costs`` exactly as warp-ctc's
+     ``cpu_ctc`` contract says (softmax inside, blank 0, per-utterance costs,
+     gradient w.r.t. the UNNORMALISED activations, zero for t >= act_len),
+     computed with torch.nn.functional.ctc_loss in float64.  Infeasible
+     alignments give cost 0 / grad 0 (zero_infinity), the documented choice.
+     Its backward scales by grad_output (chain rule; SURVEY §8c decision).
+  2. ``torch.nn.modules.loss._assert_no_grad`` is restored as a no-op.
+  3. ``AttentionMechanism.forward`` and ``cross_entropy_label_smoothing`` index
+     ``x_lens[b].data[0]``; 1-D length tensors are passed as ``[B, 1]``.
+  4. ``compute_xe_loss`` returns a 0-dim tensor on torch 2.x; it is reshaped to
+     ``[1]`` so ``loss += ctc_loss`` works (attention_seq2seq.py:547).
+
+Usage (from the repo root, in the build container):
+    python tests/golden/make_golden.py
+"""
+import json
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+REF = '/root/reference'
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+# --------------------------------------------------------------------------
+# Shims (harness only; never shipped)
+# --------------------------------------------------------------------------
+def _install_shims():
+    import torch.nn.modules.loss as L
+    if not hasattr(L, '_assert_no_grad'):
+        L._assert_no_grad = lambda v: None
+
+    wc = types.ModuleType('warpctc_pytorch')
+
+    class _CTC(torch.autograd.Function):
+        @staticmethod
+        def backward(ctx, grad_output):
+            g = ctx.grads
+            if hasattr(g, 'data'):
+                g = g.data
+            return g * grad_output.to(g.dtype).reshape(()), None, None, None, None
+
+    def cpu_ctc(acts, grads, labels, label_lens, act_lens, minibatch, costs):
+        a = acts.detach().double().clone().requires_grad_(True)
+        with torch.enable_grad():
+            lp = a.log_softmax(-1)
+            c = F.ctc_loss(lp, labels.long(), act_lens.long(), label_lens.long(),
+                           blank=0, reduction='none', zero_infinity=True)
+            c.sum().backward()
+        grads.copy_(a.grad.to(grads.dtype))
+        costs.copy_(c.detach().to(costs.dtype))
+
+    class CTCLoss(object):
+        pass
+
+    wc._CTC = _CTC
+    wc.cpu_ctc = cpu_ctc
+    wc.gpu_ctc = cpu_ctc
+    wc.CTCLoss = CTCLoss
+    sys.modules['warpctc_pytorch'] = wc
+
+    sys.path.insert(0, REF)
+
+    from models.pytorch_v3.attention import attention_layer as al
+    orig_fwd = al.AttentionMechanism.forward
+
+    def fwd(self, enc_out, enc_out_a, x_lens, dec_out, aw_step):
+        if x_lens.dim() == 1:
+            x_lens = x_lens.view(-1, 1)
+        return orig_fwd(self, enc_out, enc_out_a, x_lens, dec_out, aw_step)
+    al.AttentionMechanism.forward = fwd
+
+    from models.pytorch_v3 import criterion as cr
+    orig_ls = cr.cross_entropy_label_smoothing
+
+    def ls(logits, y_lens, label_smoothing_prob, distribution='uniform',
+           size_average=False):
+        if y_lens.dim() == 1:
+            y_lens = y_lens.view(-1, 1)
+        return orig_ls(logits, y_lens, label_smoothing_prob, distribution, size_average)
+    cr.cross_entropy_label_smoothing = ls
+
+    from models.pytorch_v3.attention import attention_seq2seq as asq
+    asq.cross_entropy_label_smoothing = ls
+    from models.pytorch_v3.ctc import ctc as ctcmod
+    ctcmod.cross_entropy_label_smoothing = ls
+    orig_xe = asq.AttentionSeq2seq.compute_xe_loss
+
+    def xe(self, *a, **k):
+        return orig_xe(self, *a, **k).reshape(1)
+    asq.AttentionSeq2seq.compute_xe_loss = xe
+
+
+def _save(name, **arrays):
+    path = os.path.join(OUT, name + '.npz')
+    np.savez_compressed(path, **arrays)
+    sz = os.path.getsize(path)
+    print('wrote %s (%d bytes)' % (path, sz))
+
+
+def _sd(model, prefix='sd/'):
+    return {prefix + k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items()}
+
+
+def _grads(model, prefix='grad/'):
+    out = {}
+    for k, p in model.named_parameters():
+        g = p.grad
+        out[prefix + k] = (np.zeros(p.shape, np.float32) if g is None
+                           else g.detach().cpu().numpy().copy())
+    return out
+
+
+# --------------------------------------------------------------------------
+# Case 1: CTC loss / gradient on raw activations (warp-ctc contract)
+# --------------------------------------------------------------------------
+def case_ctc():
+    rng = np.random.RandomState(0)
+    cases = []
+    # (B, V, act_lens, label lists)
+    # last utterance is infeasible (L + repeats = 5 > T = 3): cost 0, grad 0
+    cases.append(('ctc_v6', 6, [30, 25, 20, 12, 3, 3],
+                  [[1, 1, 2, 3], [4, 5, 5, 5, 1], [2], [1, 2, 1, 2, 1, 2, 1, 2], [3, 3],
+                   [3, 3, 3]]))
+    cases.append(('ctc_v29', 29, [50, 47, 40, 33],
+                  [list(rng.randint(1, 29, 20)), list(rng.randint(1, 29, 15)),
+                   [5, 5, 5, 5, 5, 5], list(rng.randint(1, 29, 12))]))
+    cases.append(('ctc_v1000', 1000, [40, 37],
+                  [list(rng.randint(1, 1000, 10)), list(rng.randint(1, 1000, 7))]))
+    wc = sys.modules['warpctc_pytorch']
+    for name, V, act_lens, labels in cases:
+        B = len(act_lens)
+        T = max(act_lens)
+        acts = (rng.randn(T, B, V) * 2).astype(np.float32)
+        lab_lens = np.array([len(l) for l in labels], np.int32)
+        flat = np.concatenate([np.array(l, np.int32) for l in labels])
+        grads = torch.zeros(T, B, V)
+        costs = torch.zeros(B)
+        wc.cpu_ctc(torch.from_numpy(acts), grads, torch.from_numpy(flat),
+                   torch.from_numpy(lab_lens), torch.from_numpy(np.array(act_lens, np.int32)),
+                   B, costs)
+        _save(name, acts=acts, labels=flat, label_lens=lab_lens,
+              act_lens=np.array(act_lens, np.int32), costs=costs.numpy(),
+              grads=grads.numpy())
+
+
+# --------------------------------------------------------------------------
+# Case 2: BLSTM encoder (RNNEncoder) forward / backward
+# --------------------------------------------------------------------------
+def case_encoder():
+    from models.pytorch_v3.encoders.rnn import RNNEncoder
+    specs = [
+        ('enc_fast', dict(input_size=7, rnn_type='lstm', bidirectional=True, num_units=5,
+                          num_proj=0, num_layers=2, dropout_input=0, dropout_hidden=0,
+                          subsample_list=[], subsample_type='drop', batch_first=True,
+                          merge_bidirectional=False, pack_sequence=True)),
+        ('enc_sub', dict(input_size=7, rnn_type='lstm', bidirectional=True, num_units=5,
+                         num_proj=0, num_layers=3, dropout_input=0, dropout_hidden=0,
+                         subsample_list=[False, True, False], subsample_type='drop',
+                         batch_first=True, merge_bidirectional=False, pack_sequence=True)),
+    ]
+    for name, kw in specs:
+        torch.manual_seed(1623)
+        enc = RNNEncoder(**kw)
+        for p in enc.parameters():
+            torch.nn.init.uniform_(p, -0.3, 0.3)
+        rng = np.random.RandomState(1)
+        B, T = 4, 21
+        x_lens = np.array([17, 21, 9, 13], np.int32)     # unsorted, distinct
+        xs = rng.randn(B, T, kw['input_size']).astype(np.float32)
+        for b in range(B):
+            xs[b, x_lens[b]:] = 0
+        xs_t = torch.from_numpy(xs).requires_grad_(True)
+        out, out_lens, perm = enc(xs_t, torch.from_numpy(x_lens))
+        R = torch.from_numpy(rng.randn(*out.shape).astype(np.float32))
+        (out * R).sum().backward()
+        _save(name, kwargs=np.array(json.dumps(kw)), xs=xs, x_lens=x_lens,
+              out=out.detach().numpy(), out_lens=out_lens.numpy().astype(np.int32),
+              perm=perm.numpy().astype(np.int64), R=R.numpy(), dxs=xs_t.grad.numpy(),
+              **_sd(enc), **_grads(enc))
+
+
+# --------------------------------------------------------------------------
+# Case 3: location-aware attention step forward / backward
+# --------------------------------------------------------------------------
+def case_attention_step():
+    from models.pytorch_v3.attention.attention_layer import AttentionMechanism
+    kw = dict(encoder_num_units=12, decoder_num_units=10, attention_type='location',
+              attention_dim=8, sharpening_factor=2.0, sigmoid_smoothing=False,
+              out_channels=3, kernel_size=7, num_heads=1)
+    torch.manual_seed(1623)
+    att = AttentionMechanism(**kw)
+    for p in att.parameters():
+        torch.nn.init.uniform_(p, -0.3, 0.3)
+    rng = np.random.RandomState(2)
+    B, T = 3, 15
+    x_lens = np.array([15, 11, 15], np.int32)
+    enc_out = torch.from_numpy(rng.randn(B, T, 12).astype(np.float32)).requires_grad_(True)
+    enc_out_a = torch.from_numpy(rng.randn(B, T, 8, 1).astype(np.float32)).requires_grad_(True)
+    dec_out = torch.from_numpy(rng.randn(B, 1, 10).astype(np.float32)).requires_grad_(True)
+    aw = np.abs(rng.rand(B, T, 1)).astype(np.float32)
+    aw /= aw.sum(1, keepdims=True)
+    aw_t = torch.from_numpy(aw).requires_grad_(True)
+    ctx, aw_out = att(enc_out, enc_out_a, torch.from_numpy(x_lens), dec_out, aw_t)
+    Rc = torch.from_numpy(rng.randn(*ctx.shape).astype(np.float32))
+    Ra = torch.from_numpy(rng.randn(*aw_out.shape).astype(np.float32))
+    ((ctx * Rc).sum() + (aw_out * Ra).sum()).backward()
+    _save('att_step', kwargs=np.array(json.dumps(kw)), x_lens=x_lens,
+          enc_out=enc_out.detach().numpy(), enc_out_a=enc_out_a.detach().numpy(),
+          dec_out=dec_out.detach().numpy(), aw_in=aw, ctx=ctx.detach().numpy(),
+          aw_out=aw_out.detach().numpy(), Rc=Rc.numpy(), Ra=Ra.numpy(),
+          d_enc_out=enc_out.grad.numpy(), d_enc_out_a=enc_out_a.grad.numpy(),
+          d_dec_out=dec_out.grad.numpy(), d_aw_in=aw_t.grad.numpy(),
+          **_sd(att), **_grads(att))
+
+
+# --------------------------------------------------------------------------
+# Case 4: whole CTC model: loss, grads, greedy best path
+# --------------------------------------------------------------------------
+def _batch(rng, B, T, F_, y_lens, num_classes, x_lens):
+    xs = rng.randn(B, T, F_).astype(np.float32)
+    for b in range(B):
+        xs[b, x_lens[b]:] = 0
+    L = max(y_lens)
+    ys = np.full((B, L), -1, np.int32)
+    for b in range(B):
+        ys[b, :y_lens[b]] = rng.randint(0, num_classes, y_lens[b])
+    return xs, ys
+
+
+def case_ctc_model():
+    from models.pytorch_v3.ctc.ctc import CTC
+    from models.pytorch_v3.ctc.decoders.greedy_decoder import GreedyDecoder
+    specs = [
+        ('model_ctc_sub', dict(input_size=8, encoder_type='lstm', encoder_bidirectional=True,
+                               encoder_num_units=6, encoder_num_proj=0, encoder_num_layers=3,
+                               fc_list=[], dropout_input=0, dropout_encoder=0, num_classes=5,
+                               parameter_init=0.1, subsample_list=[False, True, False],
+                               subsample_type='drop')),
+        ('model_ctc_fast', dict(input_size=8, encoder_type='lstm', encoder_bidirectional=True,
+                                encoder_num_units=6, encoder_num_proj=0, encoder_num_layers=2,
+                                fc_list=[], dropout_input=0, dropout_encoder=0, num_classes=5,
+                                parameter_init=0.1, subsample_list=[], subsample_type='drop')),
+    ]
+    for name, kw in specs:
+        torch.manual_seed(1623)
+        model = CTC(**kw)
+        model.train()
+        rng = np.random.RandomState(3)
+        B, T = 4, 24
+        x_lens = np.array([20, 24, 15, 11], np.int32)
+        y_lens = np.array([5, 3, 4, 2], np.int32)
+        xs, ys = _batch(rng, B, T, 8, y_lens, 5, x_lens)
+        loss = model(xs, ys, x_lens, y_lens)
+        loss.backward()
+        # greedy decode: reference GreedyDecoder per utterance (ragged output)
+        model.eval()
+        with torch.no_grad():
+            logits, out_lens, perm = model._encode(torch.from_numpy(xs),
+                                                   torch.from_numpy(x_lens))
+        dec = GreedyDecoder(blank_index=0)
+        lg = logits.numpy()
+        hyps = [dec(lg[b:b + 1], out_lens.numpy()[b:b + 1])[0] - 1 for b in range(B)]
+        hyp_lens = np.array([len(h) for h in hyps], np.int32)
+        hyp_flat = (np.concatenate(hyps).astype(np.int32) if hyp_lens.sum()
+                    else np.zeros(0, np.int32))
+        _save(name, kwargs=np.array(json.dumps(kw)), xs=xs, ys=ys, x_lens=x_lens,
+              y_lens=y_lens, loss=loss.detach().numpy().reshape(1), logits=lg,
+              out_lens=out_lens.numpy().astype(np.int32), perm=perm.numpy().astype(np.int64),
+              hyp_flat=hyp_flat, hyp_lens=hyp_lens, **_sd(model), **_grads(model))
+
+
+# --------------------------------------------------------------------------
+# Case 5: attention enc-dec (location, bahdanau) with / without auxiliary CTC
+# --------------------------------------------------------------------------
+def case_attention_model():
+    from models.pytorch_v3.attention.attention_seq2seq import AttentionSeq2seq
+    base = dict(input_size=8, encoder_type='lstm', encoder_bidirectional=True,
+                encoder_num_units=6, encoder_num_proj=0, encoder_num_layers=2,
+                attention_type='location', attention_dim=7, decoder_type='lstm',
+                decoder_num_units=9, decoder_num_layers=1, embedding_dim=4,
+                dropout_input=0, dropout_encoder=0, dropout_decoder=0, dropout_embedding=0,
+                num_classes=5, parameter_init=0.1, subsample_list=[False, True],
+                subsample_type='drop', attention_conv_num_channels=3,
+                attention_conv_width=5, bottleneck_dim=11, decoding_order='bahdanau')
+    specs = [
+        ('model_att', dict(base, init_dec_state='zero', ctc_loss_weight=0,
+                           label_smoothing_prob=0)),
+        ('model_att_hybrid', dict(base, init_dec_state='first', ctc_loss_weight=0.3,
+                                  label_smoothing_prob=0, sharpening_factor=1.5)),
+        ('model_att_ls', dict(base, init_dec_state='zero', ctc_loss_weight=0.3,
+                              label_smoothing_prob=0.1)),
+    ]
+    for name, kw in specs:
+        torch.manual_seed(1623)
+        model = AttentionSeq2seq(**kw)
+        model.train()
+        rng = np.random.RandomState(4)
+        B, T = 3, 22
+        x_lens = np.array([22, 19, 14], np.int32)
+        y_lens = np.array([4, 6, 3], np.int32)
+        xs, ys = _batch(rng, B, T, 8, y_lens, 5, x_lens)
+        loss = model(xs, ys, x_lens, y_lens)
+        loss.backward()
+        _save(name, kwargs=np.array(json.dumps(kw)), xs=xs, ys=ys, x_lens=x_lens,
+              y_lens=y_lens, loss=loss.detach().numpy().reshape(1),
+              **_sd(model), **_grads(model))
+
+
+if __name__ == '__main__':
+    _install_shims()
+    case_ctc()
+    case_encoder()
+    case_attention_step()
+    case_ctc_model()
+    case_attention_model()
