@@ -1,0 +1,97 @@
+"""ctypes binding of libasr_hip.so (the C ABI declared in include/asr_hip.h).
+
+The library must be built in-tree (``python __graft_entry__.py`` or ``make -C
+pytorch_end2end_speech_recognition_amd/csrc``).  There is NO fallback: if the
+library is missing or fails to load, every op raises.  torch is imported
+first so that the library binds to the HIP runtime torch already loaded
+(same soname libamdhip64.so.7).
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the dlopen: shared HIP runtime)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'libasr_hip.so')
+
+c_int = ctypes.c_int
+c_ll = ctypes.c_longlong
+c_float = ctypes.c_float
+c_size = ctypes.c_size_t
+c_vp = ctypes.c_void_p
+c_str = ctypes.c_char_p
+
+ASR_OK = 0
+ASR_DT_F32 = 0
+ASR_DT_BF16 = 1
+
+# name -> (restype, argtypes); must mirror include/asr_hip.h exactly.
+SIGNATURES = {
+    'asr_version': (c_str, []),
+    'asr_last_error': (c_str, []),
+    'asr_arch_is_gfx950': (c_int, []),
+    'asr_ctc_workspace_bytes': (c_size, [c_int, c_int, c_int, c_int]),
+    'asr_ctc_forward': (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int,
+                                c_int, c_int, c_vp, c_vp, c_float, c_vp, c_size, c_vp]),
+    'asr_ctc_backward': (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int,
+                                 c_int, c_vp, c_float, c_vp, c_ll, c_ll, c_vp, c_size, c_vp]),
+    'asr_ctc_fwd_bwd': (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int,
+                                c_int, c_int, c_vp, c_vp, c_vp, c_size, c_vp]),
+}
+
+
+class NativeError(RuntimeError):
+    """Raised for any failure of the native library (load or call).  A
+    RuntimeError, so the reference's train_step skip-batch policy
+    (utils/training/training_loop.py:69-76) applies unchanged."""
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NativeError('libasr_hip.so not built at %s -- run `python -c "import '
+                              '__graft_entry__ as g; g.build()"` (no CPU fallback exists)'
+                              % LIB_PATH)
+        try:
+            h = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        except OSError as e:
+            raise NativeError('failed to load %s: %s' % (LIB_PATH, e))
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(h, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = h
+    return _lib
+
+
+def call(name, *args):
+    rc = getattr(lib(), name)(*args)
+    if rc != ASR_OK:
+        msg = lib().asr_last_error().decode(errors='replace')
+        raise NativeError('%s failed (rc=%d): %s' % (name, rc, msg))
+    return rc
+
+
+def query(name, *args):
+    return getattr(lib(), name)(*args)
+
+
+def ptr(t):
+    """Raw device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream_handle(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_device(*tensors):
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise NativeError('HIP op called with a CPU tensor (no CPU fallback by design)')

@@ -1,0 +1,90 @@
+// Shared helpers for the gfx950 (MI355X / CDNA4) kernels of libasr_hip.so.
+// Wave64 everywhere; no CUDA shims, no dual paths.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+#include <math.h>
+
+#include "../../include/asr_hip.h"
+
+#define ASR_WAVE 64
+
+namespace asr {
+
+// Thread-local last error text, surfaced through asr_last_error().
+void set_error(const char* fmt, ...);
+
+#define ASR_CHECK_HIP(expr)                                                     \
+  do {                                                                          \
+    hipError_t _e = (expr);                                                     \
+    if (_e != hipSuccess) {                                                     \
+      ::asr::set_error("%s:%d %s: %s", __FILE__, __LINE__, #expr,               \
+                       hipGetErrorString(_e));                                  \
+      return ASR_ERR_HIP;                                                       \
+    }                                                                           \
+  } while (0)
+
+#define ASR_LAUNCH_CHECK()                                                      \
+  do {                                                                          \
+    hipError_t _e = hipGetLastError();                                          \
+    if (_e != hipSuccess) {                                                     \
+      ::asr::set_error("%s:%d launch: %s", __FILE__, __LINE__,                  \
+                       hipGetErrorString(_e));                                  \
+      return ASR_ERR_HIP;                                                       \
+    }                                                                           \
+  } while (0)
+
+#define ASR_REQUIRE(cond, code, ...)                                            \
+  do {                                                                          \
+    if (!(cond)) {                                                              \
+      ::asr::set_error(__VA_ARGS__);                                            \
+      return (code);                                                            \
+    }                                                                           \
+  } while (0)
+
+__device__ __forceinline__ float neg_inf() { return -__builtin_huge_valf(); }
+
+// log(exp(a) + exp(b)) with -inf handling.
+__device__ __forceinline__ float lse2(float a, float b) {
+  float m = fmaxf(a, b);
+  if (m == neg_inf()) return m;
+  return m + __logf(__expf(a - m) + __expf(b - m));
+}
+
+__device__ __forceinline__ float lse3(float a, float b, float c) {
+  float m = fmaxf(fmaxf(a, b), c);
+  if (m == neg_inf()) return m;
+  return m + __logf(__expf(a - m) + __expf(b - m) + __expf(c - m));
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+
+// Accurate tanh for the fp32 parity path (libm), fast enough for the recurrence.
+__device__ __forceinline__ float tanhf_(float x) { return tanhf(x); }
+
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  // round-to-nearest-even; NaN kept NaN via the hardware convert
+  __hip_bfloat16 h = __float2bfloat16(f);
+  return *reinterpret_cast<uint16_t*>(&h);
+}
+
+__device__ __forceinline__ float bf2f(uint16_t u) {
+  return __uint_as_float(((uint32_t)u) << 16);
+}
+
+inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+}  // namespace asr

@@ -1,0 +1,77 @@
+"""CTC HIP kernels vs the reference's golden vectors and the numpy oracle."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import ctc_ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _native():
+    from pytorch_end2end_speech_recognition_amd import native_ops
+    return native_ops
+
+
+def _run(acts_btv, labels, label_lens, act_lens, dev, loss_scale=1.0):
+    ops = _native()
+    logits = torch.from_numpy(np.ascontiguousarray(acts_btv)).to(dev).requires_grad_(True)
+    lab = torch.from_numpy(np.asarray(labels, np.int32)).to(dev)
+    ll = torch.from_numpy(np.asarray(label_lens, np.int32)).to(dev)
+    al = torch.from_numpy(np.asarray(act_lens, np.int32)).to(dev)
+    loss, costs = ops.ctc_loss(logits, lab, ll, al, int(max(label_lens)), loss_scale)
+    loss.backward()
+    torch.cuda.synchronize()
+    return loss.item(), costs.cpu().numpy(), logits.grad.cpu().numpy()
+
+
+@pytest.mark.parametrize('name', ['ctc_v6', 'ctc_v29', 'ctc_v1000'])
+def test_ctc_matches_golden(name, cuda_dev):
+    d = golden(name)
+    acts = d['acts'].transpose(1, 0, 2)                     # [B, T, V]
+    loss, costs, grads = _run(acts, d['labels'], d['label_lens'], d['act_lens'], cuda_dev)
+    np.testing.assert_allclose(costs, d['costs'], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(loss, d['costs'].sum(), rtol=1e-4)
+    np.testing.assert_allclose(grads, d['grads'].transpose(1, 0, 2), rtol=1e-3, atol=2e-5)
+
+
+def test_ctc_scaled_grad_and_random_vs_oracle(cuda_dev):
+    rng = np.random.RandomState(7)
+    B, T, V = 8, 120, 29
+    act_lens = np.sort(rng.randint(60, T + 1, B))[::-1].copy()
+    act_lens[0] = T
+    label_lens = rng.randint(1, 40, B)
+    labels = np.concatenate([rng.randint(1, V, l) for l in label_lens])
+    acts = (rng.randn(B, T, V) * 3).astype(np.float32)
+    loss, costs, grads = _run(acts, labels, label_lens, act_lens, cuda_dev, loss_scale=1.0 / B)
+    c_ref, g_ref = ctc_ref.ctc_batch(acts, labels, label_lens, act_lens, time_major=False)
+    np.testing.assert_allclose(costs, c_ref, rtol=1e-4)
+    np.testing.assert_allclose(loss, c_ref.sum() / B, rtol=1e-4)
+    # f32 lattice vs float64 oracle: tolerance on the unscaled gradient (|g| <= 1)
+    np.testing.assert_allclose(grads * B, g_ref, rtol=1e-3, atol=5e-5)
+
+
+def test_ctc_long_labels_k8(cuda_dev):
+    """S = 2L+1 > 256 exercises 8 lattice states per lane."""
+    rng = np.random.RandomState(8)
+    B, T, V = 2, 400, 50
+    act_lens = np.array([400, 350])
+    label_lens = np.array([200, 150])
+    labels = np.concatenate([rng.randint(1, V, l) for l in label_lens])
+    acts = rng.randn(B, T, V).astype(np.float32)
+    _, costs, grads = _run(acts, labels, label_lens, act_lens, cuda_dev)
+    c_ref, g_ref = ctc_ref.ctc_batch(acts, labels, label_lens, act_lens, time_major=False)
+    np.testing.assert_allclose(costs, c_ref, rtol=1e-4)
+    np.testing.assert_allclose(grads, g_ref, rtol=1e-3, atol=5e-5)
+
+
+def test_ctc_deterministic(cuda_dev):
+    rng = np.random.RandomState(9)
+    B, T, V = 4, 64, 29
+    acts = rng.randn(B, T, V).astype(np.float32)
+    labels = rng.randint(1, V, 40)
+    lens = [10, 10, 10, 10]
+    a = _run(acts, labels, lens, [64, 60, 50, 40], cuda_dev)
+    b = _run(acts, labels, lens, [64, 60, 50, 40], cuda_dev)
+    np.testing.assert_array_equal(a[1], b[1])

@@ -1,0 +1,49 @@
+"""CPU checks of the C ABI boundary: the library loads and exports every symbol
+declared in include/asr_hip.h, and the ctypes table mirrors the header.  No
+compute calls (no GPU here)."""
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, 'include', 'asr_hip.h')
+
+
+def _declared():
+    src = open(HEADER).read()
+    src = re.sub(r'/\*.*?\*/', '', src, flags=re.S)
+    return sorted(set(re.findall(r'\b(asr_[a-z0-9_]+)\s*\(', src)))
+
+
+def test_header_declares_entry_points():
+    names = _declared()
+    assert 'asr_ctc_forward' in names and 'asr_version' in names
+
+
+def test_ctypes_table_mirrors_header():
+    from pytorch_end2end_speech_recognition_amd import _native
+    assert sorted(_native.SIGNATURES) == _declared()
+
+
+def test_library_loads_and_exports_every_symbol():
+    from pytorch_end2end_speech_recognition_amd import _native
+    if not os.path.exists(_native.LIB_PATH):
+        pytest.fail('libasr_hip.so not built (run __graft_entry__.build())')
+    lib = _native.lib()
+    for name in _declared():
+        assert hasattr(lib, name), name
+    assert lib.asr_version().decode().startswith('asr_hip')
+
+
+def test_workspace_query_without_gpu():
+    from pytorch_end2end_speech_recognition_amd import _native
+    n = _native.query('asr_ctc_workspace_bytes', 1000, 32, 29, 125)
+    assert n >= 2 * 32 * 1000 * 256 * 4
+
+
+def test_bad_args_raise_runtime_error():
+    from pytorch_end2end_speech_recognition_amd import _native
+    with pytest.raises(RuntimeError):
+        _native.call('asr_ctc_forward', None, 29, 29000, 1000, 32, 29, None, None, None, 10,
+                     0, 1, None, None, 1.0, None, 0, None)
