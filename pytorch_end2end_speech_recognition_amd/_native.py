@@ -37,7 +37,34 @@ SIGNATURES = {
                                  c_int, c_vp, c_float, c_vp, c_ll, c_ll, c_vp, c_size, c_vp]),
     'asr_ctc_fwd_bwd': (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int,
                                 c_int, c_int, c_vp, c_vp, c_vp, c_size, c_vp]),
+    'asr_gemm': (c_int, [c_vp, c_int, c_int, c_vp]),
+    'asr_colsum_workspace_bytes': (c_size, [c_int, c_int]),
+    'asr_colsum_accumulate': (c_int, [c_vp, c_ll, c_int, c_int, c_float, c_vp, c_vp, c_vp, c_size,
+                                      c_vp]),
+    'asr_lstm_workspace_bytes': (c_size, [c_int, c_int, c_int, c_int]),
+    'asr_lstm_forward': (c_int, [c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp,
+                                 c_vp, c_vp, c_size, c_vp]),
+    'asr_lstm_backward': (c_int, [c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int,
+                                  c_vp, c_vp, c_vp, c_size, c_vp]),
 }
+
+
+class RowMap(ctypes.Structure):
+    """asr_rowmap_t"""
+    _fields_ = [('stride_b', c_ll), ('stride_t', c_ll), ('rows_per_b', c_int), ('t_mul', c_int),
+                ('t_add', c_int), ('t_limit', c_int), ('perm', c_vp)]
+
+
+class Operand(ctypes.Structure):
+    """asr_operand_t"""
+    _fields_ = [('ptr', c_vp), ('dtype', c_int), ('trans', c_int), ('map', RowMap)]
+
+
+class Gemm(ctypes.Structure):
+    """asr_gemm_t"""
+    _fields_ = [('a', Operand), ('b', Operand), ('c', c_vp), ('c_map', RowMap), ('bias', c_vp),
+                ('bias2', c_vp), ('M', c_int), ('N', c_int), ('K', c_int), ('alpha', c_float),
+                ('beta', c_float)]
 
 
 class NativeError(RuntimeError):

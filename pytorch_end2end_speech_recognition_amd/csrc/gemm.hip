@@ -1,0 +1,365 @@
+// General MFMA GEMM for the ASR step (gfx950):
+//   C(m,n) = alpha * sum_k A(m,k) * B(n,k) + beta * C(m,n) + bias[n]
+// Operands are addressed through a RowMap so the encoder's row gathers fuse into
+// the operand loads instead of separate copy passes:
+//   * batch permutation (length sort, rnn.py:319-326)       -> perm
+//   * pyramidal "drop" subsampling xs[:, 1::2] (rnn.py:417)  -> t_mul=2, t_add=1
+//   * h_{t-1} / h_{t+1} for dW_hh with zero boundary rows   -> t_add=-1/+1, t_limit
+// Element (i,k) of an operand lives at row(i)+k (trans=0, k contiguous) or at
+// row(k)+i (trans=1, i contiguous).  Loads are f32 or bf16; compute is exact-f32
+// MFMA (v_mfma_f32_16x16x4_f32, parity mode) or bf16 MFMA
+// (v_mfma_f32_16x16x32_bf16, fp32 accumulate, performance mode).
+//
+// Tile 128x128x32, 256 threads = 4 waves in 2x2, each wave 64x64 = 4x4 MFMA
+// blocks.  Register-staged double buffering: the next K tile's global loads are
+// issued before the MFMAs of the current tile and written to LDS after the
+// barrier.  Block ids are remapped so consecutive tiles share an XCD's L2.
+#include "mfma.h"
+
+namespace asr {
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 32, NT = 256;
+constexpr int LDB16 = BK + 8;  // bf16 LDS row pitch (80 B: 16-B aligned fragment reads)
+constexpr int LDF32 = BK + 1;  // f32 LDS row pitch
+
+struct RowMap {
+  const void* base;
+  long long stride_b, stride_t;
+  int rows_per_b, t_mul, t_add, t_limit;
+  const int32_t* perm;
+};
+
+struct Operand {
+  RowMap map;
+  int dtype;  // ASR_DT_F32 / ASR_DT_BF16
+  int trans;
+  int vec_ok; // 16-element vector loads legal (alignment of base and strides)
+};
+
+struct Problem {
+  Operand a, b;
+  RowMap c;
+  const float* bias;
+  const float* bias2;
+  int M, N, K;
+  float alpha, beta;
+};
+
+struct Params {
+  Problem p[2];
+  int nprob;
+};
+
+// Element offset of logical row r, or -1 when the row maps outside [0, t_limit).
+__device__ __forceinline__ long long row_off(const RowMap& m, int r) {
+  const int b = r / m.rows_per_b;
+  const int t = r - b * m.rows_per_b;
+  const int tp = t * m.t_mul + m.t_add;
+  if (tp < 0 || tp >= m.t_limit) return -1;
+  const int bp = m.perm ? m.perm[b] : b;
+  return (long long)bp * m.stride_b + (long long)tp * m.stride_t;
+}
+
+// Load 16 contiguous elements (along the contiguous dim) starting at logical
+// (row r, col c0) of the stored matrix; `ncols` bounds the contiguous dim.
+__device__ __forceinline__ void load16(const Operand& op, int r, int nrows, int c0, int ncols,
+                                       float (&v)[16]) {
+  long long off = (r < nrows) ? row_off(op.map, r) : -1;
+  if (off < 0) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = 0.f;
+    return;
+  }
+  if (op.dtype == ASR_DT_F32) {
+    const float* p = (const float*)op.map.base + off + c0;
+    if (op.vec_ok && c0 + 16 <= ncols) {
+#pragma unroll
+      for (int j = 0; j < 16; j += 4) {
+        float4 x = *reinterpret_cast<const float4*>(p + j);
+        v[j] = x.x; v[j + 1] = x.y; v[j + 2] = x.z; v[j + 3] = x.w;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[j] = (c0 + j < ncols) ? p[j] : 0.f;
+    }
+  } else {
+    const uint16_t* p = (const uint16_t*)op.map.base + off + c0;
+    if (op.vec_ok && c0 + 16 <= ncols) {
+#pragma unroll
+      for (int j = 0; j < 16; j += 8) {
+        u16x8 x = *reinterpret_cast<const u16x8*>(p + j);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[j + q] = bf2f(x[q]);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[j] = (c0 + j < ncols) ? bf2f(p[j]) : 0.f;
+    }
+  }
+}
+
+// Thread -> (stored row, contiguous offset) of its 16-element load for a tile.
+//   trans=0: tile is 128 logical rows x 32 k: row = tid/2, k = (tid&1)*16
+//   trans=1: tile is 32 k-rows x 128 logical cols: k = tid/8, i = (tid&7)*16
+__device__ __forceinline__ void load_tile(const Operand& op, int tile0, int nrows_logical, int k0,
+                                          int K, float (&v)[16]) {
+  const int tid = threadIdx.x;
+  if (!op.trans) {
+    load16(op, tile0 + (tid >> 1), nrows_logical, k0 + (tid & 1) * 16, K, v);
+  } else {
+    load16(op, k0 + (tid >> 3), K, tile0 + (tid & 7) * 16, nrows_logical, v);
+  }
+}
+
+template <bool BF16>
+__device__ __forceinline__ void store_tile(const Operand& op, void* lds, const float (&v)[16]) {
+  const int tid = threadIdx.x;
+  if (BF16) {
+    uint16_t* s = (uint16_t*)lds;
+    if (!op.trans) {
+      uint16_t* d = s + (tid >> 1) * LDB16 + (tid & 1) * 16;
+      u16x8 x0, x1;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { x0[j] = f2bf(v[j]); x1[j] = f2bf(v[8 + j]); }
+      *reinterpret_cast<u16x8*>(d) = x0;
+      *reinterpret_cast<u16x8*>(d + 8) = x1;
+    } else {
+      const int k = tid >> 3, i0 = (tid & 7) * 16;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) s[(i0 + j) * LDB16 + k] = f2bf(v[j]);
+    }
+  } else {
+    float* s = (float*)lds;
+    if (!op.trans) {
+      float* d = s + (tid >> 1) * LDF32 + (tid & 1) * 16;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) d[j] = v[j];
+    } else {
+      const int k = tid >> 3, i0 = (tid & 7) * 16;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) s[(i0 + j) * LDF32 + k] = v[j];
+    }
+  }
+}
+
+template <bool BF16>
+__global__ void __launch_bounds__(NT) gemm_kernel(Params P) {
+  constexpr int TILE_ELEMS = BF16 ? BM * LDB16 : BM * LDF32;
+  constexpr int ESZ = BF16 ? 2 : 4;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  void* As = smem;
+  void* Bs = smem + TILE_ELEMS * ESZ;
+
+  const Problem& pr = P.p[blockIdx.z];
+  const int gm = (pr.M + BM - 1) / BM, gn = (pr.N + BN - 1) / BN;
+  const int nwg = gm * gn;
+  int id = blockIdx.x;
+  if (id >= nwg) return;
+  {  // bijective XCD-grouping remap: blocks b, b+8, ... land on one XCD
+    const int q = nwg / 8, r = nwg % 8, x = id % 8;
+    id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + id / 8;
+  }
+  const int tm = (id % gm) * BM, tn = (id / gm) * BN;
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wr = (w >> 1) * 64, wc = (w & 1) * 64;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (pr.K + BK - 1) / BK;
+  float va[16], vb[16];
+  load_tile(pr.a, tm, pr.M, 0, pr.K, va);
+  load_tile(pr.b, tn, pr.N, 0, pr.K, vb);
+  store_tile<BF16>(pr.a, As, va);
+  store_tile<BF16>(pr.b, Bs, vb);
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const bool more = kt + 1 < nk;
+    if (more) {
+      load_tile(pr.a, tm, pr.M, (kt + 1) * BK, pr.K, va);
+      load_tile(pr.b, tn, pr.N, (kt + 1) * BK, pr.K, vb);
+    }
+    if (BF16) {
+      const uint16_t* a = (const uint16_t*)As;
+      const uint16_t* b = (const uint16_t*)Bs;
+      bf16x8 fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        fa[i] = load_bf16x8(a + (wr + i * 16 + (lane & 15)) * LDB16 + 8 * (lane >> 4));
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        fb[j] = load_bf16x8(b + (wc + j * 16 + (lane & 15)) * LDB16 + 8 * (lane >> 4));
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma_bf16(fa[i], fb[j], acc[i][j]);
+    } else {
+      const float* a = (const float*)As;
+      const float* b = (const float*)Bs;
+#pragma unroll
+      for (int kk = 0; kk < BK; kk += 4) {
+        float fa[4], fb[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[i] = a[(wr + i * 16 + (lane & 15)) * LDF32 + kk + (lane >> 4)];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fb[j] = b[(wc + j * 16 + (lane & 15)) * LDF32 + kk + (lane >> 4)];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma_f32(fa[i], fb[j], acc[i][j]);
+      }
+    }
+    __syncthreads();
+    if (more) {
+      store_tile<BF16>(pr.a, As, va);
+      store_tile<BF16>(pr.b, Bs, vb);
+    }
+    __syncthreads();
+  }
+
+  // epilogue: C/D layout col = lane&15, row = 4*(lane>>4) + r
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = tm + wr + i * 16 + 4 * (lane >> 4) + r;
+      if (m >= pr.M) continue;
+      const long long off = row_off(pr.c, m);
+      if (off < 0) continue;
+      float* crow = (float*)pr.c.base + off;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = tn + wc + j * 16 + (lane & 15);
+        if (n >= pr.N) continue;
+        float v = pr.alpha * acc[i][j][r];
+        if (pr.bias) v += pr.bias[n];
+        if (pr.bias2) v += pr.bias2[n];
+        if (pr.beta != 0.f) v += pr.beta * crow[n];
+        crow[n] = v;
+      }
+    }
+  }
+}
+
+// Column sums: partial[chunk][n] = sum over rows of chunk; then ordered final sum.
+__global__ void colsum_partial(const float* __restrict__ g, long long ld, int M, int N,
+                               int rows_per_chunk, float* __restrict__ partial) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  const int chunk = blockIdx.y;
+  if (n >= N) return;
+  const int m0 = chunk * rows_per_chunk, m1 = min(M, m0 + rows_per_chunk);
+  float s = 0.f;
+  for (int m = m0; m < m1; ++m) s += g[(long long)m * ld + n];
+  partial[(long long)chunk * N + n] = s;
+}
+
+__global__ void colsum_final(const float* __restrict__ partial, int nchunk, int N, float alpha,
+                             float* __restrict__ out0, float* __restrict__ out1) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.f;
+  for (int c = 0; c < nchunk; ++c) s += partial[(long long)c * N + n];
+  s *= alpha;
+  out0[n] += s;
+  if (out1) out1[n] += s;
+}
+
+RowMap make_map(const asr_rowmap_t& m, const void* base) {
+  RowMap r;
+  r.base = base;
+  r.stride_b = m.stride_b;
+  r.stride_t = m.stride_t;
+  r.rows_per_b = m.rows_per_b > 0 ? m.rows_per_b : 0x7fffffff;
+  r.t_mul = m.t_mul == 0 ? 1 : m.t_mul;
+  r.t_add = m.t_add;
+  r.t_limit = m.t_limit > 0 ? m.t_limit : 0x7fffffff;
+  r.perm = m.perm;
+  return r;
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+int fill_operand(const asr_operand_t& o, Operand* op, const char* name) {
+  ASR_REQUIRE(o.ptr, ASR_ERR_ARG, "gemm: operand %s is null", name);
+  ASR_REQUIRE(o.dtype == ASR_DT_F32 || o.dtype == ASR_DT_BF16, ASR_ERR_ARG,
+              "gemm: operand %s bad dtype", name);
+  op->map = make_map(o.map, o.ptr);
+  op->dtype = o.dtype;
+  op->trans = o.trans;
+  const int esz = o.dtype == ASR_DT_F32 ? 4 : 2;
+  const int vec = o.dtype == ASR_DT_F32 ? 4 : 8;
+  op->vec_ok = aligned16(o.ptr) && (o.map.stride_t % vec == 0) && (o.map.stride_b % vec == 0);
+  (void)esz;
+  return ASR_OK;
+}
+
+}  // namespace
+}  // namespace asr
+
+using namespace asr;
+
+extern "C" int asr_gemm(const asr_gemm_t* problems, int nprob, int compute_dtype, void* stream) {
+  ASR_REQUIRE(problems && nprob >= 1 && nprob <= 2, ASR_ERR_ARG, "gemm: nprob must be 1 or 2");
+  Params P;
+  P.nprob = nprob;
+  int maxwg = 0;
+  for (int i = 0; i < nprob; ++i) {
+    const asr_gemm_t& g = problems[i];
+    ASR_REQUIRE(g.M >= 0 && g.N >= 0 && g.K >= 0, ASR_ERR_ARG, "gemm: negative size");
+    Problem& p = P.p[i];
+    int rc = fill_operand(g.a, &p.a, "A");
+    if (rc) return rc;
+    rc = fill_operand(g.b, &p.b, "B");
+    if (rc) return rc;
+    ASR_REQUIRE(g.c, ASR_ERR_ARG, "gemm: C is null");
+    p.c = make_map(g.c_map, g.c);
+    p.bias = g.bias;
+    p.bias2 = g.bias2;
+    p.M = g.M; p.N = g.N; p.K = g.K;
+    p.alpha = g.alpha;
+    p.beta = g.beta;
+    maxwg = max(maxwg, ceil_div(g.M, BM) * ceil_div(g.N, BN));
+  }
+  if (nprob == 1) P.p[1] = P.p[0];
+  if (maxwg == 0) return ASR_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (compute_dtype == ASR_DT_BF16) {
+    const size_t lds = 2 * BM * LDB16 * 2;
+    hipLaunchKernelGGL(gemm_kernel<true>, dim3(maxwg, 1, nprob), dim3(NT), lds, s, P);
+  } else {
+    const size_t lds = 2 * BM * LDF32 * 4;
+    hipLaunchKernelGGL(gemm_kernel<false>, dim3(maxwg, 1, nprob), dim3(NT), lds, s, P);
+  }
+  ASR_LAUNCH_CHECK();
+  return ASR_OK;
+}
+
+extern "C" size_t asr_colsum_workspace_bytes(int M, int N) {
+  const int nchunk = M < 256 ? 1 : min(64, (M + 255) / 256);
+  return (size_t)nchunk * N * sizeof(float);
+}
+
+extern "C" int asr_colsum_accumulate(const float* g, long long ld, int M, int N, float alpha,
+                                     float* out0, float* out1, void* workspace, size_t ws_bytes,
+                                     void* stream) {
+  ASR_REQUIRE(g && out0 && workspace, ASR_ERR_ARG, "colsum: null pointer");
+  if (M <= 0 || N <= 0) return ASR_OK;
+  const int nchunk = M < 256 ? 1 : min(64, (M + 255) / 256);
+  ASR_REQUIRE(ws_bytes >= asr_colsum_workspace_bytes(M, N), ASR_ERR_WORKSPACE,
+              "colsum: workspace too small");
+  const int rpc = (M + nchunk - 1) / nchunk;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(colsum_partial, dim3(ceil_div(N, 256), nchunk), dim3(256), 0, s, g, ld, M, N,
+                     rpc, (float*)workspace);
+  ASR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(colsum_final, dim3(ceil_div(N, 256)), dim3(256), 0, s,
+                     (const float*)workspace, nchunk, N, alpha, out0, out1);
+  ASR_LAUNCH_CHECK();
+  return ASR_OK;
+}

@@ -1,0 +1,344 @@
+// Bidirectional LSTM recurrence for the encoder (gfx950).  Replaces the cuDNN /
+// MIOpen packed nn.LSTM(bidirectional=True) of models/pytorch_v3/encoders/rnn.py
+// (:166-172 fast path, :218-224 per-layer path, packing :343-358, :377-390).
+//
+// Semantics (nn.LSTM, gate order i,f,g,o; h0 = c0 = 0, rnn.py:499-536):
+//   pre  = gx[b,t] + h_prev @ W_hh^T          (gx = x @ W_ih^T + b_ih + b_hh, one GEMM)
+//   c    = sig(f) * c_prev + sig(i) * tanh(g),  h = sig(o) * tanh(c)
+// Packed-sequence behaviour is reproduced with per-utterance length masks: for
+// t >= len[b] the state and the output are 0, so the reverse direction starts at
+// each utterance's own last frame and padded outputs are zero (pad_packed).
+//
+// One launch per time step processes BOTH directions (forward at t = s, reverse
+// at t = T-1-s).  Work-group = (4 hidden units x 4 gates = 16 gate columns) x 32
+// utterances; its 4 waves split the K = H reduction and combine through LDS, so
+// the 16x16 MFMA tile holds all four gates of its units and the cell update is
+// fused into the same kernel.  h_{t-1} is read from a ping-pong buffer kept in
+// the compute dtype (bf16 in performance mode: half the bytes per step).
+//
+// Backward: one launch per step in reverse processing order.  Work-group = 16
+// units x 32 utterances, K = 4H over the previous step's gate gradients times
+// W_hh (a transposed copy, so each lane's 8-element MFMA fragment is contiguous).
+// The gate gradients are written over the saved activations and then feed the
+// weight-gradient GEMMs (asr_gemm) outside the recurrence.
+#include "mfma.h"
+
+namespace asr {
+namespace {
+
+constexpr int FU = 4;    // forward: units per work-group (16 gate columns)
+constexpr int BU = 16;   // backward: units per work-group
+constexpr int MB = 32;   // utterances per work-group (two 16-row MFMA blocks)
+
+// ---- operand fragment loads (guarded for arbitrary H / B) ----------------
+template <typename T>
+__device__ __forceinline__ float ldf(const T* p, long long i);
+template <>
+__device__ __forceinline__ float ldf<float>(const float* p, long long i) { return p[i]; }
+template <>
+__device__ __forceinline__ float ldf<uint16_t>(const uint16_t* p, long long i) { return bf2f(p[i]); }
+
+// 8 consecutive elements [k, k+8) of row `row` (nullptr row -> zeros), k < klim.
+template <typename T>
+__device__ __forceinline__ bf16x8 frag8(const T* row, int k, int klim, bool vec) {
+  if (row == nullptr) return as_bf16x8(u16x8{0, 0, 0, 0, 0, 0, 0, 0});
+  if (vec && k + 8 <= klim) {
+    if constexpr (sizeof(T) == 2) return load_bf16x8((const uint16_t*)row + k);
+    else return load_bf16x8_from_f32((const float*)row + k);
+  }
+  u16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (k + j < klim) ? f2bf(ldf<T>(row, k + j)) : (uint16_t)0;
+  return as_bf16x8(r);
+}
+
+template <typename T>
+__device__ __forceinline__ float frag1(const T* row, int k, int klim) {
+  return (row != nullptr && k < klim) ? ldf<T>(row, k) : 0.f;
+}
+
+// Partial products of one wave: acc[mb] (+)= A[rows of block mb][k-range] * B[cols][k-range]
+// A rows: a_row[mb] (per lane: row l&15 of block mb), B row: b_row (per lane: col l&15).
+template <bool BF16, typename TA, typename TB>
+__device__ __forceinline__ void wave_dot(const TA* a_row0, const TA* a_row1, const TB* b_row,
+                                         int K, int wave, bool vec, f32x4& acc0, f32x4& acc1) {
+  const int lane = threadIdx.x & 63;
+  if (BF16) {
+    for (int k0 = wave * 32; k0 < K; k0 += 4 * 32) {
+      const int k = k0 + 8 * (lane >> 4);
+      const bf16x8 b = frag8<TB>(b_row, k, K, vec);
+      acc0 = mfma_bf16(frag8<TA>(a_row0, k, K, vec), b, acc0);
+      acc1 = mfma_bf16(frag8<TA>(a_row1, k, K, vec), b, acc1);
+    }
+  } else {
+    for (int k0 = wave * 4; k0 < K; k0 += 4 * 4) {
+      const int k = k0 + (lane >> 4);
+      const float b = frag1<TB>(b_row, k, K);
+      acc0 = mfma_f32(frag1<TA>(a_row0, k, K), b, acc0);
+      acc1 = mfma_f32(frag1<TA>(a_row1, k, K), b, acc1);
+    }
+  }
+}
+
+__device__ __forceinline__ void store_state(float* p, long long i, float v) { p[i] = v; }
+__device__ __forceinline__ void store_state(uint16_t* p, long long i, float v) { p[i] = f2bf(v); }
+
+// ---------------------------------------------------------------------------
+// forward step.  grid = (ceil(H/FU), 2 directions, ceil(B/MB)), block = 256
+// ---------------------------------------------------------------------------
+template <bool BF16, typename TW, typename TS>
+__global__ void __launch_bounds__(256) lstm_fwd_step(
+    int s, int B, int T, int H, const int32_t* __restrict__ lens, const TW* __restrict__ whh_f,
+    const TW* __restrict__ whh_r, float* __restrict__ gx_act, float* __restrict__ y,
+    float* __restrict__ cst, TS* __restrict__ hbuf, int vec) {
+  __shared__ float part[4][MB][16];
+  const int dir = blockIdx.y;
+  const int u0 = blockIdx.x * FU;
+  const int b0 = blockIdx.z * MB;
+  const int t = dir == 0 ? s : T - 1 - s;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const TW* W = dir == 0 ? whh_f : whh_r;
+  const long long BH = (long long)B * H;
+  // ping-pong h: hbuf[parity][dir][b][H]; step s reads parity (s+1)&1, writes s&1
+  const TS* hprev = hbuf + ((long long)((s + 1) & 1) * 2 + dir) * BH;
+  TS* hnext = hbuf + ((long long)(s & 1) * 2 + dir) * BH;
+
+  // fragment rows for this lane
+  const int ra = b0 + (lane & 15), rb = b0 + 16 + (lane & 15);
+  const TS* a_row0 = ra < B ? hprev + (long long)ra * H : nullptr;
+  const TS* a_row1 = rb < B ? hprev + (long long)rb * H : nullptr;
+  const int n = lane & 15, g = n >> 2, u = u0 + (n & 3);
+  const TW* b_row = u < H ? W + (long long)(g * H + u) * H : nullptr;
+
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  if (s > 0) wave_dot<BF16, TS, TW>(a_row0, a_row1, b_row, H, wave, vec != 0, acc0, acc1);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    part[wave][4 * (lane >> 4) + r][lane & 15] = acc0[r];
+    part[wave][16 + 4 * (lane >> 4) + r][lane & 15] = acc1[r];
+  }
+  __syncthreads();
+  if (threadIdx.x >= MB * FU) return;
+  const int row = threadIdx.x >> 2, uu = threadIdx.x & 3;
+  const int b = b0 + row, j = u0 + uu;
+  if (b >= B || j >= H) return;
+  const bool active = t < lens[b];
+  const long long gbase = ((long long)b * T + t) * 8 * H + (long long)dir * 4 * H + j;
+  const long long sidx = ((long long)b * T + t) * 2 * H + (long long)dir * H + j;
+  float pre[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    pre[q] = part[0][row][q * 4 + uu] + part[1][row][q * 4 + uu] + part[2][row][q * 4 + uu] +
+             part[3][row][q * 4 + uu] + gx_act[gbase + (long long)q * H];
+  const int tp = dir == 0 ? t - 1 : t + 1;
+  const float cprev = (tp >= 0 && tp < T) ? cst[sidx + (long long)(tp - t) * 2 * H] : 0.f;
+  const float ig = sigmoidf_(pre[0]), fg = sigmoidf_(pre[1]);
+  const float gg = tanhf_(pre[2]), og = sigmoidf_(pre[3]);
+  float c = fg * cprev + ig * gg;
+  float h = og * tanhf_(c);
+  if (!active) { c = 0.f; h = 0.f; }
+  y[sidx] = h;
+  cst[sidx] = c;
+  gx_act[gbase] = active ? ig : 0.f;
+  gx_act[gbase + H] = active ? fg : 0.f;
+  gx_act[gbase + 2 * H] = active ? gg : 0.f;
+  gx_act[gbase + 3 * H] = active ? og : 0.f;
+  store_state(hnext, (long long)b * H + j, h);
+}
+
+// ---------------------------------------------------------------------------
+// backward step (processing index q: forward dir at t = T-1-q, reverse at t = q)
+// grid = (ceil(H/BU), 2, ceil(B/MB)), block = 256
+// ---------------------------------------------------------------------------
+template <bool BF16, typename TS>
+__global__ void __launch_bounds__(256) lstm_bwd_step(
+    int q, int B, int T, int H, const int32_t* __restrict__ lens, const TS* __restrict__ wt,
+    const float* __restrict__ dy, float* __restrict__ act_dg, const float* __restrict__ cst,
+    TS* __restrict__ dgbuf, float* __restrict__ dc, int vec) {
+  __shared__ float part[4][MB][16];
+  const int dir = blockIdx.y;
+  const int u0 = blockIdx.x * BU;
+  const int b0 = blockIdx.z * MB;
+  const int t = dir == 0 ? T - 1 - q : q;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int H4 = 4 * H;
+  const long long BG = (long long)B * H4;
+  const TS* gprev = dgbuf + ((long long)((q + 1) & 1) * 2 + dir) * BG;
+  TS* gnext = dgbuf + ((long long)(q & 1) * 2 + dir) * BG;
+  const TS* W = wt + (long long)dir * H * H4;   // W_hh^T: [H][4H]
+
+  const int ra = b0 + (lane & 15), rb = b0 + 16 + (lane & 15);
+  const TS* a_row0 = ra < B ? gprev + (long long)ra * H4 : nullptr;
+  const TS* a_row1 = rb < B ? gprev + (long long)rb * H4 : nullptr;
+  const int j_l = u0 + (lane & 15);
+  const TS* b_row = j_l < H ? W + (long long)j_l * H4 : nullptr;
+
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  if (q > 0) wave_dot<BF16, TS, TS>(a_row0, a_row1, b_row, H4, wave, vec != 0, acc0, acc1);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    part[wave][4 * (lane >> 4) + r][lane & 15] = acc0[r];
+    part[wave][16 + 4 * (lane >> 4) + r][lane & 15] = acc1[r];
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < MB * BU; idx += 256) {
+    const int row = idx / BU, uu = idx % BU;
+    const int b = b0 + row, j = u0 + uu;
+    if (b >= B || j >= H) continue;
+    const long long gbase = ((long long)b * T + t) * 8 * H + (long long)dir * H4 + j;
+    const long long sidx = ((long long)b * T + t) * 2 * H + (long long)dir * H + j;
+    const long long cidx = ((long long)dir * B + b) * H + j;
+    TS* gn = gnext + (long long)b * H4 + j;
+    if (t >= lens[b]) {
+      act_dg[gbase] = 0.f; act_dg[gbase + H] = 0.f; act_dg[gbase + 2 * H] = 0.f;
+      act_dg[gbase + 3 * H] = 0.f;
+      store_state(gn, 0, 0.f); store_state(gn, H, 0.f); store_state(gn, 2 * H, 0.f);
+      store_state(gn, 3 * H, 0.f);
+      dc[cidx] = 0.f;
+      continue;
+    }
+    const float dh = part[0][row][uu] + part[1][row][uu] + part[2][row][uu] + part[3][row][uu] +
+                     (dy ? dy[sidx] : 0.f);
+    const float ig = act_dg[gbase], fg = act_dg[gbase + H], gg = act_dg[gbase + 2 * H],
+                og = act_dg[gbase + 3 * H];
+    const float c = cst[sidx];
+    const int tp = dir == 0 ? t - 1 : t + 1;
+    const float cprev = (tp >= 0 && tp < T) ? cst[sidx + (long long)(tp - t) * 2 * H] : 0.f;
+    const float tc = tanhf_(c);
+    const float dcell = dc[cidx] + dh * og * (1.f - tc * tc);
+    const float d_i = dcell * gg * ig * (1.f - ig);
+    const float d_f = dcell * cprev * fg * (1.f - fg);
+    const float d_g = dcell * ig * (1.f - gg * gg);
+    const float d_o = dh * tc * og * (1.f - og);
+    dc[cidx] = dcell * fg;
+    act_dg[gbase] = d_i; act_dg[gbase + H] = d_f; act_dg[gbase + 2 * H] = d_g;
+    act_dg[gbase + 3 * H] = d_o;
+    store_state(gn, 0, d_i); store_state(gn, H, d_f); store_state(gn, 2 * H, d_g);
+    store_state(gn, 3 * H, d_o);
+  }
+}
+
+// W_hh [4H][H] (f32 or bf16) -> W_hh^T [H][4H] in the compute dtype, both dirs.
+template <typename TW, typename TS>
+__global__ void transpose_whh(const TW* __restrict__ wf, const TW* __restrict__ wr, int H,
+                              TS* __restrict__ out) {
+  __shared__ float tile[32][33];
+  const int dir = blockIdx.z;
+  const TW* w = dir == 0 ? wf : wr;
+  const int R = 4 * H, C = H;
+  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 32 x 8
+  for (int i = ty; i < 32; i += 8) {
+    const int r = r0 + i, c = c0 + tx;
+    tile[i][tx] = (r < R && c < C) ? ldf<TW>(w, (long long)r * C + c) : 0.f;
+  }
+  __syncthreads();
+  TS* o = out + (long long)dir * C * R;
+  for (int i = ty; i < 32; i += 8) {
+    const int c = c0 + i, r = r0 + tx;
+    if (c < C && r < R) store_state(o, (long long)c * R + r, tile[tx][i]);
+  }
+}
+
+size_t fwd_ws(int B, int H, int cdt) {
+  return (size_t)4 * B * H * (cdt == ASR_DT_BF16 ? 2 : 4);
+}
+
+size_t bwd_ws(int B, int H, int cdt) {
+  const size_t es = cdt == ASR_DT_BF16 ? 2 : 4;
+  const size_t wt = (size_t)2 * H * 4 * H * es;
+  const size_t dg = (size_t)4 * B * 4 * H * es;
+  const size_t dcb = (size_t)2 * B * H * 4;
+  return ((wt + 255) & ~size_t(255)) + ((dg + 255) & ~size_t(255)) + dcb;
+}
+
+}  // namespace
+}  // namespace asr
+
+using namespace asr;
+
+extern "C" size_t asr_lstm_workspace_bytes(int B, int H, int compute_dtype, int backward) {
+  return backward ? bwd_ws(B, H, compute_dtype) : fwd_ws(B, H, compute_dtype);
+}
+
+extern "C" int asr_lstm_forward(float* gx_act, const void* whh_f, const void* whh_r, int w_dtype,
+                                const int32_t* lens, int B, int T, int H, int compute_dtype,
+                                float* y, float* cst, void* workspace, size_t ws_bytes,
+                                void* stream) {
+  ASR_REQUIRE(gx_act && whh_f && whh_r && lens && y && cst && workspace, ASR_ERR_ARG,
+              "lstm_forward: null pointer");
+  ASR_REQUIRE(B > 0 && T > 0 && H > 0, ASR_ERR_ARG, "lstm_forward: bad shape");
+  ASR_REQUIRE(ws_bytes >= fwd_ws(B, H, compute_dtype), ASR_ERR_WORKSPACE,
+              "lstm_forward: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const bool bf = compute_dtype == ASR_DT_BF16;
+  ASR_CHECK_HIP(hipMemsetAsync(workspace, 0, fwd_ws(B, H, compute_dtype), s));
+  const int vec = (H % 8 == 0) ? 1 : 0;
+  dim3 grid(ceil_div(H, FU), 2, ceil_div(B, MB));
+  for (int st = 0; st < T; ++st) {
+    if (bf) {
+      if (w_dtype == ASR_DT_BF16)
+        hipLaunchKernelGGL((lstm_fwd_step<true, uint16_t, uint16_t>), grid, dim3(256), 0, s, st, B,
+                           T, H, lens, (const uint16_t*)whh_f, (const uint16_t*)whh_r, gx_act, y,
+                           cst, (uint16_t*)workspace, vec);
+      else
+        hipLaunchKernelGGL((lstm_fwd_step<true, float, uint16_t>), grid, dim3(256), 0, s, st, B, T,
+                           H, lens, (const float*)whh_f, (const float*)whh_r, gx_act, y, cst,
+                           (uint16_t*)workspace, vec);
+    } else {
+      ASR_REQUIRE(w_dtype == ASR_DT_F32, ASR_ERR_ARG, "lstm_forward: f32 compute needs f32 W");
+      hipLaunchKernelGGL((lstm_fwd_step<false, float, float>), grid, dim3(256), 0, s, st, B, T, H,
+                         lens, (const float*)whh_f, (const float*)whh_r, gx_act, y, cst,
+                         (float*)workspace, vec);
+    }
+    ASR_LAUNCH_CHECK();
+  }
+  return ASR_OK;
+}
+
+extern "C" int asr_lstm_backward(const float* dy, const void* whh_f, const void* whh_r,
+                                 int w_dtype, const int32_t* lens, int B, int T, int H,
+                                 int compute_dtype, float* act_dg, const float* cst,
+                                 void* workspace, size_t ws_bytes, void* stream) {
+  ASR_REQUIRE(whh_f && whh_r && lens && act_dg && cst && workspace, ASR_ERR_ARG,
+              "lstm_backward: null pointer");
+  ASR_REQUIRE(B > 0 && T > 0 && H > 0, ASR_ERR_ARG, "lstm_backward: bad shape");
+  ASR_REQUIRE(ws_bytes >= bwd_ws(B, H, compute_dtype), ASR_ERR_WORKSPACE,
+              "lstm_backward: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const bool bf = compute_dtype == ASR_DT_BF16;
+  const size_t es = bf ? 2 : 4;
+  const size_t wt_bytes = ((size_t)2 * H * 4 * H * es + 255) & ~size_t(255);
+  const size_t dg_bytes = ((size_t)4 * B * 4 * H * es + 255) & ~size_t(255);
+  char* base = (char*)workspace;
+  void* wt = base;
+  void* dg = base + wt_bytes;
+  float* dcb = (float*)(base + wt_bytes + dg_bytes);
+  ASR_CHECK_HIP(hipMemsetAsync(dg, 0, dg_bytes + (size_t)2 * B * H * 4, s));
+  dim3 tg(ceil_div(H, 32), ceil_div(4 * H, 32), 2);
+  if (bf) {
+    if (w_dtype == ASR_DT_BF16)
+      hipLaunchKernelGGL((transpose_whh<uint16_t, uint16_t>), tg, dim3(256), 0, s,
+                         (const uint16_t*)whh_f, (const uint16_t*)whh_r, H, (uint16_t*)wt);
+    else
+      hipLaunchKernelGGL((transpose_whh<float, uint16_t>), tg, dim3(256), 0, s,
+                         (const float*)whh_f, (const float*)whh_r, H, (uint16_t*)wt);
+  } else {
+    ASR_REQUIRE(w_dtype == ASR_DT_F32, ASR_ERR_ARG, "lstm_backward: f32 compute needs f32 W");
+    hipLaunchKernelGGL((transpose_whh<float, float>), tg, dim3(256), 0, s, (const float*)whh_f,
+                       (const float*)whh_r, H, (float*)wt);
+  }
+  ASR_LAUNCH_CHECK();
+  const int vec = (H % 8 == 0) ? 1 : 0;
+  dim3 grid(ceil_div(H, BU), 2, ceil_div(B, MB));
+  for (int q = 0; q < T; ++q) {
+    if (bf)
+      hipLaunchKernelGGL((lstm_bwd_step<true, uint16_t>), grid, dim3(256), 0, s, q, B, T, H, lens,
+                         (const uint16_t*)wt, dy, act_dg, cst, (uint16_t*)dg, dcb, vec);
+    else
+      hipLaunchKernelGGL((lstm_bwd_step<false, float>), grid, dim3(256), 0, s, q, B, T, H, lens,
+                         (const float*)wt, dy, act_dg, cst, (float*)dg, dcb, vec);
+    ASR_LAUNCH_CHECK();
+  }
+  return ASR_OK;
+}

