@@ -1,0 +1,237 @@
+#!/usr/bin/env python
+"""Training-throughput benchmark of the MI355X hybrid CTC/attention step.
+
+Workload (BASELINE.json configs[1]): LibriSpeech-100h char CTC, 5-layer
+bidirectional LSTM, 512 units per direction, no subsampling, dropout 0.2, Adam
+lr 1e-3 wd 1e-6, clip 5.0; per GPU B = 32 synthetic utterances of 80-dim fbank,
+x_lens ~ U[800, 1000] sorted descending (x_lens[0] = 1000), char labels
+U[0, 27] (V = 28 + blank), y_lens ~ U[60, 125].  One step = the
+reference's full train_step: H2D of the numpy batch, forward, CTC loss,
+backward, RCCL gradient all-reduce (N > 1), fused global-norm clip + Adam, loss
+read back.  Weak scaling: B = 32 per GPU.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Prints ONE JSON line (rank 0) with the metric, a live roofline of the dominant
+kernel (per-launch HIP events on the kernel's own stream) and the CPU oracle
+baseline timed on this host.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from pytorch_end2end_speech_recognition_amd import _native as N  # noqa: E402
+from pytorch_end2end_speech_recognition_amd import native_ops  # noqa: E402
+from pytorch_end2end_speech_recognition_amd.models.load_model import load  # noqa: E402
+from pytorch_end2end_speech_recognition_amd.utils.training.training_loop import train_step  # noqa
+
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
+BF16_PEAK_TFLOPS = 2500.0    # dense bf16 MFMA (spec, no sparsity)
+
+CONFIGS = {
+    'ctc5x512': dict(
+        workload='librispeech100h_char_ctc_blstm5x512', model_type='ctc',
+        params=dict(input_freq=80, use_delta=False, use_double_delta=False, input_channel=1,
+                    splice=1, num_stack=1, encoder_type='lstm', conv_channels=[],
+                    conv_kernel_sizes=[], conv_strides=[], poolings=[], activation='relu',
+                    batch_norm=False, encoder_bidirectional=True, encoder_residual=False,
+                    encoder_dense_residual=False, encoder_num_units=512, encoder_num_proj=0,
+                    encoder_num_layers=5, subsample_list=[], subsample_type='drop', fc_list=[],
+                    optimizer='adam', learning_rate=1e-3, parameter_init_distribution='uniform',
+                    parameter_init=0.1, recurrent_weight_orthogonal=False,
+                    init_forget_gate_bias_with_one=True, char_init=False, clip_grad_norm=5.0,
+                    dropout_input=0, dropout_encoder=0.2, weight_decay=1e-6,
+                    logits_temperature=1, label_smoothing_prob=0, weight_noise_std=0,
+                    num_classes=28)),
+}
+
+
+def synthetic_batch(B, T, F, num_classes, seed):
+    """SURVEY §8d synthetic inputs (numpy seed per rank)."""
+    rng = np.random.RandomState(seed)
+    x_lens = np.sort(rng.randint(800, T + 1, B))[::-1].astype(np.int32)
+    x_lens[0] = T
+    xs = rng.randn(B, T, F).astype(np.float32)
+    for b in range(B):
+        xs[b, x_lens[b]:] = 0
+    y_lens = rng.randint(60, 126, B).astype(np.int32)
+    ys = np.full((B, int(y_lens.max())), -1, np.int32)
+    for b in range(B):
+        ys[b, :y_lens[b]] = rng.randint(0, num_classes, y_lens[b])
+    return dict(xs=xs, ys=ys, x_lens=x_lens, y_lens=y_lens)
+
+
+def cpu_baseline(cfg, batch, n_utts):
+    """Oracle (torch-CPU restatement of the reference path) on a bounded sample:
+    the first n_utts utterances of this rank's batch, one full training step
+    (forward, backward, clip, Adam)."""
+    from oracle import asr_ref
+    cores = len(os.sched_getaffinity(0))
+    threads = max(1, min(16, cores))
+    torch.set_num_threads(threads)
+    p = cfg['params']
+    torch.manual_seed(0)
+    model = load(cfg['model_type'], dict(p), 'pytorch')           # host-side init only
+    sd = {k: v.detach().clone().requires_grad_(True) for k, v in model.state_dict().items()}
+    opt = torch.optim.Adam(list(sd.values()), lr=p['learning_rate'],
+                           weight_decay=p['weight_decay'])
+    sub = {k: v[:n_utts] for k, v in batch.items()}
+    sub['ys'] = sub['ys'][:, :int(sub['y_lens'].max())]
+    ocfg = dict(num_layers=p['encoder_num_layers'], subsample_list=p['subsample_list'],
+                fc_list=p['fc_list'])
+    t0 = time.perf_counter()
+    opt.zero_grad()
+    loss, _, _, _ = asr_ref.ctc_model_loss(sd, ocfg, sub['xs'], sub['ys'], sub['x_lens'],
+                                           sub['y_lens'])
+    loss.backward()
+    torch.nn.utils.clip_grad_norm_(list(sd.values()), p['clip_grad_norm'])
+    opt.step()
+    dt = time.perf_counter() - t0
+    frames = float(np.sum(sub['x_lens']))
+    return {'value': frames / dt, 'unit': 'frames/s', 'cores': threads, 'kind': 'port',
+            'sample': '%d utterances x %d max frames (%d frames), 1 full training step (fwd + '
+                      'bwd + clip + Adam) of the fp32 torch-CPU oracle, %.1f s'
+                      % (n_utts, int(sub['x_lens'].max()), int(frames), dt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=10)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--config', default='ctc5x512', choices=sorted(CONFIGS))
+    ap.add_argument('--precision', default='bf16', choices=['bf16', 'fp32'])
+    ap.add_argument('--batch', type=int, default=32)
+    ap.add_argument('--frames', type=int, default=1000)
+    ap.add_argument('--cpu-utts', type=int, default=2)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--prof-stride', type=int, default=8)
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device('cuda', local_rank)
+    if world > 1:
+        dist.init_process_group('nccl', device_id=dev)
+
+    cfg = CONFIGS[args.config]
+    p = dict(cfg['params'])
+    torch.manual_seed(1623)
+    native_ops.manual_seed(1623 + rank)
+    model = load(cfg['model_type'], p, 'pytorch')
+    if world > 1:   # identical initial weights on every rank
+        model.set_cuda()
+        dist.broadcast(model._flat_param, src=0)
+    else:
+        model.set_cuda()
+    model.set_precision(args.precision)
+    model.set_optimizer(p['optimizer'], p['learning_rate'], weight_decay=p['weight_decay'],
+                        lr_schedule=False)
+    batch = synthetic_batch(args.batch, args.frames, p['input_freq'], p['num_classes'],
+                            seed=rank)
+    frames_per_step = float(batch['x_lens'].sum())
+
+    for _ in range(args.warmup):
+        model, _ = train_step(model, batch, p['clip_grad_norm'])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    N.call('asr_prof_begin', args.prof_stride)
+    t0 = time.perf_counter()
+    losses = []
+    for _ in range(args.steps):
+        model, lv = train_step(model, batch, p['clip_grad_norm'])
+        losses.append(lv)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    import ctypes
+    mean_us = (ctypes.c_double * 2)()
+    launches = (ctypes.c_longlong * 2)()
+    N.call('asr_prof_end', ctypes.cast(mean_us, ctypes.c_void_p),
+           ctypes.cast(launches, ctypes.c_void_p), 2)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        fr = torch.tensor([frames_per_step], dtype=torch.float64, device=dev)
+        dist.all_reduce(fr, op=dist.ReduceOp.SUM)
+        total_frames_per_step = float(fr.item())
+    else:
+        total_frames_per_step = frames_per_step
+
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+
+    # ---- roofline of the dominant kernel (the recurrence step) ------------
+    B, H = args.batch, p['encoder_num_units']
+    esz = 2 if args.precision == 'bf16' else 4
+    # one launch = one time step of BOTH directions of one layer
+    flops_per_launch = 2 * 2 * B * 4 * H * H                      # h @ W_hh^T, 2 dirs
+    bytes_fwd = (2 * 4 * H * H * esz        # W_hh (both dirs) streamed once per launch
+                 + 2 * B * H * esz          # h_{t-1}
+                 + 2 * B * 4 * H * 4        # gx read
+                 + 2 * B * 4 * H * 4        # gate activations written
+                 + 2 * B * H * 4 * 3        # c_{t-1} read, c_t and h_t written
+                 + 2 * B * H * esz)         # h_t state copy
+    bytes_bwd = (2 * 4 * H * H * esz + 2 * B * 4 * H * esz   # W_hh^T, dG_{t+1}
+                 + 2 * B * 4 * H * 4 * 2                     # act read, dG written
+                 + 2 * B * H * 4 * 4                         # dy, c_t, c_{t-1}, dc carry
+                 + 2 * B * 4 * H * esz)                      # dG state copy
+    kinds = [('lstm_fwd_step', mean_us[0], launches[0], bytes_fwd),
+             ('lstm_bwd_step', mean_us[1], launches[1], bytes_bwd)]
+    dom = max(kinds, key=lambda k: k[1] * k[2])
+    name, us, nl, nbytes = dom
+    achieved_gbs = nbytes / (us * 1e-6) / 1e9 if us > 0 else 0.0
+    roofline = {'bound': 'hbm', 'kernel': name, 'achieved': round(achieved_gbs, 1),
+                'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(achieved_gbs / HBM_PEAK_GBS, 4),
+                'traffic': None, 'mean_launch_us': round(us, 3), 'launches_timed': int(nl),
+                'algorithmic_bytes_per_launch': int(nbytes),
+                'mfma_view': {'flops_per_launch': flops_per_launch,
+                              'achieved_tflops': round(flops_per_launch / (us * 1e-6) / 1e12, 2)
+                              if us > 0 else 0.0,
+                              'peak_tflops': BF16_PEAK_TFLOPS},
+                'other_kernels': {k[0]: {'mean_launch_us': round(k[1], 3),
+                                         'launches': int(k[2])} for k in kinds if k[0] != name}}
+
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(cfg, batch, args.cpu_utts)
+
+    value = total_frames_per_step * args.steps / elapsed
+    out = {
+        'metric': 'training frames/sec', 'value': round(value, 1), 'unit': 'frames/s',
+        'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
+        'ms_per_step': round(1000.0 * elapsed / args.steps, 3), 'higher_is_better': True,
+        'scaling': 'weak', 'vs_baseline': None, 'dtype': args.precision, 'data': 'synthetic',
+        'config': {'workload': cfg['workload'], 'batch_per_gpu': args.batch,
+                   'global_batch': args.batch * world, 'max_frames': args.frames,
+                   'feat_dim': p['input_freq'], 'vocab': p['num_classes'] + 1,
+                   'parallelism': 'dp%d' % world, 'frames_per_step': total_frames_per_step},
+        'loss_last': losses[-1] if losses else None,
+        'roofline': roofline,
+        'cpu_baseline': cpu,
+    }
+    print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -126,6 +126,8 @@ typedef struct {
   const float* bias2; /* nullable, f32 [N], added too (nn.LSTM b_ih + b_hh) */
   int M, N, K;
   float alpha, beta;
+  int batch;          /* <= 1: single; else `batch` independent products */
+  long long batch_stride_a, batch_stride_b, batch_stride_c; /* elements */
 } asr_gemm_t;
 
 int asr_gemm(const asr_gemm_t* problems, int nprob, int compute_dtype, void* stream);
@@ -157,6 +159,138 @@ int asr_lstm_forward(float* gx_act, const void* whh_f, const void* whh_r, int w_
 int asr_lstm_backward(const float* dy, const void* whh_f, const void* whh_r, int w_dtype,
                       const int32_t* lens, int B, int T, int H, int compute_dtype, float* act_dg,
                       const float* cst, void* workspace, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------ optimizer
+ * Replaces torch.nn.utils.clip_grad_norm(params, max_norm)
+ * (utils/training/training_loop.py:46-50) + torch.optim Adam / SGD /
+ * momentum / nesterov (models/pytorch_v3/base.py:141-194) over the model's
+ * flat f32 parameter and gradient buffers.
+ * asr_grad_sqnorm: out[0] = sum g^2 (deterministic; g 16-B aligned).
+ * asr_optim_step: kind 0 adam (m, v), 1 sgd, 2 momentum (m), 3 nesterov (m);
+ *   the clip coefficient min(1, max_norm / (sqrt(*grad_sqnorm) + 1e-6)) is
+ *   computed on device (grad_sqnorm NULL or max_norm <= 0: no clipping);
+ *   weight decay is L2 added to the gradient (torch semantics); step is the
+ *   1-based step count for Adam bias correction; bf16_shadow (nullable)
+ *   receives a bf16 copy of the updated parameters.
+ */
+size_t asr_grad_sqnorm_workspace_bytes(void);
+int asr_grad_sqnorm(const float* g, long long n, float* out, void* workspace, size_t ws_bytes,
+                    void* stream);
+int asr_optim_step(int kind, float* params, const float* grads, float* m, float* v, long long n,
+                   float lr, float beta1, float beta2, float eps, float weight_decay,
+                   long long step, float momentum, float dampening, const float* grad_sqnorm,
+                   float max_norm, uint16_t* bf16_shadow, void* stream);
+
+/* ------------------------------------------------------- elementwise
+ * asr_dropout: y = x * (u(seed, i) >= p) / (1 - p), u a counter hash (the
+ *   mask is recomputed from (seed, i) in backward: call again on dy).
+ *   Replaces nn.Dropout on the encoder / decoder activations.
+ * asr_embedding_*: nn.Embedding(padding_idx) lookup / gradient (linear.py:50-77;
+ *   trans=1: weight stored [E][V], the one-hot @ W^T of Embedding_LS,
+ *   linear.py:80-116).  idx int64 [n].  Backward is deterministic and skips
+ *   padding_idx (pass -1 for none).
+ * asr_tanh_*: F.tanh of the encoder projection / attention bottleneck.
+ */
+int asr_dropout(const float* x, float* y, long long n, float p, unsigned long long seed,
+                void* stream);
+int asr_embedding_forward(const long long* idx, const float* weight, int n, int V, int E,
+                          int trans, float* out, void* stream);
+int asr_embedding_backward(const long long* idx, const float* dout, int n, int V, int E,
+                           int trans, int padding_idx, float* grad_weight, void* stream);
+int asr_tanh_forward(const float* x, float* y, long long n, void* stream);
+int asr_tanh_backward(const float* y, const float* dy, float* dx, long long n, void* stream);
+
+/* ------------------------------------------------------------ decoding
+ * asr_ctc_best_path: CTC greedy best path (greedy_decoder.py:19-47): per
+ *   utterance argmax over V for t < lens[b] (first maximum wins ties, as
+ *   np.argmax), collapse repeats, drop `blank`.  hyps int32 [B][T] (first
+ *   hyp_lens[b] valid), hyp_lens int32 [B].  Bit-exact with the reference.
+ * asr_row_argmax: out[r] = argmax_v x[r*V + v] (int64; first max on ties).
+ */
+int asr_ctc_best_path(const float* logits, long long stride_t, long long stride_b, int T, int B,
+                      int V, const int32_t* lens, int blank, int32_t* hyps, int32_t* hyp_lens,
+                      void* stream);
+int asr_row_argmax(const float* x, int rows, int V, long long* out, void* stream);
+
+/* -------------------------------------------------------------- losses
+ * Fused softmax cross-entropy + uniform label smoothing over rows of V logits
+ * (attention_seq2seq.py:588-601, criterion.py:51-80, ctc.py:329-337):
+ *   loss = ce_scale * sum_{r: tgt[r]>=0} (lse_r - x[r,tgt[r]])
+ *        + ls_scale * sum_{r in LS rows} -(1/V) sum_v (x[r,v] - lse_r)
+ * LS rows: r = b*T + t with t < lens[b] if lens != NULL, else tgt[r] >= 0.
+ * targets int64 (nullable), -1 = ignore.  workspace keeps the row lse for
+ * backward (asr_xent_workspace_bytes(R)).  Backward writes
+ * dlogits = scale * (*grad_scale) * dloss/dlogits.
+ */
+size_t asr_xent_workspace_bytes(int R);
+int asr_xent_forward(const float* logits, int R, int V, int T, const long long* targets,
+                     const int32_t* lens, float ce_scale, float ls_scale, float* loss_out,
+                     void* workspace, size_t ws_bytes, void* stream);
+int asr_xent_backward(const float* logits, int R, int V, int T, const long long* targets,
+                      const int32_t* lens, float ce_scale, float ls_scale,
+                      const float* grad_scale, float scale, float* dlogits,
+                      const void* workspace, size_t ws_bytes, void* stream);
+int asr_softmax(const float* x, int R, int V, float* y, void* stream);
+
+/* ---------------------------------------------------- attention decoder
+ * Teacher-forced decoder loop of AttentionSeq2seq._decode_train
+ * (attention_seq2seq.py:704-799; bahdanau order, 1-layer LSTMCell decoder
+ * rnn_decoder.py:63-113, location attention attention_layer.py:74-251, 1 head).
+ * Dims: B utterances, T encoder frames, E encoder width, A attention dim,
+ * C conv channels, K conv width (odd), D decoder units, S decoder steps (L+1).
+ * Inputs: enc [B][T][E], enc_a [B][T][A] (= W_enc enc + b), lens [B] (the
+ *   multiplicative energy mask, :216-225), w_ih_ctx = &W_ih[0][emb] with row
+ *   stride ld_ih (the context columns of the decoder LSTMCell W_ih), w_hh
+ *   [4D][D], w_dec [A][D], w_conv [A][C], conv_w [C][K], v [A],
+ *   pre_emb [B][S][4D] (= emb(y_in) W_ih_emb^T + b_ih + b_hh, one GEMM for all
+ *   steps), h0 [B][D] (nullable = zeros; init_dec_state).
+ * Forward outputs (all saved for backward): dec [B][S][D] (dec_out_t; t=0:
+ *   h0), c [B][S][D], gates [B][S][4D], x [B][S][E+D] (= [ctx_{t-1}; h_{t-1}]),
+ *   ctx [B][S][E], aw [B][S][T].
+ * Backward inputs: d_dec_in [B][S][D], d_ctx_in [B][S][E] (from the hoisted
+ *   W_d / W_c GEMMs).  Outputs: gates_dg (dgates over the saved gates; feeds
+ *   dW_ih, dW_hh, db and the embedding gradient), dctx_tot [B][S][E] (feeds
+ *   d enc = aw^T dctx_tot), d_enc_a [B][T][A], d_h0 [B][D] (nullable),
+ *   dwd_all [B][S][A] (dW_dec = dwd^T dec), per-step partials dv_part
+ *   [B][S][A], dwc_part [B][S][A*C], dcw_part [B][S][C*K] (column sums give
+ *   dV, dW_conv, d conv kernel; deterministic).
+ */
+typedef struct {
+  int B, T, E, A, C, K, D, S;
+  float sharpening;
+  int sigmoid_smoothing;
+} asr_attdec_dims_t;
+
+size_t asr_attdec_workspace_bytes(const asr_attdec_dims_t* dims, int compute_dtype,
+                                  int backward);
+int asr_attdec_forward(const asr_attdec_dims_t* dims, int compute_dtype, const float* enc,
+                       const float* enc_a, const int32_t* lens, const float* w_ih_ctx,
+                       long long ld_ih, const float* w_hh, const float* w_dec,
+                       const float* w_conv, const float* conv_w, const float* v,
+                       const float* pre_emb, const float* h0, float* dec, float* c, float* gates,
+                       float* x, float* ctx, float* aw, void* workspace, size_t ws_bytes,
+                       void* stream);
+int asr_attdec_backward(const asr_attdec_dims_t* dims, int compute_dtype, const float* enc,
+                        const float* enc_a, const int32_t* lens, const float* w_ih_ctx,
+                        long long ld_ih, const float* w_hh, const float* w_dec,
+                        const float* w_conv, const float* conv_w, const float* v,
+                        const float* dec, const float* c, const float* aw,
+                        const float* d_dec_in, const float* d_ctx_in, float* gates_dg,
+                        float* dctx_tot, float* d_enc_a, float* d_h0, float* dwd_all,
+                        float* dv_part, float* dwc_part, float* dcw_part, void* workspace,
+                        size_t ws_bytes, void* stream);
+
+/* ----------------------------------------------------------- profiling
+ * Sampled HIP-event timing of the recurrence step kernels on their own stream
+ * (bench.py's live roofline measurement).  asr_prof_begin(stride): bracket
+ * every stride-th launch of each tracked kernel with an event pair.
+ * asr_prof_end: synchronises on the recorded events (the only entry point
+ * that does), fills mean_us[k] (mean launch duration, microseconds) and
+ * launches[k] (all launches seen) for k = 0 lstm forward step, 1 lstm
+ * backward step.
+ */
+int asr_prof_begin(int stride);
+int asr_prof_end(double* mean_us, long long* launches, int nkinds);
 
 #ifdef __cplusplus
 }

@@ -46,6 +46,33 @@ SIGNATURES = {
                                  c_vp, c_vp, c_size, c_vp]),
     'asr_lstm_backward': (c_int, [c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int,
                                   c_vp, c_vp, c_vp, c_size, c_vp]),
+    'asr_grad_sqnorm_workspace_bytes': (c_size, []),
+    'asr_grad_sqnorm': (c_int, [c_vp, c_ll, c_vp, c_vp, c_size, c_vp]),
+    'asr_optim_step': (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_ll, c_float, c_float, c_float,
+                               c_float, c_float, c_ll, c_float, c_float, c_vp, c_float, c_vp,
+                               c_vp]),
+    'asr_dropout': (c_int, [c_vp, c_vp, c_ll, c_float, ctypes.c_ulonglong, c_vp]),
+    'asr_embedding_forward': (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp]),
+    'asr_embedding_backward': (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp,
+                                       c_vp]),
+    'asr_tanh_forward': (c_int, [c_vp, c_vp, c_ll, c_vp]),
+    'asr_tanh_backward': (c_int, [c_vp, c_vp, c_vp, c_ll, c_vp]),
+    'asr_ctc_best_path': (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp,
+                                  c_vp]),
+    'asr_row_argmax': (c_int, [c_vp, c_int, c_int, c_vp, c_vp]),
+    'asr_xent_workspace_bytes': (c_size, [c_int]),
+    'asr_xent_forward': (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_float, c_float, c_vp,
+                                 c_vp, c_size, c_vp]),
+    'asr_xent_backward': (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_float, c_float, c_vp,
+                                  c_float, c_vp, c_vp, c_size, c_vp]),
+    'asr_softmax': (c_int, [c_vp, c_int, c_int, c_vp, c_vp]),
+    'asr_attdec_workspace_bytes': (c_size, [c_vp, c_int, c_int]),
+    'asr_attdec_forward': (c_int, [c_vp, c_int] + [c_vp] * 4 + [c_ll] + [c_vp] * 14 + [c_size,
+                                                                                     c_vp]),
+    'asr_attdec_backward': (c_int, [c_vp, c_int] + [c_vp] * 4 + [c_ll] + [c_vp] * 20 + [c_size,
+                                                                                      c_vp]),
+    'asr_prof_begin': (c_int, [c_int]),
+    'asr_prof_end': (c_int, [c_vp, c_vp, c_int]),
 }
 
 
@@ -60,11 +87,18 @@ class Operand(ctypes.Structure):
     _fields_ = [('ptr', c_vp), ('dtype', c_int), ('trans', c_int), ('map', RowMap)]
 
 
+class AttDecDims(ctypes.Structure):
+    """asr_attdec_dims_t"""
+    _fields_ = [(n, c_int) for n in ('B', 'T', 'E', 'A', 'C', 'K', 'D', 'S')] + [
+        ('sharpening', c_float), ('sigmoid_smoothing', c_int)]
+
+
 class Gemm(ctypes.Structure):
     """asr_gemm_t"""
     _fields_ = [('a', Operand), ('b', Operand), ('c', c_vp), ('c_map', RowMap), ('bias', c_vp),
                 ('bias2', c_vp), ('M', c_int), ('N', c_int), ('K', c_int), ('alpha', c_float),
-                ('beta', c_float)]
+                ('beta', c_float), ('batch', c_int), ('batch_stride_a', c_ll),
+                ('batch_stride_b', c_ll), ('batch_stride_c', c_ll)]
 
 
 class NativeError(RuntimeError):

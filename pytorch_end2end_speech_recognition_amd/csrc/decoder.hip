@@ -1,0 +1,644 @@
+// Teacher-forced location-attention decoder loop on gfx950 -- the sequential
+// part of AttentionSeq2seq._decode_train (attention_seq2seq.py:704-799) with
+// the bahdanau order, one LSTMCell layer (rnn_decoder.py:63-113) and location
+// attention (attention_layer.py:74-98, 155-251).
+//
+// Everything that does not depend on the recurrence is hoisted out of the
+// loop by the host into large GEMMs (the embedding projection of all steps,
+// W_enc, the bottleneck W_d / W_c, the output layer fc and their gradients),
+// so the per-step sequential work is exactly two kernels forward:
+//   cell_fwd : gates = pre_emb[t] + [ctx_{t-1}; h_{t-1}] @ Wcat^T, Wcat = [W_ih_ctx | W_hh]
+//              (16 gate columns x 32 utterances per work-group, MFMA, 4 waves split K)
+//   att_fwd  : one work-group per utterance: conv(aw_{t-1}) -> energy
+//              V.tanh(enc_a + W_dec h + W_conv f) -> multiplicative mask, sharpen,
+//              softmax -> context = sum_t aw enc (enc/enc_a stay L2/MALL resident)
+// and three backward:
+//   r        = dgates_{t+1} @ Wcat       (asr_gemm; d ctx_t and d h_t from step t+1)
+//   att_bwd  : softmax / tanh / conv backward, per-step partial weight gradients
+//   cell_bwd : LSTMCell backward, dgates written over the saved gates
+// Bahdanau quirk (attention_seq2seq.py:750-759): at t = 0 there is no cell step;
+// the first attention uses the initial state h0.
+#include <string.h>
+
+#include "mfma.h"
+
+namespace asr {
+namespace {
+
+struct Dims {
+  int B, T, E, A, C, K, D, S;
+  float sharpen;
+  int sigmoid;
+};
+
+inline Dims to_dims(const asr_attdec_dims_t& d) {
+  return Dims{d.B, d.T, d.E, d.A, d.C, d.K, d.D, d.S, d.sharpening, d.sigmoid_smoothing};
+}
+
+constexpr int MB = 32;   // utterances per cell work-group
+constexpr int CU = 4;    // hidden units per cell work-group (16 gate columns)
+constexpr int ATT_THREADS = 256;
+
+template <typename T>
+__device__ __forceinline__ float ldw(const T* p, long long i);
+template <>
+__device__ __forceinline__ float ldw<float>(const float* p, long long i) { return p[i]; }
+template <>
+__device__ __forceinline__ float ldw<uint16_t>(const uint16_t* p, long long i) { return bf2f(p[i]); }
+
+template <typename T>
+__device__ __forceinline__ bf16x8 frag8g(const T* row, int k, int klim, bool vec) {
+  if (row == nullptr) return as_bf16x8(u16x8{0, 0, 0, 0, 0, 0, 0, 0});
+  if (vec && k + 8 <= klim) {
+    if constexpr (sizeof(T) == 2) return load_bf16x8((const uint16_t*)row + k);
+    else return load_bf16x8_from_f32((const float*)row + k);
+  }
+  u16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (k + j < klim) ? f2bf(ldw<T>(row, k + j)) : (uint16_t)0;
+  return as_bf16x8(r);
+}
+
+// -------------------------------------------------------------- init kernel
+// dec[b,0] = h0, x[b,1,E:] = h0, c[b,0] = 0, gates[b,0,:] = 0
+__global__ void dec_init(Dims d, const float* __restrict__ h0, float* __restrict__ dec,
+                         float* __restrict__ x, float* __restrict__ c, float* __restrict__ gates) {
+  const int b = blockIdx.x;
+  const int ED = d.E + d.D;
+  for (int j = threadIdx.x; j < d.D; j += blockDim.x) {
+    const float h = h0 ? h0[(long long)b * d.D + j] : 0.f;
+    dec[((long long)b * d.S) * d.D + j] = h;
+    c[((long long)b * d.S) * d.D + j] = 0.f;
+    if (d.S > 1) x[((long long)b * d.S + 1) * ED + d.E + j] = h;
+  }
+  for (int j = threadIdx.x; j < 4 * d.D; j += blockDim.x) gates[((long long)b * d.S) * 4 * d.D + j] = 0.f;
+  for (int j = threadIdx.x; j < ED; j += blockDim.x) x[((long long)b * d.S) * ED + j] = 0.f;
+}
+
+// Wcat[g][0:E] = w_ih[g][emb : emb+E] (row stride ld_ih), Wcat[g][E:] = w_hh[g][:]
+template <typename TO>
+__global__ void build_wcat(Dims d, const float* __restrict__ w_ih_ctx, long long ld_ih,
+                           const float* __restrict__ w_hh, TO* __restrict__ out) {
+  const int ED = d.E + d.D;
+  const long long n = 4LL * d.D * ED;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long g = i / ED;
+    const int k = (int)(i % ED);
+    const float v = k < d.E ? w_ih_ctx[g * ld_ih + k] : w_hh[g * d.D + (k - d.E)];
+    if constexpr (sizeof(TO) == 2) out[i] = f2bf(v);
+    else out[i] = v;
+  }
+}
+
+// -------------------------------------------------------------- cell forward
+template <bool BF16, typename TW>
+__global__ void __launch_bounds__(256) cell_fwd(int t, Dims d, const TW* __restrict__ wcat,
+                                                const float* __restrict__ pre_emb,
+                                                float* __restrict__ x, float* __restrict__ gates,
+                                                float* __restrict__ c_all, float* __restrict__ dec,
+                                                int vec) {
+  __shared__ float part[4][MB][16];
+  const int ED = d.E + d.D, G = 4 * d.D;
+  const int u0 = blockIdx.x * CU, b0 = blockIdx.y * MB;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int ra = b0 + (lane & 15), rb = b0 + 16 + (lane & 15);
+  const float* xr0 = ra < d.B ? x + ((long long)ra * d.S + t) * ED : nullptr;
+  const float* xr1 = rb < d.B ? x + ((long long)rb * d.S + t) * ED : nullptr;
+  const int n = lane & 15, g = n >> 2, u = u0 + (n & 3);
+  const TW* wr = u < d.D ? wcat + (long long)(g * d.D + u) * ED : nullptr;
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  if (BF16) {
+    for (int k0 = wave * 32; k0 < ED; k0 += 128) {
+      const int k = k0 + 8 * (lane >> 4);
+      const bf16x8 bw = frag8g<TW>(wr, k, ED, vec != 0);
+      acc0 = mfma_bf16(frag8g<float>(xr0, k, ED, vec != 0), bw, acc0);
+      acc1 = mfma_bf16(frag8g<float>(xr1, k, ED, vec != 0), bw, acc1);
+    }
+  } else {
+    for (int k0 = wave * 4; k0 < ED; k0 += 16) {
+      const int k = k0 + (lane >> 4);
+      const float bw = (wr && k < ED) ? ldw<TW>(wr, k) : 0.f;
+      acc0 = mfma_f32((xr0 && k < ED) ? xr0[k] : 0.f, bw, acc0);
+      acc1 = mfma_f32((xr1 && k < ED) ? xr1[k] : 0.f, bw, acc1);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    part[wave][4 * (lane >> 4) + r][lane & 15] = acc0[r];
+    part[wave][16 + 4 * (lane >> 4) + r][lane & 15] = acc1[r];
+  }
+  __syncthreads();
+  if (threadIdx.x >= MB * CU) return;
+  const int row = threadIdx.x >> 2, uu = threadIdx.x & 3;
+  const int b = b0 + row, j = u0 + uu;
+  if (b >= d.B || j >= d.D) return;
+  const long long gb = ((long long)b * d.S + t) * G + j;
+  float pre[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    pre[q] = part[0][row][q * 4 + uu] + part[1][row][q * 4 + uu] + part[2][row][q * 4 + uu] +
+             part[3][row][q * 4 + uu] + pre_emb[gb + (long long)q * d.D];
+  const float cprev = c_all[((long long)b * d.S + t - 1) * d.D + j];
+  const float ig = sigmoidf_(pre[0]), fg = sigmoidf_(pre[1]);
+  const float gg = tanhf_(pre[2]), og = sigmoidf_(pre[3]);
+  const float c = fg * cprev + ig * gg;
+  const float h = og * tanhf_(c);
+  c_all[((long long)b * d.S + t) * d.D + j] = c;
+  dec[((long long)b * d.S + t) * d.D + j] = h;
+  gates[gb] = ig;
+  gates[gb + d.D] = fg;
+  gates[gb + 2 * d.D] = gg;
+  gates[gb + 3 * d.D] = og;
+  if (t + 1 < d.S) x[((long long)b * d.S + t + 1) * ED + d.E + j] = h;
+}
+
+// -------------------------------------------------------- attention helpers
+struct AttLds {
+  float* aw;   // [T]   aw_{t-1}
+  float* f;    // [T*C] conv features
+  float* e;    // [T]   energies -> weights
+  float* wd;   // [A]   W_dec h
+  float* wc;   // [A*C] W_conv
+  float* cw;   // [C*K] conv kernel
+  float* v;    // [A]
+  float* h;    // [D]
+  float* red;  // [64]
+};
+
+__host__ __device__ inline size_t att_lds_floats(const Dims& d) {
+  return (size_t)d.T * (2 + d.C) + (size_t)d.A * (2 + d.C) + (size_t)d.C * d.K + d.D + 64 +
+         (size_t)d.T * d.C /* backward: d_f */ + d.T /* backward: d_aw */ + d.A /* d_wd */;
+}
+
+__device__ inline AttLds carve(float* s, const Dims& d) {
+  AttLds L;
+  L.aw = s; s += d.T;
+  L.f = s; s += (size_t)d.T * d.C;
+  L.e = s; s += d.T;
+  L.wd = s; s += d.A;
+  L.wc = s; s += (size_t)d.A * d.C;
+  L.cw = s; s += (size_t)d.C * d.K;
+  L.v = s; s += d.A;
+  L.h = s; s += d.D;
+  L.red = s;
+  return L;
+}
+
+__device__ __forceinline__ float block_reduce(float v, float* red, bool is_max) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = is_max ? wave_max(v) : wave_sum(v);
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float r = red[0];
+  for (int i = 1; i < nw; ++i) r = is_max ? fmaxf(r, red[i]) : r + red[i];
+  return r;
+}
+
+// Shared prologue of att_fwd / att_bwd: aw_{t-1}, weights, W_dec h, conv features.
+__device__ void att_prologue(int t, const Dims& d, int b, const AttLds& L,
+                             const float* __restrict__ w_dec, const float* __restrict__ w_conv,
+                             const float* __restrict__ conv_w, const float* __restrict__ vw,
+                             const float* __restrict__ dec, const float* __restrict__ aw_all) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  for (int i = tid; i < d.T; i += nt)
+    L.aw[i] = t > 0 ? aw_all[((long long)b * d.S + t - 1) * d.T + i] : 0.f;
+  for (int i = tid; i < d.A * d.C; i += nt) L.wc[i] = w_conv[i];
+  for (int i = tid; i < d.C * d.K; i += nt) L.cw[i] = conv_w[i];
+  for (int i = tid; i < d.A; i += nt) L.v[i] = vw[i];
+  for (int i = tid; i < d.D; i += nt) L.h[i] = dec[((long long)b * d.S + t) * d.D + i];
+  __syncthreads();
+  for (int a = tid; a < d.A; a += nt) {
+    const float* wr = w_dec + (long long)a * d.D;
+    float s = 0.f;
+    for (int k = 0; k < d.D; ++k) s += wr[k] * L.h[k];
+    L.wd[a] = s;
+  }
+  const int half = d.K / 2;
+  for (int i = tid; i < d.T * d.C; i += nt) {
+    const int tt = i / d.C, c = i % d.C;
+    float s = 0.f;
+    const float* cw = L.cw + c * d.K;
+    const int k0 = max(0, half - tt), k1 = min(d.K, d.T + half - tt);
+    for (int k = k0; k < k1; ++k) s += cw[k] * L.aw[tt + k - half];
+    L.f[i] = s;
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ float att_pre(const Dims& d, const AttLds& L, const float* ea_row,
+                                         int tt, int a) {
+  float p = ea_row[a] + L.wd[a];
+  const float* fr = L.f + tt * d.C;
+  const float* wr = L.wc + a * d.C;
+  for (int c = 0; c < d.C; ++c) p += fr[c] * wr[c];
+  return p;
+}
+
+// -------------------------------------------------------------- attention fwd
+__global__ void __launch_bounds__(ATT_THREADS) att_fwd(
+    int t, Dims d, const float* __restrict__ enc, const float* __restrict__ enc_a,
+    const int32_t* __restrict__ lens, const float* __restrict__ w_dec,
+    const float* __restrict__ w_conv, const float* __restrict__ conv_w,
+    const float* __restrict__ vw, const float* __restrict__ dec, float* __restrict__ aw_all,
+    float* __restrict__ ctx_all, float* __restrict__ x) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const Dims dd = d;
+  AttLds L = carve(smem, dd);
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
+  att_prologue(t, dd, b, L, w_dec, w_conv, conv_w, vw, dec, aw_all);
+  // energies: one wave per frame, lanes over the attention dim
+  for (int tt = w; tt < d.T; tt += nw) {
+    const float* ea = enc_a + ((long long)b * d.T + tt) * d.A;
+    float s = 0.f;
+    for (int a = lane; a < d.A; a += 64) s += L.v[a] * tanhf(att_pre(dd, L, ea, tt, a));
+    s = wave_sum(s);
+    if (lane == 0) L.e[tt] = s;
+  }
+  __syncthreads();
+  const int len = lens[b];
+  float mx = -__builtin_huge_valf();
+  for (int i = tid; i < d.T; i += blockDim.x) {
+    float e = (i < len ? L.e[i] : 0.f) * d.sharpen;   // multiplicative mask (:216-225)
+    L.e[i] = e;
+    mx = fmaxf(mx, e);
+  }
+  __syncthreads();
+  if (d.sigmoid) {
+    for (int i = tid; i < d.T; i += blockDim.x) L.e[i] = sigmoidf_(L.e[i]);
+  } else {
+    mx = block_reduce(mx, L.red, true);
+    float sm = 0.f;
+    for (int i = tid; i < d.T; i += blockDim.x) {
+      const float p = __expf(L.e[i] - mx);
+      L.e[i] = p;
+      sm += p;
+    }
+    sm = block_reduce(sm, L.red, false);
+    const float inv = 1.f / sm;
+    for (int i = tid; i < d.T; i += blockDim.x) L.e[i] *= inv;
+  }
+  __syncthreads();
+  for (int i = tid; i < d.T; i += blockDim.x) aw_all[((long long)b * d.S + t) * d.T + i] = L.e[i];
+  const int ED = d.E + d.D;
+  for (int e = tid; e < d.E; e += blockDim.x) {
+    const float* er = enc + (long long)b * d.T * d.E + e;
+    float s = 0.f;
+    for (int tt = 0; tt < d.T; ++tt) s += L.e[tt] * er[(long long)tt * d.E];
+    ctx_all[((long long)b * d.S + t) * d.E + e] = s;
+    if (t + 1 < d.S) x[((long long)b * d.S + t + 1) * ED + e] = s;
+  }
+}
+
+// -------------------------------------------------------------- attention bwd
+// d_ctx total for step t = d_ctx_in[b,t] + r[b, 0:E]  (stored into dctx_tot)
+// d_aw_t = carry[b] (from step t+1); writes carry[b] = d aw_{t-1}
+__global__ void __launch_bounds__(ATT_THREADS) att_bwd(
+    int t, Dims d, const float* __restrict__ enc, const float* __restrict__ enc_a,
+    const int32_t* __restrict__ lens, const float* __restrict__ w_dec,
+    const float* __restrict__ w_conv, const float* __restrict__ conv_w,
+    const float* __restrict__ vw, const float* __restrict__ dec,
+    const float* __restrict__ aw_all, const float* __restrict__ dctx_in,
+    const float* __restrict__ r, float* __restrict__ carry, float* __restrict__ dctx_tot,
+    float* __restrict__ d_enc_a, float* __restrict__ ddec_att, float* __restrict__ dwd_all,
+    float* __restrict__ dv_part, float* __restrict__ dwc_part, float* __restrict__ dcw_part) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const Dims dd = d;
+  AttLds L = carve(smem, dd);
+  float* dF = L.red + 64;           // [T*C]
+  float* dA = dF + (size_t)d.T * d.C;  // [T]  d aw_t, then d energy
+  float* dWd = dA + d.T;            // [A]
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
+  const int ED = d.E + d.D;
+  att_prologue(t, dd, b, L, w_dec, w_conv, conv_w, vw, dec, aw_all);
+  const float* awt = aw_all + ((long long)b * d.S + t) * d.T;
+  for (int i = tid; i < d.T; i += blockDim.x) {
+    L.e[i] = awt[i];
+    dA[i] = carry[(long long)b * d.T + i];
+  }
+  // total d_ctx (into LDS-free global buffer, read back below)
+  float* dct = dctx_tot + ((long long)b * d.S + t) * d.E;
+  for (int e = tid; e < d.E; e += blockDim.x)
+    dct[e] = dctx_in[((long long)b * d.S + t) * d.E + e] + (r ? r[(long long)b * ED + e] : 0.f);
+  for (int a = tid; a < d.A; a += blockDim.x) dWd[a] = 0.f;
+  __syncthreads();
+  // d aw[tt] += enc[tt,:] . d_ctx   (one wave per frame)
+  for (int tt = w; tt < d.T; tt += nw) {
+    const float* er = enc + ((long long)b * d.T + tt) * d.E;
+    float s = 0.f;
+    for (int e = lane; e < d.E; e += 64) s += er[e] * dct[e];
+    s = wave_sum(s);
+    if (lane == 0) dA[tt] += s;
+  }
+  __syncthreads();
+  // softmax / sigmoid backward -> d energy (after mask & sharpen)
+  const int len = lens[b];
+  if (d.sigmoid) {
+    for (int i = tid; i < d.T; i += blockDim.x) dA[i] = dA[i] * L.e[i] * (1.f - L.e[i]);
+  } else {
+    float s = 0.f;
+    for (int i = tid; i < d.T; i += blockDim.x) s += L.e[i] * dA[i];
+    s = block_reduce(s, L.red, false);
+    for (int i = tid; i < d.T; i += blockDim.x) dA[i] = L.e[i] * (dA[i] - s);
+  }
+  __syncthreads();
+  for (int i = tid; i < d.T; i += blockDim.x) dA[i] = (i < len ? dA[i] : 0.f) * d.sharpen;
+  for (int i = tid; i < d.T * d.C; i += blockDim.x) dF[i] = 0.f;
+  __syncthreads();
+  // per frame: d_pre[a] = dE * V[a] * (1 - tanh^2); accumulate dV, dWd, dWconv (registers),
+  // d_enc_a (global RMW, utterance-private), d_f (LDS, per (tt, c) over a: wave reduce)
+  float* dvp = dv_part + ((long long)b * d.S + t) * d.A;
+  float* dwcp = dwc_part + ((long long)b * d.S + t) * d.A * d.C;
+  // each lane owns attention rows a = lane, lane+64, ... (<= 4 rows => A <= 256)
+  float accV[4] = {0.f, 0.f, 0.f, 0.f}, accWd[4] = {0.f, 0.f, 0.f, 0.f};
+  float accWc[4][16];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int c = 0; c < 16; ++c) accWc[q][c] = 0.f;
+  for (int tt = w; tt < d.T; tt += nw) {
+    const float de = dA[tt];
+    const float* ea = enc_a + ((long long)b * d.T + tt) * d.A;
+    float* dea = d_enc_a + ((long long)b * d.T + tt) * d.A;
+    float dfc[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) dfc[c] = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int a = lane + 64 * q;
+      if (a < d.A) {
+        const float th = tanhf(att_pre(dd, L, ea, tt, a));
+        const float dp = de * L.v[a] * (1.f - th * th);
+        accV[q] += de * th;
+        accWd[q] += dp;
+        dea[a] += dp;
+        const float* fr = L.f + tt * d.C;
+        const float* wr = L.wc + a * d.C;
+#pragma unroll
+        for (int c = 0; c < 16; ++c)
+          if (c < d.C) {
+            accWc[q][c] += dp * fr[c];
+            dfc[c] += dp * wr[c];
+          }
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      if (c < d.C) {
+        const float s = wave_sum(dfc[c]);
+        if (lane == 0) dF[tt * d.C + c] = s;
+      }
+    }
+  }
+  // combine the per-wave register partials through LDS (reuse L.f region is still needed: use
+  // atomics on LDS for the small A / A*C partial sums -- order fixed per wave, 4 waves)
+  __syncthreads();
+  for (int pass = 0; pass < nw; ++pass) {
+    if (w == pass) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int a = lane + 64 * q;
+        if (a < d.A) {
+          if (pass == 0) { dvp[a] = accV[q]; dWd[a] = accWd[q]; }
+          else { dvp[a] += accV[q]; dWd[a] += accWd[q]; }
+#pragma unroll
+          for (int c = 0; c < 16; ++c)
+            if (c < d.C) {
+              if (pass == 0) dwcp[a * d.C + c] = accWc[q][c];
+              else dwcp[a * d.C + c] += accWc[q][c];
+            }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // d W_dec input: ddec_att[b, k] = sum_a W_dec[a, k] dWd[a];  dwd_all[b,t,:] = dWd
+  for (int a = tid; a < d.A; a += blockDim.x) dwd_all[((long long)b * d.S + t) * d.A + a] = dWd[a];
+  for (int k = tid; k < d.D; k += blockDim.x) {
+    float s = 0.f;
+    for (int a = 0; a < d.A; ++a) s += w_dec[(long long)a * d.D + k] * dWd[a];
+    ddec_att[(long long)b * d.D + k] = s;
+  }
+  // conv backward: d aw_{t-1}[j] = sum_c sum_k dF[j - k + half, c] * cw[c, k]
+  const int half = d.K / 2;
+  for (int j = tid; j < d.T; j += blockDim.x) {
+    float s = 0.f;
+    for (int c = 0; c < d.C; ++c) {
+      const float* cw = L.cw + c * d.K;
+      const int k0 = max(0, j + half - (d.T - 1)), k1 = min(d.K, j + half + 1);
+      for (int k = k0; k < k1; ++k) s += dF[(j - k + half) * d.C + c] * cw[k];
+    }
+    carry[(long long)b * d.T + j] = s;
+  }
+  // d conv kernel partial: dcw[c, k] = sum_tt dF[tt, c] * aw_{t-1}[tt + k - half]
+  float* dcwp = dcw_part + ((long long)b * d.S + t) * d.C * d.K;
+  for (int i = tid; i < d.C * d.K; i += blockDim.x) {
+    const int c = i / d.K, k = i % d.K;
+    const int t0 = max(0, half - k), t1 = min(d.T, d.T + half - k);
+    float s = 0.f;
+    for (int tt = t0; tt < t1; ++tt) s += dF[tt * d.C + c] * L.aw[tt + k - half];
+    dcwp[i] = s;
+  }
+}
+
+// -------------------------------------------------------------- cell backward
+// dh = d_dec_in[b,t] + r[b, E:] + ddec_att[b];  writes dgates over gates (t >= 1),
+// or d_h0 (t == 0).
+__global__ void cell_bwd(int t, Dims d, const float* __restrict__ d_dec_in,
+                         const float* __restrict__ r, const float* __restrict__ ddec_att,
+                         float* __restrict__ gates, const float* __restrict__ c_all,
+                         float* __restrict__ dc, float* __restrict__ d_h0) {
+  const int ED = d.E + d.D, G = 4 * d.D;
+  const long long n = (long long)d.B * d.D;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int b = (int)(i / d.D), j = (int)(i % d.D);
+    const float dh = d_dec_in[((long long)b * d.S + t) * d.D + j] +
+                     (r ? r[(long long)b * ED + d.E + j] : 0.f) + ddec_att[i];
+    if (t == 0) {
+      if (d_h0) d_h0[i] = dh;
+      continue;
+    }
+    const long long gb = ((long long)b * d.S + t) * G + j;
+    const float ig = gates[gb], fg = gates[gb + d.D], gg = gates[gb + 2 * d.D],
+                og = gates[gb + 3 * d.D];
+    const float c = c_all[((long long)b * d.S + t) * d.D + j];
+    const float cp = c_all[((long long)b * d.S + t - 1) * d.D + j];
+    const float tc = tanhf(c);
+    const float dcell = dc[i] + dh * og * (1.f - tc * tc);
+    gates[gb] = dcell * gg * ig * (1.f - ig);
+    gates[gb + d.D] = dcell * cp * fg * (1.f - fg);
+    gates[gb + 2 * d.D] = dcell * ig * (1.f - gg * gg);
+    gates[gb + 3 * d.D] = dh * tc * og * (1.f - og);
+    dc[i] = dcell * fg;
+  }
+}
+
+size_t wcat_bytes(const Dims& d, int cdt) {
+  return ((size_t)4 * d.D * (d.E + d.D) * (cdt == ASR_DT_BF16 ? 2 : 4) + 255) & ~size_t(255);
+}
+
+int check_dims(const Dims& d) {
+  ASR_REQUIRE(d.B > 0 && d.T > 0 && d.E > 0 && d.A > 0 && d.C > 0 && d.K > 0 && d.D > 0 &&
+                  d.S > 0,
+              ASR_ERR_ARG, "attdec: bad dims");
+  ASR_REQUIRE(d.A <= 256 && d.C <= 16, ASR_ERR_UNSUPPORTED,
+              "attdec: attention_dim <= 256 and conv channels <= 16 supported (A=%d C=%d)", d.A,
+              d.C);
+  ASR_REQUIRE(d.K % 2 == 1, ASR_ERR_ARG, "attdec: conv width must be odd");
+  ASR_REQUIRE(att_lds_floats(d) * 4 <= 160 * 1024, ASR_ERR_UNSUPPORTED,
+              "attdec: LDS need %zu B > 160 KiB", att_lds_floats(d) * 4);
+  return ASR_OK;
+}
+
+}  // namespace
+}  // namespace asr
+
+using namespace asr;
+
+extern "C" size_t asr_attdec_workspace_bytes(const asr_attdec_dims_t* dims, int compute_dtype,
+                                             int backward) {
+  const Dims d = to_dims(*dims);
+  size_t n = wcat_bytes(d, compute_dtype);
+  if (backward) {
+    n += ((size_t)d.B * (d.E + d.D) * 4 + 255) & ~size_t(255);  // r
+    n += ((size_t)d.B * d.T * 4 + 255) & ~size_t(255);          // carry
+    n += ((size_t)d.B * d.D * 4 + 255) & ~size_t(255);          // ddec_att
+    n += ((size_t)d.B * d.D * 4 + 255) & ~size_t(255);          // dc
+  }
+  return n;
+}
+
+extern "C" int asr_attdec_forward(const asr_attdec_dims_t* dims, int compute_dtype,
+                                  const float* enc, const float* enc_a, const int32_t* lens,
+                                  const float* w_ih_ctx, long long ld_ih, const float* w_hh,
+                                  const float* w_dec, const float* w_conv, const float* conv_w,
+                                  const float* v, const float* pre_emb, const float* h0,
+                                  float* dec, float* c_all, float* gates, float* x,
+                                  float* ctx_all, float* aw_all, void* workspace,
+                                  size_t ws_bytes, void* stream) {
+  ASR_REQUIRE(dims, ASR_ERR_ARG, "attdec: dims is null");
+  const Dims d = to_dims(*dims);
+  int rc = check_dims(d);
+  if (rc) return rc;
+  ASR_REQUIRE(enc && enc_a && lens && w_ih_ctx && w_hh && w_dec && w_conv && conv_w && v &&
+                  pre_emb && dec && c_all && gates && x && ctx_all && aw_all && workspace,
+              ASR_ERR_ARG, "attdec_forward: null pointer");
+  ASR_REQUIRE(ws_bytes >= asr_attdec_workspace_bytes(dims, compute_dtype, 0), ASR_ERR_WORKSPACE,
+              "attdec_forward: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const bool bf = compute_dtype == ASR_DT_BF16;
+  const long long nw = 4LL * d.D * (d.E + d.D);
+  const int gb = (int)((nw + 255) / 256 < 4096 ? (nw + 255) / 256 : 4096);
+  if (bf)
+    hipLaunchKernelGGL((build_wcat<uint16_t>), dim3(gb), dim3(256), 0, s, d, w_ih_ctx, ld_ih, w_hh,
+                       (uint16_t*)workspace);
+  else
+    hipLaunchKernelGGL((build_wcat<float>), dim3(gb), dim3(256), 0, s, d, w_ih_ctx, ld_ih, w_hh,
+                       (float*)workspace);
+  ASR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(dec_init, dim3(d.B), dim3(256), 0, s, d, h0, dec, x, c_all, gates);
+  ASR_LAUNCH_CHECK();
+  const size_t lds = att_lds_floats(d) * 4;
+  const int vec = ((d.E + d.D) % 8 == 0) ? 1 : 0;
+  const dim3 cg(ceil_div(d.D, CU), ceil_div(d.B, MB));
+  for (int t = 0; t < d.S; ++t) {
+    if (t > 0) {
+      if (bf)
+        hipLaunchKernelGGL((cell_fwd<true, uint16_t>), cg, dim3(256), 0, s, t, d,
+                           (const uint16_t*)workspace, pre_emb, x, gates, c_all, dec, vec);
+      else
+        hipLaunchKernelGGL((cell_fwd<false, float>), cg, dim3(256), 0, s, t, d,
+                           (const float*)workspace, pre_emb, x, gates, c_all, dec, vec);
+      ASR_LAUNCH_CHECK();
+    }
+    hipLaunchKernelGGL(att_fwd, dim3(d.B), dim3(ATT_THREADS), lds, s, t, d, enc, enc_a, lens,
+                       w_dec, w_conv, conv_w, v, dec, aw_all, ctx_all, x);
+    ASR_LAUNCH_CHECK();
+  }
+  return ASR_OK;
+}
+
+extern "C" int asr_attdec_backward(const asr_attdec_dims_t* dims, int compute_dtype,
+                                   const float* enc, const float* enc_a, const int32_t* lens,
+                                   const float* w_ih_ctx, long long ld_ih, const float* w_hh,
+                                   const float* w_dec, const float* w_conv, const float* conv_w,
+                                   const float* v, const float* dec, const float* c_all,
+                                   const float* aw_all, const float* d_dec_in,
+                                   const float* d_ctx_in, float* gates_dg, float* dctx_tot,
+                                   float* d_enc_a, float* d_h0, float* dwd_all, float* dv_part,
+                                   float* dwc_part, float* dcw_part, void* workspace,
+                                   size_t ws_bytes, void* stream) {
+  ASR_REQUIRE(dims, ASR_ERR_ARG, "attdec: dims is null");
+  const Dims d = to_dims(*dims);
+  int rc = check_dims(d);
+  if (rc) return rc;
+  ASR_REQUIRE(enc && enc_a && lens && w_ih_ctx && w_hh && w_dec && w_conv && conv_w && v &&
+                  dec && c_all && aw_all && d_dec_in && d_ctx_in && gates_dg && dctx_tot &&
+                  d_enc_a && dwd_all && dv_part && dwc_part && dcw_part && workspace,
+              ASR_ERR_ARG, "attdec_backward: null pointer");
+  ASR_REQUIRE(ws_bytes >= asr_attdec_workspace_bytes(dims, compute_dtype, 1), ASR_ERR_WORKSPACE,
+              "attdec_backward: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const bool bf = compute_dtype == ASR_DT_BF16;
+  const int ED = d.E + d.D, G = 4 * d.D;
+  char* p = (char*)workspace;
+  void* wcat = p;
+  p += wcat_bytes(d, compute_dtype);
+  float* r = (float*)p;
+  p += ((size_t)d.B * ED * 4 + 255) & ~size_t(255);
+  float* carry = (float*)p;
+  p += ((size_t)d.B * d.T * 4 + 255) & ~size_t(255);
+  float* ddec_att = (float*)p;
+  p += ((size_t)d.B * d.D * 4 + 255) & ~size_t(255);
+  float* dc = (float*)p;
+  const long long nw = 4LL * d.D * ED;
+  const int gb = (int)((nw + 255) / 256 < 4096 ? (nw + 255) / 256 : 4096);
+  if (bf)
+    hipLaunchKernelGGL((build_wcat<uint16_t>), dim3(gb), dim3(256), 0, s, d, w_ih_ctx, ld_ih, w_hh,
+                       (uint16_t*)wcat);
+  else
+    hipLaunchKernelGGL((build_wcat<float>), dim3(gb), dim3(256), 0, s, d, w_ih_ctx, ld_ih, w_hh,
+                       (float*)wcat);
+  ASR_LAUNCH_CHECK();
+  ASR_CHECK_HIP(hipMemsetAsync(carry, 0, (size_t)d.B * d.T * 4, s));
+  ASR_CHECK_HIP(hipMemsetAsync(dc, 0, (size_t)d.B * d.D * 4, s));
+  ASR_CHECK_HIP(hipMemsetAsync(d_enc_a, 0, (size_t)d.B * d.T * d.A * 4, s));
+  const size_t lds = att_lds_floats(d) * 4;
+  const long long nbd = (long long)d.B * d.D;
+  const int cgrid = (int)((nbd + 255) / 256);
+  for (int t = d.S - 1; t >= 0; --t) {
+    const float* rp = nullptr;
+    if (t + 1 < d.S) {
+      // r = dgates_{t+1} (B x 4D, row stride S*4D) @ Wcat (4D x ED)
+      asr_gemm_t g;
+      memset(&g, 0, sizeof(g));
+      g.a.ptr = gates_dg + (long long)(t + 1) * G;
+      g.a.dtype = ASR_DT_F32;
+      g.a.trans = 0;
+      g.a.map.stride_t = (long long)d.S * G;
+      g.b.ptr = wcat;
+      g.b.dtype = bf ? ASR_DT_BF16 : ASR_DT_F32;
+      g.b.trans = 1;
+      g.b.map.stride_t = ED;
+      g.c = r;
+      g.c_map.stride_t = ED;
+      g.M = d.B; g.N = ED; g.K = G;
+      g.alpha = 1.f; g.beta = 0.f; g.batch = 1;
+      rc = asr_gemm(&g, 1, compute_dtype, stream);
+      if (rc) return rc;
+      rp = r;
+    }
+    hipLaunchKernelGGL(att_bwd, dim3(d.B), dim3(ATT_THREADS), lds, s, t, d, enc, enc_a, lens,
+                       w_dec, w_conv, conv_w, v, dec, aw_all, d_ctx_in, rp, carry, dctx_tot,
+                       d_enc_a, ddec_att, dwd_all, dv_part, dwc_part, dcw_part);
+    ASR_LAUNCH_CHECK();
+    hipLaunchKernelGGL(cell_bwd, dim3(cgrid), dim3(256), 0, s, t, d, d_dec_in, rp, ddec_att,
+                       gates_dg, c_all, dc, d_h0);
+    ASR_LAUNCH_CHECK();
+  }
+  return ASR_OK;
+}

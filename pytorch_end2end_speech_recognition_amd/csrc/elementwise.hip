@@ -1,0 +1,127 @@
+// Small memory-bound ops of the step (gfx950): dropout with a counter-based
+// RNG (mask recomputed in backward, never stored), embedding lookup /
+// gradient, tanh.  Vectorised 16 B per lane where the layout allows.
+#include "common.h"
+
+namespace asr {
+namespace {
+
+// 64-bit counter hash -> uniform [0,1) (splitmix64 finaliser).
+__device__ __forceinline__ float u01(unsigned long long seed, unsigned long long i) {
+  unsigned long long z = seed + 0x9E3779B97F4A7C15ull * (i + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (float)(z >> 40) * (1.0f / 16777216.0f);
+}
+
+__global__ void dropout_kernel(const float* __restrict__ x, float* __restrict__ y, long long n,
+                               float p, unsigned long long seed) {
+  const float scale = 1.f / (1.f - p);
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    y[i] = u01(seed, i) >= p ? x[i] * scale : 0.f;
+}
+
+// out[r, :] = W[idx[r], :]   (W [V][E]) or W[:, idx[r]] (W^T stored [E][V])
+__global__ void embedding_fwd(const long long* __restrict__ idx, const float* __restrict__ w,
+                              int n, int V, int E, int trans, float* __restrict__ out) {
+  const long long total = (long long)n * E;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int r = (int)(i / E), e = (int)(i % E);
+    long long v = idx[r];
+    v = v < 0 ? 0 : (v >= V ? V - 1 : v);
+    out[i] = trans ? w[(long long)e * V + v] : w[v * E + e];
+  }
+}
+
+// gw[v, e] += sum_{r: idx[r]==v} dout[r, e]  (skip v == padding_idx); fixed
+// order over r -> deterministic.  One thread per (v, e).
+__global__ void embedding_bwd(const long long* __restrict__ idx, const float* __restrict__ dout,
+                              int n, int V, int E, int trans, int padding_idx,
+                              float* __restrict__ gw) {
+  const long long total = (long long)V * E;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int v = (int)(i / E), e = (int)(i % E);
+    if (v == padding_idx) continue;
+    float s = 0.f;
+    for (int r = 0; r < n; ++r)
+      if (idx[r] == v) s += dout[(long long)r * E + e];
+    if (trans) gw[(long long)e * V + v] += s;
+    else gw[i] += s;
+  }
+}
+
+__global__ void tanh_fwd(const float* __restrict__ x, float* __restrict__ y, long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    y[i] = tanhf(x[i]);
+}
+
+__global__ void tanh_bwd(const float* __restrict__ y, const float* __restrict__ dy,
+                         float* __restrict__ dx, long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    dx[i] = dy[i] * (1.f - y[i] * y[i]);
+}
+
+inline int grid_for(long long n) {
+  long long b = (n + 255) / 256;
+  return (int)(b < 4096 ? (b > 0 ? b : 1) : 4096);
+}
+
+}  // namespace
+}  // namespace asr
+
+using namespace asr;
+
+extern "C" int asr_dropout(const float* x, float* y, long long n, float p,
+                           unsigned long long seed, void* stream) {
+  ASR_REQUIRE(x && y, ASR_ERR_ARG, "dropout: null pointer");
+  ASR_REQUIRE(p >= 0.f && p < 1.f, ASR_ERR_ARG, "dropout: p=%f", p);
+  if (n <= 0) return ASR_OK;
+  hipLaunchKernelGGL(dropout_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, y,
+                     n, p, seed);
+  ASR_LAUNCH_CHECK();
+  return ASR_OK;
+}
+
+extern "C" int asr_embedding_forward(const long long* idx, const float* weight, int n, int V,
+                                     int E, int trans, float* out, void* stream) {
+  ASR_REQUIRE(idx && weight && out, ASR_ERR_ARG, "embedding: null pointer");
+  if (n <= 0) return ASR_OK;
+  hipLaunchKernelGGL(embedding_fwd, dim3(grid_for((long long)n * E)), dim3(256), 0,
+                     (hipStream_t)stream, idx, weight, n, V, E, trans, out);
+  ASR_LAUNCH_CHECK();
+  return ASR_OK;
+}
+
+extern "C" int asr_embedding_backward(const long long* idx, const float* dout, int n, int V,
+                                      int E, int trans, int padding_idx, float* grad_weight,
+                                      void* stream) {
+  ASR_REQUIRE(idx && dout && grad_weight, ASR_ERR_ARG, "embedding_backward: null pointer");
+  if (n <= 0) return ASR_OK;
+  hipLaunchKernelGGL(embedding_bwd, dim3(grid_for((long long)V * E)), dim3(256), 0,
+                     (hipStream_t)stream, idx, dout, n, V, E, trans, padding_idx, grad_weight);
+  ASR_LAUNCH_CHECK();
+  return ASR_OK;
+}
+
+extern "C" int asr_tanh_forward(const float* x, float* y, long long n, void* stream) {
+  ASR_REQUIRE(x && y, ASR_ERR_ARG, "tanh: null pointer");
+  if (n <= 0) return ASR_OK;
+  hipLaunchKernelGGL(tanh_fwd, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, y, n);
+  ASR_LAUNCH_CHECK();
+  return ASR_OK;
+}
+
+extern "C" int asr_tanh_backward(const float* y, const float* dy, float* dx, long long n,
+                                 void* stream) {
+  ASR_REQUIRE(y && dy && dx, ASR_ERR_ARG, "tanh_backward: null pointer");
+  if (n <= 0) return ASR_OK;
+  hipLaunchKernelGGL(tanh_bwd, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, y, dy, dx, n);
+  ASR_LAUNCH_CHECK();
+  return ASR_OK;
+}

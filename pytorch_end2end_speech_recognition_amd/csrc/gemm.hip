@@ -44,6 +44,8 @@ struct Problem {
   const float* bias2;
   int M, N, K;
   float alpha, beta;
+  int batch;
+  long long sA, sB, sC;
 };
 
 struct Params {
@@ -151,7 +153,14 @@ __global__ void __launch_bounds__(NT) gemm_kernel(Params P) {
   void* As = smem;
   void* Bs = smem + TILE_ELEMS * ESZ;
 
-  const Problem& pr = P.p[blockIdx.z];
+  const int zb = blockIdx.z / P.nprob, zp = blockIdx.z % P.nprob;
+  Problem pr = P.p[zp];
+  if (zb >= pr.batch) return;
+  if (zb > 0) {  // batched product: shift every base by its batch stride
+    pr.a.map.base = (const char*)pr.a.map.base + zb * pr.sA * (pr.a.dtype == ASR_DT_F32 ? 4 : 2);
+    pr.b.map.base = (const char*)pr.b.map.base + zb * pr.sB * (pr.b.dtype == ASR_DT_F32 ? 4 : 2);
+    pr.c.base = (const char*)pr.c.base + zb * pr.sC * 4;
+  }
   const int gm = (pr.M + BM - 1) / BM, gn = (pr.N + BN - 1) / BN;
   const int nwg = gm * gn;
   int id = blockIdx.x;
@@ -308,7 +317,7 @@ extern "C" int asr_gemm(const asr_gemm_t* problems, int nprob, int compute_dtype
   ASR_REQUIRE(problems && nprob >= 1 && nprob <= 2, ASR_ERR_ARG, "gemm: nprob must be 1 or 2");
   Params P;
   P.nprob = nprob;
-  int maxwg = 0;
+  int maxwg = 0, maxb = 1;
   for (int i = 0; i < nprob; ++i) {
     const asr_gemm_t& g = problems[i];
     ASR_REQUIRE(g.M >= 0 && g.N >= 0 && g.K >= 0, ASR_ERR_ARG, "gemm: negative size");
@@ -324,17 +333,27 @@ extern "C" int asr_gemm(const asr_gemm_t* problems, int nprob, int compute_dtype
     p.M = g.M; p.N = g.N; p.K = g.K;
     p.alpha = g.alpha;
     p.beta = g.beta;
+    p.batch = g.batch > 1 ? g.batch : 1;
+    p.sA = g.batch_stride_a;
+    p.sB = g.batch_stride_b;
+    p.sC = g.batch_stride_c;
+    if (p.batch > 1)  // vector loads stay legal only if every batch base stays 16-B aligned
+      ASR_REQUIRE(p.sA >= 0 && p.sB >= 0 && p.sC >= 0, ASR_ERR_ARG, "gemm: batch strides");
+    if (p.batch > 1 && (p.sA % 8 || p.sB % 8)) { p.a.vec_ok = 0; p.b.vec_ok = 0; }
     maxwg = max(maxwg, ceil_div(g.M, BM) * ceil_div(g.N, BN));
+    maxb = max(maxb, p.batch);
   }
   if (nprob == 1) P.p[1] = P.p[0];
   if (maxwg == 0) return ASR_OK;
   hipStream_t s = (hipStream_t)stream;
+  const dim3 grid(maxwg, 1, nprob * maxb);
+  ASR_REQUIRE(grid.z <= 65535, ASR_ERR_ARG, "gemm: batch too large");
   if (compute_dtype == ASR_DT_BF16) {
     const size_t lds = 2 * BM * LDB16 * 2;
-    hipLaunchKernelGGL(gemm_kernel<true>, dim3(maxwg, 1, nprob), dim3(NT), lds, s, P);
+    hipLaunchKernelGGL(gemm_kernel<true>, grid, dim3(NT), lds, s, P);
   } else {
     const size_t lds = 2 * BM * LDF32 * 4;
-    hipLaunchKernelGGL(gemm_kernel<false>, dim3(maxwg, 1, nprob), dim3(NT), lds, s, P);
+    hipLaunchKernelGGL(gemm_kernel<false>, grid, dim3(NT), lds, s, P);
   }
   ASR_LAUNCH_CHECK();
   return ASR_OK;

@@ -22,6 +22,7 @@
 // The gate gradients are written over the saved activations and then feed the
 // weight-gradient GEMMs (asr_gemm) outside the recurrence.
 #include "mfma.h"
+#include "prof.h"
 
 namespace asr {
 namespace {
@@ -240,8 +241,28 @@ __global__ void transpose_whh(const TW* __restrict__ wf, const TW* __restrict__ 
   }
 }
 
+// [fwd W_hh (n) ; rev W_hh (n)] f32 -> bf16, n = 4H*H each
+__global__ void convert_bf16(const float* __restrict__ wf, const float* __restrict__ wr,
+                             long long n, uint16_t* __restrict__ out) {
+  const long long i0 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const long long i = i0 + j;
+    if (i < n) {
+      out[i] = f2bf(wf[i]);
+      out[n + i] = f2bf(wr[i]);
+    }
+  }
+}
+
+// ping-pong h state: [2 parity][2 dir][B][H] in the compute dtype
+size_t fwd_state_bytes(int B, int H, int cdt) {
+  return ((size_t)4 * B * H * (cdt == ASR_DT_BF16 ? 2 : 4) + 255) & ~size_t(255);
+}
+
 size_t fwd_ws(int B, int H, int cdt) {
-  return (size_t)4 * B * H * (cdt == ASR_DT_BF16 ? 2 : 4);
+  size_t w = cdt == ASR_DT_BF16 ? (size_t)2 * 4 * H * H * 2 : 0;  // bf16 copy of W_hh
+  return fwd_state_bytes(B, H, cdt) + w;
 }
 
 size_t bwd_ws(int B, int H, int cdt) {
@@ -272,26 +293,35 @@ extern "C" int asr_lstm_forward(float* gx_act, const void* whh_f, const void* wh
               "lstm_forward: workspace too small");
   hipStream_t s = (hipStream_t)stream;
   const bool bf = compute_dtype == ASR_DT_BF16;
-  ASR_CHECK_HIP(hipMemsetAsync(workspace, 0, fwd_ws(B, H, compute_dtype), s));
+  ASR_CHECK_HIP(hipMemsetAsync(workspace, 0, fwd_state_bytes(B, H, compute_dtype), s));
   const int vec = (H % 8 == 0) ? 1 : 0;
   dim3 grid(ceil_div(H, FU), 2, ceil_div(B, MB));
+  ASR_REQUIRE(bf || w_dtype == ASR_DT_F32, ASR_ERR_ARG, "lstm_forward: f32 compute needs f32 W");
+  // bf16 mode with f32 weights: one conversion pass so the T step launches
+  // stream 2 bytes per weight instead of 4.
+  const uint16_t* wbf_f = (const uint16_t*)whh_f;
+  const uint16_t* wbf_r = (const uint16_t*)whh_r;
+  if (bf && w_dtype == ASR_DT_F32) {
+    uint16_t* wb = (uint16_t*)((char*)workspace + fwd_state_bytes(B, H, compute_dtype));
+    const long long n = 4LL * H * H;
+    hipLaunchKernelGGL(convert_bf16, dim3(ceil_div(n, 256 * 4)), dim3(256), 0, s,
+                       (const float*)whh_f, (const float*)whh_r, n, wb);
+    ASR_LAUNCH_CHECK();
+    wbf_f = wb;
+    wbf_r = wb + n;
+  }
   for (int st = 0; st < T; ++st) {
+    const int slot = prof_begin_launch(ASR_PROF_LSTM_FWD, s);
     if (bf) {
-      if (w_dtype == ASR_DT_BF16)
-        hipLaunchKernelGGL((lstm_fwd_step<true, uint16_t, uint16_t>), grid, dim3(256), 0, s, st, B,
-                           T, H, lens, (const uint16_t*)whh_f, (const uint16_t*)whh_r, gx_act, y,
-                           cst, (uint16_t*)workspace, vec);
-      else
-        hipLaunchKernelGGL((lstm_fwd_step<true, float, uint16_t>), grid, dim3(256), 0, s, st, B, T,
-                           H, lens, (const float*)whh_f, (const float*)whh_r, gx_act, y, cst,
-                           (uint16_t*)workspace, vec);
+      hipLaunchKernelGGL((lstm_fwd_step<true, uint16_t, uint16_t>), grid, dim3(256), 0, s, st, B,
+                         T, H, lens, wbf_f, wbf_r, gx_act, y, cst, (uint16_t*)workspace, vec);
     } else {
-      ASR_REQUIRE(w_dtype == ASR_DT_F32, ASR_ERR_ARG, "lstm_forward: f32 compute needs f32 W");
       hipLaunchKernelGGL((lstm_fwd_step<false, float, float>), grid, dim3(256), 0, s, st, B, T, H,
                          lens, (const float*)whh_f, (const float*)whh_r, gx_act, y, cst,
                          (float*)workspace, vec);
     }
     ASR_LAUNCH_CHECK();
+    prof_end_launch(ASR_PROF_LSTM_FWD, slot, s);
   }
   return ASR_OK;
 }
@@ -332,6 +362,7 @@ extern "C" int asr_lstm_backward(const float* dy, const void* whh_f, const void*
   const int vec = (H % 8 == 0) ? 1 : 0;
   dim3 grid(ceil_div(H, BU), 2, ceil_div(B, MB));
   for (int q = 0; q < T; ++q) {
+    const int slot = prof_begin_launch(ASR_PROF_LSTM_BWD, s);
     if (bf)
       hipLaunchKernelGGL((lstm_bwd_step<true, uint16_t>), grid, dim3(256), 0, s, q, B, T, H, lens,
                          (const uint16_t*)wt, dy, act_dg, cst, (uint16_t*)dg, dcb, vec);
@@ -339,6 +370,7 @@ extern "C" int asr_lstm_backward(const float* dy, const void* whh_f, const void*
       hipLaunchKernelGGL((lstm_bwd_step<false, float>), grid, dim3(256), 0, s, q, B, T, H, lens,
                          (const float*)wt, dy, act_dg, cst, (float*)dg, dcb, vec);
     ASR_LAUNCH_CHECK();
+    prof_end_launch(ASR_PROF_LSTM_BWD, slot, s);
   }
   return ASR_OK;
 }

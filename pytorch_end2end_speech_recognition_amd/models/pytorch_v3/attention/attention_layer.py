@@ -1,0 +1,49 @@
+"""AttentionMechanism (reference models/pytorch_v3/attention/attention_layer.py).
+
+Same constructor, submodule and parameter names (W_enc_head0, W_dec_head0,
+W_conv_head0, conv_head0 [Conv2d 1->C, (1, K)], V_head0) and the same torch RNG
+consumption, so state_dicts interchange.  The location-attention step itself
+runs inside the fused HIP decoder loop (native_ops.att_decoder, csrc/decoder.hip):
+conv over the previous weights, energy V.tanh(W_enc h_enc + W_dec h_dec +
+W_conv f), MULTIPLICATIVE length mask (:216-225), sharpening, softmax (or
+sigmoid smoothing) and the context vector, fused in one kernel per step.
+"""
+import torch.nn as nn
+
+from ..linear import LinearND
+
+ATTENTION_TYPE = ['content', 'location', 'dot_product', 'rnn_attention', 'coverage']
+
+
+class AttentionMechanism(nn.Module):
+
+    def __init__(self, encoder_num_units, decoder_num_units, attention_type, attention_dim,
+                 sharpening_factor=1, sigmoid_smoothing=False, out_channels=10, kernel_size=201,
+                 num_heads=1):
+        super(AttentionMechanism, self).__init__()
+        if attention_type not in ATTENTION_TYPE:
+            raise TypeError('attention_type should be one of [%s], you provided %s.' %
+                            (', '.join(ATTENTION_TYPE), attention_type))
+        if attention_type != 'location' or num_heads != 1:
+            raise NotImplementedError('MI355X fused decoder: location attention, 1 head '
+                                      '(content / dot_product / multi-head are next-round items)')
+        assert kernel_size % 2 == 1
+        self.attention_type = attention_type
+        self.attention_dim = attention_dim
+        self.sharpening_factor = sharpening_factor
+        self.sigmoid_smoothing = sigmoid_smoothing
+        self.num_heads = num_heads
+        self.out_channels = out_channels
+        self.kernel_size = kernel_size
+        # registration order = attention_layer.py:77-98 (RNG parity)
+        self.W_enc_head0 = LinearND(encoder_num_units, attention_dim, bias=True)
+        self.W_dec_head0 = LinearND(decoder_num_units, attention_dim, bias=False)
+        self.W_conv_head0 = LinearND(out_channels, attention_dim, bias=False)
+        self.conv_head0 = nn.Conv2d(in_channels=1, out_channels=out_channels,
+                                    kernel_size=(1, kernel_size), stride=1,
+                                    padding=(0, kernel_size // 2), bias=False)
+        self.V_head0 = LinearND(attention_dim, 1, bias=False)
+
+    def forward(self, enc_out, enc_out_a, x_lens, dec_out, aw_step):
+        raise NotImplementedError('the location-attention step runs inside the fused decoder '
+                                  'loop (AttentionSeq2seq._decode_train)')

@@ -1,0 +1,288 @@
+"""AttentionSeq2seq (reference models/pytorch_v3/attention/attention_seq2seq.py)
+on the MI355X hot path: hybrid CTC + location-attention training step.
+
+Drop-in: same constructor kwargs / defaults (:110-163), same submodule and
+parameter names and the same torch RNG consumption at construction (state_dicts
+interchange bit for bit), same ``forward(xs, ys, x_lens, y_lens, is_eval)``
+contract and loss assembly (:422-562):
+
+    loss = w_fwd * L_att + lambda * L_ctc                (NOT (1 - lambda) L_att)
+    L_att = (1 - ls) * CE_sum / B + LS / B   (ls > 0)     else CE_sum / B
+    L_ctc = sum_b cost_b / B
+
+MI355X design: the teacher-forced decoder loop (bahdanau order) is ONE fused
+op (native_ops.att_decoder): everything that does not depend on the
+recurrence -- the input-embedding projection of every step, W_enc of the
+encoder states, the W_d / W_c bottleneck, the output layer and the loss -- is
+hoisted into full-batch GEMMs before / after the loop; per step only the
+LSTMCell and the fused location-attention kernel run.
+"""
+import numpy as np
+import torch
+
+from .... import native_ops as ops
+from ..base import ModelBase
+from ..linear import LinearND, Embedding, Embedding_LS
+from ..encoders.load_encoder import load
+from .rnn_decoder import RNNDecoder
+from .attention_layer import AttentionMechanism
+from ..ctc.ctc import _concatenate_labels_np
+from ..ctc.decoders.greedy_decoder import GreedyDecoder
+
+
+class AttentionSeq2seq(ModelBase):
+
+    def __init__(self, input_size, encoder_type, encoder_bidirectional, encoder_num_units,
+                 encoder_num_proj, encoder_num_layers, attention_type, attention_dim,
+                 decoder_type, decoder_num_units, decoder_num_layers, embedding_dim,
+                 dropout_input, dropout_encoder, dropout_decoder, dropout_embedding, num_classes,
+                 parameter_init_distribution='uniform', parameter_init=0.1,
+                 recurrent_weight_orthogonal=False, init_forget_gate_bias_with_one=True,
+                 subsample_list=[], subsample_type='drop', bridge_layer=False,
+                 init_dec_state='first', sharpening_factor=1, logits_temperature=1,
+                 sigmoid_smoothing=False, coverage_weight=0, ctc_loss_weight=0,
+                 attention_conv_num_channels=10, attention_conv_width=201, num_stack=1,
+                 splice=1, input_channel=1, conv_channels=[], conv_kernel_sizes=[],
+                 conv_strides=[], poolings=[], activation='relu', batch_norm=False,
+                 scheduled_sampling_prob=0, scheduled_sampling_max_step=0,
+                 label_smoothing_prob=0, weight_noise_std=0, encoder_residual=False,
+                 encoder_dense_residual=False, decoder_residual=False,
+                 decoder_dense_residual=False, decoding_order='bahdanau', bottleneck_dim=256,
+                 backward_loss_weight=0, num_heads=1):
+        super(ModelBase, self).__init__()
+        self.model_type = 'attention'
+        self.input_size = input_size
+        self.num_stack = num_stack
+        self.encoder_type = encoder_type
+        self.encoder_num_units = encoder_num_units * (2 if encoder_bidirectional else 1)
+        self.encoder_num_proj = encoder_num_proj
+        self.encoder_num_layers = encoder_num_layers
+        self.subsample_list = subsample_list
+        self.decoder_type = decoder_type
+        self.decoder_num_units_0 = decoder_num_units
+        self.decoder_num_layers_0 = decoder_num_layers
+        self.embedding_dim = embedding_dim
+        self.num_classes = num_classes + 1
+        self.sos_0 = num_classes
+        self.eos_0 = num_classes
+        self.decoding_order = decoding_order
+        assert 0 <= backward_loss_weight <= 1
+        self.fwd_weight_0 = 1 - backward_loss_weight
+        self.bwd_weight_0 = backward_loss_weight
+        if init_dec_state not in ['zero', 'mean', 'final', 'first']:
+            raise ValueError('init_dec_state must be "zero" or "mean" or "final" or "first".')
+        self.init_dec_state_0_fwd = init_dec_state
+        self.init_dec_state_0_bwd = init_dec_state
+        if encoder_type != decoder_type:
+            self.init_dec_state_0_fwd = 'zero'
+            self.init_dec_state_0_bwd = 'zero'
+        self.sharpening_factor = sharpening_factor
+        self.logits_temperature = logits_temperature
+        self.sigmoid_smoothing = sigmoid_smoothing
+        self.coverage_weight = coverage_weight
+        self.num_heads_0 = num_heads
+        self.weight_noise_injection = False
+        self.weight_noise_std = float(weight_noise_std)
+        if scheduled_sampling_prob > 0 and scheduled_sampling_max_step == 0:
+            raise ValueError
+        self.ss_prob = scheduled_sampling_prob
+        self._ss_prob = scheduled_sampling_prob
+        self.ss_max_step = scheduled_sampling_max_step
+        self._step = 0
+        self.ls_prob = label_smoothing_prob
+        self.ctc_loss_weight = ctc_loss_weight
+        self.dropout_decoder = float(dropout_decoder)
+        self.dropout_embedding = float(dropout_embedding)
+
+        unsupported = []
+        if decoding_order != 'bahdanau':
+            unsupported.append('decoding_order=%s' % decoding_order)
+        if backward_loss_weight > 0:
+            unsupported.append('backward decoder')
+        if bridge_layer or encoder_type == 'cnn':
+            unsupported.append('bridge layer / cnn encoder')
+        if coverage_weight != 0:
+            unsupported.append('coverage')
+        if unsupported:
+            raise NotImplementedError('MI355X AttentionSeq2seq: not yet supported: ' +
+                                      ', '.join(unsupported))
+
+        self.encoder = load(encoder_type=encoder_type)(
+            input_size=input_size, rnn_type=encoder_type, bidirectional=encoder_bidirectional,
+            num_units=encoder_num_units, num_proj=encoder_num_proj,
+            num_layers=encoder_num_layers, dropout_input=dropout_input,
+            dropout_hidden=dropout_encoder, subsample_list=subsample_list,
+            subsample_type=subsample_type, batch_first=True, merge_bidirectional=False,
+            pack_sequence=True, num_stack=num_stack, splice=splice,
+            input_channel=input_channel, conv_channels=conv_channels,
+            conv_kernel_sizes=conv_kernel_sizes, conv_strides=conv_strides, poolings=poolings,
+            activation=activation, batch_norm=batch_norm, residual=encoder_residual,
+            dense_residual=encoder_dense_residual, nin=0)
+        self.is_bridge = False
+
+        # :293-361, forward direction only (registration order = RNG order)
+        if self.init_dec_state_0_fwd != 'zero':
+            self.W_dec_init_0_fwd = LinearND(self.encoder_num_units, decoder_num_units)
+        self.decoder_0_fwd = RNNDecoder(input_size=self.encoder_num_units + embedding_dim,
+                                        rnn_type=decoder_type, num_units=decoder_num_units,
+                                        num_layers=decoder_num_layers, dropout=dropout_decoder,
+                                        residual=decoder_residual,
+                                        dense_residual=decoder_dense_residual)
+        self.attend_0_fwd = AttentionMechanism(
+            encoder_num_units=self.encoder_num_units, decoder_num_units=decoder_num_units,
+            attention_type=attention_type, attention_dim=attention_dim,
+            sharpening_factor=sharpening_factor, sigmoid_smoothing=sigmoid_smoothing,
+            out_channels=attention_conv_num_channels, kernel_size=attention_conv_width,
+            num_heads=num_heads)
+        self.W_d_0_fwd = LinearND(decoder_num_units, bottleneck_dim, dropout=dropout_decoder)
+        self.W_c_0_fwd = LinearND(self.encoder_num_units, bottleneck_dim, dropout=dropout_decoder)
+        self.fc_0_fwd = LinearND(bottleneck_dim, self.num_classes)
+        if label_smoothing_prob > 0:
+            self.embed_0 = Embedding_LS(num_classes=self.num_classes,
+                                        embedding_dim=embedding_dim, dropout=dropout_embedding,
+                                        label_smoothing_prob=label_smoothing_prob)
+        else:
+            self.embed_0 = Embedding(num_classes=self.num_classes, embedding_dim=embedding_dim,
+                                     dropout=dropout_embedding)
+        if ctc_loss_weight > 0:
+            self.fc_ctc_0 = LinearND(self.encoder_num_units, num_classes + 1)
+            self._decode_ctc_greedy_np = GreedyDecoder(blank_index=0)
+
+        # :397-420
+        self.init_weights(parameter_init, distribution=parameter_init_distribution,
+                          ignore_keys=['bias'])
+        self.init_weights(0, distribution='constant', keys=['bias'])
+        if recurrent_weight_orthogonal:
+            self.init_weights(parameter_init, distribution='orthogonal',
+                              keys=[encoder_type, 'weight'], ignore_keys=['bias'])
+            self.init_weights(parameter_init, distribution='orthogonal',
+                              keys=[decoder_type, 'weight'], ignore_keys=['bias'])
+        if init_forget_gate_bias_with_one:
+            self.init_forget_gate_bias_with_one()
+        self.flatten_parameters_()
+        self.encoder.__dict__['_owner'] = self
+
+    # ------------------------------------------------------------------
+    def forward(self, xs, ys, x_lens, y_lens, is_eval=False):
+        """attention_seq2seq.py:422-562."""
+        if is_eval:
+            self.eval()
+        else:
+            self.train()
+            if self.weight_noise_injection:
+                with torch.no_grad():
+                    self._flat_param.add_(torch.randn_like(self._flat_param) *
+                                          self.weight_noise_std)
+        ss_active = (self.ss_prob > 0 and self._step > 0 and not is_eval and
+                     self._ss_prob > 0)
+        if ss_active:
+            raise NotImplementedError('scheduled sampling needs the per-step decode path '
+                                      '(next-round item)')
+        B = len(xs)
+        xs_d = self.np2var(xs, dtype='float')
+        enc_out, enc_lens_d, perm_d = self._encode(xs_d, x_lens)
+        perm = self.encoder.last_perm_np
+        ys = np.asarray(ys)
+        y_lens = np.asarray(y_lens).astype(np.int64)
+
+        # ys_in = [<sos>, y, <eos>...], ys_out = [y, <eos>, -1...]   (:458-473), host, vectorised
+        Lp = ys.shape[1]
+        pos = np.arange(Lp + 1)[None, :]
+        ys_pad = np.concatenate([ys, np.full((B, 1), -1, ys.dtype)], axis=1)
+        ys_out = np.where(pos < y_lens[:, None], ys_pad,
+                          np.where(pos == y_lens[:, None], self.eos_0, -1)).astype(np.int64)
+        ys_in = np.full((B, Lp + 1), self.eos_0, np.int64)
+        ys_in[:, 1:] = np.where(pos[:, :-1] < y_lens[:, None], ys, self.eos_0)
+        ys_in, ys_out = ys_in[perm], ys_out[perm]
+
+        loss = self.compute_xe_loss(enc_out, self.np2var(ys_in), self.np2var(ys_out), enc_lens_d,
+                                    None, task=0, dir='fwd', weight=self.fwd_weight_0)
+        if self.ctc_loss_weight > 0:
+            ys_ctc = (ys + 1)[perm]
+            yl = y_lens[perm].astype(np.int32)
+            loss = loss + self.compute_ctc_loss(enc_out, ys_ctc, enc_lens_d, yl,
+                                                scale=self.ctc_loss_weight)
+        if is_eval:
+            return float(loss.item())
+        self._step += 1
+        if self.ss_prob > 0:
+            self._ss_prob = min(self.ss_prob, self.ss_prob / self.ss_max_step * self._step)
+        return loss
+
+    def compute_xe_loss(self, enc_out, ys_in, ys_out, x_lens, y_lens, task, dir, weight=1.0):
+        """:564-607 (forward decoder, loss already multiplied by `weight`)."""
+        logits, _ = self._decode_train(enc_out, x_lens, ys_in, task, dir)
+        if self.logits_temperature != 1:
+            logits = logits * (1.0 / self.logits_temperature)
+        B = enc_out.shape[0]
+        ls = self.ls_prob
+        ce = weight * (1 - ls) / B if ls > 0 else weight / B
+        # LS rows are t < y_len + 1 == the rows whose target is not -1
+        return ops.xent(logits, ys_out, None, 0, ce_scale=ce, ls_scale=weight * ls / B)
+
+    def compute_ctc_loss(self, enc_out, ys_ctc, x_lens, y_lens, task=0, scale=1.0):
+        """:609-653 on the HIP CTC kernel; ys_ctc already +1 (blank 0)."""
+        logits = self.fc_ctc_0(enc_out)
+        labels = self.np2var(_concatenate_labels_np(ys_ctc, y_lens))
+        yl_d = self.np2var(y_lens.astype(np.int32))
+        B = enc_out.shape[0]
+        max_l = int(y_lens.max()) if len(y_lens) else 0
+        loss, _ = ops.ctc_loss(logits, labels, yl_d, x_lens, max_l, loss_scale=scale / B)
+        return loss
+
+    def _encode(self, xs, x_lens, is_multi_task=False):
+        """:655-698."""
+        if is_multi_task:
+            raise NotImplementedError
+        return self.encoder(xs, x_lens, volatile=not self.training)
+
+    def _init_h0(self, enc_out):
+        """_init_dec_state (:801-864): zero / first / final; 'mean' is a next item."""
+        mode = self.init_dec_state_0_fwd
+        if mode == 'zero':
+            return None
+        if mode == 'mean':
+            raise NotImplementedError("init_dec_state='mean'")
+        T = enc_out.shape[1]
+        lin = self.W_dec_init_0_fwd.fc
+        h = ops.linear_ex(enc_out, lin.weight, lin.bias, t_index=0 if mode == 'first' else T - 1)
+        return ops.tanh(h)
+
+    def _decode_train(self, enc_out, x_lens, ys, task=0, dir='fwd'):
+        """:704-799 as one fused op (bahdanau order).  Returns (logits [B,S,V], aw)."""
+        if self.training and self.dropout_decoder > 0:
+            raise NotImplementedError('decoder dropout inside the fused loop is a next-round item')
+        att = self.attend_0_fwd
+        cell = self.decoder_0_fwd.lstm_l0
+        h0 = self._init_h0(enc_out)
+        enc_a = att.W_enc_head0(enc_out)                          # one GEMM for all frames
+        y_emb = self.embed_0(ys)                                  # [B, S, emb]
+        pre_emb = ops.linear_ex(y_emb, cell.weight_ih, cell.bias_ih, cell.bias_hh, c0=0,
+                                K=self.embedding_dim)             # all steps' input projection
+        dec, ctx, aw = ops.att_decoder(enc_out, enc_a, x_lens, pre_emb, h0, self.embedding_dim,
+                                       self.sharpening_factor, self.sigmoid_smoothing,
+                                       cell.weight_ih, cell.weight_hh, att.W_dec_head0.fc.weight,
+                                       att.W_conv_head0.fc.weight, att.conv_head0.weight,
+                                       att.V_head0.fc.weight)
+        z = ops.tanh(ops.linear2(dec, self.W_d_0_fwd.fc.weight, self.W_d_0_fwd.fc.bias, ctx,
+                                 self.W_c_0_fwd.fc.weight, self.W_c_0_fwd.fc.bias))
+        logits = self.fc_0_fwd(z)
+        return logits, aw
+
+    @torch.no_grad()
+    def decode_ctc(self, xs, x_lens, beam_width=1, task_index=0):
+        """:1239-1289 (greedy; HIP best path)."""
+        self.eval()
+        if beam_width != 1:
+            raise NotImplementedError
+        xs_d = self.np2var(xs, dtype='float')
+        enc_out, enc_lens_d, _ = self._encode(xs_d, x_lens)
+        logits = self.fc_ctc_0(enc_out)
+        hyps = self._decode_ctc_greedy_np(logits, enc_lens_d)
+        best = np.array([h - 1 for h in hyps] + [None], dtype=object)[:-1]
+        return best, self.encoder.last_perm_np.copy()
+
+    def decode(self, xs, x_lens, beam_width, max_decode_len, min_decode_len=0,
+               length_penalty=0, coverage_penalty=0, task_index=0, resolving_unk=False):
+        raise NotImplementedError('attention inference decoding (greedy / beam) is a next-round '
+                                  'item (SURVEY §8f rank 2)')

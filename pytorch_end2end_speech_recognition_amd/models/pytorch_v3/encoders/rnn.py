@@ -1,0 +1,154 @@
+"""RNNEncoder: the reference's (B)LSTM encoder (models/pytorch_v3/encoders/rnn.py)
+on the MI355X HIP layer op.
+
+Same constructor kwargs, same parameter names (``lstm.weight_ih_l{l}[_reverse]``
+for the fast path, ``lstm_l{l}.weight_ih_l0[_reverse]`` for the per-layer path:
+rnn.py:162-246) and the same torch RNG consumption at construction, so a model
+built under the same seed holds bit-identical initial weights.  ``nn.LSTM``
+modules are used only as parameter holders; their forward never runs.
+
+Forward semantics (rnn.py:284-487): input dropout, length sort (perm_idx is
+returned; outputs stay in sorted order), packed-sequence behaviour through
+per-utterance length masks, dropout after every layer, pyramidal ``drop``
+subsampling ``xs[:, 1::2]`` fused into the next layer's input GEMM, and the
+reference's x_lens quirk: after any subsampling every utterance's length is
+the padded length (rnn.py:435-439).
+"""
+import numpy as np
+import torch
+import torch.nn as nn
+
+from .... import native_ops as ops
+
+
+class RNNEncoder(nn.Module):
+
+    def __init__(self, input_size, rnn_type, bidirectional, num_units, num_proj, num_layers,
+                 dropout_input, dropout_hidden, subsample_list=[], subsample_type='drop',
+                 use_cuda=False, batch_first=False, merge_bidirectional=False,
+                 pack_sequence=True, num_stack=1, splice=1, input_channel=1, conv_channels=[],
+                 conv_kernel_sizes=[], conv_strides=[], poolings=[], activation='relu',
+                 batch_norm=False, residual=False, dense_residual=False, num_layers_sub=0,
+                 nin=0):
+        super(RNNEncoder, self).__init__()
+        if len(subsample_list) > 0 and len(subsample_list) != num_layers:
+            raise ValueError('subsample_list must be the same size as num_layers.')
+        if subsample_type not in ['drop', 'concat']:
+            raise TypeError('subsample_type must be "drop" or "concat".')
+        if num_layers_sub < 0 or (num_layers_sub > 1 and num_layers < num_layers_sub):
+            raise ValueError('Set num_layers_sub between 1 to num_layers.')
+        unsupported = []
+        if rnn_type != 'lstm':
+            unsupported.append('rnn_type=%s' % rnn_type)
+        if not bidirectional:
+            unsupported.append('unidirectional')
+        if num_proj:
+            unsupported.append('num_proj')
+        if subsample_type != 'drop' and sum(subsample_list):
+            unsupported.append('subsample_type=concat')
+        if residual or dense_residual:
+            unsupported.append('residual')
+        if len(conv_channels) > 0:
+            unsupported.append('conv front-end')
+        if num_layers_sub or nin or merge_bidirectional or not batch_first or not pack_sequence:
+            unsupported.append('num_layers_sub/nin/merge/time-major/no-pack')
+        if unsupported:
+            raise NotImplementedError('MI355X RNNEncoder: not yet supported: ' +
+                                      ', '.join(unsupported))
+
+        self.rnn_type = rnn_type
+        self.bidirectional = bidirectional
+        self.num_directions = 2
+        self.num_units = num_units
+        self.num_proj = 0
+        self.num_layers = num_layers
+        self.batch_first = batch_first
+        self.pack_sequence = pack_sequence
+        self.num_layers_sub = num_layers_sub
+        self.subsample_list = list(subsample_list) if len(subsample_list) else [False] * num_layers
+        self.subsample_type = subsample_type
+        self.dropout_input_p = float(dropout_input)
+        self.dropout_hidden_p = float(dropout_hidden)
+        self.dropout_input = nn.Dropout(p=dropout_input)
+        self.conv = None
+        input_size = input_size * splice * num_stack
+        self.input_size = input_size
+
+        self.fast_impl = sum(self.subsample_list) == 0
+        if self.fast_impl:   # rnn.py:162-198: one multi-layer nn.LSTM
+            self.lstm = nn.LSTM(input_size, hidden_size=num_units, num_layers=num_layers,
+                                bias=True, batch_first=batch_first, dropout=dropout_hidden,
+                                bidirectional=True)
+            self.dropout_last = nn.Dropout(p=dropout_hidden)
+        else:                # rnn.py:200-251: one nn.LSTM per layer
+            for l in range(num_layers):
+                din = input_size if l == 0 else num_units * 2
+                setattr(self, 'lstm_l%d' % l,
+                        nn.LSTM(din, hidden_size=num_units, num_layers=1, bias=True,
+                                batch_first=batch_first, dropout=0, bidirectional=True))
+                setattr(self, 'dropout_l%d' % l, nn.Dropout(p=dropout_hidden))
+
+    # parameters of layer l: (w_ih_f, w_ih_r), (w_hh_f, w_hh_r), (b_ih_f, b_ih_r), (b_hh_f, b_hh_r)
+    def _layer_params(self, l):
+        if self.fast_impl:
+            mod, k = self.lstm, l
+        else:
+            mod, k = getattr(self, 'lstm_l%d' % l), 0
+        return [(getattr(mod, '%s_l%d' % (n, k)), getattr(mod, '%s_l%d_reverse' % (n, k)))
+                for n in ('weight_ih', 'weight_hh', 'bias_ih', 'bias_hh')]
+
+    def flat_order(self):
+        """Forward and reverse tensors of each LSTM weight adjacent in the flat
+        buffer, so one GEMM / one recurrence launch covers both directions."""
+        groups = []
+        for l in range(self.num_layers):
+            for pair in self._layer_params(l):
+                groups.append(list(pair))
+        return groups
+
+    def _layer_tensors(self, l):
+        """Combined [fwd; rev] views (params and their grads) of layer l."""
+        model = self._owner
+        ts, gs = [], []
+        for f, r in self._layer_params(l):
+            n = f.numel() + r.numel()
+            shape = (f.shape[0] * 2,) + tuple(f.shape[1:])
+            ts.append(model.flat_view(f, n).view(shape))
+            gs.append(model.flat_view(f, n, grad=True).view(shape))
+        return ts, gs
+
+    def forward(self, xs, x_lens, volatile=False):
+        """xs: device tensor [B, T, input_size]; x_lens: numpy / list / tensor [B].
+        Returns (xs [B, T', 2H], x_lens int32 device tensor [B], perm_idx int64
+        device tensor [B]) like rnn.py:284-487; host copies of the output
+        lengths and perm are kept in ``self.last_lens_np`` / ``self.last_perm_np``."""
+        if torch.is_tensor(x_lens):
+            x_lens = x_lens.detach().cpu().numpy()
+        x_lens = np.asarray(x_lens).astype(np.int64)
+        dev = xs.device
+        if self.training and self.dropout_input_p > 0:
+            xs = ops.dropout(xs, self.dropout_input_p)
+
+        perm = np.argsort(-x_lens, kind='stable')                   # rnn.py:319-326
+        lens = x_lens[perm]
+        perm_d = torch.from_numpy(perm.astype(np.int32)).to(dev, non_blocking=True)
+        T = int(lens.max())                                          # pad_packed length
+        h, pm, t_mul, t_add = xs.contiguous(), perm_d, 1, 0
+        for l in range(self.num_layers):
+            (w_ih, w_hh, b_ih, b_hh), gbufs = self._layer_tensors(l)
+            lens_d = torch.from_numpy(lens.astype(np.int32)).to(dev, non_blocking=True)
+            h = ops.blstm_layer(h, lens_d, T, w_ih, w_hh, b_ih, b_hh, perm=pm, t_mul=t_mul,
+                                t_add=t_add, gbufs=tuple(gbufs))
+            if self.training and self.dropout_hidden_p > 0:
+                h = ops.dropout(h, self.dropout_hidden_p)
+            pm, t_mul, t_add = None, 1, 0
+            if l != self.num_layers - 1 and self.subsample_list[l]:  # rnn.py:413-439
+                T = T // 2
+                t_mul, t_add = 2, 1
+                lens = np.full_like(lens, T)
+        assert t_mul == 1
+        self.last_lens_np = lens.astype(np.int32)
+        self.last_perm_np = perm.astype(np.int64)
+        out_lens = torch.from_numpy(self.last_lens_np).to(dev, non_blocking=True)
+        perm_idx = torch.from_numpy(self.last_perm_np).to(dev, non_blocking=True)
+        return h, out_lens, perm_idx

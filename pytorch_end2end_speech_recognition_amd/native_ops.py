@@ -55,11 +55,13 @@ def operand(t, trans, rmap, offset=0):
     return N.Operand(t.data_ptr() + offset * t.element_size(), dt, int(trans), rmap)
 
 
-def gemm_problem(a, b, c, c_map, M, N_, K, alpha=1.0, beta=0.0, bias=None, bias2=None, c_offset=0):
+def gemm_problem(a, b, c, c_map, M, N_, K, alpha=1.0, beta=0.0, bias=None, bias2=None, c_offset=0,
+                 batch=1, batch_strides=(0, 0, 0)):
     return N.Gemm(a, b, c.data_ptr() + 4 * c_offset, c_map,
                   bias.data_ptr() if bias is not None else None,
                   bias2.data_ptr() if bias2 is not None else None, int(M), int(N_), int(K),
-                  float(alpha), float(beta))
+                  float(alpha), float(beta), int(batch), int(batch_strides[0]),
+                  int(batch_strides[1]), int(batch_strides[2]))
 
 
 def run_gemm(problems, device):
@@ -122,6 +124,212 @@ class LinearFn(torch.autograd.Function):
 
 def linear(x, weight, bias=None):
     return LinearFn.apply(x, weight, bias)
+
+
+class LinearExFn(torch.autograd.Function):
+    """y = x @ W[:, c0:c0+K]^T + b + b2, with x rows optionally gathered from a
+    3-D tensor at a fixed time index (x_src[b, t_index, :]).  Covers the
+    decoder-input projection of all steps (columns [0, emb) of the LSTMCell
+    W_ih plus both biases) and the init_dec_state 'first' / 'final' rows."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, bias2, c0, K, t_index):
+        N.require_device(x, weight)
+        x = x.contiguous()
+        ldw = weight.shape[1]
+        Nout = weight.shape[0]
+        if t_index is None:
+            M = x.numel() // K
+            amap = rowmap(K)
+            out_shape = tuple(x.shape[:-1]) + (Nout,)
+            a_off = 0
+        else:
+            B, T, _ = x.shape
+            M = B
+            amap = rowmap(T * K)
+            out_shape = (B, Nout)
+            a_off = t_index * K
+        y = torch.empty(out_shape, dtype=torch.float32, device=x.device)
+        p = gemm_problem(operand(x, 0, amap, offset=a_off), operand(weight, 0, rowmap(ldw), offset=c0),
+                         y, rowmap(Nout), M, Nout, K, bias=bias, bias2=bias2)
+        run_gemm([p], x.device)
+        ctx.save_for_backward(x, weight)
+        ctx.meta = (bias, bias2, c0, K, t_index, M, amap, a_off)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        bias, bias2, c0, K, t_index, M, amap, a_off = ctx.meta
+        dy = dy.contiguous()
+        ldw, Nout = weight.shape[1], weight.shape[0]
+        dx = None
+        probs = []
+        if ctx.needs_input_grad[0]:
+            dx = torch.zeros_like(x) if t_index is not None else torch.empty_like(x)
+            probs.append(gemm_problem(operand(dy, 0, rowmap(Nout)),
+                                      operand(weight, 1, rowmap(ldw), offset=c0), dx, amap, M, K,
+                                      Nout, c_offset=a_off))
+        probs.append(gemm_problem(operand(dy, 1, rowmap(Nout)), operand(x, 1, amap, offset=a_off),
+                                  grad_buffer(weight), rowmap(ldw), Nout, K, M, beta=1.0,
+                                  c_offset=c0))
+        run_gemm(probs, x.device)
+        if bias is not None:
+            colsum_accumulate(dy.view(M, Nout), grad_buffer(bias),
+                              grad_buffer(bias2) if bias2 is not None else None)
+        return dx, None, None, None, None, None, None
+
+
+def linear_ex(x, weight, bias=None, bias2=None, c0=0, K=None, t_index=None):
+    K = weight.shape[1] - c0 if K is None else K
+    return LinearExFn.apply(x, weight, bias, bias2, c0, K, t_index)
+
+
+class Linear2Fn(torch.autograd.Function):
+    """y = x1 W1^T + b1 + x2 W2^T + b2 (the attention bottleneck
+    W_d(dec_out) + W_c(context), attention_seq2seq.py:788-790): two GEMMs into
+    one output, no elementwise add pass."""
+
+    @staticmethod
+    def forward(ctx, x1, w1, b1, x2, w2, b2):
+        N.require_device(x1, w1, x2, w2)
+        x1, x2 = x1.contiguous(), x2.contiguous()
+        K1, K2, Nout = x1.shape[-1], x2.shape[-1], w1.shape[0]
+        M = x1.numel() // K1
+        y = torch.empty(*x1.shape[:-1], Nout, dtype=torch.float32, device=x1.device)
+        run_gemm([gemm_problem(operand(x1, 0, rowmap(K1)), operand(w1, 0, rowmap(K1)), y,
+                               rowmap(Nout), M, Nout, K1, bias=b1, bias2=b2)], x1.device)
+        run_gemm([gemm_problem(operand(x2, 0, rowmap(K2)), operand(w2, 0, rowmap(K2)), y,
+                               rowmap(Nout), M, Nout, K2, beta=1.0)], x1.device)
+        ctx.save_for_backward(x1, w1, x2, w2)
+        ctx.biases = (b1, b2)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x1, w1, x2, w2 = ctx.saved_tensors
+        b1, b2 = ctx.biases
+        dy = dy.contiguous()
+        K1, K2, Nout = x1.shape[-1], x2.shape[-1], w1.shape[0]
+        M = x1.numel() // K1
+        dx1, dx2 = torch.empty_like(x1), torch.empty_like(x2)
+        run_gemm([gemm_problem(operand(dy, 0, rowmap(Nout)), operand(w1, 1, rowmap(K1)), dx1,
+                               rowmap(K1), M, K1, Nout),
+                  gemm_problem(operand(dy, 0, rowmap(Nout)), operand(w2, 1, rowmap(K2)), dx2,
+                               rowmap(K2), M, K2, Nout)], x1.device)
+        run_gemm([gemm_problem(operand(dy, 1, rowmap(Nout)), operand(x1, 1, rowmap(K1)),
+                               grad_buffer(w1), rowmap(K1), Nout, K1, M, beta=1.0),
+                  gemm_problem(operand(dy, 1, rowmap(Nout)), operand(x2, 1, rowmap(K2)),
+                               grad_buffer(w2), rowmap(K2), Nout, K2, M, beta=1.0)], x1.device)
+        if b1 is not None:
+            colsum_accumulate(dy.view(M, Nout), grad_buffer(b1),
+                              grad_buffer(b2) if b2 is not None else None)
+        return dx1, None, None, dx2, None, None
+
+
+def linear2(x1, w1, b1, x2, w2, b2):
+    return Linear2Fn.apply(x1, w1, b1, x2, w2, b2)
+
+
+# ---------------------------------------------------------------------------
+# Teacher-forced location-attention decoder loop (attention_seq2seq.py:704-799)
+# ---------------------------------------------------------------------------
+class AttDecoderFn(torch.autograd.Function):
+    """Returns (dec_out [B,S,D], ctx [B,S,E], aw [B,S,T]).  Weights:
+    w_ih [4D, emb+E] (LSTMCell; only the context columns are used here, the
+    embedding columns enter through pre_emb), w_hh [4D, D], w_dec [A, D],
+    w_conv [A, C], conv_w [C,1,1,K], v [1, A]."""
+
+    @staticmethod
+    def forward(ctx, enc, enc_a, lens, pre_emb, h0, emb_dim, sharpen, sigmoid, w_ih, w_hh,
+                w_dec, w_conv, conv_w, v):
+        N.require_device(enc, enc_a, lens, pre_emb, w_ih)
+        enc, enc_a, pre_emb = enc.contiguous(), enc_a.contiguous(), pre_emb.contiguous()
+        B, T, E = enc.shape
+        A = enc_a.shape[-1]
+        D = w_hh.shape[1]
+        S = pre_emb.shape[1]
+        C, K = conv_w.shape[0], conv_w.shape[-1]
+        dims = N.AttDecDims(B, T, E, A, C, K, D, S, float(sharpen), int(bool(sigmoid)))
+        dev = enc.device
+        cd = compute_dtype()
+        f32 = dict(dtype=torch.float32, device=dev)
+        dec = torch.empty(B, S, D, **f32)
+        cst = torch.empty(B, S, D, **f32)
+        gates = torch.empty(B, S, 4 * D, **f32)
+        x = torch.empty(B, S, E + D, **f32)
+        ctxv = torch.empty(B, S, E, **f32)
+        aw = torch.empty(B, S, T, **f32)
+        nb = N.query('asr_attdec_workspace_bytes', ctypes.byref(dims), cd, 0)
+        ws = _ws(nb, dev)
+        ld_ih = w_ih.shape[1]
+        w_ih_ctx = ctypes.c_void_p(w_ih.data_ptr() + 4 * emb_dim)
+        N.call('asr_attdec_forward', ctypes.byref(dims), cd, N.ptr(enc), N.ptr(enc_a), N.ptr(lens),
+               w_ih_ctx, ld_ih, N.ptr(w_hh), N.ptr(w_dec), N.ptr(w_conv), N.ptr(conv_w), N.ptr(v),
+               N.ptr(pre_emb), N.ptr(h0.contiguous() if h0 is not None else None), N.ptr(dec),
+               N.ptr(cst), N.ptr(gates), N.ptr(x), N.ptr(ctxv), N.ptr(aw), N.ptr(ws), nb,
+               N.stream_handle(dev))
+        ctx.save_for_backward(enc, enc_a, lens, w_ih, w_hh, w_dec, w_conv, conv_w, v, dec, cst,
+                              gates, x, aw)
+        ctx.meta = (dims, emb_dim, h0 is not None)
+        ctx.mark_non_differentiable(aw)
+        return dec, ctxv, aw
+
+    @staticmethod
+    def backward(ctx, d_dec, d_ctx, d_aw):
+        (enc, enc_a, lens, w_ih, w_hh, w_dec, w_conv, conv_w, v, dec, cst, gates, x,
+         aw) = ctx.saved_tensors
+        dims, emb_dim, has_h0 = ctx.meta
+        B, T, E, A, C, K, D, S = (dims.B, dims.T, dims.E, dims.A, dims.C, dims.K, dims.D, dims.S)
+        dev = enc.device
+        cd = compute_dtype()
+        f32 = dict(dtype=torch.float32, device=dev)
+        d_dec = d_dec.contiguous() if d_dec is not None else torch.zeros(B, S, D, **f32)
+        d_ctx = d_ctx.contiguous() if d_ctx is not None else torch.zeros(B, S, E, **f32)
+        dctx_tot = torch.empty(B, S, E, **f32)
+        d_enc_a = torch.empty(B, T, A, **f32)
+        d_h0 = torch.empty(B, D, **f32) if has_h0 else None
+        dwd = torch.empty(B, S, A, **f32)
+        dv_part = torch.empty(B * S, A, **f32)
+        dwc_part = torch.empty(B * S, A * C, **f32)
+        dcw_part = torch.empty(B * S, C * K, **f32)
+        nb = N.query('asr_attdec_workspace_bytes', ctypes.byref(dims), cd, 1)
+        ws = _ws(nb, dev)
+        ld_ih = w_ih.shape[1]
+        w_ih_ctx = ctypes.c_void_p(w_ih.data_ptr() + 4 * emb_dim)
+        N.call('asr_attdec_backward', ctypes.byref(dims), cd, N.ptr(enc), N.ptr(enc_a),
+               N.ptr(lens), w_ih_ctx, ld_ih, N.ptr(w_hh), N.ptr(w_dec), N.ptr(w_conv),
+               N.ptr(conv_w), N.ptr(v), N.ptr(dec), N.ptr(cst), N.ptr(aw), N.ptr(d_dec),
+               N.ptr(d_ctx), N.ptr(gates), N.ptr(dctx_tot), N.ptr(d_enc_a), N.ptr(d_h0),
+               N.ptr(dwd), N.ptr(dv_part), N.ptr(dwc_part), N.ptr(dcw_part), N.ptr(ws), nb,
+               N.stream_handle(dev))
+        dg = gates                          # dgates (row t = 0 is zero)
+        BS, G, ED = B * S, 4 * D, E + D
+        # LSTMCell weights: dW_ih[:, emb:] += dG^T x[:, :E]; dW_hh += dG^T x[:, E:]
+        run_gemm([gemm_problem(operand(dg, 1, rowmap(G)), operand(x, 1, rowmap(ED)),
+                               grad_buffer(w_ih), rowmap(ld_ih), G, E, BS, beta=1.0,
+                               c_offset=emb_dim),
+                  gemm_problem(operand(dg, 1, rowmap(G)), operand(x, 1, rowmap(ED), offset=E),
+                               grad_buffer(w_hh), rowmap(D), G, D, BS, beta=1.0)], dev)
+        # attention weights
+        run_gemm([gemm_problem(operand(dwd, 1, rowmap(A)), operand(dec, 1, rowmap(D)),
+                               grad_buffer(w_dec), rowmap(D), A, D, BS, beta=1.0)], dev)
+        colsum_accumulate(dv_part, grad_buffer(v))
+        colsum_accumulate(dwc_part, grad_buffer(w_conv))
+        colsum_accumulate(dcw_part, grad_buffer(conv_w))
+        # d enc[b] = aw[b]^T dctx_tot[b]   (batched over utterances)
+        d_enc = torch.empty_like(enc)
+        run_gemm([gemm_problem(operand(aw, 1, rowmap(T)), operand(dctx_tot, 1, rowmap(E)), d_enc,
+                               rowmap(E), T, E, S, batch=B,
+                               batch_strides=(S * T, S * E, T * E))], dev)
+        return (d_enc, d_enc_a, None, dg, d_h0, None, None, None, None, None, None, None, None,
+                None)
+
+
+def att_decoder(enc, enc_a, lens, pre_emb, h0, emb_dim, sharpen, sigmoid, w_ih, w_hh, w_dec,
+                w_conv, conv_w, v):
+    return AttDecoderFn.apply(enc, enc_a, lens, pre_emb, h0, emb_dim, sharpen, sigmoid, w_ih,
+                              w_hh, w_dec, w_conv, conv_w, v)
 
 
 # ---------------------------------------------------------------------------
@@ -222,6 +430,105 @@ def blstm_layer(x_src, lens, T, w_ih, w_hh, b_ih, b_hh, perm=None, t_mul=1, t_ad
 
 
 # ---------------------------------------------------------------------------
+# Elementwise: dropout (counter RNG), tanh, embedding
+# ---------------------------------------------------------------------------
+_seed = {'v': 1623}
+
+
+def manual_seed(seed):
+    _seed['v'] = int(seed)
+
+
+def _next_seed():
+    _seed['v'] = (_seed['v'] * 6364136223846793005 + 1442695040888963407) % (1 << 64)
+    return _seed['v']
+
+
+class DropoutFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, p):
+        N.require_device(x)
+        x = x.contiguous()
+        y = torch.empty_like(x)
+        seed = _next_seed()
+        N.call('asr_dropout', N.ptr(x), N.ptr(y), x.numel(), float(p), seed,
+               N.stream_handle(x.device))
+        ctx.meta = (float(p), seed)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        p, seed = ctx.meta
+        dy = dy.contiguous()
+        dx = torch.empty_like(dy)
+        N.call('asr_dropout', N.ptr(dy), N.ptr(dx), dy.numel(), p, seed,
+               N.stream_handle(dy.device))
+        return dx, None
+
+
+def dropout(x, p):
+    return DropoutFn.apply(x, p) if p > 0 else x
+
+
+class TanhFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        N.require_device(x)
+        x = x.contiguous()
+        y = torch.empty_like(x)
+        N.call('asr_tanh_forward', N.ptr(x), N.ptr(y), x.numel(), N.stream_handle(x.device))
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        y, = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = torch.empty_like(dy)
+        N.call('asr_tanh_backward', N.ptr(y), N.ptr(dy), N.ptr(dx), y.numel(),
+               N.stream_handle(y.device))
+        return dx
+
+
+def tanh(x):
+    return TanhFn.apply(x)
+
+
+class EmbeddingFn(torch.autograd.Function):
+    """trans=0: weight [V, E] (nn.Embedding); trans=1: weight [E, V] (Embedding_LS)."""
+
+    @staticmethod
+    def forward(ctx, idx, weight, trans, padding_idx):
+        N.require_device(idx, weight)
+        idx = idx.contiguous().long()
+        V, E = (weight.shape[1], weight.shape[0]) if trans else weight.shape
+        out = torch.empty(*idx.shape, E, dtype=torch.float32, device=idx.device)
+        N.call('asr_embedding_forward', N.ptr(idx), N.ptr(weight), idx.numel(), V, E, int(trans),
+               N.ptr(out), N.stream_handle(idx.device))
+        ctx.save_for_backward(idx, weight)
+        ctx.meta = (trans, padding_idx, V, E)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        idx, weight = ctx.saved_tensors
+        trans, padding_idx, V, E = ctx.meta
+        dout = dout.contiguous()
+        N.call('asr_embedding_backward', N.ptr(idx), N.ptr(dout), idx.numel(), V, E, int(trans),
+               -1 if padding_idx is None else int(padding_idx), N.ptr(grad_buffer(weight)),
+               N.stream_handle(idx.device))
+        return None, None, None, None
+
+
+def embedding(idx, weight, padding_idx=None):
+    return EmbeddingFn.apply(idx, weight, 0, padding_idx)
+
+
+def embedding_t(idx, weight_ev):
+    return EmbeddingFn.apply(idx, weight_ev, 1, None)
+
+
+# ---------------------------------------------------------------------------
 # CTC (warp-ctc replacement; models/pytorch_v3/ctc/ctc.py:30-66)
 # ---------------------------------------------------------------------------
 class CTCLossFn(torch.autograd.Function):
@@ -260,6 +567,75 @@ class CTCLossFn(torch.autograd.Function):
                loss_scale if g is not None else 0.0, N.ptr(grads), V, T * V, N.ptr(ws), nbytes,
                N.stream_handle(logits.device))
         return grads, None, None, None, None, None, None, None
+
+
+class XentFn(torch.autograd.Function):
+    """Fused CE (ignore -1) + uniform label smoothing over rows of logits."""
+
+    @staticmethod
+    def forward(ctx, logits, targets, lens, T, ce_scale, ls_scale):
+        N.require_device(logits)
+        logits = logits.contiguous()
+        V = logits.shape[-1]
+        R = logits.numel() // V
+        nb = N.query('asr_xent_workspace_bytes', R)
+        ws = _ws(nb, logits.device)
+        loss = torch.empty(1, dtype=torch.float32, device=logits.device)
+        tg = targets.contiguous().long() if targets is not None else None
+        ln = lens.contiguous().int() if lens is not None else None
+        N.call('asr_xent_forward', N.ptr(logits), R, V, int(T), N.ptr(tg), N.ptr(ln),
+               float(ce_scale), float(ls_scale), N.ptr(loss), N.ptr(ws), nb,
+               N.stream_handle(logits.device))
+        ctx.save_for_backward(logits, ws)
+        ctx.meta = (tg, ln, int(T), float(ce_scale), float(ls_scale), nb)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        logits, ws = ctx.saved_tensors
+        tg, ln, T, ce_scale, ls_scale, nb = ctx.meta
+        V = logits.shape[-1]
+        R = logits.numel() // V
+        d = torch.empty_like(logits)
+        g = g.contiguous()
+        N.call('asr_xent_backward', N.ptr(logits), R, V, T, N.ptr(tg), N.ptr(ln), ce_scale,
+               ls_scale, N.ptr(g), 1.0, N.ptr(d), N.ptr(ws), nb, N.stream_handle(logits.device))
+        return d, None, None, None, None, None
+
+
+def xent(logits, targets=None, lens=None, T=0, ce_scale=1.0, ls_scale=0.0):
+    """Returns loss [1] = ce_scale * CE_sum + ls_scale * LS_sum (see asr_xent_forward)."""
+    return XentFn.apply(logits, targets, lens, T, ce_scale, ls_scale)
+
+
+def softmax(x):
+    N.require_device(x)
+    x = x.contiguous()
+    y = torch.empty_like(x)
+    V = x.shape[-1]
+    N.call('asr_softmax', N.ptr(x), x.numel() // V, V, N.ptr(y), N.stream_handle(x.device))
+    return y
+
+
+def ctc_best_path(logits, lens, blank=0):
+    """CTC greedy best path on device: returns (hyps int32 [B, T], hyp_lens int32 [B])."""
+    N.require_device(logits, lens)
+    logits = logits.contiguous()
+    B, T, V = logits.shape
+    hyps = torch.empty(B, T, dtype=torch.int32, device=logits.device)
+    hl = torch.empty(B, dtype=torch.int32, device=logits.device)
+    N.call('asr_ctc_best_path', N.ptr(logits), V, T * V, T, B, V, N.ptr(lens.int().contiguous()),
+           int(blank), N.ptr(hyps), N.ptr(hl), N.stream_handle(logits.device))
+    return hyps, hl
+
+
+def row_argmax(x):
+    N.require_device(x)
+    x = x.contiguous()
+    V = x.shape[-1]
+    out = torch.empty(x.shape[:-1], dtype=torch.int64, device=x.device)
+    N.call('asr_row_argmax', N.ptr(x), x.numel() // V, V, N.ptr(out), N.stream_handle(x.device))
+    return out
 
 
 def ctc_loss(logits, labels_flat, label_lens, act_lens, max_label_len, loss_scale=1.0, blank=0,
