@@ -25,6 +25,33 @@ def _world():
     return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
 
 
+def shard_batch(batch, rank, world):
+    """Deal a length-sorted global batch round-robin to the ranks:
+    rank r takes utterances r, r + world, ...  Every rank's longest utterance is
+    within one position of the global order, so per-rank Tmax (the recurrence
+    length, i.e. the step time) stays balanced; contiguous chunks would hand
+    rank 0 all the longest utterances.  Returns (local batch, grad_scale) where
+    grad_scale = local_B / global_B makes the summed gradient of the
+    per-rank-mean losses equal the 1-GPU gradient of the global batch."""
+    import numpy as np
+    B = len(batch['xs'])
+    if world <= 1:
+        return batch, None
+    idx = np.arange(rank, B, world)
+    if len(idx) == 0:
+        raise ValueError('global batch %d smaller than world size %d' % (B, world))
+    local = {}
+    for k, v in batch.items():
+        v = np.asarray(v)
+        local[k] = v[idx] if v.ndim >= 1 and len(v) == B else v
+    # trim padding to the local maxima (the reference pads per batch)
+    tmax = int(np.max(local['x_lens']))
+    local['xs'] = local['xs'][:, :tmax]
+    if 'ys' in local and 'y_lens' in local:
+        local['ys'] = local['ys'][:, :max(1, int(np.max(local['y_lens'])))]
+    return local, float(len(idx)) / float(B)
+
+
 def allreduce_gradients(model, grad_scale=None):
     """Sum the flat gradient over ranks (one contiguous RCCL collective)."""
     if _world() > 1:
@@ -42,7 +69,10 @@ def train_step(model, batch, clip_grad_norm, backend='pytorch', grad_scale=None)
     loss_val = 0.
     ok = 1
     try:
-        model.optimizer.zero_grad()
+        # ModelBase.zero_grad zeroes the flat gradient and re-binds every
+        # param.grad view (torch.optim's zero_grad would set them to None and
+        # detach them from the buffer the all-reduce / fused step work on)
+        model.zero_grad()
         loss = model(batch['xs'], batch['ys'], batch['x_lens'], batch['y_lens'])
         loss.backward()
     except RuntimeError as e:
@@ -55,7 +85,7 @@ def train_step(model, batch, clip_grad_norm, backend='pytorch', grad_scale=None)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         ok = int(flag.item())
     if not ok:
-        model.optimizer.zero_grad()
+        model.zero_grad()
         return model, 0.
     allreduce_gradients(model, grad_scale)
     if hasattr(model.optimizer, 'clip_and_step'):
