@@ -69,7 +69,7 @@ SIGNATURES = {
     'asr_attdec_workspace_bytes': (c_size, [c_vp, c_int, c_int]),
     'asr_attdec_forward': (c_int, [c_vp, c_int] + [c_vp] * 4 + [c_ll] + [c_vp] * 14 + [c_size,
                                                                                      c_vp]),
-    'asr_attdec_backward': (c_int, [c_vp, c_int] + [c_vp] * 4 + [c_ll] + [c_vp] * 20 + [c_size,
+    'asr_attdec_backward': (c_int, [c_vp, c_int] + [c_vp] * 4 + [c_ll] + [c_vp] * 19 + [c_size,
                                                                                       c_vp]),
     'asr_prof_begin': (c_int, [c_int]),
     'asr_prof_end': (c_int, [c_vp, c_vp, c_int]),

@@ -137,8 +137,9 @@ class RNNEncoder(nn.Module):
         for l in range(self.num_layers):
             (w_ih, w_hh, b_ih, b_hh), gbufs = self._layer_tensors(l)
             lens_d = torch.from_numpy(lens.astype(np.int32)).to(dev, non_blocking=True)
+            graph = tuple(p for pair in self._layer_params(l) for p in pair)
             h = ops.blstm_layer(h, lens_d, T, w_ih, w_hh, b_ih, b_hh, perm=pm, t_mul=t_mul,
-                                t_add=t_add, gbufs=tuple(gbufs))
+                                t_add=t_add, gbufs=tuple(gbufs), graph_params=graph)
             if self.training and self.dropout_hidden_p > 0:
                 h = ops.dropout(h, self.dropout_hidden_p)
             pm, t_mul, t_add = None, 1, 0

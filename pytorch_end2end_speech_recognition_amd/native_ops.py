@@ -343,7 +343,8 @@ class BLSTMLayerFn(torch.autograd.Function):
     (the flat layout of models/pytorch_v3/base.py)."""
 
     @staticmethod
-    def forward(ctx, x_src, lens, T, perm, t_mul, t_add, gbufs, w_ih, w_hh, b_ih, b_hh):
+    def forward(ctx, x_src, lens, T, perm, t_mul, t_add, gbufs, w_ih, w_hh, b_ih, b_hh,
+                *graph_params):
         N.require_device(x_src, lens, w_ih, w_hh, b_ih, b_hh)
         x_src = x_src.contiguous()
         B, T_src, Din = x_src.shape
@@ -365,6 +366,7 @@ class BLSTMLayerFn(torch.autograd.Function):
                B, T, H, cd, N.ptr(y), N.ptr(cst), N.ptr(ws), nb, N.stream_handle(dev))
         ctx.save_for_backward(x_src, lens, w_ih, w_hh, b_ih, b_hh, gx, cst, y)
         ctx.meta = (T, perm, t_mul, t_add, gbufs)
+        ctx.n_graph = len(graph_params)
         return y
 
     @staticmethod
@@ -420,13 +422,17 @@ class BLSTMLayerFn(torch.autograd.Function):
             p = gemm_problem(operand(dg, 0, rowmap(8 * H)), operand(w_ih, 1, rowmap(Din)), dx,
                              c_map, BT, Din, 8 * H)
             run_gemm([p], dev)
-        return dx, None, None, None, None, None, None, None, None, None, None
+        return (dx,) + (None,) * (10 + ctx.n_graph)
 
 
-def blstm_layer(x_src, lens, T, w_ih, w_hh, b_ih, b_hh, perm=None, t_mul=1, t_add=0, gbufs=None):
+def blstm_layer(x_src, lens, T, w_ih, w_hh, b_ih, b_hh, perm=None, t_mul=1, t_add=0, gbufs=None,
+                graph_params=()):
     """gbufs: optional (g_w_ih, g_w_hh, g_b_ih, g_b_hh) gradient views to accumulate
-    into; default: the tensors' own .grad."""
-    return BLSTMLayerFn.apply(x_src, lens, T, perm, t_mul, t_add, gbufs, w_ih, w_hh, b_ih, b_hh)
+    into; default: the tensors' own .grad.  graph_params: the nn.Parameters the
+    combined [fwd; rev] views alias -- passed only so autograd records that the
+    output depends on them (their gradients are written by the kernels)."""
+    return BLSTMLayerFn.apply(x_src, lens, T, perm, t_mul, t_add, gbufs, w_ih, w_hh, b_ih, b_hh,
+                              *graph_params)
 
 
 # ---------------------------------------------------------------------------

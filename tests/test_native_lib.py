@@ -26,6 +26,23 @@ def test_ctypes_table_mirrors_header():
     assert sorted(_native.SIGNATURES) == _declared()
 
 
+def _prototypes():
+    src = open(HEADER).read()
+    src = re.sub(r'/\*.*?\*/', '', src, flags=re.S)
+    out = {}
+    for m in re.finditer(r'\b(asr_[a-z0-9_]+)\s*\(([^)]*)\)\s*;', src):
+        args = m.group(2).strip()
+        out[m.group(1)] = 0 if args in ('', 'void') else args.count(',') + 1
+    return out
+
+
+def test_ctypes_argument_counts_match_header():
+    from pytorch_end2end_speech_recognition_amd import _native
+    protos = _prototypes()
+    for name, (_, args) in _native.SIGNATURES.items():
+        assert len(args) == protos[name], (name, len(args), protos[name])
+
+
 def test_library_loads_and_exports_every_symbol():
     from pytorch_end2end_speech_recognition_amd import _native
     if not os.path.exists(_native.LIB_PATH):
