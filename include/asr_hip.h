@@ -132,6 +132,16 @@ typedef struct {
 
 int asr_gemm(const asr_gemm_t* problems, int nprob, int compute_dtype, void* stream);
 
+/* Same product with a workspace for deterministic split-K: weight-gradient
+ * GEMMs (dW = dgates^T x over B*T rows, K ~ 32000) have few output tiles and
+ * a long K; they are split along K into fixed f32 slabs and summed in a fixed
+ * order by a second kernel (bit-reproducible run to run).  The split is a pure
+ * function of the shapes; asr_gemm_workspace_bytes returns 0 when no problem
+ * splits (then workspace may be NULL and this equals asr_gemm). */
+size_t asr_gemm_workspace_bytes(const asr_gemm_t* problems, int nprob);
+int asr_gemm_ws(const asr_gemm_t* problems, int nprob, int compute_dtype, void* workspace,
+                size_t ws_bytes, void* stream);
+
 /* out0[n] (+ out1[n] if non-NULL) += alpha * sum_m g[m*ld + n]  (bias grads of
  * nn.Linear / nn.LSTM bias_ih and bias_hh); fixed-order, deterministic. */
 size_t asr_colsum_workspace_bytes(int M, int N);

@@ -46,6 +46,9 @@ struct Problem {
   float alpha, beta;
   int batch;
   long long sA, sB, sC;
+  int ksplit;   // > 1: split-K into f32 slabs [ksplit][M][N], reduced by splitk_reduce
+  int kchunk;   // K elements per split (multiple of BK)
+  float* slab;
 };
 
 struct Params {
@@ -101,16 +104,51 @@ __device__ __forceinline__ void load16(const Operand& op, int r, int nrows, int 
   }
 }
 
-// Thread -> (stored row, contiguous offset) of its 16-element load for a tile.
-//   trans=0: tile is 128 logical rows x 32 k: row = tid/2, k = (tid&1)*16
-//   trans=1: tile is 32 k-rows x 128 logical cols: k = tid/8, i = (tid&7)*16
+// 4 contiguous elements starting at logical (row r, col c0) of the stored matrix.
+__device__ __forceinline__ void load4(const Operand& op, int r, int nrows, int c0, int ncols,
+                                      float* v) {
+  long long off = (r < nrows) ? row_off(op.map, r) : -1;
+  if (off < 0) {
+    v[0] = v[1] = v[2] = v[3] = 0.f;
+    return;
+  }
+  if (op.dtype == ASR_DT_F32) {
+    const float* p = (const float*)op.map.base + off + c0;
+    if (op.vec_ok && c0 + 4 <= ncols) {
+      float4 x = *reinterpret_cast<const float4*>(p);
+      v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = (c0 + j < ncols) ? p[j] : 0.f;
+    }
+  } else {
+    const uint16_t* p = (const uint16_t*)op.map.base + off + c0;
+    if (op.vec_ok && c0 + 4 <= ncols) {
+      uint2 x = *reinterpret_cast<const uint2*>(p);
+      v[0] = __uint_as_float(x.x << 16); v[1] = __uint_as_float(x.x & 0xffff0000u);
+      v[2] = __uint_as_float(x.y << 16); v[3] = __uint_as_float(x.y & 0xffff0000u);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = (c0 + j < ncols) ? bf2f(p[j]) : 0.f;
+    }
+  }
+}
+
+// Thread -> its 16 elements of a tile.
+//   trans=0: tile is 128 logical rows x 32 k: row = tid/2, k = (tid&1)*16..+15
+//   trans=1: tile is 32 k-rows x 128 logical rows (contiguous): a 4(k) x 4(row)
+//            block per thread, k = 4*(tid/32)..+3, row = 4*(tid%32)..+3, so each
+//            row's 4 k land as one 8-B (bf16) LDS store instead of 4 scalars.
+//            v[kk*4 + mi] = element (k0 + 4*(tid/32) + kk, row tile0 + 4*(tid%32) + mi)
 __device__ __forceinline__ void load_tile(const Operand& op, int tile0, int nrows_logical, int k0,
                                           int K, float (&v)[16]) {
   const int tid = threadIdx.x;
   if (!op.trans) {
     load16(op, tile0 + (tid >> 1), nrows_logical, k0 + (tid & 1) * 16, K, v);
   } else {
-    load16(op, k0 + (tid >> 3), K, tile0 + (tid & 7) * 16, nrows_logical, v);
+    const int kb = k0 + 4 * (tid >> 5), m4 = tile0 + 4 * (tid & 31);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) load4(op, kb + kk, K, m4, nrows_logical, v + 4 * kk);
   }
 }
 
@@ -127,9 +165,14 @@ __device__ __forceinline__ void store_tile(const Operand& op, void* lds, const f
       *reinterpret_cast<u16x8*>(d) = x0;
       *reinterpret_cast<u16x8*>(d + 8) = x1;
     } else {
-      const int k = tid >> 3, i0 = (tid & 7) * 16;
+      const int kk0 = 4 * (tid >> 5), m0 = 4 * (tid & 31);
 #pragma unroll
-      for (int j = 0; j < 16; ++j) s[(i0 + j) * LDB16 + k] = f2bf(v[j]);
+      for (int mi = 0; mi < 4; ++mi) {
+        uint2 w;
+        w.x = (uint32_t)f2bf(v[mi]) | ((uint32_t)f2bf(v[4 + mi]) << 16);
+        w.y = (uint32_t)f2bf(v[8 + mi]) | ((uint32_t)f2bf(v[12 + mi]) << 16);
+        *reinterpret_cast<uint2*>(s + (m0 + mi) * LDB16 + kk0) = w;
+      }
     }
   } else {
     float* s = (float*)lds;
@@ -138,9 +181,11 @@ __device__ __forceinline__ void store_tile(const Operand& op, void* lds, const f
 #pragma unroll
       for (int j = 0; j < 16; ++j) d[j] = v[j];
     } else {
-      const int k = tid >> 3, i0 = (tid & 7) * 16;
+      const int kk0 = 4 * (tid >> 5), m0 = 4 * (tid & 31);
 #pragma unroll
-      for (int j = 0; j < 16; ++j) s[(i0 + j) * LDF32 + k] = v[j];
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) s[(m0 + mi) * LDF32 + kk0 + kk] = v[4 * kk + mi];
     }
   }
 }
@@ -163,13 +208,19 @@ __global__ void __launch_bounds__(NT) gemm_kernel(Params P) {
   }
   const int gm = (pr.M + BM - 1) / BM, gn = (pr.N + BN - 1) / BN;
   const int nwg = gm * gn;
+  const int nsplit = pr.ksplit > 1 ? pr.ksplit : 1;
+  const int ntot = nwg * nsplit;
   int id = blockIdx.x;
-  if (id >= nwg) return;
+  if (id >= ntot) return;
   {  // bijective XCD-grouping remap: blocks b, b+8, ... land on one XCD
-    const int q = nwg / 8, r = nwg % 8, x = id % 8;
+    const int q = ntot / 8, r = ntot % 8, x = id % 8;
     id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + id / 8;
   }
+  const int split = id / nwg;
+  id -= split * nwg;
   const int tm = (id % gm) * BM, tn = (id / gm) * BN;
+  const int kbeg = nsplit > 1 ? split * pr.kchunk : 0;
+  const int kend = nsplit > 1 ? min(pr.K, kbeg + pr.kchunk) : pr.K;
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wr = (w >> 1) * 64, wc = (w & 1) * 64;
@@ -180,10 +231,10 @@ __global__ void __launch_bounds__(NT) gemm_kernel(Params P) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (pr.K + BK - 1) / BK;
+  const int nk = (kend - kbeg + BK - 1) / BK;
   float va[16], vb[16];
-  load_tile(pr.a, tm, pr.M, 0, pr.K, va);
-  load_tile(pr.b, tn, pr.N, 0, pr.K, vb);
+  load_tile(pr.a, tm, pr.M, kbeg, kend, va);
+  load_tile(pr.b, tn, pr.N, kbeg, kend, vb);
   store_tile<BF16>(pr.a, As, va);
   store_tile<BF16>(pr.b, Bs, vb);
   __syncthreads();
@@ -191,8 +242,8 @@ __global__ void __launch_bounds__(NT) gemm_kernel(Params P) {
   for (int kt = 0; kt < nk; ++kt) {
     const bool more = kt + 1 < nk;
     if (more) {
-      load_tile(pr.a, tm, pr.M, (kt + 1) * BK, pr.K, va);
-      load_tile(pr.b, tn, pr.N, (kt + 1) * BK, pr.K, vb);
+      load_tile(pr.a, tm, pr.M, kbeg + (kt + 1) * BK, kend, va);
+      load_tile(pr.b, tn, pr.N, kbeg + (kt + 1) * BK, kend, vb);
     }
     if (BF16) {
       const uint16_t* a = (const uint16_t*)As;
@@ -233,6 +284,22 @@ __global__ void __launch_bounds__(NT) gemm_kernel(Params P) {
   }
 
   // epilogue: C/D layout col = lane&15, row = 4*(lane>>4) + r
+  if (nsplit > 1) {  // raw partial sums into this split's slab; splitk_reduce finishes
+    float* slab = pr.slab + (long long)split * pr.M * pr.N;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = tm + wr + i * 16 + 4 * (lane >> 4) + r;
+        if (m >= pr.M) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = tn + wc + j * 16 + (lane & 15);
+          if (n < pr.N) slab[(long long)m * pr.N + n] = acc[i][j][r];
+        }
+      }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
 #pragma unroll
@@ -254,6 +321,27 @@ __global__ void __launch_bounds__(NT) gemm_kernel(Params P) {
       }
     }
   }
+}
+
+// Split-K finish: C(m,n) = alpha * sum_s slab[s][m][n] (fixed order s = 0..) +
+// bias + bias2 + beta * C, through C's row map.
+__global__ void splitk_reduce(const float* __restrict__ slab, int ksplit, int M, int N, RowMap c,
+                              float alpha, float beta, const float* __restrict__ bias,
+                              const float* __restrict__ bias2) {
+  const long long MN = (long long)M * N;
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= MN) return;
+  const int m = (int)(e / N), n = (int)(e - (long long)m * N);
+  const long long off = row_off(c, m);
+  if (off < 0) return;
+  float s = 0.f;
+  for (int k = 0; k < ksplit; ++k) s += slab[k * MN + e];
+  float v = alpha * s;
+  if (bias) v += bias[n];
+  if (bias2) v += bias2[n];
+  float* crow = (float*)c.base + off;
+  if (beta != 0.f) v += beta * crow[n];
+  crow[n] = v;
 }
 
 // Column sums: partial[chunk][n] = sum over rows of chunk; then ordered final sum.
@@ -308,13 +396,49 @@ int fill_operand(const asr_operand_t& o, Operand* op, const char* name) {
   return ASR_OK;
 }
 
-}  // namespace
-}  // namespace asr
+// Split-K plan (pure function of the shapes): a launch with fewer than two
+// waves of 128x128 tiles over 256 CUs and K >= 4096 is split into ~1024 work
+// groups, each K chunk >= 1024 (a multiple of BK).
+struct SplitPlan {
+  int ksplit[2], kchunk[2];
+  size_t slab_off[2];
+  size_t bytes;
+};
 
-using namespace asr;
+SplitPlan plan_split(const asr_gemm_t* g, int nprob) {
+  SplitPlan sp{};
+  int tiles = 0;
+  for (int i = 0; i < nprob; ++i)
+    tiles += ceil_div(g[i].M, BM) * ceil_div(g[i].N, BN) * (g[i].batch > 1 ? g[i].batch : 1);
+  for (int i = 0; i < nprob; ++i) {
+    int ks = 1;
+    if (g[i].batch <= 1 && tiles > 0 && tiles < 512 && g[i].K >= 4096) {
+      ks = min(ceil_div(1024, tiles), g[i].K / 1024);
+      ks = max(ks, 1);
+    }
+    int kc = g[i].K;
+    if (ks > 1) {
+      kc = ceil_div(ceil_div(g[i].K, ks), BK) * BK;
+      ks = ceil_div(g[i].K, kc);
+    }
+    sp.ksplit[i] = ks;
+    sp.kchunk[i] = kc;
+    sp.slab_off[i] = sp.bytes;
+    if (ks > 1) sp.bytes += ((size_t)ks * g[i].M * g[i].N * sizeof(float) + 255) & ~(size_t)255;
+  }
+  return sp;
+}
 
-extern "C" int asr_gemm(const asr_gemm_t* problems, int nprob, int compute_dtype, void* stream) {
+int gemm_launch(const asr_gemm_t* problems, int nprob, int compute_dtype, void* workspace,
+                size_t ws_bytes, void* stream) {
   ASR_REQUIRE(problems && nprob >= 1 && nprob <= 2, ASR_ERR_ARG, "gemm: nprob must be 1 or 2");
+  SplitPlan sp{};
+  if (workspace) {
+    sp = plan_split(problems, nprob);
+    ASR_REQUIRE(ws_bytes >= sp.bytes, ASR_ERR_WORKSPACE, "gemm: workspace too small");
+  } else {
+    for (int i = 0; i < nprob; ++i) { sp.ksplit[i] = 1; sp.kchunk[i] = problems[i].K; }
+  }
   Params P;
   P.nprob = nprob;
   int maxwg = 0, maxb = 1;
@@ -340,10 +464,13 @@ extern "C" int asr_gemm(const asr_gemm_t* problems, int nprob, int compute_dtype
     if (p.batch > 1)  // vector loads stay legal only if every batch base stays 16-B aligned
       ASR_REQUIRE(p.sA >= 0 && p.sB >= 0 && p.sC >= 0, ASR_ERR_ARG, "gemm: batch strides");
     if (p.batch > 1 && (p.sA % 8 || p.sB % 8)) { p.a.vec_ok = 0; p.b.vec_ok = 0; }
-    maxwg = max(maxwg, ceil_div(g.M, BM) * ceil_div(g.N, BN));
+    p.ksplit = sp.ksplit[i];
+    p.kchunk = sp.kchunk[i];
+    p.slab = p.ksplit > 1 ? (float*)((char*)workspace + sp.slab_off[i]) : nullptr;
+    maxwg = max(maxwg, ceil_div(g.M, BM) * ceil_div(g.N, BN) * p.ksplit);
     maxb = max(maxb, p.batch);
   }
-  if (nprob == 1) P.p[1] = P.p[0];
+  if (nprob == 1) { P.p[1] = P.p[0]; P.p[1].batch = 0; }
   if (maxwg == 0) return ASR_OK;
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid(maxwg, 1, nprob * maxb);
@@ -356,7 +483,37 @@ extern "C" int asr_gemm(const asr_gemm_t* problems, int nprob, int compute_dtype
     hipLaunchKernelGGL(gemm_kernel<false>, grid, dim3(NT), lds, s, P);
   }
   ASR_LAUNCH_CHECK();
+  for (int i = 0; i < nprob; ++i) {
+    const Problem& p = P.p[i];
+    if (p.ksplit <= 1) continue;
+    const long long mn = (long long)p.M * p.N;
+    if (mn == 0) continue;
+    hipLaunchKernelGGL(splitk_reduce, dim3((unsigned)((mn + 255) / 256)), dim3(256), 0, s, p.slab,
+                       p.ksplit, p.M, p.N, p.c, p.alpha, p.beta, p.bias, p.bias2);
+    ASR_LAUNCH_CHECK();
+  }
   return ASR_OK;
+}
+
+}  // namespace
+}  // namespace asr
+
+using namespace asr;
+
+extern "C" int asr_gemm(const asr_gemm_t* problems, int nprob, int compute_dtype, void* stream) {
+  return gemm_launch(problems, nprob, compute_dtype, nullptr, 0, stream);
+}
+
+extern "C" size_t asr_gemm_workspace_bytes(const asr_gemm_t* problems, int nprob) {
+  if (!problems || nprob < 1 || nprob > 2) return 0;
+  return plan_split(problems, nprob).bytes;
+}
+
+extern "C" int asr_gemm_ws(const asr_gemm_t* problems, int nprob, int compute_dtype,
+                           void* workspace, size_t ws_bytes, void* stream) {
+  if (!workspace) ASR_REQUIRE(asr_gemm_workspace_bytes(problems, nprob) == 0, ASR_ERR_WORKSPACE,
+                              "gemm: split-K workspace required");
+  return gemm_launch(problems, nprob, compute_dtype, workspace, ws_bytes, stream);
 }
 
 extern "C" size_t asr_colsum_workspace_bytes(int M, int N) {

@@ -148,6 +148,186 @@ __global__ void __launch_bounds__(256) lstm_fwd_step(
 }
 
 // ---------------------------------------------------------------------------
+// Latency-optimised bf16 step kernels (H % 32 == 0).  A step is a short
+// dependent chain, so everything a thread will need is put in flight at kernel
+// entry: the epilogue operands (gates input, c_{t-1}, length) and ALL of the
+// wave's MFMA fragments (no guards, clamped rows -> no branches between loads
+// and one vmcnt wait), then the MFMAs, one LDS combine, the fused cell update.
+// ---------------------------------------------------------------------------
+template <int MAXKS>
+__global__ void __launch_bounds__(256) lstm_fwd_step_fast(
+    int s, int B, int T, int H, const int32_t* __restrict__ lens,
+    const uint16_t* __restrict__ whh_f, const uint16_t* __restrict__ whh_r,
+    float* __restrict__ gx_act, float* __restrict__ y, float* __restrict__ cst,
+    uint16_t* __restrict__ hbuf) {
+  __shared__ float part[4][MB][16];
+  const int dir = blockIdx.y;
+  const int u0 = blockIdx.x * FU;
+  const int b0 = blockIdx.z * MB;
+  const int t = dir == 0 ? s : T - 1 - s;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const long long BH = (long long)B * H;
+
+  // epilogue prefetch (threads < 128: one (utterance, unit) each)
+  const int row = tid >> 2, uu = tid & 3;
+  const int b = b0 + row, j = u0 + uu;
+  const bool own = tid < MB * FU && b < B && j < H;
+  const int bc = own ? b : 0, jc = own ? j : 0;
+  const long long gbase = ((long long)bc * T + t) * 8 * H + (long long)dir * 4 * H + jc;
+  const long long sidx = ((long long)bc * T + t) * 2 * H + (long long)dir * H + jc;
+  const int tp = dir == 0 ? t - 1 : t + 1;
+  const bool has_prev = tp >= 0 && tp < T;
+  float gxv[4], cprev = 0.f;
+  int len = 0;
+  if (own) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) gxv[q] = gx_act[gbase + (long long)q * H];
+    cprev = has_prev ? cst[sidx + (long long)(tp - t) * 2 * H] : 0.f;
+    len = lens[bc];
+  }
+
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  if (s > 0) {
+    const uint16_t* hprev = hbuf + ((long long)((s + 1) & 1) * 2 + dir) * BH;
+    const uint16_t* W = dir == 0 ? whh_f : whh_r;
+    const int ra = min(b0 + (lane & 15), B - 1), rb = min(b0 + 16 + (lane & 15), B - 1);
+    const int n = lane & 15, g = n >> 2, u = min(u0 + (n & 3), H - 1);
+    const uint16_t* pa0 = hprev + (long long)ra * H + 8 * (lane >> 4);
+    const uint16_t* pa1 = hprev + (long long)rb * H + 8 * (lane >> 4);
+    const uint16_t* pb = W + (long long)(g * H + u) * H + 8 * (lane >> 4);
+    const int nks = H >> 5;
+    bf16x8 fa0[MAXKS], fa1[MAXKS], fb[MAXKS];
+#pragma unroll
+    for (int i = 0; i < MAXKS; ++i) {   // unconditional (clamped) loads: no branch, one wait
+      const int kc = min(wave + 4 * i, nks - 1) * 32;
+      fb[i] = load_bf16x8(pb + kc);
+      fa0[i] = load_bf16x8(pa0 + kc);
+      fa1[i] = load_bf16x8(pa1 + kc);
+    }
+#pragma unroll
+    for (int i = 0; i < MAXKS; ++i) {
+      if (wave + 4 * i < nks) {
+        acc0 = mfma_bf16(fa0[i], fb[i], acc0);
+        acc1 = mfma_bf16(fa1[i], fb[i], acc1);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    part[tid >> 6][4 * (lane >> 4) + r][lane & 15] = acc0[r];
+    part[tid >> 6][16 + 4 * (lane >> 4) + r][lane & 15] = acc1[r];
+  }
+  __syncthreads();
+  if (!own) return;
+  float pre[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    pre[q] = part[0][row][q * 4 + uu] + part[1][row][q * 4 + uu] + part[2][row][q * 4 + uu] +
+             part[3][row][q * 4 + uu] + gxv[q];
+  const bool active = t < len;
+  const float ig = sigmoidf_(pre[0]), fg = sigmoidf_(pre[1]);
+  const float gg = tanhf_(pre[2]), og = sigmoidf_(pre[3]);
+  float c = fg * cprev + ig * gg;
+  float h = og * tanhf_(c);
+  if (!active) { c = 0.f; h = 0.f; }
+  y[sidx] = h;
+  cst[sidx] = c;
+  gx_act[gbase] = active ? ig : 0.f;
+  gx_act[gbase + H] = active ? fg : 0.f;
+  gx_act[gbase + 2 * H] = active ? gg : 0.f;
+  gx_act[gbase + 3 * H] = active ? og : 0.f;
+  hbuf[((long long)(s & 1) * 2 + dir) * BH + (long long)b * H + j] = f2bf(h);
+}
+
+// backward: WG = 16 units x 16 utterances, 8 waves split K = 4H.
+constexpr int BMB = 16;
+template <int MAXKS>
+__global__ void __launch_bounds__(512) lstm_bwd_step_fast(
+    int q, int B, int T, int H, const int32_t* __restrict__ lens,
+    const uint16_t* __restrict__ wt, const float* __restrict__ dy,
+    float* __restrict__ act_dg, const float* __restrict__ cst, uint16_t* __restrict__ dgbuf,
+    float* __restrict__ dc) {
+  __shared__ float part[8][BMB][16];
+  const int dir = blockIdx.y;
+  const int u0 = blockIdx.x * BU;
+  const int b0 = blockIdx.z * BMB;
+  const int t = dir == 0 ? T - 1 - q : q;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int H4 = 4 * H;
+  const long long BG = (long long)B * H4;
+
+  // epilogue prefetch (threads < 256: one (utterance, unit) each)
+  const int row = tid >> 4, uu = tid & 15;
+  const int b = b0 + row, j = u0 + uu;
+  const bool own = tid < BMB * BU && b < B && j < H;
+  const int bc = own ? b : 0, jc = own ? j : 0;
+  const long long gbase = ((long long)bc * T + t) * 8 * H + (long long)dir * H4 + jc;
+  const long long sidx = ((long long)bc * T + t) * 2 * H + (long long)dir * H + jc;
+  const long long cidx = ((long long)dir * B + bc) * H + jc;
+  const int tp = dir == 0 ? t - 1 : t + 1;
+  float av[4] = {0.f, 0.f, 0.f, 0.f}, c = 0.f, cp = 0.f, dyv = 0.f, dcv = 0.f;
+  int len = 0;
+  if (own) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) av[k] = act_dg[gbase + (long long)k * H];
+    c = cst[sidx];
+    cp = (tp >= 0 && tp < T) ? cst[sidx + (long long)(tp - t) * 2 * H] : 0.f;
+    dyv = dy ? dy[sidx] : 0.f;
+    dcv = dc[cidx];
+    len = lens[bc];
+  }
+
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (q > 0) {
+    const uint16_t* gprev = dgbuf + ((long long)((q + 1) & 1) * 2 + dir) * BG;
+    const uint16_t* W = wt + (long long)dir * H * H4;
+    const int ra = min(b0 + (lane & 15), B - 1);
+    const int jl = min(u0 + (lane & 15), H - 1);
+    const uint16_t* pa = gprev + (long long)ra * H4 + 8 * (lane >> 4);
+    const uint16_t* pb = W + (long long)jl * H4 + 8 * (lane >> 4);
+    const int nks = H4 >> 5;
+    bf16x8 fa[MAXKS], fb[MAXKS];
+#pragma unroll
+    for (int i = 0; i < MAXKS; ++i) {   // unconditional (clamped) loads: no branch, one wait
+      const int kc = min(wave + 8 * i, nks - 1) * 32;
+      fa[i] = load_bf16x8(pa + kc);
+      fb[i] = load_bf16x8(pb + kc);
+    }
+#pragma unroll
+    for (int i = 0; i < MAXKS; ++i)
+      if (wave + 8 * i < nks) acc = mfma_bf16(fa[i], fb[i], acc);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) part[tid >> 6][4 * (lane >> 4) + r][lane & 15] = acc[r];
+  __syncthreads();
+  if (!own) return;
+  uint16_t* gn = dgbuf + ((long long)(q & 1) * 2 + dir) * BG + (long long)b * H4 + j;
+  if (t >= len) {
+    act_dg[gbase] = 0.f; act_dg[gbase + H] = 0.f; act_dg[gbase + 2 * H] = 0.f;
+    act_dg[gbase + 3 * H] = 0.f;
+    gn[0] = 0; gn[H] = 0; gn[2 * H] = 0; gn[3 * H] = 0;
+    dc[cidx] = 0.f;
+    return;
+  }
+  float dh = dyv;
+#pragma unroll
+  for (int w = 0; w < 8; ++w) dh += part[w][row][uu];
+  const float ig = av[0], fg = av[1], gg = av[2], og = av[3];
+  const float tc = tanhf_(c);
+  const float dcell = dcv + dh * og * (1.f - tc * tc);
+  const float d_i = dcell * gg * ig * (1.f - ig);
+  const float d_f = dcell * cp * fg * (1.f - fg);
+  const float d_g = dcell * ig * (1.f - gg * gg);
+  const float d_o = dh * tc * og * (1.f - og);
+  dc[cidx] = dcell * fg;
+  act_dg[gbase] = d_i; act_dg[gbase + H] = d_f; act_dg[gbase + 2 * H] = d_g;
+  act_dg[gbase + 3 * H] = d_o;
+  gn[0] = f2bf(d_i); gn[H] = f2bf(d_f); gn[2 * H] = f2bf(d_g); gn[3 * H] = f2bf(d_o);
+}
+
+// ---------------------------------------------------------------------------
 // backward step (processing index q: forward dir at t = T-1-q, reverse at t = q)
 // grid = (ceil(H/BU), 2, ceil(B/MB)), block = 256
 // ---------------------------------------------------------------------------
@@ -310,9 +490,23 @@ extern "C" int asr_lstm_forward(float* gx_act, const void* whh_f, const void* wh
     wbf_f = wb;
     wbf_r = wb + n;
   }
+  const int nks = H / 32;
+  const int fast_ks = (bf && H % 32 == 0) ? (nks <= 4 ? 1 : nks <= 8 ? 2 : nks <= 16 ? 4 :
+                                             nks <= 32 ? 8 : 0) : 0;
   for (int st = 0; st < T; ++st) {
     const int slot = prof_begin_launch(ASR_PROF_LSTM_FWD, s);
-    if (bf) {
+    if (fast_ks) {
+#define ASR_FWD_FAST(KS)                                                                       \
+  hipLaunchKernelGGL(lstm_fwd_step_fast<KS>, grid, dim3(256), 0, s, st, B, T, H, lens, wbf_f,  \
+                     wbf_r, gx_act, y, cst, (uint16_t*)workspace)
+      switch (fast_ks) {
+        case 1: ASR_FWD_FAST(1); break;
+        case 2: ASR_FWD_FAST(2); break;
+        case 4: ASR_FWD_FAST(4); break;
+        default: ASR_FWD_FAST(8); break;
+      }
+#undef ASR_FWD_FAST
+    } else if (bf) {
       hipLaunchKernelGGL((lstm_fwd_step<true, uint16_t, uint16_t>), grid, dim3(256), 0, s, st, B,
                          T, H, lens, wbf_f, wbf_r, gx_act, y, cst, (uint16_t*)workspace, vec);
     } else {
@@ -361,9 +555,25 @@ extern "C" int asr_lstm_backward(const float* dy, const void* whh_f, const void*
   ASR_LAUNCH_CHECK();
   const int vec = (H % 8 == 0) ? 1 : 0;
   dim3 grid(ceil_div(H, BU), 2, ceil_div(B, MB));
+  const int nks = 4 * H / 32;
+  const int fast_ks = (bf && H % 32 == 0) ? (nks <= 8 ? 1 : nks <= 16 ? 2 : nks <= 32 ? 4 :
+                                             nks <= 64 ? 8 : nks <= 128 ? 16 : 0) : 0;
+  const dim3 fgrid(ceil_div(H, BU), 2, ceil_div(B, BMB));
   for (int q = 0; q < T; ++q) {
     const int slot = prof_begin_launch(ASR_PROF_LSTM_BWD, s);
-    if (bf)
+    if (fast_ks) {
+#define ASR_BWD_FAST(KS)                                                                       \
+  hipLaunchKernelGGL(lstm_bwd_step_fast<KS>, fgrid, dim3(512), 0, s, q, B, T, H, lens,         \
+                     (const uint16_t*)wt, dy, act_dg, cst, (uint16_t*)dg, dcb)
+      switch (fast_ks) {
+        case 1: ASR_BWD_FAST(1); break;
+        case 2: ASR_BWD_FAST(2); break;
+        case 4: ASR_BWD_FAST(4); break;
+        case 8: ASR_BWD_FAST(8); break;
+        default: ASR_BWD_FAST(16); break;
+      }
+#undef ASR_BWD_FAST
+    } else if (bf)
       hipLaunchKernelGGL((lstm_bwd_step<true, uint16_t>), grid, dim3(256), 0, s, q, B, T, H, lens,
                          (const uint16_t*)wt, dy, act_dg, cst, (uint16_t*)dg, dcb, vec);
     else

@@ -65,8 +65,13 @@ def gemm_problem(a, b, c, c_map, M, N_, K, alpha=1.0, beta=0.0, bias=None, bias2
 
 
 def run_gemm(problems, device):
+    """One launch of up to two products; long-K / few-tile products (weight
+    gradients) get a split-K workspace from torch's caching allocator."""
     arr = (N.Gemm * len(problems))(*problems)
-    N.call('asr_gemm', ctypes.cast(arr, ctypes.c_void_p), len(problems), compute_dtype(),
+    parr = ctypes.cast(arr, ctypes.c_void_p)
+    nb = N.query('asr_gemm_workspace_bytes', parr, len(problems))
+    ws = _ws(nb, device) if nb else None
+    N.call('asr_gemm_ws', parr, len(problems), compute_dtype(), N.ptr(ws), nb,
            N.stream_handle(device))
 
 

@@ -134,7 +134,10 @@ def test_gemm_linear_vs_torch(cuda_dev):
     ops = _ops()
     ops.set_compute_dtype('fp32')
     rng = np.random.RandomState(3)
-    for (M, K, Nn) in [(300, 123, 29), (7, 5, 3), (1000, 640, 320)]:
+    # the last two take the split-K path for dW (reduction length M >= 4096,
+    # few output tiles), incl. a ragged final K chunk (4500 = 3*1152 + 1044)
+    for (M, K, Nn) in [(300, 123, 29), (7, 5, 3), (1000, 640, 320), (8192, 256, 29),
+                       (4500, 96, 130)]:
         x = torch.from_numpy(rng.randn(M, K).astype(np.float32))
         w = torch.from_numpy(rng.randn(Nn, K).astype(np.float32) * 0.1)
         b = torch.from_numpy(rng.randn(Nn).astype(np.float32))

@@ -59,6 +59,27 @@ def test_workspace_query_without_gpu():
     assert n >= 2 * 32 * 1000 * 256 * 4
 
 
+def test_gemm_split_plan_without_gpu():
+    """Split-K is chosen from shapes only: the encoder's dW_hh product (two
+    2048x512 outputs, K = B*T = 32000) splits; the gate GEMM does not."""
+    import ctypes
+    from pytorch_end2end_speech_recognition_amd import _native as N
+
+    def prob(M, Nn, K):
+        g = N.Gemm()
+        g.M, g.N, g.K, g.batch = M, Nn, K, 1
+        return g
+
+    def nbytes(*ps):
+        arr = (N.Gemm * len(ps))(*ps)
+        return N.query('asr_gemm_workspace_bytes', ctypes.cast(arr, ctypes.c_void_p), len(ps))
+
+    n = nbytes(prob(2048, 512, 32000), prob(2048, 512, 32000))
+    assert n >= 2 * 2 * 2048 * 512 * 4
+    assert nbytes(prob(32000, 4096, 1024)) == 0
+    assert nbytes(prob(300, 29, 123)) == 0
+
+
 def test_bad_args_raise_runtime_error():
     from pytorch_end2end_speech_recognition_amd import _native
     with pytest.raises(RuntimeError):
