@@ -71,6 +71,75 @@ def synthetic_batch(B, T, F, num_classes, seed):
     return dict(xs=xs, ys=ys, x_lens=x_lens, y_lens=y_lens)
 
 
+def roofline_report(args, p, mean_us, launches, mean_work):
+    """Roofline of the dominant kernel (largest mean launch time x launches over
+    the timed steps), from HIP-event timings taken on the kernels' own stream by
+    the library's prof hooks (asr_prof_*).  Algorithmic work per launch:
+      * lstm_{fwd,bwd}_pass (persistent, one launch = one layer pass, T steps x
+        2 directions): HBM bytes that must move once -- gx / gate activations /
+        y / c / dy read or written once per (b, t) cell plus W_hh once -- and
+        the recurrent h @ W_hh^T flops;
+      * lstm_{fwd,bwd}_step (per-step kernels): the same per time step, W_hh
+        re-streamed every step;
+      * gemm: 2*M*N*K summed over the launch's problems, reported by the library.
+    """
+    B, H, T = args.batch, p['encoder_num_units'], args.frames
+    esz = 2 if args.precision == 'bf16' else 4
+    cell = B * H                              # (utterance, unit) cells per direction
+    w_hh = 2 * 4 * H * H * esz                # both directions
+    flops_step = 2 * 2 * B * 4 * H * H        # h @ W_hh^T, 2 directions
+    fwd_cell = 4 * 4 * 2 + 4 * 2              # gx read + act write (4 gates f32), y + c write
+    bwd_cell = 4 * 4 * 2 + 4 * 3              # act read + dG write, dy + c_t + c_{t-1} read
+    kinds = [
+        ('lstm_fwd_step', 'hbm', 2 * cell * fwd_cell + w_hh, flops_step),
+        ('lstm_bwd_step', 'hbm', 2 * cell * bwd_cell + w_hh, flops_step),
+        ('lstm_fwd_pass', 'hbm', T * 2 * cell * fwd_cell + w_hh, T * flops_step),
+        ('lstm_bwd_pass', 'hbm', T * 2 * cell * bwd_cell + w_hh, T * flops_step),
+        ('gemm', 'mfma', 0, mean_work[4]),
+    ]
+    rows = []
+    for i, (name, bound, nbytes, flops) in enumerate(kinds):
+        us = mean_us[i]
+        if us <= 0 or launches[i] == 0:
+            continue
+        gbs = nbytes / (us * 1e-6) / 1e9
+        tfs = flops / (us * 1e-6) / 1e12
+        rows.append(dict(name=name, bound=bound, us=us, n=int(launches[i]), bytes=nbytes,
+                         flops=flops, gbs=gbs, tfs=tfs, total=us * launches[i]))
+    if not rows:
+        return None
+    dom = max(rows, key=lambda r: r['total'])
+
+    def view(r):
+        if r['bound'] == 'mfma':
+            return {'achieved': round(r['tfs'], 2), 'peak': BF16_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+                    'frac': round(r['tfs'] / BF16_PEAK_TFLOPS, 4)}
+        return {'achieved': round(r['gbs'], 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                'frac': round(r['gbs'] / HBM_PEAK_GBS, 4)}
+
+    out = {'bound': dom['bound']}
+    out.update(view(dom))
+    out.update({'traffic': None, 'kernel': dom['name'], 'mean_launch_us': round(dom['us'], 3),
+                'launches_timed': dom['n'],
+                'algorithmic_bytes_per_launch': int(dom['bytes']),
+                'algorithmic_flops_per_launch': float(dom['flops']),
+                'share_of_timed_kernel_time': round(dom['total'] / sum(r['total'] for r in rows),
+                                                    3)})
+    others = {}
+    for r in rows:
+        if r is dom:
+            continue
+        v = {'bound': r['bound'], 'mean_launch_us': round(r['us'], 3), 'launches': r['n']}
+        v.update(view(r))
+        if r['name'].startswith('lstm'):
+            v['mfma_tflops'] = round(r['tfs'], 2)
+            if r['name'].endswith('_pass'):
+                v['us_per_time_step'] = round(r['us'] / T, 3)
+        others[r['name']] = v
+    out['other_kernels'] = others
+    return out
+
+
 def cpu_baseline(cfg, batch, n_utts):
     """Oracle (torch-CPU restatement of the reference path) on a bounded sample:
     the first n_utts utterances of this rank's batch, one full training step
@@ -161,10 +230,12 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     import ctypes
-    mean_us = (ctypes.c_double * 2)()
-    launches = (ctypes.c_longlong * 2)()
+    NK = 5
+    mean_us = (ctypes.c_double * NK)()
+    launches = (ctypes.c_longlong * NK)()
+    mean_work = (ctypes.c_double * NK)()
     N.call('asr_prof_end', ctypes.cast(mean_us, ctypes.c_void_p),
-           ctypes.cast(launches, ctypes.c_void_p), 2)
+           ctypes.cast(launches, ctypes.c_void_p), ctypes.cast(mean_work, ctypes.c_void_p), NK)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -179,36 +250,7 @@ def main():
         dist.destroy_process_group()
         return
 
-    # ---- roofline of the dominant kernel (the recurrence step) ------------
-    B, H = args.batch, p['encoder_num_units']
-    esz = 2 if args.precision == 'bf16' else 4
-    # one launch = one time step of BOTH directions of one layer
-    flops_per_launch = 2 * 2 * B * 4 * H * H                      # h @ W_hh^T, 2 dirs
-    bytes_fwd = (2 * 4 * H * H * esz        # W_hh (both dirs) streamed once per launch
-                 + 2 * B * H * esz          # h_{t-1}
-                 + 2 * B * 4 * H * 4        # gx read
-                 + 2 * B * 4 * H * 4        # gate activations written
-                 + 2 * B * H * 4 * 3        # c_{t-1} read, c_t and h_t written
-                 + 2 * B * H * esz)         # h_t state copy
-    bytes_bwd = (2 * 4 * H * H * esz + 2 * B * 4 * H * esz   # W_hh^T, dG_{t+1}
-                 + 2 * B * 4 * H * 4 * 2                     # act read, dG written
-                 + 2 * B * H * 4 * 4                         # dy, c_t, c_{t-1}, dc carry
-                 + 2 * B * 4 * H * esz)                      # dG state copy
-    kinds = [('lstm_fwd_step', mean_us[0], launches[0], bytes_fwd),
-             ('lstm_bwd_step', mean_us[1], launches[1], bytes_bwd)]
-    dom = max(kinds, key=lambda k: k[1] * k[2])
-    name, us, nl, nbytes = dom
-    achieved_gbs = nbytes / (us * 1e-6) / 1e9 if us > 0 else 0.0
-    roofline = {'bound': 'hbm', 'kernel': name, 'achieved': round(achieved_gbs, 1),
-                'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(achieved_gbs / HBM_PEAK_GBS, 4),
-                'traffic': None, 'mean_launch_us': round(us, 3), 'launches_timed': int(nl),
-                'algorithmic_bytes_per_launch': int(nbytes),
-                'mfma_view': {'flops_per_launch': flops_per_launch,
-                              'achieved_tflops': round(flops_per_launch / (us * 1e-6) / 1e12, 2)
-                              if us > 0 else 0.0,
-                              'peak_tflops': BF16_PEAK_TFLOPS},
-                'other_kernels': {k[0]: {'mean_launch_us': round(k[1], 3),
-                                         'launches': int(k[2])} for k in kinds if k[0] != name}}
+    roofline = roofline_report(args, p, mean_us, launches, mean_work)
 
     cpu = None
     if world == 1 and not args.no_cpu_baseline:

@@ -297,10 +297,18 @@ int asr_attdec_backward(const asr_attdec_dims_t* dims, int compute_dtype, const 
  * asr_prof_end: synchronises on the recorded events (the only entry point
  * that does), fills mean_us[k] (mean launch duration, microseconds) and
  * launches[k] (all launches seen) for k = 0 lstm forward step, 1 lstm
- * backward step.
+ * backward step (per-step kernels, sampled), 2 lstm forward pass, 3 lstm
+ * backward pass (persistent kernels, one launch per layer pass, all timed),
+ * 4 the asr_gemm main kernel (all timed; mean_work[4] = mean algorithmic
+ * flops 2*M*N*K per timed launch).  mean_work may be NULL.
  */
 int asr_prof_begin(int stride);
-int asr_prof_end(double* mean_us, long long* launches, int nkinds);
+int asr_prof_end(double* mean_us, long long* launches, double* mean_work, int nkinds);
+
+/* Status word of the persistent recurrence kernels: bit 0 set when a bounded
+ * inter-work-group wait gave up (a co-residency failure; that pass's outputs
+ * are invalid).  Synchronises `stream`; clear != 0 resets the word. */
+int asr_lstm_persist_status(int* status, int clear, void* stream);
 
 #ifdef __cplusplus
 }

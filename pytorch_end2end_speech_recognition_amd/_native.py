@@ -74,7 +74,8 @@ SIGNATURES = {
     'asr_attdec_backward': (c_int, [c_vp, c_int] + [c_vp] * 4 + [c_ll] + [c_vp] * 19 + [c_size,
                                                                                       c_vp]),
     'asr_prof_begin': (c_int, [c_int]),
-    'asr_prof_end': (c_int, [c_vp, c_vp, c_int]),
+    'asr_prof_end': (c_int, [c_vp, c_vp, c_vp, c_int]),
+    'asr_lstm_persist_status': (c_int, [c_vp, c_int, c_vp]),
 }
 
 

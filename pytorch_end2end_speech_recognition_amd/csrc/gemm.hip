@@ -15,6 +15,7 @@
 // issued before the MFMAs of the current tile and written to LDS after the
 // barrier.  Block ids are remapped so consecutive tiles share an XCD's L2.
 #include "mfma.h"
+#include "prof.h"
 
 namespace asr {
 namespace {
@@ -407,13 +408,15 @@ struct SplitPlan {
 
 SplitPlan plan_split(const asr_gemm_t* g, int nprob) {
   SplitPlan sp{};
-  int tiles = 0;
-  for (int i = 0; i < nprob; ++i)
-    tiles += ceil_div(g[i].M, BM) * ceil_div(g[i].N, BN) * (g[i].batch > 1 ? g[i].batch : 1);
   for (int i = 0; i < nprob; ++i) {
+    // per problem: the problems of one launch run side by side (blockIdx.z), so
+    // a few-tile dW next to a many-tile dX still gets its own K split
+    const int tiles = ceil_div(g[i].M, BM) * ceil_div(g[i].N, BN);
     int ks = 1;
     if (g[i].batch <= 1 && tiles > 0 && tiles < 512 && g[i].K >= 4096) {
       ks = min(ceil_div(1024, tiles), g[i].K / 1024);
+      const long long mn = (long long)g[i].M * g[i].N;
+      while (ks > 1 && (long long)ks * mn * 4 > (64LL << 20)) --ks;  // slab <= 64 MB
       ks = max(ks, 1);
     }
     int kc = g[i].K;
@@ -475,6 +478,10 @@ int gemm_launch(const asr_gemm_t* problems, int nprob, int compute_dtype, void* 
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid(maxwg, 1, nprob * maxb);
   ASR_REQUIRE(grid.z <= 65535, ASR_ERR_ARG, "gemm: batch too large");
+  double flops = 0.0;
+  for (int i = 0; i < nprob; ++i)
+    flops += 2.0 * problems[i].M * problems[i].N * problems[i].K * P.p[i].batch;
+  const int slot = prof_begin_launch(ASR_PROF_GEMM, s, flops);
   if (compute_dtype == ASR_DT_BF16) {
     const size_t lds = 2 * BM * LDB16 * 2;
     hipLaunchKernelGGL(gemm_kernel<true>, grid, dim3(NT), lds, s, P);
@@ -483,6 +490,7 @@ int gemm_launch(const asr_gemm_t* problems, int nprob, int compute_dtype, void* 
     hipLaunchKernelGGL(gemm_kernel<false>, grid, dim3(NT), lds, s, P);
   }
   ASR_LAUNCH_CHECK();
+  prof_end_launch(ASR_PROF_GEMM, slot, s);
   for (int i = 0; i < nprob; ++i) {
     const Problem& p = P.p[i];
     if (p.ksplit <= 1) continue;

@@ -25,9 +25,20 @@
 #include "prof.h"
 
 namespace asr {
+
+// persistent recurrence (lstm_persist.hip)
+size_t persist_ctr_bytes(int B);
+int persist_rows(int B);
+int lstm_fwd_persistent(int B, int T, int H, const int32_t* lens, const uint16_t* wbf,
+                        float* gx_act, float* y, float* cst, uint16_t* hx, int* ctr,
+                        hipStream_t s, bool dry);
+int lstm_bwd_persistent(int B, int T, int H, const int32_t* lens, const uint16_t* wt,
+                        const float* dy, float* act_dg, const float* cst, uint16_t* dgx, int* ctr,
+                        hipStream_t s, bool dry);
+
 namespace {
 
-constexpr int FU = 4;    // forward: units per work-group (16 gate columns)
+constexpr int FU = 4;   // forward: units per work-group (16 gate columns)
 constexpr int BU = 16;   // backward: units per work-group
 constexpr int MB = 32;   // utterances per work-group (two 16-row MFMA blocks)
 
@@ -435,9 +446,13 @@ __global__ void convert_bf16(const float* __restrict__ wf, const float* __restri
   }
 }
 
-// ping-pong h state: [2 parity][2 dir][B][H] in the compute dtype
+size_t al256(size_t n) { return (n + 255) & ~size_t(255); }
+
+// Forward workspace: [hand-off counters][ping-pong h: 2 parity x 2 dir x Bp x H,
+// compute dtype][bf16 copy of W_hh (bf16 mode)], Bp = B rounded up to 16.
+size_t fwd_ctr_bytes(int B) { return al256(persist_ctr_bytes(B)); }
 size_t fwd_state_bytes(int B, int H, int cdt) {
-  return ((size_t)4 * B * H * (cdt == ASR_DT_BF16 ? 2 : 4) + 255) & ~size_t(255);
+  return fwd_ctr_bytes(B) + al256((size_t)4 * persist_rows(B) * H * (cdt == ASR_DT_BF16 ? 2 : 4));
 }
 
 size_t fwd_ws(int B, int H, int cdt) {
@@ -445,13 +460,21 @@ size_t fwd_ws(int B, int H, int cdt) {
   return fwd_state_bytes(B, H, cdt) + w;
 }
 
-size_t bwd_ws(int B, int H, int cdt) {
+// Backward workspace: [counters][W_hh^T][ping-pong dgates: 2 x 2 x Bp x 4H][dc f32 2 x B x H]
+struct BwdLayout {
+  size_t ctr, wt, dg, dcb, total;
+};
+BwdLayout bwd_layout(int B, int H, int cdt) {
   const size_t es = cdt == ASR_DT_BF16 ? 2 : 4;
-  const size_t wt = (size_t)2 * H * 4 * H * es;
-  const size_t dg = (size_t)4 * B * 4 * H * es;
-  const size_t dcb = (size_t)2 * B * H * 4;
-  return ((wt + 255) & ~size_t(255)) + ((dg + 255) & ~size_t(255)) + dcb;
+  BwdLayout l;
+  l.ctr = 0;
+  l.wt = fwd_ctr_bytes(B);
+  l.dg = l.wt + al256((size_t)2 * H * 4 * H * es);
+  l.dcb = l.dg + al256((size_t)4 * persist_rows(B) * 4 * H * es);
+  l.total = l.dcb + (size_t)2 * B * H * 4;
+  return l;
 }
+size_t bwd_ws(int B, int H, int cdt) { return bwd_layout(B, H, cdt).total; }
 
 }  // namespace
 }  // namespace asr
@@ -473,7 +496,8 @@ extern "C" int asr_lstm_forward(float* gx_act, const void* whh_f, const void* wh
               "lstm_forward: workspace too small");
   hipStream_t s = (hipStream_t)stream;
   const bool bf = compute_dtype == ASR_DT_BF16;
-  ASR_CHECK_HIP(hipMemsetAsync(workspace, 0, fwd_state_bytes(B, H, compute_dtype), s));
+  int* ctr = (int*)workspace;
+  void* hbuf = (char*)workspace + fwd_ctr_bytes(B);
   const int vec = (H % 8 == 0) ? 1 : 0;
   dim3 grid(ceil_div(H, FU), 2, ceil_div(B, MB));
   ASR_REQUIRE(bf || w_dtype == ASR_DT_F32, ASR_ERR_ARG, "lstm_forward: f32 compute needs f32 W");
@@ -490,6 +514,18 @@ extern "C" int asr_lstm_forward(float* gx_act, const void* whh_f, const void* wh
     wbf_f = wb;
     wbf_r = wb + n;
   }
+  if (bf && wbf_r == wbf_f + 4LL * H * H &&
+      lstm_fwd_persistent(B, T, H, lens, wbf_f, gx_act, y, cst, (uint16_t*)hbuf, ctr, s, true)) {
+    // one persistent launch for the whole pass
+    ASR_CHECK_HIP(hipMemsetAsync(ctr, 0, fwd_ctr_bytes(B), s));
+    const int slot = prof_begin_launch(ASR_PROF_LSTM_FWD_SEQ, s);
+    const int rc = lstm_fwd_persistent(B, T, H, lens, wbf_f, gx_act, y, cst, (uint16_t*)hbuf,
+                                       ctr, s, false);
+    ASR_REQUIRE(rc == 1, ASR_ERR_HIP, "lstm_forward: persistent launch failed");
+    prof_end_launch(ASR_PROF_LSTM_FWD_SEQ, slot, s);
+    return ASR_OK;
+  }
+  ASR_CHECK_HIP(hipMemsetAsync(workspace, 0, fwd_state_bytes(B, H, compute_dtype), s));
   const int nks = H / 32;
   const int fast_ks = (bf && H % 32 == 0) ? (nks <= 4 ? 1 : nks <= 8 ? 2 : nks <= 16 ? 4 :
                                              nks <= 32 ? 8 : 0) : 0;
@@ -498,7 +534,7 @@ extern "C" int asr_lstm_forward(float* gx_act, const void* whh_f, const void* wh
     if (fast_ks) {
 #define ASR_FWD_FAST(KS)                                                                       \
   hipLaunchKernelGGL(lstm_fwd_step_fast<KS>, grid, dim3(256), 0, s, st, B, T, H, lens, wbf_f,  \
-                     wbf_r, gx_act, y, cst, (uint16_t*)workspace)
+                     wbf_r, gx_act, y, cst, (uint16_t*)hbuf)
       switch (fast_ks) {
         case 1: ASR_FWD_FAST(1); break;
         case 2: ASR_FWD_FAST(2); break;
@@ -508,11 +544,11 @@ extern "C" int asr_lstm_forward(float* gx_act, const void* whh_f, const void* wh
 #undef ASR_FWD_FAST
     } else if (bf) {
       hipLaunchKernelGGL((lstm_fwd_step<true, uint16_t, uint16_t>), grid, dim3(256), 0, s, st, B,
-                         T, H, lens, wbf_f, wbf_r, gx_act, y, cst, (uint16_t*)workspace, vec);
+                         T, H, lens, wbf_f, wbf_r, gx_act, y, cst, (uint16_t*)hbuf, vec);
     } else {
       hipLaunchKernelGGL((lstm_fwd_step<false, float, float>), grid, dim3(256), 0, s, st, B, T, H,
                          lens, (const float*)whh_f, (const float*)whh_r, gx_act, y, cst,
-                         (float*)workspace, vec);
+                         (float*)hbuf, vec);
     }
     ASR_LAUNCH_CHECK();
     prof_end_launch(ASR_PROF_LSTM_FWD, slot, s);
@@ -531,14 +567,18 @@ extern "C" int asr_lstm_backward(const float* dy, const void* whh_f, const void*
               "lstm_backward: workspace too small");
   hipStream_t s = (hipStream_t)stream;
   const bool bf = compute_dtype == ASR_DT_BF16;
-  const size_t es = bf ? 2 : 4;
-  const size_t wt_bytes = ((size_t)2 * H * 4 * H * es + 255) & ~size_t(255);
-  const size_t dg_bytes = ((size_t)4 * B * 4 * H * es + 255) & ~size_t(255);
+  const BwdLayout L = bwd_layout(B, H, compute_dtype);
   char* base = (char*)workspace;
-  void* wt = base;
-  void* dg = base + wt_bytes;
-  float* dcb = (float*)(base + wt_bytes + dg_bytes);
-  ASR_CHECK_HIP(hipMemsetAsync(dg, 0, dg_bytes + (size_t)2 * B * H * 4, s));
+  int* ctr = (int*)base;
+  void* wt = base + L.wt;
+  void* dg = base + L.dg;
+  float* dcb = (float*)(base + L.dcb);
+  const bool persist = bf && lstm_bwd_persistent(B, T, H, lens, (const uint16_t*)wt, dy, act_dg,
+                                                 cst, (uint16_t*)dg, ctr, s, true);
+  if (persist)
+    ASR_CHECK_HIP(hipMemsetAsync(ctr, 0, L.wt, s));
+  else
+    ASR_CHECK_HIP(hipMemsetAsync(dg, 0, L.total - L.dg, s));
   dim3 tg(ceil_div(H, 32), ceil_div(4 * H, 32), 2);
   if (bf) {
     if (w_dtype == ASR_DT_BF16)
@@ -553,6 +593,14 @@ extern "C" int asr_lstm_backward(const float* dy, const void* whh_f, const void*
                        (const float*)whh_r, H, (float*)wt);
   }
   ASR_LAUNCH_CHECK();
+  if (persist) {  // one persistent launch for the whole pass
+    const int slot = prof_begin_launch(ASR_PROF_LSTM_BWD_SEQ, s);
+    const int rc = lstm_bwd_persistent(B, T, H, lens, (const uint16_t*)wt, dy, act_dg, cst,
+                                       (uint16_t*)dg, ctr, s, false);
+    ASR_REQUIRE(rc == 1, ASR_ERR_HIP, "lstm_backward: persistent launch failed");
+    prof_end_launch(ASR_PROF_LSTM_BWD_SEQ, slot, s);
+    return ASR_OK;
+  }
   const int vec = (H % 8 == 0) ? 1 : 0;
   dim3 grid(ceil_div(H, BU), 2, ceil_div(B, MB));
   const int nks = 4 * H / 32;

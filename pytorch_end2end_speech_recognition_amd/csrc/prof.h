@@ -2,12 +2,15 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
-#define ASR_PROF_LSTM_FWD 0
-#define ASR_PROF_LSTM_BWD 1
-#define ASR_PROF_NKINDS 2
+#define ASR_PROF_LSTM_FWD 0      /* per-step forward kernel (sampled every `stride`) */
+#define ASR_PROF_LSTM_BWD 1      /* per-step backward kernel (sampled) */
+#define ASR_PROF_LSTM_FWD_SEQ 2  /* persistent forward pass (every launch timed) */
+#define ASR_PROF_LSTM_BWD_SEQ 3  /* persistent backward pass (every launch timed) */
+#define ASR_PROF_GEMM 4          /* asr_gemm main kernel (every launch timed, flops recorded) */
+#define ASR_PROF_NKINDS 5
 
 namespace asr {
 bool prof_on();
-int prof_begin_launch(int kind, hipStream_t s);
+int prof_begin_launch(int kind, hipStream_t s, double work = 0.0);
 void prof_end_launch(int kind, int slot, hipStream_t s);
 }  // namespace asr

@@ -18,6 +18,7 @@ struct KindState {
   int used = 0;
   long long seen = 0;
   long long launches = 0;
+  double work = 0.0;  // summed over the timed launches
 };
 
 struct Prof {
@@ -34,13 +35,15 @@ Prof& prof() {
 
 bool prof_on() { return prof().on; }
 
-int prof_begin_launch(int kind, hipStream_t s) {
+int prof_begin_launch(int kind, hipStream_t s, double work) {
   Prof& p = prof();
   if (!p.on) return -1;
   KindState& k = p.k[kind];
   k.launches++;
-  if ((k.seen++ % p.stride) != 0 || k.used >= kMaxPairs) return -1;
+  const int stride = kind >= ASR_PROF_LSTM_FWD_SEQ ? 1 : p.stride;
+  if ((k.seen++ % stride) != 0 || k.used >= kMaxPairs) return -1;
   const int slot = k.used++;
+  k.work += work;
   (void)hipEventRecord(k.ev[2 * slot], s);
   return slot;
 }
@@ -65,12 +68,14 @@ extern "C" int asr_prof_begin(int stride) {
     k.used = 0;
     k.seen = 0;
     k.launches = 0;
+    k.work = 0.0;
   }
   p.on = true;
   return ASR_OK;
 }
 
-extern "C" int asr_prof_end(double* mean_us, long long* launches, int nkinds) {
+extern "C" int asr_prof_end(double* mean_us, long long* launches, double* mean_work,
+                            int nkinds) {
   Prof& p = prof();
   p.on = false;
   for (int i = 0; i < ASR_PROF_NKINDS && i < nkinds; ++i) {
@@ -84,6 +89,7 @@ extern "C" int asr_prof_end(double* mean_us, long long* launches, int nkinds) {
     }
     mean_us[i] = k.used ? 1000.0 * tot / k.used : 0.0;
     launches[i] = k.launches;
+    if (mean_work) mean_work[i] = k.used ? k.work / k.used : 0.0;
   }
   return ASR_OK;
 }

@@ -153,3 +153,50 @@ def test_gemm_linear_vs_torch(cuda_dev):
         torch.cuda.synchronize()
         for a, r in ((xd, xr), (wd, wr), (bd, br)):
             np.testing.assert_allclose(a.grad.cpu().numpy(), r.grad.numpy(), rtol=1e-4, atol=1e-3)
+
+
+def _persist_status():
+    import ctypes
+    from pytorch_end2end_speech_recognition_amd import _native as N
+    st = ctypes.c_int(0)
+    N.call('asr_lstm_persist_status', ctypes.byref(st), 1, N.stream_handle())
+    return st.value
+
+
+@pytest.mark.parametrize('B,T,H', [(20, 37, 64), (32, 120, 512), (7, 15, 320)])
+def test_persistent_recurrence_matches_step_kernels(B, T, H, cuda_dev, monkeypatch):
+    """bf16 mode: the persistent one-launch-per-pass recurrence (lstm_persist.hip)
+    against the per-step kernels on the same inputs: outputs, input grads and
+    every weight grad.  Ragged lengths, B not a multiple of 16 (padded row
+    group), H = 320 (odd k-step count per wave)."""
+    ops = _ops()
+    ops.set_compute_dtype('bf16')
+    rng = np.random.RandomState(B * 1000 + H)
+    Din = 48
+    lens = np.sort(rng.randint(1, T + 1, B))[::-1].astype(np.int32)
+    lens[0] = T
+    x = torch.from_numpy(rng.randn(B, T, Din).astype(np.float32))
+    ws = [torch.from_numpy(rng.uniform(-0.1, 0.1, s).astype(np.float32))
+          for s in ((8 * H, Din), (8 * H, H), (8 * H,), (8 * H,))]
+    R = torch.from_numpy(rng.randn(B, T, 2 * H).astype(np.float32)).to(cuda_dev)
+    res = {}
+    _persist_status()
+    for mode in ('1', '0'):
+        monkeypatch.setenv('ASR_LSTM_PERSIST', mode)
+        xd = x.to(cuda_dev).requires_grad_(True)
+        wd = [w.to(cuda_dev).requires_grad_(True) for w in ws]
+        lens_d = torch.from_numpy(lens).to(cuda_dev)
+        y = ops.blstm_layer(xd, lens_d, T, *wd)
+        (y * R).sum().backward()
+        torch.cuda.synchronize()
+        res[mode] = [y.detach().cpu().numpy(), xd.grad.cpu().numpy()] + \
+            [w.grad.cpu().numpy() for w in wd]
+    assert _persist_status() == 0
+    names = ['y', 'dx', 'dW_ih', 'dW_hh', 'db_ih', 'db_hh']
+    for n, a, b in zip(names, res['1'], res['0']):
+        scale = np.abs(b).max() + 1e-6
+        assert np.abs(a - b).max() / scale < 2e-2, (n, np.abs(a - b).max(), scale)
+    # padded frames are exactly zero in both
+    for b in range(B):
+        assert not res['1'][0][b, lens[b]:].any()
+    ops.set_compute_dtype('fp32')
