@@ -47,6 +47,13 @@ const char* asr_last_error(void);
 /* Number of gfx950 code objects linked in (sanity check for loaders). */
 int asr_arch_is_gfx950(void);
 
+/* A HIP stream restricted to CUs [cu_begin, cu_begin + cu_count) of the
+ * current device (hipExtStreamCreateWithCUMask).  The weight-gradient GEMMs
+ * of encoder layer l run on it beside the persistent backward recurrence of
+ * layer l-1, which keeps the remaining CUs to itself. */
+int asr_stream_create_cu_masked(int cu_begin, int cu_count, void** stream_out);
+int asr_stream_destroy(void* stream);
+
 /* ----------------------------------------------------------------- CTC
  * Replaces warpctc_pytorch.gpu_ctc(acts, grads, labels, label_lens,
  * act_lens, minibatch, costs) (models/pytorch_v3/ctc/ctc.py:35-45).
@@ -115,6 +122,10 @@ typedef struct {
   int dtype;
   int trans;
   asr_rowmap_t map;
+  /* bytes readable from ptr (the rest of its allocation), 0 = unknown.  Known
+   * extents < 2 GiB let bf16 operands use the range-checked buffer-load path
+   * (out-of-range and masked rows read as zeros straight into LDS). */
+  long long bytes;
 } asr_operand_t;
 
 typedef struct {
@@ -161,14 +172,19 @@ int asr_colsum_accumulate(const float* g, long long ld, int M, int N, float alph
  * Backward: dy f32 [B][T][2H] (nullable = 0); act_dg holds the saved gates on
  *   entry and the pre-activation gate gradients dG on exit (feeds the weight
  *   gradient GEMMs: dW_ih = dG^T x, dW_hh = dG^T h_prev, db = colsum dG).
+ * ybf / dgbf (nullable): bf16 copies of y [B][T][2H] / dG [B][T][8H], written by
+ *   the persistent kernels as they go, for the bf16 weight-gradient GEMMs.
+ * bf16 mode runs each pass as ONE persistent launch when the grid is
+ *   co-resident (see lstm_persist.hip), else one launch per time step.
  */
 size_t asr_lstm_workspace_bytes(int B, int H, int compute_dtype, int backward);
 int asr_lstm_forward(float* gx_act, const void* whh_f, const void* whh_r, int w_dtype,
                      const int32_t* lens, int B, int T, int H, int compute_dtype, float* y,
-                     float* cst, void* workspace, size_t ws_bytes, void* stream);
+                     float* cst, uint16_t* ybf, void* workspace, size_t ws_bytes, void* stream);
 int asr_lstm_backward(const float* dy, const void* whh_f, const void* whh_r, int w_dtype,
                       const int32_t* lens, int B, int T, int H, int compute_dtype, float* act_dg,
-                      const float* cst, void* workspace, size_t ws_bytes, void* stream);
+                      const float* cst, uint16_t* dgbf, void* workspace, size_t ws_bytes,
+                      void* stream);
 
 /* ------------------------------------------------------------ optimizer
  * Replaces torch.nn.utils.clip_grad_norm(params, max_norm)
@@ -209,6 +225,13 @@ int asr_embedding_backward(const long long* idx, const float* dout, int n, int V
                            int trans, int padding_idx, float* grad_weight, void* stream);
 int asr_tanh_forward(const float* x, float* y, long long n, void* stream);
 int asr_tanh_backward(const float* y, const float* dy, float* dx, long long n, void* stream);
+
+/* dst[r][0:ncols] = bf16(src[row(r) + 0:ncols]) (round to nearest even) for r <
+ * nrows, rows through an asr_rowmap_t (perm / subsample gathers; rows outside
+ * [0, t_limit) become zeros).  Builds the dense bf16 GEMM operands of the
+ * encoder layer (its input X, W_ih) in bf16 mode. */
+int asr_convert_rows_bf16(const float* src, asr_rowmap_t map, int nrows, int ncols,
+                          uint16_t* dst, void* stream);
 
 /* ------------------------------------------------------------ decoding
  * asr_ctc_best_path: CTC greedy best path (greedy_decoder.py:19-47): per

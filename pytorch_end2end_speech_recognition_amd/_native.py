@@ -30,6 +30,8 @@ SIGNATURES = {
     'asr_version': (c_str, []),
     'asr_last_error': (c_str, []),
     'asr_arch_is_gfx950': (c_int, []),
+    'asr_stream_create_cu_masked': (c_int, [c_int, c_int, c_vp]),
+    'asr_stream_destroy': (c_int, [c_vp]),
     'asr_ctc_workspace_bytes': (c_size, [c_int, c_int, c_int, c_int]),
     'asr_ctc_forward': (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int,
                                 c_int, c_int, c_vp, c_vp, c_float, c_vp, c_size, c_vp]),
@@ -45,9 +47,9 @@ SIGNATURES = {
                                       c_vp]),
     'asr_lstm_workspace_bytes': (c_size, [c_int, c_int, c_int, c_int]),
     'asr_lstm_forward': (c_int, [c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp,
-                                 c_vp, c_vp, c_size, c_vp]),
+                                 c_vp, c_vp, c_vp, c_size, c_vp]),
     'asr_lstm_backward': (c_int, [c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int,
-                                  c_vp, c_vp, c_vp, c_size, c_vp]),
+                                  c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
     'asr_grad_sqnorm_workspace_bytes': (c_size, []),
     'asr_grad_sqnorm': (c_int, [c_vp, c_ll, c_vp, c_vp, c_size, c_vp]),
     'asr_optim_step': (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_ll, c_float, c_float, c_float,
@@ -59,6 +61,7 @@ SIGNATURES = {
                                        c_vp]),
     'asr_tanh_forward': (c_int, [c_vp, c_vp, c_ll, c_vp]),
     'asr_tanh_backward': (c_int, [c_vp, c_vp, c_vp, c_ll, c_vp]),
+    'asr_convert_rows_bf16': None,  # set below, after RowMap (struct passed by value)
     'asr_ctc_best_path': (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp,
                                   c_vp]),
     'asr_row_argmax': (c_int, [c_vp, c_int, c_int, c_vp, c_vp]),
@@ -85,9 +88,13 @@ class RowMap(ctypes.Structure):
                 ('t_add', c_int), ('t_limit', c_int), ('perm', c_vp)]
 
 
+SIGNATURES['asr_convert_rows_bf16'] = (c_int, [c_vp, RowMap, c_int, c_int, c_vp, c_vp])
+
+
 class Operand(ctypes.Structure):
     """asr_operand_t"""
-    _fields_ = [('ptr', c_vp), ('dtype', c_int), ('trans', c_int), ('map', RowMap)]
+    _fields_ = [('ptr', c_vp), ('dtype', c_int), ('trans', c_int), ('map', RowMap),
+                ('bytes', c_ll)]
 
 
 class AttDecDims(ctypes.Structure):

@@ -26,3 +26,27 @@ extern "C" int asr_arch_is_gfx950(void) {
   return 1;  // host pass: the library is only ever built with --offload-arch=gfx950
 #endif
 }
+
+// A stream restricted to CUs [cu_begin, cu_begin + cu_count) of the current
+// device (hipExtStreamCreateWithCUMask).  Used for the weight-gradient GEMMs
+// that run beside the persistent backward recurrence, so the two never compete
+// for the CUs the recurrence's co-resident work-groups need.
+extern "C" int asr_stream_create_cu_masked(int cu_begin, int cu_count, void** stream_out) {
+  ASR_REQUIRE(stream_out && cu_begin >= 0 && cu_count > 0, ASR_ERR_ARG, "stream: bad args");
+  int dev = 0, ncu = 0;
+  ASR_CHECK_HIP(hipGetDevice(&dev));
+  ASR_CHECK_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  ASR_REQUIRE(cu_begin + cu_count <= ncu, ASR_ERR_ARG, "stream: CU range beyond %d CUs", ncu);
+  uint32_t mask[16] = {0};
+  ASR_REQUIRE(ncu <= 512, ASR_ERR_ARG, "stream: too many CUs");
+  for (int c = cu_begin; c < cu_begin + cu_count; ++c) mask[c >> 5] |= 1u << (c & 31);
+  hipStream_t s = nullptr;
+  ASR_CHECK_HIP(hipExtStreamCreateWithCUMask(&s, (uint32_t)((ncu + 31) / 32), mask));
+  *stream_out = (void*)s;
+  return ASR_OK;
+}
+
+extern "C" int asr_stream_destroy(void* stream) {
+  if (stream) ASR_CHECK_HIP(hipStreamDestroy((hipStream_t)stream));
+  return ASR_OK;
+}

@@ -1,7 +1,7 @@
 // Small memory-bound ops of the step (gfx950): dropout with a counter-based
 // RNG (mask recomputed in backward, never stored), embedding lookup /
 // gradient, tanh.  Vectorised 16 B per lane where the layout allows.
-#include "common.h"
+#include "mfma.h"
 
 namespace asr {
 namespace {
@@ -67,6 +67,43 @@ __global__ void tanh_bwd(const float* __restrict__ y, const float* __restrict__ 
     dx[i] = dy[i] * (1.f - y[i] * y[i]);
 }
 
+// dst[r][c] = bf16(src[row(r) + c]) for the rows of an asr_rowmap_t (zeros for
+// rows mapping outside [0, t_limit)); 8 columns per thread, 16-B stores when
+// ncols % 8 == 0.
+__global__ void convert_rows_kernel(const float* __restrict__ src, asr_rowmap_t m, int nrows,
+                                    int ncols, uint16_t* __restrict__ dst) {
+  const int cpr = (ncols + 7) >> 3;
+  const long long nchunks = (long long)nrows * cpr;
+  const int rpb = m.rows_per_b > 0 ? m.rows_per_b : 0x7fffffff;
+  const int tmul = m.t_mul == 0 ? 1 : m.t_mul;
+  const int tlim = m.t_limit > 0 ? m.t_limit : 0x7fffffff;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < nchunks;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int r = (int)(e / cpr), c0 = (int)(e - (long long)r * cpr) * 8;
+    const int b = r / rpb, t = r - b * rpb;
+    const int tp = t * tmul + m.t_add;
+    const bool ok = tp >= 0 && tp < tlim;
+    const float* s = ok ? src + (long long)(m.perm ? m.perm[b] : b) * m.stride_b +
+                              (long long)tp * m.stride_t + c0
+                        : nullptr;
+    uint16_t* d = dst + (long long)r * ncols + c0;
+    if (ncols % 8 == 0) {
+      u16x8 v;
+      if (ok) {
+        const float4 x0 = *reinterpret_cast<const float4*>(s);
+        const float4 x1 = *reinterpret_cast<const float4*>(s + 4);
+        v = u16x8{f2bf(x0.x), f2bf(x0.y), f2bf(x0.z), f2bf(x0.w),
+                  f2bf(x1.x), f2bf(x1.y), f2bf(x1.z), f2bf(x1.w)};
+      } else {
+        v = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      }
+      *reinterpret_cast<u16x8*>(d) = v;
+    } else {
+      for (int j = 0; j < 8 && c0 + j < ncols; ++j) d[j] = ok ? f2bf(s[j]) : (uint16_t)0;
+    }
+  }
+}
+
 inline int grid_for(long long n) {
   long long b = (n + 255) / 256;
   return (int)(b < 4096 ? (b > 0 ? b : 1) : 4096);
@@ -122,6 +159,21 @@ extern "C" int asr_tanh_backward(const float* y, const float* dy, float* dx, lon
   ASR_REQUIRE(y && dy && dx, ASR_ERR_ARG, "tanh_backward: null pointer");
   if (n <= 0) return ASR_OK;
   hipLaunchKernelGGL(tanh_bwd, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, y, dy, dx, n);
+  ASR_LAUNCH_CHECK();
+  return ASR_OK;
+}
+
+extern "C" int asr_convert_rows_bf16(const float* src, asr_rowmap_t map, int nrows, int ncols,
+                                     uint16_t* dst, void* stream) {
+  ASR_REQUIRE(src && dst && nrows >= 0 && ncols >= 0, ASR_ERR_ARG, "convert_rows: bad args");
+  if (ncols % 8 == 0)
+    ASR_REQUIRE(((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0 &&
+                    map.stride_t % 4 == 0 && map.stride_b % 4 == 0,
+                ASR_ERR_ARG, "convert_rows: vector path needs 16-B aligned rows");
+  const long long n = (long long)nrows * ((ncols + 7) / 8);
+  if (n <= 0) return ASR_OK;
+  hipLaunchKernelGGL(convert_rows_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
+                     src, map, nrows, ncols, dst);
   ASR_LAUNCH_CHECK();
   return ASR_OK;
 }

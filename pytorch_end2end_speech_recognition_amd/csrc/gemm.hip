@@ -36,6 +36,7 @@ struct Operand {
   int dtype;  // ASR_DT_F32 / ASR_DT_BF16
   int trans;
   int vec_ok; // 16-element vector loads legal (alignment of base and strides)
+  long long bytes;  // readable bytes from base (0 = unknown)
 };
 
 struct Problem {
@@ -191,6 +192,49 @@ __device__ __forceinline__ void store_tile(const Operand& op, void* lds, const f
   }
 }
 
+// Epilogue shared by the GEMM kernels.  C/D layout: col = lane&15, row = 4*(lane>>4) + r.
+__device__ __forceinline__ void store_acc(const Problem& pr, const f32x4 (&acc)[4][4], int tm,
+                                          int tn, int wr, int wc, int lane, int split,
+                                          int nsplit) {
+  if (nsplit > 1) {  // raw partial sums into this split's slab; splitk_reduce finishes
+    float* slab = pr.slab + (long long)split * pr.M * pr.N;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = tm + wr + i * 16 + 4 * (lane >> 4) + r;
+        if (m >= pr.M) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = tn + wc + j * 16 + (lane & 15);
+          if (n < pr.N) slab[(long long)m * pr.N + n] = acc[i][j][r];
+        }
+      }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = tm + wr + i * 16 + 4 * (lane >> 4) + r;
+      if (m >= pr.M) continue;
+      const long long off = row_off(pr.c, m);
+      if (off < 0) continue;
+      float* crow = (float*)pr.c.base + off;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = tn + wc + j * 16 + (lane & 15);
+        if (n >= pr.N) continue;
+        float v = pr.alpha * acc[i][j][r];
+        if (pr.bias) v += pr.bias[n];
+        if (pr.bias2) v += pr.bias2[n];
+        if (pr.beta != 0.f) v += pr.beta * crow[n];
+        crow[n] = v;
+      }
+    }
+  }
+}
+
 template <bool BF16>
 __global__ void __launch_bounds__(NT) gemm_kernel(Params P) {
   constexpr int TILE_ELEMS = BF16 ? BM * LDB16 : BM * LDF32;
@@ -284,44 +328,187 @@ __global__ void __launch_bounds__(NT) gemm_kernel(Params P) {
     __syncthreads();
   }
 
-  // epilogue: C/D layout col = lane&15, row = 4*(lane>>4) + r
-  if (nsplit > 1) {  // raw partial sums into this split's slab; splitk_reduce finishes
-    float* slab = pr.slab + (long long)split * pr.M * pr.N;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = tm + wr + i * 16 + 4 * (lane >> 4) + r;
-        if (m >= pr.M) continue;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int n = tn + wc + j * 16 + (lane & 15);
-          if (n < pr.N) slab[(long long)m * pr.N + n] = acc[i][j][r];
-        }
-      }
-    return;
-  }
+  store_acc(pr, acc, tm, tn, wr, wc, lane, split, nsplit);
+}
+
+// ---------------------------------------------------------------------------
+// bf16 fast path: both operands bf16 in memory with known extents (< 2 GiB).
+// Tiles go global -> LDS by range-checked buffer loads (buffer_load ... lds,
+// 16 B per lane, no pass through VGPRs); rows outside the row map, k outside
+// the split's range and bytes past the allocation read as zeros.
+//   R mode (trans=0, k contiguous): LDS image [128 rows][64 k], 128-B rows;
+//     16-B chunk c of row r sits at chunk c ^ ((r>>1)&7), so one ds_read_b128
+//     fragment read of 16 consecutive rows touches 16 distinct bank slots.
+//   K mode (trans=1, rows contiguous): LDS image [64 k][128 rows], 256-B
+//     k-rows; 32-B granule g of k-row k sits at g ^ h(k), h(k) = (k&3) |
+//     ((k>>3)&1)<<2, and fragments come from two ds_read_b64_tr_b16 (hardware
+//     transpose) per 16 x 32 block -- conflict-free across each 32-lane half.
+//     This is how dW = dG^T X (K = B*T rows) runs without transposed copies.
+// 128x128x64 tiles, 4 waves (2x2, 64x64 each), two LDS stages (64 KB): the
+// next k-tile's loads are issued before this tile's MFMAs, one vmcnt(0) +
+// barrier per k-tile.  The swizzle is applied on the global source address
+// (the LDS destination of a buffer->LDS load is lane-linear) and on the read.
+// ---------------------------------------------------------------------------
+constexpr int FBK = 64;
+constexpr int FTILE = 128 * FBK * 2;   // bytes per operand tile (16 KB)
+constexpr unsigned OOB_OFF = 0x7ffffff0u;
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((ext_vector_type(4))) short v4s_t;
+typedef __attribute__((address_space(3))) v4s_t lds_v4s_t;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
+
+__device__ __forceinline__ int swz_h(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
+
+// row_off without the batch permutation (the fast path requires perm == NULL,
+// so the staging code issues no global load the compiler would wait for).
+__device__ __forceinline__ long long row_off_np(const RowMap& m, int r) {
+  const int b = r / m.rows_per_b;
+  const int t = r - b * m.rows_per_b;
+  const int tp = t * m.t_mul + m.t_add;
+  if (tp < 0 || tp >= m.t_limit) return -1;
+  return (long long)b * m.stride_b + (long long)tp * m.stride_t;
+}
+
+// This thread's 4 buffer->LDS loads of one operand tile.  Instruction i of
+// wave w fills LDS bytes [1024*(4w+i), +1024): R mode tile rows (4w+i)*8..+7,
+// K mode tile k-rows (4w+i)*4..+3.
+template <int MODE>
+__device__ __forceinline__ void stage_tile(const Operand& op, __amdgpu_buffer_rsrc_t rs,
+                                           char* lds_tile, int tile0, int nrows, int k0, int kend,
+                                           int wave, int lane) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = tm + wr + i * 16 + 4 * (lane >> 4) + r;
-      if (m >= pr.M) continue;
-      const long long off = row_off(pr.c, m);
-      if (off < 0) continue;
-      float* crow = (float*)pr.c.base + off;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = tn + wc + j * 16 + (lane & 15);
-        if (n >= pr.N) continue;
-        float v = pr.alpha * acc[i][j][r];
-        if (pr.bias) v += pr.bias[n];
-        if (pr.bias2) v += pr.bias2[n];
-        if (pr.beta != 0.f) v += pr.beta * crow[n];
-        crow[n] = v;
+    const int blk = wave * 4 + i;
+    unsigned voff = OOB_OFF;
+    if (MODE == 0) {
+      const int r = blk * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      const int row = tile0 + r, k = k0 + 8 * c;
+      if (row < nrows && k < kend) {
+        const long long off = row_off_np(op.map, row);
+        if (off >= 0) voff = (unsigned)((off + k) * 2);
+      }
+    } else {
+      const int kr = blk * 4 + (lane >> 4);
+      const int j = lane & 15;
+      const int c = 2 * ((j >> 1) ^ swz_h(kr)) + (j & 1);
+      const int k = k0 + kr;
+      if (k < kend) {
+        const long long off = row_off_np(op.map, k);
+        if (off >= 0) voff = (unsigned)((off + tile0 + 8 * c) * 2);
       }
     }
+    // LDS-DMA in inline asm: hipcc neither counts it (so it does not drain it
+    // with vmcnt(0) before the current stage's ds_reads) nor keeps M0; the
+    // statement saves / restores M0 itself.  Completion: the caller's vmcnt(0).
+    const unsigned lds_addr =
+        (unsigned)(uintptr_t)(lds_void_t*)(lds_tile + blk * 1024);
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(rs), "s"(lds_addr)
+        : "memory");
   }
+}
+
+// MFMA fragment (16 rows x 32 k) of the block starting at tile row rb, k-half kk.
+template <int MODE>
+__device__ __forceinline__ bf16x8 frag_bf16(const char* lds_tile, int rb, int kk, int lane) {
+  if (MODE == 0) {
+    const int r = rb + (lane & 15);
+    const int c = (4 * kk + (lane >> 4)) ^ ((r >> 1) & 7);
+    return __builtin_bit_cast(bf16x8, *(const u32x4_t*)(lds_tile + r * 128 + c * 16));
+  } else {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int G = rb >> 4;
+    const int k0 = 32 * kk + 8 * g + q, k1 = k0 + 4;
+    const char* a0 = lds_tile + k0 * 256 + ((G ^ swz_h(k0)) << 5) + 8 * p;
+    const char* a1 = lds_tile + k1 * 256 + ((G ^ swz_h(k1)) << 5) + 8 * p;
+    const v4s_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t*)a0);
+    const v4s_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t*)a1);
+    typedef __attribute__((ext_vector_type(8))) short v8s_t;
+    const v8s_t v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8, v);
+  }
+}
+
+template <int AMODE, int BMODE>
+__global__ void __launch_bounds__(NT) gemm_bf16_fast(Params P) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // 2 stages x (A, B) tiles
+
+  const int zb = blockIdx.z / P.nprob, zp = blockIdx.z % P.nprob;
+  Problem pr = P.p[zp];
+  if (zb >= pr.batch) return;
+  if (zb > 0) {
+    pr.a.map.base = (const char*)pr.a.map.base + zb * pr.sA * 2;
+    pr.b.map.base = (const char*)pr.b.map.base + zb * pr.sB * 2;
+    pr.a.bytes -= zb * pr.sA * 2;
+    pr.b.bytes -= zb * pr.sB * 2;
+    pr.c.base = (const char*)pr.c.base + zb * pr.sC * 4;
+  }
+  const int gm = (pr.M + BM - 1) / BM, gn = (pr.N + BN - 1) / BN;
+  const int nwg = gm * gn;
+  const int nsplit = pr.ksplit > 1 ? pr.ksplit : 1;
+  const int ntot = nwg * nsplit;
+  int id = blockIdx.x;
+  if (id >= ntot) return;
+  {
+    const int q = ntot / 8, r = ntot % 8, x = id % 8;
+    id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + id / 8;
+  }
+  const int split = id / nwg;
+  id -= split * nwg;
+  const int tm = (id % gm) * BM, tn = (id / gm) * BN;
+  const int kbeg = nsplit > 1 ? split * pr.kchunk : 0;
+  const int kend = nsplit > 1 ? min(pr.K, kbeg + pr.kchunk) : pr.K;
+
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = (w >> 1) * 64, wc = (w & 1) * 64;
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc((void*)pr.a.map.base, 0, (int)pr.a.bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)pr.b.map.base, 0, (int)pr.b.bytes, 0x00020000);
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (kend - kbeg + FBK - 1) / FBK;
+  stage_tile<AMODE>(pr.a, ra, smem, tm, pr.M, kbeg, kend, w, lane);
+  stage_tile<BMODE>(pr.b, rb, smem + FTILE, tn, pr.N, kbeg, kend, w, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* cur = smem + (kt & 1) * 2 * FTILE;
+    if (kt + 1 < nk) {
+      char* nxt = smem + ((kt + 1) & 1) * 2 * FTILE;
+      const int k0 = kbeg + (kt + 1) * FBK;
+      stage_tile<AMODE>(pr.a, ra, nxt, tm, pr.M, k0, kend, w, lane);
+      stage_tile<BMODE>(pr.b, rb, nxt + FTILE, tn, pr.N, k0, kend, w, lane);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = frag_bf16<AMODE>(cur, wr + 16 * i, kk, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = frag_bf16<BMODE>(cur + FTILE, wc + 16 * j, kk, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma_bf16(fa[i], fb[j], acc[i][j]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  store_acc(pr, acc, tm, tn, wr, wc, lane, split, nsplit);
 }
 
 // Split-K finish: C(m,n) = alpha * sum_s slab[s][m][n] (fixed order s = 0..) +
@@ -393,6 +580,7 @@ int fill_operand(const asr_operand_t& o, Operand* op, const char* name) {
   const int esz = o.dtype == ASR_DT_F32 ? 4 : 2;
   const int vec = o.dtype == ASR_DT_F32 ? 4 : 8;
   op->vec_ok = aligned16(o.ptr) && (o.map.stride_t % vec == 0) && (o.map.stride_b % vec == 0);
+  op->bytes = o.bytes;
   (void)esz;
   return ASR_OK;
 }
@@ -421,7 +609,7 @@ SplitPlan plan_split(const asr_gemm_t* g, int nprob) {
     }
     int kc = g[i].K;
     if (ks > 1) {
-      kc = ceil_div(ceil_div(g[i].K, ks), BK) * BK;
+      kc = ceil_div(ceil_div(g[i].K, ks), 64) * 64;  // whole fast-path k-tiles
       ks = ceil_div(g[i].K, kc);
     }
     sp.ksplit[i] = ks;
@@ -430,6 +618,34 @@ SplitPlan plan_split(const asr_gemm_t* g, int nprob) {
     if (ks > 1) sp.bytes += ((size_t)ks * g[i].M * g[i].N * sizeof(float) + 255) & ~(size_t)255;
   }
   return sp;
+}
+
+// The bf16 fast path's operand mode pair (2*a.trans + b.trans) when every
+// problem of the launch qualifies and all share it, else -1 (generic kernel).
+bool fast_operand_ok(const asr_operand_t& o, const Operand& op, long long batch_stride,
+                     int batch, int kdim) {
+  if (o.dtype != ASR_DT_BF16 || o.bytes <= 0 || o.bytes > 0x7fff0000LL) return false;
+  if (o.map.perm) return false;
+  if (!aligned16(o.ptr) || o.map.stride_t % 8 || o.map.stride_b % 8) return false;
+  if (batch > 1 && batch_stride % 8) return false;
+  if (!o.trans && kdim % 8) return false;
+  (void)op;
+  return true;
+}
+
+int fast_modes(const asr_gemm_t* g, const Params& P) {
+  if (getenv("ASR_GEMM_FAST") && getenv("ASR_GEMM_FAST")[0] == '0') return -1;
+  int modes = -1;
+  for (int i = 0; i < P.nprob; ++i) {
+    const Problem& p = P.p[i];
+    if (!fast_operand_ok(g[i].a, p.a, p.sA, p.batch, p.K) ||
+        !fast_operand_ok(g[i].b, p.b, p.sB, p.batch, p.K))
+      return -1;
+    const int m = 2 * (g[i].a.trans ? 1 : 0) + (g[i].b.trans ? 1 : 0);
+    if (modes >= 0 && m != modes) return -1;
+    modes = m;
+  }
+  return modes;
 }
 
 int gemm_launch(const asr_gemm_t* problems, int nprob, int compute_dtype, void* workspace,
@@ -482,7 +698,16 @@ int gemm_launch(const asr_gemm_t* problems, int nprob, int compute_dtype, void* 
   for (int i = 0; i < nprob; ++i)
     flops += 2.0 * problems[i].M * problems[i].N * problems[i].K * P.p[i].batch;
   const int slot = prof_begin_launch(ASR_PROF_GEMM, s, flops);
-  if (compute_dtype == ASR_DT_BF16) {
+  const int fast = compute_dtype == ASR_DT_BF16 ? fast_modes(problems, P) : -1;
+  if (fast >= 0) {
+    const size_t lds = 4 * FTILE;
+    switch (fast) {
+      case 0: hipLaunchKernelGGL((gemm_bf16_fast<0, 0>), grid, dim3(NT), lds, s, P); break;
+      case 1: hipLaunchKernelGGL((gemm_bf16_fast<0, 1>), grid, dim3(NT), lds, s, P); break;
+      case 2: hipLaunchKernelGGL((gemm_bf16_fast<1, 0>), grid, dim3(NT), lds, s, P); break;
+      default: hipLaunchKernelGGL((gemm_bf16_fast<1, 1>), grid, dim3(NT), lds, s, P); break;
+    }
+  } else if (compute_dtype == ASR_DT_BF16) {
     const size_t lds = 2 * BM * LDB16 * 2;
     hipLaunchKernelGGL(gemm_kernel<true>, grid, dim3(NT), lds, s, P);
   } else {

@@ -31,10 +31,10 @@ size_t persist_ctr_bytes(int B);
 int persist_rows(int B);
 int lstm_fwd_persistent(int B, int T, int H, const int32_t* lens, const uint16_t* wbf,
                         float* gx_act, float* y, float* cst, uint16_t* hx, int* ctr,
-                        hipStream_t s, bool dry);
+                        uint16_t* ybf, hipStream_t s, bool dry);
 int lstm_bwd_persistent(int B, int T, int H, const int32_t* lens, const uint16_t* wt,
                         const float* dy, float* act_dg, const float* cst, uint16_t* dgx, int* ctr,
-                        hipStream_t s, bool dry);
+                        uint16_t* dgbf, hipStream_t s, bool dry);
 
 namespace {
 
@@ -448,6 +448,12 @@ __global__ void convert_bf16(const float* __restrict__ wf, const float* __restri
 
 size_t al256(size_t n) { return (n + 255) & ~size_t(255); }
 
+__global__ void to_bf16(const float* __restrict__ x, uint16_t* __restrict__ y, long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    y[i] = f2bf(x[i]);
+}
+
 // Forward workspace: [hand-off counters][ping-pong h: 2 parity x 2 dir x Bp x H,
 // compute dtype][bf16 copy of W_hh (bf16 mode)], Bp = B rounded up to 16.
 size_t fwd_ctr_bytes(int B) { return al256(persist_ctr_bytes(B)); }
@@ -487,8 +493,8 @@ extern "C" size_t asr_lstm_workspace_bytes(int B, int H, int compute_dtype, int 
 
 extern "C" int asr_lstm_forward(float* gx_act, const void* whh_f, const void* whh_r, int w_dtype,
                                 const int32_t* lens, int B, int T, int H, int compute_dtype,
-                                float* y, float* cst, void* workspace, size_t ws_bytes,
-                                void* stream) {
+                                float* y, float* cst, uint16_t* ybf, void* workspace,
+                                size_t ws_bytes, void* stream) {
   ASR_REQUIRE(gx_act && whh_f && whh_r && lens && y && cst && workspace, ASR_ERR_ARG,
               "lstm_forward: null pointer");
   ASR_REQUIRE(B > 0 && T > 0 && H > 0, ASR_ERR_ARG, "lstm_forward: bad shape");
@@ -515,12 +521,13 @@ extern "C" int asr_lstm_forward(float* gx_act, const void* whh_f, const void* wh
     wbf_r = wb + n;
   }
   if (bf && wbf_r == wbf_f + 4LL * H * H &&
-      lstm_fwd_persistent(B, T, H, lens, wbf_f, gx_act, y, cst, (uint16_t*)hbuf, ctr, s, true)) {
+      lstm_fwd_persistent(B, T, H, lens, wbf_f, gx_act, y, cst, (uint16_t*)hbuf, ctr, ybf, s,
+                          true)) {
     // one persistent launch for the whole pass
     ASR_CHECK_HIP(hipMemsetAsync(ctr, 0, fwd_ctr_bytes(B), s));
     const int slot = prof_begin_launch(ASR_PROF_LSTM_FWD_SEQ, s);
     const int rc = lstm_fwd_persistent(B, T, H, lens, wbf_f, gx_act, y, cst, (uint16_t*)hbuf,
-                                       ctr, s, false);
+                                       ctr, ybf, s, false);
     ASR_REQUIRE(rc == 1, ASR_ERR_HIP, "lstm_forward: persistent launch failed");
     prof_end_launch(ASR_PROF_LSTM_FWD_SEQ, slot, s);
     return ASR_OK;
@@ -553,13 +560,20 @@ extern "C" int asr_lstm_forward(float* gx_act, const void* whh_f, const void* wh
     ASR_LAUNCH_CHECK();
     prof_end_launch(ASR_PROF_LSTM_FWD, slot, s);
   }
+  if (ybf) {  // bf16 copy of y (the persistent path writes it in-kernel)
+    const long long n = (long long)B * T * 2 * H;
+    hipLaunchKernelGGL(to_bf16, dim3((unsigned)min(4096LL, (n + 255) / 256)), dim3(256), 0, s, y,
+                       ybf, n);
+    ASR_LAUNCH_CHECK();
+  }
   return ASR_OK;
 }
 
 extern "C" int asr_lstm_backward(const float* dy, const void* whh_f, const void* whh_r,
                                  int w_dtype, const int32_t* lens, int B, int T, int H,
                                  int compute_dtype, float* act_dg, const float* cst,
-                                 void* workspace, size_t ws_bytes, void* stream) {
+                                 uint16_t* dgbf, void* workspace, size_t ws_bytes,
+                                 void* stream) {
   ASR_REQUIRE(whh_f && whh_r && lens && act_dg && cst && workspace, ASR_ERR_ARG,
               "lstm_backward: null pointer");
   ASR_REQUIRE(B > 0 && T > 0 && H > 0, ASR_ERR_ARG, "lstm_backward: bad shape");
@@ -574,7 +588,7 @@ extern "C" int asr_lstm_backward(const float* dy, const void* whh_f, const void*
   void* dg = base + L.dg;
   float* dcb = (float*)(base + L.dcb);
   const bool persist = bf && lstm_bwd_persistent(B, T, H, lens, (const uint16_t*)wt, dy, act_dg,
-                                                 cst, (uint16_t*)dg, ctr, s, true);
+                                                 cst, (uint16_t*)dg, ctr, dgbf, s, true);
   if (persist)
     ASR_CHECK_HIP(hipMemsetAsync(ctr, 0, L.wt, s));
   else
@@ -596,7 +610,7 @@ extern "C" int asr_lstm_backward(const float* dy, const void* whh_f, const void*
   if (persist) {  // one persistent launch for the whole pass
     const int slot = prof_begin_launch(ASR_PROF_LSTM_BWD_SEQ, s);
     const int rc = lstm_bwd_persistent(B, T, H, lens, (const uint16_t*)wt, dy, act_dg, cst,
-                                       (uint16_t*)dg, ctr, s, false);
+                                       (uint16_t*)dg, ctr, dgbf, s, false);
     ASR_REQUIRE(rc == 1, ASR_ERR_HIP, "lstm_backward: persistent launch failed");
     prof_end_launch(ASR_PROF_LSTM_BWD_SEQ, slot, s);
     return ASR_OK;
@@ -629,6 +643,12 @@ extern "C" int asr_lstm_backward(const float* dy, const void* whh_f, const void*
                          (const float*)wt, dy, act_dg, cst, (float*)dg, dcb, vec);
     ASR_LAUNCH_CHECK();
     prof_end_launch(ASR_PROF_LSTM_BWD, slot, s);
+  }
+  if (dgbf) {  // bf16 copy of the gate gradients (the persistent path writes it in-kernel)
+    const long long n = (long long)B * T * 8 * H;
+    hipLaunchKernelGGL(to_bf16, dim3((unsigned)min(4096LL, (n + 255) / 256)), dim3(256), 0, s,
+                       act_dg, dgbf, n);
+    ASR_LAUNCH_CHECK();
   }
   return ASR_OK;
 }

@@ -34,7 +34,9 @@ constexpr int PFU = 8;           // forward: hidden units per work-group (32 gat
 constexpr int PBU = 16;          // backward: hidden units per work-group
 constexpr int CTR_STRIDE = 64;   // ints between polled words (own 256-B line each)
 constexpr unsigned SPIN_LIMIT = 1u << 18;
-constexpr size_t PIN_LDS = 96 * 1024;  // > 80 KB dynamic LDS -> one work-group per CU
+constexpr size_t PIN_LDS = 96 * 1024;   // forward: > 80 KB dynamic LDS -> one work-group per CU
+constexpr size_t PIN_LDS_B = 140 * 1024; // backward: also leaves no room for a GEMM work-group
+                                         // (20 KB) running beside it on another stream
 
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 typedef __attribute__((address_space(1))) int gint;
@@ -75,7 +77,7 @@ template <int KSW>
 __global__ void __launch_bounds__(256) lstm_fwd_persist(
     int B, int T, int H, const int32_t* __restrict__ lens, const uint16_t* __restrict__ wbf,
     float* __restrict__ gx_act, float* __restrict__ y, float* __restrict__ cst, uint16_t* hx,
-    int* ctr) {
+    int* ctr, int pubw, uint16_t* __restrict__ ybf) {
   __shared__ float part[4][PRB][2 * PRB];
   __shared__ __attribute__((aligned(16))) uint16_t hrow[PRB][PFU];
   __shared__ int s_ok;
@@ -175,7 +177,9 @@ __global__ void __launch_bounds__(256) lstm_fwd_persist(
       hrow[r][uu] = hb;
     }
     __syncthreads();
-    if (wave == 0) {  // publish h_t: 16 rows x 16 B, write-through; drain; one arrival
+    // publish h_t: 16 rows x 16 B, write-through; drain; one arrival (by wave
+    // pubw: 0 by default, see pub_last_wave)
+    if (wave == pubw) {
       if (lane < PRB) {
         const u32x4 v = *reinterpret_cast<const u32x4*>(&hrow[lane][0]);
         const unsigned off =
@@ -184,6 +188,12 @@ __global__ void __launch_bounds__(256) lstm_fwd_persist(
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) arrive(my_ctr);
+      // bf16 copy of y for the weight-gradient GEMMs (after the arrival: off the
+      // hand-off's critical path)
+      if (ybf && lane < PRB && b0 + lane < B) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(&hrow[lane][0]);
+        *reinterpret_cast<u32x4*>(ybf + ((long long)(b0 + lane) * T + t) * 2 * H + dir * H + u0) = v;
+      }
     }
   }
 }
@@ -198,7 +208,7 @@ template <int KSW>
 __global__ void __launch_bounds__(512) lstm_bwd_persist(
     int B, int T, int H, const int32_t* __restrict__ lens, const uint16_t* __restrict__ wt,
     const float* __restrict__ dy, float* __restrict__ act_dg, const float* __restrict__ cst,
-    uint16_t* dgx, int* ctr) {
+    uint16_t* dgx, int* ctr, int pubw, uint16_t* __restrict__ dgbf) {
   __shared__ float part[8][PRB][PBU];
   __shared__ __attribute__((aligned(16))) uint16_t dgrow[PRB][4][PBU];
   __shared__ int s_ok;
@@ -291,7 +301,9 @@ __global__ void __launch_bounds__(512) lstm_bwd_persist(
       dgrow[r][3][uu] = f2bf(d_o);
     }
     __syncthreads();
-    if (wave == 0) {  // publish dg_t: 16 rows x 4 gates x 32 B = 128 x 16 B, write-through
+    // publish dg_t: 16 rows x 4 gates x 32 B = 128 x 16 B, write-through; drain;
+    // one arrival (by wave pubw)
+    if (wave == pubw) {
       const unsigned rowbase = (unsigned)((((q & 1) * 2 + dir) * Bp + b0) * (long long)H4 * 2);
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
@@ -303,6 +315,18 @@ __global__ void __launch_bounds__(512) lstm_bwd_persist(
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) arrive(my_ctr);
+      if (dgbf) {  // bf16 gate gradients [B][T][8H] for the weight-gradient GEMMs
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const int e = lane + 64 * p;
+          const int rr = e >> 3, g = (e >> 1) & 3, half = e & 1;
+          if (b0 + rr < B) {
+            const u32x4 v = *reinterpret_cast<const u32x4*>(&dgrow[rr][g][half * 8]);
+            *reinterpret_cast<u32x4*>(dgbf + ((long long)(b0 + rr) * T + t) * 8 * H +
+                                      dir * H4 + g * H + u0 + half * 8) = v;
+          }
+        }
+      }
     }
   }
 }
@@ -326,10 +350,18 @@ bool persist_enabled() {
   return !(e && e[0] == '0');
 }
 
+// Which wave publishes the hand-off payload: wave 0 (owns cells; default, it
+// measured 4 % faster per pass in an interleaved A/B) or, with
+// ASR_LSTM_PUBW=1, the last wave (owns no cells).
+bool pub_last_wave() {
+  const char* e = getenv("ASR_LSTM_PUBW");
+  return e && e[0] == '1';
+}
+
 template <typename K>
-bool fits(K kernel, int threads, int grid) {
+bool fits(K kernel, int threads, int grid, size_t lds) {
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, PIN_LDS) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, lds) !=
       hipSuccess)
     return false;
   return per_cu >= 1 && grid <= num_cus();  // one work-group per CU (PIN_LDS)
@@ -349,17 +381,18 @@ int persist_rows(int B) { return ((B + PRB - 1) / PRB) * PRB; }
 // returns 1, or 0 / -1 if not eligible / the launch failed.
 int lstm_fwd_persistent(int B, int T, int H, const int32_t* lens, const uint16_t* wbf,
                         float* gx_act, float* y, float* cst, uint16_t* hx, int* ctr,
-                        hipStream_t s, bool dry) {
+                        uint16_t* ybf, hipStream_t s, bool dry) {
   if (!persist_enabled() || H % 32 != 0) return 0;
   const int nks = H / 32;
   const int ksw = (nks + 3) / 4;
   const int grid = (H / PFU) * 2 * ((B + PRB - 1) / PRB);
+  const int pw = pub_last_wave() ? 3 : 0;
 #define ASR_FWD_P(KS)                                                                          \
   do {                                                                                         \
-    if (!fits(lstm_fwd_persist<KS>, 256, grid)) return 0;                                      \
+    if (!fits(lstm_fwd_persist<KS>, 256, grid, PIN_LDS)) return 0;                                      \
     if (dry) return 1;                                                                         \
     hipLaunchKernelGGL(lstm_fwd_persist<KS>, dim3(grid), dim3(256), PIN_LDS, s, B, T, H, lens, \
-                       wbf, gx_act, y, cst, hx, ctr);                                          \
+                       wbf, gx_act, y, cst, hx, ctr, pw, ybf);                                  \
   } while (0)
   if (ksw <= 1) ASR_FWD_P(1);
   else if (ksw <= 2) ASR_FWD_P(2);
@@ -372,17 +405,18 @@ int lstm_fwd_persistent(int B, int T, int H, const int32_t* lens, const uint16_t
 
 int lstm_bwd_persistent(int B, int T, int H, const int32_t* lens, const uint16_t* wt,
                         const float* dy, float* act_dg, const float* cst, uint16_t* dgx, int* ctr,
-                        hipStream_t s, bool dry) {
+                        uint16_t* dgbf, hipStream_t s, bool dry) {
   if (!persist_enabled() || H % 32 != 0) return 0;
   const int nks = H / 8;
   const int ksw = (nks + 7) / 8;
   const int grid = (H / PBU) * 2 * ((B + PRB - 1) / PRB);
+  const int pw = pub_last_wave() ? 7 : 0;
 #define ASR_BWD_P(KS)                                                                          \
   do {                                                                                         \
-    if (!fits(lstm_bwd_persist<KS>, 512, grid)) return 0;                                      \
+    if (!fits(lstm_bwd_persist<KS>, 512, grid, PIN_LDS_B)) return 0;                                      \
     if (dry) return 1;                                                                         \
-    hipLaunchKernelGGL(lstm_bwd_persist<KS>, dim3(grid), dim3(512), PIN_LDS, s, B, T, H, lens, \
-                       wt, dy, act_dg, cst, dgx, ctr);                                         \
+    hipLaunchKernelGGL(lstm_bwd_persist<KS>, dim3(grid), dim3(512), PIN_LDS_B, s, B, T, H, lens, \
+                       wt, dy, act_dg, cst, dgx, ctr, pw, dgbf);                                  \
   } while (0)
   if (ksw <= 2) ASR_BWD_P(2);
   else if (ksw <= 4) ASR_BWD_P(4);

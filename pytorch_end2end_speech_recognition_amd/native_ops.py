@@ -9,6 +9,7 @@ Weight gradients are accumulated by the kernels directly into ``param.grad``
 the Functions therefore return ``None`` for weights.
 """
 import ctypes
+import os
 
 import torch
 
@@ -52,7 +53,9 @@ def rowmap(stride_t, stride_b=0, rows_per_b=0, t_mul=1, t_add=0, t_limit=0, perm
 
 def operand(t, trans, rmap, offset=0):
     dt = BF16 if t.dtype == torch.bfloat16 else F32
-    return N.Operand(t.data_ptr() + offset * t.element_size(), dt, int(trans), rmap)
+    es = t.element_size()
+    nbytes = t.untyped_storage().nbytes() - (t.storage_offset() + offset) * es
+    return N.Operand(t.data_ptr() + offset * es, dt, int(trans), rmap, int(nbytes))
 
 
 def gemm_problem(a, b, c, c_map, M, N_, K, alpha=1.0, beta=0.0, bias=None, bias2=None, c_offset=0,
@@ -345,7 +348,13 @@ class BLSTMLayerFn(torch.autograd.Function):
     x_src[perm[b] if perm else b, t*t_mul + t_add].  Parameters are passed as
     (w_ih [8H, Din], w_hh [8H, H], b_ih [8H], b_hh [8H]) where each is the
     forward-direction tensor immediately followed in memory by the reverse one
-    (the flat layout of models/pytorch_v3/base.py)."""
+    (the flat layout of models/pytorch_v3/base.py).
+
+    bf16 mode stages every GEMM operand in bf16 once (the gathered input X and
+    W_ih by one conversion pass each; y and dG are written in bf16 by the
+    recurrence kernels themselves), so all four layer GEMMs take the
+    buffer->LDS bf16 fast path of gemm.hip.  fp32 mode reads the f32 tensors
+    directly (exact-f32 MFMA, parity mode)."""
 
     @staticmethod
     def forward(ctx, x_src, lens, T, perm, t_mul, t_add, gbufs, w_ih, w_hh, b_ih, b_hh,
@@ -355,79 +364,147 @@ class BLSTMLayerFn(torch.autograd.Function):
         B, T_src, Din = x_src.shape
         H = w_hh.shape[1]
         dev = x_src.device
+        cd = compute_dtype()
         a_map = rowmap(Din, stride_b=T_src * Din, rows_per_b=T, t_mul=t_mul, t_add=t_add,
                        t_limit=T_src, perm=perm)
         gx = torch.empty(B, T, 8 * H, dtype=torch.float32, device=dev)
-        p = gemm_problem(operand(x_src, 0, a_map), operand(w_ih, 0, rowmap(Din)), gx,
-                         rowmap(8 * H), B * T, 8 * H, Din, bias=b_ih, bias2=b_hh)
+        if cd == BF16:
+            x_op = convert_rows_bf16(x_src, a_map, B * T, Din)        # [B*T, Din]
+            w_op = convert_rows_bf16(w_ih, rowmap(Din), 8 * H, Din)   # [8H, Din]
+            p = gemm_problem(operand(x_op, 0, rowmap(Din)), operand(w_op, 0, rowmap(Din)), gx,
+                             rowmap(8 * H), B * T, 8 * H, Din, bias=b_ih, bias2=b_hh)
+            y_bf = torch.empty(B, T, 2 * H, dtype=torch.bfloat16, device=dev)
+        else:
+            x_op, w_op, y_bf = x_src, w_ih, None
+            p = gemm_problem(operand(x_src, 0, a_map), operand(w_ih, 0, rowmap(Din)), gx,
+                             rowmap(8 * H), B * T, 8 * H, Din, bias=b_ih, bias2=b_hh)
         run_gemm([p], dev)
         y = torch.empty(B, T, 2 * H, dtype=torch.float32, device=dev)
         cst = torch.empty(B, T, 2 * H, dtype=torch.float32, device=dev)
-        cd = compute_dtype()
         nb = N.query('asr_lstm_workspace_bytes', B, H, cd, 0)
         ws = _ws(nb, dev)
         whh_r = w_hh.data_ptr() + 4 * H * H * 4
         N.call('asr_lstm_forward', N.ptr(gx), N.ptr(w_hh), ctypes.c_void_p(whh_r), F32, N.ptr(lens),
-               B, T, H, cd, N.ptr(y), N.ptr(cst), N.ptr(ws), nb, N.stream_handle(dev))
-        ctx.save_for_backward(x_src, lens, w_ih, w_hh, b_ih, b_hh, gx, cst, y)
-        ctx.meta = (T, perm, t_mul, t_add, gbufs)
+               B, T, H, cd, N.ptr(y), N.ptr(cst), N.ptr(y_bf), N.ptr(ws), nb,
+               N.stream_handle(dev))
+        ctx.save_for_backward(x_op, w_op, lens, w_hh, b_ih, b_hh, gx, cst,
+                              y_bf if y_bf is not None else y)
+        ctx.meta = (T, perm, t_mul, t_add, gbufs, cd, (B, T_src, Din), w_ih)
         ctx.n_graph = len(graph_params)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x_src, lens, w_ih, w_hh, b_ih, b_hh, act, cst, y = ctx.saved_tensors
-        T, perm, t_mul, t_add, gbufs = ctx.meta
-        B, T_src, Din = x_src.shape
+        x_op, w_op, lens, w_hh, b_ih, b_hh, act, cst, y_op = ctx.saved_tensors
+        T, perm, t_mul, t_add, gbufs, cd, (B, T_src, Din), w_ih = ctx.meta
         H = w_hh.shape[1]
-        dev = x_src.device
+        dev = act.device
         dy = dy.contiguous()
-        cd = compute_dtype()
         nb = N.query('asr_lstm_workspace_bytes', B, H, cd, 1)
         ws = _ws(nb, dev)
         whh_r = w_hh.data_ptr() + 4 * H * H * 4
+        dg_bf = (torch.empty(B, T, 8 * H, dtype=torch.bfloat16, device=dev) if cd == BF16
+                 else None)
         # the saved activations become the gate gradients dG in place
         N.call('asr_lstm_backward', N.ptr(dy), N.ptr(w_hh), ctypes.c_void_p(whh_r), F32,
-               N.ptr(lens), B, T, H, cd, N.ptr(act), N.ptr(cst), N.ptr(ws), nb,
+               N.ptr(lens), B, T, H, cd, N.ptr(act), N.ptr(cst), N.ptr(dg_bf), N.ptr(ws), nb,
                N.stream_handle(dev))
-        dg = act
-        BT = B * T
-        a_map = rowmap(Din, stride_b=T_src * Din, rows_per_b=T, t_mul=t_mul, t_add=t_add,
-                       t_limit=T_src, perm=perm)
+        dg_op = dg_bf if dg_bf is not None else act
         if gbufs is None:
             gbufs = tuple(grad_buffer(p) for p in (w_ih, w_hh, b_ih, b_hh))
-        g_ih, g_hh, g_bih, g_bhh = gbufs
-        probs = [
-            # dW_ih [8H, Din] += dG^T x   (both directions in one problem)
-            gemm_problem(operand(dg, 1, rowmap(8 * H)), operand(x_src, 1, a_map), g_ih,
-                         rowmap(Din), 8 * H, Din, BT, beta=1.0),
-        ]
-        run_gemm(probs, dev)
-        # dW_hh[dir] += dG_dir^T h_prev_dir ; h_prev = y[b, t-1, :H] (fwd), y[b, t+1, H:] (rev)
-        hp_f = rowmap(2 * H, stride_b=T * 2 * H, rows_per_b=T, t_add=-1, t_limit=T)
-        hp_r = rowmap(2 * H, stride_b=T * 2 * H, rows_per_b=T, t_add=1, t_limit=T)
-        probs = [
-            gemm_problem(operand(dg, 1, rowmap(8 * H)), operand(y, 1, hp_f), g_hh, rowmap(H),
-                         4 * H, H, BT, beta=1.0),
-            gemm_problem(operand(dg, 1, rowmap(8 * H), offset=4 * H),
-                         operand(y, 1, hp_r, offset=H), g_hh, rowmap(H), 4 * H, H, BT, beta=1.0,
-                         c_offset=4 * H * H),
-        ]
-        run_gemm(probs, dev)
-        colsum_accumulate(dg.view(BT, 8 * H), g_bih, g_bhh)
+        # X as the dW_ih operand: the bf16 copy is already gathered (identity map)
+        if cd == BF16:
+            x_map = rowmap(Din)
+        else:
+            x_map = rowmap(Din, stride_b=T_src * Din, rows_per_b=T, t_mul=t_mul, t_add=t_add,
+                           t_limit=T_src, perm=perm)
+        side = _wgrad_side_stream(dev, B, H)
+        if side is None:
+            _blstm_wgrad(dg_op, act, x_op, x_map, y_op, T, gbufs, dev)
+        else:
+            # weight gradients on a CU-masked side stream, overlapping this
+            # layer's dX GEMM and the previous layer's backward recurrence;
+            # joined back into the main stream at the end of the backward pass
+            main = torch.cuda.current_stream(dev)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                _blstm_wgrad(dg_op, act, x_op, x_map, y_op, T, gbufs, dev)
+            for t in (dg_op, act, x_op, y_op) + ((perm,) if perm is not None else ()):
+                t.record_stream(side)
+            torch.autograd.Variable._execution_engine.queue_callback(
+                lambda: main.wait_stream(side))
+        BT = B * T
         dx = None
         if ctx.needs_input_grad[0]:
             # dX [BT, Din] = dG [BT, 8H] W_ih [8H, Din], scattered back through the input map
             if perm is None and t_mul == 1 and t_add == 0 and T == T_src:
-                dx = torch.empty_like(x_src)
+                dx = torch.empty(B, T_src, Din, dtype=torch.float32, device=dev)
             else:
-                dx = torch.zeros_like(x_src)
+                dx = torch.zeros(B, T_src, Din, dtype=torch.float32, device=dev)
             c_map = rowmap(Din, stride_b=T_src * Din, rows_per_b=T, t_mul=t_mul, t_add=t_add,
                            t_limit=T_src, perm=perm)
-            p = gemm_problem(operand(dg, 0, rowmap(8 * H)), operand(w_ih, 1, rowmap(Din)), dx,
+            p = gemm_problem(operand(dg_op, 0, rowmap(8 * H)), operand(w_op, 1, rowmap(Din)), dx,
                              c_map, BT, Din, 8 * H)
             run_gemm([p], dev)
         return (dx,) + (None,) * (10 + ctx.n_graph)
+
+
+def convert_rows_bf16(src, rmap, nrows, ncols):
+    """Dense bf16 [nrows, ncols] copy of the rows of `src` selected by a row map."""
+    out = torch.empty(nrows, ncols, dtype=torch.bfloat16, device=src.device)
+    N.call('asr_convert_rows_bf16', N.ptr(src), rmap, int(nrows), int(ncols), N.ptr(out),
+           N.stream_handle(src.device))
+    return out
+
+
+def _blstm_wgrad(dg, dg_f32, x_op, x_map, y_op, T, gbufs, dev):
+    """dW_ih, dW_hh, db_ih, db_hh of one BLSTM layer from its gate gradients
+    (dg: bf16 copy in bf16 mode, else the f32 tensor; biases always from f32)."""
+    B = dg.shape[0]
+    H = y_op.shape[2] // 2
+    Din = x_op.shape[-1]
+    BT = B * T
+    g_ih, g_hh, g_bih, g_bhh = gbufs
+    # dW_ih [8H, Din] += dG^T x   (both directions in one problem)
+    run_gemm([gemm_problem(operand(dg, 1, rowmap(8 * H)), operand(x_op, 1, x_map), g_ih,
+                           rowmap(Din), 8 * H, Din, BT, beta=1.0)], dev)
+    # dW_hh[dir] += dG_dir^T h_prev_dir ; h_prev = y[b, t-1, :H] (fwd), y[b, t+1, H:] (rev)
+    hp_f = rowmap(2 * H, stride_b=T * 2 * H, rows_per_b=T, t_add=-1, t_limit=T)
+    hp_r = rowmap(2 * H, stride_b=T * 2 * H, rows_per_b=T, t_add=1, t_limit=T)
+    run_gemm([
+        gemm_problem(operand(dg, 1, rowmap(8 * H)), operand(y_op, 1, hp_f), g_hh, rowmap(H),
+                     4 * H, H, BT, beta=1.0),
+        gemm_problem(operand(dg, 1, rowmap(8 * H), offset=4 * H),
+                     operand(y_op, 1, hp_r, offset=H), g_hh, rowmap(H), 4 * H, H, BT, beta=1.0,
+                     c_offset=4 * H * H),
+    ], dev)
+    colsum_accumulate(dg_f32.view(BT, 8 * H), g_bih, g_bhh)
+
+
+_side_streams = {}
+
+
+def _wgrad_side_stream(dev, B, H):
+    """The CU-masked stream (upper half of the CUs) for the weight-gradient
+    GEMMs when ASR_OVERLAP_WGRAD=1, else None (weight gradients stay on the
+    main stream).  Also None in fp32 parity mode, without the persistent
+    recurrence, or when the backward recurrence is too large to keep its
+    co-resident work-groups (one per CU) within the other half."""
+    if compute_dtype() != BF16 or os.environ.get('ASR_OVERLAP_WGRAD', '0') != '1':
+        return None
+    if os.environ.get('ASR_LSTM_PERSIST', '1') == '0' or H % 32:
+        return None
+    ent = _side_streams.get(dev.index)
+    if ent is None:
+        ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+        h = ctypes.c_void_p()
+        with torch.cuda.device(dev):
+            N.call('asr_stream_create_cu_masked', ncu // 2, ncu - ncu // 2, ctypes.byref(h))
+        ent = (torch.cuda.ExternalStream(h.value, device=dev), ncu // 2)
+        _side_streams[dev.index] = ent
+    stream, free_cus = ent
+    grid_bwd = (H // 16) * 2 * ((B + 15) // 16)
+    return stream if grid_bwd <= free_cus else None
 
 
 def blstm_layer(x_src, lens, T, w_ih, w_hh, b_ih, b_hh, perm=None, t_mul=1, t_add=0, gbufs=None,

@@ -200,3 +200,95 @@ def test_persistent_recurrence_matches_step_kernels(B, T, H, cuda_dev, monkeypat
     for b in range(B):
         assert not res['1'][0][b, lens[b]:].any()
     ops.set_compute_dtype('fp32')
+
+
+def _logical(store, trans, nrows, K, stride_t, stride_b=0, rows_per_b=0, t_add=0, t_limit=0):
+    """Materialise the logical [nrows, K] operand of asr_gemm from its flat
+    storage and row map (include/asr_hip.h): trans=0 -> element (i, k) at
+    row(i) + k; trans=1 -> at row(k) + i."""
+    flat = store.reshape(-1)
+    nlog = K if trans else nrows
+    width = nrows if trans else K
+    rpb = rows_per_b if rows_per_b > 0 else nlog + 1
+    out = np.zeros((nlog, width), np.float32)
+    for r in range(nlog):
+        b, t = divmod(r, rpb)
+        tp = t + t_add
+        if tp < 0 or (t_limit > 0 and tp >= t_limit):
+            continue
+        o = b * stride_b + tp * stride_t
+        out[r] = flat[o:o + width]
+    return out.T if trans else out
+
+
+@pytest.mark.parametrize('fast', ['1', '0'])
+def test_gemm_bf16_operand_modes(fast, cuda_dev, monkeypatch):
+    """bf16 operands through the range-checked buffer->LDS fast path (and the
+    generic kernel for comparison): all four (A, B) layout modes, k-row maps
+    with boundary zeros and per-utterance padding, a ragged K, split-K and a
+    batched product, against float64 of the same bf16 values."""
+    monkeypatch.setenv('ASR_GEMM_FAST', fast)
+    ops = _ops()
+    ops.set_compute_dtype('bf16')
+    rng = np.random.RandomState(7)
+
+    def bf(a):
+        return torch.from_numpy(a.astype(np.float32)).to(torch.bfloat16)
+
+    cases = [
+        # (M, N, K, a_trans, b_trans, k-row map for trans operands)
+        (300, 200, 136, 0, 0, None),
+        (200, 130, 4500, 1, 0, None),          # split-K (4 tiles, K >= 4096)
+        (256, 96, 700, 1, 1, (350, -1)),       # h_{t-1} style map: 2 groups of 350
+        (130, 257, 520, 0, 1, (260, 1)),       # h_{t+1} style map
+    ]
+    for M, Nn, K, at, bt, kmap in cases:
+        ops_ = []
+        mats = []
+        for trans, nrows in ((at, M), (bt, Nn)):
+            if not trans:
+                store = rng.randn(nrows, K).astype(np.float32)
+                rm = ops.rowmap(K)
+                logical = _logical(bf(store).float().numpy(), 0, nrows, K, K)
+            elif kmap is None:
+                store = rng.randn(K, nrows).astype(np.float32)
+                rm = ops.rowmap(nrows)
+                logical = _logical(bf(store).float().numpy(), 1, nrows, K, nrows)
+            else:
+                rpb, tadd = kmap
+                ngrp = K // rpb
+                store = rng.randn(ngrp * (rpb + 1), nrows).astype(np.float32)
+                rm = ops.rowmap(nrows, stride_b=(rpb + 1) * nrows, rows_per_b=rpb, t_add=tadd,
+                                t_limit=rpb)
+                logical = _logical(bf(store).float().numpy(), 1, nrows, K, nrows,
+                                   stride_b=(rpb + 1) * nrows, rows_per_b=rpb, t_add=tadd,
+                                   t_limit=rpb)
+            t = bf(store).to(cuda_dev)
+            ops_.append(ops.operand(t, trans, rm))
+            mats.append((t, logical))
+        C = torch.full((M, Nn), 0.5, dtype=torch.float32, device=cuda_dev)
+        bias = torch.from_numpy(rng.randn(Nn).astype(np.float32)).to(cuda_dev)
+        p = ops.gemm_problem(ops_[0], ops_[1], C, ops.rowmap(Nn), M, Nn, K, alpha=0.75,
+                             beta=1.0, bias=bias)
+        ops.run_gemm([p], cuda_dev)
+        torch.cuda.synchronize()
+        A = mats[0][1].astype(np.float64)
+        Bm = mats[1][1].astype(np.float64)
+        ref = 0.75 * A @ Bm.T + 0.5 + bias.cpu().numpy()[None, :]
+        got = C.cpu().numpy()
+        err = np.abs(got - ref).max() / (np.abs(ref).max() + 1e-6)
+        assert err < 1e-4, (M, Nn, K, at, bt, err)
+    # batched NT product (3 independent products, strided)
+    Bt, M, Nn, K = 3, 70, 40, 64
+    a = rng.randn(Bt, M, K).astype(np.float32)
+    b = rng.randn(Bt, Nn, K).astype(np.float32)
+    ad, bd = bf(a).to(cuda_dev), bf(b).to(cuda_dev)
+    C = torch.zeros(Bt, M, Nn, dtype=torch.float32, device=cuda_dev)
+    p = ops.gemm_problem(ops.operand(ad, 0, ops.rowmap(K)), ops.operand(bd, 0, ops.rowmap(K)), C,
+                         ops.rowmap(Nn), M, Nn, K, batch=Bt,
+                         batch_strides=(M * K, Nn * K, M * Nn))
+    ops.run_gemm([p], cuda_dev)
+    torch.cuda.synchronize()
+    ref = np.einsum('bmk,bnk->bmn', bf(a).double().numpy(), bf(b).double().numpy())
+    np.testing.assert_allclose(C.cpu().numpy(), ref, rtol=1e-4, atol=1e-3)
+    ops.set_compute_dtype('fp32')
