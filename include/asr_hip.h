@@ -333,6 +333,17 @@ int asr_prof_end(double* mean_us, long long* launches, double* mean_work, int nk
  * are invalid).  Synchronises `stream`; clear != 0 resets the word. */
 int asr_lstm_persist_status(int* status, int clear, void* stream);
 
+/* Hand-off protocols the tagged-granule recurrence (lstm_xg.hip) has run
+ * since the last clear: bit 0 write-through (sc1, any placement), bit 1
+ * XCD-local (every group's work-groups registered on one XCD).  Synchronises
+ * the device. */
+int asr_lstm_xg_mode(int* mode, int clear);
+
+/* Diagnostics (ASR_XG_TRACE=1 at the first recurrence launch): copies the
+ * per-step phase timestamps of work-groups 0..3 (4 x 128 steps x 6 u64) to
+ * `host` (may be NULL); returns the element count, 0 when tracing is off. */
+long long asr_xg_trace_read(unsigned long long* host);
+
 #ifdef __cplusplus
 }
 #endif

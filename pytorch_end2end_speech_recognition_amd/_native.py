@@ -79,6 +79,8 @@ SIGNATURES = {
     'asr_prof_begin': (c_int, [c_int]),
     'asr_prof_end': (c_int, [c_vp, c_vp, c_vp, c_int]),
     'asr_lstm_persist_status': (c_int, [c_vp, c_int, c_vp]),
+    'asr_lstm_xg_mode': (c_int, [c_vp, c_int]),
+    'asr_xg_trace_read': (c_ll, [c_vp]),
 }
 
 

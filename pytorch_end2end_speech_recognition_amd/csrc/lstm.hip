@@ -21,6 +21,8 @@
 // W_hh (a transposed copy, so each lane's 8-element MFMA fragment is contiguous).
 // The gate gradients are written over the saved activations and then feed the
 // weight-gradient GEMMs (asr_gemm) outside the recurrence.
+#include <algorithm>
+
 #include "mfma.h"
 #include "prof.h"
 
@@ -35,6 +37,15 @@ int lstm_fwd_persistent(int B, int T, int H, const int32_t* lens, const uint16_t
 int lstm_bwd_persistent(int B, int T, int H, const int32_t* lens, const uint16_t* wt,
                         const float* dy, float* act_dg, const float* cst, uint16_t* dgx, int* ctr,
                         uint16_t* dgbf, hipStream_t s, bool dry);
+// tagged-granule persistent recurrence (lstm_xg.hip), preferred when eligible
+size_t lstm_xg_fwd_bytes(int B, int H);
+size_t lstm_xg_bwd_bytes(int B, int H);
+int lstm_fwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* whh_f,
+                       const float* whh_r, float* gx_act, float* y, float* cst, void* ws,
+                       uint16_t* ybf, hipStream_t s, bool dry);
+int lstm_bwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* whh_f,
+                       const float* whh_r, const float* dy, float* act_dg, const float* cst,
+                       void* ws, uint16_t* dgbf, hipStream_t s, bool dry);
 
 namespace {
 
@@ -463,7 +474,8 @@ size_t fwd_state_bytes(int B, int H, int cdt) {
 
 size_t fwd_ws(int B, int H, int cdt) {
   size_t w = cdt == ASR_DT_BF16 ? (size_t)2 * 4 * H * H * 2 : 0;  // bf16 copy of W_hh
-  return fwd_state_bytes(B, H, cdt) + w;
+  const size_t xg = cdt == ASR_DT_BF16 ? lstm_xg_fwd_bytes(B, H) : 0;
+  return std::max(fwd_state_bytes(B, H, cdt) + w, xg);
 }
 
 // Backward workspace: [counters][W_hh^T][ping-pong dgates: 2 x 2 x Bp x 4H][dc f32 2 x B x H]
@@ -480,7 +492,10 @@ BwdLayout bwd_layout(int B, int H, int cdt) {
   l.total = l.dcb + (size_t)2 * B * H * 4;
   return l;
 }
-size_t bwd_ws(int B, int H, int cdt) { return bwd_layout(B, H, cdt).total; }
+size_t bwd_ws(int B, int H, int cdt) {
+  const size_t xg = cdt == ASR_DT_BF16 ? lstm_xg_bwd_bytes(B, H) : 0;
+  return std::max(bwd_layout(B, H, cdt).total, xg);
+}
 
 }  // namespace
 }  // namespace asr
@@ -507,6 +522,17 @@ extern "C" int asr_lstm_forward(float* gx_act, const void* whh_f, const void* wh
   const int vec = (H % 8 == 0) ? 1 : 0;
   dim3 grid(ceil_div(H, FU), 2, ceil_div(B, MB));
   ASR_REQUIRE(bf || w_dtype == ASR_DT_F32, ASR_ERR_ARG, "lstm_forward: f32 compute needs f32 W");
+  if (bf && w_dtype == ASR_DT_F32 &&
+      lstm_fwd_xg_launch(B, T, H, lens, (const float*)whh_f, (const float*)whh_r, gx_act, y, cst,
+                         workspace, ybf, s, true) == 1) {
+    // one persistent launch, tagged-granule hand-off (lstm_xg.hip)
+    const int slot = prof_begin_launch(ASR_PROF_LSTM_FWD_SEQ, s);
+    const int rc = lstm_fwd_xg_launch(B, T, H, lens, (const float*)whh_f, (const float*)whh_r,
+                                      gx_act, y, cst, workspace, ybf, s, false);
+    ASR_REQUIRE(rc == 1, ASR_ERR_HIP, "lstm_forward: tagged-granule launch failed");
+    prof_end_launch(ASR_PROF_LSTM_FWD_SEQ, slot, s);
+    return ASR_OK;
+  }
   // bf16 mode with f32 weights: one conversion pass so the T step launches
   // stream 2 bytes per weight instead of 4.
   const uint16_t* wbf_f = (const uint16_t*)whh_f;
@@ -581,6 +607,16 @@ extern "C" int asr_lstm_backward(const float* dy, const void* whh_f, const void*
               "lstm_backward: workspace too small");
   hipStream_t s = (hipStream_t)stream;
   const bool bf = compute_dtype == ASR_DT_BF16;
+  if (bf && w_dtype == ASR_DT_F32 &&
+      lstm_bwd_xg_launch(B, T, H, lens, (const float*)whh_f, (const float*)whh_r, dy, act_dg, cst,
+                         workspace, dgbf, s, true) == 1) {
+    const int slot = prof_begin_launch(ASR_PROF_LSTM_BWD_SEQ, s);
+    const int rc = lstm_bwd_xg_launch(B, T, H, lens, (const float*)whh_f, (const float*)whh_r, dy,
+                                      act_dg, cst, workspace, dgbf, s, false);
+    ASR_REQUIRE(rc == 1, ASR_ERR_HIP, "lstm_backward: tagged-granule launch failed");
+    prof_end_launch(ASR_PROF_LSTM_BWD_SEQ, slot, s);
+    return ASR_OK;
+  }
   const BwdLayout L = bwd_layout(B, H, compute_dtype);
   char* base = (char*)workspace;
   int* ctr = (int*)base;

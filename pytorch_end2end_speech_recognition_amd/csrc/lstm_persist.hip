@@ -429,6 +429,10 @@ int lstm_bwd_persistent(int B, int T, int H, const int32_t* lens, const uint16_t
 
 }  // namespace asr
 
+namespace asr {
+int lstm_xg_status(int* status, int clear, hipStream_t s);  // lstm_xg.hip
+}
+
 using namespace asr;
 
 extern "C" int asr_lstm_persist_status(int* status, int clear, void* stream) {
@@ -443,5 +447,7 @@ extern "C" int asr_lstm_persist_status(int* status, int clear, void* stream) {
                                          hipMemcpyHostToDevice, s));
     ASR_CHECK_HIP(hipStreamSynchronize(s));
   }
+  ASR_REQUIRE(lstm_xg_status(status, clear, s) == 0, ASR_ERR_HIP,
+              "persist_status: tagged-granule status read failed");
   return ASR_OK;
 }

@@ -1,0 +1,812 @@
+// Bidirectional LSTM recurrence, one persistent launch per layer pass, with the
+// recurrent hand-off done by tagged granules (gfx950, bf16 MFMA, f32 state).
+// Same semantics as lstm.hip / lstm_persist.hip (nn.LSTM bidirectional with
+// pack/pad behaviour, models/pytorch_v3/encoders/rnn.py:166-172, :218-224,
+// :343-390): gate order i,f,g,o; h0 = c0 = 0; the reverse direction starts at
+// each utterance's own last frame; padded frames produce zeros.
+//
+// Why a second persistent design (lstm_persist.hip is the counter form): a
+// hand-off there is payload store -> drain -> atomic arrival on a counter that
+// 64 producers share -> relaxed poll -> workgroup barrier -> payload loads,
+// i.e. three dependent fabric round trips plus a 64-way atomic fan-in per time
+// step.  Here the data IS the flag (cdna_hip_programming.md §6 Guideline 16,
+// form R2): every 8-byte granule is {32-bit payload, 32-bit tag = step + 1},
+// written by ONE sc1 store and swept by the consumer with sc1 loads until all
+// its tags match, so one step costs one store->load round trip.  Granule words
+// are zeroed by a memset before every launch (tag 0 never matches).
+//
+// Work split.  Groups of R utterances x one direction (R = 8, or 16 for larger
+// batches); a group is H/16 work-groups, each owning 16 hidden units for the
+// whole pass, its slice of W_hh held in VGPRs as MFMA fragments (converted to
+// bf16 once at kernel start), its cell states in registers.  Work-groups are
+// pinned one per CU and the grid is launched only when it is co-resident.
+//
+//   forward  (256 threads, 4 waves split K = H): publishes h_t [R][16] as bf16
+//            pairs; consumers gather the group's whole h_t [R][H] (K of the
+//            recurrent product) -- 16 KB of granules per work-group per step at
+//            R = 8, H = 512.
+//   backward (512 threads): the owner of units J turns dh_t(J) into the gate
+//            gradients dg_t [R][4 x 16] and multiplies them by ITS OWN 64 rows of
+//            W_hh, publishing f32 partial sums of dh_{t-1} for ALL H units.  A
+//            consumer sums the WPG partials of its 16 units.  This exchanges f32
+//            partials (better than rounding dg to bf16 for transport) and
+//            needs no transposed copy of W_hh.
+//
+// Spins are bounded; on give-up a work-group sets the abort word (seen by every
+// other spinner) and g_xg_status, and exits: results are then invalid and
+// asr_lstm_persist_status reports it.
+#include <algorithm>
+#include <cstdlib>
+
+#include "mfma.h"
+#include "prof.h"
+
+namespace asr {
+
+__device__ int g_xg_status;  // bit 0: a bounded spin gave up (results invalid)
+__device__ int g_xg_mode;    // bit 0: a launch ran write-through (sc1); bit 1: XCD-local
+// Diagnostics only (ASR_XG_TRACE=1): per-step phase timestamps (100 MHz
+// s_memrealtime) of work-groups 0..XG_TR_WG-1, steps 0..XG_TR_STEPS-1.
+__device__ unsigned long long* g_xg_trace;
+#define XG_TR_WG 4
+#define XG_TR_STEPS 128
+#define XG_TR_K 6
+#define XG_TR(step, k, val)                                                              \
+  do {                                                                                  \
+    if (tr && (step) < XG_TR_STEPS && lane == 0 && wave == 0)                          \
+      tr[((long long)blockIdx.x * XG_TR_STEPS + (step)) * XG_TR_K + (k)] = (val);      \
+  } while (0)
+
+namespace {
+
+constexpr int XU = 16;                 // hidden units per work-group
+constexpr unsigned XG_SPIN_LIMIT = 1u << 20;
+constexpr size_t XG_PIN_FWD = 96 * 1024;   // > 80 KB dynamic LDS: one work-group per CU
+constexpr size_t XG_PIN_BWD = 140 * 1024;
+constexpr unsigned AUX_SC1_VOL = 16u | (1u << 31);  // sc1; volatile (never hoisted from a spin)
+constexpr unsigned AUX_SC1 = 16u;
+
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+typedef __attribute__((address_space(1))) int gint;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t xg_rsrc(void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(p, 0, (int)bytes, 0x00020000);
+}
+
+__device__ __forceinline__ u32x4 ld_sc1(__amdgpu_buffer_rsrc_t rs, unsigned off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, AUX_SC1_VOL);
+}
+
+__device__ __forceinline__ int tags_ok(const u32x4& v, unsigned tag) {
+  return (int)(v[1] == tag) & (int)(v[3] == tag);
+}
+
+// Called by a whole wave after a failed sweep; false = give up (abort word set
+// by someone, or this wave's spin budget is spent).
+__device__ int g_xg_sleep;   // s_sleep(1) units between polls (ASR_XG_SLEEP, default 1)
+__device__ int g_xg_delay;   // s_sleep(1) units before a step's first poll (ASR_XG_DELAY)
+
+__device__ __forceinline__ void nap(int n) {
+  for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(1);
+}
+
+__device__ __forceinline__ bool keep_spinning(unsigned spins, int* abortw, int nsleep) {
+  if ((spins & 31u) == 31u) {
+    if (__hip_atomic_load((gint*)abortw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+    if (spins >= XG_SPIN_LIMIT) {
+      __hip_atomic_store((gint*)abortw, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      atomicOr(&g_xg_status, 1);
+      return false;
+    }
+  }
+  nap(nsleep);
+  return true;
+}
+
+// Work-group placement, decided once per launch.  tid 0 reads its XCD
+// (HW_REG_XCC_ID) and registers with ONE 64-bit agent-scope atomic add of
+// 1 << (8 * xcc) on the header's registry word, so a single word holds every
+// XCD's count consistently; it then waits until all gridDim.x work-groups
+// have registered.  If every XCD holds a whole number of groups, groups are
+// formed per XCD ("local" mode: a group's producers and consumers share one
+// L2, so hand-offs are plain stores into that L2 and sc1 loads that bypass
+// only the CU's L1).  Otherwise (or with allow_local = 0) groups follow
+// blockIdx and every granule is stored write-through (sc1), which is correct
+// for any placement.  Results never depend on placement: placement only
+// selects which of the two correct protocols runs.
+__device__ __forceinline__ void xg_place(int WPG, int allow_local, int* hdr, int* s_pl) {
+  if (threadIdx.x == 0) {
+    int* abortw = hdr;
+    typedef __attribute__((address_space(1))) unsigned long long gu64r;
+    gu64r* regw = (gu64r*)(hdr + 16);
+    const unsigned xcc =
+        __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 15u;  // XCC_ID[3:0]
+    int ok = xcc < 8;
+    unsigned long long old = 0, now = 0;
+    if (ok) old = __hip_atomic_fetch_add(regw, 1ull << (8 * xcc), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    for (unsigned spins = 0; ok; ++spins) {
+      now = __hip_atomic_load(regw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      unsigned tot = 0;
+      for (int x = 0; x < 8; ++x) tot += (unsigned)((now >> (8 * x)) & 255u);
+      if (tot >= gridDim.x) break;
+      if (__hip_atomic_load((gint*)abortw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
+          spins >= XG_SPIN_LIMIT) {
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (!ok) {
+      __hip_atomic_store((gint*)abortw, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      atomicOr(&g_xg_status, 1);
+    }
+    int local = ok && allow_local;
+    int before = 0;
+    for (int x = 0; x < 8; ++x) {
+      const int c = (int)((now >> (8 * x)) & 255u);
+      if (c % WPG) local = 0;
+      if (x < (int)xcc) before += c / WPG;
+    }
+    const int slot = (int)((old >> (8 * xcc)) & 255u);
+    if (local) {
+      s_pl[0] = before + slot / WPG;
+      s_pl[1] = slot % WPG;
+    } else {
+      s_pl[0] = blockIdx.x / WPG;
+      s_pl[1] = blockIdx.x % WPG;
+    }
+    s_pl[2] = local;
+    s_pl[3] = ok;
+    if (blockIdx.x == 0 && ok) atomicOr(&g_xg_mode, local ? 2 : 1);
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ bf16x8 frag_lo(const u32x4& a, const u32x4& b) {
+  // payload words of two 16-B granule pairs -> 8 bf16 (units in order)
+  u32x4 w = {a[0], a[2], b[0], b[2]};
+  return __builtin_bit_cast(bf16x8, w);
+}
+
+__device__ __forceinline__ bf16x8 cvt_f32x8(const float* p) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + 4);
+  u16x8 r;
+  r[0] = f2bf(a.x); r[1] = f2bf(a.y); r[2] = f2bf(a.z); r[3] = f2bf(a.w);
+  r[4] = f2bf(b.x); r[5] = f2bf(b.y); r[6] = f2bf(b.z); r[7] = f2bf(b.w);
+  return as_bf16x8(r);
+}
+
+__device__ __forceinline__ float fsig(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+__device__ __forceinline__ float ftanh(float x) { return 2.f * fsig(2.f * x) - 1.f; }
+
+// ---------------------------------------------------------------------------
+// forward.  grid = G * WPG (G = 2 * ceil(B / R) groups, WPG = H / 16).
+// Block -> (group, member); group -> (direction = grp & 1, row group).
+// Granules: xg[par][grp][row][H/2] u64 = {bf16 pair (units 2p, 2p+1), tag}.
+// Wave roles (each wave's vector-memory counter only waits for its own ops):
+//   waves 0..3 (sweepers): poll h_{t-1} granules, MFMA over their K quarter,
+//     partial gate sums -> LDS, barrier, next poll.  They issue nothing else,
+//     so a poll never waits behind output stores or input prefetches.
+//   waves 4.. (R/4 cell waves, one thread per (row, unit)): barrier, sum the
+//     partials + the prefetched input projection, cell update, publish h_t
+//     granules FIRST, then the y / c / activation / bf16-y stores and the next
+//     step's input-projection prefetch.
+// One __syncthreads per step; `part` is double-buffered by step parity.
+// ---------------------------------------------------------------------------
+template <int R, int KSW>
+__global__ void __launch_bounds__(256 + R * XU) lstm_fwd_xg(
+    int B, int T, int H, const int32_t* __restrict__ lens, const float* __restrict__ whh_f,
+    const float* __restrict__ whh_r, float* __restrict__ gx_act, float* __restrict__ y,
+    float* __restrict__ cst, unsigned long long* xg, int* hdr, uint16_t* __restrict__ ybf,
+    unsigned epoch, int allow_local) {
+  __shared__ float part[2][4][R][4 * XU + 4];
+  __shared__ int s_dead;  // a sweeper gave up: every wave exits after the next barrier
+  __shared__ int s_pl[4];
+  int* abortw = hdr;
+  const int WPG = H / XU;
+  const int G = gridDim.x / WPG;
+  if (threadIdx.x == 0) s_dead = 0;
+  xg_place(WPG, allow_local, hdr, s_pl);
+  if (!s_pl[3]) return;
+  const int grp = s_pl[0], mem = s_pl[1];
+  const bool local = s_pl[2] != 0;
+  const unsigned ep = epoch << 20;  // tag = launch epoch | (step + 1)
+  const int dir = grp & 1, rg = grp >> 1;
+  const int u0 = mem * XU, b0 = rg * R;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nks = H >> 5;
+  const unsigned half = (unsigned)(H / 2);
+  unsigned long long* tr = blockIdx.x < XG_TR_WG ? g_xg_trace : nullptr;
+
+  if (wave < 4) {
+    // ------------------------------ sweeper -------------------------------
+    const int kq = lane >> 4, ln = lane & 15;
+    const bool sweeper = ln < R;
+    // B fragments: B[k][n] = W_hh[g*H + u0 + n][k], n = ln, k = 32 ks + 8 kq + j
+    bf16x8 wf[KSW][4];
+    {
+      const float* W = dir ? whh_r : whh_f;
+#pragma unroll
+      for (int i = 0; i < KSW; ++i) {
+        const int ks = min(wave + 4 * i, nks - 1);
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          wf[i][g] = cvt_f32x8(W + (long long)(g * H + u0 + ln) * H + 32 * ks + 8 * kq);
+      }
+    }
+    const unsigned xg_bytes = (unsigned)(2ull * G * R * half * 8);
+    const __amdgpu_buffer_rsrc_t rs = xg_rsrc(xg, xg_bytes);
+    const int nsleep = __builtin_amdgcn_readfirstlane(g_xg_sleep);
+    const int ndelay = __builtin_amdgcn_readfirstlane(g_xg_delay);
+    for (int s = 0; s < T; ++s) {
+      XG_TR(s, 0, __builtin_amdgcn_s_memrealtime());
+      f32x4 acc[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (s > 0) {
+        const unsigned tag = ep | (unsigned)s;
+        const unsigned rowoff = (unsigned)((((((s - 1) & 1) * G + grp) * R + (sweeper ? ln : 0)) *
+                                            (long long)half) * 8);
+        u32x4 v[KSW][2];
+        nap(ndelay);
+        for (unsigned spins = 0;; ++spins) {
+          int ok = 1;  // bitwise ANDs: every load is issued before the first wait
+          if (sweeper) {
+            // k-steps past nks re-read the last one (no branch between the loads)
+#pragma unroll
+            for (int i = 0; i < KSW; ++i) {
+              const unsigned off =
+                  rowoff + (unsigned)((16 * min(wave + 4 * i, nks - 1) + 4 * kq) * 8);
+              v[i][0] = ld_sc1(rs, off);
+              v[i][1] = ld_sc1(rs, off + 16);
+            }
+#pragma unroll
+            for (int i = 0; i < KSW; ++i) ok &= tags_ok(v[i][0], tag) & tags_ok(v[i][1], tag);
+          }
+          if (__all(ok)) {
+            XG_TR(s, 1, __builtin_amdgcn_s_memrealtime());
+            XG_TR(s, 5, spins);
+            break;
+          }
+          if (!keep_spinning(spins, abortw, nsleep)) {
+            s_dead = 1;
+            break;
+          }
+        }
+        // MFMA is a whole-wave operation: never under a lane-divergent branch.
+        // Rows >= R (lanes that did not sweep) multiply zeros.
+#pragma unroll
+        for (int i = 0; i < KSW; ++i) {
+          if (wave + 4 * i < nks) {  // wave-uniform
+            u32x4 z = {0u, 0u, 0u, 0u};
+            const bf16x8 a = sweeper ? frag_lo(v[i][0], v[i][1]) : __builtin_bit_cast(bf16x8, z);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) acc[g] = mfma_bf16(a, wf[i][g], acc[g]);
+          }
+        }
+      }
+      // partial gate sums -> LDS (rows 4 kq + r; only rows < R are real)
+      if (4 * kq < R) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) part[s & 1][wave][4 * kq + r][g * XU + ln] = acc[g][r];
+      }
+      __syncthreads();
+      XG_TR(s, 2, __builtin_amdgcn_s_memrealtime());
+      if (s_dead) return;
+    }
+    return;
+  }
+
+  // -------------------------------- cell ----------------------------------
+  const int ct = tid - 256;
+  const int row = ct >> 4, unit = ct & 15;
+  const int b = b0 + row, j = u0 + unit;
+  const bool own = b < B;
+  const int len = own ? lens[b] : 0;
+  float c = 0.f;
+  const long long H8 = 8LL * H;
+  const long long gcol = (long long)dir * 4 * H + j;
+  gu64* xgg = (gu64*)xg;
+  float gxv[4] = {0.f, 0.f, 0.f, 0.f};
+  if (own) {
+    const int t0 = dir ? T - 1 : 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) gxv[q] = gx_act[((long long)b * T + t0) * H8 + gcol + (long long)q * H];
+  }
+  const int cw = wave - 4;  // trace as this block's first cell wave
+  for (int s = 0; s < T; ++s) {
+    const int t = dir ? T - 1 - s : s;
+    __syncthreads();
+    if (s_dead) return;
+    float h = 0.f, cn = 0.f, ig = 0.f, fg = 0.f, gg = 0.f, og = 0.f;
+    const bool active = own && t < len;
+    if (active) {
+      float pre[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int col = q * XU + unit;
+        pre[q] = part[s & 1][0][row][col] + part[s & 1][1][row][col] + part[s & 1][2][row][col] +
+                 part[s & 1][3][row][col] + gxv[q];
+      }
+      ig = fsig(pre[0]);
+      fg = fsig(pre[1]);
+      gg = ftanh(pre[2]);
+      og = fsig(pre[3]);
+      cn = fg * c + ig * gg;
+      h = og * ftanh(cn);
+    }
+    c = cn;
+    const unsigned hb = f2bf(h);
+    const unsigned hn = (unsigned)__shfl_down((int)hb, 1, 64);
+    const unsigned val = hb | (hn << 16);
+    if ((unit & 1) == 0) {
+      const unsigned long long gr = ((unsigned long long)(ep | (unsigned)(s + 1)) << 32) | val;
+      gu64* p = xgg + ((((long long)(s & 1) * G + grp) * R + row) * half + (j >> 1));
+      if (local)  // plain 8-B store: into this XCD's L2, where the group reads
+        __hip_atomic_store(p, gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      else        // write-through (sc1) 8-B store
+        __hip_atomic_store(p, gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (cw == 0 && lane == 0 && tr && s < XG_TR_STEPS)
+      tr[((long long)blockIdx.x * XG_TR_STEPS + s) * XG_TR_K + 3] = __builtin_amdgcn_s_memrealtime();
+    if (own) {
+      const long long sidx = ((long long)b * T + t) * 2 * H + (long long)dir * H + j;
+      y[sidx] = h;
+      cst[sidx] = cn;
+      const long long gb = ((long long)b * T + t) * H8 + gcol;
+      gx_act[gb] = ig;
+      gx_act[gb + H] = fg;
+      gx_act[gb + 2 * H] = gg;
+      gx_act[gb + 3 * H] = og;
+      if (ybf && (unit & 1) == 0)
+        *reinterpret_cast<uint32_t*>(ybf + ((long long)b * T + t) * 2 * H + dir * H + j) = val;
+      if (s + 1 < T) {
+        const int tn = dir ? t - 1 : t + 1;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          gxv[q] = gx_act[((long long)b * T + tn) * H8 + gcol + (long long)q * H];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// backward.  grid = G * WPG.  Processing step q handles the forward direction
+// at t = T-1-q and the reverse direction at t = q.
+// Granules: pg[par][grp][producer][row][H] u64 = {f32 partial of dh, tag}.
+// Wave roles, two barriers per step (B1: partials summed; B2: dg in LDS):
+//   waves 0..3 (sweepers): poll the partials of dh for this block's 16 units
+//     from every producer of the group, sum per producer subset -> LDS, B1, B2.
+//   R/4 cell waves: B1, dh = dy + sum, cell backward -> dg (bf16 -> LDS), B2,
+//     then the f32 / bf16 dg stores and the next step's prefetch.
+//   4 MFMA waves: B1, B2, partial dh_{t-1}[rows][all units] = dg x (this
+//     block's 64 rows of W_hh) -> write-through granules.
+// A fragments (VGPRs): A[m][k] = W_hh[gaterow(k)][m] for output unit m (M block
+// mb = mw + 4 i) and local gate row k in [0, 64): gate k >> 4, unit u0 + (k & 15).
+// ---------------------------------------------------------------------------
+template <int R, int MB>
+__global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
+    int B, int T, int H, const int32_t* __restrict__ lens, const float* __restrict__ whh_f,
+    const float* __restrict__ whh_r, const float* __restrict__ dy, float* __restrict__ act_dg,
+    const float* __restrict__ cst, unsigned long long* pg, int* hdr,
+    uint16_t* __restrict__ dgbf, unsigned epoch, int allow_local) {
+  constexpr int NPG = 256 / (8 * R);   // producer subsets swept in parallel
+  __shared__ float red[NPG][R][XU + 1];
+  __shared__ __attribute__((aligned(16))) uint16_t dgt[16][4 * XU + 8];
+  __shared__ int s_dead;
+  __shared__ int s_pl[4];
+  int* abortw = hdr;
+  const int WPG = H / XU;
+  const int G = gridDim.x / WPG;
+  if (threadIdx.x == 0) s_dead = 0;
+  xg_place(WPG, allow_local, hdr, s_pl);
+  if (!s_pl[3]) return;
+  const int grp = s_pl[0], mem = s_pl[1];
+  const bool local = s_pl[2] != 0;
+  const unsigned ep = epoch << 20;
+  const int dir = grp & 1, rg = grp >> 1;
+  const int u0 = mem * XU, b0 = rg * R;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int HB = H / XU;                 // output M blocks
+  const int H4 = 4 * H;
+  const unsigned pg_bytes = (unsigned)(2ull * G * WPG * R * H * 8);
+  const __amdgpu_buffer_rsrc_t rs = xg_rsrc(pg, pg_bytes);
+  unsigned long long* tr = blockIdx.x < XG_TR_WG ? g_xg_trace : nullptr;
+  for (int e = tid; e < 16 * (4 * XU + 8); e += blockDim.x) (&dgt[0][0])[e] = 0;
+  const int NCW = R / 4;                 // cell waves: 4 .. 4 + NCW - 1; MFMA waves after
+
+  if (wave < 4) {
+    // ------------------------------ sweeper -------------------------------
+    const int sl = tid & (8 * R - 1);
+    const int srow = sl >> 3, spr = sl & 7;
+    const int pgi = tid / (8 * R);
+    constexpr int MAXP = 64;  // WPG <= 64
+    const int nsleep = __builtin_amdgcn_readfirstlane(g_xg_sleep);
+    const int ndelay = __builtin_amdgcn_readfirstlane(g_xg_delay);
+    for (int q = 0; q < T; ++q) {
+      XG_TR(q, 0, __builtin_amdgcn_s_memrealtime());
+      if (q > 0) {
+        const unsigned tag = ep | (unsigned)q;
+        const long long base = ((long long)((q - 1) & 1) * G + grp) * WPG;
+        float s0 = 0.f, s1 = 0.f;
+        nap(ndelay);
+        for (unsigned spins = 0;; ++spins) {
+          int ok = 1;
+          s0 = 0.f;
+          s1 = 0.f;
+#pragma unroll 8
+          for (int w = pgi; w < MAXP; w += NPG) {
+            if (w >= WPG) break;
+            const unsigned off =
+                (unsigned)((((base + w) * R + srow) * (long long)H + u0 + 2 * spr) * 8);
+            const u32x4 v = ld_sc1(rs, off);
+            ok &= tags_ok(v, tag);
+            s0 += __uint_as_float(v[0]);
+            s1 += __uint_as_float(v[2]);
+          }
+          if (__all(ok)) {
+            XG_TR(q, 1, __builtin_amdgcn_s_memrealtime());
+            XG_TR(q, 5, spins);
+            break;
+          }
+          if (!keep_spinning(spins, abortw, nsleep)) {
+            s_dead = 1;
+            break;
+          }
+        }
+        red[pgi][srow][2 * spr] = s0;
+        red[pgi][srow][2 * spr + 1] = s1;
+      }
+      __syncthreads();  // B1
+      XG_TR(q, 2, __builtin_amdgcn_s_memrealtime());
+      if (s_dead) return;
+      __syncthreads();  // B2
+      XG_TR(q, 3, __builtin_amdgcn_s_memrealtime());
+    }
+    return;
+  }
+
+  if (wave < 4 + NCW) {
+    // -------------------------------- cell --------------------------------
+    const int ct = tid - 256;
+    const int row = ct >> 4, unit = ct & 15;
+    const int b = b0 + row, j = u0 + unit;
+    const bool own = b < B;
+    const int len = own ? lens[b] : 0;
+    float dc = 0.f;
+    auto load_cell = [&](int q, float (&av)[4], float& cc, float& cp, float& dyv) {
+      const int t = dir == 0 ? T - 1 - q : q;
+      const int tp = dir == 0 ? t - 1 : t + 1;
+      const long long gb = ((long long)b * T + t) * 8 * H + (long long)dir * H4 + j;
+      const long long si = ((long long)b * T + t) * 2 * H + (long long)dir * H + j;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) av[k] = act_dg[gb + (long long)k * H];
+      cc = cst[si];
+      cp = (tp >= 0 && tp < T) ? cst[si + (long long)(tp - t) * 2 * H] : 0.f;
+      dyv = dy ? dy[si] : 0.f;
+    };
+    float av[4] = {0.f, 0.f, 0.f, 0.f}, cc = 0.f, cp = 0.f, dyv = 0.f;
+    if (own) load_cell(0, av, cc, cp, dyv);
+    for (int q = 0; q < T; ++q) {
+      const int t = dir == 0 ? T - 1 - q : q;
+      __syncthreads();  // B1
+      if (s_dead) return;
+      float d_i = 0.f, d_f = 0.f, d_g = 0.f, d_o = 0.f;
+      if (own && t < len) {
+        float dh = dyv;
+        if (q > 0) {
+#pragma unroll
+          for (int p = 0; p < NPG; ++p) dh += red[p][row][unit];
+        }
+        const float ig = av[0], fg = av[1], gg = av[2], og = av[3];
+        const float tc = ftanh(cc);
+        const float dcell = dc + dh * og * (1.f - tc * tc);
+        d_i = dcell * gg * ig * (1.f - ig);
+        d_f = dcell * cp * fg * (1.f - fg);
+        d_g = dcell * ig * (1.f - gg * gg);
+        d_o = dh * tc * og * (1.f - og);
+        dc = dcell * fg;
+      } else {
+        dc = 0.f;
+      }
+      const uint16_t bi = f2bf(d_i), bff = f2bf(d_f), bg = f2bf(d_g), bo = f2bf(d_o);
+      dgt[row][unit] = bi;
+      dgt[row][XU + unit] = bff;
+      dgt[row][2 * XU + unit] = bg;
+      dgt[row][3 * XU + unit] = bo;
+      __syncthreads();  // B2
+      if (own) {
+        const long long gb = ((long long)b * T + t) * 8 * H + (long long)dir * H4 + j;
+        act_dg[gb] = d_i;
+        act_dg[gb + H] = d_f;
+        act_dg[gb + 2 * H] = d_g;
+        act_dg[gb + 3 * H] = d_o;
+        if (dgbf) {
+          uint16_t* o = dgbf + ((long long)b * T + t) * 8 * H + (long long)dir * H4 + j;
+          o[0] = bi;
+          o[H] = bff;
+          o[2 * H] = bg;
+          o[3 * H] = bo;
+        }
+        if (q + 1 < T) load_cell(q + 1, av, cc, cp, dyv);
+      }
+    }
+    return;
+  }
+
+  // --------------------------------- MFMA -----------------------------------
+  const int mw = wave - 4 - NCW;         // 0..3
+  const int kq = lane >> 4, ln = lane & 15;
+  bf16x8 wa[MB][2];
+  {
+    const float* W = dir ? whh_r : whh_f;
+#pragma unroll
+    for (int i = 0; i < MB; ++i) {
+      const int mb = min(mw + 4 * i, HB - 1);
+      const int m = 16 * mb + ln;
+#pragma unroll
+      for (int kst = 0; kst < 2; ++kst) {
+        u16x8 r;
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+          const int k = 32 * kst + 8 * kq + jj;
+          r[jj] = f2bf(W[(long long)((k >> 4) * H + u0 + (k & 15)) * H + m]);
+        }
+        wa[i][kst] = as_bf16x8(r);
+      }
+    }
+  }
+  for (int q = 0; q < T; ++q) {
+    __syncthreads();  // B1
+    if (s_dead) return;
+    __syncthreads();  // B2
+    const bf16x8 bf0 = *reinterpret_cast<const bf16x8*>(&dgt[ln][8 * kq]);
+    const bf16x8 bf1 = *reinterpret_cast<const bf16x8*>(&dgt[ln][32 + 8 * kq]);
+    const unsigned tag = ep | (unsigned)(q + 1);
+    const long long obase = (((long long)(q & 1) * G + grp) * WPG + mem) * R;
+#pragma unroll
+    for (int i = 0; i < MB; ++i) {
+      const int mb = mw + 4 * i;
+      if (mb < HB) {  // wave-uniform
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        acc = mfma_bf16(wa[i][0], bf0, acc);
+        acc = mfma_bf16(wa[i][1], bf1, acc);
+        if (ln < R) {  // C[m][n]: n = ln (row), m = 16 mb + 4 kq + r
+          const unsigned off =
+              (unsigned)(((obase + ln) * (long long)H + 16 * mb + 4 * kq) * 8);
+          const u32x4 v0 = {__float_as_uint(acc[0]), tag, __float_as_uint(acc[1]), tag};
+          const u32x4 v1 = {__float_as_uint(acc[2]), tag, __float_as_uint(acc[3]), tag};
+          if (local) {  // plain: into this XCD's L2
+            __builtin_amdgcn_raw_buffer_store_b128(v0, rs, off, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(v1, rs, off + 16, 0, 0);
+          } else {      // write-through
+            __builtin_amdgcn_raw_buffer_store_b128(v0, rs, off, 0, AUX_SC1);
+            __builtin_amdgcn_raw_buffer_store_b128(v1, rs, off + 16, 0, AUX_SC1);
+          }
+        }
+      }
+    }
+    if (mw == 0 && lane == 0 && tr && q < XG_TR_STEPS)
+      tr[((long long)blockIdx.x * XG_TR_STEPS + q) * XG_TR_K + 4] = __builtin_amdgcn_s_memrealtime();
+  }
+}
+
+int xg_num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n = 0;
+  }
+  return n;
+}
+
+// ASR_LSTM_XG=0 disables this path (A/B tests against lstm_persist.hip).
+bool xg_enabled() {
+  const char* e = getenv("ASR_LSTM_XG");
+  return !(e && e[0] == '0') && !(getenv("ASR_LSTM_PERSIST") && getenv("ASR_LSTM_PERSIST")[0] == '0');
+}
+
+// rows per group for this shape, or 0 if the grid cannot be co-resident
+int xg_rows(int B, int H) {
+  if (H % 32 != 0 || H / XU > 64) return 0;
+  const int ncu = xg_num_cus();
+  const int wpg = H / XU;
+  for (int R : {8, 16}) {
+    const int G = 2 * ((B + R - 1) / R);
+    if (G * wpg <= ncu) return R;
+  }
+  return 0;
+}
+
+template <typename K>
+bool xg_fits(K kernel, int threads, size_t lds) {
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, lds) != hipSuccess)
+    return false;
+  return per_cu >= 1;
+}
+
+}  // namespace
+
+void xg_trace_setup(hipStream_t s);
+
+constexpr size_t XG_HDR = 256;  // abort word + placement registry, zeroed with the granules
+
+unsigned xg_next_epoch() {
+  static unsigned e = 0;
+  e = (e + 1) & 0xFFFu;
+  return e;
+}
+
+int xg_allow_local() {
+  const char* e = getenv("ASR_XG_LOCAL");
+  return !(e && e[0] == '0');
+}
+
+size_t lstm_xg_fwd_bytes(int B, int H) {
+  const int R = xg_rows(B, H);
+  if (!R) return 0;
+  const long long rows = 2LL * ((B + R - 1) / R) * R;
+  return XG_HDR + (size_t)2 * rows * (H / 2) * 8;
+}
+
+size_t lstm_xg_bwd_bytes(int B, int H) {
+  const int R = xg_rows(B, H);
+  if (!R) return 0;
+  const long long rows = 2LL * ((B + R - 1) / R) * R;
+  return XG_HDR + (size_t)2 * rows * (H / XU) * H * 8;
+}
+
+// Returns 1 if launched (or, with dry, if this shape/device can take the
+// path), 0 if not eligible, -1 on a launch error.  ws must hold
+// lstm_xg_{fwd,bwd}_bytes; it is zeroed here before the launch.
+int lstm_fwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* whh_f,
+                       const float* whh_r, float* gx_act, float* y, float* cst, void* ws,
+                       uint16_t* ybf, hipStream_t s, bool dry) {
+  if (!xg_enabled()) return 0;
+  const int R = xg_rows(B, H);
+  if (!R) return 0;
+  int ksw = (H / 32 + 3) / 4;
+  if (ksw > 8) return 0;
+  if (getenv("ASR_XG_KSW")) ksw = std::max(ksw, atoi(getenv("ASR_XG_KSW")));  // diagnostics
+  const int grid = 2 * ((B + R - 1) / R) * (H / XU);
+  int* hdr = (int*)ws;
+  unsigned long long* g = (unsigned long long*)((char*)ws + XG_HDR);
+  const unsigned ep = xg_next_epoch();
+  const int al = xg_allow_local();
+#define ASR_XGF(RR, KS)                                                                         \
+  do {                                                                                          \
+    if (!xg_fits(lstm_fwd_xg<RR, KS>, 256 + RR * XU, XG_PIN_FWD)) return 0;                              \
+    if (dry) return 1;                                                                          \
+    if (hipMemsetAsync(ws, 0, lstm_xg_fwd_bytes(B, H), s) != hipSuccess) return -1;             \
+    xg_trace_setup(s);             \
+    hipLaunchKernelGGL((lstm_fwd_xg<RR, KS>), dim3(grid), dim3(256 + RR * XU), XG_PIN_FWD, s, B, T, H,     \
+                       lens, whh_f, whh_r, gx_act, y, cst, g, hdr, ybf, ep, al);                     \
+  } while (0)
+#define ASR_XGF_K(RR)                   \
+  do {                                  \
+    if (ksw <= 1) ASR_XGF(RR, 1);       \
+    else if (ksw <= 2) ASR_XGF(RR, 2);  \
+    else if (ksw <= 3) ASR_XGF(RR, 3);  \
+    else if (ksw <= 4) ASR_XGF(RR, 4);  \
+    else ASR_XGF(RR, 8);                \
+  } while (0)
+  if (R == 8) ASR_XGF_K(8);
+  else ASR_XGF_K(16);
+#undef ASR_XGF_K
+#undef ASR_XGF
+  return hipGetLastError() == hipSuccess ? 1 : -1;
+}
+
+int lstm_bwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* whh_f,
+                       const float* whh_r, const float* dy, float* act_dg, const float* cst,
+                       void* ws, uint16_t* dgbf, hipStream_t s, bool dry) {
+  if (!xg_enabled()) return 0;
+  const int R = xg_rows(B, H);
+  if (!R) return 0;
+  const int mb = (H / XU + 3) / 4;
+  if (mb > 16) return 0;
+  const int grid = 2 * ((B + R - 1) / R) * (H / XU);
+  int* hdr = (int*)ws;
+  unsigned long long* g = (unsigned long long*)((char*)ws + XG_HDR);
+  const unsigned ep = xg_next_epoch();
+  const int al = xg_allow_local();
+#define ASR_XGB(RR, M)                                                                          \
+  do {                                                                                          \
+    if (!xg_fits(lstm_bwd_xg<RR, M>, 512 + RR * XU, XG_PIN_BWD)) return 0;                               \
+    if (dry) return 1;                                                                          \
+    if (hipMemsetAsync(ws, 0, lstm_xg_bwd_bytes(B, H), s) != hipSuccess) return -1;             \
+    xg_trace_setup(s);             \
+    hipLaunchKernelGGL((lstm_bwd_xg<RR, M>), dim3(grid), dim3(512 + RR * XU), XG_PIN_BWD, s, B, T, H,      \
+                       lens, whh_f, whh_r, dy, act_dg, cst, g, hdr, dgbf, ep, al);                   \
+  } while (0)
+#define ASR_XGB_M(RR)                  \
+  do {                                 \
+    if (mb <= 1) ASR_XGB(RR, 1);       \
+    else if (mb <= 2) ASR_XGB(RR, 2);  \
+    else if (mb <= 4) ASR_XGB(RR, 4);  \
+    else if (mb <= 5) ASR_XGB(RR, 5);  \
+    else if (mb <= 8) ASR_XGB(RR, 8);  \
+    else ASR_XGB(RR, 16);              \
+  } while (0)
+  if (R == 8) ASR_XGB_M(8);
+  else ASR_XGB_M(16);
+#undef ASR_XGB_M
+#undef ASR_XGB
+  return hipGetLastError() == hipSuccess ? 1 : -1;
+}
+
+// ASR_XG_TRACE=1: allocate the trace buffer once and publish its pointer.
+void xg_tuning_setup(hipStream_t s) {
+  static bool done = false;
+  if (done) return;
+  done = true;
+  const char* a = getenv("ASR_XG_SLEEP");
+  const char* b = getenv("ASR_XG_DELAY");
+  const int sl = a ? atoi(a) : 1, dl = b ? atoi(b) : 0;
+  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_xg_sleep), &sl, sizeof(int), 0, hipMemcpyHostToDevice, s);
+  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_xg_delay), &dl, sizeof(int), 0, hipMemcpyHostToDevice, s);
+}
+
+void xg_trace_setup(hipStream_t s) {
+  xg_tuning_setup(s);
+  static unsigned long long* buf = nullptr;
+  if (!getenv("ASR_XG_TRACE") || buf) return;
+  const size_t n = (size_t)XG_TR_WG * XG_TR_STEPS * XG_TR_K;
+  if (hipMalloc(&buf, n * 8) != hipSuccess) return;
+  (void)hipMemsetAsync(buf, 0, n * 8, s);
+  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_xg_trace), &buf, sizeof(buf), 0, hipMemcpyHostToDevice, s);
+}
+
+int lstm_xg_status(int* status, int clear, hipStream_t s) {
+  int v = 0;
+  if (hipMemcpyFromSymbolAsync(&v, HIP_SYMBOL(g_xg_status), sizeof(int), 0,
+                               hipMemcpyDeviceToHost, s) != hipSuccess)
+    return -1;
+  if (hipStreamSynchronize(s) != hipSuccess) return -1;
+  *status |= v;
+  if (clear) {
+    const int zero = 0;
+    if (hipMemcpyToSymbolAsync(HIP_SYMBOL(g_xg_status), &zero, sizeof(int), 0,
+                               hipMemcpyHostToDevice, s) != hipSuccess)
+      return -1;
+    if (hipStreamSynchronize(s) != hipSuccess) return -1;
+  }
+  return 0;
+}
+
+}  // namespace asr
+
+// Diagnostics: copy the phase-timestamp trace (ASR_XG_TRACE=1) to host memory
+// (XG_TR_WG * XG_TR_STEPS * XG_TR_K u64).  Returns the element count, 0 if off.
+extern "C" long long asr_xg_trace_read(unsigned long long* host) {
+  unsigned long long* buf = nullptr;
+  if (hipMemcpyFromSymbol(&buf, HIP_SYMBOL(asr::g_xg_trace), sizeof(buf)) != hipSuccess || !buf)
+    return 0;
+  const size_t n = (size_t)XG_TR_WG * XG_TR_STEPS * XG_TR_K;
+  if (host && hipMemcpy(host, buf, n * 8, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return (long long)n;
+}
+
+// Which hand-off protocols the tagged-granule recurrence used since the last
+// clear: bit 0 write-through (sc1, any placement), bit 1 XCD-local.
+extern "C" int asr_lstm_xg_mode(int* mode, int clear) {
+  if (!mode) return ASR_ERR_ARG;
+  if (hipDeviceSynchronize() != hipSuccess) return ASR_ERR_HIP;
+  if (hipMemcpyFromSymbol(mode, HIP_SYMBOL(asr::g_xg_mode), sizeof(int)) != hipSuccess)
+    return ASR_ERR_HIP;
+  if (clear) {
+    const int zero = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(asr::g_xg_mode), &zero, sizeof(int)) != hipSuccess)
+      return ASR_ERR_HIP;
+  }
+  return ASR_OK;
+}

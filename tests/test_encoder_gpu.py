@@ -163,12 +163,22 @@ def _persist_status():
     return st.value
 
 
-@pytest.mark.parametrize('B,T,H', [(20, 37, 64), (32, 120, 512), (7, 15, 320)])
+_RECURRENCE_MODES = {
+    'xg': {},                                   # tagged-granule persistent (lstm_xg.hip)
+    'xg_sc1': {'ASR_XG_LOCAL': '0'},            # ... forced write-through hand-off
+    'counter': {'ASR_LSTM_XG': '0'},            # counter-form persistent (lstm_persist.hip)
+    'step': {'ASR_LSTM_PERSIST': '0'},          # one launch per time step (lstm.hip)
+}
+
+
+@pytest.mark.parametrize('B,T,H', [(20, 37, 64), (32, 120, 512), (7, 15, 320), (48, 50, 256),
+                                   (64, 40, 512)])
 def test_persistent_recurrence_matches_step_kernels(B, T, H, cuda_dev, monkeypatch):
-    """bf16 mode: the persistent one-launch-per-pass recurrence (lstm_persist.hip)
-    against the per-step kernels on the same inputs: outputs, input grads and
-    every weight grad.  Ragged lengths, B not a multiple of 16 (padded row
-    group), H = 320 (odd k-step count per wave)."""
+    """bf16 mode: both persistent one-launch-per-pass recurrences (tagged-granule
+    lstm_xg.hip and counter-form lstm_persist.hip) against the per-step kernels
+    on the same inputs: outputs, input grads and every weight grad.  Ragged
+    lengths, B not a multiple of the row group (padded rows), H = 320 (odd
+    k-step count per wave), B = 64 (16-row groups)."""
     ops = _ops()
     ops.set_compute_dtype('bf16')
     rng = np.random.RandomState(B * 1000 + H)
@@ -181,8 +191,11 @@ def test_persistent_recurrence_matches_step_kernels(B, T, H, cuda_dev, monkeypat
     R = torch.from_numpy(rng.randn(B, T, 2 * H).astype(np.float32)).to(cuda_dev)
     res = {}
     _persist_status()
-    for mode in ('1', '0'):
-        monkeypatch.setenv('ASR_LSTM_PERSIST', mode)
+    for mode, env in _RECURRENCE_MODES.items():
+        for k in ('ASR_LSTM_XG', 'ASR_LSTM_PERSIST', 'ASR_XG_LOCAL'):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
         xd = x.to(cuda_dev).requires_grad_(True)
         wd = [w.to(cuda_dev).requires_grad_(True) for w in ws]
         lens_d = torch.from_numpy(lens).to(cuda_dev)
@@ -191,14 +204,70 @@ def test_persistent_recurrence_matches_step_kernels(B, T, H, cuda_dev, monkeypat
         torch.cuda.synchronize()
         res[mode] = [y.detach().cpu().numpy(), xd.grad.cpu().numpy()] + \
             [w.grad.cpu().numpy() for w in wd]
-    assert _persist_status() == 0
+        assert _persist_status() == 0, mode
+    # forward output of every mode against the fp32 torch-CPU oracle
+    H4 = 4 * H
+    ref_y = torch.cat([asr_ref.lstm_direction(x, lens, ws[0][:H4], ws[1][:H4], ws[2][:H4],
+                                              ws[3][:H4], False),
+                       asr_ref.lstm_direction(x, lens, ws[0][H4:], ws[1][H4:], ws[2][H4:],
+                                              ws[3][H4:], True)], dim=2).numpy()
+    for mode in res:
+        err = np.abs(res[mode][0] - ref_y).max() / (np.abs(ref_y).max() + 1e-6)
+        assert err < 2e-2, (mode, 'y vs oracle', err)
     names = ['y', 'dx', 'dW_ih', 'dW_hh', 'db_ih', 'db_hh']
-    for n, a, b in zip(names, res['1'], res['0']):
-        scale = np.abs(b).max() + 1e-6
-        assert np.abs(a - b).max() / scale < 2e-2, (n, np.abs(a - b).max(), scale)
-    # padded frames are exactly zero in both
-    for b in range(B):
-        assert not res['1'][0][b, lens[b]:].any()
+    for mode in ('xg', 'xg_sc1', 'counter'):
+        for n, a, b in zip(names, res[mode], res['step']):
+            scale = np.abs(b).max() + 1e-6
+            assert np.abs(a - b).max() / scale < 2e-2, (mode, n, np.abs(a - b).max(), scale)
+        # padded frames are exactly zero
+        for b in range(B):
+            assert not res[mode][0][b, lens[b]:].any()
+    ops.set_compute_dtype('fp32')
+
+
+def _xg_mode():
+    import ctypes
+    from pytorch_end2end_speech_recognition_amd import _native as N
+    m = ctypes.c_int(0)
+    N.call('asr_lstm_xg_mode', ctypes.byref(m), 1)
+    return m.value
+
+
+@pytest.mark.parametrize('B,H', [(32, 512), (64, 512), (28, 256)])
+def test_xg_local_and_write_through_agree_bitwise(B, H, cuda_dev, monkeypatch):
+    """The tagged-granule recurrence picks its hand-off protocol from the
+    placement it measures (XCD-local when every XCD holds whole groups, else
+    write-through).  Both run the same arithmetic on the same data, so the
+    outputs and all gradients must be bit-identical; and at the bench shape
+    the XCD-local protocol must actually be the one that ran."""
+    ops = _ops()
+    ops.set_compute_dtype('bf16')
+    rng = np.random.RandomState(B + H)
+    T, Din = 64, 40
+    lens = np.sort(rng.randint(T // 2, T + 1, B))[::-1].astype(np.int32)
+    lens[0] = T
+    x = torch.from_numpy(rng.randn(B, T, Din).astype(np.float32))
+    ws = [torch.from_numpy(rng.uniform(-0.1, 0.1, s).astype(np.float32))
+          for s in ((8 * H, Din), (8 * H, H), (8 * H,), (8 * H,))]
+    R = torch.from_numpy(rng.randn(B, T, 2 * H).astype(np.float32)).to(cuda_dev)
+    out, modes = {}, {}
+    for name, local in (('local', '1'), ('sc1', '0')):
+        monkeypatch.setenv('ASR_XG_LOCAL', local)
+        _xg_mode()
+        xd = x.to(cuda_dev).requires_grad_(True)
+        wd = [w.to(cuda_dev).requires_grad_(True) for w in ws]
+        y = ops.blstm_layer(xd, torch.from_numpy(lens).to(cuda_dev), T, *wd)
+        (y * R).sum().backward()
+        torch.cuda.synchronize()
+        modes[name] = _xg_mode()
+        out[name] = [y.detach().cpu().numpy(), xd.grad.cpu().numpy()] + \
+            [w.grad.cpu().numpy() for w in wd]
+    assert _persist_status() == 0
+    assert modes['sc1'] == 1, modes
+    if B == 32:
+        assert modes['local'] == 2, modes     # one group per XCD at the bench shape
+    for a, b in zip(out['local'], out['sc1']):
+        np.testing.assert_array_equal(a, b)
     ops.set_compute_dtype('fp32')
 
 

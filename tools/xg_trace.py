@@ -1,0 +1,60 @@
+"""Per-step phase timing of the tagged-granule recurrence (ASR_XG_TRACE=1):
+one forward + backward layer pass at the bench shape, then the median
+duration of each phase over steps 8..127 of work-groups 0..3."""
+import ctypes
+import os
+import sys
+
+os.environ['ASR_XG_TRACE'] = '1'
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from pytorch_end2end_speech_recognition_amd import _native as N  # noqa: E402
+from pytorch_end2end_speech_recognition_amd import native_ops as ops  # noqa: E402
+
+WG, STEPS, K = 4, 128, 6
+
+
+def read():
+    buf = (ctypes.c_ulonglong * (WG * STEPS * K))()
+    N.query('asr_xg_trace_read', ctypes.cast(buf, ctypes.c_void_p))
+    return np.frombuffer(buf, dtype=np.uint64).reshape(WG, STEPS, K).astype(np.int64)
+
+
+def report(name, tr, names):
+    print(name)
+    for w in range(WG):
+        d = tr[w, 8:]
+        step = np.diff(d[:, 0])
+        parts = ['step %.2f us' % (np.median(step) / 100.0)]
+        for a, b, nm in names:
+            parts.append('%s %.2f' % (nm, np.median(d[:, b] - d[:, a]) / 100.0))
+        parts.append('spins %.0f' % np.median(d[:, 5]))
+        print('  wg%d ' % w + '  '.join(parts))
+
+
+def main():
+    B, T, H, Din = 32, 1000, 512, 1024
+    ops.set_compute_dtype('bf16')
+    dev = torch.device('cuda:0')
+    rng = np.random.RandomState(0)
+    x = torch.from_numpy(rng.randn(B, T, Din).astype(np.float32)).to(dev).requires_grad_(True)
+    ws = [torch.from_numpy(rng.uniform(-0.1, 0.1, s).astype(np.float32)).to(dev).requires_grad_(True)
+          for s in ((8 * H, Din), (8 * H, H), (8 * H,), (8 * H,))]
+    lens = torch.full((B,), T, dtype=torch.int32, device=dev)
+    for _ in range(2):
+        y = ops.blstm_layer(x, lens, T, *ws)
+        torch.cuda.synchronize()
+        fwd = read()
+        y.backward(torch.randn_like(y))
+        torch.cuda.synchronize()
+        bwd = read()
+    report('forward (us): sweep = start->sweep ok, comb = sweep->barrier, cell = barrier->publish',
+           fwd, [(0, 1, 'sweep'), (1, 2, 'comb'), (2, 3, 'cell')])
+    report('backward (us)', bwd, [(0, 1, 'sweep'), (1, 2, 'b1'), (2, 3, 'cell+b2'),
+                                  (3, 4, 'mfma+pub')])
+
+
+if __name__ == '__main__':
+    main()
