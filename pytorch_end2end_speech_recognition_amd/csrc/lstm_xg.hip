@@ -48,9 +48,9 @@ __device__ int g_xg_mode;    // bit 0: a launch ran write-through (sc1); bit 1: 
 // Diagnostics only (ASR_XG_TRACE=1): per-step phase timestamps (100 MHz
 // s_memrealtime) of work-groups 0..XG_TR_WG-1, steps 0..XG_TR_STEPS-1.
 __device__ unsigned long long* g_xg_trace;
-#define XG_TR_WG 4
+#define XG_TR_WG 64
 #define XG_TR_STEPS 128
-#define XG_TR_K 6
+#define XG_TR_K 8
 #define XG_TR(step, k, val)                                                              \
   do {                                                                                  \
     if (tr && (step) < XG_TR_STEPS && lane == 0 && wave == 0)                          \
@@ -254,6 +254,7 @@ __global__ void __launch_bounds__(256 + R * XU) lstm_fwd_xg(
         u32x4 v[KSW][2];
         nap(ndelay);
         for (unsigned spins = 0;; ++spins) {
+          const unsigned long long t_iss = tr ? __builtin_amdgcn_s_memrealtime() : 0;
           int ok = 1;  // bitwise ANDs: every load is issued before the first wait
           if (sweeper) {
             // k-steps past nks re-read the last one (no branch between the loads)
@@ -270,6 +271,8 @@ __global__ void __launch_bounds__(256 + R * XU) lstm_fwd_xg(
           if (__all(ok)) {
             XG_TR(s, 1, __builtin_amdgcn_s_memrealtime());
             XG_TR(s, 5, spins);
+            XG_TR(s, 6, t_iss);
+            XG_TR(s, 7, (unsigned long long)(grp * 256 + mem));
             break;
           }
           if (!keep_spinning(spins, abortw, nsleep)) {
@@ -296,9 +299,13 @@ __global__ void __launch_bounds__(256 + R * XU) lstm_fwd_xg(
 #pragma unroll
           for (int r = 0; r < 4; ++r) part[s & 1][wave][4 * kq + r][g * XU + ln] = acc[g][r];
       }
-      __syncthreads();
+      __syncthreads();  // B(s): partial sums in LDS
       XG_TR(s, 2, __builtin_amdgcn_s_memrealtime());
       if (s_dead) return;
+      // Bp(s): this block's cell waves have issued their h_s granules.  Polling
+      // for h_s before that cannot succeed, and would only queue this CU's
+      // vector-memory pipe ahead of those stores.
+      __syncthreads();
     }
     return;
   }
@@ -319,6 +326,7 @@ __global__ void __launch_bounds__(256 + R * XU) lstm_fwd_xg(
 #pragma unroll
     for (int q = 0; q < 4; ++q) gxv[q] = gx_act[((long long)b * T + t0) * H8 + gcol + (long long)q * H];
   }
+  __builtin_amdgcn_s_setprio(2);  // the cell update + publish is the critical path
   const int cw = wave - 4;  // trace as this block's first cell wave
   for (int s = 0; s < T; ++s) {
     const int t = dir ? T - 1 - s : s;
@@ -355,6 +363,7 @@ __global__ void __launch_bounds__(256 + R * XU) lstm_fwd_xg(
     }
     if (cw == 0 && lane == 0 && tr && s < XG_TR_STEPS)
       tr[((long long)blockIdx.x * XG_TR_STEPS + s) * XG_TR_K + 3] = __builtin_amdgcn_s_memrealtime();
+    __syncthreads();  // Bp(s)
     if (own) {
       const long long sidx = ((long long)b * T + t) * 2 * H + (long long)dir * H + j;
       y[sidx] = h;
@@ -438,6 +447,7 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
         float s0 = 0.f, s1 = 0.f;
         nap(ndelay);
         for (unsigned spins = 0;; ++spins) {
+          const unsigned long long t_iss = tr ? __builtin_amdgcn_s_memrealtime() : 0;
           int ok = 1;
           s0 = 0.f;
           s1 = 0.f;
@@ -454,6 +464,8 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
           if (__all(ok)) {
             XG_TR(q, 1, __builtin_amdgcn_s_memrealtime());
             XG_TR(q, 5, spins);
+            XG_TR(q, 6, t_iss);
+            XG_TR(q, 7, (unsigned long long)(grp * 256 + mem));
             break;
           }
           if (!keep_spinning(spins, abortw, nsleep)) {
@@ -469,12 +481,14 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
       if (s_dead) return;
       __syncthreads();  // B2
       XG_TR(q, 3, __builtin_amdgcn_s_memrealtime());
+      __syncthreads();  // B3: this block's MFMA waves have issued their partials
     }
     return;
   }
 
   if (wave < 4 + NCW) {
     // -------------------------------- cell --------------------------------
+    __builtin_amdgcn_s_setprio(2);
     const int ct = tid - 256;
     const int row = ct >> 4, unit = ct & 15;
     const int b = b0 + row, j = u0 + unit;
@@ -537,11 +551,13 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
         }
         if (q + 1 < T) load_cell(q + 1, av, cc, cp, dyv);
       }
+      __syncthreads();  // B3
     }
     return;
   }
 
   // --------------------------------- MFMA -----------------------------------
+  __builtin_amdgcn_s_setprio(2);
   const int mw = wave - 4 - NCW;         // 0..3
   const int kq = lane >> 4, ln = lane & 15;
   bf16x8 wa[MB][2];
@@ -595,6 +611,7 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
     }
     if (mw == 0 && lane == 0 && tr && q < XG_TR_STEPS)
       tr[((long long)blockIdx.x * XG_TR_STEPS + q) * XG_TR_K + 4] = __builtin_amdgcn_s_memrealtime();
+    __syncthreads();  // B3
   }
 }
 

@@ -13,7 +13,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from pytorch_end2end_speech_recognition_amd import _native as N  # noqa: E402
 from pytorch_end2end_speech_recognition_amd import native_ops as ops  # noqa: E402
 
-WG, STEPS, K = 4, 128, 6
+WG, STEPS, K = 64, 128, 8
 
 
 def read():
@@ -22,9 +22,31 @@ def read():
     return np.frombuffer(buf, dtype=np.uint64).reshape(WG, STEPS, K).astype(np.int64)
 
 
+def hop(name, tr, pub_k):
+    """Per group (k=7 ids) and step: last producer publish (k=pub_k) -> each
+    consumer's issue of its successful poll (k=6) and its success (k=1)."""
+    ids = tr[:, 20, 7]
+    grp = ids // 256
+    lat_iss, lat_ok, late = [], [], []
+    for g in np.unique(grp):
+        mem = np.where(grp == g)[0]
+        if len(mem) < 2:
+            continue
+        for s in range(8, STEPS - 1):
+            last_pub = tr[mem, s, pub_k].max()
+            for m in mem:
+                lat_ok.append(tr[m, s + 1, 1] - last_pub)
+                lat_iss.append(tr[m, s + 1, 6] - last_pub)
+    lat_ok, lat_iss = np.array(lat_ok) / 100.0, np.array(lat_iss) / 100.0
+    print('%s: last publish -> poll success median %.2f us (p10 %.2f, p90 %.2f); '
+          '-> issue of the successful poll median %.2f us' % (
+              name, np.median(lat_ok), np.percentile(lat_ok, 10), np.percentile(lat_ok, 90),
+              np.median(lat_iss)))
+
+
 def report(name, tr, names):
     print(name)
-    for w in range(WG):
+    for w in range(4):
         d = tr[w, 8:]
         step = np.diff(d[:, 0])
         parts = ['step %.2f us' % (np.median(step) / 100.0)]
@@ -50,6 +72,8 @@ def main():
         y.backward(torch.randn_like(y))
         torch.cuda.synchronize()
         bwd = read()
+    hop('forward', fwd, 3)
+    hop('backward', bwd, 4)
     report('forward (us): sweep = start->sweep ok, comb = sweep->barrier, cell = barrier->publish',
            fwd, [(0, 1, 'sweep'), (1, 2, 'comb'), (2, 3, 'cell')])
     report('backward (us)', bwd, [(0, 1, 'sweep'), (1, 2, 'b1'), (2, 3, 'cell+b2'),
