@@ -119,12 +119,15 @@ def roofline_report(args, p, mean_us, launches, mean_work):
 
     out = {'bound': dom['bound']}
     out.update(view(dom))
-    out.update({'traffic': None, 'kernel': dom['name'], 'mean_launch_us': round(dom['us'], 3),
+    traffic, tsrc = pmc_traffic(dom['name'])
+    out.update({'traffic': traffic, 'kernel': dom['name'], 'mean_launch_us': round(dom['us'], 3),
                 'launches_timed': dom['n'],
                 'algorithmic_bytes_per_launch': int(dom['bytes']),
                 'algorithmic_flops_per_launch': float(dom['flops']),
                 'share_of_timed_kernel_time': round(dom['total'] / sum(r['total'] for r in rows),
                                                     3)})
+    if tsrc:
+        out['traffic_source'] = tsrc
     others = {}
     for r in rows:
         if r is dom:
@@ -138,6 +141,24 @@ def roofline_report(args, p, mean_us, launches, mean_work):
         others[r['name']] = v
     out['other_kernels'] = others
     return out
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/rNN_pmc_traffic.json, written by tools/pmc_traffic.py from
+    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench's
+    own command; counters cannot be read inside the timed run).  (None, None)
+    when no summary covers the kernel."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r*_pmc_traffic.json')))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if kernel in d:
+            return d[kernel]['traffic_bytes_per_launch'], os.path.relpath(f, ROOT)
+    return None, None
 
 
 def cpu_baseline(cfg, batch, n_utts):
