@@ -185,6 +185,15 @@ int asr_lstm_backward(const float* dy, const void* whh_f, const void* whh_r, int
                       const int32_t* lens, int B, int T, int H, int compute_dtype, float* act_dg,
                       const float* cst, uint16_t* dgbf, void* workspace, size_t ws_bytes,
                       void* stream);
+/* asr_lstm_backward plus the bias gradients of nn.LSTM's bias_ih / bias_hh
+ * (both [2 dirs x 4H], accumulated +=, identical values: both biases feed the
+ * same gate pre-activation, rnn.py:166-172).  The tagged-granule recurrence
+ * sums them inside the pass; other paths reduce dG afterwards.  workspace:
+ * asr_lstm_workspace_bytes(B, H, compute_dtype, 2). */
+int asr_lstm_backward_db(const float* dy, const void* whh_f, const void* whh_r, int w_dtype,
+                         const int32_t* lens, int B, int T, int H, int compute_dtype,
+                         float* act_dg, const float* cst, uint16_t* dgbf, float* db_ih,
+                         float* db_hh, void* workspace, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------ optimizer
  * Replaces torch.nn.utils.clip_grad_norm(params, max_norm)

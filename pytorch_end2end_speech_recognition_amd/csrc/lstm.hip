@@ -45,9 +45,21 @@ int lstm_fwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* wh
                        uint16_t* ybf, hipStream_t s, bool dry);
 int lstm_bwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* whh_f,
                        const float* whh_r, const float* dy, float* act_dg, const float* cst,
-                       void* ws, uint16_t* dgbf, hipStream_t s, bool dry);
+                       void* ws, uint16_t* dgbf, float* dbpart, hipStream_t s, bool dry);
 
 namespace {
+
+// db_ih[n] += sum_b part[b][n]; db_hh[n] += the same (fixed order over b).
+__global__ void bias_from_partials(const float* __restrict__ part, int B, int N,
+                                   float* __restrict__ db_ih, float* __restrict__ db_hh) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.f;
+  for (int b = 0; b < B; ++b) s += part[(long long)b * N + n];
+  db_ih[n] += s;
+  if (db_hh) db_hh[n] += s;
+}
+
 
 constexpr int FU = 4;   // forward: units per work-group (16 gate columns)
 constexpr int BU = 16;   // backward: units per work-group
@@ -496,13 +508,26 @@ size_t bwd_ws(int B, int H, int cdt) {
   const size_t xg = cdt == ASR_DT_BF16 ? lstm_xg_bwd_bytes(B, H) : 0;
   return std::max(bwd_layout(B, H, cdt).total, xg);
 }
+// Bias-gradient scratch behind the backward workspace: [max(B, 64)][8H] f32
+// (per-utterance partials of the fused path, or the colsum chunks otherwise).
+size_t bias_ws_off(int B, int H, int cdt) { return al256(bwd_ws(B, H, cdt)); }
+size_t bwd_ws_bias(int B, int H, int cdt) {
+  return bias_ws_off(B, H, cdt) + (size_t)std::max(B, 64) * 8 * H * sizeof(float);
+}
 
 }  // namespace
 }  // namespace asr
 
 using namespace asr;
 
+extern "C" size_t asr_colsum_workspace_bytes(int M, int N);
+extern "C" int asr_colsum_accumulate(const float* g, long long ld, int M, int N, float alpha,
+                                     float* out0, float* out1, void* workspace, size_t ws_bytes,
+                                     void* stream);
+
+// backward: 0 forward, 1 backward, 2 backward with bias gradients (asr_lstm_backward_db)
 extern "C" size_t asr_lstm_workspace_bytes(int B, int H, int compute_dtype, int backward) {
+  if (backward == 2) return bwd_ws_bias(B, H, compute_dtype);
   return backward ? bwd_ws(B, H, compute_dtype) : fwd_ws(B, H, compute_dtype);
 }
 
@@ -595,11 +620,12 @@ extern "C" int asr_lstm_forward(float* gx_act, const void* whh_f, const void* wh
   return ASR_OK;
 }
 
-extern "C" int asr_lstm_backward(const float* dy, const void* whh_f, const void* whh_r,
-                                 int w_dtype, const int32_t* lens, int B, int T, int H,
-                                 int compute_dtype, float* act_dg, const float* cst,
-                                 uint16_t* dgbf, void* workspace, size_t ws_bytes,
-                                 void* stream) {
+static int lstm_backward_impl(const float* dy, const void* whh_f, const void* whh_r,
+                              int w_dtype, const int32_t* lens, int B, int T, int H,
+                              int compute_dtype, float* act_dg, const float* cst,
+                              uint16_t* dgbf, float* dbpart, void* workspace, size_t ws_bytes,
+                              void* stream, bool* fused_bias) {
+  *fused_bias = false;
   ASR_REQUIRE(whh_f && whh_r && lens && act_dg && cst && workspace, ASR_ERR_ARG,
               "lstm_backward: null pointer");
   ASR_REQUIRE(B > 0 && T > 0 && H > 0, ASR_ERR_ARG, "lstm_backward: bad shape");
@@ -609,12 +635,13 @@ extern "C" int asr_lstm_backward(const float* dy, const void* whh_f, const void*
   const bool bf = compute_dtype == ASR_DT_BF16;
   if (bf && w_dtype == ASR_DT_F32 &&
       lstm_bwd_xg_launch(B, T, H, lens, (const float*)whh_f, (const float*)whh_r, dy, act_dg, cst,
-                         workspace, dgbf, s, true) == 1) {
+                         workspace, dgbf, dbpart, s, true) == 1) {
     const int slot = prof_begin_launch(ASR_PROF_LSTM_BWD_SEQ, s);
     const int rc = lstm_bwd_xg_launch(B, T, H, lens, (const float*)whh_f, (const float*)whh_r, dy,
-                                      act_dg, cst, workspace, dgbf, s, false);
+                                      act_dg, cst, workspace, dgbf, dbpart, s, false);
     ASR_REQUIRE(rc == 1, ASR_ERR_HIP, "lstm_backward: tagged-granule launch failed");
     prof_end_launch(ASR_PROF_LSTM_BWD_SEQ, slot, s);
+    *fused_bias = dbpart != nullptr;
     return ASR_OK;
   }
   const BwdLayout L = bwd_layout(B, H, compute_dtype);
@@ -687,4 +714,45 @@ extern "C" int asr_lstm_backward(const float* dy, const void* whh_f, const void*
     ASR_LAUNCH_CHECK();
   }
   return ASR_OK;
+}
+
+extern "C" int asr_lstm_backward(const float* dy, const void* whh_f, const void* whh_r,
+                                 int w_dtype, const int32_t* lens, int B, int T, int H,
+                                 int compute_dtype, float* act_dg, const float* cst,
+                                 uint16_t* dgbf, void* workspace, size_t ws_bytes,
+                                 void* stream) {
+  bool fused = false;
+  return lstm_backward_impl(dy, whh_f, whh_r, w_dtype, lens, B, T, H, compute_dtype, act_dg, cst,
+                            dgbf, nullptr, workspace, ws_bytes, stream, &fused);
+}
+
+// asr_lstm_backward plus the bias gradients: db_ih[n] += sum_{b,t} dG[b][t][n] and
+// db_hh[n] += the same (both biases feed the same gate pre-activation).  The
+// tagged-granule path sums them inside the recurrence (no pass over dG);
+// other paths reduce the written dG.
+extern "C" int asr_lstm_backward_db(const float* dy, const void* whh_f, const void* whh_r,
+                                    int w_dtype, const int32_t* lens, int B, int T, int H,
+                                    int compute_dtype, float* act_dg, const float* cst,
+                                    uint16_t* dgbf, float* db_ih, float* db_hh, void* workspace,
+                                    size_t ws_bytes, void* stream) {
+  ASR_REQUIRE(db_ih, ASR_ERR_ARG, "lstm_backward_db: null bias gradient");
+  ASR_REQUIRE(B > 0 && T > 0 && H > 0, ASR_ERR_ARG, "lstm_backward_db: bad shape");
+  ASR_REQUIRE(ws_bytes >= bwd_ws_bias(B, H, compute_dtype), ASR_ERR_WORKSPACE,
+              "lstm_backward_db: workspace too small");
+  float* part = (float*)((char*)workspace + bias_ws_off(B, H, compute_dtype));
+  bool fused = false;
+  const int rc = lstm_backward_impl(dy, whh_f, whh_r, w_dtype, lens, B, T, H, compute_dtype,
+                                    act_dg, cst, dgbf, part, workspace, ws_bytes, stream, &fused);
+  if (rc != ASR_OK) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  const int N = 8 * H;
+  if (fused) {
+    hipLaunchKernelGGL(bias_from_partials, dim3(ceil_div(N, 256)), dim3(256), 0, s, part, B, N,
+                       db_ih, db_hh);
+    ASR_LAUNCH_CHECK();
+    return ASR_OK;
+  }
+  const int M = B * T;
+  return asr_colsum_accumulate(act_dg, N, M, N, 1.f, db_ih, db_hh, part,
+                               asr_colsum_workspace_bytes(M, N), stream);
 }

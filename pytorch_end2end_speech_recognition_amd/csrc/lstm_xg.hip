@@ -404,7 +404,7 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
     int B, int T, int H, const int32_t* __restrict__ lens, const float* __restrict__ whh_f,
     const float* __restrict__ whh_r, const float* __restrict__ dy, float* __restrict__ act_dg,
     const float* __restrict__ cst, unsigned long long* pg, int* hdr,
-    uint16_t* __restrict__ dgbf, unsigned epoch, int allow_local) {
+    uint16_t* __restrict__ dgbf, float* __restrict__ dbpart, unsigned epoch, int allow_local) {
   constexpr int NPG = 256 / (8 * R);   // producer subsets swept in parallel
   __shared__ float red[NPG][R][XU + 1];
   __shared__ __attribute__((aligned(16))) uint16_t dgt[16][4 * XU + 8];
@@ -507,6 +507,8 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
       dyv = dy ? dy[si] : 0.f;
     };
     float av[4] = {0.f, 0.f, 0.f, 0.f}, cc = 0.f, cp = 0.f, dyv = 0.f;
+    // bias gradient: sum over t of this (utterance, unit)'s four gate gradients
+    float sb_i = 0.f, sb_f = 0.f, sb_g = 0.f, sb_o = 0.f;
     if (own) load_cell(0, av, cc, cp, dyv);
     for (int q = 0; q < T; ++q) {
       const int t = dir == 0 ? T - 1 - q : q;
@@ -527,6 +529,10 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
         d_g = dcell * ig * (1.f - gg * gg);
         d_o = dh * tc * og * (1.f - og);
         dc = dcell * fg;
+        sb_i += d_i;
+        sb_f += d_f;
+        sb_g += d_g;
+        sb_o += d_o;
       } else {
         dc = 0.f;
       }
@@ -552,6 +558,13 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
         if (q + 1 < T) load_cell(q + 1, av, cc, cp, dyv);
       }
       __syncthreads();  // B3
+    }
+    if (own && dbpart) {  // per-utterance bias-gradient partials [B][8H]
+      float* o = dbpart + (long long)b * 8 * H + (long long)dir * H4 + j;
+      o[0] = sb_i;
+      o[H] = sb_f;
+      o[2 * H] = sb_g;
+      o[3 * H] = sb_o;
     }
     return;
   }
@@ -725,7 +738,7 @@ int lstm_fwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* wh
 
 int lstm_bwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* whh_f,
                        const float* whh_r, const float* dy, float* act_dg, const float* cst,
-                       void* ws, uint16_t* dgbf, hipStream_t s, bool dry) {
+                       void* ws, uint16_t* dgbf, float* dbpart, hipStream_t s, bool dry) {
   if (!xg_enabled()) return 0;
   const int R = xg_rows(B, H);
   if (!R) return 0;
@@ -743,7 +756,7 @@ int lstm_bwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* wh
     if (hipMemsetAsync(ws, 0, lstm_xg_bwd_bytes(B, H), s) != hipSuccess) return -1;             \
     xg_trace_setup(s);             \
     hipLaunchKernelGGL((lstm_bwd_xg<RR, M>), dim3(grid), dim3(512 + RR * XU), XG_PIN_BWD, s, B, T, H,      \
-                       lens, whh_f, whh_r, dy, act_dg, cst, g, hdr, dgbf, ep, al);                   \
+                       lens, whh_f, whh_r, dy, act_dg, cst, g, hdr, dgbf, dbpart, ep, al);                   \
   } while (0)
 #define ASR_XGB_M(RR)                  \
   do {                                 \

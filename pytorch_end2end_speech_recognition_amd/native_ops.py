@@ -400,18 +400,26 @@ class BLSTMLayerFn(torch.autograd.Function):
         H = w_hh.shape[1]
         dev = act.device
         dy = dy.contiguous()
-        nb = N.query('asr_lstm_workspace_bytes', B, H, cd, 1)
+        if gbufs is None:
+            gbufs = tuple(grad_buffer(p) for p in (w_ih, w_hh, b_ih, b_hh))
+        fused_db = os.environ.get('ASR_BIAS_FUSED', '1') != '0'
+        nb = N.query('asr_lstm_workspace_bytes', B, H, cd, 2 if fused_db else 1)
         ws = _ws(nb, dev)
         whh_r = w_hh.data_ptr() + 4 * H * H * 4
         dg_bf = (torch.empty(B, T, 8 * H, dtype=torch.bfloat16, device=dev) if cd == BF16
                  else None)
-        # the saved activations become the gate gradients dG in place
-        N.call('asr_lstm_backward', N.ptr(dy), N.ptr(w_hh), ctypes.c_void_p(whh_r), F32,
-               N.ptr(lens), B, T, H, cd, N.ptr(act), N.ptr(cst), N.ptr(dg_bf), N.ptr(ws), nb,
-               N.stream_handle(dev))
+        # the saved activations become the gate gradients dG in place; the bias
+        # gradients (sum of dG over b, t) are accumulated by the same call
+        if fused_db:
+            N.call('asr_lstm_backward_db', N.ptr(dy), N.ptr(w_hh), ctypes.c_void_p(whh_r), F32,
+                   N.ptr(lens), B, T, H, cd, N.ptr(act), N.ptr(cst), N.ptr(dg_bf),
+                   N.ptr(gbufs[2]), N.ptr(gbufs[3]), N.ptr(ws), nb, N.stream_handle(dev))
+        else:   # A/B: separate column-sum pass over dG
+            N.call('asr_lstm_backward', N.ptr(dy), N.ptr(w_hh), ctypes.c_void_p(whh_r), F32,
+                   N.ptr(lens), B, T, H, cd, N.ptr(act), N.ptr(cst), N.ptr(dg_bf), N.ptr(ws), nb,
+                   N.stream_handle(dev))
+            colsum_accumulate(act.view(B * T, 8 * H), gbufs[2], gbufs[3])
         dg_op = dg_bf if dg_bf is not None else act
-        if gbufs is None:
-            gbufs = tuple(grad_buffer(p) for p in (w_ih, w_hh, b_ih, b_hh))
         # X as the dW_ih operand: the bf16 copy is already gathered (identity map)
         if cd == BF16:
             x_map = rowmap(Din)
@@ -458,8 +466,9 @@ def convert_rows_bf16(src, rmap, nrows, ncols):
 
 
 def _blstm_wgrad(dg, dg_f32, x_op, x_map, y_op, T, gbufs, dev):
-    """dW_ih, dW_hh, db_ih, db_hh of one BLSTM layer from its gate gradients
-    (dg: bf16 copy in bf16 mode, else the f32 tensor; biases always from f32)."""
+    """dW_ih, dW_hh of one BLSTM layer from its gate gradients (dg: bf16 copy
+    in bf16 mode, else the f32 tensor).  db_ih / db_hh were accumulated by
+    asr_lstm_backward_db."""
     B = dg.shape[0]
     H = y_op.shape[2] // 2
     Din = x_op.shape[-1]
@@ -478,7 +487,6 @@ def _blstm_wgrad(dg, dg_f32, x_op, x_map, y_op, T, gbufs, dev):
                      operand(y_op, 1, hp_r, offset=H), g_hh, rowmap(H), 4 * H, H, BT, beta=1.0,
                      c_offset=4 * H * H),
     ], dev)
-    colsum_accumulate(dg_f32.view(BT, 8 * H), g_bih, g_bhh)
 
 
 _side_streams = {}

@@ -361,3 +361,54 @@ def test_gemm_bf16_operand_modes(fast, cuda_dev, monkeypatch):
     ref = np.einsum('bmk,bnk->bmn', bf(a).double().numpy(), bf(b).double().numpy())
     np.testing.assert_allclose(C.cpu().numpy(), ref, rtol=1e-4, atol=1e-3)
     ops.set_compute_dtype('fp32')
+
+
+@pytest.mark.parametrize('B,T,H', [(32, 64, 512), (20, 37, 64), (7, 15, 320)])
+def test_lstm_backward_db_is_column_sum_of_dg(B, T, H, cuda_dev, monkeypatch):
+    """asr_lstm_backward_db (bias gradients summed inside the tagged-granule
+    recurrence) against the column sums of the dG it wrote, in float64 on the
+    host; and its dG / dG-bf16 bit-identical to asr_lstm_backward's."""
+    import ctypes
+    from pytorch_end2end_speech_recognition_amd import _native as N
+    for k in ('ASR_LSTM_XG', 'ASR_LSTM_PERSIST', 'ASR_XG_LOCAL'):
+        monkeypatch.delenv(k, raising=False)
+    rng = np.random.RandomState(B + T + H)
+    lens = np.sort(rng.randint(1, T + 1, B))[::-1].astype(np.int32)
+    lens[0] = T
+    lens_d = torch.from_numpy(lens).to(cuda_dev)
+    gx = torch.from_numpy(rng.randn(B, T, 8 * H).astype(np.float32)).to(cuda_dev)
+    whh = torch.from_numpy(rng.uniform(-0.1, 0.1, (8 * H, H)).astype(np.float32)).to(cuda_dev)
+    dy = torch.from_numpy(rng.randn(B, T, 2 * H).astype(np.float32)).to(cuda_dev)
+    y = torch.empty(B, T, 2 * H, device=cuda_dev)
+    cst = torch.empty(B, T, 2 * H, device=cuda_dev)
+    ybf = torch.empty(B, T, 2 * H, dtype=torch.bfloat16, device=cuda_dev)
+    BF = N.ASR_DT_BF16
+    whh_r = ctypes.c_void_p(whh.data_ptr() + 4 * H * H * 4)
+    nb = N.query('asr_lstm_workspace_bytes', B, H, BF, 0)
+    ws = torch.empty(nb, dtype=torch.uint8, device=cuda_dev)
+    N.call('asr_lstm_forward', N.ptr(gx), N.ptr(whh), whh_r, N.ASR_DT_F32, N.ptr(lens_d), B, T, H,
+           BF, N.ptr(y), N.ptr(cst), N.ptr(ybf), N.ptr(ws), nb, N.stream_handle(cuda_dev))
+    outs = []
+    for kind in (1, 2):
+        act = gx.clone()
+        dgbf = torch.empty(B, T, 8 * H, dtype=torch.bfloat16, device=cuda_dev)
+        db = torch.full((2, 8 * H), 0.5, device=cuda_dev)     # accumulates (+=)
+        nb = N.query('asr_lstm_workspace_bytes', B, H, BF, kind)
+        ws = torch.empty(nb, dtype=torch.uint8, device=cuda_dev)
+        if kind == 1:
+            N.call('asr_lstm_backward', N.ptr(dy), N.ptr(whh), whh_r, N.ASR_DT_F32, N.ptr(lens_d),
+                   B, T, H, BF, N.ptr(act), N.ptr(cst), N.ptr(dgbf), N.ptr(ws), nb,
+                   N.stream_handle(cuda_dev))
+        else:
+            N.call('asr_lstm_backward_db', N.ptr(dy), N.ptr(whh), whh_r, N.ASR_DT_F32,
+                   N.ptr(lens_d), B, T, H, BF, N.ptr(act), N.ptr(cst), N.ptr(dgbf), N.ptr(db[0]),
+                   N.ptr(db[1]), N.ptr(ws), nb, N.stream_handle(cuda_dev))
+        torch.cuda.synchronize()
+        outs.append((act.cpu().numpy(), dgbf.cpu(), db.cpu().numpy()))
+    (a1, g1, _), (a2, g2, db2) = outs
+    np.testing.assert_array_equal(a1, a2)
+    assert torch.equal(g1, g2)
+    ref = a2.astype(np.float64).sum(axis=(0, 1)) + 0.5
+    scale = np.abs(ref).max()
+    for r in (0, 1):
+        assert np.abs(db2[r] - ref).max() / scale < 1e-5, r
