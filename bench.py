@@ -56,6 +56,34 @@ CONFIGS = {
 }
 
 
+def _attention_params(ctc_weight):
+    """configs[2] / configs[3]: the reference's LibriSpeech-100h location-attention
+    recipe (examples/librispeech/s5/conf/attention/char_blstm_att_100h.yml, kept
+    as the fixture tests/golden/char_blstm_att_100h.yml): 4x320 BLSTM with x4
+    drop subsampling, location attention (128, 10 ch x 201), LSTM decoder 320,
+    embedding 32, dropout 0.2 everywhere, scheduled sampling 0.2; hybrid adds
+    lambda * CTC."""
+    import yaml
+    with open(os.path.join(ROOT, 'tests', 'golden', 'char_blstm_att_100h.yml')) as f:
+        prm = yaml.safe_load(f)['param']
+    prm.update(num_classes=28, ctc_loss_weight=ctc_weight)
+    for k in ('learning_rate', 'weight_decay'):
+        prm[k] = float(prm[k])
+    return prm
+
+
+CONFIGS['att4x320'] = dict(workload='librispeech100h_char_location_attention_blstm4x320',
+                           model_type='attention', params=None, ctc_weight=0.0)
+CONFIGS['hybrid4x320'] = dict(workload='librispeech_char_hybrid_ctc0.3_attention_blstm4x320',
+                              model_type='attention', params=None, ctc_weight=0.3)
+
+
+def config_params(cfg):
+    if cfg['params'] is None:
+        cfg['params'] = _attention_params(cfg['ctc_weight'])
+    return cfg['params']
+
+
 def synthetic_batch(B, T, F, num_classes, seed):
     """SURVEY §8d synthetic inputs (numpy seed per rank)."""
     rng = np.random.RandomState(seed)
@@ -83,7 +111,14 @@ def roofline_report(args, p, mean_us, launches, mean_work):
         re-streamed every step;
       * gemm: 2*M*N*K summed over the launch's problems, reported by the library.
     """
-    B, H, T = args.batch, p['encoder_num_units'], args.frames
+    B, H = args.batch, p['encoder_num_units']
+    # time steps of a layer pass, averaged over the layers (pyramidal drop
+    # subsampling halves T after each flagged layer, rnn.py:413-439)
+    T_l, t = [], args.frames
+    for flag in (p.get('subsample_list') or [False] * p['encoder_num_layers']):
+        T_l.append(t)
+        t = t // 2 if flag else t
+    T = sum(T_l) / len(T_l)
     esz = 2 if args.precision == 'bf16' else 4
     cell = B * H                              # (utterance, unit) cells per direction
     w_hh = 2 * 4 * H * H * esz                # both directions
@@ -169,7 +204,7 @@ def cpu_baseline(cfg, batch, n_utts):
     cores = len(os.sched_getaffinity(0))
     threads = max(1, min(16, cores))
     torch.set_num_threads(threads)
-    p = cfg['params']
+    p = config_params(cfg)
     torch.manual_seed(0)
     model = load(cfg['model_type'], dict(p), 'pytorch')           # host-side init only
     sd = {k: v.detach().clone().requires_grad_(True) for k, v in model.state_dict().items()}
@@ -177,12 +212,16 @@ def cpu_baseline(cfg, batch, n_utts):
                            weight_decay=p['weight_decay'])
     sub = {k: v[:n_utts] for k, v in batch.items()}
     sub['ys'] = sub['ys'][:, :int(sub['y_lens'].max())]
-    ocfg = dict(num_layers=p['encoder_num_layers'], subsample_list=p['subsample_list'],
-                fc_list=p['fc_list'])
     t0 = time.perf_counter()
     opt.zero_grad()
-    loss, _, _, _ = asr_ref.ctc_model_loss(sd, ocfg, sub['xs'], sub['ys'], sub['x_lens'],
-                                           sub['y_lens'])
+    if cfg['model_type'] == 'attention':   # oracle decoder: teacher forcing, no dropout
+        loss = asr_ref.attention_model_loss(sd, p, sub['xs'], sub['ys'], sub['x_lens'],
+                                            sub['y_lens'])
+    else:
+        ocfg = dict(num_layers=p['encoder_num_layers'], subsample_list=p['subsample_list'],
+                    fc_list=p['fc_list'])
+        loss, _, _, _ = asr_ref.ctc_model_loss(sd, ocfg, sub['xs'], sub['ys'], sub['x_lens'],
+                                               sub['y_lens'])
     loss.backward()
     torch.nn.utils.clip_grad_norm_(list(sd.values()), p['clip_grad_norm'])
     opt.step()
@@ -190,8 +229,10 @@ def cpu_baseline(cfg, batch, n_utts):
     frames = float(np.sum(sub['x_lens']))
     return {'value': frames / dt, 'unit': 'frames/s', 'cores': threads, 'kind': 'port',
             'sample': '%d utterances x %d max frames (%d frames), 1 full training step (fwd + '
-                      'bwd + clip + Adam) of the fp32 torch-CPU oracle, %.1f s'
-                      % (n_utts, int(sub['x_lens'].max()), int(frames), dt)}
+                      'bwd + clip + Adam) of the fp32 torch-CPU oracle%s, %.1f s'
+                      % (n_utts, int(sub['x_lens'].max()), int(frames),
+                         ' (decoder without dropout / scheduled sampling)'
+                         if cfg['model_type'] == 'attention' else '', dt)}
 
 
 def main():
@@ -217,7 +258,7 @@ def main():
         dist.init_process_group('nccl', device_id=dev)
 
     cfg = CONFIGS[args.config]
-    p = dict(cfg['params'])
+    p = dict(config_params(cfg))
     torch.manual_seed(1623)
     native_ops.manual_seed(1623 + rank)
     model = load(cfg['model_type'], p, 'pytorch')

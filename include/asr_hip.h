@@ -234,6 +234,9 @@ int asr_embedding_backward(const long long* idx, const float* dout, int n, int V
                            int trans, int padding_idx, float* grad_weight, void* stream);
 int asr_tanh_forward(const float* x, float* y, long long n, void* stream);
 int asr_tanh_backward(const float* y, const float* dy, float* dx, long long n, void* stream);
+/* y = tanh(a + b) (attention bottleneck with per-branch dropout,
+ * attention_seq2seq.py:788-790); its backward is asr_tanh_backward for both. */
+int asr_add_tanh_forward(const float* a, const float* b, float* y, long long n, void* stream);
 
 /* dst[r][0:ncols] = bf16(src[row(r) + 0:ncols]) (round to nearest even) for r <
  * nrows, rows through an asr_rowmap_t (perm / subsample gathers; rows outside
@@ -303,6 +306,55 @@ typedef struct {
   int sigmoid_smoothing;
 } asr_attdec_dims_t;
 
+/* Training-mode options of the decoder loop (NULL = none of them).
+ * dropout_hidden: RNNDecoder dropout on h after the LSTMCell
+ *   (rnn_decoder.py:97-98); the dropped h is both dec_out and the recurrent
+ *   state.  Mask of element (b, t, j): asr dropout RNG, seed_hidden, index
+ *   (b*S + t)*D + j (regenerated in backward).
+ * Scheduled sampling (attention_seq2seq.py:744-748): ss_steps_host[t] != 0
+ *   (host memory, [S], t >= 1) feeds step t with embed(argmax logits_{t-1})
+ *   instead of the teacher token, where logits_{t-1} = fc(tanh(drop_d(W_d
+ *   dec_{t-1} + b_d) + drop_c(W_c ctx_{t-1} + b_c))) -- the same logits the loss
+ *   sees when the caller applies its post-loop dropouts with seed_d / seed_c
+ *   over [B][S][Dz] (index (b*S + t)*Dz + k).  The sampled embedding (row of
+ *   emb_w [V][Y], or column of emb_w [Y][V] when emb_trans) is dropped with
+ *   drop_emb / seed_emb (index (b*S + t)*Y + y), written to emb_ss [B][S][Y]
+ *   (caller zeroes it; teacher steps stay 0) and projected:
+ *   pre_ss[b,t] = W_ih[:, :Y] e + b_ih + b_hh (w_ih_emb row stride ld_ih).
+ *   tok_ss [B][S] (nullable) receives the sampled tokens.  In backward,
+ *   d_pre [B][S][4D] = dG with sampled steps zeroed (the gradient of pre_emb)
+ *   and dg_ss [B][S][4D] = dG at sampled steps only (for W_ih[:, :Y] and the
+ *   biases through emb_ss); both NULL when no step is sampled. */
+typedef struct {
+  float dropout_hidden;
+  unsigned long long seed_hidden;
+  const int32_t* ss_steps_host;
+  int Y, Dz, V;
+  const float* w_d;
+  const float* b_d;
+  float drop_d;
+  unsigned long long seed_d;
+  const float* w_c;
+  const float* b_c;
+  float drop_c;
+  unsigned long long seed_c;
+  const float* w_fc;
+  const float* b_fc;
+  const float* emb_w;
+  int emb_trans;
+  float drop_emb;
+  unsigned long long seed_emb;
+  const float* w_ih_emb;
+  long long ld_ih;
+  const float* b_ih;
+  const float* b_hh;
+  float* pre_ss;
+  float* emb_ss;
+  long long* tok_ss;
+  float* d_pre;
+  float* dg_ss;
+} asr_attdec_opts_t;
+
 size_t asr_attdec_workspace_bytes(const asr_attdec_dims_t* dims, int compute_dtype,
                                   int backward);
 int asr_attdec_forward(const asr_attdec_dims_t* dims, int compute_dtype, const float* enc,
@@ -321,6 +373,24 @@ int asr_attdec_backward(const asr_attdec_dims_t* dims, int compute_dtype, const 
                         float* dctx_tot, float* d_enc_a, float* d_h0, float* dwd_all,
                         float* dv_part, float* dwc_part, float* dcw_part, void* workspace,
                         size_t ws_bytes, void* stream);
+/* The same two calls with training-mode options (asr_attdec_opts_t above). */
+int asr_attdec_forward_ex(const asr_attdec_dims_t* dims, const asr_attdec_opts_t* opts,
+                          int compute_dtype, const float* enc, const float* enc_a,
+                          const int32_t* lens, const float* w_ih_ctx, long long ld_ih,
+                          const float* w_hh, const float* w_dec, const float* w_conv,
+                          const float* conv_w, const float* v, const float* pre_emb,
+                          const float* h0, float* dec, float* c, float* gates, float* x,
+                          float* ctx, float* aw, void* workspace, size_t ws_bytes, void* stream);
+int asr_attdec_backward_ex(const asr_attdec_dims_t* dims, const asr_attdec_opts_t* opts,
+                           int compute_dtype, const float* enc, const float* enc_a,
+                           const int32_t* lens, const float* w_ih_ctx, long long ld_ih,
+                           const float* w_hh, const float* w_dec, const float* w_conv,
+                           const float* conv_w, const float* v, const float* dec,
+                           const float* c, const float* aw, const float* d_dec_in,
+                           const float* d_ctx_in, float* gates_dg, float* dctx_tot,
+                           float* d_enc_a, float* d_h0, float* dwd_all, float* dv_part,
+                           float* dwc_part, float* dcw_part, void* workspace, size_t ws_bytes,
+                           void* stream);
 
 /* ----------------------------------------------------------- profiling
  * Sampled HIP-event timing of the recurrence step kernels on their own stream

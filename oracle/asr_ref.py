@@ -162,10 +162,19 @@ def lstm_cell(p, name, x, h, c):
     return torch.sigmoid(o) * torch.tanh(c), c
 
 
-def attention_model_loss(p, cfg, xs, ys, x_lens, y_lens):
+def attention_model_loss(p, cfg, xs, ys, x_lens, y_lens, train=None):
     """AttentionSeq2seq.forward (attention_seq2seq.py:422-562) for the
     bahdanau order, location attention, 1 head, LSTM decoder, forward
-    direction only (backward_loss_weight = 0), ss_prob = 0, dropout = 0."""
+    direction only (backward_loss_weight = 0), encoder dropout 0.
+
+    train (optional): replayed training-mode randomness, all in the sorted
+    utterance order -- 'h' [B,S,D] decoder dropout scales on h after the
+    LSTMCell (rnn_decoder.py:97-98; the dropped h is dec_out and the state),
+    'd' / 'c' [B,S,Dz] scales on the W_d / W_c LinearND outputs (linear.py:45),
+    'emb' [B,S,Y] scales on the teacher embeddings, and scheduled sampling
+    (attention_seq2seq.py:744-748): 'ss' [S] flags, 'emb_ss' [B,S,Y] scales on
+    the sampled embedding embed(argmax logits_{t-1}) (detached)."""
+    train = train or {}
     xs_t = torch.from_numpy(np.asarray(xs, np.float32))
     enc_cfg = dict(num_layers=cfg['encoder_num_layers'], subsample_list=cfg['subsample_list'])
     enc_out, enc_lens, perm = blstm_encoder(p, 'encoder.', enc_cfg, xs_t, x_lens)
@@ -201,16 +210,34 @@ def attention_model_loss(p, cfg, xs, ys, x_lens, y_lens):
     else:                                                    # Embedding, padding_idx=-1
         emb_w = p['embed_0.embed.weight']
     ys_emb = emb_w[torch.as_tensor(ys_in)]                   # [B, L+1, emb]
+    mk = {k: torch.from_numpy(np.asarray(v, np.float32)) for k, v in train.items() if k != 'ss'}
+    if 'emb' in mk:
+        ys_emb = ys_emb * mk['emb']
+    ss = train.get('ss')
     logits = []
     for t in range(Lp + 1):                                  # :742-793
         if t > 0:
-            dec_in = torch.cat([ys_emb[:, t], ctx], dim=-1)
+            if ss is not None and ss[t]:                     # scheduled sampling :744-748
+                tok = torch.argmax(logits[-1], dim=-1)
+                y = emb_w[tok].detach()
+                if 'emb_ss' in mk:
+                    y = y * mk['emb_ss'][:, t]
+            else:
+                y = ys_emb[:, t]
+            dec_in = torch.cat([y, ctx], dim=-1)
             h, c = lstm_cell(p, 'decoder_0_fwd.lstm_l0', dec_in, h, c)
+            if 'h' in mk:
+                h = h * mk['h'][:, t]
             dec_out = h
         ctx, aw = location_attention(p, pre, enc_out, enc_out_a, enc_lens, dec_out, aw,
                                      cfg.get('sharpening_factor', 1),
                                      cfg.get('sigmoid_smoothing', False))
-        z = torch.tanh(linear_nd(p, 'W_d_0_fwd', dec_out) + linear_nd(p, 'W_c_0_fwd', ctx))
+        a = linear_nd(p, 'W_d_0_fwd', dec_out)
+        cc = linear_nd(p, 'W_c_0_fwd', ctx)
+        if 'd' in mk:
+            a = a * mk['d'][:, t]
+            cc = cc * mk['c'][:, t]
+        z = torch.tanh(a + cc)
         logits.append(linear_nd(p, 'fc_0_fwd', z))
     logits = torch.stack(logits, 1)                          # [B, L+1, V]
     if cfg.get('logits_temperature', 1) != 1:

@@ -63,6 +63,7 @@ SIGNATURES = {
                                        c_vp]),
     'asr_tanh_forward': (c_int, [c_vp, c_vp, c_ll, c_vp]),
     'asr_tanh_backward': (c_int, [c_vp, c_vp, c_vp, c_ll, c_vp]),
+    'asr_add_tanh_forward': (c_int, [c_vp, c_vp, c_vp, c_ll, c_vp]),
     'asr_convert_rows_bf16': None,  # set below, after RowMap (struct passed by value)
     'asr_ctc_best_path': (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp,
                                   c_vp]),
@@ -78,6 +79,10 @@ SIGNATURES = {
                                                                                      c_vp]),
     'asr_attdec_backward': (c_int, [c_vp, c_int] + [c_vp] * 4 + [c_ll] + [c_vp] * 19 + [c_size,
                                                                                       c_vp]),
+    'asr_attdec_forward_ex': (c_int, [c_vp, c_vp, c_int] + [c_vp] * 4 + [c_ll] + [c_vp] * 14 +
+                              [c_size, c_vp]),
+    'asr_attdec_backward_ex': (c_int, [c_vp, c_vp, c_int] + [c_vp] * 4 + [c_ll] + [c_vp] * 19 +
+                               [c_size, c_vp]),
     'asr_prof_begin': (c_int, [c_int]),
     'asr_prof_end': (c_int, [c_vp, c_vp, c_vp, c_int]),
     'asr_lstm_persist_status': (c_int, [c_vp, c_int, c_vp]),
@@ -105,6 +110,18 @@ class AttDecDims(ctypes.Structure):
     """asr_attdec_dims_t"""
     _fields_ = [(n, c_int) for n in ('B', 'T', 'E', 'A', 'C', 'K', 'D', 'S')] + [
         ('sharpening', c_float), ('sigmoid_smoothing', c_int)]
+
+
+class AttDecOpts(ctypes.Structure):
+    """asr_attdec_opts_t (decoder dropout + scheduled sampling)"""
+    _fields_ = [('dropout_hidden', c_float), ('seed_hidden', ctypes.c_ulonglong),
+                ('ss_steps_host', c_vp), ('Y', c_int), ('Dz', c_int), ('V', c_int),
+                ('w_d', c_vp), ('b_d', c_vp), ('drop_d', c_float), ('seed_d', ctypes.c_ulonglong),
+                ('w_c', c_vp), ('b_c', c_vp), ('drop_c', c_float), ('seed_c', ctypes.c_ulonglong),
+                ('w_fc', c_vp), ('b_fc', c_vp), ('emb_w', c_vp), ('emb_trans', c_int),
+                ('drop_emb', c_float), ('seed_emb', ctypes.c_ulonglong), ('w_ih_emb', c_vp),
+                ('ld_ih', c_ll), ('b_ih', c_vp), ('b_hh', c_vp), ('pre_ss', c_vp),
+                ('emb_ss', c_vp), ('tok_ss', c_vp), ('d_pre', c_vp), ('dg_ss', c_vp)]
 
 
 class Gemm(ctypes.Structure):
@@ -160,6 +177,11 @@ def ptr(t):
     if t is None:
         return None
     return ctypes.c_void_p(t.data_ptr())
+
+
+def ptr_struct(s):
+    """Pointer to a ctypes struct (None -> NULL)."""
+    return None if s is None else ctypes.byref(s)
 
 
 def stream_handle(device=None):

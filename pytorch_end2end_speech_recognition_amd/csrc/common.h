@@ -70,6 +70,22 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// Dropout RNG shared by every kernel that applies or regenerates a mask:
+// 64-bit counter hash -> uniform [0,1) (splitmix64 finaliser).  Element i of a
+// tensor dropped with `seed` is kept iff u01(seed, i) >= p.
+__device__ __forceinline__ float u01(unsigned long long seed, unsigned long long i) {
+  unsigned long long z = seed + 0x9E3779B97F4A7C15ull * (i + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (float)(z >> 40) * (1.0f / 16777216.0f);
+}
+
+__device__ __forceinline__ float drop_scale(float p, unsigned long long seed,
+                                            unsigned long long i) {
+  return u01(seed, i) >= p ? 1.f / (1.f - p) : 0.f;
+}
+
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
 
 // Accurate tanh for the fp32 parity path (libm), fast enough for the recurrence.

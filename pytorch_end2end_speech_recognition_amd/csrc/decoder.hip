@@ -97,7 +97,7 @@ __global__ void __launch_bounds__(256) cell_fwd(int t, Dims d, const TW* __restr
                                                 const float* __restrict__ pre_emb,
                                                 float* __restrict__ x, float* __restrict__ gates,
                                                 float* __restrict__ c_all, float* __restrict__ dec,
-                                                int vec) {
+                                                int vec, float drop_h, unsigned long long seed_h) {
   __shared__ float part[4][MB][16];
   const int ED = d.E + d.D, G = 4 * d.D;
   const int u0 = blockIdx.x * CU, b0 = blockIdx.y * MB;
@@ -143,7 +143,8 @@ __global__ void __launch_bounds__(256) cell_fwd(int t, Dims d, const TW* __restr
   const float ig = sigmoidf_(pre[0]), fg = sigmoidf_(pre[1]);
   const float gg = tanhf_(pre[2]), og = sigmoidf_(pre[3]);
   const float c = fg * cprev + ig * gg;
-  const float h = og * tanhf_(c);
+  float h = og * tanhf_(c);
+  if (drop_h > 0.f) h *= drop_scale(drop_h, seed_h, ((unsigned long long)b * d.S + t) * d.D + j);
   c_all[((long long)b * d.S + t) * d.D + j] = c;
   dec[((long long)b * d.S + t) * d.D + j] = h;
   gates[gb] = ig;
@@ -450,7 +451,8 @@ __global__ void __launch_bounds__(ATT_THREADS) att_bwd(
 __global__ void cell_bwd(int t, Dims d, const float* __restrict__ d_dec_in,
                          const float* __restrict__ r, const float* __restrict__ ddec_att,
                          float* __restrict__ gates, const float* __restrict__ c_all,
-                         float* __restrict__ dc, float* __restrict__ d_h0) {
+                         float* __restrict__ dc, float* __restrict__ d_h0, float drop_h,
+                         unsigned long long seed_h) {
   const int ED = d.E + d.D, G = 4 * d.D;
   const long long n = (long long)d.B * d.D;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
@@ -462,18 +464,109 @@ __global__ void cell_bwd(int t, Dims d, const float* __restrict__ d_dec_in,
       if (d_h0) d_h0[i] = dh;
       continue;
     }
+    // dh is w.r.t. the dropped h (dec_out and the recurrent state): back through the mask
+    const float dhr =
+        drop_h > 0.f ? dh * drop_scale(drop_h, seed_h, ((unsigned long long)b * d.S + t) * d.D + j)
+                     : dh;
     const long long gb = ((long long)b * d.S + t) * G + j;
     const float ig = gates[gb], fg = gates[gb + d.D], gg = gates[gb + 2 * d.D],
                 og = gates[gb + 3 * d.D];
     const float c = c_all[((long long)b * d.S + t) * d.D + j];
     const float cp = c_all[((long long)b * d.S + t - 1) * d.D + j];
     const float tc = tanhf(c);
-    const float dcell = dc[i] + dh * og * (1.f - tc * tc);
+    const float dcell = dc[i] + dhr * og * (1.f - tc * tc);
     gates[gb] = dcell * gg * ig * (1.f - ig);
     gates[gb + d.D] = dcell * cp * fg * (1.f - fg);
     gates[gb + 2 * d.D] = dcell * ig * (1.f - gg * gg);
-    gates[gb + 3 * d.D] = dh * tc * og * (1.f - og);
+    gates[gb + 3 * d.D] = dhr * tc * og * (1.f - og);
     dc[i] = dcell * fg;
+  }
+}
+
+// ------------------------------------------------------ scheduled sampling
+// One work-group per utterance, before the cell of a sampled step t >= 1:
+// logits_{t-1} = fc(tanh(drop_d(W_d dec_{t-1} + b_d) + drop_c(W_c ctx_{t-1} + b_c))),
+// tok = first argmax, e = drop_emb(emb(tok)), pre_ss[b,t] = W_ih[:, :Y] e + b_ih + b_hh.
+constexpr int SS_THREADS = 256;
+
+__global__ void __launch_bounds__(SS_THREADS) ss_step(int t, Dims d, asr_attdec_opts_t o,
+                                                      const float* __restrict__ dec,
+                                                      const float* __restrict__ ctx_all) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* h = sm;              // [D]
+  float* cx = h + d.D;        // [E]
+  float* z = cx + d.E;        // [Dz]
+  float* e = z + o.Dz;        // [Y]
+  float* rv = e + o.Y;        // [SS_THREADS / 64] best values
+  int* ri = (int*)(rv + SS_THREADS / 64);
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = SS_THREADS / 64;
+  const long long prev = (long long)b * d.S + (t - 1);
+  for (int i = tid; i < d.D; i += SS_THREADS) h[i] = dec[prev * d.D + i];
+  for (int i = tid; i < d.E; i += SS_THREADS) cx[i] = ctx_all[prev * d.E + i];
+  __syncthreads();
+  for (int k = w; k < o.Dz; k += nw) {   // one wave per bottleneck unit, lanes over K
+    const float* wd = o.w_d + (long long)k * d.D;
+    const float* wc = o.w_c + (long long)k * d.E;
+    float sa = 0.f, sc = 0.f;
+    for (int j = lane; j < d.D; j += 64) sa += wd[j] * h[j];
+    for (int j = lane; j < d.E; j += 64) sc += wc[j] * cx[j];
+    sa = wave_sum(sa);
+    sc = wave_sum(sc);
+    if (lane == 0) {
+      float a = sa + (o.b_d ? o.b_d[k] : 0.f), c = sc + (o.b_c ? o.b_c[k] : 0.f);
+      const unsigned long long idx = (unsigned long long)prev * o.Dz + k;
+      if (o.drop_d > 0.f) a *= drop_scale(o.drop_d, o.seed_d, idx);
+      if (o.drop_c > 0.f) c *= drop_scale(o.drop_c, o.seed_c, idx);
+      z[k] = tanhf(a + c);
+    }
+  }
+  __syncthreads();
+  float best = -__builtin_huge_valf();
+  int bi = 0x7fffffff;
+  for (int v = w; v < o.V; v += nw) {    // one wave per class; classes ascending per wave
+    const float* wr = o.w_fc + (long long)v * o.Dz;
+    float s = 0.f;
+    for (int k = lane; k < o.Dz; k += 64) s += wr[k] * z[k];
+    s = wave_sum(s) + (o.b_fc ? o.b_fc[v] : 0.f);
+    if (s > best) { best = s; bi = v; }   // strict: the first maximum wins
+  }
+  if (lane == 0) { rv[w] = best; ri[w] = bi; }
+  __syncthreads();
+  float bv = rv[0];
+  int tok = ri[0];
+  for (int i = 1; i < nw; ++i)
+    if (rv[i] > bv || (rv[i] == bv && ri[i] < tok)) { bv = rv[i]; tok = ri[i]; }
+  const long long cur = (long long)b * d.S + t;
+  for (int y = tid; y < o.Y; y += SS_THREADS) {
+    float ev = o.emb_trans ? o.emb_w[(long long)y * o.V + tok] : o.emb_w[(long long)tok * o.Y + y];
+    if (o.drop_emb > 0.f) ev *= drop_scale(o.drop_emb, o.seed_emb, (unsigned long long)cur * o.Y + y);
+    e[y] = ev;
+    o.emb_ss[cur * o.Y + y] = ev;
+  }
+  if (tid == 0 && o.tok_ss) o.tok_ss[cur] = tok;
+  __syncthreads();
+  const int G = 4 * d.D;
+  for (int g = tid; g < G; g += SS_THREADS) {
+    const float* wr = o.w_ih_emb + (long long)g * o.ld_ih;
+    float s = o.b_ih[g] + o.b_hh[g];
+    for (int y = 0; y < o.Y; ++y) s += wr[y] * e[y];
+    o.pre_ss[cur * G + g] = s;
+  }
+}
+
+// d_pre = dG with sampled steps zeroed; dg_ss = dG at sampled steps only.
+__global__ void ss_split(Dims d, const int32_t* __restrict__ flags, const float* __restrict__ dg,
+                         float* __restrict__ d_pre, float* __restrict__ dg_ss) {
+  const int G = 4 * d.D;
+  const long long n = (long long)d.B * d.S * G;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int t = (int)((i / G) % d.S);
+    const float v = dg[i];
+    const bool smp = flags[t] != 0;
+    d_pre[i] = smp ? 0.f : v;
+    dg_ss[i] = smp ? v : 0.f;
   }
 }
 
@@ -508,9 +601,29 @@ extern "C" size_t asr_attdec_workspace_bytes(const asr_attdec_dims_t* dims, int 
     n += ((size_t)d.B * d.T * 4 + 255) & ~size_t(255);          // carry
     n += ((size_t)d.B * d.D * 4 + 255) & ~size_t(255);          // ddec_att
     n += ((size_t)d.B * d.D * 4 + 255) & ~size_t(255);          // dc
+    n += ((size_t)d.S * 4 + 255) & ~size_t(255);                // sampled-step flags
   }
   return n;
 }
+
+namespace {
+int check_opts(const Dims& d, const asr_attdec_opts_t* o, bool* ss) {
+  *ss = false;
+  if (!o) return ASR_OK;
+  ASR_REQUIRE(o->dropout_hidden >= 0.f && o->dropout_hidden < 1.f, ASR_ERR_ARG,
+              "attdec: dropout_hidden=%f", o->dropout_hidden);
+  if (!o->ss_steps_host) return ASR_OK;
+  for (int t = 1; t < d.S; ++t) *ss |= o->ss_steps_host[t] != 0;
+  if (!*ss) return ASR_OK;
+  ASR_REQUIRE(o->Y > 0 && o->Dz > 0 && o->V > 0 && o->w_d && o->w_c && o->w_fc && o->emb_w &&
+                  o->w_ih_emb && o->b_ih && o->b_hh && o->pre_ss && o->emb_ss,
+              ASR_ERR_ARG, "attdec: scheduled sampling needs Y/Dz/V and its weights");
+  ASR_REQUIRE(o->drop_d >= 0.f && o->drop_d < 1.f && o->drop_c >= 0.f && o->drop_c < 1.f &&
+                  o->drop_emb >= 0.f && o->drop_emb < 1.f,
+              ASR_ERR_ARG, "attdec: bad dropout probability");
+  return ASR_OK;
+}
+}  // namespace
 
 extern "C" int asr_attdec_forward(const asr_attdec_dims_t* dims, int compute_dtype,
                                   const float* enc, const float* enc_a, const int32_t* lens,
@@ -520,10 +633,28 @@ extern "C" int asr_attdec_forward(const asr_attdec_dims_t* dims, int compute_dty
                                   float* dec, float* c_all, float* gates, float* x,
                                   float* ctx_all, float* aw_all, void* workspace,
                                   size_t ws_bytes, void* stream) {
+  return asr_attdec_forward_ex(dims, nullptr, compute_dtype, enc, enc_a, lens, w_ih_ctx, ld_ih,
+                               w_hh, w_dec, w_conv, conv_w, v, pre_emb, h0, dec, c_all, gates, x,
+                               ctx_all, aw_all, workspace, ws_bytes, stream);
+}
+
+extern "C" int asr_attdec_forward_ex(const asr_attdec_dims_t* dims, const asr_attdec_opts_t* opts,
+                                     int compute_dtype, const float* enc, const float* enc_a,
+                                     const int32_t* lens, const float* w_ih_ctx, long long ld_ih,
+                                     const float* w_hh, const float* w_dec, const float* w_conv,
+                                     const float* conv_w, const float* v, const float* pre_emb,
+                                     const float* h0, float* dec, float* c_all, float* gates,
+                                     float* x, float* ctx_all, float* aw_all, void* workspace,
+                                     size_t ws_bytes, void* stream) {
   ASR_REQUIRE(dims, ASR_ERR_ARG, "attdec: dims is null");
   const Dims d = to_dims(*dims);
   int rc = check_dims(d);
   if (rc) return rc;
+  bool ss = false;
+  rc = check_opts(d, opts, &ss);
+  if (rc) return rc;
+  const float drop_h = opts ? opts->dropout_hidden : 0.f;
+  const unsigned long long seed_h = opts ? opts->seed_hidden : 0ull;
   ASR_REQUIRE(enc && enc_a && lens && w_ih_ctx && w_hh && w_dec && w_conv && conv_w && v &&
                   pre_emb && dec && c_all && gates && x && ctx_all && aw_all && workspace,
               ASR_ERR_ARG, "attdec_forward: null pointer");
@@ -545,14 +676,26 @@ extern "C" int asr_attdec_forward(const asr_attdec_dims_t* dims, int compute_dty
   const size_t lds = att_lds_floats(d) * 4;
   const int vec = ((d.E + d.D) % 8 == 0) ? 1 : 0;
   const dim3 cg(ceil_div(d.D, CU), ceil_div(d.B, MB));
+  const size_t ss_lds = ss ? ((size_t)d.D + d.E + opts->Dz + opts->Y + 2 * (SS_THREADS / 64)) * 4
+                          : 0;
+  ASR_REQUIRE(ss_lds <= 160 * 1024, ASR_ERR_UNSUPPORTED, "attdec: sampling LDS %zu B", ss_lds);
   for (int t = 0; t < d.S; ++t) {
     if (t > 0) {
+      const bool smp = ss && opts->ss_steps_host[t] != 0;
+      if (smp) {
+        hipLaunchKernelGGL(ss_step, dim3(d.B), dim3(SS_THREADS), ss_lds, s, t, d, *opts, dec,
+                           ctx_all);
+        ASR_LAUNCH_CHECK();
+      }
+      const float* pre = smp ? opts->pre_ss : pre_emb;
       if (bf)
         hipLaunchKernelGGL((cell_fwd<true, uint16_t>), cg, dim3(256), 0, s, t, d,
-                           (const uint16_t*)workspace, pre_emb, x, gates, c_all, dec, vec);
+                           (const uint16_t*)workspace, pre, x, gates, c_all, dec, vec, drop_h,
+                           seed_h);
       else
         hipLaunchKernelGGL((cell_fwd<false, float>), cg, dim3(256), 0, s, t, d,
-                           (const float*)workspace, pre_emb, x, gates, c_all, dec, vec);
+                           (const float*)workspace, pre, x, gates, c_all, dec, vec, drop_h,
+                           seed_h);
       ASR_LAUNCH_CHECK();
     }
     hipLaunchKernelGGL(att_fwd, dim3(d.B), dim3(ATT_THREADS), lds, s, t, d, enc, enc_a, lens,
@@ -572,10 +715,34 @@ extern "C" int asr_attdec_backward(const asr_attdec_dims_t* dims, int compute_dt
                                    float* d_enc_a, float* d_h0, float* dwd_all, float* dv_part,
                                    float* dwc_part, float* dcw_part, void* workspace,
                                    size_t ws_bytes, void* stream) {
+  return asr_attdec_backward_ex(dims, nullptr, compute_dtype, enc, enc_a, lens, w_ih_ctx, ld_ih,
+                                w_hh, w_dec, w_conv, conv_w, v, dec, c_all, aw_all, d_dec_in,
+                                d_ctx_in, gates_dg, dctx_tot, d_enc_a, d_h0, dwd_all, dv_part,
+                                dwc_part, dcw_part, workspace, ws_bytes, stream);
+}
+
+extern "C" int asr_attdec_backward_ex(const asr_attdec_dims_t* dims, const asr_attdec_opts_t* opts,
+                                      int compute_dtype, const float* enc, const float* enc_a,
+                                      const int32_t* lens, const float* w_ih_ctx, long long ld_ih,
+                                      const float* w_hh, const float* w_dec, const float* w_conv,
+                                      const float* conv_w, const float* v, const float* dec,
+                                      const float* c_all, const float* aw_all,
+                                      const float* d_dec_in, const float* d_ctx_in,
+                                      float* gates_dg, float* dctx_tot, float* d_enc_a,
+                                      float* d_h0, float* dwd_all, float* dv_part,
+                                      float* dwc_part, float* dcw_part, void* workspace,
+                                      size_t ws_bytes, void* stream) {
   ASR_REQUIRE(dims, ASR_ERR_ARG, "attdec: dims is null");
   const Dims d = to_dims(*dims);
   int rc = check_dims(d);
   if (rc) return rc;
+  bool ss = false;
+  rc = check_opts(d, opts, &ss);
+  if (rc) return rc;
+  ASR_REQUIRE(!ss || (opts->d_pre && opts->dg_ss), ASR_ERR_ARG,
+              "attdec_backward: scheduled sampling needs d_pre and dg_ss");
+  const float drop_h = opts ? opts->dropout_hidden : 0.f;
+  const unsigned long long seed_h = opts ? opts->seed_hidden : 0ull;
   ASR_REQUIRE(enc && enc_a && lens && w_ih_ctx && w_hh && w_dec && w_conv && conv_w && v &&
                   dec && c_all && aw_all && d_dec_in && d_ctx_in && gates_dg && dctx_tot &&
                   d_enc_a && dwd_all && dv_part && dwc_part && dcw_part && workspace,
@@ -595,6 +762,8 @@ extern "C" int asr_attdec_backward(const asr_attdec_dims_t* dims, int compute_dt
   float* ddec_att = (float*)p;
   p += ((size_t)d.B * d.D * 4 + 255) & ~size_t(255);
   float* dc = (float*)p;
+  p += ((size_t)d.B * d.D * 4 + 255) & ~size_t(255);
+  int32_t* flags = (int32_t*)p;
   const long long nw = 4LL * d.D * ED;
   const int gb = (int)((nw + 255) / 256 < 4096 ? (nw + 255) / 256 : 4096);
   if (bf)
@@ -637,7 +806,16 @@ extern "C" int asr_attdec_backward(const asr_attdec_dims_t* dims, int compute_dt
                        d_enc_a, ddec_att, dwd_all, dv_part, dwc_part, dcw_part);
     ASR_LAUNCH_CHECK();
     hipLaunchKernelGGL(cell_bwd, dim3(cgrid), dim3(256), 0, s, t, d, d_dec_in, rp, ddec_att,
-                       gates_dg, c_all, dc, d_h0);
+                       gates_dg, c_all, dc, d_h0, drop_h, seed_h);
+    ASR_LAUNCH_CHECK();
+  }
+  if (ss) {
+    ASR_CHECK_HIP(hipMemcpyAsync(flags, opts->ss_steps_host, (size_t)d.S * 4,
+                                 hipMemcpyHostToDevice, s));
+    const long long n = (long long)d.B * d.S * G;
+    const int gs = (int)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+    hipLaunchKernelGGL(ss_split, dim3(gs), dim3(256), 0, s, d, flags, gates_dg, opts->d_pre,
+                       opts->dg_ss);
     ASR_LAUNCH_CHECK();
   }
   return ASR_OK;

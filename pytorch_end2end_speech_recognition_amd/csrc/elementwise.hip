@@ -6,15 +6,6 @@
 namespace asr {
 namespace {
 
-// 64-bit counter hash -> uniform [0,1) (splitmix64 finaliser).
-__device__ __forceinline__ float u01(unsigned long long seed, unsigned long long i) {
-  unsigned long long z = seed + 0x9E3779B97F4A7C15ull * (i + 1);
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= z >> 31;
-  return (float)(z >> 40) * (1.0f / 16777216.0f);
-}
-
 __global__ void dropout_kernel(const float* __restrict__ x, float* __restrict__ y, long long n,
                                float p, unsigned long long seed) {
   const float scale = 1.f / (1.f - p);
@@ -104,6 +95,15 @@ __global__ void convert_rows_kernel(const float* __restrict__ src, asr_rowmap_t 
   }
 }
 
+// y = tanh(a + b): the attention bottleneck tanh(W_d(dec) + W_c(ctx)) when the
+// two LinearND outputs carry their own dropout (attention_seq2seq.py:788-790)
+__global__ void add_tanh_fwd(const float* __restrict__ a, const float* __restrict__ b,
+                             float* __restrict__ y, long long n) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    y[i] = tanhf(a[i] + b[i]);
+}
+
 inline int grid_for(long long n) {
   long long b = (n + 255) / 256;
   return (int)(b < 4096 ? (b > 0 ? b : 1) : 4096);
@@ -150,6 +150,16 @@ extern "C" int asr_tanh_forward(const float* x, float* y, long long n, void* str
   ASR_REQUIRE(x && y, ASR_ERR_ARG, "tanh: null pointer");
   if (n <= 0) return ASR_OK;
   hipLaunchKernelGGL(tanh_fwd, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, y, n);
+  ASR_LAUNCH_CHECK();
+  return ASR_OK;
+}
+
+extern "C" int asr_add_tanh_forward(const float* a, const float* b, float* y, long long n,
+                                    void* stream) {
+  ASR_REQUIRE(a && b && y, ASR_ERR_ARG, "add_tanh: null pointer");
+  if (n <= 0) return ASR_OK;
+  hipLaunchKernelGGL(add_tanh_fwd, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, a, b, y,
+                     n);
   ASR_LAUNCH_CHECK();
   return ASR_OK;
 }

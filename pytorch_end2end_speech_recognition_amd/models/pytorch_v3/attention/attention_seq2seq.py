@@ -17,6 +17,8 @@ encoder states, the W_d / W_c bottleneck, the output layer and the loss -- is
 hoisted into full-batch GEMMs before / after the loop; per step only the
 LSTMCell and the fused location-attention kernel run.
 """
+import random
+
 import numpy as np
 import torch
 
@@ -173,11 +175,6 @@ class AttentionSeq2seq(ModelBase):
                 with torch.no_grad():
                     self._flat_param.add_(torch.randn_like(self._flat_param) *
                                           self.weight_noise_std)
-        ss_active = (self.ss_prob > 0 and self._step > 0 and not is_eval and
-                     self._ss_prob > 0)
-        if ss_active:
-            raise NotImplementedError('scheduled sampling needs the per-step decode path '
-                                      '(next-round item)')
         B = len(xs)
         xs_d = self.np2var(xs, dtype='float')
         enc_out, enc_lens_d, perm_d = self._encode(xs_d, x_lens)
@@ -248,24 +245,64 @@ class AttentionSeq2seq(ModelBase):
         h = ops.linear_ex(enc_out, lin.weight, lin.bias, t_index=0 if mode == 'first' else T - 1)
         return ops.tanh(h)
 
+    def _ss_steps(self, S):
+        """Scheduled-sampling decisions of one decoder pass (attention_seq2seq.py:744):
+        the reference draws ``random.random() < self._ss_prob`` at every step
+        t > 0 once training has stepped (same Python RNG stream)."""
+        if not (self.training and self.ss_prob > 0 and self._step > 0):
+            return None
+        flags = np.zeros(S, np.int32)
+        for t in range(1, S):
+            flags[t] = random.random() < self._ss_prob
+        return flags if flags.any() else None
+
     def _decode_train(self, enc_out, x_lens, ys, task=0, dir='fwd'):
-        """:704-799 as one fused op (bahdanau order).  Returns (logits [B,S,V], aw)."""
-        if self.training and self.dropout_decoder > 0:
-            raise NotImplementedError('decoder dropout inside the fused loop is a next-round item')
+        """:704-799 as one fused op (bahdanau order).  Returns (logits [B,S,V], aw).
+
+        Training mode: decoder dropout on h (rnn_decoder.py:97-98) inside the
+        fused loop, dropout on the W_d / W_c bottleneck outputs (LinearND,
+        linear.py:44-45), embedding dropout, and scheduled sampling -- sampled
+        steps take embed(argmax logits_{t-1}) computed inside the loop from the
+        same dropped bottleneck the loss sees (shared dropout seeds)."""
         att = self.attend_0_fwd
         cell = self.decoder_0_fwd.lstm_l0
+        W_d, W_c = self.W_d_0_fwd, self.W_c_0_fwd
+        S = ys.shape[1]
         h0 = self._init_h0(enc_out)
         enc_a = att.W_enc_head0(enc_out)                          # one GEMM for all frames
-        y_emb = self.embed_0(ys)                                  # [B, S, emb]
+        y_emb = self.embed_0(ys)                                  # [B, S, emb] (+ dropout)
         pre_emb = ops.linear_ex(y_emb, cell.weight_ih, cell.bias_ih, cell.bias_hh, c0=0,
                                 K=self.embedding_dim)             # all steps' input projection
+        p_h = self.dropout_decoder if self.training else 0.0
+        p_b = W_d.dropout_p if self.training else 0.0
+        seed_d = ops.next_seed() if p_b > 0 else 0
+        seed_c = ops.next_seed() if p_b > 0 else 0
+        ss = self._ss_steps(S)
+        train_opts = None
+        if p_h > 0 or ss is not None:
+            train_opts = dict(dropout_hidden=p_h, seed_hidden=ops.next_seed() if p_h > 0 else 0)
+            if ss is not None:
+                emb_ls = isinstance(self.embed_0, Embedding_LS)
+                emb_w = self.embed_0.embed.fc.weight if emb_ls else self.embed_0.embed.weight
+                p_e = self.dropout_embedding if self.training else 0.0
+                train_opts.update(
+                    ss_steps=ss, w_d=W_d.fc.weight, b_d=W_d.fc.bias, w_c=W_c.fc.weight,
+                    b_c=W_c.fc.bias, w_fc=self.fc_0_fwd.fc.weight, b_fc=self.fc_0_fwd.fc.bias,
+                    emb_w=emb_w, emb_trans=int(emb_ls), b_ih=cell.bias_ih, b_hh=cell.bias_hh,
+                    drop_d=p_b, seed_d=seed_d, drop_c=p_b, seed_c=seed_c, drop_emb=p_e,
+                    seed_emb=ops.next_seed() if p_e > 0 else 0)
         dec, ctx, aw = ops.att_decoder(enc_out, enc_a, x_lens, pre_emb, h0, self.embedding_dim,
                                        self.sharpening_factor, self.sigmoid_smoothing,
                                        cell.weight_ih, cell.weight_hh, att.W_dec_head0.fc.weight,
                                        att.W_conv_head0.fc.weight, att.conv_head0.weight,
-                                       att.V_head0.fc.weight)
-        z = ops.tanh(ops.linear2(dec, self.W_d_0_fwd.fc.weight, self.W_d_0_fwd.fc.bias, ctx,
-                                 self.W_c_0_fwd.fc.weight, self.W_c_0_fwd.fc.bias))
+                                       att.V_head0.fc.weight, train_opts)
+        if p_b > 0:   # two LinearND with their own dropout masks, then tanh of the sum
+            a = ops.dropout(ops.linear(dec, W_d.fc.weight, W_d.fc.bias), p_b, seed=seed_d)
+            c = ops.dropout(ops.linear(ctx, W_c.fc.weight, W_c.fc.bias), p_b, seed=seed_c)
+            z = ops.add_tanh(a, c)
+        else:
+            z = ops.tanh(ops.linear2(dec, W_d.fc.weight, W_d.fc.bias, ctx, W_c.fc.weight,
+                                     W_c.fc.bias))
         logits = self.fc_0_fwd(z)
         return logits, aw
 

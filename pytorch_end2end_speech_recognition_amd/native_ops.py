@@ -11,6 +11,7 @@ the Functions therefore return ``None`` for weights.
 import ctypes
 import os
 
+import numpy as np
 import torch
 
 from . import _native as N
@@ -250,7 +251,7 @@ class AttDecoderFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, enc, enc_a, lens, pre_emb, h0, emb_dim, sharpen, sigmoid, w_ih, w_hh,
-                w_dec, w_conv, conv_w, v):
+                w_dec, w_conv, conv_w, v, train_opts):
         N.require_device(enc, enc_a, lens, pre_emb, w_ih)
         enc, enc_a, pre_emb = enc.contiguous(), enc_a.contiguous(), pre_emb.contiguous()
         B, T, E = enc.shape
@@ -272,14 +273,17 @@ class AttDecoderFn(torch.autograd.Function):
         ws = _ws(nb, dev)
         ld_ih = w_ih.shape[1]
         w_ih_ctx = ctypes.c_void_p(w_ih.data_ptr() + 4 * emb_dim)
-        N.call('asr_attdec_forward', ctypes.byref(dims), cd, N.ptr(enc), N.ptr(enc_a), N.ptr(lens),
-               w_ih_ctx, ld_ih, N.ptr(w_hh), N.ptr(w_dec), N.ptr(w_conv), N.ptr(conv_w), N.ptr(v),
-               N.ptr(pre_emb), N.ptr(h0.contiguous() if h0 is not None else None), N.ptr(dec),
-               N.ptr(cst), N.ptr(gates), N.ptr(x), N.ptr(ctxv), N.ptr(aw), N.ptr(ws), nb,
+        opts, keep = _attdec_opts(train_opts, B, S, D, emb_dim, w_ih, dev)
+        N.call('asr_attdec_forward_ex', ctypes.byref(dims), N.ptr_struct(opts), cd, N.ptr(enc),
+               N.ptr(enc_a), N.ptr(lens), w_ih_ctx, ld_ih, N.ptr(w_hh), N.ptr(w_dec),
+               N.ptr(w_conv), N.ptr(conv_w), N.ptr(v), N.ptr(pre_emb),
+               N.ptr(h0.contiguous() if h0 is not None else None), N.ptr(dec), N.ptr(cst),
+               N.ptr(gates), N.ptr(x), N.ptr(ctxv), N.ptr(aw), N.ptr(ws), nb,
                N.stream_handle(dev))
         ctx.save_for_backward(enc, enc_a, lens, w_ih, w_hh, w_dec, w_conv, conv_w, v, dec, cst,
                               gates, x, aw)
         ctx.meta = (dims, emb_dim, h0 is not None)
+        ctx.opts = (opts, keep, train_opts)
         ctx.mark_non_differentiable(aw)
         return dec, ctxv, aw
 
@@ -305,13 +309,32 @@ class AttDecoderFn(torch.autograd.Function):
         ws = _ws(nb, dev)
         ld_ih = w_ih.shape[1]
         w_ih_ctx = ctypes.c_void_p(w_ih.data_ptr() + 4 * emb_dim)
-        N.call('asr_attdec_backward', ctypes.byref(dims), cd, N.ptr(enc), N.ptr(enc_a),
-               N.ptr(lens), w_ih_ctx, ld_ih, N.ptr(w_hh), N.ptr(w_dec), N.ptr(w_conv),
-               N.ptr(conv_w), N.ptr(v), N.ptr(dec), N.ptr(cst), N.ptr(aw), N.ptr(d_dec),
-               N.ptr(d_ctx), N.ptr(gates), N.ptr(dctx_tot), N.ptr(d_enc_a), N.ptr(d_h0),
-               N.ptr(dwd), N.ptr(dv_part), N.ptr(dwc_part), N.ptr(dcw_part), N.ptr(ws), nb,
-               N.stream_handle(dev))
+        opts, keep, train_opts = ctx.opts
+        sampled = 'emb_ss' in keep
+        if sampled:
+            d_pre = torch.empty(B, S, 4 * D, **f32)
+            dg_ss = torch.empty(B, S, 4 * D, **f32)
+            opts.d_pre, opts.dg_ss = d_pre.data_ptr(), dg_ss.data_ptr()
+        N.call('asr_attdec_backward_ex', ctypes.byref(dims), N.ptr_struct(opts), cd, N.ptr(enc),
+               N.ptr(enc_a), N.ptr(lens), w_ih_ctx, ld_ih, N.ptr(w_hh), N.ptr(w_dec),
+               N.ptr(w_conv), N.ptr(conv_w), N.ptr(v), N.ptr(dec), N.ptr(cst), N.ptr(aw),
+               N.ptr(d_dec), N.ptr(d_ctx), N.ptr(gates), N.ptr(dctx_tot), N.ptr(d_enc_a),
+               N.ptr(d_h0), N.ptr(dwd), N.ptr(dv_part), N.ptr(dwc_part), N.ptr(dcw_part),
+               N.ptr(ws), nb, N.stream_handle(dev))
         dg = gates                          # dgates (row t = 0 is zero)
+        d_pre_out = dg
+        if sampled:
+            # sampled steps were fed embed(argmax) (detached): their gate gradients
+            # reach W_ih[:, :Y] through the embedding actually used and both
+            # biases, never the teacher embedding (attention_seq2seq.py:744-748)
+            emb_ss = keep['emb_ss']
+            Y = emb_dim
+            run_gemm([gemm_problem(operand(dg_ss, 1, rowmap(4 * D)), operand(emb_ss, 1, rowmap(Y)),
+                                   grad_buffer(w_ih), rowmap(ld_ih), 4 * D, Y, B * S, beta=1.0)],
+                     dev)
+            colsum_accumulate(dg_ss.view(B * S, 4 * D), grad_buffer(train_opts['b_ih']),
+                              grad_buffer(train_opts['b_hh']))
+            d_pre_out = d_pre
         BS, G, ED = B * S, 4 * D, E + D
         # LSTMCell weights: dW_ih[:, emb:] += dG^T x[:, :E]; dW_hh += dG^T x[:, E:]
         run_gemm([gemm_problem(operand(dg, 1, rowmap(G)), operand(x, 1, rowmap(ED)),
@@ -330,14 +353,52 @@ class AttDecoderFn(torch.autograd.Function):
         run_gemm([gemm_problem(operand(aw, 1, rowmap(T)), operand(dctx_tot, 1, rowmap(E)), d_enc,
                                rowmap(E), T, E, S, batch=B,
                                batch_strides=(S * T, S * E, T * E))], dev)
-        return (d_enc, d_enc_a, None, dg, d_h0, None, None, None, None, None, None, None, None,
-                None)
+        return (d_enc, d_enc_a, None, d_pre_out, d_h0, None, None, None, None, None, None, None,
+                None, None, None)
+
+
+def _attdec_opts(o, B, S, D, Y, w_ih, dev):
+    """asr_attdec_opts_t from the training options dict (None = inference
+    semantics: no dropout, teacher forcing).  Returns (opts | None, buffers to
+    keep alive)."""
+    keep = {}
+    if not o:
+        return None, keep
+    opts = N.AttDecOpts()
+    opts.dropout_hidden = float(o.get('dropout_hidden', 0.0))
+    opts.seed_hidden = int(o.get('seed_hidden', 0))
+    ss = o.get('ss_steps')
+    if ss is not None and np.any(ss[1:]):
+        flags = np.ascontiguousarray(ss, dtype=np.int32)
+        keep['flags'] = flags
+        f32 = dict(dtype=torch.float32, device=dev)
+        keep['pre_ss'] = torch.empty(B, S, 4 * D, **f32)
+        keep['emb_ss'] = torch.zeros(B, S, Y, **f32)
+        keep['tok_ss'] = torch.full((B, S), -1, dtype=torch.int64, device=dev)
+        opts.ss_steps_host = flags.ctypes.data
+        opts.Y, opts.Dz, opts.V = Y, o['w_d'].shape[0], o['w_fc'].shape[0]
+        for k in ('w_d', 'b_d', 'w_c', 'b_c', 'w_fc', 'b_fc', 'emb_w', 'b_ih', 'b_hh'):
+            setattr(opts, k, o[k].data_ptr() if o.get(k) is not None else None)
+        opts.drop_d, opts.seed_d = float(o.get('drop_d', 0.0)), int(o.get('seed_d', 0))
+        opts.drop_c, opts.seed_c = float(o.get('drop_c', 0.0)), int(o.get('seed_c', 0))
+        opts.drop_emb, opts.seed_emb = float(o.get('drop_emb', 0.0)), int(o.get('seed_emb', 0))
+        opts.emb_trans = int(o.get('emb_trans', 0))
+        opts.w_ih_emb, opts.ld_ih = w_ih.data_ptr(), w_ih.shape[1]
+        opts.pre_ss = keep['pre_ss'].data_ptr()
+        opts.emb_ss = keep['emb_ss'].data_ptr()
+        opts.tok_ss = keep['tok_ss'].data_ptr()
+    return opts, keep
 
 
 def att_decoder(enc, enc_a, lens, pre_emb, h0, emb_dim, sharpen, sigmoid, w_ih, w_hh, w_dec,
-                w_conv, conv_w, v):
+                w_conv, conv_w, v, train_opts=None):
+    """train_opts (training mode): dict with dropout_hidden / seed_hidden and,
+    for scheduled sampling, ss_steps (host int array [S]) plus the weights
+    w_d, b_d, w_c, b_c, w_fc, b_fc, emb_w (emb_trans), b_ih, b_hh and the
+    bottleneck / embedding dropout rates and seeds (drop_d, seed_d, drop_c,
+    seed_c, drop_emb, seed_emb)."""
     return AttDecoderFn.apply(enc, enc_a, lens, pre_emb, h0, emb_dim, sharpen, sigmoid, w_ih,
-                              w_hh, w_dec, w_conv, conv_w, v)
+                              w_hh, w_dec, w_conv, conv_w, v, train_opts)
 
 
 # ---------------------------------------------------------------------------
@@ -535,18 +596,23 @@ def manual_seed(seed):
     _seed['v'] = int(seed)
 
 
+_seed_log = {'on': False, 'seeds': []}   # tests: record the dropout seeds a step drew
+
+
 def _next_seed():
     _seed['v'] = (_seed['v'] * 6364136223846793005 + 1442695040888963407) % (1 << 64)
+    if _seed_log['on']:
+        _seed_log['seeds'].append(_seed['v'])
     return _seed['v']
 
 
 class DropoutFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, p):
+    def forward(ctx, x, p, seed=None):
         N.require_device(x)
         x = x.contiguous()
         y = torch.empty_like(x)
-        seed = _next_seed()
+        seed = _next_seed() if seed is None else int(seed)
         N.call('asr_dropout', N.ptr(x), N.ptr(y), x.numel(), float(p), seed,
                N.stream_handle(x.device))
         ctx.meta = (float(p), seed)
@@ -559,11 +625,44 @@ class DropoutFn(torch.autograd.Function):
         dx = torch.empty_like(dy)
         N.call('asr_dropout', N.ptr(dy), N.ptr(dx), dy.numel(), p, seed,
                N.stream_handle(dy.device))
-        return dx, None
+        return dx, None, None
 
 
-def dropout(x, p):
-    return DropoutFn.apply(x, p) if p > 0 else x
+def dropout(x, p, seed=None):
+    """nn.Dropout in training mode; element i of x is kept iff the counter RNG
+    u01(seed, i) >= p (seed drawn from the module stream unless given)."""
+    return DropoutFn.apply(x, p, seed) if p > 0 else x
+
+
+def next_seed():
+    return _next_seed()
+
+
+class AddTanhFn(torch.autograd.Function):
+    """y = tanh(a + b), one pass; d a = d b = dy (1 - y^2)."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        N.require_device(a, b)
+        a, b = a.contiguous(), b.contiguous()
+        y = torch.empty_like(a)
+        N.call('asr_add_tanh_forward', N.ptr(a), N.ptr(b), N.ptr(y), y.numel(),
+               N.stream_handle(a.device))
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        y, = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = torch.empty_like(dy)
+        N.call('asr_tanh_backward', N.ptr(y), N.ptr(dy), N.ptr(dx), y.numel(),
+               N.stream_handle(y.device))
+        return dx, dx
+
+
+def add_tanh(a, b):
+    return AddTanhFn.apply(a, b)
 
 
 class TanhFn(torch.autograd.Function):
