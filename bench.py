@@ -99,7 +99,7 @@ def synthetic_batch(B, T, F, num_classes, seed):
     return dict(xs=xs, ys=ys, x_lens=x_lens, y_lens=y_lens)
 
 
-def roofline_report(args, p, mean_us, launches, mean_work):
+def roofline_report(args, p, mean_us, launches, mean_work, workload):
     """Roofline of the dominant kernel (largest mean launch time x launches over
     the timed steps), from HIP-event timings taken on the kernels' own stream by
     the library's prof hooks (asr_prof_*).  Algorithmic work per launch:
@@ -154,7 +154,7 @@ def roofline_report(args, p, mean_us, launches, mean_work):
 
     out = {'bound': dom['bound']}
     out.update(view(dom))
-    traffic, tsrc = pmc_traffic(dom['name'])
+    traffic, tsrc = pmc_traffic(dom['name'], workload)
     out.update({'traffic': traffic, 'kernel': dom['name'], 'mean_launch_us': round(dom['us'], 3),
                 'launches_timed': dom['n'],
                 'algorithmic_bytes_per_launch': int(dom['bytes']),
@@ -178,7 +178,7 @@ def roofline_report(args, p, mean_us, launches, mean_work):
     return out
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(kernel, workload):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
     (profiles/rNN_pmc_traffic.json, written by tools/pmc_traffic.py from
     separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench's
@@ -190,6 +190,8 @@ def pmc_traffic(kernel):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
+            continue
+        if d.get('_workload', 'librispeech100h_char_ctc_blstm5x512') != workload:
             continue
         if kernel in d:
             return d[kernel]['traffic_bytes_per_launch'], os.path.relpath(f, ROOT)
@@ -312,7 +314,7 @@ def main():
         dist.destroy_process_group()
         return
 
-    roofline = roofline_report(args, p, mean_us, launches, mean_work)
+    roofline = roofline_report(args, p, mean_us, launches, mean_work, cfg['workload'])
 
     cpu = None
     if world == 1 and not args.no_cpu_baseline:

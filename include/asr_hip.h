@@ -296,8 +296,9 @@ int asr_softmax(const float* x, int R, int V, float* y, void* stream);
  *   W_d / W_c GEMMs).  Outputs: gates_dg (dgates over the saved gates; feeds
  *   dW_ih, dW_hh, db and the embedding gradient), dctx_tot [B][S][E] (feeds
  *   d enc = aw^T dctx_tot), d_enc_a [B][T][A], d_h0 [B][D] (nullable),
- *   dwd_all [B][S][A] (dW_dec = dwd^T dec), per-step partials dv_part
- *   [B][S][A], dwc_part [B][S][A*C], dcw_part [B][S][C*K] (column sums give
+ *   dwd_all [B][S][A] (dW_dec = dwd^T dec), per-(step, frame chunk) partials
+ *   dv_part [B][S][NC][A], dwc_part [B][S][NC][A*C], dcw_part [B][S][NC][C*K]
+ *   with NC = asr_attdec_chunks(dims) (column sums give
  *   dV, dW_conv, d conv kernel; deterministic).
  */
 typedef struct {
@@ -357,6 +358,7 @@ typedef struct {
 
 size_t asr_attdec_workspace_bytes(const asr_attdec_dims_t* dims, int compute_dtype,
                                   int backward);
+int asr_attdec_chunks(const asr_attdec_dims_t* dims);
 int asr_attdec_forward(const asr_attdec_dims_t* dims, int compute_dtype, const float* enc,
                        const float* enc_a, const int32_t* lens, const float* w_ih_ctx,
                        long long ld_ih, const float* w_hh, const float* w_dec,

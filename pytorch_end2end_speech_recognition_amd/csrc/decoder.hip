@@ -91,6 +91,22 @@ __global__ void build_wcat(Dims d, const float* __restrict__ w_ih_ctx, long long
   }
 }
 
+// Wcat^T[n][g] (n < E + D): the backward's per-step r = dgates @ Wcat reads rows
+template <typename TO>
+__global__ void build_wcat_t(Dims d, const float* __restrict__ w_ih_ctx, long long ld_ih,
+                             const float* __restrict__ w_hh, TO* __restrict__ out) {
+  const int ED = d.E + d.D, G = 4 * d.D;
+  const long long n = (long long)G * ED;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int col = (int)(i / G);
+    const long long g = i % G;
+    const float v = col < d.E ? w_ih_ctx[g * ld_ih + col] : w_hh[g * d.D + (col - d.E)];
+    if constexpr (sizeof(TO) == 2) out[i] = f2bf(v);
+    else out[i] = v;
+  }
+}
+
 // -------------------------------------------------------------- cell forward
 template <bool BF16, typename TW>
 __global__ void __launch_bounds__(256) cell_fwd(int t, Dims d, const TW* __restrict__ wcat,
@@ -154,34 +170,59 @@ __global__ void __launch_bounds__(256) cell_fwd(int t, Dims d, const TW* __restr
   if (t + 1 < d.S) x[((long long)b * d.S + t + 1) * ED + d.E + j] = h;
 }
 
-// -------------------------------------------------------- attention helpers
-struct AttLds {
-  float* aw;   // [T]   aw_{t-1}
-  float* f;    // [T*C] conv features
-  float* e;    // [T]   energies -> weights
-  float* wd;   // [A]   W_dec h
-  float* wc;   // [A*C] W_conv
-  float* cw;   // [C*K] conv kernel
-  float* v;    // [A]
-  float* h;    // [D]
-  float* red;  // [64]
+// -------------------------------------------------------- attention kernels
+// The location-attention step is spread over (frame chunk, utterance) work
+// groups -- TCH frames each -- instead of one work-group per utterance, so a
+// B = 32 batch at T' = 250 fills 256 work-groups.  The only cross-chunk
+// dependencies of a step are the softmax over T (recomputed per work-group
+// from the [B][T] energies, which costs T flops) and the 201-tap convolution
+// windows (read from the previous kernel's output).  Forward per step:
+//   att_energy  (chunk, b): W_dec h, conv(aw_{t-1}) features, energies, mask, sharpen
+//   att_context (E chunk, b): softmax (or sigmoid) over T, context slice
+// Backward per step:
+//   rgemm            : r = dgates_{t+1} @ Wcat (d [ctx_t; h_t] from step t+1)
+//   att_bwd_daw      (chunk, b): d ctx total, d aw_t = carry + enc . d ctx
+//   att_bwd_energy   (chunk, b): softmax / tanh backward, d enc_a, dF, weight partials
+//   att_bwd_conv     (chunk, b): d aw_{t-1} (conv transpose), conv-kernel partials,
+//                                (chunk 0) dW_dec input sum and d dec
+constexpr int TCH = 32;   // frames per attention work-group
+constexpr int ECH = 64;   // context columns per work-group
+
+inline int att_chunks(const Dims& d) { return (d.T + TCH - 1) / TCH; }
+
+struct EnLds {
+  float* h;     // [D]      dec_out_t
+  float* wd;    // [A]      W_dec h
+  float* cw;    // [C*K]    conv kernel
+  float* wc;    // [A*C]    W_conv
+  float* v;     // [A]
+  float* awin;  // [TCH+K-1] aw_{t-1}[tt0 - K/2 + i] (0 outside [0, T))
+  float* f;     // [TCH*C]  conv features of the chunk
+  float* e;     // [TCH]    d energy (backward)
+  float* awt;   // [T]      aw_t (backward)
+  float* red;   // [64]
 };
 
-__host__ __device__ inline size_t att_lds_floats(const Dims& d) {
-  return (size_t)d.T * (2 + d.C) + (size_t)d.A * (2 + d.C) + (size_t)d.C * d.K + d.D + 64 +
-         (size_t)d.T * d.C /* backward: d_f */ + d.T /* backward: d_aw */ + d.A /* d_wd */;
+__host__ __device__ inline size_t conv_lds_floats(const Dims& d) {
+  return (size_t)d.C * d.K + (size_t)(TCH + d.K - 1) * (d.C + 1) + d.A;
 }
 
-__device__ inline AttLds carve(float* s, const Dims& d) {
-  AttLds L;
-  L.aw = s; s += d.T;
-  L.f = s; s += (size_t)d.T * d.C;
-  L.e = s; s += d.T;
-  L.wd = s; s += d.A;
-  L.wc = s; s += (size_t)d.A * d.C;
-  L.cw = s; s += (size_t)d.C * d.K;
-  L.v = s; s += d.A;
+__host__ __device__ inline size_t en_lds_floats(const Dims& d) {
+  return (size_t)d.D + 2 * d.A + (size_t)d.C * d.K + (size_t)d.A * d.C + (TCH + d.K - 1) +
+         (size_t)TCH * d.C + TCH + d.T + 64;
+}
+
+__device__ inline EnLds carve_en(float* s, const Dims& d) {
+  EnLds L;
   L.h = s; s += d.D;
+  L.wd = s; s += d.A;
+  L.cw = s; s += (size_t)d.C * d.K;
+  L.wc = s; s += (size_t)d.A * d.C;
+  L.v = s; s += d.A;
+  L.awin = s; s += TCH + d.K - 1;
+  L.f = s; s += (size_t)TCH * d.C;
+  L.e = s; s += TCH;
+  L.awt = s; s += d.T;
   L.red = s;
   return L;
 }
@@ -194,176 +235,255 @@ __device__ __forceinline__ float block_reduce(float v, float* red, bool is_max) 
   __syncthreads();
   float r = red[0];
   for (int i = 1; i < nw; ++i) r = is_max ? fmaxf(r, red[i]) : r + red[i];
+  __syncthreads();
   return r;
 }
 
-// Shared prologue of att_fwd / att_bwd: aw_{t-1}, weights, W_dec h, conv features.
-__device__ void att_prologue(int t, const Dims& d, int b, const AttLds& L,
-                             const float* __restrict__ w_dec, const float* __restrict__ w_conv,
-                             const float* __restrict__ conv_w, const float* __restrict__ vw,
-                             const float* __restrict__ dec, const float* __restrict__ aw_all) {
-  const int tid = threadIdx.x, nt = blockDim.x;
-  for (int i = tid; i < d.T; i += nt)
-    L.aw[i] = t > 0 ? aw_all[((long long)b * d.S + t - 1) * d.T + i] : 0.f;
+// Weights, h_t, W_dec h_t, the aw_{t-1} window and the chunk's conv features.
+__device__ void en_prologue(int t, const Dims& d, int b, int tt0, const EnLds& L,
+                            const float* __restrict__ w_dec, const float* __restrict__ w_conv,
+                            const float* __restrict__ conv_w, const float* __restrict__ vw,
+                            const float* __restrict__ dec, const float* __restrict__ aw_all) {
+  const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, w = tid >> 6, nw = nt >> 6;
+  const int half = d.K / 2;
   for (int i = tid; i < d.A * d.C; i += nt) L.wc[i] = w_conv[i];
   for (int i = tid; i < d.C * d.K; i += nt) L.cw[i] = conv_w[i];
   for (int i = tid; i < d.A; i += nt) L.v[i] = vw[i];
   for (int i = tid; i < d.D; i += nt) L.h[i] = dec[((long long)b * d.S + t) * d.D + i];
+  for (int i = tid; i < TCH + d.K - 1; i += nt) {
+    const int tt = tt0 - half + i;
+    L.awin[i] = (t > 0 && tt >= 0 && tt < d.T) ? aw_all[((long long)b * d.S + t - 1) * d.T + tt]
+                                                : 0.f;
+  }
   __syncthreads();
-  for (int a = tid; a < d.A; a += nt) {
+  for (int a = w; a < d.A; a += nw) {   // one wave per attention row, lanes over D
     const float* wr = w_dec + (long long)a * d.D;
     float s = 0.f;
-    for (int k = 0; k < d.D; ++k) s += wr[k] * L.h[k];
-    L.wd[a] = s;
+    for (int k = lane; k < d.D; k += 64) s += wr[k] * L.h[k];
+    s = wave_sum(s);
+    if (lane == 0) L.wd[a] = s;
   }
-  const int half = d.K / 2;
-  for (int i = tid; i < d.T * d.C; i += nt) {
-    const int tt = i / d.C, c = i % d.C;
+  for (int i = tid; i < TCH * d.C; i += nt) {
+    const int fi = i / d.C, c = i % d.C;
     float s = 0.f;
-    const float* cw = L.cw + c * d.K;
-    const int k0 = max(0, half - tt), k1 = min(d.K, d.T + half - tt);
-    for (int k = k0; k < k1; ++k) s += cw[k] * L.aw[tt + k - half];
+    if (tt0 + fi < d.T) {
+      const float* cwr = L.cw + c * d.K;
+      const float* aw = L.awin + fi;        // aw_{t-1}[tt - half + k] = awin[fi + k]
+      for (int k = 0; k < d.K; ++k) s += cwr[k] * aw[k];
+    }
     L.f[i] = s;
   }
   __syncthreads();
 }
 
-__device__ __forceinline__ float att_pre(const Dims& d, const AttLds& L, const float* ea_row,
-                                         int tt, int a) {
-  float p = ea_row[a] + L.wd[a];
-  const float* fr = L.f + tt * d.C;
-  const float* wr = L.wc + a * d.C;
-  for (int c = 0; c < d.C; ++c) p += fr[c] * wr[c];
-  return p;
-}
-
-// -------------------------------------------------------------- attention fwd
-__global__ void __launch_bounds__(ATT_THREADS) att_fwd(
-    int t, Dims d, const float* __restrict__ enc, const float* __restrict__ enc_a,
-    const int32_t* __restrict__ lens, const float* __restrict__ w_dec,
-    const float* __restrict__ w_conv, const float* __restrict__ conv_w,
-    const float* __restrict__ vw, const float* __restrict__ dec, float* __restrict__ aw_all,
-    float* __restrict__ ctx_all, float* __restrict__ x) {
+__global__ void __launch_bounds__(ATT_THREADS) att_energy(
+    int t, Dims d, const float* __restrict__ enc_a, const int32_t* __restrict__ lens,
+    const float* __restrict__ w_dec, const float* __restrict__ w_conv,
+    const float* __restrict__ conv_w, const float* __restrict__ vw, const float* __restrict__ dec,
+    const float* __restrict__ aw_all, float* __restrict__ ebuf) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const Dims dd = d;
-  AttLds L = carve(smem, dd);
-  const int b = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
-  att_prologue(t, dd, b, L, w_dec, w_conv, conv_w, vw, dec, aw_all);
-  // energies: one wave per frame, lanes over the attention dim
-  for (int tt = w; tt < d.T; tt += nw) {
-    const float* ea = enc_a + ((long long)b * d.T + tt) * d.A;
-    float s = 0.f;
-    for (int a = lane; a < d.A; a += 64) s += L.v[a] * tanhf(att_pre(dd, L, ea, tt, a));
-    s = wave_sum(s);
-    if (lane == 0) L.e[tt] = s;
-  }
-  __syncthreads();
+  EnLds L = carve_en(smem, dd);
+  const int b = blockIdx.y, tt0 = blockIdx.x * TCH;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  en_prologue(t, dd, b, tt0, L, w_dec, w_conv, conv_w, vw, dec, aw_all);
   const int len = lens[b];
+  for (int i = w; i < TCH; i += nw) {   // one wave per frame, lanes over the attention dim
+    const int tt = tt0 + i;
+    if (tt >= d.T) break;
+    const float* ea = enc_a + ((long long)b * d.T + tt) * d.A;
+    const float* fr = L.f + i * d.C;
+    float s = 0.f;
+    for (int a = lane; a < d.A; a += 64) {
+      float p = ea[a] + L.wd[a];
+      const float* wr = L.wc + a * d.C;
+      for (int c = 0; c < d.C; ++c) p += fr[c] * wr[c];
+      s += L.v[a] * tanhf(p);
+    }
+    s = wave_sum(s);
+    // multiplicative mask (attention_layer.py:216-225), then sharpening
+    if (lane == 0) ebuf[(long long)b * d.T + tt] = (tt < len ? s : 0.f) * d.sharpen;
+  }
+}
+
+__global__ void __launch_bounds__(ATT_THREADS) att_context(
+    int t, Dims d, const float* __restrict__ enc, const float* __restrict__ ebuf,
+    float* __restrict__ aw_all, float* __restrict__ ctx_all, float* __restrict__ x) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* aw = smem;             // [T]
+  float* red = aw + d.T;        // [64]
+  float* part = red + 64;       // [4][ECH]
+  const int b = blockIdx.y, e0 = blockIdx.x * ECH;
+  const int tid = threadIdx.x;
   float mx = -__builtin_huge_valf();
   for (int i = tid; i < d.T; i += blockDim.x) {
-    float e = (i < len ? L.e[i] : 0.f) * d.sharpen;   // multiplicative mask (:216-225)
-    L.e[i] = e;
+    const float e = ebuf[(long long)b * d.T + i];
+    aw[i] = e;
     mx = fmaxf(mx, e);
   }
   __syncthreads();
   if (d.sigmoid) {
-    for (int i = tid; i < d.T; i += blockDim.x) L.e[i] = sigmoidf_(L.e[i]);
+    for (int i = tid; i < d.T; i += blockDim.x) aw[i] = sigmoidf_(aw[i]);
   } else {
-    mx = block_reduce(mx, L.red, true);
+    mx = block_reduce(mx, red, true);
     float sm = 0.f;
     for (int i = tid; i < d.T; i += blockDim.x) {
-      const float p = __expf(L.e[i] - mx);
-      L.e[i] = p;
+      const float p = __expf(aw[i] - mx);
+      aw[i] = p;
       sm += p;
     }
-    sm = block_reduce(sm, L.red, false);
+    sm = block_reduce(sm, red, false);
     const float inv = 1.f / sm;
-    for (int i = tid; i < d.T; i += blockDim.x) L.e[i] *= inv;
+    for (int i = tid; i < d.T; i += blockDim.x) aw[i] *= inv;
   }
   __syncthreads();
-  for (int i = tid; i < d.T; i += blockDim.x) aw_all[((long long)b * d.S + t) * d.T + i] = L.e[i];
-  const int ED = d.E + d.D;
-  for (int e = tid; e < d.E; e += blockDim.x) {
+  if (blockIdx.x == 0)
+    for (int i = tid; i < d.T; i += blockDim.x) aw_all[((long long)b * d.S + t) * d.T + i] = aw[i];
+  const int col = tid & (ECH - 1), r = tid / ECH, nr = blockDim.x / ECH;
+  const int e = e0 + col;
+  float s = 0.f;
+  if (e < d.E) {
     const float* er = enc + (long long)b * d.T * d.E + e;
-    float s = 0.f;
-    for (int tt = 0; tt < d.T; ++tt) s += L.e[tt] * er[(long long)tt * d.E];
-    ctx_all[((long long)b * d.S + t) * d.E + e] = s;
-    if (t + 1 < d.S) x[((long long)b * d.S + t + 1) * ED + e] = s;
+    for (int tt = r; tt < d.T; tt += nr) s += aw[tt] * er[(long long)tt * d.E];
+  }
+  part[r * ECH + col] = s;
+  __syncthreads();
+  if (r == 0 && e < d.E) {
+    float c = part[col];
+    for (int q = 1; q < nr; ++q) c += part[q * ECH + col];
+    ctx_all[((long long)b * d.S + t) * d.E + e] = c;
+    if (t + 1 < d.S) x[((long long)b * d.S + t + 1) * (d.E + d.D) + e] = c;
   }
 }
 
-// -------------------------------------------------------------- attention bwd
-// d_ctx total for step t = d_ctx_in[b,t] + r[b, 0:E]  (stored into dctx_tot)
-// d_aw_t = carry[b] (from step t+1); writes carry[b] = d aw_{t-1}
-__global__ void __launch_bounds__(ATT_THREADS) att_bwd(
-    int t, Dims d, const float* __restrict__ enc, const float* __restrict__ enc_a,
-    const int32_t* __restrict__ lens, const float* __restrict__ w_dec,
-    const float* __restrict__ w_conv, const float* __restrict__ conv_w,
-    const float* __restrict__ vw, const float* __restrict__ dec,
-    const float* __restrict__ aw_all, const float* __restrict__ dctx_in,
-    const float* __restrict__ r, float* __restrict__ carry, float* __restrict__ dctx_tot,
-    float* __restrict__ d_enc_a, float* __restrict__ ddec_att, float* __restrict__ dwd_all,
-    float* __restrict__ dv_part, float* __restrict__ dwc_part, float* __restrict__ dcw_part) {
+// r[b][n] = sum_g dg[b, t+1, g] * WcatT[n][g]   (n < E + D; 16 columns x 32 rows
+// per work-group, 4 waves split K = 4D; same fragment scheme as cell_fwd)
+template <bool BF16, typename TW>
+__global__ void __launch_bounds__(256) rgemm(int t1, Dims d, const TW* __restrict__ wT,
+                                             const float* __restrict__ dg, float* __restrict__ r,
+                                             int vec) {
+  __shared__ float part[4][MB][16];
+  const int ED = d.E + d.D, G = 4 * d.D;
+  const int n0 = blockIdx.x * 16, b0 = blockIdx.y * MB;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int ra = b0 + (lane & 15), rb = b0 + 16 + (lane & 15);
+  const float* xr0 = ra < d.B ? dg + ((long long)ra * d.S + t1) * G : nullptr;
+  const float* xr1 = rb < d.B ? dg + ((long long)rb * d.S + t1) * G : nullptr;
+  const int n = n0 + (lane & 15);
+  const TW* wr = n < ED ? wT + (long long)n * G : nullptr;
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  if (BF16) {
+    for (int k0 = wave * 32; k0 < G; k0 += 128) {
+      const int k = k0 + 8 * (lane >> 4);
+      const bf16x8 bw = frag8g<TW>(wr, k, G, vec != 0);
+      acc0 = mfma_bf16(frag8g<float>(xr0, k, G, vec != 0), bw, acc0);
+      acc1 = mfma_bf16(frag8g<float>(xr1, k, G, vec != 0), bw, acc1);
+    }
+  } else {
+    for (int k0 = wave * 4; k0 < G; k0 += 16) {
+      const int k = k0 + (lane >> 4);
+      const float bw = (wr && k < G) ? ldw<TW>(wr, k) : 0.f;
+      acc0 = mfma_f32((xr0 && k < G) ? xr0[k] : 0.f, bw, acc0);
+      acc1 = mfma_f32((xr1 && k < G) ? xr1[k] : 0.f, bw, acc1);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    part[wave][4 * (lane >> 4) + q][lane & 15] = acc0[q];
+    part[wave][16 + 4 * (lane >> 4) + q][lane & 15] = acc1[q];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < MB * 16; i += blockDim.x) {
+    const int row = i >> 4, cc = i & 15;
+    const int b = b0 + row, nn = n0 + cc;
+    if (b < d.B && nn < ED)
+      r[(long long)b * ED + nn] = part[0][row][cc] + part[1][row][cc] + part[2][row][cc] +
+                                  part[3][row][cc];
+  }
+}
+
+// d ctx total for step t = d_ctx_in[b,t] + r[b, 0:E] (stored into dctx_tot by chunk 0);
+// d aw_t[tt] = carry[b,tt] (from step t+1) + enc[b,tt,:] . d ctx
+__global__ void __launch_bounds__(ATT_THREADS) att_bwd_daw(
+    int t, Dims d, const float* __restrict__ enc, const float* __restrict__ dctx_in,
+    const float* __restrict__ r, const float* __restrict__ carry, float* __restrict__ dctx_tot,
+    float* __restrict__ dawbuf) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const Dims dd = d;
-  AttLds L = carve(smem, dd);
-  float* dF = L.red + 64;           // [T*C]
-  float* dA = dF + (size_t)d.T * d.C;  // [T]  d aw_t, then d energy
-  float* dWd = dA + d.T;            // [A]
-  const int b = blockIdx.x;
+  float* dct = smem;   // [E]
+  const int b = blockIdx.y, tt0 = blockIdx.x * TCH;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
   const int ED = d.E + d.D;
-  att_prologue(t, dd, b, L, w_dec, w_conv, conv_w, vw, dec, aw_all);
-  const float* awt = aw_all + ((long long)b * d.S + t) * d.T;
-  for (int i = tid; i < d.T; i += blockDim.x) {
-    L.e[i] = awt[i];
-    dA[i] = carry[(long long)b * d.T + i];
+  for (int e = tid; e < d.E; e += blockDim.x) {
+    const float v = dctx_in[((long long)b * d.S + t) * d.E + e] + (r ? r[(long long)b * ED + e] : 0.f);
+    dct[e] = v;
+    if (blockIdx.x == 0) dctx_tot[((long long)b * d.S + t) * d.E + e] = v;
   }
-  // total d_ctx (into LDS-free global buffer, read back below)
-  float* dct = dctx_tot + ((long long)b * d.S + t) * d.E;
-  for (int e = tid; e < d.E; e += blockDim.x)
-    dct[e] = dctx_in[((long long)b * d.S + t) * d.E + e] + (r ? r[(long long)b * ED + e] : 0.f);
-  for (int a = tid; a < d.A; a += blockDim.x) dWd[a] = 0.f;
   __syncthreads();
-  // d aw[tt] += enc[tt,:] . d_ctx   (one wave per frame)
-  for (int tt = w; tt < d.T; tt += nw) {
+  for (int i = w; i < TCH; i += nw) {
+    const int tt = tt0 + i;
+    if (tt >= d.T) break;
     const float* er = enc + ((long long)b * d.T + tt) * d.E;
     float s = 0.f;
     for (int e = lane; e < d.E; e += 64) s += er[e] * dct[e];
     s = wave_sum(s);
-    if (lane == 0) dA[tt] += s;
+    if (lane == 0) dawbuf[(long long)b * d.T + tt] = carry[(long long)b * d.T + tt] + s;
   }
+}
+
+// softmax / sigmoid backward -> d energy; per (frame, a): tanh backward -> d enc_a
+// (utterance-private RMW), dF [B][T][C], and chunk partials of dV, dW_dec-input,
+// dW_conv (fixed-order sums: deterministic).
+__global__ void __launch_bounds__(ATT_THREADS) att_bwd_energy(
+    int t, Dims d, const float* __restrict__ enc_a, const int32_t* __restrict__ lens,
+    const float* __restrict__ w_dec, const float* __restrict__ w_conv,
+    const float* __restrict__ conv_w, const float* __restrict__ vw, const float* __restrict__ dec,
+    const float* __restrict__ aw_all, const float* __restrict__ dawbuf,
+    float* __restrict__ d_enc_a, float* __restrict__ dFbuf, float* __restrict__ dwd_chunk,
+    float* __restrict__ dv_part, float* __restrict__ dwc_part) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const Dims dd = d;
+  EnLds L = carve_en(smem, dd);
+  const int b = blockIdx.y, ch = blockIdx.x, tt0 = ch * TCH, NC = gridDim.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
+  const float* awt = aw_all + ((long long)b * d.S + t) * d.T;
+  const float* daw = dawbuf + (long long)b * d.T;
+  float sdot = 0.f;
+  for (int i = tid; i < d.T; i += blockDim.x) {
+    const float a = awt[i];
+    L.awt[i] = a;
+    sdot += a * daw[i];
+  }
+  if (!d.sigmoid) sdot = block_reduce(sdot, L.red, false);
   __syncthreads();
-  // softmax / sigmoid backward -> d energy (after mask & sharpen)
   const int len = lens[b];
-  if (d.sigmoid) {
-    for (int i = tid; i < d.T; i += blockDim.x) dA[i] = dA[i] * L.e[i] * (1.f - L.e[i]);
-  } else {
-    float s = 0.f;
-    for (int i = tid; i < d.T; i += blockDim.x) s += L.e[i] * dA[i];
-    s = block_reduce(s, L.red, false);
-    for (int i = tid; i < d.T; i += blockDim.x) dA[i] = L.e[i] * (dA[i] - s);
+  for (int i = tid; i < TCH; i += blockDim.x) {
+    const int tt = tt0 + i;
+    float de = 0.f;
+    if (tt < d.T && tt < len) {
+      const float a = L.awt[tt], g = daw[tt];
+      de = (d.sigmoid ? g * a * (1.f - a) : a * (g - sdot)) * d.sharpen;
+    }
+    L.e[i] = de;
   }
-  __syncthreads();
-  for (int i = tid; i < d.T; i += blockDim.x) dA[i] = (i < len ? dA[i] : 0.f) * d.sharpen;
-  for (int i = tid; i < d.T * d.C; i += blockDim.x) dF[i] = 0.f;
-  __syncthreads();
-  // per frame: d_pre[a] = dE * V[a] * (1 - tanh^2); accumulate dV, dWd, dWconv (registers),
-  // d_enc_a (global RMW, utterance-private), d_f (LDS, per (tt, c) over a: wave reduce)
-  float* dvp = dv_part + ((long long)b * d.S + t) * d.A;
-  float* dwcp = dwc_part + ((long long)b * d.S + t) * d.A * d.C;
-  // each lane owns attention rows a = lane, lane+64, ... (<= 4 rows => A <= 256)
+  en_prologue(t, dd, b, tt0, L, w_dec, w_conv, conv_w, vw, dec, aw_all);
   float accV[4] = {0.f, 0.f, 0.f, 0.f}, accWd[4] = {0.f, 0.f, 0.f, 0.f};
   float accWc[4][16];
 #pragma unroll
   for (int q = 0; q < 4; ++q)
 #pragma unroll
     for (int c = 0; c < 16; ++c) accWc[q][c] = 0.f;
-  for (int tt = w; tt < d.T; tt += nw) {
-    const float de = dA[tt];
+  for (int i = w; i < TCH; i += nw) {
+    const int tt = tt0 + i;
+    if (tt >= d.T) break;
+    const float de = L.e[i];
+    float* dfo = dFbuf + ((long long)b * d.T + tt) * d.C;
+    if (de == 0.f) {               // padded / masked frame: nothing flows
+      if (lane < d.C) dfo[lane] = 0.f;
+      continue;
+    }
     const float* ea = enc_a + ((long long)b * d.T + tt) * d.A;
     float* dea = d_enc_a + ((long long)b * d.T + tt) * d.A;
+    const float* fr = L.f + i * d.C;
     float dfc[16];
 #pragma unroll
     for (int c = 0; c < 16; ++c) dfc[c] = 0.f;
@@ -371,13 +491,16 @@ __global__ void __launch_bounds__(ATT_THREADS) att_bwd(
     for (int q = 0; q < 4; ++q) {
       const int a = lane + 64 * q;
       if (a < d.A) {
-        const float th = tanhf(att_pre(dd, L, ea, tt, a));
+        const float* wr = L.wc + a * d.C;
+        float p = ea[a] + L.wd[a];
+#pragma unroll
+        for (int c = 0; c < 16; ++c)
+          if (c < d.C) p += fr[c] * wr[c];
+        const float th = tanhf(p);
         const float dp = de * L.v[a] * (1.f - th * th);
         accV[q] += de * th;
         accWd[q] += dp;
         dea[a] += dp;
-        const float* fr = L.f + tt * d.C;
-        const float* wr = L.wc + a * d.C;
 #pragma unroll
         for (int c = 0; c < 16; ++c)
           if (c < d.C) {
@@ -389,13 +512,16 @@ __global__ void __launch_bounds__(ATT_THREADS) att_bwd(
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
       if (c < d.C) {
-        const float s = wave_sum(dfc[c]);
-        if (lane == 0) dF[tt * d.C + c] = s;
+        const float sv = wave_sum(dfc[c]);
+        if (lane == 0) dfo[c] = sv;
       }
     }
   }
-  // combine the per-wave register partials through LDS (reuse L.f region is still needed: use
-  // atomics on LDS for the small A / A*C partial sums -- order fixed per wave, 4 waves)
+  // combine the per-wave partials in a fixed wave order into this chunk's slots
+  const long long slot = ((long long)b * d.S + t) * NC + ch;
+  float* dvp = dv_part + slot * d.A;
+  float* dwcp = dwc_part + slot * d.A * d.C;
+  float* dwdp = dwd_chunk + ((long long)b * NC + ch) * d.A;
   __syncthreads();
   for (int pass = 0; pass < nw; ++pass) {
     if (w == pass) {
@@ -403,8 +529,8 @@ __global__ void __launch_bounds__(ATT_THREADS) att_bwd(
       for (int q = 0; q < 4; ++q) {
         const int a = lane + 64 * q;
         if (a < d.A) {
-          if (pass == 0) { dvp[a] = accV[q]; dWd[a] = accWd[q]; }
-          else { dvp[a] += accV[q]; dWd[a] += accWd[q]; }
+          if (pass == 0) { dvp[a] = accV[q]; dwdp[a] = accWd[q]; }
+          else { dvp[a] += accV[q]; dwdp[a] += accWd[q]; }
 #pragma unroll
           for (int c = 0; c < 16; ++c)
             if (c < d.C) {
@@ -416,32 +542,70 @@ __global__ void __launch_bounds__(ATT_THREADS) att_bwd(
     }
     __syncthreads();
   }
-  // d W_dec input: ddec_att[b, k] = sum_a W_dec[a, k] dWd[a];  dwd_all[b,t,:] = dWd
-  for (int a = tid; a < d.A; a += blockDim.x) dwd_all[((long long)b * d.S + t) * d.A + a] = dWd[a];
-  for (int k = tid; k < d.D; k += blockDim.x) {
-    float s = 0.f;
-    for (int a = 0; a < d.A; ++a) s += w_dec[(long long)a * d.D + k] * dWd[a];
-    ddec_att[(long long)b * d.D + k] = s;
-  }
-  // conv backward: d aw_{t-1}[j] = sum_c sum_k dF[j - k + half, c] * cw[c, k]
+}
+
+// d aw_{t-1} (conv transpose of dF; written over carry for step t-1), this
+// chunk's conv-kernel partial, and (chunk 0) the dW_dec input sum dwd_all[b,t]
+// and d dec_t from the attention (ddec_att = W_dec^T dWd).
+__global__ void __launch_bounds__(ATT_THREADS) att_bwd_conv(
+    int t, Dims d, const float* __restrict__ conv_w, const float* __restrict__ aw_all,
+    const float* __restrict__ dFbuf, const float* __restrict__ w_dec,
+    const float* __restrict__ dwd_chunk, float* __restrict__ carry, float* __restrict__ dcw_part,
+    float* __restrict__ dwd_all, float* __restrict__ ddec_att) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int W = TCH + d.K - 1;
+  float* cw = smem;                        // [C*K]
+  float* dFw = cw + d.C * d.K;             // [W][C] rows j0 - half ..
+  float* awin = dFw + (size_t)W * d.C;     // [W]   aw_{t-1}[j0 - half + i]
+  float* dWd = awin + W;                   // [A]
+  const int b = blockIdx.y, ch = blockIdx.x, j0 = ch * TCH, NC = gridDim.x;
+  const int tid = threadIdx.x, nt = blockDim.x;
   const int half = d.K / 2;
-  for (int j = tid; j < d.T; j += blockDim.x) {
+  for (int i = tid; i < d.C * d.K; i += nt) cw[i] = conv_w[i];
+  for (int i = tid; i < W * d.C; i += nt) {
+    const int row = j0 - half + i / d.C;
+    dFw[i] = (row >= 0 && row < d.T) ? dFbuf[((long long)b * d.T + row) * d.C + i % d.C] : 0.f;
+  }
+  for (int i = tid; i < W; i += nt) {
+    const int tt = j0 - half + i;
+    awin[i] = (t > 0 && tt >= 0 && tt < d.T) ? aw_all[((long long)b * d.S + t - 1) * d.T + tt]
+                                             : 0.f;
+  }
+  __syncthreads();
+  // d aw_{t-1}[j] = sum_c sum_k dF[j - k + half, c] cw[c, k]; window row of j - k + half
+  // is (j - j0) + (K - 1) - k
+  for (int jj = tid; jj < TCH; jj += nt) {
+    const int j = j0 + jj;
+    if (j >= d.T) break;
     float s = 0.f;
     for (int c = 0; c < d.C; ++c) {
-      const float* cw = L.cw + c * d.K;
-      const int k0 = max(0, j + half - (d.T - 1)), k1 = min(d.K, j + half + 1);
-      for (int k = k0; k < k1; ++k) s += dF[(j - k + half) * d.C + c] * cw[k];
+      const float* cwr = cw + c * d.K;
+      const float* dfr = dFw + (size_t)(jj + d.K - 1) * d.C + c;
+      for (int k = 0; k < d.K; ++k) s += dfr[-(long long)k * d.C] * cwr[k];
     }
     carry[(long long)b * d.T + j] = s;
   }
-  // d conv kernel partial: dcw[c, k] = sum_tt dF[tt, c] * aw_{t-1}[tt + k - half]
-  float* dcwp = dcw_part + ((long long)b * d.S + t) * d.C * d.K;
-  for (int i = tid; i < d.C * d.K; i += blockDim.x) {
+  // conv-kernel partial: dcw[c, k] = sum_{tt in chunk} dF[tt, c] aw_{t-1}[tt + k - half]
+  float* dcwp = dcw_part + (((long long)b * d.S + t) * NC + ch) * d.C * d.K;
+  const int nrow = min(TCH, d.T - j0);
+  for (int i = tid; i < d.C * d.K; i += nt) {
     const int c = i / d.K, k = i % d.K;
-    const int t0 = max(0, half - k), t1 = min(d.T, d.T + half - k);
     float s = 0.f;
-    for (int tt = t0; tt < t1; ++tt) s += dF[tt * d.C + c] * L.aw[tt + k - half];
+    for (int q = 0; q < nrow; ++q) s += dFw[(size_t)(q + half) * d.C + c] * awin[q + k];
     dcwp[i] = s;
+  }
+  if (ch != 0) return;
+  for (int a = tid; a < d.A; a += nt) {
+    float s = 0.f;
+    for (int q = 0; q < NC; ++q) s += dwd_chunk[((long long)b * NC + q) * d.A + a];
+    dWd[a] = s;
+    dwd_all[((long long)b * d.S + t) * d.A + a] = s;
+  }
+  __syncthreads();
+  for (int k = tid; k < d.D; k += nt) {
+    float s = 0.f;
+    for (int a = 0; a < d.A; ++a) s += w_dec[(long long)a * d.D + k] * dWd[a];
+    ddec_att[(long long)b * d.D + k] = s;
   }
 }
 
@@ -582,9 +746,35 @@ int check_dims(const Dims& d) {
               "attdec: attention_dim <= 256 and conv channels <= 16 supported (A=%d C=%d)", d.A,
               d.C);
   ASR_REQUIRE(d.K % 2 == 1, ASR_ERR_ARG, "attdec: conv width must be odd");
-  ASR_REQUIRE(att_lds_floats(d) * 4 <= 160 * 1024, ASR_ERR_UNSUPPORTED,
-              "attdec: LDS need %zu B > 160 KiB", att_lds_floats(d) * 4);
+  ASR_REQUIRE(en_lds_floats(d) * 4 <= 160 * 1024 && conv_lds_floats(d) * 4 <= 160 * 1024 &&
+                  ((size_t)d.T + 64 + 4 * ECH) * 4 <= 160 * 1024,
+              ASR_ERR_UNSUPPORTED, "attdec: LDS need %zu B > 160 KiB", en_lds_floats(d) * 4);
   return ASR_OK;
+}
+
+size_t al256(size_t n) { return (n + 255) & ~size_t(255); }
+
+// Workspace: [Wcat (fwd) or Wcat^T (bwd)][energies / d aw [B][T]] and, backward
+// only, [r][carry][ddec_att][dc][flags][dF [B][T][C]][dWd chunk partials].
+struct AttWs {
+  size_t wcat, ebuf, r, carry, ddec, dc, flags, dF, dwdc, total;
+};
+AttWs att_ws(const Dims& d, int cdt, bool bwd) {
+  AttWs w;
+  size_t o = 0;
+  w.wcat = o; o += wcat_bytes(d, cdt);
+  w.ebuf = o; o += al256((size_t)d.B * d.T * 4);
+  if (bwd) {
+    w.r = o; o += al256((size_t)d.B * (d.E + d.D) * 4);
+    w.carry = o; o += al256((size_t)d.B * d.T * 4);
+    w.ddec = o; o += al256((size_t)d.B * d.D * 4);
+    w.dc = o; o += al256((size_t)d.B * d.D * 4);
+    w.flags = o; o += al256((size_t)d.S * 4);
+    w.dF = o; o += al256((size_t)d.B * d.T * d.C * 4);
+    w.dwdc = o; o += al256((size_t)d.B * att_chunks(d) * d.A * 4);
+  }
+  w.total = o;
+  return w;
 }
 
 }  // namespace
@@ -594,16 +784,13 @@ using namespace asr;
 
 extern "C" size_t asr_attdec_workspace_bytes(const asr_attdec_dims_t* dims, int compute_dtype,
                                              int backward) {
-  const Dims d = to_dims(*dims);
-  size_t n = wcat_bytes(d, compute_dtype);
-  if (backward) {
-    n += ((size_t)d.B * (d.E + d.D) * 4 + 255) & ~size_t(255);  // r
-    n += ((size_t)d.B * d.T * 4 + 255) & ~size_t(255);          // carry
-    n += ((size_t)d.B * d.D * 4 + 255) & ~size_t(255);          // ddec_att
-    n += ((size_t)d.B * d.D * 4 + 255) & ~size_t(255);          // dc
-    n += ((size_t)d.S * 4 + 255) & ~size_t(255);                // sampled-step flags
-  }
-  return n;
+  return att_ws(to_dims(*dims), compute_dtype, backward != 0).total;
+}
+
+// Attention frame chunks per utterance: the backward partials dv_part,
+// dwc_part and dcw_part hold B * S * chunks rows.
+extern "C" int asr_attdec_chunks(const asr_attdec_dims_t* dims) {
+  return att_chunks(to_dims(*dims));
 }
 
 namespace {
@@ -673,7 +860,11 @@ extern "C" int asr_attdec_forward_ex(const asr_attdec_dims_t* dims, const asr_at
   ASR_LAUNCH_CHECK();
   hipLaunchKernelGGL(dec_init, dim3(d.B), dim3(256), 0, s, d, h0, dec, x, c_all, gates);
   ASR_LAUNCH_CHECK();
-  const size_t lds = att_lds_floats(d) * 4;
+  const AttWs W = att_ws(d, compute_dtype, false);
+  float* ebuf = (float*)((char*)workspace + W.ebuf);
+  const size_t en_lds = en_lds_floats(d) * 4;
+  const size_t cx_lds = ((size_t)d.T + 64 + 4 * ECH) * 4;
+  const dim3 eg(att_chunks(d), d.B), xg(ceil_div(d.E, ECH), d.B);
   const int vec = ((d.E + d.D) % 8 == 0) ? 1 : 0;
   const dim3 cg(ceil_div(d.D, CU), ceil_div(d.B, MB));
   const size_t ss_lds = ss ? ((size_t)d.D + d.E + opts->Dz + opts->Y + 2 * (SS_THREADS / 64)) * 4
@@ -698,8 +889,11 @@ extern "C" int asr_attdec_forward_ex(const asr_attdec_dims_t* dims, const asr_at
                            seed_h);
       ASR_LAUNCH_CHECK();
     }
-    hipLaunchKernelGGL(att_fwd, dim3(d.B), dim3(ATT_THREADS), lds, s, t, d, enc, enc_a, lens,
-                       w_dec, w_conv, conv_w, v, dec, aw_all, ctx_all, x);
+    hipLaunchKernelGGL(att_energy, eg, dim3(ATT_THREADS), en_lds, s, t, d, enc_a, lens, w_dec,
+                       w_conv, conv_w, v, dec, aw_all, ebuf);
+    ASR_LAUNCH_CHECK();
+    hipLaunchKernelGGL(att_context, xg, dim3(ATT_THREADS), cx_lds, s, t, d, enc, ebuf, aw_all,
+                       ctx_all, x);
     ASR_LAUNCH_CHECK();
   }
   return ASR_OK;
@@ -752,58 +946,58 @@ extern "C" int asr_attdec_backward_ex(const asr_attdec_dims_t* dims, const asr_a
   hipStream_t s = (hipStream_t)stream;
   const bool bf = compute_dtype == ASR_DT_BF16;
   const int ED = d.E + d.D, G = 4 * d.D;
+  const AttWs W = att_ws(d, compute_dtype, true);
   char* p = (char*)workspace;
-  void* wcat = p;
-  p += wcat_bytes(d, compute_dtype);
-  float* r = (float*)p;
-  p += ((size_t)d.B * ED * 4 + 255) & ~size_t(255);
-  float* carry = (float*)p;
-  p += ((size_t)d.B * d.T * 4 + 255) & ~size_t(255);
-  float* ddec_att = (float*)p;
-  p += ((size_t)d.B * d.D * 4 + 255) & ~size_t(255);
-  float* dc = (float*)p;
-  p += ((size_t)d.B * d.D * 4 + 255) & ~size_t(255);
-  int32_t* flags = (int32_t*)p;
+  void* wcatT = p + W.wcat;
+  float* dawbuf = (float*)(p + W.ebuf);
+  float* r = (float*)(p + W.r);
+  float* carry = (float*)(p + W.carry);
+  float* ddec_att = (float*)(p + W.ddec);
+  float* dc = (float*)(p + W.dc);
+  int32_t* flags = (int32_t*)(p + W.flags);
+  float* dFbuf = (float*)(p + W.dF);
+  float* dwd_chunk = (float*)(p + W.dwdc);
   const long long nw = 4LL * d.D * ED;
   const int gb = (int)((nw + 255) / 256 < 4096 ? (nw + 255) / 256 : 4096);
   if (bf)
-    hipLaunchKernelGGL((build_wcat<uint16_t>), dim3(gb), dim3(256), 0, s, d, w_ih_ctx, ld_ih, w_hh,
-                       (uint16_t*)wcat);
+    hipLaunchKernelGGL((build_wcat_t<uint16_t>), dim3(gb), dim3(256), 0, s, d, w_ih_ctx, ld_ih,
+                       w_hh, (uint16_t*)wcatT);
   else
-    hipLaunchKernelGGL((build_wcat<float>), dim3(gb), dim3(256), 0, s, d, w_ih_ctx, ld_ih, w_hh,
-                       (float*)wcat);
+    hipLaunchKernelGGL((build_wcat_t<float>), dim3(gb), dim3(256), 0, s, d, w_ih_ctx, ld_ih, w_hh,
+                       (float*)wcatT);
   ASR_LAUNCH_CHECK();
   ASR_CHECK_HIP(hipMemsetAsync(carry, 0, (size_t)d.B * d.T * 4, s));
   ASR_CHECK_HIP(hipMemsetAsync(dc, 0, (size_t)d.B * d.D * 4, s));
   ASR_CHECK_HIP(hipMemsetAsync(d_enc_a, 0, (size_t)d.B * d.T * d.A * 4, s));
-  const size_t lds = att_lds_floats(d) * 4;
+  const size_t en_lds = en_lds_floats(d) * 4;
+  const size_t cv_lds = conv_lds_floats(d) * 4;
+  const size_t dw_lds = (size_t)d.E * 4;
+  const dim3 eg(att_chunks(d), d.B);
+  const dim3 rg(ceil_div(ED, 16), ceil_div(d.B, MB));
+  const int vec = (G % 8 == 0) ? 1 : 0;
   const long long nbd = (long long)d.B * d.D;
   const int cgrid = (int)((nbd + 255) / 256);
   for (int t = d.S - 1; t >= 0; --t) {
     const float* rp = nullptr;
-    if (t + 1 < d.S) {
-      // r = dgates_{t+1} (B x 4D, row stride S*4D) @ Wcat (4D x ED)
-      asr_gemm_t g;
-      memset(&g, 0, sizeof(g));
-      g.a.ptr = gates_dg + (long long)(t + 1) * G;
-      g.a.dtype = ASR_DT_F32;
-      g.a.trans = 0;
-      g.a.map.stride_t = (long long)d.S * G;
-      g.b.ptr = wcat;
-      g.b.dtype = bf ? ASR_DT_BF16 : ASR_DT_F32;
-      g.b.trans = 1;
-      g.b.map.stride_t = ED;
-      g.c = r;
-      g.c_map.stride_t = ED;
-      g.M = d.B; g.N = ED; g.K = G;
-      g.alpha = 1.f; g.beta = 0.f; g.batch = 1;
-      rc = asr_gemm(&g, 1, compute_dtype, stream);
-      if (rc) return rc;
+    if (t + 1 < d.S) {   // r = dgates_{t+1} @ Wcat: d [ctx_t; h_t] through step t+1's cell
+      if (bf)
+        hipLaunchKernelGGL((rgemm<true, uint16_t>), rg, dim3(256), 0, s, t + 1, d,
+                           (const uint16_t*)wcatT, gates_dg, r, vec);
+      else
+        hipLaunchKernelGGL((rgemm<false, float>), rg, dim3(256), 0, s, t + 1, d,
+                           (const float*)wcatT, gates_dg, r, vec);
+      ASR_LAUNCH_CHECK();
       rp = r;
     }
-    hipLaunchKernelGGL(att_bwd, dim3(d.B), dim3(ATT_THREADS), lds, s, t, d, enc, enc_a, lens,
-                       w_dec, w_conv, conv_w, v, dec, aw_all, d_ctx_in, rp, carry, dctx_tot,
-                       d_enc_a, ddec_att, dwd_all, dv_part, dwc_part, dcw_part);
+    hipLaunchKernelGGL(att_bwd_daw, eg, dim3(ATT_THREADS), dw_lds, s, t, d, enc, d_ctx_in, rp,
+                       carry, dctx_tot, dawbuf);
+    ASR_LAUNCH_CHECK();
+    hipLaunchKernelGGL(att_bwd_energy, eg, dim3(ATT_THREADS), en_lds, s, t, d, enc_a, lens, w_dec,
+                       w_conv, conv_w, v, dec, aw_all, dawbuf, d_enc_a, dFbuf, dwd_chunk, dv_part,
+                       dwc_part);
+    ASR_LAUNCH_CHECK();
+    hipLaunchKernelGGL(att_bwd_conv, eg, dim3(ATT_THREADS), cv_lds, s, t, d, conv_w, aw_all, dFbuf,
+                       w_dec, dwd_chunk, carry, dcw_part, dwd_all, ddec_att);
     ASR_LAUNCH_CHECK();
     hipLaunchKernelGGL(cell_bwd, dim3(cgrid), dim3(256), 0, s, t, d, d_dec_in, rp, ddec_att,
                        gates_dg, c_all, dc, d_h0, drop_h, seed_h);

@@ -302,9 +302,10 @@ class AttDecoderFn(torch.autograd.Function):
         d_enc_a = torch.empty(B, T, A, **f32)
         d_h0 = torch.empty(B, D, **f32) if has_h0 else None
         dwd = torch.empty(B, S, A, **f32)
-        dv_part = torch.empty(B * S, A, **f32)
-        dwc_part = torch.empty(B * S, A * C, **f32)
-        dcw_part = torch.empty(B * S, C * K, **f32)
+        nrow = B * S * N.query('asr_attdec_chunks', ctypes.byref(dims))   # per frame chunk
+        dv_part = torch.empty(nrow, A, **f32)
+        dwc_part = torch.empty(nrow, A * C, **f32)
+        dcw_part = torch.empty(nrow, C * K, **f32)
         nb = N.query('asr_attdec_workspace_bytes', ctypes.byref(dims), cd, 1)
         ws = _ws(nb, dev)
         ld_ih = w_ih.shape[1]

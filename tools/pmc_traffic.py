@@ -3,7 +3,8 @@
 Usage (on the GPU box, one pass per counter group, never combined with tracing):
     rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -- python3 bench.py ...
     rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -- python3 bench.py ...
-    python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write > profiles/rNN_pmc_traffic.json
+    python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write <workload> \
+        > profiles/rNN_pmc_traffic.json
 
 Corrections applied (MI355X_MICROARCH.md §HBM): FETCH_SIZE and WRITE_SIZE are
 KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide coalesced read, so it
@@ -54,7 +55,7 @@ def read_counter(d, counter):
     return out
 
 
-def main(fetch_dir, write_dir):
+def main(fetch_dir, write_dir, workload):
     fetch = read_counter(fetch_dir, 'FETCH_SIZE')
     write = read_counter(write_dir, 'WRITE_SIZE')
     res = {}
@@ -67,6 +68,7 @@ def main(fetch_dir, write_dir):
         res[fam] = {'launches_fetch': len(f), 'launches_write': len(w),
                     'fetch_bytes_per_launch': int(fb), 'write_bytes_per_launch': int(wb),
                     'traffic_bytes_per_launch': int(fb + wb)}
+    res['_workload'] = workload
     res['_method'] = ('rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), KiB '
                       'converted to bytes, FETCH_SIZE x2 (gfx950 correction, '
                       'MI355X_MICROARCH.md HBM section)')
@@ -75,4 +77,5 @@ def main(fetch_dir, write_dir):
 
 
 if __name__ == '__main__':
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else
+         'librispeech100h_char_ctc_blstm5x512')
