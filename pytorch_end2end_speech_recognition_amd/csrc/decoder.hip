@@ -204,7 +204,7 @@ struct EnLds {
 };
 
 __host__ __device__ inline size_t conv_lds_floats(const Dims& d) {
-  return (size_t)d.C * d.K + (size_t)(TCH + d.K - 1) * (d.C + 1) + d.A;
+  return (size_t)d.C * d.K + (size_t)(TCH + d.K - 1) * (d.C + 1) + d.A + (size_t)TCH * d.C;
 }
 
 __host__ __device__ inline size_t en_lds_floats(const Dims& d) {
@@ -244,7 +244,7 @@ __device__ void en_prologue(int t, const Dims& d, int b, int tt0, const EnLds& L
                             const float* __restrict__ w_dec, const float* __restrict__ w_conv,
                             const float* __restrict__ conv_w, const float* __restrict__ vw,
                             const float* __restrict__ dec, const float* __restrict__ aw_all) {
-  const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, w = tid >> 6, nw = nt >> 6;
+  const int tid = threadIdx.x, nt = blockDim.x;
   const int half = d.K / 2;
   for (int i = tid; i < d.A * d.C; i += nt) L.wc[i] = w_conv[i];
   for (int i = tid; i < d.C * d.K; i += nt) L.cw[i] = conv_w[i];
@@ -256,12 +256,20 @@ __device__ void en_prologue(int t, const Dims& d, int b, int tt0, const EnLds& L
                                                 : 0.f;
   }
   __syncthreads();
-  for (int a = w; a < d.A; a += nw) {   // one wave per attention row, lanes over D
+  for (int a = tid; a < d.A; a += nt) {  // one thread per attention row: independent loads
     const float* wr = w_dec + (long long)a * d.D;
-    float s = 0.f;
-    for (int k = lane; k < d.D; k += 64) s += wr[k] * L.h[k];
-    s = wave_sum(s);
-    if (lane == 0) L.wd[a] = s;
+    float s0 = 0.f, s1 = 0.f;
+    int k = 0;
+    if ((d.D & 3) == 0) {
+      for (; k + 8 <= d.D; k += 8) {
+        const float4 u = *reinterpret_cast<const float4*>(wr + k);
+        const float4 q = *reinterpret_cast<const float4*>(wr + k + 4);
+        s0 += u.x * L.h[k] + u.y * L.h[k + 1] + u.z * L.h[k + 2] + u.w * L.h[k + 3];
+        s1 += q.x * L.h[k + 4] + q.y * L.h[k + 5] + q.z * L.h[k + 6] + q.w * L.h[k + 7];
+      }
+    }
+    for (; k < d.D; ++k) s0 += wr[k] * L.h[k];
+    L.wd[a] = s0 + s1;
   }
   for (int i = tid; i < TCH * d.C; i += nt) {
     const int fi = i / d.C, c = i % d.C;
@@ -288,17 +296,37 @@ __global__ void __launch_bounds__(ATT_THREADS) att_energy(
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
   en_prologue(t, dd, b, tt0, L, w_dec, w_conv, conv_w, vw, dec, aw_all);
   const int len = lens[b];
-  for (int i = w; i < TCH; i += nw) {   // one wave per frame, lanes over the attention dim
+  // one wave per frame, lanes over the attention dim (a = lane + 64 q, A <= 256);
+  // the next frame's enc_a row is loaded before this frame's math
+  float ean[4];
+  auto load_ea = [&](int i) {
+    const int tt = tt0 + i;
+    const float* ea = enc_a + ((long long)b * d.T + tt) * d.A;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int a = lane + 64 * q;
+      ean[q] = (i < TCH && tt < d.T && a < d.A) ? ea[a] : 0.f;
+    }
+  };
+  load_ea(w);
+  for (int i = w; i < TCH; i += nw) {
     const int tt = tt0 + i;
     if (tt >= d.T) break;
-    const float* ea = enc_a + ((long long)b * d.T + tt) * d.A;
+    float eac[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) eac[q] = ean[q];
+    load_ea(i + nw);
     const float* fr = L.f + i * d.C;
     float s = 0.f;
-    for (int a = lane; a < d.A; a += 64) {
-      float p = ea[a] + L.wd[a];
-      const float* wr = L.wc + a * d.C;
-      for (int c = 0; c < d.C; ++c) p += fr[c] * wr[c];
-      s += L.v[a] * tanhf(p);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int a = lane + 64 * q;
+      if (a < d.A) {
+        float p = eac[q] + L.wd[a];
+        const float* wr = L.wc + a * d.C;
+        for (int c = 0; c < d.C; ++c) p += fr[c] * wr[c];
+        s += L.v[a] * tanhf(p);
+      }
     }
     s = wave_sum(s);
     // multiplicative mask (attention_layer.py:216-225), then sharpening
@@ -419,14 +447,25 @@ __global__ void __launch_bounds__(ATT_THREADS) att_bwd_daw(
     if (blockIdx.x == 0) dctx_tot[((long long)b * d.S + t) * d.E + e] = v;
   }
   __syncthreads();
-  for (int i = w; i < TCH; i += nw) {
-    const int tt = tt0 + i;
-    if (tt >= d.T) break;
-    const float* er = enc + ((long long)b * d.T + tt) * d.E;
-    float s = 0.f;
-    for (int e = lane; e < d.E; e += 64) s += er[e] * dct[e];
-    s = wave_sum(s);
-    if (lane == 0) dawbuf[(long long)b * d.T + tt] = carry[(long long)b * d.T + tt] + s;
+  constexpr int FB = 4;   // frames in flight per wave
+  for (int i0 = w * FB; i0 < TCH; i0 += nw * FB) {
+    float s[FB];
+#pragma unroll
+    for (int f = 0; f < FB; ++f) {
+      const int tt = tt0 + i0 + f;
+      s[f] = 0.f;
+      if (i0 + f < TCH && tt < d.T) {
+        const float* er = enc + ((long long)b * d.T + tt) * d.E;
+        for (int e = lane; e < d.E; e += 64) s[f] += er[e] * dct[e];
+      }
+    }
+#pragma unroll
+    for (int f = 0; f < FB; ++f) {
+      const int tt = tt0 + i0 + f;
+      const float v = wave_sum(s[f]);
+      if (lane == 0 && i0 + f < TCH && tt < d.T)
+        dawbuf[(long long)b * d.T + tt] = carry[(long long)b * d.T + tt] + v;
+    }
   }
 }
 
@@ -472,16 +511,36 @@ __global__ void __launch_bounds__(ATT_THREADS) att_bwd_energy(
   for (int q = 0; q < 4; ++q)
 #pragma unroll
     for (int c = 0; c < 16; ++c) accWc[q][c] = 0.f;
+  // the next frame's enc_a / d_enc_a rows are loaded before this frame's math
+  float ean[4], dean[4];
+  auto load_rows = [&](int i) {
+    const int tt = tt0 + i;
+    const bool ok = i < TCH && tt < d.T && L.e[i] != 0.f;
+    const long long ro = ((long long)b * d.T + tt) * d.A;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int a = lane + 64 * q;
+      ean[q] = (ok && a < d.A) ? enc_a[ro + a] : 0.f;
+      dean[q] = (ok && a < d.A) ? d_enc_a[ro + a] : 0.f;
+    }
+  };
+  load_rows(w);
   for (int i = w; i < TCH; i += nw) {
     const int tt = tt0 + i;
     if (tt >= d.T) break;
     const float de = L.e[i];
+    float eac[4], deac[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      eac[q] = ean[q];
+      deac[q] = dean[q];
+    }
+    load_rows(i + nw);
     float* dfo = dFbuf + ((long long)b * d.T + tt) * d.C;
     if (de == 0.f) {               // padded / masked frame: nothing flows
       if (lane < d.C) dfo[lane] = 0.f;
       continue;
     }
-    const float* ea = enc_a + ((long long)b * d.T + tt) * d.A;
     float* dea = d_enc_a + ((long long)b * d.T + tt) * d.A;
     const float* fr = L.f + i * d.C;
     float dfc[16];
@@ -492,7 +551,7 @@ __global__ void __launch_bounds__(ATT_THREADS) att_bwd_energy(
       const int a = lane + 64 * q;
       if (a < d.A) {
         const float* wr = L.wc + a * d.C;
-        float p = ea[a] + L.wd[a];
+        float p = eac[q] + L.wd[a];
 #pragma unroll
         for (int c = 0; c < 16; ++c)
           if (c < d.C) p += fr[c] * wr[c];
@@ -500,7 +559,7 @@ __global__ void __launch_bounds__(ATT_THREADS) att_bwd_energy(
         const float dp = de * L.v[a] * (1.f - th * th);
         accV[q] += de * th;
         accWd[q] += dp;
-        dea[a] += dp;
+        dea[a] = deac[q] + dp;
 #pragma unroll
         for (int c = 0; c < 16; ++c)
           if (c < d.C) {
@@ -558,6 +617,7 @@ __global__ void __launch_bounds__(ATT_THREADS) att_bwd_conv(
   float* dFw = cw + d.C * d.K;             // [W][C] rows j0 - half ..
   float* awin = dFw + (size_t)W * d.C;     // [W]   aw_{t-1}[j0 - half + i]
   float* dWd = awin + W;                   // [A]
+  float* cpart = dWd + d.A;                // [TCH][C]
   const int b = blockIdx.y, ch = blockIdx.x, j0 = ch * TCH, NC = gridDim.x;
   const int tid = threadIdx.x, nt = blockDim.x;
   const int half = d.K / 2;
@@ -574,15 +634,22 @@ __global__ void __launch_bounds__(ATT_THREADS) att_bwd_conv(
   __syncthreads();
   // d aw_{t-1}[j] = sum_c sum_k dF[j - k + half, c] cw[c, k]; window row of j - k + half
   // is (j - j0) + (K - 1) - k
-  for (int jj = tid; jj < TCH; jj += nt) {
-    const int j = j0 + jj;
-    if (j >= d.T) break;
+  for (int i = tid; i < TCH * d.C; i += nt) {   // one thread per (frame, channel)
+    const int jj = i / d.C, c = i % d.C;
     float s = 0.f;
-    for (int c = 0; c < d.C; ++c) {
+    if (j0 + jj < d.T) {
       const float* cwr = cw + c * d.K;
       const float* dfr = dFw + (size_t)(jj + d.K - 1) * d.C + c;
       for (int k = 0; k < d.K; ++k) s += dfr[-(long long)k * d.C] * cwr[k];
     }
+    cpart[i] = s;
+  }
+  __syncthreads();
+  for (int jj = tid; jj < TCH; jj += nt) {
+    const int j = j0 + jj;
+    if (j >= d.T) break;
+    float s = 0.f;
+    for (int c = 0; c < d.C; ++c) s += cpart[jj * d.C + c];
     carry[(long long)b * d.T + j] = s;
   }
   // conv-kernel partial: dcw[c, k] = sum_{tt in chunk} dF[tt, c] aw_{t-1}[tt + k - half]
