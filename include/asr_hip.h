@@ -232,6 +232,12 @@ int asr_embedding_forward(const long long* idx, const float* weight, int n, int 
                           int trans, float* out, void* stream);
 int asr_embedding_backward(const long long* idx, const float* dout, int n, int V, int E,
                            int trans, int padding_idx, float* grad_weight, void* stream);
+/* The embedding gradient with the rows grouped by token (CSR built on the host
+ * from the label array the caller already holds: rows order[starts[v] ..
+ * starts[v+1]) carry token v in ascending order).  Same sums, O(n E). */
+int asr_embedding_backward_csr(const int32_t* order, const int32_t* starts, const float* dout,
+                               int V, int E, int trans, int padding_idx, float* grad_weight,
+                               void* stream);
 int asr_tanh_forward(const float* x, float* y, long long n, void* stream);
 int asr_tanh_backward(const float* y, const float* dy, float* dx, long long n, void* stream);
 /* y = tanh(a + b) (attention bottleneck with per-branch dropout,

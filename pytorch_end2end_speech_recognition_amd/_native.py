@@ -61,6 +61,8 @@ SIGNATURES = {
     'asr_embedding_forward': (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp]),
     'asr_embedding_backward': (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp,
                                        c_vp]),
+    'asr_embedding_backward_csr': (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp,
+                                           c_vp]),
     'asr_tanh_forward': (c_int, [c_vp, c_vp, c_ll, c_vp]),
     'asr_tanh_backward': (c_int, [c_vp, c_vp, c_vp, c_ll, c_vp]),
     'asr_add_tanh_forward': (c_int, [c_vp, c_vp, c_vp, c_ll, c_vp]),

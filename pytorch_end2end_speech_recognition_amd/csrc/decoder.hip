@@ -201,6 +201,7 @@ struct EnLds {
   float* e;     // [TCH]    d energy (backward)
   float* awt;   // [T]      aw_t (backward)
   float* red;   // [64]
+  float* cmb;   // [2A + A*C] wave-combine of the backward partials
 };
 
 __host__ __device__ inline size_t conv_lds_floats(const Dims& d) {
@@ -209,7 +210,7 @@ __host__ __device__ inline size_t conv_lds_floats(const Dims& d) {
 
 __host__ __device__ inline size_t en_lds_floats(const Dims& d) {
   return (size_t)d.D + 2 * d.A + (size_t)d.C * d.K + (size_t)d.A * d.C + (TCH + d.K - 1) +
-         (size_t)TCH * d.C + TCH + d.T + 64;
+         (size_t)TCH * d.C + TCH + d.T + 64 + 2 * d.A + (size_t)d.A * d.C;
 }
 
 __device__ inline EnLds carve_en(float* s, const Dims& d) {
@@ -223,7 +224,8 @@ __device__ inline EnLds carve_en(float* s, const Dims& d) {
   L.f = s; s += (size_t)TCH * d.C;
   L.e = s; s += TCH;
   L.awt = s; s += d.T;
-  L.red = s;
+  L.red = s; s += 64;
+  L.cmb = s;
   return L;
 }
 
@@ -243,7 +245,8 @@ __device__ __forceinline__ float block_reduce(float v, float* red, bool is_max) 
 __device__ void en_prologue(int t, const Dims& d, int b, int tt0, const EnLds& L,
                             const float* __restrict__ w_dec, const float* __restrict__ w_conv,
                             const float* __restrict__ conv_w, const float* __restrict__ vw,
-                            const float* __restrict__ dec, const float* __restrict__ aw_all) {
+                            const float* __restrict__ dec, const float* __restrict__ aw_all,
+                            const float* __restrict__ wd_pre = nullptr) {
   const int tid = threadIdx.x, nt = blockDim.x;
   const int half = d.K / 2;
   for (int i = tid; i < d.A * d.C; i += nt) L.wc[i] = w_conv[i];
@@ -256,7 +259,10 @@ __device__ void en_prologue(int t, const Dims& d, int b, int tt0, const EnLds& L
                                                 : 0.f;
   }
   __syncthreads();
-  for (int a = tid; a < d.A; a += nt) {  // one thread per attention row: independent loads
+  if (wd_pre) {   // backward: W_dec h_t of every step from one GEMM before the loop
+    for (int a = tid; a < d.A; a += nt) L.wd[a] = wd_pre[((long long)b * d.S + t) * d.A + a];
+  }
+  for (int a = tid; a < d.A && !wd_pre; a += nt) {  // one thread per attention row
     const float* wr = w_dec + (long long)a * d.D;
     float s0 = 0.f, s1 = 0.f;
     int k = 0;
@@ -477,8 +483,8 @@ __global__ void __launch_bounds__(ATT_THREADS) att_bwd_energy(
     const float* __restrict__ w_dec, const float* __restrict__ w_conv,
     const float* __restrict__ conv_w, const float* __restrict__ vw, const float* __restrict__ dec,
     const float* __restrict__ aw_all, const float* __restrict__ dawbuf,
-    float* __restrict__ d_enc_a, float* __restrict__ dFbuf, float* __restrict__ dwd_chunk,
-    float* __restrict__ dv_part, float* __restrict__ dwc_part) {
+    const float* __restrict__ wd_all, float* __restrict__ d_enc_a, float* __restrict__ dFbuf,
+    float* __restrict__ dwd_chunk, float* __restrict__ dv_part, float* __restrict__ dwc_part) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const Dims dd = d;
   EnLds L = carve_en(smem, dd);
@@ -504,7 +510,7 @@ __global__ void __launch_bounds__(ATT_THREADS) att_bwd_energy(
     }
     L.e[i] = de;
   }
-  en_prologue(t, dd, b, tt0, L, w_dec, w_conv, conv_w, vw, dec, aw_all);
+  en_prologue(t, dd, b, tt0, L, w_dec, w_conv, conv_w, vw, dec, aw_all, wd_all);
   float accV[4] = {0.f, 0.f, 0.f, 0.f}, accWd[4] = {0.f, 0.f, 0.f, 0.f};
   float accWc[4][16];
 #pragma unroll
@@ -576,31 +582,36 @@ __global__ void __launch_bounds__(ATT_THREADS) att_bwd_energy(
       }
     }
   }
-  // combine the per-wave partials in a fixed wave order into this chunk's slots
+  // combine the per-wave partials in LDS in a fixed wave order, then one store
+  // of this chunk's slots
   const long long slot = ((long long)b * d.S + t) * NC + ch;
-  float* dvp = dv_part + slot * d.A;
-  float* dwcp = dwc_part + slot * d.A * d.C;
-  float* dwdp = dwd_chunk + ((long long)b * NC + ch) * d.A;
-  __syncthreads();
+  float* cV = L.cmb;                  // [A]
+  float* cWd = cV + d.A;              // [A]
+  float* cWc = cWd + d.A;             // [A*C]
   for (int pass = 0; pass < nw; ++pass) {
     if (w == pass) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int a = lane + 64 * q;
         if (a < d.A) {
-          if (pass == 0) { dvp[a] = accV[q]; dwdp[a] = accWd[q]; }
-          else { dvp[a] += accV[q]; dwdp[a] += accWd[q]; }
+          cV[a] = pass ? cV[a] + accV[q] : accV[q];
+          cWd[a] = pass ? cWd[a] + accWd[q] : accWd[q];
 #pragma unroll
           for (int c = 0; c < 16; ++c)
-            if (c < d.C) {
-              if (pass == 0) dwcp[a * d.C + c] = accWc[q][c];
-              else dwcp[a * d.C + c] += accWc[q][c];
-            }
+            if (c < d.C) cWc[a * d.C + c] = pass ? cWc[a * d.C + c] + accWc[q][c] : accWc[q][c];
         }
       }
     }
     __syncthreads();
   }
+  float* dvp = dv_part + slot * d.A;
+  float* dwcp = dwc_part + slot * d.A * d.C;
+  float* dwdp = dwd_chunk + ((long long)b * NC + ch) * d.A;
+  for (int i = tid; i < d.A; i += blockDim.x) {
+    dvp[i] = cV[i];
+    dwdp[i] = cWd[i];
+  }
+  for (int i = tid; i < d.A * d.C; i += blockDim.x) dwcp[i] = cWc[i];
 }
 
 // d aw_{t-1} (conv transpose of dF; written over carry for step t-1), this
@@ -824,7 +835,7 @@ size_t al256(size_t n) { return (n + 255) & ~size_t(255); }
 // Workspace: [Wcat (fwd) or Wcat^T (bwd)][energies / d aw [B][T]] and, backward
 // only, [r][carry][ddec_att][dc][flags][dF [B][T][C]][dWd chunk partials].
 struct AttWs {
-  size_t wcat, ebuf, r, carry, ddec, dc, flags, dF, dwdc, total;
+  size_t wcat, ebuf, r, carry, ddec, dc, flags, dF, dwdc, wd, total;
 };
 AttWs att_ws(const Dims& d, int cdt, bool bwd) {
   AttWs w;
@@ -839,6 +850,7 @@ AttWs att_ws(const Dims& d, int cdt, bool bwd) {
     w.flags = o; o += al256((size_t)d.S * 4);
     w.dF = o; o += al256((size_t)d.B * d.T * d.C * 4);
     w.dwdc = o; o += al256((size_t)d.B * att_chunks(d) * d.A * 4);
+    w.wd = o; o += al256((size_t)d.B * d.S * d.A * 4);
   }
   w.total = o;
   return w;
@@ -1024,6 +1036,23 @@ extern "C" int asr_attdec_backward_ex(const asr_attdec_dims_t* dims, const asr_a
   int32_t* flags = (int32_t*)(p + W.flags);
   float* dFbuf = (float*)(p + W.dF);
   float* dwd_chunk = (float*)(p + W.dwdc);
+  float* wd_all = (float*)(p + W.wd);
+  {  // W_dec dec_t for every step at once (exact-f32 MFMA, as the forward's f32 dot products)
+    asr_gemm_t g;
+    memset(&g, 0, sizeof(g));
+    g.a.ptr = dec;
+    g.a.dtype = ASR_DT_F32;
+    g.a.map.stride_t = d.D;
+    g.b.ptr = w_dec;
+    g.b.dtype = ASR_DT_F32;
+    g.b.map.stride_t = d.D;
+    g.c = wd_all;
+    g.c_map.stride_t = d.A;
+    g.M = d.B * d.S; g.N = d.A; g.K = d.D;
+    g.alpha = 1.f; g.beta = 0.f; g.batch = 1;
+    rc = asr_gemm(&g, 1, ASR_DT_F32, stream);
+    if (rc) return rc;
+  }
   const long long nw = 4LL * d.D * ED;
   const int gb = (int)((nw + 255) / 256 < 4096 ? (nw + 255) / 256 : 4096);
   if (bf)
@@ -1060,8 +1089,8 @@ extern "C" int asr_attdec_backward_ex(const asr_attdec_dims_t* dims, const asr_a
                        carry, dctx_tot, dawbuf);
     ASR_LAUNCH_CHECK();
     hipLaunchKernelGGL(att_bwd_energy, eg, dim3(ATT_THREADS), en_lds, s, t, d, enc_a, lens, w_dec,
-                       w_conv, conv_w, v, dec, aw_all, dawbuf, d_enc_a, dFbuf, dwd_chunk, dv_part,
-                       dwc_part);
+                       w_conv, conv_w, v, dec, aw_all, dawbuf, wd_all, d_enc_a, dFbuf, dwd_chunk,
+                       dv_part, dwc_part);
     ASR_LAUNCH_CHECK();
     hipLaunchKernelGGL(att_bwd_conv, eg, dim3(ATT_THREADS), cv_lds, s, t, d, conv_w, aw_all, dFbuf,
                        w_dec, dwd_chunk, carry, dcw_part, dwd_all, ddec_att);

@@ -45,6 +45,25 @@ __global__ void embedding_bwd(const long long* __restrict__ idx, const float* __
   }
 }
 
+// Same sum with the rows grouped by token on the host (CSR: rows order[starts[v]
+// .. starts[v+1]) hold token v, ascending): one work-group per token, O(n E)
+// total, same fixed summation order.
+__global__ void embedding_bwd_csr(const int32_t* __restrict__ order,
+                                  const int32_t* __restrict__ starts,
+                                  const float* __restrict__ dout, int V, int E, int trans,
+                                  int padding_idx, float* __restrict__ gw) {
+  const int v = blockIdx.x;
+  if (v == padding_idx) return;
+  const int j0 = starts[v], j1 = starts[v + 1];
+  if (j0 == j1) return;
+  for (int e = threadIdx.x; e < E; e += blockDim.x) {
+    float s = 0.f;
+    for (int j = j0; j < j1; ++j) s += dout[(long long)order[j] * E + e];
+    if (trans) gw[(long long)e * V + v] += s;
+    else gw[(long long)v * E + e] += s;
+  }
+}
+
 __global__ void tanh_fwd(const float* __restrict__ x, float* __restrict__ y, long long n) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x)
@@ -142,6 +161,18 @@ extern "C" int asr_embedding_backward(const long long* idx, const float* dout, i
   if (n <= 0) return ASR_OK;
   hipLaunchKernelGGL(embedding_bwd, dim3(grid_for((long long)V * E)), dim3(256), 0,
                      (hipStream_t)stream, idx, dout, n, V, E, trans, padding_idx, grad_weight);
+  ASR_LAUNCH_CHECK();
+  return ASR_OK;
+}
+
+extern "C" int asr_embedding_backward_csr(const int32_t* order, const int32_t* starts,
+                                          const float* dout, int V, int E, int trans,
+                                          int padding_idx, float* grad_weight, void* stream) {
+  ASR_REQUIRE(order && starts && dout && grad_weight, ASR_ERR_ARG,
+              "embedding_backward_csr: null pointer");
+  if (V <= 0 || E <= 0) return ASR_OK;
+  hipLaunchKernelGGL(embedding_bwd_csr, dim3(V), dim3(64), 0, (hipStream_t)stream, order, starts,
+                     dout, V, E, trans, padding_idx, grad_weight);
   ASR_LAUNCH_CHECK();
   return ASR_OK;
 }

@@ -586,8 +586,8 @@ int fill_operand(const asr_operand_t& o, Operand* op, const char* name) {
 }
 
 // Split-K plan (pure function of the shapes): a launch with fewer than two
-// waves of 128x128 tiles over 256 CUs and K >= 4096 is split into ~1024 work
-// groups, each K chunk >= 1024 (a multiple of BK).
+// waves of 128x128 tiles over 256 CUs and K >= 1024 is split into ~1024 work
+// groups, each K chunk >= 128 (a multiple of the fast path's k-tile).
 struct SplitPlan {
   int ksplit[2], kchunk[2];
   size_t slab_off[2];
@@ -601,8 +601,10 @@ SplitPlan plan_split(const asr_gemm_t* g, int nprob) {
     // a few-tile dW next to a many-tile dX still gets its own K split
     const int tiles = ceil_div(g[i].M, BM) * ceil_div(g[i].N, BN);
     int ks = 1;
-    if (g[i].batch <= 1 && tiles > 0 && tiles < 512 && g[i].K >= 4096) {
-      ks = min(ceil_div(1024, tiles), g[i].K / 1024);
+    if (g[i].batch <= 1 && tiles > 0 && tiles < 512 && g[i].K >= 1024) {
+      // a few-tile, long-K product (the decoder / projection weight gradients,
+      // K = B*S or B*T) is latency-bound per work-group: chunks >= 128
+      ks = min(ceil_div(1024, tiles), g[i].K / 128);
       const long long mn = (long long)g[i].M * g[i].N;
       while (ks > 1 && (long long)ks * mn * 4 > (64LL << 20)) --ks;  // slab <= 64 MB
       ks = max(ks, 1);

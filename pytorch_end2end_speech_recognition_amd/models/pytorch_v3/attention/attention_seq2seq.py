@@ -192,6 +192,7 @@ class AttentionSeq2seq(ModelBase):
         ys_in[:, 1:] = np.where(pos[:, :-1] < y_lens[:, None], ys, self.eos_0)
         ys_in, ys_out = ys_in[perm], ys_out[perm]
 
+        self._ys_in_host = ys_in          # host copy: token-grouped embedding gradient
         loss = self.compute_xe_loss(enc_out, self.np2var(ys_in), self.np2var(ys_out), enc_lens_d,
                                     None, task=0, dir='fwd', weight=self.fwd_weight_0)
         if self.ctc_loss_weight > 0:
@@ -270,7 +271,10 @@ class AttentionSeq2seq(ModelBase):
         S = ys.shape[1]
         h0 = self._init_h0(enc_out)
         enc_a = att.W_enc_head0(enc_out)                          # one GEMM for all frames
-        y_emb = self.embed_0(ys)                                  # [B, S, emb] (+ dropout)
+        ys_host, self._ys_in_host = getattr(self, '_ys_in_host', None), None   # one use only
+        if ys_host is not None and tuple(ys_host.shape) != tuple(ys.shape):
+            ys_host = None
+        y_emb = self.embed_0(ys, ys_host)                         # [B, S, emb] (+ dropout)
         pre_emb = ops.linear_ex(y_emb, cell.weight_ih, cell.bias_ih, cell.bias_hh, c0=0,
                                 K=self.embedding_dim)             # all steps' input projection
         p_h = self.dropout_decoder if self.training else 0.0

@@ -35,8 +35,8 @@ class Embedding(nn.Module):
         self.padding_idx = self.embed.padding_idx
         self.dropout_p = float(dropout)
 
-    def forward(self, y):
-        e = ops.embedding(y, self.embed.weight, self.padding_idx)
+    def forward(self, y, y_host=None):
+        e = ops.embedding(y, self.embed.weight, self.padding_idx, idx_host=y_host)
         if self.training and self.dropout_p > 0:
             e = ops.dropout(e, self.dropout_p)
         return e
@@ -54,8 +54,8 @@ class Embedding_LS(nn.Module):
         self.label_smoothing_prob = label_smoothing_prob
         self.embed = LinearND(num_classes, embedding_dim, bias=False, dropout=dropout)
 
-    def forward(self, y):
-        e = ops.embedding_t(y, self.embed.fc.weight)
+    def forward(self, y, y_host=None):
+        e = ops.embedding_t(y, self.embed.fc.weight, idx_host=y_host)
         if self.training and self.embed.dropout_p > 0:
             e = ops.dropout(e, self.embed.dropout_p)
         return e

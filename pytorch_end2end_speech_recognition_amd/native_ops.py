@@ -691,10 +691,12 @@ def tanh(x):
 
 
 class EmbeddingFn(torch.autograd.Function):
-    """trans=0: weight [V, E] (nn.Embedding); trans=1: weight [E, V] (Embedding_LS)."""
+    """trans=0: weight [V, E] (nn.Embedding); trans=1: weight [E, V] (Embedding_LS).
+    idx_host (optional numpy copy of idx): the backward groups rows by token on
+    the host (CSR) instead of scanning every row per (token, column)."""
 
     @staticmethod
-    def forward(ctx, idx, weight, trans, padding_idx):
+    def forward(ctx, idx, weight, trans, padding_idx, idx_host=None):
         N.require_device(idx, weight)
         idx = idx.contiguous().long()
         V, E = (weight.shape[1], weight.shape[0]) if trans else weight.shape
@@ -702,31 +704,39 @@ class EmbeddingFn(torch.autograd.Function):
         N.call('asr_embedding_forward', N.ptr(idx), N.ptr(weight), idx.numel(), V, E, int(trans),
                N.ptr(out), N.stream_handle(idx.device))
         ctx.save_for_backward(idx, weight)
-        ctx.meta = (trans, padding_idx, V, E)
+        ctx.meta = (trans, padding_idx, V, E, idx_host)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         idx, weight = ctx.saved_tensors
-        trans, padding_idx, V, E = ctx.meta
+        trans, padding_idx, V, E, idx_host = ctx.meta
         dout = dout.contiguous()
-        N.call('asr_embedding_backward', N.ptr(idx), N.ptr(dout), idx.numel(), V, E, int(trans),
-               -1 if padding_idx is None else int(padding_idx), N.ptr(grad_buffer(weight)),
-               N.stream_handle(idx.device))
-        return None, None, None, None
+        pad = -1 if padding_idx is None else int(padding_idx)
+        if idx_host is not None:
+            flat = np.clip(np.asarray(idx_host, np.int64).reshape(-1), 0, V - 1)
+            order = np.argsort(flat, kind='stable').astype(np.int32)
+            starts = np.zeros(V + 1, np.int32)
+            np.cumsum(np.bincount(flat, minlength=V), out=starts[1:])
+            dev = idx.device
+            order_d = torch.from_numpy(order).to(dev, non_blocking=True)
+            starts_d = torch.from_numpy(starts).to(dev, non_blocking=True)
+            N.call('asr_embedding_backward_csr', N.ptr(order_d), N.ptr(starts_d), N.ptr(dout), V,
+                   E, int(trans), pad, N.ptr(grad_buffer(weight)), N.stream_handle(dev))
+        else:
+            N.call('asr_embedding_backward', N.ptr(idx), N.ptr(dout), idx.numel(), V, E,
+                   int(trans), pad, N.ptr(grad_buffer(weight)), N.stream_handle(idx.device))
+        return None, None, None, None, None
 
 
-def embedding(idx, weight, padding_idx=None):
-    return EmbeddingFn.apply(idx, weight, 0, padding_idx)
+def embedding(idx, weight, padding_idx=None, idx_host=None):
+    return EmbeddingFn.apply(idx, weight, 0, padding_idx, idx_host)
 
 
-def embedding_t(idx, weight_ev):
-    return EmbeddingFn.apply(idx, weight_ev, 1, None)
+def embedding_t(idx, weight_ev, idx_host=None):
+    return EmbeddingFn.apply(idx, weight_ev, 1, None, idx_host)
 
 
-# ---------------------------------------------------------------------------
-# CTC (warp-ctc replacement; models/pytorch_v3/ctc/ctc.py:30-66)
-# ---------------------------------------------------------------------------
 class CTCLossFn(torch.autograd.Function):
     """loss = loss_scale * sum_b CTC(logits_b, labels_b); logits [B, T, V] f32
     batch-major (no time-major transpose copy).  The gradient is produced in
