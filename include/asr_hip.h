@@ -126,6 +126,15 @@ typedef struct {
    * extents < 2 GiB let bf16 operands use the range-checked buffer-load path
    * (out-of-range and masked rows read as zeros straight into LDS). */
   long long bytes;
+  /* 3x3 "tap" addressing (implicit-GEMM convolution over a zero-haloed
+   * [rows = padded pixels][channels] layout), 0 = off.  The contiguous index x
+   * (k for trans=0, the output index for trans=1) splits into tap = x /
+   * tap_group and x' = x % tap_group; the element is read at column x' of row
+   * r + tap_sign * ((tap / 3 - 1) * tap_pitch + tap % 3 - 1).  Needs
+   * tap_group % 16 == 0 (trans=0) or % 8 == 0 (trans=1). */
+  int tap_group;
+  int tap_pitch;
+  int tap_sign;
 } asr_operand_t;
 
 typedef struct {
@@ -399,6 +408,56 @@ int asr_attdec_backward_ex(const asr_attdec_dims_t* dims, const asr_attdec_opts_
                            float* d_enc_a, float* d_h0, float* dwd_all, float* dv_part,
                            float* dwc_part, float* dcw_part, void* workspace, size_t ws_bytes,
                            void* stream);
+
+/* ------------------------------------------------------------- VGG front-end
+ * Replaces CNNEncoder (models/pytorch_v3/encoders/cnn.py:124-165): Conv2d 3x3
+ * (padding 1) -> ReLU -> MaxPool (first floor mode, later ceil) -> BatchNorm2d
+ * -> Dropout per layer, input viewed [B, 1, F, T] (cnn.py:143-149), output
+ * [B, T', F'*C] (cnn.py:155-157).  Layer tensors are channels-last with a zero
+ * halo: [B][T+2][F+2][C] ("padded pixels").  Layers with C_in >= 16 run the
+ * 3x3 convolution as one asr_gemm with tap addressing (asr_operand_t);
+ * C_in = 1 (and channel counts that are not multiples of 16) use
+ * asr_conv_direct_*.
+ * asr_vgg_pool_dims: output extent of a pool (kernel = stride), torch's
+ *   floor / ceil rules.
+ * asr_vgg_block_forward / _backward: ReLU + pool + BatchNorm (training batch
+ *   statistics over every (b, f, t) incl. padding frames, running stats with
+ *   momentum / unbiased variance; or eval with running stats) + dropout (asr
+ *   dropout RNG, index = element of [B][T'][F'][C]).  See cnn.hip. */
+int asr_vgg_pad_input(const float* xs, int B, int T, int F, float* out, void* stream);
+/* GEMM images of a Conv2d weight W [Co][Ci][3][3] (tap j = kw*3 + kh):
+ * mode 0 out[co][j*Ci + ci] (forward B operand), mode 1 out[ci][j*Co + co]
+ * (input-gradient B operand); unpack_acc: dW [Co][Ci][3][3] += [Co][9 Ci]. */
+int asr_conv_weight_pack(const float* w, int Co, int Ci, int mode, int out_dtype, void* out,
+                         void* stream);
+int asr_conv_weight_unpack_acc(const float* packed, int Co, int Ci, float* dw, void* stream);
+/* Direct 3x3 convolution (layers the tap-addressed GEMM cannot take: C_in = 1,
+ * channel counts not multiples of 16): x [padded pixels][Ci] f32, w the torch
+ * weight [Co][Ci][3][3]; z / dx over valid pixels; dw / dbias accumulate. */
+int asr_conv_direct_forward(const float* x, int B, int T, int F, int Ci, int Co, const float* w,
+                            const float* bias, float* z, void* stream);
+int asr_conv_direct_dgrad(const float* dz, int B, int T, int F, int Ci, int Co, const float* w,
+                          float* dx, void* stream);
+size_t asr_conv_direct_wgrad_workspace_bytes(int B, int T, int F, int Ci, int Co);
+int asr_conv_direct_wgrad(const float* x, const float* dz, int B, int T, int F, int Ci, int Co,
+                          float* dw, float* dbias, void* workspace, size_t ws_bytes,
+                          void* stream);
+int asr_vgg_accumulate(const float* a, float* dst, int n, const float* a2, float* dst2, int n2,
+                       void* stream);
+int asr_vgg_pool_dims(int T, int F, int pt, int pf, int ceil_mode, int* To, int* Fo);
+size_t asr_vgg_block_workspace_bytes(int B, int To, int Fo, int C);
+int asr_vgg_block_forward(const float* z, int B, int T, int F, int C, int pt, int pf,
+                          int ceil_mode, float* P, uint8_t* slot, const float* gamma,
+                          const float* beta, float* run_mean, float* run_var, int training,
+                          float momentum, float eps, float* bn_mean, float* bn_rstd, float drop,
+                          unsigned long long seed, void* out, int out_dtype, int flat,
+                          void* workspace, size_t ws_bytes, void* stream);
+int asr_vgg_block_backward(const float* dnext, int flat, const float* z, int B, int T, int F,
+                           int C, int pt, int pf, int ceil_mode, const float* P,
+                           const uint8_t* slot, const float* gamma, const float* bn_mean,
+                           const float* bn_rstd, float* dgamma, float* dbeta, float drop,
+                           unsigned long long seed, void* dz, int dz_dtype, void* workspace,
+                           size_t ws_bytes, void* stream);
 
 /* ----------------------------------------------------------- profiling
  * Sampled HIP-event timing of the recurrence step kernels on their own stream

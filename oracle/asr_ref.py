@@ -38,18 +38,59 @@ def lstm_direction(x, lens, w_ih, w_hh, b_ih, b_hh, reverse):
     return torch.stack(outs, dim=1)
 
 
+def vgg_front(p, prefix, cfg, xs, x_lens, masks=None, training=True):
+    """CNNEncoder.forward (encoders/cnn.py:124-165) with relu, 3x3 / stride 1 /
+    padding 1 convs, max-pool (first floor mode, later ceil mode), BatchNorm2d
+    in training mode (batch statistics; running stats returned, not written)
+    and optional replayed dropout masks (masks[l]: [B, T', F', C] scales).
+    Returns (out [B, T', F'*C], lens np.int64 via ConvOutSize's floor rule
+    (cnn_utils.py:25-37), running-stat updates {name: tensor})."""
+    Fn = torch.nn.functional
+    x = xs.transpose(1, 2).unsqueeze(1)                       # [B, 1, F, T] (cnn.py:143-149)
+    lens = np.asarray(x_lens).astype(np.int64)
+    idx, first_pool, stats = 0, True, {}
+    for l, C in enumerate(cfg['conv_channels']):
+        conv = '%sconv.layers.%d.' % (prefix, idx)
+        x = Fn.conv2d(x, p[conv + 'weight'], p.get(conv + 'bias'), stride=1, padding=1)
+        idx += 2                                              # conv, relu
+        x = torch.relu(x)
+        pl = cfg['poolings'][l]
+        if len(pl):
+            x = Fn.max_pool2d(x, kernel_size=tuple(pl), stride=tuple(pl),
+                              ceil_mode=not first_pool)
+            lens = np.floor((lens - pl[1]) / pl[1] + 1).astype(np.int64)
+            first_pool = False
+            idx += 1
+        if cfg.get('batch_norm'):
+            bn = '%sconv.layers.%d.' % (prefix, idx)
+            rm = p[bn + 'running_mean'].clone()
+            rv = p[bn + 'running_var'].clone()
+            x = Fn.batch_norm(x, rm, rv, p[bn + 'weight'], p[bn + 'bias'], training=training,
+                              momentum=0.1, eps=1e-5)
+            stats[bn + 'running_mean'], stats[bn + 'running_var'] = rm, rv
+            idx += 1
+        if masks is not None:
+            x = x * torch.from_numpy(masks[l]).permute(0, 3, 2, 1)   # [B,T',F',C] -> NCHW
+        idx += 1                                              # dropout
+    B, C, Fo, To = x.shape
+    return x.transpose(1, 3).reshape(B, To, Fo * C), lens, stats
+
+
 def blstm_encoder(p, prefix, cfg, xs, x_lens):
     """RNNEncoder.forward (rnn.py:284-487) for rnn_type='lstm', bidirectional,
-    subsample_type 'drop', no projection / residual / conv (dropout = 0).
+    subsample_type 'drop', no projection / residual, optional VGG front-end
+    (cfg['conv_channels'], rnn.py:314-316), dropout = 0.
 
     Returns (out [B, T', 2H], out_lens np.int32 [B], perm np.int64 [B])."""
     x_lens = np.asarray(x_lens)
+    if cfg.get('conv_channels'):
+        xs, x_lens, _ = vgg_front(p, prefix, cfg, xs, x_lens)
     perm = np.argsort(-x_lens, kind='stable')                 # rnn.py:319-326
     xs = xs[torch.as_tensor(perm)]
     lens = x_lens[perm].astype(np.int64)
     n_layers = cfg['num_layers']
     sub = cfg.get('subsample_list') or [False] * n_layers
-    fast = sum(sub) == 0
+    fast = sum(sub) == 0 and not cfg.get('batch_norm')       # rnn.py:162
     for l in range(n_layers):
         if fast:   # one multi-layer nn.LSTM: lstm.weight_ih_l{l}{_reverse}
             names = [prefix + 'lstm.%s_l%d%s' % (n, l, s) for s in ('', '_reverse')

@@ -86,6 +86,27 @@ SIGNATURES = {
                               [c_size, c_vp]),
     'asr_attdec_backward_ex': (c_int, [c_vp, c_vp, c_int] + [c_vp] * 4 + [c_ll] + [c_vp] * 19 +
                                [c_size, c_vp]),
+    'asr_vgg_pad_input': (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp]),
+    'asr_conv_weight_pack': (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp]),
+    'asr_conv_weight_unpack_acc': (c_int, [c_vp, c_int, c_int, c_vp, c_vp]),
+    'asr_conv_direct_forward': (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp,
+                                        c_vp, c_vp]),
+    'asr_conv_direct_dgrad': (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp,
+                                      c_vp]),
+    'asr_conv_direct_wgrad_workspace_bytes': (c_size, [c_int, c_int, c_int, c_int, c_int]),
+    'asr_conv_direct_wgrad': (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp,
+                                      c_vp, c_size, c_vp]),
+    'asr_vgg_accumulate': (c_int, [c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_vp]),
+    'asr_vgg_pool_dims': (c_int, [c_int, c_int, c_int, c_int, c_int, c_vp, c_vp]),
+    'asr_vgg_block_workspace_bytes': (c_size, [c_int, c_int, c_int, c_int]),
+    'asr_vgg_block_forward': (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                      c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_float, c_float,
+                                      c_vp, c_vp, c_float, ctypes.c_ulonglong, c_vp, c_int, c_int,
+                                      c_vp, c_size, c_vp]),
+    'asr_vgg_block_backward': (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int,
+                                       c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                       c_float, ctypes.c_ulonglong, c_vp, c_int, c_vp, c_size,
+                                       c_vp]),
     'asr_prof_begin': (c_int, [c_int]),
     'asr_prof_end': (c_int, [c_vp, c_vp, c_vp, c_int]),
     'asr_lstm_persist_status': (c_int, [c_vp, c_int, c_vp]),
@@ -106,7 +127,7 @@ SIGNATURES['asr_convert_rows_bf16'] = (c_int, [c_vp, RowMap, c_int, c_int, c_vp,
 class Operand(ctypes.Structure):
     """asr_operand_t"""
     _fields_ = [('ptr', c_vp), ('dtype', c_int), ('trans', c_int), ('map', RowMap),
-                ('bytes', c_ll)]
+                ('bytes', c_ll), ('tap_group', c_int), ('tap_pitch', c_int), ('tap_sign', c_int)]
 
 
 class AttDecDims(ctypes.Structure):

@@ -1,0 +1,631 @@
+// VGG front-end of the encoder (models/pytorch_v3/encoders/cnn.py:124-165) on
+// gfx950: per layer Conv2d 3x3 (stride 1, padding 1) -> ReLU -> MaxPool
+// (kernel = stride; the first pool floor mode, later ones ceil mode) ->
+// BatchNorm2d (training: batch statistics over every (b, f, t), padding frames
+// included, as the reference computes them) -> Dropout.
+//
+// Layout: the reference's NCHW view [B, C, F, T] (cnn.py:143-149) is kept
+// channels-last and zero-haloed: a layer input is [B][T+2][F+2][C] ("padded
+// pixels" x channels), so a 3x3 tap is a constant row shift of
+// (dt)*(F+2) + df and the convolution is ONE implicit GEMM on the MFMA kernels
+// of gemm.hip (asr_operand_t tap addressing): M = padded pixels, N = C_out,
+// K = 9 C_in.  Rows of halo pixels are computed and ignored.  Layers whose
+// channel counts the tap addressing cannot take (the first layer, C_in = 1)
+// use direct kernels.  This file holds the bandwidth-bound
+// pieces around the GEMMs:
+//   vgg_pad_input   xs [B][T][F] -> [B][T+2][F+2] (zero halo)
+//   conv_direct_*   3x3 conv without the GEMM (C_in = 1, small channel counts)
+//   post_fwd        ReLU + max-pool -> P [B][T'][F'][C], argmax slot per output
+//   bn stats        per-channel mean / inverse std over P (two passes, fixed order)
+//   apply_fwd       BN affine + dropout -> next layer's padded input (f32 or
+//                   bf16) or the encoder input [B][T'][F'*C] (cnn.py:155-157)
+//   bwd             dropout, BN backward (sum dy, sum dy xhat), pool + ReLU
+//                   routing into dZ [padded pixels][C] (halo zero)
+#include "mfma.h"
+
+namespace asr {
+namespace {
+
+constexpr int CT = 256;
+
+__device__ __forceinline__ long long pad_row(int b, int t, int f, int T, int F) {
+  return ((long long)b * (T + 2) + (t + 1)) * (F + 2) + (f + 1);
+}
+
+__global__ void vgg_pad_input(const float* __restrict__ xs, int B, int T, int F,
+                              float* __restrict__ out) {
+  const long long n = (long long)B * (T + 2) * (F + 2);
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int fp = (int)(i % (F + 2));
+    const long long q = i / (F + 2);
+    const int tp = (int)(q % (T + 2));
+    const int b = (int)(q / (T + 2));
+    const int t = tp - 1, f = fp - 1;
+    out[i] = (t >= 0 && t < T && f >= 0 && f < F) ? xs[((long long)b * T + t) * F + f] : 0.f;
+  }
+}
+
+// Direct 3x3 convolution for layers whose channel counts do not suit the
+// tap-addressed GEMM (C_in = 1 of the first layer, small test configs).
+// x [padded pixels][Ci] f32, w the torch weight [Co][Ci][3(f)][3(t)].
+// z[p][co] = sum_{ci,kh,kw} w[co][ci][kh][kw] x[p + (kw-1)(F+2) + kh-1][ci] (+ bias),
+// valid pixels only.
+__global__ void conv_direct_fwd(const float* __restrict__ x, int B, int T, int F, int Ci, int Co,
+                                const float* __restrict__ w, const float* __restrict__ bias,
+                                float* __restrict__ z) {
+  const long long n = (long long)B * T * F * Co;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int co = (int)(i % Co);
+    const long long pix = i / Co;
+    const int f = (int)(pix % F);
+    const int t = (int)((pix / F) % T);
+    const int b = (int)(pix / ((long long)F * T));
+    const long long p = pad_row(b, t, f, T, F);
+    float s = bias ? bias[co] : 0.f;
+    for (int ci = 0; ci < Ci; ++ci) {
+      const float* wr = w + ((long long)co * Ci + ci) * 9;
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw)
+          s += wr[kh * 3 + kw] * x[(p + (long long)(kw - 1) * (F + 2) + (kh - 1)) * Ci + ci];
+    }
+    z[p * Co + co] = s;
+  }
+}
+
+// dx[p][ci] = sum_{co,kh,kw} dz[p - shift][co] w[co][ci][kh][kw] (dz halo rows zero)
+__global__ void conv_direct_dgrad(const float* __restrict__ dz, int B, int T, int F, int Ci,
+                                  int Co, const float* __restrict__ w, float* __restrict__ dx) {
+  const long long n = (long long)B * T * F * Ci;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int ci = (int)(i % Ci);
+    const long long pix = i / Ci;
+    const int f = (int)(pix % F);
+    const int t = (int)((pix / F) % T);
+    const int b = (int)(pix / ((long long)F * T));
+    const long long p = pad_row(b, t, f, T, F);
+    float s = 0.f;
+    for (int co = 0; co < Co; ++co) {
+      const float* wr = w + ((long long)co * Ci + ci) * 9;
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw)
+          s += wr[kh * 3 + kw] * dz[(p - (long long)(kw - 1) * (F + 2) - (kh - 1)) * Co + co];
+    }
+    dx[p * Ci + ci] = s;
+  }
+}
+
+// partial[chunk][(co*Ci + ci)*9 + kh*3 + kw] = sum over the chunk's valid pixels of
+// dz[p][co] x[p + shift][ci]; partial[chunk][Co*Ci*9 + co] = sum dz (bias).
+__global__ void conv_direct_wgrad(const float* __restrict__ x, const float* __restrict__ dz,
+                                  int B, int T, int F, int Ci, int Co, int pix_per_chunk,
+                                  float* __restrict__ partial) {
+  const long long npix = (long long)B * T * F;
+  const long long p0 = (long long)blockIdx.x * pix_per_chunk;
+  const long long p1 = min(npix, p0 + pix_per_chunk);
+  const int nw = Co * Ci * 9, nout = nw + Co;
+  for (int o = threadIdx.x; o < nout; o += blockDim.x) {
+    const bool isb = o >= nw;
+    const int co = isb ? o - nw : o / (Ci * 9);
+    const int ci = isb ? 0 : (o / 9) % Ci, tap = isb ? 0 : o % 9;
+    const int kh = tap / 3, kw = tap % 3;
+    float s = 0.f;
+    for (long long q = p0; q < p1; ++q) {
+      const int f = (int)(q % F);
+      const int t = (int)((q / F) % T);
+      const int b = (int)(q / ((long long)F * T));
+      const long long p = pad_row(b, t, f, T, F);
+      const float g = dz[p * Co + co];
+      s += isb ? g : g * x[(p + (long long)(kw - 1) * (F + 2) + (kh - 1)) * Ci + ci];
+    }
+    partial[(long long)blockIdx.x * nout + o] = s;
+  }
+}
+
+struct Pool {
+  int pt, pf;     // pool size = stride along time / freq (0 = no pooling)
+  int To, Fo;     // output extent
+};
+
+// P[b][t'][f'][c] = max over the window of relu(z); slot = argmax in torch's
+// scan order (freq outer, time inner; first maximum wins).
+__global__ void post_fwd(const float* __restrict__ z, int B, int T, int F, int C, Pool pl,
+                         float* __restrict__ P, uint8_t* __restrict__ slot) {
+  const long long n = (long long)B * pl.To * pl.Fo * C;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const long long q = i / C;
+    const int fo = (int)(q % pl.Fo);
+    const int to = (int)((q / pl.Fo) % pl.To);
+    const int b = (int)(q / ((long long)pl.Fo * pl.To));
+    if (!pl.pt) {
+      P[i] = fmaxf(z[pad_row(b, to, fo, T, F) * C + c], 0.f);
+      continue;
+    }
+    float best = -__builtin_huge_valf();
+    int bs = 0;
+    for (int df = 0; df < pl.pf; ++df) {
+      const int f = fo * pl.pf + df;
+      if (f >= F) break;
+      for (int dt = 0; dt < pl.pt; ++dt) {
+        const int t = to * pl.pt + dt;
+        if (t >= T) break;
+        const float v = fmaxf(z[pad_row(b, t, f, T, F) * C + c], 0.f);
+        if (v > best) { best = v; bs = df * pl.pt + dt; }
+      }
+    }
+    P[i] = best;
+    slot[i] = (uint8_t)bs;
+  }
+}
+
+// Column statistics of X [n][C] in fixed chunk order: partial[chunk][c] =
+// sum over the chunk of (x - shift[c]) (shift = nullptr: 0) or of its square.
+__global__ void col_moment(const float* __restrict__ X, long long n, int C, long long rows_per,
+                           const float* __restrict__ shift, int square,
+                           float* __restrict__ partial) {
+  const long long r0 = (long long)blockIdx.x * rows_per;
+  const long long r1 = min(n, r0 + rows_per);
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const float m = shift ? shift[c] : 0.f;
+    float s = 0.f;
+    for (long long r = r0; r < r1; ++r) {
+      const float d = X[r * C + c] - m;
+      s += square ? d * d : d;
+    }
+    partial[(long long)blockIdx.x * C + c] = s;
+  }
+}
+
+__global__ void sum_partials(const float* __restrict__ partial, int nchunk, int C, float scale,
+                             float* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int q = 0; q < nchunk; ++q) s += partial[(long long)q * C + c];
+  out[c] = s * scale;
+}
+
+// mean -> (mean, rstd) from the centred second moment; running stats update
+// (momentum, unbiased variance) as nn.BatchNorm2d in training mode.
+__global__ void bn_finalize(const float* __restrict__ mean, const float* __restrict__ m2,
+                            int C, long long n, float eps, float momentum,
+                            float* __restrict__ rstd, float* __restrict__ run_mean,
+                            float* __restrict__ run_var) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float var = m2[c];   // biased (already / n)
+  rstd[c] = rsqrtf(var + eps);
+  if (run_mean) {
+    const float unb = n > 1 ? var * ((float)n / (float)(n - 1)) : var;
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean[c];
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * unb;
+  }
+}
+
+__global__ void bn_eval_stats(const float* __restrict__ run_mean, const float* __restrict__ run_var,
+                              int C, float eps, float* __restrict__ mean, float* __restrict__ rstd) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  mean[c] = run_mean[c];
+  rstd[c] = rsqrtf(run_var[c] + eps);
+}
+
+struct Affine {
+  const float* mean;    // nullable: no BN
+  const float* rstd;
+  const float* gamma;
+  const float* beta;
+  float drop;
+  unsigned long long seed;
+};
+
+// y = dropout(BN(P)); written to the next layer's padded input (bf16 / f32,
+// halo untouched: the caller zeroes it) or, out_flat, to [B][T'][F'][C].
+template <typename TO>
+__global__ void apply_fwd(const float* __restrict__ P, int B, int To, int Fo, int C, Affine af,
+                          TO* __restrict__ out, int flat) {
+  const long long n = (long long)B * To * Fo * C;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    float y = P[i];
+    if (af.mean) y = (y - af.mean[c]) * af.rstd[c] * af.gamma[c] + af.beta[c];
+    if (af.drop > 0.f) y *= drop_scale(af.drop, af.seed, (unsigned long long)i);
+    long long o = i;
+    if (!flat) {
+      const long long q = i / C;
+      const int fo = (int)(q % Fo);
+      const int to = (int)((q / Fo) % To);
+      const int b = (int)(q / ((long long)Fo * To));
+      o = pad_row(b, to, fo, To, Fo) * C + c;
+    }
+    if constexpr (sizeof(TO) == 2) out[o] = f2bf(y);
+    else out[o] = y;
+  }
+}
+
+// dy (after the dropout mask) of output element i, from the next layer's dX
+// (padded rows, flat = 0) or the encoder's gradient [B][T'][F'][C] (flat = 1).
+__device__ __forceinline__ float dy_at(const float* __restrict__ dnext, long long i, int To,
+                                       int Fo, int C, int flat, float drop,
+                                       unsigned long long seed) {
+  long long o = i;
+  if (!flat) {
+    const int c = (int)(i % C);
+    const long long q = i / C;
+    const int fo = (int)(q % Fo);
+    const int to = (int)((q / Fo) % To);
+    const int b = (int)(q / ((long long)Fo * To));
+    o = pad_row(b, to, fo, To, Fo) * C + c;
+  }
+  float g = dnext[o];
+  if (drop > 0.f) g *= drop_scale(drop, seed, (unsigned long long)i);
+  return g;
+}
+
+// partial sums per channel of dy and dy * xhat over row chunks
+__global__ void bn_bwd_moments(const float* __restrict__ dnext, const float* __restrict__ P,
+                               int B, int To, int Fo, int C, int flat, Affine af,
+                               long long rows_per, float* __restrict__ partial) {
+  const long long n = (long long)B * To * Fo;
+  const long long r0 = (long long)blockIdx.x * rows_per;
+  const long long r1 = min(n, r0 + rows_per);
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float s1 = 0.f, s2 = 0.f;
+    for (long long r = r0; r < r1; ++r) {
+      const long long i = r * C + c;
+      const float g = dy_at(dnext, i, To, Fo, C, flat, af.drop, af.seed);
+      s1 += g;
+      s2 += g * (P[i] - af.mean[c]) * af.rstd[c];
+    }
+    partial[((long long)blockIdx.x * 2) * C + c] = s1;
+    partial[((long long)blockIdx.x * 2 + 1) * C + c] = s2;
+  }
+}
+
+__global__ void bn_bwd_finalize(const float* __restrict__ partial, int nchunk, int C,
+                                float* __restrict__ sums, float* __restrict__ dgamma,
+                                float* __restrict__ dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s1 = 0.f, s2 = 0.f;
+  for (int q = 0; q < nchunk; ++q) {
+    s1 += partial[((long long)q * 2) * C + c];
+    s2 += partial[((long long)q * 2 + 1) * C + c];
+  }
+  sums[c] = s1;
+  sums[C + c] = s2;
+  if (dgamma) dgamma[c] += s2;
+  if (dbeta) dbeta[c] += s1;
+}
+
+// dP = BN backward (or dy without BN); routed to the pooled-from pixel if its
+// conv output was positive (ReLU), written into dZ [padded pixels][C] (TO).
+template <typename TO>
+__global__ void post_bwd(const float* __restrict__ dnext, const float* __restrict__ P,
+                         const float* __restrict__ z, const uint8_t* __restrict__ slot, int B,
+                         int T, int F, int C, Pool pl, int flat, Affine af,
+                         const float* __restrict__ sums, TO* __restrict__ dz) {
+  const long long nr = (long long)B * pl.To * pl.Fo;
+  const long long n = nr * C;
+  const float inv_n = 1.f / (float)nr;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    float g = dy_at(dnext, i, pl.To, pl.Fo, C, flat, af.drop, af.seed);
+    if (af.mean) {
+      const float xh = (P[i] - af.mean[c]) * af.rstd[c];
+      g = af.gamma[c] * af.rstd[c] * (g - sums[c] * inv_n - xh * sums[C + c] * inv_n);
+    }
+    const long long q = i / C;
+    const int fo = (int)(q % pl.Fo);
+    const int to = (int)((q / pl.Fo) % pl.To);
+    const int b = (int)(q / ((long long)pl.Fo * pl.To));
+    int t = to, f = fo;
+    if (pl.pt) {
+      const int s = slot[i];
+      t = to * pl.pt + s % pl.pt;
+      f = fo * pl.pf + s / pl.pt;
+    }
+    const long long p = pad_row(b, t, f, T, F) * C + c;
+    const float v = z[p] > 0.f ? g : 0.f;
+    if constexpr (sizeof(TO) == 2) dz[p] = f2bf(v);
+    else dz[p] = v;
+  }
+}
+
+// GEMM weight images of a torch Conv2d weight W [Co][Ci][3(f)][3(t)], tap
+// j = kw*3 + kh (the row shift (kw-1)(F+2) + (kh-1) of gemm.hip tap addressing):
+//   mode 0 (forward):  out[co][j*Ci + ci] = W[co][ci][kh][kw]
+//   mode 1 (d input):  out[ci][j*Co + co] = W[co][ci][kh][kw]
+template <typename TO>
+__global__ void weight_pack(const float* __restrict__ w, int Co, int Ci, int mode,
+                            TO* __restrict__ out) {
+  const long long n = (long long)Co * Ci * 9;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int kw = (int)(i % 3), kh = (int)((i / 3) % 3);
+    const int ci = (int)((i / 9) % Ci), co = (int)(i / (9LL * Ci));
+    const int j = kw * 3 + kh;
+    const long long o = mode == 0 ? ((long long)co * 9 + j) * Ci + ci
+                                  : ((long long)ci * 9 + j) * Co + co;
+    if constexpr (sizeof(TO) == 2) out[o] = f2bf(w[i]);
+    else out[o] = w[i];
+  }
+}
+
+// dW [Co][Ci][3][3] += packed [Co][9 Ci] (mode-0 image layout)
+__global__ void weight_unpack_acc(const float* __restrict__ pk, int Co, int Ci,
+                                  float* __restrict__ dw) {
+  const long long n = (long long)Co * Ci * 9;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int kw = (int)(i % 3), kh = (int)((i / 3) % 3);
+    const int ci = (int)((i / 9) % Ci), co = (int)(i / (9LL * Ci));
+    dw[i] += pk[((long long)co * 9 + kw * 3 + kh) * Ci + ci];
+  }
+}
+
+inline int grid_for(long long n) {
+  const long long b = (n + CT - 1) / CT;
+  return (int)(b < 8192 ? (b > 0 ? b : 1) : 8192);
+}
+
+inline long long rows_per_chunk(long long n) {
+  const long long nchunk = n < 1024 ? 1 : 1024;
+  return (n + nchunk - 1) / nchunk;
+}
+
+Pool make_pool(int T, int F, int pt, int pf, int ceil_mode) {
+  Pool pl{pt, pf, T, F};
+  if (pt > 0) {
+    auto out = [&](int n, int k) {
+      if (!ceil_mode) return (n - k) / k + 1;
+      int o = (n - k + k - 1) / k + 1;
+      if ((o - 1) * k >= n) --o;   // the last window must start inside the input
+      return o;
+    };
+    pl.To = out(T, pt);
+    pl.Fo = out(F, pf);
+  }
+  return pl;
+}
+
+}  // namespace
+}  // namespace asr
+
+using namespace asr;
+
+extern "C" int asr_vgg_pad_input(const float* xs, int B, int T, int F, float* out, void* stream) {
+  ASR_REQUIRE(xs && out && B > 0 && T > 0 && F > 0, ASR_ERR_ARG, "vgg_pad_input: bad args");
+  hipLaunchKernelGGL(vgg_pad_input, dim3(grid_for((long long)B * (T + 2) * (F + 2))), dim3(CT),
+                     0, (hipStream_t)stream, xs, B, T, F, out);
+  ASR_LAUNCH_CHECK();
+  return ASR_OK;
+}
+
+extern "C" int asr_conv_weight_pack(const float* w, int Co, int Ci, int mode, int out_dtype,
+                                    void* out, void* stream) {
+  ASR_REQUIRE(w && out && Co > 0 && Ci > 0 && (mode == 0 || mode == 1), ASR_ERR_ARG,
+              "conv_weight_pack: bad args");
+  const long long n = (long long)Co * Ci * 9;
+  if (out_dtype == ASR_DT_BF16)
+    hipLaunchKernelGGL((weight_pack<uint16_t>), dim3(grid_for(n)), dim3(CT), 0,
+                       (hipStream_t)stream, w, Co, Ci, mode, (uint16_t*)out);
+  else
+    hipLaunchKernelGGL((weight_pack<float>), dim3(grid_for(n)), dim3(CT), 0, (hipStream_t)stream,
+                       w, Co, Ci, mode, (float*)out);
+  ASR_LAUNCH_CHECK();
+  return ASR_OK;
+}
+
+extern "C" int asr_conv_weight_unpack_acc(const float* packed, int Co, int Ci, float* dw,
+                                          void* stream) {
+  ASR_REQUIRE(packed && dw && Co > 0 && Ci > 0, ASR_ERR_ARG, "conv_weight_unpack_acc: bad args");
+  hipLaunchKernelGGL(weight_unpack_acc, dim3(grid_for((long long)Co * Ci * 9)), dim3(CT), 0,
+                     (hipStream_t)stream, packed, Co, Ci, dw);
+  ASR_LAUNCH_CHECK();
+  return ASR_OK;
+}
+
+extern "C" int asr_conv_direct_forward(const float* x, int B, int T, int F, int Ci, int Co,
+                                       const float* w, const float* bias, float* z,
+                                       void* stream) {
+  ASR_REQUIRE(x && w && z && B > 0 && T > 0 && F > 0 && Ci > 0 && Co > 0, ASR_ERR_ARG,
+              "conv_direct_forward: bad args");
+  hipLaunchKernelGGL(conv_direct_fwd, dim3(grid_for((long long)B * T * F * Co)), dim3(CT), 0,
+                     (hipStream_t)stream, x, B, T, F, Ci, Co, w, bias, z);
+  ASR_LAUNCH_CHECK();
+  return ASR_OK;
+}
+
+extern "C" int asr_conv_direct_dgrad(const float* dz, int B, int T, int F, int Ci, int Co,
+                                     const float* w, float* dx, void* stream) {
+  ASR_REQUIRE(dz && w && dx && B > 0 && T > 0 && F > 0 && Ci > 0 && Co > 0, ASR_ERR_ARG,
+              "conv_direct_dgrad: bad args");
+  hipLaunchKernelGGL(conv_direct_dgrad, dim3(grid_for((long long)B * T * F * Ci)), dim3(CT), 0,
+                     (hipStream_t)stream, dz, B, T, F, Ci, Co, w, dx);
+  ASR_LAUNCH_CHECK();
+  return ASR_OK;
+}
+
+namespace asr {
+namespace {
+__global__ void acc_kernel(const float* __restrict__ a, float* __restrict__ d, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) d[i] += a[i];
+}
+}  // namespace
+}  // namespace asr
+
+extern "C" int asr_vgg_accumulate(const float* a, float* dst, int n, const float* a2, float* dst2,
+                                  int n2, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (n > 0) hipLaunchKernelGGL(acc_kernel, dim3((n + CT - 1) / CT), dim3(CT), 0, s, a, dst, n);
+  if (a2 && dst2 && n2 > 0)
+    hipLaunchKernelGGL(acc_kernel, dim3((n2 + CT - 1) / CT), dim3(CT), 0, s, a2, dst2, n2);
+  ASR_LAUNCH_CHECK();
+  return ASR_OK;
+}
+
+extern "C" size_t asr_conv_direct_wgrad_workspace_bytes(int B, int T, int F, int Ci, int Co) {
+  const long long npix = (long long)B * T * F;
+  const long long per = rows_per_chunk(npix);
+  const long long nchunk = (npix + per - 1) / per;
+  return (size_t)nchunk * (Co * Ci * 9 + Co) * sizeof(float);
+}
+
+extern "C" int asr_conv_direct_wgrad(const float* x, const float* dz, int B, int T, int F, int Ci,
+                                     int Co, float* dw, float* dbias, void* workspace,
+                                     size_t ws_bytes, void* stream) {
+  ASR_REQUIRE(x && dz && dw && workspace, ASR_ERR_ARG, "conv_direct_wgrad: null pointer");
+  ASR_REQUIRE(ws_bytes >= asr_conv_direct_wgrad_workspace_bytes(B, T, F, Ci, Co),
+              ASR_ERR_WORKSPACE, "conv_direct_wgrad: workspace too small");
+  const long long npix = (long long)B * T * F;
+  const long long per = rows_per_chunk(npix);
+  const int nchunk = (int)((npix + per - 1) / per);
+  const int nout = Co * Ci * 9 + Co;
+  hipStream_t s = (hipStream_t)stream;
+  float* part = (float*)workspace;
+  hipLaunchKernelGGL(conv_direct_wgrad, dim3(nchunk), dim3(CT), 0, s, x, dz, B, T, F, Ci, Co,
+                     (int)per, part);
+  ASR_LAUNCH_CHECK();
+  // row 0 <- column totals (each column is read entirely before its thread writes it)
+  hipLaunchKernelGGL(sum_partials, dim3((nout + CT - 1) / CT), dim3(CT), 0, s, part, nchunk, nout,
+                     1.f, part);
+  ASR_LAUNCH_CHECK();
+  return asr_vgg_accumulate(part, dw, Co * Ci * 9, dbias ? part + Co * Ci * 9 : nullptr, dbias,
+                            Co, stream);
+}
+
+extern "C" int asr_vgg_pool_dims(int T, int F, int pt, int pf, int ceil_mode, int* To, int* Fo) {
+  ASR_REQUIRE(To && Fo, ASR_ERR_ARG, "vgg_pool_dims: null pointer");
+  const Pool pl = make_pool(T, F, pt, pf, ceil_mode);
+  *To = pl.To;
+  *Fo = pl.Fo;
+  return ASR_OK;
+}
+
+extern "C" size_t asr_vgg_block_workspace_bytes(int B, int To, int Fo, int C) {
+  const long long n = (long long)B * To * Fo;
+  const long long per = rows_per_chunk(n);
+  const long long nchunk = (n + per - 1) / per;
+  return (size_t)(nchunk * 2 + 4) * C * sizeof(float);
+}
+
+// ReLU + pool + BatchNorm (+ stats) + dropout of one VGG layer.
+// z: conv output [padded pixels of (T, F)][C]; P / slot: saved for backward;
+// bn_mean / bn_rstd: the statistics used ([C] each, written); gamma == NULL: no
+// BN.  training: batch statistics and running-stat update, else running stats.
+// out: next layer input, padded rows of (T', F') (out_dtype f32 / bf16; the
+// caller zeroes it) or, flat, [B][T'][F'][C] f32.
+extern "C" int asr_vgg_block_forward(const float* z, int B, int T, int F, int C, int pt, int pf,
+                                     int ceil_mode, float* P, uint8_t* slot, const float* gamma,
+                                     const float* beta, float* run_mean, float* run_var,
+                                     int training, float momentum, float eps, float* bn_mean,
+                                     float* bn_rstd, float drop, unsigned long long seed,
+                                     void* out, int out_dtype, int flat, void* workspace,
+                                     size_t ws_bytes, void* stream) {
+  ASR_REQUIRE(z && P && out && B > 0 && T > 0 && F > 0 && C > 0, ASR_ERR_ARG,
+              "vgg_block_forward: bad args");
+  ASR_REQUIRE(!pt || slot, ASR_ERR_ARG, "vgg_block_forward: pooling needs slot");
+  const Pool pl = make_pool(T, F, pt, pf, ceil_mode);
+  ASR_REQUIRE(pl.To > 0 && pl.Fo > 0, ASR_ERR_ARG, "vgg_block_forward: empty output");
+  hipStream_t s = (hipStream_t)stream;
+  const long long nr = (long long)B * pl.To * pl.Fo;
+  hipLaunchKernelGGL(post_fwd, dim3(grid_for(nr * C)), dim3(CT), 0, s, z, B, T, F, C, pl, P, slot);
+  ASR_LAUNCH_CHECK();
+  Affine af{nullptr, nullptr, nullptr, nullptr, drop, seed};
+  if (gamma) {
+    ASR_REQUIRE(beta && bn_mean && bn_rstd && workspace, ASR_ERR_ARG,
+                "vgg_block_forward: BN needs beta / mean / rstd / workspace");
+    ASR_REQUIRE(ws_bytes >= asr_vgg_block_workspace_bytes(B, pl.To, pl.Fo, C), ASR_ERR_WORKSPACE,
+                "vgg_block_forward: workspace too small");
+    if (training) {
+      const long long per = rows_per_chunk(nr);
+      const int nchunk = (int)((nr + per - 1) / per);
+      float* part = (float*)workspace;
+      float* m2 = part + (size_t)nchunk * C;
+      hipLaunchKernelGGL(col_moment, dim3(nchunk), dim3(CT), 0, s, P, nr, C, per, nullptr, 0,
+                         part);
+      hipLaunchKernelGGL(sum_partials, dim3((C + CT - 1) / CT), dim3(CT), 0, s, part, nchunk, C,
+                         1.f / (float)nr, bn_mean);
+      hipLaunchKernelGGL(col_moment, dim3(nchunk), dim3(CT), 0, s, P, nr, C, per, bn_mean, 1,
+                         part);
+      hipLaunchKernelGGL(sum_partials, dim3((C + CT - 1) / CT), dim3(CT), 0, s, part, nchunk, C,
+                         1.f / (float)nr, m2);
+      hipLaunchKernelGGL(bn_finalize, dim3((C + CT - 1) / CT), dim3(CT), 0, s, bn_mean, m2, C, nr,
+                         eps, momentum, bn_rstd, run_mean, run_var);
+    } else {
+      ASR_REQUIRE(run_mean && run_var, ASR_ERR_ARG, "vgg_block_forward: eval needs running stats");
+      hipLaunchKernelGGL(bn_eval_stats, dim3((C + CT - 1) / CT), dim3(CT), 0, s, run_mean,
+                         run_var, C, eps, bn_mean, bn_rstd);
+    }
+    ASR_LAUNCH_CHECK();
+    af.mean = bn_mean;
+    af.rstd = bn_rstd;
+    af.gamma = gamma;
+    af.beta = beta;
+  }
+  if (out_dtype == ASR_DT_BF16 && !flat)
+    hipLaunchKernelGGL((apply_fwd<uint16_t>), dim3(grid_for(nr * C)), dim3(CT), 0, s, P, B,
+                       pl.To, pl.Fo, C, af, (uint16_t*)out, 0);
+  else
+    hipLaunchKernelGGL((apply_fwd<float>), dim3(grid_for(nr * C)), dim3(CT), 0, s, P, B, pl.To,
+                       pl.Fo, C, af, (float*)out, flat);
+  ASR_LAUNCH_CHECK();
+  return ASR_OK;
+}
+
+// Backward of asr_vgg_block_forward (same geometry / saved tensors): dnext is
+// the gradient of `out` (padded rows f32 or flat); dz [padded pixels][C] of
+// dz_dtype receives d(conv output) (the caller zeroes it: halo and
+// not-selected pixels stay 0); dgamma / dbeta accumulate (+=).
+extern "C" int asr_vgg_block_backward(const float* dnext, int flat, const float* z, int B, int T,
+                                      int F, int C, int pt, int pf, int ceil_mode,
+                                      const float* P, const uint8_t* slot, const float* gamma,
+                                      const float* bn_mean, const float* bn_rstd, float* dgamma,
+                                      float* dbeta, float drop, unsigned long long seed,
+                                      void* dz, int dz_dtype, void* workspace, size_t ws_bytes,
+                                      void* stream) {
+  ASR_REQUIRE(dnext && z && P && dz && B > 0 && T > 0 && F > 0 && C > 0, ASR_ERR_ARG,
+              "vgg_block_backward: bad args");
+  const Pool pl = make_pool(T, F, pt, pf, ceil_mode);
+  hipStream_t s = (hipStream_t)stream;
+  const long long nr = (long long)B * pl.To * pl.Fo;
+  Affine af{nullptr, nullptr, nullptr, nullptr, drop, seed};
+  float* sums = nullptr;
+  if (gamma) {
+    ASR_REQUIRE(bn_mean && bn_rstd && workspace, ASR_ERR_ARG, "vgg_block_backward: BN args");
+    ASR_REQUIRE(ws_bytes >= asr_vgg_block_workspace_bytes(B, pl.To, pl.Fo, C), ASR_ERR_WORKSPACE,
+                "vgg_block_backward: workspace too small");
+    af.mean = bn_mean;
+    af.rstd = bn_rstd;
+    af.gamma = gamma;
+    const long long per = rows_per_chunk(nr);
+    const int nchunk = (int)((nr + per - 1) / per);
+    float* part = (float*)workspace;
+    sums = part + (size_t)nchunk * 2 * C;
+    hipLaunchKernelGGL(bn_bwd_moments, dim3(nchunk), dim3(CT), 0, s, dnext, P, B, pl.To, pl.Fo,
+                       C, flat, af, per, part);
+    hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + CT - 1) / CT), dim3(CT), 0, s, part, nchunk, C,
+                       sums, dgamma, dbeta);
+    ASR_LAUNCH_CHECK();
+  }
+  if (dz_dtype == ASR_DT_BF16)
+    hipLaunchKernelGGL((post_bwd<uint16_t>), dim3(grid_for(nr * C)), dim3(CT), 0, s, dnext, P, z,
+                       slot, B, T, F, C, pl, flat, af, sums, (uint16_t*)dz);
+  else
+    hipLaunchKernelGGL((post_bwd<float>), dim3(grid_for(nr * C)), dim3(CT), 0, s, dnext, P, z,
+                       slot, B, T, F, C, pl, flat, af, sums, (float*)dz);
+  ASR_LAUNCH_CHECK();
+  return ASR_OK;
+}

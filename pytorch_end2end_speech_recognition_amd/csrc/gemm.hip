@@ -37,7 +37,17 @@ struct Operand {
   int trans;
   int vec_ok; // 16-element vector loads legal (alignment of base and strides)
   long long bytes;  // readable bytes from base (0 = unknown)
+  int tap_g, tap_w, tap_s;  // 3x3 tap addressing (asr_operand_t), tap_g = 0: off
 };
+
+// Tap addressing: contiguous index x -> (tap, x'), row shifted by the tap's offset.
+__device__ __forceinline__ void tap_adjust(const Operand& op, int& row, int& col) {
+  if (op.tap_g) {
+    const int tap = col / op.tap_g;
+    col -= tap * op.tap_g;
+    row += op.tap_s * ((tap / 3 - 1) * op.tap_w + (tap % 3 - 1));
+  }
+}
 
 struct Problem {
   Operand a, b;
@@ -142,15 +152,35 @@ __device__ __forceinline__ void load4(const Operand& op, int r, int nrows, int c
 //            block per thread, k = 4*(tid/32)..+3, row = 4*(tid%32)..+3, so each
 //            row's 4 k land as one 8-B (bf16) LDS store instead of 4 scalars.
 //            v[kk*4 + mi] = element (k0 + 4*(tid/32) + kk, row tile0 + 4*(tid%32) + mi)
+// K: end of this work-group's k range (split-K chunk end); Ktot: the operand's
+// full k extent (a tap-shifted k-row may read past the chunk, never past Ktot).
 __device__ __forceinline__ void load_tile(const Operand& op, int tile0, int nrows_logical, int k0,
-                                          int K, float (&v)[16]) {
+                                          int K, int Ktot, float (&v)[16]) {
   const int tid = threadIdx.x;
   if (!op.trans) {
-    load16(op, tile0 + (tid >> 1), nrows_logical, k0 + (tid & 1) * 16, K, v);
+    int r = tile0 + (tid >> 1), c = k0 + (tid & 1) * 16;
+    if (op.tap_g) {
+      const int kv = K - c;   // elements of this chunk inside K
+      tap_adjust(op, r, c);
+      if (kv <= 0) r = nrows_logical;   // past K: zeros
+      load16(op, r, nrows_logical, c, c + min(kv, 16), v);
+    } else {
+      load16(op, r, nrows_logical, c, K, v);
+    }
   } else {
     const int kb = k0 + 4 * (tid >> 5), m4 = tile0 + 4 * (tid & 31);
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk) load4(op, kb + kk, K, m4, nrows_logical, v + 4 * kk);
+    for (int kk = 0; kk < 4; ++kk) {
+      if (op.tap_g) {
+        int r = kb + kk, c = m4;
+        const int nv = nrows_logical - c;
+        tap_adjust(op, r, c);
+        if (nv <= 0 || kb + kk >= K) r = Ktot;
+        load4(op, r, Ktot, c, c + min(nv, 4), v + 4 * kk);
+      } else {
+        load4(op, kb + kk, K, m4, nrows_logical, v + 4 * kk);
+      }
+    }
   }
 }
 
@@ -278,8 +308,8 @@ __global__ void __launch_bounds__(NT) gemm_kernel(Params P) {
 
   const int nk = (kend - kbeg + BK - 1) / BK;
   float va[16], vb[16];
-  load_tile(pr.a, tm, pr.M, kbeg, kend, va);
-  load_tile(pr.b, tn, pr.N, kbeg, kend, vb);
+  load_tile(pr.a, tm, pr.M, kbeg, kend, pr.K, va);
+  load_tile(pr.b, tn, pr.N, kbeg, kend, pr.K, vb);
   store_tile<BF16>(pr.a, As, va);
   store_tile<BF16>(pr.b, Bs, vb);
   __syncthreads();
@@ -287,8 +317,8 @@ __global__ void __launch_bounds__(NT) gemm_kernel(Params P) {
   for (int kt = 0; kt < nk; ++kt) {
     const bool more = kt + 1 < nk;
     if (more) {
-      load_tile(pr.a, tm, pr.M, kbeg + (kt + 1) * BK, kend, va);
-      load_tile(pr.b, tn, pr.N, kbeg + (kt + 1) * BK, kend, vb);
+      load_tile(pr.a, tm, pr.M, kbeg + (kt + 1) * BK, kend, pr.K, va);
+      load_tile(pr.b, tn, pr.N, kbeg + (kt + 1) * BK, kend, pr.K, vb);
     }
     if (BF16) {
       const uint16_t* a = (const uint16_t*)As;
@@ -384,8 +414,9 @@ __device__ __forceinline__ void stage_tile(const Operand& op, __amdgpu_buffer_rs
     if (MODE == 0) {
       const int r = blk * 8 + (lane >> 3);
       const int c = (lane & 7) ^ ((r >> 1) & 7);
-      const int row = tile0 + r, k = k0 + 8 * c;
+      int row = tile0 + r, k = k0 + 8 * c;
       if (row < nrows && k < kend) {
+        tap_adjust(op, row, k);
         const long long off = row_off_np(op.map, row);
         if (off >= 0) voff = (unsigned)((off + k) * 2);
       }
@@ -393,10 +424,11 @@ __device__ __forceinline__ void stage_tile(const Operand& op, __amdgpu_buffer_rs
       const int kr = blk * 4 + (lane >> 4);
       const int j = lane & 15;
       const int c = 2 * ((j >> 1) ^ swz_h(kr)) + (j & 1);
-      const int k = k0 + kr;
+      int k = k0 + kr, col = tile0 + 8 * c;
       if (k < kend) {
+        tap_adjust(op, k, col);
         const long long off = row_off_np(op.map, k);
-        if (off >= 0) voff = (unsigned)((off + tile0 + 8 * c) * 2);
+        if (off >= 0) voff = (unsigned)((off + col) * 2);
       }
     }
     // LDS-DMA in inline asm: hipcc neither counts it (so it does not drain it
@@ -581,6 +613,12 @@ int fill_operand(const asr_operand_t& o, Operand* op, const char* name) {
   const int vec = o.dtype == ASR_DT_F32 ? 4 : 8;
   op->vec_ok = aligned16(o.ptr) && (o.map.stride_t % vec == 0) && (o.map.stride_b % vec == 0);
   op->bytes = o.bytes;
+  op->tap_g = o.tap_group;
+  op->tap_w = o.tap_pitch;
+  op->tap_s = o.tap_sign ? o.tap_sign : 1;
+  if (o.tap_group)
+    ASR_REQUIRE(o.tap_group > 0 && o.tap_group % (o.trans ? 8 : 16) == 0 && !o.map.perm,
+                ASR_ERR_ARG, "gemm: operand %s tap_group %d unsupported", name, o.tap_group);
   (void)esz;
   return ASR_OK;
 }

@@ -7,7 +7,8 @@ rnn.py:162-246) and the same torch RNG consumption at construction, so a model
 built under the same seed holds bit-identical initial weights.  ``nn.LSTM``
 modules are used only as parameter holders; their forward never runs.
 
-Forward semantics (rnn.py:284-487): input dropout, length sort (perm_idx is
+Forward semantics (rnn.py:284-487): input dropout, the optional VGG front-end
+(encoders/cnn.py, rnn.py:143-160, 314-316), length sort (perm_idx is
 returned; outputs stay in sorted order), packed-sequence behaviour through
 per-utterance length masks, dropout after every layer, pyramidal ``drop``
 subsampling ``xs[:, 1::2]`` fused into the next layer's input GEMM, and the
@@ -19,6 +20,7 @@ import torch
 import torch.nn as nn
 
 from .... import native_ops as ops
+from .cnn import CNNEncoder
 
 
 class RNNEncoder(nn.Module):
@@ -48,8 +50,6 @@ class RNNEncoder(nn.Module):
             unsupported.append('subsample_type=concat')
         if residual or dense_residual:
             unsupported.append('residual')
-        if len(conv_channels) > 0:
-            unsupported.append('conv front-end')
         if num_layers_sub or nin or merge_bidirectional or not batch_first or not pack_sequence:
             unsupported.append('num_layers_sub/nin/merge/time-major/no-pack')
         if unsupported:
@@ -70,11 +70,24 @@ class RNNEncoder(nn.Module):
         self.dropout_input_p = float(dropout_input)
         self.dropout_hidden_p = float(dropout_hidden)
         self.dropout_input = nn.Dropout(p=dropout_input)
-        self.conv = None
-        input_size = input_size * splice * num_stack
+        self.batch_norm = batch_norm
+        if len(conv_channels) > 0 and len(conv_channels) == len(conv_kernel_sizes) and \
+                len(conv_kernel_sizes) == len(conv_strides):   # rnn.py:143-160
+            assert num_stack == 1 and splice == 1
+            self.conv = CNNEncoder(input_size, input_channel=input_channel,
+                                   conv_channels=conv_channels,
+                                   conv_kernel_sizes=conv_kernel_sizes,
+                                   conv_strides=conv_strides, poolings=poolings, dropout_input=0,
+                                   dropout_hidden=dropout_hidden, activation=activation,
+                                   batch_norm=batch_norm)
+            input_size = self.conv.output_size
+        else:
+            self.conv = None
+            input_size = input_size * splice * num_stack
         self.input_size = input_size
 
-        self.fast_impl = sum(self.subsample_list) == 0
+        # rnn.py:162 (batch_norm forces the per-layer modules, as in the reference)
+        self.fast_impl = sum(self.subsample_list) == 0 and not batch_norm
         if self.fast_impl:   # rnn.py:162-198: one multi-layer nn.LSTM
             self.lstm = nn.LSTM(input_size, hidden_size=num_units, num_layers=num_layers,
                                 bias=True, batch_first=batch_first, dropout=dropout_hidden,
@@ -128,6 +141,10 @@ class RNNEncoder(nn.Module):
         dev = xs.device
         if self.training and self.dropout_input_p > 0:
             xs = ops.dropout(xs, self.dropout_input_p)
+        if self.conv is not None:                                   # rnn.py:314-316
+            self.conv.train(self.training)
+            xs, x_lens = self.conv(xs, x_lens)
+            x_lens = x_lens.astype(np.int64)
 
         perm = np.argsort(-x_lens, kind='stable')                   # rnn.py:319-326
         lens = x_lens[perm]

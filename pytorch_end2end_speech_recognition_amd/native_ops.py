@@ -849,3 +849,163 @@ def ctc_loss(logits, labels_flat, label_lens, act_lens, max_label_len, loss_scal
     """Returns (loss [1], costs [B])."""
     return CTCLossFn.apply(logits, labels_flat, label_lens, act_lens, max_label_len, loss_scale,
                            blank, zero_infinity)
+
+
+# ---------------------------------------------------------------------------
+# VGG front-end (CNNEncoder, models/pytorch_v3/encoders/cnn.py:124-165)
+# ---------------------------------------------------------------------------
+def _tap_operand(t, trans, stride, group, pitch, sign):
+    op = operand(t, trans, rowmap(stride))
+    op.tap_group, op.tap_pitch, op.tap_sign = int(group), int(pitch), int(sign)
+    return op
+
+
+def _pool_dims(T, F, pt, pf, ceil):
+    To, Fo = ctypes.c_int(), ctypes.c_int()
+    N.call('asr_vgg_pool_dims', T, F, pt, pf, ceil, ctypes.byref(To), ctypes.byref(Fo))
+    return To.value, Fo.value
+
+
+class VGGFn(torch.autograd.Function):
+    """The whole conv stack as one op.  Layer l input: zero-haloed channels-last
+    [B][T_l+2][F_l+2][C_in] (compute dtype for GEMM layers, f32 for direct
+    ones); conv output z_l f32 over the same padded pixels; the 3x3 conv of a
+    layer with C_in, C_out multiples of 16 = ONE GEMM with tap-addressed
+    operands (csrc/gemm.hip), other layers (C_in = 1) = asr_conv_direct_*;
+    ReLU, pool, batch norm and dropout = asr_vgg_block_*.  Output
+    [B, T', F'*C] f32."""
+
+    @staticmethod
+    def forward(ctx, xs, specs, training, p_drop, *params):
+        N.require_device(xs)
+        xs = xs.contiguous()
+        dev = xs.device
+        cd = compute_dtype()
+        B, T, F = xs.shape
+        f32 = dict(dtype=torch.float32, device=dev)
+        opdt = torch.bfloat16 if cd == BF16 else torch.float32
+        x_op = torch.empty(B * (T + 2) * (F + 2), **f32)
+        N.call('asr_vgg_pad_input', N.ptr(xs), B, T, F, N.ptr(x_op), N.stream_handle(dev))
+        cT, cF, cC = T, F, 1
+        saved, layers = [], []
+        L = len(specs)
+        use_gemm = [sp['w'].shape[1] % 16 == 0 and sp['w'].shape[0] % 16 == 0 for sp in specs]
+        for l, sp in enumerate(specs):
+            w = sp['w']
+            Co = w.shape[0]
+            npad = B * (cT + 2) * (cF + 2)
+            z = torch.empty(npad, Co, **f32)
+            if not use_gemm[l]:
+                N.call('asr_conv_direct_forward', N.ptr(x_op), B, cT, cF, cC, Co, N.ptr(w),
+                       N.ptr(sp['b']), N.ptr(z), N.stream_handle(dev))
+            else:
+                wg = torch.empty(Co, 9 * cC, dtype=opdt, device=dev)
+                N.call('asr_conv_weight_pack', N.ptr(w), Co, cC, 0, cd, N.ptr(wg),
+                       N.stream_handle(dev))
+                p = gemm_problem(_tap_operand(x_op, 0, cC, cC, cF + 2, 1),
+                                 operand(wg, 0, rowmap(9 * cC)), z, rowmap(Co), npad, Co, 9 * cC,
+                                 bias=sp['b'])
+                run_gemm([p], dev)
+            pt, pf, ceil = sp['pt'], sp['pf'], sp['ceil']
+            To, Fo = _pool_dims(cT, cF, pt, pf, ceil) if pt else (cT, cF)
+            P = torch.empty(B * To * Fo, Co, **f32)
+            slot = torch.empty(B * To * Fo * Co, dtype=torch.uint8, device=dev) if pt else None
+            bn = sp['gamma'] is not None
+            mean = torch.empty(Co, **f32) if bn else None
+            rstd = torch.empty(Co, **f32) if bn else None
+            drop = float(p_drop) if training else 0.0
+            seed = _next_seed() if drop > 0 else 0
+            last = l == L - 1
+            if last:
+                out = torch.empty(B, To, Fo * Co, **f32)
+                out_dt, flat = F32, 1
+            else:
+                nxt_dt = opdt if use_gemm[l + 1] else torch.float32
+                out = torch.zeros(B * (To + 2) * (Fo + 2), Co, dtype=nxt_dt, device=dev)
+                out_dt, flat = (cd if use_gemm[l + 1] else F32), 0
+            nb = N.query('asr_vgg_block_workspace_bytes', B, To, Fo, Co)
+            ws = _ws(nb, dev)
+            N.call('asr_vgg_block_forward', N.ptr(z), B, cT, cF, Co, pt, pf, ceil, N.ptr(P),
+                   N.ptr(slot), N.ptr(sp['gamma']), N.ptr(sp['beta']), N.ptr(sp['run_mean']),
+                   N.ptr(sp['run_var']), int(bool(training)), float(sp['momentum']),
+                   float(sp['eps']), N.ptr(mean), N.ptr(rstd), drop, seed, N.ptr(out), out_dt,
+                   flat, N.ptr(ws), nb, N.stream_handle(dev))
+            saved += [x_op, z, P, slot, mean, rstd]
+            layers.append((cT, cF, cC, Co, pt, pf, ceil, drop, seed, use_gemm[l]))
+            x_op, cT, cF, cC = out, To, Fo, Co
+        ctx.save_for_backward(*[t if t is not None else torch.empty(0, device=dev)
+                                for t in saved])
+        ctx.layers = layers
+        ctx.specs = specs
+        ctx.B = B
+        return x_op
+
+    @staticmethod
+    def backward(ctx, dout):
+        saved = ctx.saved_tensors
+        specs, layers, B = ctx.specs, ctx.layers, ctx.B
+        dev = dout.device
+        cd = compute_dtype()
+        f32 = dict(dtype=torch.float32, device=dev)
+        opdt = torch.bfloat16 if cd == BF16 else torch.float32
+        dnext, flat = dout.contiguous(), 1
+        for l in range(len(layers) - 1, -1, -1):
+            x_op, z, P, slot, mean, rstd = saved[6 * l:6 * l + 6]
+            slot = slot if slot.numel() else None
+            mean = mean if mean.numel() else None
+            rstd = rstd if rstd.numel() else None
+            cT, cF, cC, Co, pt, pf, ceil, drop, seed, gemm = layers[l]
+            sp = specs[l]
+            npad = B * (cT + 2) * (cF + 2)
+            dz_f32 = not gemm or sp['b'] is not None
+            dz = torch.zeros(npad, Co, **f32) if dz_f32 else torch.zeros(npad, Co, dtype=opdt,
+                                                                          device=dev)
+            To, Fo = _pool_dims(cT, cF, pt, pf, ceil) if pt else (cT, cF)
+            nb = N.query('asr_vgg_block_workspace_bytes', B, To, Fo, Co)
+            ws = _ws(nb, dev)
+            bn = sp['gamma'] is not None
+            N.call('asr_vgg_block_backward', N.ptr(dnext), flat, N.ptr(z), B, cT, cF, Co, pt, pf,
+                   ceil, N.ptr(P), N.ptr(slot), N.ptr(sp['gamma']), N.ptr(mean), N.ptr(rstd),
+                   N.ptr(grad_buffer(sp['gamma']) if bn else None),
+                   N.ptr(grad_buffer(sp['beta']) if bn else None), drop, seed, N.ptr(dz),
+                   F32 if dz_f32 else cd, N.ptr(ws), nb, N.stream_handle(dev))
+            w = sp['w']
+            if not gemm:
+                nb = N.query('asr_conv_direct_wgrad_workspace_bytes', B, cT, cF, cC, Co)
+                ws = _ws(nb, dev)
+                N.call('asr_conv_direct_wgrad', N.ptr(x_op), N.ptr(dz), B, cT, cF, cC, Co,
+                       N.ptr(grad_buffer(w)),
+                       N.ptr(grad_buffer(sp['b']) if sp['b'] is not None else None), N.ptr(ws),
+                       nb, N.stream_handle(dev))
+                if l == 0:
+                    break
+                dx = torch.empty(npad, cC, **f32)
+                N.call('asr_conv_direct_dgrad', N.ptr(dz), B, cT, cF, cC, Co, N.ptr(w), N.ptr(dx),
+                       N.stream_handle(dev))
+                dnext, flat = dx, 0
+                continue
+            # dW image [Co][9 Ci] = dz^T X (taps on the output index), K = padded pixels
+            packed = torch.empty(Co, 9 * cC, **f32)
+            run_gemm([gemm_problem(operand(dz, 1, rowmap(Co)),
+                                   _tap_operand(x_op, 1, cC, cC, cF + 2, 1), packed,
+                                   rowmap(9 * cC), Co, 9 * cC, npad)], dev)
+            N.call('asr_conv_weight_unpack_acc', N.ptr(packed), Co, cC, N.ptr(grad_buffer(w)),
+                   N.stream_handle(dev))
+            if sp['b'] is not None:
+                colsum_accumulate(dz, grad_buffer(sp['b']))
+            # d input (padded rows of layer l's input) = dz (taps, mirrored) x W^T image
+            wt = torch.empty(cC, 9 * Co, dtype=opdt, device=dev)
+            N.call('asr_conv_weight_pack', N.ptr(w), Co, cC, 1, cd, N.ptr(wt),
+                   N.stream_handle(dev))
+            dx = torch.empty(npad, cC, **f32)
+            run_gemm([gemm_problem(_tap_operand(dz, 0, Co, Co, cF + 2, -1),
+                                   operand(wt, 0, rowmap(9 * Co)), dx, rowmap(cC), npad, cC,
+                                   9 * Co)], dev)
+            dnext, flat = dx, 0
+        return (None, None, None, None) + (None,) * len(ctx.needs_input_grad[4:])
+
+
+def vgg_front(xs, specs, training, p_drop):
+    params = [t for sp in specs for t in (sp['w'], sp['b'], sp['gamma'], sp['beta'])
+              if t is not None]
+    return VGGFn.apply(xs, specs, training, p_drop, *params)

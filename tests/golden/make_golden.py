@@ -287,6 +287,43 @@ def case_ctc_model():
 
 
 # --------------------------------------------------------------------------
+# Case 4b: VGG-BLSTM CTC (CNNEncoder front-end, models/pytorch_v3/encoders/cnn.py)
+# --------------------------------------------------------------------------
+def case_vgg_model():
+    from models.pytorch_v3.ctc.ctc import CTC
+    vgg = dict(input_size=16, encoder_type='lstm', encoder_bidirectional=True,
+               encoder_num_units=6, encoder_num_proj=0, encoder_num_layers=2, fc_list=[],
+               dropout_input=0, dropout_encoder=0, num_classes=5, parameter_init=0.1,
+               subsample_list=[], subsample_type='drop', conv_channels=[4, 4, 16, 16],
+               conv_kernel_sizes=[[3, 3]] * 4, conv_strides=[[1, 1]] * 4,
+               poolings=[[], [2, 2], [], [2, 2]], activation='relu')
+    specs = [('model_vgg_bn', dict(vgg, batch_norm=True)),
+             ('model_vgg_nobn', dict(vgg, batch_norm=False, poolings=[[2, 2], [], [2, 2], []]))]
+    for name, kw in specs:
+        torch.manual_seed(1623)
+        model = CTC(**kw)
+        model.train()
+        sd0 = _sd(model)                    # before the step (BN running stats move)
+        rng = np.random.RandomState(5)
+        B, T = 3, 23                        # odd T: the ceil-mode pool keeps a partial window
+        x_lens = np.array([23, 17, 12], np.int32)
+        y_lens = np.array([3, 2, 2], np.int32)
+        xs, ys = _batch(rng, B, T, 16, y_lens, 5, x_lens)
+        loss = model(xs, ys, x_lens, y_lens)
+        loss.backward()
+        after = {'after/' + k: v.detach().numpy().copy() for k, v in model.state_dict().items()
+                 if 'running' in k}     # one training forward's running-stat update
+        enc = model.encoder
+        enc.conv.eval()                 # (eval: no second running-stat update)
+        with torch.no_grad():
+            conv_out, conv_lens = enc.conv(torch.from_numpy(xs), torch.from_numpy(x_lens))
+        _save(name, kwargs=np.array(json.dumps(kw)), xs=xs, ys=ys, x_lens=x_lens,
+              y_lens=y_lens, loss=loss.detach().numpy().reshape(1),
+              conv_lens=conv_lens.numpy().astype(np.int32), conv_T=np.int32(conv_out.shape[1]),
+              **sd0, **after, **_grads(model))
+
+
+# --------------------------------------------------------------------------
 # Case 5: attention enc-dec (location, bahdanau) with / without auxiliary CTC
 # --------------------------------------------------------------------------
 def case_attention_model():
@@ -329,4 +366,5 @@ if __name__ == '__main__':
     case_encoder()
     case_attention_step()
     case_ctc_model()
+    case_vgg_model()
     case_attention_model()
