@@ -90,7 +90,7 @@ def blstm_encoder(p, prefix, cfg, xs, x_lens):
     lens = x_lens[perm].astype(np.int64)
     n_layers = cfg['num_layers']
     sub = cfg.get('subsample_list') or [False] * n_layers
-    fast = sum(sub) == 0 and not cfg.get('batch_norm')       # rnn.py:162
+    fast = sum(sub) == 0 and not cfg.get('batch_norm') and cfg.get('fast', True)   # rnn.py:162
     for l in range(n_layers):
         if fast:   # one multi-layer nn.LSTM: lstm.weight_ih_l{l}{_reverse}
             names = [prefix + 'lstm.%s_l%d%s' % (n, l, s) for s in ('', '_reverse')
@@ -148,6 +148,27 @@ def ls_xent(logits, lens, ls_prob, size_average):
     lp = torch.log_softmax(logits, dim=-1)
     tot = sum((-(ls_prob / V) * lp[b, :int(lens[b])]).sum() for b in range(B))
     return tot / B if size_average else tot
+
+
+def hierarchical_ctc_loss(p, cfg, xs, ys, x_lens, y_lens, ys_sub, y_lens_sub):
+    """HierarchicalCTC.forward (hierarchical_ctc.py:267-365): word CTC on the top
+    layer, char CTC on the output of layer num_layers_sub (after its dropout,
+    before any subsampling, rnn.py:400-407); loss = w_main L_main + w_sub L_sub."""
+    xs_t = torch.from_numpy(np.asarray(xs, np.float32))
+    sub_cfg = dict(cfg, num_layers=cfg['num_layers_sub'])
+    top, lens, perm = blstm_encoder(p, 'encoder.', dict(cfg, fast=False), xs_t, x_lens)
+    mid, lens_sub, _ = blstm_encoder(p, 'encoder.', dict(sub_cfg, fast=False), xs_t, x_lens)
+    B = xs.shape[0]
+    terms = []
+    for h, ln, head, y, yl in ((top, lens, 'fc_out', ys, y_lens),
+                               (mid, lens_sub, 'fc_out_sub', ys_sub, y_lens_sub)):
+        logits = linear_nd(p, head, h)
+        ys_s = (np.asarray(y) + 1)[perm]
+        yl_s = np.asarray(yl)[perm]
+        terms.append(ctc_sum(logits, _concat_labels(ys_s, yl_s), yl_s, ln) / B)
+    loss_main = terms[0] * cfg['main_loss_weight']
+    loss_sub = terms[1] * cfg['sub_loss_weight']
+    return loss_main + loss_sub, loss_main, loss_sub
 
 
 def ctc_model_loss(p, cfg, xs, ys, x_lens, y_lens):

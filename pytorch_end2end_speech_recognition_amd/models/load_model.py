@@ -118,6 +118,89 @@ def load(model_type, params, backend='pytorch'):
             model.name += '_charinit'
         return model
 
+    if model_type == 'hierarchical_ctc' or params.get('model_type') == 'hierarchical_ctc':
+        # load_model.py:191-268 (the reference keys this branch on params['model_type'])
+        if 'activation' not in params.keys():
+            params['activation'] = 'relu'
+        from .pytorch_v3.ctc.hierarchical_ctc import HierarchicalCTC
+        model = HierarchicalCTC(
+            input_size=_input_size(params),
+            encoder_type=params['encoder_type'],
+            encoder_bidirectional=params['encoder_bidirectional'],
+            encoder_num_units=params['encoder_num_units'],
+            encoder_num_proj=params['encoder_num_proj'],
+            encoder_num_layers=params['encoder_num_layers'],
+            encoder_num_layers_sub=params['encoder_num_layers_sub'],
+            fc_list=params['fc_list'],
+            fc_list_sub=params['fc_list_sub'],
+            dropout_input=params['dropout_input'],
+            dropout_encoder=params['dropout_encoder'],
+            main_loss_weight=params['main_loss_weight'],
+            sub_loss_weight=params['sub_loss_weight'],
+            num_classes=params['num_classes'],
+            num_classes_sub=params['num_classes_sub'],
+            parameter_init_distribution=params['parameter_init_distribution'],
+            parameter_init=params['parameter_init'],
+            recurrent_weight_orthogonal=params['recurrent_weight_orthogonal'],
+            init_forget_gate_bias_with_one=params['init_forget_gate_bias_with_one'],
+            subsample_list=params['subsample_list'],
+            subsample_type=params['subsample_type'],
+            logits_temperature=params['logits_temperature'],
+            num_stack=params['num_stack'],
+            splice=params['splice'],
+            input_channel=params['input_channel'],
+            conv_channels=params['conv_channels'],
+            conv_kernel_sizes=params['conv_kernel_sizes'],
+            conv_strides=params['conv_strides'],
+            poolings=params['poolings'],
+            activation=params['activation'],
+            batch_norm=params['batch_norm'],
+            label_smoothing_prob=params['label_smoothing_prob'],
+            weight_noise_std=params['weight_noise_std'],
+            encoder_residual=params['encoder_residual'],
+            encoder_dense_residual=params['encoder_dense_residual'])
+        model.name = model_name
+        if params['encoder_type'] not in ['cnn', 'resnet']:
+            model.name += str(params['encoder_num_units']) + 'H'
+            model.name += str(params['encoder_num_layers']) + 'L'
+            model.name += str(params['encoder_num_layers_sub']) + 'L'
+            if params['encoder_num_proj'] != 0:
+                model.name += '_proj' + str(params['encoder_num_proj'])
+            if sum(params['subsample_list']) > 0:
+                model.name += '_' + params['subsample_type'] + \
+                    str(2 ** sum(params['subsample_list']))
+            if params['num_stack'] != 1:
+                model.name += '_stack' + str(params['num_stack'])
+        if len(params['fc_list']) != 0:
+            model.name += '_fc'
+            for l in params['fc_list']:
+                model.name += '_' + str(l)
+        if bool(params['batch_norm']):
+            model.name += '_bn'
+        model.name += '_' + params['optimizer']
+        model.name += '_lr' + str(params['learning_rate'])
+        if params['dropout_encoder'] != 0:
+            model.name += '_drop'
+            if params['dropout_input'] != 0:
+                model.name += 'in' + str(params['dropout_input'])
+            model.name += 'en' + str(params['dropout_encoder'])
+        if params['logits_temperature'] != 1:
+            model.name += '_temp' + str(params['logits_temperature'])
+        if params['label_smoothing_prob'] > 0:
+            model.name += '_ls' + str(params['label_smoothing_prob'])
+        if params['weight_noise_std'] != 0:
+            model.name += '_noise' + str(params['weight_noise_std'])
+        if bool(params['encoder_residual']):
+            model.name += '_res'
+        if bool(params['encoder_dense_residual']):
+            model.name += '_dense_res'
+        model.name += '_main' + str(params['main_loss_weight'])
+        model.name += '_sub' + str(params['sub_loss_weight'])
+        model.name += '_input' + str(model.input_size)
+        if isdir(str(params.get('char_init', ''))):
+            model.name += '_charinit'
+        return model
+
     if model_type == 'attention':
         from .pytorch_v3.attention.attention_seq2seq import AttentionSeq2seq
         model = AttentionSeq2seq(

@@ -51,6 +51,7 @@ class CTC(ModelBase):
         self.encoder_type = encoder_type
         self.encoder_num_units = encoder_num_units * (2 if encoder_bidirectional else 1)
         self.fc_list = fc_list
+        self.fc_list_sub = []
         self.subsample_list = subsample_list
         self.num_classes = num_classes + 1
         self.logits_temperature = logits_temperature
@@ -110,19 +111,7 @@ class CTC(ModelBase):
         if self.logits_temperature != 1:
             logits = logits * (1.0 / self.logits_temperature)
 
-        perm = self.encoder.last_perm_np
-        ys_s = (np.asarray(ys) + 1)[perm]                      # blank = 0 (ctc.py:300)
-        yl_s = np.asarray(y_lens).astype(np.int32)[perm]
-        labels = self.np2var(_concatenate_labels_np(ys_s, yl_s))
-        yl_d = self.np2var(yl_s)
-        max_l = int(yl_s.max()) if len(yl_s) else 0
-        loss, _ = ops.ctc_loss(logits, labels, yl_d, out_lens_d, max_l, loss_scale=1.0 / B)
-
-        if self.ls_prob > 0:                                   # ctc.py:329-337
-            loss_ls = cross_entropy_label_smoothing(
-                logits, y_lens=out_lens_d, label_smoothing_prob=self.ls_prob,
-                distribution='uniform', size_average=False) * (1.0 / B)
-            loss = loss * (1 - self.ls_prob) + loss_ls
+        loss = self._ctc_term(logits, out_lens_d, ys, y_lens, self.encoder.last_perm_np, B)
         if is_eval:
             return float(loss.item())
         return loss
@@ -130,12 +119,34 @@ class CTC(ModelBase):
     def _encode(self, xs, x_lens, is_multi_task=False):
         """ctc.py:344-396."""
         if is_multi_task:
-            raise NotImplementedError('hierarchical CTC is a next-round item')
-        xs, x_lens, perm_idx = self.encoder(xs, x_lens, volatile=not self.training)
+            xs, x_lens, xs_sub, x_lens_sub, perm_idx = self.encoder(
+                xs, x_lens, volatile=not self.training)
+        else:
+            xs, x_lens, perm_idx = self.encoder(xs, x_lens, volatile=not self.training)
         for i in range(len(self.fc_list)):
             xs = getattr(self, 'fc_' + str(i))(xs)
         logits = self.fc_out(xs)
+        if is_multi_task:
+            for i in range(len(self.fc_list_sub)):
+                xs_sub = getattr(self, 'fc_sub_' + str(i))(xs_sub)
+            logits_sub = self.fc_out_sub(xs_sub)
+            return logits, x_lens, logits_sub, x_lens_sub, perm_idx
         return logits, x_lens, perm_idx
+
+    def _ctc_term(self, logits, lens_d, ys, y_lens, perm, B):
+        """sum_b cost_b / B on the HIP CTC kernel (+ label smoothing, ctc.py:319-337)."""
+        ys_s = (np.asarray(ys) + 1)[perm]                      # blank = 0 (ctc.py:300)
+        yl_s = np.asarray(y_lens).astype(np.int32)[perm]
+        labels = self.np2var(_concatenate_labels_np(ys_s, yl_s))
+        yl_d = self.np2var(yl_s)
+        max_l = int(yl_s.max()) if len(yl_s) else 0
+        loss, _ = ops.ctc_loss(logits, labels, yl_d, lens_d, max_l, loss_scale=1.0 / B)
+        if self.ls_prob > 0:
+            loss_ls = cross_entropy_label_smoothing(
+                logits, y_lens=lens_d, label_smoothing_prob=self.ls_prob,
+                distribution='uniform', size_average=False) * (1.0 / B)
+            loss = loss * (1 - self.ls_prob) + loss_ls
+        return loss
 
     def inject_weight_noise(self, mean, std):
         """base.py:85-99 (Gaussian weight noise; not on the default hot path)."""

@@ -50,8 +50,8 @@ class RNNEncoder(nn.Module):
             unsupported.append('subsample_type=concat')
         if residual or dense_residual:
             unsupported.append('residual')
-        if num_layers_sub or nin or merge_bidirectional or not batch_first or not pack_sequence:
-            unsupported.append('num_layers_sub/nin/merge/time-major/no-pack')
+        if nin or merge_bidirectional or not batch_first or not pack_sequence:
+            unsupported.append('nin/merge/time-major/no-pack')
         if unsupported:
             raise NotImplementedError('MI355X RNNEncoder: not yet supported: ' +
                                       ', '.join(unsupported))
@@ -87,7 +87,7 @@ class RNNEncoder(nn.Module):
         self.input_size = input_size
 
         # rnn.py:162 (batch_norm forces the per-layer modules, as in the reference)
-        self.fast_impl = sum(self.subsample_list) == 0 and not batch_norm
+        self.fast_impl = sum(self.subsample_list) == 0 and not batch_norm and num_layers_sub == 0
         if self.fast_impl:   # rnn.py:162-198: one multi-layer nn.LSTM
             self.lstm = nn.LSTM(input_size, hidden_size=num_units, num_layers=num_layers,
                                 bias=True, batch_first=batch_first, dropout=dropout_hidden,
@@ -151,6 +151,7 @@ class RNNEncoder(nn.Module):
         perm_d = torch.from_numpy(perm.astype(np.int32)).to(dev, non_blocking=True)
         T = int(lens.max())                                          # pad_packed length
         h, pm, t_mul, t_add = xs.contiguous(), perm_d, 1, 0
+        h_sub = lens_sub = None
         for l in range(self.num_layers):
             (w_ih, w_hh, b_ih, b_hh), gbufs = self._layer_tensors(l)
             lens_d = torch.from_numpy(lens.astype(np.int32)).to(dev, non_blocking=True)
@@ -159,6 +160,8 @@ class RNNEncoder(nn.Module):
                                 t_add=t_add, gbufs=tuple(gbufs), graph_params=graph)
             if self.training and self.dropout_hidden_p > 0:
                 h = ops.dropout(h, self.dropout_hidden_p)
+            if self.num_layers_sub >= 1 and l == self.num_layers_sub - 1:   # rnn.py:400-407
+                h_sub, lens_sub = h, lens.astype(np.int32)
             pm, t_mul, t_add = None, 1, 0
             if l != self.num_layers - 1 and self.subsample_list[l]:  # rnn.py:413-439
                 T = T // 2
@@ -169,4 +172,8 @@ class RNNEncoder(nn.Module):
         self.last_perm_np = perm.astype(np.int64)
         out_lens = torch.from_numpy(self.last_lens_np).to(dev, non_blocking=True)
         perm_idx = torch.from_numpy(self.last_perm_np).to(dev, non_blocking=True)
+        if self.num_layers_sub >= 1:                              # rnn.py:479-487
+            self.last_lens_sub_np = lens_sub
+            lens_sub_d = torch.from_numpy(lens_sub).to(dev, non_blocking=True)
+            return h, out_lens, h_sub, lens_sub_d, perm_idx
         return h, out_lens, perm_idx

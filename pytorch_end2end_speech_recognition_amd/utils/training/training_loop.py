@@ -49,6 +49,8 @@ def shard_batch(batch, rank, world):
     local['xs'] = local['xs'][:, :tmax]
     if 'ys' in local and 'y_lens' in local:
         local['ys'] = local['ys'][:, :max(1, int(np.max(local['y_lens'])))]
+    if 'ys_sub' in local and 'y_lens_sub' in local:
+        local['ys_sub'] = local['ys_sub'][:, :max(1, int(np.max(local['y_lens_sub'])))]
     return local, float(len(idx)) / float(B)
 
 
@@ -60,33 +62,29 @@ def allreduce_gradients(model, grad_scale=None):
             model._flat_grad.mul_(grad_scale)
 
 
-def train_step(model, batch, clip_grad_norm, backend='pytorch', grad_scale=None):
-    """Returns (model, loss_value) like training_loop.py:27-83.
-
-    grad_scale: optional factor applied to the all-reduced gradient (data
-    parallel: pass local_batch / global_batch when every rank divides its loss
-    by its local batch size, so the update equals the 1-GPU update)."""
-    loss_val = 0.
+def _step(model, forward, clip_grad_norm, n_losses, grad_scale):
+    """zero_grad -> forward (returns n_losses loss tensors, the first is the
+    total) -> backward -> collective skip flag -> gradient all-reduce ->
+    fused clip + optimizer step.  Returns the losses as floats (0 on skip)."""
     ok = 1
     try:
         # ModelBase.zero_grad zeroes the flat gradient and re-binds every
         # param.grad view (torch.optim's zero_grad would set them to None and
         # detach them from the buffer the all-reduce / fused step work on)
         model.zero_grad()
-        loss = model(batch['xs'], batch['ys'], batch['x_lens'], batch['y_lens'])
-        loss.backward()
+        losses = forward()
+        losses[0].backward()
     except RuntimeError as e:
-        logger.warning('!!!Skip mini-batch!!! (max_frame_num: %d, batch: %d) %s' %
-                       (max(batch['x_lens']) * model.num_stack, len(batch['xs']), e))
+        logger.warning('!!!Skip mini-batch!!! %s' % e)
         ok = 0
-        loss = None
+        losses = None
     if _world() > 1:
         flag = torch.tensor([ok], dtype=torch.int32, device=model.device)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         ok = int(flag.item())
     if not ok:
         model.zero_grad()
-        return model, 0.
+        return [0.] * n_losses
     allreduce_gradients(model, grad_scale)
     if hasattr(model.optimizer, 'clip_and_step'):
         model.optimizer.clip_and_step(clip_grad_norm if clip_grad_norm > 0 else 0.0)
@@ -94,8 +92,28 @@ def train_step(model, batch, clip_grad_norm, backend='pytorch', grad_scale=None)
         if clip_grad_norm > 0:
             torch.nn.utils.clip_grad_norm_(model.parameters(), clip_grad_norm)
         model.optimizer.step()
-    loss_val = float(loss.item())
-    if loss_val == INF or loss_val == -INF:
+    vals = [float(l.item()) for l in losses]
+    if vals[0] == INF or vals[0] == -INF:
         logger.warning('WARNING: received an inf loss, setting loss value to 0.')
-        loss_val = 0
-    return model, loss_val
+        vals = [0.] * n_losses
+    return vals
+
+
+def train_step(model, batch, clip_grad_norm, backend='pytorch', grad_scale=None):
+    """Returns (model, loss_value) like training_loop.py:27-83.
+
+    grad_scale: optional factor applied to the all-reduced gradient (data
+    parallel: pass local_batch / global_batch when every rank divides its loss
+    by its local batch size, so the update equals the 1-GPU update)."""
+    vals = _step(model, lambda: [model(batch['xs'], batch['ys'], batch['x_lens'],
+                                       batch['y_lens'])], clip_grad_norm, 1, grad_scale)
+    return model, vals[0]
+
+
+def train_hierarchical_step(model, batch, clip_grad_norm, backend='pytorch', grad_scale=None):
+    """Returns (model, loss, loss_main, loss_sub) like training_loop.py:86-153
+    (batch carries ys_sub / y_lens_sub for the sub task)."""
+    vals = _step(model, lambda: list(model(batch['xs'], batch['ys'], batch['x_lens'],
+                                           batch['y_lens'], batch['ys_sub'],
+                                           batch['y_lens_sub'])), clip_grad_norm, 3, grad_scale)
+    return (model,) + tuple(vals)

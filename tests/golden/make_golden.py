@@ -324,6 +324,45 @@ def case_vgg_model():
 
 
 # --------------------------------------------------------------------------
+# Case 4c: hierarchical CTC (word CTC on top, char CTC on layer num_layers_sub)
+# --------------------------------------------------------------------------
+def case_hier_ctc_model():
+    from models.pytorch_v3.ctc.hierarchical_ctc import HierarchicalCTC
+    base = dict(input_size=16, encoder_type='lstm', encoder_bidirectional=True,
+                encoder_num_units=6, encoder_num_proj=0, encoder_num_layers=3,
+                encoder_num_layers_sub=2, fc_list=[], fc_list_sub=[], dropout_input=0,
+                dropout_encoder=0, main_loss_weight=0.5, sub_loss_weight=0.5, num_classes=9,
+                num_classes_sub=5, parameter_init=0.1, subsample_list=[], subsample_type='drop')
+    specs = [('model_hier', base),
+             ('model_hier_vgg', dict(base, main_loss_weight=0.7, sub_loss_weight=0.3,
+                                     conv_channels=[4, 4, 16, 16],
+                                     conv_kernel_sizes=[[3, 3]] * 4, conv_strides=[[1, 1]] * 4,
+                                     poolings=[[], [2, 2], [], [2, 2]], batch_norm=True,
+                                     activation='relu'))]
+    for name, kw in specs:
+        torch.manual_seed(1623)
+        model = HierarchicalCTC(**kw)
+        model.train()
+        sd0 = _sd(model)
+        rng = np.random.RandomState(6)
+        B, T = 3, 26
+        x_lens = np.array([26, 21, 13], np.int32)
+        y_lens = np.array([2, 3, 1], np.int32)
+        y_lens_sub = np.array([5, 4, 3], np.int32)
+        xs, ys = _batch(rng, B, T, 16, y_lens, 9, x_lens)
+        ys_sub = np.full((B, 5), -1, np.int32)
+        for b in range(B):
+            ys_sub[b, :y_lens_sub[b]] = rng.randint(0, 5, y_lens_sub[b])
+        loss, loss_main, loss_sub = model(xs, ys, x_lens, y_lens, ys_sub, y_lens_sub)
+        loss.backward()
+        _save(name, kwargs=np.array(json.dumps(kw)), xs=xs, ys=ys, x_lens=x_lens,
+              y_lens=y_lens, ys_sub=ys_sub, y_lens_sub=y_lens_sub,
+              loss=loss.detach().numpy().reshape(1),
+              loss_main=loss_main.detach().numpy().reshape(1),
+              loss_sub=loss_sub.detach().numpy().reshape(1), **sd0, **_grads(model))
+
+
+# --------------------------------------------------------------------------
 # Case 5: attention enc-dec (location, bahdanau) with / without auxiliary CTC
 # --------------------------------------------------------------------------
 def case_attention_model():
@@ -367,4 +406,5 @@ if __name__ == '__main__':
     case_attention_step()
     case_ctc_model()
     case_vgg_model()
+    case_hier_ctc_model()
     case_attention_model()
