@@ -33,7 +33,8 @@ sys.path.insert(0, ROOT)
 from pytorch_end2end_speech_recognition_amd import _native as N  # noqa: E402
 from pytorch_end2end_speech_recognition_amd import native_ops  # noqa: E402
 from pytorch_end2end_speech_recognition_amd.models.load_model import load  # noqa: E402
-from pytorch_end2end_speech_recognition_amd.utils.training.training_loop import train_step  # noqa
+from pytorch_end2end_speech_recognition_amd.utils.training.training_loop import (  # noqa: E402
+    train_hierarchical_step, train_step)
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
 BF16_PEAK_TFLOPS = 2500.0    # dense bf16 MFMA (spec, no sparsity)
@@ -78,6 +79,24 @@ CONFIGS['hybrid4x320'] = dict(workload='librispeech_char_hybrid_ctc0.3_attention
                               model_type='attention', params=None, ctc_weight=0.3)
 
 
+CONFIGS['vgg_hier'] = dict(
+    workload='swbd_vgg_blstm4x320_hierarchical_word10k_char_ctc', model_type='hierarchical_ctc',
+    params=dict(
+        input_freq=80, use_delta=False, use_double_delta=False, input_channel=1, splice=1,
+        num_stack=1, encoder_type='lstm', conv_channels=[64, 64, 128, 128],
+        conv_kernel_sizes=[[3, 3]] * 4, conv_strides=[[1, 1]] * 4,
+        poolings=[[], [2, 2], [], [2, 2]], activation='relu', batch_norm=True,
+        encoder_bidirectional=True, encoder_residual=False, encoder_dense_residual=False,
+        encoder_num_units=320, encoder_num_proj=0, encoder_num_layers=4,
+        encoder_num_layers_sub=3, subsample_list=[], subsample_type='drop', fc_list=[],
+        fc_list_sub=[], main_loss_weight=0.5, sub_loss_weight=0.5, optimizer='adam',
+        learning_rate=1e-3, parameter_init_distribution='uniform', parameter_init=0.1,
+        recurrent_weight_orthogonal=False, init_forget_gate_bias_with_one=True, char_init=False,
+        clip_grad_norm=5.0, dropout_input=0, dropout_encoder=0.2, weight_decay=1e-6,
+        logits_temperature=1, label_smoothing_prob=0, weight_noise_std=0,
+        num_classes=10000, num_classes_sub=28))
+
+
 def config_params(cfg):
     if cfg['params'] is None:
         cfg['params'] = _attention_params(cfg['ctc_weight'])
@@ -97,6 +116,20 @@ def synthetic_batch(B, T, F, num_classes, seed):
     for b in range(B):
         ys[b, :y_lens[b]] = rng.randint(0, num_classes, y_lens[b])
     return dict(xs=xs, ys=ys, x_lens=x_lens, y_lens=y_lens)
+
+
+def synthetic_hier_batch(B, T, F, num_words, num_chars, seed):
+    """configs[4]: word targets (U[10, 25] words of a synthetic 10k vocabulary)
+    for the main CTC, char targets (U[60, 125]) for the sub-task CTC."""
+    batch = synthetic_batch(B, T, F, num_chars, seed)
+    batch['ys_sub'], batch['y_lens_sub'] = batch.pop('ys'), batch.pop('y_lens')
+    rng = np.random.RandomState(seed + 7919)
+    y_lens = rng.randint(10, 26, B).astype(np.int32)
+    ys = np.full((B, int(y_lens.max())), -1, np.int32)
+    for b in range(B):
+        ys[b, :y_lens[b]] = rng.randint(0, num_words, y_lens[b])
+    batch['ys'], batch['y_lens'] = ys, y_lens
+    return batch
 
 
 def roofline_report(args, p, mean_us, launches, mean_work, workload):
@@ -209,14 +242,25 @@ def cpu_baseline(cfg, batch, n_utts):
     p = config_params(cfg)
     torch.manual_seed(0)
     model = load(cfg['model_type'], dict(p), 'pytorch')           # host-side init only
-    sd = {k: v.detach().clone().requires_grad_(True) for k, v in model.state_dict().items()}
-    opt = torch.optim.Adam(list(sd.values()), lr=p['learning_rate'],
-                           weight_decay=p['weight_decay'])
+    sd = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    trainable = [v.requires_grad_(True) for k, v in sd.items()
+                 if v.is_floating_point() and 'running' not in k]
+    opt = torch.optim.Adam(trainable, lr=p['learning_rate'], weight_decay=p['weight_decay'])
     sub = {k: v[:n_utts] for k, v in batch.items()}
     sub['ys'] = sub['ys'][:, :int(sub['y_lens'].max())]
+    if 'ys_sub' in sub:
+        sub['ys_sub'] = sub['ys_sub'][:, :int(sub['y_lens_sub'].max())]
     t0 = time.perf_counter()
     opt.zero_grad()
-    if cfg['model_type'] == 'attention':   # oracle decoder: teacher forcing, no dropout
+    if cfg['model_type'] == 'hierarchical_ctc':
+        ocfg = dict(num_layers=p['encoder_num_layers'], num_layers_sub=p['encoder_num_layers_sub'],
+                    subsample_list=p['subsample_list'], conv_channels=p['conv_channels'],
+                    poolings=p['poolings'], batch_norm=p['batch_norm'],
+                    main_loss_weight=p['main_loss_weight'], sub_loss_weight=p['sub_loss_weight'])
+        loss, _, _ = asr_ref.hierarchical_ctc_loss(sd, ocfg, sub['xs'], sub['ys'], sub['x_lens'],
+                                                   sub['y_lens'], sub['ys_sub'],
+                                                   sub['y_lens_sub'])
+    elif cfg['model_type'] == 'attention':   # oracle decoder: teacher forcing, no dropout
         loss = asr_ref.attention_model_loss(sd, p, sub['xs'], sub['ys'], sub['x_lens'],
                                             sub['y_lens'])
     else:
@@ -225,7 +269,7 @@ def cpu_baseline(cfg, batch, n_utts):
         loss, _, _, _ = asr_ref.ctc_model_loss(sd, ocfg, sub['xs'], sub['ys'], sub['x_lens'],
                                                sub['y_lens'])
     loss.backward()
-    torch.nn.utils.clip_grad_norm_(list(sd.values()), p['clip_grad_norm'])
+    torch.nn.utils.clip_grad_norm_(trainable, p['clip_grad_norm'])
     opt.step()
     dt = time.perf_counter() - t0
     frames = float(np.sum(sub['x_lens']))
@@ -272,12 +316,23 @@ def main():
     model.set_precision(args.precision)
     model.set_optimizer(p['optimizer'], p['learning_rate'], weight_decay=p['weight_decay'],
                         lr_schedule=False)
-    batch = synthetic_batch(args.batch, args.frames, p['input_freq'], p['num_classes'],
-                            seed=rank)
+    if cfg['model_type'] == 'hierarchical_ctc':
+        batch = synthetic_hier_batch(args.batch, args.frames, p['input_freq'], p['num_classes'],
+                                     p['num_classes_sub'], seed=rank)
+
+        def step(m, b):
+            m, lv, _, _ = train_hierarchical_step(m, b, p['clip_grad_norm'])
+            return m, lv
+    else:
+        batch = synthetic_batch(args.batch, args.frames, p['input_freq'], p['num_classes'],
+                                seed=rank)
+
+        def step(m, b):
+            return train_step(m, b, p['clip_grad_norm'])
     frames_per_step = float(batch['x_lens'].sum())
 
     for _ in range(args.warmup):
-        model, _ = train_step(model, batch, p['clip_grad_norm'])
+        model, _ = step(model, batch)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -286,7 +341,7 @@ def main():
     t0 = time.perf_counter()
     losses = []
     for _ in range(args.steps):
-        model, lv = train_step(model, batch, p['clip_grad_norm'])
+        model, lv = step(model, batch)
         losses.append(lv)
     torch.cuda.synchronize()
     if world > 1:

@@ -425,12 +425,22 @@ int asr_attdec_backward_ex(const asr_attdec_dims_t* dims, const asr_attdec_opts_
  *   momentum / unbiased variance; or eval with running stats) + dropout (asr
  *   dropout RNG, index = element of [B][T'][F'][C]).  See cnn.hip. */
 int asr_vgg_pad_input(const float* xs, int B, int T, int F, float* out, void* stream);
+/* ... as a Cp-channel image (channel 0 = xs, the rest 0; out_dtype f32 / bf16):
+ * the first conv layer on the GEMM path with its one input channel padded to 16 */
+int asr_vgg_pad_input_ch(const float* xs, int B, int T, int F, int Cp, int out_dtype, void* out,
+                         void* stream);
 /* GEMM images of a Conv2d weight W [Co][Ci][3][3] (tap j = kw*3 + kh):
  * mode 0 out[co][j*Ci + ci] (forward B operand), mode 1 out[ci][j*Co + co]
  * (input-gradient B operand); unpack_acc: dW [Co][Ci][3][3] += [Co][9 Ci]. */
 int asr_conv_weight_pack(const float* w, int Co, int Ci, int mode, int out_dtype, void* out,
                          void* stream);
 int asr_conv_weight_unpack_acc(const float* packed, int Co, int Ci, float* dw, void* stream);
+/* mode-0 image / unpack with an input-channel pitch Cip >= Ci (padded channels
+ * stay as the caller zeroed them) */
+int asr_conv_weight_pack_pad(const float* w, int Co, int Ci, int Cip, int mode, int out_dtype,
+                             void* out, void* stream);
+int asr_conv_weight_unpack_acc_pad(const float* packed, int Co, int Ci, int Cip, float* dw,
+                                   void* stream);
 /* Direct 3x3 convolution (layers the tap-addressed GEMM cannot take: C_in = 1,
  * channel counts not multiples of 16): x [padded pixels][Ci] f32, w the torch
  * weight [Co][Ci][3][3]; z / dx over valid pixels; dw / dbias accumulate. */

@@ -88,6 +88,9 @@ SIGNATURES = {
                                [c_size, c_vp]),
     'asr_vgg_pad_input': (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp]),
     'asr_conv_weight_pack': (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp]),
+    'asr_vgg_pad_input_ch': (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp]),
+    'asr_conv_weight_pack_pad': (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp]),
+    'asr_conv_weight_unpack_acc_pad': (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp]),
     'asr_conv_weight_unpack_acc': (c_int, [c_vp, c_int, c_int, c_vp, c_vp]),
     'asr_conv_direct_forward': (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp,
                                         c_vp, c_vp]),

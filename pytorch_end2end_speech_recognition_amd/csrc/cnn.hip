@@ -32,17 +32,25 @@ __device__ __forceinline__ long long pad_row(int b, int t, int f, int T, int F) 
   return ((long long)b * (T + 2) + (t + 1)) * (F + 2) + (f + 1);
 }
 
-__global__ void vgg_pad_input(const float* __restrict__ xs, int B, int T, int F,
-                              float* __restrict__ out) {
-  const long long n = (long long)B * (T + 2) * (F + 2);
+// out[b][t+1][f+1][c] = xs[b][t][f] for c = 0, 0 for c < Cp and on the halo
+// (the input plane as a Cp-channel padded image, Cp = 1 or 16 for the GEMM path)
+template <typename TO>
+__global__ void vgg_pad_input(const float* __restrict__ xs, int B, int T, int F, int Cp,
+                              TO* __restrict__ out) {
+  const long long n = (long long)B * (T + 2) * (F + 2) * Cp;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x) {
-    const int fp = (int)(i % (F + 2));
-    const long long q = i / (F + 2);
+    const int c = (int)(i % Cp);
+    const long long pix = i / Cp;
+    const int fp = (int)(pix % (F + 2));
+    const long long q = pix / (F + 2);
     const int tp = (int)(q % (T + 2));
     const int b = (int)(q / (T + 2));
     const int t = tp - 1, f = fp - 1;
-    out[i] = (t >= 0 && t < T && f >= 0 && f < F) ? xs[((long long)b * T + t) * F + f] : 0.f;
+    const float v = (c == 0 && t >= 0 && t < T && f >= 0 && f < F)
+                        ? xs[((long long)b * T + t) * F + f] : 0.f;
+    if constexpr (sizeof(TO) == 2) out[i] = f2bf(v);
+    else out[i] = v;
   }
 }
 
@@ -167,30 +175,66 @@ __global__ void post_fwd(const float* __restrict__ z, int B, int T, int F, int C
 }
 
 // Column statistics of X [n][C] in fixed chunk order: partial[chunk][c] =
-// sum over the chunk of (x - shift[c]) (shift = nullptr: 0) or of its square.
-__global__ void col_moment(const float* __restrict__ X, long long n, int C, long long rows_per,
-                           const float* __restrict__ shift, int square,
-                           float* __restrict__ partial) {
+// sum over the chunk's rows of (x - shift[c]) (shift = nullptr: 0) or of its
+// square.  The block's threads split the rows into CT / C interleaved phases
+// (C divides CT), four accumulators each; phases combine in LDS in order.
+__global__ void __launch_bounds__(CT) col_moment(const float* __restrict__ X, long long n, int C,
+                                                 long long rows_per,
+                                                 const float* __restrict__ shift, int square,
+                                                 float* __restrict__ partial) {
+  __shared__ float red[CT];
   const long long r0 = (long long)blockIdx.x * rows_per;
   const long long r1 = min(n, r0 + rows_per);
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+  const int tid = threadIdx.x;
+  const int ph = CT / C, c = tid % C, q = tid / C;
+  float acc = 0.f;
+  if (q < ph) {
     const float m = shift ? shift[c] : 0.f;
-    float s = 0.f;
-    for (long long r = r0; r < r1; ++r) {
-      const float d = X[r * C + c] - m;
-      s += square ? d * d : d;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    long long r = r0 + q;
+    for (; r + 3 * ph < r1; r += 4 * ph) {
+      const float d0 = X[r * C + c] - m, d1 = X[(r + ph) * C + c] - m;
+      const float d2 = X[(r + 2 * ph) * C + c] - m, d3 = X[(r + 3 * ph) * C + c] - m;
+      s0 += square ? d0 * d0 : d0;
+      s1 += square ? d1 * d1 : d1;
+      s2 += square ? d2 * d2 : d2;
+      s3 += square ? d3 * d3 : d3;
     }
-    partial[(long long)blockIdx.x * C + c] = s;
+    for (; r < r1; r += ph) {
+      const float d = X[r * C + c] - m;
+      s0 += square ? d * d : d;
+    }
+    acc = (s0 + s1) + (s2 + s3);
+  }
+  red[tid] = acc;
+  __syncthreads();
+  if (tid < C) {
+    float t = 0.f;
+    for (int j = 0; j < ph; ++j) t += red[j * C + tid];
+    partial[(long long)blockIdx.x * C + tid] = t;
   }
 }
 
-__global__ void sum_partials(const float* __restrict__ partial, int nchunk, int C, float scale,
-                             float* __restrict__ out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float s = 0.f;
-  for (int q = 0; q < nchunk; ++q) s += partial[(long long)q * C + c];
-  out[c] = s * scale;
+// out[c] = scale * sum_q partial[q][c], fixed order: 4 interleaved phases per
+// column (64 columns per block), combined in LDS.
+__global__ void __launch_bounds__(CT) sum_partials(const float* __restrict__ partial, int nchunk,
+                                                   int C, float scale, float* __restrict__ out) {
+  __shared__ float red[CT];
+  const int tid = threadIdx.x;
+  const int cl = tid & 63, q0 = tid >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  float s0 = 0.f, s1 = 0.f;
+  if (c < C) {
+    int q = q0;
+    for (; q + 4 < nchunk; q += 8) {
+      s0 += partial[(long long)q * C + c];
+      s1 += partial[(long long)(q + 4) * C + c];
+    }
+    for (; q < nchunk; q += 4) s0 += partial[(long long)q * C + c];
+  }
+  red[tid] = s0 + s1;
+  __syncthreads();
+  if (q0 == 0 && c < C) out[c] = (red[cl] + red[64 + cl] + red[128 + cl] + red[192 + cl]) * scale;
 }
 
 // mean -> (mean, rstd) from the centred second moment; running stats update
@@ -271,40 +315,50 @@ __device__ __forceinline__ float dy_at(const float* __restrict__ dnext, long lon
   return g;
 }
 
-// partial sums per channel of dy and dy * xhat over row chunks
-__global__ void bn_bwd_moments(const float* __restrict__ dnext, const float* __restrict__ P,
-                               int B, int To, int Fo, int C, int flat, Affine af,
-                               long long rows_per, float* __restrict__ partial) {
+// partial[chunk][c] = sum dy, partial[chunk][C + c] = sum dy * xhat over the
+// chunk's rows (row phases as col_moment)
+__global__ void __launch_bounds__(CT) bn_bwd_moments(const float* __restrict__ dnext,
+                                                     const float* __restrict__ P, int B, int To,
+                                                     int Fo, int C, int flat, Affine af,
+                                                     long long rows_per,
+                                                     float* __restrict__ partial) {
+  __shared__ float red[2 * CT];
   const long long n = (long long)B * To * Fo;
   const long long r0 = (long long)blockIdx.x * rows_per;
   const long long r1 = min(n, r0 + rows_per);
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float s1 = 0.f, s2 = 0.f;
-    for (long long r = r0; r < r1; ++r) {
+  const int tid = threadIdx.x;
+  const int ph = CT / C, c = tid % C, q = tid / C;
+  float s1 = 0.f, s2 = 0.f;
+  if (q < ph) {
+    const float m = af.mean[c], rs = af.rstd[c];
+    for (long long r = r0 + q; r < r1; r += ph) {
       const long long i = r * C + c;
       const float g = dy_at(dnext, i, To, Fo, C, flat, af.drop, af.seed);
       s1 += g;
-      s2 += g * (P[i] - af.mean[c]) * af.rstd[c];
+      s2 += g * (P[i] - m) * rs;
     }
-    partial[((long long)blockIdx.x * 2) * C + c] = s1;
-    partial[((long long)blockIdx.x * 2 + 1) * C + c] = s2;
+  }
+  red[tid] = s1;
+  red[CT + tid] = s2;
+  __syncthreads();
+  if (tid < C) {
+    float t1 = 0.f, t2 = 0.f;
+    for (int j = 0; j < ph; ++j) {
+      t1 += red[j * C + tid];
+      t2 += red[CT + j * C + tid];
+    }
+    partial[((long long)blockIdx.x * 2) * C + tid] = t1;
+    partial[((long long)blockIdx.x * 2 + 1) * C + tid] = t2;
   }
 }
 
-__global__ void bn_bwd_finalize(const float* __restrict__ partial, int nchunk, int C,
-                                float* __restrict__ sums, float* __restrict__ dgamma,
+// sums [2C] (sum dy, sum dy xhat) -> dgamma += sum dy xhat, dbeta += sum dy
+__global__ void bn_bwd_finalize(const float* __restrict__ sums, int C, float* __restrict__ dgamma,
                                 float* __restrict__ dbeta) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  float s1 = 0.f, s2 = 0.f;
-  for (int q = 0; q < nchunk; ++q) {
-    s1 += partial[((long long)q * 2) * C + c];
-    s2 += partial[((long long)q * 2 + 1) * C + c];
-  }
-  sums[c] = s1;
-  sums[C + c] = s2;
-  if (dgamma) dgamma[c] += s2;
-  if (dbeta) dbeta[c] += s1;
+  if (dgamma) dgamma[c] += sums[C + c];
+  if (dbeta) dbeta[c] += sums[c];
 }
 
 // dP = BN backward (or dy without BN); routed to the pooled-from pixel if its
@@ -346,8 +400,10 @@ __global__ void post_bwd(const float* __restrict__ dnext, const float* __restric
 // j = kw*3 + kh (the row shift (kw-1)(F+2) + (kh-1) of gemm.hip tap addressing):
 //   mode 0 (forward):  out[co][j*Ci + ci] = W[co][ci][kh][kw]
 //   mode 1 (d input):  out[ci][j*Co + co] = W[co][ci][kh][kw]
+// (Cip >= Ci: the image's input-channel pitch; padded channels are left as the
+// caller zeroed them)
 template <typename TO>
-__global__ void weight_pack(const float* __restrict__ w, int Co, int Ci, int mode,
+__global__ void weight_pack(const float* __restrict__ w, int Co, int Ci, int Cip, int mode,
                             TO* __restrict__ out) {
   const long long n = (long long)Co * Ci * 9;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
@@ -355,7 +411,7 @@ __global__ void weight_pack(const float* __restrict__ w, int Co, int Ci, int mod
     const int kw = (int)(i % 3), kh = (int)((i / 3) % 3);
     const int ci = (int)((i / 9) % Ci), co = (int)(i / (9LL * Ci));
     const int j = kw * 3 + kh;
-    const long long o = mode == 0 ? ((long long)co * 9 + j) * Ci + ci
+    const long long o = mode == 0 ? ((long long)co * 9 + j) * Cip + ci
                                   : ((long long)ci * 9 + j) * Co + co;
     if constexpr (sizeof(TO) == 2) out[o] = f2bf(w[i]);
     else out[o] = w[i];
@@ -363,14 +419,14 @@ __global__ void weight_pack(const float* __restrict__ w, int Co, int Ci, int mod
 }
 
 // dW [Co][Ci][3][3] += packed [Co][9 Ci] (mode-0 image layout)
-__global__ void weight_unpack_acc(const float* __restrict__ pk, int Co, int Ci,
+__global__ void weight_unpack_acc(const float* __restrict__ pk, int Co, int Ci, int Cip,
                                   float* __restrict__ dw) {
   const long long n = (long long)Co * Ci * 9;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x) {
     const int kw = (int)(i % 3), kh = (int)((i / 3) % 3);
     const int ci = (int)((i / 9) % Ci), co = (int)(i / (9LL * Ci));
-    dw[i] += pk[((long long)co * 9 + kw * 3 + kh) * Ci + ci];
+    dw[i] += pk[((long long)co * 9 + kw * 3 + kh) * Cip + ci];
   }
 }
 
@@ -404,34 +460,66 @@ Pool make_pool(int T, int F, int pt, int pf, int ceil_mode) {
 
 using namespace asr;
 
+extern "C" int asr_vgg_pad_input_ch(const float* xs, int B, int T, int F, int Cp, int out_dtype,
+                                    void* out, void* stream);
+
 extern "C" int asr_vgg_pad_input(const float* xs, int B, int T, int F, float* out, void* stream) {
-  ASR_REQUIRE(xs && out && B > 0 && T > 0 && F > 0, ASR_ERR_ARG, "vgg_pad_input: bad args");
-  hipLaunchKernelGGL(vgg_pad_input, dim3(grid_for((long long)B * (T + 2) * (F + 2))), dim3(CT),
-                     0, (hipStream_t)stream, xs, B, T, F, out);
+  return asr_vgg_pad_input_ch(xs, B, T, F, 1, ASR_DT_F32, out, stream);
+}
+
+extern "C" int asr_vgg_pad_input_ch(const float* xs, int B, int T, int F, int Cp, int out_dtype,
+                                    void* out, void* stream) {
+  ASR_REQUIRE(xs && out && B > 0 && T > 0 && F > 0 && Cp > 0, ASR_ERR_ARG,
+              "vgg_pad_input: bad args");
+  const long long n = (long long)B * (T + 2) * (F + 2) * Cp;
+  if (out_dtype == ASR_DT_BF16)
+    hipLaunchKernelGGL((vgg_pad_input<uint16_t>), dim3(grid_for(n)), dim3(CT), 0,
+                       (hipStream_t)stream, xs, B, T, F, Cp, (uint16_t*)out);
+  else
+    hipLaunchKernelGGL((vgg_pad_input<float>), dim3(grid_for(n)), dim3(CT), 0,
+                       (hipStream_t)stream, xs, B, T, F, Cp, (float*)out);
   ASR_LAUNCH_CHECK();
   return ASR_OK;
 }
 
+extern "C" int asr_conv_weight_pack_pad(const float* w, int Co, int Ci, int Cip, int mode,
+                                        int out_dtype, void* out, void* stream);
+extern "C" int asr_conv_weight_unpack_acc_pad(const float* packed, int Co, int Ci, int Cip,
+                                              float* dw, void* stream);
+
 extern "C" int asr_conv_weight_pack(const float* w, int Co, int Ci, int mode, int out_dtype,
                                     void* out, void* stream) {
+  return asr_conv_weight_pack_pad(w, Co, Ci, Ci, mode, out_dtype, out, stream);
+}
+
+extern "C" int asr_conv_weight_pack_pad(const float* w, int Co, int Ci, int Cip, int mode,
+                                        int out_dtype, void* out, void* stream) {
   ASR_REQUIRE(w && out && Co > 0 && Ci > 0 && (mode == 0 || mode == 1), ASR_ERR_ARG,
               "conv_weight_pack: bad args");
+  ASR_REQUIRE(Cip >= Ci && (mode == 0 || Cip == Ci), ASR_ERR_ARG,
+              "conv_weight_pack: channel pitch %d < %d (or padded mode 1)", Cip, Ci);
   const long long n = (long long)Co * Ci * 9;
   if (out_dtype == ASR_DT_BF16)
     hipLaunchKernelGGL((weight_pack<uint16_t>), dim3(grid_for(n)), dim3(CT), 0,
-                       (hipStream_t)stream, w, Co, Ci, mode, (uint16_t*)out);
+                       (hipStream_t)stream, w, Co, Ci, Cip, mode, (uint16_t*)out);
   else
     hipLaunchKernelGGL((weight_pack<float>), dim3(grid_for(n)), dim3(CT), 0, (hipStream_t)stream,
-                       w, Co, Ci, mode, (float*)out);
+                       w, Co, Ci, Cip, mode, (float*)out);
   ASR_LAUNCH_CHECK();
   return ASR_OK;
 }
 
 extern "C" int asr_conv_weight_unpack_acc(const float* packed, int Co, int Ci, float* dw,
                                           void* stream) {
-  ASR_REQUIRE(packed && dw && Co > 0 && Ci > 0, ASR_ERR_ARG, "conv_weight_unpack_acc: bad args");
+  return asr_conv_weight_unpack_acc_pad(packed, Co, Ci, Ci, dw, stream);
+}
+
+extern "C" int asr_conv_weight_unpack_acc_pad(const float* packed, int Co, int Ci, int Cip,
+                                              float* dw, void* stream) {
+  ASR_REQUIRE(packed && dw && Co > 0 && Ci > 0 && Cip >= Ci, ASR_ERR_ARG,
+              "conv_weight_unpack_acc: bad args");
   hipLaunchKernelGGL(weight_unpack_acc, dim3(grid_for((long long)Co * Ci * 9)), dim3(CT), 0,
-                     (hipStream_t)stream, packed, Co, Ci, dw);
+                     (hipStream_t)stream, packed, Co, Ci, Cip, dw);
   ASR_LAUNCH_CHECK();
   return ASR_OK;
 }
@@ -499,7 +587,7 @@ extern "C" int asr_conv_direct_wgrad(const float* x, const float* dz, int B, int
                      (int)per, part);
   ASR_LAUNCH_CHECK();
   // row 0 <- column totals (each column is read entirely before its thread writes it)
-  hipLaunchKernelGGL(sum_partials, dim3((nout + CT - 1) / CT), dim3(CT), 0, s, part, nchunk, nout,
+  hipLaunchKernelGGL(sum_partials, dim3((nout + 63) / 64), dim3(CT), 0, s, part, nchunk, nout,
                      1.f, part);
   ASR_LAUNCH_CHECK();
   return asr_vgg_accumulate(part, dw, Co * Ci * 9, dbias ? part + Co * Ci * 9 : nullptr, dbias,
@@ -539,6 +627,8 @@ extern "C" int asr_vgg_block_forward(const float* z, int B, int T, int F, int C,
   ASR_REQUIRE(!pt || slot, ASR_ERR_ARG, "vgg_block_forward: pooling needs slot");
   const Pool pl = make_pool(T, F, pt, pf, ceil_mode);
   ASR_REQUIRE(pl.To > 0 && pl.Fo > 0, ASR_ERR_ARG, "vgg_block_forward: empty output");
+  ASR_REQUIRE(C <= CT && CT % C == 0, ASR_ERR_UNSUPPORTED,
+              "vgg_block_forward: channels %d must divide %d", C, CT);
   hipStream_t s = (hipStream_t)stream;
   const long long nr = (long long)B * pl.To * pl.Fo;
   hipLaunchKernelGGL(post_fwd, dim3(grid_for(nr * C)), dim3(CT), 0, s, z, B, T, F, C, pl, P, slot);
@@ -556,11 +646,11 @@ extern "C" int asr_vgg_block_forward(const float* z, int B, int T, int F, int C,
       float* m2 = part + (size_t)nchunk * C;
       hipLaunchKernelGGL(col_moment, dim3(nchunk), dim3(CT), 0, s, P, nr, C, per, nullptr, 0,
                          part);
-      hipLaunchKernelGGL(sum_partials, dim3((C + CT - 1) / CT), dim3(CT), 0, s, part, nchunk, C,
+      hipLaunchKernelGGL(sum_partials, dim3((C + 63) / 64), dim3(CT), 0, s, part, nchunk, C,
                          1.f / (float)nr, bn_mean);
       hipLaunchKernelGGL(col_moment, dim3(nchunk), dim3(CT), 0, s, P, nr, C, per, bn_mean, 1,
                          part);
-      hipLaunchKernelGGL(sum_partials, dim3((C + CT - 1) / CT), dim3(CT), 0, s, part, nchunk, C,
+      hipLaunchKernelGGL(sum_partials, dim3((C + 63) / 64), dim3(CT), 0, s, part, nchunk, C,
                          1.f / (float)nr, m2);
       hipLaunchKernelGGL(bn_finalize, dim3((C + CT - 1) / CT), dim3(CT), 0, s, bn_mean, m2, C, nr,
                          eps, momentum, bn_rstd, run_mean, run_var);
@@ -616,8 +706,10 @@ extern "C" int asr_vgg_block_backward(const float* dnext, int flat, const float*
     sums = part + (size_t)nchunk * 2 * C;
     hipLaunchKernelGGL(bn_bwd_moments, dim3(nchunk), dim3(CT), 0, s, dnext, P, B, pl.To, pl.Fo,
                        C, flat, af, per, part);
-    hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + CT - 1) / CT), dim3(CT), 0, s, part, nchunk, C,
-                       sums, dgamma, dbeta);
+    hipLaunchKernelGGL(sum_partials, dim3((2 * C + 63) / 64), dim3(CT), 0, s, part, nchunk, 2 * C,
+                       1.f, sums);
+    hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + CT - 1) / CT), dim3(CT), 0, s, sums, C, dgamma,
+                       dbeta);
     ASR_LAUNCH_CHECK();
   }
   if (dz_dtype == ASR_DT_BF16)

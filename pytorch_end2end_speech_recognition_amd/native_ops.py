@@ -884,12 +884,19 @@ class VGGFn(torch.autograd.Function):
         B, T, F = xs.shape
         f32 = dict(dtype=torch.float32, device=dev)
         opdt = torch.bfloat16 if cd == BF16 else torch.float32
-        x_op = torch.empty(B * (T + 2) * (F + 2), **f32)
-        N.call('asr_vgg_pad_input', N.ptr(xs), B, T, F, N.ptr(x_op), N.stream_handle(dev))
-        cT, cF, cC = T, F, 1
+        # GEMM layers need C_in and C_out multiples of 16; the single input
+        # channel of layer 0 is padded to 16 (zero channels, zero weights)
+        use_gemm = [sp['w'].shape[0] % 16 == 0 and (sp['w'].shape[1] % 16 == 0 or l == 0)
+                    for l, sp in enumerate(specs)]
+        cC = 1
+        cCp = 16 if use_gemm[0] else 1
+        x_op = torch.empty(B * (T + 2) * (F + 2), cCp, dtype=opdt if use_gemm[0] else
+                           torch.float32, device=dev)
+        N.call('asr_vgg_pad_input_ch', N.ptr(xs), B, T, F, cCp, cd if use_gemm[0] else F32,
+               N.ptr(x_op), N.stream_handle(dev))
+        cT, cF = T, F
         saved, layers = [], []
         L = len(specs)
-        use_gemm = [sp['w'].shape[1] % 16 == 0 and sp['w'].shape[0] % 16 == 0 for sp in specs]
         for l, sp in enumerate(specs):
             w = sp['w']
             Co = w.shape[0]
@@ -899,12 +906,13 @@ class VGGFn(torch.autograd.Function):
                 N.call('asr_conv_direct_forward', N.ptr(x_op), B, cT, cF, cC, Co, N.ptr(w),
                        N.ptr(sp['b']), N.ptr(z), N.stream_handle(dev))
             else:
-                wg = torch.empty(Co, 9 * cC, dtype=opdt, device=dev)
-                N.call('asr_conv_weight_pack', N.ptr(w), Co, cC, 0, cd, N.ptr(wg),
+                wg = (torch.zeros if cCp != cC else torch.empty)(Co, 9 * cCp, dtype=opdt,
+                                                                 device=dev)
+                N.call('asr_conv_weight_pack_pad', N.ptr(w), Co, cC, cCp, 0, cd, N.ptr(wg),
                        N.stream_handle(dev))
-                p = gemm_problem(_tap_operand(x_op, 0, cC, cC, cF + 2, 1),
-                                 operand(wg, 0, rowmap(9 * cC)), z, rowmap(Co), npad, Co, 9 * cC,
-                                 bias=sp['b'])
+                p = gemm_problem(_tap_operand(x_op, 0, cCp, cCp, cF + 2, 1),
+                                 operand(wg, 0, rowmap(9 * cCp)), z, rowmap(Co), npad, Co,
+                                 9 * cCp, bias=sp['b'])
                 run_gemm([p], dev)
             pt, pf, ceil = sp['pt'], sp['pf'], sp['ceil']
             To, Fo = _pool_dims(cT, cF, pt, pf, ceil) if pt else (cT, cF)
@@ -931,8 +939,8 @@ class VGGFn(torch.autograd.Function):
                    float(sp['eps']), N.ptr(mean), N.ptr(rstd), drop, seed, N.ptr(out), out_dt,
                    flat, N.ptr(ws), nb, N.stream_handle(dev))
             saved += [x_op, z, P, slot, mean, rstd]
-            layers.append((cT, cF, cC, Co, pt, pf, ceil, drop, seed, use_gemm[l]))
-            x_op, cT, cF, cC = out, To, Fo, Co
+            layers.append((cT, cF, cC, cCp, Co, pt, pf, ceil, drop, seed, use_gemm[l]))
+            x_op, cT, cF, cC, cCp = out, To, Fo, Co, Co
         ctx.save_for_backward(*[t if t is not None else torch.empty(0, device=dev)
                                 for t in saved])
         ctx.layers = layers
@@ -954,7 +962,7 @@ class VGGFn(torch.autograd.Function):
             slot = slot if slot.numel() else None
             mean = mean if mean.numel() else None
             rstd = rstd if rstd.numel() else None
-            cT, cF, cC, Co, pt, pf, ceil, drop, seed, gemm = layers[l]
+            cT, cF, cC, cCp, Co, pt, pf, ceil, drop, seed, gemm = layers[l]
             sp = specs[l]
             npad = B * (cT + 2) * (cF + 2)
             dz_f32 = not gemm or sp['b'] is not None
@@ -985,14 +993,16 @@ class VGGFn(torch.autograd.Function):
                 dnext, flat = dx, 0
                 continue
             # dW image [Co][9 Ci] = dz^T X (taps on the output index), K = padded pixels
-            packed = torch.empty(Co, 9 * cC, **f32)
+            packed = torch.empty(Co, 9 * cCp, **f32)
             run_gemm([gemm_problem(operand(dz, 1, rowmap(Co)),
-                                   _tap_operand(x_op, 1, cC, cC, cF + 2, 1), packed,
-                                   rowmap(9 * cC), Co, 9 * cC, npad)], dev)
-            N.call('asr_conv_weight_unpack_acc', N.ptr(packed), Co, cC, N.ptr(grad_buffer(w)),
-                   N.stream_handle(dev))
+                                   _tap_operand(x_op, 1, cCp, cCp, cF + 2, 1), packed,
+                                   rowmap(9 * cCp), Co, 9 * cCp, npad)], dev)
+            N.call('asr_conv_weight_unpack_acc_pad', N.ptr(packed), Co, cC, cCp,
+                   N.ptr(grad_buffer(w)), N.stream_handle(dev))
             if sp['b'] is not None:
                 colsum_accumulate(dz, grad_buffer(sp['b']))
+            if l == 0:
+                break
             # d input (padded rows of layer l's input) = dz (taps, mirrored) x W^T image
             wt = torch.empty(cC, 9 * Co, dtype=opdt, device=dev)
             N.call('asr_conv_weight_pack', N.ptr(w), Co, cC, 1, cd, N.ptr(wt),
