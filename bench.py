@@ -147,7 +147,11 @@ def roofline_report(args, p, mean_us, launches, mean_work, workload):
     B, H = args.batch, p['encoder_num_units']
     # time steps of a layer pass, averaged over the layers (pyramidal drop
     # subsampling halves T after each flagged layer, rnn.py:413-439)
-    T_l, t = [], args.frames
+    t = args.frames
+    for pool in p.get('poolings') or []:    # VGG front-end time pooling (ConvOutSize floor)
+        if len(pool):
+            t = (t - pool[1]) // pool[1] + 1
+    T_l = []
     for flag in (p.get('subsample_list') or [False] * p['encoder_num_layers']):
         T_l.append(t)
         t = t // 2 if flag else t
@@ -164,6 +168,8 @@ def roofline_report(args, p, mean_us, launches, mean_work, workload):
         ('lstm_fwd_pass', 'hbm', T * 2 * cell * fwd_cell + w_hh, T * flops_step),
         ('lstm_bwd_pass', 'hbm', T * 2 * cell * bwd_cell + w_hh, T * flops_step),
         ('gemm', 'mfma', 0, mean_work[4]),
+        ('ctc_fwd', 'hbm', mean_work[5], 0.0),
+        ('ctc_grad', 'hbm', mean_work[6], 0.0),
     ]
     rows = []
     for i, (name, bound, nbytes, flops) in enumerate(kinds):
@@ -349,7 +355,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     import ctypes
-    NK = 5
+    NK = 7
     mean_us = (ctypes.c_double * NK)()
     launches = (ctypes.c_longlong * NK)()
     mean_work = (ctypes.c_double * NK)()

@@ -18,6 +18,7 @@
 //               once; occupancy of repeated labels summed through LDS.
 //   ctc_loss    1 block: loss = scale * sum_b cost_b (fixed-order tree).
 #include "common.h"
+#include "prof.h"
 
 namespace asr {
 namespace {
@@ -402,6 +403,8 @@ extern "C" int asr_ctc_forward(const float* acts, long long stride_t, long long 
                      max_label_len, ws.offs, ws.status);
   ASR_LAUNCH_CHECK();
   const long long rows = (long long)B * T;
+  // algorithmic HBM bytes of the forward: the activations read once
+  const int pslot = prof_begin_launch(ASR_PROF_CTC_FWD, s, 4.0 * (double)V * (double)rows);
   hipLaunchKernelGGL(ctc_emit, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, acts, stride_t,
                      stride_b, T, B, V, labels_flat, label_lens, act_lens, ws.offs, blank, Spad,
                      ws.lse, ws.emit);
@@ -419,6 +422,7 @@ extern "C" int asr_ctc_forward(const float* acts, long long stride_t, long long 
   }
 #undef ASR_CTC_LAT
   ASR_LAUNCH_CHECK();
+  prof_end_launch(ASR_PROF_CTC_FWD, pslot, s);
   if (loss_out) {
     hipLaunchKernelGGL(ctc_loss_reduce, dim3(1), dim3(256), 0, s, costs, B, loss_scale, loss_out);
     ASR_LAUNCH_CHECK();
@@ -443,11 +447,14 @@ extern "C" int asr_ctc_backward(const float* acts, long long stride_t, long long
   ws_layout(T, B, max_label_len, &ws, (char*)workspace);
   const int Spad = 64 * pick_k(max_label_len);
   const int threads = V <= 256 ? 64 : 256;
+  // algorithmic HBM bytes: activations read + gradient written
+  const int pslot = prof_begin_launch(ASR_PROF_CTC_GRAD, s, 8.0 * (double)V * B * T);
   hipLaunchKernelGGL(ctc_grad, dim3((unsigned)((long long)B * T)), dim3(threads), V * sizeof(float),
                      s, acts, stride_t, stride_b, T, V, labels_flat, label_lens, act_lens, ws.offs,
                      blank, Spad, ws.lse, ws.occ, ws.logp, grad_scale, scale, grads, gstride_t,
                      gstride_b);
   ASR_LAUNCH_CHECK();
+  prof_end_launch(ASR_PROF_CTC_GRAD, pslot, s);
   return ASR_OK;
 }
 

@@ -7,7 +7,9 @@
 #define ASR_PROF_LSTM_FWD_SEQ 2  /* persistent forward pass (every launch timed) */
 #define ASR_PROF_LSTM_BWD_SEQ 3  /* persistent backward pass (every launch timed) */
 #define ASR_PROF_GEMM 4          /* asr_gemm main kernel (every launch timed, flops recorded) */
-#define ASR_PROF_NKINDS 5
+#define ASR_PROF_CTC_FWD 5       /* CTC emissions + lattice (algorithmic bytes recorded) */
+#define ASR_PROF_CTC_GRAD 6      /* CTC gradient pass (algorithmic bytes recorded) */
+#define ASR_PROF_NKINDS 7
 
 namespace asr {
 bool prof_on();
