@@ -27,10 +27,10 @@
 //            R = 8, H = 512.
 //   backward (512 threads): the owner of units J turns dh_t(J) into the gate
 //            gradients dg_t [R][4 x 16] and multiplies them by ITS OWN 64 rows of
-//            W_hh, publishing f32 partial sums of dh_{t-1} for ALL H units.  A
-//            consumer sums the WPG partials of its 16 units.  This exchanges f32
-//            partials (better than rounding dg to bf16 for transport) and
-//            needs no transposed copy of W_hh.
+//            W_hh, publishing partial sums of dh_{t-1} for ALL H units as bf16
+//            pairs (8 KB of granules per work-group per step at R = 8, H = 512,
+//            the forward's hand-off volume).  A consumer sums the WPG partials
+//            of its 16 units in f32.  No transposed copy of W_hh is needed.
 //
 // Spins are bounded; on give-up a work-group sets the abort word (seen by every
 // other spinner) and g_xg_status, and exits: results are then invalid and
@@ -388,7 +388,10 @@ __global__ void __launch_bounds__(256 + R * XU) lstm_fwd_xg(
 // ---------------------------------------------------------------------------
 // backward.  grid = G * WPG.  Processing step q handles the forward direction
 // at t = T-1-q and the reverse direction at t = q.
-// Granules: pg[par][grp][producer][row][H] u64 = {f32 partial of dh, tag}.
+// Granules: pg[par][grp][producer][row][H/2] u64 = {bf16 pair of partials of dh
+// (units 2p, 2p+1), tag} -- the partials are sums of bf16 dg x bf16 W_hh
+// products accumulated in f32 and rounded once for transport; the consumer
+// sums the WPG partials in f32.
 // Wave roles, two barriers per step (B1: partials summed; B2: dg in LDS):
 //   waves 0..3 (sweepers): poll the partials of dh for this block's 16 units
 //     from every producer of the group, sum per producer subset -> LDS, B1, B2.
@@ -405,7 +408,7 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
     const float* __restrict__ whh_r, const float* __restrict__ dy, float* __restrict__ act_dg,
     const float* __restrict__ cst, unsigned long long* pg, int* hdr,
     uint16_t* __restrict__ dgbf, float* __restrict__ dbpart, unsigned epoch, int allow_local) {
-  constexpr int NPG = 256 / (8 * R);   // producer subsets swept in parallel
+  constexpr int NPG = 256 / (4 * R);   // producer subsets swept in parallel
   __shared__ float red[NPG][R][XU + 1];
   __shared__ __attribute__((aligned(16))) uint16_t dgt[16][4 * XU + 8];
   __shared__ int s_dead;
@@ -425,7 +428,7 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int HB = H / XU;                 // output M blocks
   const int H4 = 4 * H;
-  const unsigned pg_bytes = (unsigned)(2ull * G * WPG * R * H * 8);
+  const unsigned pg_bytes = (unsigned)(2ull * G * WPG * R * (H / 2) * 8);
   const __amdgpu_buffer_rsrc_t rs = xg_rsrc(pg, pg_bytes);
   unsigned long long* tr = blockIdx.x < XG_TR_WG ? g_xg_trace : nullptr;
   for (int e = tid; e < 16 * (4 * XU + 8); e += blockDim.x) (&dgt[0][0])[e] = 0;
@@ -433,9 +436,9 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
 
   if (wave < 4) {
     // ------------------------------ sweeper -------------------------------
-    const int sl = tid & (8 * R - 1);
-    const int srow = sl >> 3, spr = sl & 7;
-    const int pgi = tid / (8 * R);
+    const int sl = tid & (4 * R - 1);
+    const int srow = sl >> 2, sq = sl & 3;   // row, quad of units 4 sq .. 4 sq + 3
+    const int pgi = tid / (4 * R);
     constexpr int MAXP = 64;  // WPG <= 64
     const int nsleep = __builtin_amdgcn_readfirstlane(g_xg_sleep);
     const int ndelay = __builtin_amdgcn_readfirstlane(g_xg_delay);
@@ -444,22 +447,24 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
       if (q > 0) {
         const unsigned tag = ep | (unsigned)q;
         const long long base = ((long long)((q - 1) & 1) * G + grp) * WPG;
-        float s0 = 0.f, s1 = 0.f;
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+        const int hh = H / 2;
         nap(ndelay);
         for (unsigned spins = 0;; ++spins) {
           const unsigned long long t_iss = tr ? __builtin_amdgcn_s_memrealtime() : 0;
           int ok = 1;
-          s0 = 0.f;
-          s1 = 0.f;
+          s0 = s1 = s2 = s3 = 0.f;
 #pragma unroll 8
           for (int w = pgi; w < MAXP; w += NPG) {
             if (w >= WPG) break;
             const unsigned off =
-                (unsigned)((((base + w) * R + srow) * (long long)H + u0 + 2 * spr) * 8);
+                (unsigned)((((base + w) * R + srow) * (long long)hh + (u0 >> 1) + 2 * sq) * 8);
             const u32x4 v = ld_sc1(rs, off);
             ok &= tags_ok(v, tag);
-            s0 += __uint_as_float(v[0]);
-            s1 += __uint_as_float(v[2]);
+            s0 += bf2f((uint16_t)(v[0] & 0xffffu));
+            s1 += bf2f((uint16_t)(v[0] >> 16));
+            s2 += bf2f((uint16_t)(v[2] & 0xffffu));
+            s3 += bf2f((uint16_t)(v[2] >> 16));
           }
           if (__all(ok)) {
             XG_TR(q, 1, __builtin_amdgcn_s_memrealtime());
@@ -473,8 +478,10 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
             break;
           }
         }
-        red[pgi][srow][2 * spr] = s0;
-        red[pgi][srow][2 * spr + 1] = s1;
+        red[pgi][srow][4 * sq] = s0;
+        red[pgi][srow][4 * sq + 1] = s1;
+        red[pgi][srow][4 * sq + 2] = s2;
+        red[pgi][srow][4 * sq + 3] = s3;
       }
       __syncthreads();  // B1
       XG_TR(q, 2, __builtin_amdgcn_s_memrealtime());
@@ -609,16 +616,14 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
         acc = mfma_bf16(wa[i][1], bf1, acc);
         if (ln < R) {  // C[m][n]: n = ln (row), m = 16 mb + 4 kq + r
           const unsigned off =
-              (unsigned)(((obase + ln) * (long long)H + 16 * mb + 4 * kq) * 8);
-          const u32x4 v0 = {__float_as_uint(acc[0]), tag, __float_as_uint(acc[1]), tag};
-          const u32x4 v1 = {__float_as_uint(acc[2]), tag, __float_as_uint(acc[3]), tag};
-          if (local) {  // plain: into this XCD's L2
+              (unsigned)(((obase + ln) * (long long)(H / 2) + 8 * mb + 2 * kq) * 8);
+          const unsigned p01 = f2bf(acc[0]) | ((unsigned)f2bf(acc[1]) << 16);
+          const unsigned p23 = f2bf(acc[2]) | ((unsigned)f2bf(acc[3]) << 16);
+          const u32x4 v0 = {p01, tag, p23, tag};
+          if (local)  // plain: into this XCD's L2
             __builtin_amdgcn_raw_buffer_store_b128(v0, rs, off, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b128(v1, rs, off + 16, 0, 0);
-          } else {      // write-through
+          else        // write-through
             __builtin_amdgcn_raw_buffer_store_b128(v0, rs, off, 0, AUX_SC1);
-            __builtin_amdgcn_raw_buffer_store_b128(v1, rs, off + 16, 0, AUX_SC1);
-          }
         }
       }
     }
@@ -692,7 +697,7 @@ size_t lstm_xg_bwd_bytes(int B, int H) {
   const int R = xg_rows(B, H);
   if (!R) return 0;
   const long long rows = 2LL * ((B + R - 1) / R) * R;
-  return XG_HDR + (size_t)2 * rows * (H / XU) * H * 8;
+  return XG_HDR + (size_t)2 * rows * (H / XU) * (H / 2) * 8;
 }
 
 // Returns 1 if launched (or, with dry, if this shape/device can take the
