@@ -1,0 +1,99 @@
+"""Plain bf16 products that asr_gemm hands to hipBLASLt (csrc/gemm_lib.hip):
+the three layouts it takes (K-major x K-major stays on the own split-K kernel
+and is checked here too), padded leading dimensions, alpha/beta, one bias and
+the summed bias pair (nn.LSTM's b_ih + b_hh), and a launch that mixes a library
+problem with a row-mapped one.  Small-integer operands make bf16 products with
+f32 accumulation exact, so the results must equal float64 bit for bit."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _ops():
+    from pytorch_end2end_speech_recognition_amd import native_ops
+    return native_ops
+
+
+def _store(rng, rows, cols, ld):
+    a = np.zeros((rows, ld), np.float32)
+    a[:, :cols] = rng.randint(-3, 4, (rows, cols))
+    return a
+
+
+@pytest.mark.parametrize('at,bt', [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize('nbias', [0, 1, 2])
+def test_library_gemm_exact(at, bt, nbias, cuda_dev):
+    from pytorch_end2end_speech_recognition_amd import _native as N
+    ops = _ops()
+    assert N.query('asr_gemm_library_ready') == 1
+    ops.set_compute_dtype('bf16')
+    try:
+        rng = np.random.RandomState(10 * at + bt + 100 * nbias)
+        M, Nn, K = 2048, 1024, 1032     # 2*M*N*K >= 4e9: library-eligible
+        pad = 8
+        sa = _store(rng, K if at else M, M if at else K, (M if at else K) + pad)
+        sb = _store(rng, K if bt else Nn, Nn if bt else K, (Nn if bt else K) + pad)
+        A = (sa[:, :M].T if at else sa[:, :K]).astype(np.float64)
+        Bm = (sb[:, :Nn].T if bt else sb[:, :K]).astype(np.float64)
+        ad = torch.from_numpy(sa).to(torch.bfloat16).to(cuda_dev)
+        bd = torch.from_numpy(sb).to(torch.bfloat16).to(cuda_dev)
+        ldc = Nn + 4
+        c0 = rng.randint(-4, 5, (M, ldc)).astype(np.float32)
+        C = torch.from_numpy(c0).to(cuda_dev)
+        b1 = rng.randint(-8, 9, Nn).astype(np.float32)
+        b2 = rng.randint(-8, 9, Nn).astype(np.float32)
+        kw = {}
+        if nbias >= 1:
+            kw['bias'] = torch.from_numpy(b1).to(cuda_dev)
+        if nbias == 2:
+            kw['bias2'] = torch.from_numpy(b2).to(cuda_dev)
+        p = ops.gemm_problem(ops.operand(ad, at, ops.rowmap(sa.shape[1])),
+                             ops.operand(bd, bt, ops.rowmap(sb.shape[1])), C, ops.rowmap(ldc),
+                             M, Nn, K, alpha=0.5, beta=1.0, **kw)
+        ops.run_gemm([p], cuda_dev)
+        torch.cuda.synchronize()
+        ref = c0.astype(np.float64).copy()
+        ref[:, :Nn] += 0.5 * A @ Bm.T
+        if nbias >= 1:
+            ref[:, :Nn] += b1
+        if nbias == 2:
+            ref[:, :Nn] += b2
+        np.testing.assert_array_equal(C.cpu().numpy(), ref)
+    finally:
+        ops.set_compute_dtype('fp32')
+
+
+def test_library_and_mapped_problems_in_one_launch(cuda_dev):
+    """nprob = 2: a plain product (library) next to a subsampled-row product
+    (own kernel, t_mul = 2) that also needs a split-K slab."""
+    ops = _ops()
+    ops.set_compute_dtype('bf16')
+    try:
+        rng = np.random.RandomState(3)
+        M, Nn, K = 4096, 1024, 1024
+        a = rng.randint(-3, 4, (M, K)).astype(np.float32)
+        b = rng.randint(-3, 4, (Nn, K)).astype(np.float32)
+        ad = torch.from_numpy(a).to(torch.bfloat16).to(cuda_dev)
+        bd = torch.from_numpy(b).to(torch.bfloat16).to(cuda_dev)
+        C1 = torch.zeros(M, Nn, device=cuda_dev)
+        p1 = ops.gemm_problem(ops.operand(ad, 0, ops.rowmap(K)), ops.operand(bd, 0, ops.rowmap(K)),
+                              C1, ops.rowmap(Nn), M, Nn, K)
+        # dW-shaped: C2[Nn2][K] = sum over every other row t of g[t] x[t]
+        Tn, N2 = 4096, 256
+        g = rng.randint(-3, 4, (2 * Tn, 64)).astype(np.float32)
+        x = rng.randint(-3, 4, (2 * Tn, N2)).astype(np.float32)
+        gd = torch.from_numpy(g).to(torch.bfloat16).to(cuda_dev)
+        xd = torch.from_numpy(x).to(torch.bfloat16).to(cuda_dev)
+        C2 = torch.zeros(64, N2, device=cuda_dev)
+        p2 = ops.gemm_problem(ops.operand(gd, 1, ops.rowmap(64, t_mul=2, t_add=1)),
+                              ops.operand(xd, 1, ops.rowmap(N2, t_mul=2, t_add=1)), C2,
+                              ops.rowmap(N2), 64, N2, Tn)
+        ops.run_gemm([p1, p2], cuda_dev)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(C1.cpu().numpy(), a.astype(np.float64) @ b.T)
+        ref2 = g[1::2].T.astype(np.float64) @ x[1::2]
+        np.testing.assert_array_equal(C2.cpu().numpy(), ref2)
+    finally:
+        ops.set_compute_dtype('fp32')

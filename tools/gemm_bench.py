@@ -1,0 +1,47 @@
+"""bf16 GEMM throughput at the BLSTM layer shapes of the 5x512 bench (B*T =
+32000, H = 512): forward gx (R x R), input gradient (R x K), weight gradient
+(K x K, split-K), each timed with HIP events over n launches."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from pytorch_end2end_speech_recognition_amd import native_ops as ops  # noqa: E402
+
+dev = torch.device('cuda:0')
+ops.set_compute_dtype('bf16')
+M, H = 32000, 512
+D = 2 * H
+bf = dict(dtype=torch.bfloat16, device=dev)
+x = torch.randn(M, D, **bf)
+w = torch.randn(8 * H, D, **bf) * 0.05
+dg = torch.randn(M, 8 * H, **bf)
+gx = torch.empty(M, 8 * H, device=dev)
+dx = torch.empty(M, D, device=dev)
+dw = torch.zeros(8 * H, D, device=dev)
+R = ops.rowmap
+shapes = {
+    'fwd  M=32000 N=4096 K=1024 (RR)': [ops.gemm_problem(ops.operand(x, 0, R(D)), ops.operand(w, 0, R(D)),
+                                                         gx, R(8 * H), M, 8 * H, D)],
+    'dX   M=32000 N=1024 K=4096 (RK)': [ops.gemm_problem(ops.operand(dg, 0, R(8 * H)),
+                                                         ops.operand(w, 1, R(D)), dx, R(D), M, D,
+                                                         8 * H)],
+    'dW   M=4096 N=1024 K=32000 (KK)': [ops.gemm_problem(ops.operand(dg, 1, R(8 * H)),
+                                                         ops.operand(x, 1, R(D)), dw, R(D), 8 * H,
+                                                         D, M, beta=1.0)],
+}
+for name, probs in shapes.items():
+    for _ in range(3):
+        ops.run_gemm(probs, dev)
+    torch.cuda.synchronize()
+    n = 20
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        ops.run_gemm(probs, dev)
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1000 / n
+    fl = sum(2.0 * p.M * p.N * p.K for p in probs)
+    print('%s  %8.1f us  %6.0f TF/s' % (name, us, fl / us / 1e6))
