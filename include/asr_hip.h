@@ -259,6 +259,9 @@ int asr_tanh_backward(const float* y, const float* dy, float* dx, long long n, v
 /* y = tanh(a + b) (attention bottleneck with per-branch dropout,
  * attention_seq2seq.py:788-790); its backward is asr_tanh_backward for both. */
 int asr_add_tanh_forward(const float* a, const float* b, float* y, long long n, void* stream);
+/* y = a + b: the encoder's residual / dense-residual sums (rnn.py:456-462);
+ * the backward is the identity to both inputs. */
+int asr_add_forward(const float* a, const float* b, float* y, long long n, void* stream);
 
 /* dst[r][0:ncols] = bf16(src[row(r) + 0:ncols]) (round to nearest even) for r <
  * nrows, rows through an asr_rowmap_t (perm / subsample gathers; rows outside

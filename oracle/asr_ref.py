@@ -76,12 +76,17 @@ def vgg_front(p, prefix, cfg, xs, x_lens, masks=None, training=True):
     return x.transpose(1, 3).reshape(B, To, Fo * C), lens, stats
 
 
-def blstm_encoder(p, prefix, cfg, xs, x_lens):
+def blstm_encoder(p, prefix, cfg, xs, x_lens, capture_layer=0):
     """RNNEncoder.forward (rnn.py:284-487) for rnn_type='lstm', bidirectional,
-    subsample_type 'drop', no projection / residual, optional VGG front-end
-    (cfg['conv_channels'], rnn.py:314-316), dropout = 0.
+    dropout = 0, optional VGG front-end (cfg['conv_channels'], rnn.py:314-316),
+    and the inter-layer ops of rnn.py:409-465 on every layer but the last:
+    projection tanh(proj_l(x)) (cfg['num_proj']), subsampling 'drop'
+    x[:, 1::2] or 'concat' [x_{2t}; x_{2t+1}] (cfg['subsample_type']), residual
+    / dense residual sums from layer residual_start_layer - 1 on (rnn.py:126-133).
 
-    Returns (out [B, T', 2H], out_lens np.int32 [B], perm np.int64 [B])."""
+    Returns (out [B, T', 2H], out_lens np.int32 [B], perm np.int64 [B]); with
+    capture_layer = k >= 1 also (out_k, lens_k) of layer k-1 after its dropout,
+    before projection / subsampling (rnn.py:400-407)."""
     x_lens = np.asarray(x_lens)
     if cfg.get('conv_channels'):
         xs, x_lens, _ = vgg_front(p, prefix, cfg, xs, x_lens)
@@ -90,7 +95,17 @@ def blstm_encoder(p, prefix, cfg, xs, x_lens):
     lens = x_lens[perm].astype(np.int64)
     n_layers = cfg['num_layers']
     sub = cfg.get('subsample_list') or [False] * n_layers
-    fast = sum(sub) == 0 and not cfg.get('batch_norm') and cfg.get('fast', True)   # rnn.py:162
+    n_proj = cfg.get('num_proj', 0) or 0
+    concat = cfg.get('subsample_type', 'drop') == 'concat'
+    res, dres = bool(cfg.get('residual')), bool(cfg.get('dense_residual'))
+    fast = (sum(sub) == 0 and not cfg.get('batch_norm') and n_proj == 0 and not res and
+            not dres and capture_layer == 0 and cfg.get('fast', True))   # rnn.py:162
+    last_sub = 0                                              # rnn.py:126-132
+    for l_rev, s_ in enumerate(sub[::-1]):
+        if s_:
+            last_sub = n_layers - l_rev
+            break
+    res_list, captured = [], None
     for l in range(n_layers):
         if fast:   # one multi-layer nn.LSTM: lstm.weight_ih_l{l}{_reverse}
             names = [prefix + 'lstm.%s_l%d%s' % (n, l, s) for s in ('', '_reverse')
@@ -103,9 +118,25 @@ def blstm_encoder(p, prefix, cfg, xs, x_lens):
         fw = lstm_direction(xs, lens, *[p[n] for n in names[:4]], reverse=False)
         bw = lstm_direction(xs, lens, *[p[n] for n in names[4:]], reverse=True)
         xs = torch.cat([fw, bw], dim=2)
-        if not fast and l != n_layers - 1 and sub[l]:
-            xs = xs[:, 1::2]                                  # rnn.py:415-419
+        if capture_layer and l == capture_layer - 1:
+            captured = (xs, lens.astype(np.int32))
+        if fast or l == n_layers - 1 or not (res or dres or n_proj > 0 or sub[l]):
+            continue
+        if n_proj > 0:                                        # rnn.py:409-411
+            xs = torch.tanh(linear_nd(p, prefix + 'proj_l%d' % l, xs))
+        if sub[l]:
+            if concat:                                        # rnn.py:421-431
+                B_, T_, D_ = xs.shape
+                xs = xs[:, :T_ // 2 * 2].reshape(B_, T_ // 2, 2 * D_)
+            else:                                             # rnn.py:415-419
+                xs = xs[:, 1::2]
             lens = np.full(len(lens), xs.shape[1], np.int64)  # quirk rnn.py:435-439
+        elif (res or dres) and l >= last_sub:                 # rnn.py:454-462
+            for lower in res_list:
+                xs = xs + lower
+            res_list = [xs] if res else res_list + [xs]
+    if capture_layer:
+        return xs, lens.astype(np.int32), perm.astype(np.int64), captured
     return xs, lens.astype(np.int32), perm.astype(np.int64)
 
 
@@ -155,9 +186,8 @@ def hierarchical_ctc_loss(p, cfg, xs, ys, x_lens, y_lens, ys_sub, y_lens_sub):
     layer, char CTC on the output of layer num_layers_sub (after its dropout,
     before any subsampling, rnn.py:400-407); loss = w_main L_main + w_sub L_sub."""
     xs_t = torch.from_numpy(np.asarray(xs, np.float32))
-    sub_cfg = dict(cfg, num_layers=cfg['num_layers_sub'])
-    top, lens, perm = blstm_encoder(p, 'encoder.', dict(cfg, fast=False), xs_t, x_lens)
-    mid, lens_sub, _ = blstm_encoder(p, 'encoder.', dict(sub_cfg, fast=False), xs_t, x_lens)
+    top, lens, perm, (mid, lens_sub) = blstm_encoder(p, 'encoder.', dict(cfg, fast=False), xs_t,
+                                                     x_lens, capture_layer=cfg['num_layers_sub'])
     B = xs.shape[0]
     terms = []
     for h, ln, head, y, yl in ((top, lens, 'fc_out', ys, y_lens),

@@ -67,6 +67,7 @@ SIGNATURES = {
     'asr_tanh_forward': (c_int, [c_vp, c_vp, c_ll, c_vp]),
     'asr_tanh_backward': (c_int, [c_vp, c_vp, c_vp, c_ll, c_vp]),
     'asr_add_tanh_forward': (c_int, [c_vp, c_vp, c_vp, c_ll, c_vp]),
+    'asr_add_forward': (c_int, [c_vp, c_vp, c_vp, c_ll, c_vp]),
     'asr_convert_rows_bf16': None,  # set below, after RowMap (struct passed by value)
     'asr_ctc_best_path': (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp,
                                   c_vp]),

@@ -123,6 +123,14 @@ __global__ void add_tanh_fwd(const float* __restrict__ a, const float* __restric
     y[i] = tanhf(a[i] + b[i]);
 }
 
+// Residual connection sum (rnn.py:456-462), one read of each operand.
+__global__ void add_fwd(const float* __restrict__ a, const float* __restrict__ b,
+                        float* __restrict__ y, long long n) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    y[i] = a[i] + b[i];
+}
+
 inline int grid_for(long long n) {
   long long b = (n + 255) / 256;
   return (int)(b < 4096 ? (b > 0 ? b : 1) : 4096);
@@ -191,6 +199,15 @@ extern "C" int asr_add_tanh_forward(const float* a, const float* b, float* y, lo
   if (n <= 0) return ASR_OK;
   hipLaunchKernelGGL(add_tanh_fwd, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, a, b, y,
                      n);
+  ASR_LAUNCH_CHECK();
+  return ASR_OK;
+}
+
+extern "C" int asr_add_forward(const float* a, const float* b, float* y, long long n,
+                               void* stream) {
+  ASR_REQUIRE(a && b && y, ASR_ERR_ARG, "add: null pointer");
+  if (n <= 0) return ASR_OK;
+  hipLaunchKernelGGL(add_fwd, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, a, b, y, n);
   ASR_LAUNCH_CHECK();
   return ASR_OK;
 }

@@ -10,16 +10,20 @@ modules are used only as parameter holders; their forward never runs.
 Forward semantics (rnn.py:284-487): input dropout, the optional VGG front-end
 (encoders/cnn.py, rnn.py:143-160, 314-316), length sort (perm_idx is
 returned; outputs stay in sorted order), packed-sequence behaviour through
-per-utterance length masks, dropout after every layer, pyramidal ``drop``
-subsampling ``xs[:, 1::2]`` fused into the next layer's input GEMM, and the
-reference's x_lens quirk: after any subsampling every utterance's length is
-the padded length (rnn.py:435-439).
+per-utterance length masks, dropout after every layer, and between layers
+(rnn.py:409-465): the projection ``tanh(proj_l(x))``, pyramidal ``drop``
+subsampling ``xs[:, 1::2]`` or ``concat`` subsampling (successive frame pairs
+side by side) -- both read in place by the next layer's input GEMM through its
+row map -- and residual / dense-residual sums from the last subsampling layer
+on; plus the reference's x_lens quirk: after any subsampling every
+utterance's length is the padded length (rnn.py:435-439).
 """
 import numpy as np
 import torch
 import torch.nn as nn
 
 from .... import native_ops as ops
+from ..linear import LinearND
 from .cnn import CNNEncoder
 
 
@@ -44,12 +48,6 @@ class RNNEncoder(nn.Module):
             unsupported.append('rnn_type=%s' % rnn_type)
         if not bidirectional:
             unsupported.append('unidirectional')
-        if num_proj:
-            unsupported.append('num_proj')
-        if subsample_type != 'drop' and sum(subsample_list):
-            unsupported.append('subsample_type=concat')
-        if residual or dense_residual:
-            unsupported.append('residual')
         if nin or merge_bidirectional or not batch_first or not pack_sequence:
             unsupported.append('nin/merge/time-major/no-pack')
         if unsupported:
@@ -60,7 +58,7 @@ class RNNEncoder(nn.Module):
         self.bidirectional = bidirectional
         self.num_directions = 2
         self.num_units = num_units
-        self.num_proj = 0
+        self.num_proj = num_proj if num_proj is not None else 0
         self.num_layers = num_layers
         self.batch_first = batch_first
         self.pack_sequence = pack_sequence
@@ -71,6 +69,15 @@ class RNNEncoder(nn.Module):
         self.dropout_hidden_p = float(dropout_hidden)
         self.dropout_input = nn.Dropout(p=dropout_input)
         self.batch_norm = batch_norm
+        assert not (residual and dense_residual)
+        self.residual = residual
+        self.dense_residual = dense_residual
+        subsample_last_layer = 0                      # rnn.py:126-133
+        for l_reverse, is_subsample in enumerate(self.subsample_list[::-1]):
+            if is_subsample:
+                subsample_last_layer = num_layers - l_reverse
+                break
+        self.residual_start_layer = subsample_last_layer + 1
         if len(conv_channels) > 0 and len(conv_channels) == len(conv_kernel_sizes) and \
                 len(conv_kernel_sizes) == len(conv_strides):   # rnn.py:143-160
             assert num_stack == 1 and splice == 1
@@ -87,19 +94,28 @@ class RNNEncoder(nn.Module):
         self.input_size = input_size
 
         # rnn.py:162 (batch_norm forces the per-layer modules, as in the reference)
-        self.fast_impl = sum(self.subsample_list) == 0 and not batch_norm and num_layers_sub == 0
+        self.fast_impl = (sum(self.subsample_list) == 0 and self.num_proj == 0 and not residual and
+                          not dense_residual and num_layers_sub == 0 and not batch_norm)
         if self.fast_impl:   # rnn.py:162-198: one multi-layer nn.LSTM
             self.lstm = nn.LSTM(input_size, hidden_size=num_units, num_layers=num_layers,
                                 bias=True, batch_first=batch_first, dropout=dropout_hidden,
                                 bidirectional=True)
             self.dropout_last = nn.Dropout(p=dropout_hidden)
-        else:                # rnn.py:200-251: one nn.LSTM per layer
+        else:                # rnn.py:200-251: one nn.LSTM per layer (+ projection)
             for l in range(num_layers):
-                din = input_size if l == 0 else num_units * 2
+                if l == 0:
+                    din = input_size
+                else:
+                    din = self.num_proj if self.num_proj > 0 else num_units * 2
+                    if subsample_type == 'concat' and self.subsample_list[l - 1]:
+                        din *= 2
                 setattr(self, 'lstm_l%d' % l,
                         nn.LSTM(din, hidden_size=num_units, num_layers=1, bias=True,
                                 batch_first=batch_first, dropout=0, bidirectional=True))
                 setattr(self, 'dropout_l%d' % l, nn.Dropout(p=dropout_hidden))
+                if l != num_layers - 1 and self.num_proj > 0:
+                    setattr(self, 'proj_l%d' % l,
+                            LinearND(num_units * 2, self.num_proj, dropout=dropout_hidden))
 
     # parameters of layer l: (w_ih_f, w_ih_r), (w_hh_f, w_hh_r), (b_ih_f, b_ih_r), (b_hh_f, b_hh_r)
     def _layer_params(self, l):
@@ -150,23 +166,39 @@ class RNNEncoder(nn.Module):
         lens = x_lens[perm]
         perm_d = torch.from_numpy(perm.astype(np.int32)).to(dev, non_blocking=True)
         T = int(lens.max())                                          # pad_packed length
-        h, pm, t_mul, t_add = xs.contiguous(), perm_d, 1, 0
+        h, pm, t_mul, t_add, concat = xs.contiguous(), perm_d, 1, 0, False
         h_sub = lens_sub = None
+        res_outputs = []
         for l in range(self.num_layers):
             (w_ih, w_hh, b_ih, b_hh), gbufs = self._layer_tensors(l)
             lens_d = torch.from_numpy(lens.astype(np.int32)).to(dev, non_blocking=True)
             graph = tuple(p for pair in self._layer_params(l) for p in pair)
             h = ops.blstm_layer(h, lens_d, T, w_ih, w_hh, b_ih, b_hh, perm=pm, t_mul=t_mul,
-                                t_add=t_add, gbufs=tuple(gbufs), graph_params=graph)
+                                t_add=t_add, gbufs=tuple(gbufs), graph_params=graph,
+                                concat=concat)
             if self.training and self.dropout_hidden_p > 0:
                 h = ops.dropout(h, self.dropout_hidden_p)
             if self.num_layers_sub >= 1 and l == self.num_layers_sub - 1:   # rnn.py:400-407
                 h_sub, lens_sub = h, lens.astype(np.int32)
-            pm, t_mul, t_add = None, 1, 0
-            if l != self.num_layers - 1 and self.subsample_list[l]:  # rnn.py:413-439
+            pm, t_mul, t_add, concat = None, 1, 0, False
+            if l == self.num_layers - 1 or not (self.residual or self.dense_residual or
+                                                self.num_proj > 0 or self.subsample_list[l]):
+                continue
+            if self.num_proj > 0:                                    # rnn.py:409-411
+                h = ops.tanh(getattr(self, 'proj_l%d' % l)(h))
+            if self.subsample_list[l]:                               # rnn.py:413-439
+                # fused into the next layer's input GEMM: 'drop' reads frame 2t+1,
+                # 'concat' reads frames 2t and 2t+1 as one row of twice the width
                 T = T // 2
-                t_mul, t_add = 2, 1
+                if self.subsample_type == 'drop':
+                    t_mul, t_add = 2, 1
+                else:
+                    t_mul, t_add, concat = 2, 0, True
                 lens = np.full_like(lens, T)
+            elif (self.residual or self.dense_residual) and l >= self.residual_start_layer - 1:
+                for lower in res_outputs:                            # rnn.py:454-462
+                    h = ops.add(h, lower)
+                res_outputs = [h] if self.residual else res_outputs + [h]
         assert t_mul == 1
         self.last_lens_np = lens.astype(np.int32)
         self.last_perm_np = perm.astype(np.int64)

@@ -419,15 +419,19 @@ class BLSTMLayerFn(torch.autograd.Function):
     directly (exact-f32 MFMA, parity mode)."""
 
     @staticmethod
-    def forward(ctx, x_src, lens, T, perm, t_mul, t_add, gbufs, w_ih, w_hh, b_ih, b_hh,
+    def forward(ctx, x_src, lens, T, perm, t_mul, t_add, gbufs, concat, w_ih, w_hh, b_ih, b_hh,
                 *graph_params):
         N.require_device(x_src, lens, w_ih, w_hh, b_ih, b_hh)
         x_src = x_src.contiguous()
-        B, T_src, Din = x_src.shape
+        B, T_src, Dsrc = x_src.shape
+        # concat: the input row (b, t) spans source frames t*t_mul + t_add and the
+        # next one (rnn.py:421-431), i.e. 2*Dsrc contiguous values
+        Din = 2 * Dsrc if concat else Dsrc
+        assert w_ih.shape[1] == Din, (tuple(w_ih.shape), Din)
         H = w_hh.shape[1]
         dev = x_src.device
         cd = compute_dtype()
-        a_map = rowmap(Din, stride_b=T_src * Din, rows_per_b=T, t_mul=t_mul, t_add=t_add,
+        a_map = rowmap(Dsrc, stride_b=T_src * Dsrc, rows_per_b=T, t_mul=t_mul, t_add=t_add,
                        t_limit=T_src, perm=perm)
         gx = torch.empty(B, T, 8 * H, dtype=torch.float32, device=dev)
         if cd == BF16:
@@ -451,14 +455,14 @@ class BLSTMLayerFn(torch.autograd.Function):
                N.stream_handle(dev))
         ctx.save_for_backward(x_op, w_op, lens, w_hh, b_ih, b_hh, gx, cst,
                               y_bf if y_bf is not None else y)
-        ctx.meta = (T, perm, t_mul, t_add, gbufs, cd, (B, T_src, Din), w_ih)
+        ctx.meta = (T, perm, t_mul, t_add, gbufs, cd, (B, T_src, Dsrc, Din), w_ih)
         ctx.n_graph = len(graph_params)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x_op, w_op, lens, w_hh, b_ih, b_hh, act, cst, y_op = ctx.saved_tensors
-        T, perm, t_mul, t_add, gbufs, cd, (B, T_src, Din), w_ih = ctx.meta
+        T, perm, t_mul, t_add, gbufs, cd, (B, T_src, Dsrc, Din), w_ih = ctx.meta
         H = w_hh.shape[1]
         dev = act.device
         dy = dy.contiguous()
@@ -486,7 +490,7 @@ class BLSTMLayerFn(torch.autograd.Function):
         if cd == BF16:
             x_map = rowmap(Din)
         else:
-            x_map = rowmap(Din, stride_b=T_src * Din, rows_per_b=T, t_mul=t_mul, t_add=t_add,
+            x_map = rowmap(Dsrc, stride_b=T_src * Dsrc, rows_per_b=T, t_mul=t_mul, t_add=t_add,
                            t_limit=T_src, perm=perm)
         side = _wgrad_side_stream(dev, B, H)
         if side is None:
@@ -507,16 +511,16 @@ class BLSTMLayerFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             # dX [BT, Din] = dG [BT, 8H] W_ih [8H, Din], scattered back through the input map
-            if perm is None and t_mul == 1 and t_add == 0 and T == T_src:
-                dx = torch.empty(B, T_src, Din, dtype=torch.float32, device=dev)
+            if perm is None and t_mul == 1 and t_add == 0 and T == T_src and Din == Dsrc:
+                dx = torch.empty(B, T_src, Dsrc, dtype=torch.float32, device=dev)
             else:
-                dx = torch.zeros(B, T_src, Din, dtype=torch.float32, device=dev)
-            c_map = rowmap(Din, stride_b=T_src * Din, rows_per_b=T, t_mul=t_mul, t_add=t_add,
+                dx = torch.zeros(B, T_src, Dsrc, dtype=torch.float32, device=dev)
+            c_map = rowmap(Dsrc, stride_b=T_src * Dsrc, rows_per_b=T, t_mul=t_mul, t_add=t_add,
                            t_limit=T_src, perm=perm)
             p = gemm_problem(operand(dg_op, 0, rowmap(8 * H)), operand(w_op, 1, rowmap(Din)), dx,
                              c_map, BT, Din, 8 * H)
             run_gemm([p], dev)
-        return (dx,) + (None,) * (10 + ctx.n_graph)
+        return (dx,) + (None,) * (11 + ctx.n_graph)
 
 
 def convert_rows_bf16(src, rmap, nrows, ncols):
@@ -533,9 +537,9 @@ def _blstm_wgrad(dg, dg_f32, x_op, x_map, y_op, T, gbufs, dev):
     asr_lstm_backward_db."""
     B = dg.shape[0]
     H = y_op.shape[2] // 2
-    Din = x_op.shape[-1]
     BT = B * T
     g_ih, g_hh, g_bih, g_bhh = gbufs
+    Din = g_ih.shape[-1]          # != x_op's width for 'concat' input rows
     # dW_ih [8H, Din] += dG^T x   (both directions in one problem)
     run_gemm([gemm_problem(operand(dg, 1, rowmap(8 * H)), operand(x_op, 1, x_map), g_ih,
                            rowmap(Din), 8 * H, Din, BT, beta=1.0)], dev)
@@ -578,13 +582,15 @@ def _wgrad_side_stream(dev, B, H):
 
 
 def blstm_layer(x_src, lens, T, w_ih, w_hh, b_ih, b_hh, perm=None, t_mul=1, t_add=0, gbufs=None,
-                graph_params=()):
+                graph_params=(), concat=False):
     """gbufs: optional (g_w_ih, g_w_hh, g_b_ih, g_b_hh) gradient views to accumulate
     into; default: the tensors' own .grad.  graph_params: the nn.Parameters the
     combined [fwd; rev] views alias -- passed only so autograd records that the
-    output depends on them (their gradients are written by the kernels)."""
-    return BLSTMLayerFn.apply(x_src, lens, T, perm, t_mul, t_add, gbufs, w_ih, w_hh, b_ih, b_hh,
-                              *graph_params)
+    output depends on them (their gradients are written by the kernels).
+    concat: input row t is [x_src[t*t_mul + t_add]; x_src[t*t_mul + t_add + 1]]
+    ('concat' subsampling of the previous layer, read in place)."""
+    return BLSTMLayerFn.apply(x_src, lens, T, perm, t_mul, t_add, gbufs, bool(concat), w_ih,
+                              w_hh, b_ih, b_hh, *graph_params)
 
 
 # ---------------------------------------------------------------------------
@@ -664,6 +670,27 @@ class AddTanhFn(torch.autograd.Function):
 
 def add_tanh(a, b):
     return AddTanhFn.apply(a, b)
+
+
+class AddFn(torch.autograd.Function):
+    """y = a + b (residual connections); d a = d b = dy."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        N.require_device(a, b)
+        a, b = a.contiguous(), b.contiguous()
+        y = torch.empty_like(a)
+        N.call('asr_add_forward', N.ptr(a), N.ptr(b), N.ptr(y), y.numel(),
+               N.stream_handle(a.device))
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        return dy, dy
+
+
+def add(a, b):
+    return AddFn.apply(a, b)
 
 
 class TanhFn(torch.autograd.Function):

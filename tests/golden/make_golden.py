@@ -244,6 +244,32 @@ def _batch(rng, B, T, F_, y_lens, num_classes, x_lens):
     return xs, ys
 
 
+def _ctc_variant_specs():
+    """Encoder variants of rnn.py:392-465: projection tanh(LinearND) between
+    layers, 'concat' subsampling (successive frame pairs), residual and dense
+    residual connections (from the last subsampling layer on)."""
+    base = dict(input_size=8, encoder_type='lstm', encoder_bidirectional=True,
+                encoder_num_units=6, encoder_num_proj=0, encoder_num_layers=3, fc_list=[],
+                dropout_input=0, dropout_encoder=0, num_classes=5, parameter_init=0.1,
+                subsample_list=[False, True, False], subsample_type='drop')
+    return [
+        ('model_ctc_proj', dict(base, encoder_num_proj=4)),
+        ('model_ctc_concat', dict(base, subsample_list=[True, False, False],
+                                  subsample_type='concat')),
+        ('model_ctc_proj_concat', dict(base, encoder_num_proj=5, subsample_type='concat')),
+        ('model_ctc_res', dict(base, encoder_num_layers=4,
+                               subsample_list=[True, False, False, False],
+                               encoder_residual=True)),
+        ('model_ctc_dres', dict(base, encoder_num_layers=4, subsample_list=[],
+                                encoder_dense_residual=True, encoder_num_proj=7)),
+    ]
+
+
+def _selected():
+    """Case names given on the command line (default: every case)."""
+    return set(a for a in sys.argv[1:] if not a.startswith('-'))
+
+
 def case_ctc_model():
     from models.pytorch_v3.ctc.ctc import CTC
     from models.pytorch_v3.ctc.decoders.greedy_decoder import GreedyDecoder
@@ -258,7 +284,11 @@ def case_ctc_model():
                                 fc_list=[], dropout_input=0, dropout_encoder=0, num_classes=5,
                                 parameter_init=0.1, subsample_list=[], subsample_type='drop')),
     ]
+    specs += _ctc_variant_specs()
+    only = _selected()
     for name, kw in specs:
+        if only and name not in only:
+            continue
         torch.manual_seed(1623)
         model = CTC(**kw)
         model.train()
@@ -401,6 +431,9 @@ def case_attention_model():
 
 if __name__ == '__main__':
     _install_shims()
+    if _selected():          # regenerate only the named model_ctc_* cases
+        case_ctc_model()
+        sys.exit(0)
     case_ctc()
     case_encoder()
     case_attention_step()

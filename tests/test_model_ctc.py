@@ -22,7 +22,11 @@ def _build(kw):
     return CTC(**kw)
 
 
-@pytest.mark.parametrize('name', ['model_ctc_sub', 'model_ctc_fast'])
+CTC_MODELS = ['model_ctc_sub', 'model_ctc_fast', 'model_ctc_proj', 'model_ctc_concat',
+              'model_ctc_proj_concat', 'model_ctc_res', 'model_ctc_dres']
+
+
+@pytest.mark.parametrize('name', CTC_MODELS)
 def test_init_matches_reference_state_dict(name):
     d = golden(name)
     kw = json.loads(str(d['kwargs']))
@@ -65,7 +69,7 @@ def _to_gpu_model(kw, sd, dev):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('name', ['model_ctc_sub', 'model_ctc_fast'])
+@pytest.mark.parametrize('name', CTC_MODELS)
 def test_ctc_model_matches_golden(name, cuda_dev):
     from pytorch_end2end_speech_recognition_amd import native_ops
     native_ops.set_compute_dtype('fp32')
@@ -124,3 +128,51 @@ def test_train_step_matches_torch_adam(cuda_dev):
     for k, v in model.state_dict().items():
         np.testing.assert_allclose(v.cpu().numpy(), p[k].detach().numpy(), rtol=1e-4, atol=1e-6,
                                    err_msg=k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('variant', [dict(encoder_num_proj=48, subsample_type='concat'),
+                                     dict(encoder_residual=True, subsample_type='concat'),
+                                     dict(encoder_dense_residual=True, encoder_num_proj=64,
+                                          subsample_list=[])])
+def test_encoder_variants_bf16_vs_oracle(variant, cuda_dev):
+    """bf16 mode (staged bf16 operands, incl. the in-place 'concat' rows of
+    twice the source width) for projection / concat / residual encoders at
+    H = 64 vs the fp32 CPU oracle."""
+    from pytorch_end2end_speech_recognition_amd import native_ops
+    kw = dict(input_size=16, encoder_type='lstm', encoder_bidirectional=True,
+              encoder_num_units=64, encoder_num_proj=0, encoder_num_layers=4, fc_list=[],
+              dropout_input=0, dropout_encoder=0, num_classes=9, parameter_init=0.1,
+              subsample_list=[True, False, False, False], subsample_type='drop')
+    kw.update(variant)
+    model = _build(kw)
+    sd = {k: v.clone() for k, v in model.state_dict().items()}
+    rng = np.random.RandomState(5)
+    B, T = 4, 41
+    x_lens = np.array([41, 33, 27, 40], np.int32)
+    y_lens = np.array([6, 4, 5, 3], np.int32)
+    xs = rng.randn(B, T, 16).astype(np.float32)
+    for b in range(B):
+        xs[b, x_lens[b]:] = 0
+    ys = np.full((B, 6), -1, np.int32)
+    for b in range(B):
+        ys[b, :y_lens[b]] = rng.randint(0, 9, y_lens[b])
+    from test_oracle_golden import ctc_cfg
+    p = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+    ref, _, _, _ = asr_ref.ctc_model_loss(p, ctc_cfg(kw), xs, ys, x_lens, y_lens)
+    ref.backward()
+    native_ops.set_compute_dtype('bf16')
+    try:
+        model.set_cuda()
+        model.zero_grad()
+        loss = model(xs, ys, x_lens, y_lens)
+        loss.backward()
+        torch.cuda.synchronize()
+    finally:
+        native_ops.set_compute_dtype('fp32')
+    assert abs(loss.item() - ref.item()) / abs(ref.item()) < 2e-2
+    for k, prm in model.named_parameters():
+        ga = p[k].grad.numpy()
+        gw = prm.grad.cpu().numpy()
+        scale = np.abs(ga).max() + 1e-6
+        assert np.abs(gw - ga).max() / scale < 5e-2, (k, np.abs(gw - ga).max(), scale)

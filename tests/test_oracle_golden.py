@@ -65,12 +65,24 @@ def test_attention_step_oracle_matches_golden():
         np.testing.assert_allclose(_g(v), g[k], rtol=1e-4, atol=1e-6, err_msg=k)
 
 
-@pytest.mark.parametrize('name', ['model_ctc_sub', 'model_ctc_fast'])
+CTC_MODELS = ['model_ctc_sub', 'model_ctc_fast', 'model_ctc_proj', 'model_ctc_concat',
+              'model_ctc_proj_concat', 'model_ctc_res', 'model_ctc_dres']
+
+
+def ctc_cfg(kw):
+    """Oracle encoder config from the CTC constructor kwargs."""
+    return dict(num_layers=kw['encoder_num_layers'], subsample_list=kw['subsample_list'],
+                fc_list=kw['fc_list'], num_proj=kw.get('encoder_num_proj', 0),
+                subsample_type=kw.get('subsample_type', 'drop'),
+                residual=kw.get('encoder_residual', False),
+                dense_residual=kw.get('encoder_dense_residual', False))
+
+
+@pytest.mark.parametrize('name', CTC_MODELS)
 def test_ctc_model_oracle_matches_golden(name):
     d = golden(name)
     kw = json.loads(str(d['kwargs']))
-    cfg = dict(num_layers=kw['encoder_num_layers'], subsample_list=kw['subsample_list'],
-               fc_list=kw['fc_list'])
+    cfg = ctc_cfg(kw)
     p, g = golden_params(d)
     for v in p.values():
         v.requires_grad_(True)
