@@ -349,6 +349,57 @@ def attention_model_loss(p, cfg, xs, ys, x_lens, y_lens, train=None):
     return loss
 
 
+def attention_greedy_decode(p, cfg, xs, x_lens, max_len):
+    """AttentionSeq2seq.decode(beam_width=1) (attention_seq2seq.py:866-1036):
+    bahdanau order, forward decoder, eval mode.  At t = 0 there is no
+    recurrence (the <sos> embedding is computed but unused); afterwards the
+    input is embed(argmax logits_{t-1}) (torch.max, first maximum); the loop
+    stops after the first step at which every utterance emits <eos>.  Returns
+    (best_hyps int64 [B, T_out], aw [B, T_out, T], perm) in sorted order."""
+    xs_t = torch.from_numpy(np.asarray(xs, np.float32))
+    enc_cfg = dict(num_layers=cfg['encoder_num_layers'], subsample_list=cfg['subsample_list'])
+    with torch.no_grad():
+        enc_out, enc_lens, perm = blstm_encoder(p, 'encoder.', enc_cfg, xs_t, x_lens)
+        B, T, E = enc_out.shape
+        eos = cfg['num_classes']
+        D = cfg['decoder_num_units']
+        pre = 'attend_0_fwd.'
+        enc_out_a = linear_nd(p, pre + 'W_enc_head0', enc_out)
+        init = cfg.get('init_dec_state', 'first')
+        c = enc_out.new_zeros(B, D)
+        if init == 'zero':
+            h = enc_out.new_zeros(B, D)
+        else:
+            src = {'mean': enc_out.mean(1), 'final': enc_out[:, -1], 'first': enc_out[:, 0]}[init]
+            h = torch.tanh(linear_nd(p, 'W_dec_init_0_fwd', src))
+        dec_out = h
+        aw = enc_out.new_zeros(B, T)
+        ctx = enc_out.new_zeros(B, E)
+        if cfg.get('label_smoothing_prob', 0) > 0:
+            emb_w = p['embed_0.embed.fc.weight'].t()
+        else:
+            emb_w = p['embed_0.embed.weight']
+        tok = torch.full((B,), eos, dtype=torch.long)        # <sos> == <eos> index
+        hyps, aws = [], []
+        for t in range(max_len):
+            if t > 0:
+                dec_in = torch.cat([emb_w[tok], ctx], dim=-1)
+                h, c = lstm_cell(p, 'decoder_0_fwd.lstm_l0', dec_in, h, c)
+                dec_out = h
+            ctx, aw = location_attention(p, pre, enc_out, enc_out_a, enc_lens, dec_out, aw,
+                                         cfg.get('sharpening_factor', 1),
+                                         cfg.get('sigmoid_smoothing', False))
+            z = torch.tanh(linear_nd(p, 'W_d_0_fwd', dec_out) + linear_nd(p, 'W_c_0_fwd', ctx))
+            logits = linear_nd(p, 'fc_0_fwd', z)
+            tok = torch.from_numpy(np.argmax(logits.numpy(), axis=1))   # first maximum
+            hyps.append(tok)
+            aws.append(aw)
+            if bool((tok == eos).all()):
+                break
+    return (torch.stack(hyps, 1).numpy().astype(np.int64), torch.stack(aws, 1).numpy(),
+            perm)
+
+
 def embedding_padding_row(cfg):
     """nn.Embedding(padding_idx=-1) in linear.py:63-64 zeroes the gradient of
     row num_classes (= <sos>/<eos>); the oracle applies it post-backward."""

@@ -323,7 +323,42 @@ class AttentionSeq2seq(ModelBase):
         best = np.array([h - 1 for h in hyps] + [None], dtype=object)[:-1]
         return best, self.encoder.last_perm_np.copy()
 
+    @torch.no_grad()
     def decode(self, xs, x_lens, beam_width, max_decode_len, min_decode_len=0,
                length_penalty=0, coverage_penalty=0, task_index=0, resolving_unk=False):
-        raise NotImplementedError('attention inference decoding (greedy / beam) is a next-round '
-                                  'item (SURVEY §8f rank 2)')
+        """:866-915.  Returns (best_hyps int64 [B, T_out], aw [B, T_out, T_in],
+        perm_idx), rows in the encoder's length-sorted order like the reference."""
+        self.eval()
+        if beam_width != 1:
+            raise NotImplementedError('attention beam search (attention_seq2seq.py:1037-1237)')
+        xs_d = self.np2var(xs, dtype='float')
+        enc_out, enc_lens_d, _ = self._encode(xs_d, x_lens)
+        best_hyps, aw = self._decode_infer_greedy(enc_out, enc_lens_d, max_decode_len)
+        return best_hyps, aw, self.encoder.last_perm_np.copy()
+
+    def _decode_infer_greedy(self, enc_out, x_lens, max_decode_len, task=0, dir='fwd'):
+        """:917-1036 (bahdanau order, forward decoder): the whole loop is one
+        fused decoder pass (native_ops.att_decode_greedy); the reference's early
+        exit -- stop after the first step at which EVERY utterance emits <eos>
+        -- becomes a truncation of the per-step tokens, which it does not change
+        because later steps never feed back into earlier ones."""
+        att = self.attend_0_fwd
+        cell = self.decoder_0_fwd.lstm_l0
+        W_d, W_c = self.W_d_0_fwd, self.W_c_0_fwd
+        emb_ls = isinstance(self.embed_0, Embedding_LS)
+        emb_w = self.embed_0.embed.fc.weight if emb_ls else self.embed_0.embed.weight
+        h0 = self._init_h0(enc_out)
+        enc_a = att.W_enc_head0(enc_out)
+        gen = dict(w_d=W_d.fc.weight, b_d=W_d.fc.bias, w_c=W_c.fc.weight, b_c=W_c.fc.bias,
+                   w_fc=self.fc_0_fwd.fc.weight, b_fc=self.fc_0_fwd.fc.bias, emb_w=emb_w,
+                   emb_trans=int(emb_ls), b_ih=cell.bias_ih, b_hh=cell.bias_hh)
+        toks, aw = ops.att_decode_greedy(enc_out, enc_a, x_lens, h0, self.embedding_dim,
+                                         self.sharpening_factor, self.sigmoid_smoothing,
+                                         cell.weight_ih, cell.weight_hh,
+                                         att.W_dec_head0.fc.weight, att.W_conv_head0.fc.weight,
+                                         att.conv_head0.weight, att.V_head0.fc.weight, gen,
+                                         max_decode_len)
+        toks = toks.cpu().numpy()
+        all_eos = np.nonzero((toks == self.eos_0).all(axis=0))[0]
+        n = int(all_eos[0]) + 1 if len(all_eos) else toks.shape[1]   # :1017-1019
+        return toks[:, :n], aw[:, :n].cpu().numpy()

@@ -243,6 +243,64 @@ def linear2(x1, w1, b1, x2, w2, b2):
 # ---------------------------------------------------------------------------
 # Teacher-forced location-attention decoder loop (attention_seq2seq.py:704-799)
 # ---------------------------------------------------------------------------
+def _attdec_forward(enc, enc_a, lens, pre_emb, h0, emb_dim, sharpen, sigmoid, w_ih, w_hh, w_dec,
+                    w_conv, conv_w, v, train_opts):
+    """One asr_attdec_forward_ex call over S = pre_emb.shape[1] steps.  Returns
+    (dims, (dec, cst, gates, x, ctx, aw), opts, buffers kept alive)."""
+    N.require_device(enc, enc_a, lens, pre_emb, w_ih)
+    B, T, E = enc.shape
+    A = enc_a.shape[-1]
+    D = w_hh.shape[1]
+    S = pre_emb.shape[1]
+    C, K = conv_w.shape[0], conv_w.shape[-1]
+    dims = N.AttDecDims(B, T, E, A, C, K, D, S, float(sharpen), int(bool(sigmoid)))
+    dev = enc.device
+    cd = compute_dtype()
+    f32 = dict(dtype=torch.float32, device=dev)
+    dec = torch.empty(B, S, D, **f32)
+    cst = torch.empty(B, S, D, **f32)
+    gates = torch.empty(B, S, 4 * D, **f32)
+    x = torch.empty(B, S, E + D, **f32)
+    ctxv = torch.empty(B, S, E, **f32)
+    aw = torch.empty(B, S, T, **f32)
+    nb = N.query('asr_attdec_workspace_bytes', ctypes.byref(dims), cd, 0)
+    ws = _ws(nb, dev)
+    ld_ih = w_ih.shape[1]
+    w_ih_ctx = ctypes.c_void_p(w_ih.data_ptr() + 4 * emb_dim)
+    opts, keep = _attdec_opts(train_opts, B, S, D, emb_dim, w_ih, dev)
+    N.call('asr_attdec_forward_ex', ctypes.byref(dims), N.ptr_struct(opts), cd, N.ptr(enc),
+           N.ptr(enc_a), N.ptr(lens), w_ih_ctx, ld_ih, N.ptr(w_hh), N.ptr(w_dec),
+           N.ptr(w_conv), N.ptr(conv_w), N.ptr(v), N.ptr(pre_emb),
+           N.ptr(h0.contiguous() if h0 is not None else None), N.ptr(dec), N.ptr(cst),
+           N.ptr(gates), N.ptr(x), N.ptr(ctxv), N.ptr(aw), N.ptr(ws), nb,
+           N.stream_handle(dev))
+    return dims, (dec, cst, gates, x, ctxv, aw), opts, keep
+
+
+@torch.no_grad()
+def att_decode_greedy(enc, enc_a, lens, h0, emb_dim, sharpen, sigmoid, w_ih, w_hh, w_dec, w_conv,
+                      conv_w, v, gen, max_len):
+    """Greedy attention decoding (attention_seq2seq.py:917-1036, bahdanau
+    order) as ONE fused decoder pass: every step t >= 1 is a sampled step whose
+    input token is the in-loop first argmax of logits_{t-1} = fc(tanh(W_d dec +
+    b_d + W_c ctx + b_c)) -- the same machinery as scheduled sampling, with no
+    dropout.  S = max_len + 1 steps run so the argmax of step max_len - 1 is
+    produced too.  gen: dict(w_d, b_d, w_c, b_c, w_fc, b_fc, emb_w, emb_trans,
+    b_ih, b_hh).  Returns (tokens int64 [B, max_len], aw [B, max_len, T]) on
+    the device, before the all-<eos> truncation."""
+    enc, enc_a = enc.contiguous(), enc_a.contiguous()
+    B = enc.shape[0]
+    D = w_hh.shape[1]
+    S = int(max_len) + 1
+    pre_emb = torch.zeros(B, S, 4 * D, dtype=torch.float32, device=enc.device)  # never read
+    flags = np.ones(S, np.int32)
+    flags[0] = 0
+    _, outs, _, keep = _attdec_forward(enc, enc_a, lens, pre_emb, h0, emb_dim, sharpen, sigmoid,
+                                       w_ih, w_hh, w_dec, w_conv, conv_w, v,
+                                       dict(gen, ss_steps=flags))
+    return keep['tok_ss'][:, 1:], outs[5][:, :S - 1]
+
+
 class AttDecoderFn(torch.autograd.Function):
     """Returns (dec_out [B,S,D], ctx [B,S,E], aw [B,S,T]).  Weights:
     w_ih [4D, emb+E] (LSTMCell; only the context columns are used here, the
@@ -252,34 +310,10 @@ class AttDecoderFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, enc, enc_a, lens, pre_emb, h0, emb_dim, sharpen, sigmoid, w_ih, w_hh,
                 w_dec, w_conv, conv_w, v, train_opts):
-        N.require_device(enc, enc_a, lens, pre_emb, w_ih)
         enc, enc_a, pre_emb = enc.contiguous(), enc_a.contiguous(), pre_emb.contiguous()
-        B, T, E = enc.shape
-        A = enc_a.shape[-1]
-        D = w_hh.shape[1]
-        S = pre_emb.shape[1]
-        C, K = conv_w.shape[0], conv_w.shape[-1]
-        dims = N.AttDecDims(B, T, E, A, C, K, D, S, float(sharpen), int(bool(sigmoid)))
-        dev = enc.device
-        cd = compute_dtype()
-        f32 = dict(dtype=torch.float32, device=dev)
-        dec = torch.empty(B, S, D, **f32)
-        cst = torch.empty(B, S, D, **f32)
-        gates = torch.empty(B, S, 4 * D, **f32)
-        x = torch.empty(B, S, E + D, **f32)
-        ctxv = torch.empty(B, S, E, **f32)
-        aw = torch.empty(B, S, T, **f32)
-        nb = N.query('asr_attdec_workspace_bytes', ctypes.byref(dims), cd, 0)
-        ws = _ws(nb, dev)
-        ld_ih = w_ih.shape[1]
-        w_ih_ctx = ctypes.c_void_p(w_ih.data_ptr() + 4 * emb_dim)
-        opts, keep = _attdec_opts(train_opts, B, S, D, emb_dim, w_ih, dev)
-        N.call('asr_attdec_forward_ex', ctypes.byref(dims), N.ptr_struct(opts), cd, N.ptr(enc),
-               N.ptr(enc_a), N.ptr(lens), w_ih_ctx, ld_ih, N.ptr(w_hh), N.ptr(w_dec),
-               N.ptr(w_conv), N.ptr(conv_w), N.ptr(v), N.ptr(pre_emb),
-               N.ptr(h0.contiguous() if h0 is not None else None), N.ptr(dec), N.ptr(cst),
-               N.ptr(gates), N.ptr(x), N.ptr(ctxv), N.ptr(aw), N.ptr(ws), nb,
-               N.stream_handle(dev))
+        dims, (dec, cst, gates, x, ctxv, aw), opts, keep = _attdec_forward(
+            enc, enc_a, lens, pre_emb, h0, emb_dim, sharpen, sigmoid, w_ih, w_hh, w_dec, w_conv,
+            conv_w, v, train_opts)
         ctx.save_for_backward(enc, enc_a, lens, w_ih, w_hh, w_dec, w_conv, conv_w, v, dec, cst,
                               gates, x, aw)
         ctx.meta = (dims, emb_dim, h0 is not None)

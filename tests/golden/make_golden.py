@@ -429,10 +429,63 @@ def case_attention_model():
               **_sd(model), **_grads(model))
 
 
+# --------------------------------------------------------------------------
+# Case 7: greedy attention decoding (attention_seq2seq.py:866-1036)
+# --------------------------------------------------------------------------
+def case_attention_decode():
+    """AttentionSeq2seq.decode(beam_width=1) on random-init models (uniform
+    +-1.5).  The init seed is the first of 1623, 1624, ... whose decode is not
+    constant (at least three distinct tokens); in the 'eos' case it is the
+    first whose all-<eos> early exit fires after more than one step."""
+    from models.pytorch_v3.attention.attention_seq2seq import AttentionSeq2seq
+    base = dict(input_size=8, encoder_type='lstm', encoder_bidirectional=True,
+                encoder_num_units=6, encoder_num_proj=0, encoder_num_layers=2,
+                attention_type='location', attention_dim=7, decoder_type='lstm',
+                decoder_num_units=9, decoder_num_layers=1, embedding_dim=4,
+                dropout_input=0, dropout_encoder=0, dropout_decoder=0, dropout_embedding=0,
+                num_classes=5, parameter_init=0.1, subsample_list=[False, True],
+                subsample_type='drop', attention_conv_num_channels=3,
+                attention_conv_width=5, bottleneck_dim=11, decoding_order='bahdanau',
+                ctc_loss_weight=0, label_smoothing_prob=0)
+    specs = [
+        ('dec_att', dict(base, init_dec_state='zero'), False),
+        ('dec_att_first', dict(base, init_dec_state='first', sharpening_factor=1.5), False),
+        ('dec_att_eos', dict(base, init_dec_state='zero', num_classes=3), True),
+    ]
+    only = _selected()
+    max_len = 12
+    rng0 = np.random.RandomState(6)
+    B, T = 4, 22
+    x_lens = np.array([22, 17, 20, 11], np.int32)
+    xs = rng0.randn(B, T, 8).astype(np.float32)
+    for b in range(B):
+        xs[b, x_lens[b]:] = 0
+    for name, kw, want_exit in specs:
+        if only and name not in only:
+            continue
+        for seed in range(1623, 1623 + 500):
+            torch.manual_seed(seed)
+            model = AttentionSeq2seq(**kw)
+            for p in model.parameters():
+                torch.nn.init.uniform_(p, -1.5, 1.5)
+            hyps, aw, perm = model.decode(xs, x_lens, beam_width=1, max_decode_len=max_len)
+            hyps = np.asarray(hyps)
+            ok = (1 < hyps.shape[1] < max_len) if want_exit else len(np.unique(hyps)) >= 3
+            if ok:
+                break
+        else:
+            raise RuntimeError('no seed found for ' + name)
+        _save(name, kwargs=np.array(json.dumps(kw)), seed=np.array([seed]), xs=xs,
+              x_lens=x_lens, max_decode_len=np.array([max_len]),
+              best_hyps=hyps.astype(np.int64), aw=np.asarray(aw, np.float32),
+              perm=np.asarray(perm).astype(np.int64), **_sd(model))
+
+
 if __name__ == '__main__':
     _install_shims()
-    if _selected():          # regenerate only the named model_ctc_* cases
+    if _selected():          # regenerate only the named model_ctc_* / dec_* cases
         case_ctc_model()
+        case_attention_decode()
         sys.exit(0)
     case_ctc()
     case_encoder()
@@ -441,3 +494,4 @@ if __name__ == '__main__':
     case_vgg_model()
     case_hier_ctc_model()
     case_attention_model()
+    case_attention_decode()
