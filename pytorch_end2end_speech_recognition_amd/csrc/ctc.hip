@@ -10,12 +10,15 @@
 //   ctc_emit    one wave per (b,t) row: log-sum-exp over V (one HBM read of the
 //               row) and the S emissions e_t(s) = x[lab(s)] - lse, stored
 //               lattice-contiguous so the sequential kernel streams them.
-//   ctc_lattice one wave per utterance; lane l owns K consecutive lattice states
-//               in registers; alpha forward over t with two wave shuffles per
-//               step, then beta backward fused with the occupancy
-//               exp(alpha+beta-e-logP) written over alpha.  No LDS, no barrier.
-//   ctc_grad    one row per block: grad = (softmax - occupancy) * scale written
-//               once; occupancy of repeated labels summed through LDS.
+//   ctc_lattice two waves per utterance, run concurrently: the alpha wave
+//               (forward over t, then log P and the cost) and the beta wave
+//               (backward over t); lane l owns K consecutive lattice states in
+//               registers, neighbours come through DPP wave shifts (one
+//               v_mov_dpp per step, no LDS, no barrier).  The sequential depth
+//               is T steps, not the 2T of an alpha-then-beta pass.
+//   ctc_grad    one row per block: occupancy exp(alpha+beta-e-logP) of the
+//               row's S states, summed per class through LDS (repeated
+//               labels), grad = (softmax - occupancy) * scale written once.
 //   ctc_loss    1 block: loss = scale * sum_b cost_b (fixed-order tree).
 #include "common.h"
 #include "prof.h"
@@ -28,7 +31,8 @@ constexpr int kMaxK = 16;  // up to 64*16 = 1024 lattice states (labels <= 511)
 struct CtcWs {
   float* lse;      // [B*T]
   float* emit;     // [B*T*Spad]
-  float* occ;      // [B*T*Spad]  alpha, then occupancy
+  float* alpha;    // [B*T*Spad]
+  float* beta;     // [B*T*Spad]
   float* logp;     // [B]
   int32_t* offs;   // [B]
   int32_t* status; // [4]
@@ -50,7 +54,8 @@ inline size_t ws_layout(int T, int B, int max_label_len, CtcWs* ws, char* base) 
   char* p;
   p = take(sizeof(float) * (size_t)B * T);                 if (ws) ws->lse = (float*)p;
   p = take(sizeof(float) * (size_t)B * T * Spad);          if (ws) ws->emit = (float*)p;
-  p = take(sizeof(float) * (size_t)B * T * Spad);          if (ws) ws->occ = (float*)p;
+  p = take(sizeof(float) * (size_t)B * T * Spad);          if (ws) ws->alpha = (float*)p;
+  p = take(sizeof(float) * (size_t)B * T * Spad);          if (ws) ws->beta = (float*)p;
   p = take(sizeof(float) * (size_t)B);                     if (ws) ws->logp = (float*)p;
   p = take(sizeof(int32_t) * (size_t)B);                   if (ws) ws->offs = (int32_t*)p;
   p = take(sizeof(int32_t) * 4);                           if (ws) ws->status = (int32_t*)p;
@@ -147,19 +152,31 @@ __device__ __forceinline__ void store_k(float* p, const float (&r)[K]) {
   }
 }
 
-// One wave per utterance.  Lane l owns lattice states s = l*K + k.
+// DPP wave shifts (GFX9 wave_shr:1 / wave_shl:1): lane i receives lane i-1 /
+// i+1; the lane without a source receives 0 (callers overwrite it).
+__device__ __forceinline__ float from_lower_lane(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float from_upper_lane(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x130, 0xf, 0xf, false));
+}
+
+// Two waves per utterance (blockIdx.y: 0 = alpha, 1 = beta).  Lane l owns
+// lattice states s = l*K + k.
 template <int K>
 __global__ void __launch_bounds__(64) ctc_lattice(int T, const int32_t* __restrict__ labels,
                                                   const int32_t* __restrict__ label_lens,
                                                   const int32_t* __restrict__ act_lens,
                                                   const int32_t* __restrict__ offs, int blank,
                                                   int zero_infinity, const float* __restrict__ emit,
-                                                  float* __restrict__ occ,
+                                                  float* __restrict__ alpha,
+                                                  float* __restrict__ beta,
                                                   float* __restrict__ logp_out,
                                                   float* __restrict__ costs) {
   constexpr int Spad = 64 * K;
   constexpr int D = 4;  // emission prefetch distance (steps)
   const int b = blockIdx.x;
+  const bool is_beta = blockIdx.y == 1;
   const int lane = threadIdx.x;
   const int Tb = min(act_lens[b], T);
   const int L = min(label_lens[b], (Spad - 1) / 2);
@@ -168,7 +185,7 @@ __global__ void __launch_bounds__(64) ctc_lattice(int T, const int32_t* __restri
   const float NEG = neg_inf();
 
   if (Tb <= 0) {
-    if (lane == 0) {
+    if (lane == 0 && !is_beta) {
       bool feas = (L == 0);
       logp_out[b] = feas ? 0.f : NEG;
       costs[b] = feas ? 0.f : (zero_infinity ? 0.f : __builtin_huge_valf());
@@ -176,133 +193,121 @@ __global__ void __launch_bounds__(64) ctc_lattice(int T, const int32_t* __restri
     return;
   }
 
-  // skip[k]: transition s-2 -> s allowed (s odd label state, label differs).
-  bool skip[K];
   bool valid[K];
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const int s = lane * K + k;
-    valid[k] = s < S;
-    skip[k] = false;
-    if ((s & 1) && s >= 3 && s < S) skip[k] = lab[s >> 1] != lab[(s >> 1) - 1];
+  for (int k = 0; k < K; ++k) valid[k] = lane * K + k < S;
+  const float* E = emit + (size_t)b * T * Spad + lane * K;
+  float eb[D][K];
+
+  if (!is_beta) {
+    // ---------------- alpha ----------------
+    // skip[k]: transition s-2 -> s allowed (s odd label state, label differs).
+    bool skip[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int s = lane * K + k;
+      skip[k] = (s & 1) && s >= 3 && s < S && lab[s >> 1] != lab[(s >> 1) - 1];
+    }
+    float* A = alpha + (size_t)b * T * Spad + lane * K;
+    float a[K];
+    {
+      float e0[K];
+      load_k<K>(e0, E);
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int s = lane * K + k;
+        a[k] = (s < 2 && valid[k]) ? e0[k] : NEG;
+      }
+      store_k<K>(A, a);
+    }
+#pragma unroll
+    for (int j = 0; j < D; ++j) load_k<K>(eb[j], E + (size_t)min(1 + j, T - 1) * Spad);
+
+    for (int t0 = 1; t0 < Tb; t0 += D) {
+#pragma unroll
+      for (int j = 0; j < D; ++j) {
+        const int t = t0 + j;
+        if (t < Tb) {
+          float p1 = from_lower_lane(a[K - 1]);
+          float p2 = (K >= 2) ? from_lower_lane(a[K >= 2 ? K - 2 : 0]) : from_lower_lane(p1);
+          if (lane == 0) { p1 = NEG; p2 = NEG; }
+          if (K == 1 && lane == 1) p2 = NEG;
+          float n[K];
+#pragma unroll
+          for (int k = 0; k < K; ++k) {
+            const float a1 = (k >= 1) ? a[k >= 1 ? k - 1 : 0] : p1;
+            const float a2 = (k >= 2) ? a[k >= 2 ? k - 2 : 0] : ((k == 1) ? p1 : p2);
+            const float v = lse3(a[k], a1, skip[k] ? a2 : NEG) + eb[j][k];
+            n[k] = valid[k] ? v : NEG;
+          }
+#pragma unroll
+          for (int k = 0; k < K; ++k) a[k] = n[k];
+          store_k<K>(A + (size_t)t * Spad, a);
+          load_k<K>(eb[j], E + (size_t)min(t + D, T - 1) * Spad);
+        }
+      }
+    }
+
+    // log P from the last two states at t = Tb-1
+    float part = NEG;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int s = lane * K + k;
+      if (s == S - 1 || s == S - 2) part = lse2(part, a[k]);
+    }
+    float mx = wave_max(part);
+    float sm = (mx == NEG) ? 0.f : wave_sum(__expf(part - mx));
+    const float logP = (mx == NEG) ? NEG : mx + __logf(sm);
+    if (lane == 0) {
+      logp_out[b] = logP;
+      costs[b] = (logP == NEG) ? (zero_infinity ? 0.f : __builtin_huge_valf()) : -logP;
+    }
+    return;
   }
+
+  // ---------------- beta ----------------
   // skipf[k]: transition s -> s+2 allowed (== skip of state s+2).
   bool skipf[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const int s = lane * K + k;
-    skipf[k] = false;
-    if ((s & 1) && s + 2 < S) skipf[k] = lab[s >> 1] != lab[(s >> 1) + 1];
+    skipf[k] = (s & 1) && s + 2 < S && lab[s >> 1] != lab[(s >> 1) + 1];
   }
-
-  const float* E = emit + (size_t)b * T * Spad + lane * K;
-  float* A = occ + (size_t)b * T * Spad + lane * K;
-
-  // ---------------- alpha ----------------
-  float a[K];
-  {
-    float e0[K];
-    load_k<K>(e0, E);
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int s = lane * K + k;
-      a[k] = (s < 2 && valid[k]) ? e0[k] : NEG;
-    }
-    store_k<K>(A, a);
-  }
-  float eb[D][K];
-#pragma unroll
-  for (int j = 0; j < D; ++j) load_k<K>(eb[j], E + (size_t)min(1 + j, T - 1) * Spad);
-
-  for (int t0 = 1; t0 < Tb; t0 += D) {
-#pragma unroll
-    for (int j = 0; j < D; ++j) {
-      const int t = t0 + j;
-      if (t < Tb) {
-        float p1 = __shfl_up(a[K - 1], 1, 64);
-        float p2 = (K >= 2) ? __shfl_up(a[K >= 2 ? K - 2 : 0], 1, 64) : __shfl_up(a[0], 2, 64);
-        if (lane == 0) { p1 = NEG; p2 = NEG; }
-        if (K == 1 && lane == 1) p2 = NEG;
-        float n[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          const float a1 = (k >= 1) ? a[k >= 1 ? k - 1 : 0] : p1;
-          const float a2 = (k >= 2) ? a[k >= 2 ? k - 2 : 0] : ((k == 1) ? p1 : p2);
-          const float v = lse3(a[k], a1, skip[k] ? a2 : NEG) + eb[j][k];
-          n[k] = valid[k] ? v : NEG;
-        }
-#pragma unroll
-        for (int k = 0; k < K; ++k) a[k] = n[k];
-        store_k<K>(A + (size_t)t * Spad, a);
-        load_k<K>(eb[j], E + (size_t)min(t + D, T - 1) * Spad);
-      }
-    }
-  }
-
-  // log P from the last two states at t = Tb-1
-  float part = NEG;
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const int s = lane * K + k;
-    if (s == S - 1 || s == S - 2) part = lse2(part, a[k]);
-  }
-  // wave log-sum-exp reduction of `part`
-  float mx = wave_max(part);
-  float sm = (mx == NEG) ? 0.f : wave_sum(__expf(part - mx));
-  const float logP = (mx == NEG) ? NEG : mx + __logf(sm);
-  if (lane == 0) {
-    logp_out[b] = logP;
-    costs[b] = (logP == NEG) ? (zero_infinity ? 0.f : __builtin_huge_valf()) : -logP;
-  }
-  if (logP == NEG) return;
-
-  // ---------------- beta + occupancy ----------------
+  float* Bt = beta + (size_t)b * T * Spad + lane * K;
   float be[K];
   {
-    const int t = Tb - 1;
-    float et[K], at[K];
-    load_k<K>(et, E + (size_t)t * Spad);
-    load_k<K>(at, A + (size_t)t * Spad);
-    float o[K];
+    float et[K];
+    load_k<K>(et, E + (size_t)(Tb - 1) * Spad);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const int s = lane * K + k;
       be[k] = (valid[k] && (s == S - 1 || s == S - 2)) ? et[k] : NEG;
-      o[k] = valid[k] ? __expf(at[k] + be[k] - et[k] - logP) : 0.f;
     }
-    store_k<K>(A + (size_t)t * Spad, o);
+    store_k<K>(Bt + (size_t)(Tb - 1) * Spad, be);
   }
-  float ab[D][K];
 #pragma unroll
-  for (int j = 0; j < D; ++j) {
-    const int t = max(Tb - 2 - j, 0);
-    load_k<K>(eb[j], E + (size_t)t * Spad);
-    load_k<K>(ab[j], A + (size_t)t * Spad);
-  }
+  for (int j = 0; j < D; ++j) load_k<K>(eb[j], E + (size_t)max(Tb - 2 - j, 0) * Spad);
   for (int t0 = Tb - 2; t0 >= 0; t0 -= D) {
 #pragma unroll
     for (int j = 0; j < D; ++j) {
       const int t = t0 - j;
       if (t >= 0) {
-        float n1 = __shfl_down(be[0], 1, 64);
-        float n2 = (K >= 2) ? __shfl_down(be[K >= 2 ? 1 : 0], 1, 64) : __shfl_down(be[0], 2, 64);
+        float n1 = from_upper_lane(be[0]);
+        float n2 = (K >= 2) ? from_upper_lane(be[K >= 2 ? 1 : 0]) : from_upper_lane(n1);
         if (lane == 63) { n1 = NEG; n2 = NEG; }
         if (K == 1 && lane == 62) n2 = NEG;
-        float n[K], o[K];
+        float n[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
           const float b1 = (k < K - 1) ? be[k < K - 1 ? k + 1 : 0] : n1;
           const float b2 = (k < K - 2) ? be[k < K - 2 ? k + 2 : 0] : ((k == K - 2) ? n1 : n2);
           const float v = lse3(be[k], b1, skipf[k] ? b2 : NEG) + eb[j][k];
           n[k] = valid[k] ? v : NEG;
-          o[k] = valid[k] ? __expf(ab[j][k] + n[k] - eb[j][k] - logP) : 0.f;
         }
 #pragma unroll
         for (int k = 0; k < K; ++k) be[k] = n[k];
-        store_k<K>(A + (size_t)t * Spad, o);
-        const int tn = max(t - D, 0);
-        load_k<K>(eb[j], E + (size_t)tn * Spad);
-        load_k<K>(ab[j], A + (size_t)tn * Spad);
+        store_k<K>(Bt + (size_t)t * Spad, be);
+        load_k<K>(eb[j], E + (size_t)max(t - D, 0) * Spad);
       }
     }
   }
@@ -313,7 +318,8 @@ __global__ void ctc_grad(const float* __restrict__ acts, long long st, long long
                          const int32_t* __restrict__ labels, const int32_t* __restrict__ label_lens,
                          const int32_t* __restrict__ act_lens, const int32_t* __restrict__ offs,
                          int blank, int Spad, const float* __restrict__ lse,
-                         const float* __restrict__ occ, const float* __restrict__ logp,
+                         const float* __restrict__ emit, const float* __restrict__ alpha,
+                         const float* __restrict__ beta, const float* __restrict__ logp,
                          const float* __restrict__ grad_scale, float scale_mul,
                          float* __restrict__ grads,
                          long long gst, long long gsb) {
@@ -333,11 +339,13 @@ __global__ void ctc_grad(const float* __restrict__ acts, long long st, long long
   const int L = min(label_lens[b], (Spad - 1) / 2);
   const int S = 2 * L + 1;
   const int32_t* lab = labels + offs[b];
-  const float* o = occ + row * Spad;
+  const float* al = alpha + row * Spad;
+  const float* bt = beta + row * Spad;
+  const float* em = emit + row * Spad;
   for (int s = threadIdx.x; s < S; s += blockDim.x) {
     int c = (s & 1) ? lab[s >> 1] : blank;
     c = c < 0 ? 0 : (c >= V ? V - 1 : c);
-    atomicAdd(&acc[c], o[s]);
+    atomicAdd(&acc[c], __expf(al[s] + bt[s] - em[s] - lp));
   }
   __syncthreads();
   const float* x = acts + (long long)t * st + (long long)b * sb;
@@ -410,8 +418,9 @@ extern "C" int asr_ctc_forward(const float* acts, long long stride_t, long long 
                      ws.lse, ws.emit);
   ASR_LAUNCH_CHECK();
 #define ASR_CTC_LAT(KK)                                                                        \
-  hipLaunchKernelGGL(ctc_lattice<KK>, dim3(B), dim3(64), 0, s, T, labels_flat, label_lens,     \
-                     act_lens, ws.offs, blank, zero_infinity, ws.emit, ws.occ, ws.logp, costs)
+  hipLaunchKernelGGL(ctc_lattice<KK>, dim3(B, 2), dim3(64), 0, s, T, labels_flat, label_lens,  \
+                     act_lens, ws.offs, blank, zero_infinity, ws.emit, ws.alpha, ws.beta,      \
+                     ws.logp, costs)
   switch (K) {
     case 1: ASR_CTC_LAT(1); break;
     case 2: ASR_CTC_LAT(2); break;
@@ -451,7 +460,8 @@ extern "C" int asr_ctc_backward(const float* acts, long long stride_t, long long
   const int pslot = prof_begin_launch(ASR_PROF_CTC_GRAD, s, 8.0 * (double)V * B * T);
   hipLaunchKernelGGL(ctc_grad, dim3((unsigned)((long long)B * T)), dim3(threads), V * sizeof(float),
                      s, acts, stride_t, stride_b, T, V, labels_flat, label_lens, act_lens, ws.offs,
-                     blank, Spad, ws.lse, ws.occ, ws.logp, grad_scale, scale, grads, gstride_t,
+                     blank, Spad, ws.lse, ws.emit, ws.alpha, ws.beta, ws.logp, grad_scale, scale,
+                     grads, gstride_t,
                      gstride_b);
   ASR_LAUNCH_CHECK();
   prof_end_launch(ASR_PROF_CTC_GRAD, pslot, s);

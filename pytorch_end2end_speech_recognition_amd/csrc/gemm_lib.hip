@@ -49,7 +49,8 @@ hipblasLtHandle_t handle() {
 bool plain(const asr_rowmap_t& m, long long rows) {
   if (m.perm || m.t_add != 0 || (m.t_mul != 0 && m.t_mul != 1)) return false;
   if (m.rows_per_b > 0 && m.stride_b != (long long)m.rows_per_b * m.stride_t) return false;
-  if (m.t_limit > 0 && m.t_limit < rows) return false;
+  // t_limit bounds the time index inside a group (rows_per_b rows), else the row
+  if (m.t_limit > 0 && m.t_limit < (m.rows_per_b > 0 ? m.rows_per_b : rows)) return false;
   return true;
 }
 

@@ -21,10 +21,12 @@
 // bf16 once at kernel start), its cell states in registers.  Work-groups are
 // pinned one per CU and the grid is launched only when it is co-resident.
 //
-//   forward  (256 threads, 4 waves split K = H): publishes h_t [R][16] as bf16
-//            pairs; consumers gather the group's whole h_t [R][H] (K of the
-//            recurrent product) -- 16 KB of granules per work-group per step at
-//            R = 8, H = 512.
+//   forward  (256 threads, 4 waves split K = H): publishes h_t [R][16] as
+//            granules of FOUR bf16 whose step tag is one bit (the LSB of the
+//            first value, tag_bit); consumers gather the group's whole h_t
+//            [R][H] (K of the recurrent product) -- 8 KB of granules per
+//            work-group per step at R = 8, H = 512 (the hop's cost grows with
+//            the bytes each consumer CU loads).
 //   backward (512 threads): the owner of units J turns dh_t(J) into the gate
 //            gradients dg_t [R][4 x 16] and multiplies them by ITS OWN 64 rows of
 //            W_hh, publishing partial sums of dh_{t-1} for ALL H units as bf16
@@ -164,6 +166,24 @@ __device__ __forceinline__ void xg_place(int WPG, int allow_local, int* hdr, int
   __syncthreads();
 }
 
+// Forward granules carry FOUR bf16 (units 4q..4q+3 of one row) and no tag
+// word: the tag is the least significant bit of the first value, the bf16
+// next to h (truncated or one ulp further out) whose LSB is tag_bit(step).
+// Steps s and s-2 share a buffer and have different bits; the memset's zeros
+// never match the first use (bit 1).  Error <= 1 bf16 ulp on one value in four
+// of the recurrent input; y / ybf keep the plain values.
+__device__ __forceinline__ unsigned tag_bit(int step) { return (((unsigned)step >> 1) & 1u) ^ 1u; }
+__device__ __forceinline__ unsigned bf_with_lsb(float h, unsigned bit) {
+  const unsigned t = __float_as_uint(h) >> 16;
+  return (t & 1u) == bit ? t : t + 1u;
+}
+// lane i <- lane i+n inside its row of 16 (DPP row_shl:n); the row's last n
+// lanes receive 0
+template <int N>
+__device__ __forceinline__ unsigned row_from_upper(unsigned x) {
+  return (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x100 + N, 0xf, 0xf, false);
+}
+
 __device__ __forceinline__ bf16x8 frag_lo(const u32x4& a, const u32x4& b) {
   // payload words of two 16-B granule pairs -> 8 bf16 (units in order)
   u32x4 w = {a[0], a[2], b[0], b[2]};
@@ -213,13 +233,13 @@ __global__ void __launch_bounds__(256 + R * XU) lstm_fwd_xg(
   if (!s_pl[3]) return;
   const int grp = s_pl[0], mem = s_pl[1];
   const bool local = s_pl[2] != 0;
-  const unsigned ep = epoch << 20;  // tag = launch epoch | (step + 1)
+  (void)epoch;  // forward granules carry a 1-bit step tag (tag_bit) instead
   const int dir = grp & 1, rg = grp >> 1;
   const int u0 = mem * XU, b0 = rg * R;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nks = H >> 5;
-  const unsigned half = (unsigned)(H / 2);
+  const unsigned quarter = (unsigned)(H / 4);   // granules per row
   unsigned long long* tr = blockIdx.x < XG_TR_WG ? g_xg_trace : nullptr;
 
   if (wave < 4) {
@@ -238,7 +258,7 @@ __global__ void __launch_bounds__(256 + R * XU) lstm_fwd_xg(
           wf[i][g] = cvt_f32x8(W + (long long)(g * H + u0 + ln) * H + 32 * ks + 8 * kq);
       }
     }
-    const unsigned xg_bytes = (unsigned)(2ull * G * R * half * 8);
+    const unsigned xg_bytes = (unsigned)(2ull * G * R * quarter * 8);
     const __amdgpu_buffer_rsrc_t rs = xg_rsrc(xg, xg_bytes);
     const int nsleep = __builtin_amdgcn_readfirstlane(g_xg_sleep);
     const int ndelay = __builtin_amdgcn_readfirstlane(g_xg_delay);
@@ -248,25 +268,23 @@ __global__ void __launch_bounds__(256 + R * XU) lstm_fwd_xg(
 #pragma unroll
       for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (s > 0) {
-        const unsigned tag = ep | (unsigned)s;
+        const unsigned ebit = tag_bit(s - 1);
         const unsigned rowoff = (unsigned)((((((s - 1) & 1) * G + grp) * R + (sweeper ? ln : 0)) *
-                                            (long long)half) * 8);
-        u32x4 v[KSW][2];
+                                            (long long)quarter) * 8);
+        u32x4 v[KSW];
         nap(ndelay);
         for (unsigned spins = 0;; ++spins) {
           const unsigned long long t_iss = tr ? __builtin_amdgcn_s_memrealtime() : 0;
           int ok = 1;  // bitwise ANDs: every load is issued before the first wait
           if (sweeper) {
             // k-steps past nks re-read the last one (no branch between the loads)
+            // k = 32 ks + 8 kq + 0..7: two granules, one 16-B load
 #pragma unroll
-            for (int i = 0; i < KSW; ++i) {
-              const unsigned off =
-                  rowoff + (unsigned)((16 * min(wave + 4 * i, nks - 1) + 4 * kq) * 8);
-              v[i][0] = ld_sc1(rs, off);
-              v[i][1] = ld_sc1(rs, off + 16);
-            }
+            for (int i = 0; i < KSW; ++i)
+              v[i] = ld_sc1(rs, rowoff + (unsigned)((8 * min(wave + 4 * i, nks - 1) + 2 * kq) * 8));
 #pragma unroll
-            for (int i = 0; i < KSW; ++i) ok &= tags_ok(v[i][0], tag) & tags_ok(v[i][1], tag);
+            for (int i = 0; i < KSW; ++i)
+              ok &= (int)((((v[i][0] ^ ebit) | (v[i][2] ^ ebit)) & 1u) == 0u);
           }
           if (__all(ok)) {
             XG_TR(s, 1, __builtin_amdgcn_s_memrealtime());
@@ -286,7 +304,7 @@ __global__ void __launch_bounds__(256 + R * XU) lstm_fwd_xg(
         for (int i = 0; i < KSW; ++i) {
           if (wave + 4 * i < nks) {  // wave-uniform
             u32x4 z = {0u, 0u, 0u, 0u};
-            const bf16x8 a = sweeper ? frag_lo(v[i][0], v[i][1]) : __builtin_bit_cast(bf16x8, z);
+            const bf16x8 a = __builtin_bit_cast(bf16x8, sweeper ? v[i] : z);
 #pragma unroll
             for (int g = 0; g < 4; ++g) acc[g] = mfma_bf16(a, wf[i][g], acc[g]);
           }
@@ -299,6 +317,7 @@ __global__ void __launch_bounds__(256 + R * XU) lstm_fwd_xg(
 #pragma unroll
           for (int r = 0; r < 4; ++r) part[s & 1][wave][4 * kq + r][g * XU + ln] = acc[g][r];
       }
+      XG_TR(s, 4, __builtin_amdgcn_s_memrealtime());
       __syncthreads();  // B(s): partial sums in LDS
       XG_TR(s, 2, __builtin_amdgcn_s_memrealtime());
       if (s_dead) return;
@@ -351,11 +370,14 @@ __global__ void __launch_bounds__(256 + R * XU) lstm_fwd_xg(
     }
     c = cn;
     const unsigned hb = f2bf(h);
-    const unsigned hn = (unsigned)__shfl_down((int)hb, 1, 64);
-    const unsigned val = hb | (hn << 16);
-    if ((unit & 1) == 0) {
-      const unsigned long long gr = ((unsigned long long)(ep | (unsigned)(s + 1)) << 32) | val;
-      gu64* p = xgg + ((((long long)(s & 1) * G + grp) * R + row) * half + (j >> 1));
+    const unsigned h1 = row_from_upper<1>(hb);
+    const unsigned val = hb | (h1 << 16);                 // bf16 pair for ybf
+    const unsigned h2 = row_from_upper<2>(hb), h3 = row_from_upper<3>(hb);
+    const unsigned h0t = bf_with_lsb(h, tag_bit(s));
+    if ((unit & 3) == 0) {
+      const unsigned long long gr =
+          ((unsigned long long)(h2 | (h3 << 16)) << 32) | (h0t | (h1 << 16));
+      gu64* p = xgg + ((((long long)(s & 1) * G + grp) * R + row) * quarter + (j >> 2));
       if (local)  // plain 8-B store: into this XCD's L2, where the group reads
         __hip_atomic_store(p, gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       else        // write-through (sc1) 8-B store
@@ -690,7 +712,7 @@ size_t lstm_xg_fwd_bytes(int B, int H) {
   const int R = xg_rows(B, H);
   if (!R) return 0;
   const long long rows = 2LL * ((B + R - 1) / R) * R;
-  return XG_HDR + (size_t)2 * rows * (H / 2) * 8;
+  return XG_HDR + (size_t)2 * rows * (H / 4) * 8;
 }
 
 size_t lstm_xg_bwd_bytes(int B, int H) {

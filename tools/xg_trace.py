@@ -75,7 +75,7 @@ def main():
     hop('forward', fwd, 3)
     hop('backward', bwd, 4)
     report('forward (us): sweep = start->sweep ok, comb = sweep->barrier, cell = barrier->publish',
-           fwd, [(0, 1, 'sweep'), (1, 2, 'comb'), (2, 3, 'cell')])
+           fwd, [(0, 1, 'sweep'), (1, 4, 'mfma'), (4, 2, 'bar'), (2, 3, 'cell')])
     report('backward (us)', bwd, [(0, 1, 'sweep'), (1, 2, 'b1'), (2, 3, 'cell+b2'),
                                   (3, 4, 'mfma+pub')])
 
