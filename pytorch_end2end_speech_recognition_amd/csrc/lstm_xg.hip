@@ -29,10 +29,11 @@
 //            the bytes each consumer CU loads).
 //   backward (512 threads): the owner of units J turns dh_t(J) into the gate
 //            gradients dg_t [R][4 x 16] and multiplies them by ITS OWN 64 rows of
-//            W_hh, publishing partial sums of dh_{t-1} for ALL H units as bf16
-//            pairs (8 KB of granules per work-group per step at R = 8, H = 512,
-//            the forward's hand-off volume).  A consumer sums the WPG partials
-//            of its 16 units in f32.  No transposed copy of W_hh is needed.
+//            W_hh, publishing partial sums of dh_{t-1} for ALL H units in the
+//            forward's granule format (four bf16, one-bit tag: 8 KB per
+//            consumer work-group per step at R = 8, H = 512).  A consumer sums
+//            the WPG partials of its 16 units in f32.  No transposed copy of
+//            W_hh is needed.
 //
 // Spins are bounded; on give-up a work-group sets the abort word (seen by every
 // other spinner) and g_xg_status, and exits: results are then invalid and
@@ -64,11 +65,13 @@ namespace {
 constexpr int XU = 16;                 // hidden units per work-group
 constexpr unsigned XG_SPIN_LIMIT = 1u << 20;
 constexpr size_t XG_PIN_FWD = 96 * 1024;   // > 80 KB dynamic LDS: one work-group per CU
+constexpr size_t XG_PIN_FWD8 = 64 * 1024;  // 8 sweeper waves: static `part` is >= 34 KB
 constexpr size_t XG_PIN_BWD = 140 * 1024;
 constexpr unsigned AUX_SC1_VOL = 16u | (1u << 31);  // sc1; volatile (never hoisted from a spin)
 constexpr unsigned AUX_SC1 = 16u;
 
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
 typedef __attribute__((address_space(1))) int gint;
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 
@@ -216,13 +219,13 @@ __device__ __forceinline__ float ftanh(float x) { return 2.f * fsig(2.f * x) - 1
 //     step's input-projection prefetch.
 // One __syncthreads per step; `part` is double-buffered by step parity.
 // ---------------------------------------------------------------------------
-template <int R, int KSW>
-__global__ void __launch_bounds__(256 + R * XU) lstm_fwd_xg(
+template <int R, int KSW, int NSW>
+__global__ void __launch_bounds__(64 * NSW + R * XU) lstm_fwd_xg(
     int B, int T, int H, const int32_t* __restrict__ lens, const float* __restrict__ whh_f,
     const float* __restrict__ whh_r, float* __restrict__ gx_act, float* __restrict__ y,
     float* __restrict__ cst, unsigned long long* xg, int* hdr, uint16_t* __restrict__ ybf,
     unsigned epoch, int allow_local) {
-  __shared__ float part[2][4][R][4 * XU + 4];
+  __shared__ float part[2][NSW][R][4 * XU + 4];
   __shared__ int s_dead;  // a sweeper gave up: every wave exits after the next barrier
   __shared__ int s_pl[4];
   int* abortw = hdr;
@@ -242,7 +245,7 @@ __global__ void __launch_bounds__(256 + R * XU) lstm_fwd_xg(
   const unsigned quarter = (unsigned)(H / 4);   // granules per row
   unsigned long long* tr = blockIdx.x < XG_TR_WG ? g_xg_trace : nullptr;
 
-  if (wave < 4) {
+  if (wave < NSW) {
     // ------------------------------ sweeper -------------------------------
     const int kq = lane >> 4, ln = lane & 15;
     const bool sweeper = ln < R;
@@ -252,7 +255,7 @@ __global__ void __launch_bounds__(256 + R * XU) lstm_fwd_xg(
       const float* W = dir ? whh_r : whh_f;
 #pragma unroll
       for (int i = 0; i < KSW; ++i) {
-        const int ks = min(wave + 4 * i, nks - 1);
+        const int ks = min(wave + NSW * i, nks - 1);
 #pragma unroll
         for (int g = 0; g < 4; ++g)
           wf[i][g] = cvt_f32x8(W + (long long)(g * H + u0 + ln) * H + 32 * ks + 8 * kq);
@@ -281,7 +284,7 @@ __global__ void __launch_bounds__(256 + R * XU) lstm_fwd_xg(
             // k = 32 ks + 8 kq + 0..7: two granules, one 16-B load
 #pragma unroll
             for (int i = 0; i < KSW; ++i)
-              v[i] = ld_sc1(rs, rowoff + (unsigned)((8 * min(wave + 4 * i, nks - 1) + 2 * kq) * 8));
+              v[i] = ld_sc1(rs, rowoff + (unsigned)((8 * min(wave + NSW * i, nks - 1) + 2 * kq) * 8));
 #pragma unroll
             for (int i = 0; i < KSW; ++i)
               ok &= (int)((((v[i][0] ^ ebit) | (v[i][2] ^ ebit)) & 1u) == 0u);
@@ -302,7 +305,7 @@ __global__ void __launch_bounds__(256 + R * XU) lstm_fwd_xg(
         // Rows >= R (lanes that did not sweep) multiply zeros.
 #pragma unroll
         for (int i = 0; i < KSW; ++i) {
-          if (wave + 4 * i < nks) {  // wave-uniform
+          if (wave + NSW * i < nks) {  // wave-uniform
             u32x4 z = {0u, 0u, 0u, 0u};
             const bf16x8 a = __builtin_bit_cast(bf16x8, sweeper ? v[i] : z);
 #pragma unroll
@@ -330,7 +333,7 @@ __global__ void __launch_bounds__(256 + R * XU) lstm_fwd_xg(
   }
 
   // -------------------------------- cell ----------------------------------
-  const int ct = tid - 256;
+  const int ct = tid - 64 * NSW;
   const int row = ct >> 4, unit = ct & 15;
   const int b = b0 + row, j = u0 + unit;
   const bool own = b < B;
@@ -346,7 +349,7 @@ __global__ void __launch_bounds__(256 + R * XU) lstm_fwd_xg(
     for (int q = 0; q < 4; ++q) gxv[q] = gx_act[((long long)b * T + t0) * H8 + gcol + (long long)q * H];
   }
   __builtin_amdgcn_s_setprio(2);  // the cell update + publish is the critical path
-  const int cw = wave - 4;  // trace as this block's first cell wave
+  const int cw = wave - NSW;  // trace as this block's first cell wave
   for (int s = 0; s < T; ++s) {
     const int t = dir ? T - 1 - s : s;
     __syncthreads();
@@ -358,8 +361,10 @@ __global__ void __launch_bounds__(256 + R * XU) lstm_fwd_xg(
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int col = q * XU + unit;
-        pre[q] = part[s & 1][0][row][col] + part[s & 1][1][row][col] + part[s & 1][2][row][col] +
-                 part[s & 1][3][row][col] + gxv[q];
+        float a = part[s & 1][0][row][col];
+#pragma unroll
+        for (int w = 1; w < NSW; ++w) a += part[s & 1][w][row][col];
+        pre[q] = a + gxv[q];
       }
       ig = fsig(pre[0]);
       fg = fsig(pre[1]);
@@ -410,10 +415,10 @@ __global__ void __launch_bounds__(256 + R * XU) lstm_fwd_xg(
 // ---------------------------------------------------------------------------
 // backward.  grid = G * WPG.  Processing step q handles the forward direction
 // at t = T-1-q and the reverse direction at t = q.
-// Granules: pg[par][grp][producer][row][H/2] u64 = {bf16 pair of partials of dh
-// (units 2p, 2p+1), tag} -- the partials are sums of bf16 dg x bf16 W_hh
-// products accumulated in f32 and rounded once for transport; the consumer
-// sums the WPG partials in f32.
+// Granules: pg[par][grp][producer][row][H/4] u64 = four bf16 partials of dh
+// (units 4p .. 4p+3), the first one's LSB the step tag bit -- the partials are
+// sums of bf16 dg x bf16 W_hh products accumulated in f32 and rounded once for
+// transport; the consumer sums the WPG partials in f32.
 // Wave roles, two barriers per step (B1: partials summed; B2: dg in LDS):
 //   waves 0..3 (sweepers): poll the partials of dh for this block's 16 units
 //     from every producer of the group, sum per producer subset -> LDS, B1, B2.
@@ -430,7 +435,7 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
     const float* __restrict__ whh_r, const float* __restrict__ dy, float* __restrict__ act_dg,
     const float* __restrict__ cst, unsigned long long* pg, int* hdr,
     uint16_t* __restrict__ dgbf, float* __restrict__ dbpart, unsigned epoch, int allow_local) {
-  constexpr int NPG = 256 / (4 * R);   // producer subsets swept in parallel
+  constexpr int NPG = 256 / (2 * R);   // producer subsets swept in parallel
   __shared__ float red[NPG][R][XU + 1];
   __shared__ __attribute__((aligned(16))) uint16_t dgt[16][4 * XU + 8];
   __shared__ int s_dead;
@@ -443,14 +448,15 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
   if (!s_pl[3]) return;
   const int grp = s_pl[0], mem = s_pl[1];
   const bool local = s_pl[2] != 0;
-  const unsigned ep = epoch << 20;
+  (void)epoch;  // granules carry a 1-bit step tag (tag_bit) instead
   const int dir = grp & 1, rg = grp >> 1;
   const int u0 = mem * XU, b0 = rg * R;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int HB = H / XU;                 // output M blocks
   const int H4 = 4 * H;
-  const unsigned pg_bytes = (unsigned)(2ull * G * WPG * R * (H / 2) * 8);
+  const int hq = H / 4;                  // granules per producer row
+  const unsigned pg_bytes = (unsigned)(2ull * G * WPG * R * hq * 8);
   const __amdgpu_buffer_rsrc_t rs = xg_rsrc(pg, pg_bytes);
   unsigned long long* tr = blockIdx.x < XG_TR_WG ? g_xg_trace : nullptr;
   for (int e = tid; e < 16 * (4 * XU + 8); e += blockDim.x) (&dgt[0][0])[e] = 0;
@@ -458,35 +464,37 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
 
   if (wave < 4) {
     // ------------------------------ sweeper -------------------------------
-    const int sl = tid & (4 * R - 1);
-    const int srow = sl >> 2, sq = sl & 3;   // row, quad of units 4 sq .. 4 sq + 3
-    const int pgi = tid / (4 * R);
+    const int sl = tid & (2 * R - 1);
+    const int srow = sl >> 1, sq = sl & 1;   // row, units 8 sq .. 8 sq + 7
+    const int pgi = tid / (2 * R);
     constexpr int MAXP = 64;  // WPG <= 64
     const int nsleep = __builtin_amdgcn_readfirstlane(g_xg_sleep);
     const int ndelay = __builtin_amdgcn_readfirstlane(g_xg_delay);
     for (int q = 0; q < T; ++q) {
       XG_TR(q, 0, __builtin_amdgcn_s_memrealtime());
       if (q > 0) {
-        const unsigned tag = ep | (unsigned)q;
+        const unsigned ebit = tag_bit(q - 1);
         const long long base = ((long long)((q - 1) & 1) * G + grp) * WPG;
-        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-        const int hh = H / 2;
+        float sm[8];
         nap(ndelay);
         for (unsigned spins = 0;; ++spins) {
           const unsigned long long t_iss = tr ? __builtin_amdgcn_s_memrealtime() : 0;
           int ok = 1;
-          s0 = s1 = s2 = s3 = 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) sm[e] = 0.f;
 #pragma unroll 8
           for (int w = pgi; w < MAXP; w += NPG) {
             if (w >= WPG) break;
+            // two granules = this block's units 8 sq .. 8 sq + 7 from producer w
             const unsigned off =
-                (unsigned)((((base + w) * R + srow) * (long long)hh + (u0 >> 1) + 2 * sq) * 8);
+                (unsigned)((((base + w) * R + srow) * (long long)hq + (u0 >> 2) + 2 * sq) * 8);
             const u32x4 v = ld_sc1(rs, off);
-            ok &= tags_ok(v, tag);
-            s0 += bf2f((uint16_t)(v[0] & 0xffffu));
-            s1 += bf2f((uint16_t)(v[0] >> 16));
-            s2 += bf2f((uint16_t)(v[2] & 0xffffu));
-            s3 += bf2f((uint16_t)(v[2] >> 16));
+            ok &= (int)((((v[0] ^ ebit) | (v[2] ^ ebit)) & 1u) == 0u);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              sm[2 * e] += bf2f((uint16_t)(v[e] & 0xffffu));
+              sm[2 * e + 1] += bf2f((uint16_t)(v[e] >> 16));
+            }
           }
           if (__all(ok)) {
             XG_TR(q, 1, __builtin_amdgcn_s_memrealtime());
@@ -500,10 +508,8 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
             break;
           }
         }
-        red[pgi][srow][4 * sq] = s0;
-        red[pgi][srow][4 * sq + 1] = s1;
-        red[pgi][srow][4 * sq + 2] = s2;
-        red[pgi][srow][4 * sq + 3] = s3;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) red[pgi][srow][8 * sq + e] = sm[e];
       }
       __syncthreads();  // B1
       XG_TR(q, 2, __builtin_amdgcn_s_memrealtime());
@@ -627,7 +633,7 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
     __syncthreads();  // B2
     const bf16x8 bf0 = *reinterpret_cast<const bf16x8*>(&dgt[ln][8 * kq]);
     const bf16x8 bf1 = *reinterpret_cast<const bf16x8*>(&dgt[ln][32 + 8 * kq]);
-    const unsigned tag = ep | (unsigned)(q + 1);
+    const unsigned tb = tag_bit(q);
     const long long obase = (((long long)(q & 1) * G + grp) * WPG + mem) * R;
 #pragma unroll
     for (int i = 0; i < MB; ++i) {
@@ -637,15 +643,15 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
         acc = mfma_bf16(wa[i][0], bf0, acc);
         acc = mfma_bf16(wa[i][1], bf1, acc);
         if (ln < R) {  // C[m][n]: n = ln (row), m = 16 mb + 4 kq + r
-          const unsigned off =
-              (unsigned)(((obase + ln) * (long long)(H / 2) + 8 * mb + 2 * kq) * 8);
-          const unsigned p01 = f2bf(acc[0]) | ((unsigned)f2bf(acc[1]) << 16);
+          // one granule: units 16 mb + 4 kq .. + 3, tag bit in the first value
+          const unsigned off = (unsigned)(((obase + ln) * (long long)hq + 4 * mb + kq) * 8);
+          const unsigned p01 = bf_with_lsb(acc[0], tb) | ((unsigned)f2bf(acc[1]) << 16);
           const unsigned p23 = f2bf(acc[2]) | ((unsigned)f2bf(acc[3]) << 16);
-          const u32x4 v0 = {p01, tag, p23, tag};
+          const u32x2 v0 = {p01, p23};
           if (local)  // plain: into this XCD's L2
-            __builtin_amdgcn_raw_buffer_store_b128(v0, rs, off, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b64(v0, rs, off, 0, 0);
           else        // write-through
-            __builtin_amdgcn_raw_buffer_store_b128(v0, rs, off, 0, AUX_SC1);
+            __builtin_amdgcn_raw_buffer_store_b64(v0, rs, off, 0, AUX_SC1);
         }
       }
     }
@@ -719,7 +725,7 @@ size_t lstm_xg_bwd_bytes(int B, int H) {
   const int R = xg_rows(B, H);
   if (!R) return 0;
   const long long rows = 2LL * ((B + R - 1) / R) * R;
-  return XG_HDR + (size_t)2 * rows * (H / XU) * (H / 2) * 8;
+  return XG_HDR + (size_t)2 * rows * (H / XU) * (H / 4) * 8;
 }
 
 // Returns 1 if launched (or, with dry, if this shape/device can take the
@@ -731,7 +737,11 @@ int lstm_fwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* wh
   if (!xg_enabled()) return 0;
   const int R = xg_rows(B, H);
   if (!R) return 0;
-  int ksw = (H / 32 + 3) / 4;
+  // sweeper waves: 4 (ASR_XG_NSW=8: eight -- the MFMA phase after the hop
+  // drops 0.32 -> 0.24 us but the cell's 8-way partial sum adds 0.08: no gain)
+  const char* ns = getenv("ASR_XG_NSW");
+  const int nsw = (ns && atoi(ns) == 8) ? 8 : 4;
+  int ksw = (H / 32 + nsw - 1) / nsw;
   if (ksw > 8) return 0;
   if (getenv("ASR_XG_KSW")) ksw = std::max(ksw, atoi(getenv("ASR_XG_KSW")));  // diagnostics
   const int grid = 2 * ((B + R - 1) / R) * (H / XU);
@@ -739,14 +749,19 @@ int lstm_fwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* wh
   unsigned long long* g = (unsigned long long*)((char*)ws + XG_HDR);
   const unsigned ep = xg_next_epoch();
   const int al = xg_allow_local();
-#define ASR_XGF(RR, KS)                                                                         \
+#define ASR_XGF_N(RR, KS, NS, PIN)                                                              \
   do {                                                                                          \
-    if (!xg_fits(lstm_fwd_xg<RR, KS>, 256 + RR * XU, XG_PIN_FWD)) return 0;                              \
+    if (!xg_fits(lstm_fwd_xg<RR, KS, NS>, 64 * NS + RR * XU, PIN)) return 0;                     \
     if (dry) return 1;                                                                          \
     if (hipMemsetAsync(ws, 0, lstm_xg_fwd_bytes(B, H), s) != hipSuccess) return -1;             \
-    xg_trace_setup(s);             \
-    hipLaunchKernelGGL((lstm_fwd_xg<RR, KS>), dim3(grid), dim3(256 + RR * XU), XG_PIN_FWD, s, B, T, H,     \
-                       lens, whh_f, whh_r, gx_act, y, cst, g, hdr, ybf, ep, al);                     \
+    xg_trace_setup(s);                                                                          \
+    hipLaunchKernelGGL((lstm_fwd_xg<RR, KS, NS>), dim3(grid), dim3(64 * NS + RR * XU), PIN, s,   \
+                       B, T, H, lens, whh_f, whh_r, gx_act, y, cst, g, hdr, ybf, ep, al);        \
+  } while (0)
+#define ASR_XGF(RR, KS)                                            \
+  do {                                                             \
+    if (nsw == 8) ASR_XGF_N(RR, KS, 8, XG_PIN_FWD8);               \
+    else ASR_XGF_N(RR, KS, 4, XG_PIN_FWD);                         \
   } while (0)
 #define ASR_XGF_K(RR)                   \
   do {                                  \
@@ -760,6 +775,7 @@ int lstm_fwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* wh
   else ASR_XGF_K(16);
 #undef ASR_XGF_K
 #undef ASR_XGF
+#undef ASR_XGF_N
   return hipGetLastError() == hipSuccess ? 1 : -1;
 }
 
