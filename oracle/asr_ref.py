@@ -254,10 +254,13 @@ def lstm_cell(p, name, x, h, c):
     return torch.sigmoid(o) * torch.tanh(c), c
 
 
-def attention_model_loss(p, cfg, xs, ys, x_lens, y_lens, train=None):
-    """AttentionSeq2seq.forward (attention_seq2seq.py:422-562) for the
-    bahdanau order, location attention, 1 head, LSTM decoder, forward
-    direction only (backward_loss_weight = 0), encoder dropout 0.
+def attention_xe(p, cfg, enc_out, enc_lens, ys, y_lens, perm, task=0, train=None):
+    """Teacher-forced decoder of `task` (attention_seq2seq.py:564-607, 704-799):
+    bahdanau order, location attention, 1 head, LSTM decoder, forward direction.
+    Module names carry the task index (``attend_{task}_fwd`` ...); task 1 is the
+    hierarchical model's sub task (hierarchical_attention_seq2seq.py:221-339)
+    with num_classes_sub / decoder_num_units_sub.  Returns the XE loss
+    (label smoothing included) over the batch, divided by B.
 
     train (optional): replayed training-mode randomness, all in the sorted
     utterance order -- 'h' [B,S,D] decoder dropout scales on h after the
@@ -267,12 +270,10 @@ def attention_model_loss(p, cfg, xs, ys, x_lens, y_lens, train=None):
     (attention_seq2seq.py:744-748): 'ss' [S] flags, 'emb_ss' [B,S,Y] scales on
     the sampled embedding embed(argmax logits_{t-1}) (detached)."""
     train = train or {}
-    xs_t = torch.from_numpy(np.asarray(xs, np.float32))
-    enc_cfg = dict(num_layers=cfg['encoder_num_layers'], subsample_list=cfg['subsample_list'])
-    enc_out, enc_lens, perm = blstm_encoder(p, 'encoder.', enc_cfg, xs_t, x_lens)
     B, T, E = enc_out.shape
-    V = cfg['num_classes'] + 1
-    eos = cfg['num_classes']
+    ncls = cfg['num_classes'] if task == 0 else cfg['num_classes_sub']
+    V = ncls + 1
+    eos = ncls
     ys = np.asarray(ys)
     y_lens = np.asarray(y_lens)
     Lp = ys.shape[1]
@@ -284,8 +285,9 @@ def attention_model_loss(p, cfg, xs, ys, x_lens, y_lens, train=None):
         ys_out[b, y_lens[b]] = eos
     ys_in, ys_out, yl = ys_in[perm], ys_out[perm], y_lens[perm]
 
-    D = cfg['decoder_num_units']
-    pre = 'attend_0_fwd.'
+    D = cfg['decoder_num_units'] if task == 0 else cfg['decoder_num_units_sub']
+    sfx = '_%d_fwd' % task
+    pre = 'attend%s.' % sfx
     enc_out_a = linear_nd(p, pre + 'W_enc_head0', enc_out)  # :735-739
     init = cfg.get('init_dec_state', 'first')
     c = enc_out.new_zeros(B, D)
@@ -293,14 +295,14 @@ def attention_model_loss(p, cfg, xs, ys, x_lens, y_lens, train=None):
         h = enc_out.new_zeros(B, D)
     else:                                                    # :831-857
         src = {'mean': enc_out.mean(1), 'final': enc_out[:, -1], 'first': enc_out[:, 0]}[init]
-        h = torch.tanh(linear_nd(p, 'W_dec_init_0_fwd', src))
+        h = torch.tanh(linear_nd(p, 'W_dec_init' + sfx, src))
     dec_out = h
     aw = enc_out.new_zeros(B, T)
     ctx = enc_out.new_zeros(B, E)
     if cfg.get('label_smoothing_prob', 0) > 0:               # Embedding_LS (linear.py:80-116)
-        emb_w = p['embed_0.embed.fc.weight'].t()             # [V, emb]
+        emb_w = p['embed_%d.embed.fc.weight' % task].t()     # [V, emb]
     else:                                                    # Embedding, padding_idx=-1
-        emb_w = p['embed_0.embed.weight']
+        emb_w = p['embed_%d.embed.weight' % task]
     ys_emb = emb_w[torch.as_tensor(ys_in)]                   # [B, L+1, emb]
     mk = {k: torch.from_numpy(np.asarray(v, np.float32)) for k, v in train.items() if k != 'ss'}
     if 'emb' in mk:
@@ -317,20 +319,20 @@ def attention_model_loss(p, cfg, xs, ys, x_lens, y_lens, train=None):
             else:
                 y = ys_emb[:, t]
             dec_in = torch.cat([y, ctx], dim=-1)
-            h, c = lstm_cell(p, 'decoder_0_fwd.lstm_l0', dec_in, h, c)
+            h, c = lstm_cell(p, 'decoder%s.lstm_l0' % sfx, dec_in, h, c)
             if 'h' in mk:
                 h = h * mk['h'][:, t]
             dec_out = h
         ctx, aw = location_attention(p, pre, enc_out, enc_out_a, enc_lens, dec_out, aw,
                                      cfg.get('sharpening_factor', 1),
                                      cfg.get('sigmoid_smoothing', False))
-        a = linear_nd(p, 'W_d_0_fwd', dec_out)
-        cc = linear_nd(p, 'W_c_0_fwd', ctx)
+        a = linear_nd(p, 'W_d' + sfx, dec_out)
+        cc = linear_nd(p, 'W_c' + sfx, ctx)
         if 'd' in mk:
             a = a * mk['d'][:, t]
             cc = cc * mk['c'][:, t]
         z = torch.tanh(a + cc)
-        logits.append(linear_nd(p, 'fc_0_fwd', z))
+        logits.append(linear_nd(p, 'fc' + sfx, z))
     logits = torch.stack(logits, 1)                          # [B, L+1, V]
     if cfg.get('logits_temperature', 1) != 1:
         logits = logits / cfg['logits_temperature']
@@ -340,13 +342,61 @@ def attention_model_loss(p, cfg, xs, ys, x_lens, y_lens, train=None):
     ls = cfg.get('label_smoothing_prob', 0)
     if ls > 0:
         loss = loss * (1 - ls) + ls_xent(logits, yl + 1, ls, True)
+    return loss
+
+
+def _enc_cfg(cfg):
+    return dict(num_layers=cfg['encoder_num_layers'], subsample_list=cfg['subsample_list'],
+                num_proj=cfg.get('encoder_num_proj', 0),
+                subsample_type=cfg.get('subsample_type', 'drop'),
+                residual=cfg.get('encoder_residual', False),
+                dense_residual=cfg.get('encoder_dense_residual', False))
+
+
+def attention_model_loss(p, cfg, xs, ys, x_lens, y_lens, train=None):
+    """AttentionSeq2seq.forward (attention_seq2seq.py:422-562) for the
+    bahdanau order, location attention, 1 head, LSTM decoder, forward
+    direction only (backward_loss_weight = 0), encoder dropout 0:
+    loss = (1 - w_bwd) * XE + lambda * CTC / B.  `train`: see attention_xe."""
+    xs_t = torch.from_numpy(np.asarray(xs, np.float32))
+    enc_out, enc_lens, perm = blstm_encoder(p, 'encoder.', _enc_cfg(cfg), xs_t, x_lens)
+    B = enc_out.shape[0]
+    loss = attention_xe(p, cfg, enc_out, enc_lens, ys, y_lens, perm, 0, train)
     loss = loss * (1 - cfg.get('backward_loss_weight', 0))
     lam = cfg.get('ctc_loss_weight', 0)
     if lam > 0:                                              # :534-549, :609-653
+        yl = np.asarray(y_lens)[perm]
         lg = linear_nd(p, 'fc_ctc_0', enc_out)
         lab = _concat_labels(np.asarray(ys)[perm] + 1, yl)
         loss = loss + ctc_sum(lg, lab, yl, enc_lens) / B * lam
     return loss
+
+
+def hierarchical_attention_loss(p, cfg, xs, ys, x_lens, y_lens, ys_sub, y_lens_sub):
+    """HierarchicalAttentionSeq2seq.forward (hierarchical_attention_seq2seq.py:
+    382-567): word decoder on the top layer, character decoder (task 1) on layer
+    encoder_num_layers_sub (after its dropout, before projection / subsampling),
+    optional character CTC there.  Returns (loss, loss_main, loss_sub)."""
+    xs_t = torch.from_numpy(np.asarray(xs, np.float32))
+    top, lens, perm, (mid, lens_sub) = blstm_encoder(
+        p, 'encoder.', dict(_enc_cfg(cfg), fast=False), xs_t, x_lens,
+        capture_layer=cfg['encoder_num_layers_sub'])
+    B = top.shape[0]
+    loss_main = attention_xe(p, cfg, top, lens, ys, y_lens, perm, 0) * cfg['main_loss_weight']
+    loss = loss_main
+    loss_sub = ctc_sub = None
+    if cfg['sub_loss_weight'] > 0:
+        loss_sub = attention_xe(p, cfg, mid, lens_sub, ys_sub, y_lens_sub, perm, 1) * \
+            cfg['sub_loss_weight']
+        loss = loss + loss_sub
+    w_ctc = cfg.get('ctc_loss_weight_sub', 0)
+    if w_ctc > 0:
+        yl = np.asarray(y_lens_sub)[perm]
+        lg = linear_nd(p, 'fc_ctc_1', mid)
+        lab = _concat_labels(np.asarray(ys_sub)[perm] + 1, yl)
+        ctc_sub = ctc_sum(lg, lab, yl, lens_sub) / B * w_ctc
+        loss = loss + ctc_sub
+    return loss, loss_main, (loss_sub if cfg['sub_loss_weight'] > w_ctc else ctc_sub)
 
 
 def attention_greedy_decode(p, cfg, xs, x_lens, max_len):

@@ -64,6 +64,7 @@ class AttentionSeq2seq(ModelBase):
         self.decoder_num_units_0 = decoder_num_units
         self.decoder_num_layers_0 = decoder_num_layers
         self.embedding_dim = embedding_dim
+        self._emb_dims = {0: embedding_dim}          # per task (hierarchical: task 1)
         self.num_classes = num_classes + 1
         self.sos_0 = num_classes
         self.eos_0 = num_classes
@@ -182,17 +183,9 @@ class AttentionSeq2seq(ModelBase):
         ys = np.asarray(ys)
         y_lens = np.asarray(y_lens).astype(np.int64)
 
-        # ys_in = [<sos>, y, <eos>...], ys_out = [y, <eos>, -1...]   (:458-473), host, vectorised
-        Lp = ys.shape[1]
-        pos = np.arange(Lp + 1)[None, :]
-        ys_pad = np.concatenate([ys, np.full((B, 1), -1, ys.dtype)], axis=1)
-        ys_out = np.where(pos < y_lens[:, None], ys_pad,
-                          np.where(pos == y_lens[:, None], self.eos_0, -1)).astype(np.int64)
-        ys_in = np.full((B, Lp + 1), self.eos_0, np.int64)
-        ys_in[:, 1:] = np.where(pos[:, :-1] < y_lens[:, None], ys, self.eos_0)
-        ys_in, ys_out = ys_in[perm], ys_out[perm]
+        ys_in, ys_out = self._ys_in_out(ys, y_lens, self.eos_0, perm)
 
-        self._ys_in_host = ys_in          # host copy: token-grouped embedding gradient
+        self._ys_in_host = {0: ys_in}     # host copy: token-grouped embedding gradient
         loss = self.compute_xe_loss(enc_out, self.np2var(ys_in), self.np2var(ys_out), enc_lens_d,
                                     None, task=0, dir='fwd', weight=self.fwd_weight_0)
         if self.ctc_loss_weight > 0:
@@ -207,8 +200,21 @@ class AttentionSeq2seq(ModelBase):
             self._ss_prob = min(self.ss_prob, self.ss_prob / self.ss_max_step * self._step)
         return loss
 
+    @staticmethod
+    def _ys_in_out(ys, y_lens, eos, perm):
+        """ys_in = [<sos>, y, <eos>...], ys_out = [y, <eos>, -1...] (:458-473; <sos> ==
+        <eos>), host-side and vectorised, rows in the encoder's sorted order."""
+        B, Lp = ys.shape
+        pos = np.arange(Lp + 1)[None, :]
+        ys_pad = np.concatenate([ys, np.full((B, 1), -1, ys.dtype)], axis=1)
+        ys_out = np.where(pos < y_lens[:, None], ys_pad,
+                          np.where(pos == y_lens[:, None], eos, -1)).astype(np.int64)
+        ys_in = np.full((B, Lp + 1), eos, np.int64)
+        ys_in[:, 1:] = np.where(pos[:, :-1] < y_lens[:, None], ys, eos)
+        return ys_in[perm], ys_out[perm]
+
     def compute_xe_loss(self, enc_out, ys_in, ys_out, x_lens, y_lens, task, dir, weight=1.0):
-        """:564-607 (forward decoder, loss already multiplied by `weight`)."""
+        """:564-607 (forward decoder of `task`, loss already multiplied by `weight`)."""
         logits, _ = self._decode_train(enc_out, x_lens, ys_in, task, dir)
         if self.logits_temperature != 1:
             logits = logits * (1.0 / self.logits_temperature)
@@ -220,7 +226,7 @@ class AttentionSeq2seq(ModelBase):
 
     def compute_ctc_loss(self, enc_out, ys_ctc, x_lens, y_lens, task=0, scale=1.0):
         """:609-653 on the HIP CTC kernel; ys_ctc already +1 (blank 0)."""
-        logits = self.fc_ctc_0(enc_out)
+        logits = getattr(self, 'fc_ctc_%d' % task)(enc_out)
         labels = self.np2var(_concatenate_labels_np(ys_ctc, y_lens))
         yl_d = self.np2var(y_lens.astype(np.int32))
         B = enc_out.shape[0]
@@ -229,20 +235,19 @@ class AttentionSeq2seq(ModelBase):
         return loss
 
     def _encode(self, xs, x_lens, is_multi_task=False):
-        """:655-698."""
-        if is_multi_task:
-            raise NotImplementedError
+        """:655-698 (with num_layers_sub >= 1 the encoder returns the sub-task tap
+        too: (xs, x_lens, xs_sub, x_lens_sub, perm_idx))."""
         return self.encoder(xs, x_lens, volatile=not self.training)
 
-    def _init_h0(self, enc_out):
+    def _init_h0(self, enc_out, task=0, dir='fwd'):
         """_init_dec_state (:801-864): zero / first / final; 'mean' is a next item."""
-        mode = self.init_dec_state_0_fwd
+        mode = getattr(self, 'init_dec_state_%d_%s' % (task, dir))
         if mode == 'zero':
             return None
         if mode == 'mean':
             raise NotImplementedError("init_dec_state='mean'")
         T = enc_out.shape[1]
-        lin = self.W_dec_init_0_fwd.fc
+        lin = getattr(self, 'W_dec_init_%d_%s' % (task, dir)).fc
         h = ops.linear_ex(enc_out, lin.weight, lin.bias, t_index=0 if mode == 'first' else T - 1)
         return ops.tanh(h)
 
@@ -265,18 +270,22 @@ class AttentionSeq2seq(ModelBase):
         linear.py:44-45), embedding dropout, and scheduled sampling -- sampled
         steps take embed(argmax logits_{t-1}) computed inside the loop from the
         same dropped bottleneck the loss sees (shared dropout seeds)."""
-        att = self.attend_0_fwd
-        cell = self.decoder_0_fwd.lstm_l0
-        W_d, W_c = self.W_d_0_fwd, self.W_c_0_fwd
+        att = getattr(self, 'attend_%d_%s' % (task, dir))
+        cell = getattr(self, 'decoder_%d_%s' % (task, dir)).lstm_l0
+        W_d, W_c = getattr(self, 'W_d_%d_%s' % (task, dir)), getattr(self, 'W_c_%d_%s' % (task, dir))
+        fc = getattr(self, 'fc_%d_%s' % (task, dir))
+        embed = getattr(self, 'embed_%d' % task)
+        emb_dim = self._emb_dims[task]
         S = ys.shape[1]
-        h0 = self._init_h0(enc_out)
+        h0 = self._init_h0(enc_out, task, dir)
         enc_a = att.W_enc_head0(enc_out)                          # one GEMM for all frames
-        ys_host, self._ys_in_host = getattr(self, '_ys_in_host', None), None   # one use only
+        hosts = getattr(self, '_ys_in_host', None) or {}
+        ys_host = hosts.pop(task, None)                           # one use only
         if ys_host is not None and tuple(ys_host.shape) != tuple(ys.shape):
             ys_host = None
-        y_emb = self.embed_0(ys, ys_host)                         # [B, S, emb] (+ dropout)
+        y_emb = embed(ys, ys_host)                                # [B, S, emb] (+ dropout)
         pre_emb = ops.linear_ex(y_emb, cell.weight_ih, cell.bias_ih, cell.bias_hh, c0=0,
-                                K=self.embedding_dim)             # all steps' input projection
+                                K=emb_dim)                        # all steps' input projection
         p_h = self.dropout_decoder if self.training else 0.0
         p_b = W_d.dropout_p if self.training else 0.0
         seed_d = ops.next_seed() if p_b > 0 else 0
@@ -286,16 +295,16 @@ class AttentionSeq2seq(ModelBase):
         if p_h > 0 or ss is not None:
             train_opts = dict(dropout_hidden=p_h, seed_hidden=ops.next_seed() if p_h > 0 else 0)
             if ss is not None:
-                emb_ls = isinstance(self.embed_0, Embedding_LS)
-                emb_w = self.embed_0.embed.fc.weight if emb_ls else self.embed_0.embed.weight
+                emb_ls = isinstance(embed, Embedding_LS)
+                emb_w = embed.embed.fc.weight if emb_ls else embed.embed.weight
                 p_e = self.dropout_embedding if self.training else 0.0
                 train_opts.update(
                     ss_steps=ss, w_d=W_d.fc.weight, b_d=W_d.fc.bias, w_c=W_c.fc.weight,
-                    b_c=W_c.fc.bias, w_fc=self.fc_0_fwd.fc.weight, b_fc=self.fc_0_fwd.fc.bias,
+                    b_c=W_c.fc.bias, w_fc=fc.fc.weight, b_fc=fc.fc.bias,
                     emb_w=emb_w, emb_trans=int(emb_ls), b_ih=cell.bias_ih, b_hh=cell.bias_hh,
                     drop_d=p_b, seed_d=seed_d, drop_c=p_b, seed_c=seed_c, drop_emb=p_e,
                     seed_emb=ops.next_seed() if p_e > 0 else 0)
-        dec, ctx, aw = ops.att_decoder(enc_out, enc_a, x_lens, pre_emb, h0, self.embedding_dim,
+        dec, ctx, aw = ops.att_decoder(enc_out, enc_a, x_lens, pre_emb, h0, emb_dim,
                                        self.sharpening_factor, self.sigmoid_smoothing,
                                        cell.weight_ih, cell.weight_hh, att.W_dec_head0.fc.weight,
                                        att.W_conv_head0.fc.weight, att.conv_head0.weight,
@@ -307,7 +316,7 @@ class AttentionSeq2seq(ModelBase):
         else:
             z = ops.tanh(ops.linear2(dec, W_d.fc.weight, W_d.fc.bias, ctx, W_c.fc.weight,
                                      W_c.fc.bias))
-        logits = self.fc_0_fwd(z)
+        logits = fc(z)
         return logits, aw
 
     @torch.no_grad()
@@ -342,23 +351,25 @@ class AttentionSeq2seq(ModelBase):
         exit -- stop after the first step at which EVERY utterance emits <eos>
         -- becomes a truncation of the per-step tokens, which it does not change
         because later steps never feed back into earlier ones."""
-        att = self.attend_0_fwd
-        cell = self.decoder_0_fwd.lstm_l0
-        W_d, W_c = self.W_d_0_fwd, self.W_c_0_fwd
-        emb_ls = isinstance(self.embed_0, Embedding_LS)
-        emb_w = self.embed_0.embed.fc.weight if emb_ls else self.embed_0.embed.weight
-        h0 = self._init_h0(enc_out)
+        att = getattr(self, 'attend_%d_%s' % (task, dir))
+        cell = getattr(self, 'decoder_%d_%s' % (task, dir)).lstm_l0
+        W_d, W_c = getattr(self, 'W_d_%d_%s' % (task, dir)), getattr(self, 'W_c_%d_%s' % (task, dir))
+        fc = getattr(self, 'fc_%d_%s' % (task, dir))
+        embed = getattr(self, 'embed_%d' % task)
+        emb_ls = isinstance(embed, Embedding_LS)
+        emb_w = embed.embed.fc.weight if emb_ls else embed.embed.weight
+        h0 = self._init_h0(enc_out, task, dir)
         enc_a = att.W_enc_head0(enc_out)
         gen = dict(w_d=W_d.fc.weight, b_d=W_d.fc.bias, w_c=W_c.fc.weight, b_c=W_c.fc.bias,
-                   w_fc=self.fc_0_fwd.fc.weight, b_fc=self.fc_0_fwd.fc.bias, emb_w=emb_w,
+                   w_fc=fc.fc.weight, b_fc=fc.fc.bias, emb_w=emb_w,
                    emb_trans=int(emb_ls), b_ih=cell.bias_ih, b_hh=cell.bias_hh)
-        toks, aw = ops.att_decode_greedy(enc_out, enc_a, x_lens, h0, self.embedding_dim,
+        toks, aw = ops.att_decode_greedy(enc_out, enc_a, x_lens, h0, self._emb_dims[task],
                                          self.sharpening_factor, self.sigmoid_smoothing,
                                          cell.weight_ih, cell.weight_hh,
                                          att.W_dec_head0.fc.weight, att.W_conv_head0.fc.weight,
                                          att.conv_head0.weight, att.V_head0.fc.weight, gen,
                                          max_decode_len)
         toks = toks.cpu().numpy()
-        all_eos = np.nonzero((toks == self.eos_0).all(axis=0))[0]
+        all_eos = np.nonzero((toks == getattr(self, 'eos_%d' % task)).all(axis=0))[0]
         n = int(all_eos[0]) + 1 if len(all_eos) else toks.shape[1]   # :1017-1019
         return toks[:, :n], aw[:, :n].cpu().numpy()

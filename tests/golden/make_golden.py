@@ -430,6 +430,55 @@ def case_attention_model():
 
 
 # --------------------------------------------------------------------------
+# Case 6b: hierarchical attention (word decoder on top, char decoder + CTC on
+# layer encoder_num_layers_sub)
+# --------------------------------------------------------------------------
+def case_hier_attention_model():
+    from models.pytorch_v3.attention.hierarchical_attention_seq2seq import \
+        HierarchicalAttentionSeq2seq
+    base = dict(input_size=8, encoder_type='lstm', encoder_bidirectional=True,
+                encoder_num_units=6, encoder_num_proj=0, encoder_num_layers=3,
+                encoder_num_layers_sub=2, attention_type='location', attention_dim=7,
+                decoder_type='lstm', decoder_num_units=9, decoder_num_units_sub=7,
+                decoder_num_layers=1, decoder_num_layers_sub=1, embedding_dim=4,
+                embedding_dim_sub=3, dropout_input=0, dropout_encoder=0, dropout_decoder=0,
+                dropout_embedding=0, num_classes=5, num_classes_sub=4, parameter_init=0.1,
+                subsample_list=[False, True, False], subsample_type='drop',
+                attention_conv_num_channels=3, attention_conv_width=5, bottleneck_dim=11,
+                bottleneck_dim_sub=8, decoding_order='bahdanau')
+    specs = [
+        ('model_hatt', dict(base, init_dec_state='zero', main_loss_weight=0.5,
+                            sub_loss_weight=0.5, ctc_loss_weight_sub=0)),
+        ('model_hatt_ctc', dict(base, init_dec_state='first', sharpening_factor=1.5,
+                                main_loss_weight=0.6, sub_loss_weight=0.2,
+                                ctc_loss_weight_sub=0.3, label_smoothing_prob=0.1)),
+    ]
+    only = _selected()
+    for name, kw in specs:
+        if only and name not in only:
+            continue
+        torch.manual_seed(1623)
+        model = HierarchicalAttentionSeq2seq(**kw)
+        model.train()
+        rng = np.random.RandomState(8)
+        B, T = 3, 22
+        x_lens = np.array([22, 19, 14], np.int32)
+        y_lens = np.array([3, 4, 2], np.int32)
+        y_lens_sub = np.array([6, 7, 4], np.int32)
+        xs, ys = _batch(rng, B, T, 8, y_lens, 5, x_lens)
+        ys_sub = np.full((B, int(y_lens_sub.max())), -1, np.int32)
+        for b in range(B):
+            ys_sub[b, :y_lens_sub[b]] = rng.randint(0, 4, y_lens_sub[b])
+        loss, loss_main, loss_sub = model(xs, ys, x_lens, y_lens, ys_sub, y_lens_sub)
+        loss.backward()
+        _save(name, kwargs=np.array(json.dumps(kw)), xs=xs, ys=ys, x_lens=x_lens,
+              y_lens=y_lens, ys_sub=ys_sub, y_lens_sub=y_lens_sub,
+              loss=loss.detach().numpy().reshape(1),
+              loss_main=loss_main.detach().numpy().reshape(1),
+              loss_sub=loss_sub.detach().numpy().reshape(1), **_sd(model), **_grads(model))
+
+
+# --------------------------------------------------------------------------
 # Case 7: greedy attention decoding (attention_seq2seq.py:866-1036)
 # --------------------------------------------------------------------------
 def case_attention_decode():
@@ -486,6 +535,7 @@ if __name__ == '__main__':
     if _selected():          # regenerate only the named model_ctc_* / dec_* cases
         case_ctc_model()
         case_attention_decode()
+        case_hier_attention_model()
         sys.exit(0)
     case_ctc()
     case_encoder()
@@ -494,4 +544,5 @@ if __name__ == '__main__':
     case_vgg_model()
     case_hier_ctc_model()
     case_attention_model()
+    case_hier_attention_model()
     case_attention_decode()
