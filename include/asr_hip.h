@@ -381,6 +381,10 @@ typedef struct {
   float* dg_ss;
 } asr_attdec_opts_t;
 
+/* Diagnostics: phase stamps (s_memrealtime ticks, 100 MHz) of the per-step
+ * attention kernels' work-group (0, 0) at decoder step 10 of the last pass;
+ * host must hold 64 values. */
+int asr_att_trace_read(unsigned long long* host);
 size_t asr_attdec_workspace_bytes(const asr_attdec_dims_t* dims, int compute_dtype,
                                   int backward);
 int asr_attdec_chunks(const asr_attdec_dims_t* dims);

@@ -79,6 +79,7 @@ SIGNATURES = {
                                   c_float, c_vp, c_vp, c_size, c_vp]),
     'asr_softmax': (c_int, [c_vp, c_int, c_int, c_vp, c_vp]),
     'asr_attdec_workspace_bytes': (c_size, [c_vp, c_int, c_int]),
+    'asr_att_trace_read': (c_int, [c_vp]),
     'asr_attdec_chunks': (c_int, [c_vp]),
     'asr_attdec_forward': (c_int, [c_vp, c_int] + [c_vp] * 4 + [c_ll] + [c_vp] * 14 + [c_size,
                                                                                      c_vp]),

@@ -58,16 +58,35 @@ __device__ __forceinline__ float lse3(float a, float b, float c) {
   return m + __logf(__expf(a - m) + __expf(b - m) + __expf(c - m));
 }
 
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+// Wave reductions on DPP (GFX9 row/quad permutes and row broadcasts: a few
+// cycles each) instead of six ds_bpermute round trips through the LDS
+// crossbar; the total is formed in lane 63 and broadcast with readlane.
+// Disabled rows of the row_bcast steps take `old` = the identity element.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ float dpp_f(float old, float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), CTRL,
+                                                    ROWS, 0xf, false));
 }
 
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += dpp_f<0xB1, 0xf>(0.f, v);    // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E, 0xf>(0.f, v);    // quad_perm [2,3,0,1]
+  v += dpp_f<0x141, 0xf>(0.f, v);   // row_half_mirror
+  v += dpp_f<0x140, 0xf>(0.f, v);   // row_mirror: every lane holds its row's sum
+  v += dpp_f<0x142, 0xa>(0.f, v);   // row_bcast:15 into rows 1, 3
+  v += dpp_f<0x143, 0xc>(0.f, v);   // row_bcast:31 into rows 2, 3: lane 63 = total
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+  const float lo = -__builtin_huge_valf();
+  v = fmaxf(v, dpp_f<0xB1, 0xf>(lo, v));
+  v = fmaxf(v, dpp_f<0x4E, 0xf>(lo, v));
+  v = fmaxf(v, dpp_f<0x141, 0xf>(lo, v));
+  v = fmaxf(v, dpp_f<0x140, 0xf>(lo, v));
+  v = fmaxf(v, dpp_f<0x142, 0xa>(lo, v));
+  v = fmaxf(v, dpp_f<0x143, 0xc>(lo, v));
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
 // Dropout RNG shared by every kernel that applies or regenerates a mask:

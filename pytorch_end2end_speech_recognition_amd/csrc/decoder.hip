@@ -186,6 +186,8 @@ __global__ void __launch_bounds__(256) cell_fwd(int t, Dims d, const TW* __restr
 //   att_bwd_conv     (chunk, b): d aw_{t-1} (conv transpose), conv-kernel partials,
 //                                (chunk 0) dW_dec input sum and d dec
 constexpr int TCH = 32;   // frames per attention work-group
+constexpr int ATT_WAVES = ATT_THREADS / 64;
+constexpr int FPW = TCH / ATT_WAVES;   // frames per wave
 constexpr int ECH = 64;   // context columns per work-group
 
 inline int att_chunks(const Dims& d) { return (d.T + TCH - 1) / TCH; }
@@ -205,7 +207,8 @@ struct EnLds {
 };
 
 __host__ __device__ inline size_t conv_lds_floats(const Dims& d) {
-  return (size_t)d.C * d.K + (size_t)(TCH + d.K - 1) * (d.C + 1) + d.A + (size_t)TCH * d.C;
+  return (size_t)d.C * d.K + (size_t)(TCH + d.K - 1) * (d.C + 1) + d.A + (size_t)TCH * d.C +
+         ATT_THREADS;
 }
 
 __host__ __device__ inline size_t en_lds_floats(const Dims& d) {
@@ -241,55 +244,149 @@ __device__ __forceinline__ float block_reduce(float v, float* red, bool is_max) 
   return r;
 }
 
-// Weights, h_t, W_dec h_t, the aw_{t-1} window and the chunk's conv features.
+// Diagnostics: phase stamps (s_memrealtime, 100 MHz) of work-group (0, 0) at
+// decoder step ATT_TR_STEP, read by asr_att_trace_read.
+__device__ unsigned long long g_att_tr[64];
+constexpr int ATT_TR_STEP = 10;
+#define ATT_TR(k)                                                                     \
+  do {                                                                                \
+    if (t == ATT_TR_STEP && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)   \
+      g_att_tr[k] = __builtin_amdgcn_s_memrealtime();                                 \
+  } while (0)
+
+// sum_{i < n} x[i * sx] y[i * sy] over LDS with eight products in flight (four
+// partial sums): the conv windows' serial dot products were LDS-latency-bound.
+__device__ __forceinline__ float dot_lds(const float* x, int sx, const float* y, int sy, int n) {
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int i = 0;
+  for (; i + 8 <= n; i += 8) {
+    float a[8], b[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      a[j] = x[(long long)(i + j) * sx];
+      b[j] = y[(long long)(i + j) * sy];
+    }
+    s0 += a[0] * b[0] + a[4] * b[4];
+    s1 += a[1] * b[1] + a[5] * b[5];
+    s2 += a[2] * b[2] + a[6] * b[6];
+    s3 += a[3] * b[3] + a[7] * b[7];
+  }
+  for (; i < n; ++i) s0 += x[(long long)i * sx] * y[(long long)i * sy];
+  return (s0 + s1) + (s2 + s3);
+}
+
+// Global -> LDS copy of up to four arrays in which each thread issues all of
+// its loads (16 per pass) before its first LDS store: one memory round trip for
+// up to 16 * blockDim.x floats instead of one per loop iteration.  The per-step
+// attention kernels are latency-bound (SQ_WAIT_ANY was 2/3 of their wave
+// cycles): every global read is batched like this or prefetched whole.
+struct LdsSeg {
+  float* dst;
+  const float* src;
+  int n;
+};
+__device__ __forceinline__ void lds_fill(const LdsSeg& s0, const LdsSeg& s1, const LdsSeg& s2,
+                                         const LdsSeg& s3) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int c1 = s0.n, c2 = c1 + s1.n, c3 = c2 + s2.n, total = c3 + s3.n;
+  for (int base = 0; base < total; base += 16 * nt) {
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int i = base + j * nt + tid;
+      v[j] = i < c1 ? s0.src[i] : i < c2 ? s1.src[i - c1] : i < c3 ? s2.src[i - c2]
+           : i < total ? s3.src[i - c3] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int i = base + j * nt + tid;
+      if (i < c1) s0.dst[i] = v[j];
+      else if (i < c2) s1.dst[i - c1] = v[j];
+      else if (i < c3) s2.dst[i - c2] = v[j];
+      else if (i < total) s3.dst[i - c3] = v[j];
+    }
+  }
+}
+
+// Weights, h_t (or the precomputed W_dec h_t rows), W_dec h_t, the aw_{t-1}
+// window and the chunk's conv features.
 __device__ void en_prologue(int t, const Dims& d, int b, int tt0, const EnLds& L,
                             const float* __restrict__ w_dec, const float* __restrict__ w_conv,
                             const float* __restrict__ conv_w, const float* __restrict__ vw,
                             const float* __restrict__ dec, const float* __restrict__ aw_all,
-                            const float* __restrict__ wd_pre = nullptr) {
+                            const float* __restrict__ wd_pre = nullptr, int trb = 0) {
   const int tid = threadIdx.x, nt = blockDim.x;
   const int half = d.K / 2;
-  for (int i = tid; i < d.A * d.C; i += nt) L.wc[i] = w_conv[i];
-  for (int i = tid; i < d.C * d.K; i += nt) L.cw[i] = conv_w[i];
-  for (int i = tid; i < d.A; i += nt) L.v[i] = vw[i];
-  for (int i = tid; i < d.D; i += nt) L.h[i] = dec[((long long)b * d.S + t) * d.D + i];
-  for (int i = tid; i < TCH + d.K - 1; i += nt) {
-    const int tt = tt0 - half + i;
-    L.awin[i] = (t > 0 && tt >= 0 && tt < d.T) ? aw_all[((long long)b * d.S + t - 1) * d.T + tt]
-                                                : 0.f;
+  ATT_TR(trb + 0);
+  float awv[2];   // the window (TCH + K - 1 <= 2 * blockDim.x) rides with the batch
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int i = tid + j * nt, tt = tt0 - half + i;
+    awv[j] = (i < TCH + d.K - 1 && t > 0 && tt >= 0 && tt < d.T)
+                 ? aw_all[((long long)b * d.S + t - 1) * d.T + tt] : 0.f;
   }
+  // backward: W_dec h_t of every step from one GEMM before the loop
+  const LdsSeg last = wd_pre ? LdsSeg{L.wd, wd_pre + ((long long)b * d.S + t) * d.A, d.A}
+                             : LdsSeg{L.h, dec + ((long long)b * d.S + t) * d.D, d.D};
+  lds_fill(LdsSeg{L.wc, w_conv, d.A * d.C}, LdsSeg{L.cw, conv_w, d.C * d.K},
+           LdsSeg{L.v, vw, d.A}, last);
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+    if (tid + j * nt < TCH + d.K - 1) L.awin[tid + j * nt] = awv[j];
   __syncthreads();
-  if (wd_pre) {   // backward: W_dec h_t of every step from one GEMM before the loop
-    for (int a = tid; a < d.A; a += nt) L.wd[a] = wd_pre[((long long)b * d.S + t) * d.A + a];
-  }
-  for (int a = tid; a < d.A && !wd_pre; a += nt) {  // one thread per attention row
-    const float* wr = w_dec + (long long)a * d.D;
-    float s0 = 0.f, s1 = 0.f;
-    int k = 0;
-    if ((d.D & 3) == 0) {
-      for (; k + 8 <= d.D; k += 8) {
-        const float4 u = *reinterpret_cast<const float4*>(wr + k);
-        const float4 q = *reinterpret_cast<const float4*>(wr + k + 4);
-        s0 += u.x * L.h[k] + u.y * L.h[k + 1] + u.z * L.h[k + 2] + u.w * L.h[k + 3];
-        s1 += q.x * L.h[k + 4] + q.y * L.h[k + 5] + q.z * L.h[k + 6] + q.w * L.h[k + 7];
+  ATT_TR(trb + 1);
+  if (!wd_pre) {
+    // W_dec h_t: (row a, K slice qk) per thread, ten float4 of the row in flight
+    // per round, slices summed through L.cmb (2A + A C floats: nq <= 2 + C)
+    const int a = tid % d.A, qk = tid / d.A;
+    const int nq = min(nt / d.A, 2 + d.C);                    // >= 1 (A <= 256)
+    float s = 0.f;
+    if (qk < nq && (d.D & 3) == 0) {
+      const int kq = ((d.D / 4 + nq - 1) / nq) * 4;           // K per quarter (mult of 4)
+      const int k0 = qk * kq, k1 = min(d.D, k0 + kq);
+      const float* wr = w_dec + (long long)a * d.D;
+      for (int kb = k0; kb < k1; kb += 40) {
+        float4 u[10];
+#pragma unroll
+        for (int j = 0; j < 10; ++j)
+          u[j] = kb + 4 * j < k1 ? *reinterpret_cast<const float4*>(wr + kb + 4 * j)
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int j = 0; j < 10; ++j) {
+          const int k = kb + 4 * j;
+          if (k < k1)
+            s += u[j].x * L.h[k] + u[j].y * L.h[k + 1] + u[j].z * L.h[k + 2] +
+                 u[j].w * L.h[k + 3];
+        }
       }
+    } else if (qk == 0) {
+      const float* wr = w_dec + (long long)a * d.D;
+      for (int k = 0; k < d.D; ++k) s += wr[k] * L.h[k];
     }
-    for (; k < d.D; ++k) s0 += wr[k] * L.h[k];
-    L.wd[a] = s0 + s1;
+    if (qk < nq) L.cmb[qk * d.A + a] = s;
+    __syncthreads();
+    for (int r = tid; r < d.A; r += nt) {
+      float v = L.cmb[r];
+      for (int q = 1; q < nq && (d.D & 3) == 0; ++q) v += L.cmb[q * d.A + r];
+      L.wd[r] = v;
+    }
   }
+  ATT_TR(trb + 2);
   for (int i = tid; i < TCH * d.C; i += nt) {
     const int fi = i / d.C, c = i % d.C;
     float s = 0.f;
     if (tt0 + fi < d.T) {
       const float* cwr = L.cw + c * d.K;
       const float* aw = L.awin + fi;        // aw_{t-1}[tt - half + k] = awin[fi + k]
-      for (int k = 0; k < d.K; ++k) s += cwr[k] * aw[k];
+      s = dot_lds(cwr, 1, aw, 1, d.K);
     }
     L.f[i] = s;
   }
   __syncthreads();
+  ATT_TR(trb + 3);
 }
 
+template <int CC>
 __global__ void __launch_bounds__(ATT_THREADS) att_energy(
     int t, Dims d, const float* __restrict__ enc_a, const int32_t* __restrict__ lens,
     const float* __restrict__ w_dec, const float* __restrict__ w_conv,
@@ -299,38 +396,43 @@ __global__ void __launch_bounds__(ATT_THREADS) att_energy(
   const Dims dd = d;
   EnLds L = carve_en(smem, dd);
   const int b = blockIdx.y, tt0 = blockIdx.x * TCH;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  en_prologue(t, dd, b, tt0, L, w_dec, w_conv, conv_w, vw, dec, aw_all);
-  const int len = lens[b];
-  // one wave per frame, lanes over the attention dim (a = lane + 64 q, A <= 256);
-  // the next frame's enc_a row is loaded before this frame's math
-  float ean[4];
-  auto load_ea = [&](int i) {
-    const int tt = tt0 + i;
-    const float* ea = enc_a + ((long long)b * d.T + tt) * d.A;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // one wave per frame (frames w + FPW_STRIDE f), lanes over the attention dim
+  // (a = lane + 64 q, A <= 256): every enc_a row this wave needs is loaded
+  // before the prologue, so its latency overlaps the prologue's
+  float ea[FPW][4];
+#pragma unroll
+  for (int f = 0; f < FPW; ++f) {
+    const int tt = tt0 + w + ATT_WAVES * f;
+    const float* er = enc_a + ((long long)b * d.T + tt) * d.A;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int a = lane + 64 * q;
-      ean[q] = (i < TCH && tt < d.T && a < d.A) ? ea[a] : 0.f;
+      ea[f][q] = (tt < d.T && a < d.A) ? er[a] : 0.f;
     }
-  };
-  load_ea(w);
-  for (int i = w; i < TCH; i += nw) {
+  }
+  en_prologue(t, dd, b, tt0, L, w_dec, w_conv, conv_w, vw, dec, aw_all, nullptr, 0);
+  const int len = lens[b];
+#pragma unroll
+  for (int f = 0; f < FPW; ++f) {
+    const int i = w + ATT_WAVES * f;
     const int tt = tt0 + i;
     if (tt >= d.T) break;
-    float eac[4];
+    const float* eac = ea[f];
+    constexpr int CM = CC ? CC : 16;
+    const int C = CC ? CC : d.C;
+    float frv[CM];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) eac[q] = ean[q];
-    load_ea(i + nw);
-    const float* fr = L.f + i * d.C;
+    for (int c = 0; c < CM; ++c) frv[c] = (CC || c < C) ? L.f[i * C + c] : 0.f;
     float s = 0.f;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int a = lane + 64 * q;
-      if (a < d.A) {
+      if (64 * q < d.A && a < d.A) {
         float p = eac[q] + L.wd[a];
-        const float* wr = L.wc + a * d.C;
-        for (int c = 0; c < d.C; ++c) p += fr[c] * wr[c];
+#pragma unroll
+        for (int c = 0; c < CM; ++c)
+          if (CC || c < C) p += frv[c] * L.wc[a * C + c];
         s += L.v[a] * tanhf(p);
       }
     }
@@ -338,6 +440,7 @@ __global__ void __launch_bounds__(ATT_THREADS) att_energy(
     // multiplicative mask (attention_layer.py:216-225), then sharpening
     if (lane == 0) ebuf[(long long)b * d.T + tt] = (tt < len ? s : 0.f) * d.sharpen;
   }
+  ATT_TR(4);
 }
 
 __global__ void __launch_bounds__(ATT_THREADS) att_context(
@@ -376,9 +479,21 @@ __global__ void __launch_bounds__(ATT_THREADS) att_context(
   const int col = tid & (ECH - 1), r = tid / ECH, nr = blockDim.x / ECH;
   const int e = e0 + col;
   float s = 0.f;
-  if (e < d.E) {
+  if (e < d.E) {   // sixteen frames' loads in flight per round
     const float* er = enc + (long long)b * d.T * d.E + e;
-    for (int tt = r; tt < d.T; tt += nr) s += aw[tt] * er[(long long)tt * d.E];
+    for (int tb = r; tb < d.T; tb += 16 * nr) {
+      float v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int tt = tb + j * nr;
+        v[j] = tt < d.T ? er[(long long)tt * d.E] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int tt = tb + j * nr;
+        if (tt < d.T) s += aw[tt] * v[j];
+      }
+    }
   }
   part[r * ECH + col] = s;
   __syncthreads();
@@ -447,37 +562,68 @@ __global__ void __launch_bounds__(ATT_THREADS) att_bwd_daw(
   const int b = blockIdx.y, tt0 = blockIdx.x * TCH;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
   const int ED = d.E + d.D;
-  for (int e = tid; e < d.E; e += blockDim.x) {
-    const float v = dctx_in[((long long)b * d.S + t) * d.E + e] + (r ? r[(long long)b * ED + e] : 0.f);
-    dct[e] = v;
-    if (blockIdx.x == 0) dctx_tot[((long long)b * d.S + t) * d.E + e] = v;
+  (void)nw;
+  // d ctx: every thread's elements loaded in one round (E <= 4 * blockDim.x
+  // per pass)
+  for (int e0 = 0; e0 < d.E; e0 += 4 * ATT_THREADS) {
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int e = e0 + j * ATT_THREADS + tid;
+      v[j] = e < d.E ? dctx_in[((long long)b * d.S + t) * d.E + e] +
+                           (r ? r[(long long)b * ED + e] : 0.f)
+                     : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int e = e0 + j * ATT_THREADS + tid;
+      if (e < d.E) {
+        dct[e] = v[j];
+        if (blockIdx.x == 0) dctx_tot[((long long)b * d.S + t) * d.E + e] = v[j];
+      }
+    }
   }
   __syncthreads();
-  constexpr int FB = 4;   // frames in flight per wave
-  for (int i0 = w * FB; i0 < TCH; i0 += nw * FB) {
-    float s[FB];
+  // this wave's frames (w + ATT_WAVES f): NE enc elements of every frame in
+  // flight per round
+  constexpr int NE = 4;
+  float s[FPW];
 #pragma unroll
-    for (int f = 0; f < FB; ++f) {
-      const int tt = tt0 + i0 + f;
-      s[f] = 0.f;
-      if (i0 + f < TCH && tt < d.T) {
-        const float* er = enc + ((long long)b * d.T + tt) * d.E;
-        for (int e = lane; e < d.E; e += 64) s[f] += er[e] * dct[e];
+  for (int f = 0; f < FPW; ++f) s[f] = 0.f;
+  for (int eb = lane; eb < d.E; eb += 64 * NE) {
+    float v[FPW][NE];
+#pragma unroll
+    for (int f = 0; f < FPW; ++f) {
+      const int tt = tt0 + w + ATT_WAVES * f;
+      const float* er = enc + ((long long)b * d.T + tt) * d.E;
+#pragma unroll
+      for (int j = 0; j < NE; ++j) {
+        const int e = eb + 64 * j;
+        v[f][j] = (tt < d.T && e < d.E) ? er[e] : 0.f;
       }
     }
 #pragma unroll
-    for (int f = 0; f < FB; ++f) {
-      const int tt = tt0 + i0 + f;
-      const float v = wave_sum(s[f]);
-      if (lane == 0 && i0 + f < TCH && tt < d.T)
-        dawbuf[(long long)b * d.T + tt] = carry[(long long)b * d.T + tt] + v;
-    }
+    for (int f = 0; f < FPW; ++f)
+#pragma unroll
+      for (int j = 0; j < NE; ++j) {
+        const int e = eb + 64 * j;
+        if (e < d.E) s[f] += v[f][j] * dct[e];
+      }
+  }
+#pragma unroll
+  for (int f = 0; f < FPW; ++f) {
+    const int tt = tt0 + w + ATT_WAVES * f;
+    const float v = wave_sum(s[f]);
+    if (lane == 0 && tt < d.T) dawbuf[(long long)b * d.T + tt] = carry[(long long)b * d.T + tt] + v;
   }
 }
 
 // softmax / sigmoid backward -> d energy; per (frame, a): tanh backward -> d enc_a
 // (utterance-private RMW), dF [B][T][C], and chunk partials of dV, dW_dec-input,
 // dW_conv (fixed-order sums: deterministic).
+// CC: the conv channel count at compile time (0 = runtime d.C <= 16): with it
+// the per-frame channel loops are straight-line code over registers.
+template <int CC>
 __global__ void __launch_bounds__(ATT_THREADS) att_bwd_energy(
     int t, Dims d, const float* __restrict__ enc_a, const int32_t* __restrict__ lens,
     const float* __restrict__ w_dec, const float* __restrict__ w_conv,
@@ -492,6 +638,22 @@ __global__ void __launch_bounds__(ATT_THREADS) att_bwd_energy(
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
   const float* awt = aw_all + ((long long)b * d.S + t) * d.T;
   const float* daw = dawbuf + (long long)b * d.T;
+  ATT_TR(10);
+  // every enc_a / d_enc_a row of this wave's frames (w + ATT_WAVES f) is loaded
+  // first: its latency overlaps the softmax backward and the prologue
+  float ea[FPW][4], dea_in[FPW][4];
+#pragma unroll
+  for (int f = 0; f < FPW; ++f) {
+    const int tt = tt0 + w + ATT_WAVES * f;
+    const long long ro = ((long long)b * d.T + tt) * d.A;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int a = lane + 64 * q;
+      const bool ok = tt < d.T && a < d.A;
+      ea[f][q] = ok ? enc_a[ro + a] : 0.f;
+      dea_in[f][q] = ok ? d_enc_a[ro + a] : 0.f;
+    }
+  }
   float sdot = 0.f;
   for (int i = tid; i < d.T; i += blockDim.x) {
     const float a = awt[i];
@@ -510,78 +672,67 @@ __global__ void __launch_bounds__(ATT_THREADS) att_bwd_energy(
     }
     L.e[i] = de;
   }
-  en_prologue(t, dd, b, tt0, L, w_dec, w_conv, conv_w, vw, dec, aw_all, wd_all);
+  ATT_TR(11);
+  en_prologue(t, dd, b, tt0, L, w_dec, w_conv, conv_w, vw, dec, aw_all, wd_all, 12);
+  constexpr int CM = CC ? CC : 16;
+  const int C = CC ? CC : d.C;
   float accV[4] = {0.f, 0.f, 0.f, 0.f}, accWd[4] = {0.f, 0.f, 0.f, 0.f};
-  float accWc[4][16];
+  float accWc[4][CM];
 #pragma unroll
   for (int q = 0; q < 4; ++q)
 #pragma unroll
-    for (int c = 0; c < 16; ++c) accWc[q][c] = 0.f;
-  // the next frame's enc_a / d_enc_a rows are loaded before this frame's math
-  float ean[4], dean[4];
-  auto load_rows = [&](int i) {
-    const int tt = tt0 + i;
-    const bool ok = i < TCH && tt < d.T && L.e[i] != 0.f;
-    const long long ro = ((long long)b * d.T + tt) * d.A;
+    for (int c = 0; c < CM; ++c) accWc[q][c] = 0.f;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int a = lane + 64 * q;
-      ean[q] = (ok && a < d.A) ? enc_a[ro + a] : 0.f;
-      dean[q] = (ok && a < d.A) ? d_enc_a[ro + a] : 0.f;
-    }
-  };
-  load_rows(w);
-  for (int i = w; i < TCH; i += nw) {
+  for (int f = 0; f < FPW; ++f) {
+    const int i = w + ATT_WAVES * f;
     const int tt = tt0 + i;
     if (tt >= d.T) break;
     const float de = L.e[i];
-    float eac[4], deac[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      eac[q] = ean[q];
-      deac[q] = dean[q];
-    }
-    load_rows(i + nw);
-    float* dfo = dFbuf + ((long long)b * d.T + tt) * d.C;
+    const float* eac = ea[f];
+    const float* deac = dea_in[f];
+    float* dfo = dFbuf + ((long long)b * d.T + tt) * C;
     if (de == 0.f) {               // padded / masked frame: nothing flows
-      if (lane < d.C) dfo[lane] = 0.f;
+      if (lane < C) dfo[lane] = 0.f;
       continue;
     }
     float* dea = d_enc_a + ((long long)b * d.T + tt) * d.A;
-    const float* fr = L.f + i * d.C;
-    float dfc[16];
+    float frv[CM], dfc[CM];
 #pragma unroll
-    for (int c = 0; c < 16; ++c) dfc[c] = 0.f;
+    for (int c = 0; c < CM; ++c) {
+      frv[c] = (CC || c < C) ? L.f[i * C + c] : 0.f;
+      dfc[c] = 0.f;
+    }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int a = lane + 64 * q;
-      if (a < d.A) {
-        const float* wr = L.wc + a * d.C;
-        float p = eac[q] + L.wd[a];
+      if (64 * q < d.A) {          // wave-uniform
+        float wrv[CM];
 #pragma unroll
-        for (int c = 0; c < 16; ++c)
-          if (c < d.C) p += fr[c] * wr[c];
+        for (int c = 0; c < CM; ++c) wrv[c] = (a < d.A && (CC || c < C)) ? L.wc[a * C + c] : 0.f;
+        float p = eac[q] + (a < d.A ? L.wd[a] : 0.f);
+#pragma unroll
+        for (int c = 0; c < CM; ++c) p += frv[c] * wrv[c];
         const float th = tanhf(p);
-        const float dp = de * L.v[a] * (1.f - th * th);
-        accV[q] += de * th;
+        const float dp = a < d.A ? de * L.v[a] * (1.f - th * th) : 0.f;
+        accV[q] += a < d.A ? de * th : 0.f;
         accWd[q] += dp;
-        dea[a] = deac[q] + dp;
+        if (a < d.A) dea[a] = deac[q] + dp;
 #pragma unroll
-        for (int c = 0; c < 16; ++c)
-          if (c < d.C) {
-            accWc[q][c] += dp * fr[c];
-            dfc[c] += dp * wr[c];
-          }
+        for (int c = 0; c < CM; ++c) {
+          accWc[q][c] += dp * frv[c];
+          dfc[c] += dp * wrv[c];
+        }
       }
     }
 #pragma unroll
-    for (int c = 0; c < 16; ++c) {
-      if (c < d.C) {
+    for (int c = 0; c < CM; ++c) {
+      if (CC || c < C) {
         const float sv = wave_sum(dfc[c]);
         if (lane == 0) dfo[c] = sv;
       }
     }
   }
+  ATT_TR(16);
   // combine the per-wave partials in LDS in a fixed wave order, then one store
   // of this chunk's slots
   const long long slot = ((long long)b * d.S + t) * NC + ch;
@@ -597,8 +748,8 @@ __global__ void __launch_bounds__(ATT_THREADS) att_bwd_energy(
           cV[a] = pass ? cV[a] + accV[q] : accV[q];
           cWd[a] = pass ? cWd[a] + accWd[q] : accWd[q];
 #pragma unroll
-          for (int c = 0; c < 16; ++c)
-            if (c < d.C) cWc[a * d.C + c] = pass ? cWc[a * d.C + c] + accWc[q][c] : accWc[q][c];
+          for (int c = 0; c < CM; ++c)
+            if (CC || c < C) cWc[a * C + c] = pass ? cWc[a * C + c] + accWc[q][c] : accWc[q][c];
         }
       }
     }
@@ -612,6 +763,7 @@ __global__ void __launch_bounds__(ATT_THREADS) att_bwd_energy(
     dwdp[i] = cWd[i];
   }
   for (int i = tid; i < d.A * d.C; i += blockDim.x) dwcp[i] = cWc[i];
+  ATT_TR(17);
 }
 
 // d aw_{t-1} (conv transpose of dF; written over carry for step t-1), this
@@ -629,20 +781,45 @@ __global__ void __launch_bounds__(ATT_THREADS) att_bwd_conv(
   float* awin = dFw + (size_t)W * d.C;     // [W]   aw_{t-1}[j0 - half + i]
   float* dWd = awin + W;                   // [A]
   float* cpart = dWd + d.A;                // [TCH][C]
+  float* dred = cpart + TCH * d.C;         // [blockDim.x] d dec slice partials
   const int b = blockIdx.y, ch = blockIdx.x, j0 = ch * TCH, NC = gridDim.x;
   const int tid = threadIdx.x, nt = blockDim.x;
   const int half = d.K / 2;
-  for (int i = tid; i < d.C * d.K; i += nt) cw[i] = conv_w[i];
-  for (int i = tid; i < W * d.C; i += nt) {
-    const int row = j0 - half + i / d.C;
-    dFw[i] = (row >= 0 && row < d.T) ? dFbuf[((long long)b * d.T + row) * d.C + i % d.C] : 0.f;
-  }
-  for (int i = tid; i < W; i += nt) {
-    const int tt = j0 - half + i;
-    awin[i] = (t > 0 && tt >= 0 && tt < d.T) ? aw_all[((long long)b * d.S + t - 1) * d.T + tt]
-                                             : 0.f;
+  ATT_TR(20);
+  // conv kernel, the dF window and the aw_{t-1} window in batched rounds (16
+  // loads in flight per thread), zero outside [0, T)
+  {
+    const int n1 = d.C * d.K, n2 = n1 + W * d.C, total = n2 + W;
+    const long long dfb = ((long long)b * d.T + j0 - half) * d.C;   // dF row j0 - half, col 0
+    const float* awp = aw_all + ((long long)b * d.S + t - 1) * d.T + (j0 - half);
+    for (int base = 0; base < total; base += 16 * nt) {
+      float v[16];
+#pragma unroll
+      for (int jx = 0; jx < 16; ++jx) {
+        const int i = base + jx * nt + tid;
+        float x = 0.f;
+        if (i < n1) {
+          x = conv_w[i];
+        } else if (i < n2) {
+          const int row = j0 - half + (i - n1) / d.C;
+          if (row >= 0 && row < d.T) x = dFbuf[dfb + (i - n1)];
+        } else if (i < total) {
+          const int tt = j0 - half + (i - n2);
+          if (t > 0 && tt >= 0 && tt < d.T) x = awp[i - n2];
+        }
+        v[jx] = x;
+      }
+#pragma unroll
+      for (int jx = 0; jx < 16; ++jx) {
+        const int i = base + jx * nt + tid;
+        if (i < n1) cw[i] = v[jx];
+        else if (i < n2) dFw[i - n1] = v[jx];
+        else if (i < total) awin[i - n2] = v[jx];
+      }
+    }
   }
   __syncthreads();
+  ATT_TR(21);
   // d aw_{t-1}[j] = sum_c sum_k dF[j - k + half, c] cw[c, k]; window row of j - k + half
   // is (j - j0) + (K - 1) - k
   for (int i = tid; i < TCH * d.C; i += nt) {   // one thread per (frame, channel)
@@ -651,11 +828,12 @@ __global__ void __launch_bounds__(ATT_THREADS) att_bwd_conv(
     if (j0 + jj < d.T) {
       const float* cwr = cw + c * d.K;
       const float* dfr = dFw + (size_t)(jj + d.K - 1) * d.C + c;
-      for (int k = 0; k < d.K; ++k) s += dfr[-(long long)k * d.C] * cwr[k];
+      s = dot_lds(dfr, -d.C, cwr, 1, d.K);
     }
     cpart[i] = s;
   }
   __syncthreads();
+  ATT_TR(22);
   for (int jj = tid; jj < TCH; jj += nt) {
     const int j = j0 + jj;
     if (j >= d.T) break;
@@ -669,22 +847,53 @@ __global__ void __launch_bounds__(ATT_THREADS) att_bwd_conv(
   for (int i = tid; i < d.C * d.K; i += nt) {
     const int c = i / d.K, k = i % d.K;
     float s = 0.f;
-    for (int q = 0; q < nrow; ++q) s += dFw[(size_t)(q + half) * d.C + c] * awin[q + k];
+    s = dot_lds(dFw + (size_t)half * d.C + c, d.C, awin + k, 1, nrow);
     dcwp[i] = s;
   }
-  if (ch != 0) return;
+  ATT_TR(24);
+  // dW_dec input of step t (sum of the chunks' partials: every chunk forms it,
+  // chunk 0 stores it) and d dec_t = W_dec^T dWd, its D outputs split over the
+  // utterance's NC chunk work-groups: (output k, slice of A) per thread
   for (int a = tid; a < d.A; a += nt) {
     float s = 0.f;
     for (int q = 0; q < NC; ++q) s += dwd_chunk[((long long)b * NC + q) * d.A + a];
     dWd[a] = s;
-    dwd_all[((long long)b * d.S + t) * d.A + a] = s;
+    if (ch == 0) dwd_all[((long long)b * d.S + t) * d.A + a] = s;
   }
   __syncthreads();
-  for (int k = tid; k < d.D; k += nt) {
-    float s = 0.f;
-    for (int a = 0; a < d.A; ++a) s += w_dec[(long long)a * d.D + k] * dWd[a];
-    ddec_att[(long long)b * d.D + k] = s;
+  ATT_TR(23);
+  const int KS = (d.D + NC - 1) / NC, k0 = ch * KS, nk = min(KS, d.D - k0);
+  if (nk > 0 && KS > nt) {   // few chunks, wide decoder: whole-A sums per output
+    for (int k = tid; k < nk; k += nt) {
+      float v = 0.f;
+      for (int a = 0; a < d.A; ++a) v += w_dec[(long long)a * d.D + k0 + k] * dWd[a];
+      ddec_att[(long long)b * d.D + k0 + k] = v;
+    }
+  } else if (nk > 0) {
+    const int ns = max(1, min(nt / KS, d.A));            // A slices
+    const int kk = tid % KS, sl = tid / KS;
+    const int AS = (d.A + ns - 1) / ns, a0 = sl * AS, a1 = min(d.A, a0 + AS);
+    float sacc = 0.f;
+    if (sl < ns && kk < nk) {
+      for (int ab = a0; ab < a1; ab += 16) {   // sixteen W_dec rows in flight per round
+        float v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          v[j] = ab + j < a1 ? w_dec[(long long)(ab + j) * d.D + k0 + kk] : 0.f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          if (ab + j < a1) sacc += v[j] * dWd[ab + j];
+      }
+    }
+    if (sl < ns) dred[sl * KS + kk] = sacc;
+    __syncthreads();
+    for (int k = tid; k < nk; k += nt) {
+      float v = dred[k];
+      for (int q = 1; q < ns; ++q) v += dred[q * KS + k];
+      ddec_att[(long long)b * d.D + k0 + k] = v;
+    }
   }
+  ATT_TR(26);
 }
 
 // -------------------------------------------------------------- cell backward
@@ -861,6 +1070,11 @@ AttWs att_ws(const Dims& d, int cdt, bool bwd) {
 
 using namespace asr;
 
+extern "C" int asr_att_trace_read(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(asr::g_att_tr), sizeof(asr::g_att_tr)) ==
+                 hipSuccess ? ASR_OK : ASR_ERR_HIP;
+}
+
 extern "C" size_t asr_attdec_workspace_bytes(const asr_attdec_dims_t* dims, int compute_dtype,
                                              int backward) {
   return att_ws(to_dims(*dims), compute_dtype, backward != 0).total;
@@ -968,8 +1182,15 @@ extern "C" int asr_attdec_forward_ex(const asr_attdec_dims_t* dims, const asr_at
                            seed_h);
       ASR_LAUNCH_CHECK();
     }
-    hipLaunchKernelGGL(att_energy, eg, dim3(ATT_THREADS), en_lds, s, t, d, enc_a, lens, w_dec,
-                       w_conv, conv_w, v, dec, aw_all, ebuf);
+    if (d.C == 10)
+      hipLaunchKernelGGL(att_energy<10>, eg, dim3(ATT_THREADS), en_lds, s, t, d, enc_a, lens,
+                         w_dec, w_conv, conv_w, v, dec, aw_all, ebuf);
+    else if (d.C == 3)
+      hipLaunchKernelGGL(att_energy<3>, eg, dim3(ATT_THREADS), en_lds, s, t, d, enc_a, lens,
+                         w_dec, w_conv, conv_w, v, dec, aw_all, ebuf);
+    else
+      hipLaunchKernelGGL(att_energy<0>, eg, dim3(ATT_THREADS), en_lds, s, t, d, enc_a, lens,
+                         w_dec, w_conv, conv_w, v, dec, aw_all, ebuf);
     ASR_LAUNCH_CHECK();
     hipLaunchKernelGGL(att_context, xg, dim3(ATT_THREADS), cx_lds, s, t, d, enc, ebuf, aw_all,
                        ctx_all, x);
@@ -1088,9 +1309,14 @@ extern "C" int asr_attdec_backward_ex(const asr_attdec_dims_t* dims, const asr_a
     hipLaunchKernelGGL(att_bwd_daw, eg, dim3(ATT_THREADS), dw_lds, s, t, d, enc, d_ctx_in, rp,
                        carry, dctx_tot, dawbuf);
     ASR_LAUNCH_CHECK();
-    hipLaunchKernelGGL(att_bwd_energy, eg, dim3(ATT_THREADS), en_lds, s, t, d, enc_a, lens, w_dec,
-                       w_conv, conv_w, v, dec, aw_all, dawbuf, wd_all, d_enc_a, dFbuf, dwd_chunk,
-                       dv_part, dwc_part);
+#define ASR_BWD_EN(CC)                                                                        \
+  hipLaunchKernelGGL(att_bwd_energy<CC>, eg, dim3(ATT_THREADS), en_lds, s, t, d, enc_a, lens,    \
+                     w_dec, w_conv, conv_w, v, dec, aw_all, dawbuf, wd_all, d_enc_a, dFbuf,      \
+                     dwd_chunk, dv_part, dwc_part)
+    if (d.C == 10) ASR_BWD_EN(10);
+    else if (d.C == 3) ASR_BWD_EN(3);
+    else ASR_BWD_EN(0);
+#undef ASR_BWD_EN
     ASR_LAUNCH_CHECK();
     hipLaunchKernelGGL(att_bwd_conv, eg, dim3(ATT_THREADS), cv_lds, s, t, d, conv_w, aw_all, dFbuf,
                        w_dec, dwd_chunk, carry, dcw_part, dwd_all, ddec_att);
