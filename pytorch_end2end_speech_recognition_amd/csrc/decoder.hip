@@ -37,7 +37,7 @@ inline Dims to_dims(const asr_attdec_dims_t& d) {
 
 constexpr int MB = 32;   // utterances per cell work-group
 constexpr int CU = 4;    // hidden units per cell work-group (16 gate columns)
-constexpr int ATT_THREADS = 256;
+constexpr int ATT_THREADS = 512;   // 8 waves: two per SIMD hide the per-frame latencies
 
 template <typename T>
 __device__ __forceinline__ float ldw(const T* p, long long i);
@@ -449,7 +449,7 @@ __global__ void __launch_bounds__(ATT_THREADS) att_context(
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* aw = smem;             // [T]
   float* red = aw + d.T;        // [64]
-  float* part = red + 64;       // [4][ECH]
+  float* part = red + 64;       // [ATT_THREADS / ECH][ECH]
   const int b = blockIdx.y, e0 = blockIdx.x * ECH;
   const int tid = threadIdx.x;
   float mx = -__builtin_huge_valf();
@@ -1034,7 +1034,7 @@ int check_dims(const Dims& d) {
               d.C);
   ASR_REQUIRE(d.K % 2 == 1, ASR_ERR_ARG, "attdec: conv width must be odd");
   ASR_REQUIRE(en_lds_floats(d) * 4 <= 160 * 1024 && conv_lds_floats(d) * 4 <= 160 * 1024 &&
-                  ((size_t)d.T + 64 + 4 * ECH) * 4 <= 160 * 1024,
+                  ((size_t)d.T + 64 + ATT_THREADS) * 4 <= 160 * 1024,
               ASR_ERR_UNSUPPORTED, "attdec: LDS need %zu B > 160 KiB", en_lds_floats(d) * 4);
   return ASR_OK;
 }
@@ -1156,7 +1156,7 @@ extern "C" int asr_attdec_forward_ex(const asr_attdec_dims_t* dims, const asr_at
   const AttWs W = att_ws(d, compute_dtype, false);
   float* ebuf = (float*)((char*)workspace + W.ebuf);
   const size_t en_lds = en_lds_floats(d) * 4;
-  const size_t cx_lds = ((size_t)d.T + 64 + 4 * ECH) * 4;
+  const size_t cx_lds = ((size_t)d.T + 64 + ATT_THREADS) * 4;
   const dim3 eg(att_chunks(d), d.B), xg(ceil_div(d.E, ECH), d.B);
   const int vec = ((d.E + d.D) % 8 == 0) ? 1 : 0;
   const dim3 cg(ceil_div(d.D, CU), ceil_div(d.B, MB));
