@@ -59,6 +59,55 @@ __device__ __forceinline__ bf16x8 frag8g(const T* row, int k, int klim, bool vec
   return as_bf16x8(r);
 }
 
+// acc0/acc1 += rows xr0/xr1 (K floats) x row wr (K weights), this wave's k
+// steps (wave * 32 + 128 j for bf16 MFMA, wave * 4 + 16 j for f32 MFMA) in the
+// same order as a plain loop, but with the fragments of NB steps loaded before
+// their MFMAs: one memory round trip per NB steps instead of one per step.
+template <bool BF16, typename TW>
+__device__ __forceinline__ void rows_mma(const float* xr0, const float* xr1, const TW* wr, int K,
+                                         int wave, int lane, bool vec, f32x4& acc0, f32x4& acc1) {
+  if constexpr (BF16) {
+    constexpr int NB = 4;
+    for (int kb = wave * 32; kb < K; kb += 128 * NB) {
+      bf16x8 fw[NB], f0[NB], f1[NB];
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const bool live = kb + 128 * j < K;
+        const int k = kb + 128 * j + 8 * (lane >> 4);
+        fw[j] = frag8g<TW>(live ? wr : nullptr, k, K, vec);
+        f0[j] = frag8g<float>(live ? xr0 : nullptr, k, K, vec);
+        f1[j] = frag8g<float>(live ? xr1 : nullptr, k, K, vec);
+      }
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        if (kb + 128 * j < K) {   // wave-uniform
+          acc0 = mfma_bf16(f0[j], fw[j], acc0);
+          acc1 = mfma_bf16(f1[j], fw[j], acc1);
+        }
+      }
+    }
+  } else {
+    constexpr int NB = 8;
+    for (int kb = wave * 4; kb < K; kb += 16 * NB) {
+      float w[NB], x0[NB], x1[NB];
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const int k = kb + 16 * j + (lane >> 4);
+        w[j] = (wr && k < K) ? ldw<TW>(wr, k) : 0.f;
+        x0[j] = (xr0 && k < K) ? xr0[k] : 0.f;
+        x1[j] = (xr1 && k < K) ? xr1[k] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        if (kb + 16 * j < K) {   // wave-uniform
+          acc0 = mfma_f32(x0[j], w[j], acc0);
+          acc1 = mfma_f32(x1[j], w[j], acc1);
+        }
+      }
+    }
+  }
+}
+
 // -------------------------------------------------------------- init kernel
 // dec[b,0] = h0, x[b,1,E:] = h0, c[b,0] = 0, gates[b,0,:] = 0
 __global__ void dec_init(Dims d, const float* __restrict__ h0, float* __restrict__ dec,
@@ -124,21 +173,7 @@ __global__ void __launch_bounds__(256) cell_fwd(int t, Dims d, const TW* __restr
   const int n = lane & 15, g = n >> 2, u = u0 + (n & 3);
   const TW* wr = u < d.D ? wcat + (long long)(g * d.D + u) * ED : nullptr;
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-  if (BF16) {
-    for (int k0 = wave * 32; k0 < ED; k0 += 128) {
-      const int k = k0 + 8 * (lane >> 4);
-      const bf16x8 bw = frag8g<TW>(wr, k, ED, vec != 0);
-      acc0 = mfma_bf16(frag8g<float>(xr0, k, ED, vec != 0), bw, acc0);
-      acc1 = mfma_bf16(frag8g<float>(xr1, k, ED, vec != 0), bw, acc1);
-    }
-  } else {
-    for (int k0 = wave * 4; k0 < ED; k0 += 16) {
-      const int k = k0 + (lane >> 4);
-      const float bw = (wr && k < ED) ? ldw<TW>(wr, k) : 0.f;
-      acc0 = mfma_f32((xr0 && k < ED) ? xr0[k] : 0.f, bw, acc0);
-      acc1 = mfma_f32((xr1 && k < ED) ? xr1[k] : 0.f, bw, acc1);
-    }
-  }
+  rows_mma<BF16, TW>(xr0, xr1, wr, ED, wave, lane, vec != 0, acc0, acc1);
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     part[wave][4 * (lane >> 4) + r][lane & 15] = acc0[r];
@@ -521,21 +556,7 @@ __global__ void __launch_bounds__(256) rgemm(int t1, Dims d, const TW* __restric
   const int n = n0 + (lane & 15);
   const TW* wr = n < ED ? wT + (long long)n * G : nullptr;
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-  if (BF16) {
-    for (int k0 = wave * 32; k0 < G; k0 += 128) {
-      const int k = k0 + 8 * (lane >> 4);
-      const bf16x8 bw = frag8g<TW>(wr, k, G, vec != 0);
-      acc0 = mfma_bf16(frag8g<float>(xr0, k, G, vec != 0), bw, acc0);
-      acc1 = mfma_bf16(frag8g<float>(xr1, k, G, vec != 0), bw, acc1);
-    }
-  } else {
-    for (int k0 = wave * 4; k0 < G; k0 += 16) {
-      const int k = k0 + (lane >> 4);
-      const float bw = (wr && k < G) ? ldw<TW>(wr, k) : 0.f;
-      acc0 = mfma_f32((xr0 && k < G) ? xr0[k] : 0.f, bw, acc0);
-      acc1 = mfma_f32((xr1 && k < G) ? xr1[k] : 0.f, bw, acc1);
-    }
-  }
+  rows_mma<BF16, TW>(xr0, xr1, wr, G, wave, lane, vec != 0, acc0, acc1);
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     part[wave][4 * (lane >> 4) + q][lane & 15] = acc0[q];
