@@ -240,14 +240,15 @@ class AttentionSeq2seq(ModelBase):
         return self.encoder(xs, x_lens, volatile=not self.training)
 
     def _init_h0(self, enc_out, task=0, dir='fwd'):
-        """_init_dec_state (:801-864): zero / first / final; 'mean' is a next item."""
+        """_init_dec_state (:801-864): zero / mean (over all T, padding included,
+        :832) / first / final, then tanh(W_dec_init(.))."""
         mode = getattr(self, 'init_dec_state_%d_%s' % (task, dir))
         if mode == 'zero':
             return None
-        if mode == 'mean':
-            raise NotImplementedError("init_dec_state='mean'")
         T = enc_out.shape[1]
         lin = getattr(self, 'W_dec_init_%d_%s' % (task, dir)).fc
+        if mode == 'mean':
+            return ops.tanh(ops.linear(ops.mean_time(enc_out), lin.weight, lin.bias))
         h = ops.linear_ex(enc_out, lin.weight, lin.bias, t_index=0 if mode == 'first' else T - 1)
         return ops.tanh(h)
 

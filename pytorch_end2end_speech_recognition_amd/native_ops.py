@@ -194,6 +194,41 @@ def linear_ex(x, weight, bias=None, bias2=None, c0=0, K=None, t_index=None):
     return LinearExFn.apply(x, weight, bias, bias2, c0, K, t_index)
 
 
+class MeanTimeFn(torch.autograd.Function):
+    """out[b] = mean_t x[b, t, :] over all T frames of [B, T, E] (padding
+    included, as enc_out.mean(dim=1) in attention_seq2seq.py:832), as one
+    batched GEMM ones(1 x T) . x[b] / T; backward dx[b, t] = dout[b] / T is the
+    batched K = 1 product ones(T x 1) . dout[b] / T."""
+
+    @staticmethod
+    def forward(ctx, x):
+        N.require_device(x)
+        x = x.contiguous()
+        B, T, E = x.shape
+        ones = torch.ones(T, dtype=torch.float32, device=x.device)
+        out = torch.empty(B, E, dtype=torch.float32, device=x.device)
+        run_gemm([gemm_problem(operand(ones, 0, rowmap(T)), operand(x, 1, rowmap(E)), out,
+                               rowmap(E), 1, E, T, alpha=1.0 / T, batch=B,
+                               batch_strides=(0, T * E, E))], x.device)
+        ctx.shape = (B, T, E)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        B, T, E = ctx.shape
+        dout = dout.contiguous()
+        ones = torch.ones(T, dtype=torch.float32, device=dout.device)
+        dx = torch.empty(B, T, E, dtype=torch.float32, device=dout.device)
+        run_gemm([gemm_problem(operand(ones, 0, rowmap(1)), operand(dout, 1, rowmap(E)), dx,
+                               rowmap(E), T, E, 1, alpha=1.0 / T, batch=B,
+                               batch_strides=(0, E, T * E))], dout.device)
+        return dx
+
+
+def mean_time(x):
+    return MeanTimeFn.apply(x)
+
+
 class Linear2Fn(torch.autograd.Function):
     """y = x1 W1^T + b1 + x2 W2^T + b2 (the attention bottleneck
     W_d(dec_out) + W_c(context), attention_seq2seq.py:788-790): two GEMMs into

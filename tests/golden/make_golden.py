@@ -412,8 +412,13 @@ def case_attention_model():
                                   label_smoothing_prob=0, sharpening_factor=1.5)),
         ('model_att_ls', dict(base, init_dec_state='zero', ctc_loss_weight=0.3,
                               label_smoothing_prob=0.1)),
+        ('model_att_mean', dict(base, init_dec_state='mean', ctc_loss_weight=0,
+                                label_smoothing_prob=0)),
     ]
+    only = _selected()
     for name, kw in specs:
+        if only and name not in only:
+            continue
         torch.manual_seed(1623)
         model = AttentionSeq2seq(**kw)
         model.train()
@@ -534,6 +539,7 @@ if __name__ == '__main__':
     _install_shims()
     if _selected():          # regenerate only the named model_ctc_* / dec_* cases
         case_ctc_model()
+        case_attention_model()
         case_attention_decode()
         case_hier_attention_model()
         sys.exit(0)

@@ -9,7 +9,7 @@ import torch
 
 from conftest import golden, golden_params
 
-NAMES = ['model_att', 'model_att_hybrid', 'model_att_ls']
+NAMES = ['model_att', 'model_att_hybrid', 'model_att_ls', 'model_att_mean']
 
 
 def _build(kw):

@@ -101,7 +101,7 @@ def test_ctc_model_oracle_matches_golden(name):
     np.testing.assert_array_equal(flat, d['hyp_flat'])
 
 
-@pytest.mark.parametrize('name', ['model_att', 'model_att_hybrid', 'model_att_ls'])
+@pytest.mark.parametrize('name', ['model_att', 'model_att_hybrid', 'model_att_ls', 'model_att_mean'])
 def test_attention_model_oracle_matches_golden(name):
     d = golden(name)
     kw = json.loads(str(d['kwargs']))
