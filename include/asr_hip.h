@@ -269,6 +269,10 @@ int asr_add_forward(const float* a, const float* b, float* y, long long n, void*
  * encoder layer (its input X, W_ih) in bf16 mode. */
 int asr_convert_rows_bf16(const float* src, asr_rowmap_t map, int nrows, int ncols,
                           uint16_t* dst, void* stream);
+/* Same with an output row pitch ld >= ncols; columns [ncols, ld) are zeros (a
+ * bf16 operand whose leading dimension is padded to a multiple of 8). */
+int asr_convert_rows_bf16_ld(const float* src, asr_rowmap_t map, int nrows, int ncols, int ld,
+                             uint16_t* dst, void* stream);
 
 /* ------------------------------------------------------------ decoding
  * asr_ctc_best_path: CTC greedy best path (greedy_decoder.py:19-47): per

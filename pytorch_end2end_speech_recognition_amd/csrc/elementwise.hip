@@ -81,8 +81,8 @@ __global__ void tanh_bwd(const float* __restrict__ y, const float* __restrict__ 
 // rows mapping outside [0, t_limit)); 8 columns per thread, 16-B stores when
 // ncols % 8 == 0.
 __global__ void convert_rows_kernel(const float* __restrict__ src, asr_rowmap_t m, int nrows,
-                                    int ncols, uint16_t* __restrict__ dst) {
-  const int cpr = (ncols + 7) >> 3;
+                                    int ncols, int ld, uint16_t* __restrict__ dst) {
+  const int cpr = (ld + 7) >> 3;   // columns [ncols, ld) are written as zeros
   const long long nchunks = (long long)nrows * cpr;
   const int rpb = m.rows_per_b > 0 ? m.rows_per_b : 0x7fffffff;
   const int tmul = m.t_mul == 0 ? 1 : m.t_mul;
@@ -96,10 +96,10 @@ __global__ void convert_rows_kernel(const float* __restrict__ src, asr_rowmap_t 
     const float* s = ok ? src + (long long)(m.perm ? m.perm[b] : b) * m.stride_b +
                               (long long)tp * m.stride_t + c0
                         : nullptr;
-    uint16_t* d = dst + (long long)r * ncols + c0;
-    if (ncols % 8 == 0) {
+    uint16_t* d = dst + (long long)r * ld + c0;
+    if (ncols % 8 == 0 && ld % 8 == 0) {
       u16x8 v;
-      if (ok) {
+      if (ok && c0 < ncols) {
         const float4 x0 = *reinterpret_cast<const float4*>(s);
         const float4 x1 = *reinterpret_cast<const float4*>(s + 4);
         v = u16x8{f2bf(x0.x), f2bf(x0.y), f2bf(x0.z), f2bf(x0.w),
@@ -109,7 +109,8 @@ __global__ void convert_rows_kernel(const float* __restrict__ src, asr_rowmap_t 
       }
       *reinterpret_cast<u16x8*>(d) = v;
     } else {
-      for (int j = 0; j < 8 && c0 + j < ncols; ++j) d[j] = ok ? f2bf(s[j]) : (uint16_t)0;
+      for (int j = 0; j < 8 && c0 + j < ld; ++j)
+        d[j] = (ok && c0 + j < ncols) ? f2bf(s[j]) : (uint16_t)0;
     }
   }
 }
@@ -221,17 +222,23 @@ extern "C" int asr_tanh_backward(const float* y, const float* dy, float* dx, lon
   return ASR_OK;
 }
 
-extern "C" int asr_convert_rows_bf16(const float* src, asr_rowmap_t map, int nrows, int ncols,
-                                     uint16_t* dst, void* stream) {
-  ASR_REQUIRE(src && dst && nrows >= 0 && ncols >= 0, ASR_ERR_ARG, "convert_rows: bad args");
-  if (ncols % 8 == 0)
+extern "C" int asr_convert_rows_bf16_ld(const float* src, asr_rowmap_t map, int nrows,
+                                        int ncols, int ld, uint16_t* dst, void* stream) {
+  ASR_REQUIRE(src && dst && nrows >= 0 && ncols >= 0 && ld >= ncols, ASR_ERR_ARG,
+              "convert_rows: bad args");
+  if (ncols % 8 == 0 && ld % 8 == 0)
     ASR_REQUIRE(((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0 &&
                     map.stride_t % 4 == 0 && map.stride_b % 4 == 0,
                 ASR_ERR_ARG, "convert_rows: vector path needs 16-B aligned rows");
-  const long long n = (long long)nrows * ((ncols + 7) / 8);
+  const long long n = (long long)nrows * ((ld + 7) / 8);
   if (n <= 0) return ASR_OK;
   hipLaunchKernelGGL(convert_rows_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
-                     src, map, nrows, ncols, dst);
+                     src, map, nrows, ncols, ld, dst);
   ASR_LAUNCH_CHECK();
   return ASR_OK;
+}
+
+extern "C" int asr_convert_rows_bf16(const float* src, asr_rowmap_t map, int nrows, int ncols,
+                                     uint16_t* dst, void* stream) {
+  return asr_convert_rows_bf16_ld(src, map, nrows, ncols, ncols, dst, stream);
 }

@@ -90,6 +90,24 @@ def colsum_accumulate(g2d, out0, out1=None, alpha=1.0):
 # ---------------------------------------------------------------------------
 # Linear (LinearND, linear.py:15-47): y = x W^T + b on the last dim
 # ---------------------------------------------------------------------------
+# bf16 mode stages f32 GEMM operands in bf16 (one conversion pass) when a
+# product is at least this large, so it takes the bf16 fast path / hipBLASLt
+# instead of the generic kernel converting inside its loads (the word-level CTC
+# head, 8000 x 640 x 10001, ran at ~140 TF/s that way).
+_STAGE_FLOPS = 2e9
+
+
+def _staged(t, rows, cols, ld=None):
+    """bf16 [rows, ld] copy of a dense f32 tensor viewed as rows x cols, the
+    columns [cols, ld) zero (ld: cols rounded up to a multiple of 8 by default,
+    so the copy is a legal 16-B-aligned GEMM operand)."""
+    ld = (cols + 7) // 8 * 8 if ld is None else ld
+    out = torch.empty(rows, ld, dtype=torch.bfloat16, device=t.device)
+    N.call('asr_convert_rows_bf16_ld', N.ptr(t), rowmap(cols), int(rows), int(cols), int(ld),
+           N.ptr(out), N.stream_handle(t.device))
+    return out
+
+
 class LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias):
@@ -99,35 +117,52 @@ class LinearFn(torch.autograd.Function):
         Nout = weight.shape[0]
         M = x.numel() // K
         y = torch.empty(*x.shape[:-1], Nout, dtype=torch.float32, device=x.device)
+        stage = compute_dtype() == BF16 and 2.0 * M * Nout * K >= _STAGE_FLOPS
+        # staged copies: x [M][Kp], weight [Np][Kp] (rows Nout.. and columns K.. zero)
+        Kp, Np = ((K + 7) // 8 * 8, (Nout + 7) // 8 * 8) if stage else (K, Nout)
+        if stage:
+            xo = _staged(x, M, K, Kp)
+            wo = torch.empty(Np, Kp, dtype=torch.bfloat16, device=x.device)
+            N.call('asr_convert_rows_bf16_ld', N.ptr(weight), rowmap(K), Nout, K, Kp, N.ptr(wo),
+                   N.stream_handle(x.device))
+            if Np > Nout:
+                N.call('asr_convert_rows_bf16_ld', N.ptr(weight), rowmap(0, t_limit=1,
+                       rows_per_b=Np - Nout, t_add=1), Np - Nout, Kp, Kp,
+                       ctypes.c_void_p(wo.data_ptr() + Nout * Kp * 2), N.stream_handle(x.device))
+        else:
+            xo, wo = x, weight
         if M > 0:
-            p = gemm_problem(operand(x, 0, rowmap(K)), operand(weight, 0, rowmap(K)), y,
-                             rowmap(Nout), M, Nout, K, bias=bias)
+            p = gemm_problem(operand(xo, 0, rowmap(Kp)), operand(wo, 0, rowmap(Kp)), y,
+                             rowmap(Nout), M, Nout, Kp, bias=bias)
             run_gemm([p], x.device)
-        ctx.save_for_backward(x, weight)
-        ctx.bias = bias
+        ctx.save_for_backward(xo, wo)
+        ctx.meta = (bias, stage, tuple(x.shape), weight)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, weight = ctx.saved_tensors
+        xo, wo = ctx.saved_tensors
+        bias, stage, xshape, weight = ctx.meta
         dy = dy.contiguous()
-        K = x.shape[-1]
+        K = xshape[-1]
         Nout = weight.shape[0]
-        M = x.numel() // K
+        M = dy.numel() // Nout
         dx = None
         if M == 0:
-            return torch.zeros_like(x), None, None
+            return torch.zeros(xshape, dtype=torch.float32, device=dy.device), None, None
+        Kp, Np = (xo.shape[-1], wo.shape[0]) if stage else (K, Nout)
+        dyo = _staged(dy, M, Nout, Np) if stage else dy   # zero columns meet zero W rows
         probs = []
         if ctx.needs_input_grad[0]:
-            dx = torch.empty_like(x)
-            probs.append(gemm_problem(operand(dy, 0, rowmap(Nout)), operand(weight, 1, rowmap(K)),
-                                      dx, rowmap(K), M, K, Nout))
+            dx = torch.empty(xshape, dtype=torch.float32, device=dy.device)
+            probs.append(gemm_problem(operand(dyo, 0, rowmap(Np)), operand(wo, 1, rowmap(Kp)),
+                                      dx, rowmap(K), M, K, Np))
         gw = grad_buffer(weight)
-        probs.append(gemm_problem(operand(dy, 1, rowmap(Nout)), operand(x, 1, rowmap(K)), gw,
+        probs.append(gemm_problem(operand(dyo, 1, rowmap(Np)), operand(xo, 1, rowmap(Kp)), gw,
                                   rowmap(K), Nout, K, M, beta=1.0))
-        run_gemm(probs, x.device)
-        if ctx.bias is not None:
-            colsum_accumulate(dy.view(M, Nout), grad_buffer(ctx.bias))
+        run_gemm(probs, dy.device)
+        if bias is not None:
+            colsum_accumulate(dy.view(M, Nout), grad_buffer(bias))
         return dx, None, None
 
 

@@ -97,3 +97,38 @@ def test_library_and_mapped_problems_in_one_launch(cuda_dev):
         np.testing.assert_array_equal(C2.cpu().numpy(), ref2)
     finally:
         ops.set_compute_dtype('fp32')
+
+
+def test_linear_bf16_staged_padded(cuda_dev):
+    """LinearFn in bf16 mode above the staging threshold with an output width
+    that is not a multiple of 8 (the word-level CTC head, V = 10001): operands
+    staged in bf16 with zero-padded pitches; y, dx, dW, db vs float64 of the
+    same bf16-rounded values."""
+    ops = _ops()
+    ops.set_compute_dtype('bf16')
+    try:
+        rng = np.random.RandomState(11)
+        M, K, Nout = 2048, 640, 1001            # 2 M N K = 2.6e9 >= _STAGE_FLOPS
+        x = rng.randn(M, K).astype(np.float32)
+        w = (rng.randn(Nout, K) * 0.05).astype(np.float32)
+        b = rng.randn(Nout).astype(np.float32)
+        dy = rng.randn(M, Nout).astype(np.float32)
+        xd = torch.from_numpy(x).to(cuda_dev).requires_grad_(True)
+        wd = torch.from_numpy(w).to(cuda_dev).requires_grad_(True)
+        bd = torch.from_numpy(b).to(cuda_dev).requires_grad_(True)
+        y = ops.linear(xd, wd, bd)
+        y.backward(torch.from_numpy(dy).to(cuda_dev))
+        torch.cuda.synchronize()
+
+        def r(a):
+            return torch.from_numpy(a).to(torch.bfloat16).double().numpy()
+        xr, wr, dyr = r(x), r(w), r(dy)
+        ref_y = xr @ wr.T + b
+        ref_dx = dyr @ wr
+        ref_dw = dyr.T @ xr
+        for got, ref in ((y, ref_y), (xd.grad, ref_dx), (wd.grad, ref_dw)):
+            g = got.detach().cpu().double().numpy()
+            assert np.abs(g - ref).max() / (np.abs(ref).max() + 1e-9) < 1e-3
+        np.testing.assert_allclose(bd.grad.cpu().numpy(), dy.sum(0), rtol=1e-4, atol=1e-3)
+    finally:
+        ops.set_compute_dtype('fp32')
