@@ -7,15 +7,16 @@
 // Kernels (all stream-ordered, no host sync):
 //   ctc_prep    1 block: exclusive scan of label_lens -> label offsets; label
 //               range check -> status word.
-//   ctc_emit    one wave per (b,t) row: log-sum-exp over V (one HBM read of the
-//               row) and the S emissions e_t(s) = x[lab(s)] - lse, stored
+//   ctc_emit    one wave (V <= 1024) or one work-group (ctc_emit_wide) per
+//               (b,t) row: online log-sum-exp over V (one HBM read of the row) and the S emissions e_t(s) = x[lab(s)] - lse, stored
 //               lattice-contiguous so the sequential kernel streams them.
-//   ctc_lattice two waves per utterance, run concurrently: the alpha wave
-//               (forward over t, then log P and the cost) and the beta wave
-//               (backward over t); lane l owns K consecutive lattice states in
-//               registers, neighbours come through DPP wave shifts (one
-//               v_mov_dpp per step, no LDS, no barrier).  The sequential depth
-//               is T steps, not the 2T of an alpha-then-beta pass.
+//   ctc_lattice two work-groups per utterance, run concurrently: the alpha
+//               lattice (forward over t, then log P and the cost) and the beta
+//               lattice (backward over t); lane l owns K consecutive lattice
+//               states in registers, neighbours come through DPP wave shifts.
+//               A loader wave streams the emission rows into an LDS ring so
+//               the lattice wave never waits on a global load.  The sequential
+//               depth is T steps, not the 2T of an alpha-then-beta pass.
 //   ctc_grad    one row per block: occupancy exp(alpha+beta-e-logP) of the
 //               row's S states, summed per class through LDS (repeated
 //               labels), grad = (softmax - occupancy) * scale written once.
@@ -85,7 +86,32 @@ __global__ void ctc_prep(const int32_t* __restrict__ label_lens, const int32_t* 
   }
 }
 
-// One wave per (b,t) row.
+// The lattice runs in base 2 (emissions scaled by log2 e in ctc_emit; alpha,
+// beta and log P in log2 units; the cost converted back with ln 2), so every
+// transcendental is a bare v_exp_f32 / v_log_f32.
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+__device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ __forceinline__ float lg2(float x) { return __builtin_amdgcn_logf(x); }
+
+// Online log-sum-exp accumulator (running max m, sum s of exp(x - m)).
+__device__ __forceinline__ void lse_acc4(float& m, float& s, float4 v) {
+  const float mx = fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w));
+  if (mx > m) { s *= __expf(m - mx); m = mx; }
+  s += __expf(v.x - m) + __expf(v.y - m) + __expf(v.z - m) + __expf(v.w - m);
+}
+__device__ __forceinline__ void lse_acc1(float& m, float& s, float x) {
+  if (x > m) { s *= __expf(m - x); m = x; }
+  s += __expf(x - m);
+}
+
+// Elements of a row before its first 16-B boundary.
+__device__ __forceinline__ int head_elems(const float* p) {
+  return (int)((4 - (((size_t)p >> 2) & 3)) & 3);
+}
+
+// One wave per (b,t) row; the row is read ONCE (online max / sum, 16-B loads
+// from the row's first aligned element, four in flight per lane).
 __global__ void __launch_bounds__(256) ctc_emit(const float* __restrict__ acts, long long st,
                                                 long long sb, int T, int B, int V,
                                                 const int32_t* __restrict__ labels,
@@ -100,13 +126,21 @@ __global__ void __launch_bounds__(256) ctc_emit(const float* __restrict__ acts, 
   const int b = (int)(row / T), t = (int)(row % T);
   if (t >= act_lens[b]) return;
   const float* x = acts + (long long)t * st + (long long)b * sb;
-  float m = neg_inf();
-  for (int v = lane; v < V; v += 64) m = fmaxf(m, x[v]);
-  m = wave_max(m);
-  float s = 0.f;
-  for (int v = lane; v < V; v += 64) s += __expf(x[v] - m);
-  s = wave_sum(s);
-  const float lse = m + __logf(s);
+  float m = neg_inf(), s = 0.f;
+  const int h = min(head_elems(x), V);
+  if (lane < h) lse_acc1(m, s, x[lane]);
+  const int n4 = (V - h) >> 2;
+  const float4* x4 = reinterpret_cast<const float4*>(x + h);
+  int i = lane;
+  for (; i + 192 < n4; i += 256) {
+    const float4 v0 = x4[i], v1 = x4[i + 64], v2 = x4[i + 128], v3 = x4[i + 192];
+    lse_acc4(m, s, v0); lse_acc4(m, s, v1); lse_acc4(m, s, v2); lse_acc4(m, s, v3);
+  }
+  for (; i < n4; i += 64) lse_acc4(m, s, x4[i]);
+  for (int v = h + 4 * n4 + lane; v < V; v += 64) lse_acc1(m, s, x[v]);
+  const float M = wave_max(m);
+  const float tot = wave_sum(m == neg_inf() ? 0.f : s * __expf(m - M));
+  const float lse = M + __logf(tot);
   if (lane == 0) lse_out[row] = lse;
   const int L = min(label_lens[b], (Spad - 1) / 2);
   const int S = 2 * L + 1;
@@ -117,7 +151,71 @@ __global__ void __launch_bounds__(256) ctc_emit(const float* __restrict__ acts, 
     if (st_ < S) {
       int c = (st_ & 1) ? lab[st_ >> 1] : blank;
       c = c < 0 ? 0 : (c >= V ? V - 1 : c);
-      v = x[c] - lse;
+      v = (x[c] - lse) * kLog2e;
+    }
+    e[st_] = v;
+  }
+}
+
+// Wide rows (V > 1024): one 256-thread work-group per (b,t) row, so four
+// times the loads in flight per row; (max, sum) pairs combined through LDS.
+__global__ void __launch_bounds__(256) ctc_emit_wide(const float* __restrict__ acts, long long st,
+                                                     long long sb, int T, int V,
+                                                     const int32_t* __restrict__ labels,
+                                                     const int32_t* __restrict__ label_lens,
+                                                     const int32_t* __restrict__ act_lens,
+                                                     const int32_t* __restrict__ offs, int blank,
+                                                     int Spad, float* __restrict__ lse_out,
+                                                     float* __restrict__ emit) {
+  __shared__ float red_m[4], red_s[4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const long long row = blockIdx.x;
+  const int b = (int)(row / T), t = (int)(row % T);
+  if (t >= act_lens[b]) return;
+  const float* x = acts + (long long)t * st + (long long)b * sb;
+  float m = neg_inf(), s = 0.f;
+  const int h = min(head_elems(x), V);
+  if (tid < h) lse_acc1(m, s, x[tid]);
+  const int n4 = (V - h) >> 2;
+  const float4* x4 = reinterpret_cast<const float4*>(x + h);
+  int i = tid;
+  for (; i + 768 < n4; i += 1024) {
+    const float4 v0 = x4[i], v1 = x4[i + 256], v2 = x4[i + 512], v3 = x4[i + 768];
+    // one rescale per 16 values
+    const float mx = fmaxf(fmaxf(fmaxf(fmaxf(v0.x, v0.y), fmaxf(v0.z, v0.w)),
+                                 fmaxf(fmaxf(v1.x, v1.y), fmaxf(v1.z, v1.w))),
+                           fmaxf(fmaxf(fmaxf(v2.x, v2.y), fmaxf(v2.z, v2.w)),
+                                 fmaxf(fmaxf(v3.x, v3.y), fmaxf(v3.z, v3.w))));
+    const float mn = fmaxf(m, mx);
+    s *= __expf(m - mn);  // m = -inf on the first chunk: 0 * 0
+    m = mn;
+    s += (__expf(v0.x - m) + __expf(v0.y - m) + __expf(v0.z - m) + __expf(v0.w - m)) +
+         (__expf(v1.x - m) + __expf(v1.y - m) + __expf(v1.z - m) + __expf(v1.w - m)) +
+         (__expf(v2.x - m) + __expf(v2.y - m) + __expf(v2.z - m) + __expf(v2.w - m)) +
+         (__expf(v3.x - m) + __expf(v3.y - m) + __expf(v3.z - m) + __expf(v3.w - m));
+  }
+  for (; i < n4; i += 256) lse_acc4(m, s, x4[i]);
+  for (int v = h + 4 * n4 + tid; v < V; v += 256) lse_acc1(m, s, x[v]);
+  float M = wave_max(m);
+  float tot = wave_sum(m == neg_inf() ? 0.f : s * __expf(m - M));
+  if (lane == 0) { red_m[w] = M; red_s[w] = tot; }
+  __syncthreads();
+  M = fmaxf(fmaxf(red_m[0], red_m[1]), fmaxf(red_m[2], red_m[3]));
+  tot = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) tot += red_m[q] == neg_inf() ? 0.f : red_s[q] * __expf(red_m[q] - M);
+  const float lse = M + __logf(tot);
+  if (tid == 0) lse_out[row] = lse;
+  const int L = min(label_lens[b], (Spad - 1) / 2);
+  const int S = 2 * L + 1;
+  const int32_t* lab = labels + offs[b];
+  float* e = emit + row * Spad;
+  for (int st_ = tid; st_ < Spad; st_ += 256) {
+    float v = neg_inf();
+    if (st_ < S) {
+      int c = (st_ & 1) ? lab[st_ >> 1] : blank;
+      c = c < 0 ? 0 : (c >= V ? V - 1 : c);
+      v = (x[c] - lse) * kLog2e;
     }
     e[st_] = v;
   }
@@ -161,23 +259,46 @@ __device__ __forceinline__ float from_upper_lane(float x) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x130, 0xf, 0xf, false));
 }
 
-// Two waves per utterance (blockIdx.y: 0 = alpha, 1 = beta).  Lane l owns
-// lattice states s = l*K + k.
+// log2(2^a + 2^b + 2^c): the largest term is 2^0 = 1 after the shift, so two
+// exponentials and one logarithm (max3 / med3 / min3 order the triple).
+__device__ __forceinline__ float lse3_b2(float a, float b, float c) {
+  const float m = fmaxf(fmaxf(a, b), c);
+  const float md = __builtin_amdgcn_fmed3f(a, b, c);
+  const float lo = fminf(fminf(a, b), c);
+  const float r = m + lg2(1.f + ex2(md - m) + ex2(lo - m));
+  return (m == neg_inf()) ? m : r;
+}
+__device__ __forceinline__ float lse2_b2(float a, float b) {
+  const float m = fmaxf(a, b), lo = fminf(a, b);
+  const float r = m + lg2(1.f + ex2(lo - m));
+  return (m == neg_inf()) ? m : r;
+}
+
+// One work-group of two waves per (utterance, direction) (blockIdx.y: 0 =
+// alpha, 1 = beta).  Wave 0 runs the lattice: lane l owns states s = l*K + k,
+// neighbours come through DPP wave shifts, and it issues no global load inside
+// its loop (only the alpha / beta row stores), so it never waits on memory.
+// Wave 1 is the loader: it streams the emission rows of the lattice's visit
+// order into a two-chunk LDS ring (chunk c+1 written while the lattice
+// consumes chunk c, chunk c+2 already in flight in its registers).  A single
+// wave doing both stalled one memory latency per step (the waitcnt of a
+// prefetched row also covers the row stores issued after it).
 template <int K>
-__global__ void __launch_bounds__(64) ctc_lattice(int T, const int32_t* __restrict__ labels,
-                                                  const int32_t* __restrict__ label_lens,
-                                                  const int32_t* __restrict__ act_lens,
-                                                  const int32_t* __restrict__ offs, int blank,
-                                                  int zero_infinity, const float* __restrict__ emit,
-                                                  float* __restrict__ alpha,
-                                                  float* __restrict__ beta,
-                                                  float* __restrict__ logp_out,
-                                                  float* __restrict__ costs) {
+__global__ void __launch_bounds__(128) ctc_lattice(int T, const int32_t* __restrict__ labels,
+                                                   const int32_t* __restrict__ label_lens,
+                                                   const int32_t* __restrict__ act_lens,
+                                                   const int32_t* __restrict__ offs, int blank,
+                                                   int zero_infinity, const float* __restrict__ emit,
+                                                   float* __restrict__ alpha,
+                                                   float* __restrict__ beta,
+                                                   float* __restrict__ logp_out,
+                                                   float* __restrict__ costs) {
   constexpr int Spad = 64 * K;
-  constexpr int D = 4;  // emission prefetch distance (steps)
+  constexpr int C = K <= 4 ? 16 : (K == 8 ? 8 : 4);  // rows per chunk (LDS ring 2*C*Spad*4 B)
+  __shared__ __attribute__((aligned(16))) float ring[2][C][Spad];
   const int b = blockIdx.x;
   const bool is_beta = blockIdx.y == 1;
-  const int lane = threadIdx.x;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int Tb = min(act_lens[b], T);
   const int L = min(label_lens[b], (Spad - 1) / 2);
   const int S = 2 * L + 1;
@@ -185,10 +306,47 @@ __global__ void __launch_bounds__(64) ctc_lattice(int T, const int32_t* __restri
   const float NEG = neg_inf();
 
   if (Tb <= 0) {
-    if (lane == 0 && !is_beta) {
+    if (threadIdx.x == 0 && !is_beta) {
       bool feas = (L == 0);
       logp_out[b] = feas ? 0.f : NEG;
       costs[b] = feas ? 0.f : (zero_infinity ? 0.f : __builtin_huge_valf());
+    }
+    return;
+  }
+  const int N = Tb - 1;               // lattice steps after the initial row
+  const int nch = (N + C - 1) / C;
+  // row of the n-th step in visit order (clamped: the loader's overrun rows are harmless)
+  auto row_of = [&](int n) {
+    n = min(n, N - 1);
+    return is_beta ? Tb - 2 - n : 1 + n;
+  };
+  const float* E = emit + (size_t)b * T * Spad + lane * K;
+
+  if (wave == 1) {
+    // ---------------- loader ----------------
+    float r[C][K];
+    if (nch > 0) {
+#pragma unroll
+      for (int j = 0; j < C; ++j) load_k<K>(r[j], E + (size_t)row_of(j) * Spad);
+#pragma unroll
+      for (int j = 0; j < C; ++j) store_k<K>(&ring[0][j][lane * K], r[j]);
+      if (nch > 1) {
+#pragma unroll
+        for (int j = 0; j < C; ++j) load_k<K>(r[j], E + (size_t)row_of(C + j) * Spad);
+      }
+    }
+    __syncthreads();
+    for (int c = 0; c < nch; ++c) {
+      if (c + 1 < nch) {
+#pragma unroll
+        for (int j = 0; j < C; ++j) store_k<K>(&ring[(c + 1) & 1][j][lane * K], r[j]);
+        if (c + 2 < nch) {
+#pragma unroll
+          for (int j = 0; j < C; ++j)
+            load_k<K>(r[j], E + (size_t)row_of((c + 2) * C + j) * Spad);
+        }
+      }
+      __syncthreads();
     }
     return;
   }
@@ -196,8 +354,6 @@ __global__ void __launch_bounds__(64) ctc_lattice(int T, const int32_t* __restri
   bool valid[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) valid[k] = lane * K + k < S;
-  const float* E = emit + (size_t)b * T * Spad + lane * K;
-  float eb[D][K];
 
   if (!is_beta) {
     // ---------------- alpha ----------------
@@ -220,32 +376,35 @@ __global__ void __launch_bounds__(64) ctc_lattice(int T, const int32_t* __restri
       }
       store_k<K>(A, a);
     }
+    __syncthreads();
+    for (int c = 0; c < nch; ++c) {
 #pragma unroll
-    for (int j = 0; j < D; ++j) load_k<K>(eb[j], E + (size_t)min(1 + j, T - 1) * Spad);
-
-    for (int t0 = 1; t0 < Tb; t0 += D) {
-#pragma unroll
-      for (int j = 0; j < D; ++j) {
-        const int t = t0 + j;
-        if (t < Tb) {
+      for (int j = 0; j < C; ++j) {
+        const int n = c * C + j;
+        if (n < N) {
+          float e[K];
+          load_k<K>(e, &ring[c & 1][j][lane * K]);
           float p1 = from_lower_lane(a[K - 1]);
           float p2 = (K >= 2) ? from_lower_lane(a[K >= 2 ? K - 2 : 0]) : from_lower_lane(p1);
           if (lane == 0) { p1 = NEG; p2 = NEG; }
           if (K == 1 && lane == 1) p2 = NEG;
-          float n[K];
+          float nx[K];
 #pragma unroll
           for (int k = 0; k < K; ++k) {
             const float a1 = (k >= 1) ? a[k >= 1 ? k - 1 : 0] : p1;
             const float a2 = (k >= 2) ? a[k >= 2 ? k - 2 : 0] : ((k == 1) ? p1 : p2);
-            const float v = lse3(a[k], a1, skip[k] ? a2 : NEG) + eb[j][k];
-            n[k] = valid[k] ? v : NEG;
+            // K even: state parity = k parity, and blank (even) states never skip
+            const float v = ((K % 2 == 0) && (k % 2 == 0) ? lse2_b2(a[k], a1)
+                                                          : lse3_b2(a[k], a1, skip[k] ? a2 : NEG)) +
+                            e[k];
+            nx[k] = valid[k] ? v : NEG;
           }
 #pragma unroll
-          for (int k = 0; k < K; ++k) a[k] = n[k];
-          store_k<K>(A + (size_t)t * Spad, a);
-          load_k<K>(eb[j], E + (size_t)min(t + D, T - 1) * Spad);
+          for (int k = 0; k < K; ++k) a[k] = nx[k];
+          store_k<K>(A + (size_t)(1 + n) * Spad, a);
         }
       }
+      __syncthreads();
     }
 
     // log P from the last two states at t = Tb-1
@@ -253,14 +412,14 @@ __global__ void __launch_bounds__(64) ctc_lattice(int T, const int32_t* __restri
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const int s = lane * K + k;
-      if (s == S - 1 || s == S - 2) part = lse2(part, a[k]);
+      if (s == S - 1 || s == S - 2) part = lse2_b2(part, a[k]);
     }
     float mx = wave_max(part);
-    float sm = (mx == NEG) ? 0.f : wave_sum(__expf(part - mx));
-    const float logP = (mx == NEG) ? NEG : mx + __logf(sm);
+    float sm = (mx == NEG) ? 0.f : wave_sum(ex2(part - mx));
+    const float logP = (mx == NEG) ? NEG : mx + lg2(sm);  // log2 units
     if (lane == 0) {
       logp_out[b] = logP;
-      costs[b] = (logP == NEG) ? (zero_infinity ? 0.f : __builtin_huge_valf()) : -logP;
+      costs[b] = (logP == NEG) ? (zero_infinity ? 0.f : __builtin_huge_valf()) : -logP * kLn2;
     }
     return;
   }
@@ -285,72 +444,147 @@ __global__ void __launch_bounds__(64) ctc_lattice(int T, const int32_t* __restri
     }
     store_k<K>(Bt + (size_t)(Tb - 1) * Spad, be);
   }
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
 #pragma unroll
-  for (int j = 0; j < D; ++j) load_k<K>(eb[j], E + (size_t)max(Tb - 2 - j, 0) * Spad);
-  for (int t0 = Tb - 2; t0 >= 0; t0 -= D) {
-#pragma unroll
-    for (int j = 0; j < D; ++j) {
-      const int t = t0 - j;
-      if (t >= 0) {
+    for (int j = 0; j < C; ++j) {
+      const int n = c * C + j;
+      if (n < N) {
+        float e[K];
+        load_k<K>(e, &ring[c & 1][j][lane * K]);
         float n1 = from_upper_lane(be[0]);
         float n2 = (K >= 2) ? from_upper_lane(be[K >= 2 ? 1 : 0]) : from_upper_lane(n1);
         if (lane == 63) { n1 = NEG; n2 = NEG; }
         if (K == 1 && lane == 62) n2 = NEG;
-        float n[K];
+        float nx[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
           const float b1 = (k < K - 1) ? be[k < K - 1 ? k + 1 : 0] : n1;
           const float b2 = (k < K - 2) ? be[k < K - 2 ? k + 2 : 0] : ((k == K - 2) ? n1 : n2);
-          const float v = lse3(be[k], b1, skipf[k] ? b2 : NEG) + eb[j][k];
-          n[k] = valid[k] ? v : NEG;
+          const float v = ((K % 2 == 0) && (k % 2 == 0) ? lse2_b2(be[k], b1)
+                                                        : lse3_b2(be[k], b1, skipf[k] ? b2 : NEG)) +
+                          e[k];
+          nx[k] = valid[k] ? v : NEG;
         }
 #pragma unroll
-        for (int k = 0; k < K; ++k) be[k] = n[k];
-        store_k<K>(Bt + (size_t)t * Spad, be);
-        load_k<K>(eb[j], E + (size_t)max(t - D, 0) * Spad);
+        for (int k = 0; k < K; ++k) be[k] = nx[k];
+        store_k<K>(Bt + (size_t)(Tb - 2 - n) * Spad, be);
       }
     }
+    __syncthreads();
   }
 }
 
 // grad = (softmax - occupancy) * scale, one row (b,t) per block.
-__global__ void ctc_grad(const float* __restrict__ acts, long long st, long long sb, int T, int V,
-                         const int32_t* __restrict__ labels, const int32_t* __restrict__ label_lens,
-                         const int32_t* __restrict__ act_lens, const int32_t* __restrict__ offs,
-                         int blank, int Spad, const float* __restrict__ lse,
-                         const float* __restrict__ emit, const float* __restrict__ alpha,
-                         const float* __restrict__ beta, const float* __restrict__ logp,
-                         const float* __restrict__ grad_scale, float scale_mul,
-                         float* __restrict__ grads,
-                         long long gst, long long gsb) {
-  extern __shared__ __attribute__((aligned(16))) float acc[];
+//   kTable (V <= 256): occupancies summed per class in a V-entry LDS table.
+//   otherwise, no V-sized table: (1) the S state occupancies go to LDS; (2) the
+//   first state of each distinct class sums, in state order, the occupancies
+//   of every state of its class (repeated labels and all blanks fold
+//   together); (3) the row is streamed once, softmax * scale written with 16-B
+//   accesses; (4) after the barrier the class representatives overwrite their
+//   own columns with (softmax - occupancy) * scale.
+template <bool kTable>
+__global__ void __launch_bounds__(256) ctc_grad(
+    const float* __restrict__ acts, long long st, long long sb, int T, int V,
+    const int32_t* __restrict__ labels, const int32_t* __restrict__ label_lens,
+    const int32_t* __restrict__ act_lens, const int32_t* __restrict__ offs, int blank, int Spad,
+    const float* __restrict__ lse, const float* __restrict__ emit,
+    const float* __restrict__ alpha, const float* __restrict__ beta,
+    const float* __restrict__ logp, const float* __restrict__ grad_scale, float scale_mul,
+    float* __restrict__ grads, long long gst, long long gsb) {
+  extern __shared__ __attribute__((aligned(16))) float occ[];  // [V] (kTable) or [Spad]
   const long long row = blockIdx.x;
   const int b = (int)(row / T), t = (int)(row % T);
   float* g = grads + (long long)t * gst + (long long)b * gsb;
+  const float* x = acts + (long long)t * st + (long long)b * sb;
+  const int tid = threadIdx.x, nth = blockDim.x;
   const int Tb = act_lens[b];
   const float lp = logp[b];
   if (t >= Tb || lp == neg_inf()) {
-    for (int v = threadIdx.x; v < V; v += blockDim.x) g[v] = 0.f;
+    for (int v = tid; v < V; v += nth) g[v] = 0.f;
     return;
   }
   const float scale = (grad_scale ? grad_scale[0] : 1.0f) * scale_mul;
-  for (int v = threadIdx.x; v < V; v += blockDim.x) acc[v] = 0.f;
-  __syncthreads();
+  const float z = lse[row];
   const int L = min(label_lens[b], (Spad - 1) / 2);
   const int S = 2 * L + 1;
   const int32_t* lab = labels + offs[b];
+  auto cls = [&](int s_) {
+    int c = (s_ & 1) ? lab[s_ >> 1] : blank;
+    return c < 0 ? 0 : (c >= V ? V - 1 : c);
+  };
   const float* al = alpha + row * Spad;
   const float* bt = beta + row * Spad;
   const float* em = emit + row * Spad;
-  for (int s = threadIdx.x; s < S; s += blockDim.x) {
-    int c = (s & 1) ? lab[s >> 1] : blank;
-    c = c < 0 ? 0 : (c >= V ? V - 1 : c);
-    atomicAdd(&acc[c], __expf(al[s] + bt[s] - em[s] - lp));
+
+  if constexpr (kTable) {
+    for (int v = tid; v < V; v += nth) occ[v] = 0.f;
+    __syncthreads();
+    for (int s_ = tid; s_ < S; s_ += nth) atomicAdd(&occ[cls(s_)], ex2(al[s_] + bt[s_] - em[s_] - lp));
+    __syncthreads();
+    for (int v = tid; v < V; v += nth) g[v] = (__expf(x[v] - z) - occ[v]) * scale;
+    return;
+  } else {
+    for (int s_ = tid; s_ < S; s_ += nth) occ[s_] = ex2(al[s_] + bt[s_] - em[s_] - lp);
+    __syncthreads();
+    // representatives (at most 4 states per thread: the host keeps Spad <= 4 * nth)
+    int rep_c[4];
+    float rep_v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      rep_c[r] = -1;
+      rep_v[r] = 0.f;
+      const int s_ = tid + r * nth;
+      if (s_ >= S) continue;
+      const int c = cls(s_);
+      bool first;
+      if ((s_ & 1) == 0) {
+        first = s_ == 0;
+      } else {
+        first = c != blank;
+        for (int q = 1; q < s_ && first; q += 2) first = cls(q) != c;
+      }
+      if (!first) continue;
+      float acc = 0.f;
+      for (int q = 0; q < S; ++q)
+        if (cls(q) == c) acc += occ[q];
+      rep_c[r] = c;
+      rep_v[r] = acc;
+    }
+    // stream the row: g = softmax * scale
+    if ((((size_t)x ^ (size_t)g) & 15) == 0) {
+      const int h = min(head_elems(x), V);
+      if (tid < h) g[tid] = __expf(x[tid] - z) * scale;
+      const int n4 = (V - h) >> 2;
+      const float4* x4 = reinterpret_cast<const float4*>(x + h);
+      float4* g4 = reinterpret_cast<float4*>(g + h);
+      int i = tid;
+      for (; i + 3 * nth < n4; i += 4 * nth) {
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = x4[i + u * nth];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          g4[i + u * nth] = make_float4(__expf(v[u].x - z) * scale, __expf(v[u].y - z) * scale,
+                                        __expf(v[u].z - z) * scale, __expf(v[u].w - z) * scale);
+      }
+      for (; i < n4; i += nth) {
+        const float4 v = x4[i];
+        g4[i] = make_float4(__expf(v.x - z) * scale, __expf(v.y - z) * scale,
+                            __expf(v.z - z) * scale, __expf(v.w - z) * scale);
+      }
+      for (int v = h + 4 * n4 + tid; v < V; v += nth) g[v] = __expf(x[v] - z) * scale;
+    } else {
+      for (int v = tid; v < V; v += nth) g[v] = __expf(x[v] - z) * scale;
+    }
+    // the streamed stores are acknowledged (s_waitcnt vmcnt(0): __syncthreads
+    // alone only waits for LDS) before any representative overwrites a column
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (rep_c[r] >= 0) g[rep_c[r]] = (__expf(x[rep_c[r]] - z) - rep_v[r]) * scale;
   }
-  __syncthreads();
-  const float* x = acts + (long long)t * st + (long long)b * sb;
-  const float z = lse[row];
-  for (int v = threadIdx.x; v < V; v += blockDim.x) g[v] = (__expf(x[v] - z) - acc[v]) * scale;
 }
 
 __global__ void ctc_loss_reduce(const float* __restrict__ costs, int B, float scale,
@@ -413,12 +647,17 @@ extern "C" int asr_ctc_forward(const float* acts, long long stride_t, long long 
   const long long rows = (long long)B * T;
   // algorithmic HBM bytes of the forward: the activations read once
   const int pslot = prof_begin_launch(ASR_PROF_CTC_FWD, s, 4.0 * (double)V * (double)rows);
-  hipLaunchKernelGGL(ctc_emit, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, acts, stride_t,
-                     stride_b, T, B, V, labels_flat, label_lens, act_lens, ws.offs, blank, Spad,
-                     ws.lse, ws.emit);
+  if (V > 1024)
+    hipLaunchKernelGGL(ctc_emit_wide, dim3((unsigned)rows), dim3(256), 0, s, acts, stride_t,
+                       stride_b, T, V, labels_flat, label_lens, act_lens, ws.offs, blank, Spad,
+                       ws.lse, ws.emit);
+  else
+    hipLaunchKernelGGL(ctc_emit, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, acts, stride_t,
+                       stride_b, T, B, V, labels_flat, label_lens, act_lens, ws.offs, blank, Spad,
+                       ws.lse, ws.emit);
   ASR_LAUNCH_CHECK();
 #define ASR_CTC_LAT(KK)                                                                        \
-  hipLaunchKernelGGL(ctc_lattice<KK>, dim3(B, 2), dim3(64), 0, s, T, labels_flat, label_lens,  \
+  hipLaunchKernelGGL(ctc_lattice<KK>, dim3(B, 2), dim3(128), 0, s, T, labels_flat, label_lens,  \
                      act_lens, ws.offs, blank, zero_infinity, ws.emit, ws.alpha, ws.beta,      \
                      ws.logp, costs)
   switch (K) {
@@ -450,19 +689,24 @@ extern "C" int asr_ctc_backward(const float* acts, long long stride_t, long long
                         workspace, ws_bytes);
   if (rc) return rc;
   ASR_REQUIRE(grads, ASR_ERR_ARG, "ctc: grads is null");
-  ASR_REQUIRE((size_t)V * 4 <= 160 * 1024, ASR_ERR_UNSUPPORTED, "ctc: V=%d too large", V);
   hipStream_t s = (hipStream_t)stream;
   CtcWs ws;
   ws_layout(T, B, max_label_len, &ws, (char*)workspace);
   const int Spad = 64 * pick_k(max_label_len);
-  const int threads = V <= 256 ? 64 : 256;
+  const bool table = V <= 256;
+  const int threads = table ? 64 : 256;  // compact mode: Spad <= 1024 = 4 * threads
   // algorithmic HBM bytes: activations read + gradient written
   const int pslot = prof_begin_launch(ASR_PROF_CTC_GRAD, s, 8.0 * (double)V * B * T);
-  hipLaunchKernelGGL(ctc_grad, dim3((unsigned)((long long)B * T)), dim3(threads), V * sizeof(float),
-                     s, acts, stride_t, stride_b, T, V, labels_flat, label_lens, act_lens, ws.offs,
-                     blank, Spad, ws.lse, ws.emit, ws.alpha, ws.beta, ws.logp, grad_scale, scale,
-                     grads, gstride_t,
-                     gstride_b);
+  if (table)
+    hipLaunchKernelGGL(ctc_grad<true>, dim3((unsigned)((long long)B * T)), dim3(threads),
+                       V * sizeof(float), s, acts, stride_t, stride_b, T, V, labels_flat,
+                       label_lens, act_lens, ws.offs, blank, Spad, ws.lse, ws.emit, ws.alpha,
+                       ws.beta, ws.logp, grad_scale, scale, grads, gstride_t, gstride_b);
+  else
+    hipLaunchKernelGGL(ctc_grad<false>, dim3((unsigned)((long long)B * T)), dim3(threads),
+                       Spad * sizeof(float), s, acts, stride_t, stride_b, T, V, labels_flat,
+                       label_lens, act_lens, ws.offs, blank, Spad, ws.lse, ws.emit, ws.alpha,
+                       ws.beta, ws.logp, grad_scale, scale, grads, gstride_t, gstride_b);
   ASR_LAUNCH_CHECK();
   prof_end_launch(ASR_PROF_CTC_GRAD, pslot, s);
   return ASR_OK;

@@ -77,3 +77,41 @@ def test_ctc_deterministic(cuda_dev):
     a = _run(acts, labels, lens, [64, 60, 50, 40], cuda_dev)
     b = _run(acts, labels, lens, [64, 60, 50, 40], cuda_dev)
     np.testing.assert_array_equal(a[1], b[1])
+
+
+def test_ctc_word_vocab_compact_grad(cuda_dev):
+    """V = 10001 (word CTC head): rows start at every 4-B phase of a 16-B
+    granule (40004-B rows), the gradient takes the compact per-class path
+    (no V-sized LDS table), repeated labels fold into one class, the last
+    class index is used; bit-identical across runs."""
+    rng = np.random.RandomState(11)
+    B, T, V = 3, 40, 10001
+    act_lens = np.array([40, 37, 21])
+    label_lens = np.array([12, 9, 6])
+    labels = np.concatenate([rng.randint(1, V, l) for l in label_lens])
+    labels[2] = labels[3] = labels[5]          # repeats (adjacent and not)
+    labels[13] = V - 1
+    acts = (rng.randn(B, T, V) * 2).astype(np.float32)
+    _, costs, grads = _run(acts, labels, label_lens, act_lens, cuda_dev)
+    c_ref, g_ref = ctc_ref.ctc_batch(acts, labels, label_lens, act_lens, time_major=False)
+    np.testing.assert_allclose(costs, c_ref, rtol=1e-4)
+    np.testing.assert_allclose(grads, g_ref, rtol=1e-3, atol=2e-5)
+    again = _run(acts, labels, label_lens, act_lens, cuda_dev)
+    np.testing.assert_array_equal(grads, again[2])
+
+
+def test_ctc_compact_grad_long_labels_k16(cuda_dev):
+    """V = 300 > 256 with S = 801 lattice states: 16 states per lane in the
+    lattice and four states per thread in the compact gradient."""
+    rng = np.random.RandomState(12)
+    B, T, V = 2, 500, 300
+    act_lens = np.array([500, 460])
+    label_lens = np.array([400, 300])
+    labels = np.concatenate([rng.randint(1, V, l) for l in label_lens])
+    acts = rng.randn(B, T, V).astype(np.float32)
+    _, costs, grads = _run(acts, labels, label_lens, act_lens, cuda_dev)
+    c_ref, g_ref = ctc_ref.ctc_batch(acts, labels, label_lens, act_lens, time_major=False)
+    np.testing.assert_allclose(costs, c_ref, rtol=1e-4)
+    # costs ~2600 nats: alpha + beta - log P reaches ~5e3 in magnitude, whose f32
+    # spacing (4.9e-4) bounds the occupancy's relative accuracy at ~1e-3
+    np.testing.assert_allclose(grads, g_ref, rtol=2e-3, atol=2e-4)
