@@ -603,6 +603,201 @@ __global__ void __launch_bounds__(NT) gemm_bf16_fast(Params P) {
   store_acc(pr, acc, tm, tn, wr, wc, lane, split, nsplit);
 }
 
+// ---------------------------------------------------------------------------
+// 256 x 256 tiles for K-major x K-major products (the weight gradients
+// dW = dG^T X, K = B*T): four waves, each a 128 x 128 sub-tile (8 x 8 MFMA
+// accumulators, 256 registers, in AGPRs), so each wave reads half the LDS
+// bytes per MFMA of the 128 x 128 kernel (whose 64 x 64 wave tiles put the
+// LDS read rate at the MFMA rate) and each work-group streams half the
+// L2 bytes per flop.  Same staging scheme: swizzled K-mode tiles (here 512-B
+// k-rows) filled by buffer->LDS DMA, hardware-transpose fragment reads; a
+// four-stage ring of 32-deep k-tiles (128 KB: one work-group per CU, three
+// k-tiles in flight), one barrier per k-tile.
+// ---------------------------------------------------------------------------
+constexpr int BT2 = 256;
+constexpr int BK2 = 32;                 // k-tile depth
+constexpr int NST2 = 4;                 // LDS ring stages (3 k-tiles in flight)
+constexpr int FTILE2 = BT2 * BK2 * 2;   // 16 KB per operand tile
+
+__device__ __forceinline__ void stage_tile_k256(const Operand& op, __amdgpu_buffer_rsrc_t rs,
+                                                char* lds_tile, int tile0, int k0, int kend,
+                                                int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < BK2 / 8; ++i) {
+    const int blk = wave * (BK2 / 8) + i;  // 1 KB = two 512-B k-rows
+    const int kr = blk * 2 + (lane >> 5);
+    const int j = lane & 31;               // 16-B chunk of the k-row
+    const int c = 2 * ((j >> 1) ^ swz_h(kr)) + (j & 1);
+    unsigned voff = OOB_OFF;
+    int k = k0 + kr, col = tile0 + 8 * c;
+    if (k < kend) {
+      tap_adjust(op, k, col);
+      const long long off = row_off_np(op.map, k);
+      if (off >= 0) voff = (unsigned)((off + col) * 2);
+    }
+    const unsigned lds_addr = (unsigned)(uintptr_t)(lds_void_t*)(lds_tile + blk * 1024);
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(rs), "s"(lds_addr)
+        : "memory");
+  }
+}
+
+__device__ __forceinline__ bf16x8 frag_k256(const char* lds_tile, int rb, int kk, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int G = rb >> 4;
+  const int k0 = 32 * kk + 8 * g + q, k1 = k0 + 4;
+  const char* a0 = lds_tile + k0 * 512 + ((G ^ swz_h(k0)) << 5) + 8 * p;
+  const char* a1 = lds_tile + k1 * 512 + ((G ^ swz_h(k1)) << 5) + 8 * p;
+  const v4s_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t*)a0);
+  const v4s_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t*)a1);
+  typedef __attribute__((ext_vector_type(8))) short v8s_t;
+  const v8s_t v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1)))
+gemm_bf16_kk256(Params P) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // 2 stages x (A, B) tiles
+
+  const int zb = blockIdx.z / P.nprob, zp = blockIdx.z % P.nprob;
+  Problem pr = P.p[zp];
+  if (zb >= pr.batch) return;
+  if (zb > 0) {
+    pr.a.map.base = (const char*)pr.a.map.base + zb * pr.sA * 2;
+    pr.b.map.base = (const char*)pr.b.map.base + zb * pr.sB * 2;
+    pr.a.bytes -= zb * pr.sA * 2;
+    pr.b.bytes -= zb * pr.sB * 2;
+    pr.c.base = (const char*)pr.c.base + zb * pr.sC * 4;
+  }
+  const int gm = (pr.M + BT2 - 1) / BT2, gn = (pr.N + BT2 - 1) / BT2;
+  const int nwg = gm * gn;
+  const int nsplit = pr.ksplit > 1 ? pr.ksplit : 1;
+  const int ntot = nwg * nsplit;
+  int id = blockIdx.x;
+  if (id >= ntot) return;
+  {
+    const int q = ntot / 8, r = ntot % 8, x = id % 8;
+    id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + id / 8;
+  }
+  const int split = id / nwg;
+  id -= split * nwg;
+  // column-minor walk inside groups of 4 row tiles (an XCD's resident tiles share operands)
+  int tm, tn;
+  {
+    const int per = 4 * gn;
+    const int g = id / per, r = id - g * per;
+    const int m0 = g * 4;
+    const int gs = min(4, gm - m0);
+    tm = (m0 + r % gs) * BT2;
+    tn = (r / gs) * BT2;
+  }
+  const int kbeg = nsplit > 1 ? split * pr.kchunk : 0;
+  const int kend = nsplit > 1 ? min(pr.K, kbeg + pr.kchunk) : pr.K;
+
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = (w >> 1) * 128, wc = (w & 1) * 128;
+  // descriptors built from wave-uniform values (readfirstlane) so they live in SGPRs
+  auto uni_ptr = [](const void* p) {
+    const unsigned long long v = (unsigned long long)p;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+    return (void*)(((unsigned long long)hi << 32) | lo);
+  };
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      uni_ptr(pr.a.map.base), 0, __builtin_amdgcn_readfirstlane((int)pr.a.bytes), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+      uni_ptr(pr.b.map.base), 0, __builtin_amdgcn_readfirstlane((int)pr.b.bytes), 0x00020000);
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // Ring of NST2 stages, k-tiles issued NST2 - 1 ahead; iteration kt: counted
+  // wait for tile kt (each tile is 2 * BK2 / 8 DMA instructions per thread),
+  // barrier, refill the stage read in iteration kt - 1, compute tile kt.
+  constexpr int PER = 2 * (BK2 / 8);
+  const int nk = (kend - kbeg + BK2 - 1) / BK2;
+#pragma unroll
+  for (int j = 0; j < NST2 - 1; ++j) {
+    if (j < nk) {
+      char* st = smem + j * 2 * FTILE2;
+      stage_tile_k256(pr.a, ra, st, tm, kbeg + j * BK2, kend, w, lane);
+      stage_tile_k256(pr.b, rb, st + FTILE2, tn, kbeg + j * BK2, kend, w, lane);
+    }
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    const int after = min(NST2 - 2, nk - 1 - kt);
+    if (after >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
+    else if (after == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + NST2 - 1 < nk) {
+      char* st = smem + ((kt + NST2 - 1) % NST2) * 2 * FTILE2;
+      const int k0 = kbeg + (kt + NST2 - 1) * BK2;
+      stage_tile_k256(pr.a, ra, st, tm, k0, kend, w, lane);
+      stage_tile_k256(pr.b, rb, st + FTILE2, tn, k0, kend, w, lane);
+    }
+    const char* cur = smem + (kt % NST2) * 2 * FTILE2;
+#pragma unroll
+    for (int kk = 0; kk < BK2 / 32; ++kk) {
+      bf16x8 fb[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) fb[j] = frag_k256(cur + FTILE2, wc + 16 * j, kk, lane);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const bf16x8 fa = frag_k256(cur, wr + 16 * i, kk, lane);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = mfma_bf16(fa, fb[j], acc[i][j]);
+      }
+    }
+  }
+
+  if (nsplit > 1) {  // raw partial sums into this split's slab; splitk_reduce finishes
+    float* slab = pr.slab + (long long)split * pr.M * pr.N;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = tm + wr + i * 16 + 4 * (lane >> 4) + r;
+        if (m >= pr.M) continue;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int n = tn + wc + j * 16 + (lane & 15);
+          if (n < pr.N) slab[(long long)m * pr.N + n] = acc[i][j][r];
+        }
+      }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = tm + wr + i * 16 + 4 * (lane >> 4) + r;
+      if (m >= pr.M) continue;
+      const long long off = row_off(pr.c, m);
+      if (off < 0) continue;
+      float* crow = (float*)pr.c.base + off;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int n = tn + wc + j * 16 + (lane & 15);
+        if (n >= pr.N) continue;
+        float v = pr.alpha * acc[i][j][r];
+        if (pr.bias) v += pr.bias[n];
+        if (pr.bias2) v += pr.bias2[n];
+        if (pr.beta != 0.f) v += pr.beta * crow[n];
+        crow[n] = v;
+      }
+    }
+  }
+}
+
 // Split-K finish: C(m,n) = alpha * sum_s slab[s][m][n] (fixed order s = 0..) +
 // bias + bias2 + beta * C, through C's row map.
 __global__ void splitk_reduce(const float* __restrict__ slab, int ksplit, int M, int N, RowMap c,
@@ -779,6 +974,20 @@ int fast_modes(const asr_gemm_t* g, const Params& P) {
   return modes;
 }
 
+// K-major x K-major problems with both output extents >= 256 take the 256 x 256
+// kernel (ASR_GEMM_KK256=0 keeps them on the 128 x 128 kernel).
+bool kk256_ok(const asr_gemm_t* g, int nprob) {
+  static int en = -1;
+  if (en < 0) {
+    const char* e = getenv("ASR_GEMM_KK256");
+    en = (e && e[0] == '0') ? 0 : 1;
+  }
+  if (!en) return false;
+  for (int i = 0; i < nprob; ++i)
+    if (g[i].M < BT2 || g[i].N < BT2) return false;
+  return true;
+}
+
 int gemm_launch_own(const asr_gemm_t* problems, int nprob, int compute_dtype, void* workspace,
                     size_t ws_bytes, void* stream) {
   SplitPlan sp{};
@@ -829,7 +1038,34 @@ int gemm_launch_own(const asr_gemm_t* problems, int nprob, int compute_dtype, vo
     flops += 2.0 * problems[i].M * problems[i].N * problems[i].K * P.p[i].batch;
   const int slot = prof_begin_launch(ASR_PROF_GEMM, s, flops);
   const int fast = compute_dtype == ASR_DT_BF16 ? fast_modes(problems, P) : -1;
-  if (fast >= 0) {
+  if (fast == 3 && kk256_ok(problems, nprob)) {
+    // 256 x 256 tiles; the split never exceeds the workspace plan's (128 x 128) split
+    int maxwg2 = 0;
+    for (int i = 0; i < nprob; ++i) {
+      Problem& p = P.p[i];
+      const int tiles2 = ceil_div(p.M, BT2) * ceil_div(p.N, BT2);
+      int ks = 1;
+      if (p.ksplit > 1) {
+        ks = min(p.ksplit, max(1, ceil_div(256, tiles2)));
+        const int kc = ceil_div(ceil_div(p.K, ks), BK2) * BK2;
+        ks = ceil_div(p.K, kc);
+        p.kchunk = kc;
+      }
+      if (ks <= 1) { ks = 1; p.kchunk = p.K; }
+      p.ksplit = ks;
+      maxwg2 = max(maxwg2, tiles2 * ks);
+    }
+    static bool attr = false;
+    if (!attr) {
+      ASR_REQUIRE(hipFuncSetAttribute((const void*)gemm_bf16_kk256,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      NST2 * 2 * FTILE2) == hipSuccess,
+                  ASR_ERR_HIP, "gemm: cannot raise the LDS limit of the 256x256 kernel");
+      attr = true;
+    }
+    hipLaunchKernelGGL(gemm_bf16_kk256, dim3(maxwg2, 1, nprob * maxb), dim3(NT),
+                       (size_t)NST2 * 2 * FTILE2, s, P);
+  } else if (fast >= 0) {
     const int nst = fast_stages();
     const size_t lds = (size_t)nst * 2 * FTILE;
     switch (fast) {

@@ -132,3 +132,70 @@ def test_linear_bf16_staged_padded(cuda_dev):
         np.testing.assert_allclose(bd.grad.cpu().numpy(), dy.sum(0), rtol=1e-4, atol=1e-3)
     finally:
         ops.set_compute_dtype('fp32')
+
+
+@pytest.mark.parametrize('M,N,K', [(529, 389, 3000), (256, 256, 64), (300, 260, 200),
+                                    (1024, 512, 8000)])
+def test_kmajor_256_tiles_exact(M, N, K, cuda_dev):
+    """K-major x K-major products with M, N >= 256 take the 256 x 256 kernel
+    (gemm_bf16_kk256): ragged edges, a single k-tile, a K that is not a
+    multiple of the 64-deep k-tile, split-K chunks; alpha / beta / bias."""
+    ops = _ops()
+    ops.set_compute_dtype('bf16')
+    try:
+        rng = np.random.RandomState(M + N + K)
+        a = rng.randint(-3, 4, (K, M + 8)).astype(np.float32)     # stored [K][M(+pad)]
+        b = rng.randint(-3, 4, (K, N + 16)).astype(np.float32)
+        c0 = rng.randint(-4, 5, (M, N)).astype(np.float32)
+        bias = rng.randint(-8, 9, N).astype(np.float32)
+        ad = torch.from_numpy(a).to(torch.bfloat16).to(cuda_dev)
+        bd = torch.from_numpy(b).to(torch.bfloat16).to(cuda_dev)
+        C = torch.from_numpy(c0).to(cuda_dev)
+        bias_d = torch.from_numpy(bias).to(cuda_dev)
+        p = ops.gemm_problem(ops.operand(ad, 1, ops.rowmap(M + 8)),
+                             ops.operand(bd, 1, ops.rowmap(N + 16)), C, ops.rowmap(N), M, N, K,
+                             alpha=2.0, beta=1.0, bias=bias_d)
+        ops.run_gemm([p], cuda_dev)
+        torch.cuda.synchronize()
+        ref = 2.0 * (a[:, :M].T.astype(np.float64) @ b[:, :N]) + c0 + bias
+        np.testing.assert_array_equal(C.cpu().numpy(), ref)
+    finally:
+        ops.set_compute_dtype('fp32')
+
+
+def test_kmajor_256_tiles_two_problems_rowmapped(cuda_dev):
+    """The dW_hh launch shape: two problems side by side, the second reading
+    column offsets, the B operand through a shifted per-utterance row map
+    (h_{t-1}: t_add = -1, rows past the utterance read as zeros)."""
+    ops = _ops()
+    ops.set_compute_dtype('bf16')
+    try:
+        rng = np.random.RandomState(5)
+        Bu, T, H = 4, 700, 256
+        g = rng.randint(-3, 4, (Bu * T, 8 * H)).astype(np.float32)
+        y = rng.randint(-3, 4, (Bu * T, 2 * H)).astype(np.float32)
+        gd = torch.from_numpy(g).to(torch.bfloat16).to(cuda_dev)
+        yd = torch.from_numpy(y).to(torch.bfloat16).to(cuda_dev)
+        C = torch.zeros(2, 4 * H, H, device=cuda_dev)
+        R = ops.rowmap
+        hp_f = R(2 * H, stride_b=T * 2 * H, rows_per_b=T, t_add=-1, t_limit=T)
+        hp_r = R(2 * H, stride_b=T * 2 * H, rows_per_b=T, t_add=1, t_limit=T)
+        ops.run_gemm([
+            ops.gemm_problem(ops.operand(gd, 1, R(8 * H)), ops.operand(yd, 1, hp_f), C, R(H),
+                             4 * H, H, Bu * T, beta=1.0),
+            ops.gemm_problem(ops.operand(gd, 1, R(8 * H), offset=4 * H),
+                             ops.operand(yd, 1, hp_r, offset=H), C, R(H), 4 * H, H, Bu * T,
+                             beta=1.0, c_offset=4 * H * H),
+        ], cuda_dev)
+        torch.cuda.synchronize()
+        y3 = y.reshape(Bu, T, 2 * H).astype(np.float64)
+        hf = np.zeros_like(y3[:, :, :H]); hf[:, 1:] = y3[:, :-1, :H]
+        hr = np.zeros_like(y3[:, :, H:]); hr[:, :-1] = y3[:, 1:, H:]
+        g64 = g.astype(np.float64)
+        ref_f = g64[:, :4 * H].T @ hf.reshape(-1, H)
+        ref_r = g64[:, 4 * H:].T @ hr.reshape(-1, H)
+        got = C.cpu().numpy()
+        np.testing.assert_array_equal(got[0], ref_f)
+        np.testing.assert_array_equal(got[1], ref_r)
+    finally:
+        ops.set_compute_dtype('fp32')
