@@ -975,14 +975,13 @@ int fast_modes(const asr_gemm_t* g, const Params& P) {
 }
 
 // K-major x K-major problems with both output extents >= 256 take the 256 x 256
-// kernel (ASR_GEMM_KK256=0 keeps them on the 128 x 128 kernel).
+// kernel when ASR_GEMM_KK256=1 (read per launch).  Off by default: at the
+// 5x512 weight-gradient shapes it measured 511 vs 482 TF/s (tools/gemm_bench.py)
+// but the whole step did not move beyond noise, and the 4x320 / VGG configs
+// ran 0.2-0.5 ms/step slower with it (fewer work-groups per product).
 bool kk256_ok(const asr_gemm_t* g, int nprob) {
-  static int en = -1;
-  if (en < 0) {
-    const char* e = getenv("ASR_GEMM_KK256");
-    en = (e && e[0] == '0') ? 0 : 1;
-  }
-  if (!en) return false;
+  const char* e = getenv("ASR_GEMM_KK256");
+  if (!(e && e[0] == '1')) return false;
   for (int i = 0; i < nprob; ++i)
     if (g[i].M < BT2 || g[i].N < BT2) return false;
   return true;

@@ -681,7 +681,9 @@ def _wgrad_side_stream(dev, B, H):
         ent = (torch.cuda.ExternalStream(h.value, device=dev), ncu // 2)
         _side_streams[dev.index] = ent
     stream, free_cus = ent
-    grid_bwd = (H // 16) * 2 * ((B + 15) // 16)
+    # the persistent backward recurrence (lstm_xg.hip) pins one work-group per
+    # CU: 2 directions x ceil(B / 8) utterance groups x H / 16 unit slices
+    grid_bwd = 2 * ((B + 7) // 8) * (H // 16)
     return stream if grid_bwd <= free_cus else None
 
 

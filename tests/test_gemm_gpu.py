@@ -136,10 +136,12 @@ def test_linear_bf16_staged_padded(cuda_dev):
 
 @pytest.mark.parametrize('M,N,K', [(529, 389, 3000), (256, 256, 64), (300, 260, 200),
                                     (1024, 512, 8000)])
-def test_kmajor_256_tiles_exact(M, N, K, cuda_dev):
+def test_kmajor_256_tiles_exact(M, N, K, cuda_dev, monkeypatch):
     """K-major x K-major products with M, N >= 256 take the 256 x 256 kernel
-    (gemm_bf16_kk256): ragged edges, a single k-tile, a K that is not a
-    multiple of the 64-deep k-tile, split-K chunks; alpha / beta / bias."""
+    (gemm_bf16_kk256, opt-in by ASR_GEMM_KK256=1): ragged edges, a single
+    k-tile, a K that is not a multiple of the 32-deep k-tile, split-K chunks;
+    alpha / beta / bias."""
+    monkeypatch.setenv('ASR_GEMM_KK256', '1')
     ops = _ops()
     ops.set_compute_dtype('bf16')
     try:
@@ -163,10 +165,11 @@ def test_kmajor_256_tiles_exact(M, N, K, cuda_dev):
         ops.set_compute_dtype('fp32')
 
 
-def test_kmajor_256_tiles_two_problems_rowmapped(cuda_dev):
+def test_kmajor_256_tiles_two_problems_rowmapped(cuda_dev, monkeypatch):
     """The dW_hh launch shape: two problems side by side, the second reading
     column offsets, the B operand through a shifted per-utterance row map
     (h_{t-1}: t_add = -1, rows past the utterance read as zeros)."""
+    monkeypatch.setenv('ASR_GEMM_KK256', '1')
     ops = _ops()
     ops.set_compute_dtype('bf16')
     try:
