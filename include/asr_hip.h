@@ -273,6 +273,13 @@ int asr_convert_rows_bf16(const float* src, asr_rowmap_t map, int nrows, int nco
  * bf16 operand whose leading dimension is padded to a multiple of 8). */
 int asr_convert_rows_bf16_ld(const float* src, asr_rowmap_t map, int nrows, int ncols, int ld,
                              uint16_t* dst, void* stream);
+/* asr_convert_rows_bf16 of dropout(src): element at linear offset i of src is
+ * kept iff u(seed, i) >= p and scaled by 1/(1-p) -- the mask asr_dropout(src,
+ * ., n, p, seed) applies -- so a layer's dropped output is staged as the next
+ * layer's bf16 GEMM operand in one pass (nn.Dropout after each BLSTM layer,
+ * models/pytorch_v3/encoders/rnn.py:392-393, fused with the input staging). */
+int asr_convert_rows_bf16_dropout(const float* src, asr_rowmap_t map, int nrows, int ncols,
+                                  uint16_t* dst, float p, unsigned long long seed, void* stream);
 
 /* ------------------------------------------------------------ decoding
  * asr_ctc_best_path: CTC greedy best path (greedy_decoder.py:19-47): per

@@ -69,6 +69,7 @@ SIGNATURES = {
     'asr_add_tanh_forward': (c_int, [c_vp, c_vp, c_vp, c_ll, c_vp]),
     'asr_add_forward': (c_int, [c_vp, c_vp, c_vp, c_ll, c_vp]),
     'asr_convert_rows_bf16': None,  # set below, after RowMap (struct passed by value)
+    'asr_convert_rows_bf16_dropout': None,
     'asr_ctc_best_path': (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp,
                                   c_vp]),
     'asr_row_argmax': (c_int, [c_vp, c_int, c_int, c_vp, c_vp]),
@@ -129,6 +130,8 @@ class RowMap(ctypes.Structure):
 
 SIGNATURES['asr_convert_rows_bf16'] = (c_int, [c_vp, RowMap, c_int, c_int, c_vp, c_vp])
 SIGNATURES['asr_convert_rows_bf16_ld'] = (c_int, [c_vp, RowMap, c_int, c_int, c_int, c_vp, c_vp])
+SIGNATURES['asr_convert_rows_bf16_dropout'] = (c_int, [c_vp, RowMap, c_int, c_int, c_vp, c_float,
+                                                        ctypes.c_ulonglong, c_vp])
 
 
 class Operand(ctypes.Structure):

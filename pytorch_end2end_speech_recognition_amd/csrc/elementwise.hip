@@ -80,8 +80,18 @@ __global__ void tanh_bwd(const float* __restrict__ y, const float* __restrict__ 
 // dst[r][c] = bf16(src[row(r) + c]) for the rows of an asr_rowmap_t (zeros for
 // rows mapping outside [0, t_limit)); 8 columns per thread, 16-B stores when
 // ncols % 8 == 0.
+// p > 0: the source is read through dropout (element at linear offset i of
+// src kept iff u01(seed, i) >= p, scaled by 1/(1-p)) -- the mask asr_dropout
+// would apply to the whole src tensor, fused into the bf16 staging.
+template <bool DROP>
 __global__ void convert_rows_kernel(const float* __restrict__ src, asr_rowmap_t m, int nrows,
-                                    int ncols, int ld, uint16_t* __restrict__ dst) {
+                                    int ncols, int ld, uint16_t* __restrict__ dst, float p,
+                                    unsigned long long seed) {
+  const float scale = DROP ? 1.f / (1.f - p) : 1.f;
+  auto val = [&](const float* q, float x) {
+    if (!DROP) return x;
+    return u01(seed, (unsigned long long)(q - src)) >= p ? x * scale : 0.f;
+  };
   const int cpr = (ld + 7) >> 3;   // columns [ncols, ld) are written as zeros
   const long long nchunks = (long long)nrows * cpr;
   const int rpb = m.rows_per_b > 0 ? m.rows_per_b : 0x7fffffff;
@@ -102,15 +112,16 @@ __global__ void convert_rows_kernel(const float* __restrict__ src, asr_rowmap_t 
       if (ok && c0 < ncols) {
         const float4 x0 = *reinterpret_cast<const float4*>(s);
         const float4 x1 = *reinterpret_cast<const float4*>(s + 4);
-        v = u16x8{f2bf(x0.x), f2bf(x0.y), f2bf(x0.z), f2bf(x0.w),
-                  f2bf(x1.x), f2bf(x1.y), f2bf(x1.z), f2bf(x1.w)};
+        v = u16x8{f2bf(val(s, x0.x)), f2bf(val(s + 1, x0.y)), f2bf(val(s + 2, x0.z)),
+                  f2bf(val(s + 3, x0.w)), f2bf(val(s + 4, x1.x)), f2bf(val(s + 5, x1.y)),
+                  f2bf(val(s + 6, x1.z)), f2bf(val(s + 7, x1.w))};
       } else {
         v = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
       }
       *reinterpret_cast<u16x8*>(d) = v;
     } else {
       for (int j = 0; j < 8 && c0 + j < ld; ++j)
-        d[j] = (ok && c0 + j < ncols) ? f2bf(s[j]) : (uint16_t)0;
+        d[j] = (ok && c0 + j < ncols) ? f2bf(val(s + j, s[j])) : (uint16_t)0;
     }
   }
 }
@@ -232,8 +243,26 @@ extern "C" int asr_convert_rows_bf16_ld(const float* src, asr_rowmap_t map, int 
                 ASR_ERR_ARG, "convert_rows: vector path needs 16-B aligned rows");
   const long long n = (long long)nrows * ((ld + 7) / 8);
   if (n <= 0) return ASR_OK;
-  hipLaunchKernelGGL(convert_rows_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
-                     src, map, nrows, ncols, ld, dst);
+  hipLaunchKernelGGL(convert_rows_kernel<false>, dim3(grid_for(n)), dim3(256), 0,
+                     (hipStream_t)stream, src, map, nrows, ncols, ld, dst, 0.f, 0ull);
+  ASR_LAUNCH_CHECK();
+  return ASR_OK;
+}
+
+extern "C" int asr_convert_rows_bf16_dropout(const float* src, asr_rowmap_t map, int nrows,
+                                             int ncols, uint16_t* dst, float p,
+                                             unsigned long long seed, void* stream) {
+  ASR_REQUIRE(p >= 0.f && p < 1.f, ASR_ERR_ARG, "convert_rows_dropout: p=%f", (double)p);
+  if (p == 0.f) return asr_convert_rows_bf16_ld(src, map, nrows, ncols, ncols, dst, stream);
+  ASR_REQUIRE(src && dst && nrows >= 0 && ncols >= 0, ASR_ERR_ARG, "convert_rows: bad args");
+  if (ncols % 8 == 0)
+    ASR_REQUIRE(((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0 &&
+                    map.stride_t % 4 == 0 && map.stride_b % 4 == 0,
+                ASR_ERR_ARG, "convert_rows: vector path needs 16-B aligned rows");
+  const long long n = (long long)nrows * ((ncols + 7) / 8);
+  if (n <= 0) return ASR_OK;
+  hipLaunchKernelGGL(convert_rows_kernel<true>, dim3(grid_for(n)), dim3(256), 0,
+                     (hipStream_t)stream, src, map, nrows, ncols, ncols, dst, p, seed);
   ASR_LAUNCH_CHECK();
   return ASR_OK;
 }

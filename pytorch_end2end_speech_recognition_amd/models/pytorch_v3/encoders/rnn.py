@@ -169,15 +169,26 @@ class RNNEncoder(nn.Module):
         h, pm, t_mul, t_add, concat = xs.contiguous(), perm_d, 1, 0, False
         h_sub = lens_sub = None
         res_outputs = []
+        pending = None   # (p, seed): this layer's dropout, fused into the next layer's staging
         for l in range(self.num_layers):
             (w_ih, w_hh, b_ih, b_hh), gbufs = self._layer_tensors(l)
             lens_d = torch.from_numpy(lens.astype(np.int32)).to(dev, non_blocking=True)
             graph = tuple(p for pair in self._layer_params(l) for p in pair)
             h = ops.blstm_layer(h, lens_d, T, w_ih, w_hh, b_ih, b_hh, perm=pm, t_mul=t_mul,
                                 t_add=t_add, gbufs=tuple(gbufs), graph_params=graph,
-                                concat=concat)
+                                concat=concat, drop=pending)
+            pending = None
             if self.training and self.dropout_hidden_p > 0:
-                h = ops.dropout(h, self.dropout_hidden_p)
+                # same seed stream either way; fused when the next consumer is the
+                # next layer's input staging and nothing else reads the dropped h
+                seed = ops.next_seed()
+                if (ops.fuse_dropout_ok() and l < self.num_layers - 1 and
+                        not (self.num_layers_sub >= 1 and l == self.num_layers_sub - 1) and
+                        not (self.residual or self.dense_residual or self.num_proj > 0) and
+                        not (self.subsample_list[l] and self.subsample_type != 'drop')):
+                    pending = (self.dropout_hidden_p, seed)
+                else:
+                    h = ops.dropout(h, self.dropout_hidden_p, seed=seed)
             if self.num_layers_sub >= 1 and l == self.num_layers_sub - 1:   # rnn.py:400-407
                 h_sub, lens_sub = h, lens.astype(np.int32)
             pm, t_mul, t_add, concat = None, 1, 0, False

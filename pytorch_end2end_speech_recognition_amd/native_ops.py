@@ -523,10 +523,16 @@ class BLSTMLayerFn(torch.autograd.Function):
     directly (exact-f32 MFMA, parity mode)."""
 
     @staticmethod
-    def forward(ctx, x_src, lens, T, perm, t_mul, t_add, gbufs, concat, w_ih, w_hh, b_ih, b_hh,
-                *graph_params):
+    def forward(ctx, x_src, lens, T, perm, t_mul, t_add, gbufs, concat, drop, w_ih, w_hh, b_ih,
+                b_hh, *graph_params):
         N.require_device(x_src, lens, w_ih, w_hh, b_ih, b_hh)
         x_src = x_src.contiguous()
+        fused_drop = drop is not None and compute_dtype() == BF16 and not concat
+        if drop is not None and not fused_drop:   # materialise dropout(x_src) first
+            xd = torch.empty_like(x_src)
+            N.call('asr_dropout', N.ptr(x_src), N.ptr(xd), x_src.numel(), float(drop[0]),
+                   int(drop[1]), N.stream_handle(x_src.device))
+            x_src = xd
         B, T_src, Dsrc = x_src.shape
         # concat: the input row (b, t) spans source frames t*t_mul + t_add and the
         # next one (rnn.py:421-431), i.e. 2*Dsrc contiguous values
@@ -539,7 +545,8 @@ class BLSTMLayerFn(torch.autograd.Function):
                        t_limit=T_src, perm=perm)
         gx = torch.empty(B, T, 8 * H, dtype=torch.float32, device=dev)
         if cd == BF16:
-            x_op = convert_rows_bf16(x_src, a_map, B * T, Din)        # [B*T, Din]
+            x_op = convert_rows_bf16(x_src, a_map, B * T, Din,        # [B*T, Din]
+                                     drop=drop if fused_drop else None)
             w_op = convert_rows_bf16(w_ih, rowmap(Din), 8 * H, Din)   # [8H, Din]
             p = gemm_problem(operand(x_op, 0, rowmap(Din)), operand(w_op, 0, rowmap(Din)), gx,
                              rowmap(8 * H), B * T, 8 * H, Din, bias=b_ih, bias2=b_hh)
@@ -560,6 +567,7 @@ class BLSTMLayerFn(torch.autograd.Function):
         ctx.save_for_backward(x_op, w_op, lens, w_hh, b_ih, b_hh, gx, cst,
                               y_bf if y_bf is not None else y)
         ctx.meta = (T, perm, t_mul, t_add, gbufs, cd, (B, T_src, Dsrc, Din), w_ih)
+        ctx.drop = drop
         ctx.n_graph = len(graph_params)
         return y
 
@@ -624,15 +632,31 @@ class BLSTMLayerFn(torch.autograd.Function):
             p = gemm_problem(operand(dg_op, 0, rowmap(8 * H)), operand(w_op, 1, rowmap(Din)), dx,
                              c_map, BT, Din, 8 * H)
             run_gemm([p], dev)
-        return (dx,) + (None,) * (11 + ctx.n_graph)
+        if dx is not None and ctx.drop is not None:   # dropout's backward: the same mask
+            dxm = torch.empty_like(dx)
+            N.call('asr_dropout', N.ptr(dx), N.ptr(dxm), dx.numel(), float(ctx.drop[0]),
+                   int(ctx.drop[1]), N.stream_handle(dev))
+            dx = dxm
+        return (dx,) + (None,) * (12 + ctx.n_graph)
 
 
-def convert_rows_bf16(src, rmap, nrows, ncols):
-    """Dense bf16 [nrows, ncols] copy of the rows of `src` selected by a row map."""
+def convert_rows_bf16(src, rmap, nrows, ncols, drop=None):
+    """Dense bf16 [nrows, ncols] copy of the rows of `src` selected by a row map;
+    drop=(p, seed): of dropout(src) with asr_dropout's mask, in the same pass."""
     out = torch.empty(nrows, ncols, dtype=torch.bfloat16, device=src.device)
-    N.call('asr_convert_rows_bf16', N.ptr(src), rmap, int(nrows), int(ncols), N.ptr(out),
-           N.stream_handle(src.device))
+    if drop is not None:
+        N.call('asr_convert_rows_bf16_dropout', N.ptr(src), rmap, int(nrows), int(ncols),
+               N.ptr(out), float(drop[0]), int(drop[1]), N.stream_handle(src.device))
+    else:
+        N.call('asr_convert_rows_bf16', N.ptr(src), rmap, int(nrows), int(ncols), N.ptr(out),
+               N.stream_handle(src.device))
     return out
+
+
+def fuse_dropout_ok():
+    """Inter-layer dropout is folded into the next BLSTM layer's bf16 input
+    staging (bf16 mode; ASR_FUSE_DROPOUT=0 keeps the separate pass)."""
+    return compute_dtype() == BF16 and os.environ.get('ASR_FUSE_DROPOUT', '1') != '0'
 
 
 def _blstm_wgrad(dg, dg_f32, x_op, x_map, y_op, T, gbufs, dev):
@@ -688,15 +712,17 @@ def _wgrad_side_stream(dev, B, H):
 
 
 def blstm_layer(x_src, lens, T, w_ih, w_hh, b_ih, b_hh, perm=None, t_mul=1, t_add=0, gbufs=None,
-                graph_params=(), concat=False):
+                graph_params=(), concat=False, drop=None):
     """gbufs: optional (g_w_ih, g_w_hh, g_b_ih, g_b_hh) gradient views to accumulate
     into; default: the tensors' own .grad.  graph_params: the nn.Parameters the
     combined [fwd; rev] views alias -- passed only so autograd records that the
     output depends on them (their gradients are written by the kernels).
     concat: input row t is [x_src[t*t_mul + t_add]; x_src[t*t_mul + t_add + 1]]
-    ('concat' subsampling of the previous layer, read in place)."""
-    return BLSTMLayerFn.apply(x_src, lens, T, perm, t_mul, t_add, gbufs, bool(concat), w_ih,
-                              w_hh, b_ih, b_hh, *graph_params)
+    ('concat' subsampling of the previous layer, read in place).
+    drop: optional (p, seed): the layer reads dropout(x_src) (asr_dropout's mask),
+    fused into the bf16 input staging; its input gradient gets the same mask."""
+    return BLSTMLayerFn.apply(x_src, lens, T, perm, t_mul, t_add, gbufs, bool(concat), drop,
+                              w_ih, w_hh, b_ih, b_hh, *graph_params)
 
 
 # ---------------------------------------------------------------------------

@@ -412,3 +412,51 @@ def test_lstm_backward_db_is_column_sum_of_dg(B, T, H, cuda_dev, monkeypatch):
     scale = np.abs(ref).max()
     for r in (0, 1):
         assert np.abs(db2[r] - ref).max() / scale < 1e-5, r
+
+
+@pytest.mark.parametrize('sub', [False, True])
+def test_dropout_fused_into_next_layer_staging_bitwise(sub, cuda_dev):
+    """Inter-layer dropout folded into the next layer's bf16 input staging
+    (asr_convert_rows_bf16_dropout; rnn.py:392-393) equals the separate
+    dropout pass bit for bit: outputs, the input gradient (the same mask on
+    the way back) and every weight gradient; with and without the 'drop'
+    subsampling row map between the layers."""
+    ops = _ops()
+    ops.set_compute_dtype('bf16')
+    try:
+        rng = np.random.RandomState(3)
+        B, T, F, H, p, seed = 4, 48, 24, 64, 0.3, 987654321
+        lens = np.array([48, 40, 33, 20], np.int32)
+        xs_np = rng.randn(B, T, F).astype(np.float32)
+        w0 = [rng.uniform(-0.1, 0.1, s).astype(np.float32)
+              for s in ((8 * H, F), (8 * H, H), (8 * H,), (8 * H,))]
+        w1 = [rng.uniform(-0.1, 0.1, s).astype(np.float32)
+              for s in ((8 * H, 2 * H), (8 * H, H), (8 * H,), (8 * H,))]
+
+        def run(fused):
+            xs = torch.from_numpy(xs_np).to(cuda_dev).requires_grad_(True)
+            ws0 = [torch.from_numpy(a).to(cuda_dev).requires_grad_(True) for a in w0]
+            ws1 = [torch.from_numpy(a).to(cuda_dev).requires_grad_(True) for a in w1]
+            lens_d = torch.from_numpy(lens).to(cuda_dev)
+            h = ops.blstm_layer(xs, lens_d, T, *ws0)
+            T1, tm, ta = (T // 2, 2, 1) if sub else (T, 1, 0)
+            lens1 = torch.from_numpy(np.full(B, T1, np.int32) if sub else lens).to(cuda_dev)
+            if fused:
+                y = ops.blstm_layer(h, lens1, T1, *ws1, t_mul=tm, t_add=ta, drop=(p, seed))
+            else:
+                y = ops.blstm_layer(ops.dropout(h, p, seed=seed), lens1, T1, *ws1, t_mul=tm,
+                                    t_add=ta)
+            g = torch.from_numpy(rng_g.randn(*y.shape).astype(np.float32)).to(cuda_dev)
+            (y * g).sum().backward()
+            torch.cuda.synchronize()
+            return [y.detach().cpu().numpy(), xs.grad.cpu().numpy()] + \
+                [w.grad.cpu().numpy() for w in ws0 + ws1]
+
+        rng_g = np.random.RandomState(4)
+        ref = run(False)
+        rng_g = np.random.RandomState(4)
+        got = run(True)
+        for a, b in zip(got, ref):
+            np.testing.assert_array_equal(a, b)
+    finally:
+        ops.set_compute_dtype('fp32')
