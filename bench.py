@@ -1,14 +1,19 @@
 #!/usr/bin/env python
 """Training-throughput benchmark of the MI355X hybrid CTC/attention step.
 
-Workload (BASELINE.json configs[1]): LibriSpeech-100h char CTC, 5-layer
-bidirectional LSTM, 512 units per direction, no subsampling, dropout 0.2, Adam
-lr 1e-3 wd 1e-6, clip 5.0; per GPU B = 32 synthetic utterances of 80-dim fbank,
-x_lens ~ U[800, 1000] sorted descending (x_lens[0] = 1000), char labels
-U[0, 27] (V = 28 + blank), y_lens ~ U[60, 125].  One step = the
+Workload (BASELINE.json configs[1], the default): LibriSpeech-100h char CTC,
+5-layer bidirectional LSTM, 512 units per direction, no subsampling, dropout
+0.2, Adam lr 1e-3 wd 1e-6, clip 5.0; per GPU B = 32 synthetic utterances of
+80-dim fbank, x_lens ~ U[800, 1000] (x_lens[0] = 1000), char labels U[0, 27]
+(V = 28 + blank), y_lens ~ U[60, 125].  --config selects the other
+BASELINE configs (timit2x320, att4x320, hybrid4x320, vgg_hier).  One step = the
 reference's full train_step: H2D of the numpy batch, forward, CTC loss,
-backward, RCCL gradient all-reduce (N > 1), fused global-norm clip + Adam, loss
-read back.  Weak scaling: B = 32 per GPU.
+backward, RCCL gradient all-reduce (N > 1, bucketed per BLSTM layer and
+overlapped with the backward), fused global-norm clip + Adam, loss read back.
+Weak scaling: ONE global length-sorted batch of 32 x N utterances dealt
+round-robin to the N ranks (shard_batch), each rank's gradient scaled by
+local_B / global_B before the sum.  ms_per_step / value use the median step
+(max over ranks per step).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
@@ -31,76 +36,38 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from pytorch_end2end_speech_recognition_amd import _native as N  # noqa: E402
-from pytorch_end2end_speech_recognition_amd import native_ops  # noqa: E402
+from pytorch_end2end_speech_recognition_amd import native_ops, recipes  # noqa: E402
 from pytorch_end2end_speech_recognition_amd.models.load_model import load  # noqa: E402
 from pytorch_end2end_speech_recognition_amd.utils.training.training_loop import (  # noqa: E402
-    train_hierarchical_step, train_step)
+    shard_batch, train_hierarchical_step, train_step)
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
 BF16_PEAK_TFLOPS = 2500.0    # dense bf16 MFMA (spec, no sparsity)
 
+def _cfg(workload, model_type, params, **kw):
+    d = dict(workload=workload, model_type=model_type, params=params)
+    d.update(kw)
+    return d
+
+
+# BASELINE.json configs (the params dicts live in the package: recipes.py)
 CONFIGS = {
-    'ctc5x512': dict(
-        workload='librispeech100h_char_ctc_blstm5x512', model_type='ctc',
-        params=dict(input_freq=80, use_delta=False, use_double_delta=False, input_channel=1,
-                    splice=1, num_stack=1, encoder_type='lstm', conv_channels=[],
-                    conv_kernel_sizes=[], conv_strides=[], poolings=[], activation='relu',
-                    batch_norm=False, encoder_bidirectional=True, encoder_residual=False,
-                    encoder_dense_residual=False, encoder_num_units=512, encoder_num_proj=0,
-                    encoder_num_layers=5, subsample_list=[], subsample_type='drop', fc_list=[],
-                    optimizer='adam', learning_rate=1e-3, parameter_init_distribution='uniform',
-                    parameter_init=0.1, recurrent_weight_orthogonal=False,
-                    init_forget_gate_bias_with_one=True, char_init=False, clip_grad_norm=5.0,
-                    dropout_input=0, dropout_encoder=0.2, weight_decay=1e-6,
-                    logits_temperature=1, label_smoothing_prob=0, weight_noise_std=0,
-                    num_classes=28)),
+    'timit2x320': _cfg('timit_phone61_ctc_blstm2x320_f123', 'ctc', recipes.timit2x320()),
+    'ctc5x512': _cfg('librispeech100h_char_ctc_blstm5x512', 'ctc', recipes.ctc5x512()),
+    'att4x320': _cfg('librispeech100h_char_location_attention_blstm4x320', 'attention',
+                     recipes.attention4x320(0.0)),
+    'hybrid4x320': _cfg('librispeech_char_hybrid_ctc0.3_attention_blstm4x320', 'attention',
+                        recipes.attention4x320(0.3)),
+    'vgg_hier': _cfg('swbd_vgg_blstm4x320_hierarchical_word10k_char_ctc', 'hierarchical_ctc',
+                     recipes.vgg_hier()),
 }
 
 
-def _attention_params(ctc_weight):
-    """configs[2] / configs[3]: the reference's LibriSpeech-100h location-attention
-    recipe (examples/librispeech/s5/conf/attention/char_blstm_att_100h.yml, kept
-    as the fixture tests/golden/char_blstm_att_100h.yml): 4x320 BLSTM with x4
-    drop subsampling, location attention (128, 10 ch x 201), LSTM decoder 320,
-    embedding 32, dropout 0.2 everywhere, scheduled sampling 0.2; hybrid adds
-    lambda * CTC."""
-    import yaml
-    with open(os.path.join(ROOT, 'tests', 'golden', 'char_blstm_att_100h.yml')) as f:
-        prm = yaml.safe_load(f)['param']
-    prm.update(num_classes=28, ctc_loss_weight=ctc_weight)
-    for k in ('learning_rate', 'weight_decay'):
-        prm[k] = float(prm[k])
-    return prm
-
-
-CONFIGS['att4x320'] = dict(workload='librispeech100h_char_location_attention_blstm4x320',
-                           model_type='attention', params=None, ctc_weight=0.0)
-CONFIGS['hybrid4x320'] = dict(workload='librispeech_char_hybrid_ctc0.3_attention_blstm4x320',
-                              model_type='attention', params=None, ctc_weight=0.3)
-
-
-CONFIGS['vgg_hier'] = dict(
-    workload='swbd_vgg_blstm4x320_hierarchical_word10k_char_ctc', model_type='hierarchical_ctc',
-    params=dict(
-        input_freq=80, use_delta=False, use_double_delta=False, input_channel=1, splice=1,
-        num_stack=1, encoder_type='lstm', conv_channels=[64, 64, 128, 128],
-        conv_kernel_sizes=[[3, 3]] * 4, conv_strides=[[1, 1]] * 4,
-        poolings=[[], [2, 2], [], [2, 2]], activation='relu', batch_norm=True,
-        encoder_bidirectional=True, encoder_residual=False, encoder_dense_residual=False,
-        encoder_num_units=320, encoder_num_proj=0, encoder_num_layers=4,
-        encoder_num_layers_sub=3, subsample_list=[], subsample_type='drop', fc_list=[],
-        fc_list_sub=[], main_loss_weight=0.5, sub_loss_weight=0.5, optimizer='adam',
-        learning_rate=1e-3, parameter_init_distribution='uniform', parameter_init=0.1,
-        recurrent_weight_orthogonal=False, init_forget_gate_bias_with_one=True, char_init=False,
-        clip_grad_norm=5.0, dropout_input=0, dropout_encoder=0.2, weight_decay=1e-6,
-        logits_temperature=1, label_smoothing_prob=0, weight_noise_std=0,
-        num_classes=10000, num_classes_sub=28))
-
-
-def config_params(cfg):
-    if cfg['params'] is None:
-        cfg['params'] = _attention_params(cfg['ctc_weight'])
-    return cfg['params']
+def input_dim(p):
+    """load_model.py: input_freq x (1 + delta + double delta) x splice x stack."""
+    return (p['input_freq'] * (1 + int(bool(p.get('use_delta'))) +
+                               int(bool(p.get('use_double_delta')))) *
+            p.get('splice', 1) * p.get('num_stack', 1))
 
 
 def synthetic_batch(B, T, F, num_classes, seed):
@@ -163,10 +130,10 @@ def roofline_report(args, p, mean_us, launches, mean_work, workload):
     fwd_cell = 4 * 4 * 2 + 4 * 2              # gx read + act write (4 gates f32), y + c write
     bwd_cell = 4 * 4 * 2 + 4 * 3              # act read + dG write, dy + c_t + c_{t-1} read
     kinds = [
-        ('lstm_fwd_step', 'hbm', 2 * cell * fwd_cell + w_hh, flops_step),
-        ('lstm_bwd_step', 'hbm', 2 * cell * bwd_cell + w_hh, flops_step),
-        ('lstm_fwd_pass', 'hbm', T * 2 * cell * fwd_cell + w_hh, T * flops_step),
-        ('lstm_bwd_pass', 'hbm', T * 2 * cell * bwd_cell + w_hh, T * flops_step),
+        ('lstm_fwd_step', 'mfma', 2 * cell * fwd_cell + w_hh, flops_step),
+        ('lstm_bwd_step', 'mfma', 2 * cell * bwd_cell + w_hh, flops_step),
+        ('lstm_fwd_pass', 'mfma', T * 2 * cell * fwd_cell + w_hh, T * flops_step),
+        ('lstm_bwd_pass', 'mfma', T * 2 * cell * bwd_cell + w_hh, T * flops_step),
         ('gemm', 'mfma', 0, mean_work[4]),
         ('ctc_fwd', 'hbm', mean_work[5], 0.0),
         ('ctc_grad', 'hbm', mean_work[6], 0.0),
@@ -202,6 +169,9 @@ def roofline_report(args, p, mean_us, launches, mean_work, workload):
                                                     3)})
     if tsrc:
         out['traffic_source'] = tsrc
+    if dom['name'].startswith('lstm'):
+        out['hbm_achieved_gbs'] = round(dom['gbs'], 1)
+        out['us_per_time_step'] = round(dom['us'] / T, 3)
     others = {}
     for r in rows:
         if r is dom:
@@ -209,7 +179,7 @@ def roofline_report(args, p, mean_us, launches, mean_work, workload):
         v = {'bound': r['bound'], 'mean_launch_us': round(r['us'], 3), 'launches': r['n']}
         v.update(view(r))
         if r['name'].startswith('lstm'):
-            v['mfma_tflops'] = round(r['tfs'], 2)
+            v['hbm_achieved_gbs'] = round(r['gbs'], 1)
             if r['name'].endswith('_pass'):
                 v['us_per_time_step'] = round(r['us'] / T, 3)
         others[r['name']] = v
@@ -237,27 +207,33 @@ def pmc_traffic(kernel, workload):
     return None, None
 
 
-def cpu_baseline(cfg, batch, n_utts):
-    """Oracle (torch-CPU restatement of the reference path) on a bounded sample:
-    the first n_utts utterances of this rank's batch, one full training step
-    (forward, backward, clip, Adam)."""
-    from oracle import asr_ref
+def _cpu_threads():
+    """Threads the CPU leg uses: the cores this process may run on, capped by
+    the box's per-job share (OMP_NUM_THREADS, 16 per GPU on the pool)."""
     cores = len(os.sched_getaffinity(0))
-    threads = max(1, min(16, cores))
-    torch.set_num_threads(threads)
-    p = config_params(cfg)
-    torch.manual_seed(0)
-    model = load(cfg['model_type'], dict(p), 'pytorch')           # host-side init only
-    sd = {k: v.detach().clone() for k, v in model.state_dict().items()}
-    trainable = [v.requires_grad_(True) for k, v in sd.items()
-                 if v.is_floating_point() and 'running' not in k]
-    opt = torch.optim.Adam(trainable, lr=p['learning_rate'], weight_decay=p['weight_decay'])
-    sub = {k: v[:n_utts] for k, v in batch.items()}
+    cap = int(os.environ.get('OMP_NUM_THREADS', cores) or cores)
+    return max(1, min(cores, cap)), cores
+
+
+def _sample(batch, n_utts):
+    sub = {k: np.asarray(v)[:n_utts] for k, v in batch.items()}
     sub['ys'] = sub['ys'][:, :int(sub['y_lens'].max())]
     if 'ys_sub' in sub:
         sub['ys_sub'] = sub['ys_sub'][:, :int(sub['y_lens_sub'].max())]
-    t0 = time.perf_counter()
-    opt.zero_grad()
+    return sub
+
+
+def _plain_ctc(cfg):
+    p = cfg['params']
+    return (cfg['model_type'] == 'ctc' and not p.get('conv_channels') and
+            not p.get('subsample_list') and not p.get('encoder_num_proj') and
+            not p.get('fc_list'))
+
+
+def _oracle_loss(cfg, sd, sub):
+    """Dropout-free oracle loss on the sample (torch CPU, autograd-ready)."""
+    from oracle import asr_ref
+    p = cfg['params']
     if cfg['model_type'] == 'hierarchical_ctc':
         ocfg = dict(num_layers=p['encoder_num_layers'], num_layers_sub=p['encoder_num_layers_sub'],
                     subsample_list=p['subsample_list'], conv_channels=p['conv_channels'],
@@ -266,38 +242,138 @@ def cpu_baseline(cfg, batch, n_utts):
         loss, _, _ = asr_ref.hierarchical_ctc_loss(sd, ocfg, sub['xs'], sub['ys'], sub['x_lens'],
                                                    sub['y_lens'], sub['ys_sub'],
                                                    sub['y_lens_sub'])
-    elif cfg['model_type'] == 'attention':   # oracle decoder: teacher forcing, no dropout
-        loss = asr_ref.attention_model_loss(sd, p, sub['xs'], sub['ys'], sub['x_lens'],
+        return loss
+    if cfg['model_type'] == 'attention':      # teacher forcing, no dropout / sampling
+        return asr_ref.attention_model_loss(sd, p, sub['xs'], sub['ys'], sub['x_lens'],
                                             sub['y_lens'])
+    ocfg = dict(num_layers=p['encoder_num_layers'], subsample_list=p['subsample_list'],
+                fc_list=p['fc_list'])
+    loss, _, _, _ = asr_ref.ctc_model_loss(sd, ocfg, sub['xs'], sub['ys'], sub['x_lens'],
+                                           sub['y_lens'])
+    return loss
+
+
+def cpu_baseline(cfg, batch, n_utts):
+    """The reference CPU path timed on this host over a bounded sample (the
+    first n_utts utterances of the batch at full length), one full training
+    step each.  Plain BLSTM-CTC configs run oracle/cpu_path.py -- the
+    reference's own CPU modules (packed multi-layer nn.LSTM, nn.Linear,
+    ctc_loss, clip, Adam); the others run the oracle's torch-CPU restatement.
+    Returns (baseline dict, initial state_dict, sample, {'f64': dropout-free loss
+    of the same path in float64, 'f32': the same in float32 on this host})."""
+    threads, cores = _cpu_threads()
+    torch.set_num_threads(threads)
+    p = cfg['params']
+    torch.manual_seed(1623)
+    model = load(cfg['model_type'], dict(p), 'pytorch')           # host-side init only
+    sd = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    sub = _sample(batch, n_utts)
+    if _plain_ctc(cfg):
+        from oracle import cpu_path
+        m = cpu_path.ctc_cpu_path(p, sd)
+        ref_loss = {'f32': cpu_path.eval_loss(m, sub),
+                    'f64': cpu_path.eval_loss(m, sub, torch.float64)}
+        dt, _ = cpu_path.time_train_step(m, sub, p['learning_rate'], p['weight_decay'],
+                                         p['clip_grad_norm'])
+        what = ('the reference CPU modules (packed %d-layer bidirectional nn.LSTM, nn.Linear, '
+                'ctc_loss, clip, Adam; oracle/cpu_path.py)' % p['encoder_num_layers'])
     else:
-        ocfg = dict(num_layers=p['encoder_num_layers'], subsample_list=p['subsample_list'],
-                    fc_list=p['fc_list'])
-        loss, _, _, _ = asr_ref.ctc_model_loss(sd, ocfg, sub['xs'], sub['ys'], sub['x_lens'],
-                                               sub['y_lens'])
-    loss.backward()
-    torch.nn.utils.clip_grad_norm_(trainable, p['clip_grad_norm'])
-    opt.step()
-    dt = time.perf_counter() - t0
+        with torch.no_grad():
+            ref_loss = {'f32': float(_oracle_loss(cfg, sd, sub)),
+                        'f64': float(_oracle_loss(cfg, {k: v.double() if v.is_floating_point()
+                                                        else v for k, v in sd.items()}, sub))}
+        trainable = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+        params = [v for k, v in trainable.items() if v.is_floating_point() and 'running' not in k]
+        opt = torch.optim.Adam(params, lr=p['learning_rate'], weight_decay=p['weight_decay'])
+        t0 = time.perf_counter()
+        opt.zero_grad()
+        loss = _oracle_loss(cfg, trainable, sub)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(params, p['clip_grad_norm'])
+        opt.step()
+        dt = time.perf_counter() - t0
+        what = ('the fp32 torch-CPU oracle restatement%s'
+                % (' (decoder without dropout / scheduled sampling)'
+                   if cfg['model_type'] == 'attention' else ''))
     frames = float(np.sum(sub['x_lens']))
-    return {'value': frames / dt, 'unit': 'frames/s', 'cores': threads, 'kind': 'port',
-            'sample': '%d utterances x %d max frames (%d frames), 1 full training step (fwd + '
-                      'bwd + clip + Adam) of the fp32 torch-CPU oracle%s, %.1f s'
-                      % (n_utts, int(sub['x_lens'].max()), int(frames),
-                         ' (decoder without dropout / scheduled sampling)'
-                         if cfg['model_type'] == 'attention' else '', dt)}
+    out = {'value': frames / dt, 'unit': 'frames/s', 'cores': threads, 'kind': 'port',
+           'sample': '%d utterances x %d max frames (%d frames), 1 full training step (fwd + '
+                     'bwd + clip + Adam) of %s, %d threads of %d affinity cores, %.1f s'
+                     % (n_utts, int(sub['x_lens'].max()), int(frames), what, threads, cores, dt)}
+    return out, sd, sub, ref_loss
+
+
+def parity_report(cfg, sd, sub, ref_loss):
+    """BASELINE metric's second half (CTC+attn loss rel-err vs ref): the GPU
+    model built with the same initial weights, dropout-free loss (is_eval) on
+    the CPU leg's sample, in fp32 (parity mode) and bf16 (the bench mode).
+
+    The reference is the CPU leg's path evaluated in float64.  At T = 1000 the
+    randomly initialised deep BLSTM amplifies rounding (the reference's own
+    float32 result moves by ~1 % between CPUs / BLAS builds), so the line also
+    reports the reference's own float32 error on this host, ref_f32_rel_err:
+    the floor any float32 implementation is measured against."""
+    ref = ref_loss['f64']
+    out = {'sample_utts': int(len(sub['xs'])), 'ref_loss_f64': ref,
+           'ref_loss_f32': ref_loss['f32'],
+           'ref_f32_rel_err': abs(ref_loss['f32'] - ref) / max(abs(ref), 1e-30),
+           'ref': 'cpu_baseline path in float64, same initial weights, dropout off'}
+    ref_loss = ref
+    p = cfg['params']
+    prev = native_ops.compute_dtype()
+    for prec in ('fp32', 'bf16'):
+        torch.manual_seed(1623)
+        m = load(cfg['model_type'], dict(p), 'pytorch')
+        m.load_state_dict(sd)
+        m.set_cuda()
+        m.set_precision(prec)
+        if cfg['model_type'] == 'hierarchical_ctc':
+            got = m(sub['xs'], sub['ys'], sub['x_lens'], sub['y_lens'], sub['ys_sub'],
+                    sub['y_lens_sub'], is_eval=True)
+            got = got[0] if isinstance(got, (tuple, list)) else got
+        else:
+            got = m(sub['xs'], sub['ys'], sub['x_lens'], sub['y_lens'], is_eval=True)
+        got = float(got)
+        out['loss_%s' % prec] = got
+        out['loss_rel_err_%s' % prec] = abs(got - ref_loss) / max(abs(ref_loss), 1e-30)
+        del m
+    native_ops.set_compute_dtype('bf16' if prev == native_ops.BF16 else 'fp32')
+    return out
+
+
+def encoder_flops_per_step(p, x_lens, din):
+    """BLSTM training FLOPs = 3 x fwd, fwd = sum over layers of
+    2 dirs x 2 x 4H x (Din + H) per frame at that layer (GEMM work only);
+    din = the encoder's input width (after the VGG front-end, if any), whose
+    time pooling divides the frame count."""
+    H = p['encoder_num_units']
+    frames = float(np.sum(x_lens))
+    for pool in p.get('poolings') or []:
+        if len(pool):
+            frames /= pool[1]
+    sub = p.get('subsample_list') or [False] * p['encoder_num_layers']
+    fwd, frac = 0.0, 1.0
+    for l in range(p['encoder_num_layers']):
+        d = din if l == 0 else 2 * H * (2 if (p.get('subsample_type') == 'concat' and sub[l - 1])
+                                        else 1)
+        fwd += 2 * 2 * 4 * H * (d + H) * frac
+        if sub[l]:
+            frac *= 0.5
+    return 3.0 * fwd * frames
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=10)
-    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=5)
     ap.add_argument('--config', default='ctc5x512', choices=sorted(CONFIGS))
     ap.add_argument('--precision', default='bf16', choices=['bf16', 'fp32'])
-    ap.add_argument('--batch', type=int, default=32)
+    ap.add_argument('--batch', type=int, default=32, help='utterances per GPU')
     ap.add_argument('--frames', type=int, default=1000)
-    ap.add_argument('--cpu-utts', type=int, default=2)
+    ap.add_argument('--cpu-utts', type=int, default=6)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-parity', action='store_true')
     ap.add_argument('--prof-stride', type=int, default=8)
     args = ap.parse_args()
 
@@ -310,31 +386,33 @@ def main():
         dist.init_process_group('nccl', device_id=dev)
 
     cfg = CONFIGS[args.config]
-    p = dict(config_params(cfg))
+    p = dict(cfg['params'])
     torch.manual_seed(1623)
     native_ops.manual_seed(1623 + rank)
     model = load(cfg['model_type'], p, 'pytorch')
+    model.set_cuda()
     if world > 1:   # identical initial weights on every rank
-        model.set_cuda()
         dist.broadcast(model._flat_param, src=0)
-    else:
-        model.set_cuda()
     model.set_precision(args.precision)
     model.set_optimizer(p['optimizer'], p['learning_rate'], weight_decay=p['weight_decay'],
                         lr_schedule=False)
+    # one global length-sorted batch of batch x world utterances (weak scaling:
+    # batch per GPU fixed), dealt round-robin to the ranks
+    GB = args.batch * world
     if cfg['model_type'] == 'hierarchical_ctc':
-        batch = synthetic_hier_batch(args.batch, args.frames, p['input_freq'], p['num_classes'],
-                                     p['num_classes_sub'], seed=rank)
-
+        gbatch = synthetic_hier_batch(GB, args.frames, input_dim(p), p['num_classes'],
+                                      p['num_classes_sub'], seed=0)
+    else:
+        gbatch = synthetic_batch(GB, args.frames, input_dim(p), p['num_classes'], seed=0)
+    batch, grad_scale = shard_batch(gbatch, rank, world)
+    if cfg['model_type'] == 'hierarchical_ctc':
         def step(m, b):
-            m, lv, _, _ = train_hierarchical_step(m, b, p['clip_grad_norm'])
+            m, lv, _, _ = train_hierarchical_step(m, b, p['clip_grad_norm'],
+                                                  grad_scale=grad_scale)
             return m, lv
     else:
-        batch = synthetic_batch(args.batch, args.frames, p['input_freq'], p['num_classes'],
-                                seed=rank)
-
         def step(m, b):
-            return train_step(m, b, p['clip_grad_norm'])
+            return train_step(m, b, p['clip_grad_norm'], grad_scale=grad_scale)
     frames_per_step = float(batch['x_lens'].sum())
 
     for _ in range(args.warmup):
@@ -345,10 +423,11 @@ def main():
     torch.cuda.synchronize()
     N.call('asr_prof_begin', args.prof_stride)
     t0 = time.perf_counter()
-    losses = []
+    losses, marks = [], [t0]
     for _ in range(args.steps):
-        model, lv = step(model, batch)
+        model, lv = step(model, batch)     # reads the loss back: the step has drained
         losses.append(lv)
+        marks.append(time.perf_counter())
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -361,10 +440,11 @@ def main():
     mean_work = (ctypes.c_double * NK)()
     N.call('asr_prof_end', ctypes.cast(mean_us, ctypes.c_void_p),
            ctypes.cast(launches, ctypes.c_void_p), ctypes.cast(mean_work, ctypes.c_void_p), NK)
+    step_s = np.diff(np.asarray(marks))
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed] + list(step_s), dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed, step_s = float(t[0].item()), t[1:].cpu().numpy()
         fr = torch.tensor([frames_per_step], dtype=torch.float64, device=dev)
         dist.all_reduce(fr, op=dist.ReduceOp.SUM)
         total_frames_per_step = float(fr.item())
@@ -376,24 +456,36 @@ def main():
         return
 
     roofline = roofline_report(args, p, mean_us, launches, mean_work, cfg['workload'])
+    med = float(np.median(step_s))
+    enc_flops = encoder_flops_per_step(p, gbatch['x_lens'], model.encoder.input_size) / world
+    if roofline is not None:
+        roofline['encoder_mfma_frac'] = round(enc_flops / med / 1e12 / BF16_PEAK_TFLOPS, 4)
+        roofline['encoder_train_flops_per_step_per_gpu'] = enc_flops
 
-    cpu = None
+    cpu = parity = None
     if world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(cfg, batch, args.cpu_utts)
+        cpu, sd0, sub, ref_loss = cpu_baseline(cfg, batch, args.cpu_utts)
+        if not args.no_parity:
+            parity = parity_report(cfg, sd0, sub, ref_loss)
 
-    value = total_frames_per_step * args.steps / elapsed
     out = {
-        'metric': 'training frames/sec', 'value': round(value, 1), 'unit': 'frames/s',
-        'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
-        'ms_per_step': round(1000.0 * elapsed / args.steps, 3), 'higher_is_better': True,
+        'metric': 'training frames/sec', 'value': round(total_frames_per_step / med, 1),
+        'unit': 'frames/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
+        'ms_per_step': round(1000.0 * med, 3), 'higher_is_better': True,
         'scaling': 'weak', 'vs_baseline': None, 'dtype': args.precision, 'data': 'synthetic',
         'config': {'workload': cfg['workload'], 'batch_per_gpu': args.batch,
-                   'global_batch': args.batch * world, 'max_frames': args.frames,
-                   'feat_dim': p['input_freq'], 'vocab': p['num_classes'] + 1,
+                   'global_batch': GB, 'max_frames': args.frames,
+                   'feat_dim': input_dim(p), 'vocab': p['num_classes'] + 1,
                    'parallelism': 'dp%d' % world, 'frames_per_step': total_frames_per_step},
+        'timing': {'statistic': 'median step (max over ranks)', 'ms_per_step_mean':
+                   round(1000.0 * elapsed / args.steps, 3),
+                   'value_mean': round(total_frames_per_step * args.steps / elapsed, 1),
+                   'ms_per_step_min': round(1000.0 * float(np.min(step_s)), 3),
+                   'ms_per_step_max': round(1000.0 * float(np.max(step_s)), 3)},
         'loss_last': losses[-1] if losses else None,
         'roofline': roofline,
         'cpu_baseline': cpu,
+        'parity': parity,
     }
     print(json.dumps(out))
     if world > 1:

@@ -227,6 +227,14 @@ int asr_lstm_backward_db(const float* dy, const void* whh_f, const void* whh_r, 
 size_t asr_grad_sqnorm_workspace_bytes(void);
 int asr_grad_sqnorm(const float* g, long long n, float* out, void* workspace, size_t ws_bytes,
                     void* stream);
+/* asr_optim_step_guarded: the same with guard (device int32[2], nullable):
+ * when guard[0] | guard[1] != 0 (asr_lstm_status_gather's words) the kernel
+ * leaves params and state untouched. */
+int asr_optim_step_guarded(int kind, float* params, const float* grads, float* m, float* v,
+                           long long n, float lr, float beta1, float beta2, float eps,
+                           float weight_decay, long long step, float momentum, float dampening,
+                           const float* grad_sqnorm, float max_norm, uint16_t* bf16_shadow,
+                           const int* guard, void* stream);
 int asr_optim_step(int kind, float* params, const float* grads, float* m, float* v, long long n,
                    float lr, float beta1, float beta2, float eps, float weight_decay,
                    long long step, float momentum, float dampening, const float* grad_sqnorm,
@@ -254,6 +262,16 @@ int asr_embedding_backward(const long long* idx, const float* dout, int n, int V
 int asr_embedding_backward_csr(const int32_t* order, const int32_t* starts, const float* dout,
                                int V, int E, int trans, int padding_idx, float* grad_weight,
                                void* stream);
+/* nn.LSTMCell nonlinearity (RNNDecoder.forward, rnn_decoder.py:80-86): pre
+ * [B][4D] gate pre-activations (i, f, g, o) -> h, c [B][D]; act [B][4D] the
+ * activated gates kept for the backward.  c_prev nullable (zero state).
+ * Backward: dh / dc nullable cotangents -> dpre [B][4D], dc_prev [B][D]
+ * (nullable). */
+int asr_lstm_cell_forward(const float* pre, const float* c_prev, int B, int D, float* act,
+                          float* h, float* c, void* stream);
+int asr_lstm_cell_backward(const float* act, const float* c_prev, const float* c,
+                           const float* dh, const float* dc, int B, int D, float* dpre,
+                           float* dc_prev, void* stream);
 int asr_tanh_forward(const float* x, float* y, long long n, void* stream);
 int asr_tanh_backward(const float* y, const float* dy, float* dx, long long n, void* stream);
 /* y = tanh(a + b) (attention bottleneck with per-branch dropout,
@@ -423,6 +441,36 @@ int asr_attdec_forward_ex(const asr_attdec_dims_t* dims, const asr_attdec_opts_t
                           const float* conv_w, const float* v, const float* pre_emb,
                           const float* h0, float* dec, float* c, float* gates, float* x,
                           float* ctx, float* aw, void* workspace, size_t ws_bytes, void* stream);
+/* One location-attention step as a standalone op (AttentionMechanism.forward,
+ * attention_layer.py:123-251; the layer boundary of SURVEY §8(b)); the same
+ * kernels as the decoder loop.  dims->S is ignored.  Forward: conv of aw_prev
+ * [B][T], energies from enc_a [B][T][A] + W_dec dec_out [B][D] + W_conv f,
+ * multiplicative length mask, sharpening, softmax / sigmoid -> aw_out [B][T],
+ * ctx_out [B][E] = aw_out . enc.  Backward (cotangents d_ctx [B][E],
+ * d_aw_out [B][T] nullable): d_enc_a, d_dec, d_aw_prev, dctx_tot, dwd (d of
+ * W_dec dec_out) written; dv_part / dwc_part / dcw_part hold
+ * B * 2 * asr_attdec_chunks rows whose column sums are dV, dW_conv and the
+ * conv-kernel gradient.  The caller forms dW_dec = dwd^T dec_out and
+ * d enc = aw_out^T dctx_tot. */
+size_t asr_att_step_workspace_bytes(const asr_attdec_dims_t* dims);
+int asr_att_step_forward(const asr_attdec_dims_t* dims, const float* enc, const float* enc_a,
+                         const int32_t* lens, const float* w_dec, const float* w_conv,
+                         const float* conv_w, const float* v, const float* dec_out,
+                         const float* aw_prev, float* ctx_out, float* aw_out, void* workspace,
+                         size_t ws_bytes, void* stream);
+int asr_att_step_backward(const asr_attdec_dims_t* dims, const float* enc, const float* enc_a,
+                          const int32_t* lens, const float* w_dec, const float* w_conv,
+                          const float* conv_w, const float* v, const float* dec_out,
+                          const float* aw_prev, const float* aw_out, const float* d_ctx,
+                          const float* d_aw_out, float* d_enc_a, float* d_dec, float* d_aw_prev,
+                          float* dctx_tot, float* dwd, float* dv_part, float* dwc_part,
+                          float* dcw_part, void* workspace, size_t ws_bytes, void* stream);
+
+/* Test / diagnostics: the attention-step kernel instantiations the last
+ * asr_attdec_forward_ex / _backward_ex launched: out4 = {forward conv-channel
+ * template (10 or 3; 0 = generic), forward 32-frame chunks per utterance,
+ * backward template, backward chunks}. */
+int asr_attdec_last_launch(int* out4);
 int asr_attdec_backward_ex(const asr_attdec_dims_t* dims, const asr_attdec_opts_t* opts,
                            int compute_dtype, const float* enc, const float* enc_a,
                            const int32_t* lens, const float* w_ih_ctx, long long ld_ih,
@@ -513,6 +561,17 @@ int asr_prof_end(double* mean_us, long long* launches, double* mean_work, int nk
  * inter-work-group wait gave up (a co-residency failure; that pass's outputs
  * are invalid).  Synchronises `stream`; clear != 0 resets the word. */
 int asr_lstm_persist_status(int* status, int clear, void* stream);
+
+/* The same two status words, stream-ordered and without a host sync:
+ * dst (device int32[2]) = {counter-form word, tagged-granule word}; clear != 0
+ * then zeroes both.  The training step gathers them after its backward and
+ * hands dst (MAX-all-reduced over data-parallel ranks) to
+ * asr_optim_step_guarded, so a pass whose spin gave up never updates the
+ * weights; the host reads dst at the step's loss read-back and skips the
+ * batch (training_loop.py:69-76 semantics).  asr_lstm_status_inject sets the
+ * tagged-granule word (test hook: what a spin give-up does). */
+int asr_lstm_status_gather(int* dst, int clear, void* stream);
+int asr_lstm_status_inject(int bits, void* stream);
 
 /* Hand-off protocols the tagged-granule recurrence (lstm_xg.hip) has run
  * since the last clear: bit 0 write-through (sc1, any placement), bit 1

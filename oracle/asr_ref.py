@@ -38,6 +38,58 @@ def lstm_direction(x, lens, w_ih, w_hh, b_ih, b_hh, reverse):
     return torch.stack(outs, dim=1)
 
 
+@torch.no_grad()
+def lstm_direction_bptt(x, lens, w_ih, w_hh, b_ih, b_hh, reverse, dy):
+    """lstm_direction's forward plus an explicit O(T) backward (BPTT) for the
+    cotangent dy [B, T, H] -- the same math as autograd through
+    lstm_direction (checked in tests/test_recurrence_full.py) without
+    autograd's O(T^2) slice-gradient cost, so the oracle runs at the bench
+    shape (B = 32, T = 1000, H = 512) in seconds.  Computes in x's dtype.
+    Returns (y [B, T, H], dx [B, T, Din], dW_ih, dW_hh, db) where db is the
+    gradient of b_ih (equal to that of b_hh)."""
+    B, T, _ = x.shape
+    H = w_hh.shape[1]
+    gx = torch.matmul(x, w_ih.t()) + b_ih + b_hh
+    lens_t = torch.as_tensor(np.asarray(lens), dtype=torch.long)
+    order = list(range(T - 1, -1, -1)) if reverse else list(range(T))
+    h = x.new_zeros(B, H)
+    c = x.new_zeros(B, H)
+    y = x.new_zeros(B, T, H)
+    saved = [None] * T
+    for t in order:
+        g = gx[:, t] + h @ w_hh.t()
+        i, f, gg, o = torch.sigmoid(g[:, :H]), torch.sigmoid(g[:, H:2 * H]), \
+            torch.tanh(g[:, 2 * H:3 * H]), torch.sigmoid(g[:, 3 * H:])
+        c_new = f * c + i * gg
+        tc = torch.tanh(c_new)
+        act = (lens_t > t).to(x.dtype).unsqueeze(1)
+        saved[t] = (h, c, i, f, gg, o, tc, act)
+        h = o * tc * act
+        c = c_new * act
+        y[:, t] = h
+    dgx = torch.zeros_like(gx)
+    dw_hh = torch.zeros_like(w_hh)
+    dh = x.new_zeros(B, H)
+    dc = x.new_zeros(B, H)
+    for t in reversed(order):
+        h_prev, c_prev, i, f, gg, o, tc, act = saved[t]
+        dh_t = (dy[:, t] + dh) * act
+        dc_t = dc * act + dh_t * o * (1 - tc * tc)
+        d_o = dh_t * tc * o * (1 - o)
+        d_i = dc_t * gg * i * (1 - i)
+        d_g = dc_t * i * (1 - gg * gg)
+        d_f = dc_t * c_prev * f * (1 - f)
+        dg = torch.cat([d_i, d_f, d_g, d_o], dim=1)
+        dgx[:, t] = dg
+        dw_hh += dg.t() @ h_prev
+        dh = dg @ w_hh
+        dc = dc_t * f
+    dx = torch.matmul(dgx, w_ih)
+    dw_ih = torch.einsum('btg,btd->gd', dgx, x)
+    db = dgx.sum(dim=(0, 1))
+    return y, dx, dw_ih, dw_hh, db
+
+
 def vgg_front(p, prefix, cfg, xs, x_lens, masks=None, training=True):
     """CNNEncoder.forward (encoders/cnn.py:124-165) with relu, 3x3 / stride 1 /
     padding 1 convs, max-pool (first floor mode, later ceil mode), BatchNorm2d
@@ -140,6 +192,15 @@ def blstm_encoder(p, prefix, cfg, xs, x_lens, capture_layer=0):
     return xs, lens.astype(np.int32), perm.astype(np.int64)
 
 
+def _param_dtype(p):
+    """The parameters' float dtype (float64 evaluates the whole restatement in
+    double: bench.py's parity reference)."""
+    for k, v in p.items():
+        if k.endswith('weight') and torch.is_tensor(v):
+            return v.dtype
+    return torch.float32
+
+
 def linear_nd(p, name, x):
     """LinearND (linear.py:32-47): affine on the last dim (dropout = 0)."""
     y = torch.matmul(x, p[name + '.fc.weight'].t())
@@ -185,7 +246,7 @@ def hierarchical_ctc_loss(p, cfg, xs, ys, x_lens, y_lens, ys_sub, y_lens_sub):
     """HierarchicalCTC.forward (hierarchical_ctc.py:267-365): word CTC on the top
     layer, char CTC on the output of layer num_layers_sub (after its dropout,
     before any subsampling, rnn.py:400-407); loss = w_main L_main + w_sub L_sub."""
-    xs_t = torch.from_numpy(np.asarray(xs, np.float32))
+    xs_t = torch.from_numpy(np.asarray(xs, np.float32)).to(_param_dtype(p))
     top, lens, perm, (mid, lens_sub) = blstm_encoder(p, 'encoder.', dict(cfg, fast=False), xs_t,
                                                      x_lens, capture_layer=cfg['num_layers_sub'])
     B = xs.shape[0]
@@ -203,7 +264,7 @@ def hierarchical_ctc_loss(p, cfg, xs, ys, x_lens, y_lens, ys_sub, y_lens_sub):
 
 def ctc_model_loss(p, cfg, xs, ys, x_lens, y_lens):
     """CTC.forward (ctc.py:272-342).  xs numpy [B,T,F]; ys numpy [B,L] pad -1."""
-    xs_t = torch.from_numpy(np.asarray(xs, np.float32))
+    xs_t = torch.from_numpy(np.asarray(xs, np.float32)).to(_param_dtype(p))
     out, out_lens, perm = blstm_encoder(p, 'encoder.', cfg, xs_t, x_lens)
     h = out
     for i in range(len(cfg.get('fc_list', []))):
@@ -358,7 +419,7 @@ def attention_model_loss(p, cfg, xs, ys, x_lens, y_lens, train=None):
     bahdanau order, location attention, 1 head, LSTM decoder, forward
     direction only (backward_loss_weight = 0), encoder dropout 0:
     loss = (1 - w_bwd) * XE + lambda * CTC / B.  `train`: see attention_xe."""
-    xs_t = torch.from_numpy(np.asarray(xs, np.float32))
+    xs_t = torch.from_numpy(np.asarray(xs, np.float32)).to(_param_dtype(p))
     enc_out, enc_lens, perm = blstm_encoder(p, 'encoder.', _enc_cfg(cfg), xs_t, x_lens)
     B = enc_out.shape[0]
     loss = attention_xe(p, cfg, enc_out, enc_lens, ys, y_lens, perm, 0, train)
@@ -377,7 +438,7 @@ def hierarchical_attention_loss(p, cfg, xs, ys, x_lens, y_lens, ys_sub, y_lens_s
     382-567): word decoder on the top layer, character decoder (task 1) on layer
     encoder_num_layers_sub (after its dropout, before projection / subsampling),
     optional character CTC there.  Returns (loss, loss_main, loss_sub)."""
-    xs_t = torch.from_numpy(np.asarray(xs, np.float32))
+    xs_t = torch.from_numpy(np.asarray(xs, np.float32)).to(_param_dtype(p))
     top, lens, perm, (mid, lens_sub) = blstm_encoder(
         p, 'encoder.', dict(_enc_cfg(cfg), fast=False), xs_t, x_lens,
         capture_layer=cfg['encoder_num_layers_sub'])
@@ -406,7 +467,7 @@ def attention_greedy_decode(p, cfg, xs, x_lens, max_len):
     input is embed(argmax logits_{t-1}) (torch.max, first maximum); the loop
     stops after the first step at which every utterance emits <eos>.  Returns
     (best_hyps int64 [B, T_out], aw [B, T_out, T], perm) in sorted order."""
-    xs_t = torch.from_numpy(np.asarray(xs, np.float32))
+    xs_t = torch.from_numpy(np.asarray(xs, np.float32)).to(_param_dtype(p))
     enc_cfg = dict(num_layers=cfg['encoder_num_layers'], subsample_list=cfg['subsample_list'])
     with torch.no_grad():
         enc_out, enc_lens, perm = blstm_encoder(p, 'encoder.', enc_cfg, xs_t, x_lens)

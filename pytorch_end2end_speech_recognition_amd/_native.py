@@ -58,6 +58,9 @@ SIGNATURES = {
     'asr_optim_step': (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_ll, c_float, c_float, c_float,
                                c_float, c_float, c_ll, c_float, c_float, c_vp, c_float, c_vp,
                                c_vp]),
+    'asr_optim_step_guarded': (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_ll, c_float, c_float,
+                                       c_float, c_float, c_float, c_ll, c_float, c_float, c_vp,
+                                       c_float, c_vp, c_vp, c_vp]),
     'asr_dropout': (c_int, [c_vp, c_vp, c_ll, c_float, ctypes.c_ulonglong, c_vp]),
     'asr_embedding_forward': (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp]),
     'asr_embedding_backward': (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp,
@@ -117,6 +120,15 @@ SIGNATURES = {
     'asr_prof_begin': (c_int, [c_int]),
     'asr_prof_end': (c_int, [c_vp, c_vp, c_vp, c_int]),
     'asr_lstm_persist_status': (c_int, [c_vp, c_int, c_vp]),
+    'asr_lstm_status_gather': (c_int, [c_vp, c_int, c_vp]),
+    'asr_lstm_status_inject': (c_int, [c_int, c_vp]),
+    'asr_attdec_last_launch': (c_int, [c_vp]),
+    'asr_lstm_cell_forward': (c_int, [c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
+    'asr_lstm_cell_backward': (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp,
+                                       c_vp]),
+    'asr_att_step_workspace_bytes': (c_size, [c_vp]),
+    'asr_att_step_forward': (c_int, [c_vp] + [c_vp] * 12 + [c_size, c_vp]),
+    'asr_att_step_backward': (c_int, [c_vp] + [c_vp] * 21 + [c_size, c_vp]),
     'asr_lstm_xg_mode': (c_int, [c_vp, c_int]),
     'asr_xg_trace_read': (c_ll, [c_vp]),
 }

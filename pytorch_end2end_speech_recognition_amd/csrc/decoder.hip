@@ -1139,6 +1139,11 @@ extern "C" int asr_attdec_forward(const asr_attdec_dims_t* dims, int compute_dty
                                ctx_all, aw_all, workspace, ws_bytes, stream);
 }
 
+// Which attention-step instantiations the last forward / backward launched:
+// {forward channel template (10, 3 or 0 = generic), forward frame chunks,
+//  backward channel template, backward frame chunks} (host-side record).
+static int g_att_last[4];
+
 extern "C" int asr_attdec_forward_ex(const asr_attdec_dims_t* dims, const asr_attdec_opts_t* opts,
                                      int compute_dtype, const float* enc, const float* enc_a,
                                      const int32_t* lens, const float* w_ih_ctx, long long ld_ih,
@@ -1184,6 +1189,8 @@ extern "C" int asr_attdec_forward_ex(const asr_attdec_dims_t* dims, const asr_at
   const size_t ss_lds = ss ? ((size_t)d.D + d.E + opts->Dz + opts->Y + 2 * (SS_THREADS / 64)) * 4
                           : 0;
   ASR_REQUIRE(ss_lds <= 160 * 1024, ASR_ERR_UNSUPPORTED, "attdec: sampling LDS %zu B", ss_lds);
+  g_att_last[0] = (d.C == 10 || d.C == 3) ? d.C : 0;
+  g_att_last[1] = (int)eg.x;
   for (int t = 0; t < d.S; ++t) {
     if (t > 0) {
       const bool smp = ss && opts->ss_steps_host[t] != 0;
@@ -1217,6 +1224,12 @@ extern "C" int asr_attdec_forward_ex(const asr_attdec_dims_t* dims, const asr_at
                        ctx_all, x);
     ASR_LAUNCH_CHECK();
   }
+  return ASR_OK;
+}
+
+extern "C" int asr_attdec_last_launch(int* out4) {
+  ASR_REQUIRE(out4, ASR_ERR_ARG, "attdec_last_launch: null pointer");
+  for (int i = 0; i < 4; ++i) out4[i] = g_att_last[i];
   return ASR_OK;
 }
 
@@ -1315,6 +1328,8 @@ extern "C" int asr_attdec_backward_ex(const asr_attdec_dims_t* dims, const asr_a
   const int vec = (G % 8 == 0) ? 1 : 0;
   const long long nbd = (long long)d.B * d.D;
   const int cgrid = (int)((nbd + 255) / 256);
+  g_att_last[2] = (d.C == 10 || d.C == 3) ? d.C : 0;
+  g_att_last[3] = (int)eg.x;
   for (int t = d.S - 1; t >= 0; --t) {
     const float* rp = nullptr;
     if (t + 1 < d.S) {   // r = dgates_{t+1} @ Wcat: d [ctx_t; h_t] through step t+1's cell
@@ -1355,5 +1370,203 @@ extern "C" int asr_attdec_backward_ex(const asr_attdec_dims_t* dims, const asr_a
                        opts->dg_ss);
     ASR_LAUNCH_CHECK();
   }
+  return ASR_OK;
+}
+
+// ---------------------------------------------------------------------------
+// One location-attention step as a standalone op: AttentionMechanism.forward
+// (attention_layer.py:123-251) -- the layer-level boundary, for callers that
+// drive the decoder themselves (decode loops, visualisation).  The training
+// loop runs the same kernels inside asr_attdec_forward_ex / _backward_ex.
+//
+// The step is launched as step t = 1 of a two-step layout in the workspace:
+// slot 0 holds aw_{t-1} (the caller's aw_step), slot 1 dec_out / the outputs,
+// so the kernels run unchanged (their aw_{t-1} read, masks, chunked partials).
+// ---------------------------------------------------------------------------
+namespace {
+struct StepWs {
+  size_t dec2, aw2, ctx2, dctx2, dtot2, wd2, dwd2, ebuf, carry, ddec, dF, dwdc, total;
+};
+StepWs step_ws(const Dims& d) {   // d.S == 2
+  StepWs w;
+  size_t o = 0;
+  w.dec2 = o; o += al256((size_t)d.B * 2 * d.D * 4);
+  w.aw2 = o; o += al256((size_t)d.B * 2 * d.T * 4);
+  w.ctx2 = o; o += al256((size_t)d.B * 2 * d.E * 4);
+  w.dctx2 = o; o += al256((size_t)d.B * 2 * d.E * 4);
+  w.dtot2 = o; o += al256((size_t)d.B * 2 * d.E * 4);
+  w.wd2 = o; o += al256((size_t)d.B * 2 * d.A * 4);
+  w.dwd2 = o; o += al256((size_t)d.B * 2 * d.A * 4);
+  w.ebuf = o; o += al256((size_t)d.B * d.T * 4);
+  w.carry = o; o += al256((size_t)d.B * d.T * 4);
+  w.ddec = o; o += al256((size_t)d.B * d.D * 4);
+  w.dF = o; o += al256((size_t)d.B * d.T * d.C * 4);
+  w.dwdc = o; o += al256((size_t)d.B * att_chunks(d) * d.A * 4);
+  w.total = o;
+  return w;
+}
+
+Dims step_dims(const asr_attdec_dims_t* dims) {
+  Dims d = to_dims(*dims);
+  d.S = 2;
+  return d;
+}
+
+// rows [B][n] <-> slot `slot` of a [B][2][n] layout
+hipError_t to_slot(float* dst2, int slot, const float* src, int B, int n, hipStream_t s) {
+  return hipMemcpy2DAsync(dst2 + (size_t)slot * n, 2 * n * 4, src, n * 4, n * 4, B,
+                          hipMemcpyDeviceToDevice, s);
+}
+hipError_t from_slot(float* dst, const float* src2, int slot, int B, int n, hipStream_t s) {
+  return hipMemcpy2DAsync(dst, n * 4, src2 + (size_t)slot * n, 2 * n * 4, n * 4, B,
+                          hipMemcpyDeviceToDevice, s);
+}
+}  // namespace
+
+extern "C" size_t asr_att_step_workspace_bytes(const asr_attdec_dims_t* dims) {
+  return step_ws(step_dims(dims)).total;
+}
+
+extern "C" int asr_att_step_forward(const asr_attdec_dims_t* dims, const float* enc,
+                                    const float* enc_a, const int32_t* lens, const float* w_dec,
+                                    const float* w_conv, const float* conv_w, const float* v,
+                                    const float* dec_out, const float* aw_prev, float* ctx_out,
+                                    float* aw_out, void* workspace, size_t ws_bytes,
+                                    void* stream) {
+  ASR_REQUIRE(dims, ASR_ERR_ARG, "att_step: dims is null");
+  const Dims d = step_dims(dims);
+  int rc = check_dims(d);
+  if (rc) return rc;
+  ASR_REQUIRE(enc && enc_a && lens && w_dec && w_conv && conv_w && v && dec_out && aw_prev &&
+                  ctx_out && aw_out && workspace,
+              ASR_ERR_ARG, "att_step_forward: null pointer");
+  const StepWs W = step_ws(d);
+  ASR_REQUIRE(ws_bytes >= W.total, ASR_ERR_WORKSPACE, "att_step_forward: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  char* p = (char*)workspace;
+  float* dec2 = (float*)(p + W.dec2);
+  float* aw2 = (float*)(p + W.aw2);
+  float* ctx2 = (float*)(p + W.ctx2);
+  float* ebuf = (float*)(p + W.ebuf);
+  ASR_CHECK_HIP(to_slot(dec2, 1, dec_out, d.B, d.D, s));
+  ASR_CHECK_HIP(to_slot(aw2, 0, aw_prev, d.B, d.T, s));
+  const size_t en_lds = en_lds_floats(d) * 4;
+  const size_t cx_lds = ((size_t)d.T + 64 + ATT_THREADS) * 4;
+  const dim3 eg(att_chunks(d), d.B), xg(ceil_div(d.E, ECH), d.B);
+  const int t = 1;
+  if (d.C == 10)
+    hipLaunchKernelGGL(att_energy<10>, eg, dim3(ATT_THREADS), en_lds, s, t, d, enc_a, lens, w_dec,
+                       w_conv, conv_w, v, dec2, aw2, ebuf);
+  else if (d.C == 3)
+    hipLaunchKernelGGL(att_energy<3>, eg, dim3(ATT_THREADS), en_lds, s, t, d, enc_a, lens, w_dec,
+                       w_conv, conv_w, v, dec2, aw2, ebuf);
+  else
+    hipLaunchKernelGGL(att_energy<0>, eg, dim3(ATT_THREADS), en_lds, s, t, d, enc_a, lens, w_dec,
+                       w_conv, conv_w, v, dec2, aw2, ebuf);
+  ASR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(att_context, xg, dim3(ATT_THREADS), cx_lds, s, t, d, enc, ebuf, aw2, ctx2,
+                     (float*)nullptr);
+  ASR_LAUNCH_CHECK();
+  ASR_CHECK_HIP(from_slot(aw_out, aw2, 1, d.B, d.T, s));
+  ASR_CHECK_HIP(from_slot(ctx_out, ctx2, 1, d.B, d.E, s));
+  return ASR_OK;
+}
+
+// Backward of asr_att_step_forward.  Inputs: the forward's operands, its aw_out,
+// the cotangents d_ctx [B][E] and d_aw_out [B][T] (nullable).  Outputs (all
+// written, none accumulated): d_enc_a [B][T][A], d_dec [B][D], d_aw_prev [B][T],
+// dctx_tot [B][E] (= d_ctx: d enc = aw_out^T dctx_tot is the caller's GEMM),
+// dwd [B][A] (d of W_dec dec_out: dW_dec = dwd^T dec_out), and per
+// (utterance, frame chunk) partials dv_part [B*NC][A], dwc_part [B*NC][A*C],
+// dcw_part [B*NC][C*K] whose column sums are dV, dW_conv, d conv kernel
+// (NC = asr_attdec_chunks).
+extern "C" int asr_att_step_backward(const asr_attdec_dims_t* dims, const float* enc,
+                                     const float* enc_a, const int32_t* lens, const float* w_dec,
+                                     const float* w_conv, const float* conv_w, const float* v,
+                                     const float* dec_out, const float* aw_prev,
+                                     const float* aw_out, const float* d_ctx,
+                                     const float* d_aw_out, float* d_enc_a, float* d_dec,
+                                     float* d_aw_prev, float* dctx_tot, float* dwd,
+                                     float* dv_part, float* dwc_part, float* dcw_part,
+                                     void* workspace, size_t ws_bytes, void* stream) {
+  ASR_REQUIRE(dims, ASR_ERR_ARG, "att_step: dims is null");
+  const Dims d = step_dims(dims);
+  int rc = check_dims(d);
+  if (rc) return rc;
+  ASR_REQUIRE(enc && enc_a && lens && w_dec && w_conv && conv_w && v && dec_out && aw_prev &&
+                  aw_out && d_ctx && d_enc_a && d_dec && d_aw_prev && dctx_tot && dwd &&
+                  dv_part && dwc_part && dcw_part && workspace,
+              ASR_ERR_ARG, "att_step_backward: null pointer");
+  const StepWs W = step_ws(d);
+  ASR_REQUIRE(ws_bytes >= W.total, ASR_ERR_WORKSPACE, "att_step_backward: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  char* p = (char*)workspace;
+  float* dec2 = (float*)(p + W.dec2);
+  float* aw2 = (float*)(p + W.aw2);
+  float* dctx2 = (float*)(p + W.dctx2);
+  float* dtot2 = (float*)(p + W.dtot2);
+  float* wd2 = (float*)(p + W.wd2);
+  float* dwd2 = (float*)(p + W.dwd2);
+  float* dawbuf = (float*)(p + W.ebuf);
+  float* carry = (float*)(p + W.carry);
+  float* dFbuf = (float*)(p + W.dF);
+  float* dwd_chunk = (float*)(p + W.dwdc);
+  const int NC = att_chunks(d);
+  ASR_CHECK_HIP(hipMemsetAsync(dec2, 0, (size_t)d.B * 2 * d.D * 4, s));
+  ASR_CHECK_HIP(to_slot(dec2, 1, dec_out, d.B, d.D, s));
+  ASR_CHECK_HIP(to_slot(aw2, 0, aw_prev, d.B, d.T, s));
+  ASR_CHECK_HIP(to_slot(aw2, 1, aw_out, d.B, d.T, s));
+  ASR_CHECK_HIP(to_slot(dctx2, 1, d_ctx, d.B, d.E, s));
+  if (d_aw_out)   // d aw_t enters where the loop's next step would have put its conv term
+    ASR_CHECK_HIP(hipMemcpyAsync(carry, d_aw_out, (size_t)d.B * d.T * 4, hipMemcpyDeviceToDevice,
+                                 s));
+  else
+    ASR_CHECK_HIP(hipMemsetAsync(carry, 0, (size_t)d.B * d.T * 4, s));
+  ASR_CHECK_HIP(hipMemsetAsync(d_enc_a, 0, (size_t)d.B * d.T * d.A * 4, s));
+  // the partial rows of slot 0 are never written: the caller sums all rows
+  const size_t prow = (size_t)d.B * 2 * NC;
+  ASR_CHECK_HIP(hipMemsetAsync(dv_part, 0, prow * d.A * 4, s));
+  ASR_CHECK_HIP(hipMemsetAsync(dwc_part, 0, prow * d.A * d.C * 4, s));
+  ASR_CHECK_HIP(hipMemsetAsync(dcw_part, 0, prow * d.C * d.K * 4, s));
+  {  // W_dec dec (exact-f32 MFMA, as the decoder backward)
+    asr_gemm_t g;
+    memset(&g, 0, sizeof(g));
+    g.a.ptr = dec2;
+    g.a.dtype = ASR_DT_F32;
+    g.a.map.stride_t = d.D;
+    g.b.ptr = w_dec;
+    g.b.dtype = ASR_DT_F32;
+    g.b.map.stride_t = d.D;
+    g.c = wd2;
+    g.c_map.stride_t = d.A;
+    g.M = d.B * 2; g.N = d.A; g.K = d.D;
+    g.alpha = 1.f; g.beta = 0.f; g.batch = 1;
+    rc = asr_gemm(&g, 1, ASR_DT_F32, stream);
+    if (rc) return rc;
+  }
+  const size_t en_lds = en_lds_floats(d) * 4;
+  const size_t cv_lds = conv_lds_floats(d) * 4;
+  const size_t dw_lds = (size_t)d.E * 4;
+  const dim3 eg(NC, d.B);
+  const int t = 1;
+  hipLaunchKernelGGL(att_bwd_daw, eg, dim3(ATT_THREADS), dw_lds, s, t, d, enc, dctx2,
+                     (const float*)nullptr, carry, dtot2, dawbuf);
+  ASR_LAUNCH_CHECK();
+#define ASR_STEP_BWD_EN(CC)                                                                    \
+  hipLaunchKernelGGL(att_bwd_energy<CC>, eg, dim3(ATT_THREADS), en_lds, s, t, d, enc_a, lens,    \
+                     w_dec, w_conv, conv_w, v, dec2, aw2, dawbuf, wd2, d_enc_a, dFbuf, dwd_chunk, \
+                     dv_part, dwc_part)
+  if (d.C == 10) ASR_STEP_BWD_EN(10);
+  else if (d.C == 3) ASR_STEP_BWD_EN(3);
+  else ASR_STEP_BWD_EN(0);
+#undef ASR_STEP_BWD_EN
+  ASR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(att_bwd_conv, eg, dim3(ATT_THREADS), cv_lds, s, t, d, conv_w, aw2, dFbuf,
+                     w_dec, dwd_chunk, carry, dcw_part, dwd2, d_dec);
+  ASR_LAUNCH_CHECK();
+  ASR_CHECK_HIP(hipMemcpyAsync(d_aw_prev, carry, (size_t)d.B * d.T * 4, hipMemcpyDeviceToDevice,
+                               s));
+  ASR_CHECK_HIP(from_slot(dctx_tot, dtot2, 1, d.B, d.E, s));
+  ASR_CHECK_HIP(from_slot(dwd, dwd2, 1, d.B, d.A, s));
   return ASR_OK;
 }

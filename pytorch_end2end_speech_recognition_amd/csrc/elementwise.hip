@@ -271,3 +271,73 @@ extern "C" int asr_convert_rows_bf16(const float* src, asr_rowmap_t map, int nro
                                      uint16_t* dst, void* stream) {
   return asr_convert_rows_bf16_ld(src, map, nrows, ncols, ncols, dst, stream);
 }
+
+// ---------------------------------------------------------------------------
+// nn.LSTMCell nonlinearity (RNNDecoder.forward's cell, rnn_decoder.py:80-86;
+// gate order i, f, g, o): pre [B][4D] = x W_ih^T + b_ih + h W_hh^T + b_hh (the
+// caller's GEMM) -> c = sig(f) c_prev + sig(i) tanh(g), h = sig(o) tanh(c);
+// act [B][4D] keeps the activated gates for the backward.
+// ---------------------------------------------------------------------------
+namespace {
+__global__ void lstm_cell_fwd(const float* __restrict__ pre, const float* __restrict__ c_prev,
+                              int B, int D, float* __restrict__ act, float* __restrict__ h,
+                              float* __restrict__ c) {
+  const long long n = (long long)B * D;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long b = i / D, j = i % D, g0 = b * 4 * D + j;
+    const float ig = sigmoidf_(pre[g0]), fg = sigmoidf_(pre[g0 + D]);
+    const float gg = tanhf_(pre[g0 + 2 * D]), og = sigmoidf_(pre[g0 + 3 * D]);
+    const float cc = fg * (c_prev ? c_prev[i] : 0.f) + ig * gg;
+    c[i] = cc;
+    h[i] = og * tanhf_(cc);
+    act[g0] = ig;
+    act[g0 + D] = fg;
+    act[g0 + 2 * D] = gg;
+    act[g0 + 3 * D] = og;
+  }
+}
+
+__global__ void lstm_cell_bwd(const float* __restrict__ act, const float* __restrict__ c_prev,
+                              const float* __restrict__ c, const float* __restrict__ dh,
+                              const float* __restrict__ dc, int B, int D,
+                              float* __restrict__ dpre, float* __restrict__ dc_prev) {
+  const long long n = (long long)B * D;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long b = i / D, j = i % D, g0 = b * 4 * D + j;
+    const float ig = act[g0], fg = act[g0 + D], gg = act[g0 + 2 * D], og = act[g0 + 3 * D];
+    const float tc = tanhf_(c[i]);
+    const float dhv = dh ? dh[i] : 0.f;
+    const float dct = (dc ? dc[i] : 0.f) + dhv * og * (1.f - tc * tc);
+    const float cp = c_prev ? c_prev[i] : 0.f;
+    dpre[g0] = dct * gg * ig * (1.f - ig);
+    dpre[g0 + D] = dct * cp * fg * (1.f - fg);
+    dpre[g0 + 2 * D] = dct * ig * (1.f - gg * gg);
+    dpre[g0 + 3 * D] = dhv * tc * og * (1.f - og);
+    if (dc_prev) dc_prev[i] = dct * fg;
+  }
+}
+}  // namespace
+
+extern "C" int asr_lstm_cell_forward(const float* pre, const float* c_prev, int B, int D,
+                                     float* act, float* h, float* c, void* stream) {
+  ASR_REQUIRE(pre && act && h && c && B > 0 && D > 0, ASR_ERR_ARG, "lstm_cell: bad arguments");
+  const long long n = (long long)B * D;
+  hipLaunchKernelGGL(lstm_cell_fwd, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, pre,
+                     c_prev, B, D, act, h, c);
+  ASR_LAUNCH_CHECK();
+  return ASR_OK;
+}
+
+extern "C" int asr_lstm_cell_backward(const float* act, const float* c_prev, const float* c,
+                                      const float* dh, const float* dc, int B, int D, float* dpre,
+                                      float* dc_prev, void* stream) {
+  ASR_REQUIRE(act && c && dpre && B > 0 && D > 0, ASR_ERR_ARG,
+              "lstm_cell_backward: bad arguments");
+  const long long n = (long long)B * D;
+  hipLaunchKernelGGL(lstm_cell_bwd, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, act,
+                     c_prev, c, dh, dc, B, D, dpre, dc_prev);
+  ASR_LAUNCH_CHECK();
+  return ASR_OK;
+}

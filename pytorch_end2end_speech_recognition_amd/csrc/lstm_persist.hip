@@ -431,6 +431,7 @@ int lstm_bwd_persistent(int B, int T, int H, const int32_t* lens, const uint16_t
 
 namespace asr {
 int lstm_xg_status(int* status, int clear, hipStream_t s);  // lstm_xg.hip
+int* lstm_xg_status_word();                                  // lstm_xg.hip
 }
 
 using namespace asr;
@@ -449,5 +450,35 @@ extern "C" int asr_lstm_persist_status(int* status, int clear, void* stream) {
   }
   ASR_REQUIRE(lstm_xg_status(status, clear, s) == 0, ASR_ERR_HIP,
               "persist_status: tagged-granule status read failed");
+  return ASR_OK;
+}
+
+// Stream-ordered, sync-free form for the training step: dst[0] = the counter
+// form's status word, dst[1] = the tagged-granule form's, copied device to
+// device after the recurrences that precede it on the stream; clear = 1 then
+// zeroes both words (also stream-ordered).  dst feeds asr_optim_step_guarded
+// (directly, or after a MAX all-reduce over the data-parallel ranks).
+extern "C" int asr_lstm_status_gather(int* dst, int clear, void* stream) {
+  ASR_REQUIRE(dst, ASR_ERR_ARG, "status_gather: null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  int* xg = lstm_xg_status_word();
+  void* pp = nullptr;
+  ASR_REQUIRE(xg, ASR_ERR_HIP, "status_gather: no tagged-granule status word");
+  ASR_CHECK_HIP(hipGetSymbolAddress(&pp, HIP_SYMBOL(g_persist_status)));
+  ASR_CHECK_HIP(hipMemcpyAsync(dst, pp, sizeof(int), hipMemcpyDeviceToDevice, s));
+  ASR_CHECK_HIP(hipMemcpyAsync(dst + 1, xg, sizeof(int), hipMemcpyDeviceToDevice, s));
+  if (clear) {
+    ASR_CHECK_HIP(hipMemsetAsync(pp, 0, sizeof(int), s));
+    ASR_CHECK_HIP(hipMemsetAsync(xg, 0, sizeof(int), s));
+  }
+  return ASR_OK;
+}
+
+// Test hook: mark the tagged-granule recurrence as having given up (what a
+// bounded spin that ran out does), stream-ordered.
+extern "C" int asr_lstm_status_inject(int bits, void* stream) {
+  int* xg = lstm_xg_status_word();
+  ASR_REQUIRE(xg, ASR_ERR_HIP, "status_inject: no tagged-granule status word");
+  ASR_CHECK_HIP(hipMemsetAsync(xg, bits & 0xff, 1, (hipStream_t)stream));
   return ASR_OK;
 }

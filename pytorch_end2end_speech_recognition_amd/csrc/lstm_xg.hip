@@ -856,6 +856,13 @@ int lstm_xg_status(int* status, int clear, hipStream_t s) {
   return 0;
 }
 
+// Device address of g_xg_status (stream-ordered gathers and clears, no host sync).
+int* lstm_xg_status_word() {
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_xg_status)) != hipSuccess) return nullptr;
+  return (int*)p;
+}
+
 }  // namespace asr
 
 // Diagnostics: copy the phase-timestamp trace (ASR_XG_TRACE=1) to host memory

@@ -68,7 +68,10 @@ __device__ __forceinline__ float clip_coef(const float* sqnorm, float max_norm) 
 __global__ void optim_step_kernel(float* __restrict__ p, const float* __restrict__ g,
                                   float* __restrict__ m, float* __restrict__ v, long long n,
                                   StepArgs a, const float* __restrict__ sqnorm,
-                                  uint16_t* __restrict__ shadow) {
+                                  uint16_t* __restrict__ shadow, const int* __restrict__ guard) {
+  // guard: the step's recurrence status words (asr_lstm_status_gather); a
+  // bounded spin that gave up invalidated the gradients -> no update at all
+  if (guard && (guard[0] | guard[1])) return;
   const float coef = clip_coef(sqnorm, a.max_norm);
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -115,11 +118,12 @@ extern "C" int asr_grad_sqnorm(const float* g, long long n, float* out, void* wo
   return ASR_OK;
 }
 
-extern "C" int asr_optim_step(int kind, float* params, const float* grads, float* m, float* v,
-                              long long n, float lr, float beta1, float beta2, float eps,
-                              float weight_decay, long long step, float momentum,
-                              float dampening, const float* grad_sqnorm, float max_norm,
-                              uint16_t* bf16_shadow, void* stream) {
+extern "C" int asr_optim_step_guarded(int kind, float* params, const float* grads, float* m,
+                                      float* v, long long n, float lr, float beta1, float beta2,
+                                      float eps, float weight_decay, long long step,
+                                      float momentum, float dampening, const float* grad_sqnorm,
+                                      float max_norm, uint16_t* bf16_shadow, const int* guard,
+                                      void* stream) {
   ASR_REQUIRE(params && grads, ASR_ERR_ARG, "optim_step: null pointer");
   ASR_REQUIRE(kind >= 0 && kind <= 3, ASR_ERR_ARG, "optim_step: bad kind %d", kind);
   ASR_REQUIRE(kind == 1 || m, ASR_ERR_ARG, "optim_step: state buffer m is null");
@@ -134,7 +138,17 @@ extern "C" int asr_optim_step(int kind, float* params, const float* grads, float
   const long long nb = (n + 255) / 256;
   const int blocks = (int)(nb < 8192 ? nb : 8192);
   hipLaunchKernelGGL(optim_step_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, params,
-                     grads, m, v, n, a, grad_sqnorm, bf16_shadow);
+                     grads, m, v, n, a, grad_sqnorm, bf16_shadow, guard);
   ASR_LAUNCH_CHECK();
   return ASR_OK;
+}
+
+extern "C" int asr_optim_step(int kind, float* params, const float* grads, float* m, float* v,
+                              long long n, float lr, float beta1, float beta2, float eps,
+                              float weight_decay, long long step, float momentum,
+                              float dampening, const float* grad_sqnorm, float max_norm,
+                              uint16_t* bf16_shadow, void* stream) {
+  return asr_optim_step_guarded(kind, params, grads, m, v, n, lr, beta1, beta2, eps,
+                                weight_decay, step, momentum, dampening, grad_sqnorm, max_norm,
+                                bf16_shadow, nullptr, stream);
 }

@@ -2,13 +2,19 @@
 
 Same constructor, submodule and parameter names (W_enc_head0, W_dec_head0,
 W_conv_head0, conv_head0 [Conv2d 1->C, (1, K)], V_head0) and the same torch RNG
-consumption, so state_dicts interchange.  The location-attention step itself
-runs inside the fused HIP decoder loop (native_ops.att_decoder, csrc/decoder.hip):
-conv over the previous weights, energy V.tanh(W_enc h_enc + W_dec h_dec +
-W_conv f), MULTIPLICATIVE length mask (:216-225), sharpening, softmax (or
-sigmoid smoothing) and the context vector, fused in one kernel per step.
+consumption, so state_dicts interchange.  In training the location-attention
+step runs inside the fused HIP decoder loop (native_ops.att_decoder,
+csrc/decoder.hip); ``forward`` is the same step as a standalone op
+(native_ops.att_step: the loop's kernels launched for one step): conv over the
+previous weights, energy V.tanh(W_enc h_enc + W_dec h_dec + W_conv f),
+MULTIPLICATIVE length mask (:216-225), sharpening, softmax (or sigmoid
+smoothing) and the context vector, with a HIP backward.
 """
+import numpy as np
+import torch
 import torch.nn as nn
+
+from .... import native_ops as ops
 
 from ..linear import LinearND
 
@@ -45,5 +51,20 @@ class AttentionMechanism(nn.Module):
         self.V_head0 = LinearND(attention_dim, 1, bias=False)
 
     def forward(self, enc_out, enc_out_a, x_lens, dec_out, aw_step):
-        raise NotImplementedError('the location-attention step runs inside the fused decoder '
-                                  'loop (AttentionSeq2seq._decode_train)')
+        """attention_layer.py:123-251 (location, one head).
+        enc_out [B, T, E]; enc_out_a [B, T, A, 1] = W_enc(enc_out) (the caller's
+        hoisted projection, attention_seq2seq.py:735-739); x_lens [B] (tensor,
+        list or array); dec_out [B, 1, D]; aw_step [B, T, 1] (the previous
+        step's weights).  Returns (context_vec [B, 1, E], aw_step [B, T, 1])."""
+        B, T, E = enc_out.shape
+        dev = enc_out.device
+        if torch.is_tensor(x_lens):
+            lens = x_lens.reshape(-1).to(device=dev, dtype=torch.int32)
+        else:
+            lens = torch.from_numpy(np.asarray(x_lens, np.int32).reshape(-1)).to(dev)
+        ctx, aw = ops.att_step(enc_out, enc_out_a.reshape(B, T, -1), lens,
+                               dec_out.reshape(B, -1), aw_step.reshape(B, T),
+                               self.W_dec_head0.fc.weight, self.W_conv_head0.fc.weight,
+                               self.conv_head0.weight, self.V_head0.fc.weight,
+                               self.sharpening_factor, self.sigmoid_smoothing)
+        return ctx.unsqueeze(1), aw.unsqueeze(2)

@@ -106,6 +106,8 @@ class AttentionSeq2seq(ModelBase):
             unsupported.append('bridge layer / cnn encoder')
         if coverage_weight != 0:
             unsupported.append('coverage')
+        if decoder_num_layers != 1 or decoder_residual or decoder_dense_residual:
+            unsupported.append('multi-layer / residual decoder in the fused training loop')
         if unsupported:
             raise NotImplementedError('MI355X AttentionSeq2seq: not yet supported: ' +
                                       ', '.join(unsupported))

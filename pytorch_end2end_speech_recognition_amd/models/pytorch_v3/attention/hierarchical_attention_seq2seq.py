@@ -91,6 +91,9 @@ class HierarchicalAttentionSeq2seq(AttentionSeq2seq):
         self.encoder_num_units_sub = self.encoder_num_units
         self.decoder_num_units_1 = decoder_num_units_sub
         self.decoder_num_layers_1 = decoder_num_layers_sub
+        if decoder_num_layers_sub != 1:
+            raise NotImplementedError('MI355X HierarchicalAttentionSeq2seq: multi-layer decoder '
+                                      'in the fused training loop')
         self.num_classes_sub = num_classes_sub + 1
         self.sos_1 = num_classes_sub
         self.eos_1 = num_classes_sub

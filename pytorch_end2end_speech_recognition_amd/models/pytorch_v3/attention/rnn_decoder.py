@@ -1,10 +1,16 @@
 """RNNDecoder (reference models/pytorch_v3/attention/rnn_decoder.py).
 
-Parameter holder with the reference's names (``lstm_l{l}.weight_ih`` ...);
-the LSTMCell step is fused into the HIP decoder loop (csrc/decoder.hip
-cell_fwd / cell_bwd).
+Same constructor, parameter names (``lstm_l{l}.weight_ih`` ...) and RNG
+consumption.  In training the 1-layer LSTMCell step is fused into the HIP
+decoder loop (csrc/decoder.hip cell_fwd / cell_bwd, AttentionSeq2seq);
+``forward`` is the reference's layer API (rnn_decoder.py:63-113) on the HIP
+GEMM (native_ops.linear2) + LSTM-cell kernels, for any number of layers,
+residual / dense-residual connections and dropout.
 """
+import torch
 import torch.nn as nn
+
+from .... import native_ops as ops
 
 
 class RNNDecoder(nn.Module):
@@ -12,8 +18,8 @@ class RNNDecoder(nn.Module):
     def __init__(self, input_size, rnn_type, num_units, num_layers, dropout, residual=False,
                  dense_residual=False):
         super(RNNDecoder, self).__init__()
-        if rnn_type != 'lstm' or num_layers != 1 or residual or dense_residual:
-            raise NotImplementedError('MI355X fused decoder: 1-layer LSTM decoder')
+        if rnn_type != 'lstm':
+            raise NotImplementedError('MI355X RNNDecoder: LSTM cells (GRU not yet provided)')
         self.input_size = input_size
         self.rnn_type = rnn_type
         self.num_units = num_units
@@ -28,4 +34,24 @@ class RNNDecoder(nn.Module):
             setattr(self, 'dropout_l' + str(l), nn.Dropout(p=dropout))
 
     def forward(self, dec_in, dec_state):
-        raise NotImplementedError('the decoder cell runs inside the fused decoder loop')
+        """rnn_decoder.py:63-113.  dec_in [B, 1, input_size]; dec_state =
+        (hx_list, cx_list), lists of [B, num_units] per layer (updated in place
+        like the reference).  Returns (dec_out [B, 1, num_units], dec_state)."""
+        hx_list, cx_list = dec_state
+        if torch.is_tensor(hx_list):
+            hx_list, cx_list = [hx_list], [cx_list]
+        x = dec_in.squeeze(1)
+        for l in range(self.num_layers):
+            cell = getattr(self, 'lstm_l' + str(l))
+            inp = x if l == 0 else hx_list[l - 1]
+            hx_list[l], cx_list[l] = ops.lstm_cell(inp, hx_list[l], cx_list[l], cell.weight_ih,
+                                                   cell.weight_hh, cell.bias_ih, cell.bias_hh)
+            if self.training and self.dropout > 0:
+                hx_list[l] = ops.dropout(hx_list[l], self.dropout)
+            if l > 0 and self.residual or self.dense_residual:     # rnn_decoder.py:100-104
+                if self.residual:
+                    hx_list[l] = ops.add(hx_list[l], hx_list[l - 1])
+                elif self.dense_residual:
+                    for lower in hx_list[:l]:
+                        hx_list[l] = ops.add(hx_list[l], lower)
+        return hx_list[-1].unsqueeze(1), (hx_list, cx_list)

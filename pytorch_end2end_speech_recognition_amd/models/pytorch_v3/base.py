@@ -326,7 +326,9 @@ class FlatOptimizer(torch.optim.Optimizer):
         return self._sq
 
     @torch.no_grad()
-    def step(self, closure=None, max_norm=0.0):
+    def step(self, closure=None, max_norm=0.0, guard=None):
+        """guard: optional device int32[2] (asr_lstm_status_gather words, MAX
+        over ranks); when nonzero the kernel leaves params and state alone."""
         loss = closure() if closure is not None else None
         self._step += 1
         g = self.param_groups[0]
@@ -334,14 +336,19 @@ class FlatOptimizer(torch.optim.Optimizer):
         sq = self.grad_norm_sq() if max_norm and max_norm > 0 else None
         N.require_device(p)
         b1, b2 = g['betas']
-        N.call('asr_optim_step', OPTIMIZER_KINDS[self.kind], N.ptr(p), N.ptr(gr), N.ptr(self.m),
-               N.ptr(self.v), p.numel(), float(g['lr']), float(b1), float(b2), float(g['eps']),
-               float(g['weight_decay']), self._step, float(g['momentum']), 0.0, N.ptr(sq),
-               float(max_norm or 0.0), None, N.stream_handle(p.device))
+        N.call('asr_optim_step_guarded', OPTIMIZER_KINDS[self.kind], N.ptr(p), N.ptr(gr),
+               N.ptr(self.m), N.ptr(self.v), p.numel(), float(g['lr']), float(b1), float(b2),
+               float(g['eps']), float(g['weight_decay']), self._step, float(g['momentum']), 0.0,
+               N.ptr(sq), float(max_norm or 0.0), None, N.ptr(guard), N.stream_handle(p.device))
         return loss
 
-    def clip_and_step(self, max_norm):
-        return self.step(max_norm=max_norm)
+    def clip_and_step(self, max_norm, guard=None):
+        return self.step(max_norm=max_norm, guard=guard)
+
+    def undo_step_count(self):
+        """A guarded step that did not update (skipped batch) must not advance
+        Adam's bias-correction count."""
+        self._step -= 1
 
     def state_dict(self):
         return {'kind': self.kind, 'step': self._step, 'lr': self.param_groups[0]['lr'],

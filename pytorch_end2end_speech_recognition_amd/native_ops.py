@@ -37,6 +37,40 @@ def _ws(nbytes, device):
     return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
 
 
+# Gradient-ready notifications for the data-parallel bucketed all-reduce
+# (utils/training/grad_buckets.py): 'recurrence' after a BLSTM layer's backward
+# recurrence is enqueued, ('grads', gbufs) once its weight gradients are.
+_grad_hook = [None]
+
+
+def set_grad_ready_hook(fn):
+    _grad_hook[0] = fn
+
+
+def notify_grad_event(event, arg=None):
+    fn = _grad_hook[0]
+    if fn is not None:
+        fn(event, arg)
+
+
+def recurrence_status(device):
+    """Device int32[2]: the persistent recurrences' give-up words since the
+    last call (cleared), stream-ordered, no host sync."""
+    st = torch.empty(2, dtype=torch.int32, device=device)
+    N.call('asr_lstm_status_gather', N.ptr(st), 1, N.stream_handle(device))
+    return st
+
+
+def raise_if_recurrence_failed(device=None):
+    """Host check (synchronises): NativeError when a persistent recurrence
+    gave up since the last gather (its outputs are invalid)."""
+    device = device or torch.device('cuda', torch.cuda.current_device())
+    st = recurrence_status(device)
+    if int(st.max().item()):
+        raise N.NativeError('persistent LSTM recurrence gave up a bounded wait (status %s): '
+                            'outputs of this pass are invalid' % st.tolist())
+
+
 def grad_buffer(p):
     """The gradient view a kernel accumulates into (allocated on first use)."""
     if p.grad is None:
@@ -462,6 +496,117 @@ class AttDecoderFn(torch.autograd.Function):
                 None, None, None)
 
 
+class AttStepFn(torch.autograd.Function):
+    """One location-attention step (AttentionMechanism.forward,
+    attention_layer.py:123-251) on the decoder loop's kernels:
+    (enc [B,T,E], enc_a [B,T,A], lens int32 [B], dec_out [B,D], aw_prev [B,T])
+    -> (ctx [B,E], aw [B,T]).  Weight gradients (W_dec [A,D], W_conv [A,C],
+    conv [C,1,1,K], V [1,A]) accumulate into their .grad."""
+
+    @staticmethod
+    def forward(ctx, enc, enc_a, lens, dec_out, aw_prev, w_dec, w_conv, conv_w, v, sharpen,
+                sigmoid):
+        N.require_device(enc, enc_a, lens, dec_out, aw_prev, w_dec)
+        enc, enc_a = enc.contiguous(), enc_a.contiguous()
+        dec_out, aw_prev = dec_out.contiguous(), aw_prev.contiguous()
+        B, T, E = enc.shape
+        A, D = w_dec.shape
+        C, K = conv_w.shape[0], conv_w.shape[-1]
+        dims = N.AttDecDims(B, T, E, A, C, K, D, 2, float(sharpen), int(bool(sigmoid)))
+        dev = enc.device
+        ctx_out = torch.empty(B, E, dtype=torch.float32, device=dev)
+        aw_out = torch.empty(B, T, dtype=torch.float32, device=dev)
+        nb = N.query('asr_att_step_workspace_bytes', ctypes.byref(dims))
+        ws = _ws(nb, dev)
+        N.call('asr_att_step_forward', ctypes.byref(dims), N.ptr(enc), N.ptr(enc_a), N.ptr(lens),
+               N.ptr(w_dec), N.ptr(w_conv), N.ptr(conv_w), N.ptr(v), N.ptr(dec_out),
+               N.ptr(aw_prev), N.ptr(ctx_out), N.ptr(aw_out), N.ptr(ws), nb,
+               N.stream_handle(dev))
+        ctx.save_for_backward(enc, enc_a, lens, dec_out, aw_prev, w_dec, w_conv, conv_w, v,
+                              aw_out)
+        ctx.dims = dims
+        return ctx_out, aw_out
+
+    @staticmethod
+    def backward(ctx, d_ctx, d_aw):
+        enc, enc_a, lens, dec_out, aw_prev, w_dec, w_conv, conv_w, v, aw_out = ctx.saved_tensors
+        dims = ctx.dims
+        B, T, E, A, C, K, D = dims.B, dims.T, dims.E, dims.A, dims.C, dims.K, dims.D
+        dev = enc.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        d_ctx = d_ctx.contiguous() if d_ctx is not None else torch.zeros(B, E, **f32)
+        d_aw = d_aw.contiguous() if d_aw is not None else None
+        d_enc_a = torch.empty(B, T, A, **f32)
+        d_dec = torch.empty(B, D, **f32)
+        d_aw_prev = torch.empty(B, T, **f32)
+        dctx_tot = torch.empty(B, E, **f32)
+        dwd = torch.empty(B, A, **f32)
+        nrow = B * 2 * N.query('asr_attdec_chunks', ctypes.byref(dims))
+        dv_part = torch.empty(nrow, A, **f32)
+        dwc_part = torch.empty(nrow, A * C, **f32)
+        dcw_part = torch.empty(nrow, C * K, **f32)
+        nb = N.query('asr_att_step_workspace_bytes', ctypes.byref(dims))
+        ws = _ws(nb, dev)
+        N.call('asr_att_step_backward', ctypes.byref(dims), N.ptr(enc), N.ptr(enc_a), N.ptr(lens),
+               N.ptr(w_dec), N.ptr(w_conv), N.ptr(conv_w), N.ptr(v), N.ptr(dec_out),
+               N.ptr(aw_prev), N.ptr(aw_out), N.ptr(d_ctx), N.ptr(d_aw), N.ptr(d_enc_a),
+               N.ptr(d_dec), N.ptr(d_aw_prev), N.ptr(dctx_tot), N.ptr(dwd), N.ptr(dv_part),
+               N.ptr(dwc_part), N.ptr(dcw_part), N.ptr(ws), nb, N.stream_handle(dev))
+        run_gemm([gemm_problem(operand(dwd, 1, rowmap(A)), operand(dec_out, 1, rowmap(D)),
+                               grad_buffer(w_dec), rowmap(D), A, D, B, beta=1.0)], dev)
+        colsum_accumulate(dv_part, grad_buffer(v))
+        colsum_accumulate(dwc_part, grad_buffer(w_conv))
+        colsum_accumulate(dcw_part, grad_buffer(conv_w))
+        d_enc = torch.empty_like(enc)      # d enc[b] = aw_out[b]^T dctx_tot[b] (K = 1)
+        run_gemm([gemm_problem(operand(aw_out, 1, rowmap(T)), operand(dctx_tot, 1, rowmap(E)),
+                               d_enc, rowmap(E), T, E, 1, batch=B,
+                               batch_strides=(T, E, T * E))], dev)
+        return d_enc, d_enc_a, None, d_dec, d_aw_prev, None, None, None, None, None, None
+
+
+class LSTMCellFn(torch.autograd.Function):
+    """nn.LSTMCell nonlinearity on gate pre-activations: (pre [B,4D], c_prev
+    [B,D]) -> (h, c).  The GEMMs are linear2 (x W_ih^T + b_ih + h W_hh^T + b_hh)."""
+
+    @staticmethod
+    def forward(ctx, pre, c_prev):
+        N.require_device(pre, c_prev)
+        pre, c_prev = pre.contiguous(), c_prev.contiguous()
+        B, G = pre.shape
+        D = G // 4
+        act = torch.empty_like(pre)
+        h = torch.empty(B, D, dtype=torch.float32, device=pre.device)
+        c = torch.empty(B, D, dtype=torch.float32, device=pre.device)
+        N.call('asr_lstm_cell_forward', N.ptr(pre), N.ptr(c_prev), B, D, N.ptr(act), N.ptr(h),
+               N.ptr(c), N.stream_handle(pre.device))
+        ctx.save_for_backward(act, c_prev, c)
+        return h, c
+
+    @staticmethod
+    def backward(ctx, dh, dc):
+        act, c_prev, c = ctx.saved_tensors
+        B, D = c.shape
+        dpre = torch.empty_like(act)
+        dc_prev = torch.empty_like(c)
+        N.call('asr_lstm_cell_backward', N.ptr(act), N.ptr(c_prev), N.ptr(c),
+               N.ptr(dh.contiguous() if dh is not None else None),
+               N.ptr(dc.contiguous() if dc is not None else None), B, D, N.ptr(dpre),
+               N.ptr(dc_prev), N.stream_handle(c.device))
+        return dpre, dc_prev
+
+
+def lstm_cell(x, h, c, w_ih, w_hh, b_ih, b_hh):
+    """One nn.LSTMCell step on the HIP GEMM + cell kernels."""
+    pre = linear2(x, w_ih, b_ih, h, w_hh, b_hh)
+    return LSTMCellFn.apply(pre, c)
+
+
+def att_step(enc, enc_a, lens, dec_out, aw_prev, w_dec, w_conv, conv_w, v, sharpen=1.0,
+             sigmoid=False):
+    return AttStepFn.apply(enc, enc_a, lens, dec_out, aw_prev, w_dec, w_conv, conv_w, v, sharpen,
+                           sigmoid)
+
+
 def _attdec_opts(o, B, S, D, Y, w_ih, dev):
     """asr_attdec_opts_t from the training options dict (None = inference
     semantics: no dropout, teacher forcing).  Returns (opts | None, buffers to
@@ -597,6 +742,7 @@ class BLSTMLayerFn(torch.autograd.Function):
                    N.ptr(lens), B, T, H, cd, N.ptr(act), N.ptr(cst), N.ptr(dg_bf), N.ptr(ws), nb,
                    N.stream_handle(dev))
             colsum_accumulate(act.view(B * T, 8 * H), gbufs[2], gbufs[3])
+        notify_grad_event('recurrence')
         dg_op = dg_bf if dg_bf is not None else act
         # X as the dW_ih operand: the bf16 copy is already gathered (identity map)
         if cd == BF16:
@@ -607,6 +753,7 @@ class BLSTMLayerFn(torch.autograd.Function):
         side = _wgrad_side_stream(dev, B, H)
         if side is None:
             _blstm_wgrad(dg_op, act, x_op, x_map, y_op, T, gbufs, dev)
+            notify_grad_event('grads', gbufs)      # final on the compute stream
         else:
             # weight gradients on a CU-masked side stream, overlapping this
             # layer's dX GEMM and the previous layer's backward recurrence;

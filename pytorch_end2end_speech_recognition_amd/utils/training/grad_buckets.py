@@ -1,0 +1,118 @@
+"""Bucketed gradient all-reduce overlapped with the backward pass.
+
+The flat gradient buffer (models/pytorch_v3/base.py) holds every BLSTM layer's
+weights as one contiguous range (encoders/rnn.py flat_order), so a layer is a
+natural bucket: its gradients are final once its weight-gradient GEMMs are
+enqueued (native_ops.BLSTMLayerFn.backward notifies 'grads').  The bucket's
+collective is issued right after the NEXT layer's backward recurrence has been
+enqueued (notification 'recurrence'), so on the device it starts when that
+persistent recurrence has finished and runs beside the GEMMs that follow it:
+
+  * it never competes with a persistent recurrence for co-residency at launch
+    (the recurrence pins one work-group per CU; a collective kernel that is
+    already resident when the next recurrence launches finishes on its own);
+  * the stream semantics are RCCL's own: ProcessGroupNCCL makes its stream wait
+    for the current (compute) stream at issue time, and ``wait()`` makes the
+    compute stream wait for the collective.
+
+Every rank issues the same buckets in the same canonical order (top layer
+first, then the remainder of the buffer), whatever happens during its backward:
+buckets are issued strictly in that order, and ``finish`` issues whatever is
+left.  A rank whose backward raised still pairs every collective of the others
+(its values do not matter: the skip flag that follows discards the step).
+
+Each bucket is scaled by grad_scale (local_B / global_B) on the compute stream
+before its SUM, so the reduced gradient equals the 1-GPU gradient of the
+global batch for any shard sizes.
+"""
+import torch
+import torch.distributed as dist
+
+from ... import native_ops
+
+
+class GradBuckets(object):
+    def __init__(self, model, grad_scale):
+        self.model = model
+        self.scale = grad_scale
+        flat = model._flat_grad
+        self.flat = flat
+        base = flat.data_ptr()
+        es = flat.element_size()
+        total = flat.numel()
+        layers = []           # (start, end) element ranges of the BLSTM layers
+        enc = getattr(model, 'encoder', None)
+        if enc is not None and hasattr(enc, 'flat_order') and hasattr(enc, '_layer_params'):
+            for l in range(enc.num_layers):
+                ps = [p for pair in enc._layer_params(l) for p in pair]
+                starts = [(p.grad.data_ptr() - base) // es for p in ps if p.grad is not None]
+                ends = [(p.grad.data_ptr() - base) // es + p.numel() for p in ps
+                        if p.grad is not None]
+                if len(starts) == len(ps):
+                    layers.append((min(starts), max(ends)))
+        # canonical order: top layer first (the order the backward produces them)
+        self.order = list(reversed(layers))
+        covered = sorted(layers)
+        rest, pos = [], 0
+        for a, b in covered:
+            if a > pos:
+                rest.append((pos, a))
+            pos = max(pos, b)
+        if pos < total:
+            rest.append((pos, total))
+        self.rest = rest
+        self.by_start = {a: i for i, (a, b) in enumerate(self.order)}
+        self.base, self.es = base, es
+        self.ready = [False] * len(self.order)
+        self.next = 0          # next bucket (canonical order) to issue
+        self.works = []
+        self.issued_during_backward = 0
+
+    @classmethod
+    def for_model(cls, model, grad_scale):
+        return cls(model, grad_scale)
+
+    # ---------------------------------------------------------------- hooks
+    def __enter__(self):
+        native_ops.set_grad_ready_hook(self._on_event)
+        return self
+
+    def __exit__(self, *exc):
+        native_ops.set_grad_ready_hook(None)
+        return False
+
+    def _on_event(self, event, arg=None):
+        if event == 'grads':
+            start = (arg[0].data_ptr() - self.base) // self.es
+            i = self.by_start.get(start)
+            if i is not None:
+                self.ready[i] = True
+        elif event == 'recurrence':
+            n = self._issue_ready()
+            self.issued_during_backward += n
+
+    def _issue(self, a, b):
+        seg = self.flat[a:b]
+        if self.scale is not None:
+            seg.mul_(self.scale)
+        self.works.append(dist.all_reduce(seg, op=dist.ReduceOp.SUM, async_op=True))
+
+    def _issue_ready(self):
+        n = 0
+        while self.next < len(self.order) and self.ready[self.next]:
+            self._issue(*self.order[self.next])
+            self.next += 1
+            n += 1
+        return n
+
+    def finish(self, ok=1):
+        """Issue every bucket not issued yet (canonical order), then make the
+        compute stream wait for all of them."""
+        while self.next < len(self.order):
+            self._issue(*self.order[self.next])
+            self.next += 1
+        for a, b in self.rest:
+            self._issue(a, b)
+        for w in self.works:
+            w.wait()
+        self.works = []

@@ -5,17 +5,22 @@ data-parallel form over RCCL.
 Single GPU: zero_grad -> forward -> backward -> fused clip + optimizer step
 (the global-norm clip coefficient is computed on device; no host sync until
 the loss value is read).  Data parallel (torch.distributed initialised, world
-size > 1): each rank runs forward/backward on its shard, the flat gradient
-buffer is summed over ranks with ONE RCCL all-reduce (the shard losses are
-scaled so the sum equals the 1-GPU gradient of the global batch), then every
-rank clips with the same global norm and applies the same update.  A RuntimeError
-on any rank skips the batch on every rank (a 1-int all-reduce keeps the ranks
-in lock step), mirroring training_loop.py:69-76.
+size > 1): each rank runs forward/backward on its shard; each rank's gradient
+(of its per-rank mean loss) is scaled by local_B / global_B BEFORE the SUM
+all-reduce, so the reduced gradient is the 1-GPU gradient of the global batch
+for any split (unequal shards included).  The flat gradient buffer is reduced
+in buckets (utils/training/grad_buckets.py): one per BLSTM layer, issued while
+the backward of the layers below still runs, plus the remainder at the end.
+Then every rank clips with the same global norm and applies the same update.
+A RuntimeError on any rank skips the batch on every rank (a 1-int all-reduce
+keeps the ranks in lock step), mirroring training_loop.py:69-76.
 """
 import logging
 
 import torch
 import torch.distributed as dist
+
+from .grad_buckets import GradBuckets
 
 logger = logging.getLogger('training')
 INF = float('inf')
@@ -55,56 +60,103 @@ def shard_batch(batch, rank, world):
 
 
 def allreduce_gradients(model, grad_scale=None):
-    """Sum the flat gradient over ranks (one contiguous RCCL collective)."""
+    """Scale this rank's flat gradient by grad_scale (local_B / global_B), then
+    SUM it over ranks (one contiguous RCCL collective).  Scaling before the sum
+    is what makes unequal shards correct: SUM_r (n_r / N) g_r is the gradient
+    of the global-batch mean loss on every rank."""
     if _world() > 1:
-        dist.all_reduce(model._flat_grad, op=dist.ReduceOp.SUM)
         if grad_scale is not None:
             model._flat_grad.mul_(grad_scale)
+        dist.all_reduce(model._flat_grad, op=dist.ReduceOp.SUM)
+
+
+def _status_guard(model):
+    """Device int32[2]: the recurrence status words of this step (a bounded
+    spin that gave up), gathered and cleared stream-ordered (no host sync);
+    None on a CPU model (the gloo tests) or without the library."""
+    if model.device.type != 'cuda':
+        return None
+    from ... import native_ops
+    return native_ops.recurrence_status(model.device)
 
 
 def _step(model, forward, clip_grad_norm, n_losses, grad_scale):
     """zero_grad -> forward (returns n_losses loss tensors, the first is the
     total) -> backward -> collective skip flag -> gradient all-reduce ->
-    fused clip + optimizer step.  Returns the losses as floats (0 on skip)."""
+    fused clip + optimizer step.  Returns the losses as floats (0 on skip).
+
+    Skips (training_loop.py:69-76): a RuntimeError on any rank, or a
+    persistent recurrence whose bounded spin gave up (its gradients are
+    invalid).  On the GPU both are folded into a device guard (MAX-reduced
+    over ranks) that the fused optimizer kernel checks, so the step needs no
+    host sync before the optimizer; the host reads the guard with the loss."""
     ok = 1
+    world = _world()
+    buckets = GradBuckets.for_model(model, grad_scale) if world > 1 else None
     try:
         # ModelBase.zero_grad zeroes the flat gradient and re-binds every
         # param.grad view (torch.optim's zero_grad would set them to None and
         # detach them from the buffer the all-reduce / fused step work on)
         model.zero_grad()
         losses = forward()
-        losses[0].backward()
+        if buckets is not None:
+            with buckets:                 # per-layer collectives during the backward
+                losses[0].backward()
+        else:
+            losses[0].backward()
     except RuntimeError as e:
         logger.warning('!!!Skip mini-batch!!! %s' % e)
         ok = 0
         losses = None
-    if _world() > 1:
+    if buckets is not None:
+        buckets.finish(ok)                # remainder + wait; never skipped, so every
+    guard = _status_guard(model)          # rank pairs the others' collectives
+    if guard is not None:
+        if not ok:
+            guard[0:1].fill_(1)
+        if world > 1:
+            dist.all_reduce(guard, op=dist.ReduceOp.MAX)
+    elif world > 1:
         flag = torch.tensor([ok], dtype=torch.int32, device=model.device)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         ok = int(flag.item())
-    if not ok:
+    if not ok and (guard is None or world == 1):
         model.zero_grad()
         return [0.] * n_losses
-    allreduce_gradients(model, grad_scale)
     if hasattr(model.optimizer, 'clip_and_step'):
-        model.optimizer.clip_and_step(clip_grad_norm if clip_grad_norm > 0 else 0.0)
+        model.optimizer.clip_and_step(clip_grad_norm if clip_grad_norm > 0 else 0.0, guard=guard)
     else:
+        if guard is not None and int(guard.max().item()):
+            return _skipped(model, n_losses, 'persistent recurrence gave up')
         if clip_grad_norm > 0:
             torch.nn.utils.clip_grad_norm_(model.parameters(), clip_grad_norm)
         model.optimizer.step()
-    vals = [float(l.item()) for l in losses]
+    vals = [float(l.item()) for l in losses] if losses is not None else [0.] * n_losses
+    if guard is not None and int(guard.max().item()):
+        # the fused step left the weights untouched; undo its step count
+        if hasattr(model.optimizer, 'undo_step_count'):
+            model.optimizer.undo_step_count()
+        return _skipped(model, n_losses, 'a rank failed or a persistent recurrence gave up '
+                        '(status %s)' % guard.tolist())
     if vals[0] == INF or vals[0] == -INF:
         logger.warning('WARNING: received an inf loss, setting loss value to 0.')
         vals = [0.] * n_losses
     return vals
 
 
+def _skipped(model, n_losses, why):
+    logger.warning('!!!Skip mini-batch!!! %s' % why)
+    model.zero_grad()
+    return [0.] * n_losses
+
+
 def train_step(model, batch, clip_grad_norm, backend='pytorch', grad_scale=None):
     """Returns (model, loss_value) like training_loop.py:27-83.
 
-    grad_scale: optional factor applied to the all-reduced gradient (data
-    parallel: pass local_batch / global_batch when every rank divides its loss
-    by its local batch size, so the update equals the 1-GPU update)."""
+    grad_scale: data parallel only -- the factor applied to this rank's
+    gradient before the sum over ranks: pass shard_batch's local_B / global_B
+    (every rank's loss is a mean over its local batch), so the update equals
+    the 1-GPU update of the global batch."""
     vals = _step(model, lambda: [model(batch['xs'], batch['ys'], batch['x_lens'],
                                        batch['y_lens'])], clip_grad_norm, 1, grad_scale)
     return model, vals[0]

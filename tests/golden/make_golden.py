@@ -484,6 +484,69 @@ def case_hier_attention_model():
 
 
 # --------------------------------------------------------------------------
+# Case 5b: attention at the PRODUCTION attention shape (BASELINE configs[2]/[3],
+# examples/librispeech/s5/conf/attention/char_blstm_att_100h.yml): location
+# attention 128-dim, 10 conv channels x width 201, LSTM decoder 320, embedding
+# 32, bottleneck 320, encoder 320 x 2 directions (E = 640), V = 28 + 2; T' =
+# 161 frames (six 32-frame chunks of the attention kernels), ragged lengths.
+# One encoder layer keeps the fixture small.  Weights are NOT stored (the
+# model classes reproduce the reference's initial state_dict bit for bit under
+# the same seed; per-tensor sums pin that); gradients of tensors above 64k
+# values are stored as (first 2 rows, Frobenius norm, projection on a seeded
+# N(0,1) tensor: np.random.RandomState(crc of the name)).
+# --------------------------------------------------------------------------
+PROD_ATT = dict(input_size=8, encoder_type='lstm', encoder_bidirectional=True,
+                encoder_num_units=320, encoder_num_proj=0, encoder_num_layers=1,
+                attention_type='location', attention_dim=128, decoder_type='lstm',
+                decoder_num_units=320, decoder_num_layers=1, embedding_dim=32,
+                dropout_input=0, dropout_encoder=0, dropout_decoder=0, dropout_embedding=0,
+                num_classes=28, parameter_init=0.1, subsample_list=[], subsample_type='drop',
+                attention_conv_num_channels=10, attention_conv_width=201, bottleneck_dim=320,
+                decoding_order='bahdanau', init_dec_state='zero')
+
+
+def grad_digest(name, g, big=65536):
+    """Compact gradient record (shared with tests/test_attention_prod.py)."""
+    import zlib
+    g = np.asarray(g, np.float32)
+    if g.size <= big:
+        return {'grad/' + name: g}
+    r = np.random.RandomState(zlib.crc32(name.encode()) & 0x7fffffff).randn(*g.shape)
+    return {'grad_rows/' + name: g.reshape(g.shape[0], -1)[:2].copy(),
+            'grad_norm/' + name: np.array([np.linalg.norm(g.astype(np.float64))]),
+            'grad_proj/' + name: np.array([np.sum(g.astype(np.float64) * r)])}
+
+
+def case_attention_prod():
+    from models.pytorch_v3.attention.attention_seq2seq import AttentionSeq2seq
+    specs = [('model_att_prod', dict(PROD_ATT, ctc_loss_weight=0, label_smoothing_prob=0)),
+             ('model_att_prod_hybrid', dict(PROD_ATT, ctc_loss_weight=0.3,
+                                            label_smoothing_prob=0.1))]
+    only = _selected()
+    for name, kw in specs:
+        if only and name not in only:
+            continue
+        torch.manual_seed(1623)
+        model = AttentionSeq2seq(**kw)
+        model.train()
+        sums = {'sdsum/' + k: np.array([v.double().sum().item(), (v.double() ** 2).sum().item()])
+                for k, v in model.state_dict().items()}
+        rng = np.random.RandomState(11)
+        B, T = 3, 161
+        x_lens = np.array([161, 140, 97], np.int32)
+        y_lens = np.array([23, 31, 17], np.int32)
+        xs, ys = _batch(rng, B, T, 8, y_lens, 28, x_lens)
+        loss = model(xs, ys, x_lens, y_lens)
+        loss.backward()
+        grads = {}
+        for k, p in model.named_parameters():
+            grads.update(grad_digest(k, np.zeros(p.shape, np.float32) if p.grad is None
+                                     else p.grad.detach().numpy()))
+        _save(name, kwargs=np.array(json.dumps(kw)), xs=xs, ys=ys, x_lens=x_lens,
+              y_lens=y_lens, loss=loss.detach().numpy().reshape(1), **sums, **grads)
+
+
+# --------------------------------------------------------------------------
 # Case 7: greedy attention decoding (attention_seq2seq.py:866-1036)
 # --------------------------------------------------------------------------
 def case_attention_decode():
@@ -542,6 +605,7 @@ if __name__ == '__main__':
         case_attention_model()
         case_attention_decode()
         case_hier_attention_model()
+        case_attention_prod()
         sys.exit(0)
     case_ctc()
     case_encoder()
@@ -551,4 +615,5 @@ if __name__ == '__main__':
     case_hier_ctc_model()
     case_attention_model()
     case_hier_attention_model()
+    case_attention_prod()
     case_attention_decode()

@@ -1,0 +1,152 @@
+"""The attention decoder at the PRODUCTION attention shape of BASELINE
+configs[2]/[3] (char_blstm_att_100h.yml: location attention 128-dim, 10 conv
+channels x width 201, LSTM decoder 320, embedding 32, bottleneck 320, E = 640)
+vs fixtures recorded from the reference itself (tests/golden/make_golden.py
+case_attention_prod, lambda = 0 and lambda = 0.3 + label smoothing 0.1), at
+T' = 161 frames: six 32-frame chunks, so the cross-chunk partial reductions of
+the attention kernels (decoder.hip att_energy<10>, att_bwd_energy<10>,
+att_bwd_conv, dwd_chunk / dv_part / dcw_part) are all exercised.
+
+CPU: the model classes reproduce the reference's initial weights (per-tensor
+sums, exact), and the oracle restatement reproduces the reference's loss and
+gradients.  GPU: fp32 parity mode -- loss rtol 1e-4, every gradient rtol 2e-3
+(full tensors where small; first two rows, norm and a seeded projection where
+large) -- and the bf16 mode within its stated tolerance; both runs must have
+launched the C = 10 instantiation over >= 4 chunks."""
+import ctypes
+import json
+import zlib
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import asr_ref
+
+NAMES = ['model_att_prod', 'model_att_prod_hybrid']
+
+
+def _build(kw):
+    from pytorch_end2end_speech_recognition_amd.models.pytorch_v3.attention.attention_seq2seq \
+        import AttentionSeq2seq
+    torch.manual_seed(1623)
+    return AttentionSeq2seq(**kw)
+
+
+def _check_grads(d, grads, rtol, what):
+    """grads: {name: np array}.  Small tensors compared elementwise (rtol, atol
+    = rtol x max|g_ref|); large ones by first rows, norm and projection."""
+    for k, g in grads.items():
+        g = np.asarray(g, np.float64)
+        if 'grad/' + k in d.files:
+            ref = d['grad/' + k].astype(np.float64)
+            np.testing.assert_allclose(g, ref, rtol=rtol, atol=rtol * (np.abs(ref).max() + 1e-12),
+                                       err_msg='%s %s' % (what, k))
+            continue
+        rows = d['grad_rows/' + k].astype(np.float64)
+        nrm = float(d['grad_norm/' + k][0])
+        prj = float(d['grad_proj/' + k][0])
+        got = g.reshape(g.shape[0], -1)
+        np.testing.assert_allclose(got[:2], rows, rtol=rtol, atol=rtol * (np.abs(rows).max() + 1e-12),
+                                   err_msg='%s %s rows' % (what, k))
+        assert abs(np.linalg.norm(g) - nrm) <= rtol * nrm + 1e-12, (what, k, np.linalg.norm(g), nrm)
+        r = np.random.RandomState(zlib.crc32(k.encode()) & 0x7fffffff).randn(*g.shape)
+        assert abs(np.sum(g * r) - prj) <= rtol * nrm + 1e-12, (what, k, np.sum(g * r), prj)
+
+
+@pytest.mark.parametrize('name', NAMES)
+def test_prod_init_matches_reference(name):
+    d = golden(name)
+    sd = _build(json.loads(str(d['kwargs']))).state_dict()
+    keys = sorted(k[6:] for k in d.files if k.startswith('sdsum/'))
+    assert sorted(sd) == keys
+    for k in keys:
+        v = sd[k].double()
+        assert [v.sum().item(), (v ** 2).sum().item()] == list(d['sdsum/' + k]), k
+
+
+@pytest.mark.parametrize('name', NAMES)
+def test_prod_oracle_matches_reference(name):
+    d = golden(name)
+    kw = json.loads(str(d['kwargs']))
+    p = {k: v.detach().clone().requires_grad_(v.is_floating_point())
+         for k, v in _build(kw).state_dict().items()}
+    loss = asr_ref.attention_model_loss(p, kw, d['xs'], d['ys'], d['x_lens'], d['y_lens'])
+    loss.backward()
+    np.testing.assert_allclose(float(loss), float(d['loss'][0]), rtol=1e-5)
+    _check_grads(d, {k: v.grad.numpy() for k, v in p.items() if v.grad is not None}, 1e-4,
+                 'oracle')
+
+
+def _gpu_run(name, prec, dev):
+    from pytorch_end2end_speech_recognition_amd import _native as N
+    from pytorch_end2end_speech_recognition_amd import native_ops
+    d = golden(name)
+    kw = json.loads(str(d['kwargs']))
+    native_ops.set_compute_dtype(prec)
+    try:
+        model = _build(kw)
+        model.set_cuda()
+        model.zero_grad()
+        loss = model(d['xs'], d['ys'], d['x_lens'], d['y_lens'])
+        loss.backward()
+        torch.cuda.synchronize()
+    finally:
+        native_ops.set_compute_dtype('fp32')
+    launch = (ctypes.c_int * 4)()
+    N.call('asr_attdec_last_launch', ctypes.cast(launch, ctypes.c_void_p))
+    return d, float(loss.item()), {k: p.grad.cpu().numpy() for k, p in model.named_parameters()}, \
+        list(launch)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name', NAMES)
+def test_prod_attention_fp32_matches_reference(name, cuda_dev):
+    d, loss, grads, launch = _gpu_run(name, 'fp32', cuda_dev)
+    assert launch[0] == 10 and launch[2] == 10, launch          # att_energy<10>, bwd <10>
+    assert launch[1] >= 4 and launch[3] >= 4, launch            # multi-chunk reductions
+    np.testing.assert_allclose(loss, float(d['loss'][0]), rtol=1e-4)
+    _check_grads(d, grads, 2e-3, 'fp32')
+
+
+def _norm_errors(d, grads):
+    """Per tensor: ||g - g_ref|| / ||g_ref|| (full tensors) or, for digested
+    ones, max(|norm - norm_ref|, |proj - proj_ref|) / norm_ref."""
+    out = {}
+    for k, g in grads.items():
+        g = np.asarray(g, np.float64)
+        if 'grad/' + k in d.files:
+            ref = d['grad/' + k].astype(np.float64)
+            out[k] = np.linalg.norm(g - ref) / (np.linalg.norm(ref) + 1e-30)
+        else:
+            nrm = float(d['grad_norm/' + k][0])
+            r = np.random.RandomState(zlib.crc32(k.encode()) & 0x7fffffff).randn(*g.shape)
+            out[k] = max(abs(np.linalg.norm(g) - nrm),
+                         abs(np.sum(g * r) - float(d['grad_proj/' + k][0]))) / (nrm + 1e-30)
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name', NAMES)
+def test_prod_attention_bf16_within_tolerance(name, cuda_dev):
+    """bf16 mode (bf16 operands, f32 accumulation and state; not a parity
+    mode): loss within 1e-2 relative (measured 2-4e-4); every gradient within
+    0.3 in relative L2 norm.  Measured: decoder / attention gradients <= 0.11,
+    the encoder's up to 0.22 (reverse-direction biases): the bf16 rounding of
+    the recurrent operands is amplified through the 161-step encoder BPTT at
+    this initialisation -- the same 0.15-0.22 with all three recurrence
+    implementations (tagged-granule persistent, counter persistent, per-step
+    kernels; tools/att_prod_bf16_diag.py), while the same kernels agree with
+    float64 to 4e-3 at the full bench shape when the recurrence is contracting
+    (tests/test_recurrence_full.py)."""
+    d, loss, grads, launch = _gpu_run(name, 'bf16', cuda_dev)
+    assert launch[0] == 10 and launch[1] >= 4 and launch[2] == 10 and launch[3] >= 4, launch
+    errs = _norm_errors(d, grads)
+    worst = sorted(errs.items(), key=lambda kv: -kv[1])[:6]
+    print('\nbf16 loss rel err %.2e; worst gradient rel-L2 errors: %s' % (
+        abs(loss - float(d['loss'][0])) / abs(float(d['loss'][0])),
+        ', '.join('%s %.2e' % kv for kv in worst)))
+    np.testing.assert_allclose(loss, float(d['loss'][0]), rtol=1e-2)
+    for k, e in errs.items():
+        assert e <= 0.3, (k, e)

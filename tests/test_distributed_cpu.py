@@ -15,14 +15,56 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+from pytorch_end2end_speech_recognition_amd import native_ops
 from pytorch_end2end_speech_recognition_amd.models.pytorch_v3.base import ModelBase
 from pytorch_end2end_speech_recognition_amd.utils.training import training_loop as TL
+
+
+class _LayerFn(torch.autograd.Function):
+    """Stand-in for BLSTMLayerFn: weight gradients written by the op itself into
+    the flat-buffer views, with the same 'recurrence' / 'grads' notifications."""
+
+    @staticmethod
+    def forward(ctx, x, w, gviews):
+        ctx.save_for_backward(x, w)
+        ctx.gviews = gviews
+        return torch.tanh(x @ w.t())
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        y = torch.tanh(x @ w.t())
+        dz = dy * (1 - y * y)
+        native_ops.notify_grad_event('recurrence')
+        for g in ctx.gviews:
+            g.add_(dz.t() @ x)
+        native_ops.notify_grad_event('grads', ctx.gviews)
+        return dz @ w, None, None
+
+
+class TinyEncoder(torch.nn.Module):
+    """Two 'layers', each a (forward, reverse) parameter pair kept adjacent in
+    the flat buffer like encoders/rnn.py."""
+
+    def __init__(self):
+        super().__init__()
+        self.num_layers = 2
+        for l in range(2):
+            setattr(self, 'w%d_f' % l, torch.nn.Parameter(torch.randn(3, 3) * 0.3))
+            setattr(self, 'w%d_r' % l, torch.nn.Parameter(torch.randn(3, 3) * 0.3))
+
+    def _layer_params(self, l):
+        return [(getattr(self, 'w%d_f' % l), getattr(self, 'w%d_r' % l))]
+
+    def flat_order(self):
+        return [list(pair) for l in range(2) for pair in self._layer_params(l)]
 
 
 class TinyModel(ModelBase):
     def __init__(self, fail_rank=-1):
         super(ModelBase, self).__init__()
         torch.manual_seed(0)
+        self.encoder = TinyEncoder()
         self.lin = torch.nn.Linear(3, 2)
         self.num_stack = 1
         self.fail_rank = fail_rank
@@ -31,15 +73,18 @@ class TinyModel(ModelBase):
     def forward(self, xs, ys, x_lens, y_lens, is_eval=False):
         if dist.is_initialized() and dist.get_rank() == self.fail_rank:
             raise RuntimeError('simulated OOM')
-        x = torch.from_numpy(np.asarray(xs, np.float32)).sum(1)      # [B, 3]
-        out = self.lin(x)
+        h = torch.from_numpy(np.asarray(xs, np.float32)).sum(1)      # [B, 3]
+        for l in range(2):
+            wf, wr = self.encoder._layer_params(l)[0]
+            h = _LayerFn.apply(h, wf + wr, (wf.grad, wr.grad))
+        out = self.lin(h)
         return ((out - 1.0) ** 2).mean().reshape(1)
 
 
-def _batch():
+def _batch(B=6):
     rng = np.random.RandomState(0)
-    B, T = 6, 5
-    x_lens = np.array([5, 5, 4, 3, 3, 2], np.int32)
+    T = 5
+    x_lens = np.array([5, 5, 4, 3, 3, 2][:B], np.int32)
     xs = rng.randn(B, T, 3).astype(np.float32)
     for b in range(B):
         xs[b, x_lens[b]:] = 0
@@ -55,24 +100,31 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, fail_rank, out):
+def _worker(rank, world, port, fail_rank, out, B, clip):
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
     dist.init_process_group('gloo', rank=rank, world_size=world)
     model = TinyModel(fail_rank)
     model.optimizer = torch.optim.SGD(model.parameters(), lr=0.1)
-    local, scale = TL.shard_batch(_batch(), rank, world)
+    local, scale = TL.shard_batch(_batch(B), rank, world)
     # per-rank loss is a mean over the local batch -> scale by local/global
-    _, lv = TL.train_step(model, local, clip_grad_norm=0, grad_scale=scale)
-    out[rank] = model._flat_param.clone()
+    issued = []
+    orig = TL.GradBuckets.finish
+
+    def finish(self, ok=1):
+        issued.append(self.issued_during_backward)
+        return orig(self, ok)
+    TL.GradBuckets.finish = finish
+    _, lv = TL.train_step(model, local, clip_grad_norm=clip, grad_scale=scale)
+    out[rank] = (model._flat_param.clone(), issued[0] if issued else -1)
     dist.destroy_process_group()
 
 
-def _run(world, fail_rank=-1):
+def _run(world, fail_rank=-1, B=6, clip=0.0):
     ctx = mp.get_context('spawn')
     mgr = ctx.Manager()
     out = mgr.dict()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, fail_rank, out))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fail_rank, out, B, clip))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -91,21 +143,36 @@ def test_shard_batch_round_robin():
     assert l1['xs'].shape[1] == 5 and s0 == s1 == 0.5
 
 
-def test_data_parallel_update_equals_single_process():
-    params = _run(2)
+@pytest.mark.parametrize('B,clip', [(6, 0.0), (5, 0.0), (5, 0.05)])
+def test_data_parallel_update_equals_single_process(B, clip):
+    """Equal (3/3) and unequal (3/2) shards, without and with the global-norm
+    clip: the data-parallel update equals the single-process update of the
+    global batch on every rank."""
+    res = _run(2, B=B, clip=clip)
+    params = [r[0] for r in res]
     torch.testing.assert_close(params[0], params[1])
-    # single-process reference on the global batch
+    # the layer-1 bucket went out during the backward (after layer 0's
+    # 'recurrence'), the layer-0 bucket and the remainder at the end
+    assert all(r[1] == 1 for r in res)
     model = TinyModel()
     model.optimizer = torch.optim.SGD(model.parameters(), lr=0.1)
-    b = _batch()
-    # the 1-GPU gradient of the global batch = mean of the two shard means here
-    # (equal shard sizes), i.e. the global-batch mean loss
-    TL.train_step(model, b, clip_grad_norm=0)
+    TL.train_step(model, _batch(B), clip_grad_norm=clip)
     torch.testing.assert_close(params[0], model._flat_param, rtol=1e-5, atol=1e-6)
+    assert not torch.equal(model._flat_param, TinyModel()._flat_param)
+
+
+def test_grad_buckets_partition_the_flat_buffer():
+    model = TinyModel()
+    gb = TL.GradBuckets(model, 0.5)
+    spans = sorted(gb.order + gb.rest)
+    assert spans[0][0] == 0 and spans[-1][1] == model._flat_grad.numel()
+    for (a0, b0), (a1, b1) in zip(spans, spans[1:]):
+        assert b0 == a1
+    assert len(gb.order) == 2 and gb.order[0][0] > gb.order[1][0]    # top layer first
 
 
 def test_skip_batch_is_collective():
-    params = _run(2, fail_rank=1)
+    res = _run(2, fail_rank=1)
     init = TinyModel()._flat_param
-    for p in params:                 # both ranks skipped the update
+    for p, _ in res:                 # both ranks skipped the update
         torch.testing.assert_close(p, init)

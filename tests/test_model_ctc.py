@@ -176,3 +176,41 @@ def test_encoder_variants_bf16_vs_oracle(variant, cuda_dev):
         gw = prm.grad.cpu().numpy()
         scale = np.abs(ga).max() + 1e-6
         assert np.abs(gw - ga).max() / scale < 5e-2, (k, np.abs(gw - ga).max(), scale)
+
+
+@pytest.mark.gpu
+def test_recurrence_give_up_skips_the_batch(cuda_dev):
+    """A persistent recurrence whose bounded spin gave up (simulated with the
+    status hook, exactly the word a give-up sets) must not update the weights:
+    the fused optimizer kernel sees the device guard, train_step returns 0 and
+    skips (training_loop.py:69-76), Adam's step count is unchanged, and the
+    next clean step trains normally."""
+    from pytorch_end2end_speech_recognition_amd import _native as N
+    from pytorch_end2end_speech_recognition_amd import native_ops
+    from pytorch_end2end_speech_recognition_amd.utils.training.training_loop import train_step
+    native_ops.set_compute_dtype('bf16')
+    try:
+        d = golden('model_ctc_sub')
+        kw = json.loads(str(d['kwargs']))
+        sd, _ = golden_params(d)
+        model = _to_gpu_model(kw, sd, cuda_dev)
+        model.set_optimizer('adam', 1e-3, weight_decay=1e-6)
+        batch = dict(xs=d['xs'], ys=d['ys'], x_lens=d['x_lens'], y_lens=d['y_lens'])
+        native_ops.recurrence_status(cuda_dev)             # clear
+        before = model._flat_param.clone()
+        N.call('asr_lstm_status_inject', 1, N.stream_handle(cuda_dev))
+        model, lv = train_step(model, batch, clip_grad_norm=5.0)
+        torch.cuda.synchronize()
+        assert lv == 0.0
+        assert torch.equal(before, model._flat_param)
+        assert model.optimizer._step == 0
+        assert int(native_ops.recurrence_status(cuda_dev).max().item()) == 0   # cleared
+        model, lv = train_step(model, batch, clip_grad_norm=5.0)
+        torch.cuda.synchronize()
+        assert lv > 0 and model.optimizer._step == 1
+        assert not torch.equal(before, model._flat_param)
+        N.call('asr_lstm_status_inject', 1, N.stream_handle(cuda_dev))
+        with pytest.raises(N.NativeError):
+            native_ops.raise_if_recurrence_failed(cuda_dev)
+    finally:
+        native_ops.set_compute_dtype('fp32')
