@@ -350,13 +350,75 @@ class FlatOptimizer(torch.optim.Optimizer):
         Adam's bias-correction count."""
         self._step -= 1
 
+    # ------------------------------------------------------- checkpoints
+    def _param_slices(self):
+        """(index, param, offset) in model.parameters() order -- the order
+        torch.optim numbers parameters in its state_dict."""
+        offs = {id(p): o for p, o in self.model._flat_index}
+        return [(i, p, offs[id(p)]) for i, p in enumerate(self.model.parameters())]
+
     def state_dict(self):
-        return {'kind': self.kind, 'step': self._step, 'lr': self.param_groups[0]['lr'],
-                'm': self.m.detach().cpu(), 'v': None if self.v is None else self.v.detach().cpu()}
+        """torch.optim.Adam / SGD state_dict format (what the reference's
+        save_checkpoint stores, base.py:232-264): per-parameter 'step',
+        'exp_avg', 'exp_avg_sq' (Adam) or 'momentum_buffer' (momentum /
+        nesterov), views of the flat state buffers, and one param group."""
+        g = self.param_groups[0]
+        state = {}
+        for i, p, o in self._param_slices():
+            n = p.numel()
+            if self.kind == 'adam':
+                if self._step == 0:
+                    continue
+                state[i] = {'step': torch.tensor(float(self._step)),
+                            'exp_avg': self.m[o:o + n].view(p.shape).detach().cpu().clone(),
+                            'exp_avg_sq': self.v[o:o + n].view(p.shape).detach().cpu().clone()}
+            elif self.kind in ('momentum', 'nesterov') and self._step > 0:
+                state[i] = {'momentum_buffer':
+                            self.m[o:o + n].view(p.shape).detach().cpu().clone()}
+        group = {'lr': g['lr'], 'weight_decay': g['weight_decay'],
+                 'params': [i for i, _, _ in self._param_slices()]}
+        if self.kind == 'adam':
+            group.update(betas=tuple(g['betas']), eps=g['eps'], amsgrad=False,
+                         maximize=False, foreach=None, capturable=False, differentiable=False,
+                         fused=None)
+        else:
+            group.update(momentum=g['momentum'] if self.kind != 'sgd' else 0, dampening=0,
+                         nesterov=self.kind == 'nesterov', maximize=False, foreach=None,
+                         differentiable=False, fused=None)
+        return {'state': state, 'param_groups': [group], 'flat_kind': self.kind}
 
     def load_state_dict(self, sd):
-        self._step = int(sd['step'])
-        self.param_groups[0]['lr'] = sd['lr']
-        self.m.copy_(sd['m'].to(self.m.device))
-        if self.v is not None and sd.get('v') is not None:
-            self.v.copy_(sd['v'].to(self.v.device))
+        """Accepts torch.optim.Adam / SGD state_dicts (a reference checkpoint,
+        torch 0.3 int steps or torch 2.x tensor steps) and this class's own."""
+        if 'kind' in sd and 'm' in sd:            # round-1 flat format
+            self._step = int(sd['step'])
+            self.param_groups[0]['lr'] = sd['lr']
+            self.m.copy_(sd['m'].to(self.m.device))
+            if self.v is not None and sd.get('v') is not None:
+                self.v.copy_(sd['v'].to(self.v.device))
+            return
+        grp = sd['param_groups'][0]
+        for k in ('lr', 'weight_decay', 'eps', 'momentum'):
+            if k in grp:
+                self.param_groups[0][k] = grp[k]
+        if 'betas' in grp:
+            self.param_groups[0]['betas'] = tuple(grp['betas'])
+        state = sd['state']
+        steps = []
+        with torch.no_grad():
+            self.m.zero_()
+            if self.v is not None:
+                self.v.zero_()
+            for i, p, o in self._param_slices():
+                st = state.get(grp['params'][i] if i < len(grp['params']) else i)
+                if st is None:
+                    continue
+                n = p.numel()
+                if 'exp_avg' in st:
+                    self.m[o:o + n].copy_(st['exp_avg'].reshape(-1).to(self.m.device))
+                    self.v[o:o + n].copy_(st['exp_avg_sq'].reshape(-1).to(self.v.device))
+                elif st.get('momentum_buffer') is not None:
+                    self.m[o:o + n].copy_(st['momentum_buffer'].reshape(-1).to(self.m.device))
+                if 'step' in st:
+                    steps.append(int(float(st['step'])))
+        self._step = max(steps) if steps else 0
