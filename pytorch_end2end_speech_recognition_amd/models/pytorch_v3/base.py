@@ -265,7 +265,17 @@ class ModelBase(nn.Module):
 
     # ------------------------------------------------------------ host glue
     def np2var(self, array, dtype=None, cpu=False):
-        """base.py:362-390: numpy -> tensor (pinned + async H2D when on GPU)."""
+        """base.py:362-390: numpy -> tensor (pinned + async H2D when on GPU).
+        A tensor already on the model's device (utils/dataset/device_batch.py)
+        passes through without a copy."""
+        if torch.is_tensor(array) and not cpu and array.device == self.device:
+            if dtype == 'float' and array.dtype != torch.float32:
+                return array.float()
+            if dtype == 'int' and array.dtype != torch.int32:
+                return array.int()
+            if dtype == 'long' and array.dtype != torch.int64:
+                return array.long()
+            return array
         if isinstance(array, list):
             array = np.array(array)
         t = torch.from_numpy(np.ascontiguousarray(array))

@@ -547,6 +547,89 @@ def case_attention_prod():
 
 
 # --------------------------------------------------------------------------
+# Case 8: the data path -- DatasetBase.sample_index / next / make_batch
+# (utils/dataset/loader.py:29-157, base.py:76-201) with the LibriSpeech
+# Dataset's filtering, sort and dynamic batching (load_dataset.py:104-142),
+# and the frame stacking / splicing helpers.  The reference object is built
+# with the attributes the corpus Dataset's __init__ sets (its label-file and
+# CSV plumbing is corpus preparation, out of scope).
+# --------------------------------------------------------------------------
+def case_loader():
+    import tempfile
+    import pandas as pd
+    from utils.dataset.loader import DatasetBase
+    from utils.io.inputs.frame_stacking import stack_frame
+    from utils.io.inputs.splicing import do_splice
+    sys.path.insert(0, os.path.join(REF, 'examples', 'librispeech', 's5'))
+    from exp.dataset.load_dataset import Dataset as LibriDataset
+
+    rng = np.random.RandomState(12)
+    n = 19
+    frames = rng.randint(20, 1900, n)
+    frames[3] = 35                                 # filtered (< min_frame_num 40)
+    tmp = tempfile.mkdtemp()
+    feats, trans = {}, []
+    for i in range(n):
+        # the features are at most 20 frames (the CSV's frame_num drives the
+        # sort, the dynamic batch size and the padding) so the fixture stays small
+        T = int(min(frames[i], 20))
+        x = rng.randn(T, 3 * 41).astype(np.float32)                     # static | d | dd
+        path = os.path.join(tmp, 'utt%03d.npy' % i)
+        np.save(path, x)
+        feats['feat/utt%03d' % i] = x
+        trans.append(' '.join(str(v) for v in rng.randint(0, 29, rng.randint(1, 9))))
+    df = pd.DataFrame({'frame_num': frames, 'input_path': [os.path.join(tmp, 'utt%03d.npy' % i)
+                                                           for i in range(n)],
+                       'transcript': trans})
+    vocab = os.path.join(tmp, 'vocab.txt')
+    open(vocab, 'w').write('\n'.join('c%d' % i for i in range(29)) + '\n')
+
+    def make(batch_size, sort_utt, reverse, dynamic, input_freq, use_delta, use_dd,
+             num_stack, num_skip, splice):
+        ds = DatasetBase(vocab_file_path=vocab)
+        d = df[df['frame_num'] >= 40]
+        d = d.sort_values(by='frame_num', ascending=not reverse) if sort_utt else \
+            d.sort_values(by='input_path', ascending=True)
+        ds.df, ds.rest = d, set(list(d.index))
+        ds.backend, ds.is_test, ds.batch_size, ds.max_epoch = 'pytorch', False, batch_size, 2
+        ds.input_freq, ds.use_delta, ds.use_double_delta = input_freq, use_delta, use_dd
+        ds.num_stack, ds.num_skip, ds.splice = num_stack, num_skip, splice
+        ds.shuffle, ds.sort_utt, ds.sort_stop_epoch = False, sort_utt, None
+        ds.num_enque, ds.dynamic_batching = None, dynamic
+        ds.select_batch_size = types.MethodType(LibriDataset.select_batch_size, ds)
+        return ds
+
+    specs = {'a': (6, True, False, True, 41, True, True, 1, 1, 1),
+             'b': (5, True, True, False, 40, False, False, 3, 2, 1),
+             'c': (4, False, False, False, 41, True, True, 1, 1, 3)}
+    out = {'df_frame_num': frames, 'df_transcript': np.array(trans)}
+    out.update(feats)
+    for tag, spec in specs.items():
+        ds = make(*spec)
+        out['spec/' + tag] = np.array(spec[:4] + spec[4:], dtype=np.int64)
+        k = 0
+        while True:
+            try:
+                batch, new_epoch = ds.next()
+            except StopIteration:
+                break
+            names = [int(s_[3:]) for s_ in batch['input_names']]
+            out['%s/%d/utts' % (tag, k)] = np.array(names, np.int64)
+            out['%s/%d/new_epoch' % (tag, k)] = np.array([int(new_epoch)])
+            for key in ('xs', 'ys', 'x_lens', 'y_lens'):
+                out['%s/%d/%s' % (tag, k, key)] = np.asarray(batch[key])
+            k += 1
+        out['%s/n_batches' % tag] = np.array([k])
+    x = rng.randn(37, 3 * 4 * 2).astype(np.float32)
+    out['stack_in'] = x
+    for st, sk in ((2, 1), (3, 2), (4, 3), (3, 3)):
+        out['stack/%d_%d' % (st, sk)] = stack_frame(x, st, sk)
+    for sp, ns in ((3, 1), (5, 2), (11, 1)):
+        out['splice/%d_%d' % (sp, ns)] = do_splice(x[:, :12 * ns], sp, ns)
+    _save('loader', **out)
+
+
+# --------------------------------------------------------------------------
 # Case 7: greedy attention decoding (attention_seq2seq.py:866-1036)
 # --------------------------------------------------------------------------
 def case_attention_decode():
@@ -606,6 +689,8 @@ if __name__ == '__main__':
         case_attention_decode()
         case_hier_attention_model()
         case_attention_prod()
+        if 'loader' in _selected():
+            case_loader()
         sys.exit(0)
     case_ctc()
     case_encoder()
@@ -617,3 +702,4 @@ if __name__ == '__main__':
     case_hier_attention_model()
     case_attention_prod()
     case_attention_decode()
+    case_loader()
