@@ -798,6 +798,556 @@ gemm_bf16_kk256(Params P) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// 256 x 256 x 64 tiles, 8 waves (2 x 4, each wave 128 x 64 = 8 x 4 MFMA
+// accumulators), two 64-KB LDS buffers (one work-group per CU, two waves per
+// SIMD): every plain bf16 product of the encoder (input projections R x R,
+// input gradients R x K, weight gradients K x K).  Why it beats the 128 x 128
+// kernel (one barrier + vmcnt(0) per k-tile, the "step-3 structure" whose
+// ceiling is ~900 TF/s): the staging pipeline is two k-tiles deep and never
+// drains inside the loop, and the LDS reads of one k-half overlap the MFMAs of
+// the other:
+//   prologue : DMA k-tiles 0, 1 -> buffers 0, 1; wait tile 0; kk = 0 fragments
+//   k-tile t : read kk = 1 fragments of t | MFMA kk = 0 of t
+//              lgkmcnt(0) + barrier          (buffer t & 1 fully read by all)
+//              DMA k-tile t + 2 -> buffer t & 1
+//              vmcnt(8) + barrier            (k-tile t + 1 landed: only t + 2's
+//                                             eight DMAs may stay in flight)
+//              read kk = 0 fragments of t + 1 | MFMA kk = 1 of t
+// Staging is the buffer -> LDS DMA of the 128 x 128 kernel (inline asm: hipcc
+// neither counts nor drains it; the counted waits above are the only ones),
+// with the same source-address swizzles (R mode: 128-B rows, chunk c of row r
+// at c ^ ((r >> 1) & 7); K mode: 512-B k-rows, 32-B granule g of k-row k at
+// g ^ swz_h(k), read by ds_read_b64_tr_b16).
+// ---------------------------------------------------------------------------
+constexpr int T8 = 256, BK8 = 64, NT8 = 512;
+constexpr int TILE8 = T8 * BK8 * 2;   // 32 KB per operand k-tile
+
+// Per-thread staging state of one operand: the byte offsets of this thread's
+// four 16-B DMA sources, computed once (R mode: the rows never change, only
+// k advances) or advanced incrementally (K mode: the k-rows move by 64 per
+// k-tile; their (utterance, frame) pair is carried, so the row map costs no
+// division inside the k-loop -- the division-based row_off per DMA was most of
+// the kernel's VALU work).
+struct Stage8 {
+  unsigned base[4];   // R: row byte offset + chunk; K: column byte offset
+  int b[4], t[4];     // K: utterance / frame of the current k-row
+  int kr[4];          // R: chunk k offset (8c); K: k-row within the tile
+  int valid;          // R: bit i = row i inside the operand
+};
+
+template <int MODE>
+__device__ __forceinline__ void stage8_init(const Operand& op, Stage8& st, int tile0, int nrows,
+                                            int kbeg, int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int blk = wave * 4 + i;
+    if (MODE == 0) {
+      const int r = blk * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      const int row = tile0 + r;
+      long long off = row < nrows ? row_off_np(op.map, row) : -1;
+      st.base[i] = off >= 0 ? (unsigned)(off * 2) : 0u;
+      st.kr[i] = 8 * c;
+      if (i == 0) st.valid = 0;
+      if (off >= 0) st.valid |= 1 << i;
+    } else {
+      const int kr = blk * 2 + (lane >> 5);
+      const int j = lane & 31;
+      const int c = 2 * ((j >> 1) ^ swz_h(kr)) + (j & 1);
+      st.base[i] = (unsigned)((tile0 + 8 * c) * 2);
+      st.kr[i] = kr;
+      const int k = kbeg + kr;
+      st.b[i] = k / op.map.rows_per_b;
+      st.t[i] = k - st.b[i] * op.map.rows_per_b;
+    }
+  }
+}
+
+template <int MODE>
+__device__ __forceinline__ void stage8(const Operand& op, __amdgpu_buffer_rsrc_t rs, Stage8& st,
+                                       char* lds_tile, int k0, int kend, int wave) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int blk = wave * 4 + i;          // 1 KB of the 32-KB image
+    unsigned voff = OOB_OFF;
+    if (MODE == 0) {
+      const int k = k0 + st.kr[i];
+      if (((st.valid >> i) & 1) && k < kend) voff = st.base[i] + (unsigned)(k * 2);
+    } else {
+      const int k = k0 + st.kr[i];
+      const int tp = st.t[i] * op.map.t_mul + op.map.t_add;
+      if (k < kend && tp >= 0 && tp < op.map.t_limit)
+        voff = (unsigned)(((long long)st.b[i] * op.map.stride_b +
+                           (long long)tp * op.map.stride_t) * 2) + st.base[i];
+      // advance to this k-row of the next k-tile
+      st.t[i] += BK8;
+      while (st.t[i] >= op.map.rows_per_b) {
+        st.t[i] -= op.map.rows_per_b;
+        ++st.b[i];
+      }
+    }
+    const unsigned lds_addr = (unsigned)(uintptr_t)(lds_void_t*)(lds_tile + blk * 1024);
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(rs), "s"(lds_addr)
+        : "memory");
+  }
+}
+
+// R-mode fragment read with the lane-dependent part of the address hoisted:
+// rb is a multiple of 16, so the chunk swizzle ((r >> 1) & 7) of row
+// r = rb + (lane & 15) depends on the lane only and the address is
+// tile + rb * 128 (uniform) + lane_off(kk) (one VGPR per k-half).
+__device__ __forceinline__ unsigned r_lane_off(int kk, int lane) {
+  const int r = lane & 15;
+  return (unsigned)(r * 128 + (((4 * kk + (lane >> 4)) ^ ((r >> 1) & 7)) * 16));
+}
+
+template <int MODE>
+__device__ __forceinline__ bf16x8 frag8(const char* lds_tile, int rb, int kk, int lane) {
+  if (MODE == 0)
+    return __builtin_bit_cast(bf16x8,
+                              *(const u32x4_t*)(lds_tile + rb * 128 + r_lane_off(kk, lane)));
+  return frag_k256(lds_tile, rb, kk, lane);
+}
+
+// Fragments of one k-half (kk) of a k-tile: B for the wave's 64 columns (4
+// blocks), A for 64 of its 128 rows (half ih: 4 blocks).
+template <int BMODE>
+__device__ __forceinline__ void fragsB8(const char* buf, int kk, int wc, int lane, bf16x8 (&fb)[4]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) fb[j] = frag8<BMODE>(buf + TILE8, wc + 16 * j, kk, lane);
+}
+template <int AMODE>
+__device__ __forceinline__ void fragsA8(const char* buf, int kk, int r0, int lane, bf16x8 (&fa)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) fa[i] = frag8<AMODE>(buf, r0 + 16 * i, kk, lane);
+}
+
+// 16 MFMAs: rows [ih*64, +64) of the wave's tile x its 64 columns, one k-half
+__device__ __forceinline__ void mma8(const bf16x8 (&fa)[4], const bf16x8 (&fb)[4],
+                                     f32x4 (&acc)[8][4], int ih) {
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[ih * 4 + i][j] = mfma_bf16(fa[i], fb[j], acc[ih * 4 + i][j]);
+  __builtin_amdgcn_s_setprio(0);
+}
+
+// Epilogue of the 8-wave kernel through LDS: each wave's 128 x 64 f32 tile is
+// written to LDS in four 32-row quarters (pitch 68 floats: the 4-row lane
+// groups of a ds_write land on distinct banks; 8 waves x 8.5 KB) and read
+// back as 16-B row chunks, so the global stores (and the bias / beta reads)
+// are dwordx4 over whole 256-B row segments instead of 4-B lanes.
+// C(m, n) = alpha acc + bias[n] + bias2[n] + beta C(m, n) through C's row map;
+// raw = 1 writes acc alone to a dense [M][N] slab (split-K partials).
+constexpr int EP8 = 68;
+__device__ __forceinline__ void epi8(const Problem& pr, const RowMap& cm, bool raw,
+                                     f32x4 (&acc)[8][4], int tm, int tn, int wr, int wc,
+                                     int w, int lane, char* smem) {
+  float* tile = (float*)smem + w * 32 * EP8;
+  // a plain C map (every row valid, no batch split) needs no division per row
+  const bool plain = cm.rows_per_b == 0x7fffffff && cm.t_mul == 1 && cm.t_add == 0 &&
+                     cm.t_limit == 0x7fffffff && !cm.perm;
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {
+    __syncthreads();   // LDS free (k-loop done / previous quarter read back)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          tile[(16 * i + 4 * (lane >> 4) + r) * EP8 + 16 * j + (lane & 15)] = acc[2 * h + i][j][r];
+    __syncthreads();
+#pragma unroll 4
+    for (int it = 0; it < 8; ++it) {
+      const int row = it * 4 + (lane >> 4), ch = lane & 15;
+      const int m = tm + wr + 32 * h + row;
+      const int n = tn + wc + 4 * ch;
+      if (m >= pr.M || n >= pr.N) continue;
+      const float4 v = *reinterpret_cast<const float4*>(tile + row * EP8 + 4 * ch);
+      const long long off = plain ? (long long)m * cm.stride_t : row_off(cm, m);
+      if (off < 0) continue;
+      float* cp = (float*)cm.base + off + n;
+      float o[4] = {v.x, v.y, v.z, v.w};
+      if (!raw) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          o[e] *= pr.alpha;
+          if (n + e < pr.N) {
+            if (pr.bias) o[e] += pr.bias[n + e];
+            if (pr.bias2) o[e] += pr.bias2[n + e];
+          }
+        }
+      }
+      if (n + 4 <= pr.N && ((uintptr_t)cp & 15) == 0) {
+        if (!raw && pr.beta != 0.f) {
+          const float4 c = *reinterpret_cast<const float4*>(cp);
+          o[0] += pr.beta * c.x; o[1] += pr.beta * c.y; o[2] += pr.beta * c.z; o[3] += pr.beta * c.w;
+        }
+        *reinterpret_cast<float4*>(cp) = make_float4(o[0], o[1], o[2], o[3]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (n + e < pr.N) cp[e] = (!raw && pr.beta != 0.f) ? o[e] + pr.beta * cp[e] : o[e];
+      }
+    }
+  }
+}
+
+template <int AMODE, int BMODE>
+__global__ void __launch_bounds__(NT8) __attribute__((amdgpu_waves_per_eu(2, 2)))
+gemm_bf16_8w(Params P) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // 2 buffers x (A, B)
+
+  const int zb = blockIdx.z / P.nprob, zp = blockIdx.z % P.nprob;
+  Problem pr = P.p[zp];
+  if (zb >= pr.batch) return;
+  if (zb > 0) {
+    pr.a.map.base = (const char*)pr.a.map.base + zb * pr.sA * 2;
+    pr.b.map.base = (const char*)pr.b.map.base + zb * pr.sB * 2;
+    pr.a.bytes -= zb * pr.sA * 2;
+    pr.b.bytes -= zb * pr.sB * 2;
+    pr.c.base = (const char*)pr.c.base + zb * pr.sC * 4;
+  }
+  const int gm = (pr.M + T8 - 1) / T8, gn = (pr.N + T8 - 1) / T8;
+  const int nwg = gm * gn;
+  const int nsplit = pr.ksplit > 1 ? pr.ksplit : 1;
+  const int ntot = nwg * nsplit;
+  int id = blockIdx.x;
+  if (id >= ntot) return;
+  {  // bijective XCD remap: an XCD's blocks take a contiguous id range
+    const int q = ntot / 8, r = ntot % 8, x = id % 8;
+    id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + id / 8;
+  }
+  const int split = id / nwg;
+  id -= split * nwg;
+  int tm, tn;
+  {  // column-minor walk inside groups of 4 row tiles
+    const int per = 4 * gn;
+    const int g = id / per, r = id - g * per;
+    const int m0 = g * 4;
+    const int gs = min(4, gm - m0);
+    tm = (m0 + r % gs) * T8;
+    tn = (r / gs) * T8;
+  }
+  const int kbeg = nsplit > 1 ? split * pr.kchunk : 0;
+  const int kend = nsplit > 1 ? min(pr.K, kbeg + pr.kchunk) : pr.K;
+
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = (w >> 2) * 128, wc = (w & 3) * 64;
+  auto uni_ptr = [](const void* p) {
+    const unsigned long long v = (unsigned long long)p;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+    return (void*)(((unsigned long long)hi << 32) | lo);
+  };
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      uni_ptr(pr.a.map.base), 0, __builtin_amdgcn_readfirstlane((int)pr.a.bytes), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+      uni_ptr(pr.b.map.base), 0, __builtin_amdgcn_readfirstlane((int)pr.b.bytes), 0x00020000);
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (kend - kbeg + BK8 - 1) / BK8;
+  Stage8 sa, sb;
+  stage8_init<AMODE>(pr.a, sa, tm, pr.M, kbeg, w, lane);
+  stage8_init<BMODE>(pr.b, sb, tn, pr.N, kbeg, w, lane);
+  stage8<AMODE>(pr.a, ra, sa, smem, kbeg, kend, w);
+  stage8<BMODE>(pr.b, rb, sb, smem + TILE8, kbeg, kend, w);
+  if (nk > 1) {
+    stage8<AMODE>(pr.a, ra, sa, smem + 2 * TILE8, kbeg + BK8, kend, w);
+    stage8<BMODE>(pr.b, rb, sb, smem + 3 * TILE8, kbeg + BK8, kend, w);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  // four phases per k-tile, (k-half, row-half) = (0,0) (0,1) (1,0) (1,1); the
+  // fragments of the next phase are read while the current phase's 16 MFMAs run
+  bf16x8 b0[4], b1[4], a00[4], a01[4], a10[4], a11[4];
+  fragsB8<BMODE>(smem, 0, wc, lane, b0);
+  fragsA8<AMODE>(smem, 0, wr, lane, a00);
+  for (int kt = 0; kt < nk; ++kt) {
+    char* cur = smem + (kt & 1) * 2 * TILE8;
+    fragsA8<AMODE>(cur, 0, wr + 64, lane, a01);
+    mma8(a00, b0, acc, 0);
+    fragsB8<BMODE>(cur, 1, wc, lane, b1);
+    fragsA8<AMODE>(cur, 1, wr, lane, a10);
+    mma8(a01, b0, acc, 1);
+    fragsA8<AMODE>(cur, 1, wr + 64, lane, a11);
+    mma8(a10, b1, acc, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();                         // buffer kt & 1 read by all waves
+    if (kt + 2 < nk) {
+      const int k0 = kbeg + (kt + 2) * BK8;
+      stage8<AMODE>(pr.a, ra, sa, cur, k0, kend, w);
+      stage8<BMODE>(pr.b, rb, sb, cur + TILE8, k0, kend, w);
+    }
+    if (kt + 1 < nk) {
+      if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();                       // k-tile kt + 1 landed for all
+      const char* nxt = smem + ((kt + 1) & 1) * 2 * TILE8;
+      fragsB8<BMODE>(nxt, 0, wc, lane, b0);
+      fragsA8<AMODE>(nxt, 0, wr, lane, a00);
+    }
+    mma8(a11, b1, acc, 1);
+  }
+
+  if (nsplit > 1) {  // raw partial sums into this split's slab; splitk_reduce finishes
+    RowMap sm;
+    sm.base = pr.slab + (long long)split * pr.M * pr.N;
+    sm.stride_b = 0;
+    sm.stride_t = pr.N;
+    sm.rows_per_b = 0x7fffffff;
+    sm.t_mul = 1;
+    sm.t_add = 0;
+    sm.t_limit = 0x7fffffff;
+    sm.perm = nullptr;
+    epi8(pr, sm, true, acc, tm, tn, wr, wc, w, lane, smem);
+    return;
+  }
+  epi8(pr, pr.c, false, acc, tm, tn, wr, wc, w, lane, smem);
+}
+
+// ---------------------------------------------------------------------------
+// Ring variant of the 8-wave kernel (ASR_GEMM_8R=1): 32-deep k-tiles in a
+// five-slot LDS ring (5 x 32 KB = 160 KB), three k-tiles in flight behind the
+// one being read (the 64-deep two-buffer form keeps one).  Per k-tile:
+//   read A rows 64-127 | MFMA rows 0-63
+//   lgkmcnt(0) + barrier (slot free) -> DMA k-tile t + 4 into it
+//   counted vmcnt + barrier (k-tile t + 1 landed) -> read its B, A rows 0-63
+//   | MFMA rows 64-127
+// R-mode image [256 rows][32 k]: 64-B rows, 16-B chunk c of row r at slot
+// c ^ ((r >> 2) & 3) (conflict-free ds_read_b128 over the 16-row fragment);
+// K-mode image [32 k][256 rows] as the 256 x 256 kernel's.
+// ---------------------------------------------------------------------------
+constexpr int BKR = 32, NSLOT = 5;
+constexpr int TILER = T8 * BKR * 2;    // 16 KB per operand k-tile
+
+struct StageR {
+  unsigned base[2];
+  int b[2], t[2], kr[2];
+  int valid;
+};
+
+template <int MODE>
+__device__ __forceinline__ void stager_init(const Operand& op, StageR& st, int tile0, int nrows,
+                                            int kbeg, int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int blk = wave * 2 + i;          // 1 KB of the 16-KB image
+    if (MODE == 0) {
+      const int r = blk * 16 + (lane >> 2);
+      const int c = (lane & 3) ^ ((r >> 2) & 3);
+      const int row = tile0 + r;
+      long long off = row < nrows ? row_off_np(op.map, row) : -1;
+      st.base[i] = off >= 0 ? (unsigned)(off * 2) : 0u;
+      st.kr[i] = 8 * c;
+      if (i == 0) st.valid = 0;
+      if (off >= 0) st.valid |= 1 << i;
+    } else {
+      const int kr = blk * 2 + (lane >> 5);
+      const int j = lane & 31;
+      const int c = 2 * ((j >> 1) ^ swz_h(kr)) + (j & 1);
+      st.base[i] = (unsigned)((tile0 + 8 * c) * 2);
+      st.kr[i] = kr;
+      const int k = kbeg + kr;
+      st.b[i] = k / op.map.rows_per_b;
+      st.t[i] = k - st.b[i] * op.map.rows_per_b;
+    }
+  }
+}
+
+template <int MODE>
+__device__ __forceinline__ void stager(const Operand& op, __amdgpu_buffer_rsrc_t rs, StageR& st,
+                                       char* lds_tile, int k0, int kend, int wave) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int blk = wave * 2 + i;
+    unsigned voff = OOB_OFF;
+    const int k = k0 + st.kr[i];
+    if (MODE == 0) {
+      if (((st.valid >> i) & 1) && k < kend) voff = st.base[i] + (unsigned)(k * 2);
+    } else {
+      const int tp = st.t[i] * op.map.t_mul + op.map.t_add;
+      if (k < kend && tp >= 0 && tp < op.map.t_limit)
+        voff = (unsigned)(((long long)st.b[i] * op.map.stride_b +
+                           (long long)tp * op.map.stride_t) * 2) + st.base[i];
+      st.t[i] += BKR;
+      while (st.t[i] >= op.map.rows_per_b) {
+        st.t[i] -= op.map.rows_per_b;
+        ++st.b[i];
+      }
+    }
+    const unsigned lds_addr = (unsigned)(uintptr_t)(lds_void_t*)(lds_tile + blk * 1024);
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(rs), "s"(lds_addr)
+        : "memory");
+  }
+}
+
+template <int MODE>
+__device__ __forceinline__ bf16x8 fragr(const char* lds_tile, int rb, int lane) {
+  if (MODE == 0) {
+    const int r = lane & 15;
+    const unsigned lo = (unsigned)(r * 64 + (((lane >> 4) ^ ((r >> 2) & 3)) * 16));
+    return __builtin_bit_cast(bf16x8, *(const u32x4_t*)(lds_tile + rb * 64 + lo));
+  }
+  return frag_k256(lds_tile, rb, 0, lane);
+}
+
+template <int AMODE, int BMODE>
+__device__ __forceinline__ void fragsr(const char* slot, int r0, int wc, int lane, bool withb,
+                                       bf16x8 (&fa)[4], bf16x8 (&fb)[4]) {
+  if (withb) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fb[j] = fragr<BMODE>(slot + TILER, wc + 16 * j, lane);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) fa[i] = fragr<AMODE>(slot, r0 + 16 * i, lane);
+}
+
+template <int AMODE, int BMODE>
+__global__ void __launch_bounds__(NT8) __attribute__((amdgpu_waves_per_eu(2, 2)))
+gemm_bf16_8r(Params P) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // NSLOT x (A, B)
+
+  const int zb = blockIdx.z / P.nprob, zp = blockIdx.z % P.nprob;
+  Problem pr = P.p[zp];
+  if (zb >= pr.batch) return;
+  if (zb > 0) {
+    pr.a.map.base = (const char*)pr.a.map.base + zb * pr.sA * 2;
+    pr.b.map.base = (const char*)pr.b.map.base + zb * pr.sB * 2;
+    pr.a.bytes -= zb * pr.sA * 2;
+    pr.b.bytes -= zb * pr.sB * 2;
+    pr.c.base = (const char*)pr.c.base + zb * pr.sC * 4;
+  }
+  const int gm = (pr.M + T8 - 1) / T8, gn = (pr.N + T8 - 1) / T8;
+  const int nwg = gm * gn;
+  const int nsplit = pr.ksplit > 1 ? pr.ksplit : 1;
+  const int ntot = nwg * nsplit;
+  int id = blockIdx.x;
+  if (id >= ntot) return;
+  {
+    const int q = ntot / 8, r = ntot % 8, x = id % 8;
+    id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + id / 8;
+  }
+  const int split = id / nwg;
+  id -= split * nwg;
+  int tm, tn;
+  {
+    const int per = 4 * gn;
+    const int g = id / per, r = id - g * per;
+    const int m0 = g * 4;
+    const int gs = min(4, gm - m0);
+    tm = (m0 + r % gs) * T8;
+    tn = (r / gs) * T8;
+  }
+  const int kbeg = nsplit > 1 ? split * pr.kchunk : 0;
+  const int kend = nsplit > 1 ? min(pr.K, kbeg + pr.kchunk) : pr.K;
+
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = (w >> 2) * 128, wc = (w & 3) * 64;
+  auto uni_ptr = [](const void* p) {
+    const unsigned long long v = (unsigned long long)p;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+    return (void*)(((unsigned long long)hi << 32) | lo);
+  };
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      uni_ptr(pr.a.map.base), 0, __builtin_amdgcn_readfirstlane((int)pr.a.bytes), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+      uni_ptr(pr.b.map.base), 0, __builtin_amdgcn_readfirstlane((int)pr.b.bytes), 0x00020000);
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (kend - kbeg + BKR - 1) / BKR;
+  StageR sa, sb;
+  stager_init<AMODE>(pr.a, sa, tm, pr.M, kbeg, w, lane);
+  stager_init<BMODE>(pr.b, sb, tn, pr.N, kbeg, w, lane);
+  constexpr int SLOT = 2 * TILER;
+#pragma unroll
+  for (int j = 0; j < NSLOT - 1; ++j) {
+    if (j < nk) {
+      stager<AMODE>(pr.a, ra, sa, smem + j * SLOT, kbeg + j * BKR, kend, w);
+      stager<BMODE>(pr.b, rb, sb, smem + j * SLOT + TILER, kbeg + j * BKR, kend, w);
+    }
+  }
+  {
+    const int after = min(NSLOT - 2, nk - 1);          // k-tiles issued after tile 0
+    if (after >= 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (after == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (after == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  bf16x8 b0[4], a0[4], a1[4];
+  fragsr<AMODE, BMODE>(smem, wr, wc, lane, true, a0, b0);
+  for (int kt = 0; kt < nk; ++kt) {
+    char* cur = smem + (kt % NSLOT) * SLOT;
+    fragsr<AMODE, BMODE>(cur, wr + 64, wc, lane, false, a1, b0);
+    mma8(a0, b0, acc, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();                       // slot kt % NSLOT read by all waves
+    if (kt + NSLOT - 1 < nk) {
+      const int k0 = kbeg + (kt + NSLOT - 1) * BKR;
+      stager<AMODE>(pr.a, ra, sa, cur, k0, kend, w);
+      stager<BMODE>(pr.b, rb, sb, cur + TILER, k0, kend, w);
+    }
+    bf16x8 b1[4];
+    if (kt + 1 < nk) {
+      const int after = min(NSLOT - 2, nk - 2 - kt);    // k-tiles issued after tile kt + 1
+      if (after >= 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      else if (after == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (after == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();                     // k-tile kt + 1 landed for all
+      const char* nxt = smem + ((kt + 1) % NSLOT) * SLOT;
+      fragsr<AMODE, BMODE>(nxt, wr, wc, lane, true, a0, b1);
+    }
+    mma8(a1, b0, acc, 1);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b0[j] = b1[j];
+  }
+
+  if (nsplit > 1) {
+    RowMap sm;
+    sm.base = pr.slab + (long long)split * pr.M * pr.N;
+    sm.stride_b = 0;
+    sm.stride_t = pr.N;
+    sm.rows_per_b = 0x7fffffff;
+    sm.t_mul = 1;
+    sm.t_add = 0;
+    sm.t_limit = 0x7fffffff;
+    sm.perm = nullptr;
+    epi8(pr, sm, true, acc, tm, tn, wr, wc, w, lane, smem);
+    return;
+  }
+  epi8(pr, pr.c, false, acc, tm, tn, wr, wc, w, lane, smem);
+}
+
 // Split-K finish: C(m,n) = alpha * sum_s slab[s][m][n] (fixed order s = 0..) +
 // bias + bias2 + beta * C, through C's row map.
 __global__ void splitk_reduce(const float* __restrict__ slab, int ksplit, int M, int N, RowMap c,
@@ -987,6 +1537,22 @@ bool kk256_ok(const asr_gemm_t* g, int nprob) {
   return true;
 }
 
+// Problems whose output extents both reach a 256-row tile take the 8-wave
+// 256 x 256 kernel (ASR_GEMM_8W=0 keeps them on the 128 x 128 kernel; read per
+// launch, for A/B runs).
+bool big8_ok(const asr_gemm_t* g, int nprob) {
+  const char* e = getenv("ASR_GEMM_8W");
+  if (e && e[0] == '0') return false;
+  for (int i = 0; i < nprob; ++i) {
+    if (g[i].M < T8 || g[i].N < T8) return false;
+    if (g[i].a.tap_group || g[i].b.tap_group) return false;     // taps: 128 x 128 kernel
+    // K-mode operands advance their (utterance, frame) pair by 64 k-rows per tile
+    for (const asr_operand_t* o : {&g[i].a, &g[i].b})
+      if (o->trans && o->map.rows_per_b > 0 && o->map.rows_per_b < BK8) return false;
+  }
+  return true;
+}
+
 int gemm_launch_own(const asr_gemm_t* problems, int nprob, int compute_dtype, void* workspace,
                     size_t ws_bytes, void* stream) {
   SplitPlan sp{};
@@ -1037,7 +1603,69 @@ int gemm_launch_own(const asr_gemm_t* problems, int nprob, int compute_dtype, vo
     flops += 2.0 * problems[i].M * problems[i].N * problems[i].K * P.p[i].batch;
   const int slot = prof_begin_launch(ASR_PROF_GEMM, s, flops);
   const int fast = compute_dtype == ASR_DT_BF16 ? fast_modes(problems, P) : -1;
-  if (fast == 3 && kk256_ok(problems, nprob)) {
+  if (fast >= 0 && big8_ok(problems, nprob)) {
+    // 256 x 256 8-wave kernel; the split never exceeds the workspace plan's
+    int maxwg8 = 0;
+    for (int i = 0; i < nprob; ++i) {
+      Problem& p = P.p[i];
+      const int tiles8 = ceil_div(p.M, T8) * ceil_div(p.N, T8);
+      int ks = 1;
+      if (p.ksplit > 1) {
+        ks = min(p.ksplit, max(1, ceil_div(512, tiles8)));
+        const int kc = ceil_div(ceil_div(p.K, ks), BK8) * BK8;
+        ks = ceil_div(p.K, kc);
+        p.kchunk = kc;
+      }
+      if (ks <= 1) { ks = 1; p.kchunk = p.K; }
+      p.ksplit = ks;
+      maxwg8 = max(maxwg8, tiles8 * ks);
+    }
+    static bool attr8 = false;
+    if (!attr8) {
+      bool ok = true;
+      ok &= hipFuncSetAttribute((const void*)gemm_bf16_8w<0, 0>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 4 * TILE8) == hipSuccess;
+      ok &= hipFuncSetAttribute((const void*)gemm_bf16_8w<0, 1>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 4 * TILE8) == hipSuccess;
+      ok &= hipFuncSetAttribute((const void*)gemm_bf16_8w<1, 0>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 4 * TILE8) == hipSuccess;
+      ok &= hipFuncSetAttribute((const void*)gemm_bf16_8w<1, 1>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 4 * TILE8) == hipSuccess;
+      ASR_REQUIRE(ok, ASR_ERR_HIP, "gemm: cannot raise the LDS limit of the 8-wave kernel");
+      attr8 = true;
+    }
+    const dim3 g8(maxwg8, 1, nprob * maxb);
+    const size_t lds8 = 4 * TILE8;
+    const char* er = getenv("ASR_GEMM_8R");
+    if (er && er[0] == '1') {
+      static bool attrr = false;
+      const int ldsr = NSLOT * 2 * TILER;
+      if (!attrr) {
+        bool ok = true;
+        ok &= hipFuncSetAttribute((const void*)gemm_bf16_8r<0, 0>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, ldsr) == hipSuccess;
+        ok &= hipFuncSetAttribute((const void*)gemm_bf16_8r<0, 1>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, ldsr) == hipSuccess;
+        ok &= hipFuncSetAttribute((const void*)gemm_bf16_8r<1, 0>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, ldsr) == hipSuccess;
+        ok &= hipFuncSetAttribute((const void*)gemm_bf16_8r<1, 1>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, ldsr) == hipSuccess;
+        ASR_REQUIRE(ok, ASR_ERR_HIP, "gemm: cannot raise the LDS limit of the ring kernel");
+        attrr = true;
+      }
+      switch (fast) {
+        case 0: hipLaunchKernelGGL((gemm_bf16_8r<0, 0>), g8, dim3(NT8), ldsr, s, P); break;
+        case 1: hipLaunchKernelGGL((gemm_bf16_8r<0, 1>), g8, dim3(NT8), ldsr, s, P); break;
+        case 2: hipLaunchKernelGGL((gemm_bf16_8r<1, 0>), g8, dim3(NT8), ldsr, s, P); break;
+        default: hipLaunchKernelGGL((gemm_bf16_8r<1, 1>), g8, dim3(NT8), ldsr, s, P); break;
+      }
+    } else switch (fast) {
+      case 0: hipLaunchKernelGGL((gemm_bf16_8w<0, 0>), g8, dim3(NT8), lds8, s, P); break;
+      case 1: hipLaunchKernelGGL((gemm_bf16_8w<0, 1>), g8, dim3(NT8), lds8, s, P); break;
+      case 2: hipLaunchKernelGGL((gemm_bf16_8w<1, 0>), g8, dim3(NT8), lds8, s, P); break;
+      default: hipLaunchKernelGGL((gemm_bf16_8w<1, 1>), g8, dim3(NT8), lds8, s, P); break;
+    }
+  } else if (fast == 3 && kk256_ok(problems, nprob)) {
     // 256 x 256 tiles; the split never exceeds the workspace plan's (128 x 128) split
     int maxwg2 = 0;
     for (int i = 0; i < nprob; ++i) {

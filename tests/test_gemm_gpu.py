@@ -202,3 +202,44 @@ def test_kmajor_256_tiles_two_problems_rowmapped(cuda_dev, monkeypatch):
         np.testing.assert_array_equal(got[1], ref_r)
     finally:
         ops.set_compute_dtype('fp32')
+
+
+@pytest.mark.parametrize('ring', ['0', '1'])
+@pytest.mark.parametrize('at,bt', [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize('M,N,K', [(256, 256, 64), (529, 389, 3000), (300, 260, 200),
+                                    (1024, 512, 8000), (777, 1030, 1000)])
+def test_gemm_8wave_256_tiles_exact(at, bt, M, N, K, ring, cuda_dev, monkeypatch):
+    """The 8-wave 256 x 256 kernel (gemm_bf16_8w) in every operand layout:
+    ragged M / N / K (partial tiles and a K that is not a multiple of the
+    64-deep k-tile), a single k-tile, split-K (long K, few tiles), padded
+    leading dimensions, alpha / beta / bias pair; both forms (two 64-deep
+    buffers, and the 32-deep five-slot ring: ASR_GEMM_8R).  Exact on small
+    integers."""
+    monkeypatch.setenv('ASR_GEMM_8W', '1')
+    monkeypatch.setenv('ASR_GEMM_8R', ring)
+    ops = _ops()
+    ops.set_compute_dtype('bf16')
+    try:
+        rng = np.random.RandomState(M * 7 + N * 3 + K + 11 * at + 13 * bt)
+        pa, pb = 8, 16
+        sa = _store(rng, K if at else M, M if at else K, (M if at else K) + pa)
+        sb = _store(rng, K if bt else N, N if bt else K, (N if bt else K) + pb)
+        A = (sa[:, :M].T if at else sa[:, :K]).astype(np.float64)
+        Bm = (sb[:, :N].T if bt else sb[:, :K]).astype(np.float64)
+        c0 = rng.randint(-4, 5, (M, N)).astype(np.float32)
+        b1 = rng.randint(-8, 9, N).astype(np.float32)
+        b2 = rng.randint(-8, 9, N).astype(np.float32)
+        ad = torch.from_numpy(sa).to(torch.bfloat16).to(cuda_dev)
+        bd = torch.from_numpy(sb).to(torch.bfloat16).to(cuda_dev)
+        C = torch.from_numpy(c0).to(cuda_dev)
+        p = ops.gemm_problem(ops.operand(ad, at, ops.rowmap(sa.shape[1])),
+                             ops.operand(bd, bt, ops.rowmap(sb.shape[1])), C, ops.rowmap(N),
+                             M, N, K, alpha=2.0, beta=1.0,
+                             bias=torch.from_numpy(b1).to(cuda_dev),
+                             bias2=torch.from_numpy(b2).to(cuda_dev))
+        ops.run_gemm([p], cuda_dev)
+        torch.cuda.synchronize()
+        ref = 2.0 * (A @ Bm.T) + c0 + b1 + b2
+        np.testing.assert_array_equal(C.cpu().numpy(), ref)
+    finally:
+        ops.set_compute_dtype('fp32')

@@ -30,8 +30,20 @@ shapes = {
     'dW   M=4096 N=1024 K=32000 (KK)': [ops.gemm_problem(ops.operand(dg, 1, R(8 * H)),
                                                          ops.operand(x, 1, R(D)), dw, R(D), 8 * H,
                                                          D, M, beta=1.0)],
+    'dWhh 2x M=2048 N=512 K=32000 (KK)': [
+        ops.gemm_problem(ops.operand(dg, 1, R(8 * H)), ops.operand(x, 1, R(D)), dw, R(H),
+                         4 * H, H, M, beta=1.0),
+        ops.gemm_problem(ops.operand(dg, 1, R(8 * H), offset=4 * H),
+                         ops.operand(x, 1, R(D), offset=H), dw, R(H), 4 * H, H, M, beta=1.0,
+                         c_offset=4 * H * H)],
 }
+tag = ' '.join('%s=%s' % (k, os.environ[k]) for k in ('ASR_GEMM_LIB', 'ASR_GEMM_8W')
+               if k in os.environ)
+print('--', tag or 'defaults')
+only = os.environ.get('GEMM_BENCH_ONLY')
 for name, probs in shapes.items():
+    if only and not name.startswith(only):
+        continue
     for _ in range(3):
         ops.run_gemm(probs, dev)
     torch.cuda.synchronize()
