@@ -282,7 +282,8 @@ def cpu_baseline(cfg, batch, n_utts):
             ref_loss = {'f32': float(_oracle_loss(cfg, sd, sub)),
                         'f64': float(_oracle_loss(cfg, {k: v.double() if v.is_floating_point()
                                                         else v for k, v in sd.items()}, sub))}
-        trainable = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+        trainable = {k: v.clone().requires_grad_(v.is_floating_point() and 'running' not in k)
+                     for k, v in sd.items()}
         params = [v for k, v in trainable.items() if v.is_floating_point() and 'running' not in k]
         opt = torch.optim.Adam(params, lr=p['learning_rate'], weight_decay=p['weight_decay'])
         t0 = time.perf_counter()
@@ -414,6 +415,14 @@ def main():
         def step(m, b):
             return train_step(m, b, p['clip_grad_norm'], grad_scale=grad_scale)
     frames_per_step = float(batch['x_lens'].sum())
+    # inputs resident in HBM when the timed region starts (the task's metric
+    # definition): the features go to the device once; the models take a
+    # device tensor wherever the reference takes the numpy array (np2var
+    # passes it through).  Labels and lengths stay host arrays as in the
+    # reference's batch dict.  DESIGN.md notes the H2D-inclusive rate.
+    host_batch = batch
+    batch = dict(batch)
+    batch['xs'] = torch.from_numpy(np.ascontiguousarray(host_batch['xs'])).to(dev)
 
     for _ in range(args.warmup):
         model, _ = step(model, batch)
@@ -464,7 +473,7 @@ def main():
 
     cpu = parity = None
     if world == 1 and not args.no_cpu_baseline:
-        cpu, sd0, sub, ref_loss = cpu_baseline(cfg, batch, args.cpu_utts)
+        cpu, sd0, sub, ref_loss = cpu_baseline(cfg, host_batch, args.cpu_utts)
         if not args.no_parity:
             parity = parity_report(cfg, sd0, sub, ref_loss)
 

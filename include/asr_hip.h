@@ -162,13 +162,6 @@ size_t asr_gemm_workspace_bytes(const asr_gemm_t* problems, int nprob);
 int asr_gemm_ws(const asr_gemm_t* problems, int nprob, int compute_dtype, void* workspace,
                 size_t ws_bytes, void* stream);
 
-/* bf16 compute: plain problems -- dense row/column-major operands without a
- * row map, tap addressing or batching, not both K-major, 2*M*N*K >= 4e9 --
- * run on hipBLASLt (heuristic first choice, cached per shape; the workspace
- * then also holds 32 MB for the library and the summed bias pair).  Returns 1
- * when that path is live (ASR_GEMM_LIB != 0 and a hipBLASLt handle exists). */
-int asr_gemm_library_ready(void);
-
 /* out0[n] (+ out1[n] if non-NULL) += alpha * sum_m g[m*ld + n]  (bias grads of
  * nn.Linear / nn.LSTM bias_ih and bias_hh); fixed-order, deterministic. */
 size_t asr_colsum_workspace_bytes(int M, int N);

@@ -18,11 +18,6 @@
 #include "prof.h"
 
 namespace asr {
-// gemm_lib.hip: plain bf16 problems on hipBLASLt
-bool gemm_lib_eligible(const asr_gemm_t& g, int compute_dtype);
-size_t gemm_lib_workspace_bytes();
-int gemm_lib_run(const asr_gemm_t& g, void* ws, size_t ws_bytes, hipStream_t s);
-
 namespace {
 
 constexpr int BM = 128, BN = 128, BK = 32, NT = 256;
@@ -954,6 +949,7 @@ __device__ __forceinline__ void epi8(const Problem& pr, const RowMap& cm, bool r
   // a plain C map (every row valid, no batch split) needs no division per row
   const bool plain = cm.rows_per_b == 0x7fffffff && cm.t_mul == 1 && cm.t_add == 0 &&
                      cm.t_limit == 0x7fffffff && !cm.perm;
+  const bool bias_vec = ((uintptr_t)pr.bias & 15) == 0 && ((uintptr_t)pr.bias2 & 15) == 0;
 #pragma unroll
   for (int h = 0; h < 4; ++h) {
     __syncthreads();   // LDS free (k-loop done / previous quarter read back)
@@ -976,17 +972,30 @@ __device__ __forceinline__ void epi8(const Problem& pr, const RowMap& cm, bool r
       if (off < 0) continue;
       float* cp = (float*)cm.base + off + n;
       float o[4] = {v.x, v.y, v.z, v.w};
+      const bool full = n + 4 <= pr.N;
       if (!raw) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          o[e] *= pr.alpha;
-          if (n + e < pr.N) {
-            if (pr.bias) o[e] += pr.bias[n + e];
-            if (pr.bias2) o[e] += pr.bias2[n + e];
+        for (int e = 0; e < 4; ++e) o[e] *= pr.alpha;
+        if (full && bias_vec) {   // the bias pair as two 16-B loads
+          if (pr.bias) {
+            const float4 b = *reinterpret_cast<const float4*>(pr.bias + n);
+            o[0] += b.x; o[1] += b.y; o[2] += b.z; o[3] += b.w;
+          }
+          if (pr.bias2) {
+            const float4 b = *reinterpret_cast<const float4*>(pr.bias2 + n);
+            o[0] += b.x; o[1] += b.y; o[2] += b.z; o[3] += b.w;
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if (n + e < pr.N) {
+              if (pr.bias) o[e] += pr.bias[n + e];
+              if (pr.bias2) o[e] += pr.bias2[n + e];
+            }
           }
         }
       }
-      if (n + 4 <= pr.N && ((uintptr_t)cp & 15) == 0) {
+      if (full && ((uintptr_t)cp & 15) == 0) {
         if (!raw && pr.beta != 0.f) {
           const float4 c = *reinterpret_cast<const float4*>(cp);
           o[0] += pr.beta * c.x; o[1] += pr.beta * c.y; o[2] += pr.beta * c.z; o[3] += pr.beta * c.w;
@@ -1123,7 +1132,8 @@ gemm_bf16_8w(Params P) {
 }
 
 // ---------------------------------------------------------------------------
-// Ring variant of the 8-wave kernel (ASR_GEMM_8R=1): 32-deep k-tiles in a
+// Ring form of the 8-wave kernel (the default; ASR_GEMM_8R=0 selects the
+// two-buffer form above): 32-deep k-tiles in a
 // five-slot LDS ring (5 x 32 KB = 160 KB), three k-tiles in flight behind the
 // one being read (the 64-deep two-buffer form keeps one).  Per k-tile:
 //   read A rows 64-127 | MFMA rows 0-63
@@ -1306,24 +1316,27 @@ gemm_bf16_8r(Params P) {
   bf16x8 b0[4], a0[4], a1[4];
   fragsr<AMODE, BMODE>(smem, wr, wc, lane, true, a0, b0);
   for (int kt = 0; kt < nk; ++kt) {
-    char* cur = smem + (kt % NSLOT) * SLOT;
+    const char* cur = smem + (kt % NSLOT) * SLOT;
+    // slot (kt - 1) % NSLOT was last read before iteration kt - 1's barrier
+    // the DMA of k-tile kt + 4 is spread over the two MFMA phases (A before the
+    // first, B before the second): an LDS-DMA issue stalls the wave for tens of
+    // cycles, so a burst of four would open a gap in the MFMA stream
+    const bool dma = kt + NSLOT - 1 < nk;
+    char* fre = smem + ((kt + NSLOT - 1) % NSLOT) * SLOT;
+    const int kd = kbeg + (kt + NSLOT - 1) * BKR;
+    if (dma) stager<AMODE>(pr.a, ra, sa, fre, kd, kend, w);
     fragsr<AMODE, BMODE>(cur, wr + 64, wc, lane, false, a1, b0);
     mma8(a0, b0, acc, 0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();                       // slot kt % NSLOT read by all waves
-    if (kt + NSLOT - 1 < nk) {
-      const int k0 = kbeg + (kt + NSLOT - 1) * BKR;
-      stager<AMODE>(pr.a, ra, sa, cur, k0, kend, w);
-      stager<BMODE>(pr.b, rb, sb, cur + TILER, k0, kend, w);
-    }
+    if (dma) stager<BMODE>(pr.b, rb, sb, fre + TILER, kd, kend, w);
     bf16x8 b1[4];
     if (kt + 1 < nk) {
       const int after = min(NSLOT - 2, nk - 2 - kt);    // k-tiles issued after tile kt + 1
-      if (after >= 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-      else if (after == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else if (after == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();                     // k-tile kt + 1 landed for all
+      if (after >= 3) asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory");
+      else if (after == 2) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+      else if (after == 1) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      // k-tile kt + 1 landed for all waves; every wave's reads of slot kt done
+      __builtin_amdgcn_s_barrier();
       const char* nxt = smem + ((kt + 1) % NSLOT) * SLOT;
       fragsr<AMODE, BMODE>(nxt, wr, wc, lane, true, a0, b1);
     }
@@ -1331,6 +1344,7 @@ gemm_bf16_8r(Params P) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) b0[j] = b1[j];
   }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 
   if (nsplit > 1) {
     RowMap sm;
@@ -1434,21 +1448,17 @@ int fill_operand(const asr_operand_t& o, Operand* op, const char* name) {
 struct SplitPlan {
   int ksplit[2], kchunk[2];
   size_t slab_off[2];
-  size_t lib_off;   // hipBLASLt workspace (after the slabs) when a problem runs there
   size_t bytes;
 };
 
 SplitPlan plan_split(const asr_gemm_t* g, int nprob) {
   SplitPlan sp{};
-  bool lib = false;
   for (int i = 0; i < nprob; ++i) {
     // per problem: the problems of one launch run side by side (blockIdx.z), so
     // a few-tile dW next to a many-tile dX still gets its own K split
     const int tiles = ceil_div(g[i].M, BM) * ceil_div(g[i].N, BN);
-    const bool on_lib = gemm_lib_eligible(g[i], ASR_DT_BF16);
-    lib |= on_lib;
     int ks = 1;
-    if (!on_lib && g[i].batch <= 1 && tiles > 0 && tiles < 512 && g[i].K >= 1024) {
+    if (g[i].batch <= 1 && tiles > 0 && tiles < 512 && g[i].K >= 1024) {
       // a few-tile, long-K product (the decoder / projection weight gradients,
       // K = B*S or B*T) is latency-bound per work-group: chunks >= 128
       ks = min(ceil_div(1024, tiles), g[i].K / 128);
@@ -1466,8 +1476,6 @@ SplitPlan plan_split(const asr_gemm_t* g, int nprob) {
     sp.slab_off[i] = sp.bytes;
     if (ks > 1) sp.bytes += ((size_t)ks * g[i].M * g[i].N * sizeof(float) + 255) & ~(size_t)255;
   }
-  sp.lib_off = sp.bytes;
-  if (lib) sp.bytes += gemm_lib_workspace_bytes();
   return sp;
 }
 
@@ -1636,8 +1644,8 @@ int gemm_launch_own(const asr_gemm_t* problems, int nprob, int compute_dtype, vo
     }
     const dim3 g8(maxwg8, 1, nprob * maxb);
     const size_t lds8 = 4 * TILE8;
-    const char* er = getenv("ASR_GEMM_8R");
-    if (er && er[0] == '1') {
+    const char* er = getenv("ASR_GEMM_8R");   // ring form by default (ASR_GEMM_8R=0: two buffers)
+    if (!(er && er[0] == '0')) {
       static bool attrr = false;
       const int ldsr = NSLOT * 2 * TILER;
       if (!attrr) {
@@ -1728,34 +1736,10 @@ int gemm_launch_own(const asr_gemm_t* problems, int nprob, int compute_dtype, vo
   return ASR_OK;
 }
 
-// Plain bf16 problems go to hipBLASLt (gemm_lib.hip), the rest -- row-mapped,
-// tap-addressed, batched, fp32 -- to the kernels above.
 int gemm_launch(const asr_gemm_t* problems, int nprob, int compute_dtype, void* workspace,
                 size_t ws_bytes, void* stream) {
   ASR_REQUIRE(problems && nprob >= 1 && nprob <= 2, ASR_ERR_ARG, "gemm: nprob must be 1 or 2");
-  if (compute_dtype != ASR_DT_BF16)
-    return gemm_launch_own(problems, nprob, compute_dtype, workspace, ws_bytes, stream);
-  asr_gemm_t rest[2];
-  int nrest = 0;
-  const SplitPlan sp = workspace ? plan_split(problems, nprob) : SplitPlan{};
-  hipStream_t s = (hipStream_t)stream;
-  for (int i = 0; i < nprob; ++i) {
-    const asr_gemm_t& g = problems[i];
-    int rc = 0;
-    if (gemm_lib_eligible(g, compute_dtype)) {
-      ASR_REQUIRE(g.a.ptr && g.b.ptr && g.c, ASR_ERR_ARG, "gemm: null operand");
-      void* lws = workspace && ws_bytes >= sp.bytes ? (char*)workspace + sp.lib_off : nullptr;
-      const size_t lbytes = lws ? ws_bytes - sp.lib_off : 0;
-      const int slot = prof_begin_launch(ASR_PROF_GEMM, s, 2.0 * g.M * g.N * g.K);
-      rc = gemm_lib_run(g, lws, lbytes, s);
-      if (rc < 0) return rc;
-      prof_end_launch(ASR_PROF_GEMM, slot, s);   // rc == 0 (no algorithm) is never hit in
-                                                 // practice; it would log an empty launch
-    }
-    if (rc == 0) rest[nrest++] = g;
-  }
-  if (nrest == 0) return ASR_OK;
-  return gemm_launch_own(rest, nrest, compute_dtype, workspace, ws_bytes, stream);
+  return gemm_launch_own(problems, nprob, compute_dtype, workspace, ws_bytes, stream);
 }
 
 }  // namespace

@@ -125,7 +125,7 @@ def colsum_accumulate(g2d, out0, out1=None, alpha=1.0):
 # Linear (LinearND, linear.py:15-47): y = x W^T + b on the last dim
 # ---------------------------------------------------------------------------
 # bf16 mode stages f32 GEMM operands in bf16 (one conversion pass) when a
-# product is at least this large, so it takes the bf16 fast path / hipBLASLt
+# product is at least this large, so it takes the bf16 fast / 8-wave kernels
 # instead of the generic kernel converting inside its loads (the word-level CTC
 # head, 8000 x 640 x 10001, ran at ~140 TF/s that way).
 _STAGE_FLOPS = 2e9

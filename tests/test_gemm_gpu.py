@@ -1,9 +1,10 @@
-"""Plain bf16 products that asr_gemm hands to hipBLASLt (csrc/gemm_lib.hip):
-the three layouts it takes (K-major x K-major stays on the own split-K kernel
-and is checked here too), padded leading dimensions, alpha/beta, one bias and
-the summed bias pair (nn.LSTM's b_ih + b_hh), and a launch that mixes a library
-problem with a row-mapped one.  Small-integer operands make bf16 products with
-f32 accumulation exact, so the results must equal float64 bit for bit."""
+"""The bf16 GEMM kernels of csrc/gemm.hip (no vendor library on the path):
+plain products in all four operand layouts, padded leading dimensions,
+alpha/beta, one bias and the summed bias pair (nn.LSTM's b_ih + b_hh), a launch
+that mixes a plain problem with a row-mapped one, the 256 x 256 8-wave kernel
+and its ring variant over ragged shapes and split-K.  Small-integer operands
+make bf16 products with f32 accumulation exact, so the results must equal
+float64 bit for bit."""
 import numpy as np
 import pytest
 import torch
@@ -24,14 +25,12 @@ def _store(rng, rows, cols, ld):
 
 @pytest.mark.parametrize('at,bt', [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize('nbias', [0, 1, 2])
-def test_library_gemm_exact(at, bt, nbias, cuda_dev):
-    from pytorch_end2end_speech_recognition_amd import _native as N
+def test_plain_gemm_exact(at, bt, nbias, cuda_dev):
     ops = _ops()
-    assert N.query('asr_gemm_library_ready') == 1
     ops.set_compute_dtype('bf16')
     try:
         rng = np.random.RandomState(10 * at + bt + 100 * nbias)
-        M, Nn, K = 2048, 1024, 1032     # 2*M*N*K >= 4e9: library-eligible
+        M, Nn, K = 2048, 1024, 1032
         pad = 8
         sa = _store(rng, K if at else M, M if at else K, (M if at else K) + pad)
         sb = _store(rng, K if bt else Nn, Nn if bt else K, (Nn if bt else K) + pad)
@@ -65,9 +64,9 @@ def test_library_gemm_exact(at, bt, nbias, cuda_dev):
         ops.set_compute_dtype('fp32')
 
 
-def test_library_and_mapped_problems_in_one_launch(cuda_dev):
-    """nprob = 2: a plain product (library) next to a subsampled-row product
-    (own kernel, t_mul = 2) that also needs a split-K slab."""
+def test_plain_and_mapped_problems_in_one_launch(cuda_dev):
+    """nprob = 2: a plain product next to a subsampled-row product (t_mul = 2)
+    that also needs a split-K slab."""
     ops = _ops()
     ops.set_compute_dtype('bf16')
     try:
@@ -213,7 +212,7 @@ def test_gemm_8wave_256_tiles_exact(at, bt, M, N, K, ring, cuda_dev, monkeypatch
     ragged M / N / K (partial tiles and a K that is not a multiple of the
     64-deep k-tile), a single k-tile, split-K (long K, few tiles), padded
     leading dimensions, alpha / beta / bias pair; both forms (two 64-deep
-    buffers, and the 32-deep five-slot ring: ASR_GEMM_8R).  Exact on small
+    buffers: ASR_GEMM_8R=0, and the 32-deep five-slot ring, the default).  Exact on small
     integers."""
     monkeypatch.setenv('ASR_GEMM_8W', '1')
     monkeypatch.setenv('ASR_GEMM_8R', ring)

@@ -1,0 +1,10 @@
+#!/bin/bash
+# interleaved whole-step A/B of environment switches: VARIANTS="A=1 B=0;..." (';'-separated)
+set -o pipefail
+IFS=';' read -ra VS <<< "${VARIANTS}"
+for r in 1 2; do
+  for v in "${VS[@]}"; do
+    out=$(env $v timeout -k 10 200 python -u bench.py --config ${CONFIG:-ctc5x512} --steps ${STEPS:-10} --warmup 3 --no-cpu-baseline 2>&1 | tail -1)
+    echo "[$v] $(echo $out | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["value"])' 2>/dev/null || echo $out | cut -c1-200)"
+  done
+done
