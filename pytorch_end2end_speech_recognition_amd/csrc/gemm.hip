@@ -1548,6 +1548,14 @@ bool kk256_ok(const asr_gemm_t* g, int nprob) {
 // Problems whose output extents both reach a 256-row tile take the 8-wave
 // 256 x 256 kernel (ASR_GEMM_8W=0 keeps them on the 128 x 128 kernel; read per
 // launch, for A/B runs).
+// Work-groups a split-K product of the 8-wave kernel aims for (ASR_GEMM_SPLITWG,
+// default 512: two per CU); fewer splits mean smaller f32 slabs to reduce.
+int split_target() {
+  const char* e = getenv("ASR_GEMM_SPLITWG");
+  const int v = e ? atoi(e) : 0;
+  return v > 0 ? v : 512;
+}
+
 bool big8_ok(const asr_gemm_t* g, int nprob) {
   const char* e = getenv("ASR_GEMM_8W");
   if (e && e[0] == '0') return false;
@@ -1619,7 +1627,7 @@ int gemm_launch_own(const asr_gemm_t* problems, int nprob, int compute_dtype, vo
       const int tiles8 = ceil_div(p.M, T8) * ceil_div(p.N, T8);
       int ks = 1;
       if (p.ksplit > 1) {
-        ks = min(p.ksplit, max(1, ceil_div(512, tiles8)));
+        ks = min(p.ksplit, max(1, ceil_div(split_target(), tiles8)));
         const int kc = ceil_div(ceil_div(p.K, ks), BK8) * BK8;
         ks = ceil_div(p.K, kc);
         p.kchunk = kc;
