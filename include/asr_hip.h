@@ -343,10 +343,10 @@ int asr_softmax(const float* x, int R, int V, float* y, void* stream);
  *   W_d / W_c GEMMs).  Outputs: gates_dg (dgates over the saved gates; feeds
  *   dW_ih, dW_hh, db and the embedding gradient), dctx_tot [B][S][E] (feeds
  *   d enc = aw^T dctx_tot), d_enc_a [B][T][A], d_h0 [B][D] (nullable),
- *   dwd_all [B][S][A] (dW_dec = dwd^T dec), per-(step, frame chunk) partials
- *   dv_part [B][S][NC][A], dwc_part [B][S][NC][A*C], dcw_part [B][S][NC][C*K]
- *   with NC = asr_attdec_chunks(dims) (column sums give
- *   dV, dW_conv, d conv kernel; deterministic).
+ *   dwd_all [B][S][A] (dW_dec = dwd^T dec), per-(utterance, frame chunk)
+ *   partials summed over the steps dv_part [B][NC][A], dwc_part [B][NC][A*C],
+ *   dcw_part [B][NC][C*K] with NC = asr_attdec_chunks(dims) (column sums give
+ *   dV, dW_conv, d conv kernel; fixed summation order, deterministic).
  */
 typedef struct {
   int B, T, E, A, C, K, D, S;
@@ -442,7 +442,7 @@ int asr_attdec_forward_ex(const asr_attdec_dims_t* dims, const asr_attdec_opts_t
  * ctx_out [B][E] = aw_out . enc.  Backward (cotangents d_ctx [B][E],
  * d_aw_out [B][T] nullable): d_enc_a, d_dec, d_aw_prev, dctx_tot, dwd (d of
  * W_dec dec_out) written; dv_part / dwc_part / dcw_part hold
- * B * 2 * asr_attdec_chunks rows whose column sums are dV, dW_conv and the
+ * B * asr_attdec_chunks rows whose column sums are dV, dW_conv and the
  * conv-kernel gradient.  The caller forms dW_dec = dwd^T dec_out and
  * d enc = aw_out^T dctx_tot. */
 size_t asr_att_step_workspace_bytes(const asr_attdec_dims_t* dims);
@@ -464,6 +464,10 @@ int asr_att_step_backward(const asr_attdec_dims_t* dims, const float* enc, const
  * template (10 or 3; 0 = generic), forward 32-frame chunks per utterance,
  * backward template, backward chunks}. */
 int asr_attdec_last_launch(int* out4);
+/* {forward, backward}: 1 if the last decoder pass of that direction ran as one
+ * persistent launch (bf16, B <= 32, no scheduled sampling; ASR_ATT_PERSIST=0
+ * disables it). */
+int asr_attdec_persist_last(int* out2);
 int asr_attdec_backward_ex(const asr_attdec_dims_t* dims, const asr_attdec_opts_t* opts,
                            int compute_dtype, const float* enc, const float* enc_a,
                            const int32_t* lens, const float* w_ih_ctx, long long ld_ih,

@@ -122,6 +122,7 @@ SIGNATURES = {
     'asr_lstm_status_gather': (c_int, [c_vp, c_int, c_vp]),
     'asr_lstm_status_inject': (c_int, [c_int, c_vp]),
     'asr_attdec_last_launch': (c_int, [c_vp]),
+    'asr_attdec_persist_last': (c_int, [c_vp]),
     'asr_lstm_cell_forward': (c_int, [c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
     'asr_lstm_cell_backward': (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp,
                                        c_vp]),

@@ -756,7 +756,10 @@ __global__ void __launch_bounds__(ATT_THREADS) att_bwd_energy(
   ATT_TR(16);
   // combine the per-wave partials in LDS in a fixed wave order, then one store
   // of this chunk's slots
-  const long long slot = ((long long)b * d.S + t) * NC + ch;
+  // this chunk's row of the partials, summed over the steps in backward order
+  // (the last step writes, earlier ones add: fixed order, deterministic)
+  const long long slot = (long long)b * NC + ch;
+  const bool first = t == d.S - 1;
   float* cV = L.cmb;                  // [A]
   float* cWd = cV + d.A;              // [A]
   float* cWc = cWd + d.A;             // [A*C]
@@ -780,10 +783,10 @@ __global__ void __launch_bounds__(ATT_THREADS) att_bwd_energy(
   float* dwcp = dwc_part + slot * d.A * d.C;
   float* dwdp = dwd_chunk + ((long long)b * NC + ch) * d.A;
   for (int i = tid; i < d.A; i += blockDim.x) {
-    dvp[i] = cV[i];
+    dvp[i] = first ? cV[i] : dvp[i] + cV[i];
     dwdp[i] = cWd[i];
   }
-  for (int i = tid; i < d.A * d.C; i += blockDim.x) dwcp[i] = cWc[i];
+  for (int i = tid; i < d.A * d.C; i += blockDim.x) dwcp[i] = first ? cWc[i] : dwcp[i] + cWc[i];
   ATT_TR(17);
 }
 
@@ -863,13 +866,15 @@ __global__ void __launch_bounds__(ATT_THREADS) att_bwd_conv(
     carry[(long long)b * d.T + j] = s;
   }
   // conv-kernel partial: dcw[c, k] = sum_{tt in chunk} dF[tt, c] aw_{t-1}[tt + k - half]
-  float* dcwp = dcw_part + (((long long)b * d.S + t) * NC + ch) * d.C * d.K;
+  // (row b * NC + ch, summed over the steps like att_bwd_energy's partials)
+  float* dcwp = dcw_part + ((long long)b * NC + ch) * d.C * d.K;
+  const bool first = t == d.S - 1;
   const int nrow = min(TCH, d.T - j0);
   for (int i = tid; i < d.C * d.K; i += nt) {
     const int c = i / d.K, k = i % d.K;
     float s = 0.f;
     s = dot_lds(dFw + (size_t)half * d.C + c, d.C, awin + k, 1, nrow);
-    dcwp[i] = s;
+    dcwp[i] = first ? s : dcwp[i] + s;
   }
   ATT_TR(24);
   // dW_dec input of step t (sum of the chunks' partials: every chunk forms it,
@@ -1065,7 +1070,7 @@ size_t al256(size_t n) { return (n + 255) & ~size_t(255); }
 // Workspace: [Wcat (fwd) or Wcat^T (bwd)][energies / d aw [B][T]] and, backward
 // only, [r][carry][ddec_att][dc][flags][dF [B][T][C]][dWd chunk partials].
 struct AttWs {
-  size_t wcat, ebuf, r, carry, ddec, dc, flags, dF, dwdc, wd, total;
+  size_t wcat, ebuf, r, carry, ddec, dc, flags, dF, dwdc, wd, pbuf, ctr, total;
 };
 AttWs att_ws(const Dims& d, int cdt, bool bwd) {
   AttWs w;
@@ -1081,11 +1086,415 @@ AttWs att_ws(const Dims& d, int cdt, bool bwd) {
     w.dF = o; o += al256((size_t)d.B * d.T * d.C * 4);
     w.dwdc = o; o += al256((size_t)d.B * att_chunks(d) * d.A * 4);
     w.wd = o; o += al256((size_t)d.B * d.S * d.A * 4);
+  } else {   // the persistent forward's W_dec h partials and group counters
+    w.pbuf = o; o += al256((size_t)8 * 32 * 4 * d.A * 4);
+    w.ctr = o; o += al256((size_t)(1 + 8) * 64 * 4);
   }
   w.total = o;
   return w;
 }
 
+// ---------------------------------------------------------------------------
+// Persistent forward pass (bf16 mode): all S steps of cell_fwd -> att_energy
+// -> att_context in ONE launch of 256 work-groups (one per CU).
+//
+// The batch is split into 8 groups of up to 4 utterances (b = g + 8 slot, so
+// the length-sorted batch spreads evenly); group g is the 32 work-groups
+// blockIdx % 8 == g, which the dispatcher deals to one XCD, so every
+// hand-off of a group stays in one L2.  Member m (= blockIdx / 8) of a group
+// holds, for the whole pass:
+//   cell role   : hidden units [m UPW, (m+1) UPW) of the group's 4 utterances;
+//                 its 4 UPW rows of Wcat = [W_ih_ctx | W_hh] as MFMA B
+//                 fragments in VGPRs (3 row tiles x 2 K halves on waves 0-5),
+//                 the cell states in registers, W_dec's columns of its units;
+//   frame role  : utterance slot m / 8, frames [ch FCH, (ch+1) FCH) and
+//                 context columns [ch ECW, (ch+1) ECW), ch = m % 8: the conv
+//                 kernel, W_conv, V in LDS, the frames' enc_a rows in VGPRs,
+//                 the enc column slice [T][ECW] in LDS, and aw_{t-1} of the
+//                 whole utterance (recomputed from the energies by each of its
+//                 8 work-groups, so the 201-tap conv windows need no hand-off).
+// Three group-wide hand-offs per step, each a monotonic per-group counter
+// (MI355X_MICROARCH.md visibility, valid form row 1: sc1 payload stores, every
+// storing wave's vmcnt(0), a workgroup barrier, one agent-scope add; one-lane
+// sc1 poll, workgroup barrier, sc1 payload loads):
+//   C (cell)   -> h_t into x[b][t+1][E:], W_dec[:, units] h_t partials
+//   E (energy) -> masked, sharpened energies of the frame chunk
+//   X (context)-> softmax, aw_t, ctx_t into x[b][t+1][:E]
+// Same arithmetic as the per-step kernels (bf16 MFMA for the cell, f32 for
+// the attention); only f32 summation orders differ.  Spins are bounded: a
+// give-up sets the abort word and the recurrence status bit (step skipped).
+// ---------------------------------------------------------------------------
+constexpr int PD_GROUPS = 8;
+constexpr int PD_MEMBERS = 32;
+constexpr int PD_SLOTS = 4;
+constexpr int PD_CHUNKS = PD_MEMBERS / PD_SLOTS;
+constexpr int PD_THREADS = 512;
+constexpr int PD_KMAX = 16;      // K blocks of 32 per wave: E + D <= 1024
+constexpr int PD_UMAX = 12;      // hidden units per member: 4 UPW <= 48 rows (3 MFMA tiles)
+constexpr int PD_FPW = 8;        // frames per wave: FCH <= 64
+constexpr int PD_CTR = 64;       // ints per counter (own 256-B line)
+constexpr unsigned PD_SPIN_LIMIT = 1u << 20;
+
+typedef __attribute__((address_space(1))) int pd_gint;
+typedef __attribute__((ext_vector_type(4))) unsigned int pd_u32x4;
+
+struct PdGeom {
+  int UPW, FCH, ECW, ED, NKB, half;
+  int xs, wdl, cw, wc, v, awp, wd, wq, f, hs, part, red, cpart, encs, total;   // LDS floats
+};
+
+__host__ __device__ inline PdGeom pd_geom(const Dims& d) {
+  PdGeom g;
+  g.UPW = (d.D + PD_MEMBERS - 1) / PD_MEMBERS;
+  g.FCH = (d.T + PD_CHUNKS - 1) / PD_CHUNKS;
+  g.ECW = (d.E + PD_CHUNKS - 1) / PD_CHUNKS;
+  g.ED = d.E + d.D;
+  g.NKB = (g.ED + 31) / 32;
+  g.half = d.K / 2;
+  int o = 0;
+  g.xs = o; o += PD_SLOTS * g.ED;
+  g.wdl = o; o += d.A * g.UPW;
+  g.cw = o; o += d.C * d.K;
+  g.wc = o; o += d.A * d.C;
+  g.v = o; o += d.A;
+  g.awp = o; o += d.T + 2 * g.half + 4;
+  g.wd = o; o += d.A;
+  g.wq = o; o += 4 * d.A;
+  g.f = o; o += g.FCH * d.C;
+  g.hs = o; o += PD_SLOTS * PD_UMAX;
+  g.part = o; o += 6 * PD_SLOTS * 16;
+  g.red = o; o += 64;
+  g.cpart = o; o += PD_THREADS;
+  g.encs = o; o += d.T * g.ECW;
+  g.total = (o + 3) & ~3;
+  return g;
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t pd_rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float pd_ld(__amdgpu_buffer_rsrc_t r, long long i) {   // sc1
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (unsigned)(i * 4), 0, 16));
+}
+__device__ __forceinline__ void pd_st(__amdgpu_buffer_rsrc_t r, long long i, float v) {  // sc1
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (unsigned)(i * 4), 0, 16);
+}
+
+// One lane: wait until *ctr >= target.  false = gave up (abort word set / timeout).
+__device__ __forceinline__ bool pd_wait(int* ctr, int target, int* abort_w, int* status) {
+  pd_gint* c = (pd_gint*)ctr;
+  pd_gint* a = (pd_gint*)abort_w;
+  for (unsigned spins = 0;; ++spins) {
+    if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
+    if (__hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+    if (spins >= PD_SPIN_LIMIT) {
+      __hip_atomic_store(a, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (status) atomicOr(status, 1);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// every storing wave drains its sc1 stores, the work-group joins, one add
+__device__ __forceinline__ void pd_publish(int* ctr) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_fetch_add((pd_gint*)ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int CC>
+__global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
+    Dims d, const uint16_t* __restrict__ wcat, const float* __restrict__ pre_emb,
+    const float* __restrict__ h0, const float* __restrict__ enc, const float* __restrict__ enc_a,
+    const int32_t* __restrict__ lens, const float* __restrict__ w_dec,
+    const float* __restrict__ w_conv, const float* __restrict__ conv_w,
+    const float* __restrict__ vw, float* __restrict__ dec, float* __restrict__ c_all,
+    float* __restrict__ gates, float* x, float* __restrict__ ctx_all,
+    float* __restrict__ aw_all, float* pbuf, float* ebuf, int* ctr, int* status, float drop_h,
+    unsigned long long seed_h) {
+  extern __shared__ __attribute__((aligned(16))) float L[];
+  __shared__ int s_ok;
+  const PdGeom G = pd_geom(d);
+  const int UPW = G.UPW, FCH = G.FCH, ECW = G.ECW, ED = G.ED, NKB = G.NKB, half = G.half;
+  const int grp = blockIdx.x % PD_GROUPS, m = blockIdx.x / PD_GROUPS;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int u0 = m * UPW, nu = max(0, min(UPW, d.D - u0));
+  const int G4 = 4 * d.D;
+  int* my_ctr = ctr + (1 + grp) * PD_CTR;
+  const __amdgpu_buffer_rsrc_t rx = pd_rsrc(x, (unsigned)((size_t)d.B * d.S * ED * 4));
+  const __amdgpu_buffer_rsrc_t rp =
+      pd_rsrc(pbuf, (unsigned)((size_t)PD_GROUPS * PD_MEMBERS * PD_SLOTS * d.A * 4));
+  const __amdgpu_buffer_rsrc_t re = pd_rsrc(ebuf, (unsigned)((size_t)d.B * d.T * 4));
+  // frame role
+  const int fsl = m / PD_CHUNKS, ch = m % PD_CHUNKS;
+  const int be = grp + PD_GROUPS * fsl;
+  const bool fact = be < d.B;                 // work-group uniform
+  const int tt0 = ch * FCH, nfr = max(0, min(FCH, d.T - tt0));
+  const int e0 = ch * ECW, ecn = max(0, min(ECW, d.E - e0));
+  const int len = fact ? lens[be] : 0;
+  constexpr int CM = CC ? CC : 16;
+  const int C = CC ? CC : d.C;
+
+  // ---- once per pass: weights and the utterance's constant rows
+  bf16x8 wf[PD_KMAX];
+  {
+    const int tile = wave >> 1, kh = wave & 1;
+    const int gr = tile * 16 + (lane & 15), q = gr / UPW, u = gr % UPW;
+    const bool ok = wave < 6 && q < 4 && u < nu;
+    const uint16_t* wr = wcat + (long long)(ok ? q * d.D + u0 + u : 0) * ED;
+#pragma unroll
+    for (int i = 0; i < PD_KMAX; ++i) {
+      const int k = (kh + 2 * i) * 32 + 8 * (lane >> 4);
+      wf[i] = (ok && kh + 2 * i < NKB && k < ED) ? load_bf16x8(wr + k)
+                                                  : as_bf16x8(u16x8{0, 0, 0, 0, 0, 0, 0, 0});
+    }
+  }
+  float ea[PD_FPW][4];
+#pragma unroll
+  for (int f = 0; f < PD_FPW; ++f) {
+    const int i = wave + 8 * f, tt = tt0 + i;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int a = lane + 64 * q;
+      ea[f][q] = (fact && i < nfr && a < d.A) ? enc_a[((long long)be * d.T + tt) * d.A + a] : 0.f;
+    }
+  }
+  for (int i = tid; i < d.A * UPW; i += PD_THREADS) {
+    const int a = i / UPW, u = i % UPW;
+    L[G.wdl + i] = u < nu ? w_dec[(long long)a * d.D + u0 + u] : 0.f;
+  }
+  for (int i = tid; i < d.C * d.K; i += PD_THREADS) L[G.cw + i] = conv_w[i];
+  for (int i = tid; i < d.A * d.C; i += PD_THREADS) L[G.wc + i] = w_conv[i];
+  for (int i = tid; i < d.A; i += PD_THREADS) L[G.v + i] = vw[i];
+  for (int i = tid; i < d.T + 2 * half + 4; i += PD_THREADS) L[G.awp + i] = 0.f;
+  for (int i = tid; i < d.T * ECW; i += PD_THREADS) {
+    const int tt = i / ECW, cc = i % ECW;
+    L[G.encs + i] = (fact && cc < ecn) ? enc[((long long)be * d.T + tt) * d.E + e0 + cc] : 0.f;
+  }
+  // cell role: thread (slot, unit) for tid < 4 UPW
+  const int csl = tid / UPW, cu = tid % UPW;
+  const int cb = grp + PD_GROUPS * csl, cj = u0 + cu;
+  const bool cown = tid < PD_SLOTS * UPW && cu < nu && cb < d.B;
+  float c_reg = 0.f;
+  __syncthreads();
+
+  for (int t = 0; t < d.S; ++t) {
+    // ================= C: cell step t (t = 0: the initial state h0) =================
+    if (t > 0) {
+      if (tid == 0) s_ok = pd_wait(my_ctr, PD_MEMBERS * 3 * t, ctr, status);
+      __syncthreads();
+      if (!s_ok) return;
+      const int nv = ED / 4;
+      for (int i = tid; i < PD_SLOTS * nv; i += PD_THREADS) {
+        const int sl = i / nv, k4 = i % nv, bb = grp + PD_GROUPS * sl;
+        pd_u32x4 v = {0u, 0u, 0u, 0u};
+        if (bb < d.B)
+          v = __builtin_amdgcn_raw_buffer_load_b128(
+              rx, (unsigned)((((long long)bb * d.S + t) * ED + 4 * k4) * 4), 0, 16);
+        *reinterpret_cast<pd_u32x4*>(&L[G.xs + sl * ED + 4 * k4]) = v;
+      }
+      __syncthreads();
+      if (wave < 6) {
+        const int kh = wave & 1, mm = lane & 15;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < PD_KMAX; ++i) {
+          const int kb = kh + 2 * i;
+          if (kb < NKB) {   // wave-uniform
+            const int k = kb * 32 + 8 * (lane >> 4);
+            const bf16x8 a = (mm < PD_SLOTS && k < ED) ? cvt8(&L[G.xs + mm * ED + k])
+                                                      : as_bf16x8(u16x8{0, 0, 0, 0, 0, 0, 0, 0});
+            acc = mfma_bf16(a, wf[i], acc);
+          }
+        }
+        if (lane < 16) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) L[G.part + (wave * PD_SLOTS + r) * 16 + lane] = acc[r];
+        }
+      }
+      __syncthreads();
+      if (cown) {
+        const long long gb = ((long long)cb * d.S + t) * G4 + cj;
+        float pre[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int gr = q * UPW + cu, tile = gr >> 4, col = gr & 15;
+          pre[q] = L[G.part + ((2 * tile) * PD_SLOTS + csl) * 16 + col] +
+                   L[G.part + ((2 * tile + 1) * PD_SLOTS + csl) * 16 + col] +
+                   pre_emb[gb + (long long)q * d.D];
+        }
+        const float ig = sigmoidf_(pre[0]), fg = sigmoidf_(pre[1]);
+        const float gg = tanhf_(pre[2]), og = sigmoidf_(pre[3]);
+        const float c = fg * c_reg + ig * gg;
+        float h = og * tanhf_(c);
+        if (drop_h > 0.f)
+          h *= drop_scale(drop_h, seed_h, ((unsigned long long)cb * d.S + t) * d.D + cj);
+        c_reg = c;
+        c_all[((long long)cb * d.S + t) * d.D + cj] = c;
+        dec[((long long)cb * d.S + t) * d.D + cj] = h;
+        gates[gb] = ig;
+        gates[gb + d.D] = fg;
+        gates[gb + 2 * d.D] = gg;
+        gates[gb + 3 * d.D] = og;
+        if (t + 1 < d.S) pd_st(rx, ((long long)cb * d.S + t + 1) * ED + d.E + cj, h);
+        L[G.hs + csl * PD_UMAX + cu] = h;   // absent (slot, unit) entries stay 0 from t = 0
+      }
+    } else {
+      if (tid < PD_SLOTS * PD_UMAX) {
+        const int sl = tid / PD_UMAX, u = tid % PD_UMAX, bb = grp + PD_GROUPS * sl;
+        L[G.hs + tid] = (h0 && u < nu && bb < d.B) ? h0[(long long)bb * d.D + u0 + u] : 0.f;
+      }
+    }
+    __syncthreads();
+    // partial W_dec h_t over this member's units, one (slot, a) per thread
+    for (int i = tid; i < PD_SLOTS * d.A; i += PD_THREADS) {
+      const int sl = i / d.A, a = i % d.A;
+      float s = 0.f;
+      for (int u = 0; u < nu; ++u) s += L[G.wdl + a * UPW + u] * L[G.hs + sl * PD_UMAX + u];
+      pd_st(rp, (((long long)grp * PD_MEMBERS + m) * PD_SLOTS + sl) * d.A + a, s);
+    }
+    pd_publish(my_ctr);
+
+    // ================= E: energies of this work-group's frame chunk =================
+    if (tid == 0) s_ok = pd_wait(my_ctr, PD_MEMBERS * (3 * t + 1), ctr, status);
+    __syncthreads();
+    if (!s_ok) return;
+    if (fact) {
+      for (int i = tid; i < 4 * d.A; i += PD_THREADS) {   // W_dec h_t: 32 partials, fixed order
+        const int a = i % d.A, qq = i / d.A;
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          v[j] = pd_ld(rp, (((long long)grp * PD_MEMBERS + qq * 8 + j) * PD_SLOTS + fsl) * d.A + a);
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += v[j];
+        L[G.wq + qq * d.A + a] = s;
+      }
+      // conv features of the chunk from aw_{t-1} (zero at t = 0 and outside [0, T))
+      for (int i = tid; i < FCH * C; i += PD_THREADS) {
+        const int fi = i / C, c = i % C;
+        float s = 0.f;
+        if (t > 0 && fi < nfr) s = dot_lds(&L[G.cw + c * d.K], 1, &L[G.awp + tt0 + fi], 1, d.K);
+        L[G.f + i] = s;
+      }
+      __syncthreads();
+      for (int a = tid; a < d.A; a += PD_THREADS)
+        L[G.wd + a] = (L[G.wq + a] + L[G.wq + d.A + a]) + (L[G.wq + 2 * d.A + a] + L[G.wq + 3 * d.A + a]);
+      __syncthreads();
+#pragma unroll
+      for (int f = 0; f < PD_FPW; ++f) {
+        const int i = wave + 8 * f;
+        if (i >= nfr) break;
+        const int tt = tt0 + i;
+        float frv[CM];
+#pragma unroll
+        for (int c = 0; c < CM; ++c) frv[c] = (CC || c < C) ? L[G.f + i * C + c] : 0.f;
+        float s = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int a = lane + 64 * q;
+          if (64 * q < d.A && a < d.A) {
+            float p = ea[f][q] + L[G.wd + a];
+#pragma unroll
+            for (int c = 0; c < CM; ++c)
+              if (CC || c < C) p += frv[c] * L[G.wc + a * C + c];
+            s += L[G.v + a] * tanhf(p);
+          }
+        }
+        s = wave_sum(s);
+        if (lane == 0) pd_st(re, (long long)be * d.T + tt, (tt < len ? s : 0.f) * d.sharpen);
+      }
+    }
+    pd_publish(my_ctr);
+
+    // ================= X: softmax over the utterance, context slice =================
+    if (tid == 0) s_ok = pd_wait(my_ctr, PD_MEMBERS * (3 * t + 2), ctr, status);
+    __syncthreads();
+    if (!s_ok) return;
+    if (fact) {
+      float* aw = &L[G.awp + half];
+      float mx = -__builtin_huge_valf();
+      for (int i = tid; i < d.T; i += PD_THREADS) {
+        const float e = pd_ld(re, (long long)be * d.T + i);
+        aw[i] = e;
+        mx = fmaxf(mx, e);
+      }
+      __syncthreads();
+      if (d.sigmoid) {
+        for (int i = tid; i < d.T; i += PD_THREADS) aw[i] = sigmoidf_(aw[i]);
+      } else {
+        mx = block_reduce(mx, &L[G.red], true);
+        float sm = 0.f;
+        for (int i = tid; i < d.T; i += PD_THREADS) {
+          const float p = __expf(aw[i] - mx);
+          aw[i] = p;
+          sm += p;
+        }
+        sm = block_reduce(sm, &L[G.red], false);
+        const float inv = 1.f / sm;
+        for (int i = tid; i < d.T; i += PD_THREADS) aw[i] *= inv;
+      }
+      __syncthreads();
+      for (int i = tid; i < nfr; i += PD_THREADS)
+        aw_all[((long long)be * d.S + t) * d.T + tt0 + i] = aw[tt0 + i];
+      const int NR = PD_THREADS / ECW, col = tid % ECW, r = tid / ECW;
+      float s = 0.f;
+      if (r < NR && col < ecn)
+        for (int tt = r; tt < d.T; tt += NR) s += aw[tt] * L[G.encs + tt * ECW + col];
+      if (r < NR) L[G.cpart + r * ECW + col] = s;
+      __syncthreads();
+      if (tid < ecn) {
+        float cv = 0.f;
+        for (int q = 0; q < NR; ++q) cv += L[G.cpart + q * ECW + tid];
+        ctx_all[((long long)be * d.S + t) * d.E + e0 + tid] = cv;
+        if (t + 1 < d.S) pd_st(rx, ((long long)be * d.S + t + 1) * ED + e0 + tid, cv);
+      }
+    }
+    pd_publish(my_ctr);
+  }
+}
+
+}  // namespace
+
+int* lstm_persist_status_word();   // lstm_persist.hip
+
+namespace {
+int device_cus() {
+  static int n = -1;
+  if (n < 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 0;
+  }
+  return n;
+}
+
+// The persistent forward pass takes a shape when its work split fits (see the
+// kernel's comment) and the 256-work-group grid is co-resident, one per CU.
+// ASR_ATT_PERSIST=0 keeps the per-step kernels (A/B).
+bool pd_eligible(const Dims& d) {
+  const char* e = getenv("ASR_ATT_PERSIST");
+  if (e && e[0] == '0') return false;
+  const PdGeom G = pd_geom(d);
+  const size_t lds = (size_t)G.total * 4;
+  if (d.B > PD_GROUPS * PD_SLOTS || G.UPW > PD_UMAX || G.ED % 8 != 0 || G.NKB > 2 * PD_KMAX ||
+      G.FCH > 8 * PD_FPW || d.A > 256 || d.C > 16 || G.ECW > PD_THREADS || lds > 160 * 1024 ||
+      (size_t)d.B * d.S * G.ED * 4 >= (1ull << 31) || (size_t)d.B * d.T * 4 >= (1ull << 31))
+    return false;
+  if (device_cus() < PD_GROUPS * PD_MEMBERS) return false;
+  const void* k = d.C == 10 ? (const void*)attdec_fwd_persist<10> : (const void*)attdec_fwd_persist<0>;
+  if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return false;
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, PD_THREADS, lds) != hipSuccess)
+    return false;
+  return per_cu >= 1;
+}
 }  // namespace
 }  // namespace asr
 
@@ -1102,7 +1511,7 @@ extern "C" size_t asr_attdec_workspace_bytes(const asr_attdec_dims_t* dims, int 
 }
 
 // Attention frame chunks per utterance: the backward partials dv_part,
-// dwc_part and dcw_part hold B * S * chunks rows.
+// dwc_part and dcw_part hold B * chunks rows (each summed over the steps).
 extern "C" int asr_attdec_chunks(const asr_attdec_dims_t* dims) {
   return att_chunks(to_dims(*dims));
 }
@@ -1143,6 +1552,7 @@ extern "C" int asr_attdec_forward(const asr_attdec_dims_t* dims, int compute_dty
 // {forward channel template (10, 3 or 0 = generic), forward frame chunks,
 //  backward channel template, backward frame chunks} (host-side record).
 static int g_att_last[4];
+static int g_att_persist_last[2];   // {forward pass persistent, backward pass persistent}
 
 extern "C" int asr_attdec_forward_ex(const asr_attdec_dims_t* dims, const asr_attdec_opts_t* opts,
                                      int compute_dtype, const float* enc, const float* enc_a,
@@ -1191,6 +1601,27 @@ extern "C" int asr_attdec_forward_ex(const asr_attdec_dims_t* dims, const asr_at
   ASR_REQUIRE(ss_lds <= 160 * 1024, ASR_ERR_UNSUPPORTED, "attdec: sampling LDS %zu B", ss_lds);
   g_att_last[0] = (d.C == 10 || d.C == 3) ? d.C : 0;
   g_att_last[1] = (int)eg.x;
+  g_att_persist_last[0] = 0;
+  if (bf && !ss && pd_eligible(d)) {
+    const PdGeom G = pd_geom(d);
+    int* ctr = (int*)((char*)workspace + W.ctr);
+    float* pbuf = (float*)((char*)workspace + W.pbuf);
+    ASR_CHECK_HIP(hipMemsetAsync(ctr, 0, (size_t)(1 + PD_GROUPS) * PD_CTR * 4, s));
+    const size_t lds = (size_t)G.total * 4;
+    const dim3 grid(PD_GROUPS * PD_MEMBERS);
+#define ASR_PD(CC)                                                                              \
+  hipLaunchKernelGGL(attdec_fwd_persist<CC>, grid, dim3(PD_THREADS), lds, s, d,                 \
+                     (const uint16_t*)workspace, pre_emb, h0, enc, enc_a, lens, w_dec, w_conv,   \
+                     conv_w, v, dec, c_all, gates, x, ctx_all, aw_all, pbuf, ebuf, ctr,          \
+                     lstm_persist_status_word(), drop_h, seed_h)
+    if (d.C == 10) ASR_PD(10);
+    else ASR_PD(0);
+#undef ASR_PD
+    ASR_LAUNCH_CHECK();
+    g_att_last[0] = d.C == 10 ? 10 : 0;
+    g_att_persist_last[0] = 1;
+    return ASR_OK;
+  }
   for (int t = 0; t < d.S; ++t) {
     if (t > 0) {
       const bool smp = ss && opts->ss_steps_host[t] != 0;
@@ -1224,6 +1655,15 @@ extern "C" int asr_attdec_forward_ex(const asr_attdec_dims_t* dims, const asr_at
                        ctx_all, x);
     ASR_LAUNCH_CHECK();
   }
+  return ASR_OK;
+}
+
+// {forward, backward}: 1 if the last decoder pass of that direction ran as
+// one persistent launch (host-side record).
+extern "C" int asr_attdec_persist_last(int* out2) {
+  ASR_REQUIRE(out2, ASR_ERR_ARG, "attdec_persist_last: null pointer");
+  out2[0] = g_att_persist_last[0];
+  out2[1] = g_att_persist_last[1];
   return ASR_OK;
 }
 
@@ -1478,7 +1918,7 @@ extern "C" int asr_att_step_forward(const asr_attdec_dims_t* dims, const float* 
 // dctx_tot [B][E] (= d_ctx: d enc = aw_out^T dctx_tot is the caller's GEMM),
 // dwd [B][A] (d of W_dec dec_out: dW_dec = dwd^T dec_out), and per
 // (utterance, frame chunk) partials dv_part [B*NC][A], dwc_part [B*NC][A*C],
-// dcw_part [B*NC][C*K] whose column sums are dV, dW_conv, d conv kernel
+// dcw_part [B*NC][C*K] (written: step t = 1 = S - 1) whose column sums are dV, dW_conv, d conv kernel
 // (NC = asr_attdec_chunks).
 extern "C" int asr_att_step_backward(const asr_attdec_dims_t* dims, const float* enc,
                                      const float* enc_a, const int32_t* lens, const float* w_dec,
@@ -1523,11 +1963,6 @@ extern "C" int asr_att_step_backward(const asr_attdec_dims_t* dims, const float*
   else
     ASR_CHECK_HIP(hipMemsetAsync(carry, 0, (size_t)d.B * d.T * 4, s));
   ASR_CHECK_HIP(hipMemsetAsync(d_enc_a, 0, (size_t)d.B * d.T * d.A * 4, s));
-  // the partial rows of slot 0 are never written: the caller sums all rows
-  const size_t prow = (size_t)d.B * 2 * NC;
-  ASR_CHECK_HIP(hipMemsetAsync(dv_part, 0, prow * d.A * 4, s));
-  ASR_CHECK_HIP(hipMemsetAsync(dwc_part, 0, prow * d.A * d.C * 4, s));
-  ASR_CHECK_HIP(hipMemsetAsync(dcw_part, 0, prow * d.C * d.K * 4, s));
   {  // W_dec dec (exact-f32 MFMA, as the decoder backward)
     asr_gemm_t g;
     memset(&g, 0, sizeof(g));

@@ -427,6 +427,13 @@ int lstm_bwd_persistent(int B, int T, int H, const int32_t* lens, const uint16_t
   return hipGetLastError() == hipSuccess ? 1 : -1;
 }
 
+// Device address of the counter form's status word (the persistent decoder
+// pass reports its give-ups there too).
+int* lstm_persist_status_word() {
+  void* p = nullptr;
+  return hipGetSymbolAddress(&p, HIP_SYMBOL(g_persist_status)) == hipSuccess ? (int*)p : nullptr;
+}
+
 }  // namespace asr
 
 namespace asr {

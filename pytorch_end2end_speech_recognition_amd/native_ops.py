@@ -440,7 +440,7 @@ class AttDecoderFn(torch.autograd.Function):
         d_enc_a = torch.empty(B, T, A, **f32)
         d_h0 = torch.empty(B, D, **f32) if has_h0 else None
         dwd = torch.empty(B, S, A, **f32)
-        nrow = B * S * N.query('asr_attdec_chunks', ctypes.byref(dims))   # per frame chunk
+        nrow = B * N.query('asr_attdec_chunks', ctypes.byref(dims))   # per frame chunk
         dv_part = torch.empty(nrow, A, **f32)
         dwc_part = torch.empty(nrow, A * C, **f32)
         dcw_part = torch.empty(nrow, C * K, **f32)
@@ -541,7 +541,7 @@ class AttStepFn(torch.autograd.Function):
         d_aw_prev = torch.empty(B, T, **f32)
         dctx_tot = torch.empty(B, E, **f32)
         dwd = torch.empty(B, A, **f32)
-        nrow = B * 2 * N.query('asr_attdec_chunks', ctypes.byref(dims))
+        nrow = B * N.query('asr_attdec_chunks', ctypes.byref(dims))
         dv_part = torch.empty(nrow, A, **f32)
         dwc_part = torch.empty(nrow, A * C, **f32)
         dcw_part = torch.empty(nrow, C * K, **f32)

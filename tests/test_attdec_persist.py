@@ -1,0 +1,120 @@
+"""The persistent forward decoder pass (decoder.hip attdec_fwd_persist: all S
+steps of the LSTMCell + location attention in one launch, bf16 mode) against
+the per-step kernels it replaces (ASR_ATT_PERSIST=0), on the same inputs:
+every saved tensor the backward reads (dec, c, gates, x, ctx, aw) and the
+gradients of the whole decoder pass.  The two differ only in f32 summation
+order (bf16 operands are rounded at the same points): the attention outputs
+agree to ~5e-6 relative; the cell's bf16 operands [ctx_{t-1}; h_{t-1}] turn
+some of those differences into bf16 rounding flips, so the forward bound is
+rel-L2 1e-3 per tensor (measured 2e-4 at the production shape).  The gradients pass through the
+backward's bf16 GEMMs, which turn those differences into bf16 rounding flips:
+rel-L2 5e-3 there.
+
+Shapes: the production one (B 32, T' 250, E 640, A 128, 10 channels x 201,
+D 320: 8 frame chunks of 32, 80 context columns and 10 hidden units per
+work-group) and a small ragged one (B 5, odd T', C = 3: the generic-channel
+instantiation, empty utterance slots and partial chunks).
+"""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = {
+    'prod': dict(B=32, T=250, E=640, A=128, C=10, K=201, D=320, S=40, Y=32),
+    'ragged': dict(B=5, T=61, E=52, A=24, C=3, K=11, D=20, S=7, Y=6),
+}
+
+
+def _inputs(p, dev, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    r = lambda *s, sc=0.1: (torch.rand(*s, generator=g) * 2 - 1) * sc   # noqa: E731
+    B, T, E, A, C, K, D, S, Y = (p[k] for k in 'B T E A C K D S Y'.split())
+    lens = np.linspace(T, max(1, T // 2), B).astype(np.int32)
+    t = dict(enc=r(B, T, E, sc=1.0), enc_a=r(B, T, A, sc=1.0), pre_emb=r(B, S, 4 * D, sc=0.5),
+             h0=r(B, D, sc=0.5), w_ih=r(4 * D, Y + E), w_hh=r(4 * D, D), w_dec=r(A, D),
+             w_conv=r(A, C), conv_w=r(C, 1, 1, K), v=r(1, A))
+    t = {k: v.to(dev).requires_grad_(True) for k, v in t.items()}
+    t['lens'] = torch.from_numpy(lens).to(dev)
+    t['cot'] = [torch.randn(B, S, D, generator=g).to(dev), torch.randn(B, S, E, generator=g).to(dev)]
+    return t
+
+
+def _run(p, t, persist, with_grad):
+    from pytorch_end2end_speech_recognition_amd import native_ops
+    from pytorch_end2end_speech_recognition_amd import _native as N
+    os.environ['ASR_ATT_PERSIST'] = '1' if persist else '0'
+    try:
+        for v in t.values():
+            if isinstance(v, torch.Tensor) and v.grad is not None:
+                v.grad = None
+        if not with_grad:
+            _, outs, _, _ = native_ops._attdec_forward(
+                t['enc'].detach(), t['enc_a'].detach(), t['lens'], t['pre_emb'].detach(),
+                t['h0'].detach(), p['Y'], 1.0, False, t['w_ih'].detach(), t['w_hh'].detach(),
+                t['w_dec'].detach(), t['w_conv'].detach(), t['conv_w'].detach(),
+                t['v'].detach(), {'dropout_hidden': 0.2, 'seed_hidden': 7})
+            res = [o.detach().clone() for o in outs]
+        else:
+            dec, ctx, aw = native_ops.att_decoder(
+                t['enc'], t['enc_a'], t['lens'], t['pre_emb'], t['h0'], p['Y'], 1.0, False,
+                t['w_ih'], t['w_hh'], t['w_dec'], t['w_conv'], t['conv_w'], t['v'],
+                {'dropout_hidden': 0.2, 'seed_hidden': 7})
+            ((dec * t['cot'][0]).sum() + (ctx * t['cot'][1]).sum()).backward()
+            res = [dec.detach().clone(), ctx.detach().clone(), aw.detach().clone()]
+            res += [t[k].grad.detach().clone() for k in
+                    ('enc', 'enc_a', 'pre_emb', 'h0', 'w_ih', 'w_hh', 'w_dec', 'w_conv', 'conv_w',
+                     'v')]
+        torch.cuda.synchronize()
+        flag = (ctypes.c_int * 2)()
+        N.call('asr_attdec_persist_last', flag)
+        return res, int(flag[0])
+    finally:
+        os.environ.pop('ASR_ATT_PERSIST', None)
+
+
+def _rel(a, b):
+    return float((a - b).norm() / max(float(b.norm()), 1e-30))
+
+
+@pytest.mark.parametrize('shape', sorted(SHAPES))
+def test_persistent_forward_matches_per_step(shape, cuda_dev):
+    from pytorch_end2end_speech_recognition_amd import native_ops
+    native_ops.set_compute_dtype('bf16')
+    p = SHAPES[shape]
+    t = _inputs(p, cuda_dev)
+    ref, f0 = _run(p, t, False, False)
+    got, f1 = _run(p, t, True, False)
+    assert f0 == 0 and f1 == 1, 'persistent forward did not run'
+    for name, a, b in zip(('dec', 'c', 'gates', 'x', 'ctx', 'aw'), got, ref):
+        assert torch.isfinite(a).all(), name
+        assert _rel(a, b) < 1e-3, (name, _rel(a, b))
+    # softmax rows (the multiplicative mask leaves padded frames at energy 0,
+    # as the reference does, so they keep a weight)
+    np.testing.assert_allclose(got[5].sum(-1).cpu().numpy(), 1.0, rtol=1e-5)
+
+
+@pytest.mark.parametrize('shape', sorted(SHAPES))
+def test_persistent_forward_gradients_match(shape, cuda_dev):
+    from pytorch_end2end_speech_recognition_amd import native_ops
+    native_ops.set_compute_dtype('bf16')
+    p = SHAPES[shape]
+    t = _inputs(p, cuda_dev, seed=1)
+    ref, _ = _run(p, t, False, True)
+    got, f1 = _run(p, t, True, True)
+    assert f1 == 1
+    names = ('dec', 'ctx', 'aw', 'd_enc', 'd_enc_a', 'd_pre_emb', 'd_h0', 'd_w_ih', 'd_w_hh',
+             'd_w_dec', 'd_w_conv', 'd_conv_w', 'd_v')
+    errs = {name: _rel(a, b) for name, a, b in zip(names, got, ref)}
+    print(shape, {k: '%.2e' % v for k, v in errs.items()})
+    for name, a in zip(names, got):
+        assert torch.isfinite(a).all(), name
+    # outputs as the forward test; gradients: the backward's bf16 GEMM operands
+    # (aw, dctx, dgates, x rounded to bf16) turn the forward's f32-order
+    # differences into bf16 rounding flips (2^-8 relative each), hence 5e-3
+    for name in names:
+        assert errs[name] < (1e-3 if name in ('dec', 'ctx', 'aw') else 5e-3), (name, errs[name])
