@@ -226,6 +226,10 @@ constexpr int FPW = TCH / ATT_WAVES;   // frames per wave
 constexpr int ECH = 64;   // context columns per work-group
 
 inline int att_chunks(const Dims& d) { return (d.T + TCH - 1) / TCH; }
+// rows per utterance of the backward's weight-gradient partials: the per-step
+// kernels' frame chunks or the persistent pass's 8, whichever is more (rows a
+// pass does not write are zero)
+inline int part_rows(const Dims& d) { return att_chunks(d) > 8 ? att_chunks(d) : 8; }
 
 struct EnLds {
   float* h;     // [D]      dec_out_t
@@ -1070,7 +1074,7 @@ size_t al256(size_t n) { return (n + 255) & ~size_t(255); }
 // Workspace: [Wcat (fwd) or Wcat^T (bwd)][energies / d aw [B][T]] and, backward
 // only, [r][carry][ddec_att][dc][flags][dF [B][T][C]][dWd chunk partials].
 struct AttWs {
-  size_t wcat, ebuf, r, carry, ddec, dc, flags, dF, dwdc, wd, pbuf, ctr, total;
+  size_t wcat, ebuf, r, carry, ddec, dc, flags, dF, dwdc, wd, pbuf, ctr, sbuf, total;
 };
 AttWs att_ws(const Dims& d, int cdt, bool bwd) {
   AttWs w;
@@ -1084,8 +1088,10 @@ AttWs att_ws(const Dims& d, int cdt, bool bwd) {
     w.dc = o; o += al256((size_t)d.B * d.D * 4);
     w.flags = o; o += al256((size_t)d.S * 4);
     w.dF = o; o += al256((size_t)d.B * d.T * d.C * 4);
-    w.dwdc = o; o += al256((size_t)d.B * att_chunks(d) * d.A * 4);
+    w.dwdc = o; o += al256((size_t)d.B * part_rows(d) * d.A * 4);
     w.wd = o; o += al256((size_t)d.B * d.S * d.A * 4);
+    w.sbuf = o; o += al256((size_t)d.B * 8 * 4);
+    w.ctr = o; o += al256((size_t)(1 + 8) * 64 * 4);
   } else {   // the persistent forward's W_dec h partials and group counters
     w.pbuf = o; o += al256((size_t)8 * 32 * 4 * d.A * 4);
     w.ctr = o; o += al256((size_t)(1 + 8) * 64 * 4);
@@ -1204,7 +1210,15 @@ __device__ __forceinline__ void pd_publish(int* ctr) {
     __hip_atomic_fetch_add((pd_gint*)ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int CC>
+// phase stamps of work-group 0 at decoder step ATT_TR_STEP (tools/att_trace.py)
+#define PD_TR(k)                                                                 \
+  do {                                                                           \
+    if (t == ATT_TR_STEP && blockIdx.x == 0 && threadIdx.x == 0)                 \
+      g_att_tr[k] = __builtin_amdgcn_s_memrealtime();                            \
+  } while (0)
+
+// NQ: 64-lane groups of the attention dim (A <= 64 NQ)
+template <int CC, int NQ>
 __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
     Dims d, const uint16_t* __restrict__ wcat, const float* __restrict__ pre_emb,
     const float* __restrict__ h0, const float* __restrict__ enc, const float* __restrict__ enc_a,
@@ -1252,12 +1266,12 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
                                                   : as_bf16x8(u16x8{0, 0, 0, 0, 0, 0, 0, 0});
     }
   }
-  float ea[PD_FPW][4];
+  float ea[PD_FPW][NQ];
 #pragma unroll
   for (int f = 0; f < PD_FPW; ++f) {
     const int i = wave + 8 * f, tt = tt0 + i;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < NQ; ++q) {
       const int a = lane + 64 * q;
       ea[f][q] = (fact && i < nfr && a < d.A) ? enc_a[((long long)be * d.T + tt) * d.A + a] : 0.f;
     }
@@ -1283,10 +1297,12 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
 
   for (int t = 0; t < d.S; ++t) {
     // ================= C: cell step t (t = 0: the initial state h0) =================
+    PD_TR(32);
     if (t > 0) {
       if (tid == 0) s_ok = pd_wait(my_ctr, PD_MEMBERS * 3 * t, ctr, status);
       __syncthreads();
       if (!s_ok) return;
+      PD_TR(33);
       const int nv = ED / 4;
       for (int i = tid; i < PD_SLOTS * nv; i += PD_THREADS) {
         const int sl = i / nv, k4 = i % nv, bb = grp + PD_GROUPS * sl;
@@ -1297,6 +1313,7 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
         *reinterpret_cast<pd_u32x4*>(&L[G.xs + sl * ED + 4 * k4]) = v;
       }
       __syncthreads();
+      PD_TR(34);
       if (wave < 6) {
         const int kh = wave & 1, mm = lane & 15;
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -1316,6 +1333,7 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
         }
       }
       __syncthreads();
+      PD_TR(35);
       if (cown) {
         const long long gb = ((long long)cb * d.S + t) * G4 + cj;
         float pre[4];
@@ -1349,6 +1367,7 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
       }
     }
     __syncthreads();
+    PD_TR(36);
     // partial W_dec h_t over this member's units, one (slot, a) per thread
     for (int i = tid; i < PD_SLOTS * d.A; i += PD_THREADS) {
       const int sl = i / d.A, a = i % d.A;
@@ -1357,11 +1376,13 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
       pd_st(rp, (((long long)grp * PD_MEMBERS + m) * PD_SLOTS + sl) * d.A + a, s);
     }
     pd_publish(my_ctr);
+    PD_TR(37);
 
     // ================= E: energies of this work-group's frame chunk =================
     if (tid == 0) s_ok = pd_wait(my_ctr, PD_MEMBERS * (3 * t + 1), ctr, status);
     __syncthreads();
     if (!s_ok) return;
+    PD_TR(38);
     if (fact) {
       for (int i = tid; i < 4 * d.A; i += PD_THREADS) {   // W_dec h_t: 32 partials, fixed order
         const int a = i % d.A, qq = i / d.A;
@@ -1382,9 +1403,11 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
         L[G.f + i] = s;
       }
       __syncthreads();
+      PD_TR(39);
       for (int a = tid; a < d.A; a += PD_THREADS)
         L[G.wd + a] = (L[G.wq + a] + L[G.wq + d.A + a]) + (L[G.wq + 2 * d.A + a] + L[G.wq + 3 * d.A + a]);
       __syncthreads();
+      PD_TR(40);
 #pragma unroll
       for (int f = 0; f < PD_FPW; ++f) {
         const int i = wave + 8 * f;
@@ -1395,7 +1418,7 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
         for (int c = 0; c < CM; ++c) frv[c] = (CC || c < C) ? L[G.f + i * C + c] : 0.f;
         float s = 0.f;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < NQ; ++q) {
           const int a = lane + 64 * q;
           if (64 * q < d.A && a < d.A) {
             float p = ea[f][q] + L[G.wd + a];
@@ -1409,12 +1432,15 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
         if (lane == 0) pd_st(re, (long long)be * d.T + tt, (tt < len ? s : 0.f) * d.sharpen);
       }
     }
+    PD_TR(41);
     pd_publish(my_ctr);
+    PD_TR(42);
 
     // ================= X: softmax over the utterance, context slice =================
     if (tid == 0) s_ok = pd_wait(my_ctr, PD_MEMBERS * (3 * t + 2), ctr, status);
     __syncthreads();
     if (!s_ok) return;
+    PD_TR(43);
     if (fact) {
       float* aw = &L[G.awp + half];
       float mx = -__builtin_huge_valf();
@@ -1439,6 +1465,7 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
         for (int i = tid; i < d.T; i += PD_THREADS) aw[i] *= inv;
       }
       __syncthreads();
+      PD_TR(44);
       for (int i = tid; i < nfr; i += PD_THREADS)
         aw_all[((long long)be * d.S + t) * d.T + tt0 + i] = aw[tt0 + i];
       const int NR = PD_THREADS / ECW, col = tid % ECW, r = tid / ECW;
@@ -1454,8 +1481,488 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
         if (t + 1 < d.S) pd_st(rx, ((long long)be * d.S + t + 1) * ED + e0 + tid, cv);
       }
     }
+    PD_TR(45);
     pd_publish(my_ctr);
+    PD_TR(46);
   }
+}
+
+
+// ---------------------------------------------------------------------------
+// Persistent backward pass (bf16): all S steps of rgemm -> att_bwd_daw ->
+// att_bwd_energy -> att_bwd_conv -> cell_bwd in ONE launch, with the forward
+// pass's group layout (8 per-XCD groups of 32 work-groups, 4 utterances per
+// group, b = g + 8 slot; member m = blockIdx / 8).  Member roles:
+//   r role     : columns [m NPW, (m+1) NPW) of r = dgates_{t+1} Wcat for the
+//                group's 4 utterances; its Wcat^T rows as MFMA B fragments in
+//                VGPRs (2 column tiles x 4 K quarters over the 8 waves);
+//   frame role : utterance slot m / 8, frames [ch FCH, (ch+1) FCH), ch = m % 8:
+//                the frames' enc rows and enc_a rows in LDS, their d enc_a and
+//                the chunk's dV / dW_conv / conv-kernel partial sums in
+//                registers for the whole pass, the d aw carry in LDS;
+//   cell role  : hidden units [m UPW, (m+1) UPW), their d c carries in
+//                registers, W_dec's columns of the units in LDS.
+// Four group-wide hand-offs per step t (same protocol as the forward pass):
+//   H (t+1 < S) r role     : r = dgates_{t+1} Wcat            -> r [B][E+D]
+//   E           frame role : d ctx_t = d_ctx_in + r[:E]; d aw_t = carry + enc . d ctx;
+//                            chunk sum of aw d aw (softmax)    -> sdot partials
+//                            (and, no hand-off, the conv features of aw_{t-1})
+//   F           frame role : softmax / tanh backward            -> dF rows, d W_dec-input
+//                                                                 chunk sums
+//   G           frame role : d aw_{t-1} = conv^T(dF window) (next step's carry),
+//                            conv-kernel partials
+//               cell role  : d dec_t = d_dec_in + r[E:] + W_dec^T dWd_t;
+//                            LSTMCell backward                 -> dgates_t (over gates)
+// Arithmetic as the per-step kernels (bf16 MFMA for r, f32 elsewhere); the
+// weight-gradient partials are summed over the steps in registers instead of
+// per-step rows, so their f32 summation order differs.
+// ---------------------------------------------------------------------------
+constexpr int PB_KQ = 12;         // K blocks of 32 per wave quarter: 4 D <= 1536
+constexpr int PB_CM = 4;          // conv channels of the generic instantiation (C <= 4)
+
+struct PbGeom {
+  int UPW, FCH, ECW, ED, G4, NPW, NKB, KQ, half, W;
+  int encr, ea, cw, wc, v, dct, awin, f, daw, awt, de, carry, dFw, wd, dgs, part, dwdl, wdl,
+      cmb, red, total;   // LDS floats
+};
+
+__host__ __device__ inline PbGeom pb_geom(const Dims& d) {
+  PbGeom g;
+  g.UPW = (d.D + PD_MEMBERS - 1) / PD_MEMBERS;
+  g.FCH = (d.T + PD_CHUNKS - 1) / PD_CHUNKS;
+  g.ECW = (d.E + PD_CHUNKS - 1) / PD_CHUNKS;
+  g.ED = d.E + d.D;
+  g.G4 = 4 * d.D;
+  g.NPW = (g.ED + PD_MEMBERS - 1) / PD_MEMBERS;
+  g.NKB = (g.G4 + 31) / 32;
+  g.KQ = (g.NKB + 3) / 4;
+  g.half = d.K / 2;
+  g.W = g.FCH + d.K - 1;
+  int o = 0;
+  g.encr = o; o += g.FCH * d.E;
+  g.ea = o; o += g.FCH * d.A;
+  g.cw = o; o += d.C * d.K;
+  g.wc = o; o += d.A * d.C;
+  g.v = o; o += d.A;
+  g.dct = o; o += d.E;
+  g.awin = o; o += g.W;
+  g.f = o; o += g.FCH * d.C;
+  g.daw = o; o += g.FCH;
+  g.awt = o; o += g.FCH;
+  g.de = o; o += g.FCH;
+  g.carry = o; o += g.FCH;
+  g.dFw = o; o += g.W * d.C;
+  g.wd = o; o += d.A;
+  o = (o + 3) & ~3;
+  g.dgs = o; o += PD_SLOTS * g.G4 / 2 + 4;   // bf16 [4][G4]
+  g.part = o; o += 8 * PD_SLOTS * 16;
+  g.dwdl = o; o += PD_SLOTS * d.A;
+  g.wdl = o; o += d.A * g.UPW;
+  g.cmb = o; o += 8 * d.A > 2 * d.A + d.A * d.C ? 8 * d.A : 2 * d.A + d.A * d.C;
+  g.red = o; o += 64;
+  g.total = (o + 3) & ~3;
+  return g;
+}
+
+template <int CC, int NQ>
+__global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
+    Dims d, const uint16_t* __restrict__ wcatT, const float* __restrict__ enc,
+    const float* __restrict__ enc_a, const int32_t* __restrict__ lens,
+    const float* __restrict__ w_dec, const float* __restrict__ w_conv,
+    const float* __restrict__ conv_w, const float* __restrict__ vw,
+    const float* __restrict__ c_all, const float* __restrict__ aw_all,
+    const float* __restrict__ wd_all, const float* __restrict__ d_dec_in,
+    const float* __restrict__ d_ctx_in, float* gates, float* __restrict__ dctx_tot,
+    float* __restrict__ d_enc_a, float* __restrict__ d_h0, float* __restrict__ dwd_all,
+    float* __restrict__ dv_part, float* __restrict__ dwc_part, float* __restrict__ dcw_part,
+    float* rbuf, float* sbuf, float* dwdc, float* dFbuf, int* ctr, int* status, float drop_h,
+    unsigned long long seed_h) {
+  extern __shared__ __attribute__((aligned(16))) float L[];
+  __shared__ int s_ok;
+  __shared__ float s_sdot;
+  const PbGeom G = pb_geom(d);
+  const int UPW = G.UPW, FCH = G.FCH, ECW = G.ECW, ED = G.ED, G4 = G.G4, NPW = G.NPW;
+  const int half = G.half, KW = G.W;
+  const int grp = blockIdx.x % PD_GROUPS, m = blockIdx.x / PD_GROUPS;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int u0 = m * UPW, nu = max(0, min(UPW, d.D - u0));
+  const int n0 = m * NPW, nn = max(0, min(NPW, ED - n0));
+  int* my_ctr = ctr + (1 + grp) * PD_CTR;
+  const __amdgpu_buffer_rsrc_t rg = pd_rsrc(gates, (unsigned)((size_t)d.B * d.S * G4 * 4));
+  const __amdgpu_buffer_rsrc_t rr = pd_rsrc(rbuf, (unsigned)((size_t)d.B * ED * 4));
+  const __amdgpu_buffer_rsrc_t rs = pd_rsrc(sbuf, (unsigned)((size_t)d.B * PD_CHUNKS * 4));
+  const __amdgpu_buffer_rsrc_t rw = pd_rsrc(dwdc, (unsigned)((size_t)d.B * PD_CHUNKS * d.A * 4));
+  const __amdgpu_buffer_rsrc_t rf = pd_rsrc(dFbuf, (unsigned)((size_t)d.B * d.T * d.C * 4));
+  // frame role
+  const int fsl = m / PD_CHUNKS, ch = m % PD_CHUNKS;
+  const int be = grp + PD_GROUPS * fsl;
+  const bool fact = be < d.B;
+  const int tt0 = ch * FCH, nfr = max(0, min(FCH, d.T - tt0));
+  const int e0 = ch * ECW, ecn = max(0, min(ECW, d.E - e0));
+  const int len = fact ? lens[be] : 0;
+  constexpr int CM = CC ? CC : PB_CM;
+  const int C = CC ? CC : d.C;
+  // cell role
+  const int csl = tid / UPW, cu = tid % UPW;
+  const int cb = grp + PD_GROUPS * csl, cj = u0 + cu;
+  const bool cown = tid < PD_SLOTS * UPW && cu < nu && cb < d.B;
+  float dc_reg = 0.f;
+
+  // ---- once per pass
+  bf16x8 wf[PB_KQ];
+  {
+    const int tile = wave & 1, kq = wave >> 1;
+    const int c16 = tile * 16 + (lane & 15);
+    const bool ok = c16 < nn;
+    const uint16_t* wr = wcatT + (long long)(ok ? n0 + c16 : 0) * G4;
+#pragma unroll
+    for (int i = 0; i < PB_KQ; ++i) {
+      const int kb = kq * G.KQ + i;
+      const int k = kb * 32 + 8 * (lane >> 4);
+      wf[i] = (ok && i < G.KQ && kb < G.NKB && k < G4)
+                  ? load_bf16x8(wr + k) : as_bf16x8(u16x8{0, 0, 0, 0, 0, 0, 0, 0});
+    }
+  }
+  for (int i = tid; i < FCH * d.E; i += PD_THREADS) {
+    const int fi = i / d.E, e = i % d.E;
+    L[G.encr + i] = (fact && fi < nfr) ? enc[((long long)be * d.T + tt0 + fi) * d.E + e] : 0.f;
+  }
+  for (int i = tid; i < FCH * d.A; i += PD_THREADS) {
+    const int fi = i / d.A, a = i % d.A;
+    L[G.ea + i] = (fact && fi < nfr) ? enc_a[((long long)be * d.T + tt0 + fi) * d.A + a] : 0.f;
+  }
+  for (int i = tid; i < d.C * d.K; i += PD_THREADS) L[G.cw + i] = conv_w[i];
+  for (int i = tid; i < d.A * d.C; i += PD_THREADS) L[G.wc + i] = w_conv[i];
+  for (int i = tid; i < d.A; i += PD_THREADS) L[G.v + i] = vw[i];
+  for (int i = tid; i < d.A * UPW; i += PD_THREADS) {
+    const int a = i / UPW, u = i % UPW;
+    L[G.wdl + i] = u < nu ? w_dec[(long long)a * d.D + u0 + u] : 0.f;
+  }
+  for (int i = tid; i < FCH; i += PD_THREADS) L[G.carry + i] = 0.f;
+  // register accumulators over the pass: the chunk's dV / dW_conv per lane,
+  // the conv-kernel partial per thread (d enc_a: this work-group's rows of
+  // d_enc_a, zeroed by the host, read-modify-written per step)
+  float accV[NQ];
+  float accWc[NQ][CM];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) accV[q] = 0.f;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+#pragma unroll
+    for (int c = 0; c < CM; ++c) accWc[q][c] = 0.f;
+  constexpr int NDCW = 4;   // (c, k) pairs per thread: C K <= 4 * 512
+  float dcwacc[NDCW] = {0.f, 0.f, 0.f, 0.f};
+  int nph = 0;
+  __syncthreads();
+
+#define PB_WAIT()                                                              \
+  do {                                                                         \
+    if (nph > 0) {                                                             \
+      if (tid == 0) s_ok = pd_wait(my_ctr, PD_MEMBERS * nph, ctr, status);     \
+      __syncthreads();                                                         \
+      if (!s_ok) return;                                                       \
+    }                                                                          \
+  } while (0)
+#define PB_PUBLISH()     \
+  do {                   \
+    pd_publish(my_ctr);  \
+    ++nph;               \
+  } while (0)
+
+  for (int t = d.S - 1; t >= 0; --t) {
+    const bool has_r = t + 1 < d.S;
+    // ================= H: r = dgates_{t+1} Wcat (this member's columns) =================
+    if (has_r) {
+      PB_WAIT();
+      uint16_t* dgs = reinterpret_cast<uint16_t*>(&L[G.dgs]);
+      const int nv = G4 / 4;
+      for (int i = tid; i < PD_SLOTS * nv; i += PD_THREADS) {
+        const int sl = i / nv, k4 = i % nv, bb = grp + PD_GROUPS * sl;
+        pd_u32x4 v = {0u, 0u, 0u, 0u};
+        if (bb < d.B)
+          v = __builtin_amdgcn_raw_buffer_load_b128(
+              rg, (unsigned)((((long long)bb * d.S + t + 1) * G4 + 4 * k4) * 4), 0, 16);
+        uint16_t* o = dgs + sl * G4 + 4 * k4;
+        o[0] = f2bf(__uint_as_float(v[0]));
+        o[1] = f2bf(__uint_as_float(v[1]));
+        o[2] = f2bf(__uint_as_float(v[2]));
+        o[3] = f2bf(__uint_as_float(v[3]));
+      }
+      __syncthreads();
+      {
+        const int kq = wave >> 1, mm = lane & 15;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < PB_KQ; ++i) {
+          const int kb = kq * G.KQ + i;
+          if (i < G.KQ && kb < G.NKB) {   // wave-uniform
+            const int k = kb * 32 + 8 * (lane >> 4);
+            const bf16x8 a = (mm < PD_SLOTS && k < G4) ? load_bf16x8(dgs + mm * G4 + k)
+                                                      : as_bf16x8(u16x8{0, 0, 0, 0, 0, 0, 0, 0});
+            acc = mfma_bf16(a, wf[i], acc);
+          }
+        }
+        if (lane < 16) {
+#pragma unroll
+          for (int rr4 = 0; rr4 < 4; ++rr4) L[G.part + (wave * PD_SLOTS + rr4) * 16 + lane] = acc[rr4];
+        }
+      }
+      __syncthreads();
+      if (tid < PD_SLOTS * 32) {
+        const int sl = tid >> 5, c32 = tid & 31, tile = c32 >> 4, col = c32 & 15;
+        const int bb = grp + PD_GROUPS * sl;
+        if (c32 < nn && bb < d.B) {
+          float s = 0.f;
+#pragma unroll
+          for (int kq = 0; kq < 4; ++kq) s += L[G.part + ((2 * kq + tile) * PD_SLOTS + sl) * 16 + col];
+          pd_st(rr, (long long)bb * ED + n0 + c32, s);
+        }
+      }
+      PB_PUBLISH();
+    }
+
+    // ================= E: d ctx_t, d aw_t, softmax chunk sums; conv features =================
+    PB_WAIT();
+    if (fact) {
+      for (int e = tid; e < d.E; e += PD_THREADS) {
+        float v = d_ctx_in[((long long)be * d.S + t) * d.E + e];
+        if (has_r) v += pd_ld(rr, (long long)be * ED + e);
+        L[G.dct + e] = v;
+        if (e >= e0 && e < e0 + ecn) dctx_tot[((long long)be * d.S + t) * d.E + e] = v;
+      }
+      // aw_t of the chunk, aw_{t-1} window, W_dec h_t (forward outputs: plain loads)
+      for (int i = tid; i < FCH; i += PD_THREADS)
+        L[G.awt + i] = i < nfr ? aw_all[((long long)be * d.S + t) * d.T + tt0 + i] : 0.f;
+      for (int i = tid; i < KW; i += PD_THREADS) {
+        const int tt = tt0 - half + i;
+        L[G.awin + i] = (t > 0 && tt >= 0 && tt < d.T)
+                            ? aw_all[((long long)be * d.S + t - 1) * d.T + tt] : 0.f;
+      }
+      for (int a = tid; a < d.A; a += PD_THREADS) L[G.wd + a] = wd_all[((long long)be * d.S + t) * d.A + a];
+      __syncthreads();
+      // d aw over this wave's frames: lanes over e
+#pragma unroll
+      for (int f = 0; f < PD_FPW; ++f) {
+        const int i = wave + 8 * f;
+        if (i >= nfr) break;
+        float s = 0.f;
+        for (int e = lane; e < d.E; e += 64) s += L[G.encr + i * d.E + e] * L[G.dct + e];
+        s = wave_sum(s);
+        if (lane == 0) L[G.daw + i] = L[G.carry + i] + s;
+      }
+      // conv features of aw_{t-1} for the chunk (independent of the hand-off)
+      for (int i = tid; i < FCH * C; i += PD_THREADS) {
+        const int fi = i / C, c = i % C;
+        float s = 0.f;
+        if (fi < nfr) s = dot_lds(&L[G.cw + c * d.K], 1, &L[G.awin + fi], 1, d.K);
+        L[G.f + i] = s;
+      }
+      __syncthreads();
+      if (wave == 0) {
+        float s = 0.f;
+        for (int i = lane; i < nfr; i += 64) s += L[G.awt + i] * L[G.daw + i];
+        s = wave_sum(s);
+        if (lane == 0) pd_st(rs, (long long)be * PD_CHUNKS + ch, s);
+      }
+    }
+    PB_PUBLISH();
+
+    // ================= F: softmax / tanh backward of the chunk =================
+    PB_WAIT();
+    if (fact) {
+      if (wave == 0) {
+        float s = lane < PD_CHUNKS ? pd_ld(rs, (long long)be * PD_CHUNKS + lane) : 0.f;
+        s = wave_sum(s);
+        if (lane == 0) s_sdot = s;
+      }
+      __syncthreads();
+      const float sdot = s_sdot;
+      for (int i = tid; i < FCH; i += PD_THREADS) {
+        const int tt = tt0 + i;
+        float de = 0.f;
+        if (i < nfr && tt < len) {
+          const float a = L[G.awt + i], g = L[G.daw + i];
+          de = (d.sigmoid ? g * a * (1.f - a) : a * (g - sdot)) * d.sharpen;
+        }
+        L[G.de + i] = de;
+      }
+      __syncthreads();
+      float accWd[NQ];
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) accWd[q] = 0.f;
+#pragma unroll 1
+      for (int i = wave; i < nfr; i += 8) {
+        const int tt = tt0 + i;
+        const float de = L[G.de + i];
+        const long long fo = ((long long)be * d.T + tt) * d.C;
+        if (de == 0.f) {   // padded / masked frame: nothing flows
+          if (lane < C) pd_st(rf, fo + lane, 0.f);
+          continue;
+        }
+        float* dear = d_enc_a + ((long long)be * d.T + tt) * d.A;
+        float deav[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) deav[q] = (lane + 64 * q < d.A) ? dear[lane + 64 * q] : 0.f;
+        float frv[CM], dfc[CM];
+#pragma unroll
+        for (int c = 0; c < CM; ++c) {
+          frv[c] = (CC || c < C) ? L[G.f + i * C + c] : 0.f;
+          dfc[c] = 0.f;
+        }
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          const int a = lane + 64 * q;
+          if (64 * q < d.A) {   // wave-uniform
+            float wrv[CM];
+#pragma unroll
+            for (int c = 0; c < CM; ++c) wrv[c] = (a < d.A && (CC || c < C)) ? L[G.wc + a * C + c] : 0.f;
+            float p = (a < d.A ? L[G.ea + i * d.A + a] + L[G.wd + a] : 0.f);
+#pragma unroll
+            for (int c = 0; c < CM; ++c) p += frv[c] * wrv[c];
+            const float th = tanhf(p);
+            const float dp = a < d.A ? de * L[G.v + a] * (1.f - th * th) : 0.f;
+            accV[q] += a < d.A ? de * th : 0.f;
+            accWd[q] += dp;
+            if (a < d.A) dear[a] = deav[q] + dp;
+#pragma unroll
+            for (int c = 0; c < CM; ++c) {
+              accWc[q][c] += dp * frv[c];
+              dfc[c] += dp * wrv[c];
+            }
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < CM; ++c) {
+          if (CC || c < C) {
+            const float sv = wave_sum(dfc[c]);
+            if (lane == 0) pd_st(rf, fo + c, sv);
+          }
+        }
+      }
+      // the chunk's d W_dec-input sum: per-wave rows combined in wave order
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int a = lane + 64 * q;
+        if (a < d.A) L[G.cmb + wave * d.A + a] = accWd[q];
+      }
+      __syncthreads();
+      for (int a = tid; a < d.A; a += PD_THREADS) {
+        float s = 0.f;
+        for (int w = 0; w < 8; ++w) s += L[G.cmb + w * d.A + a];
+        pd_st(rw, ((long long)be * PD_CHUNKS + ch) * d.A + a, s);
+      }
+    }
+    PB_PUBLISH();
+
+    // ================= G: conv transpose (frames), LSTMCell backward (units) =================
+    PB_WAIT();
+    if (fact && t > 0) {
+      for (int i = tid; i < KW * C; i += PD_THREADS) {
+        const int row = i / C, c = i % C, tt = tt0 - half + row;
+        L[G.dFw + i] = (tt >= 0 && tt < d.T) ? pd_ld(rf, ((long long)be * d.T + tt) * d.C + c) : 0.f;
+      }
+    }
+    for (int i = tid; i < PD_SLOTS * d.A; i += PD_THREADS) {   // dWd_t of the 4 utterances
+      const int sl = i / d.A, a = i % d.A, bb = grp + PD_GROUPS * sl;
+      float s = 0.f;
+      if (bb < d.B) {
+        float v8[PD_CHUNKS];
+#pragma unroll
+        for (int j = 0; j < PD_CHUNKS; ++j)
+          v8[j] = pd_ld(rw, ((long long)bb * PD_CHUNKS + j) * d.A + a);
+#pragma unroll
+        for (int j = 0; j < PD_CHUNKS; ++j) s += v8[j];
+        if (m == 0) dwd_all[((long long)bb * d.S + t) * d.A + a] = s;
+      }
+      L[G.dwdl + i] = s;
+    }
+    __syncthreads();
+    if (fact && t > 0) {
+      // d aw_{t-1}[j] = sum_c sum_k dF[j - k + half, c] cw[c, k]: one (frame, channel) per thread
+      float* cp = &L[G.cmb];
+      for (int i = tid; i < FCH * C; i += PD_THREADS) {
+        const int fi = i / C, c = i % C;
+        float s = 0.f;
+        if (fi < nfr) s = dot_lds(&L[G.dFw + (fi + d.K - 1) * C + c], -C, &L[G.cw + c * d.K], 1, d.K);
+        cp[i] = s;
+      }
+      // conv-kernel partial: dcw[c, k] += sum_{own frames} dF[tt, c] aw_{t-1}[tt + k - half]
+#pragma unroll
+      for (int j = 0; j < NDCW; ++j) {
+        const int i = tid + j * PD_THREADS;
+        if (i < d.C * d.K) {
+          const int c = i / d.K, k = i % d.K;
+          dcwacc[j] += dot_lds(&L[G.dFw + half * C + c], C, &L[G.awin + k], 1, nfr);
+        }
+      }
+    }
+    if (cown) {
+      float dd = 0.f;
+      for (int a = 0; a < d.A; ++a) dd += L[G.wdl + a * UPW + cu] * L[G.dwdl + csl * d.A + a];
+      const float dh = d_dec_in[((long long)cb * d.S + t) * d.D + cj] +
+                       (has_r ? pd_ld(rr, (long long)cb * ED + d.E + cj) : 0.f) + dd;
+      if (t == 0) {
+        if (d_h0) d_h0[(long long)cb * d.D + cj] = dh;
+      } else {
+        const float dhr =
+            drop_h > 0.f ? dh * drop_scale(drop_h, seed_h, ((unsigned long long)cb * d.S + t) * d.D + cj)
+                         : dh;
+        const long long gb = ((long long)cb * d.S + t) * G4 + cj;
+        const float ig = gates[gb], fg = gates[gb + d.D], gg = gates[gb + 2 * d.D],
+                    og = gates[gb + 3 * d.D];
+        const float c = c_all[((long long)cb * d.S + t) * d.D + cj];
+        const float cprev = c_all[((long long)cb * d.S + t - 1) * d.D + cj];
+        const float tc = tanhf(c);
+        const float dcell = dc_reg + dhr * og * (1.f - tc * tc);
+        pd_st(rg, gb, dcell * gg * ig * (1.f - ig));
+        pd_st(rg, gb + d.D, dcell * cprev * fg * (1.f - fg));
+        pd_st(rg, gb + 2 * d.D, dcell * ig * (1.f - gg * gg));
+        pd_st(rg, gb + 3 * d.D, dhr * tc * og * (1.f - og));
+        dc_reg = dcell * fg;
+      }
+    }
+    __syncthreads();
+    if (fact && t > 0) {
+      for (int i = tid; i < FCH; i += PD_THREADS) {
+        float s = 0.f;
+        for (int c = 0; c < C; ++c) s += L[G.cmb + i * C + c];
+        L[G.carry + i] = s;
+      }
+    }
+    PB_PUBLISH();
+  }
+#undef PB_WAIT
+#undef PB_PUBLISH
+
+  // ---- end of pass: the chunk's weight-gradient partial rows
+  if (!fact) return;
+  const long long row = (long long)be * PD_CHUNKS + ch;
+#pragma unroll
+  for (int j = 0; j < NDCW; ++j) {
+    const int i = tid + j * PD_THREADS;
+    if (i < d.C * d.K) dcw_part[row * d.C * d.K + i] = dcwacc[j];
+  }
+  float* cV = &L[G.cmb];
+  float* cWc = cV + d.A;
+  __syncthreads();
+  for (int pass = 0; pass < 8; ++pass) {
+    if (wave == pass) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int a = lane + 64 * q;
+        if (a < d.A) {
+          cV[a] = pass ? cV[a] + accV[q] : accV[q];
+#pragma unroll
+          for (int c = 0; c < CM; ++c)
+            if (CC || c < C) cWc[a * C + c] = pass ? cWc[a * C + c] + accWc[q][c] : accWc[q][c];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  for (int i = tid; i < d.A; i += PD_THREADS) dv_part[row * d.A + i] = cV[i];
+  for (int i = tid; i < d.A * d.C; i += PD_THREADS) dwc_part[row * d.A * d.C + i] = cWc[i];
 }
 
 }  // namespace
@@ -1477,6 +1984,9 @@ int device_cus() {
 // The persistent forward pass takes a shape when its work split fits (see the
 // kernel's comment) and the 256-work-group grid is co-resident, one per CU.
 // ASR_ATT_PERSIST=0 keeps the per-step kernels (A/B).
+// the production instantiation: 10 conv channels, A <= 128
+bool pd_ten(const Dims& d) { return d.C == 10 && d.A <= 128; }
+
 bool pd_eligible(const Dims& d) {
   const char* e = getenv("ASR_ATT_PERSIST");
   if (e && e[0] == '0') return false;
@@ -1487,7 +1997,30 @@ bool pd_eligible(const Dims& d) {
       (size_t)d.B * d.S * G.ED * 4 >= (1ull << 31) || (size_t)d.B * d.T * 4 >= (1ull << 31))
     return false;
   if (device_cus() < PD_GROUPS * PD_MEMBERS) return false;
-  const void* k = d.C == 10 ? (const void*)attdec_fwd_persist<10> : (const void*)attdec_fwd_persist<0>;
+  const void* k = pd_ten(d) ? (const void*)attdec_fwd_persist<10, 2> : (const void*)attdec_fwd_persist<0, 4>;
+  if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return false;
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, PD_THREADS, lds) != hipSuccess)
+    return false;
+  return per_cu >= 1;
+}
+
+bool pb_eligible(const Dims& d) {
+  const char* e = getenv("ASR_ATT_PERSIST");
+  if (e && e[0] == '0') return false;
+  const char* eb = getenv("ASR_ATT_PERSIST_BWD");
+  if (eb && eb[0] == '0') return false;
+  const PbGeom G = pb_geom(d);
+  const size_t lds = (size_t)G.total * 4;
+  if (d.B > PD_GROUPS * PD_SLOTS || G.UPW > PD_UMAX || G.NPW > 32 || G.G4 % 8 != 0 ||
+      G.KQ > PB_KQ || G.FCH > 8 * PD_FPW || d.A > 256 || (!pd_ten(d) && d.C > PB_CM) ||
+      d.C * d.K > 4 * PD_THREADS ||
+      lds > 160 * 1024 || (size_t)d.B * d.S * G.G4 * 4 >= (1ull << 31) ||
+      (size_t)d.B * d.T * d.C * 4 >= (1ull << 31))
+    return false;
+  if (device_cus() < PD_GROUPS * PD_MEMBERS) return false;
+  const void* k = pd_ten(d) ? (const void*)attdec_bwd_persist<10, 2> : (const void*)attdec_bwd_persist<0, 4>;
   if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return false;
   int per_cu = 0;
@@ -1510,10 +2043,11 @@ extern "C" size_t asr_attdec_workspace_bytes(const asr_attdec_dims_t* dims, int 
   return att_ws(to_dims(*dims), compute_dtype, backward != 0).total;
 }
 
-// Attention frame chunks per utterance: the backward partials dv_part,
-// dwc_part and dcw_part hold B * chunks rows (each summed over the steps).
+// Rows per utterance of the backward partials dv_part, dwc_part and dcw_part
+// (B * this many rows, each summed over the steps; rows a pass does not use
+// are written zero).
 extern "C" int asr_attdec_chunks(const asr_attdec_dims_t* dims) {
-  return att_chunks(to_dims(*dims));
+  return part_rows(to_dims(*dims));
 }
 
 namespace {
@@ -1609,16 +2143,16 @@ extern "C" int asr_attdec_forward_ex(const asr_attdec_dims_t* dims, const asr_at
     ASR_CHECK_HIP(hipMemsetAsync(ctr, 0, (size_t)(1 + PD_GROUPS) * PD_CTR * 4, s));
     const size_t lds = (size_t)G.total * 4;
     const dim3 grid(PD_GROUPS * PD_MEMBERS);
-#define ASR_PD(CC)                                                                              \
-  hipLaunchKernelGGL(attdec_fwd_persist<CC>, grid, dim3(PD_THREADS), lds, s, d,                 \
+#define ASR_PD(CC, NQ)                                                                            \
+  hipLaunchKernelGGL((attdec_fwd_persist<CC, NQ>), grid, dim3(PD_THREADS), lds, s, d,                 \
                      (const uint16_t*)workspace, pre_emb, h0, enc, enc_a, lens, w_dec, w_conv,   \
                      conv_w, v, dec, c_all, gates, x, ctx_all, aw_all, pbuf, ebuf, ctr,          \
                      lstm_persist_status_word(), drop_h, seed_h)
-    if (d.C == 10) ASR_PD(10);
-    else ASR_PD(0);
+    if (pd_ten(d)) ASR_PD(10, 2);
+    else ASR_PD(0, 4);
 #undef ASR_PD
     ASR_LAUNCH_CHECK();
-    g_att_last[0] = d.C == 10 ? 10 : 0;
+    g_att_last[0] = pd_ten(d) ? 10 : 0;
     g_att_persist_last[0] = 1;
     return ASR_OK;
   }
@@ -1757,6 +2291,34 @@ extern "C" int asr_attdec_backward_ex(const asr_attdec_dims_t* dims, const asr_a
     hipLaunchKernelGGL((build_wcat_t<float>), dim3(gb), dim3(256), 0, s, d, w_ih_ctx, ld_ih, w_hh,
                        (float*)wcatT);
   ASR_LAUNCH_CHECK();
+  {  // rows of the partials a pass does not write stay zero
+    const size_t prow = (size_t)d.B * part_rows(d);
+    ASR_CHECK_HIP(hipMemsetAsync(dv_part, 0, prow * d.A * 4, s));
+    ASR_CHECK_HIP(hipMemsetAsync(dwc_part, 0, prow * d.A * d.C * 4, s));
+    ASR_CHECK_HIP(hipMemsetAsync(dcw_part, 0, prow * d.C * d.K * 4, s));
+  }
+  g_att_persist_last[1] = 0;
+  if (bf && pb_eligible(d)) {
+    const PbGeom PG = pb_geom(d);
+    int* ctr = (int*)(p + W.ctr);
+    float* sbuf = (float*)(p + W.sbuf);
+    ASR_CHECK_HIP(hipMemsetAsync(ctr, 0, (size_t)(1 + PD_GROUPS) * PD_CTR * 4, s));
+    ASR_CHECK_HIP(hipMemsetAsync(d_enc_a, 0, (size_t)d.B * d.T * d.A * 4, s));
+    const size_t lds = (size_t)PG.total * 4;
+    const dim3 grid(PD_GROUPS * PD_MEMBERS);
+#define ASR_PB(CC, NQ)                                                                            \
+  hipLaunchKernelGGL((attdec_bwd_persist<CC, NQ>), grid, dim3(PD_THREADS), lds, s, d,                 \
+                     (const uint16_t*)wcatT, enc, enc_a, lens, w_dec, w_conv, conv_w, v, c_all,  \
+                     aw_all, wd_all, d_dec_in, d_ctx_in, gates_dg, dctx_tot, d_enc_a, d_h0,      \
+                     dwd_all, dv_part, dwc_part, dcw_part, r, sbuf, dwd_chunk, dFbuf, ctr,       \
+                     lstm_persist_status_word(), drop_h, seed_h)
+    if (pd_ten(d)) ASR_PB(10, 2);
+    else ASR_PB(0, 4);
+#undef ASR_PB
+    ASR_LAUNCH_CHECK();
+    g_att_last[2] = pd_ten(d) ? 10 : 0;
+    g_att_persist_last[1] = 1;
+  } else {
   ASR_CHECK_HIP(hipMemsetAsync(carry, 0, (size_t)d.B * d.T * 4, s));
   ASR_CHECK_HIP(hipMemsetAsync(dc, 0, (size_t)d.B * d.D * 4, s));
   ASR_CHECK_HIP(hipMemsetAsync(d_enc_a, 0, (size_t)d.B * d.T * d.A * 4, s));
@@ -1800,6 +2362,7 @@ extern "C" int asr_attdec_backward_ex(const asr_attdec_dims_t* dims, const asr_a
     hipLaunchKernelGGL(cell_bwd, dim3(cgrid), dim3(256), 0, s, t, d, d_dec_in, rp, ddec_att,
                        gates_dg, c_all, dc, d_h0, drop_h, seed_h);
     ASR_LAUNCH_CHECK();
+  }
   }
   if (ss) {
     ASR_CHECK_HIP(hipMemcpyAsync(flags, opts->ss_steps_host, (size_t)d.S * 4,
@@ -1963,6 +2526,12 @@ extern "C" int asr_att_step_backward(const asr_attdec_dims_t* dims, const float*
   else
     ASR_CHECK_HIP(hipMemsetAsync(carry, 0, (size_t)d.B * d.T * 4, s));
   ASR_CHECK_HIP(hipMemsetAsync(d_enc_a, 0, (size_t)d.B * d.T * d.A * 4, s));
+  {  // rows the step's chunks do not write stay zero
+    const size_t prow = (size_t)d.B * part_rows(d);
+    ASR_CHECK_HIP(hipMemsetAsync(dv_part, 0, prow * d.A * 4, s));
+    ASR_CHECK_HIP(hipMemsetAsync(dwc_part, 0, prow * d.A * d.C * 4, s));
+    ASR_CHECK_HIP(hipMemsetAsync(dcw_part, 0, prow * d.C * d.K * 4, s));
+  }
   {  // W_dec dec (exact-f32 MFMA, as the decoder backward)
     asr_gemm_t g;
     memset(&g, 0, sizeof(g));
