@@ -1146,7 +1146,7 @@ typedef __attribute__((ext_vector_type(4))) unsigned int pd_u32x4;
 
 struct PdGeom {
   int UPW, FCH, ECW, ED, NKB, half;
-  int xs, wdl, cw, wc, v, awp, wd, wq, f, hs, part, red, cpart, encs, total;   // LDS floats
+  int xs, wdl, cw, wc, v, awp, wd, wq, f, hs, part, red, cpart, mp, encs, total;   // LDS floats
 };
 
 __host__ __device__ inline PdGeom pd_geom(const Dims& d) {
@@ -1163,7 +1163,7 @@ __host__ __device__ inline PdGeom pd_geom(const Dims& d) {
   g.cw = o; o += d.C * d.K;
   g.wc = o; o += d.A * d.C;
   g.v = o; o += d.A;
-  g.awp = o; o += d.T + 2 * g.half + 4;
+  g.awp = o; o += d.T + 2 * g.half + 16;
   g.wd = o; o += d.A;
   g.wq = o; o += 4 * d.A;
   g.f = o; o += g.FCH * d.C;
@@ -1171,9 +1171,57 @@ __host__ __device__ inline PdGeom pd_geom(const Dims& d) {
   g.part = o; o += 6 * PD_SLOTS * 16;
   g.red = o; o += 64;
   g.cpart = o; o += PD_THREADS;
+  g.mp = o; o += 2048;
   g.encs = o; o += d.T * g.ECW;
   g.total = (o + 3) & ~3;
   return g;
+}
+
+// Conv features of a frame chunk on the f32 MFMA (16x16x4): f[i][c] =
+// sum_k cw[c][k] win[i + k] for frames i < FCH <= 64, channels c < C <= 16
+// (win[i + k] = aw_{t-1}[tt0 + i + k - K/2]).  All 8 waves: wave w takes row
+// tile w % MT and K part w / MT (MT = ceil(FCH / 16)); the K parts' tiles are
+// summed in order through part (LDS, 2048 floats).  A Toeplitz product: one
+// window load and one kernel load per lane per 4 taps, against two LDS loads
+// per tap of a dot-product loop.
+__device__ __forceinline__ void pd_conv_feat(const float* cw, const float* win, int C, int K,
+                                             int FCH, float* part, float* f) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int MT = FCH <= 16 ? 1 : FCH <= 32 ? 2 : 4;
+  const int KP = 8 / MT;
+  const int mt = wave % MT, kp = wave / MT;
+  const int nks = (K + 3) / 4, per = (nks + KP - 1) / KP;
+  const int s0 = kp * per, s1 = min(nks, s0 + per);
+  const int row = mt * 16 + (lane & 15), kk = lane >> 4, col = lane & 15;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int st = s0; st < s1; st += 4) {
+    float a[4], b[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = (st + j) * 4 + kk;
+      const bool ok = st + j < s1 && k < K;
+      a[j] = (ok && row < FCH) ? win[row + k] : 0.f;
+      b[j] = (ok && col < C) ? cw[col * K + k] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc = mfma_f32(a[j], b[j], acc);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) part[(wave * 16 + 4 * (lane >> 4) + r) * 16 + col] = acc[r];
+  __syncthreads();
+  for (int i = threadIdx.x; i < FCH * C; i += blockDim.x) {
+    const int fi = i / C, c = i % C, tl = fi >> 4, rr = fi & 15;
+    float v = 0.f;
+    for (int q = 0; q < KP; ++q) v += part[((q * MT + tl) * 16 + rr) * 16 + c];
+    f[i] = v;
+  }
+}
+
+// tanh through one exp and one reciprocal (the persistent passes' energy
+// tanh; |error| ~1e-7, the per-step kernels use libm tanhf)
+__device__ __forceinline__ float pd_tanh(float x) {
+  const float e = __expf(2.f * fminf(fmaxf(x, -15.f), 15.f));
+  return 1.f - 2.f / (e + 1.f);
 }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t pd_rsrc(const void* p, unsigned bytes) {
@@ -1283,7 +1331,7 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
   for (int i = tid; i < d.C * d.K; i += PD_THREADS) L[G.cw + i] = conv_w[i];
   for (int i = tid; i < d.A * d.C; i += PD_THREADS) L[G.wc + i] = w_conv[i];
   for (int i = tid; i < d.A; i += PD_THREADS) L[G.v + i] = vw[i];
-  for (int i = tid; i < d.T + 2 * half + 4; i += PD_THREADS) L[G.awp + i] = 0.f;
+  for (int i = tid; i < d.T + 2 * half + 16; i += PD_THREADS) L[G.awp + i] = 0.f;
   for (int i = tid; i < d.T * ECW; i += PD_THREADS) {
     const int tt = i / ECW, cc = i % ECW;
     L[G.encs + i] = (fact && cc < ecn) ? enc[((long long)be * d.T + tt) * d.E + e0 + cc] : 0.f;
@@ -1303,6 +1351,8 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
       __syncthreads();
       if (!s_ok) return;
       PD_TR(33);
+      // x_t rows of the 4 utterances, rounded to bf16 once (the MFMA A operand)
+      uint16_t* xsb = reinterpret_cast<uint16_t*>(&L[G.xs]);
       const int nv = ED / 4;
       for (int i = tid; i < PD_SLOTS * nv; i += PD_THREADS) {
         const int sl = i / nv, k4 = i % nv, bb = grp + PD_GROUPS * sl;
@@ -1310,7 +1360,9 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
         if (bb < d.B)
           v = __builtin_amdgcn_raw_buffer_load_b128(
               rx, (unsigned)((((long long)bb * d.S + t) * ED + 4 * k4) * 4), 0, 16);
-        *reinterpret_cast<pd_u32x4*>(&L[G.xs + sl * ED + 4 * k4]) = v;
+        const unsigned lo = f2bf(__uint_as_float(v[0])) | ((unsigned)f2bf(__uint_as_float(v[1])) << 16);
+        const unsigned hi = f2bf(__uint_as_float(v[2])) | ((unsigned)f2bf(__uint_as_float(v[3])) << 16);
+        *reinterpret_cast<uint2*>(xsb + sl * ED + 4 * k4) = make_uint2(lo, hi);
       }
       __syncthreads();
       PD_TR(34);
@@ -1322,7 +1374,7 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
           const int kb = kh + 2 * i;
           if (kb < NKB) {   // wave-uniform
             const int k = kb * 32 + 8 * (lane >> 4);
-            const bf16x8 a = (mm < PD_SLOTS && k < ED) ? cvt8(&L[G.xs + mm * ED + k])
+            const bf16x8 a = (mm < PD_SLOTS && k < ED) ? load_bf16x8(xsb + mm * ED + k)
                                                       : as_bf16x8(u16x8{0, 0, 0, 0, 0, 0, 0, 0});
             acc = mfma_bf16(a, wf[i], acc);
           }
@@ -1361,6 +1413,7 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
         L[G.hs + csl * PD_UMAX + cu] = h;   // absent (slot, unit) entries stay 0 from t = 0
       }
     } else {
+      for (int i = tid; i < FCH * C; i += PD_THREADS) L[G.f + i] = 0.f;   // aw_{-1} = 0
       if (tid < PD_SLOTS * PD_UMAX) {
         const int sl = tid / PD_UMAX, u = tid % PD_UMAX, bb = grp + PD_GROUPS * sl;
         L[G.hs + tid] = (h0 && u < nu && bb < d.B) ? h0[(long long)bb * d.D + u0 + u] : 0.f;
@@ -1377,6 +1430,8 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
     }
     pd_publish(my_ctr);
     PD_TR(37);
+    // conv features of aw_{t-1} for this chunk (local data: before the wait)
+    if (fact && t > 0) pd_conv_feat(&L[G.cw], &L[G.awp + tt0], C, d.K, FCH, &L[G.mp], &L[G.f]);
 
     // ================= E: energies of this work-group's frame chunk =================
     if (tid == 0) s_ok = pd_wait(my_ctr, PD_MEMBERS * (3 * t + 1), ctr, status);
@@ -1395,41 +1450,47 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
         for (int j = 0; j < 8; ++j) s += v[j];
         L[G.wq + qq * d.A + a] = s;
       }
-      // conv features of the chunk from aw_{t-1} (zero at t = 0 and outside [0, T))
-      for (int i = tid; i < FCH * C; i += PD_THREADS) {
-        const int fi = i / C, c = i % C;
-        float s = 0.f;
-        if (t > 0 && fi < nfr) s = dot_lds(&L[G.cw + c * d.K], 1, &L[G.awp + tt0 + fi], 1, d.K);
-        L[G.f + i] = s;
-      }
       __syncthreads();
       PD_TR(39);
       for (int a = tid; a < d.A; a += PD_THREADS)
         L[G.wd + a] = (L[G.wq + a] + L[G.wq + d.A + a]) + (L[G.wq + 2 * d.A + a] + L[G.wq + 3 * d.A + a]);
       __syncthreads();
       PD_TR(40);
+      // every frame's lane partial first, then the wave sums together (independent
+      // reduction chains in flight)
+      float sf[PD_FPW];
 #pragma unroll
       for (int f = 0; f < PD_FPW; ++f) {
         const int i = wave + 8 * f;
-        if (i >= nfr) break;
-        const int tt = tt0 + i;
-        float frv[CM];
+        sf[f] = 0.f;
+        if (i < nfr) {   // wave-uniform
+          float frv[CM];
 #pragma unroll
-        for (int c = 0; c < CM; ++c) frv[c] = (CC || c < C) ? L[G.f + i * C + c] : 0.f;
-        float s = 0.f;
+          for (int c = 0; c < CM; ++c) frv[c] = (CC || c < C) ? L[G.f + i * C + c] : 0.f;
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-          const int a = lane + 64 * q;
-          if (64 * q < d.A && a < d.A) {
-            float p = ea[f][q] + L[G.wd + a];
+          for (int q = 0; q < NQ; ++q) {
+            const int a = lane + 64 * q;
+            if (64 * q < d.A && a < d.A) {
+              float p = ea[f][q] + L[G.wd + a];
 #pragma unroll
-            for (int c = 0; c < CM; ++c)
-              if (CC || c < C) p += frv[c] * L[G.wc + a * C + c];
-            s += L[G.v + a] * tanhf(p);
+              for (int c = 0; c < CM; ++c)
+                if (CC || c < C) p += frv[c] * L[G.wc + a * C + c];
+              sf[f] += L[G.v + a] * pd_tanh(p);
+            }
           }
         }
-        s = wave_sum(s);
-        if (lane == 0) pd_st(re, (long long)be * d.T + tt, (tt < len ? s : 0.f) * d.sharpen);
+      }
+#pragma unroll
+      for (int f = 0; f < PD_FPW; ++f) {
+        const int i = wave + 8 * f;
+        if (i < nfr) sf[f] = wave_sum(sf[f]);
+      }
+      if (lane == 0) {
+#pragma unroll
+        for (int f = 0; f < PD_FPW; ++f) {
+          const int i = wave + 8 * f, tt = tt0 + i;
+          if (i < nfr) pd_st(re, (long long)be * d.T + tt, (tt < len ? sf[f] : 0.f) * d.sharpen);
+        }
       }
     }
     PD_TR(41);
@@ -1443,24 +1504,34 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
     PD_TR(43);
     if (fact) {
       float* aw = &L[G.awp + half];
+      float* red = &L[G.red];
       float mx = -__builtin_huge_valf();
       for (int i = tid; i < d.T; i += PD_THREADS) {
         const float e = pd_ld(re, (long long)be * d.T + i);
         aw[i] = e;
         mx = fmaxf(mx, e);
       }
-      __syncthreads();
       if (d.sigmoid) {
         for (int i = tid; i < d.T; i += PD_THREADS) aw[i] = sigmoidf_(aw[i]);
-      } else {
-        mx = block_reduce(mx, &L[G.red], true);
+      } else {   // (each thread re-reads only the elements it wrote: no barrier)
+        mx = wave_max(mx);
+        if (lane == 0) red[wave] = mx;
+        __syncthreads();
+        mx = red[0];
+#pragma unroll
+        for (int w = 1; w < 8; ++w) mx = fmaxf(mx, red[w]);
         float sm = 0.f;
         for (int i = tid; i < d.T; i += PD_THREADS) {
           const float p = __expf(aw[i] - mx);
           aw[i] = p;
           sm += p;
         }
-        sm = block_reduce(sm, &L[G.red], false);
+        sm = wave_sum(sm);
+        if (lane == 0) red[8 + wave] = sm;
+        __syncthreads();
+        sm = red[8];
+#pragma unroll
+        for (int w = 1; w < 8; ++w) sm += red[8 + w];
         const float inv = 1.f / sm;
         for (int i = tid; i < d.T; i += PD_THREADS) aw[i] *= inv;
       }
@@ -1470,8 +1541,8 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
         aw_all[((long long)be * d.S + t) * d.T + tt0 + i] = aw[tt0 + i];
       const int NR = PD_THREADS / ECW, col = tid % ECW, r = tid / ECW;
       float s = 0.f;
-      if (r < NR && col < ecn)
-        for (int tt = r; tt < d.T; tt += NR) s += aw[tt] * L[G.encs + tt * ECW + col];
+      if (r < NR && col < ecn && r < d.T)
+        s = dot_lds(&aw[r], NR, &L[G.encs + r * ECW + col], NR * ECW, (d.T - r + NR - 1) / NR);
       if (r < NR) L[G.cpart + r * ECW + col] = s;
       __syncthreads();
       if (tid < ecn) {
@@ -1522,7 +1593,7 @@ constexpr int PB_CM = 4;          // conv channels of the generic instantiation 
 
 struct PbGeom {
   int UPW, FCH, ECW, ED, G4, NPW, NKB, KQ, half, W;
-  int encr, ea, cw, wc, v, dct, awin, f, daw, awt, de, carry, dFw, wd, dgs, part, dwdl, wdl,
+  int encr, ea, cw, wc, v, dct, awin, f, daw, awt, de, carry, wd, un, dgs, part, dwdl, wdl,
       cmb, red, total;   // LDS floats
 };
 
@@ -1551,10 +1622,17 @@ __host__ __device__ inline PbGeom pb_geom(const Dims& d) {
   g.awt = o; o += g.FCH;
   g.de = o; o += g.FCH;
   g.carry = o; o += g.FCH;
-  g.dFw = o; o += g.W * d.C;
   g.wd = o; o += d.A;
   o = (o + 3) & ~3;
-  g.dgs = o; o += PD_SLOTS * g.G4 / 2 + 4;   // bf16 [4][G4]
+  {  // one region, used by phase H (bf16 dgates rows [4][G4]), F (the chunk's
+     // d enc_a rows) and G (dF window [W][C] + the W_dec^T dWd partials)
+    int un = PD_SLOTS * g.G4 / 2 + 4;
+    un = max(un, g.FCH * d.A);
+    un = max(un, g.W * d.C + PD_SLOTS * g.UPW * 8);
+    un = max(un, 2048);   // E: the conv features' MFMA partial tiles
+    g.un = o; o += un;
+    g.dgs = g.un;
+  }
   g.part = o; o += 8 * PD_SLOTS * 16;
   g.dwdl = o; o += PD_SLOTS * d.A;
   g.wdl = o; o += d.A * g.UPW;
@@ -1672,9 +1750,11 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
 
   for (int t = d.S - 1; t >= 0; --t) {
     const bool has_r = t + 1 < d.S;
+    PD_TR(48);
     // ================= H: r = dgates_{t+1} Wcat (this member's columns) =================
     if (has_r) {
       PB_WAIT();
+      PD_TR(49);
       uint16_t* dgs = reinterpret_cast<uint16_t*>(&L[G.dgs]);
       const int nv = G4 / 4;
       for (int i = tid; i < PD_SLOTS * nv; i += PD_THREADS) {
@@ -1719,44 +1799,69 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
           pd_st(rr, (long long)bb * ED + n0 + c32, s);
         }
       }
+      PD_TR(50);
       PB_PUBLISH();
     }
+    PD_TR(51);
 
     // ================= E: d ctx_t, d aw_t, softmax chunk sums; conv features =================
+    // before the wait (forward outputs, no hand-off): d_ctx_in, aw_t of the
+    // chunk, the aw_{t-1} window, W_dec h_t, in one batch of loads; the conv
+    // features of aw_{t-1}
+    if (fact) {
+      const int n1 = d.E, n2 = n1 + FCH, n3 = n2 + KW, total = n3 + d.A;
+      const long long st = (long long)be * d.S + t;
+      for (int base = 0; base < total; base += 4 * PD_THREADS) {
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int i = base + j * PD_THREADS + tid;
+          float x = 0.f;
+          if (i < n1) {
+            x = d_ctx_in[st * d.E + i];
+          } else if (i < n2) {
+            if (i - n1 < nfr) x = aw_all[st * d.T + tt0 + (i - n1)];
+          } else if (i < n3) {
+            const int tt = tt0 - half + (i - n2);
+            if (t > 0 && tt >= 0 && tt < d.T) x = aw_all[(st - 1) * d.T + tt];
+          } else if (i < total) {
+            x = wd_all[st * d.A + (i - n3)];
+          }
+          v[j] = x;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int i = base + j * PD_THREADS + tid;
+          if (i < n1) L[G.dct + i] = v[j];
+          else if (i < n2) L[G.awt + i - n1] = v[j];
+          else if (i < n3) L[G.awin + i - n2] = v[j];
+          else if (i < total) L[G.wd + i - n3] = v[j];
+        }
+      }
+      __syncthreads();
+      if (t > 0) pd_conv_feat(&L[G.cw], &L[G.awin], C, d.K, FCH, &L[G.un], &L[G.f]);
+      else
+        for (int i = tid; i < FCH * C; i += PD_THREADS) L[G.f + i] = 0.f;
+    }
     PB_WAIT();
+    PD_TR(52);
     if (fact) {
       for (int e = tid; e < d.E; e += PD_THREADS) {
-        float v = d_ctx_in[((long long)be * d.S + t) * d.E + e];
+        float v = L[G.dct + e];
         if (has_r) v += pd_ld(rr, (long long)be * ED + e);
         L[G.dct + e] = v;
         if (e >= e0 && e < e0 + ecn) dctx_tot[((long long)be * d.S + t) * d.E + e] = v;
       }
-      // aw_t of the chunk, aw_{t-1} window, W_dec h_t (forward outputs: plain loads)
-      for (int i = tid; i < FCH; i += PD_THREADS)
-        L[G.awt + i] = i < nfr ? aw_all[((long long)be * d.S + t) * d.T + tt0 + i] : 0.f;
-      for (int i = tid; i < KW; i += PD_THREADS) {
-        const int tt = tt0 - half + i;
-        L[G.awin + i] = (t > 0 && tt >= 0 && tt < d.T)
-                            ? aw_all[((long long)be * d.S + t - 1) * d.T + tt] : 0.f;
-      }
-      for (int a = tid; a < d.A; a += PD_THREADS) L[G.wd + a] = wd_all[((long long)be * d.S + t) * d.A + a];
       __syncthreads();
       // d aw over this wave's frames: lanes over e
 #pragma unroll
       for (int f = 0; f < PD_FPW; ++f) {
         const int i = wave + 8 * f;
         if (i >= nfr) break;
-        float s = 0.f;
-        for (int e = lane; e < d.E; e += 64) s += L[G.encr + i * d.E + e] * L[G.dct + e];
+        float s = lane < d.E ? dot_lds(&L[G.encr + i * d.E + lane], 64, &L[G.dct + lane], 64,
+                                       (d.E - lane + 63) / 64) : 0.f;
         s = wave_sum(s);
         if (lane == 0) L[G.daw + i] = L[G.carry + i] + s;
-      }
-      // conv features of aw_{t-1} for the chunk (independent of the hand-off)
-      for (int i = tid; i < FCH * C; i += PD_THREADS) {
-        const int fi = i / C, c = i % C;
-        float s = 0.f;
-        if (fi < nfr) s = dot_lds(&L[G.cw + c * d.K], 1, &L[G.awin + fi], 1, d.K);
-        L[G.f + i] = s;
       }
       __syncthreads();
       if (wave == 0) {
@@ -1766,10 +1871,20 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
         if (lane == 0) pd_st(rs, (long long)be * PD_CHUNKS + ch, s);
       }
     }
+    PD_TR(53);
     PB_PUBLISH();
+    PD_TR(54);
 
     // ================= F: softmax / tanh backward of the chunk =================
+    // before the wait: this work-group's d enc_a rows (its own earlier
+    // read-modify-writes; sc1 loads: other waves of the work-group wrote them)
+    if (fact) {
+      const __amdgpu_buffer_rsrc_t ra =
+          pd_rsrc(d_enc_a + (long long)be * d.T * d.A, (unsigned)((size_t)d.T * d.A * 4));
+      for (int i = tid; i < nfr * d.A; i += PD_THREADS) L[G.un + i] = pd_ld(ra, (long long)tt0 * d.A + i);
+    }
     PB_WAIT();
+    PD_TR(55);
     if (fact) {
       if (wave == 0) {
         float s = lane < PD_CHUNKS ? pd_ld(rs, (long long)be * PD_CHUNKS + lane) : 0.f;
@@ -1801,9 +1916,7 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
           continue;
         }
         float* dear = d_enc_a + ((long long)be * d.T + tt) * d.A;
-        float deav[NQ];
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) deav[q] = (lane + 64 * q < d.A) ? dear[lane + 64 * q] : 0.f;
+        const float* deal = &L[G.un + i * d.A];
         float frv[CM], dfc[CM];
 #pragma unroll
         for (int c = 0; c < CM; ++c) {
@@ -1820,11 +1933,11 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
             float p = (a < d.A ? L[G.ea + i * d.A + a] + L[G.wd + a] : 0.f);
 #pragma unroll
             for (int c = 0; c < CM; ++c) p += frv[c] * wrv[c];
-            const float th = tanhf(p);
+            const float th = pd_tanh(p);
             const float dp = a < d.A ? de * L[G.v + a] * (1.f - th * th) : 0.f;
             accV[q] += a < d.A ? de * th : 0.f;
             accWd[q] += dp;
-            if (a < d.A) dear[a] = deav[q] + dp;
+            if (a < d.A) dear[a] = deal[a] + dp;
 #pragma unroll
             for (int c = 0; c < CM; ++c) {
               accWc[q][c] += dp * frv[c];
@@ -1853,14 +1966,33 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
         pd_st(rw, ((long long)be * PD_CHUNKS + ch) * d.A + a, s);
       }
     }
+    PD_TR(56);
     PB_PUBLISH();
+    PD_TR(57);
 
     // ================= G: conv transpose (frames), LSTMCell backward (units) =================
+    // before the wait: the cell's operands (forward outputs; r of step t+1 was
+    // handed off before phase E)
+    float g_ig = 0.f, g_fg = 0.f, g_gg = 0.f, g_og = 0.f, g_c = 0.f, g_cp = 0.f, g_dh = 0.f;
+    if (cown) {
+      g_dh = d_dec_in[((long long)cb * d.S + t) * d.D + cj] +
+             (has_r ? pd_ld(rr, (long long)cb * ED + d.E + cj) : 0.f);
+      if (t > 0) {
+        const long long gb = ((long long)cb * d.S + t) * G4 + cj;
+        g_ig = gates[gb];
+        g_fg = gates[gb + d.D];
+        g_gg = gates[gb + 2 * d.D];
+        g_og = gates[gb + 3 * d.D];
+        g_c = c_all[((long long)cb * d.S + t) * d.D + cj];
+        g_cp = c_all[((long long)cb * d.S + t - 1) * d.D + cj];
+      }
+    }
     PB_WAIT();
+    PD_TR(58);
     if (fact && t > 0) {
       for (int i = tid; i < KW * C; i += PD_THREADS) {
         const int row = i / C, c = i % C, tt = tt0 - half + row;
-        L[G.dFw + i] = (tt >= 0 && tt < d.T) ? pd_ld(rf, ((long long)be * d.T + tt) * d.C + c) : 0.f;
+        L[G.un + i] = (tt >= 0 && tt < d.T) ? pd_ld(rf, ((long long)be * d.T + tt) * d.C + c) : 0.f;
       }
     }
     for (int i = tid; i < PD_SLOTS * d.A; i += PD_THREADS) {   // dWd_t of the 4 utterances
@@ -1878,13 +2010,14 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
       L[G.dwdl + i] = s;
     }
     __syncthreads();
+    PD_TR(59);
     if (fact && t > 0) {
       // d aw_{t-1}[j] = sum_c sum_k dF[j - k + half, c] cw[c, k]: one (frame, channel) per thread
       float* cp = &L[G.cmb];
       for (int i = tid; i < FCH * C; i += PD_THREADS) {
         const int fi = i / C, c = i % C;
         float s = 0.f;
-        if (fi < nfr) s = dot_lds(&L[G.dFw + (fi + d.K - 1) * C + c], -C, &L[G.cw + c * d.K], 1, d.K);
+        if (fi < nfr) s = dot_lds(&L[G.un + (fi + d.K - 1) * C + c], -C, &L[G.cw + c * d.K], 1, d.K);
         cp[i] = s;
       }
       // conv-kernel partial: dcw[c, k] += sum_{own frames} dF[tt, c] aw_{t-1}[tt + k - half]
@@ -1893,15 +2026,35 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
         const int i = tid + j * PD_THREADS;
         if (i < d.C * d.K) {
           const int c = i / d.K, k = i % d.K;
-          dcwacc[j] += dot_lds(&L[G.dFw + half * C + c], C, &L[G.awin + k], 1, nfr);
+          dcwacc[j] += dot_lds(&L[G.un + half * C + c], C, &L[G.awin + k], 1, nfr);
         }
       }
     }
+    // d dec from the attention, W_dec^T dWd_t over this member's units:
+    // (slot, unit, eighth of A) per thread, eighths summed in order
+    float* ddp = &L[G.un + KW * C];
+    {
+      const int np = PD_SLOTS * UPW * 8;
+      const int a8 = (d.A + 7) / 8;
+      for (int i = tid; i < np; i += PD_THREADS) {
+        const int su = i >> 3, e8 = i & 7, sl = su / UPW, u = su % UPW;
+        const int a0 = e8 * a8, a1 = min(d.A, a0 + a8);
+        float s0 = 0.f, s1 = 0.f;
+        int a = a0;
+        for (; a + 1 < a1; a += 2) {
+          s0 += L[G.wdl + a * UPW + u] * L[G.dwdl + sl * d.A + a];
+          s1 += L[G.wdl + (a + 1) * UPW + u] * L[G.dwdl + sl * d.A + a + 1];
+        }
+        if (a < a1) s0 += L[G.wdl + a * UPW + u] * L[G.dwdl + sl * d.A + a];
+        ddp[i] = s0 + s1;
+      }
+    }
+    __syncthreads();
     if (cown) {
       float dd = 0.f;
-      for (int a = 0; a < d.A; ++a) dd += L[G.wdl + a * UPW + cu] * L[G.dwdl + csl * d.A + a];
-      const float dh = d_dec_in[((long long)cb * d.S + t) * d.D + cj] +
-                       (has_r ? pd_ld(rr, (long long)cb * ED + d.E + cj) : 0.f) + dd;
+#pragma unroll
+      for (int e8 = 0; e8 < 8; ++e8) dd += ddp[tid * 8 + e8];
+      const float dh = g_dh + dd;
       if (t == 0) {
         if (d_h0) d_h0[(long long)cb * d.D + cj] = dh;
       } else {
@@ -1909,10 +2062,7 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
             drop_h > 0.f ? dh * drop_scale(drop_h, seed_h, ((unsigned long long)cb * d.S + t) * d.D + cj)
                          : dh;
         const long long gb = ((long long)cb * d.S + t) * G4 + cj;
-        const float ig = gates[gb], fg = gates[gb + d.D], gg = gates[gb + 2 * d.D],
-                    og = gates[gb + 3 * d.D];
-        const float c = c_all[((long long)cb * d.S + t) * d.D + cj];
-        const float cprev = c_all[((long long)cb * d.S + t - 1) * d.D + cj];
+        const float ig = g_ig, fg = g_fg, gg = g_gg, og = g_og, c = g_c, cprev = g_cp;
         const float tc = tanhf(c);
         const float dcell = dc_reg + dhr * og * (1.f - tc * tc);
         pd_st(rg, gb, dcell * gg * ig * (1.f - ig));
@@ -1930,7 +2080,9 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
         L[G.carry + i] = s;
       }
     }
+    PD_TR(60);
     PB_PUBLISH();
+    PD_TR(61);
   }
 #undef PB_WAIT
 #undef PB_PUBLISH

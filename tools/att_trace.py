@@ -43,3 +43,8 @@ ph('persist_fwd C', [32, 33, 34, 35, 36, 37])
 ph('persist_fwd E', [37, 38, 39, 40, 41, 42])
 ph('persist_fwd X', [42, 43, 44, 45, 46])
 ph('persist_fwd step', [32, 37, 42, 46])
+ph('persist_bwd H', [48, 49, 50, 51])
+ph('persist_bwd E', [51, 52, 53, 54])
+ph('persist_bwd F', [54, 55, 56, 57])
+ph('persist_bwd G', [57, 58, 59, 60, 61])
+ph('persist_bwd step', [48, 51, 54, 57, 61])
