@@ -1139,13 +1139,14 @@ constexpr int PD_KMAX = 16;      // K blocks of 32 per wave: E + D <= 1024
 constexpr int PD_UMAX = 12;      // hidden units per member: 4 UPW <= 48 rows (3 MFMA tiles)
 constexpr int PD_FPW = 8;        // frames per wave: FCH <= 64
 constexpr int PD_CTR = 64;       // ints per counter (own 256-B line)
+constexpr int PD_CM = 4;         // conv channels of the generic instantiations (C <= 4)
 constexpr unsigned PD_SPIN_LIMIT = 1u << 20;
 
 typedef __attribute__((address_space(1))) int pd_gint;
 typedef __attribute__((ext_vector_type(4))) unsigned int pd_u32x4;
 
 struct PdGeom {
-  int UPW, FCH, ECW, ED, NKB, half;
+  int UPW, FCH, ECW, ED, NKB, half, FS;
   int xs, wdl, cw, wc, v, awp, wd, wq, f, hs, part, red, cpart, mp, encs, total;   // LDS floats
 };
 
@@ -1166,7 +1167,9 @@ __host__ __device__ inline PdGeom pd_geom(const Dims& d) {
   g.awp = o; o += d.T + 2 * g.half + 16;
   g.wd = o; o += d.A;
   g.wq = o; o += 4 * d.A;
-  g.f = o; o += g.FCH * d.C;
+  o = (o + 3) & ~3;
+  g.FS = (d.C + 3) & ~3;
+  g.f = o; o += g.FCH * g.FS;
   g.hs = o; o += PD_SLOTS * PD_UMAX;
   g.part = o; o += 6 * PD_SLOTS * 16;
   g.red = o; o += 64;
@@ -1185,7 +1188,7 @@ __host__ __device__ inline PdGeom pd_geom(const Dims& d) {
 // window load and one kernel load per lane per 4 taps, against two LDS loads
 // per tap of a dot-product loop.
 __device__ __forceinline__ void pd_conv_feat(const float* cw, const float* win, int C, int K,
-                                             int FCH, float* part, float* f) {
+                                             int FCH, float* part, float* f, int fs) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int MT = FCH <= 16 ? 1 : FCH <= 32 ? 2 : 4;
   const int KP = 8 / MT;
@@ -1209,10 +1212,11 @@ __device__ __forceinline__ void pd_conv_feat(const float* cw, const float* win, 
 #pragma unroll
   for (int r = 0; r < 4; ++r) part[(wave * 16 + 4 * (lane >> 4) + r) * 16 + col] = acc[r];
   __syncthreads();
-  for (int i = threadIdx.x; i < FCH * C; i += blockDim.x) {
-    const int fi = i / C, c = i % C, tl = fi >> 4, rr = fi & 15;
+  for (int i = threadIdx.x; i < FCH * fs; i += blockDim.x) {   // rows padded to fs (zeros)
+    const int fi = i / fs, c = i % fs, tl = fi >> 4, rr = fi & 15;
     float v = 0.f;
-    for (int q = 0; q < KP; ++q) v += part[((q * MT + tl) * 16 + rr) * 16 + c];
+    if (c < C)
+      for (int q = 0; q < KP; ++q) v += part[((q * MT + tl) * 16 + rr) * 16 + c];
     f[i] = v;
   }
 }
@@ -1221,7 +1225,7 @@ __device__ __forceinline__ void pd_conv_feat(const float* cw, const float* win, 
 // tanh; |error| ~1e-7, the per-step kernels use libm tanhf)
 __device__ __forceinline__ float pd_tanh(float x) {
   const float e = __expf(2.f * fminf(fmaxf(x, -15.f), 15.f));
-  return 1.f - 2.f / (e + 1.f);
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f);
 }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t pd_rsrc(const void* p, unsigned bytes) {
@@ -1265,10 +1269,12 @@ __device__ __forceinline__ void pd_publish(int* ctr) {
       g_att_tr[k] = __builtin_amdgcn_s_memrealtime();                            \
   } while (0)
 
-// NQ: 64-lane groups of the attention dim (A <= 64 NQ)
-template <int CC, int NQ>
+// NQ: 64-lane groups of the attention dim (A <= 64 NQ).  SA, SE, SD, SK: the
+// attention / encoder / decoder dims and the conv width fixed at compile time
+// (0 = from Dims): the production instantiation folds its whole geometry.
+template <int CC, int NQ, int SA, int SE, int SD, int SK>
 __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
-    Dims d, const uint16_t* __restrict__ wcat, const float* __restrict__ pre_emb,
+    Dims dd, const uint16_t* __restrict__ wcat, const float* __restrict__ pre_emb,
     const float* __restrict__ h0, const float* __restrict__ enc, const float* __restrict__ enc_a,
     const int32_t* __restrict__ lens, const float* __restrict__ w_dec,
     const float* __restrict__ w_conv, const float* __restrict__ conv_w,
@@ -1277,6 +1283,12 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
     float* __restrict__ aw_all, float* pbuf, float* ebuf, int* ctr, int* status, float drop_h,
     unsigned long long seed_h) {
   extern __shared__ __attribute__((aligned(16))) float L[];
+  Dims d = dd;
+  if (CC) d.C = CC;
+  if (SA) d.A = SA;
+  if (SE) d.E = SE;
+  if (SD) d.D = SD;
+  if (SK) d.K = SK;
   __shared__ int s_ok;
   const PdGeom G = pd_geom(d);
   const int UPW = G.UPW, FCH = G.FCH, ECW = G.ECW, ED = G.ED, NKB = G.NKB, half = G.half;
@@ -1297,7 +1309,7 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
   const int tt0 = ch * FCH, nfr = max(0, min(FCH, d.T - tt0));
   const int e0 = ch * ECW, ecn = max(0, min(ECW, d.E - e0));
   const int len = fact ? lens[be] : 0;
-  constexpr int CM = CC ? CC : 16;
+  constexpr int CM = CC ? CC : PD_CM;
   const int C = CC ? CC : d.C;
 
   // ---- once per pass: weights and the utterance's constant rows
@@ -1323,6 +1335,15 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
       const int a = lane + 64 * q;
       ea[f][q] = (fact && i < nfr && a < d.A) ? enc_a[((long long)be * d.T + tt) * d.A + a] : 0.f;
     }
+  }
+  constexpr int CM4 = (CM + 3) / 4;
+  float wcr[NQ][CM], vr[NQ];   // this lane's attention units' W_conv rows and V
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int a = lane + 64 * q;
+    vr[q] = a < d.A ? vw[a] : 0.f;
+#pragma unroll
+    for (int c = 0; c < CM; ++c) wcr[q][c] = (a < d.A && (CC || c < C)) ? w_conv[a * C + c] : 0.f;
   }
   for (int i = tid; i < d.A * UPW; i += PD_THREADS) {
     const int a = i / UPW, u = i % UPW;
@@ -1413,7 +1434,7 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
         L[G.hs + csl * PD_UMAX + cu] = h;   // absent (slot, unit) entries stay 0 from t = 0
       }
     } else {
-      for (int i = tid; i < FCH * C; i += PD_THREADS) L[G.f + i] = 0.f;   // aw_{-1} = 0
+      for (int i = tid; i < FCH * G.FS; i += PD_THREADS) L[G.f + i] = 0.f;   // aw_{-1} = 0
       if (tid < PD_SLOTS * PD_UMAX) {
         const int sl = tid / PD_UMAX, u = tid % PD_UMAX, bb = grp + PD_GROUPS * sl;
         L[G.hs + tid] = (h0 && u < nu && bb < d.B) ? h0[(long long)bb * d.D + u0 + u] : 0.f;
@@ -1431,7 +1452,7 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
     pd_publish(my_ctr);
     PD_TR(37);
     // conv features of aw_{t-1} for this chunk (local data: before the wait)
-    if (fact && t > 0) pd_conv_feat(&L[G.cw], &L[G.awp + tt0], C, d.K, FCH, &L[G.mp], &L[G.f]);
+    if (fact && t > 0) pd_conv_feat(&L[G.cw], &L[G.awp + tt0], C, d.K, FCH, &L[G.mp], &L[G.f], G.FS);
 
     // ================= E: energies of this work-group's frame chunk =================
     if (tid == 0) s_ok = pd_wait(my_ctr, PD_MEMBERS * (3 * t + 1), ctr, status);
@@ -1464,9 +1485,16 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
         const int i = wave + 8 * f;
         sf[f] = 0.f;
         if (i < nfr) {   // wave-uniform
-          float frv[CM];
+          float frv[CM4 * 4];
 #pragma unroll
-          for (int c = 0; c < CM; ++c) frv[c] = (CC || c < C) ? L[G.f + i * C + c] : 0.f;
+          for (int c4 = 0; c4 < CM4; ++c4) {
+            const float4 v4 = 4 * c4 < G.FS ? *reinterpret_cast<const float4*>(&L[G.f + i * G.FS + 4 * c4])
+                                            : make_float4(0.f, 0.f, 0.f, 0.f);
+            frv[4 * c4] = v4.x;
+            frv[4 * c4 + 1] = v4.y;
+            frv[4 * c4 + 2] = v4.z;
+            frv[4 * c4 + 3] = v4.w;
+          }
 #pragma unroll
           for (int q = 0; q < NQ; ++q) {
             const int a = lane + 64 * q;
@@ -1474,8 +1502,8 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
               float p = ea[f][q] + L[G.wd + a];
 #pragma unroll
               for (int c = 0; c < CM; ++c)
-                if (CC || c < C) p += frv[c] * L[G.wc + a * C + c];
-              sf[f] += L[G.v + a] * pd_tanh(p);
+                if (CC || c < C) p += frv[c] * wcr[q][c];
+              sf[f] += vr[q] * pd_tanh(p);
             }
           }
         }
@@ -1589,10 +1617,10 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
 // per-step rows, so their f32 summation order differs.
 // ---------------------------------------------------------------------------
 constexpr int PB_KQ = 12;         // K blocks of 32 per wave quarter: 4 D <= 1536
-constexpr int PB_CM = 4;          // conv channels of the generic instantiation (C <= 4)
+constexpr int PB_CM = PD_CM;
 
 struct PbGeom {
-  int UPW, FCH, ECW, ED, G4, NPW, NKB, KQ, half, W;
+  int UPW, FCH, ECW, ED, G4, NPW, NKB, KQ, half, W, FS, AP;
   int encr, ea, cw, wc, v, dct, awin, f, daw, awt, de, carry, wd, un, dgs, part, dwdl, wdl,
       cmb, red, total;   // LDS floats
 };
@@ -1617,7 +1645,9 @@ __host__ __device__ inline PbGeom pb_geom(const Dims& d) {
   g.v = o; o += d.A;
   g.dct = o; o += d.E;
   g.awin = o; o += g.W;
-  g.f = o; o += g.FCH * d.C;
+  o = (o + 3) & ~3;
+  g.FS = (d.C + 3) & ~3;
+  g.f = o; o += g.FCH * g.FS;
   g.daw = o; o += g.FCH;
   g.awt = o; o += g.FCH;
   g.de = o; o += g.FCH;
@@ -1627,7 +1657,8 @@ __host__ __device__ inline PbGeom pb_geom(const Dims& d) {
   {  // one region, used by phase H (bf16 dgates rows [4][G4]), F (the chunk's
      // d enc_a rows) and G (dF window [W][C] + the W_dec^T dWd partials)
     int un = PD_SLOTS * g.G4 / 2 + 4;
-    un = max(un, g.FCH * d.A);
+    g.AP = d.A + 1;   // the [frames][A] tiles' row stride (odd: no bank conflicts down a column)
+    un = max(un, g.FCH * g.AP);
     un = max(un, g.W * d.C + PD_SLOTS * g.UPW * 8);
     un = max(un, 2048);   // E: the conv features' MFMA partial tiles
     g.un = o; o += un;
@@ -1636,15 +1667,15 @@ __host__ __device__ inline PbGeom pb_geom(const Dims& d) {
   g.part = o; o += 8 * PD_SLOTS * 16;
   g.dwdl = o; o += PD_SLOTS * d.A;
   g.wdl = o; o += d.A * g.UPW;
-  g.cmb = o; o += 8 * d.A > 2 * d.A + d.A * d.C ? 8 * d.A : 2 * d.A + d.A * d.C;
+  g.cmb = o; o += max(max(8 * d.A, PD_THREADS), 4 * ((g.FCH + 3) / 4) * 4 * d.C);
   g.red = o; o += 64;
   g.total = (o + 3) & ~3;
   return g;
 }
 
-template <int CC, int NQ>
+template <int CC, int NQ, int SA, int SE, int SD, int SK>
 __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
-    Dims d, const uint16_t* __restrict__ wcatT, const float* __restrict__ enc,
+    Dims dd, const uint16_t* __restrict__ wcatT, const float* __restrict__ enc,
     const float* __restrict__ enc_a, const int32_t* __restrict__ lens,
     const float* __restrict__ w_dec, const float* __restrict__ w_conv,
     const float* __restrict__ conv_w, const float* __restrict__ vw,
@@ -1656,6 +1687,12 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
     float* rbuf, float* sbuf, float* dwdc, float* dFbuf, int* ctr, int* status, float drop_h,
     unsigned long long seed_h) {
   extern __shared__ __attribute__((aligned(16))) float L[];
+  Dims d = dd;
+  if (CC) d.C = CC;
+  if (SA) d.A = SA;
+  if (SE) d.E = SE;
+  if (SD) d.D = SD;
+  if (SK) d.K = SK;
   __shared__ int s_ok;
   __shared__ float s_sdot;
   const PbGeom G = pb_geom(d);
@@ -1718,19 +1755,18 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
     L[G.wdl + i] = u < nu ? w_dec[(long long)a * d.D + u0 + u] : 0.f;
   }
   for (int i = tid; i < FCH; i += PD_THREADS) L[G.carry + i] = 0.f;
-  // register accumulators over the pass: the chunk's dV / dW_conv per lane,
-  // the conv-kernel partial per thread (d enc_a: this work-group's rows of
-  // d_enc_a, zeroed by the host, read-modify-written per step)
-  float accV[NQ];
-  float accWc[NQ][CM];
+  // accumulators over the whole pass: the dV partial of this thread's (unit,
+  // frame group) pairs; the chunk's dW_conv tiles (rows a = (wave + 8 j) 16 ..,
+  // columns c) and conv-kernel tiles (rows c, columns k = (wave + 8 j) 16 ..)
+  // as MFMA accumulators.  d enc_a: this work-group's rows of d_enc_a, zeroed
+  // by the host, read-modify-written per step.
+  const int NG = PD_THREADS / d.A, ta = tid % d.A, fg = tid / d.A;
+  float accVr = 0.f;
+  f32x4 accWcM[NQ / 2], dcwM[2];
 #pragma unroll
-  for (int q = 0; q < NQ; ++q) accV[q] = 0.f;
-#pragma unroll
-  for (int q = 0; q < NQ; ++q)
-#pragma unroll
-    for (int c = 0; c < CM; ++c) accWc[q][c] = 0.f;
-  constexpr int NDCW = 4;   // (c, k) pairs per thread: C K <= 4 * 512
-  float dcwacc[NDCW] = {0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < NQ / 2; ++j) accWcM[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  dcwM[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+  dcwM[1] = f32x4{0.f, 0.f, 0.f, 0.f};
   int nph = 0;
   __syncthreads();
 
@@ -1839,9 +1875,9 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
         }
       }
       __syncthreads();
-      if (t > 0) pd_conv_feat(&L[G.cw], &L[G.awin], C, d.K, FCH, &L[G.un], &L[G.f]);
+      if (t > 0) pd_conv_feat(&L[G.cw], &L[G.awin], C, d.K, FCH, &L[G.un], &L[G.f], G.FS);
       else
-        for (int i = tid; i < FCH * C; i += PD_THREADS) L[G.f + i] = 0.f;
+        for (int i = tid; i < FCH * G.FS; i += PD_THREADS) L[G.f + i] = 0.f;
     }
     PB_WAIT();
     PD_TR(52);
@@ -1881,7 +1917,8 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
     if (fact) {
       const __amdgpu_buffer_rsrc_t ra =
           pd_rsrc(d_enc_a + (long long)be * d.T * d.A, (unsigned)((size_t)d.T * d.A * 4));
-      for (int i = tid; i < nfr * d.A; i += PD_THREADS) L[G.un + i] = pd_ld(ra, (long long)tt0 * d.A + i);
+      for (int i = tid; i < nfr * d.A; i += PD_THREADS)
+        L[G.un + (i / d.A) * G.AP + i % d.A] = pd_ld(ra, (long long)tt0 * d.A + i);
     }
     PB_WAIT();
     PD_TR(55);
@@ -1892,6 +1929,7 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
         if (lane == 0) s_sdot = s;
       }
       __syncthreads();
+      PD_TR(0);
       const float sdot = s_sdot;
       for (int i = tid; i < FCH; i += PD_THREADS) {
         const int tt = tt0 + i;
@@ -1903,67 +1941,103 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
         L[G.de + i] = de;
       }
       __syncthreads();
-      float accWd[NQ];
+      PD_TR(1);
+      // (frame, attention unit) pairs, thread (a = tid % A, frame group tid / A):
+      // tanh backward -> dp, d enc_a; dp tile [FCH][A] over the d enc_a rows
+      if (fg < NG) {
+        float wcr[CM];
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) accWd[q] = 0.f;
-#pragma unroll 1
-      for (int i = wave; i < nfr; i += 8) {
-        const int tt = tt0 + i;
-        const float de = L[G.de + i];
-        const long long fo = ((long long)be * d.T + tt) * d.C;
-        if (de == 0.f) {   // padded / masked frame: nothing flows
-          if (lane < C) pd_st(rf, fo + lane, 0.f);
-          continue;
-        }
-        float* dear = d_enc_a + ((long long)be * d.T + tt) * d.A;
-        const float* deal = &L[G.un + i * d.A];
-        float frv[CM], dfc[CM];
+        for (int c = 0; c < CM; ++c) wcr[c] = (CC || c < C) ? L[G.wc + ta * C + c] : 0.f;
+        const float va = L[G.v + ta], wda = L[G.wd + ta];
+        for (int i = fg; i < FCH; i += NG) {
+          const float de = L[G.de + i];   // 0 beyond nfr
+          float dp = 0.f;
+          if (de != 0.f) {
+            constexpr int CM4 = (CM + 3) / 4;
+            float frv[CM4 * 4];
 #pragma unroll
-        for (int c = 0; c < CM; ++c) {
-          frv[c] = (CC || c < C) ? L[G.f + i * C + c] : 0.f;
-          dfc[c] = 0.f;
-        }
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-          const int a = lane + 64 * q;
-          if (64 * q < d.A) {   // wave-uniform
-            float wrv[CM];
-#pragma unroll
-            for (int c = 0; c < CM; ++c) wrv[c] = (a < d.A && (CC || c < C)) ? L[G.wc + a * C + c] : 0.f;
-            float p = (a < d.A ? L[G.ea + i * d.A + a] + L[G.wd + a] : 0.f);
-#pragma unroll
-            for (int c = 0; c < CM; ++c) p += frv[c] * wrv[c];
-            const float th = pd_tanh(p);
-            const float dp = a < d.A ? de * L[G.v + a] * (1.f - th * th) : 0.f;
-            accV[q] += a < d.A ? de * th : 0.f;
-            accWd[q] += dp;
-            if (a < d.A) dear[a] = deal[a] + dp;
-#pragma unroll
-            for (int c = 0; c < CM; ++c) {
-              accWc[q][c] += dp * frv[c];
-              dfc[c] += dp * wrv[c];
+            for (int c4 = 0; c4 < CM4; ++c4) {
+              const float4 v4 = 4 * c4 < G.FS ? *reinterpret_cast<const float4*>(&L[G.f + i * G.FS + 4 * c4])
+                                              : make_float4(0.f, 0.f, 0.f, 0.f);
+              frv[4 * c4] = v4.x;
+              frv[4 * c4 + 1] = v4.y;
+              frv[4 * c4 + 2] = v4.z;
+              frv[4 * c4 + 3] = v4.w;
             }
-          }
-        }
+            float p = L[G.ea + i * d.A + ta] + wda;
 #pragma unroll
-        for (int c = 0; c < CM; ++c) {
-          if (CC || c < C) {
-            const float sv = wave_sum(dfc[c]);
-            if (lane == 0) pd_st(rf, fo + c, sv);
+            for (int c = 0; c < CM; ++c)
+              if (CC || c < C) p += frv[c] * wcr[c];
+            const float th = pd_tanh(p);
+            dp = de * va * (1.f - th * th);
+            accVr += de * th;
+            d_enc_a[((long long)be * d.T + tt0 + i) * d.A + ta] = L[G.un + i * G.AP + ta] + dp;
           }
+          L[G.un + i * G.AP + ta] = dp;
         }
-      }
-      // the chunk's d W_dec-input sum: per-wave rows combined in wave order
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        const int a = lane + 64 * q;
-        if (a < d.A) L[G.cmb + wave * d.A + a] = accWd[q];
       }
       __syncthreads();
+      PD_TR(2);
+      const int MT = FCH <= 16 ? 1 : FCH <= 32 ? 2 : 4;
+      if (wave < MT) {   // dF [frames][C] = dp . W_conv, one row tile per wave
+        const int row = wave * 16 + (lane & 15), kk = lane >> 4, col = lane & 15;
+        const int nks = (d.A + 3) / 4;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        for (int st = 0; st < nks; st += 4) {
+          float a4[4], b4[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int k = (st + j) * 4 + kk;
+            const bool ok = st + j < nks && k < d.A;
+            a4[j] = (ok && row < FCH) ? L[G.un + row * G.AP + k] : 0.f;
+            b4[j] = (ok && col < C) ? L[G.wc + k * C + col] : 0.f;
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc = mfma_f32(a4[j], b4[j], acc);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = wave * 16 + 4 * (lane >> 4) + r;
+          if (i < nfr && col < C) pd_st(rf, ((long long)be * d.T + tt0 + i) * d.C + col, acc[r]);
+        }
+      }
+      PD_TR(3);
+      // dW_conv [A][C] += dp^T . f (the pass's accumulators)
+#pragma unroll
+      for (int j = 0; j < NQ / 2; ++j) {
+        const int mtile = wave + 8 * j;
+        if (mtile * 16 < d.A) {   // wave-uniform
+          const int arow = mtile * 16 + (lane & 15), kk = lane >> 4, col = lane & 15;
+          const int nks = (FCH + 3) / 4;
+          f32x4 acc = accWcM[j];
+          for (int st = 0; st < nks; st += 4) {
+            float a4[4], b4[4];
+#pragma unroll
+            for (int j2 = 0; j2 < 4; ++j2) {
+              const int i = (st + j2) * 4 + kk;
+              const bool ok = st + j2 < nks && i < FCH;
+              a4[j2] = (ok && arow < d.A) ? L[G.un + i * G.AP + arow] : 0.f;
+              b4[j2] = (ok && col < C) ? L[G.f + i * G.FS + col] : 0.f;
+            }
+#pragma unroll
+            for (int j2 = 0; j2 < 4; ++j2) acc = mfma_f32(a4[j2], b4[j2], acc);
+          }
+          accWcM[j] = acc;
+        }
+      }
+      PD_TR(4);
+      // the chunk's d W_dec-input sum over its frames
       for (int a = tid; a < d.A; a += PD_THREADS) {
-        float s = 0.f;
-        for (int w = 0; w < 8; ++w) s += L[G.cmb + w * d.A + a];
-        pd_st(rw, ((long long)be * PD_CHUNKS + ch) * d.A + a, s);
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+        int i = 0;
+        for (; i + 4 <= FCH; i += 4) {
+          s0 += L[G.un + i * G.AP + a];
+          s1 += L[G.un + (i + 1) * G.AP + a];
+          s2 += L[G.un + (i + 2) * G.AP + a];
+          s3 += L[G.un + (i + 3) * G.AP + a];
+        }
+        for (; i < FCH; ++i) s0 += L[G.un + i * G.AP + a];
+        pd_st(rw, ((long long)be * PD_CHUNKS + ch) * d.A + a, (s0 + s1) + (s2 + s3));
       }
     }
     PD_TR(56);
@@ -2012,24 +2086,76 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
     __syncthreads();
     PD_TR(59);
     if (fact && t > 0) {
-      // d aw_{t-1}[j] = sum_c sum_k dF[j - k + half, c] cw[c, k]: one (frame, channel) per thread
-      float* cp = &L[G.cmb];
-      for (int i = tid; i < FCH * C; i += PD_THREADS) {
-        const int fi = i / C, c = i % C;
-        float s = 0.f;
-        if (fi < nfr) s = dot_lds(&L[G.un + (fi + d.K - 1) * C + c], -C, &L[G.cw + c * d.K], 1, d.K);
-        cp[i] = s;
-      }
-      // conv-kernel partial: dcw[c, k] += sum_{own frames} dF[tt, c] aw_{t-1}[tt + k - half]
+      // d aw_{t-1}[j] = sum_c sum_k dF[j - k + half, c] cw[c, k] (dF window row
+      // j + K - 1 - k): (channel, 4 frames, K quarter) per item with a sliding
+      // 4-row register window -- two LDS loads per 4 products
+      const float* dFw = &L[G.un];
+      float* cp = &L[G.cmb];   // [4 quarters][FCH4][C]
+      const int NJG = (FCH + 3) / 4, FCH4 = NJG * 4, KQ4 = (d.K + 3) / 4;
+      for (int it = tid; it < C * NJG * 4; it += PD_THREADS) {
+        const int kq = it & 3, rest = it >> 2, c = rest % C, jg = rest / C;
+        const int j0 = jg * 4, k0 = kq * KQ4, k1 = min(d.K, k0 + KQ4);
+        float o0 = 0.f, o1 = 0.f, o2 = 0.f, o3 = 0.f;
+        if (j0 < nfr && k0 < k1) {
+          int r = j0 + d.K - 1 - k0;
+          float w0 = dFw[r * C + c], w1 = dFw[(r + 1) * C + c], w2 = dFw[(r + 2) * C + c],
+                w3 = dFw[(r + 3) * C + c];
+          for (int k = k0; k < k1; k += 4) {   // four taps' loads first
+            float cv[4], nw[4];
 #pragma unroll
-      for (int j = 0; j < NDCW; ++j) {
-        const int i = tid + j * PD_THREADS;
-        if (i < d.C * d.K) {
-          const int c = i / d.K, k = i % d.K;
-          dcwacc[j] += dot_lds(&L[G.un + half * C + c], C, &L[G.awin + k], 1, nfr);
+            for (int u = 0; u < 4; ++u) {
+              const int ru = r - 1 - u;
+              cv[u] = k + u < k1 ? L[G.cw + c * d.K + k + u] : 0.f;
+              nw[u] = (k + u < k1 && ru >= 0) ? dFw[ru * C + c] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              if (k + u < k1) {
+                o0 += w0 * cv[u];
+                o1 += w1 * cv[u];
+                o2 += w2 * cv[u];
+                o3 += w3 * cv[u];
+                w3 = w2;
+                w2 = w1;
+                w1 = w0;
+                w0 = nw[u];
+              }
+            }
+            r -= 4;
+          }
+        }
+        float* o = cp + (kq * FCH4 + j0) * C + c;
+        o[0] = o0;
+        o[C] = o1;
+        o[2 * C] = o2;
+        o[3 * C] = o3;
+      }
+      PD_TR(10);
+      // conv-kernel tiles: dcw[c][k] += sum_{own frames} dF[i][c] aw_{t-1}[i + k]
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int nt = wave + 8 * jj;
+        if (nt * 16 < d.K) {   // wave-uniform
+          const int crow = lane & 15, kk = lane >> 4, kcol = nt * 16 + (lane & 15);
+          const int nks = (FCH + 3) / 4;
+          f32x4 acc = dcwM[jj];
+          for (int st = 0; st < nks; st += 4) {
+            float a4[4], b4[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int i = (st + j) * 4 + kk;
+              const bool ok = st + j < nks && i < nfr;
+              a4[j] = (ok && crow < C) ? dFw[(half + i) * C + crow] : 0.f;
+              b4[j] = (ok && kcol < d.K) ? L[G.awin + i + kcol] : 0.f;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc = mfma_f32(a4[j], b4[j], acc);
+          }
+          dcwM[jj] = acc;
         }
       }
     }
+    PD_TR(11);
     // d dec from the attention, W_dec^T dWd_t over this member's units:
     // (slot, unit, eighth of A) per thread, eighths summed in order
     float* ddp = &L[G.un + KW * C];
@@ -2050,6 +2176,7 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
       }
     }
     __syncthreads();
+    PD_TR(12);
     if (cown) {
       float dd = 0.f;
 #pragma unroll
@@ -2072,11 +2199,15 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
         dc_reg = dcell * fg;
       }
     }
+    PD_TR(13);
     __syncthreads();
+    PD_TR(14);
     if (fact && t > 0) {
+      const int FCH4 = ((FCH + 3) / 4) * 4;
       for (int i = tid; i < FCH; i += PD_THREADS) {
         float s = 0.f;
-        for (int c = 0; c < C; ++c) s += L[G.cmb + i * C + c];
+        for (int kq = 0; kq < 4; ++kq)
+          for (int c = 0; c < C; ++c) s += L[G.cmb + (kq * FCH4 + i) * C + c];
         L[G.carry + i] = s;
       }
     }
@@ -2090,31 +2221,33 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
   // ---- end of pass: the chunk's weight-gradient partial rows
   if (!fact) return;
   const long long row = (long long)be * PD_CHUNKS + ch;
-#pragma unroll
-  for (int j = 0; j < NDCW; ++j) {
-    const int i = tid + j * PD_THREADS;
-    if (i < d.C * d.K) dcw_part[row * d.C * d.K + i] = dcwacc[j];
-  }
   float* cV = &L[G.cmb];
-  float* cWc = cV + d.A;
   __syncthreads();
-  for (int pass = 0; pass < 8; ++pass) {
-    if (wave == pass) {
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        const int a = lane + 64 * q;
-        if (a < d.A) {
-          cV[a] = pass ? cV[a] + accV[q] : accV[q];
-#pragma unroll
-          for (int c = 0; c < CM; ++c)
-            if (CC || c < C) cWc[a * C + c] = pass ? cWc[a * C + c] + accWc[q][c] : accWc[q][c];
-        }
-      }
-    }
-    __syncthreads();
+  if (fg < NG) cV[fg * d.A + ta] = accVr;
+  __syncthreads();
+  for (int a = tid; a < d.A; a += PD_THREADS) {
+    float s = 0.f;
+    for (int q = 0; q < NG; ++q) s += cV[q * d.A + a];
+    dv_part[row * d.A + a] = s;
   }
-  for (int i = tid; i < d.A; i += PD_THREADS) dv_part[row * d.A + i] = cV[i];
-  for (int i = tid; i < d.A * d.C; i += PD_THREADS) dwc_part[row * d.A * d.C + i] = cWc[i];
+#pragma unroll
+  for (int j = 0; j < NQ / 2; ++j) {
+    const int mtile = wave + 8 * j;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int a = mtile * 16 + 4 * (lane >> 4) + r, c = lane & 15;
+      if (a < d.A && c < C) dwc_part[row * d.A * d.C + a * d.C + c] = accWcM[j][r];
+    }
+  }
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj) {
+    const int nt = wave + 8 * jj;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int c = 4 * (lane >> 4) + r, k = nt * 16 + (lane & 15);
+      if (c < C && k < d.K) dcw_part[row * d.C * d.K + c * d.K + k] = dcwM[jj][r];
+    }
+  }
 }
 
 }  // namespace
@@ -2136,8 +2269,17 @@ int device_cus() {
 // The persistent forward pass takes a shape when its work split fits (see the
 // kernel's comment) and the 256-work-group grid is co-resident, one per CU.
 // ASR_ATT_PERSIST=0 keeps the per-step kernels (A/B).
-// the production instantiation: 10 conv channels, A <= 128
-bool pd_ten(const Dims& d) { return d.C == 10 && d.A <= 128; }
+// the instantiations: 2 = the production shape folded at compile time (10
+// channels x 201, A 128, E 640, D 320), 1 = 10 channels with A <= 128, 0 =
+// generic (C <= 4)
+int pd_kind(const Dims& d) {
+  if (d.C == 10 && d.A == 128 && d.E == 640 && d.D == 320 && d.K == 201) return 2;
+  return d.C == 10 && d.A <= 128 ? 1 : 0;
+}
+bool pd_ten(const Dims& d) { return pd_kind(d) > 0; }
+#define PD_SEL(K, KIND)                                                                    \
+  ((KIND) == 2 ? (const void*)K<10, 2, 128, 640, 320, 201>                                 \
+               : (KIND) == 1 ? (const void*)K<10, 2, 0, 0, 0, 0> : (const void*)K<0, 4, 0, 0, 0, 0>)
 
 bool pd_eligible(const Dims& d) {
   const char* e = getenv("ASR_ATT_PERSIST");
@@ -2145,11 +2287,12 @@ bool pd_eligible(const Dims& d) {
   const PdGeom G = pd_geom(d);
   const size_t lds = (size_t)G.total * 4;
   if (d.B > PD_GROUPS * PD_SLOTS || G.UPW > PD_UMAX || G.ED % 8 != 0 || G.NKB > 2 * PD_KMAX ||
-      G.FCH > 8 * PD_FPW || d.A > 256 || d.C > 16 || G.ECW > PD_THREADS || lds > 160 * 1024 ||
+      G.FCH > 8 * PD_FPW || d.A > 256 || (!pd_ten(d) && d.C > PD_CM) || G.ECW > PD_THREADS ||
+      lds > 160 * 1024 ||
       (size_t)d.B * d.S * G.ED * 4 >= (1ull << 31) || (size_t)d.B * d.T * 4 >= (1ull << 31))
     return false;
   if (device_cus() < PD_GROUPS * PD_MEMBERS) return false;
-  const void* k = pd_ten(d) ? (const void*)attdec_fwd_persist<10, 2> : (const void*)attdec_fwd_persist<0, 4>;
+  const void* k = PD_SEL(attdec_fwd_persist, pd_kind(d));
   if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return false;
   int per_cu = 0;
@@ -2167,12 +2310,12 @@ bool pb_eligible(const Dims& d) {
   const size_t lds = (size_t)G.total * 4;
   if (d.B > PD_GROUPS * PD_SLOTS || G.UPW > PD_UMAX || G.NPW > 32 || G.G4 % 8 != 0 ||
       G.KQ > PB_KQ || G.FCH > 8 * PD_FPW || d.A > 256 || (!pd_ten(d) && d.C > PB_CM) ||
-      d.C * d.K > 4 * PD_THREADS ||
+      d.K > 16 * 16 ||
       lds > 160 * 1024 || (size_t)d.B * d.S * G.G4 * 4 >= (1ull << 31) ||
       (size_t)d.B * d.T * d.C * 4 >= (1ull << 31))
     return false;
   if (device_cus() < PD_GROUPS * PD_MEMBERS) return false;
-  const void* k = pd_ten(d) ? (const void*)attdec_bwd_persist<10, 2> : (const void*)attdec_bwd_persist<0, 4>;
+  const void* k = PD_SEL(attdec_bwd_persist, pd_kind(d));
   if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return false;
   int per_cu = 0;
@@ -2295,13 +2438,14 @@ extern "C" int asr_attdec_forward_ex(const asr_attdec_dims_t* dims, const asr_at
     ASR_CHECK_HIP(hipMemsetAsync(ctr, 0, (size_t)(1 + PD_GROUPS) * PD_CTR * 4, s));
     const size_t lds = (size_t)G.total * 4;
     const dim3 grid(PD_GROUPS * PD_MEMBERS);
-#define ASR_PD(CC, NQ)                                                                            \
-  hipLaunchKernelGGL((attdec_fwd_persist<CC, NQ>), grid, dim3(PD_THREADS), lds, s, d,                 \
+#define ASR_PD(CC, NQ, SA, SE, SD, SK)                                                                            \
+  hipLaunchKernelGGL((attdec_fwd_persist<CC, NQ, SA, SE, SD, SK>), grid, dim3(PD_THREADS), lds, s, d,                 \
                      (const uint16_t*)workspace, pre_emb, h0, enc, enc_a, lens, w_dec, w_conv,   \
                      conv_w, v, dec, c_all, gates, x, ctx_all, aw_all, pbuf, ebuf, ctr,          \
                      lstm_persist_status_word(), drop_h, seed_h)
-    if (pd_ten(d)) ASR_PD(10, 2);
-    else ASR_PD(0, 4);
+    if (pd_kind(d) == 2) ASR_PD(10, 2, 128, 640, 320, 201);
+    else if (pd_kind(d) == 1) ASR_PD(10, 2, 0, 0, 0, 0);
+    else ASR_PD(0, 4, 0, 0, 0, 0);
 #undef ASR_PD
     ASR_LAUNCH_CHECK();
     g_att_last[0] = pd_ten(d) ? 10 : 0;
@@ -2458,14 +2602,15 @@ extern "C" int asr_attdec_backward_ex(const asr_attdec_dims_t* dims, const asr_a
     ASR_CHECK_HIP(hipMemsetAsync(d_enc_a, 0, (size_t)d.B * d.T * d.A * 4, s));
     const size_t lds = (size_t)PG.total * 4;
     const dim3 grid(PD_GROUPS * PD_MEMBERS);
-#define ASR_PB(CC, NQ)                                                                            \
-  hipLaunchKernelGGL((attdec_bwd_persist<CC, NQ>), grid, dim3(PD_THREADS), lds, s, d,                 \
+#define ASR_PB(CC, NQ, SA, SE, SD, SK)                                                                            \
+  hipLaunchKernelGGL((attdec_bwd_persist<CC, NQ, SA, SE, SD, SK>), grid, dim3(PD_THREADS), lds, s, d,                 \
                      (const uint16_t*)wcatT, enc, enc_a, lens, w_dec, w_conv, conv_w, v, c_all,  \
                      aw_all, wd_all, d_dec_in, d_ctx_in, gates_dg, dctx_tot, d_enc_a, d_h0,      \
                      dwd_all, dv_part, dwc_part, dcw_part, r, sbuf, dwd_chunk, dFbuf, ctr,       \
                      lstm_persist_status_word(), drop_h, seed_h)
-    if (pd_ten(d)) ASR_PB(10, 2);
-    else ASR_PB(0, 4);
+    if (pd_kind(d) == 2) ASR_PB(10, 2, 128, 640, 320, 201);
+    else if (pd_kind(d) == 1) ASR_PB(10, 2, 0, 0, 0, 0);
+    else ASR_PB(0, 4, 0, 0, 0, 0);
 #undef ASR_PB
     ASR_LAUNCH_CHECK();
     g_att_last[2] = pd_ten(d) ? 10 : 0;

@@ -13,8 +13,10 @@ rel-L2 5e-3 there.
 
 Shapes: the production one (B 32, T' 250, E 640, A 128, 10 channels x 201,
 D 320: 8 frame chunks of 32, 80 context columns and 10 hidden units per
-work-group) and a small ragged one (B 5, odd T', C = 3: the generic-channel
-instantiation, empty utterance slots and partial chunks).
+work-group; the instantiation with that geometry fixed at compile time), a
+small ragged one (B 5, odd T', C = 3: the generic-channel instantiation, empty
+utterance slots and partial chunks) and a 10-channel one with other dims (the
+runtime-geometry 10-channel instantiation).
 """
 import ctypes
 import os
@@ -28,6 +30,7 @@ pytestmark = pytest.mark.gpu
 SHAPES = {
     'prod': dict(B=32, T=250, E=640, A=128, C=10, K=201, D=320, S=40, Y=32),
     'ragged': dict(B=5, T=61, E=52, A=24, C=3, K=11, D=20, S=7, Y=6),
+    'ten': dict(B=9, T=100, E=96, A=64, C=10, K=21, D=40, S=9, Y=8),
 }
 
 
@@ -131,4 +134,4 @@ def test_persistent_forward_gradients_match(shape, cuda_dev):
     # shape, whose steps carry no flips, agrees to ~3e-7 -- every code path
     # but the 10-channel instantiation's constants is exercised there)
     for name in names:
-        assert errs[name] < (2e-3 if shape == 'prod' else 1e-5), (name, errs[name])
+        assert errs[name] < (2e-3 if shape != 'ragged' else 1e-5), (name, errs[name])
