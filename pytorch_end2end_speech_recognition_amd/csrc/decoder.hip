@@ -1188,7 +1188,7 @@ __host__ __device__ inline PdGeom pd_geom(const Dims& d) {
 // window load and one kernel load per lane per 4 taps, against two LDS loads
 // per tap of a dot-product loop.
 __device__ __forceinline__ void pd_conv_feat(const float* cw, const float* win, int C, int K,
-                                             int FCH, float* part, float* f, int fs) {
+                                             int FCH, float* part, float* f, int fs, int ks) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int MT = FCH <= 16 ? 1 : FCH <= 32 ? 2 : 4;
   const int KP = 8 / MT;
@@ -1204,7 +1204,7 @@ __device__ __forceinline__ void pd_conv_feat(const float* cw, const float* win, 
       const int k = (st + j) * 4 + kk;
       const bool ok = st + j < s1 && k < K;
       a[j] = (ok && row < FCH) ? win[row + k] : 0.f;
-      b[j] = (ok && col < C) ? cw[col * K + k] : 0.f;
+      b[j] = (ok && col < C) ? cw[col * ks + k] : 0.f;
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc = mfma_f32(a[j], b[j], acc);
@@ -1452,7 +1452,8 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
     pd_publish(my_ctr);
     PD_TR(37);
     // conv features of aw_{t-1} for this chunk (local data: before the wait)
-    if (fact && t > 0) pd_conv_feat(&L[G.cw], &L[G.awp + tt0], C, d.K, FCH, &L[G.mp], &L[G.f], G.FS);
+    if (fact && t > 0)
+      pd_conv_feat(&L[G.cw], &L[G.awp + tt0], C, d.K, FCH, &L[G.mp], &L[G.f], G.FS, d.K);
 
     // ================= E: energies of this work-group's frame chunk =================
     if (tid == 0) s_ok = pd_wait(my_ctr, PD_MEMBERS * (3 * t + 1), ctr, status);
@@ -1620,7 +1621,7 @@ constexpr int PB_KQ = 12;         // K blocks of 32 per wave quarter: 4 D <= 153
 constexpr int PB_CM = PD_CM;
 
 struct PbGeom {
-  int UPW, FCH, ECW, ED, G4, NPW, NKB, KQ, half, W, FS, AP;
+  int UPW, FCH, ECW, ED, G4, NPW, NKB, KQ, half, W, FS, AP, KQ4, KP;
   int encr, ea, cw, wc, v, dct, awin, f, daw, awt, de, carry, wd, un, dgs, part, dwdl, wdl,
       cmb, red, total;   // LDS floats
 };
@@ -1640,7 +1641,10 @@ __host__ __device__ inline PbGeom pb_geom(const Dims& d) {
   int o = 0;
   g.encr = o; o += g.FCH * d.E;
   g.ea = o; o += g.FCH * d.A;
-  g.cw = o; o += d.C * d.K;
+  g.KQ4 = 4 * ((d.K + 15) / 16);   // taps per quarter of the conv transpose (multiple of 4)
+  g.KP = 4 * g.KQ4;                 // conv kernel rows padded with zero taps to KP
+  o = (o + 3) & ~3;
+  g.cw = o; o += d.C * g.KP;
   g.wc = o; o += d.A * d.C;
   g.v = o; o += d.A;
   g.dct = o; o += d.E;
@@ -1659,7 +1663,7 @@ __host__ __device__ inline PbGeom pb_geom(const Dims& d) {
     int un = PD_SLOTS * g.G4 / 2 + 4;
     g.AP = d.A + 1;   // the [frames][A] tiles' row stride (odd: no bank conflicts down a column)
     un = max(un, g.FCH * g.AP);
-    un = max(un, g.W * d.C + PD_SLOTS * g.UPW * 8);
+    un = max(un, (8 + g.W) * d.C + PD_SLOTS * g.UPW * 8);   // dF window after 8 zero rows
     un = max(un, 2048);   // E: the conv features' MFMA partial tiles
     g.un = o; o += un;
     g.dgs = g.un;
@@ -1747,7 +1751,10 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
     const int fi = i / d.A, a = i % d.A;
     L[G.ea + i] = (fact && fi < nfr) ? enc_a[((long long)be * d.T + tt0 + fi) * d.A + a] : 0.f;
   }
-  for (int i = tid; i < d.C * d.K; i += PD_THREADS) L[G.cw + i] = conv_w[i];
+  for (int i = tid; i < d.C * G.KP; i += PD_THREADS) {
+    const int c = i / G.KP, k = i % G.KP;
+    L[G.cw + i] = k < d.K ? conv_w[c * d.K + k] : 0.f;
+  }
   for (int i = tid; i < d.A * d.C; i += PD_THREADS) L[G.wc + i] = w_conv[i];
   for (int i = tid; i < d.A; i += PD_THREADS) L[G.v + i] = vw[i];
   for (int i = tid; i < d.A * UPW; i += PD_THREADS) {
@@ -1875,7 +1882,7 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
         }
       }
       __syncthreads();
-      if (t > 0) pd_conv_feat(&L[G.cw], &L[G.awin], C, d.K, FCH, &L[G.un], &L[G.f], G.FS);
+      if (t > 0) pd_conv_feat(&L[G.cw], &L[G.awin], C, d.K, FCH, &L[G.un], &L[G.f], G.FS, G.KP);
       else
         for (int i = tid; i < FCH * G.FS; i += PD_THREADS) L[G.f + i] = 0.f;
     }
@@ -2063,10 +2070,11 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
     }
     PB_WAIT();
     PD_TR(58);
-    if (fact && t > 0) {
-      for (int i = tid; i < KW * C; i += PD_THREADS) {
-        const int row = i / C, c = i % C, tt = tt0 - half + row;
-        L[G.un + i] = (tt >= 0 && tt < d.T) ? pd_ld(rf, ((long long)be * d.T + tt) * d.C + c) : 0.f;
+    if (fact && t > 0) {   // dF window rows [tt0 - half, tt0 + FCH + half) after 8 zero rows
+      for (int i = tid; i < (8 + KW) * C; i += PD_THREADS) {
+        const int row = i / C - 8, c = i % C, tt = tt0 - half + row;
+        L[G.un + i] = (row >= 0 && tt >= 0 && tt < d.T)
+                          ? pd_ld(rf, ((long long)be * d.T + tt) * d.C + c) : 0.f;
       }
     }
     for (int i = tid; i < PD_SLOTS * d.A; i += PD_THREADS) {   // dWd_t of the 4 utterances
@@ -2089,38 +2097,30 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
       // d aw_{t-1}[j] = sum_c sum_k dF[j - k + half, c] cw[c, k] (dF window row
       // j + K - 1 - k): (channel, 4 frames, K quarter) per item with a sliding
       // 4-row register window -- two LDS loads per 4 products
-      const float* dFw = &L[G.un];
+      const float* dFw = &L[G.un + 8 * C];   // row r of the window (rows -8..-1 are zero)
       float* cp = &L[G.cmb];   // [4 quarters][FCH4][C]
-      const int NJG = (FCH + 3) / 4, FCH4 = NJG * 4, KQ4 = (d.K + 3) / 4;
+      const int NJG = (FCH + 3) / 4, FCH4 = NJG * 4, KQ4 = G.KQ4;
       for (int it = tid; it < C * NJG * 4; it += PD_THREADS) {
         const int kq = it & 3, rest = it >> 2, c = rest % C, jg = rest / C;
-        const int j0 = jg * 4, k0 = kq * KQ4, k1 = min(d.K, k0 + KQ4);
+        const int j0 = jg * 4, k0 = kq * KQ4;
         float o0 = 0.f, o1 = 0.f, o2 = 0.f, o3 = 0.f;
-        if (j0 < nfr && k0 < k1) {
+        if (j0 < nfr) {   // taps past K are zero in the padded kernel rows
           int r = j0 + d.K - 1 - k0;
           float w0 = dFw[r * C + c], w1 = dFw[(r + 1) * C + c], w2 = dFw[(r + 2) * C + c],
                 w3 = dFw[(r + 3) * C + c];
-          for (int k = k0; k < k1; k += 4) {   // four taps' loads first
-            float cv[4], nw[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              const int ru = r - 1 - u;
-              cv[u] = k + u < k1 ? L[G.cw + c * d.K + k + u] : 0.f;
-              nw[u] = (k + u < k1 && ru >= 0) ? dFw[ru * C + c] : 0.f;
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              if (k + u < k1) {
-                o0 += w0 * cv[u];
-                o1 += w1 * cv[u];
-                o2 += w2 * cv[u];
-                o3 += w3 * cv[u];
-                w3 = w2;
-                w2 = w1;
-                w1 = w0;
-                w0 = nw[u];
-              }
-            }
+          const float* cwr = &L[G.cw + c * G.KP + k0];
+          for (int k = 0; k < KQ4; k += 4) {   // four taps' loads first, no branches
+            const float4 cv = *reinterpret_cast<const float4*>(cwr + k);
+            const float n0 = dFw[(r - 1) * C + c], n1 = dFw[(r - 2) * C + c],
+                        n2 = dFw[(r - 3) * C + c], n3 = dFw[(r - 4) * C + c];
+            o0 += w0 * cv.x; o1 += w1 * cv.x; o2 += w2 * cv.x; o3 += w3 * cv.x;
+            o0 += n0 * cv.y; o1 += w0 * cv.y; o2 += w1 * cv.y; o3 += w2 * cv.y;
+            o0 += n1 * cv.z; o1 += n0 * cv.z; o2 += w0 * cv.z; o3 += w1 * cv.z;
+            o0 += n2 * cv.w; o1 += n1 * cv.w; o2 += n0 * cv.w; o3 += w0 * cv.w;
+            w0 = n3;
+            w1 = n2;
+            w2 = n1;
+            w3 = n0;
             r -= 4;
           }
         }
@@ -2145,7 +2145,7 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
             for (int j = 0; j < 4; ++j) {
               const int i = (st + j) * 4 + kk;
               const bool ok = st + j < nks && i < nfr;
-              a4[j] = (ok && crow < C) ? dFw[(half + i) * C + crow] : 0.f;
+              a4[j] = (ok && crow < C) ? dFw[(half + i) * C + crow] : 0.f;   // (window base)
               b4[j] = (ok && kcol < d.K) ? L[G.awin + i + kcol] : 0.f;
             }
 #pragma unroll
@@ -2158,7 +2158,7 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
     PD_TR(11);
     // d dec from the attention, W_dec^T dWd_t over this member's units:
     // (slot, unit, eighth of A) per thread, eighths summed in order
-    float* ddp = &L[G.un + KW * C];
+    float* ddp = &L[G.un + (8 + KW) * C];
     {
       const int np = PD_SLOTS * UPW * 8;
       const int a8 = (d.A + 7) / 8;
