@@ -1203,8 +1203,11 @@ __device__ __forceinline__ void pd_conv_feat(const float* cw, const float* win, 
     for (int j = 0; j < 4; ++j) {
       const int k = (st + j) * 4 + kk;
       const bool ok = st + j < s1 && k < K;
-      a[j] = (ok && row < FCH) ? win[row + k] : 0.f;
-      b[j] = (ok && col < C) ? cw[col * ks + k] : 0.f;
+      // unconditional loads at clamped (in-range) indices, then selects: no branches
+      const int kc = min(k, K - 1);
+      const float av = win[min(row, FCH - 1) + kc], bv = cw[min(col, C - 1) * ks + kc];
+      a[j] = (ok && row < FCH) ? av : 0.f;
+      b[j] = (ok && col < C) ? bv : 0.f;
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc = mfma_f32(a[j], b[j], acc);
@@ -1996,8 +1999,11 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
           for (int j = 0; j < 4; ++j) {
             const int k = (st + j) * 4 + kk;
             const bool ok = st + j < nks && k < d.A;
-            a4[j] = (ok && row < FCH) ? L[G.un + row * G.AP + k] : 0.f;
-            b4[j] = (ok && col < C) ? L[G.wc + k * C + col] : 0.f;
+            const int kc = min(k, d.A - 1);
+            const float av = L[G.un + min(row, FCH - 1) * G.AP + kc];
+            const float bv = L[G.wc + kc * C + min(col, C - 1)];
+            a4[j] = (ok && row < FCH) ? av : 0.f;
+            b4[j] = (ok && col < C) ? bv : 0.f;
           }
 #pragma unroll
           for (int j = 0; j < 4; ++j) acc = mfma_f32(a4[j], b4[j], acc);
@@ -2023,8 +2029,11 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
             for (int j2 = 0; j2 < 4; ++j2) {
               const int i = (st + j2) * 4 + kk;
               const bool ok = st + j2 < nks && i < FCH;
-              a4[j2] = (ok && arow < d.A) ? L[G.un + i * G.AP + arow] : 0.f;
-              b4[j2] = (ok && col < C) ? L[G.f + i * G.FS + col] : 0.f;
+              const int ic = min(i, FCH - 1);
+              const float av = L[G.un + ic * G.AP + min(arow, d.A - 1)];
+              const float bv = L[G.f + ic * G.FS + min(col, G.FS - 1)];
+              a4[j2] = (ok && arow < d.A) ? av : 0.f;
+              b4[j2] = (ok && col < C) ? bv : 0.f;
             }
 #pragma unroll
             for (int j2 = 0; j2 < 4; ++j2) acc = mfma_f32(a4[j2], b4[j2], acc);
@@ -2145,8 +2154,11 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
             for (int j = 0; j < 4; ++j) {
               const int i = (st + j) * 4 + kk;
               const bool ok = st + j < nks && i < nfr;
-              a4[j] = (ok && crow < C) ? dFw[(half + i) * C + crow] : 0.f;   // (window base)
-              b4[j] = (ok && kcol < d.K) ? L[G.awin + i + kcol] : 0.f;
+              const int ic = min(i, FCH - 1);
+              const float av = dFw[(half + ic) * C + min(crow, C - 1)];
+              const float bv = L[G.awin + ic + min(kcol, d.K - 1)];
+              a4[j] = (ok && crow < C) ? av : 0.f;
+              b4[j] = (ok && kcol < d.K) ? bv : 0.f;
             }
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc = mfma_f32(a4[j], b4[j], acc);
