@@ -14,6 +14,8 @@
 // blocks.  Register-staged double buffering: the next K tile's global loads are
 // issued before the MFMAs of the current tile and written to LDS after the
 // barrier.  Block ids are remapped so consecutive tiles share an XCD's L2.
+#include <string.h>
+
 #include "mfma.h"
 #include "prof.h"
 
@@ -1744,9 +1746,90 @@ int gemm_launch_own(const asr_gemm_t* problems, int nprob, int compute_dtype, vo
   return ASR_OK;
 }
 
+// bf16 staging of f32 operands.  In bf16 mode a product with an f32 operand
+// (the decoder / bottleneck / attention projections fed by f32 activations)
+// would run on the generic register-staged kernel, converting inside its
+// loads (30-50 TF/s at these shapes).  A product of at least STAGE_FLOPS
+// instead stages each f32 operand once into a dense bf16 copy in the workspace
+// (one convert_rows pass through the operand's row map) and takes the fast /
+// 8-wave kernels; the arithmetic is unchanged (bf16 operands, f32 accumulate).
+// ASR_GEMM_STAGE=0 keeps the generic kernel (A/B).
+constexpr double STAGE_FLOPS = 3.2e7;
+
+struct StagePlan {
+  bool on[2][2];
+  int rows[2][2], cols[2][2], ld[2][2];
+  size_t off[2][2];
+  size_t bytes;
+};
+
+StagePlan plan_stage(const asr_gemm_t* g, int nprob, size_t base) {
+  StagePlan sp{};
+  const char* e = getenv("ASR_GEMM_STAGE");
+  if (e && e[0] == '0') return sp;
+  bool any = false;
+  for (int i = 0; i < nprob; ++i) {
+    if (g[i].batch > 1 || g[i].K % 8 || 2.0 * g[i].M * g[i].N * g[i].K < STAGE_FLOPS) return sp;
+    for (int j = 0; j < 2; ++j) {
+      const asr_operand_t& op = j ? g[i].b : g[i].a;
+      if (op.dtype != ASR_DT_F32) continue;
+      if (op.tap_group) return sp;
+      const int outer = j ? g[i].N : g[i].M;
+      const int cols = op.trans ? outer : g[i].K;
+      if (cols % 8 == 0 && (!aligned16(op.ptr) || op.map.stride_t % 4 || op.map.stride_b % 4))
+        return sp;   // the conversion's vector path needs aligned rows
+      any = true;
+    }
+  }
+  if (!any) return sp;
+  size_t o = base;
+  for (int i = 0; i < nprob; ++i)
+    for (int j = 0; j < 2; ++j) {
+      const asr_operand_t& op = j ? g[i].b : g[i].a;
+      if (op.dtype != ASR_DT_F32) continue;
+      const int outer = j ? g[i].N : g[i].M;
+      sp.on[i][j] = true;
+      sp.rows[i][j] = op.trans ? g[i].K : outer;
+      sp.cols[i][j] = op.trans ? outer : g[i].K;
+      sp.ld[i][j] = (sp.cols[i][j] + 7) / 8 * 8;
+      sp.off[i][j] = o;
+      o += ((size_t)sp.rows[i][j] * sp.ld[i][j] * 2 + 255) & ~(size_t)255;
+    }
+  sp.bytes = o - base;
+  return sp;
+}
+
+size_t split_bytes_aligned(const asr_gemm_t* g, int nprob) {
+  return (plan_split(g, nprob).bytes + 255) & ~(size_t)255;
+}
+
 int gemm_launch(const asr_gemm_t* problems, int nprob, int compute_dtype, void* workspace,
                 size_t ws_bytes, void* stream) {
   ASR_REQUIRE(problems && nprob >= 1 && nprob <= 2, ASR_ERR_ARG, "gemm: nprob must be 1 or 2");
+  if (compute_dtype == ASR_DT_BF16 && workspace) {
+    const size_t base = split_bytes_aligned(problems, nprob);
+    const StagePlan st = plan_stage(problems, nprob, base);
+    if (st.bytes > 0 && ws_bytes >= base + st.bytes) {
+      asr_gemm_t g2[2];
+      for (int i = 0; i < nprob; ++i) {
+        g2[i] = problems[i];
+        for (int j = 0; j < 2; ++j) {
+          if (!st.on[i][j]) continue;
+          asr_operand_t& op = j ? g2[i].b : g2[i].a;
+          uint16_t* dst = (uint16_t*)((char*)workspace + st.off[i][j]);
+          const int rc = asr_convert_rows_bf16_ld((const float*)op.ptr, op.map, st.rows[i][j],
+                                                  st.cols[i][j], st.ld[i][j], dst, stream);
+          if (rc) return rc;
+          op.ptr = dst;
+          op.dtype = ASR_DT_BF16;
+          memset(&op.map, 0, sizeof(op.map));
+          op.map.stride_t = st.ld[i][j];
+          op.bytes = (long long)st.rows[i][j] * st.ld[i][j] * 2;
+        }
+      }
+      return gemm_launch_own(g2, nprob, compute_dtype, workspace, ws_bytes, stream);
+    }
+  }
   return gemm_launch_own(problems, nprob, compute_dtype, workspace, ws_bytes, stream);
 }
 
@@ -1761,13 +1844,16 @@ extern "C" int asr_gemm(const asr_gemm_t* problems, int nprob, int compute_dtype
 
 extern "C" size_t asr_gemm_workspace_bytes(const asr_gemm_t* problems, int nprob) {
   if (!problems || nprob < 1 || nprob > 2) return 0;
-  return plan_split(problems, nprob).bytes;
+  // split-K slabs, then the bf16 staging copies (used in bf16 mode only)
+  const size_t base = split_bytes_aligned(problems, nprob);
+  const size_t stage = plan_stage(problems, nprob, base).bytes;
+  return stage ? base + stage : plan_split(problems, nprob).bytes;
 }
 
 extern "C" int asr_gemm_ws(const asr_gemm_t* problems, int nprob, int compute_dtype,
                            void* workspace, size_t ws_bytes, void* stream) {
-  if (!workspace) ASR_REQUIRE(asr_gemm_workspace_bytes(problems, nprob) == 0, ASR_ERR_WORKSPACE,
-                              "gemm: split-K workspace required");
+  if (!workspace) ASR_REQUIRE(plan_split(problems, nprob).bytes == 0, ASR_ERR_WORKSPACE,
+                              "gemm: split-K workspace required");   // (staging is optional)
   return gemm_launch(problems, nprob, compute_dtype, workspace, ws_bytes, stream);
 }
 

@@ -65,9 +65,10 @@ def test_gemm_split_plan_without_gpu():
     import ctypes
     from pytorch_end2end_speech_recognition_amd import _native as N
 
-    def prob(M, Nn, K):
+    def prob(M, Nn, K, dtype=N.ASR_DT_BF16):
         g = N.Gemm()
         g.M, g.N, g.K, g.batch = M, Nn, K, 1
+        g.a.dtype = g.b.dtype = dtype
         return g
 
     def nbytes(*ps):
@@ -78,6 +79,10 @@ def test_gemm_split_plan_without_gpu():
     assert n >= 2 * 2 * 2048 * 512 * 4
     assert nbytes(prob(32000, 4096, 1024)) == 0
     assert nbytes(prob(300, 29, 123)) == 0
+    # f32 operands of a large enough product get bf16 staging copies (bf16 mode
+    # converts them once and takes the fast kernels): M*K + N*K bf16 elements
+    assert nbytes(prob(4032, 320, 640, N.ASR_DT_F32)) >= (4032 + 320) * 640 * 2
+    assert nbytes(prob(300, 29, 123, N.ASR_DT_F32)) == 0   # too small: generic kernel
 
 
 def test_bad_args_raise_runtime_error():
