@@ -230,14 +230,17 @@ def _plain_ctc(cfg):
             not p.get('fc_list'))
 
 
-def _oracle_loss(cfg, sd, sub):
-    """Dropout-free oracle loss on the sample (torch CPU, autograd-ready)."""
+def _oracle_loss(cfg, sd, sub, bn_training=True):
+    """Dropout-free oracle loss on the sample (torch CPU, autograd-ready);
+    bn_training=False: BatchNorm on its running statistics (eval mode)."""
     from oracle import asr_ref
     p = cfg['params']
     if cfg['model_type'] == 'hierarchical_ctc':
+        # BatchNorm in eval mode (running statistics), as the GPU model's
+        # is_eval=True forward in parity_report
         ocfg = dict(num_layers=p['encoder_num_layers'], num_layers_sub=p['encoder_num_layers_sub'],
                     subsample_list=p['subsample_list'], conv_channels=p['conv_channels'],
-                    poolings=p['poolings'], batch_norm=p['batch_norm'],
+                    poolings=p['poolings'], batch_norm=p['batch_norm'], bn_training=bn_training,
                     main_loss_weight=p['main_loss_weight'], sub_loss_weight=p['sub_loss_weight'])
         loss, _, _ = asr_ref.hierarchical_ctc_loss(sd, ocfg, sub['xs'], sub['ys'], sub['x_lens'],
                                                    sub['y_lens'], sub['ys_sub'],
@@ -278,10 +281,11 @@ def cpu_baseline(cfg, batch, n_utts):
         what = ('the reference CPU modules (packed %d-layer bidirectional nn.LSTM, nn.Linear, '
                 'ctc_loss, clip, Adam; oracle/cpu_path.py)' % p['encoder_num_layers'])
     else:
-        with torch.no_grad():
-            ref_loss = {'f32': float(_oracle_loss(cfg, sd, sub)),
+        with torch.no_grad():   # (eval mode, as the GPU parity forward)
+            ref_loss = {'f32': float(_oracle_loss(cfg, sd, sub, bn_training=False)),
                         'f64': float(_oracle_loss(cfg, {k: v.double() if v.is_floating_point()
-                                                        else v for k, v in sd.items()}, sub))}
+                                                        else v for k, v in sd.items()}, sub,
+                                                  bn_training=False))}
         trainable = {k: v.clone().requires_grad_(v.is_floating_point() and 'running' not in k)
                      for k, v in sd.items()}
         params = [v for k, v in trainable.items() if v.is_floating_point() and 'running' not in k]

@@ -141,7 +141,8 @@ def blstm_encoder(p, prefix, cfg, xs, x_lens, capture_layer=0):
     before projection / subsampling (rnn.py:400-407)."""
     x_lens = np.asarray(x_lens)
     if cfg.get('conv_channels'):
-        xs, x_lens, _ = vgg_front(p, prefix, cfg, xs, x_lens)
+        xs, x_lens, _ = vgg_front(p, prefix, cfg, xs, x_lens,
+                                  training=cfg.get('bn_training', True))
     perm = np.argsort(-x_lens, kind='stable')                 # rnn.py:319-326
     xs = xs[torch.as_tensor(perm)]
     lens = x_lens[perm].astype(np.int64)
