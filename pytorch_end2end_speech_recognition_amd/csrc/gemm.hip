@@ -1386,17 +1386,37 @@ __global__ void splitk_reduce(const float* __restrict__ slab, int ksplit, int M,
 }
 
 // Column sums: partial[chunk][n] = sum over rows of chunk; then ordered final sum.
-__global__ void colsum_partial(const float* __restrict__ g, long long ld, int M, int N,
-                               int rows_per_chunk, float* __restrict__ partial) {
-  const int n = blockIdx.x * 256 + threadIdx.x;
+// One (64-column, row chunk) tile per work-group: 4 waves split the chunk's
+// rows (wave w takes rows w, w + 4, ...), each lane keeps eight rows' loads in
+// flight; the waves' sums are combined in LDS in wave order (deterministic).
+__global__ void __launch_bounds__(256) colsum_partial(const float* __restrict__ g, long long ld,
+                                                      int M, int N, int rows_per_chunk,
+                                                      float* __restrict__ partial) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + lane;
   const int chunk = blockIdx.y;
-  if (n >= N) return;
   const int m0 = chunk * rows_per_chunk, m1 = min(M, m0 + rows_per_chunk);
-  float s = 0.f;
-  for (int m = m0; m < m1; ++m) s += g[(long long)m * ld + n];
-  partial[(long long)chunk * N + n] = s;
+  float s0 = 0.f, s1 = 0.f;
+  if (n < N) {
+    int m = m0 + w;
+    for (; m + 28 < m1; m += 32) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = g[(long long)(m + 4 * j) * ld + n];
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        s0 += v[j];
+        s1 += v[j + 1];
+      }
+    }
+    for (; m < m1; m += 4) s0 += g[(long long)m * ld + n];
+  }
+  red[w][lane] = s0 + s1;
+  __syncthreads();
+  if (w == 0 && n < N)
+    partial[(long long)chunk * N + n] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
-
 __global__ void colsum_final(const float* __restrict__ partial, int nchunk, int N, float alpha,
                              float* __restrict__ out0, float* __restrict__ out1) {
   const int n = blockIdx.x * 256 + threadIdx.x;
@@ -1857,9 +1877,17 @@ extern "C" int asr_gemm_ws(const asr_gemm_t* problems, int nprob, int compute_dt
   return gemm_launch(problems, nprob, compute_dtype, workspace, ws_bytes, stream);
 }
 
+// Row chunks of a column sum: enough (64-column, chunk) work-groups to cover
+// the chip (~512), chunks of >= 64 rows, at most 64 partial rows.
+int colsum_chunks(int M, int N) {
+  const int cblocks = (N + 63) / 64;
+  int nc = max(1, 512 / max(cblocks, 1));
+  nc = min(nc, max(1, M / 64));
+  return min(nc, 64);
+}
+
 extern "C" size_t asr_colsum_workspace_bytes(int M, int N) {
-  const int nchunk = M < 256 ? 1 : min(64, (M + 255) / 256);
-  return (size_t)nchunk * N * sizeof(float);
+  return (size_t)colsum_chunks(M, N) * N * sizeof(float);
 }
 
 extern "C" int asr_colsum_accumulate(const float* g, long long ld, int M, int N, float alpha,
@@ -1867,12 +1895,12 @@ extern "C" int asr_colsum_accumulate(const float* g, long long ld, int M, int N,
                                      void* stream) {
   ASR_REQUIRE(g && out0 && workspace, ASR_ERR_ARG, "colsum: null pointer");
   if (M <= 0 || N <= 0) return ASR_OK;
-  const int nchunk = M < 256 ? 1 : min(64, (M + 255) / 256);
+  const int nchunk = colsum_chunks(M, N);
   ASR_REQUIRE(ws_bytes >= asr_colsum_workspace_bytes(M, N), ASR_ERR_WORKSPACE,
               "colsum: workspace too small");
   const int rpc = (M + nchunk - 1) / nchunk;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(colsum_partial, dim3(ceil_div(N, 256), nchunk), dim3(256), 0, s, g, ld, M, N,
+  hipLaunchKernelGGL(colsum_partial, dim3(ceil_div(N, 64), nchunk), dim3(256), 0, s, g, ld, M, N,
                      rpc, (float*)workspace);
   ASR_LAUNCH_CHECK();
   hipLaunchKernelGGL(colsum_final, dim3(ceil_div(N, 256)), dim3(256), 0, s,
