@@ -141,36 +141,87 @@ struct Pool {
   int To, Fo;     // output extent
 };
 
+// Index math of the element-wise passes: 32-bit (the host checks every extent
+// fits) and per V-channel group, not per element -- 64-bit division per
+// element made these passes ALU-bound (post_bwd 544 us at the first vgg_hier
+// layer against ~60 us of traffic).
+struct PixIdx {
+  int b, to, fo;
+};
+__device__ __forceinline__ PixIdx pix_of(unsigned q, int To, int Fo) {
+  PixIdx p;
+  const unsigned r = q / (unsigned)Fo;
+  p.fo = (int)(q - r * (unsigned)Fo);
+  p.b = (int)(r / (unsigned)To);
+  p.to = (int)(r - (unsigned)p.b * (unsigned)To);
+  return p;
+}
+
+template <int V>
+struct VecF;
+template <>
+struct VecF<1> {
+  float v[1];
+  __device__ __forceinline__ void load(const float* p) { v[0] = *p; }
+  __device__ __forceinline__ void store(float* p) const { *p = v[0]; }
+};
+template <>
+struct VecF<4> {
+  float v[4];
+  __device__ __forceinline__ void load(const float* p) {
+    const float4 x = *reinterpret_cast<const float4*>(p);
+    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+  }
+  __device__ __forceinline__ void store(float* p) const {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+};
+
 // P[b][t'][f'][c] = max over the window of relu(z); slot = argmax in torch's
-// scan order (freq outer, time inner; first maximum wins).
+// scan order (freq outer, time inner; first maximum wins).  V channels per
+// thread (V = 4 when C % 4 == 0).
+template <int V>
 __global__ void post_fwd(const float* __restrict__ z, int B, int T, int F, int C, Pool pl,
                          float* __restrict__ P, uint8_t* __restrict__ slot) {
-  const long long n = (long long)B * pl.To * pl.Fo * C;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    const long long q = i / C;
-    const int fo = (int)(q % pl.Fo);
-    const int to = (int)((q / pl.Fo) % pl.To);
-    const int b = (int)(q / ((long long)pl.Fo * pl.To));
+  const unsigned CV = (unsigned)(C / V);
+  const unsigned n = (unsigned)B * pl.To * pl.Fo * CV;
+  for (unsigned e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+    const unsigned q = e / CV;
+    const int c = (int)(e - q * CV) * V;
+    const PixIdx px = pix_of(q, pl.To, pl.Fo);
+    const long long i = (long long)q * C + c;
+    VecF<V> best;
     if (!pl.pt) {
-      P[i] = fmaxf(z[pad_row(b, to, fo, T, F) * C + c], 0.f);
+      best.load(z + pad_row(px.b, px.to, px.fo, T, F) * C + c);
+#pragma unroll
+      for (int j = 0; j < V; ++j) best.v[j] = fmaxf(best.v[j], 0.f);
+      best.store(P + i);
       continue;
     }
-    float best = -__builtin_huge_valf();
-    int bs = 0;
+    int bs[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      best.v[j] = -__builtin_huge_valf();
+      bs[j] = 0;
+    }
     for (int df = 0; df < pl.pf; ++df) {
-      const int f = fo * pl.pf + df;
+      const int f = px.fo * pl.pf + df;
       if (f >= F) break;
       for (int dt = 0; dt < pl.pt; ++dt) {
-        const int t = to * pl.pt + dt;
+        const int t = px.to * pl.pt + dt;
         if (t >= T) break;
-        const float v = fmaxf(z[pad_row(b, t, f, T, F) * C + c], 0.f);
-        if (v > best) { best = v; bs = df * pl.pt + dt; }
+        VecF<V> x;
+        x.load(z + pad_row(px.b, t, f, T, F) * C + c);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          const float v = fmaxf(x.v[j], 0.f);
+          if (v > best.v[j]) { best.v[j] = v; bs[j] = df * pl.pt + dt; }
+        }
       }
     }
-    P[i] = best;
-    slot[i] = (uint8_t)bs;
+    best.store(P + i);
+#pragma unroll
+    for (int j = 0; j < V; ++j) slot[i + j] = (uint8_t)bs[j];
   }
 }
 
@@ -273,82 +324,109 @@ struct Affine {
 
 // y = dropout(BN(P)); written to the next layer's padded input (bf16 / f32,
 // halo untouched: the caller zeroes it) or, out_flat, to [B][T'][F'][C].
-template <typename TO>
+template <typename TO, int V>
 __global__ void apply_fwd(const float* __restrict__ P, int B, int To, int Fo, int C, Affine af,
                           TO* __restrict__ out, int flat) {
-  const long long n = (long long)B * To * Fo * C;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    float y = P[i];
-    if (af.mean) y = (y - af.mean[c]) * af.rstd[c] * af.gamma[c] + af.beta[c];
-    if (af.drop > 0.f) y *= drop_scale(af.drop, af.seed, (unsigned long long)i);
+  const unsigned CV = (unsigned)(C / V);
+  const unsigned n = (unsigned)B * To * Fo * CV;
+  for (unsigned e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+    const unsigned q = e / CV;
+    const int c = (int)(e - q * CV) * V;
+    const long long i = (long long)q * C + c;
+    VecF<V> y;
+    y.load(P + i);
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      if (af.mean)
+        y.v[j] = (y.v[j] - af.mean[c + j]) * af.rstd[c + j] * af.gamma[c + j] + af.beta[c + j];
+      if (af.drop > 0.f) y.v[j] *= drop_scale(af.drop, af.seed, (unsigned long long)(i + j));
+    }
     long long o = i;
     if (!flat) {
-      const long long q = i / C;
-      const int fo = (int)(q % Fo);
-      const int to = (int)((q / Fo) % To);
-      const int b = (int)(q / ((long long)Fo * To));
-      o = pad_row(b, to, fo, To, Fo) * C + c;
+      const PixIdx px = pix_of(q, To, Fo);
+      o = pad_row(px.b, px.to, px.fo, To, Fo) * C + c;
     }
-    if constexpr (sizeof(TO) == 2) out[o] = f2bf(y);
-    else out[o] = y;
+    if constexpr (sizeof(TO) == 2) {
+#pragma unroll
+      for (int j = 0; j < V; ++j) out[o + j] = f2bf(y.v[j]);
+    } else {
+      y.store(reinterpret_cast<float*>(out) + o);
+    }
   }
 }
 
-// dy (after the dropout mask) of output element i, from the next layer's dX
-// (padded rows, flat = 0) or the encoder's gradient [B][T'][F'][C] (flat = 1).
-__device__ __forceinline__ float dy_at(const float* __restrict__ dnext, long long i, int To,
-                                       int Fo, int C, int flat, float drop,
-                                       unsigned long long seed) {
+// dy (after the dropout mask) of the V elements at (pooled pixel q, channel c),
+// from the next layer's dX (padded rows, flat = 0) or the encoder's gradient
+// [B][T'][F'][C] (flat = 1).
+template <int V>
+__device__ __forceinline__ VecF<V> dy_at(const float* __restrict__ dnext, unsigned q, int c,
+                                         int To, int Fo, int C, int flat, float drop,
+                                         unsigned long long seed) {
+  const long long i = (long long)q * C + c;
   long long o = i;
   if (!flat) {
-    const int c = (int)(i % C);
-    const long long q = i / C;
-    const int fo = (int)(q % Fo);
-    const int to = (int)((q / Fo) % To);
-    const int b = (int)(q / ((long long)Fo * To));
-    o = pad_row(b, to, fo, To, Fo) * C + c;
+    const PixIdx px = pix_of(q, To, Fo);
+    o = pad_row(px.b, px.to, px.fo, To, Fo) * C + c;
   }
-  float g = dnext[o];
-  if (drop > 0.f) g *= drop_scale(drop, seed, (unsigned long long)i);
+  VecF<V> g;
+  g.load(dnext + o);
+  if (drop > 0.f) {
+#pragma unroll
+    for (int j = 0; j < V; ++j) g.v[j] *= drop_scale(drop, seed, (unsigned long long)(i + j));
+  }
   return g;
 }
 
 // partial[chunk][c] = sum dy, partial[chunk][C + c] = sum dy * xhat over the
-// chunk's rows (row phases as col_moment)
+// chunk's rows: thread (channel group, row phase), V channels per thread,
+// row phases combined in LDS in order
+template <int V>
 __global__ void __launch_bounds__(CT) bn_bwd_moments(const float* __restrict__ dnext,
                                                      const float* __restrict__ P, int B, int To,
                                                      int Fo, int C, int flat, Affine af,
                                                      long long rows_per,
                                                      float* __restrict__ partial) {
-  __shared__ float red[2 * CT];
+  __shared__ float red[2 * CT * V];
   const long long n = (long long)B * To * Fo;
   const long long r0 = (long long)blockIdx.x * rows_per;
   const long long r1 = min(n, r0 + rows_per);
   const int tid = threadIdx.x;
-  const int ph = CT / C, c = tid % C, q = tid / C;
-  float s1 = 0.f, s2 = 0.f;
+  const int CV = C / V, ph = CT / CV, cg = tid % CV, q = tid / CV, c = cg * V;
+  float s1[V], s2[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) s1[j] = s2[j] = 0.f;
   if (q < ph) {
-    const float m = af.mean[c], rs = af.rstd[c];
+    float m[V], rs[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      m[j] = af.mean[c + j];
+      rs[j] = af.rstd[c + j];
+    }
     for (long long r = r0 + q; r < r1; r += ph) {
-      const long long i = r * C + c;
-      const float g = dy_at(dnext, i, To, Fo, C, flat, af.drop, af.seed);
-      s1 += g;
-      s2 += g * (P[i] - m) * rs;
+      const VecF<V> g = dy_at<V>(dnext, (unsigned)r, c, To, Fo, C, flat, af.drop, af.seed);
+      VecF<V> x;
+      x.load(P + r * C + c);
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        s1[j] += g.v[j];
+        s2[j] += g.v[j] * (x.v[j] - m[j]) * rs[j];
+      }
     }
   }
-  red[tid] = s1;
-  red[CT + tid] = s2;
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    red[(q * CV + cg) * V + j] = s1[j];          // == red[q * C + c + j]
+    red[CT * V + (q * CV + cg) * V + j] = s2[j];
+  }
   __syncthreads();
-  if (tid < C) {
+  for (int cc = tid; cc < C; cc += CT) {
     float t1 = 0.f, t2 = 0.f;
-    for (int j = 0; j < ph; ++j) {
-      t1 += red[j * C + tid];
-      t2 += red[CT + j * C + tid];
+    for (int jq = 0; jq < ph; ++jq) {
+      t1 += red[jq * C + cc];
+      t2 += red[CT * V + jq * C + cc];
     }
-    partial[((long long)blockIdx.x * 2) * C + tid] = t1;
-    partial[((long long)blockIdx.x * 2 + 1) * C + tid] = t2;
+    partial[((long long)blockIdx.x * 2) * C + cc] = t1;
+    partial[((long long)blockIdx.x * 2 + 1) * C + cc] = t2;
   }
 }
 
@@ -363,36 +441,45 @@ __global__ void bn_bwd_finalize(const float* __restrict__ sums, int C, float* __
 
 // dP = BN backward (or dy without BN); routed to the pooled-from pixel if its
 // conv output was positive (ReLU), written into dZ [padded pixels][C] (TO).
-template <typename TO>
+template <typename TO, int V>
 __global__ void post_bwd(const float* __restrict__ dnext, const float* __restrict__ P,
                          const float* __restrict__ z, const uint8_t* __restrict__ slot, int B,
                          int T, int F, int C, Pool pl, int flat, Affine af,
                          const float* __restrict__ sums, TO* __restrict__ dz) {
-  const long long nr = (long long)B * pl.To * pl.Fo;
-  const long long n = nr * C;
+  const unsigned nr = (unsigned)B * pl.To * pl.Fo;
+  const unsigned CV = (unsigned)(C / V);
+  const unsigned n = nr * CV;
   const float inv_n = 1.f / (float)nr;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    float g = dy_at(dnext, i, pl.To, pl.Fo, C, flat, af.drop, af.seed);
+  for (unsigned e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+    const unsigned q = e / CV;
+    const int c = (int)(e - q * CV) * V;
+    const long long i = (long long)q * C + c;
+    VecF<V> g = dy_at<V>(dnext, q, c, pl.To, pl.Fo, C, flat, af.drop, af.seed);
     if (af.mean) {
-      const float xh = (P[i] - af.mean[c]) * af.rstd[c];
-      g = af.gamma[c] * af.rstd[c] * (g - sums[c] * inv_n - xh * sums[C + c] * inv_n);
+      VecF<V> x;
+      x.load(P + i);
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const int cj = c + j;
+        const float xh = (x.v[j] - af.mean[cj]) * af.rstd[cj];
+        g.v[j] = af.gamma[cj] * af.rstd[cj] *
+                 (g.v[j] - sums[cj] * inv_n - xh * sums[C + cj] * inv_n);
+      }
     }
-    const long long q = i / C;
-    const int fo = (int)(q % pl.Fo);
-    const int to = (int)((q / pl.Fo) % pl.To);
-    const int b = (int)(q / ((long long)pl.Fo * pl.To));
-    int t = to, f = fo;
-    if (pl.pt) {
-      const int s = slot[i];
-      t = to * pl.pt + s % pl.pt;
-      f = fo * pl.pf + s / pl.pt;
+    const PixIdx px = pix_of(q, pl.To, pl.Fo);
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      int t = px.to, f = px.fo;
+      if (pl.pt) {
+        const int sl = slot[i + j];
+        t = px.to * pl.pt + sl % pl.pt;
+        f = px.fo * pl.pf + sl / pl.pt;
+      }
+      const long long p = pad_row(px.b, t, f, T, F) * C + c + j;
+      const float v = z[p] > 0.f ? g.v[j] : 0.f;
+      if constexpr (sizeof(TO) == 2) dz[p] = f2bf(v);
+      else dz[p] = v;
     }
-    const long long p = pad_row(b, t, f, T, F) * C + c;
-    const float v = z[p] > 0.f ? g : 0.f;
-    if constexpr (sizeof(TO) == 2) dz[p] = f2bf(v);
-    else dz[p] = v;
   }
 }
 
@@ -631,7 +718,15 @@ extern "C" int asr_vgg_block_forward(const float* z, int B, int T, int F, int C,
               "vgg_block_forward: channels %d must divide %d", C, CT);
   hipStream_t s = (hipStream_t)stream;
   const long long nr = (long long)B * pl.To * pl.Fo;
-  hipLaunchKernelGGL(post_fwd, dim3(grid_for(nr * C)), dim3(CT), 0, s, z, B, T, F, C, pl, P, slot);
+  ASR_REQUIRE((long long)B * (T + 2) * (F + 2) * C < (1LL << 31), ASR_ERR_UNSUPPORTED,
+              "vgg_block_forward: layer too large for 32-bit element indices");
+  const bool v4 = C % 4 == 0;
+  if (v4)
+    hipLaunchKernelGGL(post_fwd<4>, dim3(grid_for(nr * C / 4)), dim3(CT), 0, s, z, B, T, F, C, pl,
+                       P, slot);
+  else
+    hipLaunchKernelGGL(post_fwd<1>, dim3(grid_for(nr * C)), dim3(CT), 0, s, z, B, T, F, C, pl, P,
+                       slot);
   ASR_LAUNCH_CHECK();
   Affine af{nullptr, nullptr, nullptr, nullptr, drop, seed};
   if (gamma) {
@@ -665,12 +760,22 @@ extern "C" int asr_vgg_block_forward(const float* z, int B, int T, int F, int C,
     af.gamma = gamma;
     af.beta = beta;
   }
-  if (out_dtype == ASR_DT_BF16 && !flat)
-    hipLaunchKernelGGL((apply_fwd<uint16_t>), dim3(grid_for(nr * C)), dim3(CT), 0, s, P, B,
-                       pl.To, pl.Fo, C, af, (uint16_t*)out, 0);
-  else
-    hipLaunchKernelGGL((apply_fwd<float>), dim3(grid_for(nr * C)), dim3(CT), 0, s, P, B, pl.To,
-                       pl.Fo, C, af, (float*)out, flat);
+  const long long ng = v4 ? nr * C / 4 : nr * C;
+  if (out_dtype == ASR_DT_BF16 && !flat) {
+    if (v4)
+      hipLaunchKernelGGL((apply_fwd<uint16_t, 4>), dim3(grid_for(ng)), dim3(CT), 0, s, P, B,
+                         pl.To, pl.Fo, C, af, (uint16_t*)out, 0);
+    else
+      hipLaunchKernelGGL((apply_fwd<uint16_t, 1>), dim3(grid_for(ng)), dim3(CT), 0, s, P, B,
+                         pl.To, pl.Fo, C, af, (uint16_t*)out, 0);
+  } else {
+    if (v4)
+      hipLaunchKernelGGL((apply_fwd<float, 4>), dim3(grid_for(ng)), dim3(CT), 0, s, P, B, pl.To,
+                         pl.Fo, C, af, (float*)out, flat);
+    else
+      hipLaunchKernelGGL((apply_fwd<float, 1>), dim3(grid_for(ng)), dim3(CT), 0, s, P, B, pl.To,
+                         pl.Fo, C, af, (float*)out, flat);
+  }
   ASR_LAUNCH_CHECK();
   return ASR_OK;
 }
@@ -691,6 +796,11 @@ extern "C" int asr_vgg_block_backward(const float* dnext, int flat, const float*
   const Pool pl = make_pool(T, F, pt, pf, ceil_mode);
   hipStream_t s = (hipStream_t)stream;
   const long long nr = (long long)B * pl.To * pl.Fo;
+  ASR_REQUIRE((long long)B * (T + 2) * (F + 2) * C < (1LL << 31), ASR_ERR_UNSUPPORTED,
+              "vgg_block_backward: layer too large for 32-bit element indices");
+  ASR_REQUIRE(C <= CT && CT % C == 0, ASR_ERR_UNSUPPORTED,
+              "vgg_block_backward: channels %d must divide %d", C, CT);
+  const bool v4 = C % 4 == 0;
   Affine af{nullptr, nullptr, nullptr, nullptr, drop, seed};
   float* sums = nullptr;
   if (gamma) {
@@ -704,20 +814,34 @@ extern "C" int asr_vgg_block_backward(const float* dnext, int flat, const float*
     const int nchunk = (int)((nr + per - 1) / per);
     float* part = (float*)workspace;
     sums = part + (size_t)nchunk * 2 * C;
-    hipLaunchKernelGGL(bn_bwd_moments, dim3(nchunk), dim3(CT), 0, s, dnext, P, B, pl.To, pl.Fo,
-                       C, flat, af, per, part);
+    if (v4)
+      hipLaunchKernelGGL(bn_bwd_moments<4>, dim3(nchunk), dim3(CT), 0, s, dnext, P, B, pl.To,
+                         pl.Fo, C, flat, af, per, part);
+    else
+      hipLaunchKernelGGL(bn_bwd_moments<1>, dim3(nchunk), dim3(CT), 0, s, dnext, P, B, pl.To,
+                         pl.Fo, C, flat, af, per, part);
     hipLaunchKernelGGL(sum_partials, dim3((2 * C + 63) / 64), dim3(CT), 0, s, part, nchunk, 2 * C,
                        1.f, sums);
     hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + CT - 1) / CT), dim3(CT), 0, s, sums, C, dgamma,
                        dbeta);
     ASR_LAUNCH_CHECK();
   }
-  if (dz_dtype == ASR_DT_BF16)
-    hipLaunchKernelGGL((post_bwd<uint16_t>), dim3(grid_for(nr * C)), dim3(CT), 0, s, dnext, P, z,
-                       slot, B, T, F, C, pl, flat, af, sums, (uint16_t*)dz);
-  else
-    hipLaunchKernelGGL((post_bwd<float>), dim3(grid_for(nr * C)), dim3(CT), 0, s, dnext, P, z,
-                       slot, B, T, F, C, pl, flat, af, sums, (float*)dz);
+  const long long ng = v4 ? nr * C / 4 : nr * C;
+  if (dz_dtype == ASR_DT_BF16) {
+    if (v4)
+      hipLaunchKernelGGL((post_bwd<uint16_t, 4>), dim3(grid_for(ng)), dim3(CT), 0, s, dnext, P, z,
+                         slot, B, T, F, C, pl, flat, af, sums, (uint16_t*)dz);
+    else
+      hipLaunchKernelGGL((post_bwd<uint16_t, 1>), dim3(grid_for(ng)), dim3(CT), 0, s, dnext, P, z,
+                         slot, B, T, F, C, pl, flat, af, sums, (uint16_t*)dz);
+  } else {
+    if (v4)
+      hipLaunchKernelGGL((post_bwd<float, 4>), dim3(grid_for(ng)), dim3(CT), 0, s, dnext, P, z,
+                         slot, B, T, F, C, pl, flat, af, sums, (float*)dz);
+    else
+      hipLaunchKernelGGL((post_bwd<float, 1>), dim3(grid_for(ng)), dim3(CT), 0, s, dnext, P, z,
+                         slot, B, T, F, C, pl, flat, af, sums, (float*)dz);
+  }
   ASR_LAUNCH_CHECK();
   return ASR_OK;
 }
