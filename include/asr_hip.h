@@ -538,6 +538,14 @@ int asr_vgg_block_backward(const float* dnext, int flat, const float* z, int B, 
                            const float* bn_rstd, float* dgamma, float* dbeta, float drop,
                            unsigned long long seed, void* dz, int dz_dtype, void* workspace,
                            size_t ws_bytes, void* stream);
+/* ... and dbias (nullable) += the conv bias gradient (per-channel sum of the
+ * f32 dZ values, fixed order), so dZ can be stored as a bf16 GEMM operand. */
+int asr_vgg_block_backward_ex(const float* dnext, int flat, const float* z, int B, int T, int F,
+                              int C, int pt, int pf, int ceil_mode, const float* P,
+                              const uint8_t* slot, const float* gamma, const float* bn_mean,
+                              const float* bn_rstd, float* dgamma, float* dbeta, float drop,
+                              unsigned long long seed, void* dz, int dz_dtype, float* dbias,
+                              void* workspace, size_t ws_bytes, void* stream);
 
 /* ----------------------------------------------------------- profiling
  * Sampled HIP-event timing of the recurrence step kernels on their own stream

@@ -335,18 +335,29 @@ __global__ void apply_fwd(const float* __restrict__ P, int B, int To, int Fo, in
     const long long i = (long long)q * C + c;
     VecF<V> y;
     y.load(P + i);
+    if (af.mean) {
+      VecF<V> m, r, g, bt;
+      m.load(af.mean + c);
+      r.load(af.rstd + c);
+      g.load(af.gamma + c);
+      bt.load(af.beta + c);
 #pragma unroll
-    for (int j = 0; j < V; ++j) {
-      if (af.mean)
-        y.v[j] = (y.v[j] - af.mean[c + j]) * af.rstd[c + j] * af.gamma[c + j] + af.beta[c + j];
-      if (af.drop > 0.f) y.v[j] *= drop_scale(af.drop, af.seed, (unsigned long long)(i + j));
+      for (int j = 0; j < V; ++j) y.v[j] = (y.v[j] - m.v[j]) * r.v[j] * g.v[j] + bt.v[j];
+    }
+    if (af.drop > 0.f) {
+#pragma unroll
+      for (int j = 0; j < V; ++j) y.v[j] *= drop_scale(af.drop, af.seed, (unsigned long long)(i + j));
     }
     long long o = i;
     if (!flat) {
       const PixIdx px = pix_of(q, To, Fo);
       o = pad_row(px.b, px.to, px.fo, To, Fo) * C + c;
     }
-    if constexpr (sizeof(TO) == 2) {
+    if constexpr (sizeof(TO) == 2 && V == 4) {   // one 8-B store of four bf16
+      const unsigned lo = f2bf(y.v[0]) | ((unsigned)f2bf(y.v[1]) << 16);
+      const unsigned hi = f2bf(y.v[2]) | ((unsigned)f2bf(y.v[3]) << 16);
+      *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + o) = make_uint2(lo, hi);
+    } else if constexpr (sizeof(TO) == 2) {
 #pragma unroll
       for (int j = 0; j < V; ++j) out[o + j] = f2bf(y.v[j]);
     } else {
@@ -441,29 +452,44 @@ __global__ void bn_bwd_finalize(const float* __restrict__ sums, int C, float* __
 
 // dP = BN backward (or dy without BN); routed to the pooled-from pixel if its
 // conv output was positive (ReLU), written into dZ [padded pixels][C] (TO).
+// bias_part (nullable): per-block column sums of the f32 dZ values, the conv
+// bias gradient before its fixed-order sum over blocks -- so dZ itself can be
+// a bf16 GEMM operand (C divides the block size: a thread's channels are the
+// same in every grid-stride iteration).
 template <typename TO, int V>
-__global__ void post_bwd(const float* __restrict__ dnext, const float* __restrict__ P,
-                         const float* __restrict__ z, const uint8_t* __restrict__ slot, int B,
-                         int T, int F, int C, Pool pl, int flat, Affine af,
-                         const float* __restrict__ sums, TO* __restrict__ dz) {
+__global__ void __launch_bounds__(CT) post_bwd(const float* __restrict__ dnext,
+                                               const float* __restrict__ P,
+                                               const float* __restrict__ z,
+                                               const uint8_t* __restrict__ slot, int B, int T,
+                                               int F, int C, Pool pl, int flat, Affine af,
+                                               const float* __restrict__ sums,
+                                               TO* __restrict__ dz,
+                                               float* __restrict__ bias_part) {
+  __shared__ float red[CT * V];
   const unsigned nr = (unsigned)B * pl.To * pl.Fo;
   const unsigned CV = (unsigned)(C / V);
   const unsigned n = nr * CV;
   const float inv_n = 1.f / (float)nr;
+  float bacc[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) bacc[j] = 0.f;
   for (unsigned e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
     const unsigned q = e / CV;
     const int c = (int)(e - q * CV) * V;
     const long long i = (long long)q * C + c;
     VecF<V> g = dy_at<V>(dnext, q, c, pl.To, pl.Fo, C, flat, af.drop, af.seed);
     if (af.mean) {
-      VecF<V> x;
+      VecF<V> x, m, r, gm, s1, s2;
       x.load(P + i);
+      m.load(af.mean + c);
+      r.load(af.rstd + c);
+      gm.load(af.gamma + c);
+      s1.load(sums + c);
+      s2.load(sums + C + c);
 #pragma unroll
       for (int j = 0; j < V; ++j) {
-        const int cj = c + j;
-        const float xh = (x.v[j] - af.mean[cj]) * af.rstd[cj];
-        g.v[j] = af.gamma[cj] * af.rstd[cj] *
-                 (g.v[j] - sums[cj] * inv_n - xh * sums[C + cj] * inv_n);
+        const float xh = (x.v[j] - m.v[j]) * r.v[j];
+        g.v[j] = gm.v[j] * r.v[j] * (g.v[j] - s1.v[j] * inv_n - xh * s2.v[j] * inv_n);
       }
     }
     const PixIdx px = pix_of(q, pl.To, pl.Fo);
@@ -477,9 +503,23 @@ __global__ void post_bwd(const float* __restrict__ dnext, const float* __restric
       }
       const long long p = pad_row(px.b, t, f, T, F) * C + c + j;
       const float v = z[p] > 0.f ? g.v[j] : 0.f;
+      bacc[j] += v;
       if constexpr (sizeof(TO) == 2) dz[p] = f2bf(v);
       else dz[p] = v;
     }
+  }
+  if (bias_part) {   // threads tid, tid + CV, ... hold the same channels
+    const int tid = threadIdx.x, cg = tid % (int)CV;
+#pragma unroll
+    for (int j = 0; j < V; ++j) red[tid * V + j] = bacc[j];
+    __syncthreads();
+    for (int cc = tid; cc < C; cc += CT) {
+      const int g2 = cc / V, j = cc % V;
+      float t = 0.f;
+      for (int k = g2; k < CT; k += (int)CV) t += red[k * V + j];
+      bias_part[(long long)blockIdx.x * C + cc] = t;
+    }
+    (void)cg;
   }
 }
 
@@ -689,11 +729,18 @@ extern "C" int asr_vgg_pool_dims(int T, int F, int pt, int pf, int ceil_mode, in
   return ASR_OK;
 }
 
+// post_bwd's grid (block count) for a layer of nr pooled pixels x C channels
+inline int post_grid(long long nr, int C) {
+  return grid_for(C % 4 == 0 ? nr * C / 4 : nr * C);
+}
+
 extern "C" size_t asr_vgg_block_workspace_bytes(int B, int To, int Fo, int C) {
   const long long n = (long long)B * To * Fo;
   const long long per = rows_per_chunk(n);
   const long long nchunk = (n + per - 1) / per;
-  return (size_t)(nchunk * 2 + 4) * C * sizeof(float);
+  // BN partials + sums, then the conv-bias partials of post_bwd (+ their total)
+  return (size_t)(nchunk * 2 + 4) * C * sizeof(float) +
+         (size_t)(post_grid(n, C) + 1) * C * sizeof(float);
 }
 
 // ReLU + pool + BatchNorm (+ stats) + dropout of one VGG layer.
@@ -784,6 +831,15 @@ extern "C" int asr_vgg_block_forward(const float* z, int B, int T, int F, int C,
 // the gradient of `out` (padded rows f32 or flat); dz [padded pixels][C] of
 // dz_dtype receives d(conv output) (the caller zeroes it: halo and
 // not-selected pixels stay 0); dgamma / dbeta accumulate (+=).
+extern "C" int asr_vgg_block_backward_ex(const float* dnext, int flat, const float* z, int B,
+                                         int T, int F, int C, int pt, int pf, int ceil_mode,
+                                         const float* P, const uint8_t* slot, const float* gamma,
+                                         const float* bn_mean, const float* bn_rstd,
+                                         float* dgamma, float* dbeta, float drop,
+                                         unsigned long long seed, void* dz, int dz_dtype,
+                                         float* dbias, void* workspace, size_t ws_bytes,
+                                         void* stream);
+
 extern "C" int asr_vgg_block_backward(const float* dnext, int flat, const float* z, int B, int T,
                                       int F, int C, int pt, int pf, int ceil_mode,
                                       const float* P, const uint8_t* slot, const float* gamma,
@@ -791,6 +847,21 @@ extern "C" int asr_vgg_block_backward(const float* dnext, int flat, const float*
                                       float* dbeta, float drop, unsigned long long seed,
                                       void* dz, int dz_dtype, void* workspace, size_t ws_bytes,
                                       void* stream) {
+  return asr_vgg_block_backward_ex(dnext, flat, z, B, T, F, C, pt, pf, ceil_mode, P, slot, gamma,
+                                   bn_mean, bn_rstd, dgamma, dbeta, drop, seed, dz, dz_dtype,
+                                   nullptr, workspace, ws_bytes, stream);
+}
+
+// ... and dbias (nullable) += the conv bias gradient, sum of dZ per channel
+// (formed from the f32 values before dZ is stored, in a fixed order).
+extern "C" int asr_vgg_block_backward_ex(const float* dnext, int flat, const float* z, int B,
+                                         int T, int F, int C, int pt, int pf, int ceil_mode,
+                                         const float* P, const uint8_t* slot, const float* gamma,
+                                         const float* bn_mean, const float* bn_rstd,
+                                         float* dgamma, float* dbeta, float drop,
+                                         unsigned long long seed, void* dz, int dz_dtype,
+                                         float* dbias, void* workspace, size_t ws_bytes,
+                                         void* stream) {
   ASR_REQUIRE(dnext && z && P && dz && B > 0 && T > 0 && F > 0 && C > 0, ASR_ERR_ARG,
               "vgg_block_backward: bad args");
   const Pool pl = make_pool(T, F, pt, pf, ceil_mode);
@@ -803,6 +874,15 @@ extern "C" int asr_vgg_block_backward(const float* dnext, int flat, const float*
   const bool v4 = C % 4 == 0;
   Affine af{nullptr, nullptr, nullptr, nullptr, drop, seed};
   float* sums = nullptr;
+  float* bpart = nullptr;
+  const int pgrid = post_grid(nr, C);
+  if (dbias) {
+    ASR_REQUIRE(workspace && ws_bytes >= asr_vgg_block_workspace_bytes(B, pl.To, pl.Fo, C),
+                ASR_ERR_WORKSPACE, "vgg_block_backward: bias needs the workspace");
+    const long long per = rows_per_chunk(nr);
+    const long long nchunk = (nr + per - 1) / per;
+    bpart = (float*)workspace + (size_t)(nchunk * 2 + 4) * C;
+  }
   if (gamma) {
     ASR_REQUIRE(bn_mean && bn_rstd && workspace, ASR_ERR_ARG, "vgg_block_backward: BN args");
     ASR_REQUIRE(ws_bytes >= asr_vgg_block_workspace_bytes(B, pl.To, pl.Fo, C), ASR_ERR_WORKSPACE,
@@ -826,21 +906,28 @@ extern "C" int asr_vgg_block_backward(const float* dnext, int flat, const float*
                        dbeta);
     ASR_LAUNCH_CHECK();
   }
-  const long long ng = v4 ? nr * C / 4 : nr * C;
   if (dz_dtype == ASR_DT_BF16) {
     if (v4)
-      hipLaunchKernelGGL((post_bwd<uint16_t, 4>), dim3(grid_for(ng)), dim3(CT), 0, s, dnext, P, z,
-                         slot, B, T, F, C, pl, flat, af, sums, (uint16_t*)dz);
+      hipLaunchKernelGGL((post_bwd<uint16_t, 4>), dim3(pgrid), dim3(CT), 0, s, dnext, P, z, slot,
+                         B, T, F, C, pl, flat, af, sums, (uint16_t*)dz, bpart);
     else
-      hipLaunchKernelGGL((post_bwd<uint16_t, 1>), dim3(grid_for(ng)), dim3(CT), 0, s, dnext, P, z,
-                         slot, B, T, F, C, pl, flat, af, sums, (uint16_t*)dz);
+      hipLaunchKernelGGL((post_bwd<uint16_t, 1>), dim3(pgrid), dim3(CT), 0, s, dnext, P, z, slot,
+                         B, T, F, C, pl, flat, af, sums, (uint16_t*)dz, bpart);
   } else {
     if (v4)
-      hipLaunchKernelGGL((post_bwd<float, 4>), dim3(grid_for(ng)), dim3(CT), 0, s, dnext, P, z,
-                         slot, B, T, F, C, pl, flat, af, sums, (float*)dz);
+      hipLaunchKernelGGL((post_bwd<float, 4>), dim3(pgrid), dim3(CT), 0, s, dnext, P, z, slot, B,
+                         T, F, C, pl, flat, af, sums, (float*)dz, bpart);
     else
-      hipLaunchKernelGGL((post_bwd<float, 1>), dim3(grid_for(ng)), dim3(CT), 0, s, dnext, P, z,
-                         slot, B, T, F, C, pl, flat, af, sums, (float*)dz);
+      hipLaunchKernelGGL((post_bwd<float, 1>), dim3(pgrid), dim3(CT), 0, s, dnext, P, z, slot, B,
+                         T, F, C, pl, flat, af, sums, (float*)dz, bpart);
+  }
+  ASR_LAUNCH_CHECK();
+  if (dbias) {   // total over the blocks in order, then dbias += total
+    float* tot = bpart + (size_t)pgrid * C;
+    hipLaunchKernelGGL(sum_partials, dim3((C + 63) / 64), dim3(CT), 0, s, bpart, pgrid, C, 1.f,
+                       tot);
+    ASR_LAUNCH_CHECK();
+    return asr_vgg_accumulate(tot, dbias, C, nullptr, nullptr, 0, stream);
   }
   ASR_LAUNCH_CHECK();
   return ASR_OK;

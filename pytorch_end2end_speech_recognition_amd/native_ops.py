@@ -1271,18 +1271,23 @@ class VGGFn(torch.autograd.Function):
             cT, cF, cC, cCp, Co, pt, pf, ceil, drop, seed, gemm = layers[l]
             sp = specs[l]
             npad = B * (cT + 2) * (cF + 2)
-            dz_f32 = not gemm or sp['b'] is not None
+            # dz is the GEMM operand (compute dtype) of GEMM layers; their conv
+            # bias gradient is summed from the f32 values inside the kernel
+            dz_f32 = not gemm
             dz = torch.zeros(npad, Co, **f32) if dz_f32 else torch.zeros(npad, Co, dtype=opdt,
                                                                           device=dev)
+            fused_bias = gemm and sp['b'] is not None
             To, Fo = _pool_dims(cT, cF, pt, pf, ceil) if pt else (cT, cF)
             nb = N.query('asr_vgg_block_workspace_bytes', B, To, Fo, Co)
             ws = _ws(nb, dev)
             bn = sp['gamma'] is not None
-            N.call('asr_vgg_block_backward', N.ptr(dnext), flat, N.ptr(z), B, cT, cF, Co, pt, pf,
-                   ceil, N.ptr(P), N.ptr(slot), N.ptr(sp['gamma']), N.ptr(mean), N.ptr(rstd),
+            N.call('asr_vgg_block_backward_ex', N.ptr(dnext), flat, N.ptr(z), B, cT, cF, Co, pt,
+                   pf, ceil, N.ptr(P), N.ptr(slot), N.ptr(sp['gamma']), N.ptr(mean), N.ptr(rstd),
                    N.ptr(grad_buffer(sp['gamma']) if bn else None),
                    N.ptr(grad_buffer(sp['beta']) if bn else None), drop, seed, N.ptr(dz),
-                   F32 if dz_f32 else cd, N.ptr(ws), nb, N.stream_handle(dev))
+                   F32 if dz_f32 else cd,
+                   N.ptr(grad_buffer(sp['b']) if fused_bias else None), N.ptr(ws), nb,
+                   N.stream_handle(dev))
             w = sp['w']
             if not gemm:
                 nb = N.query('asr_conv_direct_wgrad_workspace_bytes', B, cT, cF, cC, Co)
@@ -1305,8 +1310,6 @@ class VGGFn(torch.autograd.Function):
                                    rowmap(9 * cCp), Co, 9 * cCp, npad)], dev)
             N.call('asr_conv_weight_unpack_acc_pad', N.ptr(packed), Co, cC, cCp,
                    N.ptr(grad_buffer(w)), N.stream_handle(dev))
-            if sp['b'] is not None:
-                colsum_accumulate(dz, grad_buffer(sp['b']))
             if l == 0:
                 break
             # d input (padded rows of layer l's input) = dz (taps, mirrored) x W^T image
