@@ -14,6 +14,7 @@
 // blocks.  Register-staged double buffering: the next K tile's global loads are
 // issued before the MFMAs of the current tile and written to LDS after the
 // barrier.  Block ids are remapped so consecutive tiles share an XCD's L2.
+#include <stdio.h>
 #include <string.h>
 
 #include "mfma.h"
@@ -1746,6 +1747,13 @@ int gemm_launch_own(const asr_gemm_t* problems, int nprob, int compute_dtype, vo
 #undef ASR_FAST
     }
   } else if (compute_dtype == ASR_DT_BF16) {
+    if (getenv("ASR_GEMM_DEBUG"))   // which bf16-mode products miss the fast kernels
+      for (int i = 0; i < nprob; ++i)
+        fprintf(stderr, "[asr_gemm generic] M=%d N=%d K=%d batch=%d a(dt=%d tr=%d tap=%d perm=%d) "
+                "b(dt=%d tr=%d tap=%d perm=%d)\n", problems[i].M, problems[i].N, problems[i].K,
+                problems[i].batch, problems[i].a.dtype, problems[i].a.trans,
+                problems[i].a.tap_group, problems[i].a.map.perm != nullptr, problems[i].b.dtype,
+                problems[i].b.trans, problems[i].b.tap_group, problems[i].b.map.perm != nullptr);
     const size_t lds = 2 * BM * LDB16 * 2;
     hipLaunchKernelGGL(gemm_kernel<true>, grid, dim3(NT), lds, s, P);
   } else {
@@ -1826,6 +1834,17 @@ size_t split_bytes_aligned(const asr_gemm_t* g, int nprob) {
 int gemm_launch(const asr_gemm_t* problems, int nprob, int compute_dtype, void* workspace,
                 size_t ws_bytes, void* stream) {
   ASR_REQUIRE(problems && nprob >= 1 && nprob <= 2, ASR_ERR_ARG, "gemm: nprob must be 1 or 2");
+  // The fast kernels take one operand-layout pair per launch: two products with
+  // different layouts (a Linear backward's dX + dW) run as two launches, one
+  // after the other on the stream (each within the pair's workspace), instead
+  // of one launch of the generic kernel.
+  if (nprob == 2 && compute_dtype == ASR_DT_BF16 &&
+      2 * problems[0].a.trans + problems[0].b.trans !=
+          2 * problems[1].a.trans + problems[1].b.trans) {
+    const int rc = gemm_launch(problems, 1, compute_dtype, workspace, ws_bytes, stream);
+    if (rc) return rc;
+    return gemm_launch(problems + 1, 1, compute_dtype, workspace, ws_bytes, stream);
+  }
   if (compute_dtype == ASR_DT_BF16 && workspace) {
     const size_t base = split_bytes_aligned(problems, nprob);
     const StagePlan st = plan_stage(problems, nprob, base);
