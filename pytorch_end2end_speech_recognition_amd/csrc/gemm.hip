@@ -41,6 +41,8 @@ struct Operand {
   int vec_ok; // 16-element vector loads legal (alignment of base and strides)
   long long bytes;  // readable bytes from base (0 = unknown)
   int tap_g, tap_w, tap_s;  // 3x3 tap addressing (asr_operand_t), tap_g = 0: off
+  int sf;     // division-free staging of the 128x128 kernel applies (StageF)
+  int plain;  // row map is r * stride_t, valid for 0 <= r < t_limit
 };
 
 // Tap addressing: contiguous index x -> (tap, x'), row shifted by the tap's offset.
@@ -465,6 +467,138 @@ __device__ __forceinline__ void stage_tile(const Operand& op, __amdgpu_buffer_rs
   }
 }
 
+// Division-free staging for the 128x128 kernel (the Stage8 scheme, with tap
+// addressing): per DMA slot the row / k-row state is computed once per tile
+// and advanced by FBK per k-tile, so the k-loop does no integer division --
+// the division-based row_off_np + tap split per DMA was VALU work comparable
+// to the MFMA work of a k-tile.  R mode: the rows are fixed; with taps on k the
+// slot carries (tap, k within the tap group) and the row shift of its tap.
+// K mode: the columns are fixed (their tap split and row shift once); the
+// k-row advances (plain map) or carries its (utterance, frame) pair.
+struct StageF {
+  int x[4];   // R: k within the tap group (taps) | K: current k-row (+ tap shift), plain map
+  int y[4];   // R: current tap (taps) | K: frame of the k-row (general map)
+  int z[4];   // R: pixel row (taps) | K: utterance of the k-row (general map)
+  unsigned base[4];   // R: row byte offset (no taps) | K: column byte offset
+  int valid;
+};
+
+__device__ __forceinline__ int tap_shift(const Operand& op, int tap) {
+  return op.tap_s * ((tap / 3 - 1) * op.tap_w + (tap % 3 - 1));
+}
+
+template <int MODE>
+__device__ __forceinline__ void stagef_init(const Operand& op, StageF& st, int tile0, int nrows,
+                                            int kbeg, int wave, int lane) {
+  st.valid = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int blk = wave * 4 + i;
+    if (MODE == 0) {
+      const int r = blk * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      const int row = tile0 + r, k = kbeg + 8 * c;
+      if (row < nrows) st.valid |= 1 << i;
+      if (op.tap_g) {
+        st.y[i] = k / op.tap_g;
+        st.x[i] = k - st.y[i] * op.tap_g;
+        st.z[i] = row;
+        st.base[i] = 0u;
+      } else {
+        const long long off = row < nrows ? row_off_np(op.map, row) : -1;
+        if (off < 0) st.valid &= ~(1 << i);
+        st.base[i] = off >= 0 ? (unsigned)(off * 2) : 0u;
+        st.x[i] = 8 * c;
+        st.y[i] = st.z[i] = 0;
+      }
+    } else {
+      const int kr = blk * 4 + (lane >> 4);
+      const int j = lane & 15;
+      const int c = 2 * ((j >> 1) ^ swz_h(kr)) + (j & 1);
+      int col = tile0 + 8 * c, shift = 0;
+      if (op.tap_g) {
+        const int tap = col / op.tap_g;
+        col -= tap * op.tap_g;
+        shift = tap_shift(op, tap);
+      }
+      st.base[i] = (unsigned)(col * 2);
+      const int k = kbeg + kr;
+      if (op.plain) {
+        st.x[i] = k + shift;
+        st.y[i] = st.z[i] = 0;
+      } else {
+        st.z[i] = k / op.map.rows_per_b;
+        st.y[i] = k - st.z[i] * op.map.rows_per_b;
+        st.x[i] = 0;
+      }
+    }
+  }
+}
+
+template <int MODE>
+__device__ __forceinline__ void stagef(const Operand& op, __amdgpu_buffer_rsrc_t rs, StageF& st,
+                                       char* lds_tile, int k0, int kend, int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int blk = wave * 4 + i;
+    unsigned voff = OOB_OFF;
+    if (MODE == 0) {
+      const int r = blk * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      const int k = k0 + 8 * c;
+      if (op.tap_g) {
+        const int rr = st.z[i] + tap_shift(op, st.y[i]);
+        if (((st.valid >> i) & 1) && k < kend && rr >= 0 && rr < op.map.t_limit)
+          voff = (unsigned)(((long long)rr * op.map.stride_t + st.x[i]) * 2);
+        st.x[i] += FBK;   // this slot's k in the next k-tile
+        while (st.x[i] >= op.tap_g) {
+          st.x[i] -= op.tap_g;
+          ++st.y[i];
+        }
+      } else if (((st.valid >> i) & 1) && k < kend) {
+        voff = st.base[i] + (unsigned)(k * 2);
+      }
+    } else {
+      const int kr = blk * 4 + (lane >> 4);
+      const int k = k0 + kr;
+      if (op.plain) {
+        const int rr = st.x[i];
+        if (k < kend && rr >= 0 && rr < op.map.t_limit)
+          voff = (unsigned)((long long)rr * op.map.stride_t * 2) + st.base[i];
+        st.x[i] += FBK;
+      } else {
+        const int tp = st.y[i] * op.map.t_mul + op.map.t_add;
+        if (k < kend && tp >= 0 && tp < op.map.t_limit)
+          voff = (unsigned)(((long long)st.z[i] * op.map.stride_b +
+                             (long long)tp * op.map.stride_t) * 2) + st.base[i];
+        st.y[i] += FBK;
+        while (st.y[i] >= op.map.rows_per_b) {
+          st.y[i] -= op.map.rows_per_b;
+          ++st.z[i];
+        }
+      }
+    }
+    const unsigned lds_addr = (unsigned)(uintptr_t)(lds_void_t*)(lds_tile + blk * 1024);
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(rs), "s"(lds_addr)
+        : "memory");
+  }
+}
+
+// One operand's tile of the 128x128 kernel: StageF when the operand allows it
+// (wave-uniform branch), else the per-DMA row map.
+template <int MODE>
+__device__ __forceinline__ void stage_any(const Operand& op, __amdgpu_buffer_rsrc_t rs,
+                                          StageF& st, char* lds_tile, int tile0, int nrows,
+                                          int k0, int kend, int wave, int lane) {
+  if (op.sf) stagef<MODE>(op, rs, st, lds_tile, k0, kend, wave, lane);
+  else stage_tile<MODE>(op, rs, lds_tile, tile0, nrows, k0, kend, wave, lane);
+}
+
 // MFMA fragment (16 rows x 32 k) of the block starting at tile row rb, k-half kk.
 template <int MODE>
 __device__ __forceinline__ bf16x8 frag_bf16(const char* lds_tile, int rb, int kk, int lane) {
@@ -551,9 +685,12 @@ __global__ void __launch_bounds__(NT) gemm_bf16_fast(Params P) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = (kend - kbeg + FBK - 1) / FBK;
+  StageF sa, sb;
+  if (pr.a.sf) stagef_init<AMODE>(pr.a, sa, tm, pr.M, kbeg, w, lane);
+  if (pr.b.sf) stagef_init<BMODE>(pr.b, sb, tn, pr.N, kbeg, w, lane);
   if (NSTAGE == 2) {
-    stage_tile<AMODE>(pr.a, ra, smem, tm, pr.M, kbeg, kend, w, lane);
-    stage_tile<BMODE>(pr.b, rb, smem + FTILE, tn, pr.N, kbeg, kend, w, lane);
+    stage_any<AMODE>(pr.a, ra, sa, smem, tm, pr.M, kbeg, kend, w, lane);
+    stage_any<BMODE>(pr.b, rb, sb, smem + FTILE, tn, pr.N, kbeg, kend, w, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     for (int kt = 0; kt < nk; ++kt) {
@@ -561,8 +698,8 @@ __global__ void __launch_bounds__(NT) gemm_bf16_fast(Params P) {
       if (kt + 1 < nk) {
         char* nxt = smem + ((kt + 1) & 1) * 2 * FTILE;
         const int k0 = kbeg + (kt + 1) * FBK;
-        stage_tile<AMODE>(pr.a, ra, nxt, tm, pr.M, k0, kend, w, lane);
-        stage_tile<BMODE>(pr.b, rb, nxt + FTILE, tn, pr.N, k0, kend, w, lane);
+        stage_any<AMODE>(pr.a, ra, sa, nxt, tm, pr.M, k0, kend, w, lane);
+        stage_any<BMODE>(pr.b, rb, sb, nxt + FTILE, tn, pr.N, k0, kend, w, lane);
       }
       mma_ktile<AMODE, BMODE>(cur, acc, wr, wc, lane);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -579,8 +716,8 @@ __global__ void __launch_bounds__(NT) gemm_bf16_fast(Params P) {
       if (j < nk) {
         char* st = smem + j * 2 * FTILE;
         const int k0 = kbeg + j * FBK;
-        stage_tile<AMODE>(pr.a, ra, st, tm, pr.M, k0, kend, w, lane);
-        stage_tile<BMODE>(pr.b, rb, st + FTILE, tn, pr.N, k0, kend, w, lane);
+        stage_any<AMODE>(pr.a, ra, sa, st, tm, pr.M, k0, kend, w, lane);
+        stage_any<BMODE>(pr.b, rb, sb, st + FTILE, tn, pr.N, k0, kend, w, lane);
       }
     }
     for (int kt = 0; kt < nk; ++kt) {
@@ -592,8 +729,8 @@ __global__ void __launch_bounds__(NT) gemm_bf16_fast(Params P) {
       if (kt + NSTAGE - 1 < nk) {
         char* st = smem + ((kt + NSTAGE - 1) % NSTAGE) * 2 * FTILE;
         const int k0 = kbeg + (kt + NSTAGE - 1) * FBK;
-        stage_tile<AMODE>(pr.a, ra, st, tm, pr.M, k0, kend, w, lane);
-        stage_tile<BMODE>(pr.b, rb, st + FTILE, tn, pr.N, k0, kend, w, lane);
+        stage_any<AMODE>(pr.a, ra, sa, st, tm, pr.M, k0, kend, w, lane);
+        stage_any<BMODE>(pr.b, rb, sb, st + FTILE, tn, pr.N, k0, kend, w, lane);
       }
       mma_ktile<AMODE, BMODE>(smem + (kt % NSTAGE) * 2 * FTILE, acc, wr, wc, lane);
     }
@@ -1458,6 +1595,14 @@ int fill_operand(const asr_operand_t& o, Operand* op, const char* name) {
   op->tap_g = o.tap_group;
   op->tap_w = o.tap_pitch;
   op->tap_s = o.tap_sign ? o.tap_sign : 1;
+  op->plain = (o.map.rows_per_b <= 0 && (o.map.t_mul == 0 || o.map.t_mul == 1) &&
+               o.map.t_add == 0 && !o.map.perm) ? 1 : 0;
+  // StageF: tap operands need the plain map; ASR_GEMM_STAGEF=0 keeps the
+  // per-DMA row map (A/B)
+  {
+    const char* e = getenv("ASR_GEMM_STAGEF");
+    op->sf = !(e && e[0] == '0') && (!o.tap_group || op->plain) && !o.map.perm;
+  }
   if (o.tap_group)
     ASR_REQUIRE(o.tap_group > 0 && o.tap_group % (o.trans ? 8 : 16) == 0 && !o.map.perm,
                 ASR_ERR_ARG, "gemm: operand %s tap_group %d unsupported", name, o.tap_group);
