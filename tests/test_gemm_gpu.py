@@ -242,3 +242,63 @@ def test_gemm_8wave_256_tiles_exact(at, bt, M, N, K, ring, cuda_dev, monkeypatch
         np.testing.assert_array_equal(C.cpu().numpy(), ref)
     finally:
         ops.set_compute_dtype('fp32')
+
+
+def _mapped_rows(store, rpb, stride_b, stride_t, t_mul, t_add, t_limit, nrows, ncols):
+    """Rows 0..nrows-1 of an operand read through asr_rowmap_t (zero where the
+    mapped frame falls outside [0, t_limit))."""
+    out = np.zeros((nrows, ncols), np.float64)
+    flat = store.reshape(-1)
+    for r in range(nrows):
+        b, t = (r // rpb, r % rpb) if rpb > 0 else (0, r)
+        tp = t * t_mul + t_add
+        if 0 <= tp < (t_limit if t_limit > 0 else 1 << 30):
+            off = b * stride_b + tp * stride_t
+            out[r] = flat[off:off + ncols]
+    return out
+
+
+@pytest.mark.parametrize('stagef', ['1', '0'])
+def test_fast_kernel_mapped_k_rows_exact(stagef, cuda_dev, monkeypatch):
+    """The 128 x 128 kernel (N < 256) on weight-gradient-shaped products whose
+    K rows come through a grouped row map (utterance groups, frame stride 2,
+    offset 1, frame limit: the pyramidal-subsampling and shifted-h operands),
+    with the division-free staging (StageF) and without it."""
+    monkeypatch.setenv('ASR_GEMM_STAGEF', stagef)
+    ops = _ops()
+    ops.set_compute_dtype('bf16')
+    try:
+        rng = np.random.RandomState(7)
+        M, Nn = 320, 200
+        rpb, T, t_mul, t_add, t_limit = 37, 80, 2, 1, 60
+        nb = 9
+        K = nb * rpb
+        lda, ldb = M + 8, Nn + 8
+        sa = _store(rng, nb * T, M, lda)
+        sb = _store(rng, nb * T, Nn, ldb)
+        A = _mapped_rows(sa, rpb, T * lda, lda, t_mul, t_add, t_limit, K, M)
+        Bm = _mapped_rows(sb, rpb, T * ldb, ldb, t_mul, t_add, t_limit, K, Nn)
+        ad = torch.from_numpy(sa).to(torch.bfloat16).to(cuda_dev)
+        bd = torch.from_numpy(sb).to(torch.bfloat16).to(cuda_dev)
+        C = torch.zeros(M, Nn, device=cuda_dev)
+        p = ops.gemm_problem(
+            ops.operand(ad, 1, ops.rowmap(lda, T * lda, rpb, t_mul, t_add, t_limit)),
+            ops.operand(bd, 1, ops.rowmap(ldb, T * ldb, rpb, t_mul, t_add, t_limit)),
+            C, ops.rowmap(Nn), M, Nn, K)
+        ops.run_gemm([p], cuda_dev)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(C.cpu().numpy(), A.T @ Bm)
+        # R-mode operand with mapped rows (M rows through the same kind of map)
+        Mr = nb * rpb
+        A2 = _mapped_rows(sa, rpb, T * lda, lda, t_mul, t_add, t_limit, Mr, 64)
+        sb2 = _store(rng, Nn, 64, 64)
+        bd2 = torch.from_numpy(sb2).to(torch.bfloat16).to(cuda_dev)
+        C2 = torch.zeros(Mr, Nn, device=cuda_dev)
+        p2 = ops.gemm_problem(
+            ops.operand(ad, 0, ops.rowmap(lda, T * lda, rpb, t_mul, t_add, t_limit)),
+            ops.operand(bd2, 0, ops.rowmap(64)), C2, ops.rowmap(Nn), Mr, Nn, 64)
+        ops.run_gemm([p2], cuda_dev)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(C2.cpu().numpy(), A2 @ sb2.astype(np.float64).T)
+    finally:
+        ops.set_compute_dtype('fp32')
