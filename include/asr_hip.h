@@ -162,6 +162,18 @@ size_t asr_gemm_workspace_bytes(const asr_gemm_t* problems, int nprob);
 int asr_gemm_ws(const asr_gemm_t* problems, int nprob, int compute_dtype, void* workspace,
                 size_t ws_bytes, void* stream);
 
+/* on != 0: later asr_gemm / asr_gemm_ws calls FROM THIS HOST THREAD use only the
+ * 128 x 128 kernel (64 KB of LDS per work-group) until reset with 0, so that
+ * their work-groups fit beside a persistent recurrence work-group on every CU
+ * (weight gradients co-resident with the backward recurrence). */
+int asr_gemm_set_small_tiles(int on);
+
+/* Enqueue on `stream` a one-wave gate that releases once the NEXT persistent
+ * backward recurrence (asr_lstm_backward*, any stream) has all its work-groups
+ * resident, or after ~5 ms.  Work queued behind it on `stream` (the small-tile
+ * weight-gradient GEMMs) then runs beside that recurrence.  Timing only. */
+int asr_lstm_wgrad_gate(void* stream);
+
 /* out0[n] (+ out1[n] if non-NULL) += alpha * sum_m g[m*ld + n]  (bias grads of
  * nn.Linear / nn.LSTM bias_ih and bias_hh); fixed-order, deterministic. */
 size_t asr_colsum_workspace_bytes(int M, int N);

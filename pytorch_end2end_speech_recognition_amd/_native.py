@@ -42,6 +42,8 @@ SIGNATURES = {
     'asr_gemm': (c_int, [c_vp, c_int, c_int, c_vp]),
     'asr_gemm_workspace_bytes': (c_size, [c_vp, c_int]),
     'asr_gemm_ws': (c_int, [c_vp, c_int, c_int, c_vp, c_size, c_vp]),
+    'asr_gemm_set_small_tiles': (c_int, [c_int]),
+    'asr_lstm_wgrad_gate': (c_int, [c_vp]),
     'asr_colsum_workspace_bytes': (c_size, [c_int, c_int]),
     'asr_colsum_accumulate': (c_int, [c_vp, c_ll, c_int, c_int, c_float, c_vp, c_vp, c_vp, c_size,
                                       c_vp]),

@@ -1724,9 +1724,16 @@ int split_target() {
   return v > 0 ? v : 512;
 }
 
+// asr_gemm_set_small_tiles(1): launches from this host thread keep to the
+// 128 x 128 kernel (64 KB of LDS) until reset -- the weight-gradient GEMMs that
+// run co-resident with the persistent backward recurrence (native_ops,
+// ASR_OVERLAP_WGRAD=2) must fit beside its work-group on every CU.
+thread_local int g_small_tiles = 0;
+
 bool big8_ok(const asr_gemm_t* g, int nprob) {
   const char* e = getenv("ASR_GEMM_8W");
   if (e && e[0] == '0') return false;
+  if (g_small_tiles) return false;
   for (int i = 0; i < nprob; ++i) {
     if (g[i].M < T8 || g[i].N < T8) return false;
     if (g[i].a.tap_group || g[i].b.tap_group) return false;     // taps: 128 x 128 kernel
@@ -1877,7 +1884,7 @@ int gemm_launch_own(const asr_gemm_t* problems, int nprob, int compute_dtype, vo
     hipLaunchKernelGGL(gemm_bf16_kk256, dim3(maxwg2, 1, nprob * maxb), dim3(NT),
                        (size_t)NST2 * 2 * FTILE2, s, P);
   } else if (fast >= 0) {
-    const int nst = fast_stages();
+    const int nst = g_small_tiles ? 2 : fast_stages();
     const size_t lds = (size_t)nst * 2 * FTILE;
     switch (fast) {
 #define ASR_FAST(A, B)                                                                   \
@@ -2021,6 +2028,11 @@ int gemm_launch(const asr_gemm_t* problems, int nprob, int compute_dtype, void* 
 }  // namespace asr
 
 using namespace asr;
+
+extern "C" int asr_gemm_set_small_tiles(int on) {
+  g_small_tiles = on ? 1 : 0;
+  return ASR_OK;
+}
 
 extern "C" int asr_gemm(const asr_gemm_t* problems, int nprob, int compute_dtype, void* stream) {
   return gemm_launch(problems, nprob, compute_dtype, nullptr, 0, stream);

@@ -48,6 +48,9 @@ namespace asr {
 
 __device__ int g_xg_status;  // bit 0: a bounded spin gave up (results invalid)
 __device__ int g_xg_mode;    // bit 0: a launch ran write-through (sc1); bit 1: XCD-local
+// Sequence number of the last backward launch whose work-groups were all
+// resident (written by its block 0 after placement); the wgrad gate waits on it.
+__device__ unsigned g_xg_resident;
 // Diagnostics only (ASR_XG_TRACE=1): per-step phase timestamps (100 MHz
 // s_memrealtime) of work-groups 0..XG_TR_WG-1, steps 0..XG_TR_STEPS-1.
 __device__ unsigned long long* g_xg_trace;
@@ -67,6 +70,15 @@ constexpr unsigned XG_SPIN_LIMIT = 1u << 20;
 constexpr size_t XG_PIN_FWD = 96 * 1024;   // > 80 KB dynamic LDS: one work-group per CU
 constexpr size_t XG_PIN_FWD8 = 64 * 1024;  // 8 sweeper waves: static `part` is >= 34 KB
 constexpr size_t XG_PIN_BWD = 140 * 1024;
+// ASR_XG_PIN_BWD_KB (read per launch): the backward's dynamic-LDS pin.  Any
+// value above 80 KB still keeps one work-group per CU; 96 leaves 64 KB beside
+// it, room for one 128 x 128 GEMM work-group (the co-resident weight-gradient
+// mode of native_ops, ASR_OVERLAP_WGRAD=2).
+size_t xg_pin_bwd() {
+  const char* e = getenv("ASR_XG_PIN_BWD_KB");
+  const int kb = e ? atoi(e) : 0;
+  return (kb > 80 && kb <= 160) ? (size_t)kb * 1024 : XG_PIN_BWD;
+}
 constexpr unsigned AUX_SC1_VOL = 16u | (1u << 31);  // sc1; volatile (never hoisted from a spin)
 constexpr unsigned AUX_SC1 = 16u;
 
@@ -120,7 +132,8 @@ __device__ __forceinline__ bool keep_spinning(unsigned spins, int* abortw, int n
 // blockIdx and every granule is stored write-through (sc1), which is correct
 // for any placement.  Results never depend on placement: placement only
 // selects which of the two correct protocols runs.
-__device__ __forceinline__ void xg_place(int WPG, int allow_local, int* hdr, int* s_pl) {
+__device__ __forceinline__ void xg_place(int WPG, int allow_local, int* hdr, int* s_pl,
+                                         unsigned seq = 0) {
   if (threadIdx.x == 0) {
     int* abortw = hdr;
     typedef __attribute__((address_space(1))) unsigned long long gu64r;
@@ -165,6 +178,8 @@ __device__ __forceinline__ void xg_place(int WPG, int allow_local, int* hdr, int
     s_pl[2] = local;
     s_pl[3] = ok;
     if (blockIdx.x == 0 && ok) atomicOr(&g_xg_mode, local ? 2 : 1);
+    if (blockIdx.x == 0 && ok && seq)
+      __hip_atomic_store(&g_xg_resident, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
 }
@@ -444,11 +459,10 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
   const int WPG = H / XU;
   const int G = gridDim.x / WPG;
   if (threadIdx.x == 0) s_dead = 0;
-  xg_place(WPG, allow_local, hdr, s_pl);
+  xg_place(WPG, allow_local, hdr, s_pl, epoch);  // epoch: the launch's sequence number
   if (!s_pl[3]) return;
   const int grp = s_pl[0], mem = s_pl[1];
-  const bool local = s_pl[2] != 0;
-  (void)epoch;  // granules carry a 1-bit step tag (tag_bit) instead
+  const bool local = s_pl[2] != 0;  // granules carry a 1-bit step tag (tag_bit)
   const int dir = grp & 1, rg = grp >> 1;
   const int u0 = mem * XU, b0 = rg * R;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -709,6 +723,30 @@ unsigned xg_next_epoch() {
   return e;
 }
 
+// Backward launches are numbered 1, 2, ... (never 0: 0 means "no signal").
+unsigned xg_bwd_seq(bool next) {
+  static unsigned n = 0;
+  if (next) n = n + 1 ? n + 1 : 1;
+  return n;
+}
+
+// Gate for the weight-gradient GEMMs of ASR_OVERLAP_WGRAD=2: one 64-thread
+// work-group (no LDS) that waits until backward launch `want` is resident, or
+// about `max_ticks` of s_memrealtime (100 MHz) have passed.  The GEMMs queued
+// behind it on the same stream then fill the room beside the recurrence's
+// work-groups instead of taking CUs before the recurrence is placed.  Only
+// timing depends on it.
+__global__ void xg_wgrad_gate(unsigned want, unsigned long long max_ticks) {
+  if (threadIdx.x != 0) return;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    const unsigned v = __hip_atomic_load(&g_xg_resident, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((int)(v - want) >= 0) break;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > max_ticks) break;
+    __builtin_amdgcn_s_sleep(8);
+  }
+}
+
 int xg_allow_local() {
   const char* e = getenv("ASR_XG_LOCAL");
   return !(e && e[0] == '0');
@@ -790,15 +828,16 @@ int lstm_bwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* wh
   const int grid = 2 * ((B + R - 1) / R) * (H / XU);
   int* hdr = (int*)ws;
   unsigned long long* g = (unsigned long long*)((char*)ws + XG_HDR);
-  const unsigned ep = xg_next_epoch();
+  const unsigned ep = xg_bwd_seq(true);
   const int al = xg_allow_local();
+  const size_t pin = xg_pin_bwd();
 #define ASR_XGB(RR, M)                                                                          \
   do {                                                                                          \
-    if (!xg_fits(lstm_bwd_xg<RR, M>, 512 + RR * XU, XG_PIN_BWD)) return 0;                               \
+    if (!xg_fits(lstm_bwd_xg<RR, M>, 512 + RR * XU, pin)) return 0;                               \
     if (dry) return 1;                                                                          \
     if (hipMemsetAsync(ws, 0, lstm_xg_bwd_bytes(B, H), s) != hipSuccess) return -1;             \
     xg_trace_setup(s);             \
-    hipLaunchKernelGGL((lstm_bwd_xg<RR, M>), dim3(grid), dim3(512 + RR * XU), XG_PIN_BWD, s, B, T, H,      \
+    hipLaunchKernelGGL((lstm_bwd_xg<RR, M>), dim3(grid), dim3(512 + RR * XU), pin, s, B, T, H,      \
                        lens, whh_f, whh_r, dy, act_dg, cst, g, hdr, dgbf, dbpart, ep, al);                   \
   } while (0)
 #define ASR_XGB_M(RR)                  \
@@ -889,4 +928,13 @@ extern "C" int asr_lstm_xg_mode(int* mode, int clear) {
       return ASR_ERR_HIP;
   }
   return ASR_OK;
+}
+
+// Enqueue the wgrad gate on `stream`: it releases once the NEXT persistent
+// backward recurrence launched on any stream is resident (bounded at ~5 ms).
+extern "C" int asr_lstm_wgrad_gate(void* stream) {
+  const unsigned want = asr::xg_bwd_seq(false) + 1;
+  hipLaunchKernelGGL(asr::xg_wgrad_gate, dim3(1), dim3(64), 0, (hipStream_t)stream,
+                     want ? want : 1u, 500000ull);
+  return hipGetLastError() == hipSuccess ? ASR_OK : ASR_ERR_HIP;
 }

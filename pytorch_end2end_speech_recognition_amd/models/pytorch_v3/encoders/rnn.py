@@ -176,7 +176,7 @@ class RNNEncoder(nn.Module):
             graph = tuple(p for pair in self._layer_params(l) for p in pair)
             h = ops.blstm_layer(h, lens_d, T, w_ih, w_hh, b_ih, b_hh, perm=pm, t_mul=t_mul,
                                 t_add=t_add, gbufs=tuple(gbufs), graph_params=graph,
-                                concat=concat, drop=pending)
+                                concat=concat, drop=pending, next_rec=l > 0)
             pending = None
             if self.training and self.dropout_hidden_p > 0:
                 # same seed stream either way; fused when the next consumer is the

@@ -668,8 +668,8 @@ class BLSTMLayerFn(torch.autograd.Function):
     directly (exact-f32 MFMA, parity mode)."""
 
     @staticmethod
-    def forward(ctx, x_src, lens, T, perm, t_mul, t_add, gbufs, concat, drop, w_ih, w_hh, b_ih,
-                b_hh, *graph_params):
+    def forward(ctx, x_src, lens, T, perm, t_mul, t_add, gbufs, concat, drop, next_rec, w_ih, w_hh,
+                b_ih, b_hh, *graph_params):
         N.require_device(x_src, lens, w_ih, w_hh, b_ih, b_hh)
         x_src = x_src.contiguous()
         fused_drop = drop is not None and compute_dtype() == BF16 and not concat
@@ -713,6 +713,7 @@ class BLSTMLayerFn(torch.autograd.Function):
                               y_bf if y_bf is not None else y)
         ctx.meta = (T, perm, t_mul, t_add, gbufs, cd, (B, T_src, Dsrc, Din), w_ih)
         ctx.drop = drop
+        ctx.next_rec = bool(next_rec)
         ctx.n_graph = len(graph_params)
         return y
 
@@ -742,6 +743,10 @@ class BLSTMLayerFn(torch.autograd.Function):
                    N.ptr(lens), B, T, H, cd, N.ptr(act), N.ptr(cst), N.ptr(dg_bf), N.ptr(ws), nb,
                    N.stream_handle(dev))
             colsum_accumulate(act.view(B * T, 8 * H), gbufs[2], gbufs[3])
+        # weight gradients of the layer above, if they went to a side stream: join
+        # them here (they run beside the recurrence just enqueued) so the
+        # gradient-ready bucket sees them on the compute stream
+        _join_side_wgrads(dev)
         notify_grad_event('recurrence')
         dg_op = dg_bf if dg_bf is not None else act
         # X as the dW_ih operand: the bf16 copy is already gathered (identity map)
@@ -750,22 +755,35 @@ class BLSTMLayerFn(torch.autograd.Function):
         else:
             x_map = rowmap(Dsrc, stride_b=T_src * Dsrc, rows_per_b=T, t_mul=t_mul, t_add=t_add,
                            t_limit=T_src, perm=perm)
-        side = _wgrad_side_stream(dev, B, H)
-        if side is None:
+        side_ent = _wgrad_side_stream(dev, B, H)
+        if side_ent is None:
             _blstm_wgrad(dg_op, act, x_op, x_map, y_op, T, gbufs, dev)
             notify_grad_event('grads', gbufs)      # final on the compute stream
         else:
-            # weight gradients on a CU-masked side stream, overlapping this
-            # layer's dX GEMM and the previous layer's backward recurrence;
-            # joined back into the main stream at the end of the backward pass
+            # weight gradients on a side stream, overlapping this layer's dX
+            # GEMM and the previous layer's backward recurrence; joined back
+            # into the main stream at the end of the backward pass
+            side, small = side_ent
             main = torch.cuda.current_stream(dev)
             side.wait_stream(main)
-            with torch.cuda.stream(side):
-                _blstm_wgrad(dg_op, act, x_op, x_map, y_op, T, gbufs, dev)
+            if small:
+                N.call('asr_gemm_set_small_tiles', 1)
+            try:
+                with torch.cuda.stream(side):
+                    if small and ctx.next_rec:
+                        # hold the GEMMs back until the previous layer's backward
+                        # recurrence (launched next on the main stream) is resident
+                        N.call('asr_lstm_wgrad_gate', N.stream_handle(dev))
+                    _blstm_wgrad(dg_op, act, x_op, x_map, y_op, T, gbufs, dev)
+            finally:
+                if small:
+                    N.call('asr_gemm_set_small_tiles', 0)
             for t in (dg_op, act, x_op, y_op) + ((perm,) if perm is not None else ()):
                 t.record_stream(side)
-            torch.autograd.Variable._execution_engine.queue_callback(
-                lambda: main.wait_stream(side))
+            if not _side_pending:
+                torch.autograd.Variable._execution_engine.queue_callback(
+                    lambda: _join_side_wgrads(dev, notify=False))
+            _side_pending.append((side, gbufs, main))
         BT = B * T
         dx = None
         if ctx.needs_input_grad[0]:
@@ -784,7 +802,7 @@ class BLSTMLayerFn(torch.autograd.Function):
             N.call('asr_dropout', N.ptr(dx), N.ptr(dxm), dx.numel(), float(ctx.drop[0]),
                    int(ctx.drop[1]), N.stream_handle(dev))
             dx = dxm
-        return (dx,) + (None,) * (12 + ctx.n_graph)
+        return (dx,) + (None,) * (13 + ctx.n_graph)
 
 
 def convert_rows_bf16(src, rmap, nrows, ncols, drop=None):
@@ -831,35 +849,86 @@ def _blstm_wgrad(dg, dg_f32, x_op, x_map, y_op, T, gbufs, dev):
 
 
 _side_streams = {}
+_side_pending = []     # (side stream, gbufs, compute stream) of weight gradients not joined yet
+
+
+def _join_side_wgrads(dev, notify=True):
+    """Make the compute stream wait for the side-stream weight gradients
+    enqueued so far; notify 'grads' for each (gradient-ready buckets)."""
+    if not _side_pending:
+        return
+    for side, gbufs, main in _side_pending:
+        main.wait_stream(side)
+        if notify:
+            notify_grad_event('grads', gbufs)
+    del _side_pending[:]
+
+
+def _num_cus(dev):
+    return torch.cuda.get_device_properties(dev).multi_processor_count
+
+
+def _xg_grid(B, H, ncu):
+    """Work-groups of the persistent recurrence (lstm_xg.hip xg_rows): groups of
+    R = 8 utterances (16 when 8 would not fit) x direction x H / 16 slices."""
+    if H % 32 or H // 16 > 64 or os.environ.get('ASR_LSTM_XG', '1') == '0':
+        return 1 << 30        # not the tagged-granule recurrence
+    for R in (8, 16):
+        g = 2 * ((B + R - 1) // R) * (H // 16)
+        if g <= ncu:
+            return g
+    return 1 << 30
 
 
 def _wgrad_side_stream(dev, B, H):
-    """The CU-masked stream (upper half of the CUs) for the weight-gradient
-    GEMMs when ASR_OVERLAP_WGRAD=1, else None (weight gradients stay on the
-    main stream).  Also None in fp32 parity mode, without the persistent
-    recurrence, or when the backward recurrence is too large to keep its
-    co-resident work-groups (one per CU) within the other half."""
-    if compute_dtype() != BF16 or os.environ.get('ASR_OVERLAP_WGRAD', '0') != '1':
+    """Where the weight-gradient GEMMs of a BLSTM layer's backward run:
+    (stream, small_tiles) or None (main stream, default).
+
+    ASR_OVERLAP_WGRAD=1: a CU-masked side stream (upper half of the CUs), only
+    when the persistent backward recurrence fits in the other half.
+    ASR_OVERLAP_WGRAD=2: a plain side stream whose GEMMs use the 128 x 128
+    kernel only (64 KB of LDS, asr_gemm_set_small_tiles) while the backward
+    recurrence pins just under 96 KB (ASR_XG_PIN_BWD_KB), so one GEMM
+    work-group fits beside the recurrence's one work-group on every CU and the
+    weight gradients of layer l run during the recurrence of layer l - 1.
+    Default (auto): 2 when the recurrence leaves CUs free, else 0.
+    Both need bf16 mode and the persistent recurrence."""
+    mode = os.environ.get('ASR_OVERLAP_WGRAD', 'auto')
+    if compute_dtype() != BF16 or os.environ.get('ASR_LSTM_PERSIST', '1') == '0' or H % 32:
         return None
-    if os.environ.get('ASR_LSTM_PERSIST', '1') == '0' or H % 32:
+    if mode == 'auto':
+        # co-resident weight gradients pay off when the recurrence leaves CUs
+        # free (4x320 / 2x320 at B = 32: 160 of 256 CUs); when it fills the chip
+        # (5x512: 256 work-groups) the GEMMs' memory traffic slows each
+        # recurrence step by ~25 % and the step does not gain
+        ncu = _num_cus(dev)
+        mode = '2' if _xg_grid(B, H, ncu) < ncu else '0'
+    if mode not in ('1', '2'):
         return None
-    ent = _side_streams.get(dev.index)
+    key = (dev.index, mode)
+    ent = _side_streams.get(key)
     if ent is None:
-        ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-        h = ctypes.c_void_p()
-        with torch.cuda.device(dev):
-            N.call('asr_stream_create_cu_masked', ncu // 2, ncu - ncu // 2, ctypes.byref(h))
-        ent = (torch.cuda.ExternalStream(h.value, device=dev), ncu // 2)
-        _side_streams[dev.index] = ent
+        ncu = _num_cus(dev)
+        if mode == '1':
+            h = ctypes.c_void_p()
+            with torch.cuda.device(dev):
+                N.call('asr_stream_create_cu_masked', ncu // 2, ncu - ncu // 2, ctypes.byref(h))
+            ent = (torch.cuda.ExternalStream(h.value, device=dev), ncu // 2)
+        else:
+            # dynamic pin + the kernel's ~11 KB of static LDS stays <= 96 KB
+            os.environ.setdefault('ASR_XG_PIN_BWD_KB', '84')
+            ent = (torch.cuda.Stream(device=dev), ncu)
+        _side_streams[key] = ent
     stream, free_cus = ent
+    if mode == '2':
+        return stream, True
     # the persistent backward recurrence (lstm_xg.hip) pins one work-group per
     # CU: 2 directions x ceil(B / 8) utterance groups x H / 16 unit slices
-    grid_bwd = 2 * ((B + 7) // 8) * (H // 16)
-    return stream if grid_bwd <= free_cus else None
+    return (stream, False) if _xg_grid(B, H, 2 * free_cus) <= free_cus else None
 
 
 def blstm_layer(x_src, lens, T, w_ih, w_hh, b_ih, b_hh, perm=None, t_mul=1, t_add=0, gbufs=None,
-                graph_params=(), concat=False, drop=None):
+                graph_params=(), concat=False, drop=None, next_rec=False):
     """gbufs: optional (g_w_ih, g_w_hh, g_b_ih, g_b_hh) gradient views to accumulate
     into; default: the tensors' own .grad.  graph_params: the nn.Parameters the
     combined [fwd; rev] views alias -- passed only so autograd records that the
@@ -867,9 +936,12 @@ def blstm_layer(x_src, lens, T, w_ih, w_hh, b_ih, b_hh, perm=None, t_mul=1, t_ad
     concat: input row t is [x_src[t*t_mul + t_add]; x_src[t*t_mul + t_add + 1]]
     ('concat' subsampling of the previous layer, read in place).
     drop: optional (p, seed): the layer reads dropout(x_src) (asr_dropout's mask),
-    fused into the bf16 input staging; its input gradient gets the same mask."""
+    fused into the bf16 input staging; its input gradient gets the same mask.
+    next_rec: another BLSTM layer's backward recurrence follows this layer's in
+    the backward pass (the layer below), so ASR_OVERLAP_WGRAD=2 can run this
+    layer's weight gradients beside it."""
     return BLSTMLayerFn.apply(x_src, lens, T, perm, t_mul, t_add, gbufs, bool(concat), drop,
-                              w_ih, w_hh, b_ih, b_hh, *graph_params)
+                              bool(next_rec), w_ih, w_hh, b_ih, b_hh, *graph_params)
 
 
 # ---------------------------------------------------------------------------

@@ -214,3 +214,60 @@ def test_recurrence_give_up_skips_the_batch(cuda_dev):
             native_ops.raise_if_recurrence_failed(cuda_dev)
     finally:
         native_ops.set_compute_dtype('fp32')
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('mode', ['1', '2'])
+def test_wgrad_side_stream_matches_main_stream(mode, cuda_dev, monkeypatch):
+    """Weight gradients computed on the side stream (ASR_OVERLAP_WGRAD=1: CU-masked
+    half of the chip; 2: small-tile GEMMs co-resident with the next layer's
+    persistent backward recurrence) equal the main-stream ones up to the GEMM
+    kernels' summation order, at a shape that takes the persistent recurrence
+    (B = 16, H = 256, three layers, T = 160), and the recurrence did not give up."""
+    from pytorch_end2end_speech_recognition_amd import native_ops
+    kw = dict(input_size=40, encoder_type='lstm', encoder_bidirectional=True,
+              encoder_num_units=256, encoder_num_proj=0, encoder_num_layers=3, fc_list=[],
+              dropout_input=0, dropout_encoder=0, num_classes=29, parameter_init=0.1,
+              subsample_list=[], subsample_type='drop')
+    model = _build(kw)
+    rng = np.random.RandomState(11)
+    B, T = 16, 160
+    x_lens = np.sort(rng.randint(100, T + 1, B)).astype(np.int32)[::-1].copy()
+    x_lens[0] = T
+    y_lens = rng.randint(10, 30, B).astype(np.int32)
+    xs = rng.randn(B, T, 40).astype(np.float32)
+    for b in range(B):
+        xs[b, x_lens[b]:] = 0
+    ys = np.full((B, 30), -1, np.int32)
+    for b in range(B):
+        ys[b, :y_lens[b]] = rng.randint(0, 28, y_lens[b])
+    native_ops.set_compute_dtype('bf16')
+    grads, events = {}, {}
+    try:
+        model.set_cuda()
+        for m in ('0', mode):
+            monkeypatch.setenv('ASR_OVERLAP_WGRAD', m)
+            native_ops.recurrence_status(cuda_dev)             # clear
+            model.zero_grad()
+            ev = []
+            native_ops.set_grad_ready_hook(lambda e, arg=None: ev.append(e))
+            try:
+                loss = model(xs, ys, x_lens, y_lens)
+                loss.backward()
+            finally:
+                native_ops.set_grad_ready_hook(None)
+            torch.cuda.synchronize()
+            assert int(native_ops.recurrence_status(cuda_dev).max().item()) == 0
+            grads[m] = {k: p.grad.detach().cpu().numpy().copy()
+                        for k, p in model.named_parameters()}
+            events[m] = ev
+    finally:
+        native_ops.set_compute_dtype('fp32')
+    # gradient-ready notifications (DP buckets): every layer above the lowest is
+    # reported before the next recurrence in both modes
+    assert events['0'] == ['recurrence', 'grads'] * 3
+    assert events[mode][:5] == ['recurrence', 'grads', 'recurrence', 'grads', 'recurrence']
+    for k, g0 in grads['0'].items():
+        g1 = grads[mode][k]
+        scale = np.abs(g0).max() + 1e-12
+        assert np.abs(g1 - g0).max() / scale < 1e-4, (k, np.abs(g1 - g0).max(), scale)
