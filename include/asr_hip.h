@@ -216,6 +216,25 @@ int asr_lstm_backward_db(const float* dy, const void* whh_f, const void* whh_r, 
                          float* act_dg, const float* cst, uint16_t* dgbf, float* db_ih,
                          float* db_hh, void* workspace, size_t ws_bytes, void* stream);
 
+/* ------------------------------------------------------------ GRU layer
+ * Replaces the packed nn.GRU(bidirectional=True) of
+ * models/pytorch_v3/encoders/rnn.py:173-191 (fast path) / :226-233 (per layer).
+ * Gate order r, z, n; h0 = 0; outputs and state are 0 for t >= lens[b].
+ *   gx_act [B][T][6H] f32: in  x W_ih^T + b_ih (forward cols [0,3H), reverse [3H,6H))
+ *                          out r, z, n (post-activation), then dgx after backward
+ *   whh    [2][3H][H] f32 (forward then reverse), bhh [2][3H] f32
+ *   y      [B][T][2H] f32 out = [h_fwd ; h_rev];  ghn [B][T][2H] f32 out = W_hn h + b_hn
+ * Backward: dy [B][T][2H] (nullable = 0); writes dgx over gx_act and
+ * dgh [B][T][6H] = the gate gradients of W_hh h + b_hh; the weight / bias /
+ * input gradients are GEMMs and column sums of dgx and dgh.  One launch per
+ * time step (both directions), exact-f32 MFMA. */
+size_t asr_gru_workspace_bytes(int B, int H);
+int asr_gru_forward(float* gx_act, const float* whh, const float* bhh, const int32_t* lens, int B,
+                    int T, int H, float* y, float* ghn, void* stream);
+int asr_gru_backward(const float* dy, const float* whh, const int32_t* lens, int B, int T, int H,
+                     float* act_dgx, const float* ghn, const float* y, float* dgh,
+                     void* workspace, size_t ws_bytes, void* stream);
+
 /* ------------------------------------------------------------ optimizer
  * Replaces torch.nn.utils.clip_grad_norm(params, max_norm)
  * (utils/training/training_loop.py:46-50) + torch.optim Adam / SGD /

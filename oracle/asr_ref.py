@@ -38,6 +38,31 @@ def lstm_direction(x, lens, w_ih, w_hh, b_ih, b_hh, reverse):
     return torch.stack(outs, dim=1)
 
 
+def gru_direction(x, lens, w_ih, w_hh, b_ih, b_hh, reverse):
+    """nn.GRU direction (rnn.py:173-191, 226-233; torch's GRU equations), gate
+    order r, z, n: r = sig(W_ir x + b_ir + W_hr h + b_hr), z likewise,
+    n = tanh(W_in x + b_in + r * (W_hn h + b_hn)), h' = (1 - z) n + z h; h0 = 0
+    and the same packed-sequence semantics as lstm_direction."""
+    B, T, _ = x.shape
+    H = w_hh.shape[1]
+    gx = torch.matmul(x, w_ih.t()) + b_ih                    # [B, T, 3H]
+    h = x.new_zeros(B, H)
+    outs = [None] * T
+    lens_t = torch.as_tensor(np.asarray(lens), dtype=torch.long)
+    order = range(T - 1, -1, -1) if reverse else range(T)
+    for t in order:
+        gh = h @ w_hh.t() + b_hh
+        xr, xz, xn = gx[:, t].split(H, dim=1)
+        hr, hz, hn = gh.split(H, dim=1)
+        r = torch.sigmoid(xr + hr)
+        z = torch.sigmoid(xz + hz)
+        n = torch.tanh(xn + r * hn)
+        h_new = (1 - z) * n + z * h
+        h = h_new * (lens_t > t).to(x.dtype).unsqueeze(1)
+        outs[t] = h
+    return torch.stack(outs, dim=1)
+
+
 @torch.no_grad()
 def lstm_direction_bptt(x, lens, w_ih, w_hh, b_ih, b_hh, reverse, dy):
     """lstm_direction's forward plus an explicit O(T) backward (BPTT) for the
@@ -129,7 +154,8 @@ def vgg_front(p, prefix, cfg, xs, x_lens, masks=None, training=True):
 
 
 def blstm_encoder(p, prefix, cfg, xs, x_lens, capture_layer=0):
-    """RNNEncoder.forward (rnn.py:284-487) for rnn_type='lstm', bidirectional,
+    """RNNEncoder.forward (rnn.py:284-487) for rnn_type 'lstm' or 'gru'
+    (cfg['rnn_type']), bidirectional,
     dropout = 0, optional VGG front-end (cfg['conv_channels'], rnn.py:314-316),
     and the inter-layer ops of rnn.py:409-465 on every layer but the last:
     projection tanh(proj_l(x)) (cfg['num_proj']), subsampling 'drop'
@@ -159,17 +185,19 @@ def blstm_encoder(p, prefix, cfg, xs, x_lens, capture_layer=0):
             last_sub = n_layers - l_rev
             break
     res_list, captured = [], None
+    rnn = cfg.get('rnn_type', 'lstm')                         # rnn.py:162-246 module names
+    direction = gru_direction if rnn == 'gru' else lstm_direction
     for l in range(n_layers):
-        if fast:   # one multi-layer nn.LSTM: lstm.weight_ih_l{l}{_reverse}
-            names = [prefix + 'lstm.%s_l%d%s' % (n, l, s) for s in ('', '_reverse')
+        if fast:   # one multi-layer nn.LSTM / nn.GRU: lstm.weight_ih_l{l}{_reverse}
+            names = [prefix + '%s.%s_l%d%s' % (rnn, n, l, s) for s in ('', '_reverse')
                      for n in ('weight_ih', 'weight_hh', 'bias_ih', 'bias_hh')]
-        else:      # per-layer nn.LSTM: lstm_l{l}.weight_ih_l0{_reverse}
-            names = [prefix + 'lstm_l%d.%s_l0%s' % (l, n, s) for s in ('', '_reverse')
+        else:      # per-layer modules: lstm_l{l}.weight_ih_l0{_reverse}
+            names = [prefix + '%s_l%d.%s_l0%s' % (rnn, l, n, s) for s in ('', '_reverse')
                      for n in ('weight_ih', 'weight_hh', 'bias_ih', 'bias_hh')]
         T_out = int(lens.max())                              # pad_packed -> max len
         xs = xs[:, :T_out]
-        fw = lstm_direction(xs, lens, *[p[n] for n in names[:4]], reverse=False)
-        bw = lstm_direction(xs, lens, *[p[n] for n in names[4:]], reverse=True)
+        fw = direction(xs, lens, *[p[n] for n in names[:4]], reverse=False)
+        bw = direction(xs, lens, *[p[n] for n in names[4:]], reverse=True)
         xs = torch.cat([fw, bw], dim=2)
         if capture_layer and l == capture_layer - 1:
             captured = (xs, lens.astype(np.int32))

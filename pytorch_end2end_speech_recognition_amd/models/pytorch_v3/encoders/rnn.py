@@ -1,11 +1,12 @@
-"""RNNEncoder: the reference's (B)LSTM encoder (models/pytorch_v3/encoders/rnn.py)
-on the MI355X HIP layer op.
+"""RNNEncoder: the reference's (B)LSTM / (B)GRU encoder
+(models/pytorch_v3/encoders/rnn.py) on the MI355X HIP layer ops.
 
 Same constructor kwargs, same parameter names (``lstm.weight_ih_l{l}[_reverse]``
-for the fast path, ``lstm_l{l}.weight_ih_l0[_reverse]`` for the per-layer path:
-rnn.py:162-246) and the same torch RNG consumption at construction, so a model
-built under the same seed holds bit-identical initial weights.  ``nn.LSTM``
-modules are used only as parameter holders; their forward never runs.
+for the fast path, ``lstm_l{l}.weight_ih_l0[_reverse]`` for the per-layer path,
+``gru...`` likewise: rnn.py:162-246) and the same torch RNG consumption at
+construction, so a model built under the same seed holds bit-identical initial
+weights.  ``nn.LSTM`` / ``nn.GRU`` modules are used only as parameter holders;
+their forward never runs (GRU layers: native_ops.bgru_layer, csrc/gru.hip).
 
 Forward semantics (rnn.py:284-487): input dropout, the optional VGG front-end
 (encoders/cnn.py, rnn.py:143-160, 314-316), length sort (perm_idx is
@@ -43,9 +44,11 @@ class RNNEncoder(nn.Module):
             raise TypeError('subsample_type must be "drop" or "concat".')
         if num_layers_sub < 0 or (num_layers_sub > 1 and num_layers < num_layers_sub):
             raise ValueError('Set num_layers_sub between 1 to num_layers.')
+        if rnn_type not in ('lstm', 'gru', 'rnn'):
+            raise ValueError('rnn_type must be "lstm" or "gru" or "rnn".')
         unsupported = []
-        if rnn_type != 'lstm':
-            unsupported.append('rnn_type=%s' % rnn_type)
+        if rnn_type == 'rnn':
+            unsupported.append('rnn_type=rnn')
         if not bidirectional:
             unsupported.append('unidirectional')
         if nin or merge_bidirectional or not batch_first or not pack_sequence:
@@ -96,12 +99,13 @@ class RNNEncoder(nn.Module):
         # rnn.py:162 (batch_norm forces the per-layer modules, as in the reference)
         self.fast_impl = (sum(self.subsample_list) == 0 and self.num_proj == 0 and not residual and
                           not dense_residual and num_layers_sub == 0 and not batch_norm)
-        if self.fast_impl:   # rnn.py:162-198: one multi-layer nn.LSTM
-            self.lstm = nn.LSTM(input_size, hidden_size=num_units, num_layers=num_layers,
-                                bias=True, batch_first=batch_first, dropout=dropout_hidden,
-                                bidirectional=True)
+        cell = nn.LSTM if rnn_type == 'lstm' else nn.GRU
+        if self.fast_impl:   # rnn.py:162-198: one multi-layer nn.LSTM / nn.GRU
+            setattr(self, rnn_type,
+                    cell(input_size, hidden_size=num_units, num_layers=num_layers, bias=True,
+                         batch_first=batch_first, dropout=dropout_hidden, bidirectional=True))
             self.dropout_last = nn.Dropout(p=dropout_hidden)
-        else:                # rnn.py:200-251: one nn.LSTM per layer (+ projection)
+        else:                # rnn.py:200-251: one nn.LSTM / nn.GRU per layer (+ projection)
             for l in range(num_layers):
                 if l == 0:
                     din = input_size
@@ -109,9 +113,9 @@ class RNNEncoder(nn.Module):
                     din = self.num_proj if self.num_proj > 0 else num_units * 2
                     if subsample_type == 'concat' and self.subsample_list[l - 1]:
                         din *= 2
-                setattr(self, 'lstm_l%d' % l,
-                        nn.LSTM(din, hidden_size=num_units, num_layers=1, bias=True,
-                                batch_first=batch_first, dropout=0, bidirectional=True))
+                setattr(self, '%s_l%d' % (rnn_type, l),
+                        cell(din, hidden_size=num_units, num_layers=1, bias=True,
+                             batch_first=batch_first, dropout=0, bidirectional=True))
                 setattr(self, 'dropout_l%d' % l, nn.Dropout(p=dropout_hidden))
                 if l != num_layers - 1 and self.num_proj > 0:
                     setattr(self, 'proj_l%d' % l,
@@ -120,9 +124,9 @@ class RNNEncoder(nn.Module):
     # parameters of layer l: (w_ih_f, w_ih_r), (w_hh_f, w_hh_r), (b_ih_f, b_ih_r), (b_hh_f, b_hh_r)
     def _layer_params(self, l):
         if self.fast_impl:
-            mod, k = self.lstm, l
+            mod, k = getattr(self, self.rnn_type), l
         else:
-            mod, k = getattr(self, 'lstm_l%d' % l), 0
+            mod, k = getattr(self, '%s_l%d' % (self.rnn_type, l)), 0
         return [(getattr(mod, '%s_l%d' % (n, k)), getattr(mod, '%s_l%d_reverse' % (n, k)))
                 for n in ('weight_ih', 'weight_hh', 'bias_ih', 'bias_hh')]
 
@@ -174,9 +178,16 @@ class RNNEncoder(nn.Module):
             (w_ih, w_hh, b_ih, b_hh), gbufs = self._layer_tensors(l)
             lens_d = torch.from_numpy(lens.astype(np.int32)).to(dev, non_blocking=True)
             graph = tuple(p for pair in self._layer_params(l) for p in pair)
-            h = ops.blstm_layer(h, lens_d, T, w_ih, w_hh, b_ih, b_hh, perm=pm, t_mul=t_mul,
-                                t_add=t_add, gbufs=tuple(gbufs), graph_params=graph,
-                                concat=concat, drop=pending, next_rec=l > 0)
+            if self.rnn_type == 'gru':
+                if pending is not None:
+                    h = ops.dropout(h, pending[0], seed=pending[1])
+                h = ops.bgru_layer(h, lens_d, T, w_ih, w_hh, b_ih, b_hh, perm=pm, t_mul=t_mul,
+                                   t_add=t_add, gbufs=tuple(gbufs), graph_params=graph,
+                                   concat=concat)
+            else:
+                h = ops.blstm_layer(h, lens_d, T, w_ih, w_hh, b_ih, b_hh, perm=pm, t_mul=t_mul,
+                                    t_add=t_add, gbufs=tuple(gbufs), graph_params=graph,
+                                    concat=concat, drop=pending, next_rec=l > 0)
             pending = None
             if self.training and self.dropout_hidden_p > 0:
                 # same seed stream either way; fused when the next consumer is the

@@ -805,6 +805,95 @@ class BLSTMLayerFn(torch.autograd.Function):
         return (dx,) + (None,) * (13 + ctx.n_graph)
 
 
+class BGRULayerFn(torch.autograd.Function):
+    """Bidirectional GRU layer (nn.GRU, rnn.py:173-191 / :226-233) on the HIP
+    recurrence of csrc/gru.hip.  Same input addressing as BLSTMLayerFn (row map
+    with perm / subsampling / 'concat' rows read in place); parameters are the
+    combined [fwd; rev] views (w_ih [6H, Din], w_hh [6H, H], b_ih, b_hh [6H]).
+    The recurrence runs in f32 in both modes; the GEMMs take the library's
+    bf16 operand staging in bf16 mode."""
+
+    @staticmethod
+    def forward(ctx, x_src, lens, T, perm, t_mul, t_add, gbufs, concat, w_ih, w_hh, b_ih, b_hh,
+                *graph_params):
+        N.require_device(x_src, lens, w_ih, w_hh, b_ih, b_hh)
+        x_src = x_src.contiguous()
+        B, T_src, Dsrc = x_src.shape
+        Din = 2 * Dsrc if concat else Dsrc
+        assert w_ih.shape[1] == Din, (tuple(w_ih.shape), Din)
+        H = w_hh.shape[1]
+        dev = x_src.device
+        a_map = rowmap(Dsrc, stride_b=T_src * Dsrc, rows_per_b=T, t_mul=t_mul, t_add=t_add,
+                       t_limit=T_src, perm=perm)
+        gx = torch.empty(B, T, 6 * H, dtype=torch.float32, device=dev)
+        run_gemm([gemm_problem(operand(x_src, 0, a_map), operand(w_ih, 0, rowmap(Din)), gx,
+                               rowmap(6 * H), B * T, 6 * H, Din, bias=b_ih)], dev)
+        y = torch.empty(B, T, 2 * H, dtype=torch.float32, device=dev)
+        ghn = torch.empty(B, T, 2 * H, dtype=torch.float32, device=dev)
+        N.call('asr_gru_forward', N.ptr(gx), N.ptr(w_hh), N.ptr(b_hh), N.ptr(lens), B, T, H,
+               N.ptr(y), N.ptr(ghn), N.stream_handle(dev))
+        ctx.save_for_backward(x_src, w_ih, w_hh, b_ih, b_hh, lens, gx, ghn, y)
+        ctx.meta = (T, perm, t_mul, t_add, gbufs, Din)
+        ctx.n_graph = len(graph_params)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x_src, w_ih, w_hh, b_ih, b_hh, lens, act, ghn, y = ctx.saved_tensors
+        T, perm, t_mul, t_add, gbufs, Din = ctx.meta
+        B, T_src, Dsrc = x_src.shape
+        H = w_hh.shape[1]
+        dev = act.device
+        dy = dy.contiguous()
+        if gbufs is None:
+            gbufs = tuple(grad_buffer(p) for p in (w_ih, w_hh, b_ih, b_hh))
+        g_ih, g_hh, g_bih, g_bhh = gbufs
+        nb = N.query('asr_gru_workspace_bytes', B, H)
+        ws = _ws(nb, dev)
+        dgh = torch.empty(B, T, 6 * H, dtype=torch.float32, device=dev)
+        # the saved activations become dgx in place
+        N.call('asr_gru_backward', N.ptr(dy), N.ptr(w_hh), N.ptr(lens), B, T, H, N.ptr(act),
+               N.ptr(ghn), N.ptr(y), N.ptr(dgh), N.ptr(ws), nb, N.stream_handle(dev))
+        BT = B * T
+        x_map = rowmap(Dsrc, stride_b=T_src * Dsrc, rows_per_b=T, t_mul=t_mul, t_add=t_add,
+                       t_limit=T_src, perm=perm)
+        # dW_ih [6H, Din] += dgx^T x (both directions in one problem)
+        run_gemm([gemm_problem(operand(act, 1, rowmap(6 * H)), operand(x_src, 1, x_map), g_ih,
+                               rowmap(Din), 6 * H, Din, BT, beta=1.0)], dev)
+        # dW_hh[dir] += dgh_dir^T h_prev_dir ; h_prev = y[b, t-1, :H] (fwd), y[b, t+1, H:] (rev)
+        hp_f = rowmap(2 * H, stride_b=T * 2 * H, rows_per_b=T, t_add=-1, t_limit=T)
+        hp_r = rowmap(2 * H, stride_b=T * 2 * H, rows_per_b=T, t_add=1, t_limit=T)
+        run_gemm([
+            gemm_problem(operand(dgh, 1, rowmap(6 * H)), operand(y, 1, hp_f), g_hh, rowmap(H),
+                         3 * H, H, BT, beta=1.0),
+            gemm_problem(operand(dgh, 1, rowmap(6 * H), offset=3 * H),
+                         operand(y, 1, hp_r, offset=H), g_hh, rowmap(H), 3 * H, H, BT, beta=1.0,
+                         c_offset=3 * H * H),
+        ], dev)
+        colsum_accumulate(act.view(BT, 6 * H), g_bih)
+        colsum_accumulate(dgh.view(BT, 6 * H), g_bhh)
+        notify_grad_event('recurrence')
+        notify_grad_event('grads', gbufs)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if perm is None and t_mul == 1 and t_add == 0 and T == T_src and Din == Dsrc:
+                dx = torch.empty(B, T_src, Dsrc, dtype=torch.float32, device=dev)
+            else:
+                dx = torch.zeros(B, T_src, Dsrc, dtype=torch.float32, device=dev)
+            c_map = rowmap(Dsrc, stride_b=T_src * Dsrc, rows_per_b=T, t_mul=t_mul, t_add=t_add,
+                           t_limit=T_src, perm=perm)
+            run_gemm([gemm_problem(operand(act, 0, rowmap(6 * H)), operand(w_ih, 1, rowmap(Din)),
+                                   dx, c_map, BT, Din, 6 * H)], dev)
+        return (dx,) + (None,) * (11 + ctx.n_graph)
+
+
+def bgru_layer(x_src, lens, T, w_ih, w_hh, b_ih, b_hh, perm=None, t_mul=1, t_add=0, gbufs=None,
+               graph_params=(), concat=False):
+    """The bidirectional GRU counterpart of blstm_layer (same addressing)."""
+    return BGRULayerFn.apply(x_src, lens, T, perm, t_mul, t_add, gbufs, bool(concat),
+                             w_ih, w_hh, b_ih, b_hh, *graph_params)
+
+
 def convert_rows_bf16(src, rmap, nrows, ncols, drop=None):
     """Dense bf16 [nrows, ncols] copy of the rows of `src` selected by a row map;
     drop=(p, seed): of dropout(src) with asr_dropout's mask, in the same pass."""

@@ -285,6 +285,12 @@ def case_ctc_model():
                                 parameter_init=0.1, subsample_list=[], subsample_type='drop')),
     ]
     specs += _ctc_variant_specs()
+    # GRU encoders (rnn.py:173-191 fast nn.GRU, :226-233 per layer): fast path and
+    # per-layer path with 'drop' subsampling
+    specs += [
+        ('model_ctc_gru_fast', dict(specs[1][1], encoder_type='gru')),
+        ('model_ctc_gru_sub', dict(specs[0][1], encoder_type='gru')),
+    ]
     only = _selected()
     for name, kw in specs:
         if only and name not in only:

@@ -22,7 +22,8 @@ def _build(kw):
     return CTC(**kw)
 
 
-CTC_MODELS = ['model_ctc_sub', 'model_ctc_fast', 'model_ctc_proj', 'model_ctc_concat',
+CTC_MODELS = ['model_ctc_sub', 'model_ctc_fast', 'model_ctc_gru_fast', 'model_ctc_gru_sub',
+              'model_ctc_proj', 'model_ctc_concat',
               'model_ctc_proj_concat', 'model_ctc_res', 'model_ctc_dres']
 
 
@@ -271,3 +272,49 @@ def test_wgrad_side_stream_matches_main_stream(mode, cuda_dev, monkeypatch):
         g1 = grads[mode][k]
         scale = np.abs(g0).max() + 1e-12
         assert np.abs(g1 - g0).max() / scale < 1e-4, (k, np.abs(g1 - g0).max(), scale)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('dtype', ['fp32', 'bf16'])
+def test_gru_encoder_vs_oracle(dtype, cuda_dev):
+    """BGRU CTC model (rnn.py:173-191 / :226-233, per-layer path with 'drop'
+    subsampling) at H = 96, three layers, ragged lengths, vs the fp32 CPU
+    oracle (asr_ref.gru_direction): loss and every gradient (fp32 mode: 1e-4 /
+    2e-3 of max |g|; bf16 mode: the GEMMs on bf16 operands, 2e-2 / 5e-2)."""
+    from pytorch_end2end_speech_recognition_amd import native_ops
+    kw = dict(input_size=24, encoder_type='gru', encoder_bidirectional=True,
+              encoder_num_units=96, encoder_num_proj=0, encoder_num_layers=3, fc_list=[],
+              dropout_input=0, dropout_encoder=0, num_classes=11, parameter_init=0.1,
+              subsample_list=[False, True, False], subsample_type='drop')
+    model = _build(kw)
+    sd = {k: v.clone() for k, v in model.state_dict().items()}
+    rng = np.random.RandomState(8)
+    B, T = 5, 57
+    x_lens = np.array([57, 40, 52, 31, 45], np.int32)
+    y_lens = np.array([7, 5, 6, 3, 4], np.int32)
+    xs = rng.randn(B, T, 24).astype(np.float32)
+    for b in range(B):
+        xs[b, x_lens[b]:] = 0
+    ys = np.full((B, 7), -1, np.int32)
+    for b in range(B):
+        ys[b, :y_lens[b]] = rng.randint(0, 11, y_lens[b])
+    from test_oracle_golden import ctc_cfg
+    p = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+    ref, _, _, _ = asr_ref.ctc_model_loss(p, ctc_cfg(kw), xs, ys, x_lens, y_lens)
+    ref.backward()
+    native_ops.set_compute_dtype(dtype)
+    try:
+        model.set_cuda()
+        model.zero_grad()
+        loss = model(xs, ys, x_lens, y_lens)
+        loss.backward()
+        torch.cuda.synchronize()
+    finally:
+        native_ops.set_compute_dtype('fp32')
+    tl, tg = (1e-4, 2e-3) if dtype == 'fp32' else (2e-2, 5e-2)
+    assert abs(loss.item() - ref.item()) / abs(ref.item()) < tl, (loss.item(), ref.item())
+    for k, prm in model.named_parameters():
+        ga = p[k].grad.numpy()
+        gw = prm.grad.cpu().numpy()
+        scale = np.abs(ga).max() + 1e-6
+        assert np.abs(gw - ga).max() / scale < tg, (k, np.abs(gw - ga).max(), scale)

@@ -65,7 +65,8 @@ def test_attention_step_oracle_matches_golden():
         np.testing.assert_allclose(_g(v), g[k], rtol=1e-4, atol=1e-6, err_msg=k)
 
 
-CTC_MODELS = ['model_ctc_sub', 'model_ctc_fast', 'model_ctc_proj', 'model_ctc_concat',
+CTC_MODELS = ['model_ctc_sub', 'model_ctc_fast', 'model_ctc_gru_fast', 'model_ctc_gru_sub',
+              'model_ctc_proj', 'model_ctc_concat',
               'model_ctc_proj_concat', 'model_ctc_res', 'model_ctc_dres']
 
 
@@ -75,7 +76,8 @@ def ctc_cfg(kw):
                 fc_list=kw['fc_list'], num_proj=kw.get('encoder_num_proj', 0),
                 subsample_type=kw.get('subsample_type', 'drop'),
                 residual=kw.get('encoder_residual', False),
-                dense_residual=kw.get('encoder_dense_residual', False))
+                dense_residual=kw.get('encoder_dense_residual', False),
+                rnn_type=kw.get('encoder_type', 'lstm'))
 
 
 @pytest.mark.parametrize('name', CTC_MODELS)
