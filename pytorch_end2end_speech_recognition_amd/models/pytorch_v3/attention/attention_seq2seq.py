@@ -341,12 +341,114 @@ class AttentionSeq2seq(ModelBase):
         """:866-915.  Returns (best_hyps int64 [B, T_out], aw [B, T_out, T_in],
         perm_idx), rows in the encoder's length-sorted order like the reference."""
         self.eval()
-        if beam_width != 1:
-            raise NotImplementedError('attention beam search (attention_seq2seq.py:1037-1237)')
         xs_d = self.np2var(xs, dtype='float')
         enc_out, enc_lens_d, _ = self._encode(xs_d, x_lens)
-        best_hyps, aw = self._decode_infer_greedy(enc_out, enc_lens_d, max_decode_len)
+        if beam_width == 1:
+            best_hyps, aw = self._decode_infer_greedy(enc_out, enc_lens_d, max_decode_len)
+        else:
+            best_hyps, aw = self._decode_infer_beam(enc_out, self.encoder.last_lens_np, beam_width,
+                                                    max_decode_len, min_decode_len,
+                                                    length_penalty, coverage_penalty)
         return best_hyps, aw, self.encoder.last_perm_np.copy()
+
+    def _decode_infer_beam(self, enc_out, x_lens, beam_width, max_decode_len, min_decode_len,
+                           length_penalty, coverage_penalty, task=0, dir='fwd'):
+        """:1038-1237 (bahdanau order).  Utterance by utterance like the
+        reference, each over its own frames (enc_out[b, :x_len]); the live
+        hypotheses of an utterance advance as ONE batch per step on the HIP ops
+        (embedding, LSTMCell, the location-attention step, the bottleneck and
+        output GEMMs), and the beam bookkeeping -- log-softmax, top-k, the
+        min-length <eos> rule, length penalty, stable score sort, completion --
+        runs on the host over the [n, V] log-probabilities of the step, as the
+        reference does with its per-step reads.  Returns (best_hyps: an int64
+        [B, L] array when every hypothesis has the same length, else an object
+        array of int64 rows, each ending with <eos> when it completed; aw: list
+        of [L_b, x_len_b] float32 arrays)."""
+        if coverage_penalty > 0:
+            raise NotImplementedError('coverage penalty (the reference raises too, :1150)')
+        att = getattr(self, 'attend_%d_%s' % (task, dir))
+        dec_mod = getattr(self, 'decoder_%d_%s' % (task, dir))
+        W_d, W_c = getattr(self, 'W_d_%d_%s' % (task, dir)), getattr(self, 'W_c_%d_%s' % (task, dir))
+        fc = getattr(self, 'fc_%d_%s' % (task, dir))
+        embed = getattr(self, 'embed_%d' % task)
+        sos, eos = getattr(self, 'sos_%d' % task), getattr(self, 'eos_%d' % task)
+        D = getattr(self, 'decoder_num_units_%d' % task)
+        nl = dec_mod.num_layers
+        dev = enc_out.device
+        B, _, E = enc_out.shape
+        lens = np.asarray(x_lens).reshape(-1).astype(np.int64)
+        enc_a = att.W_enc_head0(enc_out)                            # [B, T, A]
+        A = enc_a.shape[2]
+        h0 = self._init_h0(enc_out, task, dir)
+        best, aws = [], []
+        for b in range(B):
+            L = int(lens[b])
+            enc_b = enc_out[b:b + 1, :L].contiguous()
+            enc_a_b = enc_a[b:b + 1, :L].contiguous()
+            zero = torch.zeros(1, D, dtype=enc_out.dtype, device=dev)
+            h_init = h0[b:b + 1] if h0 is not None else zero
+            state = dict(h=[h_init] * nl, c=[zero] * nl, dec=h_init,
+                         ctx=torch.zeros(1, E, dtype=enc_out.dtype, device=dev),
+                         aw=torch.zeros(1, L, dtype=enc_out.dtype, device=dev))
+            beam = [dict(hyp=[sos], score=0.0, row=0, hist=[])]
+            complete, step_aw = [], []
+            for t in range(max_decode_len):
+                n = len(beam)
+                if n == 0:
+                    break
+                rows = torch.tensor([c['row'] for c in beam], dtype=torch.long, device=dev)
+                hs = [x.index_select(0, rows) for x in state['h']]
+                cs = [x.index_select(0, rows) for x in state['c']]
+                if t == 0:
+                    dec = state['dec'].index_select(0, rows)
+                else:
+                    toks = np.array([c['hyp'][-1] for c in beam], np.int64).reshape(n, 1)
+                    y = embed(torch.from_numpy(toks).to(dev), toks)          # [n, 1, emb]
+                    dec_in = torch.cat([y, state['ctx'].index_select(0, rows).unsqueeze(1)],
+                                       dim=-1)
+                    dec3, (hs, cs) = dec_mod(dec_in, (hs, cs))
+                    dec = dec3.squeeze(1)
+                ctx3, aw3 = att(enc_b.expand(n, L, E).contiguous(),
+                                enc_a_b.expand(n, L, A).contiguous().unsqueeze(3), [L] * n,
+                                dec.unsqueeze(1), state['aw'].index_select(0, rows).unsqueeze(2))
+                ctx, aw_t = ctx3.squeeze(1), aw3.squeeze(2)
+                logits = fc(ops.tanh(ops.linear2(dec, W_d.fc.weight, W_d.fc.bias, ctx,
+                                                 W_c.fc.weight, W_c.fc.bias)))
+                lg = logits.float().cpu().numpy()
+                mx = lg.max(axis=1, keepdims=True)                          # log_softmax (f32)
+                lp = lg - mx - np.log(np.exp(lg - mx).sum(axis=1, keepdims=True))
+                k_top = min(beam_width, lp.shape[1])
+                order = np.argsort(-lp, axis=1, kind='stable')[:, :k_top]   # topk, sorted
+                state = dict(h=hs, c=cs, dec=dec, ctx=ctx, aw=aw_t)
+                step_aw.append(aw_t)
+                new = []
+                for i in range(n):
+                    for k in range(k_top):
+                        tok = int(order[i, k])
+                        if tok == eos and len(beam[i]['hyp']) < min_decode_len:
+                            continue
+                        new.append(dict(hyp=beam[i]['hyp'] + [tok],
+                                        score=beam[i]['score'] + float(lp[i, tok]) + length_penalty,
+                                        row=i, hist=beam[i]['hist'] + [(t, i)]))
+                new.sort(key=lambda c: c['score'], reverse=True)     # stable, as sorted()
+                not_complete = []
+                for cand in new[:beam_width]:
+                    (complete if cand['hyp'][-1] == eos else not_complete).append(cand)
+                if len(complete) >= beam_width:
+                    complete = complete[:beam_width]
+                    break
+                beam = not_complete[:beam_width]
+            if len(complete) == 0:
+                complete = beam
+            complete.sort(key=lambda c: c['score'], reverse=True)
+            top = complete[0]
+            best.append(np.array(top['hyp'][1:], dtype=np.int64))
+            aw_rows = [step_aw[t][i] for t, i in top['hist']]
+            aws.append(torch.stack(aw_rows).cpu().numpy() if aw_rows
+                       else np.zeros((0, L), np.float32))
+        if len(set(len(h) for h in best)) <= 1:
+            return np.array(best), aws
+        return np.array(best + [None], dtype=object)[:-1], aws
 
     def _decode_infer_greedy(self, enc_out, x_lens, max_decode_len, task=0, dir='fwd'):
         """:917-1036 (bahdanau order, forward decoder): the whole loop is one

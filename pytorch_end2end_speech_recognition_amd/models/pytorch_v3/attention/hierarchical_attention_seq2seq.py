@@ -222,18 +222,25 @@ class HierarchicalAttentionSeq2seq(AttentionSeq2seq):
 
     def decode(self, xs, x_lens, beam_width, max_decode_len, min_decode_len=0,
                length_penalty=0, coverage_penalty=0, task_index=0, **kwargs):
-        """:569-648 (greedy): task_index 0 decodes words from the top layer,
-        1 characters from layer encoder_num_layers_sub."""
+        """:569-648 (greedy or beam search; the joint word/char decodings
+        are not provided): task_index 0 decodes words from the top layer, 1
+        characters from layer encoder_num_layers_sub."""
         import torch
+        if kwargs.get('joint_decoding') is not None:
+            raise NotImplementedError('joint word/char decoding (:620-880)')
         with torch.no_grad():
             self.eval()
-            if beam_width != 1:
-                raise NotImplementedError('attention beam search')
             xs_d = self.np2var(xs, dtype='float')
             enc_out, enc_lens_d, enc_sub, lens_sub_d, _ = self._encode(xs_d, x_lens,
                                                                        is_multi_task=True)
             if task_index == 0:
-                hyps, aw = self._decode_infer_greedy(enc_out, enc_lens_d, max_decode_len, task=0)
+                enc, lens_d, lens_np = enc_out, enc_lens_d, self.encoder.last_lens_np
             else:
-                hyps, aw = self._decode_infer_greedy(enc_sub, lens_sub_d, max_decode_len, task=1)
+                enc, lens_d, lens_np = enc_sub, lens_sub_d, self.encoder.last_lens_sub_np
+            if beam_width == 1:
+                hyps, aw = self._decode_infer_greedy(enc, lens_d, max_decode_len, task=task_index)
+            else:
+                hyps, aw = self._decode_infer_beam(enc, lens_np, beam_width, max_decode_len,
+                                                   min_decode_len, length_penalty,
+                                                   coverage_penalty, task=task_index)
             return hyps, aw, self.encoder.last_perm_np.copy()

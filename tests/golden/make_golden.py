@@ -687,6 +687,150 @@ def case_attention_decode():
               perm=np.asarray(perm).astype(np.int64), **_sd(model))
 
 
+def _install_beam_shims():
+    """Harness-only shims for AttentionSeq2seq._decode_infer_beam (torch-0.3 /
+    numpy < 1.24 era code on torch 2.10 / numpy 2.2):
+      5. ``.data[0]`` on a 0-dim tensor (a scalar Variable's value in torch 0.3,
+         attention_seq2seq.py:1072,1138) returns the tensor itself;
+      6. ``np.array`` of ragged hypothesis lists returns an object array (numpy
+         < 1.24 behaviour, attention_seq2seq.py:1235) instead of raising."""
+    base_getitem = torch.Tensor.__getitem__
+
+    def getitem(self, idx):
+        if self.dim() == 0 and isinstance(idx, int) and idx == 0:
+            return self
+        return base_getitem(self, idx)
+    torch.Tensor.__getitem__ = getitem
+
+    from models.pytorch_v3.attention import attention_seq2seq as asq
+
+    class _NP(types.ModuleType):
+        def __getattr__(self, k):
+            return getattr(np, k)
+
+    npx = _NP('numpy_ragged')
+
+    def array(obj, *a, **k):
+        try:
+            return np.array(obj, *a, **k)
+        except ValueError:
+            out = np.empty(len(obj), dtype=object)
+            for i, o in enumerate(obj):
+                out[i] = o
+            return out
+    npx.array = array
+    asq.np = npx
+
+
+def case_attention_beam():
+    """AttentionSeq2seq.decode(beam_width > 1) (attention_seq2seq.py:1038-1237)
+    on random-init models (uniform +-init): the seed is the first of 1623, ...
+    whose beam output has at least three distinct tokens and hypotheses of
+    different lengths (some complete with <eos> before max_decode_len)."""
+    from models.pytorch_v3.attention.attention_seq2seq import AttentionSeq2seq
+    _install_beam_shims()
+    only = _selected()
+    rng0 = np.random.RandomState(6)
+    B, T = 4, 22
+    x_lens = np.array([22, 17, 20, 11], np.int32)
+    xs = rng0.randn(B, T, 8).astype(np.float32)
+    for b in range(B):
+        xs[b, x_lens[b]:] = 0
+    base = dict(input_size=8, encoder_type='lstm', encoder_bidirectional=True,
+                encoder_num_units=6, encoder_num_proj=0, encoder_num_layers=2,
+                attention_type='location', attention_dim=7, decoder_type='lstm',
+                decoder_num_units=9, decoder_num_layers=1, embedding_dim=4,
+                dropout_input=0, dropout_encoder=0, dropout_decoder=0, dropout_embedding=0,
+                num_classes=6, parameter_init=0.1, subsample_list=[False, True],
+                subsample_type='drop', attention_conv_num_channels=3,
+                attention_conv_width=5, bottleneck_dim=11, decoding_order='bahdanau',
+                ctc_loss_weight=0, label_smoothing_prob=0, init_dec_state='zero')
+    specs = [('beam_att', base, 0.6, dict(beam_width=3, max_decode_len=12)),
+             ('beam_att_first', dict(base, init_dec_state='first', sharpening_factor=1.5), 0.6,
+              dict(beam_width=4, max_decode_len=10, min_decode_len=3, length_penalty=0.1)),
+             ('beam_att_wide', dict(base, num_classes=9), 0.8,
+              dict(beam_width=5, max_decode_len=14, length_penalty=-0.05))]
+    for name, kw, scale, opts in specs:
+        if only and name not in only:
+            continue
+        for seed in range(1623, 1623 + 500):
+            torch.manual_seed(seed)
+            model = AttentionSeq2seq(**kw)
+            for p in model.parameters():
+                torch.nn.init.uniform_(p, -scale, scale)
+            with torch.no_grad():   # torch-0.3 volatile decoding (deepcopy of non-leaf states)
+                hyps, aw, perm = model.decode(xs, x_lens, **opts)
+            hl = np.array([len(h) for h in hyps], np.int32)
+            toks = np.concatenate([np.asarray(h, np.int64) for h in hyps])
+            if len(np.unique(toks)) >= 3 and len(np.unique(hl)) >= 2:
+                break
+        else:
+            raise RuntimeError('no seed found for ' + name)
+        _save(name, kwargs=np.array(json.dumps(kw)), opts=np.array(json.dumps(opts)),
+              seed=np.array([seed]), xs=xs, x_lens=x_lens, hyp_flat=toks, hyp_lens=hl,
+              aw_flat=np.concatenate([np.asarray(a, np.float32).reshape(-1) for a in aw]),
+              perm=np.asarray(perm).astype(np.int64), **_sd(model))
+
+
+def case_hier_attention_beam():
+    """HierarchicalAttentionSeq2seq.decode(beam_width=3) for the word task
+    (task_index 0, top layer) and the character task (task_index 1, layer
+    encoder_num_layers_sub), random-init model as in case_attention_beam."""
+    from models.pytorch_v3.attention.hierarchical_attention_seq2seq import \
+        HierarchicalAttentionSeq2seq
+    _install_beam_shims()
+    if _selected() and 'beam_hatt' not in _selected():
+        return
+    kw = dict(input_size=8, encoder_type='lstm', encoder_bidirectional=True,
+              encoder_num_units=6, encoder_num_proj=0, encoder_num_layers=3,
+              encoder_num_layers_sub=2, attention_type='location', attention_dim=7,
+              decoder_type='lstm', decoder_num_units=9, decoder_num_units_sub=7,
+              decoder_num_layers=1, decoder_num_layers_sub=1, embedding_dim=4,
+              embedding_dim_sub=3, dropout_input=0, dropout_encoder=0, dropout_decoder=0,
+              dropout_embedding=0, num_classes=7, num_classes_sub=6, parameter_init=0.1,
+              subsample_list=[False, True, False], subsample_type='drop',
+              attention_conv_num_channels=3, attention_conv_width=5, bottleneck_dim=11,
+              bottleneck_dim_sub=8, decoding_order='bahdanau', init_dec_state='zero',
+              main_loss_weight=0.5, sub_loss_weight=0.5, ctc_loss_weight_sub=0)
+    rng0 = np.random.RandomState(9)
+    B, T = 3, 22
+    x_lens = np.array([22, 19, 14], np.int32)
+    xs = rng0.randn(B, T, 8).astype(np.float32)
+    for b in range(B):
+        xs[b, x_lens[b]:] = 0
+    opts = dict(beam_width=3, max_decode_len=10)
+    for seed in range(1623, 1623 + 500):
+        torch.manual_seed(seed)
+        model = HierarchicalAttentionSeq2seq(**kw)
+        for p in model.parameters():
+            torch.nn.init.uniform_(p, -0.6, 0.6)
+        out = {}
+        with torch.no_grad():
+            for task in (0, 1):
+                out[task] = model.decode(xs, x_lens, task_index=task, **opts)
+        ok, varied = True, False
+        for task in (0, 1):
+            hl = np.array([len(h) for h in out[task][0]])
+            toks = np.concatenate([np.asarray(h, np.int64) for h in out[task][0]])
+            ok &= len(np.unique(toks)) >= 2
+            varied |= len(np.unique(hl)) >= 2
+        ok &= varied
+        if ok:
+            break
+    else:
+        raise RuntimeError('no seed found for beam_hatt')
+    arrays = {}
+    for task in (0, 1):
+        hyps, aw, perm = out[task]
+        arrays['hyp_flat_%d' % task] = np.concatenate([np.asarray(h, np.int64) for h in hyps])
+        arrays['hyp_lens_%d' % task] = np.array([len(h) for h in hyps], np.int32)
+        arrays['aw_flat_%d' % task] = np.concatenate([np.asarray(a, np.float32).reshape(-1)
+                                                      for a in aw])
+        arrays['perm'] = np.asarray(perm).astype(np.int64)
+    _save('beam_hatt', kwargs=np.array(json.dumps(kw)), opts=np.array(json.dumps(opts)),
+          seed=np.array([seed]), xs=xs, x_lens=x_lens, **arrays, **_sd(model))
+
+
 if __name__ == '__main__':
     _install_shims()
     if _selected():          # regenerate only the named model_ctc_* / dec_* cases
@@ -695,6 +839,8 @@ if __name__ == '__main__':
         case_attention_decode()
         case_hier_attention_model()
         case_attention_prod()
+        case_attention_beam()
+        case_hier_attention_beam()
         if 'loader' in _selected():
             case_loader()
         sys.exit(0)
@@ -709,3 +855,5 @@ if __name__ == '__main__':
     case_attention_prod()
     case_attention_decode()
     case_loader()
+    case_attention_beam()
+    case_hier_attention_beam()

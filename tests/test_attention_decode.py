@@ -59,3 +59,62 @@ def test_greedy_decode_matches_golden(name, precision, cuda_dev):
         # step 0 -- no feedback yet -- is compared
         np.testing.assert_array_equal(hyps[:, 0], d['best_hyps'][:, 0])
         np.testing.assert_allclose(aw[:, 0], d['aw'][:, 0], rtol=5e-2, atol=2e-2)
+
+
+BEAM_NAMES = ['beam_att', 'beam_att_first', 'beam_att_wide']
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name', BEAM_NAMES)
+def test_beam_decode_matches_golden(name, cuda_dev):
+    """Beam search (attention_seq2seq.py:1038-1237): per utterance over its own
+    frames, top-k of the f32 log-softmax, <eos> below min_decode_len skipped,
+    length penalty, stable score sort, completion at beam_width complete
+    hypotheses -- hypotheses (incl. their final <eos>) bit-exact and the best
+    hypothesis' attention weights vs the reference, fp32 mode."""
+    from pytorch_end2end_speech_recognition_amd import native_ops
+    from pytorch_end2end_speech_recognition_amd.models.pytorch_v3.attention.attention_seq2seq \
+        import AttentionSeq2seq
+    d = golden(name)
+    kw = json.loads(str(d['kwargs']))
+    opts = json.loads(str(d['opts']))
+    sd, _ = golden_params(d)
+    torch.manual_seed(int(d['seed'][0]))
+    model = AttentionSeq2seq(**kw)
+    model.load_state_dict(sd)
+    model.set_cuda()
+    native_ops.set_compute_dtype('fp32')
+    hyps, aw, perm = model.decode(d['xs'], d['x_lens'], **opts)
+    np.testing.assert_array_equal(perm, d['perm'])
+    lens = np.array([len(h) for h in hyps], np.int32)
+    np.testing.assert_array_equal(lens, d['hyp_lens'])
+    np.testing.assert_array_equal(np.concatenate([np.asarray(h) for h in hyps]), d['hyp_flat'])
+    got = np.concatenate([np.asarray(a, np.float32).reshape(-1) for a in aw])
+    np.testing.assert_allclose(got, d['aw_flat'], rtol=1e-3, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_hierarchical_beam_decode_matches_golden(cuda_dev):
+    """HierarchicalAttentionSeq2seq.decode with beam_width 3 for both tasks
+    (word decoder on the top layer, character decoder on layer
+    encoder_num_layers_sub) vs the reference, fp32 mode."""
+    from pytorch_end2end_speech_recognition_amd import native_ops
+    from pytorch_end2end_speech_recognition_amd.models.pytorch_v3.attention.\
+        hierarchical_attention_seq2seq import HierarchicalAttentionSeq2seq
+    d = golden('beam_hatt')
+    kw = json.loads(str(d['kwargs']))
+    opts = json.loads(str(d['opts']))
+    sd, _ = golden_params(d)
+    torch.manual_seed(int(d['seed'][0]))
+    model = HierarchicalAttentionSeq2seq(**kw)
+    model.load_state_dict(sd)
+    model.set_cuda()
+    native_ops.set_compute_dtype('fp32')
+    for task in (0, 1):
+        hyps, aw, perm = model.decode(d['xs'], d['x_lens'], task_index=task, **opts)
+        np.testing.assert_array_equal(perm, d['perm'])
+        np.testing.assert_array_equal([len(h) for h in hyps], d['hyp_lens_%d' % task])
+        np.testing.assert_array_equal(np.concatenate([np.asarray(h) for h in hyps]),
+                                      d['hyp_flat_%d' % task])
+        got = np.concatenate([np.asarray(a, np.float32).reshape(-1) for a in aw])
+        np.testing.assert_allclose(got, d['aw_flat_%d' % task], rtol=1e-3, atol=1e-5)
