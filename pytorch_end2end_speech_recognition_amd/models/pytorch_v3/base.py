@@ -107,10 +107,20 @@ class ModelBase(nn.Module):
         self._rebind()
 
     def _rebind(self):
+        views = []
         for p, o in self._flat_index:
             n = p.numel()
             p.data = self._flat_param[o:o + n].view(p.shape)
             p.grad = self._flat_grad[o:o + n].view(p.shape)
+            views.append((p, p.grad))
+        self._grad_views = views
+
+    def _rebind_grads(self):
+        """Re-attach only the gradient views something replaced (identity
+        checks: the per-step zero_grad path, ~60 parameters)."""
+        for p, v in self._grad_views:
+            if p.grad is not v:
+                p.grad = v
 
     def flat_view(self, first_param, numel, grad=False):
         """Contiguous view starting at `first_param` (e.g. an LSTM fwd+rev pair)."""
@@ -154,7 +164,7 @@ class ModelBase(nn.Module):
 
     def zero_grad(self, set_to_none=False):
         self._flat_grad.zero_()
-        self._rebind()
+        self._rebind_grads()
 
     # ------------------------------------------------------------ properties
     @property

@@ -127,8 +127,13 @@ def colsum_accumulate(g2d, out0, out1=None, alpha=1.0):
 # bf16 mode stages f32 GEMM operands in bf16 (one conversion pass) when a
 # product is at least this large, so it takes the bf16 fast / 8-wave kernels
 # instead of the generic kernel converting inside its loads (the word-level CTC
-# head, 8000 x 640 x 10001, ran at ~140 TF/s that way).
+# head, 8000 x 640 x 10001, ran at ~140 TF/s that way).  The padded pitches
+# also put backward products whose K is the output width (the 29-class CTC
+# head's dX, K = 29) on the fast kernels, so such layers are staged from
+# 250 MFLOP (the 5x512 CTC head, 32000 x 1024 x 29: -0.1 ms/step); staging a
+# layer whose width is already a multiple of 8 below 2 GFLOP measured slower.
 _STAGE_FLOPS = 2e9
+_STAGE_FLOPS_RAGGED = float(os.environ.get("ASR_LINEAR_STAGE_FLOPS", "2.5e8"))
 
 
 def _staged(t, rows, cols, ld=None):
@@ -151,7 +156,9 @@ class LinearFn(torch.autograd.Function):
         Nout = weight.shape[0]
         M = x.numel() // K
         y = torch.empty(*x.shape[:-1], Nout, dtype=torch.float32, device=x.device)
-        stage = compute_dtype() == BF16 and 2.0 * M * Nout * K >= _STAGE_FLOPS
+        flops = 2.0 * M * Nout * K
+        stage = compute_dtype() == BF16 and (
+            flops >= _STAGE_FLOPS or (Nout % 8 != 0 and flops >= _STAGE_FLOPS_RAGGED))
         # staged copies: x [M][Kp], weight [Np][Kp] (rows Nout.. and columns K.. zero)
         Kp, Np = ((K + 7) // 8 * 8, (Nout + 7) // 8 * 8) if stage else (K, Nout)
         if stage:

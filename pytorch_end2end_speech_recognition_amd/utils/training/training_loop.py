@@ -131,8 +131,13 @@ def _step(model, forward, clip_grad_norm, n_losses, grad_scale):
         if clip_grad_norm > 0:
             torch.nn.utils.clip_grad_norm_(model.parameters(), clip_grad_norm)
         model.optimizer.step()
-    vals = [float(l.item()) for l in losses] if losses is not None else [0.] * n_losses
-    if guard is not None and int(guard.max().item()):
+    # ONE host read for the losses and the guard (each .item() is a full sync)
+    parts = [l.detach().reshape(-1)[:1].float() for l in losses] if losses is not None else []
+    if guard is not None:
+        parts.append(guard.float())
+    host = torch.cat(parts).tolist() if parts else []
+    vals = host[:n_losses] if losses is not None else [0.] * n_losses
+    if guard is not None and max(host[-guard.numel():]) > 0:
         # the fused step left the weights untouched; undo its step count
         if hasattr(model.optimizer, 'undo_step_count'):
             model.optimizer.undo_step_count()
