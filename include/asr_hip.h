@@ -148,6 +148,11 @@ typedef struct {
   float alpha, beta;
   int batch;          /* <= 1: single; else `batch` independent products */
   long long batch_stride_a, batch_stride_b, batch_stride_c; /* elements */
+  /* drop_p > 0: the written value is multiplied by asr_dropout's mask for the
+   * element's offset i from c (kept iff u01(drop_seed, i) >= drop_p, scale
+   * 1 / (1 - drop_p)): dropout's backward fused into the producing GEMM. */
+  float drop_p;
+  unsigned long long drop_seed;
 } asr_gemm_t;
 
 int asr_gemm(const asr_gemm_t* problems, int nprob, int compute_dtype, void* stream);

@@ -185,7 +185,8 @@ class Gemm(ctypes.Structure):
     _fields_ = [('a', Operand), ('b', Operand), ('c', c_vp), ('c_map', RowMap), ('bias', c_vp),
                 ('bias2', c_vp), ('M', c_int), ('N', c_int), ('K', c_int), ('alpha', c_float),
                 ('beta', c_float), ('batch', c_int), ('batch_stride_a', c_ll),
-                ('batch_stride_b', c_ll), ('batch_stride_c', c_ll)]
+                ('batch_stride_b', c_ll), ('batch_stride_c', c_ll), ('drop_p', c_float),
+                ('drop_seed', ctypes.c_ulonglong)]
 
 
 class NativeError(RuntimeError):

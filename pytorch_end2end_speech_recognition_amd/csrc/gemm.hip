@@ -66,7 +66,14 @@ struct Problem {
   int ksplit;   // > 1: split-K into f32 slabs [ksplit][M][N], reduced by splitk_reduce
   int kchunk;   // K elements per split (multiple of BK)
   float* slab;
+  float drop_p;                  // > 0: C element at offset i from C's base is kept iff
+  unsigned long long drop_seed;  // u01(drop_seed, i) >= drop_p, scaled by 1 / (1 - p)
 };
+
+// Dropout mask of the epilogue (asr_dropout's mask over C's flat offsets).
+__device__ __forceinline__ float drop_scale(const Problem& pr, long long i) {
+  return u01(pr.drop_seed, (unsigned long long)i) >= pr.drop_p ? 1.f / (1.f - pr.drop_p) : 0.f;
+}
 
 struct Params {
   Problem p[2];
@@ -279,6 +286,7 @@ __device__ __forceinline__ void store_acc(const Problem& pr, const f32x4 (&acc)[
         if (pr.bias) v += pr.bias[n];
         if (pr.bias2) v += pr.bias2[n];
         if (pr.beta != 0.f) v += pr.beta * crow[n];
+        if (pr.drop_p > 0.f) v *= drop_scale(pr, off + n);
         crow[n] = v;
       }
     }
@@ -927,6 +935,7 @@ gemm_bf16_kk256(Params P) {
         if (pr.bias) v += pr.bias[n];
         if (pr.bias2) v += pr.bias2[n];
         if (pr.beta != 0.f) v += pr.beta * crow[n];
+        if (pr.drop_p > 0.f) v *= drop_scale(pr, off + n);
         crow[n] = v;
       }
     }
@@ -1140,11 +1149,19 @@ __device__ __forceinline__ void epi8(const Problem& pr, const RowMap& cm, bool r
           const float4 c = *reinterpret_cast<const float4*>(cp);
           o[0] += pr.beta * c.x; o[1] += pr.beta * c.y; o[2] += pr.beta * c.z; o[3] += pr.beta * c.w;
         }
+        if (!raw && pr.drop_p > 0.f) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] *= drop_scale(pr, off + n + e);
+        }
         *reinterpret_cast<float4*>(cp) = make_float4(o[0], o[1], o[2], o[3]);
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          if (n + e < pr.N) cp[e] = (!raw && pr.beta != 0.f) ? o[e] + pr.beta * cp[e] : o[e];
+          if (n + e < pr.N) {
+            float x = (!raw && pr.beta != 0.f) ? o[e] + pr.beta * cp[e] : o[e];
+            if (!raw && pr.drop_p > 0.f) x *= drop_scale(pr, off + n + e);
+            cp[e] = x;
+          }
       }
     }
   }
@@ -1506,7 +1523,8 @@ gemm_bf16_8r(Params P) {
 // bias + bias2 + beta * C, through C's row map.
 __global__ void splitk_reduce(const float* __restrict__ slab, int ksplit, int M, int N, RowMap c,
                               float alpha, float beta, const float* __restrict__ bias,
-                              const float* __restrict__ bias2) {
+                              const float* __restrict__ bias2, float drop_p,
+                              unsigned long long drop_seed) {
   const long long MN = (long long)M * N;
   const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
   if (e >= MN) return;
@@ -1520,6 +1538,8 @@ __global__ void splitk_reduce(const float* __restrict__ slab, int ksplit, int M,
   if (bias2) v += bias2[n];
   float* crow = (float*)c.base + off;
   if (beta != 0.f) v += beta * crow[n];
+  if (drop_p > 0.f)
+    v *= u01(drop_seed, (unsigned long long)(off + n)) >= drop_p ? 1.f / (1.f - drop_p) : 0.f;
   crow[n] = v;
 }
 
@@ -1771,6 +1791,10 @@ int gemm_launch_own(const asr_gemm_t* problems, int nprob, int compute_dtype, vo
     p.M = g.M; p.N = g.N; p.K = g.K;
     p.alpha = g.alpha;
     p.beta = g.beta;
+    ASR_REQUIRE(g.drop_p >= 0.f && g.drop_p < 1.f, ASR_ERR_ARG, "gemm: dropout p outside [0, 1)");
+    ASR_REQUIRE(g.drop_p == 0.f || g.batch <= 1, ASR_ERR_ARG, "gemm: dropout on a batched product");
+    p.drop_p = g.drop_p;
+    p.drop_seed = g.drop_seed;
     p.batch = g.batch > 1 ? g.batch : 1;
     p.sA = g.batch_stride_a;
     p.sB = g.batch_stride_b;
@@ -1920,7 +1944,8 @@ int gemm_launch_own(const asr_gemm_t* problems, int nprob, int compute_dtype, vo
     const long long mn = (long long)p.M * p.N;
     if (mn == 0) continue;
     hipLaunchKernelGGL(splitk_reduce, dim3((unsigned)((mn + 255) / 256)), dim3(256), 0, s, p.slab,
-                       p.ksplit, p.M, p.N, p.c, p.alpha, p.beta, p.bias, p.bias2);
+                       p.ksplit, p.M, p.N, p.c, p.alpha, p.beta, p.bias, p.bias2, p.drop_p,
+                       p.drop_seed);
     ASR_LAUNCH_CHECK();
   }
   return ASR_OK;

@@ -94,12 +94,15 @@ def operand(t, trans, rmap, offset=0):
 
 
 def gemm_problem(a, b, c, c_map, M, N_, K, alpha=1.0, beta=0.0, bias=None, bias2=None, c_offset=0,
-                 batch=1, batch_strides=(0, 0, 0)):
+                 batch=1, batch_strides=(0, 0, 0), drop=None):
+    """drop=(p, seed): the written values get asr_dropout's mask for their
+    element offsets from c (dropout's backward fused into the product)."""
     return N.Gemm(a, b, c.data_ptr() + 4 * c_offset, c_map,
                   bias.data_ptr() if bias is not None else None,
                   bias2.data_ptr() if bias2 is not None else None, int(M), int(N_), int(K),
                   float(alpha), float(beta), int(batch), int(batch_strides[0]),
-                  int(batch_strides[1]), int(batch_strides[2]))
+                  int(batch_strides[1]), int(batch_strides[2]),
+                  float(drop[0]) if drop else 0.0, int(drop[1]) if drop else 0)
 
 
 def run_gemm(problems, device):
@@ -801,14 +804,11 @@ class BLSTMLayerFn(torch.autograd.Function):
                 dx = torch.zeros(B, T_src, Dsrc, dtype=torch.float32, device=dev)
             c_map = rowmap(Dsrc, stride_b=T_src * Dsrc, rows_per_b=T, t_mul=t_mul, t_add=t_add,
                            t_limit=T_src, perm=perm)
+            # dropout's backward (the forward mask over x_src's flat offsets) is
+            # applied by the GEMM's epilogue as it writes dX
             p = gemm_problem(operand(dg_op, 0, rowmap(8 * H)), operand(w_op, 1, rowmap(Din)), dx,
-                             c_map, BT, Din, 8 * H)
+                             c_map, BT, Din, 8 * H, drop=ctx.drop)
             run_gemm([p], dev)
-        if dx is not None and ctx.drop is not None:   # dropout's backward: the same mask
-            dxm = torch.empty_like(dx)
-            N.call('asr_dropout', N.ptr(dx), N.ptr(dxm), dx.numel(), float(ctx.drop[0]),
-                   int(ctx.drop[1]), N.stream_handle(dev))
-            dx = dxm
         return (dx,) + (None,) * (13 + ctx.n_graph)
 
 

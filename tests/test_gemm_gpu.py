@@ -302,3 +302,41 @@ def test_fast_kernel_mapped_k_rows_exact(stagef, cuda_dev, monkeypatch):
         np.testing.assert_array_equal(C2.cpu().numpy(), A2 @ sb2.astype(np.float64).T)
     finally:
         ops.set_compute_dtype('fp32')
+
+
+@pytest.mark.parametrize('M,N,K,dtype,kind', [
+    (2048, 1024, 512, 'bf16', '8-wave'),        # both extents >= 256: 256 x 256 kernel
+    (2048, 200, 512, 'bf16', '128x128'),        # N < 256: 128 x 128 fast kernel
+    (192, 160, 32768, 'bf16', 'split-K'),       # few tiles, long K: slabs + splitk_reduce
+    (600, 300, 96, 'fp32', 'generic'),          # f32 operands, parity mode
+])
+def test_dropout_epilogue_matches_separate_pass(M, N, K, dtype, kind, cuda_dev):
+    """Dropout's backward fused into the producing GEMM (asr_gemm_t.drop_p):
+    the result equals the product written plainly and then masked by
+    asr_dropout over the same tensor (same seed), bit for bit, on every kernel
+    family, including a row-mapped (scattered) C inside a larger tensor."""
+    from pytorch_end2end_speech_recognition_amd import _native as NL
+    ops = _ops()
+    ops.set_compute_dtype(dtype)
+    try:
+        rng = np.random.RandomState(M + N + K)
+        tdt = torch.bfloat16 if dtype == 'bf16' else torch.float32
+        a = torch.from_numpy(rng.randint(-3, 4, (M, K)).astype(np.float32)).to(tdt).to(cuda_dev)
+        b = torch.from_numpy(rng.randint(-3, 4, (N, K)).astype(np.float32)).to(tdt).to(cuda_dev)
+        # C rows scattered as rows 2t+1 of a [2M, N] tensor ('drop' subsampling's layout)
+        cmap = ops.rowmap(N, stride_b=2 * M * N, rows_per_b=M, t_mul=2, t_add=1, t_limit=2 * M)
+        p, seed = 0.3, 987654321
+        plain = torch.zeros(2 * M, N, device=cuda_dev)
+        fused = torch.zeros(2 * M, N, device=cuda_dev)
+        for c, drop in ((plain, None), (fused, (p, seed))):
+            prob = ops.gemm_problem(ops.operand(a, 0, ops.rowmap(K)), ops.operand(b, 0, ops.rowmap(K)),
+                                    c, cmap, M, N, K, drop=drop)
+            ops.run_gemm([prob], cuda_dev)
+        ref = torch.empty_like(plain)
+        NL.call('asr_dropout', NL.ptr(plain), NL.ptr(ref), plain.numel(), p, seed,
+                NL.stream_handle(cuda_dev))
+        torch.cuda.synchronize()
+        assert torch.equal(fused, ref), kind
+        assert (fused[1::2] == 0).float().mean().item() > 0.2      # the mask is applied
+    finally:
+        ops.set_compute_dtype('fp32')
