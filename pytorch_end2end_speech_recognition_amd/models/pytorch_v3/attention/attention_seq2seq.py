@@ -75,10 +75,6 @@ class AttentionSeq2seq(ModelBase):
         if init_dec_state not in ['zero', 'mean', 'final', 'first']:
             raise ValueError('init_dec_state must be "zero" or "mean" or "final" or "first".')
         self.init_dec_state_0_fwd = init_dec_state
-        self.init_dec_state_0_bwd = init_dec_state
-        if encoder_type != decoder_type:
-            self.init_dec_state_0_fwd = 'zero'
-            self.init_dec_state_0_bwd = 'zero'
         self.sharpening_factor = sharpening_factor
         self.logits_temperature = logits_temperature
         self.sigmoid_smoothing = sigmoid_smoothing
@@ -97,17 +93,25 @@ class AttentionSeq2seq(ModelBase):
         self.dropout_decoder = float(dropout_decoder)
         self.dropout_embedding = float(dropout_embedding)
 
+        self.init_dec_state_0_bwd = init_dec_state
+        if backward_loss_weight > 0:                   # :187-191
+            if init_dec_state == 'first':
+                self.init_dec_state_0_bwd = 'final'
+            elif init_dec_state == 'final':
+                self.init_dec_state_0_bwd = 'first'
+        if encoder_type != decoder_type:
+            self.init_dec_state_0_fwd = 'zero'
+            self.init_dec_state_0_bwd = 'zero'
+
         unsupported = []
-        if decoding_order != 'bahdanau':
-            unsupported.append('decoding_order=%s' % decoding_order)
-        if backward_loss_weight > 0:
-            unsupported.append('backward decoder')
-        if bridge_layer or encoder_type == 'cnn':
-            unsupported.append('bridge layer / cnn encoder')
+        if decoding_order not in ('bahdanau', 'luong', 'conditional'):
+            raise ValueError(decoding_order)
+        if encoder_type == 'cnn':
+            unsupported.append('cnn encoder')
         if coverage_weight != 0:
             unsupported.append('coverage')
-        if decoder_num_layers != 1 or decoder_residual or decoder_dense_residual:
-            unsupported.append('multi-layer / residual decoder in the fused training loop')
+        if decoder_type != 'lstm':
+            unsupported.append('decoder_type=%s' % decoder_type)
         if unsupported:
             raise NotImplementedError('MI355X AttentionSeq2seq: not yet supported: ' +
                                       ', '.join(unsupported))
@@ -123,25 +127,51 @@ class AttentionSeq2seq(ModelBase):
             conv_kernel_sizes=conv_kernel_sizes, conv_strides=conv_strides, poolings=poolings,
             activation=activation, batch_norm=batch_norm, residual=encoder_residual,
             dense_residual=encoder_dense_residual, nin=0)
-        self.is_bridge = False
+        if bridge_layer:                               # :268-278
+            self.bridge_0 = LinearND(self.encoder_num_units, decoder_num_units,
+                                     dropout=dropout_encoder)
+            self.encoder_num_units = decoder_num_units
+            self.is_bridge = True
+        else:
+            self.is_bridge = False
 
-        # :293-361, forward direction only (registration order = RNG order)
-        if self.init_dec_state_0_fwd != 'zero':
-            self.W_dec_init_0_fwd = LinearND(self.encoder_num_units, decoder_num_units)
-        self.decoder_0_fwd = RNNDecoder(input_size=self.encoder_num_units + embedding_dim,
-                                        rnn_type=decoder_type, num_units=decoder_num_units,
-                                        num_layers=decoder_num_layers, dropout=dropout_decoder,
-                                        residual=decoder_residual,
-                                        dense_residual=decoder_dense_residual)
-        self.attend_0_fwd = AttentionMechanism(
-            encoder_num_units=self.encoder_num_units, decoder_num_units=decoder_num_units,
-            attention_type=attention_type, attention_dim=attention_dim,
-            sharpening_factor=sharpening_factor, sigmoid_smoothing=sigmoid_smoothing,
-            out_channels=attention_conv_num_channels, kernel_size=attention_conv_width,
-            num_heads=num_heads)
-        self.W_d_0_fwd = LinearND(decoder_num_units, bottleneck_dim, dropout=dropout_decoder)
-        self.W_c_0_fwd = LinearND(self.encoder_num_units, bottleneck_dim, dropout=dropout_decoder)
-        self.fc_0_fwd = LinearND(bottleneck_dim, self.num_classes)
+        # :280-361 per direction (registration order = RNG order)
+        directions = (['fwd'] if self.fwd_weight_0 > 0 else []) + \
+            (['bwd'] if self.bwd_weight_0 > 0 else [])
+        self._directions = directions
+        for dir in directions:
+            if getattr(self, 'init_dec_state_0_' + dir) != 'zero':
+                setattr(self, 'W_dec_init_0_' + dir,
+                        LinearND(self.encoder_num_units, decoder_num_units))
+            if decoding_order == 'conditional':
+                setattr(self, 'decoder_first_0_' + dir,
+                        RNNDecoder(input_size=embedding_dim, rnn_type=decoder_type,
+                                   num_units=decoder_num_units, num_layers=1,
+                                   dropout=dropout_decoder, residual=False,
+                                   dense_residual=False))
+                setattr(self, 'decoder_second_0_' + dir,
+                        RNNDecoder(input_size=self.encoder_num_units, rnn_type=decoder_type,
+                                   num_units=decoder_num_units, num_layers=1,
+                                   dropout=dropout_decoder, residual=False,
+                                   dense_residual=False))
+            else:
+                setattr(self, 'decoder_0_' + dir,
+                        RNNDecoder(input_size=self.encoder_num_units + embedding_dim,
+                                   rnn_type=decoder_type, num_units=decoder_num_units,
+                                   num_layers=decoder_num_layers, dropout=dropout_decoder,
+                                   residual=decoder_residual,
+                                   dense_residual=decoder_dense_residual))
+            setattr(self, 'attend_0_' + dir, AttentionMechanism(
+                encoder_num_units=self.encoder_num_units, decoder_num_units=decoder_num_units,
+                attention_type=attention_type, attention_dim=attention_dim,
+                sharpening_factor=sharpening_factor, sigmoid_smoothing=sigmoid_smoothing,
+                out_channels=attention_conv_num_channels, kernel_size=attention_conv_width,
+                num_heads=num_heads))
+            setattr(self, 'W_d_0_' + dir,
+                    LinearND(decoder_num_units, bottleneck_dim, dropout=dropout_decoder))
+            setattr(self, 'W_c_0_' + dir,
+                    LinearND(self.encoder_num_units, bottleneck_dim, dropout=dropout_decoder))
+            setattr(self, 'fc_0_' + dir, LinearND(bottleneck_dim, self.num_classes))
         if label_smoothing_prob > 0:
             self.embed_0 = Embedding_LS(num_classes=self.num_classes,
                                         embedding_dim=embedding_dim, dropout=dropout_embedding,
@@ -150,7 +180,8 @@ class AttentionSeq2seq(ModelBase):
             self.embed_0 = Embedding(num_classes=self.num_classes, embedding_dim=embedding_dim,
                                      dropout=dropout_embedding)
         if ctc_loss_weight > 0:
-            self.fc_ctc_0 = LinearND(self.encoder_num_units, num_classes + 1)
+            self.fc_ctc_0 = LinearND(decoder_num_units if self.is_bridge
+                                     else self.encoder_num_units, num_classes + 1)
             self._decode_ctc_greedy_np = GreedyDecoder(blank_index=0)
 
         # :397-420
@@ -185,11 +216,23 @@ class AttentionSeq2seq(ModelBase):
         ys = np.asarray(ys)
         y_lens = np.asarray(y_lens).astype(np.int64)
 
-        ys_in, ys_out = self._ys_in_out(ys, y_lens, self.eos_0, perm)
-
-        self._ys_in_host = {0: ys_in}     # host copy: token-grouped embedding gradient
-        loss = self.compute_xe_loss(enc_out, self.np2var(ys_in), self.np2var(ys_out), enc_lens_d,
-                                    None, task=0, dir='fwd', weight=self.fwd_weight_0)
+        loss = None
+        if self.fwd_weight_0 > 0:
+            ys_in, ys_out = self._ys_in_out(ys, y_lens, self.eos_0, perm)
+            self._ys_in_host = {0: ys_in}     # host copy: token-grouped embedding gradient
+            loss = self.compute_xe_loss(enc_out, self.np2var(ys_in), self.np2var(ys_out),
+                                        enc_lens_d, None, task=0, dir='fwd',
+                                        weight=self.fwd_weight_0)
+        if self.bwd_weight_0 > 0:             # :489-528: each label sequence reversed
+            ys_rev = ys.copy()
+            for b in range(B):
+                ys_rev[b, :y_lens[b]] = ys[b, :y_lens[b]][::-1]
+            ys_in, ys_out = self._ys_in_out(ys_rev, y_lens, self.eos_0, perm)
+            self._ys_in_host = {0: ys_in}
+            loss_bwd = self.compute_xe_loss(enc_out, self.np2var(ys_in), self.np2var(ys_out),
+                                            enc_lens_d, None, task=0, dir='bwd',
+                                            weight=self.bwd_weight_0)
+            loss = loss_bwd if loss is None else ops.add(loss, loss_bwd)
         if self.ctc_loss_weight > 0:
             ys_ctc = (ys + 1)[perm]
             yl = y_lens[perm].astype(np.int32)
@@ -238,8 +281,12 @@ class AttentionSeq2seq(ModelBase):
 
     def _encode(self, xs, x_lens, is_multi_task=False):
         """:655-698 (with num_layers_sub >= 1 the encoder returns the sub-task tap
-        too: (xs, x_lens, xs_sub, x_lens_sub, perm_idx))."""
-        return self.encoder(xs, x_lens, volatile=not self.training)
+        too: (xs, x_lens, xs_sub, x_lens_sub, perm_idx)); the bridge layer
+        (:686-690) maps the main output to the decoder width."""
+        out = self.encoder(xs, x_lens, volatile=not self.training)
+        if getattr(self, 'is_bridge', False):
+            out = (self.bridge_0(out[0]),) + tuple(out[1:])
+        return out
 
     def _init_h0(self, enc_out, task=0, dir='fwd'):
         """_init_dec_state (:801-864): zero / mean (over all T, padding included,
@@ -265,7 +312,95 @@ class AttentionSeq2seq(ModelBase):
             flags[t] = random.random() < self._ss_prob
         return flags if flags.any() else None
 
+    def _fused_ok(self, task, dir):
+        """The fused decoder op covers bahdanau order with a 1-layer decoder
+        without residual connections (location or content attention)."""
+        dec = getattr(self, 'decoder_%d_%s' % (task, dir), None)
+        return (self.decoding_order == 'bahdanau' and dec is not None and dec.num_layers == 1
+                and not dec.residual and not dec.dense_residual)
+
     def _decode_train(self, enc_out, x_lens, ys, task=0, dir='fwd'):
+        if not self._fused_ok(task, dir):
+            return self._decode_train_steps(enc_out, x_lens, ys, task, dir)
+        return self._decode_train_fused(enc_out, x_lens, ys, task, dir)
+
+    def _decode_train_steps(self, enc_out, x_lens, ys, task=0, dir='fwd'):
+        """:704-799 step by step for what the fused op does not cover: multi-layer
+        and residual decoders (RNNDecoder.forward, HIP LSTM cells) and the luong
+        / conditional decoding orders.  Each step is HIP autograd ops (the
+        decoder cells, the attention step with its HIP backward); the W_d / W_c
+        bottleneck and the output layer run once over all steps afterwards,
+        except under scheduled sampling, which needs each step's logits."""
+        att = getattr(self, 'attend_%d_%s' % (task, dir))
+        W_d, W_c = getattr(self, 'W_d_%d_%s' % (task, dir)), getattr(self, 'W_c_%d_%s' % (task, dir))
+        fc = getattr(self, 'fc_%d_%s' % (task, dir))
+        embed = getattr(self, 'embed_%d' % task)
+        order = self.decoding_order
+        if order == 'conditional':
+            dec1 = getattr(self, 'decoder_first_%d_%s' % (task, dir))
+            dec2 = getattr(self, 'decoder_second_%d_%s' % (task, dir))
+            nl = 1
+        else:
+            dec1 = getattr(self, 'decoder_%d_%s' % (task, dir))
+            nl = dec1.num_layers
+        B, T, E = enc_out.shape
+        S = ys.shape[1]
+        D = getattr(self, 'decoder_num_units_%d' % task)
+        dev = enc_out.device
+        h0 = self._init_h0(enc_out, task, dir)
+        zero = torch.zeros(B, D, dtype=torch.float32, device=dev)
+        hx = [h0 if h0 is not None else zero for _ in range(nl)]
+        cx = [zero for _ in range(nl)]
+        dec_out = h0 if h0 is not None else zero
+        aw = torch.zeros(B, T, dtype=torch.float32, device=dev)
+        ctx = torch.zeros(B, E, dtype=torch.float32, device=dev)
+        lens = x_lens if torch.is_tensor(x_lens) else torch.from_numpy(
+            np.asarray(x_lens, np.int32)).to(dev)
+        hosts = getattr(self, '_ys_in_host', None) or {}
+        ys_host = hosts.pop(task, None)
+        if ys_host is not None and tuple(ys_host.shape) != tuple(ys.shape):
+            ys_host = None
+        y_emb = embed(ys, ys_host)                                # [B, S, emb]
+        enc_a = att.W_enc_head0(enc_out).unsqueeze(3)             # [B, T, A, 1]
+        ss = self._ss_steps(S)
+
+        def generate(d, c):
+            return fc(ops.add_tanh(W_d(d), W_c(c)))
+
+        decs, ctxs, aws, step_logits = [], [], [], []
+        for t in range(S):
+            if ss is not None and ss[t]:                          # :744-748
+                prev = step_logits[-1].detach()
+                y = embed(ops.row_argmax(prev).view(B, 1)).view(B, -1).detach()
+            else:
+                y = y_emb[:, t]
+            if order == 'bahdanau':
+                if t > 0:
+                    d3, (hx, cx) = dec1(torch.cat([y, ctx], dim=-1).unsqueeze(1), (hx, cx))
+                    dec_out = d3.squeeze(1)
+                c3, a3 = att(enc_out, enc_a, lens, dec_out.unsqueeze(1), aw.unsqueeze(2))
+            elif order == 'luong':
+                d3, (hx, cx) = dec1(torch.cat([y, ctx], dim=-1).unsqueeze(1), (hx, cx))
+                dec_out = d3.squeeze(1)
+                c3, a3 = att(enc_out, enc_a, lens, dec_out.unsqueeze(1), aw.unsqueeze(2))
+            else:                                                 # conditional
+                d3, (hx, cx) = dec1(y.unsqueeze(1), (hx, cx))
+                c3, a3 = att(enc_out, enc_a, lens, d3, aw.unsqueeze(2))
+                d3, (hx, cx) = dec2(c3, (hx, cx))
+                dec_out = d3.squeeze(1)
+            ctx, aw = c3.squeeze(1), a3.squeeze(2)
+            decs.append(dec_out)
+            ctxs.append(ctx)
+            aws.append(aw)
+            if ss is not None:
+                step_logits.append(generate(dec_out.unsqueeze(1), ctx.unsqueeze(1)))
+        if ss is not None:
+            logits = torch.cat(step_logits, dim=1)
+        else:
+            logits = generate(torch.stack(decs, dim=1), torch.stack(ctxs, dim=1))
+        return logits, torch.stack(aws, dim=1)
+
+    def _decode_train_fused(self, enc_out, x_lens, ys, task=0, dir='fwd'):
         """:704-799 as one fused op (bahdanau order).  Returns (logits [B,S,V], aw).
 
         Training mode: decoder dropout on h (rnn_decoder.py:97-98) inside the
@@ -310,7 +445,7 @@ class AttentionSeq2seq(ModelBase):
         dec, ctx, aw = ops.att_decoder(enc_out, enc_a, x_lens, pre_emb, h0, emb_dim,
                                        self.sharpening_factor, self.sigmoid_smoothing,
                                        cell.weight_ih, cell.weight_hh, att.W_dec_head0.fc.weight,
-                                       att.W_conv_head0.fc.weight, att.conv_head0.weight,
+                                       *att.conv_weights(),
                                        att.V_head0.fc.weight, train_opts)
         if p_b > 0:   # two LinearND with their own dropout masks, then tanh of the sum
             a = ops.dropout(ops.linear(dec, W_d.fc.weight, W_d.fc.bias), p_b, seed=seed_d)
@@ -343,17 +478,72 @@ class AttentionSeq2seq(ModelBase):
         self.eval()
         xs_d = self.np2var(xs, dtype='float')
         enc_out, enc_lens_d, _ = self._encode(xs_d, x_lens)
+        dir = 'fwd' if self.fwd_weight_0 >= self.bwd_weight_0 else 'bwd'   # :893
         if beam_width == 1:
-            best_hyps, aw = self._decode_infer_greedy(enc_out, enc_lens_d, max_decode_len)
+            best_hyps, aw = self._decode_infer_greedy(enc_out, enc_lens_d, max_decode_len,
+                                                      dir=dir)
         else:
             best_hyps, aw = self._decode_infer_beam(enc_out, self.encoder.last_lens_np, beam_width,
                                                     max_decode_len, min_decode_len,
-                                                    length_penalty, coverage_penalty)
+                                                    length_penalty, coverage_penalty, dir=dir)
         return best_hyps, aw, self.encoder.last_perm_np.copy()
+
+    def _infer_step(self, task, dir, t, y_emb, st, enc, enc_a, lens):
+        """One inference decoder step (:963-1001) on the HIP per-step ops, for any
+        decoding order / decoder depth.  st = dict(h, c (lists per layer), dec,
+        ctx, aw); y_emb [n, emb] (unused at t = 0 in bahdanau order).  Returns
+        (new st, logits [n, V])."""
+        att = getattr(self, 'attend_%d_%s' % (task, dir))
+        W_d, W_c = getattr(self, 'W_d_%d_%s' % (task, dir)), getattr(self, 'W_c_%d_%s' % (task, dir))
+        fc = getattr(self, 'fc_%d_%s' % (task, dir))
+        hx, cx, dec, ctx, aw = list(st['h']), list(st['c']), st['dec'], st['ctx'], st['aw']
+        n = dec.shape[0]
+        L = aw.shape[1]
+        if self.decoding_order == 'conditional':
+            d1 = getattr(self, 'decoder_first_%d_%s' % (task, dir))
+            d2 = getattr(self, 'decoder_second_%d_%s' % (task, dir))
+            dd, (hx, cx) = d1(y_emb.unsqueeze(1), (hx, cx))
+            c3, a3 = att(enc, enc_a, lens, dd, aw.unsqueeze(2))
+            d3, (hx, cx) = d2(c3, (hx, cx))
+            dec = d3.squeeze(1)
+        else:
+            dm = getattr(self, 'decoder_%d_%s' % (task, dir))
+            if self.decoding_order == 'luong' or t > 0:
+                d3, (hx, cx) = dm(torch.cat([y_emb, ctx], dim=-1).unsqueeze(1), (hx, cx))
+                dec = d3.squeeze(1)
+            c3, a3 = att(enc, enc_a, lens, dec.unsqueeze(1), aw.unsqueeze(2))
+        ctx, aw = c3.reshape(n, -1), a3.reshape(n, L)
+        logits = fc(ops.tanh(ops.linear2(dec, W_d.fc.weight, W_d.fc.bias, ctx, W_c.fc.weight,
+                                         W_c.fc.bias)))
+        return dict(h=hx, c=cx, dec=dec, ctx=ctx, aw=aw), logits
+
+    def _init_state(self, enc_out, task, dir):
+        """_init_dec_state (:801-864) as the step state dict of _infer_step."""
+        B, T, E = enc_out.shape
+        D = getattr(self, 'decoder_num_units_%d' % task)
+        dev = enc_out.device
+        if self.decoding_order == 'conditional':
+            nl = 1
+        else:
+            nl = getattr(self, 'decoder_%d_%s' % (task, dir)).num_layers
+        h0 = self._init_h0(enc_out, task, dir)
+        zero = torch.zeros(B, D, dtype=torch.float32, device=dev)
+        h = h0 if h0 is not None else zero
+        return dict(h=[h] * nl, c=[zero] * nl, dec=h,
+                    ctx=torch.zeros(B, E, dtype=torch.float32, device=dev),
+                    aw=torch.zeros(B, T, dtype=torch.float32, device=dev))
+
+    @staticmethod
+    def _reverse_bwd(best_hyps, y_lens):
+        """:1027-1034 / :1231-1234: hypotheses of the backward decoder are
+        reversed over their first y_lens tokens."""
+        for b in range(len(best_hyps)):
+            best_hyps[b][:y_lens[b]] = best_hyps[b][:y_lens[b]][::-1].copy()
+        return best_hyps
 
     def _decode_infer_beam(self, enc_out, x_lens, beam_width, max_decode_len, min_decode_len,
                            length_penalty, coverage_penalty, task=0, dir='fwd'):
-        """:1038-1237 (bahdanau order).  Utterance by utterance like the
+        """:1038-1237 (any decoding order / decoder depth).  Utterance by utterance like the
         reference, each over its own frames (enc_out[b, :x_len]); the live
         hypotheses of an utterance advance as ONE batch per step on the HIP ops
         (embedding, LSTMCell, the location-attention step, the bottleneck and
@@ -367,29 +557,28 @@ class AttentionSeq2seq(ModelBase):
         if coverage_penalty > 0:
             raise NotImplementedError('coverage penalty (the reference raises too, :1150)')
         att = getattr(self, 'attend_%d_%s' % (task, dir))
-        dec_mod = getattr(self, 'decoder_%d_%s' % (task, dir))
-        W_d, W_c = getattr(self, 'W_d_%d_%s' % (task, dir)), getattr(self, 'W_c_%d_%s' % (task, dir))
-        fc = getattr(self, 'fc_%d_%s' % (task, dir))
         embed = getattr(self, 'embed_%d' % task)
         sos, eos = getattr(self, 'sos_%d' % task), getattr(self, 'eos_%d' % task)
-        D = getattr(self, 'decoder_num_units_%d' % task)
-        nl = dec_mod.num_layers
         dev = enc_out.device
         B, _, E = enc_out.shape
         lens = np.asarray(x_lens).reshape(-1).astype(np.int64)
         enc_a = att.W_enc_head0(enc_out)                            # [B, T, A]
         A = enc_a.shape[2]
-        h0 = self._init_h0(enc_out, task, dir)
+        init = self._init_state(enc_out, task, dir)
+        dm = getattr(self, 'decoder_%d_%s' % (task, dir), None)
+        residual = dm is not None and dm.residual and dm.num_layers > 1
+
+        def _rows(st, i):
+            return {k: ([x[i:i + 1] for x in v] if isinstance(v, list) else v[i:i + 1])
+                    for k, v in st.items()}
         best, aws = [], []
         for b in range(B):
             L = int(lens[b])
             enc_b = enc_out[b:b + 1, :L].contiguous()
             enc_a_b = enc_a[b:b + 1, :L].contiguous()
-            zero = torch.zeros(1, D, dtype=enc_out.dtype, device=dev)
-            h_init = h0[b:b + 1] if h0 is not None else zero
-            state = dict(h=[h_init] * nl, c=[zero] * nl, dec=h_init,
-                         ctx=torch.zeros(1, E, dtype=enc_out.dtype, device=dev),
-                         aw=torch.zeros(1, L, dtype=enc_out.dtype, device=dev))
+            state = dict(h=[x[b:b + 1] for x in init['h']], c=[x[b:b + 1] for x in init['c']],
+                         dec=init['dec'][b:b + 1], ctx=init['ctx'][b:b + 1],
+                         aw=init['aw'][b:b + 1, :L])
             beam = [dict(hyp=[sos], score=0.0, row=0, hist=[])]
             complete, step_aw = [], []
             for t in range(max_decode_len):
@@ -397,29 +586,30 @@ class AttentionSeq2seq(ModelBase):
                 if n == 0:
                     break
                 rows = torch.tensor([c['row'] for c in beam], dtype=torch.long, device=dev)
-                hs = [x.index_select(0, rows) for x in state['h']]
-                cs = [x.index_select(0, rows) for x in state['c']]
-                if t == 0:
-                    dec = state['dec'].index_select(0, rows)
+                st = {k: ([x.index_select(0, rows) for x in v] if isinstance(v, list)
+                          else v.index_select(0, rows)) for k, v in state.items()}
+                toks = np.array([c['hyp'][-1] for c in beam], np.int64).reshape(n, 1)
+                y = embed(torch.from_numpy(toks).to(dev), toks).view(n, -1)
+                if residual:
+                    # the reference advances each hypothesis as a batch of one, and
+                    # its residual decoder sums the lower layer over the batch
+                    # (rnn_decoder.py:100-102): one step per hypothesis here too
+                    outs = [self._infer_step(task, dir, t, y[i:i + 1], _rows(st, i), enc_b,
+                                             enc_a_b.unsqueeze(3), [L]) for i in range(n)]
+                    state = {k: ([torch.cat([o[0][k][l] for o in outs]) for l in range(len(v))]
+                                 if isinstance(v, list) else torch.cat([o[0][k] for o in outs]))
+                             for k, v in outs[0][0].items()}
+                    logits = torch.cat([o[1] for o in outs])
                 else:
-                    toks = np.array([c['hyp'][-1] for c in beam], np.int64).reshape(n, 1)
-                    y = embed(torch.from_numpy(toks).to(dev), toks)          # [n, 1, emb]
-                    dec_in = torch.cat([y, state['ctx'].index_select(0, rows).unsqueeze(1)],
-                                       dim=-1)
-                    dec3, (hs, cs) = dec_mod(dec_in, (hs, cs))
-                    dec = dec3.squeeze(1)
-                ctx3, aw3 = att(enc_b.expand(n, L, E).contiguous(),
-                                enc_a_b.expand(n, L, A).contiguous().unsqueeze(3), [L] * n,
-                                dec.unsqueeze(1), state['aw'].index_select(0, rows).unsqueeze(2))
-                ctx, aw_t = ctx3.squeeze(1), aw3.squeeze(2)
-                logits = fc(ops.tanh(ops.linear2(dec, W_d.fc.weight, W_d.fc.bias, ctx,
-                                                 W_c.fc.weight, W_c.fc.bias)))
+                    state, logits = self._infer_step(
+                        task, dir, t, y, st, enc_b.expand(n, L, E).contiguous(),
+                        enc_a_b.expand(n, L, A).contiguous().unsqueeze(3), [L] * n)
+                aw_t = state['aw']
                 lg = logits.float().cpu().numpy()
                 mx = lg.max(axis=1, keepdims=True)                          # log_softmax (f32)
                 lp = lg - mx - np.log(np.exp(lg - mx).sum(axis=1, keepdims=True))
                 k_top = min(beam_width, lp.shape[1])
                 order = np.argsort(-lp, axis=1, kind='stable')[:, :k_top]   # topk, sorted
-                state = dict(h=hs, c=cs, dec=dec, ctx=ctx, aw=aw_t)
                 step_aw.append(aw_t)
                 new = []
                 for i in range(n):
@@ -446,11 +636,49 @@ class AttentionSeq2seq(ModelBase):
             aw_rows = [step_aw[t][i] for t, i in top['hist']]
             aws.append(torch.stack(aw_rows).cpu().numpy() if aw_rows
                        else np.zeros((0, L), np.float32))
+        if dir == 'bwd':                                  # :1231-1234
+            best = self._reverse_bwd(best, [len(h) for h in best])
         if len(set(len(h) for h in best)) <= 1:
             return np.array(best), aws
         return np.array(best + [None], dtype=object)[:-1], aws
 
     def _decode_infer_greedy(self, enc_out, x_lens, max_decode_len, task=0, dir='fwd'):
+        if self._fused_ok(task, dir):
+            hyps, aw = self._decode_infer_greedy_fused(enc_out, x_lens, max_decode_len, task, dir)
+        else:
+            hyps, aw = self._decode_infer_greedy_steps(enc_out, x_lens, max_decode_len, task, dir)
+        if dir == 'bwd':       # lengths counted up to the first <eos> (:1007-1014)
+            eos = getattr(self, 'eos_%d' % task)
+            y_lens = [int(np.argmax(h == eos)) if (h == eos).any() else len(h) for h in hyps]
+            hyps = self._reverse_bwd(hyps, y_lens)
+        return hyps, aw
+
+    @torch.no_grad()
+    def _decode_infer_greedy_steps(self, enc_out, x_lens, max_decode_len, task=0, dir='fwd'):
+        """:917-1036 step by step (decoders the fused greedy op does not cover)."""
+        att = getattr(self, 'attend_%d_%s' % (task, dir))
+        embed = getattr(self, 'embed_%d' % task)
+        eos, sos = getattr(self, 'eos_%d' % task), getattr(self, 'sos_%d' % task)
+        B = enc_out.shape[0]
+        dev = enc_out.device
+        enc_a = att.W_enc_head0(enc_out).unsqueeze(3)
+        lens = x_lens if torch.is_tensor(x_lens) else torch.from_numpy(
+            np.asarray(x_lens, np.int32)).to(dev)
+        st = self._init_state(enc_out, task, dir)
+        y = torch.full((B, 1), sos, dtype=torch.int64, device=dev)
+        toks, aws = [], []
+        for t in range(max_decode_len):
+            st, logits = self._infer_step(task, dir, t, embed(y).view(B, -1), st, enc_out, enc_a,
+                                          lens)
+            y = ops.row_argmax(logits).view(B, 1)
+            toks.append(y)
+            aws.append(st['aw'])
+            if bool((y == eos).all().item()):                     # :1017-1019
+                break
+        return (torch.cat(toks, dim=1).cpu().numpy(),
+                torch.stack(aws, dim=1).cpu().numpy())
+
+    def _decode_infer_greedy_fused(self, enc_out, x_lens, max_decode_len, task=0, dir='fwd'):
         """:917-1036 (bahdanau order, forward decoder): the whole loop is one
         fused decoder pass (native_ops.att_decode_greedy); the reference's early
         exit -- stop after the first step at which EVERY utterance emits <eos>
@@ -471,8 +699,8 @@ class AttentionSeq2seq(ModelBase):
         toks, aw = ops.att_decode_greedy(enc_out, enc_a, x_lens, h0, self._emb_dims[task],
                                          self.sharpening_factor, self.sigmoid_smoothing,
                                          cell.weight_ih, cell.weight_hh,
-                                         att.W_dec_head0.fc.weight, att.W_conv_head0.fc.weight,
-                                         att.conv_head0.weight, att.V_head0.fc.weight, gen,
+                                         att.W_dec_head0.fc.weight, *att.conv_weights(),
+                                         att.V_head0.fc.weight, gen,
                                          max_decode_len)
         toks = toks.cpu().numpy()
         all_eos = np.nonzero((toks == getattr(self, 'eos_%d' % task)).all(axis=0))[0]

@@ -50,7 +50,9 @@ class RNNDecoder(nn.Module):
                 hx_list[l] = ops.dropout(hx_list[l], self.dropout)
             if l > 0 and self.residual or self.dense_residual:     # rnn_decoder.py:100-104
                 if self.residual:
-                    hx_list[l] = ops.add(hx_list[l], hx_list[l - 1])
+                    # the reference's ``hx_list[l] += sum(hx_list[l - 1])``: Python's
+                    # sum over the lower layer's output runs over the batch rows
+                    hx_list[l] = ops.add_batch_sum(hx_list[l], hx_list[l - 1])
                 elif self.dense_residual:
                     for lower in hx_list[:l]:
                         hx_list[l] = ops.add(hx_list[l], lower)

@@ -1140,6 +1140,41 @@ def add(a, b):
     return AddFn.apply(a, b)
 
 
+class AddBatchSumFn(torch.autograd.Function):
+    """y[b] = h[b] + sum_b' lower[b'] -- the reference decoder's residual
+    connection ``hx_list[l] += sum(hx_list[l - 1])`` (rnn_decoder.py:100-102),
+    where Python's sum runs over the BATCH dimension of the lower layer's
+    output.  Both sums are [1 x B] x [B x D] products and the broadcast is a
+    K = 1 product accumulated onto a copy of h (asr_gemm)."""
+
+    @staticmethod
+    def _bsum_bcast(x, out):
+        """out[b] += sum_b' x[b'] for x, out [B, D] (out already holds the addend)."""
+        B, D = x.shape
+        dev = x.device
+        ones = torch.ones(B, 1, dtype=torch.float32, device=dev)
+        sm = torch.empty(1, D, dtype=torch.float32, device=dev)
+        run_gemm([gemm_problem(operand(ones, 1, rowmap(1)), operand(x, 1, rowmap(D)), sm,
+                               rowmap(D), 1, D, B)], dev)
+        run_gemm([gemm_problem(operand(ones, 0, rowmap(1)), operand(sm, 1, rowmap(D)), out,
+                               rowmap(D), B, D, 1, beta=1.0)], dev)
+        return out
+
+    @staticmethod
+    def forward(ctx, h, lower):
+        N.require_device(h, lower)
+        return AddBatchSumFn._bsum_bcast(lower.contiguous(), h.contiguous().clone())
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = dy.contiguous()
+        return dy, AddBatchSumFn._bsum_bcast(dy, torch.zeros_like(dy))
+
+
+def add_batch_sum(h, lower):
+    return AddBatchSumFn.apply(h, lower)
+
+
 class TanhFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x):

@@ -420,6 +420,20 @@ def case_attention_model():
                               label_smoothing_prob=0.1)),
         ('model_att_mean', dict(base, init_dec_state='mean', ctc_loss_weight=0,
                                 label_smoothing_prob=0)),
+        # decoder / attention variants (attention_seq2seq.py:280-361, 704-799,
+        # attention_layer.py:66-72, 145-153)
+        ('model_att_content', dict(base, attention_type='content', init_dec_state='zero')),
+        ('model_att_bwd', dict(base, init_dec_state='first', backward_loss_weight=0.4)),
+        ('model_att_bwd_only', dict(base, init_dec_state='final', backward_loss_weight=1.0)),
+        ('model_att_dec2', dict(base, init_dec_state='first', decoder_num_layers=2,
+                                decoder_residual=True)),
+        ('model_att_dec3_dres', dict(base, init_dec_state='zero', decoder_num_layers=3,
+                                     decoder_dense_residual=True)),
+        ('model_att_luong', dict(base, init_dec_state='zero', decoding_order='luong')),
+        ('model_att_cond', dict(base, init_dec_state='first', decoding_order='conditional')),
+        ('model_att_bridge', dict(base, init_dec_state='first', bridge_layer=True,
+                                  ctc_loss_weight=0.2)),
+        ('model_att_gru_enc', dict(base, encoder_type='gru', init_dec_state='first')),
     ]
     only = _selected()
     for name, kw in specs:
@@ -831,6 +845,60 @@ def case_hier_attention_beam():
           seed=np.array([seed]), xs=xs, x_lens=x_lens, **arrays, **_sd(model))
 
 
+def case_decode_variants():
+    """Greedy and beam decoding (attention_seq2seq.py:866-1237) of decoder
+    variants: luong and conditional orders, a 2-layer residual decoder, the
+    backward decoder alone (hypotheses reversed) and with a weaker forward one
+    (decodes forward).  Random init uniform +-0.6; the seed is the first whose
+    greedy output has at least three distinct tokens."""
+    from models.pytorch_v3.attention.attention_seq2seq import AttentionSeq2seq
+    _install_beam_shims()
+    only = _selected()
+    base = dict(input_size=8, encoder_type='lstm', encoder_bidirectional=True,
+                encoder_num_units=6, encoder_num_proj=0, encoder_num_layers=2,
+                attention_type='location', attention_dim=7, decoder_type='lstm',
+                decoder_num_units=9, decoder_num_layers=1, embedding_dim=4,
+                dropout_input=0, dropout_encoder=0, dropout_decoder=0, dropout_embedding=0,
+                num_classes=6, parameter_init=0.1, subsample_list=[False, True],
+                subsample_type='drop', attention_conv_num_channels=3,
+                attention_conv_width=5, bottleneck_dim=11, ctc_loss_weight=0,
+                label_smoothing_prob=0, init_dec_state='zero')
+    specs = [('decv_luong', dict(base, decoding_order='luong')),
+             ('decv_cond', dict(base, decoding_order='conditional', init_dec_state='first')),
+             ('decv_dec2', dict(base, decoder_num_layers=2, decoder_residual=True)),
+             ('decv_bwd', dict(base, backward_loss_weight=1.0, init_dec_state='final')),
+             ('decv_content', dict(base, attention_type='content'))]
+    rng0 = np.random.RandomState(6)
+    B, T = 4, 22
+    x_lens = np.array([22, 17, 20, 11], np.int32)
+    xs = rng0.randn(B, T, 8).astype(np.float32)
+    for b in range(B):
+        xs[b, x_lens[b]:] = 0
+    for name, kw in specs:
+        if only and name not in only:
+            continue
+        for seed in range(1623, 1623 + 500):
+            torch.manual_seed(seed)
+            model = AttentionSeq2seq(**kw)
+            for p in model.parameters():
+                torch.nn.init.uniform_(p, -0.6, 0.6)
+            with torch.no_grad():
+                g_hyps, g_aw, perm = model.decode(xs, x_lens, beam_width=1, max_decode_len=12)
+            if len(np.unique(np.asarray(g_hyps))) >= 3:
+                break
+        else:
+            raise RuntimeError('no seed found for ' + name)
+        with torch.no_grad():
+            b_hyps, b_aw, _ = model.decode(xs, x_lens, beam_width=3, max_decode_len=12)
+        _save(name, kwargs=np.array(json.dumps(kw)), seed=np.array([seed]), xs=xs,
+              x_lens=x_lens, greedy=np.asarray(g_hyps, np.int64),
+              greedy_aw=np.asarray(g_aw, np.float32), perm=np.asarray(perm).astype(np.int64),
+              beam_flat=np.concatenate([np.asarray(h, np.int64) for h in b_hyps]),
+              beam_lens=np.array([len(h) for h in b_hyps], np.int32),
+              beam_aw_flat=np.concatenate([np.asarray(a, np.float32).reshape(-1) for a in b_aw]),
+              **_sd(model))
+
+
 if __name__ == '__main__':
     _install_shims()
     if _selected():          # regenerate only the named model_ctc_* / dec_* cases
@@ -841,6 +909,7 @@ if __name__ == '__main__':
         case_attention_prod()
         case_attention_beam()
         case_hier_attention_beam()
+        case_decode_variants()
         if 'loader' in _selected():
             case_loader()
         sys.exit(0)
@@ -857,3 +926,4 @@ if __name__ == '__main__':
     case_loader()
     case_attention_beam()
     case_hier_attention_beam()
+    case_decode_variants()

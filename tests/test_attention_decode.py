@@ -118,3 +118,35 @@ def test_hierarchical_beam_decode_matches_golden(cuda_dev):
                                       d['hyp_flat_%d' % task])
         got = np.concatenate([np.asarray(a, np.float32).reshape(-1) for a in aw])
         np.testing.assert_allclose(got, d['aw_flat_%d' % task], rtol=1e-3, atol=1e-5)
+
+
+VARIANT_NAMES = ['decv_luong', 'decv_cond', 'decv_dec2', 'decv_bwd', 'decv_content']
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name', VARIANT_NAMES)
+def test_decode_variants_match_golden(name, cuda_dev):
+    """Greedy (per-step HIP ops for orders / depths the fused greedy pass does
+    not cover; the fused pass for content attention) and beam-3 decoding of
+    decoder variants vs the reference, fp32 mode: luong / conditional orders,
+    a 2-layer residual decoder, the backward decoder (hypotheses reversed)."""
+    from pytorch_end2end_speech_recognition_amd import native_ops
+    from pytorch_end2end_speech_recognition_amd.models.pytorch_v3.attention.attention_seq2seq \
+        import AttentionSeq2seq
+    d = golden(name)
+    kw = json.loads(str(d['kwargs']))
+    sd, _ = golden_params(d)
+    torch.manual_seed(int(d['seed'][0]))
+    model = AttentionSeq2seq(**kw)
+    model.load_state_dict(sd)
+    model.set_cuda()
+    native_ops.set_compute_dtype('fp32')
+    hyps, aw, perm = model.decode(d['xs'], d['x_lens'], beam_width=1, max_decode_len=12)
+    np.testing.assert_array_equal(perm, d['perm'])
+    np.testing.assert_array_equal(hyps, d['greedy'])
+    np.testing.assert_allclose(aw, d['greedy_aw'], rtol=1e-3, atol=1e-5)
+    hyps, aw, _ = model.decode(d['xs'], d['x_lens'], beam_width=3, max_decode_len=12)
+    np.testing.assert_array_equal([len(h) for h in hyps], d['beam_lens'])
+    np.testing.assert_array_equal(np.concatenate([np.asarray(h) for h in hyps]), d['beam_flat'])
+    got = np.concatenate([np.asarray(a, np.float32).reshape(-1) for a in aw])
+    np.testing.assert_allclose(got, d['beam_aw_flat'], rtol=1e-3, atol=1e-5)

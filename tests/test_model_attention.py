@@ -1,5 +1,6 @@
-"""Drop-in AttentionSeq2seq (location attention, bahdanau, +/- auxiliary CTC)
-vs the reference's golden vectors.  CPU: bit-identical initial state_dict under
+"""Drop-in AttentionSeq2seq (location / content attention, bahdanau / luong /
+conditional order, 1-3 layer decoders, forward and backward decoders, bridge,
++/- auxiliary CTC) vs the reference's golden vectors.  CPU: bit-identical initial state_dict under
 the reference's seed.  GPU: loss and every parameter gradient."""
 import json
 
@@ -9,7 +10,14 @@ import torch
 
 from conftest import golden, golden_params
 
-NAMES = ['model_att', 'model_att_hybrid', 'model_att_ls', 'model_att_mean']
+NAMES = ['model_att', 'model_att_hybrid', 'model_att_ls', 'model_att_mean',
+         # variants: content attention (the location kernels with one all-zero
+         # conv channel), backward decoder (+/- forward), multi-layer residual /
+         # dense-residual decoders, luong / conditional orders (the per-step
+         # loop), bridge layer + CTC, GRU encoder
+         'model_att_content', 'model_att_bwd', 'model_att_bwd_only', 'model_att_dec2',
+         'model_att_dec3_dres', 'model_att_luong', 'model_att_cond', 'model_att_bridge',
+         'model_att_gru_enc']
 
 
 def _build(kw):
