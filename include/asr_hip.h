@@ -240,6 +240,16 @@ int asr_gru_backward(const float* dy, const float* whh, const int32_t* lens, int
                      float* act_dgx, const float* ghn, const float* y, float* dgh,
                      void* workspace, size_t ws_bytes, void* stream);
 
+/* nn.GRUCell nonlinearity (decoder cells, rnn_decoder.py:91-95): gi = x W_ih^T +
+ * b_ih, gh = h W_hh^T + b_hh [B][3D] (GEMMs by the caller); act [B][3D] out =
+ * r, z, n; hout = (1 - z) n + z h.  Backward: dgi, dgh [B][3D] (the gate
+ * gradients of the two GEMMs' outputs) and dh_prev = dh z (the direct term;
+ * the caller adds dgh W_hh). */
+int asr_gru_cell_forward(const float* gi, const float* gh, const float* h, int B, int D,
+                         float* act, float* hout, void* stream);
+int asr_gru_cell_backward(const float* act, const float* gh, const float* h, const float* dh,
+                          int B, int D, float* dgi, float* dgh, float* dh_prev, void* stream);
+
 /* ------------------------------------------------------------ optimizer
  * Replaces torch.nn.utils.clip_grad_norm(params, max_norm)
  * (utils/training/training_loop.py:46-50) + torch.optim Adam / SGD /

@@ -58,6 +58,9 @@ SIGNATURES = {
     'asr_gru_forward': (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp]),
     'asr_gru_backward': (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp,
                                  c_vp, c_size, c_vp]),
+    'asr_gru_cell_forward': (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp]),
+    'asr_gru_cell_backward': (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp,
+                                      c_vp]),
     'asr_grad_sqnorm_workspace_bytes': (c_size, []),
     'asr_grad_sqnorm': (c_int, [c_vp, c_ll, c_vp, c_vp, c_size, c_vp]),
     'asr_optim_step': (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_ll, c_float, c_float, c_float,

@@ -191,6 +191,48 @@ __global__ void __launch_bounds__(256) gru_bwd_step(
 
 size_t gru_dhz_bytes(int B, int H) { return (((size_t)2 * B * 2 * H * 4) + 255) / 256 * 256; }
 
+// nn.GRUCell nonlinearity (the decoder cell, rnn_decoder.py:91-95):
+// gi = x W_ih^T + b_ih, gh = h W_hh^T + b_hh [B][3D] (GEMMs outside).
+__global__ void gru_cell_fwd(const float* __restrict__ gi, const float* __restrict__ gh,
+                             const float* __restrict__ h, int B, int D, float* __restrict__ act,
+                             float* __restrict__ hout) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long long)B * D) return;
+  const long long b = e / D, j = e - b * D;
+  const long long g = b * 3 * D + j;
+  const float r = sigmoidf_(gi[g] + gh[g]);
+  const float z = sigmoidf_(gi[g + D] + gh[g + D]);
+  const float n = tanhf_(gi[g + 2 * D] + r * gh[g + 2 * D]);
+  hout[e] = (1.f - z) * n + z * h[e];
+  act[g] = r;
+  act[g + D] = z;
+  act[g + 2 * D] = n;
+}
+
+__global__ void gru_cell_bwd(const float* __restrict__ act, const float* __restrict__ gh,
+                             const float* __restrict__ h, const float* __restrict__ dh, int B,
+                             int D, float* __restrict__ dgi, float* __restrict__ dgh,
+                             float* __restrict__ dh_prev) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long long)B * D) return;
+  const long long b = e / D, j = e - b * D;
+  const long long g = b * 3 * D + j;
+  const float r = act[g], z = act[g + D], n = act[g + 2 * D];
+  const float d = dh[e];
+  const float dn = d * (1.f - z);
+  const float dz = d * (h[e] - n);
+  const float dpn = dn * (1.f - n * n);
+  const float dpr = dpn * gh[g + 2 * D] * r * (1.f - r);
+  const float dpz = dz * z * (1.f - z);
+  dgi[g] = dpr;
+  dgi[g + D] = dpz;
+  dgi[g + 2 * D] = dpn;
+  dgh[g] = dpr;
+  dgh[g + D] = dpz;
+  dgh[g + 2 * D] = dpn * r;
+  dh_prev[e] = d * z;
+}
+
 }  // namespace
 }  // namespace asr
 
@@ -236,5 +278,27 @@ extern "C" int asr_gru_backward(const float* dy, const float* whh, const int32_t
                        ghn, y, dgh, dhz);
     ASR_LAUNCH_CHECK();
   }
+  return ASR_OK;
+}
+
+extern "C" int asr_gru_cell_forward(const float* gi, const float* gh, const float* h, int B, int D,
+                                    float* act, float* hout, void* stream) {
+  ASR_REQUIRE(gi && gh && h && act && hout && B > 0 && D > 0, ASR_ERR_ARG, "gru_cell: bad args");
+  const long long n = (long long)B * D;
+  hipLaunchKernelGGL(gru_cell_fwd, dim3(ceil_div(n, 256)), dim3(256), 0, (hipStream_t)stream, gi,
+                     gh, h, B, D, act, hout);
+  ASR_LAUNCH_CHECK();
+  return ASR_OK;
+}
+
+extern "C" int asr_gru_cell_backward(const float* act, const float* gh, const float* h,
+                                     const float* dh, int B, int D, float* dgi, float* dgh,
+                                     float* dh_prev, void* stream) {
+  ASR_REQUIRE(act && gh && h && dh && dgi && dgh && dh_prev && B > 0 && D > 0, ASR_ERR_ARG,
+              "gru_cell: bad args");
+  const long long n = (long long)B * D;
+  hipLaunchKernelGGL(gru_cell_bwd, dim3(ceil_div(n, 256)), dim3(256), 0, (hipStream_t)stream, act,
+                     gh, h, dh, B, D, dgi, dgh, dh_prev);
+  ASR_LAUNCH_CHECK();
   return ASR_OK;
 }

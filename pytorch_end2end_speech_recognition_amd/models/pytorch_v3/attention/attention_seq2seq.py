@@ -110,8 +110,6 @@ class AttentionSeq2seq(ModelBase):
             unsupported.append('cnn encoder')
         if coverage_weight != 0:
             unsupported.append('coverage')
-        if decoder_type != 'lstm':
-            unsupported.append('decoder_type=%s' % decoder_type)
         if unsupported:
             raise NotImplementedError('MI355X AttentionSeq2seq: not yet supported: ' +
                                       ', '.join(unsupported))
@@ -317,7 +315,17 @@ class AttentionSeq2seq(ModelBase):
         without residual connections (location or content attention)."""
         dec = getattr(self, 'decoder_%d_%s' % (task, dir), None)
         return (self.decoding_order == 'bahdanau' and dec is not None and dec.num_layers == 1
-                and not dec.residual and not dec.dense_residual)
+                and dec.rnn_type == 'lstm' and not dec.residual and not dec.dense_residual)
+
+    @staticmethod
+    def _run_dec(mod, inp, hx, cx):
+        """RNNDecoder.forward with the (hx, cx) pair of either cell type (GRU
+        decoders carry hx only)."""
+        if mod.rnn_type == 'gru':
+            out, hx = mod(inp, hx)
+            return out, hx, cx
+        out, (hx, cx) = mod(inp, (hx, cx))
+        return out, hx, cx
 
     def _decode_train(self, enc_out, x_lens, ys, task=0, dir='fwd'):
         if not self._fused_ok(task, dir):
@@ -376,17 +384,18 @@ class AttentionSeq2seq(ModelBase):
                 y = y_emb[:, t]
             if order == 'bahdanau':
                 if t > 0:
-                    d3, (hx, cx) = dec1(torch.cat([y, ctx], dim=-1).unsqueeze(1), (hx, cx))
+                    d3, hx, cx = self._run_dec(dec1, torch.cat([y, ctx], dim=-1).unsqueeze(1),
+                                               hx, cx)
                     dec_out = d3.squeeze(1)
                 c3, a3 = att(enc_out, enc_a, lens, dec_out.unsqueeze(1), aw.unsqueeze(2))
             elif order == 'luong':
-                d3, (hx, cx) = dec1(torch.cat([y, ctx], dim=-1).unsqueeze(1), (hx, cx))
+                d3, hx, cx = self._run_dec(dec1, torch.cat([y, ctx], dim=-1).unsqueeze(1), hx, cx)
                 dec_out = d3.squeeze(1)
                 c3, a3 = att(enc_out, enc_a, lens, dec_out.unsqueeze(1), aw.unsqueeze(2))
             else:                                                 # conditional
-                d3, (hx, cx) = dec1(y.unsqueeze(1), (hx, cx))
+                d3, hx, cx = self._run_dec(dec1, y.unsqueeze(1), hx, cx)
                 c3, a3 = att(enc_out, enc_a, lens, d3, aw.unsqueeze(2))
-                d3, (hx, cx) = dec2(c3, (hx, cx))
+                d3, hx, cx = self._run_dec(dec2, c3, hx, cx)
                 dec_out = d3.squeeze(1)
             ctx, aw = c3.squeeze(1), a3.squeeze(2)
             decs.append(dec_out)
@@ -502,14 +511,15 @@ class AttentionSeq2seq(ModelBase):
         if self.decoding_order == 'conditional':
             d1 = getattr(self, 'decoder_first_%d_%s' % (task, dir))
             d2 = getattr(self, 'decoder_second_%d_%s' % (task, dir))
-            dd, (hx, cx) = d1(y_emb.unsqueeze(1), (hx, cx))
+            dd, hx, cx = self._run_dec(d1, y_emb.unsqueeze(1), hx, cx)
             c3, a3 = att(enc, enc_a, lens, dd, aw.unsqueeze(2))
-            d3, (hx, cx) = d2(c3, (hx, cx))
+            d3, hx, cx = self._run_dec(d2, c3, hx, cx)
             dec = d3.squeeze(1)
         else:
             dm = getattr(self, 'decoder_%d_%s' % (task, dir))
             if self.decoding_order == 'luong' or t > 0:
-                d3, (hx, cx) = dm(torch.cat([y_emb, ctx], dim=-1).unsqueeze(1), (hx, cx))
+                d3, hx, cx = self._run_dec(dm, torch.cat([y_emb, ctx], dim=-1).unsqueeze(1),
+                                           hx, cx)
                 dec = d3.squeeze(1)
             c3, a3 = att(enc, enc_a, lens, dec.unsqueeze(1), aw.unsqueeze(2))
         ctx, aw = c3.reshape(n, -1), a3.reshape(n, L)

@@ -605,6 +605,38 @@ class LSTMCellFn(torch.autograd.Function):
         return dpre, dc_prev
 
 
+class GRUCellFn(torch.autograd.Function):
+    """nn.GRUCell nonlinearity on the two GEMM outputs (gi = x W_ih^T + b_ih,
+    gh = h W_hh^T + b_hh, [B, 3D]) and h -> h' (csrc/gru.hip)."""
+
+    @staticmethod
+    def forward(ctx, gi, gh, h):
+        N.require_device(gi, gh, h)
+        gi, gh, h = gi.contiguous(), gh.contiguous(), h.contiguous()
+        B, D = h.shape
+        act = torch.empty_like(gi)
+        hout = torch.empty_like(h)
+        N.call('asr_gru_cell_forward', N.ptr(gi), N.ptr(gh), N.ptr(h), B, D, N.ptr(act),
+               N.ptr(hout), N.stream_handle(h.device))
+        ctx.save_for_backward(act, gh, h)
+        return hout
+
+    @staticmethod
+    def backward(ctx, dh):
+        act, gh, h = ctx.saved_tensors
+        B, D = h.shape
+        dgi, dgh = torch.empty_like(act), torch.empty_like(act)
+        dh_prev = torch.empty_like(h)
+        N.call('asr_gru_cell_backward', N.ptr(act), N.ptr(gh), N.ptr(h), N.ptr(dh.contiguous()),
+               B, D, N.ptr(dgi), N.ptr(dgh), N.ptr(dh_prev), N.stream_handle(h.device))
+        return dgi, dgh, dh_prev
+
+
+def gru_cell(x, h, w_ih, w_hh, b_ih, b_hh):
+    """One nn.GRUCell step on the HIP GEMM + cell kernels."""
+    return GRUCellFn.apply(linear(x, w_ih, b_ih), linear(h, w_hh, b_hh), h)
+
+
 def lstm_cell(x, h, c, w_ih, w_hh, b_ih, b_hh):
     """One nn.LSTMCell step on the HIP GEMM + cell kernels."""
     pre = linear2(x, w_ih, b_ih, h, w_hh, b_hh)

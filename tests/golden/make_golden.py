@@ -434,6 +434,11 @@ def case_attention_model():
         ('model_att_bridge', dict(base, init_dec_state='first', bridge_layer=True,
                                   ctc_loss_weight=0.2)),
         ('model_att_gru_enc', dict(base, encoder_type='gru', init_dec_state='first')),
+        # TIMIT bgru_att_phone61 shape family: GRU encoder + bridge + GRU decoder
+        ('model_att_gru', dict(base, encoder_type='gru', decoder_type='gru', bridge_layer=True,
+                               init_dec_state='first')),
+        ('model_att_gru_dec2', dict(base, decoder_type='gru', decoder_num_layers=2,
+                                    init_dec_state='first', decoding_order='luong')),
     ]
     only = _selected()
     for name, kw in specs:
@@ -867,7 +872,9 @@ def case_decode_variants():
              ('decv_cond', dict(base, decoding_order='conditional', init_dec_state='first')),
              ('decv_dec2', dict(base, decoder_num_layers=2, decoder_residual=True)),
              ('decv_bwd', dict(base, backward_loss_weight=1.0, init_dec_state='final')),
-             ('decv_content', dict(base, attention_type='content'))]
+             ('decv_content', dict(base, attention_type='content')),
+             ('decv_gru', dict(base, encoder_type='gru', decoder_type='gru', bridge_layer=True,
+                               init_dec_state='first'))]
     rng0 = np.random.RandomState(6)
     B, T = 4, 22
     x_lens = np.array([22, 17, 20, 11], np.int32)

@@ -120,7 +120,7 @@ def test_hierarchical_beam_decode_matches_golden(cuda_dev):
         np.testing.assert_allclose(got, d['aw_flat_%d' % task], rtol=1e-3, atol=1e-5)
 
 
-VARIANT_NAMES = ['decv_luong', 'decv_cond', 'decv_dec2', 'decv_bwd', 'decv_content']
+VARIANT_NAMES = ['decv_luong', 'decv_cond', 'decv_dec2', 'decv_bwd', 'decv_content', 'decv_gru']
 
 
 @pytest.mark.gpu

@@ -17,7 +17,7 @@ NAMES = ['model_att', 'model_att_hybrid', 'model_att_ls', 'model_att_mean',
          # loop), bridge layer + CTC, GRU encoder
          'model_att_content', 'model_att_bwd', 'model_att_bwd_only', 'model_att_dec2',
          'model_att_dec3_dres', 'model_att_luong', 'model_att_cond', 'model_att_bridge',
-         'model_att_gru_enc']
+         'model_att_gru_enc', 'model_att_gru', 'model_att_gru_dec2']
 
 
 def _build(kw):
