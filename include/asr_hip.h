@@ -221,6 +221,20 @@ int asr_lstm_backward_db(const float* dy, const void* whh_f, const void* whh_r, 
                          float* act_dg, const float* cst, uint16_t* dgbf, float* db_ih,
                          float* db_hh, void* workspace, size_t ws_bytes, void* stream);
 
+/* Forward layer pass with the input projection fused into the persistent
+ * recurrence (bf16 mode; replaces asr_gemm(gx = x W_ih^T + b_ih + b_hh) +
+ * asr_lstm_forward): x [B*T][Din] bf16 rows (b, t) of the layer input, wih
+ * [8H][Din] bf16 = [W_ih fwd; W_ih rev], b_ih / b_hh f32 [8H], whh f32 [4H][H]
+ * per direction.  act [B][T][8H] f32 receives the post-activation gates (the
+ * backward's input, as gx_act after asr_lstm_forward); y, cst, ybf as there.
+ * ASR_ERR_UNSUPPORTED: this shape / device does not take the path
+ * (asr_lstm_forward_x_ok tells beforehand). */
+int asr_lstm_forward_x(const uint16_t* x, int Din, const uint16_t* wih, const float* b_ih,
+                       const float* b_hh, const float* whh_f, const float* whh_r,
+                       const int32_t* lens, int B, int T, int H, float* act, float* y, float* cst,
+                       uint16_t* ybf, void* workspace, size_t ws_bytes, void* stream);
+int asr_lstm_forward_x_ok(int B, int H, int Din);
+
 /* ------------------------------------------------------------ GRU layer
  * Replaces the packed nn.GRU(bidirectional=True) of
  * models/pytorch_v3/encoders/rnn.py:173-191 (fast path) / :226-233 (per layer).

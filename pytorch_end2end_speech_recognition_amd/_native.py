@@ -22,6 +22,7 @@ c_vp = ctypes.c_void_p
 c_str = ctypes.c_char_p
 
 ASR_OK = 0
+ASR_ERR_UNSUPPORTED = -4
 ASR_DT_F32 = 0
 ASR_DT_BF16 = 1
 
@@ -54,6 +55,9 @@ SIGNATURES = {
                                   c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
     'asr_lstm_backward_db': (c_int, [c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int,
                                      c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
+    'asr_lstm_forward_x': (c_int, [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int,
+                                   c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
+    'asr_lstm_forward_x_ok': (c_int, [c_int, c_int, c_int]),
     'asr_gru_workspace_bytes': (c_size, [c_int, c_int]),
     'asr_gru_forward': (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp]),
     'asr_gru_backward': (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp,

@@ -428,6 +428,269 @@ __global__ void __launch_bounds__(64 * NSW + R * XU) lstm_fwd_xg(
 }
 
 // ---------------------------------------------------------------------------
+// forward with the input projection fused (lstm_fwd_xgx).  Same hand-off,
+// sweepers and cell waves as lstm_fwd_xg, but gx = x W_ih^T + b_ih + b_hh is
+// not precomputed by a GEMM: NPW producer waves hold this work-group's 64 rows
+// of W_ih as bf16 MFMA B fragments (k-steps p, p + NPW, ... of K = Din) in
+// VGPRs and, one step ahead of the recurrence, multiply the bf16 input rows
+// x[b, t] of the group's R utterances (loaded a further step ahead).  Their
+// partial gate inputs go to LDS (double-buffered by step parity) before
+// barrier B(s); the cell waves sum them with the biases for step s + 1 after
+// publishing h_s -- where lstm_fwd_xg prefetched gx from HBM -- so nothing is
+// added to the hand-off chain.  `act` receives the post-activation gates for
+// the backward and is never read here.
+//
+// LDS hazards (producers write pre(s+1) into xpart[(s+1)&1] between Bp(s-1)
+// and B(s); cells read pre(s+1) between Bp(s) and B(s+1)): the buffer a
+// producer overwrites at iteration s was last read before B(s-1).
+// ---------------------------------------------------------------------------
+template <int R, int KSW, int NSW, int NPW, int KPW>
+__global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
+    int B, int T, int H, const int32_t* __restrict__ lens, const float* __restrict__ whh_f,
+    const float* __restrict__ whh_r, const uint16_t* __restrict__ x, int Din,
+    const uint16_t* __restrict__ wih, const float* __restrict__ b_ih,
+    const float* __restrict__ b_hh, float* __restrict__ act, float* __restrict__ y,
+    float* __restrict__ cst, unsigned long long* xg, int* hdr, uint16_t* __restrict__ ybf,
+    int allow_local) {
+  __shared__ float part[2][NSW][R][4 * XU + 4];
+  __shared__ float xpart[2][NPW][R][4 * XU + 4];
+  __shared__ int s_dead;
+  __shared__ int s_pl[4];
+  int* abortw = hdr;
+  const int WPG = H / XU;
+  const int G = gridDim.x / WPG;
+  if (threadIdx.x == 0) s_dead = 0;
+  xg_place(WPG, allow_local, hdr, s_pl);
+  if (!s_pl[3]) return;
+  const int grp = s_pl[0], mem = s_pl[1];
+  const bool local = s_pl[2] != 0;
+  const int dir = grp & 1, rg = grp >> 1;
+  const int u0 = mem * XU, b0 = rg * R;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nks = H >> 5;
+  const unsigned quarter = (unsigned)(H / 4);
+  constexpr int NCW = R * XU / 64;
+
+  if (wave < NSW) {
+    // ------------------------------ sweeper (as lstm_fwd_xg) ------------------
+    const int kq = lane >> 4, ln = lane & 15;
+    const bool sweeper = ln < R;
+    bf16x8 wf[KSW][4];
+    {
+      const float* W = dir ? whh_r : whh_f;
+#pragma unroll
+      for (int i = 0; i < KSW; ++i) {
+        const int ks = min(wave + NSW * i, nks - 1);
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          wf[i][g] = cvt_f32x8(W + (long long)(g * H + u0 + ln) * H + 32 * ks + 8 * kq);
+      }
+    }
+    const unsigned xg_bytes = (unsigned)(2ull * G * R * quarter * 8);
+    const __amdgpu_buffer_rsrc_t rs = xg_rsrc(xg, xg_bytes);
+    const int nsleep = __builtin_amdgcn_readfirstlane(g_xg_sleep);
+    const int ndelay = __builtin_amdgcn_readfirstlane(g_xg_delay);
+    __syncthreads();  // B_init: the producers' pre(0) is in LDS
+    for (int s = 0; s < T; ++s) {
+      f32x4 acc[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (s > 0) {
+        const unsigned ebit = tag_bit(s - 1);
+        const unsigned rowoff = (unsigned)((((((s - 1) & 1) * G + grp) * R + (sweeper ? ln : 0)) *
+                                            (long long)quarter) * 8);
+        u32x4 v[KSW];
+        nap(ndelay);
+        for (unsigned spins = 0;; ++spins) {
+          int ok = 1;
+          if (sweeper) {
+#pragma unroll
+            for (int i = 0; i < KSW; ++i)
+              v[i] = ld_sc1(rs, rowoff + (unsigned)((8 * min(wave + NSW * i, nks - 1) + 2 * kq) * 8));
+#pragma unroll
+            for (int i = 0; i < KSW; ++i)
+              ok &= (int)((((v[i][0] ^ ebit) | (v[i][2] ^ ebit)) & 1u) == 0u);
+          }
+          if (__all(ok)) break;
+          if (!keep_spinning(spins, abortw, nsleep)) {
+            s_dead = 1;
+            break;
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < KSW; ++i) {
+          if (wave + NSW * i < nks) {  // wave-uniform
+            u32x4 z = {0u, 0u, 0u, 0u};
+            const bf16x8 a = __builtin_bit_cast(bf16x8, sweeper ? v[i] : z);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) acc[g] = mfma_bf16(a, wf[i][g], acc[g]);
+          }
+        }
+      }
+      if (4 * kq < R) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) part[s & 1][wave][4 * kq + r][g * XU + ln] = acc[g][r];
+      }
+      __syncthreads();  // B(s)
+      if (s_dead) return;
+      __syncthreads();  // Bp(s)
+    }
+    return;
+  }
+
+  if (wave >= NSW + NCW) {
+    // ------------------------------ producer ----------------------------------
+    const int pw = wave - NSW - NCW;
+    const int kq = lane >> 4, ln = lane & 15;
+    const int nkx = (Din + 31) >> 5;
+    const u16x8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
+    // B fragments: B[k][n] = W_ih[dir*4H + g*H + u0 + n][k], n = ln, k = 32 ks + 8 kq + j
+    bf16x8 wb[KPW][4];
+#pragma unroll
+    for (int i = 0; i < KPW; ++i) {
+      const int k = 32 * (pw + NPW * i) + 8 * kq;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const long long row = (long long)dir * 4 * H + (long long)g * H + u0 + ln;
+        wb[i][g] = k < Din ? load_bf16x8(wih + row * Din + k) : as_bf16x8(z8);
+      }
+    }
+    // A fragments: A[m][k] = x[b0 + m][t][k], rows m < R real
+    const bool arow = ln < R && b0 + ln < B;
+    const uint16_t* xb = x + (long long)(arow ? b0 + ln : 0) * T * Din;
+    bf16x8 a[KPW];
+    auto load_a = [&](int st) {
+      const int t = dir ? T - 1 - st : st;
+#pragma unroll
+      for (int i = 0; i < KPW; ++i) {
+        const int k = 32 * (pw + NPW * i) + 8 * kq;
+        a[i] = (arow && k < Din) ? load_bf16x8(xb + (long long)t * Din + k) : as_bf16x8(z8);
+      }
+    };
+    auto produce = [&](int st) {
+      f32x4 acc[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < KPW; ++i) {
+        if (pw + NPW * i < nkx) {  // wave-uniform
+#pragma unroll
+          for (int g = 0; g < 4; ++g) acc[g] = mfma_bf16(a[i], wb[i][g], acc[g]);
+        }
+      }
+      if (4 * kq < R) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) xpart[st & 1][pw][4 * kq + r][g * XU + ln] = acc[g][r];
+      }
+    };
+    load_a(0);
+    produce(0);
+    if (T > 1) load_a(1);
+    __syncthreads();  // B_init
+    for (int s = 0; s < T; ++s) {
+      if (s + 1 < T) {
+        produce(s + 1);
+        if (s + 2 < T) load_a(s + 2);
+      }
+      __syncthreads();  // B(s)
+      if (s_dead) return;
+      __syncthreads();  // Bp(s)
+    }
+    return;
+  }
+
+  // -------------------------------- cell ----------------------------------
+  const int ct = tid - 64 * NSW;
+  const int row = ct >> 4, unit = ct & 15;
+  const int b = b0 + row, j = u0 + unit;
+  const bool own = b < B;
+  const int len = own ? lens[b] : 0;
+  float c = 0.f;
+  const long long H8 = 8LL * H;
+  const long long gcol = (long long)dir * 4 * H + j;
+  gu64* xgg = (gu64*)xg;
+  float bsum[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) bsum[q] = b_ih[gcol + (long long)q * H] + b_hh[gcol + (long long)q * H];
+  float gxv[4];
+  __syncthreads();  // B_init
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float v = bsum[q];
+#pragma unroll
+    for (int p = 0; p < NPW; ++p) v += xpart[0][p][row][q * XU + unit];
+    gxv[q] = v;
+  }
+  __builtin_amdgcn_s_setprio(2);  // the cell update + publish is the critical path
+  for (int s = 0; s < T; ++s) {
+    const int t = dir ? T - 1 - s : s;
+    __syncthreads();  // B(s)
+    if (s_dead) return;
+    float h = 0.f, cn = 0.f, ig = 0.f, fg = 0.f, gg = 0.f, og = 0.f;
+    const bool active = own && t < len;
+    if (active) {
+      float pre[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int col = q * XU + unit;
+        float a = part[s & 1][0][row][col];
+#pragma unroll
+        for (int w = 1; w < NSW; ++w) a += part[s & 1][w][row][col];
+        pre[q] = a + gxv[q];
+      }
+      ig = fsig(pre[0]);
+      fg = fsig(pre[1]);
+      gg = ftanh(pre[2]);
+      og = fsig(pre[3]);
+      cn = fg * c + ig * gg;
+      h = og * ftanh(cn);
+    }
+    c = cn;
+    const unsigned hb = f2bf(h);
+    const unsigned h1 = row_from_upper<1>(hb);
+    const unsigned val = hb | (h1 << 16);
+    const unsigned h2 = row_from_upper<2>(hb), h3 = row_from_upper<3>(hb);
+    const unsigned h0t = bf_with_lsb(h, tag_bit(s));
+    if ((unit & 3) == 0) {
+      const unsigned long long gr =
+          ((unsigned long long)(h2 | (h3 << 16)) << 32) | (h0t | (h1 << 16));
+      gu64* p = xgg + ((((long long)(s & 1) * G + grp) * R + row) * quarter + (j >> 2));
+      if (local)
+        __hip_atomic_store(p, gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      else
+        __hip_atomic_store(p, gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();  // Bp(s)
+    if (own) {
+      const long long sidx = ((long long)b * T + t) * 2 * H + (long long)dir * H + j;
+      y[sidx] = h;
+      cst[sidx] = cn;
+      const long long gb = ((long long)b * T + t) * H8 + gcol;
+      act[gb] = ig;
+      act[gb + H] = fg;
+      act[gb + 2 * H] = gg;
+      act[gb + 3 * H] = og;
+      if (ybf && (unit & 1) == 0)
+        *reinterpret_cast<uint32_t*>(ybf + ((long long)b * T + t) * 2 * H + dir * H + j) = val;
+    }
+    if (s + 1 < T) {  // the producers wrote pre(s+1) before B(s)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float v = bsum[q];
+#pragma unroll
+        for (int p = 0; p < NPW; ++p) v += xpart[(s + 1) & 1][p][row][q * XU + unit];
+        gxv[q] = v;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // backward.  grid = G * WPG.  Processing step q handles the forward direction
 // at t = T-1-q and the reverse direction at t = q.
 // Granules: pg[par][grp][producer][row][H/4] u64 = four bf16 partials of dh
@@ -856,6 +1119,60 @@ int lstm_bwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* wh
   return hipGetLastError() == hipSuccess ? 1 : -1;
 }
 
+
+// Fused-projection forward (lstm_fwd_xgx): 1 if launched (dry: eligible), 0 if
+// not eligible (ASR_FUSE_XPROJ=0, shape, Din % 8 or Din > 32 * 8 * KPW_MAX),
+// -1 on a launch error.
+constexpr int XGX_NPW = 6;   // 12 waves: 3 per SIMD, 170 registers per wave (8: 4 per SIMD, 128: spills)
+int lstm_fwd_xgx_launch(int B, int T, int H, const int32_t* lens, const float* whh_f,
+                        const float* whh_r, const uint16_t* x, int Din, const uint16_t* wih,
+                        const float* b_ih, const float* b_hh, float* act, float* y, float* cst,
+                        void* ws, uint16_t* ybf, hipStream_t s, bool dry) {
+  if (!xg_enabled()) return 0;
+  const char* e = getenv("ASR_FUSE_XPROJ");
+  if (e && e[0] == '0') return 0;
+  const int R = xg_rows(B, H);
+  if (R != 8) return 0;
+  if (Din <= 0 || Din % 8) return 0;
+  const int nkx = (Din + 31) / 32;
+  const int kpw = (nkx + XGX_NPW - 1) / XGX_NPW;
+  if (kpw > 6) return 0;
+  const int nks = H / 32;
+  const int ksw = (nks + 3) / 4;
+  if (ksw > 4) return 0;   // H > 512: the W_hh + W_ih fragments would spill
+  const int grid = 2 * ((B + R - 1) / R) * (H / XU);
+  const int threads = 64 * 4 + R * XU + 64 * XGX_NPW;
+  int* hdr = (int*)ws;
+  unsigned long long* g = (unsigned long long*)((char*)ws + XG_HDR);
+  const int al = xg_allow_local();
+#define ASR_XGX(KS, KP)                                                                         \
+  do {                                                                                          \
+    auto kfn = lstm_fwd_xgx<8, KS, 4, XGX_NPW, KP>;                                              \
+    hipFuncAttributes fa;                                                                       \
+    if (hipFuncGetAttributes(&fa, (const void*)kfn) != hipSuccess) return 0;                   \
+    const size_t pin = fa.sharedSizeBytes >= 84 * 1024 ? 0 : 84 * 1024 - fa.sharedSizeBytes;   \
+    if (!xg_fits(kfn, threads, pin)) return 0;                                                  \
+    if (dry) return 1;                                                                          \
+    if (hipMemsetAsync(ws, 0, lstm_xg_fwd_bytes(B, H), s) != hipSuccess) return -1;             \
+    xg_trace_setup(s);                                                                          \
+    hipLaunchKernelGGL(kfn, dim3(grid), dim3(threads), pin, s, B, T, H, lens, whh_f, whh_r, x,  \
+                       Din, wih, b_ih, b_hh, act, y, cst, g, hdr, ybf, al);                     \
+  } while (0)
+#define ASR_XGX_P(KS)                    \
+  do {                                   \
+    if (kpw <= 1) ASR_XGX(KS, 1);        \
+    else if (kpw <= 2) ASR_XGX(KS, 2);   \
+    else if (kpw <= 4) ASR_XGX(KS, 4);   \
+    else ASR_XGX(KS, 6);                 \
+  } while (0)
+  if (ksw <= 2) ASR_XGX_P(2);
+  else if (ksw <= 3) ASR_XGX_P(3);
+  else ASR_XGX_P(4);
+#undef ASR_XGX_P
+#undef ASR_XGX
+  return hipGetLastError() == hipSuccess ? 1 : -1;
+}
+
 // ASR_XG_TRACE=1: allocate the trace buffer once and publish its pointer.
 void xg_tuning_setup(hipStream_t s) {
   static bool done = false;
@@ -937,4 +1254,41 @@ extern "C" int asr_lstm_wgrad_gate(void* stream) {
   hipLaunchKernelGGL(asr::xg_wgrad_gate, dim3(1), dim3(64), 0, (hipStream_t)stream,
                      want ? want : 1u, 500000ull);
   return hipGetLastError() == hipSuccess ? ASR_OK : ASR_ERR_HIP;
+}
+
+// Forward layer pass with the input projection fused into the persistent
+// recurrence (bf16 mode): x [B*T][Din] bf16 (rows (b, t) of the layer input,
+// the dense staged GEMM operand), wih [8H][Din] bf16 ([W_ih fwd; W_ih rev]),
+// b_ih / b_hh [8H]; act [B][T][8H] receives the post-activation gates (as
+// gx_act of asr_lstm_forward after the call).  Returns ASR_ERR_UNSUPPORTED when
+// the shape does not take this path (the caller then runs the GEMM +
+// asr_lstm_forward).
+extern "C" int asr_lstm_forward_x(const uint16_t* x, int Din, const uint16_t* wih,
+                                  const float* b_ih, const float* b_hh, const float* whh_f,
+                                  const float* whh_r, const int32_t* lens, int B, int T, int H,
+                                  float* act, float* y, float* cst, uint16_t* ybf,
+                                  void* workspace, size_t ws_bytes, void* stream) {
+  ASR_REQUIRE(x && wih && b_ih && b_hh && whh_f && whh_r && lens && act && y && cst && workspace,
+              ASR_ERR_ARG, "lstm_forward_x: null pointer");
+  ASR_REQUIRE(B > 0 && T > 0 && H > 0 && Din > 0, ASR_ERR_ARG, "lstm_forward_x: bad shape");
+  hipStream_t s = (hipStream_t)stream;
+  if (asr::lstm_fwd_xgx_launch(B, T, H, lens, whh_f, whh_r, x, Din, wih, b_ih, b_hh, act, y, cst,
+                               workspace, ybf, s, true) != 1)
+    return ASR_ERR_UNSUPPORTED;
+  ASR_REQUIRE(ws_bytes >= asr::lstm_xg_fwd_bytes(B, H), ASR_ERR_WORKSPACE,
+              "lstm_forward_x: workspace too small");
+  const int slot = asr::prof_begin_launch(ASR_PROF_LSTM_FWD_SEQ, s);
+  const int rc = asr::lstm_fwd_xgx_launch(B, T, H, lens, whh_f, whh_r, x, Din, wih, b_ih, b_hh,
+                                          act, y, cst, workspace, ybf, s, false);
+  ASR_REQUIRE(rc == 1, ASR_ERR_HIP, "lstm_forward_x: launch failed");
+  asr::prof_end_launch(ASR_PROF_LSTM_FWD_SEQ, slot, s);
+  return ASR_OK;
+}
+
+// 1 when asr_lstm_forward_x takes this shape on this device, else 0.
+extern "C" int asr_lstm_forward_x_ok(int B, int H, int Din) {
+  if (B <= 0 || H <= 0 || Din <= 0) return 0;
+  return asr::lstm_fwd_xgx_launch(B, 1, H, nullptr, nullptr, nullptr, nullptr, Din, nullptr,
+                                  nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                  nullptr, true) == 1;
 }

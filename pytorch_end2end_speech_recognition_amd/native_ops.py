@@ -731,26 +731,42 @@ class BLSTMLayerFn(torch.autograd.Function):
         a_map = rowmap(Dsrc, stride_b=T_src * Dsrc, rows_per_b=T, t_mul=t_mul, t_add=t_add,
                        t_limit=T_src, perm=perm)
         gx = torch.empty(B, T, 8 * H, dtype=torch.float32, device=dev)
+        fuse_x = False
         if cd == BF16:
             x_op = convert_rows_bf16(x_src, a_map, B * T, Din,        # [B*T, Din]
                                      drop=drop if fused_drop else None)
             w_op = convert_rows_bf16(w_ih, rowmap(Din), 8 * H, Din)   # [8H, Din]
-            p = gemm_problem(operand(x_op, 0, rowmap(Din)), operand(w_op, 0, rowmap(Din)), gx,
-                             rowmap(8 * H), B * T, 8 * H, Din, bias=b_ih, bias2=b_hh)
             y_bf = torch.empty(B, T, 2 * H, dtype=torch.bfloat16, device=dev)
         else:
             x_op, w_op, y_bf = x_src, w_ih, None
-            p = gemm_problem(operand(x_src, 0, a_map), operand(w_ih, 0, rowmap(Din)), gx,
-                             rowmap(8 * H), B * T, 8 * H, Din, bias=b_ih, bias2=b_hh)
-        run_gemm([p], dev)
         y = torch.empty(B, T, 2 * H, dtype=torch.float32, device=dev)
         cst = torch.empty(B, T, 2 * H, dtype=torch.float32, device=dev)
         nb = N.query('asr_lstm_workspace_bytes', B, H, cd, 0)
         ws = _ws(nb, dev)
         whh_r = w_hh.data_ptr() + 4 * H * H * 4
-        N.call('asr_lstm_forward', N.ptr(gx), N.ptr(w_hh), ctypes.c_void_p(whh_r), F32, N.ptr(lens),
-               B, T, H, cd, N.ptr(y), N.ptr(cst), N.ptr(y_bf), N.ptr(ws), nb,
-               N.stream_handle(dev))
+        if cd == BF16 and _fuse_xproj_on():
+            # the input projection inside the persistent recurrence (no gx GEMM);
+            # ASR_ERR_UNSUPPORTED when this shape / configuration does not take it
+            rc = N.query('asr_lstm_forward_x', N.ptr(x_op), Din, N.ptr(w_op), N.ptr(b_ih),
+                         N.ptr(b_hh), N.ptr(w_hh), ctypes.c_void_p(whh_r), N.ptr(lens), B, T, H,
+                         N.ptr(gx), N.ptr(y), N.ptr(cst), N.ptr(y_bf), N.ptr(ws), nb,
+                         N.stream_handle(dev))
+            if rc not in (0, N.ASR_ERR_UNSUPPORTED):
+                raise N.NativeError('asr_lstm_forward_x failed (rc=%d): %s' % (
+                    rc, N.lib().asr_last_error().decode(errors='replace')))
+            fuse_x = rc == 0
+        if not fuse_x:
+            if cd == BF16:
+                run_gemm([gemm_problem(operand(x_op, 0, rowmap(Din)), operand(w_op, 0, rowmap(Din)),
+                                       gx, rowmap(8 * H), B * T, 8 * H, Din, bias=b_ih,
+                                       bias2=b_hh)], dev)
+            else:
+                run_gemm([gemm_problem(operand(x_src, 0, a_map), operand(w_ih, 0, rowmap(Din)), gx,
+                                       rowmap(8 * H), B * T, 8 * H, Din, bias=b_ih, bias2=b_hh)],
+                         dev)
+            N.call('asr_lstm_forward', N.ptr(gx), N.ptr(w_hh), ctypes.c_void_p(whh_r), F32,
+                   N.ptr(lens), B, T, H, cd, N.ptr(y), N.ptr(cst), N.ptr(y_bf), N.ptr(ws), nb,
+                   N.stream_handle(dev))
         ctx.save_for_backward(x_op, w_op, lens, w_hh, b_ih, b_hh, gx, cst,
                               y_bf if y_bf is not None else y)
         ctx.meta = (T, perm, t_mul, t_add, gbufs, cd, (B, T_src, Dsrc, Din), w_ih)
@@ -931,6 +947,13 @@ def bgru_layer(x_src, lens, T, w_ih, w_hh, b_ih, b_hh, perm=None, t_mul=1, t_add
     """The bidirectional GRU counterpart of blstm_layer (same addressing)."""
     return BGRULayerFn.apply(x_src, lens, T, perm, t_mul, t_add, gbufs, bool(concat),
                              w_ih, w_hh, b_ih, b_hh, *graph_params)
+
+
+def _fuse_xproj_on():
+    """bf16 mode: try the layer's input projection inside the persistent
+    forward recurrence (asr_lstm_forward_x) first (ASR_FUSE_XPROJ=0 keeps the
+    separate GEMM)."""
+    return os.environ.get('ASR_FUSE_XPROJ', '1') != '0'
 
 
 def convert_rows_bf16(src, rmap, nrows, ncols, drop=None):

@@ -460,3 +460,47 @@ def test_dropout_fused_into_next_layer_staging_bitwise(sub, cuda_dev):
             np.testing.assert_array_equal(a, b)
     finally:
         ops.set_compute_dtype('fp32')
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('B,T,H,Din', [(32, 300, 512, 1024), (32, 200, 512, 80),
+                                       (32, 160, 320, 640), (13, 90, 256, 120)])
+def test_fused_input_projection_matches_gemm_path(B, T, H, Din, cuda_dev, monkeypatch):
+    """The forward layer pass with the input projection inside the persistent
+    recurrence (asr_lstm_forward_x, bf16) against the GEMM + recurrence path
+    on the same inputs: outputs, cell states and saved gates agree to the
+    projection's f32 summation order (the bf16 operands are identical), and the
+    backward gradients that follow agree as well."""
+    from pytorch_end2end_speech_recognition_amd import _native as NL
+    from pytorch_end2end_speech_recognition_amd import native_ops as ops
+    if not NL.query('asr_lstm_forward_x_ok', B, H, Din):
+        pytest.skip('shape outside the fused path')
+    rng = np.random.RandomState(B + T + H)
+    lens = np.sort(rng.randint(T // 2, T + 1, B))[::-1].astype(np.int32)
+    lens[0] = T
+    x = torch.from_numpy(rng.randn(B, T, Din).astype(np.float32) * 0.5).to(cuda_dev)
+    w_ih = torch.from_numpy(rng.uniform(-0.1, 0.1, (8 * H, Din)).astype(np.float32)).to(cuda_dev)
+    w_hh = torch.from_numpy(rng.uniform(-0.05, 0.05, (8 * H, H)).astype(np.float32)).to(cuda_dev)
+    b_ih = torch.from_numpy(rng.uniform(-0.1, 0.1, 8 * H).astype(np.float32)).to(cuda_dev)
+    b_hh = torch.from_numpy(rng.uniform(-0.1, 0.1, 8 * H).astype(np.float32)).to(cuda_dev)
+    lens_d = torch.from_numpy(lens).to(cuda_dev)
+    dy = torch.from_numpy(rng.randn(B, T, 2 * H).astype(np.float32)).to(cuda_dev)
+    outs = {}
+    ops.set_compute_dtype('bf16')
+    try:
+        for fuse in ('0', '1'):
+            monkeypatch.setenv('ASR_FUSE_XPROJ', fuse)
+            ws = [t.clone().requires_grad_(True) for t in (w_ih, w_hh, b_ih, b_hh)]
+            xx = x.clone().requires_grad_(True)
+            y = ops.blstm_layer(xx, lens_d, T, *ws)
+            (y * dy).sum().backward()
+            torch.cuda.synchronize()
+            outs[fuse] = [y.detach().cpu().numpy(), xx.grad.cpu().numpy()] + \
+                [w.grad.cpu().numpy() for w in ws]
+    finally:
+        ops.set_compute_dtype('fp32')
+    names = ['y', 'dx', 'dW_ih', 'dW_hh', 'db_ih', 'db_hh']
+    for n, a, b in zip(names, outs['0'], outs['1']):
+        scale = np.abs(a).max() + 1e-12
+        err = np.abs(a - b).max() / scale
+        assert err < 2e-2, (n, err)
