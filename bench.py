@@ -106,7 +106,9 @@ def roofline_report(args, p, mean_us, launches, mean_work, workload):
       * lstm_{fwd,bwd}_pass (persistent, one launch = one layer pass, T steps x
         2 directions): HBM bytes that must move once -- gx / gate activations /
         y / c / dy read or written once per (b, t) cell plus W_hh once -- and
-        the recurrent h @ W_hh^T flops;
+        the recurrent h @ W_hh^T flops; with the input projection fused into
+        the forward pass (bf16, lstm_fwd_xgx) that pass also counts the
+        projection's flops and reads the bf16 input rows instead of gx;
       * lstm_{fwd,bwd}_step (per-step kernels): the same per time step, W_hh
         re-streamed every step;
       * gemm: 2*M*N*K summed over the launch's problems, reported by the library.
@@ -129,10 +131,21 @@ def roofline_report(args, p, mean_us, launches, mean_work, workload):
     flops_step = 2 * 2 * B * 4 * H * H        # h @ W_hh^T, 2 directions
     fwd_cell = 4 * 4 * 2 + 4 * 2              # gx read + act write (4 gates f32), y + c write
     bwd_cell = 4 * 4 * 2 + 4 * 3              # act read + dG write, dy + c_t + c_{t-1} read
+    fwd_pass_bytes = T * 2 * cell * fwd_cell + w_hh
+    fwd_pass_flops = T * flops_step
+    if args.precision == 'bf16' and os.environ.get('ASR_FUSE_XPROJ', '1') != '0':
+        # the input projection runs inside the forward pass (lstm_fwd_xgx): its
+        # flops join the pass, gx is never read, the bf16 input rows are
+        # (Din averaged over the layers: the input features, then 2H)
+        din = [input_dim(p)] + [2 * H] * (len(T_l) - 1)
+        din_avg = sum(d * tl for d, tl in zip(din, T_l)) / sum(T_l)
+        fwd_pass_flops += T * 2 * B * 8 * H * din_avg
+        fwd_pass_bytes = (T * 2 * cell * (fwd_cell - 4 * 4) + T * B * din_avg * 2 + w_hh +
+                          8 * H * din_avg * 2)
     kinds = [
         ('lstm_fwd_step', 'mfma', 2 * cell * fwd_cell + w_hh, flops_step),
         ('lstm_bwd_step', 'mfma', 2 * cell * bwd_cell + w_hh, flops_step),
-        ('lstm_fwd_pass', 'mfma', T * 2 * cell * fwd_cell + w_hh, T * flops_step),
+        ('lstm_fwd_pass', 'mfma', fwd_pass_bytes, fwd_pass_flops),
         ('lstm_bwd_pass', 'mfma', T * 2 * cell * bwd_cell + w_hh, T * flops_step),
         ('gemm', 'mfma', 0, mean_work[4]),
         ('ctc_fwd', 'hbm', mean_work[5], 0.0),
