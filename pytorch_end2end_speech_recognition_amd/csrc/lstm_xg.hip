@@ -451,7 +451,7 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
     const uint16_t* __restrict__ wih, const float* __restrict__ b_ih,
     const float* __restrict__ b_hh, float* __restrict__ act, float* __restrict__ y,
     float* __restrict__ cst, unsigned long long* xg, int* hdr, uint16_t* __restrict__ ybf,
-    int allow_local) {
+    int allow_local, int late_load, int defer_st) {
   __shared__ float part[2][NSW][R][4 * XU + 4];
   __shared__ float xpart[2][NPW][R][4 * XU + 4];
   __shared__ int s_dead;
@@ -592,13 +592,17 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
     produce(0);
     if (T > 1) load_a(1);
     __syncthreads();  // B_init
+    // late_load: the next input rows are requested after B(s), while the cell
+    // waves compute step s, instead of during the sweepers' poll for step s
+    // (the CU's vector-memory path is shared with the polls)
     for (int s = 0; s < T; ++s) {
       if (s + 1 < T) {
         produce(s + 1);
-        if (s + 2 < T) load_a(s + 2);
+        if (s + 2 < T && !late_load) load_a(s + 2);
       }
       __syncthreads();  // B(s)
       if (s_dead) return;
+      if (s + 2 < T && late_load) load_a(s + 2);
       __syncthreads();  // Bp(s)
     }
     return;
@@ -627,10 +631,29 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
     gxv[q] = v;
   }
   __builtin_amdgcn_s_setprio(2);  // the cell update + publish is the critical path
+  // defer_st: step s's y / c / gate / bf16-y stores are issued after B(s+1)
+  // (ahead of step s+1's cell math) instead of right after Bp(s), where they
+  // share the CU's vector-memory path with the sweepers' polls for step s+1
+  float pv[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  unsigned pval = 0u;
+  int pt = -1;
+  auto store_step = [&](int tt, const float* v, unsigned bv) {
+    const long long sidx = ((long long)b * T + tt) * 2 * H + (long long)dir * H + j;
+    y[sidx] = v[0];
+    cst[sidx] = v[1];
+    const long long gb = ((long long)b * T + tt) * H8 + gcol;
+    act[gb] = v[2];
+    act[gb + H] = v[3];
+    act[gb + 2 * H] = v[4];
+    act[gb + 3 * H] = v[5];
+    if (ybf && (unit & 1) == 0)
+      *reinterpret_cast<uint32_t*>(ybf + ((long long)b * T + tt) * 2 * H + dir * H + j) = bv;
+  };
   for (int s = 0; s < T; ++s) {
     const int t = dir ? T - 1 - s : s;
     __syncthreads();  // B(s)
     if (s_dead) return;
+    if (defer_st && own && pt >= 0) store_step(pt, pv, pval);
     float h = 0.f, cn = 0.f, ig = 0.f, fg = 0.f, gg = 0.f, og = 0.f;
     const bool active = own && t < len;
     if (active) {
@@ -666,18 +689,10 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
         __hip_atomic_store(p, gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();  // Bp(s)
-    if (own) {
-      const long long sidx = ((long long)b * T + t) * 2 * H + (long long)dir * H + j;
-      y[sidx] = h;
-      cst[sidx] = cn;
-      const long long gb = ((long long)b * T + t) * H8 + gcol;
-      act[gb] = ig;
-      act[gb + H] = fg;
-      act[gb + 2 * H] = gg;
-      act[gb + 3 * H] = og;
-      if (ybf && (unit & 1) == 0)
-        *reinterpret_cast<uint32_t*>(ybf + ((long long)b * T + t) * 2 * H + dir * H + j) = val;
-    }
+    pv[0] = h; pv[1] = cn; pv[2] = ig; pv[3] = fg; pv[4] = gg; pv[5] = og;
+    pval = val;
+    pt = t;
+    if (own && (!defer_st || s + 1 == T)) store_step(t, pv, pval);
     if (s + 1 < T) {  // the producers wrote pre(s+1) before B(s)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -1145,6 +1160,10 @@ int lstm_fwd_xgx_launch(int B, int T, int H, const int32_t* lens, const float* w
   int* hdr = (int*)ws;
   unsigned long long* g = (unsigned long long*)((char*)ws + XG_HDR);
   const int al = xg_allow_local();
+  const char* ll = getenv("ASR_XGX_LATE_LOAD");   // measured: -0.1..-0.35 ms/step (default)
+  const int late = ll ? atoi(ll) : 1;
+  const char* ds = getenv("ASR_XGX_DEFER_STORES");
+  const int defer = ds ? atoi(ds) : 0;
 #define ASR_XGX(KS, KP)                                                                         \
   do {                                                                                          \
     auto kfn = lstm_fwd_xgx<8, KS, 4, XGX_NPW, KP>;                                              \
@@ -1156,7 +1175,7 @@ int lstm_fwd_xgx_launch(int B, int T, int H, const int32_t* lens, const float* w
     if (hipMemsetAsync(ws, 0, lstm_xg_fwd_bytes(B, H), s) != hipSuccess) return -1;             \
     xg_trace_setup(s);                                                                          \
     hipLaunchKernelGGL(kfn, dim3(grid), dim3(threads), pin, s, B, T, H, lens, whh_f, whh_r, x,  \
-                       Din, wih, b_ih, b_hh, act, y, cst, g, hdr, ybf, al);                     \
+                       Din, wih, b_ih, b_hh, act, y, cst, g, hdr, ybf, al, late, defer);        \
   } while (0)
 #define ASR_XGX_P(KS)                    \
   do {                                   \
