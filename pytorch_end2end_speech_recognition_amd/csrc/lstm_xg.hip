@@ -444,6 +444,9 @@ __global__ void __launch_bounds__(64 * NSW + R * XU) lstm_fwd_xg(
 // and B(s); cells read pre(s+1) between Bp(s) and B(s+1)): the buffer a
 // producer overwrites at iteration s was last read before B(s-1).
 // ---------------------------------------------------------------------------
+constexpr int XGX_DMAX = 1024;   // largest input width of the fused projection
+typedef __attribute__((address_space(3))) void lds_void_t;
+
 template <int R, int KSW, int NSW, int NPW, int KPW>
 __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
     int B, int T, int H, const int32_t* __restrict__ lens, const float* __restrict__ whh_f,
@@ -452,8 +455,13 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
     const float* __restrict__ b_hh, float* __restrict__ act, float* __restrict__ y,
     float* __restrict__ cst, unsigned long long* xg, int* hdr, uint16_t* __restrict__ ybf,
     int allow_local, int late_load, int defer_st) {
+  (void)late_load;   // input rows now staged by LDS DMA three steps ahead
   __shared__ float part[2][NSW][R][4 * XU + 4];
   __shared__ float xpart[2][NPW][R][4 * XU + 4];
+  // input rows of steps s+1 .. s+3: [3 slots][R rows][XGX_DMAX] bf16, filled by
+  // buffer -> LDS DMA three steps ahead (16-B chunks XOR-swizzled by row when
+  // Din % 64 == 0, so a fragment read of 8 rows hits distinct banks)
+  __shared__ __attribute__((aligned(16))) uint16_t xs[3][R * XGX_DMAX];
   __shared__ int s_dead;
   __shared__ int s_pl[4];
   int* abortw = hdr;
@@ -491,6 +499,7 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
     const __amdgpu_buffer_rsrc_t rs = xg_rsrc(xg, xg_bytes);
     const int nsleep = __builtin_amdgcn_readfirstlane(g_xg_sleep);
     const int ndelay = __builtin_amdgcn_readfirstlane(g_xg_delay);
+    __syncthreads();  // B_pre: the first three steps' input rows are in LDS
     __syncthreads();  // B_init: the producers' pre(0) is in LDS
     for (int s = 0; s < T; ++s) {
       f32x4 acc[4];
@@ -558,27 +567,52 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
         wb[i][g] = k < Din ? load_bf16x8(wih + row * Din + k) : as_bf16x8(z8);
       }
     }
-    // A fragments: A[m][k] = x[b0 + m][t][k], rows m < R real
-    const bool arow = ln < R && b0 + ln < B;
-    const uint16_t* xb = x + (long long)(arow ? b0 + ln : 0) * T * Din;
-    bf16x8 a[KPW];
-    auto load_a = [&](int st) {
+    const bool swz = (Din & 63) == 0;
+    const __amdgpu_buffer_rsrc_t xr = xg_rsrc((void*)x, (unsigned)((long long)B * T * Din * 2));
+    const int slot_elems = R * Din;
+    constexpr int NI = (R * XGX_DMAX * 2 + NPW * 1024 - 1) / (NPW * 1024);  // DMAs per wave
+    // buffer -> LDS DMA of step st's R input rows into ring slot st % 3
+    auto stage_x = [&](int st) {
       const int t = dir ? T - 1 - st : st;
+      uint16_t* slot = &xs[st % 3][0];
 #pragma unroll
-      for (int i = 0; i < KPW; ++i) {
-        const int k = 32 * (pw + NPW * i) + 8 * kq;
-        a[i] = (arow && k < Din) ? load_bf16x8(xb + (long long)t * Din + k) : as_bf16x8(z8);
+      for (int i = 0; i < NI; ++i) {
+        const int blk = pw * NI + i;
+        const int e = blk * 512 + lane * 8;        // element of the slot this lane fills
+        unsigned voff = 0x7ffffff0u;               // out of range: zeros
+        if (e < slot_elems) {
+          const int r = e / Din, c = (e - r * Din) >> 3;
+          const int cs = swz ? (c ^ (r & 7)) : c;  // source chunk of LDS chunk c
+          if (b0 + r < B) voff = (unsigned)((((long long)(b0 + r) * T + t) * Din + 8 * cs) * 2);
+        }
+        if (blk * 512 < slot_elems) {              // wave-uniform
+          const unsigned lds_addr = (unsigned)(uintptr_t)(lds_void_t*)(slot + blk * 512);
+          unsigned keep;
+          asm volatile(
+              "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+              "buffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+              : "=&s"(keep)
+              : "v"(voff), "s"(xr), "s"(lds_addr)
+              : "memory");
+        }
       }
     };
     auto produce = [&](int st) {
+      const uint16_t* slot = &xs[st % 3][0];
       f32x4 acc[4];
 #pragma unroll
       for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int i = 0; i < KPW; ++i) {
         if (pw + NPW * i < nkx) {  // wave-uniform
+          const int k = 32 * (pw + NPW * i) + 8 * kq;
+          bf16x8 a = as_bf16x8(z8);
+          if (ln < R && k < Din) {
+            const int c = (k >> 3) ^ (swz ? (ln & 7) : 0);
+            a = *reinterpret_cast<const bf16x8*>(slot + ln * Din + 8 * c);
+          }
 #pragma unroll
-          for (int g = 0; g < 4; ++g) acc[g] = mfma_bf16(a[i], wb[i][g], acc[g]);
+          for (int g = 0; g < 4; ++g) acc[g] = mfma_bf16(a, wb[i][g], acc[g]);
         }
       }
       if (4 * kq < R) {
@@ -588,21 +622,20 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
           for (int r = 0; r < 4; ++r) xpart[st & 1][pw][4 * kq + r][g * XU + ln] = acc[g][r];
       }
     };
-    load_a(0);
+    for (int st = 0; st < 3 && st < T; ++st) stage_x(st);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // B_pre
     produce(0);
-    if (T > 1) load_a(1);
     __syncthreads();  // B_init
-    // late_load: the next input rows are requested after B(s), while the cell
-    // waves compute step s, instead of during the sweepers' poll for step s
-    // (the CU's vector-memory path is shared with the polls)
+    // Step s+1's gate inputs before B(s); after B(s) wait for this wave's DMA
+    // of step s+2 (issued one step ago) and issue step s+3's: the barrier Bp(s)
+    // then publishes every wave's rows of step s+2 for produce(s+2).
     for (int s = 0; s < T; ++s) {
-      if (s + 1 < T) {
-        produce(s + 1);
-        if (s + 2 < T && !late_load) load_a(s + 2);
-      }
+      if (s + 1 < T) produce(s + 1);
       __syncthreads();  // B(s)
       if (s_dead) return;
-      if (s + 2 < T && late_load) load_a(s + 2);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (s + 3 < T) stage_x(s + 3);
       __syncthreads();  // Bp(s)
     }
     return;
@@ -622,6 +655,7 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
 #pragma unroll
   for (int q = 0; q < 4; ++q) bsum[q] = b_ih[gcol + (long long)q * H] + b_hh[gcol + (long long)q * H];
   float gxv[4];
+  __syncthreads();  // B_pre
   __syncthreads();  // B_init
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -1148,7 +1182,8 @@ int lstm_fwd_xgx_launch(int B, int T, int H, const int32_t* lens, const float* w
   if (e && e[0] == '0') return 0;
   const int R = xg_rows(B, H);
   if (R != 8) return 0;
-  if (Din <= 0 || Din % 8) return 0;
+  if (Din <= 0 || Din % 8 || Din > XGX_DMAX) return 0;
+  if ((long long)B * T * Din * 2 >= 0x7fff0000LL) return 0;   // one buffer resource
   const int nkx = (Din + 31) / 32;
   const int kpw = (nkx + XGX_NPW - 1) / XGX_NPW;
   if (kpw > 6) return 0;
