@@ -220,6 +220,14 @@ int asr_lstm_backward_db(const float* dy, const void* whh_f, const void* whh_r, 
                          const int32_t* lens, int B, int T, int H, int compute_dtype,
                          float* act_dg, const float* cst, uint16_t* dgbf, float* db_ih,
                          float* db_hh, void* workspace, size_t ws_bytes, void* stream);
+/* asr_lstm_backward_db for a caller that feeds only the bf16 gate gradients
+ * (dgbf, required) to its weight / input gradient GEMMs: the tagged-granule
+ * recurrence skips the f32 dG stores and act_dg's contents are unspecified on
+ * exit.  Same workspace as asr_lstm_backward_db. */
+int asr_lstm_backward_dgbf(const float* dy, const void* whh_f, const void* whh_r, int w_dtype,
+                           const int32_t* lens, int B, int T, int H, int compute_dtype,
+                           float* act_dg, const float* cst, uint16_t* dgbf, float* db_ih,
+                           float* db_hh, void* workspace, size_t ws_bytes, void* stream);
 
 /* Forward layer pass with the input projection fused into the persistent
  * recurrence (bf16 mode; replaces asr_gemm(gx = x W_ih^T + b_ih + b_hh) +

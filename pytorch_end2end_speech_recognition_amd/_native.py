@@ -55,6 +55,8 @@ SIGNATURES = {
                                   c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
     'asr_lstm_backward_db': (c_int, [c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int,
                                      c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
+    'asr_lstm_backward_dgbf': (c_int, [c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int,
+                                       c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
     'asr_lstm_forward_x': (c_int, [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int,
                                    c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
     'asr_lstm_forward_x_ok': (c_int, [c_int, c_int, c_int]),

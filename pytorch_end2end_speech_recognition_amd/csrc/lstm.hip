@@ -45,7 +45,8 @@ int lstm_fwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* wh
                        uint16_t* ybf, hipStream_t s, bool dry);
 int lstm_bwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* whh_f,
                        const float* whh_r, const float* dy, float* act_dg, const float* cst,
-                       void* ws, uint16_t* dgbf, float* dbpart, hipStream_t s, bool dry);
+                       void* ws, uint16_t* dgbf, float* dbpart, hipStream_t s, bool dry,
+                       bool dg_f32);
 
 namespace {
 
@@ -624,7 +625,7 @@ static int lstm_backward_impl(const float* dy, const void* whh_f, const void* wh
                               int w_dtype, const int32_t* lens, int B, int T, int H,
                               int compute_dtype, float* act_dg, const float* cst,
                               uint16_t* dgbf, float* dbpart, void* workspace, size_t ws_bytes,
-                              void* stream, bool* fused_bias) {
+                              void* stream, bool* fused_bias, bool dg_f32 = true) {
   *fused_bias = false;
   ASR_REQUIRE(whh_f && whh_r && lens && act_dg && cst && workspace, ASR_ERR_ARG,
               "lstm_backward: null pointer");
@@ -635,10 +636,10 @@ static int lstm_backward_impl(const float* dy, const void* whh_f, const void* wh
   const bool bf = compute_dtype == ASR_DT_BF16;
   if (bf && w_dtype == ASR_DT_F32 &&
       lstm_bwd_xg_launch(B, T, H, lens, (const float*)whh_f, (const float*)whh_r, dy, act_dg, cst,
-                         workspace, dgbf, dbpart, s, true) == 1) {
+                         workspace, dgbf, dbpart, s, true, dg_f32) == 1) {
     const int slot = prof_begin_launch(ASR_PROF_LSTM_BWD_SEQ, s);
     const int rc = lstm_bwd_xg_launch(B, T, H, lens, (const float*)whh_f, (const float*)whh_r, dy,
-                                      act_dg, cst, workspace, dgbf, dbpart, s, false);
+                                      act_dg, cst, workspace, dgbf, dbpart, s, false, dg_f32);
     ASR_REQUIRE(rc == 1, ASR_ERR_HIP, "lstm_backward: tagged-granule launch failed");
     prof_end_launch(ASR_PROF_LSTM_BWD_SEQ, slot, s);
     *fused_bias = dbpart != nullptr;
@@ -730,11 +731,11 @@ extern "C" int asr_lstm_backward(const float* dy, const void* whh_f, const void*
 // db_hh[n] += the same (both biases feed the same gate pre-activation).  The
 // tagged-granule path sums them inside the recurrence (no pass over dG);
 // other paths reduce the written dG.
-extern "C" int asr_lstm_backward_db(const float* dy, const void* whh_f, const void* whh_r,
-                                    int w_dtype, const int32_t* lens, int B, int T, int H,
-                                    int compute_dtype, float* act_dg, const float* cst,
-                                    uint16_t* dgbf, float* db_ih, float* db_hh, void* workspace,
-                                    size_t ws_bytes, void* stream) {
+static int lstm_backward_db_impl(const float* dy, const void* whh_f, const void* whh_r,
+                                 int w_dtype, const int32_t* lens, int B, int T, int H,
+                                 int compute_dtype, float* act_dg, const float* cst,
+                                 uint16_t* dgbf, float* db_ih, float* db_hh, void* workspace,
+                                 size_t ws_bytes, void* stream, bool dg_f32) {
   ASR_REQUIRE(db_ih, ASR_ERR_ARG, "lstm_backward_db: null bias gradient");
   ASR_REQUIRE(B > 0 && T > 0 && H > 0, ASR_ERR_ARG, "lstm_backward_db: bad shape");
   ASR_REQUIRE(ws_bytes >= bwd_ws_bias(B, H, compute_dtype), ASR_ERR_WORKSPACE,
@@ -742,7 +743,8 @@ extern "C" int asr_lstm_backward_db(const float* dy, const void* whh_f, const vo
   float* part = (float*)((char*)workspace + bias_ws_off(B, H, compute_dtype));
   bool fused = false;
   const int rc = lstm_backward_impl(dy, whh_f, whh_r, w_dtype, lens, B, T, H, compute_dtype,
-                                    act_dg, cst, dgbf, part, workspace, ws_bytes, stream, &fused);
+                                    act_dg, cst, dgbf, part, workspace, ws_bytes, stream, &fused,
+                                    dg_f32);
   if (rc != ASR_OK) return rc;
   hipStream_t s = (hipStream_t)stream;
   const int N = 8 * H;
@@ -755,4 +757,29 @@ extern "C" int asr_lstm_backward_db(const float* dy, const void* whh_f, const vo
   const int M = B * T;
   return asr_colsum_accumulate(act_dg, N, M, N, 1.f, db_ih, db_hh, part,
                                asr_colsum_workspace_bytes(M, N), stream);
+}
+
+extern "C" int asr_lstm_backward_db(const float* dy, const void* whh_f, const void* whh_r,
+                                    int w_dtype, const int32_t* lens, int B, int T, int H,
+                                    int compute_dtype, float* act_dg, const float* cst,
+                                    uint16_t* dgbf, float* db_ih, float* db_hh, void* workspace,
+                                    size_t ws_bytes, void* stream) {
+  return lstm_backward_db_impl(dy, whh_f, whh_r, w_dtype, lens, B, T, H, compute_dtype, act_dg,
+                               cst, dgbf, db_ih, db_hh, workspace, ws_bytes, stream, true);
+}
+
+// asr_lstm_backward_db for callers that consume only the bf16 gate gradients
+// (dgbf, required): the tagged-granule recurrence then skips the f32 dG stores
+// (B*T*8H*4 bytes per pass) and act_dg's contents are unspecified on exit.
+// ASR_XG_DG_F32=1 keeps the f32 stores (A/B).
+extern "C" int asr_lstm_backward_dgbf(const float* dy, const void* whh_f, const void* whh_r,
+                                      int w_dtype, const int32_t* lens, int B, int T, int H,
+                                      int compute_dtype, float* act_dg, const float* cst,
+                                      uint16_t* dgbf, float* db_ih, float* db_hh, void* workspace,
+                                      size_t ws_bytes, void* stream) {
+  ASR_REQUIRE(dgbf, ASR_ERR_ARG, "lstm_backward_dgbf: null dgbf");
+  const char* e = getenv("ASR_XG_DG_F32");
+  const bool keep = e && e[0] == '1';
+  return lstm_backward_db_impl(dy, whh_f, whh_r, w_dtype, lens, B, T, H, compute_dtype, act_dg,
+                               cst, dgbf, db_ih, db_hh, workspace, ws_bytes, stream, keep);
 }

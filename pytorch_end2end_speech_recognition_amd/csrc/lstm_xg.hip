@@ -761,7 +761,8 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
     int B, int T, int H, const int32_t* __restrict__ lens, const float* __restrict__ whh_f,
     const float* __restrict__ whh_r, const float* __restrict__ dy, float* __restrict__ act_dg,
     const float* __restrict__ cst, unsigned long long* pg, int* hdr,
-    uint16_t* __restrict__ dgbf, float* __restrict__ dbpart, unsigned epoch, int allow_local) {
+    uint16_t* __restrict__ dgbf, float* __restrict__ dbpart, unsigned epoch, int allow_local,
+    int dg_f32) {
   constexpr int NPG = 256 / (2 * R);   // producer subsets swept in parallel
   __shared__ float red[NPG][R][XU + 1];
   __shared__ __attribute__((aligned(16))) uint16_t dgt[16][4 * XU + 8];
@@ -905,10 +906,12 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
       __syncthreads();  // B2
       if (own) {
         const long long gb = ((long long)b * T + t) * 8 * H + (long long)dir * H4 + j;
-        act_dg[gb] = d_i;
-        act_dg[gb + H] = d_f;
-        act_dg[gb + 2 * H] = d_g;
-        act_dg[gb + 3 * H] = d_o;
+        if (dg_f32) {  // f32 dG in place (not needed when only the bf16 copy feeds the GEMMs)
+          act_dg[gb] = d_i;
+          act_dg[gb + H] = d_f;
+          act_dg[gb + 2 * H] = d_g;
+          act_dg[gb + 3 * H] = d_o;
+        }
         if (dgbf) {
           uint16_t* o = dgbf + ((long long)b * T + t) * 8 * H + (long long)dir * H4 + j;
           o[0] = bi;
@@ -1131,7 +1134,8 @@ int lstm_fwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* wh
 
 int lstm_bwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* whh_f,
                        const float* whh_r, const float* dy, float* act_dg, const float* cst,
-                       void* ws, uint16_t* dgbf, float* dbpart, hipStream_t s, bool dry) {
+                       void* ws, uint16_t* dgbf, float* dbpart, hipStream_t s, bool dry,
+                       bool dg_f32) {
   if (!xg_enabled()) return 0;
   const int R = xg_rows(B, H);
   if (!R) return 0;
@@ -1150,7 +1154,8 @@ int lstm_bwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* wh
     if (hipMemsetAsync(ws, 0, lstm_xg_bwd_bytes(B, H), s) != hipSuccess) return -1;             \
     xg_trace_setup(s);             \
     hipLaunchKernelGGL((lstm_bwd_xg<RR, M>), dim3(grid), dim3(512 + RR * XU), pin, s, B, T, H,      \
-                       lens, whh_f, whh_r, dy, act_dg, cst, g, hdr, dgbf, dbpart, ep, al);                   \
+                       lens, whh_f, whh_r, dy, act_dg, cst, g, hdr, dgbf, dbpart, ep, al,        \
+                       (dg_f32 || !dgbf) ? 1 : 0);                                                  \
   } while (0)
 #define ASR_XGB_M(RR)                  \
   do {                                 \

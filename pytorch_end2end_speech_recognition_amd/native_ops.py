@@ -793,7 +793,9 @@ class BLSTMLayerFn(torch.autograd.Function):
         # the saved activations become the gate gradients dG in place; the bias
         # gradients (sum of dG over b, t) are accumulated by the same call
         if fused_db:
-            N.call('asr_lstm_backward_db', N.ptr(dy), N.ptr(w_hh), ctypes.c_void_p(whh_r), F32,
+            # bf16 mode: only the bf16 dG feeds the GEMMs, so the f32 dG is not stored
+            fn = 'asr_lstm_backward_dgbf' if dg_bf is not None else 'asr_lstm_backward_db'
+            N.call(fn, N.ptr(dy), N.ptr(w_hh), ctypes.c_void_p(whh_r), F32,
                    N.ptr(lens), B, T, H, cd, N.ptr(act), N.ptr(cst), N.ptr(dg_bf),
                    N.ptr(gbufs[2]), N.ptr(gbufs[3]), N.ptr(ws), nb, N.stream_handle(dev))
         else:   # A/B: separate column-sum pass over dG
