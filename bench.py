@@ -393,6 +393,10 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-parity', action='store_true')
     ap.add_argument('--prof-stride', type=int, default=8)
+    ap.add_argument('--sync-each-step', action='store_true',
+                    help='read every step\'s loss back before the next step starts (the '
+                         'reference loop\'s loss.item()); default: one step late '
+                         '(train_step(sync=False)), same updates')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -425,12 +429,16 @@ def main():
     batch, grad_scale = shard_batch(gbatch, rank, world)
     if cfg['model_type'] == 'hierarchical_ctc':
         def step(m, b):
-            m, lv, _, _ = train_hierarchical_step(m, b, p['clip_grad_norm'],
-                                                  grad_scale=grad_scale)
-            return m, lv
+            if args.sync_each_step:
+                m, lv, _, _ = train_hierarchical_step(m, b, p['clip_grad_norm'],
+                                                      grad_scale=grad_scale)
+                return m, lv
+            return train_hierarchical_step(m, b, p['clip_grad_norm'], grad_scale=grad_scale,
+                                           sync=False)
     else:
         def step(m, b):
-            return train_step(m, b, p['clip_grad_norm'], grad_scale=grad_scale)
+            return train_step(m, b, p['clip_grad_norm'], grad_scale=grad_scale,
+                              sync=args.sync_each_step)
     frames_per_step = float(batch['x_lens'].sum())
     # inputs resident in HBM when the timed region starts (the task's metric
     # definition): the features go to the device once; the models take a
@@ -442,7 +450,8 @@ def main():
     batch['xs'] = torch.from_numpy(np.ascontiguousarray(host_batch['xs'])).to(dev)
 
     for _ in range(args.warmup):
-        model, _ = step(model, batch)
+        model, lv = step(model, batch)
+    float(lv) if args.warmup else None
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -451,9 +460,12 @@ def main():
     t0 = time.perf_counter()
     losses, marks = [], [t0]
     for _ in range(args.steps):
-        model, lv = step(model, batch)     # reads the loss back: the step has drained
+        # sync_each_step: reads the loss back, the step has drained; otherwise the
+        # previous step's loss is read back when this step reaches its optimizer
+        model, lv = step(model, batch)
         losses.append(lv)
         marks.append(time.perf_counter())
+    losses = [float(lv) for lv in losses]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -503,7 +515,10 @@ def main():
                    'global_batch': GB, 'max_frames': args.frames,
                    'feat_dim': input_dim(p), 'vocab': p['num_classes'] + 1,
                    'parallelism': 'dp%d' % world, 'frames_per_step': total_frames_per_step},
-        'timing': {'statistic': 'median step (max over ranks)', 'ms_per_step_mean':
+        'timing': {'statistic': 'median step (max over ranks)',
+                   'loss_readback': ('every step (loss.item())' if args.sync_each_step else
+                                     'one step late (train_step(sync=False))'),
+                   'ms_per_step_mean':
                    round(1000.0 * elapsed / args.steps, 3),
                    'value_mean': round(total_frames_per_step * args.steps / elapsed, 1),
                    'ms_per_step_min': round(1000.0 * float(np.min(step_s)), 3),

@@ -12,7 +12,9 @@ import os
 import torch  # noqa: F401  (must precede the dlopen: shared HIP runtime)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libasr_hip.so')
+# ASR_LIB_PATH: another build of the same library (interleaved A/B runs of two
+# kernel versions on one GPU box, tools/gpu_ab.sh); the in-tree build otherwise
+LIB_PATH = os.environ.get('ASR_LIB_PATH') or os.path.join(_HERE, 'libasr_hip.so')
 
 c_int = ctypes.c_int
 c_ll = ctypes.c_longlong

@@ -762,7 +762,7 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
     const float* __restrict__ whh_r, const float* __restrict__ dy, float* __restrict__ act_dg,
     const float* __restrict__ cst, unsigned long long* pg, int* hdr,
     uint16_t* __restrict__ dgbf, float* __restrict__ dbpart, unsigned epoch, int allow_local,
-    int dg_f32) {
+    int dg_f32, int io_pos) {
   constexpr int NPG = 256 / (2 * R);   // producer subsets swept in parallel
   __shared__ float red[NPG][R][XU + 1];
   __shared__ __attribute__((aligned(16))) uint16_t dgt[16][4 * XU + 8];
@@ -857,25 +857,56 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
     const bool own = b < B;
     const int len = own ? lens[b] : 0;
     float dc = 0.f;
-    auto load_cell = [&](int q, float (&av)[4], float& cc, float& cp, float& dyv) {
+    // c_t of step q is c_{tp} of step q - 1: with `carry` it is taken from there
+    auto load_cell = [&](int q, float (&av)[4], float& cc, float& cp, float& dyv, const float* carry) {
       const int t = dir == 0 ? T - 1 - q : q;
       const int tp = dir == 0 ? t - 1 : t + 1;
       const long long gb = ((long long)b * T + t) * 8 * H + (long long)dir * H4 + j;
       const long long si = ((long long)b * T + t) * 2 * H + (long long)dir * H + j;
 #pragma unroll
       for (int k = 0; k < 4; ++k) av[k] = act_dg[gb + (long long)k * H];
-      cc = cst[si];
+      cc = carry ? *carry : cst[si];
       cp = (tp >= 0 && tp < T) ? cst[si + (long long)(tp - t) * 2 * H] : 0.f;
       dyv = dy ? dy[si] : 0.f;
     };
+    // inputs of step q (av, cc, cp, dyv) and q + 1 (n*): loaded two steps ahead
     float av[4] = {0.f, 0.f, 0.f, 0.f}, cc = 0.f, cp = 0.f, dyv = 0.f;
+    float nav[4] = {0.f, 0.f, 0.f, 0.f}, ncc = 0.f, ncp = 0.f, ndyv = 0.f;
     // bias gradient: sum over t of this (utterance, unit)'s four gate gradients
     float sb_i = 0.f, sb_f = 0.f, sb_g = 0.f, sb_o = 0.f;
-    if (own) load_cell(0, av, cc, cp, dyv);
+    if (own) load_cell(0, av, cc, cp, dyv, nullptr);
+    if (own && T > 1) load_cell(1, nav, ncc, ncp, ndyv, nullptr);
+    // io_pos: where the cell waves issue a step's dG stores and the loads of
+    // step q + 2 in the CU's vector-memory queue.  0: both after B2 (beside the
+    // partial-dh stores); 1: both after B3 (beside the next poll: measured +2.4
+    // ms / step at 5x512); 2: loads after B2, the stores after B1 of the next
+    // step, while the cell and MFMA phases run.
+    float pd[4] = {0.f, 0.f, 0.f, 0.f};
+    uint16_t pb[4] = {0, 0, 0, 0};
+    int pq = -1;
+    auto step_st = [&]() {   // stores of step pq
+      if (pq >= 0) {
+        const int t = dir == 0 ? T - 1 - pq : pq;
+        const long long gb = ((long long)b * T + t) * 8 * H + (long long)dir * H4 + j;
+        if (dg_f32) {  // f32 dG in place (not needed when only the bf16 copy feeds the GEMMs)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) act_dg[gb + (long long)k * H] = pd[k];
+        }
+        if (dgbf) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) dgbf[gb + (long long)k * H] = pb[k];
+        }
+      }
+    };
+    auto step_io = [&](int q, bool st) {   // (stores of step pq,) loads of step q + 2
+      if (st) step_st();
+      if (q + 2 < T) load_cell(q + 2, nav, ncc, ncp, ndyv, &cp);   // cp: step q + 1's
+    };
     for (int q = 0; q < T; ++q) {
-      const int t = dir == 0 ? T - 1 - q : q;
       __syncthreads();  // B1
       if (s_dead) return;
+      if (own && io_pos == 2) step_st();
+      const int t = dir == 0 ? T - 1 - q : q;
       float d_i = 0.f, d_f = 0.f, d_g = 0.f, d_o = 0.f;
       if (own && t < len) {
         float dh = dyv;
@@ -903,26 +934,21 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
       dgt[row][XU + unit] = bff;
       dgt[row][2 * XU + unit] = bg;
       dgt[row][3 * XU + unit] = bo;
+      pd[0] = d_i; pd[1] = d_f; pd[2] = d_g; pd[3] = d_o;
+      pb[0] = bi; pb[1] = bff; pb[2] = bg; pb[3] = bo;
+      pq = q;
+      // step q + 1's inputs (loaded two steps ahead)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) av[k] = nav[k];
+      cc = ncc;
+      cp = ncp;
+      dyv = ndyv;
       __syncthreads();  // B2
-      if (own) {
-        const long long gb = ((long long)b * T + t) * 8 * H + (long long)dir * H4 + j;
-        if (dg_f32) {  // f32 dG in place (not needed when only the bf16 copy feeds the GEMMs)
-          act_dg[gb] = d_i;
-          act_dg[gb + H] = d_f;
-          act_dg[gb + 2 * H] = d_g;
-          act_dg[gb + 3 * H] = d_o;
-        }
-        if (dgbf) {
-          uint16_t* o = dgbf + ((long long)b * T + t) * 8 * H + (long long)dir * H4 + j;
-          o[0] = bi;
-          o[H] = bff;
-          o[2 * H] = bg;
-          o[3 * H] = bo;
-        }
-        if (q + 1 < T) load_cell(q + 1, av, cc, cp, dyv);
-      }
+      if (own && io_pos != 1) step_io(q, io_pos == 0);
       __syncthreads();  // B3
+      if (own && io_pos == 1) step_io(q, true);
     }
+    if (own && io_pos == 2) step_st();   // the last step's stores
     if (own && dbpart) {  // per-utterance bias-gradient partials [B][8H]
       float* o = dbpart + (long long)b * 8 * H + (long long)dir * H4 + j;
       o[0] = sb_i;
@@ -964,6 +990,9 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
     const bf16x8 bf1 = *reinterpret_cast<const bf16x8*>(&dgt[ln][32 + 8 * kq]);
     const unsigned tb = tag_bit(q);
     const long long obase = (((long long)(q & 1) * G + grp) * WPG + mem) * R;
+    // block by block: MFMA pair, convert, store.  All MFMAs first and then the
+    // stores (every granule leaves in one burst) measured 0.7 ms / step slower
+    // at 5x512 (interleaved A/B), although the MFMA wave's phase got shorter.
 #pragma unroll
     for (int i = 0; i < MB; ++i) {
       const int mb = mw + 4 * i;
@@ -1147,6 +1176,8 @@ int lstm_bwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* wh
   const unsigned ep = xg_bwd_seq(true);
   const int al = xg_allow_local();
   const size_t pin = xg_pin_bwd();
+  const char* li = getenv("ASR_XG_BWD_IO");   // cell I/O position (lstm_bwd_xg), A/B
+  const int io_pos = li ? atoi(li) : 0;
 #define ASR_XGB(RR, M)                                                                          \
   do {                                                                                          \
     if (!xg_fits(lstm_bwd_xg<RR, M>, 512 + RR * XU, pin)) return 0;                               \
@@ -1155,7 +1186,7 @@ int lstm_bwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* wh
     xg_trace_setup(s);             \
     hipLaunchKernelGGL((lstm_bwd_xg<RR, M>), dim3(grid), dim3(512 + RR * XU), pin, s, B, T, H,      \
                        lens, whh_f, whh_r, dy, act_dg, cst, g, hdr, dgbf, dbpart, ep, al,        \
-                       (dg_f32 || !dgbf) ? 1 : 0);                                                  \
+                       (dg_f32 || !dgbf) ? 1 : 0, io_pos);                                          \
   } while (0)
 #define ASR_XGB_M(RR)                  \
   do {                                 \

@@ -80,7 +80,54 @@ def _status_guard(model):
     return native_ops.recurrence_status(model.device)
 
 
-def _step(model, forward, clip_grad_norm, n_losses, grad_scale):
+class PendingLosses(object):
+    """The losses of a train_step(..., sync=False), read back one step late.
+
+    The step's loss values and skip guard are copied (stream-ordered) into a
+    pinned host buffer; nothing waits for them until value() is called -- or
+    until the NEXT step reaches its optimizer, which resolves the previous
+    step first (so a skipped batch undoes its Adam step count before the next
+    update, exactly as the synchronous path does).  The host therefore runs
+    one step ahead of the GPU instead of idling it at every step boundary
+    (the reference's loss.item() per step, training_loop.py:78)."""
+
+    def __init__(self, model, host, event, n_losses, n_guard, has_losses):
+        self._model, self._host, self._event = model, host, event
+        self._n, self._ng, self._has = n_losses, n_guard, has_losses
+        self._vals = None
+
+    def value(self):
+        if self._vals is None:
+            self._event.synchronize()
+            host = self._host.tolist()
+            # no zero_grad on a skip here: the flat gradient already belongs to
+            # the next step (which zeroes it itself before its backward)
+            self._vals = _finish(self._model, host, self._n, self._ng, self._has, zero=False)
+            if getattr(self._model, '_pending_losses', None) is self:
+                self._model._pending_losses = None
+        return self._vals
+
+    def __float__(self):
+        return float(self.value()[0])
+
+
+def _finish(model, host, n_losses, n_guard, has_losses, zero=True):
+    """Loss values from the step's host read-back (skip / inf semantics of
+    training_loop.py:69-83)."""
+    vals = host[:n_losses] if has_losses else [0.] * n_losses
+    if n_guard and max(host[-n_guard:]) > 0:
+        # the fused step left the weights untouched; undo its step count
+        if hasattr(model.optimizer, 'undo_step_count'):
+            model.optimizer.undo_step_count()
+        return _skipped(model, n_losses, 'a rank failed or a persistent recurrence gave up '
+                        '(status %s)' % host[-n_guard:], zero=zero)
+    if vals[0] == INF or vals[0] == -INF:
+        logger.warning('WARNING: received an inf loss, setting loss value to 0.')
+        vals = [0.] * n_losses
+    return vals
+
+
+def _step(model, forward, clip_grad_norm, n_losses, grad_scale, sync=True):
     """zero_grad -> forward (returns n_losses loss tensors, the first is the
     total) -> backward -> collective skip flag -> gradient all-reduce ->
     fused clip + optimizer step.  Returns the losses as floats (0 on skip).
@@ -123,6 +170,9 @@ def _step(model, forward, clip_grad_norm, n_losses, grad_scale):
     if not ok and (guard is None or world == 1):
         model.zero_grad()
         return [0.] * n_losses
+    prev = getattr(model, '_pending_losses', None)
+    if prev is not None:     # the previous step's read-back (its skip undoes its step count)
+        prev.value()
     if hasattr(model.optimizer, 'clip_and_step'):
         model.optimizer.clip_and_step(clip_grad_norm if clip_grad_norm > 0 else 0.0, guard=guard)
     else:
@@ -135,42 +185,67 @@ def _step(model, forward, clip_grad_norm, n_losses, grad_scale):
     parts = [l.detach().reshape(-1)[:1].float() for l in losses] if losses is not None else []
     if guard is not None:
         parts.append(guard.float())
+    n_guard = guard.numel() if guard is not None else 0
+    if not sync and parts and model.device.type == 'cuda':
+        dev_vals = torch.cat(parts)
+        host = torch.empty(dev_vals.numel(), dtype=torch.float32, pin_memory=True)
+        host.copy_(dev_vals, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        pend = PendingLosses(model, host, ev, n_losses, n_guard, losses is not None)
+        model._pending_losses = pend
+        return pend
     host = torch.cat(parts).tolist() if parts else []
-    vals = host[:n_losses] if losses is not None else [0.] * n_losses
-    if guard is not None and max(host[-guard.numel():]) > 0:
-        # the fused step left the weights untouched; undo its step count
-        if hasattr(model.optimizer, 'undo_step_count'):
-            model.optimizer.undo_step_count()
-        return _skipped(model, n_losses, 'a rank failed or a persistent recurrence gave up '
-                        '(status %s)' % guard.tolist())
-    if vals[0] == INF or vals[0] == -INF:
-        logger.warning('WARNING: received an inf loss, setting loss value to 0.')
-        vals = [0.] * n_losses
-    return vals
+    vals = _finish(model, host, n_losses, n_guard, losses is not None)
+    return vals if sync else _Resolved(vals)
 
 
-def _skipped(model, n_losses, why):
+class _Resolved(object):
+    """PendingLosses' interface for a step that was read back synchronously."""
+
+    def __init__(self, vals):
+        self._vals = vals
+
+    def value(self):
+        return self._vals
+
+    def __float__(self):
+        return float(self._vals[0])
+
+
+def _skipped(model, n_losses, why, zero=True):
     logger.warning('!!!Skip mini-batch!!! %s' % why)
-    model.zero_grad()
+    if zero:
+        model.zero_grad()
     return [0.] * n_losses
 
 
-def train_step(model, batch, clip_grad_norm, backend='pytorch', grad_scale=None):
+def train_step(model, batch, clip_grad_norm, backend='pytorch', grad_scale=None, sync=True):
     """Returns (model, loss_value) like training_loop.py:27-83.
 
     grad_scale: data parallel only -- the factor applied to this rank's
     gradient before the sum over ranks: pass shard_batch's local_B / global_B
     (every rank's loss is a mean over its local batch), so the update equals
-    the 1-GPU update of the global batch."""
+    the 1-GPU update of the global batch.
+    sync=False: loss_value is a PendingLosses (float() / value() read it);
+    the step does not wait for the GPU, so consecutive steps queue back to
+    back (the update sequence is identical)."""
     vals = _step(model, lambda: [model(batch['xs'], batch['ys'], batch['x_lens'],
-                                       batch['y_lens'])], clip_grad_norm, 1, grad_scale)
-    return model, vals[0]
+                                       batch['y_lens'])], clip_grad_norm, 1, grad_scale, sync)
+    if sync:
+        return model, vals[0]
+    return model, (_Resolved(vals) if isinstance(vals, list) else vals)
 
 
-def train_hierarchical_step(model, batch, clip_grad_norm, backend='pytorch', grad_scale=None):
+def train_hierarchical_step(model, batch, clip_grad_norm, backend='pytorch', grad_scale=None,
+                            sync=True):
     """Returns (model, loss, loss_main, loss_sub) like training_loop.py:86-153
-    (batch carries ys_sub / y_lens_sub for the sub task)."""
+    (batch carries ys_sub / y_lens_sub for the sub task).  sync=False:
+    returns (model, PendingLosses) (see train_step)."""
     vals = _step(model, lambda: list(model(batch['xs'], batch['ys'], batch['x_lens'],
                                            batch['y_lens'], batch['ys_sub'],
-                                           batch['y_lens_sub'])), clip_grad_norm, 3, grad_scale)
-    return (model,) + tuple(vals)
+                                           batch['y_lens_sub'])), clip_grad_norm, 3, grad_scale,
+                 sync)
+    if sync:
+        return (model,) + tuple(vals)
+    return model, (_Resolved(vals) if isinstance(vals, list) else vals)

@@ -218,6 +218,44 @@ def test_recurrence_give_up_skips_the_batch(cuda_dev):
 
 
 @pytest.mark.gpu
+def test_deferred_loss_readback_matches_synchronous_steps(cuda_dev):
+    """train_step(sync=False) (the loss read back one step late, so steps queue
+    back to back) applies the same updates as the synchronous loop: bitwise
+    equal weights and losses over four steps, one of them skipped by a
+    recurrence give-up -- its step count is undone before the next update and
+    its gradients are not zeroed under the next step."""
+    from pytorch_end2end_speech_recognition_amd import _native as N
+    from pytorch_end2end_speech_recognition_amd import native_ops
+    from pytorch_end2end_speech_recognition_amd.utils.training.training_loop import train_step
+    native_ops.set_compute_dtype('bf16')
+    try:
+        d = golden('model_ctc_sub')
+        kw = json.loads(str(d['kwargs']))
+        sd, _ = golden_params(d)
+        batch = dict(xs=d['xs'], ys=d['ys'], x_lens=d['x_lens'], y_lens=d['y_lens'])
+        runs = []
+        for sync in (True, False):
+            model = _to_gpu_model(kw, sd, cuda_dev)
+            model.set_optimizer('adam', 1e-3, weight_decay=1e-6)
+            native_ops.recurrence_status(cuda_dev)             # clear
+            vals = []
+            for k in range(4):
+                if k == 1:
+                    N.call('asr_lstm_status_inject', 1, N.stream_handle(cuda_dev))
+                model, lv = train_step(model, batch, clip_grad_norm=5.0, sync=sync)
+                vals.append(lv)
+            vals = [float(v) for v in vals]
+            torch.cuda.synchronize()
+            runs.append((vals, model._flat_param.clone(), model.optimizer._step))
+        (v0, p0, s0), (v1, p1, s1) = runs
+        assert v0 == v1 and v0[1] == 0.0 and v0[0] > 0, (v0, v1)
+        assert s0 == s1 == 3
+        assert torch.equal(p0, p1)
+    finally:
+        native_ops.set_compute_dtype('fp32')
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize('mode', ['1', '2'])
 def test_wgrad_side_stream_matches_main_stream(mode, cuda_dev, monkeypatch):
     """Weight gradients computed on the side stream (ASR_OVERLAP_WGRAD=1: CU-masked
