@@ -762,7 +762,7 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
     const float* __restrict__ whh_r, const float* __restrict__ dy, float* __restrict__ act_dg,
     const float* __restrict__ cst, unsigned long long* pg, int* hdr,
     uint16_t* __restrict__ dgbf, float* __restrict__ dbpart, unsigned epoch, int allow_local,
-    int dg_f32, int io_pos) {
+    int dg_f32, int io_pos, int dg_st16) {
   constexpr int NPG = 256 / (2 * R);   // producer subsets swept in parallel
   __shared__ float red[NPG][R][XU + 1];
   __shared__ __attribute__((aligned(16))) uint16_t dgt[16][4 * XU + 8];
@@ -877,35 +877,42 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
     if (own) load_cell(0, av, cc, cp, dyv, nullptr);
     if (own && T > 1) load_cell(1, nav, ncc, ncp, ndyv, nullptr);
     // io_pos: where the cell waves issue a step's dG stores and the loads of
-    // step q + 2 in the CU's vector-memory queue.  0: both after B2 (beside the
-    // partial-dh stores); 1: both after B3 (beside the next poll: measured +2.4
-    // ms / step at 5x512); 2: loads after B2, the stores after B1 of the next
-    // step, while the cell and MFMA phases run.
-    float pd[4] = {0.f, 0.f, 0.f, 0.f};
-    uint16_t pb[4] = {0, 0, 0, 0};
-    int pq = -1;
-    auto step_st = [&]() {   // stores of step pq
-      if (pq >= 0) {
-        const int t = dir == 0 ? T - 1 - pq : pq;
+    // step q + 2 in the CU's vector-memory queue.  0: after B2 (beside the
+    // partial-dh stores); 1: after B3 (beside the next poll: measured +2.4 ms /
+    // step at 5x512; stores after B1 of the next step: +0.25 ms).
+    // bf16 dG leaves from the dgt tile (stable from B2 until the next step's B1)
+    // as ONE 16-B store per lane of the first R / 8 cell waves -- R rows x 4
+    // gates x 2 halves of 8 units -- instead of four 2-B stores per (row, unit)
+    // lane on every cell wave (dg_st16; ASR_XG_DG_ST16=0: the per-lane stores).
+    const int srow = ct >> 3, sg = (ct >> 1) & 3, sh = ct & 1;
+    const bool st16 = dg_st16 && dgbf && ct < 8 * R && b0 + srow < B;
+    auto step_io = [&](int q, int t, float d_i, float d_f, float d_g, float d_o, uint16_t bi,
+                       uint16_t bff, uint16_t bg, uint16_t bo) {
+      if (own) {
         const long long gb = ((long long)b * T + t) * 8 * H + (long long)dir * H4 + j;
         if (dg_f32) {  // f32 dG in place (not needed when only the bf16 copy feeds the GEMMs)
-#pragma unroll
-          for (int k = 0; k < 4; ++k) act_dg[gb + (long long)k * H] = pd[k];
+          act_dg[gb] = d_i;
+          act_dg[gb + H] = d_f;
+          act_dg[gb + 2 * H] = d_g;
+          act_dg[gb + 3 * H] = d_o;
         }
-        if (dgbf) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) dgbf[gb + (long long)k * H] = pb[k];
+        if (dgbf && !dg_st16) {
+          dgbf[gb] = bi;
+          dgbf[gb + H] = bff;
+          dgbf[gb + 2 * H] = bg;
+          dgbf[gb + 3 * H] = bo;
         }
       }
-    };
-    auto step_io = [&](int q, bool st) {   // (stores of step pq,) loads of step q + 2
-      if (st) step_st();
-      if (q + 2 < T) load_cell(q + 2, nav, ncc, ncp, ndyv, &cp);   // cp: step q + 1's
+      if (st16) {
+        const uint4 v = *reinterpret_cast<const uint4*>(&dgt[srow][sg * XU + 8 * sh]);
+        *reinterpret_cast<uint4*>(dgbf + ((long long)(b0 + srow) * T + t) * 8 * H +
+                                  (long long)dir * H4 + (long long)sg * H + u0 + 8 * sh) = v;
+      }
+      if (own && q + 2 < T) load_cell(q + 2, nav, ncc, ncp, ndyv, &cp);   // cp: step q + 1's
     };
     for (int q = 0; q < T; ++q) {
       __syncthreads();  // B1
       if (s_dead) return;
-      if (own && io_pos == 2) step_st();
       const int t = dir == 0 ? T - 1 - q : q;
       float d_i = 0.f, d_f = 0.f, d_g = 0.f, d_o = 0.f;
       if (own && t < len) {
@@ -934,9 +941,6 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
       dgt[row][XU + unit] = bff;
       dgt[row][2 * XU + unit] = bg;
       dgt[row][3 * XU + unit] = bo;
-      pd[0] = d_i; pd[1] = d_f; pd[2] = d_g; pd[3] = d_o;
-      pb[0] = bi; pb[1] = bff; pb[2] = bg; pb[3] = bo;
-      pq = q;
       // step q + 1's inputs (loaded two steps ahead)
 #pragma unroll
       for (int k = 0; k < 4; ++k) av[k] = nav[k];
@@ -944,11 +948,10 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
       cp = ncp;
       dyv = ndyv;
       __syncthreads();  // B2
-      if (own && io_pos != 1) step_io(q, io_pos == 0);
+      if (io_pos == 0) step_io(q, t, d_i, d_f, d_g, d_o, bi, bff, bg, bo);
       __syncthreads();  // B3
-      if (own && io_pos == 1) step_io(q, true);
+      if (io_pos == 1) step_io(q, t, d_i, d_f, d_g, d_o, bi, bff, bg, bo);
     }
-    if (own && io_pos == 2) step_st();   // the last step's stores
     if (own && dbpart) {  // per-utterance bias-gradient partials [B][8H]
       float* o = dbpart + (long long)b * 8 * H + (long long)dir * H4 + j;
       o[0] = sb_i;
@@ -1177,7 +1180,9 @@ int lstm_bwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* wh
   const int al = xg_allow_local();
   const size_t pin = xg_pin_bwd();
   const char* li = getenv("ASR_XG_BWD_IO");   // cell I/O position (lstm_bwd_xg), A/B
-  const int io_pos = li ? atoi(li) : 0;
+  const int io_pos = (li && atoi(li) == 1) ? 1 : 0;
+  const char* s16 = getenv("ASR_XG_DG_ST16");   // A/B: bf16 dG by 16-B stores from LDS
+  const int st16 = (s16 && s16[0] == '0') ? 0 : 1;
 #define ASR_XGB(RR, M)                                                                          \
   do {                                                                                          \
     if (!xg_fits(lstm_bwd_xg<RR, M>, 512 + RR * XU, pin)) return 0;                               \
@@ -1186,7 +1191,7 @@ int lstm_bwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* wh
     xg_trace_setup(s);             \
     hipLaunchKernelGGL((lstm_bwd_xg<RR, M>), dim3(grid), dim3(512 + RR * XU), pin, s, B, T, H,      \
                        lens, whh_f, whh_r, dy, act_dg, cst, g, hdr, dgbf, dbpart, ep, al,        \
-                       (dg_f32 || !dgbf) ? 1 : 0, io_pos);                                          \
+                       (dg_f32 || !dgbf) ? 1 : 0, io_pos, st16);                                         \
   } while (0)
 #define ASR_XGB_M(RR)                  \
   do {                                 \
