@@ -732,10 +732,22 @@ class BLSTMLayerFn(torch.autograd.Function):
                        t_limit=T_src, perm=perm)
         gx = torch.empty(B, T, 8 * H, dtype=torch.float32, device=dev)
         fuse_x = False
+        Dp = Din        # pitch of the bf16 operands x_op / w_op
         if cd == BF16:
-            x_op = convert_rows_bf16(x_src, a_map, B * T, Din,        # [B*T, Din]
-                                     drop=drop if fused_drop else None)
-            w_op = convert_rows_bf16(w_ih, rowmap(Din), 8 * H, Din)   # [8H, Din]
+            if Din % 8 and not fused_drop:
+                # an input width that is not a multiple of 8 (TIMIT's 123) is
+                # staged with zero-padded rows of Dp columns, so the fused
+                # projection and the fast GEMMs take it (the zero columns add
+                # nothing): no generic-kernel GEMMs on layer 0
+                Dp = (Din + 7) // 8 * 8
+                x_op = torch.empty(B * T, Dp, dtype=torch.bfloat16, device=dev)
+                N.call('asr_convert_rows_bf16_ld', N.ptr(x_src), a_map, B * T, Din, Dp,
+                       N.ptr(x_op), N.stream_handle(dev))
+                w_op = _staged(w_ih, 8 * H, Din, Dp)                  # [8H, Dp]
+            else:
+                x_op = convert_rows_bf16(x_src, a_map, B * T, Din,    # [B*T, Din]
+                                         drop=drop if fused_drop else None)
+                w_op = convert_rows_bf16(w_ih, rowmap(Din), 8 * H, Din)   # [8H, Din]
             y_bf = torch.empty(B, T, 2 * H, dtype=torch.bfloat16, device=dev)
         else:
             x_op, w_op, y_bf = x_src, w_ih, None
@@ -747,7 +759,7 @@ class BLSTMLayerFn(torch.autograd.Function):
         if cd == BF16 and _fuse_xproj_on():
             # the input projection inside the persistent recurrence (no gx GEMM);
             # ASR_ERR_UNSUPPORTED when this shape / configuration does not take it
-            rc = N.query('asr_lstm_forward_x', N.ptr(x_op), Din, N.ptr(w_op), N.ptr(b_ih),
+            rc = N.query('asr_lstm_forward_x', N.ptr(x_op), Dp, N.ptr(w_op), N.ptr(b_ih),
                          N.ptr(b_hh), N.ptr(w_hh), ctypes.c_void_p(whh_r), N.ptr(lens), B, T, H,
                          N.ptr(gx), N.ptr(y), N.ptr(cst), N.ptr(y_bf), N.ptr(ws), nb,
                          N.stream_handle(dev))
@@ -757,8 +769,8 @@ class BLSTMLayerFn(torch.autograd.Function):
             fuse_x = rc == 0
         if not fuse_x:
             if cd == BF16:
-                run_gemm([gemm_problem(operand(x_op, 0, rowmap(Din)), operand(w_op, 0, rowmap(Din)),
-                                       gx, rowmap(8 * H), B * T, 8 * H, Din, bias=b_ih,
+                run_gemm([gemm_problem(operand(x_op, 0, rowmap(Dp)), operand(w_op, 0, rowmap(Dp)),
+                                       gx, rowmap(8 * H), B * T, 8 * H, Dp, bias=b_ih,
                                        bias2=b_hh)], dev)
             else:
                 run_gemm([gemm_problem(operand(x_src, 0, a_map), operand(w_ih, 0, rowmap(Din)), gx,
@@ -769,7 +781,7 @@ class BLSTMLayerFn(torch.autograd.Function):
                    N.stream_handle(dev))
         ctx.save_for_backward(x_op, w_op, lens, w_hh, b_ih, b_hh, gx, cst,
                               y_bf if y_bf is not None else y)
-        ctx.meta = (T, perm, t_mul, t_add, gbufs, cd, (B, T_src, Dsrc, Din), w_ih)
+        ctx.meta = (T, perm, t_mul, t_add, gbufs, cd, (B, T_src, Dsrc, Din, Dp), w_ih)
         ctx.drop = drop
         ctx.next_rec = bool(next_rec)
         ctx.n_graph = len(graph_params)
@@ -778,7 +790,7 @@ class BLSTMLayerFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x_op, w_op, lens, w_hh, b_ih, b_hh, act, cst, y_op = ctx.saved_tensors
-        T, perm, t_mul, t_add, gbufs, cd, (B, T_src, Dsrc, Din), w_ih = ctx.meta
+        T, perm, t_mul, t_add, gbufs, cd, (B, T_src, Dsrc, Din, Dp), w_ih = ctx.meta
         H = w_hh.shape[1]
         dev = act.device
         dy = dy.contiguous()
@@ -811,7 +823,7 @@ class BLSTMLayerFn(torch.autograd.Function):
         dg_op = dg_bf if dg_bf is not None else act
         # X as the dW_ih operand: the bf16 copy is already gathered (identity map)
         if cd == BF16:
-            x_map = rowmap(Din)
+            x_map = rowmap(Dp)
         else:
             x_map = rowmap(Dsrc, stride_b=T_src * Dsrc, rows_per_b=T, t_mul=t_mul, t_add=t_add,
                            t_limit=T_src, perm=perm)
@@ -856,7 +868,7 @@ class BLSTMLayerFn(torch.autograd.Function):
                            t_limit=T_src, perm=perm)
             # dropout's backward (the forward mask over x_src's flat offsets) is
             # applied by the GEMM's epilogue as it writes dX
-            p = gemm_problem(operand(dg_op, 0, rowmap(8 * H)), operand(w_op, 1, rowmap(Din)), dx,
+            p = gemm_problem(operand(dg_op, 0, rowmap(8 * H)), operand(w_op, 1, rowmap(Dp)), dx,
                              c_map, BT, Din, 8 * H, drop=ctx.drop)
             run_gemm([p], dev)
         return (dx,) + (None,) * (13 + ctx.n_graph)

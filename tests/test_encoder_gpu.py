@@ -504,3 +504,39 @@ def test_fused_input_projection_matches_gemm_path(B, T, H, Din, cuda_dev, monkey
         scale = np.abs(a).max() + 1e-12
         err = np.abs(a - b).max() / scale
         assert err < 2e-2, (n, err)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('B,T,H,Din', [(32, 120, 320, 123), (9, 40, 64, 13)])
+def test_padded_input_width_matches_fp32(B, T, H, Din, cuda_dev):
+    """A layer input whose width is not a multiple of 8 (TIMIT's 123 features,
+    BASELINE configs[0]) is staged in bf16 with zero-padded rows, so it takes
+    the fused projection and the fast GEMMs: y, dx and every weight gradient
+    against the exact-f32 path (unpadded) within the bf16 bound."""
+    from pytorch_end2end_speech_recognition_amd import native_ops as ops
+    rng = np.random.RandomState(B + Din)
+    lens = np.sort(rng.randint(T // 2, T + 1, B))[::-1].astype(np.int32)
+    lens[0] = T
+    x = torch.from_numpy(rng.randn(B, T, Din).astype(np.float32) * 0.5).to(cuda_dev)
+    params = [torch.from_numpy(rng.uniform(-0.1, 0.1, s).astype(np.float32)).to(cuda_dev)
+              for s in ((8 * H, Din), (8 * H, H), (8 * H,), (8 * H,))]
+    lens_d = torch.from_numpy(lens).to(cuda_dev)
+    dy = torch.from_numpy(rng.randn(B, T, 2 * H).astype(np.float32)).to(cuda_dev)
+    outs = {}
+    try:
+        for cd in ('fp32', 'bf16'):
+            ops.set_compute_dtype(cd)
+            ws = [t.clone().requires_grad_(True) for t in params]
+            xx = x.clone().requires_grad_(True)
+            y = ops.blstm_layer(xx, lens_d, T, *ws)
+            (y * dy).sum().backward()
+            torch.cuda.synchronize()
+            outs[cd] = [y.detach().cpu().numpy(), xx.grad.cpu().numpy()] + \
+                [w.grad.cpu().numpy() for w in ws]
+    finally:
+        ops.set_compute_dtype('fp32')
+    for n, a, b in zip(['y', 'dx', 'dW_ih', 'dW_hh', 'db_ih', 'db_hh'], outs['fp32'], outs['bf16']):
+        err = np.abs(a - b).max() / (np.abs(a).max() + 1e-12)
+        assert err < 2e-2, (n, err)
+    for b in range(B):      # padded frames stay exactly zero
+        assert not outs['bf16'][0][b, lens[b]:].any()
