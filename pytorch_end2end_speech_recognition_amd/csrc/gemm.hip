@@ -1543,6 +1543,43 @@ __global__ void splitk_reduce(const float* __restrict__ slab, int ksplit, int M,
   crow[n] = v;
 }
 
+// splitk_reduce over 4 columns per thread (N % 4 == 0, C rows 16-B aligned):
+// 16-B slab / C accesses, 32-bit index math (M * N < 2^31), same fixed order.
+__global__ void splitk_reduce4(const float* __restrict__ slab, int ksplit, int M, int N, RowMap c,
+                               float alpha, float beta, const float* __restrict__ bias,
+                               const float* __restrict__ bias2, float drop_p,
+                               unsigned long long drop_seed) {
+  const int MN = M * N;
+  const int e = 4 * (blockIdx.x * 256 + threadIdx.x);
+  if (e >= MN) return;
+  const int m = e / N, n = e - m * N;
+  const long long off = row_off(c, m);
+  if (off < 0) return;
+  float4 s = *reinterpret_cast<const float4*>(slab + e);
+  for (int k = 1; k < ksplit; ++k) {
+    const float4 t = *reinterpret_cast<const float4*>(slab + (long long)k * MN + e);
+    s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
+  }
+  float v[4] = {alpha * s.x, alpha * s.y, alpha * s.z, alpha * s.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (bias) v[q] += bias[n + q];
+    if (bias2) v[q] += bias2[n + q];
+  }
+  float* crow = (float*)c.base + off + n;
+  if (beta != 0.f) {
+    const float4 o = *reinterpret_cast<const float4*>(crow);
+    v[0] += beta * o.x; v[1] += beta * o.y; v[2] += beta * o.z; v[3] += beta * o.w;
+  }
+  if (drop_p > 0.f) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      v[q] *= u01(drop_seed, (unsigned long long)(off + n + q)) >= drop_p ? 1.f / (1.f - drop_p)
+                                                                         : 0.f;
+  }
+  *reinterpret_cast<float4*>(crow) = make_float4(v[0], v[1], v[2], v[3]);
+}
+
 // Column sums: partial[chunk][n] = sum over rows of chunk; then ordered final sum.
 // One (64-column, row chunk) tile per work-group: 4 waves split the chunk's
 // rows (wave w takes rows w, w + 4, ...), each lane keeps eight rows' loads in
@@ -1943,9 +1980,16 @@ int gemm_launch_own(const asr_gemm_t* problems, int nprob, int compute_dtype, vo
     if (p.ksplit <= 1) continue;
     const long long mn = (long long)p.M * p.N;
     if (mn == 0) continue;
-    hipLaunchKernelGGL(splitk_reduce, dim3((unsigned)((mn + 255) / 256)), dim3(256), 0, s, p.slab,
-                       p.ksplit, p.M, p.N, p.c, p.alpha, p.beta, p.bias, p.bias2, p.drop_p,
-                       p.drop_seed);
+    const bool v4 = p.N % 4 == 0 && mn < 0x7fffffffLL && ((uintptr_t)p.c.base & 15) == 0 &&
+                    p.c.stride_t % 4 == 0 && p.c.stride_b % 4 == 0;
+    if (v4)
+      hipLaunchKernelGGL(splitk_reduce4, dim3((unsigned)((mn / 4 + 255) / 256)), dim3(256), 0, s,
+                         p.slab, p.ksplit, p.M, p.N, p.c, p.alpha, p.beta, p.bias, p.bias2,
+                         p.drop_p, p.drop_seed);
+    else
+      hipLaunchKernelGGL(splitk_reduce, dim3((unsigned)((mn + 255) / 256)), dim3(256), 0, s,
+                         p.slab, p.ksplit, p.M, p.N, p.c, p.alpha, p.beta, p.bias, p.bias2,
+                         p.drop_p, p.drop_seed);
     ASR_LAUNCH_CHECK();
   }
   return ASR_OK;
