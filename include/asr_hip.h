@@ -584,6 +584,14 @@ int asr_conv_weight_unpack_acc_pad(const float* packed, int Co, int Ci, int Cip,
  * weight [Co][Ci][3][3]; z / dx over valid pixels; dw / dbias accumulate. */
 int asr_conv_direct_forward(const float* x, int B, int T, int F, int Ci, int Co, const float* w,
                             const float* bias, float* z, void* stream);
+/* Single-input-channel 3x3 convolution forward (the first VGG layer) from
+ * channel 0 of a padded operand x [B][T+2][F+2][cstride] (x_dtype ASR_DT_F32
+ * or ASR_DT_BF16, e.g. the GEMM path's 16-channel bf16 staging): z
+ * [B][T+2][F+2][Co] f32 at valid pixels (+ bias); Co % 4 == 0, Co <= 512.
+ * Same sum as asr_conv_direct_forward with Ci = 1 (CNNEncoder's first Conv2d,
+ * cnn.py:124-165). */
+int asr_conv3x3_c1_forward(const void* x, int x_dtype, int cstride, int B, int T, int F, int Co,
+                           const float* w, const float* bias, float* z, void* stream);
 int asr_conv_direct_dgrad(const float* dz, int B, int T, int F, int Ci, int Co, const float* w,
                           float* dx, void* stream);
 size_t asr_conv_direct_wgrad_workspace_bytes(int B, int T, int F, int Ci, int Co);

@@ -50,6 +50,8 @@ SIGNATURES = {
     'asr_colsum_workspace_bytes': (c_size, [c_int, c_int]),
     'asr_colsum_accumulate': (c_int, [c_vp, c_ll, c_int, c_int, c_float, c_vp, c_vp, c_vp, c_size,
                                       c_vp]),
+    'asr_conv3x3_c1_forward': (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp,
+                                       c_vp, c_vp]),
     'asr_lstm_workspace_bytes': (c_size, [c_int, c_int, c_int, c_int]),
     'asr_lstm_forward': (c_int, [c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp,
                                  c_vp, c_vp, c_vp, c_size, c_vp]),

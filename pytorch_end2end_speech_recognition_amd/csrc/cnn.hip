@@ -84,6 +84,54 @@ __global__ void conv_direct_fwd(const float* __restrict__ x, int B, int T, int F
   }
 }
 
+// First VGG layer (one input channel) forward as a direct stencil: one
+// work-group per (utterance, frame); the three padded input rows it needs
+// (channel 0 of the padded operand, pitch cstride elements) and the Co x 9
+// weights go to LDS; each thread produces 4 channels of a pixel per
+// iteration (16-B z stores, 16 threads = one pixel's 64 channels).  The
+// tap-addressed GEMM did this with the channel padded to 16 (K = 144 of which
+// 9 useful) in 837 us at vgg_hier; this is bound by z's f32 write.
+template <typename TX>
+__global__ void __launch_bounds__(CT) conv3x3_c1_fwd(const TX* __restrict__ x, int cstride, int T,
+                                                     int F, int Co, const float* __restrict__ w,
+                                                     const float* __restrict__ bias,
+                                                     float* __restrict__ z) {
+  extern __shared__ float sm[];
+  float* xr = sm;                    // [3][F + 2]
+  float* ws = sm + 3 * (F + 2);      // [9][Co]: tap-major, channel fastest
+  const int bt = blockIdx.x;
+  const int b = bt / T, t = bt - b * T;
+  const long long row0 = ((long long)b * (T + 2) + t) * (F + 2);   // padded row t - 1
+  for (int i = threadIdx.x; i < 3 * (F + 2); i += CT) {
+    const TX v = x[(row0 + i) * cstride];
+    if constexpr (sizeof(TX) == 2) xr[i] = bf2f((uint16_t)v);
+    else xr[i] = (float)v;
+  }
+  for (int i = threadIdx.x; i < 9 * Co; i += CT) {
+    const int co = i % Co, tap = i / Co;     // tap = kh * 3 + kw
+    ws[i] = w[co * 9 + tap];
+  }
+  __syncthreads();
+  const int ng = Co >> 2;
+  for (int i = threadIdx.x; i < F * ng; i += CT) {
+    const int f = i / ng, c4 = 4 * (i - (i / ng) * ng);
+    float4 acc = bias ? *reinterpret_cast<const float4*>(bias + c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        // z[p] += w[co][kh][kw] x[p + (kw - 1)(F + 2) + (kh - 1)]
+        const float xv = xr[kw * (F + 2) + f + kh];
+        const float4 wv = *reinterpret_cast<const float4*>(ws + (kh * 3 + kw) * Co + c4);
+        acc.x += wv.x * xv;
+        acc.y += wv.y * xv;
+        acc.z += wv.z * xv;
+        acc.w += wv.w * xv;
+      }
+    *reinterpret_cast<float4*>(z + (row0 + (F + 2) + f + 1) * Co + c4) = acc;
+  }
+}
+
 // dx[p][ci] = sum_{co,kh,kw} dz[p - shift][co] w[co][ci][kh][kw] (dz halo rows zero)
 __global__ void conv_direct_dgrad(const float* __restrict__ dz, int B, int T, int F, int Ci,
                                   int Co, const float* __restrict__ w, float* __restrict__ dx) {
@@ -658,6 +706,31 @@ extern "C" int asr_conv_direct_forward(const float* x, int B, int T, int F, int 
               "conv_direct_forward: bad args");
   hipLaunchKernelGGL(conv_direct_fwd, dim3(grid_for((long long)B * T * F * Co)), dim3(CT), 0,
                      (hipStream_t)stream, x, B, T, F, Ci, Co, w, bias, z);
+  ASR_LAUNCH_CHECK();
+  return ASR_OK;
+}
+
+// Single-input-channel 3x3 convolution forward from channel 0 of a padded
+// operand x [B][T+2][F+2][cstride] (x_dtype F32 or BF16): z [B][T+2][F+2][Co]
+// f32 at valid pixels, + bias.  Co % 4 == 0, Co <= 512.
+extern "C" int asr_conv3x3_c1_forward(const void* x, int x_dtype, int cstride, int B, int T,
+                                      int F, int Co, const float* w, const float* bias, float* z,
+                                      void* stream) {
+  ASR_REQUIRE(x && w && z && B > 0 && T > 0 && F > 0 && cstride > 0, ASR_ERR_ARG,
+              "conv3x3_c1_forward: bad args");
+  ASR_REQUIRE(Co > 0 && Co % 4 == 0 && Co <= 512, ASR_ERR_UNSUPPORTED,
+              "conv3x3_c1_forward: Co must be a multiple of 4, <= 512");
+  ASR_REQUIRE(((uintptr_t)z & 15) == 0 && (!bias || ((uintptr_t)bias & 15) == 0), ASR_ERR_ARG,
+              "conv3x3_c1_forward: z / bias not 16-B aligned");
+  const size_t lds = (size_t)(3 * (F + 2) + 9 * Co) * 4;
+  ASR_REQUIRE(lds <= 64 * 1024, ASR_ERR_UNSUPPORTED, "conv3x3_c1_forward: F too large");
+  hipStream_t s = (hipStream_t)stream;
+  if (x_dtype == ASR_DT_BF16)
+    hipLaunchKernelGGL(conv3x3_c1_fwd<uint16_t>, dim3(B * T), dim3(CT), lds, s,
+                       (const uint16_t*)x, cstride, T, F, Co, w, bias, z);
+  else
+    hipLaunchKernelGGL(conv3x3_c1_fwd<float>, dim3(B * T), dim3(CT), lds, s, (const float*)x,
+                       cstride, T, F, Co, w, bias, z);
   ASR_LAUNCH_CHECK();
   return ASR_OK;
 }

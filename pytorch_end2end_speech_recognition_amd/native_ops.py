@@ -1483,6 +1483,12 @@ class VGGFn(torch.autograd.Function):
             if not use_gemm[l]:
                 N.call('asr_conv_direct_forward', N.ptr(x_op), B, cT, cF, cC, Co, N.ptr(w),
                        N.ptr(sp['b']), N.ptr(z), N.stream_handle(dev))
+            elif cC == 1 and Co % 4 == 0 and os.environ.get('ASR_VGG_C1_DIRECT', '1') != '0':
+                # one input channel: a direct stencil from channel 0 of the padded
+                # operand (the GEMM would run K = 144 for 9 useful taps); the
+                # backward still takes the weight-gradient GEMM over this operand
+                N.call('asr_conv3x3_c1_forward', N.ptr(x_op), cd, cCp, B, cT, cF, Co, N.ptr(w),
+                       N.ptr(sp['b']), N.ptr(z), N.stream_handle(dev))
             else:
                 wg = (torch.zeros if cCp != cC else torch.empty)(Co, 9 * cCp, dtype=opdt,
                                                                  device=dev)
