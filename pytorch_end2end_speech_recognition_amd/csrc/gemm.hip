@@ -432,13 +432,13 @@ __device__ __forceinline__ long long row_off_np(const RowMap& m, int r) {
 // This thread's 4 buffer->LDS loads of one operand tile.  Instruction i of
 // wave w fills LDS bytes [1024*(4w+i), +1024): R mode tile rows (4w+i)*8..+7,
 // K mode tile k-rows (4w+i)*4..+3.
-template <int MODE>
+template <int MODE, int NB = 4>
 __device__ __forceinline__ void stage_tile(const Operand& op, __amdgpu_buffer_rsrc_t rs,
                                            char* lds_tile, int tile0, int nrows, int k0, int kend,
                                            int wave, int lane) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int blk = wave * 4 + i;
+  for (int i = 0; i < NB; ++i) {
+    const int blk = wave * NB + i;
     unsigned voff = OOB_OFF;
     if (MODE == 0) {
       const int r = blk * 8 + (lane >> 3);
@@ -495,13 +495,13 @@ __device__ __forceinline__ int tap_shift(const Operand& op, int tap) {
   return op.tap_s * ((tap / 3 - 1) * op.tap_w + (tap % 3 - 1));
 }
 
-template <int MODE>
+template <int MODE, int NB = 4>
 __device__ __forceinline__ void stagef_init(const Operand& op, StageF& st, int tile0, int nrows,
                                             int kbeg, int wave, int lane) {
   st.valid = 0;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int blk = wave * 4 + i;
+  for (int i = 0; i < NB; ++i) {
+    const int blk = wave * NB + i;
     if (MODE == 0) {
       const int r = blk * 8 + (lane >> 3);
       const int c = (lane & 7) ^ ((r >> 1) & 7);
@@ -543,12 +543,12 @@ __device__ __forceinline__ void stagef_init(const Operand& op, StageF& st, int t
   }
 }
 
-template <int MODE>
+template <int MODE, int NB = 4>
 __device__ __forceinline__ void stagef(const Operand& op, __amdgpu_buffer_rsrc_t rs, StageF& st,
                                        char* lds_tile, int k0, int kend, int wave, int lane) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int blk = wave * 4 + i;
+  for (int i = 0; i < NB; ++i) {
+    const int blk = wave * NB + i;
     unsigned voff = OOB_OFF;
     if (MODE == 0) {
       const int r = blk * 8 + (lane >> 3);
@@ -599,12 +599,12 @@ __device__ __forceinline__ void stagef(const Operand& op, __amdgpu_buffer_rsrc_t
 
 // One operand's tile of the 128x128 kernel: StageF when the operand allows it
 // (wave-uniform branch), else the per-DMA row map.
-template <int MODE>
+template <int MODE, int NB = 4>
 __device__ __forceinline__ void stage_any(const Operand& op, __amdgpu_buffer_rsrc_t rs,
                                           StageF& st, char* lds_tile, int tile0, int nrows,
                                           int k0, int kend, int wave, int lane) {
-  if (op.sf) stagef<MODE>(op, rs, st, lds_tile, k0, kend, wave, lane);
-  else stage_tile<MODE>(op, rs, lds_tile, tile0, nrows, k0, kend, wave, lane);
+  if (op.sf) stagef<MODE, NB>(op, rs, st, lds_tile, k0, kend, wave, lane);
+  else stage_tile<MODE, NB>(op, rs, lds_tile, tile0, nrows, k0, kend, wave, lane);
 }
 
 // MFMA fragment (16 rows x 32 k) of the block starting at tile row rb, k-half kk.
@@ -742,6 +742,94 @@ __global__ void __launch_bounds__(NT) gemm_bf16_fast(Params P) {
       }
       mma_ktile<AMODE, BMODE>(smem + (kt % NSTAGE) * 2 * FTILE, acc, wr, wc, lane);
     }
+  }
+  store_acc(pr, acc, tm, tn, wr, wc, lane, split, nsplit);
+}
+
+// 256 x 64 tiles for products with N <= 64 and B in R mode (B stored [N][K]:
+// the 3x3 convolutions of the 64-channel VGG layers, forward and input
+// gradient).  The 128 x 128 kernel computed those with half of every B tile
+// and of every MFMA empty.  Four waves stacked along M (64 x 64 each, the
+// same fragments and MFMA order as gemm_bf16_fast), the A tile staged as two
+// 128-row halves (own StageF states), the B tile as 64 rows (two DMAs per
+// wave); double-buffered, 80 KB of LDS (two work-groups per CU).
+constexpr int N64_BM = 256;
+constexpr int N64_STAGE = 2 * FTILE + FTILE / 2;   // A (32 KB) + B (8 KB)
+
+template <int AMODE>
+__global__ void __launch_bounds__(NT) gemm_bf16_n64(Params P) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int zb = blockIdx.z / P.nprob, zp = blockIdx.z % P.nprob;
+  Problem pr = P.p[zp];
+  if (zb >= pr.batch) return;
+  if (zb > 0) {
+    pr.a.map.base = (const char*)pr.a.map.base + zb * pr.sA * 2;
+    pr.b.map.base = (const char*)pr.b.map.base + zb * pr.sB * 2;
+    pr.a.bytes -= zb * pr.sA * 2;
+    pr.b.bytes -= zb * pr.sB * 2;
+    pr.c.base = (const char*)pr.c.base + zb * pr.sC * 4;
+  }
+  const int gm = (pr.M + N64_BM - 1) / N64_BM;
+  const int nsplit = pr.ksplit > 1 ? pr.ksplit : 1;
+  const int ntot = gm * nsplit;
+  int id = blockIdx.x;
+  if (id >= ntot) return;
+  {
+    const int q = ntot / 8, r = ntot % 8, x = id % 8;
+    id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + id / 8;
+  }
+  const int split = id / gm;
+  const int tm = (id - split * gm) * N64_BM, tn = 0;
+  const int kbeg = nsplit > 1 ? split * pr.kchunk : 0;
+  const int kend = nsplit > 1 ? min(pr.K, kbeg + pr.kchunk) : pr.K;
+
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = w * 64, wc = 0;
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc((void*)pr.a.map.base, 0, (int)pr.a.bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)pr.b.map.base, 0, (int)pr.b.bytes, 0x00020000);
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (kend - kbeg + FBK - 1) / FBK;
+  StageF sa0, sa1, sb;
+  if (pr.a.sf) {
+    stagef_init<AMODE>(pr.a, sa0, tm, pr.M, kbeg, w, lane);
+    stagef_init<AMODE>(pr.a, sa1, tm + 128, pr.M, kbeg, w, lane);
+  }
+  if (pr.b.sf) stagef_init<0, 2>(pr.b, sb, tn, pr.N, kbeg, w, lane);
+  auto stage = [&](char* st, int k0) {
+    stage_any<AMODE>(pr.a, ra, sa0, st, tm, pr.M, k0, kend, w, lane);
+    stage_any<AMODE>(pr.a, ra, sa1, st + FTILE, tm + 128, pr.M, k0, kend, w, lane);
+    stage_any<0, 2>(pr.b, rb, sb, st + 2 * FTILE, tn, pr.N, k0, kend, w, lane);
+  };
+  stage(smem, kbeg);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* cur = smem + (kt & 1) * N64_STAGE;
+    if (kt + 1 < nk) stage(smem + ((kt + 1) & 1) * N64_STAGE, kbeg + (kt + 1) * FBK);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)   // waves 2, 3 read the second 128-row half
+        fa[i] = frag_bf16<AMODE>(cur + (wr >> 7) * FTILE, (wr & 127) + 16 * i, kk, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = frag_bf16<0>(cur + 2 * FTILE, wc + 16 * j, kk, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma_bf16(fa[i], fb[j], acc[i][j]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
   }
   store_acc(pr, acc, tm, tn, wr, wc, lane, split, nsplit);
 }
@@ -1787,6 +1875,18 @@ int split_target() {
 // ASR_OVERLAP_WGRAD=2) must fit beside its work-group on every CU.
 thread_local int g_small_tiles = 0;
 
+// Products with N <= 64 and many rows take the 256 x 64 kernel (B in R mode;
+// ASR_GEMM_N64=0 keeps them on the 128 x 128 kernel; read per launch).
+bool n64_ok(const asr_gemm_t* g, int nprob) {
+  if (g_small_tiles) return false;
+  const char* e = getenv("ASR_GEMM_N64");
+  if (e && e[0] == '0') return false;
+  for (int i = 0; i < nprob; ++i)
+    if (g[i].N > 64 || g[i].M < 4096) return false;
+  return true;
+}
+
+
 bool big8_ok(const asr_gemm_t* g, int nprob) {
   const char* e = getenv("ASR_GEMM_8W");
   if (e && e[0] == '0') return false;
@@ -1944,6 +2044,24 @@ int gemm_launch_own(const asr_gemm_t* problems, int nprob, int compute_dtype, vo
     }
     hipLaunchKernelGGL(gemm_bf16_kk256, dim3(maxwg2, 1, nprob * maxb), dim3(NT),
                        (size_t)NST2 * 2 * FTILE2, s, P);
+  } else if ((fast == 0 || fast == 2) && n64_ok(problems, nprob)) {
+    static bool attr64 = false;
+    if (!attr64) {
+      bool ok = hipFuncSetAttribute((const void*)gemm_bf16_n64<0>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    2 * N64_STAGE) == hipSuccess;
+      ok &= hipFuncSetAttribute((const void*)gemm_bf16_n64<1>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                2 * N64_STAGE) == hipSuccess;
+      ASR_REQUIRE(ok, ASR_ERR_HIP, "gemm: cannot raise the LDS limit of the 256x64 kernel");
+      attr64 = true;
+    }
+    int maxwg64 = 0;
+    for (int i = 0; i < nprob; ++i)
+      maxwg64 = max(maxwg64, ceil_div(P.p[i].M, N64_BM) * max(1, P.p[i].ksplit));
+    const dim3 g64(maxwg64, 1, nprob * maxb);
+    if (fast == 0) hipLaunchKernelGGL(gemm_bf16_n64<0>, g64, dim3(NT), 2 * N64_STAGE, s, P);
+    else hipLaunchKernelGGL(gemm_bf16_n64<1>, g64, dim3(NT), 2 * N64_STAGE, s, P);
   } else if (fast >= 0) {
     const int nst = g_small_tiles ? 2 : fast_stages();
     const size_t lds = (size_t)nst * 2 * FTILE;

@@ -340,3 +340,39 @@ def test_dropout_epilogue_matches_separate_pass(M, N, K, dtype, kind, cuda_dev):
         assert (fused[1::2] == 0).float().mean().item() > 0.2      # the mask is applied
     finally:
         ops.set_compute_dtype('fp32')
+
+
+@pytest.mark.parametrize('M,N,K,atrans', [(5000, 64, 576, 0), (4391, 40, 200, 0),
+                                          (6000, 64, 1152, 1), (4096, 17, 72, 1)])
+def test_n64_kernel_exact(M, N, K, atrans, cuda_dev, monkeypatch):
+    """The 256 x 64 kernel (products with N <= 64, B stored [N][K]: the
+    64-channel VGG convolutions) on small-integer bf16 operands, exact in f32:
+    both A layouts, N below 64, K not a multiple of the 64-deep k-tile, M not a
+    multiple of the 256-row tile, bias pair and beta; equal to the 128 x 128
+    kernel's result (ASR_GEMM_N64=0) bit for bit."""
+    ops = _ops()
+    ops.set_compute_dtype('bf16')
+    try:
+        rng = np.random.RandomState(M + N + K)
+        a_np = rng.randint(-3, 4, (M, K)).astype(np.float32)
+        b_np = rng.randint(-3, 4, (N, K)).astype(np.float32)
+        bias = torch.from_numpy(rng.randint(-2, 3, N).astype(np.float32)).to(cuda_dev)
+        c0 = rng.randint(-2, 3, (M, N)).astype(np.float32)
+        a_st = a_np.T.copy() if atrans else a_np
+        a = torch.from_numpy(a_st).to(torch.bfloat16).to(cuda_dev)
+        b = torch.from_numpy(b_np).to(torch.bfloat16).to(cuda_dev)
+        outs = []
+        for n64 in ('1', '0'):
+            monkeypatch.setenv('ASR_GEMM_N64', n64)
+            c = torch.from_numpy(c0).to(cuda_dev)
+            p = ops.gemm_problem(ops.operand(a, atrans, ops.rowmap(M if atrans else K)),
+                                 ops.operand(b, 0, ops.rowmap(K)), c, ops.rowmap(N), M, N, K,
+                                 bias=bias, beta=1.0)
+            ops.run_gemm([p], cuda_dev)
+            torch.cuda.synchronize()
+            outs.append(c.cpu().numpy())
+        ref = a_np.astype(np.float64) @ b_np.astype(np.float64).T + bias.cpu().numpy() + c0
+        np.testing.assert_array_equal(outs[0], ref)
+        np.testing.assert_array_equal(outs[0], outs[1])
+    finally:
+        ops.set_compute_dtype('fp32')
