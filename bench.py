@@ -130,7 +130,9 @@ def roofline_report(args, p, mean_us, launches, mean_work, workload):
     w_hh = 2 * 4 * H * H * esz                # both directions
     flops_step = 2 * 2 * B * 4 * H * H        # h @ W_hh^T, 2 directions
     fwd_cell = 4 * 4 * 2 + 4 * 2              # gx read + act write (4 gates f32), y + c write
-    bwd_cell = 4 * 4 * 2 + 4 * 3              # act read + dG write, dy + c_t + c_{t-1} read
+    # act read + dG write (f32; bf16 mode writes only the bf16 copy), dy + c read
+    # (bf16 mode carries c_t over from the previous step's c_{t-1}: one read)
+    bwd_cell = (4 * 4 + 2 * 4 + 4 * 2) if args.precision == 'bf16' else (4 * 4 * 2 + 4 * 3)
     fwd_pass_bytes = T * 2 * cell * fwd_cell + w_hh
     fwd_pass_flops = T * flops_step
     if args.precision == 'bf16' and os.environ.get('ASR_FUSE_XPROJ', '1') != '0':
