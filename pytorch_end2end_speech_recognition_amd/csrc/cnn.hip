@@ -571,6 +571,98 @@ __global__ void __launch_bounds__(CT) post_bwd(const float* __restrict__ dnext,
   }
 }
 
+// post_bwd over the full-resolution pixels: thread (pixel, 4 channels) finds
+// its pool window, takes the window's gradient (BN backward applied) where
+// the pixel was the window's argmax and z > 0, and writes dz for EVERY pixel
+// as one 8-B (bf16) / 16-B store next to one 16-B z load.  post_bwd instead
+// walked the pooled elements and gathered z / scattered dz one channel at a
+// time (554 us at the first pooled vgg_hier layer).  The window's gradient is
+// recomputed by each of its pixels (dnext / P / slot are a quarter of z's
+// size and come from the cache).  Bias partials as in post_bwd.
+template <typename TO>
+__global__ void __launch_bounds__(CT) post_bwd_full(const float* __restrict__ dnext,
+                                                    const float* __restrict__ P,
+                                                    const float* __restrict__ z,
+                                                    const uint8_t* __restrict__ slot, int B, int T,
+                                                    int F, int C, Pool pl, int flat, Affine af,
+                                                    const float* __restrict__ sums,
+                                                    TO* __restrict__ dz,
+                                                    float* __restrict__ bias_part) {
+  constexpr int V = 4;
+  __shared__ float red[CT * V];
+  const unsigned nr = (unsigned)B * pl.To * pl.Fo;
+  const unsigned CV = (unsigned)(C / V);
+  const unsigned n = (unsigned)B * T * F * CV;
+  const float inv_n = 1.f / (float)nr;
+  float bacc[V] = {0.f, 0.f, 0.f, 0.f};
+  for (unsigned e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+    const unsigned q = e / CV;
+    const int c = (int)(e - q * CV) * V;
+    const PixIdx px = pix_of(q, T, F);            // (b, t, f) at full resolution
+    int to = px.to, fo = px.fo;
+    bool in = true;
+    if (pl.pt) {
+      to = px.to / pl.pt;
+      fo = px.fo / pl.pf;
+      in = to < pl.To && fo < pl.Fo;
+    }
+    const long long p = pad_row(px.b, px.to, px.fo, T, F) * C + c;
+    float v[V] = {0.f, 0.f, 0.f, 0.f};
+    if (in) {
+      const unsigned qp = ((unsigned)px.b * pl.To + to) * pl.Fo + fo;
+      const long long ip = (long long)qp * C + c;
+      VecF<V> g = dy_at<V>(dnext, qp, c, pl.To, pl.Fo, C, flat, af.drop, af.seed);
+      if (af.mean) {
+        VecF<V> x, m, r, gm, s1, s2;
+        x.load(P + ip);
+        m.load(af.mean + c);
+        r.load(af.rstd + c);
+        gm.load(af.gamma + c);
+        s1.load(sums + c);
+        s2.load(sums + C + c);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          const float xh = (x.v[j] - m.v[j]) * r.v[j];
+          g.v[j] = gm.v[j] * r.v[j] * (g.v[j] - s1.v[j] * inv_n - xh * s2.v[j] * inv_n);
+        }
+      }
+      VecF<V> zv;
+      zv.load(z + p);
+      unsigned sl = 0u, me = 0u;
+      if (pl.pt) {
+        sl = *reinterpret_cast<const unsigned*>(slot + ip);   // four channels' argmax slots
+        me = (unsigned)((px.fo - fo * pl.pf) * pl.pt + (px.to - to * pl.pt));
+      }
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const bool hit = !pl.pt || ((sl >> (8 * j)) & 0xffu) == me;
+        v[j] = (hit && zv.v[j] > 0.f) ? g.v[j] : 0.f;
+        bacc[j] += v[j];
+      }
+    }
+    if constexpr (sizeof(TO) == 2) {
+      uint2 o;
+      o.x = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
+      o.y = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+      *reinterpret_cast<uint2*>(dz + p) = o;
+    } else {
+      *reinterpret_cast<float4*>(dz + p) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  }
+  if (bias_part) {   // threads tid, tid + CV, ... hold the same channels
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < V; ++j) red[tid * V + j] = bacc[j];
+    __syncthreads();
+    for (int cc = tid; cc < C; cc += CT) {
+      const int g2 = cc / V, j = cc % V;
+      float t = 0.f;
+      for (int k = g2; k < CT; k += (int)CV) t += red[k * V + j];
+      bias_part[(long long)blockIdx.x * C + cc] = t;
+    }
+  }
+}
+
 // GEMM weight images of a torch Conv2d weight W [Co][Ci][3(f)][3(t)], tap
 // j = kw*3 + kh (the row shift (kw-1)(F+2) + (kh-1) of gemm.hip tap addressing):
 //   mode 0 (forward):  out[co][j*Ci + ci] = W[co][ci][kh][kw]
@@ -979,7 +1071,16 @@ extern "C" int asr_vgg_block_backward_ex(const float* dnext, int flat, const flo
                        dbeta);
     ASR_LAUNCH_CHECK();
   }
-  if (dz_dtype == ASR_DT_BF16) {
+  const char* pfe = getenv("ASR_VGG_POST_FULL");   // A/B: full-resolution dz pass
+  const bool full = v4 && !(pfe && pfe[0] == '0') && ((uintptr_t)dz & 15) == 0 &&
+                    ((uintptr_t)z & 15) == 0;
+  if (full && dz_dtype == ASR_DT_BF16) {
+    hipLaunchKernelGGL(post_bwd_full<uint16_t>, dim3(pgrid), dim3(CT), 0, s, dnext, P, z, slot, B,
+                       T, F, C, pl, flat, af, sums, (uint16_t*)dz, bpart);
+  } else if (full) {
+    hipLaunchKernelGGL(post_bwd_full<float>, dim3(pgrid), dim3(CT), 0, s, dnext, P, z, slot, B, T,
+                       F, C, pl, flat, af, sums, (float*)dz, bpart);
+  } else if (dz_dtype == ASR_DT_BF16) {
     if (v4)
       hipLaunchKernelGGL((post_bwd<uint16_t, 4>), dim3(pgrid), dim3(CT), 0, s, dnext, P, z, slot,
                          B, T, F, C, pl, flat, af, sums, (uint16_t*)dz, bpart);
