@@ -74,6 +74,9 @@ class CTC(ModelBase):
         else:
             raise NotImplementedError('encoder_type=%s' % encoder_type)
 
+        # the first layer after the encoder folds the encoder's output dropout
+        # into its product (bf16 mode; rnn.py:392-393 semantics, same mask)
+        self.encoder.defer_output_dropout = True
         if len(fc_list) > 0:
             for i in range(len(fc_list)):
                 din = self.encoder_num_units if i == 0 else fc_list[i - 1]
@@ -123,9 +126,14 @@ class CTC(ModelBase):
                 xs, x_lens, volatile=not self.training)
         else:
             xs, x_lens, perm_idx = self.encoder(xs, x_lens, volatile=not self.training)
+        # the encoder's output dropout, when handed over, is folded into the
+        # first layer that reads xs (LinearND input_drop: same mask)
+        pd = self.encoder.pending_output_drop
+        self.encoder.pending_output_drop = None
         for i in range(len(self.fc_list)):
-            xs = getattr(self, 'fc_' + str(i))(xs)
-        logits = self.fc_out(xs)
+            xs = getattr(self, 'fc_' + str(i))(xs, input_drop=pd)
+            pd = None
+        logits = self.fc_out(xs, input_drop=pd)
         if is_multi_task:
             for i in range(len(self.fc_list_sub)):
                 xs_sub = getattr(self, 'fc_sub_' + str(i))(xs_sub)

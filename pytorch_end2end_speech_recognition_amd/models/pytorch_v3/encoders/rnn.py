@@ -70,6 +70,11 @@ class RNNEncoder(nn.Module):
         self.subsample_type = subsample_type
         self.dropout_input_p = float(dropout_input)
         self.dropout_hidden_p = float(dropout_hidden)
+        # set by a model whose head consumes the output directly: the last
+        # layer's dropout is then handed over in pending_output_drop instead of
+        # applied (the head folds it into its product; training mode only)
+        self.defer_output_dropout = False
+        self.pending_output_drop = None
         self.dropout_input = nn.Dropout(p=dropout_input)
         self.batch_norm = batch_norm
         assert not (residual and dense_residual)
@@ -174,6 +179,7 @@ class RNNEncoder(nn.Module):
         h_sub = lens_sub = None
         res_outputs = []
         pending = None   # (p, seed): this layer's dropout, fused into the next layer's staging
+        self.pending_output_drop = None
         for l in range(self.num_layers):
             (w_ih, w_hh, b_ih, b_hh), gbufs = self._layer_tensors(l)
             lens_d = torch.from_numpy(lens.astype(np.int32)).to(dev, non_blocking=True)
@@ -198,6 +204,11 @@ class RNNEncoder(nn.Module):
                         not (self.residual or self.dense_residual or self.num_proj > 0) and
                         not (self.subsample_list[l] and self.subsample_type != 'drop')):
                     pending = (self.dropout_hidden_p, seed)
+                elif (l == self.num_layers - 1 and self.defer_output_dropout and
+                      self.num_layers_sub < 1 and ops.fuse_dropout_ok()):
+                    # the owning model folds the output dropout into its head's
+                    # product (LinearND input_drop); same seed, same mask
+                    self.pending_output_drop = (self.dropout_hidden_p, seed)
                 else:
                     h = ops.dropout(h, self.dropout_hidden_p, seed=seed)
             if self.num_layers_sub >= 1 and l == self.num_layers_sub - 1:   # rnn.py:400-407

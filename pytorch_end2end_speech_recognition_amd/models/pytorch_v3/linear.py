@@ -18,8 +18,10 @@ class LinearND(nn.Module):
         self.fc = nn.Linear(*size, bias=bias)
         self.dropout_p = float(dropout)
 
-    def forward(self, xs):
-        ys = ops.linear(xs, self.fc.weight, self.fc.bias)
+    def forward(self, xs, input_drop=None):
+        """input_drop=(p, seed): the caller's dropout of xs (same mask as
+        ops.dropout(xs, p, seed)), folded into this layer's product."""
+        ys = ops.linear(xs, self.fc.weight, self.fc.bias, drop=input_drop)
         if self.training and self.dropout_p > 0:
             ys = ops.dropout(ys, self.dropout_p)
         return ys

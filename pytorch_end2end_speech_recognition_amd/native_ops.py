@@ -151,8 +151,13 @@ def _staged(t, rows, cols, ld=None):
 
 
 class LinearFn(torch.autograd.Function):
+    """y = dropout(x) W^T + b.  drop=(p, seed): dropout of the INPUT with
+    asr_dropout's mask, folded into the bf16 staging of x (forward) and the dX
+    GEMM's epilogue (backward) when the product is staged; otherwise applied
+    as a separate pass first."""
+
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, x, weight, bias, drop=None):
         N.require_device(x, weight)
         x = x.contiguous()
         K = x.shape[-1]
@@ -162,10 +167,18 @@ class LinearFn(torch.autograd.Function):
         flops = 2.0 * M * Nout * K
         stage = compute_dtype() == BF16 and (
             flops >= _STAGE_FLOPS or (Nout % 8 != 0 and flops >= _STAGE_FLOPS_RAGGED))
+        fused_drop = drop is not None and stage and K % 8 == 0
+        if drop is not None and not fused_drop:        # materialise dropout(x) first
+            xd = torch.empty_like(x)
+            N.call('asr_dropout', N.ptr(x), N.ptr(xd), x.numel(), float(drop[0]), int(drop[1]),
+                   N.stream_handle(x.device))
+            x = xd
         # staged copies: x [M][Kp], weight [Np][Kp] (rows Nout.. and columns K.. zero)
         Kp, Np = ((K + 7) // 8 * 8, (Nout + 7) // 8 * 8) if stage else (K, Nout)
         if stage:
-            xo = _staged(x, M, K, Kp)
+            # fused_drop: K % 8 == 0, so Kp == K and the dropped copy is the operand
+            xo = (convert_rows_bf16(x, rowmap(K), M, K, drop=drop) if fused_drop else
+                  _staged(x, M, K, Kp))
             wo = torch.empty(Np, Kp, dtype=torch.bfloat16, device=x.device)
             N.call('asr_convert_rows_bf16_ld', N.ptr(weight), rowmap(K), Nout, K, Kp, N.ptr(wo),
                    N.stream_handle(x.device))
@@ -181,37 +194,41 @@ class LinearFn(torch.autograd.Function):
             run_gemm([p], x.device)
         ctx.save_for_backward(xo, wo)
         ctx.meta = (bias, stage, tuple(x.shape), weight)
+        ctx.drop = drop
         return y
 
     @staticmethod
     def backward(ctx, dy):
         xo, wo = ctx.saved_tensors
         bias, stage, xshape, weight = ctx.meta
+        drop = ctx.drop     # dropout's backward = its mask, applied by the dX epilogue
         dy = dy.contiguous()
         K = xshape[-1]
         Nout = weight.shape[0]
         M = dy.numel() // Nout
         dx = None
         if M == 0:
-            return torch.zeros(xshape, dtype=torch.float32, device=dy.device), None, None
+            return torch.zeros(xshape, dtype=torch.float32, device=dy.device), None, None, None
         Kp, Np = (xo.shape[-1], wo.shape[0]) if stage else (K, Nout)
         dyo = _staged(dy, M, Nout, Np) if stage else dy   # zero columns meet zero W rows
         probs = []
         if ctx.needs_input_grad[0]:
             dx = torch.empty(xshape, dtype=torch.float32, device=dy.device)
             probs.append(gemm_problem(operand(dyo, 0, rowmap(Np)), operand(wo, 1, rowmap(Kp)),
-                                      dx, rowmap(K), M, K, Np))
+                                      dx, rowmap(K), M, K, Np, drop=drop))
         gw = grad_buffer(weight)
         probs.append(gemm_problem(operand(dyo, 1, rowmap(Np)), operand(xo, 1, rowmap(Kp)), gw,
                                   rowmap(K), Nout, K, M, beta=1.0))
         run_gemm(probs, dy.device)
         if bias is not None:
             colsum_accumulate(dy.view(M, Nout), grad_buffer(bias))
-        return dx, None, None
+        return dx, None, None, None
 
 
-def linear(x, weight, bias=None):
-    return LinearFn.apply(x, weight, bias)
+def linear(x, weight, bias=None, drop=None):
+    """drop=(p, seed): y = dropout(x) W^T + b with dropout folded into the
+    product (LinearFn)."""
+    return LinearFn.apply(x, weight, bias, drop)
 
 
 class LinearExFn(torch.autograd.Function):

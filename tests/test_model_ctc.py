@@ -356,3 +356,48 @@ def test_gru_encoder_vs_oracle(dtype, cuda_dev):
         gw = prm.grad.cpu().numpy()
         scale = np.abs(ga).max() + 1e-6
         assert np.abs(gw - ga).max() / scale < tg, (k, np.abs(gw - ga).max(), scale)
+
+
+@pytest.mark.gpu
+def test_output_dropout_folded_into_head_bitwise(cuda_dev, monkeypatch):
+    """bf16 training with encoder dropout: the last BLSTM layer's output
+    dropout handed to the CTC head (LinearND input_drop: the mask applied in
+    the head's bf16 staging and its dX GEMM epilogue) and the inter-layer
+    dropouts folded into the next layer's staging give the same loss and
+    gradients, bit for bit, as separate asr_dropout passes (ASR_FUSE_DROPOUT=0)
+    under the same seed stream."""
+    from pytorch_end2end_speech_recognition_amd import native_ops
+    kw = dict(input_size=40, encoder_type='lstm', encoder_bidirectional=True,
+              encoder_num_units=64, encoder_num_proj=0, encoder_num_layers=2, fc_list=[],
+              dropout_input=0, dropout_encoder=0.3, num_classes=29, parameter_init=0.1,
+              subsample_list=[], subsample_type='drop')
+    rng = np.random.RandomState(3)
+    B, T = 8, 60
+    x_lens = np.sort(rng.randint(40, T + 1, B)).astype(np.int32)[::-1].copy()
+    x_lens[0] = T
+    y_lens = rng.randint(5, 15, B).astype(np.int32)
+    xs = rng.randn(B, T, 40).astype(np.float32)
+    ys = np.full((B, 15), -1, np.int32)
+    for b in range(B):
+        ys[b, :y_lens[b]] = rng.randint(0, 28, y_lens[b])
+    outs = []
+    native_ops.set_compute_dtype('bf16')
+    # stage the head's operands at this size too (the path the dropout folds into)
+    monkeypatch.setattr(native_ops, '_STAGE_FLOPS_RAGGED', 1.0)
+    try:
+        for fuse in ('1', '0'):
+            monkeypatch.setenv('ASR_FUSE_DROPOUT', fuse)
+            native_ops.manual_seed(1234)
+            model = _build(kw)
+            model.set_cuda()
+            model.zero_grad()
+            loss = model(xs, ys, x_lens, y_lens)
+            loss.backward()
+            torch.cuda.synchronize()
+            outs.append((loss.item(), model._flat_grad.clone()))
+    finally:
+        native_ops.set_compute_dtype('fp32')
+    (l1, g1), (l0, g0) = outs
+    assert l1 == l0, (l1, l0)
+    assert torch.equal(g1, g0)
+    assert g1.abs().sum().item() > 0
