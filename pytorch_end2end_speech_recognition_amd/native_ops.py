@@ -844,7 +844,11 @@ class BLSTMLayerFn(torch.autograd.Function):
         else:
             x_map = rowmap(Dsrc, stride_b=T_src * Dsrc, rows_per_b=T, t_mul=t_mul, t_add=t_add,
                            t_limit=T_src, perm=perm)
-        side_ent = _wgrad_side_stream(dev, B, H)
+        # the bottom layer's weight gradients have no recurrence left to run
+        # beside: they take the main stream and the full-size GEMM kernels (on
+        # the co-resident small tiles the 4x320 layer-0 dW_ih ran at 29 TF/s)
+        last_main = not ctx.next_rec and os.environ.get('ASR_WGRAD_LAST_MAIN', '1') != '0'
+        side_ent = None if last_main else _wgrad_side_stream(dev, B, H)
         if side_ent is None:
             _blstm_wgrad(dg_op, act, x_op, x_map, y_op, T, gbufs, dev)
             notify_grad_event('grads', gbufs)      # final on the compute stream
