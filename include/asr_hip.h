@@ -172,6 +172,9 @@ int asr_gemm_ws(const asr_gemm_t* problems, int nprob, int compute_dtype, void* 
  * their work-groups fit beside a persistent recurrence work-group on every CU
  * (weight gradients co-resident with the backward recurrence). */
 int asr_gemm_set_small_tiles(int on);
+/* asr_gemm_set_n64_kmode(1): products with N <= 64 (M >= 4096) whose B is
+ * K-major also take the 256 x 64 kernel (launches from this host thread). */
+int asr_gemm_set_n64_kmode(int on);
 
 /* Enqueue on `stream` a one-wave gate that releases once the NEXT persistent
  * backward recurrence (asr_lstm_backward*, any stream) has all its work-groups
@@ -577,6 +580,10 @@ int asr_conv_weight_unpack_acc(const float* packed, int Co, int Ci, float* dw, v
  * stay as the caller zeroed them) */
 int asr_conv_weight_pack_pad(const float* w, int Co, int Ci, int Cip, int mode, int out_dtype,
                              void* out, void* stream);
+/* The same from the transposed image packed_t [9 Cip][Co] (the weight
+ * gradient computed as X^T dZ, so that C_out is the product's narrow N). */
+int asr_conv_weight_unpack_acc_pad_t(const float* packed_t, int Co, int Ci, int Cip, float* dw,
+                                     void* stream);
 int asr_conv_weight_unpack_acc_pad(const float* packed, int Co, int Ci, int Cip, float* dw,
                                    void* stream);
 /* Direct 3x3 convolution (layers the tap-addressed GEMM cannot take: C_in = 1,

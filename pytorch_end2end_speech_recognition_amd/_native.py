@@ -46,6 +46,7 @@ SIGNATURES = {
     'asr_gemm_workspace_bytes': (c_size, [c_vp, c_int]),
     'asr_gemm_ws': (c_int, [c_vp, c_int, c_int, c_vp, c_size, c_vp]),
     'asr_gemm_set_small_tiles': (c_int, [c_int]),
+    'asr_gemm_set_n64_kmode': (c_int, [c_int]),
     'asr_lstm_wgrad_gate': (c_int, [c_vp]),
     'asr_colsum_workspace_bytes': (c_size, [c_int, c_int]),
     'asr_colsum_accumulate': (c_int, [c_vp, c_ll, c_int, c_int, c_float, c_vp, c_vp, c_vp, c_size,
@@ -116,6 +117,7 @@ SIGNATURES = {
     'asr_vgg_pad_input_ch': (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp]),
     'asr_conv_weight_pack_pad': (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp]),
     'asr_conv_weight_unpack_acc_pad': (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp]),
+    'asr_conv_weight_unpack_acc_pad_t': (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp]),
     'asr_conv_weight_unpack_acc': (c_int, [c_vp, c_int, c_int, c_vp, c_vp]),
     'asr_conv_direct_forward': (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp,
                                         c_vp, c_vp]),

@@ -697,6 +697,18 @@ __global__ void weight_unpack_acc(const float* __restrict__ pk, int Co, int Ci, 
   }
 }
 
+// dW [Co][Ci][3][3] += packed_t [9 Cip][Co] (the transposed mode-0 image)
+__global__ void weight_unpack_acc_t(const float* __restrict__ pk, int Co, int Ci, int Cip,
+                                    float* __restrict__ dw) {
+  const long long n = (long long)Co * Ci * 9;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int kw = (int)(i % 3), kh = (int)((i / 3) % 3);
+    const int ci = (int)((i / 9) % Ci), co = (int)(i / (9LL * Ci));
+    dw[i] += pk[((long long)(kw * 3 + kh) * Cip + ci) * Co + co];
+  }
+}
+
 inline int grid_for(long long n) {
   const long long b = (n + CT - 1) / CT;
   return (int)(b < 8192 ? (b > 0 ? b : 1) : 8192);
@@ -779,6 +791,17 @@ extern "C" int asr_conv_weight_pack_pad(const float* w, int Co, int Ci, int Cip,
 extern "C" int asr_conv_weight_unpack_acc(const float* packed, int Co, int Ci, float* dw,
                                           void* stream) {
   return asr_conv_weight_unpack_acc_pad(packed, Co, Ci, Ci, dw, stream);
+}
+
+extern "C" int asr_conv_weight_unpack_acc_pad_t(const float* packed_t, int Co, int Ci, int Cip,
+                                                float* dw, void* stream) {
+  ASR_REQUIRE(packed_t && dw && Co > 0 && Ci > 0 && Cip >= Ci, ASR_ERR_ARG,
+              "conv_weight_unpack_t: bad args");
+  const long long n = (long long)Co * Ci * 9;
+  hipLaunchKernelGGL(weight_unpack_acc_t, dim3(grid_for(n)), dim3(CT), 0, (hipStream_t)stream,
+                     packed_t, Co, Ci, Cip, dw);
+  ASR_LAUNCH_CHECK();
+  return ASR_OK;
 }
 
 extern "C" int asr_conv_weight_unpack_acc_pad(const float* packed, int Co, int Ci, int Cip,

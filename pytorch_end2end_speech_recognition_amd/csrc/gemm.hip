@@ -754,10 +754,13 @@ __global__ void __launch_bounds__(NT) gemm_bf16_fast(Params P) {
 // 128-row halves (own StageF states), the B tile as 64 rows (two DMAs per
 // wave); double-buffered, 80 KB of LDS (two work-groups per CU).
 constexpr int N64_BM = 256;
-constexpr int N64_STAGE = 2 * FTILE + FTILE / 2;   // A (32 KB) + B (8 KB)
+// stage bytes: A (32 KB) + B (R mode: 64 rows, 8 KB; K mode: the 128-column
+// k-row layout of the 128 x 128 kernel with columns 64.. zero, 16 KB)
+__host__ __device__ constexpr int n64_stage(int bmode) { return 2 * FTILE + (bmode ? FTILE : FTILE / 2); }
 
-template <int AMODE>
+template <int AMODE, int BMODE>
 __global__ void __launch_bounds__(NT) gemm_bf16_n64(Params P) {
+  constexpr int N64_STAGE = n64_stage(BMODE);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int zb = blockIdx.z / P.nprob, zp = blockIdx.z % P.nprob;
   Problem pr = P.p[zp];
@@ -803,11 +806,11 @@ __global__ void __launch_bounds__(NT) gemm_bf16_n64(Params P) {
     stagef_init<AMODE>(pr.a, sa0, tm, pr.M, kbeg, w, lane);
     stagef_init<AMODE>(pr.a, sa1, tm + 128, pr.M, kbeg, w, lane);
   }
-  if (pr.b.sf) stagef_init<0, 2>(pr.b, sb, tn, pr.N, kbeg, w, lane);
+  if (pr.b.sf) stagef_init<BMODE, BMODE ? 4 : 2>(pr.b, sb, tn, pr.N, kbeg, w, lane);
   auto stage = [&](char* st, int k0) {
     stage_any<AMODE>(pr.a, ra, sa0, st, tm, pr.M, k0, kend, w, lane);
     stage_any<AMODE>(pr.a, ra, sa1, st + FTILE, tm + 128, pr.M, k0, kend, w, lane);
-    stage_any<0, 2>(pr.b, rb, sb, st + 2 * FTILE, tn, pr.N, k0, kend, w, lane);
+    stage_any<BMODE, BMODE ? 4 : 2>(pr.b, rb, sb, st + 2 * FTILE, tn, pr.N, k0, kend, w, lane);
   };
   stage(smem, kbeg);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -822,7 +825,7 @@ __global__ void __launch_bounds__(NT) gemm_bf16_n64(Params P) {
       for (int i = 0; i < 4; ++i)   // waves 2, 3 read the second 128-row half
         fa[i] = frag_bf16<AMODE>(cur + (wr >> 7) * FTILE, (wr & 127) + 16 * i, kk, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) fb[j] = frag_bf16<0>(cur + 2 * FTILE, wc + 16 * j, kk, lane);
+      for (int j = 0; j < 4; ++j) fb[j] = frag_bf16<BMODE>(cur + 2 * FTILE, wc + 16 * j, kk, lane);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1874,15 +1877,19 @@ int split_target() {
 // run co-resident with the persistent backward recurrence (native_ops,
 // ASR_OVERLAP_WGRAD=2) must fit beside its work-group on every CU.
 thread_local int g_small_tiles = 0;
+thread_local int g_n64_kmode = 0;
 
 // Products with N <= 64 and many rows take the 256 x 64 kernel (B in R mode;
 // ASR_GEMM_N64=0 keeps them on the 128 x 128 kernel; read per launch).
-bool n64_ok(const asr_gemm_t* g, int nprob) {
+bool n64_ok(const asr_gemm_t* g, int nprob, int bmode) {
   if (g_small_tiles) return false;
   const char* e = getenv("ASR_GEMM_N64");
   if (e && e[0] == '0') return false;
-  for (int i = 0; i < nprob; ++i)
-    if (g[i].N > 64 || g[i].M < 4096) return false;
+  // K-mode B (its tile keeps the 128-column layout, 96 KB of LDS): opt-in per
+  // launch thread (asr_gemm_set_n64_kmode), used by the VGG weight gradients
+  if (bmode && !g_n64_kmode) return false;
+  for (int i = 0; i < nprob; ++i)   // many rows, or a long K that split-K spreads
+    if (g[i].N > 64 || (g[i].M < 4096 && g[i].K < 65536)) return false;
   return true;
 }
 
@@ -2044,15 +2051,22 @@ int gemm_launch_own(const asr_gemm_t* problems, int nprob, int compute_dtype, vo
     }
     hipLaunchKernelGGL(gemm_bf16_kk256, dim3(maxwg2, 1, nprob * maxb), dim3(NT),
                        (size_t)NST2 * 2 * FTILE2, s, P);
-  } else if ((fast == 0 || fast == 2) && n64_ok(problems, nprob)) {
+  } else if (fast >= 0 && n64_ok(problems, nprob, fast & 1)) {
     static bool attr64 = false;
     if (!attr64) {
-      bool ok = hipFuncSetAttribute((const void*)gemm_bf16_n64<0>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    2 * N64_STAGE) == hipSuccess;
-      ok &= hipFuncSetAttribute((const void*)gemm_bf16_n64<1>,
+      bool ok = true;
+      ok &= hipFuncSetAttribute((const void*)gemm_bf16_n64<0, 0>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
-                                2 * N64_STAGE) == hipSuccess;
+                                2 * n64_stage(0)) == hipSuccess;
+      ok &= hipFuncSetAttribute((const void*)gemm_bf16_n64<1, 0>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                2 * n64_stage(0)) == hipSuccess;
+      ok &= hipFuncSetAttribute((const void*)gemm_bf16_n64<0, 1>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                2 * n64_stage(1)) == hipSuccess;
+      ok &= hipFuncSetAttribute((const void*)gemm_bf16_n64<1, 1>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                2 * n64_stage(1)) == hipSuccess;
       ASR_REQUIRE(ok, ASR_ERR_HIP, "gemm: cannot raise the LDS limit of the 256x64 kernel");
       attr64 = true;
     }
@@ -2060,8 +2074,12 @@ int gemm_launch_own(const asr_gemm_t* problems, int nprob, int compute_dtype, vo
     for (int i = 0; i < nprob; ++i)
       maxwg64 = max(maxwg64, ceil_div(P.p[i].M, N64_BM) * max(1, P.p[i].ksplit));
     const dim3 g64(maxwg64, 1, nprob * maxb);
-    if (fast == 0) hipLaunchKernelGGL(gemm_bf16_n64<0>, g64, dim3(NT), 2 * N64_STAGE, s, P);
-    else hipLaunchKernelGGL(gemm_bf16_n64<1>, g64, dim3(NT), 2 * N64_STAGE, s, P);
+    switch (fast) {
+      case 0: hipLaunchKernelGGL((gemm_bf16_n64<0, 0>), g64, dim3(NT), 2 * n64_stage(0), s, P); break;
+      case 2: hipLaunchKernelGGL((gemm_bf16_n64<1, 0>), g64, dim3(NT), 2 * n64_stage(0), s, P); break;
+      case 1: hipLaunchKernelGGL((gemm_bf16_n64<0, 1>), g64, dim3(NT), 2 * n64_stage(1), s, P); break;
+      default: hipLaunchKernelGGL((gemm_bf16_n64<1, 1>), g64, dim3(NT), 2 * n64_stage(1), s, P); break;
+    }
   } else if (fast >= 0) {
     const int nst = g_small_tiles ? 2 : fast_stages();
     const size_t lds = (size_t)nst * 2 * FTILE;
@@ -2218,6 +2236,13 @@ using namespace asr;
 
 extern "C" int asr_gemm_set_small_tiles(int on) {
   g_small_tiles = on ? 1 : 0;
+  return ASR_OK;
+}
+
+// asr_gemm_set_n64_kmode(1): products with N <= 64 and a K-major B (the VGG
+// weight gradients computed transposed) take the 256 x 64 kernel too.
+extern "C" int asr_gemm_set_n64_kmode(int on) {
+  g_n64_kmode = on ? 1 : 0;
   return ASR_OK;
 }
 

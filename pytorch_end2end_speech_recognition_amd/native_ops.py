@@ -1602,13 +1602,29 @@ class VGGFn(torch.autograd.Function):
                        N.stream_handle(dev))
                 dnext, flat = dx, 0
                 continue
-            # dW image [Co][9 Ci] = dz^T X (taps on the output index), K = padded pixels
-            packed = torch.empty(Co, 9 * cCp, **f32)
-            run_gemm([gemm_problem(operand(dz, 1, rowmap(Co)),
-                                   _tap_operand(x_op, 1, cCp, cCp, cF + 2, 1), packed,
-                                   rowmap(9 * cCp), Co, 9 * cCp, npad)], dev)
-            N.call('asr_conv_weight_unpack_acc_pad', N.ptr(packed), Co, cC, cCp,
-                   N.ptr(grad_buffer(w)), N.stream_handle(dev))
+            if Co <= 64 and cd == BF16 and os.environ.get('ASR_VGG_DW_T', '0') == '1':
+                # transposed image [9 Ci][Co] = X^T dz: C_out becomes the narrow N
+                # of the 256 x 64 kernel (dz^T X puts C_out on half-empty 128-row
+                # tiles).  Opt-in: measured 0.27 ms / step SLOWER at vgg_hier (the
+                # K-major 256 x 64 tile needs 96 KB of LDS, one work-group per CU)
+                packed_t = torch.empty(9 * cCp, Co, **f32)
+                N.call('asr_gemm_set_n64_kmode', 1)
+                try:
+                    run_gemm([gemm_problem(_tap_operand(x_op, 1, cCp, cCp, cF + 2, 1),
+                                           operand(dz, 1, rowmap(Co)), packed_t, rowmap(Co),
+                                           9 * cCp, Co, npad)], dev)
+                finally:
+                    N.call('asr_gemm_set_n64_kmode', 0)
+                N.call('asr_conv_weight_unpack_acc_pad_t', N.ptr(packed_t), Co, cC, cCp,
+                       N.ptr(grad_buffer(w)), N.stream_handle(dev))
+            else:
+                # dW image [Co][9 Ci] = dz^T X (taps on the output index), K = padded pixels
+                packed = torch.empty(Co, 9 * cCp, **f32)
+                run_gemm([gemm_problem(operand(dz, 1, rowmap(Co)),
+                                       _tap_operand(x_op, 1, cCp, cCp, cF + 2, 1), packed,
+                                       rowmap(9 * cCp), Co, 9 * cCp, npad)], dev)
+                N.call('asr_conv_weight_unpack_acc_pad', N.ptr(packed), Co, cC, cCp,
+                       N.ptr(grad_buffer(w)), N.stream_handle(dev))
             if l == 0:
                 break
             # d input (padded rows of layer l's input) = dz (taps, mirrored) x W^T image

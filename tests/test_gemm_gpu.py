@@ -342,9 +342,10 @@ def test_dropout_epilogue_matches_separate_pass(M, N, K, dtype, kind, cuda_dev):
         ops.set_compute_dtype('fp32')
 
 
-@pytest.mark.parametrize('M,N,K,atrans', [(5000, 64, 576, 0), (4391, 40, 200, 0),
-                                          (6000, 64, 1152, 1), (4096, 17, 72, 1)])
-def test_n64_kernel_exact(M, N, K, atrans, cuda_dev, monkeypatch):
+@pytest.mark.parametrize('M,N,K,atrans,btrans', [(5000, 64, 576, 0, 0), (4391, 40, 200, 0, 0),
+                                                 (6000, 64, 1152, 1, 0), (4096, 17, 72, 1, 0),
+                                                 (576, 64, 70000, 1, 1), (4100, 48, 264, 0, 1)])
+def test_n64_kernel_exact(M, N, K, atrans, btrans, cuda_dev, monkeypatch):
     """The 256 x 64 kernel (products with N <= 64, B stored [N][K]: the
     64-channel VGG convolutions) on small-integer bf16 operands, exact in f32:
     both A layouts, N below 64, K not a multiple of the 64-deep k-tile, M not a
@@ -359,16 +360,22 @@ def test_n64_kernel_exact(M, N, K, atrans, cuda_dev, monkeypatch):
         bias = torch.from_numpy(rng.randint(-2, 3, N).astype(np.float32)).to(cuda_dev)
         c0 = rng.randint(-2, 3, (M, N)).astype(np.float32)
         a_st = a_np.T.copy() if atrans else a_np
+        b_st = b_np.T.copy() if btrans else b_np
         a = torch.from_numpy(a_st).to(torch.bfloat16).to(cuda_dev)
-        b = torch.from_numpy(b_np).to(torch.bfloat16).to(cuda_dev)
+        b = torch.from_numpy(b_st).to(torch.bfloat16).to(cuda_dev)
+        from pytorch_end2end_speech_recognition_amd import _native as NL
         outs = []
         for n64 in ('1', '0'):
             monkeypatch.setenv('ASR_GEMM_N64', n64)
             c = torch.from_numpy(c0).to(cuda_dev)
             p = ops.gemm_problem(ops.operand(a, atrans, ops.rowmap(M if atrans else K)),
-                                 ops.operand(b, 0, ops.rowmap(K)), c, ops.rowmap(N), M, N, K,
-                                 bias=bias, beta=1.0)
-            ops.run_gemm([p], cuda_dev)
+                                 ops.operand(b, btrans, ops.rowmap(N if btrans else K)), c,
+                                 ops.rowmap(N), M, N, K, bias=bias, beta=1.0)
+            NL.call('asr_gemm_set_n64_kmode', 1)
+            try:
+                ops.run_gemm([p], cuda_dev)
+            finally:
+                NL.call('asr_gemm_set_n64_kmode', 0)
             torch.cuda.synchronize()
             outs.append(c.cpu().numpy())
         ref = a_np.astype(np.float64) @ b_np.astype(np.float64).T + bias.cpu().numpy() + c0
