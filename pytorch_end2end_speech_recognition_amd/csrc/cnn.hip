@@ -229,10 +229,19 @@ struct VecF<4> {
 // scan order (freq outer, time inner; first maximum wins).  V channels per
 // thread (V = 4 when C % 4 == 0).
 template <int V>
-__global__ void post_fwd(const float* __restrict__ z, int B, int T, int F, int C, Pool pl,
-                         float* __restrict__ P, uint8_t* __restrict__ slot) {
+__global__ void __launch_bounds__(CT) post_fwd(const float* __restrict__ z, int B, int T, int F,
+                                               int C, Pool pl, float* __restrict__ P,
+                                               uint8_t* __restrict__ slot,
+                                               float* __restrict__ mpart) {
+  // mpart (nullable): per-block column sums of the P values written (the batch
+  // norm's mean pass folded in: threads tid, tid + CV, ... hold the same
+  // channels; the block's phases are combined in a fixed order)
+  __shared__ float red[CT * V];
   const unsigned CV = (unsigned)(C / V);
   const unsigned n = (unsigned)B * pl.To * pl.Fo * CV;
+  float macc[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) macc[j] = 0.f;
   for (unsigned e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
     const unsigned q = e / CV;
     const int c = (int)(e - q * CV) * V;
@@ -242,7 +251,10 @@ __global__ void post_fwd(const float* __restrict__ z, int B, int T, int F, int C
     if (!pl.pt) {
       best.load(z + pad_row(px.b, px.to, px.fo, T, F) * C + c);
 #pragma unroll
-      for (int j = 0; j < V; ++j) best.v[j] = fmaxf(best.v[j], 0.f);
+      for (int j = 0; j < V; ++j) {
+        best.v[j] = fmaxf(best.v[j], 0.f);
+        macc[j] += best.v[j];
+      }
       best.store(P + i);
       continue;
     }
@@ -267,9 +279,23 @@ __global__ void post_fwd(const float* __restrict__ z, int B, int T, int F, int C
         }
       }
     }
+#pragma unroll
+    for (int j = 0; j < V; ++j) macc[j] += best.v[j];
     best.store(P + i);
 #pragma unroll
     for (int j = 0; j < V; ++j) slot[i + j] = (uint8_t)bs[j];
+  }
+  if (mpart) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < V; ++j) red[tid * V + j] = macc[j];
+    __syncthreads();
+    for (int cc = tid; cc < C; cc += CT) {
+      const int g2 = cc / V, j = cc % V;
+      float t = 0.f;
+      for (int k = g2; k < CT; k += (int)CV) t += red[k * V + j];
+      mpart[(long long)blockIdx.x * C + cc] = t;
+    }
   }
 }
 
@@ -956,12 +982,26 @@ extern "C" int asr_vgg_block_forward(const float* z, int B, int T, int F, int C,
   ASR_REQUIRE((long long)B * (T + 2) * (F + 2) * C < (1LL << 31), ASR_ERR_UNSUPPORTED,
               "vgg_block_forward: layer too large for 32-bit element indices");
   const bool v4 = C % 4 == 0;
+  // batch-norm mean folded into the pool pass: per-block sums into the
+  // workspace's post_bwd partial region (unused in the forward)
+  const char* fm = getenv("ASR_VGG_FUSED_MEAN");
+  const bool fused_mean = gamma && training && v4 && workspace && !(fm && fm[0] == '0') &&
+                          ws_bytes >= asr_vgg_block_workspace_bytes(B, pl.To, pl.Fo, C);
+  float* mpart = nullptr;
+  if (fused_mean) {
+    const long long per = rows_per_chunk(nr);
+    const long long nchunk = (nr + per - 1) / per;
+    mpart = (float*)workspace + (size_t)(nchunk * 2 + 4) * C;
+  }
+  // fused: at most 1024 blocks, so the ordered partial sum (one thread per
+  // column phase) stays short -- 8192 partials took 1 ms / step at vgg_hier
+  const int fgrid = fused_mean ? std::min(post_grid(nr, C), 1024) : post_grid(nr, C);
   if (v4)
-    hipLaunchKernelGGL(post_fwd<4>, dim3(grid_for(nr * C / 4)), dim3(CT), 0, s, z, B, T, F, C, pl,
-                       P, slot);
+    hipLaunchKernelGGL(post_fwd<4>, dim3(fgrid), dim3(CT), 0, s, z, B, T, F, C, pl, P, slot,
+                       mpart);
   else
-    hipLaunchKernelGGL(post_fwd<1>, dim3(grid_for(nr * C)), dim3(CT), 0, s, z, B, T, F, C, pl, P,
-                       slot);
+    hipLaunchKernelGGL(post_fwd<1>, dim3(post_grid(nr, C)), dim3(CT), 0, s, z, B, T, F, C, pl, P,
+                       slot, (float*)nullptr);
   ASR_LAUNCH_CHECK();
   Affine af{nullptr, nullptr, nullptr, nullptr, drop, seed};
   if (gamma) {
@@ -974,10 +1014,15 @@ extern "C" int asr_vgg_block_forward(const float* z, int B, int T, int F, int C,
       const int nchunk = (int)((nr + per - 1) / per);
       float* part = (float*)workspace;
       float* m2 = part + (size_t)nchunk * C;
-      hipLaunchKernelGGL(col_moment, dim3(nchunk), dim3(CT), 0, s, P, nr, C, per, nullptr, 0,
-                         part);
-      hipLaunchKernelGGL(sum_partials, dim3((C + 63) / 64), dim3(CT), 0, s, part, nchunk, C,
-                         1.f / (float)nr, bn_mean);
+      if (fused_mean) {
+        hipLaunchKernelGGL(sum_partials, dim3((C + 63) / 64), dim3(CT), 0, s, mpart, fgrid, C,
+                           1.f / (float)nr, bn_mean);
+      } else {
+        hipLaunchKernelGGL(col_moment, dim3(nchunk), dim3(CT), 0, s, P, nr, C, per, nullptr, 0,
+                           part);
+        hipLaunchKernelGGL(sum_partials, dim3((C + 63) / 64), dim3(CT), 0, s, part, nchunk, C,
+                           1.f / (float)nr, bn_mean);
+      }
       hipLaunchKernelGGL(col_moment, dim3(nchunk), dim3(CT), 0, s, P, nr, C, per, bn_mean, 1,
                          part);
       hipLaunchKernelGGL(sum_partials, dim3((C + 63) / 64), dim3(CT), 0, s, part, nchunk, C,
