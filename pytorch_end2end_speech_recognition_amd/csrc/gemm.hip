@@ -2096,6 +2096,20 @@ int gemm_launch_own(const asr_gemm_t* problems, int nprob, int compute_dtype, vo
 #undef ASR_FAST
     }
   } else if (compute_dtype == ASR_DT_BF16) {
+    static bool warned = false;   // a bf16-mode product of real size on the slow path: say so once
+    if (!warned && !getenv("ASR_GEMM_DEBUG")) {
+      for (int i = 0; i < nprob; ++i) {
+        const double fl = 2.0 * problems[i].M * problems[i].N * problems[i].K * problems[i].batch;
+        if (fl >= 32e6) {
+          warned = true;
+          fprintf(stderr, "[asr_gemm] warning: a bf16-mode product (M=%d N=%d K=%d batch=%d) runs "
+                  "on the generic register-staged kernel, not the LDS-DMA fast kernels "
+                  "(ASR_GEMM_DEBUG=1 lists every such product)\n", problems[i].M, problems[i].N,
+                  problems[i].K, problems[i].batch);
+          break;
+        }
+      }
+    }
     if (getenv("ASR_GEMM_DEBUG"))   // which bf16-mode products miss the fast kernels
       for (int i = 0; i < nprob; ++i)
         fprintf(stderr, "[asr_gemm generic] M=%d N=%d K=%d batch=%d a(dt=%d tr=%d tap=%d perm=%d) "

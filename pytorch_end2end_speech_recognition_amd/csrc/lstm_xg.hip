@@ -77,7 +77,24 @@ constexpr size_t XG_PIN_BWD = 140 * 1024;
 size_t xg_pin_bwd() {
   const char* e = getenv("ASR_XG_PIN_BWD_KB");
   const int kb = e ? atoi(e) : 0;
+  static bool warned = false;
+  if (e && !(kb > 80 && kb <= 160) && !warned) {
+    warned = true;
+    fprintf(stderr, "[lstm_xg] warning: ASR_XG_PIN_BWD_KB=%s outside (80, 160]; using %d KB\n", e,
+            (int)(XG_PIN_BWD / 1024));
+  }
   return (kb > 80 && kb <= 160) ? (size_t)kb * 1024 : XG_PIN_BWD;
+}
+
+// The backward's pin leaves no room for the kernel's static LDS: the layer
+// would silently take the slower counter-form recurrence -- say so once.
+static void xg_warn_pin_unfit(size_t pin) {
+  static bool warned = false;
+  if (warned) return;
+  warned = true;
+  fprintf(stderr, "[lstm_xg] warning: backward LDS pin %zu KB + static LDS exceeds the CU's "
+          "160 KB; the tagged-granule backward recurrence is skipped and the counter-form "
+          "recurrence runs instead (ASR_XG_PIN_BWD_KB <= 150 keeps it)\n", pin / 1024);
 }
 constexpr unsigned AUX_SC1_VOL = 16u | (1u << 31);  // sc1; volatile (never hoisted from a spin)
 constexpr unsigned AUX_SC1 = 16u;
@@ -1185,7 +1202,10 @@ int lstm_bwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* wh
   const int st16 = (s16 && s16[0] == '0') ? 0 : 1;
 #define ASR_XGB(RR, M)                                                                          \
   do {                                                                                          \
-    if (!xg_fits(lstm_bwd_xg<RR, M>, 512 + RR * XU, pin)) return 0;                               \
+    if (!xg_fits(lstm_bwd_xg<RR, M>, 512 + RR * XU, pin)) {                                     \
+      if (pin != XG_PIN_BWD) xg_warn_pin_unfit(pin);                                             \
+      return 0;                                                                                 \
+    }                                                                                           \
     if (dry) return 1;                                                                          \
     if (hipMemsetAsync(ws, 0, lstm_xg_bwd_bytes(B, H), s) != hipSuccess) return -1;             \
     xg_trace_setup(s);             \

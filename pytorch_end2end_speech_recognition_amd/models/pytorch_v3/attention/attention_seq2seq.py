@@ -23,7 +23,7 @@ import numpy as np
 import torch
 
 from .... import native_ops as ops
-from ..base import ModelBase
+from ..base import ModelBase, check_recurrences
 from ..linear import LinearND, Embedding, Embedding_LS
 from ..encoders.load_encoder import load
 from .rnn_decoder import RNNDecoder
@@ -237,6 +237,7 @@ class AttentionSeq2seq(ModelBase):
             loss = loss + self.compute_ctc_loss(enc_out, ys_ctc, enc_lens_d, yl,
                                                 scale=self.ctc_loss_weight)
         if is_eval:
+            check_recurrences(self)
             return float(loss.item())
         self._step += 1
         if self.ss_prob > 0:
@@ -475,6 +476,7 @@ class AttentionSeq2seq(ModelBase):
         xs_d = self.np2var(xs, dtype='float')
         enc_out, enc_lens_d, _ = self._encode(xs_d, x_lens)
         logits = self.fc_ctc_0(enc_out)
+        check_recurrences(self)
         hyps = self._decode_ctc_greedy_np(logits, enc_lens_d)
         best = np.array([h - 1 for h in hyps] + [None], dtype=object)[:-1]
         return best, self.encoder.last_perm_np.copy()
@@ -495,6 +497,7 @@ class AttentionSeq2seq(ModelBase):
             best_hyps, aw = self._decode_infer_beam(enc_out, self.encoder.last_lens_np, beam_width,
                                                     max_decode_len, min_decode_len,
                                                     length_penalty, coverage_penalty, dir=dir)
+        check_recurrences(self)
         return best_hyps, aw, self.encoder.last_perm_np.copy()
 
     def _infer_step(self, task, dir, t, y_emb, st, enc, enc_a, lens):

@@ -24,6 +24,7 @@ the HIP CTC kernel.
 import numpy as np
 
 from .attention_seq2seq import AttentionSeq2seq
+from ..base import check_recurrences
 from .attention_layer import AttentionMechanism
 from .rnn_decoder import RNNDecoder
 from ..encoders.load_encoder import load
@@ -213,6 +214,7 @@ class HierarchicalAttentionSeq2seq(AttentionSeq2seq):
             loss = loss + ctc_loss_sub
         second = loss_sub if self.sub_loss_weight > self.ctc_loss_weight_sub else ctc_loss_sub
         if is_eval:
+            check_recurrences(self)
             return (float(loss.item()), float(loss_main.item()),
                     float(second.item()) if second is not None else 0.0)
         self._step += 1
@@ -243,4 +245,5 @@ class HierarchicalAttentionSeq2seq(AttentionSeq2seq):
                 hyps, aw = self._decode_infer_beam(enc, lens_np, beam_width, max_decode_len,
                                                    min_decode_len, length_penalty,
                                                    coverage_penalty, task=task_index)
+            check_recurrences(self)
             return hyps, aw, self.encoder.last_perm_np.copy()

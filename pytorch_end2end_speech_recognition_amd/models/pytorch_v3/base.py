@@ -31,6 +31,24 @@ OPTIMIZER_KINDS = {'adam': 0, 'sgd': 1, 'momentum': 2, 'nesterov': 3}
 TORCH_ONLY = ('adadelta', 'adagrad', 'rmsprop')
 
 
+def resolve_pending_losses(model):
+    """Read back a train_step(..., sync=False) still in flight, so a skipped
+    last step has undone its optimizer step count before anyone records it."""
+    pend = getattr(model, '_pending_losses', None)
+    if pend is not None:
+        pend.value()
+
+
+def check_recurrences(model):
+    """Eval / decode entry points: a persistent recurrence that gave up its
+    bounded wait during this pass left invalid outputs -- raise instead of
+    returning them (and the status words are consumed here, so the next
+    train_step's guard does not skip a healthy batch for it)."""
+    if getattr(model, 'device', None) is not None and model.device.type == 'cuda':
+        from ... import native_ops
+        native_ops.raise_if_recurrence_failed(model.device)
+
+
 class ModelBase(nn.Module):
     """Base class of CTC / AttentionSeq2seq (reference base.py:36)."""
 
@@ -240,6 +258,7 @@ class ModelBase(nn.Module):
         if remove_old_checkpoints:
             for path in glob(join(save_path, 'model.epoch-*')):
                 os.remove(path)
+        resolve_pending_losses(self)
         sd = {k: v.detach().cpu().clone() for k, v in self.state_dict().items()}
         checkpoint = {'state_dict': sd, 'optimizer': self.optimizer.state_dict(), 'epoch': epoch,
                       'step': step, 'lr': lr, 'metric_dev_best': metric_dev_best}
@@ -382,6 +401,7 @@ class FlatOptimizer(torch.optim.Optimizer):
         save_checkpoint stores, base.py:232-264): per-parameter 'step',
         'exp_avg', 'exp_avg_sq' (Adam) or 'momentum_buffer' (momentum /
         nesterov), views of the flat state buffers, and one param group."""
+        resolve_pending_losses(self.model)   # a skipped last step undoes its count first
         g = self.param_groups[0]
         state = {}
         for i, p, o in self._param_slices():

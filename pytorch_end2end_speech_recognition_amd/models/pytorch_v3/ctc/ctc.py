@@ -17,7 +17,7 @@ import numpy as np
 import torch
 
 from .... import native_ops as ops
-from ..base import ModelBase
+from ..base import ModelBase, check_recurrences
 from ..linear import LinearND
 from ..encoders.load_encoder import load
 from ..criterion import cross_entropy_label_smoothing
@@ -116,6 +116,7 @@ class CTC(ModelBase):
 
         loss = self._ctc_term(logits, out_lens_d, ys, y_lens, self.encoder.last_perm_np, B)
         if is_eval:
+            check_recurrences(self)
             return float(loss.item())
         return loss
 
@@ -172,6 +173,7 @@ class CTC(ModelBase):
                                       'the training hot path (SURVEY §2 #12)')
         xs_d = self.np2var(xs, dtype='float')
         logits, out_lens_d, perm_d = self._encode(xs_d, x_lens)
+        check_recurrences(self)
         best_hyps = self._decode_greedy_np(logits, out_lens_d)
         best_hyps = np.array([h - 1 for h in best_hyps] + [None], dtype=object)[:-1]
         return best_hyps, None, self.encoder.last_perm_np.copy()
@@ -184,6 +186,7 @@ class CTC(ModelBase):
             raise NotImplementedError
         xs_d = self.np2var(xs, dtype='float')
         logits, out_lens_d, perm_d = self._encode(xs_d, x_lens)
+        check_recurrences(self)
         probs = ops.softmax(logits * (1.0 / temperature))
         return self.var2np(probs), self.encoder.last_lens_np.copy(), \
             self.encoder.last_perm_np.copy()

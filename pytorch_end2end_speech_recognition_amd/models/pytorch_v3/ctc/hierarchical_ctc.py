@@ -15,6 +15,7 @@ returns (loss, loss_main, loss_sub) with
 import numpy as np
 
 from .ctc import CTC
+from ..base import check_recurrences
 from ..linear import LinearND
 from ..encoders.load_encoder import load
 
@@ -115,5 +116,6 @@ class HierarchicalCTC(CTC):
                                   B) * self.sub_loss_weight
         loss = loss_main + loss_sub
         if is_eval:
+            check_recurrences(self)
             return float(loss.item()), float(loss_main.item()), float(loss_sub.item())
         return loss, loss_main, loss_sub

@@ -1050,6 +1050,18 @@ def _join_side_wgrads(dev, notify=True):
     del _side_pending[:]
 
 
+def discard_side_wgrads():
+    """After a backward that raised: make each compute stream wait for the
+    side-stream weight gradients still pending (so a later zero of the flat
+    gradient cannot race a beta = 1 accumulation) and forget them WITHOUT
+    notifying 'grads' (their values belong to the skipped batch; a bucket
+    hook must not see them as ready).  The end-of-backward join callback of
+    a failed backward never runs, so nothing else would clear them."""
+    for side, _gbufs, main in _side_pending:
+        main.wait_stream(side)
+    del _side_pending[:]
+
+
 def _num_cus(dev):
     return torch.cuda.get_device_properties(dev).multi_processor_count
 

@@ -74,6 +74,9 @@ class GradBuckets(object):
 
     # ---------------------------------------------------------------- hooks
     def __enter__(self):
+        # weight gradients left pending by an earlier failed backward must not
+        # be reported into this step's buckets
+        native_ops.discard_side_wgrads()
         native_ops.set_grad_ready_hook(self._on_event)
         return self
 

@@ -139,6 +139,14 @@ def _step(model, forward, clip_grad_norm, n_losses, grad_scale, sync=True):
     host sync before the optimizer; the host reads the guard with the loss."""
     ok = 1
     world = _world()
+    if model.device.type == 'cuda':
+        from ... import native_ops
+        # weight gradients a failed backward outside train_step left pending
+        # are joined and forgotten; status words set outside a training step
+        # (an eval pass the caller did not check) are dropped, so the guard
+        # below covers only this step's own recurrences
+        native_ops.discard_side_wgrads()
+        native_ops.recurrence_status(model.device)
     buckets = GradBuckets.for_model(model, grad_scale) if world > 1 else None
     try:
         # ModelBase.zero_grad zeroes the flat gradient and re-binds every
@@ -155,6 +163,12 @@ def _step(model, forward, clip_grad_norm, n_losses, grad_scale, sync=True):
         logger.warning('!!!Skip mini-batch!!! %s' % e)
         ok = 0
         losses = None
+        if model.device.type == 'cuda':
+            # side-stream weight gradients of the failed backward: the zero of
+            # the flat gradient (skip path / next step) must wait for them, and
+            # no bucket may report them ready
+            from ... import native_ops
+            native_ops.discard_side_wgrads()
     if buckets is not None:
         buckets.finish(ok)                # remainder + wait; never skipped, so every
     guard = _status_guard(model)          # rank pairs the others' collectives

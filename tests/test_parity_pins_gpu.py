@@ -1,0 +1,244 @@
+"""Reference-anchored bounds for the bench-path kernels that round 2 only
+checked loosely (VERDICT r02 "What's weak" #1):
+
+* the VGG front-end at the PRODUCTION channel plan [64, 64, 128, 128] with
+  BatchNorm and a ceil-mode pool (encoders/cnn.py:124-165), fp32 mode, against
+  the oracle restatement (pinned to the reference's fixtures by
+  test_vgg_oracle_matches_golden): loss 1e-4, every gradient 2e-3;
+* the first layer's direct stencil (csrc/cnn.hip conv3x3_c1_fwd) bit-equal to
+  the tap-addressed GEMM it replaces, on integer operands where both are exact
+  (ASR_VGG_C1_DIRECT=0 selects the GEMM);
+* the full-resolution pool / ReLU / BN backward (post_bwd_full) bit-equal to
+  the gather form (ASR_VGG_POST_FULL=0);
+* the bf16 bench kernels against float64 where the arithmetic does not
+  amplify rounding: the persistent attention decoder passes at the production
+  attention shape with contracting recurrent weights (uniform +-0.03 W_hh in
+  the encoder and the decoder LSTM), and the bf16 VGG front-end -- relative
+  L2 error of every gradient <= 1e-2 (the same method test_recurrence_full.py
+  applies to the recurrence).
+"""
+import ctypes
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import asr_ref
+
+VGG_PROD = dict(encoder_type='lstm', encoder_bidirectional=True, encoder_num_units=32,
+                encoder_num_proj=0, encoder_num_layers=2, fc_list=[], dropout_input=0,
+                dropout_encoder=0, num_classes=6, parameter_init=0.1, subsample_list=[],
+                subsample_type='drop', conv_channels=[64, 64, 128, 128],
+                conv_kernel_sizes=[[3, 3]] * 4, conv_strides=[[1, 1]] * 4,
+                poolings=[[], [2, 2], [], [2, 2]], activation='relu', batch_norm=True)
+
+
+def _ctc(kw):
+    from pytorch_end2end_speech_recognition_amd.models.pytorch_v3.ctc.ctc import CTC
+    torch.manual_seed(1623)
+    return CTC(**kw)
+
+
+def _vgg_cfg(kw):
+    return dict(num_layers=kw['encoder_num_layers'], subsample_list=kw['subsample_list'],
+                fc_list=kw['fc_list'], conv_channels=kw['conv_channels'],
+                poolings=kw['poolings'], batch_norm=kw['batch_norm'])
+
+
+def _trainable(p):
+    return {k: v for k, v in p.items() if v.is_floating_point() and 'running' not in k}
+
+
+def _vgg_batch(F, B=4, T=61, seed=9, integer=False):
+    rng = np.random.RandomState(seed)
+    x_lens = np.array([T, T - 8, T - 19, T - 30][:B], np.int32)
+    y_lens = np.array([4, 3, 3, 2][:B], np.int32)
+    xs = (rng.randint(-3, 4, (B, T, F)) if integer else rng.randn(B, T, F)).astype(np.float32)
+    for b in range(B):
+        xs[b, x_lens[b]:] = 0
+    ys = np.full((B, 4), -1, np.int32)
+    for b in range(B):
+        ys[b, :y_lens[b]] = rng.randint(0, 6, y_lens[b])
+    return xs, ys, x_lens, y_lens
+
+
+def _gpu_grads(model, batch, prec):
+    from pytorch_end2end_speech_recognition_amd import native_ops
+    native_ops.set_compute_dtype(prec)
+    try:
+        model.zero_grad()
+        loss = model(*batch)
+        loss.backward()
+        torch.cuda.synchronize()
+    finally:
+        native_ops.set_compute_dtype('fp32')
+    return float(loss.item()), {k: p.grad.detach().cpu().numpy().copy()
+                                for k, p in model.named_parameters()}
+
+
+def _oracle(sd, cfg_fn, batch, dtype=torch.float32, attention=None):
+    p = {k: (v.to(dtype) if v.is_floating_point() else v).clone() for k, v in sd.items()}
+    for v in _trainable(p).values():
+        v.requires_grad_(True)
+    if attention is not None:
+        loss = asr_ref.attention_model_loss(p, attention, *batch)
+    else:
+        loss, _, _, _ = asr_ref.ctc_model_loss(p, cfg_fn, *batch)
+    loss.backward()
+    return float(loss), {k: v.grad.numpy().astype(np.float64) for k, v in _trainable(p).items()
+                         if v.grad is not None}
+
+
+def _rel_l2(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / (np.linalg.norm(b) + 1e-30))
+
+
+@pytest.mark.gpu
+def test_vgg_prod_channels_fp32_vs_oracle(cuda_dev):
+    kw = dict(VGG_PROD, input_size=40)
+    model = _ctc(kw)
+    sd = {k: v.clone() for k, v in model.state_dict().items()}
+    batch = _vgg_batch(40)
+    ref_loss, ref_g = _oracle(sd, _vgg_cfg(kw), batch)
+    model.set_cuda()
+    loss, g = _gpu_grads(model, batch, 'fp32')
+    np.testing.assert_allclose(loss, ref_loss, rtol=1e-4)
+    for k, ga in ref_g.items():
+        scale = np.abs(ga).max() + 1e-12
+        err = np.abs(g[k] - ga).max() / scale
+        assert err <= 2e-3, (k, err)
+
+
+def _with_env(monkeypatch, name, value, model, batch, prec):
+    monkeypatch.setenv(name, value)
+    try:
+        return _gpu_grads(model, batch, prec)
+    finally:
+        monkeypatch.delenv(name)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('prec', ['bf16', 'fp32'])
+def test_vgg_c1_direct_stencil_equals_tap_gemm(prec, cuda_dev, monkeypatch):
+    """Integer input features and integer first-layer weights / bias: every
+    product and partial sum of layer 0 is exact in both the direct stencil
+    and the (bf16 or f32) MFMA GEMM, so z -- and with it the loss and every
+    gradient downstream -- must be bit-equal."""
+    kw = dict(VGG_PROD, input_size=40)
+    model = _ctc(kw)
+    rng = np.random.RandomState(3)
+    sd = model.state_dict()
+    wkey = 'encoder.conv.layers.0.weight'           # [64, 1, 3, 3]; BN: no conv bias
+    with torch.no_grad():
+        w = sd[wkey]
+        w.copy_(torch.from_numpy(rng.randint(-2, 3, tuple(w.shape)).astype(np.float32)))
+    model.set_cuda()
+    batch = _vgg_batch(40, integer=True, seed=4)
+    l1, g1 = _with_env(monkeypatch, 'ASR_VGG_C1_DIRECT', '1', model, batch, prec)
+    l0, g0 = _with_env(monkeypatch, 'ASR_VGG_C1_DIRECT', '0', model, batch, prec)
+    assert l1 == l0
+    for k in g0:
+        np.testing.assert_array_equal(g1[k], g0[k], err_msg=k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('prec', ['bf16', 'fp32'])
+def test_vgg_post_bwd_full_equals_gather_form(prec, cuda_dev, monkeypatch):
+    kw = dict(VGG_PROD, input_size=40)
+    model = _ctc(kw)
+    model.set_cuda()
+    batch = _vgg_batch(40, seed=5)
+    l1, g1 = _with_env(monkeypatch, 'ASR_VGG_POST_FULL', '1', model, batch, prec)
+    l0, g0 = _with_env(monkeypatch, 'ASR_VGG_POST_FULL', '0', model, batch, prec)
+    assert l1 == l0
+    for k in g0:
+        np.testing.assert_array_equal(g1[k], g0[k], err_msg=k)
+
+
+@pytest.mark.gpu
+def test_vgg_bf16_vs_float64(cuda_dev):
+    """bf16 VGG front-end (conv3x3_c1_fwd, gemm_bf16_n64 / fast tap GEMMs,
+    post_bwd_full, fused BN moments) vs the float64 oracle at the production
+    channel plan.  B = 8 utterances x 101 frames x 40 bins, so BatchNorm's
+    per-channel mean subtraction averages over >= 4000 pixels per channel."""
+    kw = dict(VGG_PROD, input_size=40)
+    model = _ctc(kw)
+    sd = {k: v.clone() for k, v in model.state_dict().items()}
+    rng = np.random.RandomState(21)
+    B, T = 8, 101
+    x_lens = np.sort(rng.randint(70, T + 1, B))[::-1].astype(np.int32)
+    x_lens[0] = T
+    y_lens = rng.randint(2, 5, B).astype(np.int32)
+    xs = rng.randn(B, T, 40).astype(np.float32)
+    for b in range(B):
+        xs[b, x_lens[b]:] = 0
+    ys = np.full((B, 4), -1, np.int32)
+    for b in range(B):
+        ys[b, :y_lens[b]] = rng.randint(0, 6, y_lens[b])
+    batch = (xs, ys, x_lens, y_lens)
+    ref_loss, ref_g = _oracle(sd, _vgg_cfg(kw), batch, torch.float64)
+    model.set_cuda()
+    loss, g = _gpu_grads(model, batch, 'bf16')
+    errs = {k: _rel_l2(g[k], ga) for k, ga in ref_g.items()}
+    worst = sorted(errs.items(), key=lambda kv: -kv[1])[:6]
+    print('\nbf16 VGG vs float64: loss %.2e, worst grads %s' % (
+        abs(loss - ref_loss) / abs(ref_loss), ', '.join('%s %.2e' % kv for kv in worst)))
+    assert abs(loss - ref_loss) / abs(ref_loss) <= 1e-2
+    for k, e in errs.items():
+        assert e <= 1e-2, (k, e)
+
+
+def _small_whh(sd, scale=0.03, seed=1623):
+    g = torch.Generator().manual_seed(seed)
+    out = {k: v.clone() for k, v in sd.items()}
+    for k in sorted(sd):
+        if 'weight_hh' in k:
+            out[k] = (torch.rand(sd[k].shape, generator=g, dtype=torch.float64) * 2 - 1).mul(
+                scale).float()
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name', ['model_att_prod', 'model_att_prod_hybrid'])
+def test_attention_persistent_bf16_contracting_vs_float64(name, cuda_dev):
+    """The bf16 persistent decoder passes (attdec_fwd_persist /
+    attdec_bwd_persist) plus the bf16 encoder at the production attention
+    shape of configs[2]/[3], with contracting recurrent weights, against the
+    oracle in float64: loss 1e-3, every gradient <= 1e-2 relative L2.  The
+    launch records prove both passes ran persistent with the C = 10 geometry."""
+    from pytorch_end2end_speech_recognition_amd import _native as N
+    from pytorch_end2end_speech_recognition_amd import native_ops
+    from pytorch_end2end_speech_recognition_amd.models.pytorch_v3.attention.attention_seq2seq \
+        import AttentionSeq2seq
+    d = golden(name)
+    kw = json.loads(str(d['kwargs']))
+    torch.manual_seed(1623)
+    model = AttentionSeq2seq(**kw)
+    sd = _small_whh(model.state_dict())
+    model.load_state_dict(sd)
+    batch = (d['xs'], d['ys'], d['x_lens'], d['y_lens'])
+    ref_loss, ref_g = _oracle(sd, None, batch, torch.float64, attention=kw)
+    model.set_cuda()
+    native_ops.set_compute_dtype('bf16')
+    try:
+        model.zero_grad()
+        loss = model(*batch)
+        loss.backward()
+        torch.cuda.synchronize()
+    finally:
+        native_ops.set_compute_dtype('fp32')
+    flag = (ctypes.c_int * 2)()
+    N.call('asr_attdec_persist_last', ctypes.cast(flag, ctypes.c_void_p))
+    assert list(flag) == [1, 1], list(flag)
+    g = {k: p.grad.detach().cpu().numpy() for k, p in model.named_parameters()}
+    errs = {k: _rel_l2(g[k], ga) for k, ga in ref_g.items()}
+    worst = sorted(errs.items(), key=lambda kv: -kv[1])[:6]
+    lerr = abs(float(loss.item()) - ref_loss) / abs(ref_loss)
+    print('\nbf16 attention (contracting) vs float64: loss %.2e, worst grads %s' % (
+        lerr, ', '.join('%s %.2e' % kv for kv in worst)))
+    assert lerr <= 1e-3
+    for k, e in errs.items():
+        assert e <= 1e-2, (k, e)
