@@ -155,6 +155,22 @@ def roofline_report(args, p, mean_us, launches, mean_work, workload):
         fwd_pass_flops += T * 2 * B * 8 * H * din_avg
         fwd_pass_bytes = (T * 2 * cell * (fwd_cell - 4 * 4) + T * B * din_avg * 2 + w_hh +
                           8 * H * din_avg * 2)
+    # attention decoder passes (one persistent launch each): bytes per launch
+    # recorded by the library ((A + E + 2) * 4 * T' per decoder
+    # step and utterance); flops from the same launch's B * S decoder steps:
+    # the LSTMCell [4D x (E + D)], W_dec h [A x D] and per frame the location
+    # conv (C x K), W_conv f (A x C), V tanh (A) and the context (E); the
+    # backward does twice the forward's multiply-adds
+    att_flops = [0.0, 0.0]
+    if p.get('attention_dim'):
+        A, D = p['attention_dim'], p['decoder_num_units']
+        E = 2 * H
+        C, K = p['attention_conv_num_channels'], p['attention_conv_width']
+        Tq = T_l[-1] // 2 if (p.get('subsample_list') or [False])[-1] else T_l[-1]
+        for i in (0, 1):
+            bs = mean_work[7 + i] / ((A + E + 2) * 4.0 * Tq) if mean_work[7 + i] else 0.0
+            mac = 4 * D * (E + D) + A * D + Tq * (A * C + C * K + A + E)
+            att_flops[i] = 2.0 * bs * mac * (1 if i == 0 else 2)
     kinds = [
         ('lstm_fwd_step', 'mfma', 2 * cell * fwd_cell + w_hh, flops_step),
         ('lstm_bwd_step', 'mfma', 2 * cell * bwd_cell + w_hh, flops_step),
@@ -163,6 +179,8 @@ def roofline_report(args, p, mean_us, launches, mean_work, workload):
         ('gemm', 'mfma', 0, mean_work[4]),
         ('ctc_fwd', 'hbm', mean_work[5], 0.0),
         ('ctc_grad', 'hbm', mean_work[6], 0.0),
+        ('attdec_fwd_pass', 'hbm', mean_work[7], att_flops[0]),
+        ('attdec_bwd_pass', 'hbm', mean_work[8], att_flops[1]),
     ]
     rows = []
     for i, (name, bound, nbytes, flops) in enumerate(kinds):
@@ -204,6 +222,10 @@ def roofline_report(args, p, mean_us, launches, mean_work, workload):
             continue
         v = {'bound': r['bound'], 'mean_launch_us': round(r['us'], 3), 'launches': r['n']}
         v.update(view(r))
+        if r['bound'] == 'hbm' and r['flops']:
+            v['mfma_tflops'] = round(r['tfs'], 2)
+            v['algorithmic_bytes_per_launch'] = int(r['bytes'])
+            v['algorithmic_flops_per_launch'] = float(r['flops'])
         if r['name'].startswith('lstm'):
             v['hbm_achieved_gbs'] = round(r['gbs'], 1)
             if r['name'].endswith('_pass'):
@@ -617,7 +639,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     import ctypes
-    NK = 7
+    NK = 9
     mean_us = (ctypes.c_double * NK)()
     launches = (ctypes.c_longlong * NK)()
     mean_work = (ctypes.c_double * NK)()

@@ -245,6 +245,25 @@ int asr_lstm_forward_x(const uint16_t* x, int Din, const uint16_t* wih, const fl
                        const int32_t* lens, int B, int T, int H, float* act, float* y, float* cst,
                        uint16_t* ybf, void* workspace, size_t ws_bytes, void* stream);
 int asr_lstm_forward_x_ok(int B, int H, int Din);
+/* asr_lstm_forward_x with the gate activations stored packed as fp16:
+ * act_h [B][T][2][H][4] (i, f, g, o of one (utterance, frame, direction,
+ * unit) in one 8-B word; 8 B per cell instead of 16, one store instead of
+ * four).  Read back by asr_lstm_backward_dgbf_h (or unpacked to the f32
+ * [B][T][8H] layout by asr_lstm_unpack_act_h).  Replaces the same nn.LSTM
+ * forward as asr_lstm_forward_x (models/pytorch_v3/encoders/rnn.py:166-172). */
+int asr_lstm_forward_xh(const uint16_t* x, int Din, const uint16_t* wih, const float* b_ih,
+                        const float* b_hh, const float* whh_f, const float* whh_r,
+                        const int32_t* lens, int B, int T, int H, uint16_t* act_h, float* y,
+                        float* cst, uint16_t* ybf, void* workspace, size_t ws_bytes,
+                        void* stream);
+/* asr_lstm_backward_dgbf reading act_h of asr_lstm_forward_xh (tagged-granule
+ * recurrence only; ASR_ERR_UNSUPPORTED otherwise).  Same workspace. */
+int asr_lstm_backward_dgbf_h(const float* dy, const void* whh_f, const void* whh_r, int w_dtype,
+                             const int32_t* lens, int B, int T, int H, int compute_dtype,
+                             const uint16_t* act_h, const float* cst, uint16_t* dgbf,
+                             float* db_ih, float* db_hh, void* workspace, size_t ws_bytes,
+                             void* stream);
+int asr_lstm_unpack_act_h(const uint16_t* act_h, int B, int T, int H, float* act, void* stream);
 
 /* ------------------------------------------------------------ GRU layer
  * Replaces the packed nn.GRU(bidirectional=True) of

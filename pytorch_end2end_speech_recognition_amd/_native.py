@@ -65,6 +65,11 @@ SIGNATURES = {
     'asr_lstm_forward_x': (c_int, [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int,
                                    c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
     'asr_lstm_forward_x_ok': (c_int, [c_int, c_int, c_int]),
+    'asr_lstm_forward_xh': (c_int, [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int,
+                                    c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
+    'asr_lstm_backward_dgbf_h': (c_int, [c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int,
+                                         c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
+    'asr_lstm_unpack_act_h': (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp]),
     'asr_gru_workspace_bytes': (c_size, [c_int, c_int]),
     'asr_gru_forward': (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp]),
     'asr_gru_backward': (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp,

@@ -21,6 +21,7 @@
 #include <string.h>
 
 #include "mfma.h"
+#include "prof.h"
 
 namespace asr {
 namespace {
@@ -2389,6 +2390,13 @@ extern "C" int asr_attdec_forward(const asr_attdec_dims_t* dims, int compute_dty
                                ctx_all, aw_all, workspace, ws_bytes, stream);
 }
 
+// Algorithmic bytes of one decoder pass: per decoder step and
+// utterance the attention reads enc_out_a (A), enc_out (E) and the previous
+// weights / writes the new ones (2 values) over T' frames, 4 B each.
+static double att_pass_bytes(const Dims& d) {
+  return (double)d.B * d.S * (d.A + d.E + 2) * 4.0 * d.T;
+}
+
 // Which attention-step instantiations the last forward / backward launched:
 // {forward channel template (10, 3 or 0 = generic), forward frame chunks,
 //  backward channel template, backward frame chunks} (host-side record).
@@ -2450,6 +2458,8 @@ extern "C" int asr_attdec_forward_ex(const asr_attdec_dims_t* dims, const asr_at
     ASR_CHECK_HIP(hipMemsetAsync(ctr, 0, (size_t)(1 + PD_GROUPS) * PD_CTR * 4, s));
     const size_t lds = (size_t)G.total * 4;
     const dim3 grid(PD_GROUPS * PD_MEMBERS);
+    // (A + E + 2) * 4 * T' algorithmic bytes per decoder step and utterance
+    const int pslot = prof_begin_launch(ASR_PROF_ATT_FWD, s, att_pass_bytes(d));
 #define ASR_PD(CC, NQ, SA, SE, SD, SK)                                                                            \
   hipLaunchKernelGGL((attdec_fwd_persist<CC, NQ, SA, SE, SD, SK>), grid, dim3(PD_THREADS), lds, s, d,                 \
                      (const uint16_t*)workspace, pre_emb, h0, enc, enc_a, lens, w_dec, w_conv,   \
@@ -2460,6 +2470,7 @@ extern "C" int asr_attdec_forward_ex(const asr_attdec_dims_t* dims, const asr_at
     else ASR_PD(0, 4, 0, 0, 0, 0);
 #undef ASR_PD
     ASR_LAUNCH_CHECK();
+    prof_end_launch(ASR_PROF_ATT_FWD, pslot, s);
     g_att_last[0] = pd_ten(d) ? 10 : 0;
     g_att_persist_last[0] = 1;
     return ASR_OK;
@@ -2614,6 +2625,7 @@ extern "C" int asr_attdec_backward_ex(const asr_attdec_dims_t* dims, const asr_a
     ASR_CHECK_HIP(hipMemsetAsync(d_enc_a, 0, (size_t)d.B * d.T * d.A * 4, s));
     const size_t lds = (size_t)PG.total * 4;
     const dim3 grid(PD_GROUPS * PD_MEMBERS);
+    const int pslot = prof_begin_launch(ASR_PROF_ATT_BWD, s, att_pass_bytes(d));
 #define ASR_PB(CC, NQ, SA, SE, SD, SK)                                                                            \
   hipLaunchKernelGGL((attdec_bwd_persist<CC, NQ, SA, SE, SD, SK>), grid, dim3(PD_THREADS), lds, s, d,                 \
                      (const uint16_t*)wcatT, enc, enc_a, lens, w_dec, w_conv, conv_w, v, c_all,  \
@@ -2625,6 +2637,7 @@ extern "C" int asr_attdec_backward_ex(const asr_attdec_dims_t* dims, const asr_a
     else ASR_PB(0, 4, 0, 0, 0, 0);
 #undef ASR_PB
     ASR_LAUNCH_CHECK();
+    prof_end_launch(ASR_PROF_ATT_BWD, pslot, s);
     g_att_last[2] = pd_ten(d) ? 10 : 0;
     g_att_persist_last[1] = 1;
   } else {

@@ -46,7 +46,7 @@ int lstm_fwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* wh
 int lstm_bwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* whh_f,
                        const float* whh_r, const float* dy, float* act_dg, const float* cst,
                        void* ws, uint16_t* dgbf, float* dbpart, hipStream_t s, bool dry,
-                       bool dg_f32);
+                       bool dg_f32, const uint16_t* acth = nullptr);
 
 namespace {
 
@@ -766,6 +766,39 @@ extern "C" int asr_lstm_backward_db(const float* dy, const void* whh_f, const vo
                                     size_t ws_bytes, void* stream) {
   return lstm_backward_db_impl(dy, whh_f, whh_r, w_dtype, lens, B, T, H, compute_dtype, act_dg,
                                cst, dgbf, db_ih, db_hh, workspace, ws_bytes, stream, true);
+}
+
+// asr_lstm_backward_dgbf reading the packed fp16 gate activations of
+// asr_lstm_forward_xh (act_h [B][T][2][H][4]).  Only the tagged-granule
+// recurrence reads that layout: ASR_ERR_UNSUPPORTED when it does not take
+// this shape (the caller unpacks with asr_lstm_unpack_act_h and runs
+// asr_lstm_backward_dgbf).
+extern "C" int asr_lstm_backward_dgbf_h(const float* dy, const void* whh_f, const void* whh_r,
+                                        int w_dtype, const int32_t* lens, int B, int T, int H,
+                                        int compute_dtype, const uint16_t* act_h, const float* cst,
+                                        uint16_t* dgbf, float* db_ih, float* db_hh,
+                                        void* workspace, size_t ws_bytes, void* stream) {
+  ASR_REQUIRE(whh_f && whh_r && lens && act_h && cst && dgbf && db_ih && workspace, ASR_ERR_ARG,
+              "lstm_backward_dgbf_h: null pointer");
+  ASR_REQUIRE(B > 0 && T > 0 && H > 0, ASR_ERR_ARG, "lstm_backward_dgbf_h: bad shape");
+  ASR_REQUIRE(compute_dtype == ASR_DT_BF16 && w_dtype == ASR_DT_F32, ASR_ERR_ARG,
+              "lstm_backward_dgbf_h: bf16 compute with f32 W_hh only");
+  ASR_REQUIRE(ws_bytes >= bwd_ws_bias(B, H, compute_dtype), ASR_ERR_WORKSPACE,
+              "lstm_backward_dgbf_h: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  float* part = (float*)((char*)workspace + bias_ws_off(B, H, compute_dtype));
+  if (lstm_bwd_xg_launch(B, T, H, lens, (const float*)whh_f, (const float*)whh_r, dy, nullptr, cst,
+                         workspace, dgbf, part, s, true, false, act_h) != 1)
+    return ASR_ERR_UNSUPPORTED;
+  const int slot = prof_begin_launch(ASR_PROF_LSTM_BWD_SEQ, s);
+  const int rc = lstm_bwd_xg_launch(B, T, H, lens, (const float*)whh_f, (const float*)whh_r, dy,
+                                    nullptr, cst, workspace, dgbf, part, s, false, false, act_h);
+  ASR_REQUIRE(rc == 1, ASR_ERR_HIP, "lstm_backward_dgbf_h: tagged-granule launch failed");
+  prof_end_launch(ASR_PROF_LSTM_BWD_SEQ, slot, s);
+  hipLaunchKernelGGL(bias_from_partials, dim3(ceil_div(8 * H, 256)), dim3(256), 0, s, part, B,
+                     8 * H, db_ih, db_hh);
+  ASR_LAUNCH_CHECK();
+  return ASR_OK;
 }
 
 // asr_lstm_backward_db for callers that consume only the bf16 gate gradients

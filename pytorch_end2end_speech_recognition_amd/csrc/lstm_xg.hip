@@ -101,6 +101,8 @@ constexpr unsigned AUX_SC1 = 16u;
 
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+// packed gate activations of one (utterance, frame, direction, unit): i, f, g, o
+typedef __attribute__((ext_vector_type(4))) _Float16 h16x4;
 typedef __attribute__((address_space(1))) int gint;
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 
@@ -208,6 +210,10 @@ __device__ __forceinline__ void xg_place(int WPG, int allow_local, int* hdr, int
 // never match the first use (bit 1).  Error <= 1 bf16 ulp on one value in four
 // of the recurrent input; y / ybf keep the plain values.
 __device__ __forceinline__ unsigned tag_bit(int step) { return (((unsigned)step >> 1) & 1u) ^ 1u; }
+// Second tag bit (LSB of the second value) of the two-bit tag: with both bits
+// the steps s, s-2, s-4, s-6 that share a buffer all carry different codes, so
+// a granule left over from step s-4 can never pass for step s.
+__device__ __forceinline__ unsigned tag_bit_hi(int step) { return (((unsigned)step >> 2) & 1u) ^ 1u; }
 __device__ __forceinline__ unsigned bf_with_lsb(float h, unsigned bit) {
   const unsigned t = __float_as_uint(h) >> 16;
   return (t & 1u) == bit ? t : t + 1u;
@@ -471,7 +477,7 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
     const uint16_t* __restrict__ wih, const float* __restrict__ b_ih,
     const float* __restrict__ b_hh, float* __restrict__ act, float* __restrict__ y,
     float* __restrict__ cst, unsigned long long* xg, int* hdr, uint16_t* __restrict__ ybf,
-    int allow_local, int late_load, int defer_st) {
+    int allow_local, int late_load, int defer_st, h16x4* __restrict__ acth) {
   (void)late_load;   // input rows now staged by LDS DMA three steps ahead
   __shared__ float part[2][NSW][R][4 * XU + 4];
   __shared__ float xpart[2][NPW][R][4 * XU + 4];
@@ -692,11 +698,16 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
     const long long sidx = ((long long)b * T + tt) * 2 * H + (long long)dir * H + j;
     y[sidx] = v[0];
     cst[sidx] = v[1];
-    const long long gb = ((long long)b * T + tt) * H8 + gcol;
-    act[gb] = v[2];
-    act[gb + H] = v[3];
-    act[gb + 2 * H] = v[4];
-    act[gb + 3 * H] = v[5];
+    if (acth) {   // the four gates of (b, t, dir, j) as one 8-B fp16 store
+      const h16x4 hv = {(_Float16)v[2], (_Float16)v[3], (_Float16)v[4], (_Float16)v[5]};
+      acth[(((long long)b * T + tt) * 2 + dir) * H + j] = hv;
+    } else {
+      const long long gb = ((long long)b * T + tt) * H8 + gcol;
+      act[gb] = v[2];
+      act[gb + H] = v[3];
+      act[gb + 2 * H] = v[4];
+      act[gb + 3 * H] = v[5];
+    }
     if (ybf && (unit & 1) == 0)
       *reinterpret_cast<uint32_t*>(ybf + ((long long)b * T + tt) * 2 * H + dir * H + j) = bv;
   };
@@ -779,7 +790,7 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
     const float* __restrict__ whh_r, const float* __restrict__ dy, float* __restrict__ act_dg,
     const float* __restrict__ cst, unsigned long long* pg, int* hdr,
     uint16_t* __restrict__ dgbf, float* __restrict__ dbpart, unsigned epoch, int allow_local,
-    int dg_f32, int io_pos, int dg_st16) {
+    int dg_f32, int io_pos, int dg_st16, int tag2, const h16x4* __restrict__ acth) {
   constexpr int NPG = 256 / (2 * R);   // producer subsets swept in parallel
   __shared__ float red[NPG][R][XU + 1];
   __shared__ __attribute__((aligned(16))) uint16_t dgt[16][4 * XU + 8];
@@ -818,6 +829,9 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
       XG_TR(q, 0, __builtin_amdgcn_s_memrealtime());
       if (q > 0) {
         const unsigned ebit = tag_bit(q - 1);
+        const unsigned ebit2 = tag2 == 1 ? tag_bit_hi(q - 1) : 0u;
+        const unsigned hmask = tag2 == 1 ? 1u : 0u;   // second tag bit checked only with tag2
+        const unsigned dmask = tag2 == 2 ? 1u : 0u;   // tag2 == 2: the tag in both dwords
         const long long base = ((long long)((q - 1) & 1) * G + grp) * WPG;
         float sm[8];
         nap(ndelay);
@@ -834,6 +848,8 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
                 (unsigned)((((base + w) * R + srow) * (long long)hq + (u0 >> 2) + 2 * sq) * 8);
             const u32x4 v = ld_sc1(rs, off);
             ok &= (int)((((v[0] ^ ebit) | (v[2] ^ ebit)) & 1u) == 0u);
+            ok &= (int)(((((v[0] >> 16) ^ ebit2) | ((v[2] >> 16) ^ ebit2)) & hmask) == 0u);
+            ok &= (int)((((v[1] ^ ebit) | (v[3] ^ ebit)) & dmask) == 0u);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
               sm[2 * e] += bf2f((uint16_t)(v[e] & 0xffffu));
@@ -875,13 +891,18 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
     const int len = own ? lens[b] : 0;
     float dc = 0.f;
     // c_t of step q is c_{tp} of step q - 1: with `carry` it is taken from there
-    auto load_cell = [&](int q, float (&av)[4], float& cc, float& cp, float& dyv, const float* carry) {
+    auto load_cell = [&](int q, float (&av)[4], h16x4& avh, float& cc, float& cp, float& dyv,
+                         const float* carry) {
       const int t = dir == 0 ? T - 1 - q : q;
       const int tp = dir == 0 ? t - 1 : t + 1;
       const long long gb = ((long long)b * T + t) * 8 * H + (long long)dir * H4 + j;
       const long long si = ((long long)b * T + t) * 2 * H + (long long)dir * H + j;
+      if (acth) {   // one 8-B load of the four fp16 gates, converted when used
+        avh = acth[(((long long)b * T + t) * 2 + dir) * H + j];
+      } else {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) av[k] = act_dg[gb + (long long)k * H];
+        for (int k = 0; k < 4; ++k) av[k] = act_dg[gb + (long long)k * H];
+      }
       cc = carry ? *carry : cst[si];
       cp = (tp >= 0 && tp < T) ? cst[si + (long long)(tp - t) * 2 * H] : 0.f;
       dyv = dy ? dy[si] : 0.f;
@@ -889,10 +910,11 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
     // inputs of step q (av, cc, cp, dyv) and q + 1 (n*): loaded two steps ahead
     float av[4] = {0.f, 0.f, 0.f, 0.f}, cc = 0.f, cp = 0.f, dyv = 0.f;
     float nav[4] = {0.f, 0.f, 0.f, 0.f}, ncc = 0.f, ncp = 0.f, ndyv = 0.f;
+    h16x4 avh = {0, 0, 0, 0}, navh = {0, 0, 0, 0};
     // bias gradient: sum over t of this (utterance, unit)'s four gate gradients
     float sb_i = 0.f, sb_f = 0.f, sb_g = 0.f, sb_o = 0.f;
-    if (own) load_cell(0, av, cc, cp, dyv, nullptr);
-    if (own && T > 1) load_cell(1, nav, ncc, ncp, ndyv, nullptr);
+    if (own) load_cell(0, av, avh, cc, cp, dyv, nullptr);
+    if (own && T > 1) load_cell(1, nav, navh, ncc, ncp, ndyv, nullptr);
     // io_pos: where the cell waves issue a step's dG stores and the loads of
     // step q + 2 in the CU's vector-memory queue.  0: after B2 (beside the
     // partial-dh stores); 1: after B3 (beside the next poll: measured +2.4 ms /
@@ -925,7 +947,7 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
         *reinterpret_cast<uint4*>(dgbf + ((long long)(b0 + srow) * T + t) * 8 * H +
                                   (long long)dir * H4 + (long long)sg * H + u0 + 8 * sh) = v;
       }
-      if (own && q + 2 < T) load_cell(q + 2, nav, ncc, ncp, ndyv, &cp);   // cp: step q + 1's
+      if (own && q + 2 < T) load_cell(q + 2, nav, navh, ncc, ncp, ndyv, &cp);   // cp: step q + 1's
     };
     for (int q = 0; q < T; ++q) {
       __syncthreads();  // B1
@@ -937,6 +959,10 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
         if (q > 0) {
 #pragma unroll
           for (int p = 0; p < NPG; ++p) dh += red[p][row][unit];
+        }
+        if (acth) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) av[k] = (float)avh[k];
         }
         const float ig = av[0], fg = av[1], gg = av[2], og = av[3];
         const float tc = ftanh(cc);
@@ -961,6 +987,7 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
       // step q + 1's inputs (loaded two steps ahead)
 #pragma unroll
       for (int k = 0; k < 4; ++k) av[k] = nav[k];
+      avh = navh;
       cc = ncc;
       cp = ncp;
       dyv = ndyv;
@@ -1009,6 +1036,7 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
     const bf16x8 bf0 = *reinterpret_cast<const bf16x8*>(&dgt[ln][8 * kq]);
     const bf16x8 bf1 = *reinterpret_cast<const bf16x8*>(&dgt[ln][32 + 8 * kq]);
     const unsigned tb = tag_bit(q);
+    const unsigned tb2 = tag_bit_hi(q);
     const long long obase = (((long long)(q & 1) * G + grp) * WPG + mem) * R;
     // block by block: MFMA pair, convert, store.  All MFMAs first and then the
     // stores (every granule leaves in one burst) measured 0.7 ms / step slower
@@ -1023,8 +1051,10 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
         if (ln < R) {  // C[m][n]: n = ln (row), m = 16 mb + 4 kq + r
           // one granule: units 16 mb + 4 kq .. + 3, tag bit in the first value
           const unsigned off = (unsigned)(((obase + ln) * (long long)hq + 4 * mb + kq) * 8);
-          const unsigned p01 = bf_with_lsb(acc[0], tb) | ((unsigned)f2bf(acc[1]) << 16);
-          const unsigned p23 = f2bf(acc[2]) | ((unsigned)f2bf(acc[3]) << 16);
+          const unsigned p01 = bf_with_lsb(acc[0], tb) |
+                               ((tag2 == 1 ? bf_with_lsb(acc[1], tb2) : (unsigned)f2bf(acc[1])) << 16);
+          const unsigned p23 = (tag2 == 2 ? bf_with_lsb(acc[2], tb) : (unsigned)f2bf(acc[2])) |
+                               ((unsigned)f2bf(acc[3]) << 16);
           const u32x2 v0 = {p01, p23};
           if (local)  // plain: into this XCD's L2
             __builtin_amdgcn_raw_buffer_store_b64(v0, rs, off, 0, 0);
@@ -1184,7 +1214,8 @@ int lstm_fwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* wh
 int lstm_bwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* whh_f,
                        const float* whh_r, const float* dy, float* act_dg, const float* cst,
                        void* ws, uint16_t* dgbf, float* dbpart, hipStream_t s, bool dry,
-                       bool dg_f32) {
+                       bool dg_f32, const uint16_t* acth) {
+  if (acth && (dg_f32 || !dgbf)) return 0;   // packed activations: bf16 dG only
   if (!xg_enabled()) return 0;
   const int R = xg_rows(B, H);
   if (!R) return 0;
@@ -1200,6 +1231,8 @@ int lstm_bwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* wh
   const int io_pos = (li && atoi(li) == 1) ? 1 : 0;
   const char* s16 = getenv("ASR_XG_DG_ST16");   // A/B: bf16 dG by 16-B stores from LDS
   const int st16 = (s16 && s16[0] == '0') ? 0 : 1;
+  const char* t2e = getenv("ASR_XG_TAG2");      // two-bit step tags on the dh partials
+  const int tag2 = t2e ? atoi(t2e) : 0;
 #define ASR_XGB(RR, M)                                                                          \
   do {                                                                                          \
     if (!xg_fits(lstm_bwd_xg<RR, M>, 512 + RR * XU, pin)) {                                     \
@@ -1211,7 +1244,7 @@ int lstm_bwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* wh
     xg_trace_setup(s);             \
     hipLaunchKernelGGL((lstm_bwd_xg<RR, M>), dim3(grid), dim3(512 + RR * XU), pin, s, B, T, H,      \
                        lens, whh_f, whh_r, dy, act_dg, cst, g, hdr, dgbf, dbpart, ep, al,        \
-                       (dg_f32 || !dgbf) ? 1 : 0, io_pos, st16);                                         \
+                       (dg_f32 || !dgbf) ? 1 : 0, io_pos, st16, tag2, (const h16x4*)acth);             \
   } while (0)
 #define ASR_XGB_M(RR)                  \
   do {                                 \
@@ -1237,7 +1270,7 @@ constexpr int XGX_NPW = 6;   // 12 waves: 3 per SIMD, 170 registers per wave (8:
 int lstm_fwd_xgx_launch(int B, int T, int H, const int32_t* lens, const float* whh_f,
                         const float* whh_r, const uint16_t* x, int Din, const uint16_t* wih,
                         const float* b_ih, const float* b_hh, float* act, float* y, float* cst,
-                        void* ws, uint16_t* ybf, hipStream_t s, bool dry) {
+                        void* ws, uint16_t* ybf, hipStream_t s, bool dry, uint16_t* acth) {
   if (!xg_enabled()) return 0;
   const char* e = getenv("ASR_FUSE_XPROJ");
   if (e && e[0] == '0') return 0;
@@ -1271,7 +1304,8 @@ int lstm_fwd_xgx_launch(int B, int T, int H, const int32_t* lens, const float* w
     if (hipMemsetAsync(ws, 0, lstm_xg_fwd_bytes(B, H), s) != hipSuccess) return -1;             \
     xg_trace_setup(s);                                                                          \
     hipLaunchKernelGGL(kfn, dim3(grid), dim3(threads), pin, s, B, T, H, lens, whh_f, whh_r, x,  \
-                       Din, wih, b_ih, b_hh, act, y, cst, g, hdr, ybf, al, late, defer);        \
+                       Din, wih, b_ih, b_hh, act, y, cst, g, hdr, ybf, al, late, defer,          \
+                       (h16x4*)acth);                                                            \
   } while (0)
 #define ASR_XGX_P(KS)                    \
   do {                                   \
@@ -1388,15 +1422,74 @@ extern "C" int asr_lstm_forward_x(const uint16_t* x, int Din, const uint16_t* wi
   ASR_REQUIRE(B > 0 && T > 0 && H > 0 && Din > 0, ASR_ERR_ARG, "lstm_forward_x: bad shape");
   hipStream_t s = (hipStream_t)stream;
   if (asr::lstm_fwd_xgx_launch(B, T, H, lens, whh_f, whh_r, x, Din, wih, b_ih, b_hh, act, y, cst,
-                               workspace, ybf, s, true) != 1)
+                               workspace, ybf, s, true, nullptr) != 1)
     return ASR_ERR_UNSUPPORTED;
   ASR_REQUIRE(ws_bytes >= asr::lstm_xg_fwd_bytes(B, H), ASR_ERR_WORKSPACE,
               "lstm_forward_x: workspace too small");
   const int slot = asr::prof_begin_launch(ASR_PROF_LSTM_FWD_SEQ, s);
   const int rc = asr::lstm_fwd_xgx_launch(B, T, H, lens, whh_f, whh_r, x, Din, wih, b_ih, b_hh,
-                                          act, y, cst, workspace, ybf, s, false);
+                                          act, y, cst, workspace, ybf, s, false, nullptr);
   ASR_REQUIRE(rc == 1, ASR_ERR_HIP, "lstm_forward_x: launch failed");
   asr::prof_end_launch(ASR_PROF_LSTM_FWD_SEQ, slot, s);
+  return ASR_OK;
+}
+
+// asr_lstm_forward_x writing the gate activations packed as fp16 (act_h
+// [B][T][2][H][4]: i, f, g, o of one (utterance, frame, direction, unit) in
+// one 8-B word) instead of f32 [B][T][8H]; the backward then reads them with
+// asr_lstm_backward_dgbf_h.
+extern "C" int asr_lstm_forward_xh(const uint16_t* x, int Din, const uint16_t* wih,
+                                   const float* b_ih, const float* b_hh, const float* whh_f,
+                                   const float* whh_r, const int32_t* lens, int B, int T, int H,
+                                   uint16_t* act_h, float* y, float* cst, uint16_t* ybf,
+                                   void* workspace, size_t ws_bytes, void* stream) {
+  ASR_REQUIRE(x && wih && b_ih && b_hh && whh_f && whh_r && lens && act_h && y && cst &&
+              workspace, ASR_ERR_ARG, "lstm_forward_xh: null pointer");
+  ASR_REQUIRE(B > 0 && T > 0 && H > 0 && Din > 0, ASR_ERR_ARG, "lstm_forward_xh: bad shape");
+  ASR_REQUIRE(((uintptr_t)act_h & 7) == 0, ASR_ERR_ARG, "lstm_forward_xh: act_h not 8-B aligned");
+  hipStream_t s = (hipStream_t)stream;
+  if (asr::lstm_fwd_xgx_launch(B, T, H, lens, whh_f, whh_r, x, Din, wih, b_ih, b_hh, nullptr, y,
+                               cst, workspace, ybf, s, true, act_h) != 1)
+    return ASR_ERR_UNSUPPORTED;
+  ASR_REQUIRE(ws_bytes >= asr::lstm_xg_fwd_bytes(B, H), ASR_ERR_WORKSPACE,
+              "lstm_forward_xh: workspace too small");
+  const int slot = asr::prof_begin_launch(ASR_PROF_LSTM_FWD_SEQ, s);
+  const int rc = asr::lstm_fwd_xgx_launch(B, T, H, lens, whh_f, whh_r, x, Din, wih, b_ih, b_hh,
+                                          nullptr, y, cst, workspace, ybf, s, false, act_h);
+  ASR_REQUIRE(rc == 1, ASR_ERR_HIP, "lstm_forward_xh: launch failed");
+  asr::prof_end_launch(ASR_PROF_LSTM_FWD_SEQ, slot, s);
+  return ASR_OK;
+}
+
+// act [B][T][8H] f32 (forward columns [0, 4H), reverse [4H, 8H)) from the
+// packed fp16 activations of asr_lstm_forward_xh (for a backward that cannot
+// take the tagged-granule recurrence).
+namespace asr {
+namespace {
+__global__ void unpack_act_h(const h16x4* __restrict__ a, long long n, int H,
+                             float* __restrict__ act) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long bt = i / (2LL * H);
+    const int r = (int)(i - bt * 2LL * H), dir = r / H, j = r - dir * H;
+    const h16x4 v = a[i];
+    float* o = act + bt * 8LL * H + (long long)dir * 4 * H + j;
+    o[0] = (float)v[0];
+    o[H] = (float)v[1];
+    o[2LL * H] = (float)v[2];
+    o[3LL * H] = (float)v[3];
+  }
+}
+}  // namespace
+}  // namespace asr
+
+extern "C" int asr_lstm_unpack_act_h(const uint16_t* act_h, int B, int T, int H, float* act,
+                                     void* stream) {
+  ASR_REQUIRE(act_h && act && B > 0 && T > 0 && H > 0, ASR_ERR_ARG, "lstm_unpack_act_h: args");
+  const long long n = (long long)B * T * 2 * H;
+  hipLaunchKernelGGL(asr::unpack_act_h, dim3((unsigned)std::min(8192LL, (n + 255) / 256)),
+                     dim3(256), 0, (hipStream_t)stream, (const asr::h16x4*)act_h, n, H, act);
+  ASR_LAUNCH_CHECK();
   return ASR_OK;
 }
 
@@ -1405,5 +1498,5 @@ extern "C" int asr_lstm_forward_x_ok(int B, int H, int Din) {
   if (B <= 0 || H <= 0 || Din <= 0) return 0;
   return asr::lstm_fwd_xgx_launch(B, 1, H, nullptr, nullptr, nullptr, nullptr, Din, nullptr,
                                   nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-                                  nullptr, true) == 1;
+                                  nullptr, true, nullptr) == 1;
 }

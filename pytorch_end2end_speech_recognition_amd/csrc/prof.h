@@ -9,7 +9,9 @@
 #define ASR_PROF_GEMM 4          /* asr_gemm main kernel (every launch timed, flops recorded) */
 #define ASR_PROF_CTC_FWD 5       /* CTC emissions + lattice (algorithmic bytes recorded) */
 #define ASR_PROF_CTC_GRAD 6      /* CTC gradient pass (algorithmic bytes recorded) */
-#define ASR_PROF_NKINDS 7
+#define ASR_PROF_ATT_FWD 7       /* persistent attention-decoder forward pass (bytes recorded) */
+#define ASR_PROF_ATT_BWD 8       /* persistent attention-decoder backward pass (bytes recorded) */
+#define ASR_PROF_NKINDS 9
 
 namespace asr {
 bool prof_on();

@@ -40,7 +40,7 @@ int prof_begin_launch(int kind, hipStream_t s, double work) {
   if (!p.on) return -1;
   KindState& k = p.k[kind];
   k.launches++;
-  const int stride = kind >= ASR_PROF_LSTM_FWD_SEQ ? 1 : p.stride;
+  const int stride = kind >= ASR_PROF_LSTM_FWD_SEQ ? 1 : p.stride;   // passes: every launch
   if ((k.seen++ % stride) != 0 || k.used >= kMaxPairs) return -1;
   const int slot = k.used++;
   k.work += work;

@@ -747,9 +747,9 @@ class BLSTMLayerFn(torch.autograd.Function):
         cd = compute_dtype()
         a_map = rowmap(Dsrc, stride_b=T_src * Dsrc, rows_per_b=T, t_mul=t_mul, t_add=t_add,
                        t_limit=T_src, perm=perm)
-        gx = torch.empty(B, T, 8 * H, dtype=torch.float32, device=dev)
         fuse_x = False
-        Dp = Din        # pitch of the bf16 operands x_op / w_op
+        gx = None       # f32 gate pre-activations -> activations [B, T, 8H], or
+        Dp = Din        # packed fp16 activations [B, T, 2, H, 4] (fused bf16 path)
         if cd == BF16:
             if Din % 8 and not fused_drop:
                 # an input width that is not a multiple of 8 (TIMIT's 123) is
@@ -775,16 +775,25 @@ class BLSTMLayerFn(torch.autograd.Function):
         whh_r = w_hh.data_ptr() + 4 * H * H * 4
         if cd == BF16 and _fuse_xproj_on():
             # the input projection inside the persistent recurrence (no gx GEMM);
-            # ASR_ERR_UNSUPPORTED when this shape / configuration does not take it
-            rc = N.query('asr_lstm_forward_x', N.ptr(x_op), Dp, N.ptr(w_op), N.ptr(b_ih),
+            # ASR_ERR_UNSUPPORTED when this shape / configuration does not take it.
+            # The gate activations are kept as packed fp16 (8 B per cell instead
+            # of 16; ASR_XG_ACT_H=0 keeps the f32 layout)
+            if _act_h_on():
+                gx = torch.empty(B, T, 2, H, 4, dtype=torch.float16, device=dev)
+                fn = 'asr_lstm_forward_xh'
+            else:
+                gx = torch.empty(B, T, 8 * H, dtype=torch.float32, device=dev)
+                fn = 'asr_lstm_forward_x'
+            rc = N.query(fn, N.ptr(x_op), Dp, N.ptr(w_op), N.ptr(b_ih),
                          N.ptr(b_hh), N.ptr(w_hh), ctypes.c_void_p(whh_r), N.ptr(lens), B, T, H,
                          N.ptr(gx), N.ptr(y), N.ptr(cst), N.ptr(y_bf), N.ptr(ws), nb,
                          N.stream_handle(dev))
             if rc not in (0, N.ASR_ERR_UNSUPPORTED):
-                raise N.NativeError('asr_lstm_forward_x failed (rc=%d): %s' % (
-                    rc, N.lib().asr_last_error().decode(errors='replace')))
+                raise N.NativeError('%s failed (rc=%d): %s' % (
+                    fn, rc, N.lib().asr_last_error().decode(errors='replace')))
             fuse_x = rc == 0
         if not fuse_x:
+            gx = torch.empty(B, T, 8 * H, dtype=torch.float32, device=dev)
             if cd == BF16:
                 run_gemm([gemm_problem(operand(x_op, 0, rowmap(Dp)), operand(w_op, 0, rowmap(Dp)),
                                        gx, rowmap(8 * H), B * T, 8 * H, Dp, bias=b_ih,
@@ -814,14 +823,34 @@ class BLSTMLayerFn(torch.autograd.Function):
         if gbufs is None:
             gbufs = tuple(grad_buffer(p) for p in (w_ih, w_hh, b_ih, b_hh))
         fused_db = os.environ.get('ASR_BIAS_FUSED', '1') != '0'
-        nb = N.query('asr_lstm_workspace_bytes', B, H, cd, 2 if fused_db else 1)
-        ws = _ws(nb, dev)
         whh_r = w_hh.data_ptr() + 4 * H * H * 4
         dg_bf = (torch.empty(B, T, 8 * H, dtype=torch.bfloat16, device=dev) if cd == BF16
                  else None)
+        done = False
+        if act.dtype == torch.float16:
+            # packed fp16 activations of asr_lstm_forward_xh: the tagged-granule
+            # backward reads them directly; otherwise they are unpacked to f32
+            nb = N.query('asr_lstm_workspace_bytes', B, H, cd, 2)
+            ws = _ws(nb, dev)
+            rc = N.query('asr_lstm_backward_dgbf_h', N.ptr(dy), N.ptr(w_hh), ctypes.c_void_p(whh_r),
+                         F32, N.ptr(lens), B, T, H, cd, N.ptr(act), N.ptr(cst), N.ptr(dg_bf),
+                         N.ptr(gbufs[2]), N.ptr(gbufs[3]), N.ptr(ws), nb, N.stream_handle(dev))
+            if rc not in (0, N.ASR_ERR_UNSUPPORTED):
+                raise N.NativeError('asr_lstm_backward_dgbf_h failed (rc=%d): %s' % (
+                    rc, N.lib().asr_last_error().decode(errors='replace')))
+            done = rc == 0
+            if not done:
+                a32 = torch.empty(B, T, 8 * H, dtype=torch.float32, device=dev)
+                N.call('asr_lstm_unpack_act_h', N.ptr(act), B, T, H, N.ptr(a32),
+                       N.stream_handle(dev))
+                act = a32
+        nb = N.query('asr_lstm_workspace_bytes', B, H, cd, 2 if fused_db else 1)
+        ws = _ws(nb, dev)
         # the saved activations become the gate gradients dG in place; the bias
         # gradients (sum of dG over b, t) are accumulated by the same call
-        if fused_db:
+        if done:
+            pass
+        elif fused_db:
             # bf16 mode: only the bf16 dG feeds the GEMMs, so the f32 dG is not stored
             fn = 'asr_lstm_backward_dgbf' if dg_bf is not None else 'asr_lstm_backward_db'
             N.call(fn, N.ptr(dy), N.ptr(w_hh), ctypes.c_void_p(whh_r), F32,
@@ -867,7 +896,10 @@ class BLSTMLayerFn(torch.autograd.Function):
                         # hold the GEMMs back until the previous layer's backward
                         # recurrence (launched next on the main stream) is resident
                         N.call('asr_lstm_wgrad_gate', N.stream_handle(dev))
-                    _blstm_wgrad(dg_op, act, x_op, x_map, y_op, T, gbufs, dev)
+                    wbufs = gbufs
+                    if os.environ.get('ASR_DIAG_WGRAD_SCRATCH') == '1':   # diagnostics only
+                        wbufs = tuple(torch.zeros_like(g) for g in gbufs)
+                    _blstm_wgrad(dg_op, act, x_op, x_map, y_op, T, wbufs, dev)
             finally:
                 if small:
                     N.call('asr_gemm_set_small_tiles', 0)
@@ -982,6 +1014,12 @@ def bgru_layer(x_src, lens, T, w_ih, w_hh, b_ih, b_hh, perm=None, t_mul=1, t_add
     """The bidirectional GRU counterpart of blstm_layer (same addressing)."""
     return BGRULayerFn.apply(x_src, lens, T, perm, t_mul, t_add, gbufs, bool(concat),
                              w_ih, w_hh, b_ih, b_hh, *graph_params)
+
+
+def _act_h_on():
+    """Fused bf16 forward: keep the gate activations as packed fp16
+    (asr_lstm_forward_xh; ASR_XG_ACT_H=0 keeps f32)."""
+    return os.environ.get('ASR_XG_ACT_H', '1') != '0'
 
 
 def _fuse_xproj_on():

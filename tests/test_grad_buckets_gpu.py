@@ -51,8 +51,11 @@ def _batch(B=32, T=240, seed=0):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('overlap', ['auto', '2'])
-def test_buckets_on_real_model(overlap, cuda_dev, monkeypatch):
+@pytest.mark.parametrize('overlap,H,L', [('auto', 512, 5), ('2', 320, 4)])
+def test_buckets_on_real_model(overlap, H, L, cuda_dev, monkeypatch):
+    """ctc5x512's encoder (auto = weight gradients on the compute stream,
+    the recurrence fills the chip) and the 4x320 encoder of configs[2]-[4]
+    with its weight gradients on the side stream beside the next recurrence."""
     from pytorch_end2end_speech_recognition_amd import native_ops
     from pytorch_end2end_speech_recognition_amd.utils.training import training_loop as TL
     monkeypatch.setenv('ASR_OVERLAP_WGRAD', overlap)
@@ -60,10 +63,10 @@ def test_buckets_on_real_model(overlap, cuda_dev, monkeypatch):
     native_ops.set_compute_dtype('bf16')
     try:
         torch.manual_seed(1623)
-        sd = {k: v.clone() for k, v in _build(_kw()).state_dict().items()}
+        sd = {k: v.clone() for k, v in _build(_kw(H, L)).state_dict().items()}
 
         def fresh():
-            m = _build(_kw())
+            m = _build(_kw(H, L))
             m.load_state_dict(sd)
             m.set_cuda()
             m.set_optimizer('adam', 1e-3, weight_decay=1e-6)
@@ -99,7 +102,7 @@ def test_buckets_on_real_model(overlap, cuda_dev, monkeypatch):
         for a, b, _ in issued:
             cover[a:b] += 1
         assert cover.min() == 1 and cover.max() == 1
-        # per-layer buckets first, top layer first (5 layers + the remainder)
+        # per-layer buckets first, top layer first (L layers + the remainder)
         enc = m.encoder
         starts = []
         for l in range(enc.num_layers):

@@ -199,8 +199,17 @@ def test_recurrence_give_up_skips_the_batch(cuda_dev):
         batch = dict(xs=d['xs'], ys=d['ys'], x_lens=d['x_lens'], y_lens=d['y_lens'])
         native_ops.recurrence_status(cuda_dev)             # clear
         before = model._flat_param.clone()
-        N.call('asr_lstm_status_inject', 1, N.stream_handle(cuda_dev))
+        # a give-up during the step's own pass (train_step drops status words
+        # left from before it starts)
+        orig = model.forward
+
+        def fwd(*a, **k):
+            N.call('asr_lstm_status_inject', 1, N.stream_handle(cuda_dev))
+            return orig(*a, **k)
+
+        model.forward = fwd
         model, lv = train_step(model, batch, clip_grad_norm=5.0)
+        model.forward = orig
         torch.cuda.synchronize()
         assert lv == 0.0
         assert torch.equal(before, model._flat_param)
@@ -239,11 +248,17 @@ def test_deferred_loss_readback_matches_synchronous_steps(cuda_dev):
             model.set_optimizer('adam', 1e-3, weight_decay=1e-6)
             native_ops.recurrence_status(cuda_dev)             # clear
             vals = []
+            orig = model.forward
+
+            def fwd(*a, **k):
+                N.call('asr_lstm_status_inject', 1, N.stream_handle(cuda_dev))
+                return orig(*a, **k)
+
             for k in range(4):
-                if k == 1:
-                    N.call('asr_lstm_status_inject', 1, N.stream_handle(cuda_dev))
+                model.forward = fwd if k == 1 else orig     # a give-up inside step 1
                 model, lv = train_step(model, batch, clip_grad_norm=5.0, sync=sync)
                 vals.append(lv)
+            model.forward = orig
             vals = [float(v) for v in vals]
             torch.cuda.synchronize()
             runs.append((vals, model._flat_param.clone(), model.optimizer._step))

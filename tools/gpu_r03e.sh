@@ -1,0 +1,9 @@
+#!/bin/bash
+mkdir -p gpurun_out
+run() {  # name, env...
+  local name=$1; shift
+  env "$@" timeout -k 10 120 python -u tools/buckets_diag.py trace 2 2>&1 | grep -v amdgpu.ids > gpurun_out/r03e_$name.log; local rc=$?
+  echo "== $name rc=$rc"; grep "dx" gpurun_out/r03e_$name.log
+  return $rc
+}
+run scratch ASR_DIAG_WGRAD_SCRATCH=1 && run scratch_b ASR_DIAG_WGRAD_SCRATCH=1
