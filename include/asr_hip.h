@@ -618,6 +618,11 @@ int asr_conv_direct_forward(const float* x, int B, int T, int F, int Ci, int Co,
  * cnn.py:124-165). */
 int asr_conv3x3_c1_forward(const void* x, int x_dtype, int cstride, int B, int T, int F, int Co,
                            const float* w, const float* bias, float* z, void* stream);
+/* asr_conv3x3_c1_forward reading the raw features xs [B][T][F] f32 (the first
+ * VGG layer, encoders/cnn.py:124-165), each value rounded to bf16 first when
+ * round_bf16 (the bf16 operand's values); Co / 4 must divide 256. */
+int asr_conv3x3_c1_forward_xs(const float* xs, int round_bf16, int B, int T, int F, int Co,
+                              const float* w, const float* bias, float* z, void* stream);
 int asr_conv_direct_dgrad(const float* dz, int B, int T, int F, int Ci, int Co, const float* w,
                           float* dx, void* stream);
 size_t asr_conv_direct_wgrad_workspace_bytes(int B, int T, int F, int Ci, int Co);

@@ -51,6 +51,8 @@ SIGNATURES = {
     'asr_colsum_workspace_bytes': (c_size, [c_int, c_int]),
     'asr_colsum_accumulate': (c_int, [c_vp, c_ll, c_int, c_int, c_float, c_vp, c_vp, c_vp, c_size,
                                       c_vp]),
+    'asr_conv3x3_c1_forward_xs': (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp,
+                                          c_vp, c_vp]),
     'asr_conv3x3_c1_forward': (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp,
                                        c_vp, c_vp]),
     'asr_lstm_workspace_bytes': (c_size, [c_int, c_int, c_int, c_int]),
@@ -69,6 +71,7 @@ SIGNATURES = {
                                     c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
     'asr_lstm_backward_dgbf_h': (c_int, [c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int,
                                          c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
+    'asr_diag_lds_spin': (c_int, [c_int, c_int, c_vp, c_vp]),
     'asr_lstm_unpack_act_h': (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp]),
     'asr_gru_workspace_bytes': (c_size, [c_int, c_int]),
     'asr_gru_forward': (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp]),

@@ -132,6 +132,69 @@ __global__ void __launch_bounds__(CT) conv3x3_c1_fwd(const TX* __restrict__ x, i
   }
 }
 
+// The same stencil from the raw features xs [B][T][F] (f32, contiguous rows)
+// instead of channel 0 of the padded operand: a work-group takes C1_FT frames
+// of one utterance, stages their C1_FT + 2 input rows with a zero halo (each
+// value rounded to bf16 first when round_bf16, exactly as the bf16 operand the
+// weight-gradient GEMM reads), and each thread keeps the 9 taps of its 4
+// output channels in registers (its channel group is fixed: CT % (Co / 4) == 0).
+// One wave writes 4 pixels x 64 channels = 1 KB of contiguous z per store.
+constexpr int C1_FT = 4;
+
+__global__ void __launch_bounds__(CT) conv3x3_c1_fwd_xs(const float* __restrict__ xs, int T,
+                                                        int F, int Co, int round_bf16,
+                                                        const float* __restrict__ w,
+                                                        const float* __restrict__ bias,
+                                                        float* __restrict__ z) {
+  extern __shared__ float sm[];
+  float* xr = sm;                    // [C1_FT + 2][F + 2], zero halo
+  const int ntile = (T + C1_FT - 1) / C1_FT;
+  const int b = blockIdx.x / ntile, t0 = (blockIdx.x - b * ntile) * C1_FT;
+  const int W = F + 2;
+  for (int i = threadIdx.x; i < (C1_FT + 2) * W; i += CT) {
+    const int r = i / W, fp = i - r * W;
+    const int t = t0 - 1 + r, f = fp - 1;
+    float v = 0.f;
+    if (t >= 0 && t < T && f >= 0 && f < F) {
+      v = xs[((long long)b * T + t) * F + f];
+      if (round_bf16) v = bf2f(f2bf(v));
+    }
+    xr[i] = v;
+  }
+  const int ng = Co >> 2;
+  const int c4 = 4 * (threadIdx.x % ng);
+  float4 wr[9];
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {   // torch weight [Co][1][3 (f)][3 (t)], tap = kh * 3 + kw
+    wr[tap].x = w[(c4 + 0) * 9 + tap];
+    wr[tap].y = w[(c4 + 1) * 9 + tap];
+    wr[tap].z = w[(c4 + 2) * 9 + tap];
+    wr[tap].w = w[(c4 + 3) * 9 + tap];
+  }
+  const float4 b4 = bias ? *reinterpret_cast<const float4*>(bias + c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();
+  const int nt = min(C1_FT, T - t0);
+  const int ppi = CT / ng;           // pixels per iteration
+  for (int q = threadIdx.x / ng; q < nt * F; q += ppi) {
+    const int r = q / F, f = q - r * F;
+    float4 acc = b4;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        // z[p] += w[co][kh][kw] x[p + (kw - 1)(F + 2) + (kh - 1)]
+        const float xv = xr[(r + kw) * W + f + kh];
+        const float4 wv = wr[kh * 3 + kw];
+        acc.x += wv.x * xv;
+        acc.y += wv.y * xv;
+        acc.z += wv.z * xv;
+        acc.w += wv.w * xv;
+      }
+    const long long p = ((long long)b * (T + 2) + t0 + r + 1) * W + f + 1;
+    *reinterpret_cast<float4*>(z + p * Co + c4) = acc;
+  }
+}
+
 // dx[p][ci] = sum_{co,kh,kw} dz[p - shift][co] w[co][ci][kh][kw] (dz halo rows zero)
 __global__ void conv_direct_dgrad(const float* __restrict__ dz, int B, int T, int F, int Ci,
                                   int Co, const float* __restrict__ w, float* __restrict__ dx) {
@@ -872,6 +935,28 @@ extern "C" int asr_conv3x3_c1_forward(const void* x, int x_dtype, int cstride, i
   else
     hipLaunchKernelGGL(conv3x3_c1_fwd<float>, dim3(B * T), dim3(CT), lds, s, (const float*)x,
                        cstride, T, F, Co, w, bias, z);
+  ASR_LAUNCH_CHECK();
+  return ASR_OK;
+}
+
+// asr_conv3x3_c1_forward from the raw features xs [B][T][F] f32 (rounded to
+// bf16 first when round_bf16: the values of the bf16 padded operand).
+// Co % 4 == 0 and 256 % (Co / 4) == 0.
+extern "C" int asr_conv3x3_c1_forward_xs(const float* xs, int round_bf16, int B, int T, int F,
+                                         int Co, const float* w, const float* bias, float* z,
+                                         void* stream) {
+  ASR_REQUIRE(xs && w && z && B > 0 && T > 0 && F > 0, ASR_ERR_ARG,
+              "conv3x3_c1_forward_xs: bad args");
+  ASR_REQUIRE(Co > 0 && Co % 4 == 0 && CT % (Co / 4) == 0, ASR_ERR_UNSUPPORTED,
+              "conv3x3_c1_forward_xs: Co / 4 must divide %d", CT);
+  ASR_REQUIRE(((uintptr_t)z & 15) == 0 && (!bias || ((uintptr_t)bias & 15) == 0), ASR_ERR_ARG,
+              "conv3x3_c1_forward_xs: z / bias not 16-B aligned");
+  const size_t lds = (size_t)(C1_FT + 2) * (F + 2) * 4;
+  ASR_REQUIRE(lds <= 64 * 1024, ASR_ERR_UNSUPPORTED, "conv3x3_c1_forward_xs: F too large");
+  const long long nwg = (long long)B * ((T + C1_FT - 1) / C1_FT);
+  ASR_REQUIRE(nwg < (1LL << 31), ASR_ERR_UNSUPPORTED, "conv3x3_c1_forward_xs: grid too large");
+  hipLaunchKernelGGL(conv3x3_c1_fwd_xs, dim3((unsigned)nwg), dim3(CT), lds, (hipStream_t)stream, xs,
+                     T, F, Co, round_bf16, w, bias, z);
   ASR_LAUNCH_CHECK();
   return ASR_OK;
 }

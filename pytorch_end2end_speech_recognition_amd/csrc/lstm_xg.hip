@@ -790,7 +790,7 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
     const float* __restrict__ whh_r, const float* __restrict__ dy, float* __restrict__ act_dg,
     const float* __restrict__ cst, unsigned long long* pg, int* hdr,
     uint16_t* __restrict__ dgbf, float* __restrict__ dbpart, unsigned epoch, int allow_local,
-    int dg_f32, int io_pos, int dg_st16, int tag2, const h16x4* __restrict__ acth) {
+    int dg_f32, int io_pos, int dg_st16, int tag2, const h16x4* __restrict__ acth, int acq) {
   constexpr int NPG = 256 / (2 * R);   // producer subsets swept in parallel
   __shared__ float red[NPG][R][XU + 1];
   __shared__ __attribute__((aligned(16))) uint16_t dgt[16][4 * XU + 8];
@@ -802,6 +802,7 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
   if (threadIdx.x == 0) s_dead = 0;
   xg_place(WPG, allow_local, hdr, s_pl, epoch);  // epoch: the launch's sequence number
   if (!s_pl[3]) return;
+  if (acq) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // diagnostics (ASR_XG_ACQ)
   const int grp = s_pl[0], mem = s_pl[1];
   const bool local = s_pl[2] != 0;  // granules carry a 1-bit step tag (tag_bit)
   const int dir = grp & 1, rg = grp >> 1;
@@ -1233,6 +1234,8 @@ int lstm_bwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* wh
   const int st16 = (s16 && s16[0] == '0') ? 0 : 1;
   const char* t2e = getenv("ASR_XG_TAG2");      // two-bit step tags on the dh partials
   const int tag2 = t2e ? atoi(t2e) : 0;
+  const char* acqe = getenv("ASR_XG_ACQ");
+  const int acq = (acqe && acqe[0] == '1') ? 1 : 0;
 #define ASR_XGB(RR, M)                                                                          \
   do {                                                                                          \
     if (!xg_fits(lstm_bwd_xg<RR, M>, 512 + RR * XU, pin)) {                                     \
@@ -1244,7 +1247,7 @@ int lstm_bwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* wh
     xg_trace_setup(s);             \
     hipLaunchKernelGGL((lstm_bwd_xg<RR, M>), dim3(grid), dim3(512 + RR * XU), pin, s, B, T, H,      \
                        lens, whh_f, whh_r, dy, act_dg, cst, g, hdr, dgbf, dbpart, ep, al,        \
-                       (dg_f32 || !dgbf) ? 1 : 0, io_pos, st16, tag2, (const h16x4*)acth);             \
+                       (dg_f32 || !dgbf) ? 1 : 0, io_pos, st16, tag2, (const h16x4*)acth, acq);        \
   } while (0)
 #define ASR_XGB_M(RR)                  \
   do {                                 \
@@ -1398,6 +1401,32 @@ extern "C" int asr_lstm_xg_mode(int* mode, int clear) {
 
 // Enqueue the wgrad gate on `stream`: it releases once the NEXT persistent
 // backward recurrence launched on any stream is resident (bounded at ~5 ms).
+// Diagnostics only (ASR_DIAG_SPIN, native_ops): work-groups that fill `lds`
+// bytes of LDS with a pattern and rewrite / check it for `iters` rounds, as a
+// stand-in for the co-resident weight-gradient GEMMs (no global memory
+// traffic).  bad[0] counts pattern mismatches.
+namespace asr {
+__global__ void diag_lds_spin(int iters, int* bad) {
+  extern __shared__ unsigned dl[];
+  const int words = 16384;   // 64 KB
+  unsigned err = 0;
+  for (int it = 0; it < iters; ++it) {
+    for (int i = threadIdx.x; i < words; i += blockDim.x) dl[i] = (unsigned)(i * 2654435761u) ^ it;
+    __syncthreads();
+    for (int i = threadIdx.x; i < words; i += blockDim.x)
+      err += dl[(i * 7 + 1) % words] != ((unsigned)(((i * 7 + 1) % words) * 2654435761u) ^ it);
+    __syncthreads();
+  }
+  if (err) atomicAdd(bad, (int)err);
+}
+}  // namespace asr
+
+extern "C" int asr_diag_lds_spin(int nwg, int iters, int* bad, void* stream) {
+  hipLaunchKernelGGL(asr::diag_lds_spin, dim3(nwg), dim3(256), 64 * 1024, (hipStream_t)stream,
+                     iters, bad);
+  return hipGetLastError() == hipSuccess ? ASR_OK : ASR_ERR_HIP;
+}
+
 extern "C" int asr_lstm_wgrad_gate(void* stream) {
   const unsigned want = asr::xg_bwd_seq(false) + 1;
   hipLaunchKernelGGL(asr::xg_wgrad_gate, dim3(1), dim3(64), 0, (hipStream_t)stream,

@@ -899,7 +899,13 @@ class BLSTMLayerFn(torch.autograd.Function):
                     wbufs = gbufs
                     if os.environ.get('ASR_DIAG_WGRAD_SCRATCH') == '1':   # diagnostics only
                         wbufs = tuple(torch.zeros_like(g) for g in gbufs)
-                    _blstm_wgrad(dg_op, act, x_op, x_map, y_op, T, wbufs, dev)
+                    if os.environ.get('ASR_DIAG_SPIN'):   # diagnostics: an LDS-only stand-in
+                        bad = torch.zeros(1, dtype=torch.int32, device=dev)
+                        N.call('asr_diag_lds_spin', 256, int(os.environ['ASR_DIAG_SPIN']),
+                               N.ptr(bad), N.stream_handle(dev))
+                        _diag_bad.append(bad)    # (weight gradients skipped)
+                    else:
+                        _blstm_wgrad(dg_op, act, x_op, x_map, y_op, T, wbufs, dev)
             finally:
                 if small:
                     N.call('asr_gemm_set_small_tiles', 0)
@@ -1073,6 +1079,7 @@ def _blstm_wgrad(dg, dg_f32, x_op, x_map, y_op, T, gbufs, dev):
 
 
 _side_streams = {}
+_diag_bad = []         # ASR_DIAG_SPIN pattern-mismatch counters (diagnostics)
 _side_pending = []     # (side stream, gbufs, compute stream) of weight gradients not joined yet
 
 
@@ -1098,6 +1105,16 @@ def discard_side_wgrads():
     for side, _gbufs, main in _side_pending:
         main.wait_stream(side)
     del _side_pending[:]
+
+
+_warned = set()
+
+
+def _warn_once(msg):
+    if msg not in _warned:
+        _warned.add(msg)
+        import warnings
+        warnings.warn(msg, RuntimeWarning, stacklevel=3)
 
 
 def _num_cus(dev):
@@ -1133,12 +1150,19 @@ def _wgrad_side_stream(dev, B, H):
     if compute_dtype() != BF16 or os.environ.get('ASR_LSTM_PERSIST', '1') == '0' or H % 32:
         return None
     if mode == 'auto':
-        # co-resident weight gradients pay off when the recurrence leaves CUs
-        # free (4x320 / 2x320 at B = 32: 160 of 256 CUs); when it fills the chip
-        # (5x512: 256 work-groups) the GEMMs' memory traffic slows each
-        # recurrence step by ~25 % and the step does not gain
-        ncu = _num_cus(dev)
-        mode = '2' if _xg_grid(B, H, ncu) < ncu else '0'
+        # Round 3: OFF.  With GEMM work-groups co-resident on the recurrence's
+        # CUs the backward recurrence's results change from run to run by up to
+        # 2 % relative even with contracting weights (tools/buckets_diag.py
+        # trace) -- wrong gradients, not rounding.  An LDS-only
+        # co-resident stand-in leaves them bitwise stable; GEMMs writing to
+        # scratch outputs do not.  Until that is understood, the weight
+        # gradients stay on the compute stream (mode 1, CU-disjoint, remains
+        # available where the recurrence fits in half the chip).
+        mode = '0'
+    elif mode == '2':
+        _warn_once('ASR_OVERLAP_WGRAD=2: weight-gradient GEMMs co-resident with the backward '
+                   'recurrence give run-to-run different (wrong) recurrence results on '
+                   'gfx950 (DESIGN.md §5); use for timing experiments only')
     if mode not in ('1', '2'):
         return None
     key = (dev.index, mode)
@@ -1558,8 +1582,14 @@ class VGGFn(torch.autograd.Function):
                 # one input channel: a direct stencil from channel 0 of the padded
                 # operand (the GEMM would run K = 144 for 9 useful taps); the
                 # backward still takes the weight-gradient GEMM over this operand
-                N.call('asr_conv3x3_c1_forward', N.ptr(x_op), cd, cCp, B, cT, cF, Co, N.ptr(w),
-                       N.ptr(sp['b']), N.ptr(z), N.stream_handle(dev))
+                if 256 % (Co // 4) == 0 and os.environ.get('ASR_VGG_C1_XS', '1') != '0':
+                    # from the raw features (contiguous rows; rounded to bf16 as the
+                    # staged operand is in bf16 mode)
+                    N.call('asr_conv3x3_c1_forward_xs', N.ptr(xs), int(cd == BF16), B, cT, cF, Co,
+                           N.ptr(w), N.ptr(sp['b']), N.ptr(z), N.stream_handle(dev))
+                else:
+                    N.call('asr_conv3x3_c1_forward', N.ptr(x_op), cd, cCp, B, cT, cF, Co,
+                           N.ptr(w), N.ptr(sp['b']), N.ptr(z), N.stream_handle(dev))
             else:
                 wg = (torch.zeros if cCp != cC else torch.empty)(Co, 9 * cCp, dtype=opdt,
                                                                  device=dev)

@@ -70,6 +70,11 @@ def layer_trace():
     no.set_compute_dtype('bf16')
     torch.manual_seed(1623)
     sd = {k: v.clone() for k, v in _build(_kw(H, L)).state_dict().items()}
+    if os.environ.get('DIAG_WHH'):     # contracting recurrence: no chaotic amplification
+        sc = float(os.environ['DIAG_WHH'])
+        for k in sd:
+            if 'weight_hh' in k:
+                sd[k] = sd[k] * (sc / 0.1)
     orig = no.BLSTMLayerFn.backward
 
     extras = []
@@ -105,6 +110,8 @@ def layer_trace():
         return rec
 
     a, b = run(), run()
+    if no._diag_bad:
+        print('diag spin LDS pattern errors:', sum(int(t.item()) for t in no._diag_bad))
     if extras[0]:
         for i, (x, y) in enumerate(zip(extras[0], extras[1])):
             print('call %d after-run inputs maxdiff x_op %.3e act %.3e cst %.3e y_op %.3e dy %.3e' % (
