@@ -144,17 +144,23 @@ def roofline_report(args, p, mean_us, launches, mean_work, workload):
     # act read + dG write (f32; bf16 mode writes only the bf16 copy), dy + c read
     # (bf16 mode carries c_t over from the previous step's c_{t-1}: one read)
     bwd_cell = (4 * 4 + 2 * 4 + 4 * 2) if args.precision == 'bf16' else (4 * 4 * 2 + 4 * 3)
+    fused = args.precision == 'bf16' and os.environ.get('ASR_FUSE_XPROJ', '1') != '0'
+    act_h = fused and os.environ.get('ASR_XG_ACT_H', '1') != '0'
+    act_b = 4 * 2 if act_h else 4 * 4          # gate activations per cell: fp16 packed or f32
+    if act_h:
+        bwd_cell += act_b - 4 * 4
     fwd_pass_bytes = T * 2 * cell * fwd_cell + w_hh
     fwd_pass_flops = T * flops_step
-    if args.precision == 'bf16' and os.environ.get('ASR_FUSE_XPROJ', '1') != '0':
+    if fused:
         # the input projection runs inside the forward pass (lstm_fwd_xgx): its
         # flops join the pass, gx is never read, the bf16 input rows are
-        # (Din averaged over the layers: the input features, then 2H)
+        # (Din averaged over the layers: the input features, then 2H); the
+        # gate activations leave as packed fp16 (asr_lstm_forward_xh)
         din = [input_dim(p)] + [2 * H] * (len(T_l) - 1)
         din_avg = sum(d * tl for d, tl in zip(din, T_l)) / sum(T_l)
         fwd_pass_flops += T * 2 * B * 8 * H * din_avg
-        fwd_pass_bytes = (T * 2 * cell * (fwd_cell - 4 * 4) + T * B * din_avg * 2 + w_hh +
-                          8 * H * din_avg * 2)
+        fwd_pass_bytes = (T * 2 * cell * (fwd_cell - 4 * 4 - 4 * 4 + act_b) + T * B * din_avg * 2 +
+                          w_hh + 8 * H * din_avg * 2)
     # attention decoder passes (one persistent launch each): bytes per launch
     # recorded by the library ((A + E + 2) * 4 * T' per decoder
     # step and utterance); flops from the same launch's B * S decoder steps:

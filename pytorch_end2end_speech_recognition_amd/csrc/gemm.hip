@@ -758,7 +758,10 @@ constexpr int N64_BM = 256;
 // k-row layout of the 128 x 128 kernel with columns 64.. zero, 16 KB)
 __host__ __device__ constexpr int n64_stage(int bmode) { return 2 * FTILE + (bmode ? FTILE : FTILE / 2); }
 
-template <int AMODE, int BMODE>
+// NSTAGE = 2: double buffer (80 KB, two work-groups per CU), one k-tile of
+// prefetch; NSTAGE = 3: a ring (120 KB, one work-group per CU), two k-tiles in
+// flight (the tap-addressed convolutions wait on L2 for every k-tile).
+template <int AMODE, int BMODE, int NSTAGE = 2>
 __global__ void __launch_bounds__(NT) gemm_bf16_n64(Params P) {
   constexpr int N64_STAGE = n64_stage(BMODE);
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -812,12 +815,7 @@ __global__ void __launch_bounds__(NT) gemm_bf16_n64(Params P) {
     stage_any<AMODE>(pr.a, ra, sa1, st + FTILE, tm + 128, pr.M, k0, kend, w, lane);
     stage_any<BMODE, BMODE ? 4 : 2>(pr.b, rb, sb, st + 2 * FTILE, tn, pr.N, k0, kend, w, lane);
   };
-  stage(smem, kbeg);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  for (int kt = 0; kt < nk; ++kt) {
-    const char* cur = smem + (kt & 1) * N64_STAGE;
-    if (kt + 1 < nk) stage(smem + ((kt + 1) & 1) * N64_STAGE, kbeg + (kt + 1) * FBK);
+  auto compute = [&](const char* cur) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       bf16x8 fa[4], fb[4];
@@ -831,8 +829,36 @@ __global__ void __launch_bounds__(NT) gemm_bf16_n64(Params P) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = mfma_bf16(fa[i], fb[j], acc[i][j]);
     }
+  };
+  static_assert(NSTAGE == 2 || NSTAGE == 3, "n64: two or three stages");
+  if constexpr (NSTAGE == 2) {
+    stage(smem, kbeg);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+    for (int kt = 0; kt < nk; ++kt) {
+      const char* cur = smem + (kt & 1) * N64_STAGE;
+      if (kt + 1 < nk) stage(smem + ((kt + 1) & 1) * N64_STAGE, kbeg + (kt + 1) * FBK);
+      compute(cur);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+  } else {
+    // ring: k-tiles issued NSTAGE - 1 ahead; iteration kt waits for tile kt
+    // (each k-tile is N64_DMA buffer->LDS loads per wave; the later tiles stay
+    // in flight), one barrier (tile kt visible to every wave, and every wave
+    // done with slot (kt - 1) % NSTAGE), refills that slot, computes tile kt
+    constexpr int N64_DMA = 8 + (BMODE ? 4 : 2);
+#pragma unroll
+    for (int j = 0; j < NSTAGE - 1; ++j)
+      if (j < nk) stage(smem + j * N64_STAGE, kbeg + j * FBK);
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N64_DMA) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (kt + NSTAGE - 1 < nk)
+        stage(smem + ((kt + NSTAGE - 1) % NSTAGE) * N64_STAGE, kbeg + (kt + NSTAGE - 1) * FBK);
+      compute(smem + (kt % NSTAGE) * N64_STAGE);
+    }
   }
   store_acc(pr, acc, tm, tn, wr, wc, lane, split, nsplit);
 }
@@ -1769,12 +1795,14 @@ struct SplitPlan {
 
 SplitPlan plan_split(const asr_gemm_t* g, int nprob) {
   SplitPlan sp{};
+  const char* ns = getenv("ASR_GEMM_NOSPLIT");   // diagnostics: no split-K slabs
+  const bool nosplit = ns && ns[0] == '1';
   for (int i = 0; i < nprob; ++i) {
     // per problem: the problems of one launch run side by side (blockIdx.z), so
     // a few-tile dW next to a many-tile dX still gets its own K split
     const int tiles = ceil_div(g[i].M, BM) * ceil_div(g[i].N, BN);
     int ks = 1;
-    if (g[i].batch <= 1 && tiles > 0 && tiles < 512 && g[i].K >= 1024) {
+    if (!nosplit && g[i].batch <= 1 && tiles > 0 && tiles < 512 && g[i].K >= 1024) {
       // a few-tile, long-K product (the decoder / projection weight gradients,
       // K = B*S or B*T) is latency-bound per work-group: chunks >= 128
       ks = min(ceil_div(1024, tiles), g[i].K / 128);
@@ -2052,21 +2080,19 @@ int gemm_launch_own(const asr_gemm_t* problems, int nprob, int compute_dtype, vo
     hipLaunchKernelGGL(gemm_bf16_kk256, dim3(maxwg2, 1, nprob * maxb), dim3(NT),
                        (size_t)NST2 * 2 * FTILE2, s, P);
   } else if (fast >= 0 && n64_ok(problems, nprob, fast & 1)) {
+    // ASR_GEMM_N64_STAGES=3: the three-stage ring (read per launch)
+    const char* n64e = getenv("ASR_GEMM_N64_STAGES");
+    const int n64st = (n64e && n64e[0] == '3') ? 3 : 2;
     static bool attr64 = false;
     if (!attr64) {
       bool ok = true;
-      ok &= hipFuncSetAttribute((const void*)gemm_bf16_n64<0, 0>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                2 * n64_stage(0)) == hipSuccess;
-      ok &= hipFuncSetAttribute((const void*)gemm_bf16_n64<1, 0>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                2 * n64_stage(0)) == hipSuccess;
-      ok &= hipFuncSetAttribute((const void*)gemm_bf16_n64<0, 1>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                2 * n64_stage(1)) == hipSuccess;
-      ok &= hipFuncSetAttribute((const void*)gemm_bf16_n64<1, 1>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                2 * n64_stage(1)) == hipSuccess;
+#define ASR_N64_ATTR(A, B, NS)                                                               \
+  ok &= hipFuncSetAttribute((const void*)gemm_bf16_n64<A, B, NS>,                            \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, NS * n64_stage(B)) ==   \
+        hipSuccess
+      ASR_N64_ATTR(0, 0, 2); ASR_N64_ATTR(1, 0, 2); ASR_N64_ATTR(0, 1, 2); ASR_N64_ATTR(1, 1, 2);
+      ASR_N64_ATTR(0, 0, 3); ASR_N64_ATTR(1, 0, 3); ASR_N64_ATTR(0, 1, 3); ASR_N64_ATTR(1, 1, 3);
+#undef ASR_N64_ATTR
       ASR_REQUIRE(ok, ASR_ERR_HIP, "gemm: cannot raise the LDS limit of the 256x64 kernel");
       attr64 = true;
     }
@@ -2074,12 +2100,20 @@ int gemm_launch_own(const asr_gemm_t* problems, int nprob, int compute_dtype, vo
     for (int i = 0; i < nprob; ++i)
       maxwg64 = max(maxwg64, ceil_div(P.p[i].M, N64_BM) * max(1, P.p[i].ksplit));
     const dim3 g64(maxwg64, 1, nprob * maxb);
+#define ASR_N64(A, B)                                                                          \
+  do {                                                                                         \
+    if (n64st == 3)                                                                            \
+      hipLaunchKernelGGL((gemm_bf16_n64<A, B, 3>), g64, dim3(NT), 3 * n64_stage(B), s, P);     \
+    else                                                                                       \
+      hipLaunchKernelGGL((gemm_bf16_n64<A, B, 2>), g64, dim3(NT), 2 * n64_stage(B), s, P);     \
+  } while (0)
     switch (fast) {
-      case 0: hipLaunchKernelGGL((gemm_bf16_n64<0, 0>), g64, dim3(NT), 2 * n64_stage(0), s, P); break;
-      case 2: hipLaunchKernelGGL((gemm_bf16_n64<1, 0>), g64, dim3(NT), 2 * n64_stage(0), s, P); break;
-      case 1: hipLaunchKernelGGL((gemm_bf16_n64<0, 1>), g64, dim3(NT), 2 * n64_stage(1), s, P); break;
-      default: hipLaunchKernelGGL((gemm_bf16_n64<1, 1>), g64, dim3(NT), 2 * n64_stage(1), s, P); break;
+      case 0: ASR_N64(0, 0); break;
+      case 2: ASR_N64(1, 0); break;
+      case 1: ASR_N64(0, 1); break;
+      default: ASR_N64(1, 1); break;
     }
+#undef ASR_N64
   } else if (fast >= 0) {
     const int nst = g_small_tiles ? 2 : fast_stages();
     const size_t lds = (size_t)nst * 2 * FTILE;

@@ -827,6 +827,10 @@ class BLSTMLayerFn(torch.autograd.Function):
         dg_bf = (torch.empty(B, T, 8 * H, dtype=torch.bfloat16, device=dev) if cd == BF16
                  else None)
         done = False
+        # data parallel: every collective issued so far completes before this
+        # persistent recurrence starts (a kernel co-resident with the
+        # recurrence perturbs it)
+        notify_grad_event('pre_recurrence')
         if act.dtype == torch.float16:
             # packed fp16 activations of asr_lstm_forward_xh: the tagged-granule
             # backward reads them directly; otherwise they are unpacked to f32

@@ -6,7 +6,9 @@ natural bucket: its gradients are final once its weight-gradient GEMMs are
 enqueued (native_ops.BLSTMLayerFn.backward notifies 'grads').  The bucket's
 collective is issued right after the NEXT layer's backward recurrence has been
 enqueued (notification 'recurrence'), so on the device it starts when that
-persistent recurrence has finished and runs beside the GEMMs that follow it:
+persistent recurrence has finished and runs beside the GEMMs that follow it,
+and the compute stream waits for it before the recurrence after those GEMMs is
+enqueued (notification 'pre_recurrence'):
 
   * it never competes with a persistent recurrence for co-residency at launch
     (the recurrence pins one work-group per CU; a collective kernel that is
@@ -66,6 +68,7 @@ class GradBuckets(object):
         self.ready = [False] * len(self.order)
         self.next = 0          # next bucket (canonical order) to issue
         self.works = []
+        self.waited = 0
         self.issued_during_backward = 0
 
     @classmethod
@@ -85,7 +88,16 @@ class GradBuckets(object):
         return False
 
     def _on_event(self, event, arg=None):
-        if event == 'grads':
+        if event == 'pre_recurrence':
+            # the compute stream waits for every collective issued so far, so
+            # no RCCL kernel is co-resident with the persistent recurrence
+            # about to be enqueued (co-resident kernels perturb its results,
+            # DESIGN.md §5); the collectives ran beside the GEMMs that follow
+            # the previous recurrence, so the wait is normally already met
+            for w in self.works[self.waited:]:
+                w.wait()
+            self.waited = len(self.works)
+        elif event == 'grads':
             start = (arg[0].data_ptr() - self.base) // self.es
             i = self.by_start.get(start)
             if i is not None:
@@ -116,6 +128,7 @@ class GradBuckets(object):
             self.next += 1
         for a, b in self.rest:
             self._issue(a, b)
-        for w in self.works:
+        for w in self.works[self.waited:]:
             w.wait()
         self.works = []
+        self.waited = 0

@@ -35,6 +35,7 @@ class _LayerFn(torch.autograd.Function):
         x, w = ctx.saved_tensors
         y = torch.tanh(x @ w.t())
         dz = dy * (1 - y * y)
+        native_ops.notify_grad_event('pre_recurrence')
         native_ops.notify_grad_event('recurrence')
         for g in ctx.gviews:
             g.add_(dz.t() @ x)

@@ -317,8 +317,9 @@ def test_wgrad_side_stream_matches_main_stream(mode, cuda_dev, monkeypatch):
             monkeypatch.setenv('ASR_OVERLAP_WGRAD', m)
             native_ops.recurrence_status(cuda_dev)             # clear
             model.zero_grad()
-            ev = []
-            native_ops.set_grad_ready_hook(lambda e, arg=None: ev.append(e))
+            ev, pre = [], []
+            native_ops.set_grad_ready_hook(
+                lambda e, arg=None: ev.append(e) if e != 'pre_recurrence' else pre.append(e))
             try:
                 loss = model(xs, ys, x_lens, y_lens)
                 loss.backward()
@@ -329,6 +330,7 @@ def test_wgrad_side_stream_matches_main_stream(mode, cuda_dev, monkeypatch):
             grads[m] = {k: p.grad.detach().cpu().numpy().copy()
                         for k, p in model.named_parameters()}
             events[m] = ev
+            assert len(pre) == 3     # one before every backward recurrence
     finally:
         native_ops.set_compute_dtype('fp32')
     # gradient-ready notifications (DP buckets): every layer above the lowest is

@@ -155,9 +155,9 @@ def test_vgg_bf16_fast_path_vs_oracle(cuda_dev):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('fast', ['1', '0'])
+@pytest.mark.parametrize('fast,n64st', [('1', '2'), ('1', '3'), ('0', '2')])
 @pytest.mark.parametrize('Ci,Co', [(64, 64), (64, 128), (128, 128)])
-def test_tap_gemm_conv_exact(fast, Ci, Co, cuda_dev, monkeypatch):
+def test_tap_gemm_conv_exact(fast, n64st, Ci, Co, cuda_dev, monkeypatch):
     """The three tap-addressed GEMMs of a 3x3 conv layer (forward, input
     gradient, weight gradient incl. split-K over the pixels) on small-integer
     bf16 operands, where bf16 MFMA with f32 accumulation is exact: bit-equal to
@@ -165,10 +165,11 @@ def test_tap_gemm_conv_exact(fast, Ci, Co, cuda_dev, monkeypatch):
     the generic kernel."""
     from pytorch_end2end_speech_recognition_amd import native_ops as ops
     monkeypatch.setenv('ASR_GEMM_FAST', fast)
+    monkeypatch.setenv('ASR_GEMM_N64_STAGES', n64st)   # 256 x 64 kernel: double buffer / ring
     ops.set_compute_dtype('bf16')
     try:
         rng = np.random.RandomState(Ci + Co)
-        B, T, F = 2, 37, 14
+        B, T, F = 2, 101, 30   # M = B (T+2)(F+2) >= 4096: the 256 x 64 kernel takes N = 64
         Fn = torch.nn.functional
         x = rng.randint(-3, 4, (B, Ci, F, T)).astype(np.float64)          # NCHW, H = F, W = T
         w = rng.randint(-2, 3, (Co, Ci, 3, 3)).astype(np.float64)

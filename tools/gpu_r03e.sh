@@ -6,4 +6,4 @@ run() {  # name, env...
   echo "== $name rc=$rc"; grep "dx\|diag" gpurun_out/r03e_$name.log
   return $rc
 }
-run spin DIAG_WHH=0.03 ASR_DIAG_SPIN=200 && run spin_b DIAG_WHH=0.03 ASR_DIAG_SPIN=200
+run nosplit DIAG_WHH=0.03 ASR_GEMM_NOSPLIT=1 && run nosplit_b DIAG_WHH=0.03 ASR_GEMM_NOSPLIT=1 && run nosplit_scr DIAG_WHH=0.03 ASR_GEMM_NOSPLIT=1 ASR_DIAG_WGRAD_SCRATCH=1
