@@ -153,6 +153,10 @@ typedef struct {
    * 1 / (1 - drop_p)): dropout's backward fused into the producing GEMM. */
   float drop_p;
   unsigned long long drop_seed;
+  /* ASR_DT_F32 (0, the default of a zeroed struct) or ASR_DT_BF16: C is
+   * written as bf16 (bf16 compute, beta 0; the product is not split over K;
+   * the 128 x 128 / 256 x 64 / generic kernels). */
+  int c_dtype;
 } asr_gemm_t;
 
 int asr_gemm(const asr_gemm_t* problems, int nprob, int compute_dtype, void* stream);
@@ -622,7 +626,8 @@ int asr_conv3x3_c1_forward(const void* x, int x_dtype, int cstride, int B, int T
  * VGG layer, encoders/cnn.py:124-165), each value rounded to bf16 first when
  * round_bf16 (the bf16 operand's values); Co / 4 must divide 256. */
 int asr_conv3x3_c1_forward_xs(const float* xs, int round_bf16, int B, int T, int F, int Co,
-                              const float* w, const float* bias, float* z, void* stream);
+                              const float* w, const float* bias, void* z, int z_dtype,
+                              void* stream);
 int asr_conv_direct_dgrad(const float* dz, int B, int T, int F, int Ci, int Co, const float* w,
                           float* dx, void* stream);
 size_t asr_conv_direct_wgrad_workspace_bytes(int B, int T, int F, int Ci, int Co);
@@ -653,6 +658,22 @@ int asr_vgg_block_backward_ex(const float* dnext, int flat, const float* z, int 
                               const float* bn_rstd, float* dgamma, float* dbeta, float drop,
                               unsigned long long seed, void* dz, int dz_dtype, float* dbias,
                               void* workspace, size_t ws_bytes, void* stream);
+/* asr_vgg_block_forward / asr_vgg_block_backward_ex with the conv output z of
+ * dtype z_dtype (ASR_DT_F32 or ASR_DT_BF16, C % 4 == 0): in bf16 mode the
+ * convolution GEMMs write z as bf16 (asr_gemm_t.c_dtype), halving its
+ * write and its two reads (ReLU + pool forward, ReLU mask backward). */
+int asr_vgg_block_forward_z(const void* z, int z_dtype, int B, int T, int F, int C, int pt,
+                            int pf, int ceil_mode, float* P, uint8_t* slot, const float* gamma,
+                            const float* beta, float* run_mean, float* run_var, int training,
+                            float momentum, float eps, float* bn_mean, float* bn_rstd, float drop,
+                            unsigned long long seed, void* out, int out_dtype, int flat,
+                            void* workspace, size_t ws_bytes, void* stream);
+int asr_vgg_block_backward_z(const float* dnext, int flat, const void* z, int z_dtype, int B,
+                             int T, int F, int C, int pt, int pf, int ceil_mode, const float* P,
+                             const uint8_t* slot, const float* gamma, const float* bn_mean,
+                             const float* bn_rstd, float* dgamma, float* dbeta, float drop,
+                             unsigned long long seed, void* dz, int dz_dtype, float* dbias,
+                             void* workspace, size_t ws_bytes, void* stream);
 
 /* ----------------------------------------------------------- profiling
  * Sampled HIP-event timing of the recurrence step kernels on their own stream

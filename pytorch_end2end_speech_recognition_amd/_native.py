@@ -52,7 +52,7 @@ SIGNATURES = {
     'asr_colsum_accumulate': (c_int, [c_vp, c_ll, c_int, c_int, c_float, c_vp, c_vp, c_vp, c_size,
                                       c_vp]),
     'asr_conv3x3_c1_forward_xs': (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp,
-                                          c_vp, c_vp]),
+                                          c_vp, c_int, c_vp]),
     'asr_conv3x3_c1_forward': (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp,
                                        c_vp, c_vp]),
     'asr_lstm_workspace_bytes': (c_size, [c_int, c_int, c_int, c_int]),
@@ -149,6 +149,14 @@ SIGNATURES = {
                                           c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                           c_float, ctypes.c_ulonglong, c_vp, c_int, c_vp, c_vp,
                                           c_size, c_vp]),
+    'asr_vgg_block_forward_z': (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                        c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_float,
+                                        c_float, c_vp, c_vp, c_float, ctypes.c_ulonglong, c_vp,
+                                        c_int, c_int, c_vp, c_size, c_vp]),
+    'asr_vgg_block_backward_z': (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int,
+                                         c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                         c_vp, c_float, ctypes.c_ulonglong, c_vp, c_int, c_vp, c_vp,
+                                         c_size, c_vp]),
     'asr_prof_begin': (c_int, [c_int]),
     'asr_prof_end': (c_int, [c_vp, c_vp, c_vp, c_int]),
     'asr_lstm_persist_status': (c_int, [c_vp, c_int, c_vp]),
@@ -209,7 +217,7 @@ class Gemm(ctypes.Structure):
                 ('bias2', c_vp), ('M', c_int), ('N', c_int), ('K', c_int), ('alpha', c_float),
                 ('beta', c_float), ('batch', c_int), ('batch_stride_a', c_ll),
                 ('batch_stride_b', c_ll), ('batch_stride_c', c_ll), ('drop_p', c_float),
-                ('drop_seed', ctypes.c_ulonglong)]
+                ('drop_seed', ctypes.c_ulonglong), ('c_dtype', c_int)]
 
 
 class NativeError(RuntimeError):

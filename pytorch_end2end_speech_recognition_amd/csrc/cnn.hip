@@ -141,11 +141,12 @@ __global__ void __launch_bounds__(CT) conv3x3_c1_fwd(const TX* __restrict__ x, i
 // One wave writes 4 pixels x 64 channels = 1 KB of contiguous z per store.
 constexpr int C1_FT = 4;
 
+template <typename TZ>
 __global__ void __launch_bounds__(CT) conv3x3_c1_fwd_xs(const float* __restrict__ xs, int T,
                                                         int F, int Co, int round_bf16,
                                                         const float* __restrict__ w,
                                                         const float* __restrict__ bias,
-                                                        float* __restrict__ z) {
+                                                        TZ* __restrict__ z) {
   extern __shared__ float sm[];
   float* xr = sm;                    // [C1_FT + 2][F + 2], zero halo
   const int ntile = (T + C1_FT - 1) / C1_FT;
@@ -191,7 +192,14 @@ __global__ void __launch_bounds__(CT) conv3x3_c1_fwd_xs(const float* __restrict_
         acc.w += wv.w * xv;
       }
     const long long p = ((long long)b * (T + 2) + t0 + r + 1) * W + f + 1;
-    *reinterpret_cast<float4*>(z + p * Co + c4) = acc;
+    if constexpr (sizeof(TZ) == 2) {   // bf16 z: one 8-B store
+      uint2 o;
+      o.x = (unsigned)f2bf(acc.x) | ((unsigned)f2bf(acc.y) << 16);
+      o.y = (unsigned)f2bf(acc.z) | ((unsigned)f2bf(acc.w) << 16);
+      *reinterpret_cast<uint2*>(z + p * Co + c4) = o;
+    } else {
+      *reinterpret_cast<float4*>(z + p * Co + c4) = acc;
+    }
   }
 }
 
@@ -274,6 +282,7 @@ template <>
 struct VecF<1> {
   float v[1];
   __device__ __forceinline__ void load(const float* p) { v[0] = *p; }
+  __device__ __forceinline__ void load(const uint16_t* p) { v[0] = bf2f(*p); }
   __device__ __forceinline__ void store(float* p) const { *p = v[0]; }
 };
 template <>
@@ -283,6 +292,11 @@ struct VecF<4> {
     const float4 x = *reinterpret_cast<const float4*>(p);
     v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
   }
+  __device__ __forceinline__ void load(const uint16_t* p) {   // four bf16 (8-B aligned)
+    const uint2 x = *reinterpret_cast<const uint2*>(p);
+    v[0] = bf2f((uint16_t)(x.x & 0xffffu)); v[1] = bf2f((uint16_t)(x.x >> 16));
+    v[2] = bf2f((uint16_t)(x.y & 0xffffu)); v[3] = bf2f((uint16_t)(x.y >> 16));
+  }
   __device__ __forceinline__ void store(float* p) const {
     *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
   }
@@ -291,8 +305,8 @@ struct VecF<4> {
 // P[b][t'][f'][c] = max over the window of relu(z); slot = argmax in torch's
 // scan order (freq outer, time inner; first maximum wins).  V channels per
 // thread (V = 4 when C % 4 == 0).
-template <int V>
-__global__ void __launch_bounds__(CT) post_fwd(const float* __restrict__ z, int B, int T, int F,
+template <int V, typename TZ = float>
+__global__ void __launch_bounds__(CT) post_fwd(const TZ* __restrict__ z, int B, int T, int F,
                                                int C, Pool pl, float* __restrict__ P,
                                                uint8_t* __restrict__ slot,
                                                float* __restrict__ mpart) {
@@ -593,10 +607,10 @@ __global__ void bn_bwd_finalize(const float* __restrict__ sums, int C, float* __
 // bias gradient before its fixed-order sum over blocks -- so dZ itself can be
 // a bf16 GEMM operand (C divides the block size: a thread's channels are the
 // same in every grid-stride iteration).
-template <typename TO, int V>
+template <typename TO, int V, typename TZ = float>
 __global__ void __launch_bounds__(CT) post_bwd(const float* __restrict__ dnext,
                                                const float* __restrict__ P,
-                                               const float* __restrict__ z,
+                                               const TZ* __restrict__ z,
                                                const uint8_t* __restrict__ slot, int B, int T,
                                                int F, int C, Pool pl, int flat, Affine af,
                                                const float* __restrict__ sums,
@@ -639,7 +653,10 @@ __global__ void __launch_bounds__(CT) post_bwd(const float* __restrict__ dnext,
         f = px.fo * pl.pf + sl / pl.pt;
       }
       const long long p = pad_row(px.b, t, f, T, F) * C + c + j;
-      const float v = z[p] > 0.f ? g.v[j] : 0.f;
+      float zp;
+      if constexpr (sizeof(TZ) == 2) zp = bf2f(z[p]);
+      else zp = z[p];
+      const float v = zp > 0.f ? g.v[j] : 0.f;
       bacc[j] += v;
       if constexpr (sizeof(TO) == 2) dz[p] = f2bf(v);
       else dz[p] = v;
@@ -668,10 +685,10 @@ __global__ void __launch_bounds__(CT) post_bwd(const float* __restrict__ dnext,
 // time (554 us at the first pooled vgg_hier layer).  The window's gradient is
 // recomputed by each of its pixels (dnext / P / slot are a quarter of z's
 // size and come from the cache).  Bias partials as in post_bwd.
-template <typename TO>
+template <typename TO, typename TZ = float>
 __global__ void __launch_bounds__(CT) post_bwd_full(const float* __restrict__ dnext,
                                                     const float* __restrict__ P,
-                                                    const float* __restrict__ z,
+                                                    const TZ* __restrict__ z,
                                                     const uint8_t* __restrict__ slot, int B, int T,
                                                     int F, int C, Pool pl, int flat, Affine af,
                                                     const float* __restrict__ sums,
@@ -943,8 +960,8 @@ extern "C" int asr_conv3x3_c1_forward(const void* x, int x_dtype, int cstride, i
 // bf16 first when round_bf16: the values of the bf16 padded operand).
 // Co % 4 == 0 and 256 % (Co / 4) == 0.
 extern "C" int asr_conv3x3_c1_forward_xs(const float* xs, int round_bf16, int B, int T, int F,
-                                         int Co, const float* w, const float* bias, float* z,
-                                         void* stream) {
+                                         int Co, const float* w, const float* bias, void* z,
+                                         int z_dtype, void* stream) {
   ASR_REQUIRE(xs && w && z && B > 0 && T > 0 && F > 0, ASR_ERR_ARG,
               "conv3x3_c1_forward_xs: bad args");
   ASR_REQUIRE(Co > 0 && Co % 4 == 0 && CT % (Co / 4) == 0, ASR_ERR_UNSUPPORTED,
@@ -955,8 +972,12 @@ extern "C" int asr_conv3x3_c1_forward_xs(const float* xs, int round_bf16, int B,
   ASR_REQUIRE(lds <= 64 * 1024, ASR_ERR_UNSUPPORTED, "conv3x3_c1_forward_xs: F too large");
   const long long nwg = (long long)B * ((T + C1_FT - 1) / C1_FT);
   ASR_REQUIRE(nwg < (1LL << 31), ASR_ERR_UNSUPPORTED, "conv3x3_c1_forward_xs: grid too large");
-  hipLaunchKernelGGL(conv3x3_c1_fwd_xs, dim3((unsigned)nwg), dim3(CT), lds, (hipStream_t)stream, xs,
-                     T, F, Co, round_bf16, w, bias, z);
+  if (z_dtype == ASR_DT_BF16)
+    hipLaunchKernelGGL(conv3x3_c1_fwd_xs<uint16_t>, dim3((unsigned)nwg), dim3(CT), lds,
+                       (hipStream_t)stream, xs, T, F, Co, round_bf16, w, bias, (uint16_t*)z);
+  else
+    hipLaunchKernelGGL(conv3x3_c1_fwd_xs<float>, dim3((unsigned)nwg), dim3(CT), lds,
+                       (hipStream_t)stream, xs, T, F, Co, round_bf16, w, bias, (float*)z);
   ASR_LAUNCH_CHECK();
   return ASR_OK;
 }
@@ -1048,6 +1069,14 @@ extern "C" size_t asr_vgg_block_workspace_bytes(int B, int To, int Fo, int C) {
 // BN.  training: batch statistics and running-stat update, else running stats.
 // out: next layer input, padded rows of (T', F') (out_dtype f32 / bf16; the
 // caller zeroes it) or, flat, [B][T'][F'][C] f32.
+extern "C" int asr_vgg_block_forward_z(const void* z, int z_dtype, int B, int T, int F, int C,
+                                       int pt, int pf, int ceil_mode, float* P, uint8_t* slot,
+                                       const float* gamma, const float* beta, float* run_mean,
+                                       float* run_var, int training, float momentum, float eps,
+                                       float* bn_mean, float* bn_rstd, float drop,
+                                       unsigned long long seed, void* out, int out_dtype, int flat,
+                                       void* workspace, size_t ws_bytes, void* stream);
+
 extern "C" int asr_vgg_block_forward(const float* z, int B, int T, int F, int C, int pt, int pf,
                                      int ceil_mode, float* P, uint8_t* slot, const float* gamma,
                                      const float* beta, float* run_mean, float* run_var,
@@ -1055,6 +1084,20 @@ extern "C" int asr_vgg_block_forward(const float* z, int B, int T, int F, int C,
                                      float* bn_rstd, float drop, unsigned long long seed,
                                      void* out, int out_dtype, int flat, void* workspace,
                                      size_t ws_bytes, void* stream) {
+  return asr_vgg_block_forward_z(z, ASR_DT_F32, B, T, F, C, pt, pf, ceil_mode, P, slot, gamma,
+                                 beta, run_mean, run_var, training, momentum, eps, bn_mean,
+                                 bn_rstd, drop, seed, out, out_dtype, flat, workspace, ws_bytes,
+                                 stream);
+}
+
+// z_dtype ASR_DT_BF16: the conv output z is bf16 (P and the statistics stay f32)
+extern "C" int asr_vgg_block_forward_z(const void* z, int z_dtype, int B, int T, int F, int C,
+                                       int pt, int pf, int ceil_mode, float* P, uint8_t* slot,
+                                       const float* gamma, const float* beta, float* run_mean,
+                                       float* run_var, int training, float momentum, float eps,
+                                       float* bn_mean, float* bn_rstd, float drop,
+                                       unsigned long long seed, void* out, int out_dtype, int flat,
+                                       void* workspace, size_t ws_bytes, void* stream) {
   ASR_REQUIRE(z && P && out && B > 0 && T > 0 && F > 0 && C > 0, ASR_ERR_ARG,
               "vgg_block_forward: bad args");
   ASR_REQUIRE(!pt || slot, ASR_ERR_ARG, "vgg_block_forward: pooling needs slot");
@@ -1081,12 +1124,18 @@ extern "C" int asr_vgg_block_forward(const float* z, int B, int T, int F, int C,
   // fused: at most 1024 blocks, so the ordered partial sum (one thread per
   // column phase) stays short -- 8192 partials took 1 ms / step at vgg_hier
   const int fgrid = fused_mean ? std::min(post_grid(nr, C), 1024) : post_grid(nr, C);
-  if (v4)
-    hipLaunchKernelGGL(post_fwd<4>, dim3(fgrid), dim3(CT), 0, s, z, B, T, F, C, pl, P, slot,
-                       mpart);
+  const bool zb = z_dtype == ASR_DT_BF16;
+  ASR_REQUIRE(!zb || (v4 && ((uintptr_t)z & 7) == 0), ASR_ERR_UNSUPPORTED,
+              "vgg_block_forward: bf16 z needs C % 4 == 0 and 8-B alignment");
+  if (zb)
+    hipLaunchKernelGGL((post_fwd<4, uint16_t>), dim3(fgrid), dim3(CT), 0, s, (const uint16_t*)z, B,
+                       T, F, C, pl, P, slot, mpart);
+  else if (v4)
+    hipLaunchKernelGGL(post_fwd<4>, dim3(fgrid), dim3(CT), 0, s, (const float*)z, B, T, F, C, pl,
+                       P, slot, mpart);
   else
-    hipLaunchKernelGGL(post_fwd<1>, dim3(post_grid(nr, C)), dim3(CT), 0, s, z, B, T, F, C, pl, P,
-                       slot, (float*)nullptr);
+    hipLaunchKernelGGL(post_fwd<1>, dim3(post_grid(nr, C)), dim3(CT), 0, s, (const float*)z, B, T,
+                       F, C, pl, P, slot, (float*)nullptr);
   ASR_LAUNCH_CHECK();
   Affine af{nullptr, nullptr, nullptr, nullptr, drop, seed};
   if (gamma) {
@@ -1172,6 +1221,15 @@ extern "C" int asr_vgg_block_backward(const float* dnext, int flat, const float*
 
 // ... and dbias (nullable) += the conv bias gradient, sum of dZ per channel
 // (formed from the f32 values before dZ is stored, in a fixed order).
+extern "C" int asr_vgg_block_backward_z(const float* dnext, int flat, const void* z,
+                                        int z_dtype, int B, int T, int F, int C, int pt, int pf,
+                                        int ceil_mode, const float* P, const uint8_t* slot,
+                                        const float* gamma, const float* bn_mean,
+                                        const float* bn_rstd, float* dgamma, float* dbeta,
+                                        float drop, unsigned long long seed, void* dz,
+                                        int dz_dtype, float* dbias, void* workspace,
+                                        size_t ws_bytes, void* stream);
+
 extern "C" int asr_vgg_block_backward_ex(const float* dnext, int flat, const float* z, int B,
                                          int T, int F, int C, int pt, int pf, int ceil_mode,
                                          const float* P, const uint8_t* slot, const float* gamma,
@@ -1180,6 +1238,20 @@ extern "C" int asr_vgg_block_backward_ex(const float* dnext, int flat, const flo
                                          unsigned long long seed, void* dz, int dz_dtype,
                                          float* dbias, void* workspace, size_t ws_bytes,
                                          void* stream) {
+  return asr_vgg_block_backward_z(dnext, flat, z, ASR_DT_F32, B, T, F, C, pt, pf, ceil_mode, P,
+                                  slot, gamma, bn_mean, bn_rstd, dgamma, dbeta, drop, seed, dz,
+                                  dz_dtype, dbias, workspace, ws_bytes, stream);
+}
+
+// z_dtype ASR_DT_BF16: the saved conv output z is bf16 (the ReLU mask read back)
+extern "C" int asr_vgg_block_backward_z(const float* dnext, int flat, const void* z,
+                                        int z_dtype, int B, int T, int F, int C, int pt, int pf,
+                                        int ceil_mode, const float* P, const uint8_t* slot,
+                                        const float* gamma, const float* bn_mean,
+                                        const float* bn_rstd, float* dgamma, float* dbeta,
+                                        float drop, unsigned long long seed, void* dz,
+                                        int dz_dtype, float* dbias, void* workspace,
+                                        size_t ws_bytes, void* stream) {
   ASR_REQUIRE(dnext && z && P && dz && B > 0 && T > 0 && F > 0 && C > 0, ASR_ERR_ARG,
               "vgg_block_backward: bad args");
   const Pool pl = make_pool(T, F, pt, pf, ceil_mode);
@@ -1225,27 +1297,44 @@ extern "C" int asr_vgg_block_backward_ex(const float* dnext, int flat, const flo
     ASR_LAUNCH_CHECK();
   }
   const char* pfe = getenv("ASR_VGG_POST_FULL");   // A/B: full-resolution dz pass
+  const bool zb = z_dtype == ASR_DT_BF16;
   const bool full = v4 && !(pfe && pfe[0] == '0') && ((uintptr_t)dz & 15) == 0 &&
-                    ((uintptr_t)z & 15) == 0;
-  if (full && dz_dtype == ASR_DT_BF16) {
-    hipLaunchKernelGGL(post_bwd_full<uint16_t>, dim3(pgrid), dim3(CT), 0, s, dnext, P, z, slot, B,
+                    ((uintptr_t)z & (zb ? 7 : 15)) == 0;
+  ASR_REQUIRE(!zb || v4, ASR_ERR_UNSUPPORTED, "vgg_block_backward: bf16 z needs C % 4 == 0");
+  const float* zf = (const float*)z;
+  const uint16_t* zh = (const uint16_t*)z;
+  if (zb) {
+    if (full && dz_dtype == ASR_DT_BF16)
+      hipLaunchKernelGGL((post_bwd_full<uint16_t, uint16_t>), dim3(pgrid), dim3(CT), 0, s, dnext,
+                         P, zh, slot, B, T, F, C, pl, flat, af, sums, (uint16_t*)dz, bpart);
+    else if (full)
+      hipLaunchKernelGGL((post_bwd_full<float, uint16_t>), dim3(pgrid), dim3(CT), 0, s, dnext, P,
+                         zh, slot, B, T, F, C, pl, flat, af, sums, (float*)dz, bpart);
+    else if (dz_dtype == ASR_DT_BF16)
+      hipLaunchKernelGGL((post_bwd<uint16_t, 4, uint16_t>), dim3(pgrid), dim3(CT), 0, s, dnext, P,
+                         zh, slot, B, T, F, C, pl, flat, af, sums, (uint16_t*)dz, bpart);
+    else
+      hipLaunchKernelGGL((post_bwd<float, 4, uint16_t>), dim3(pgrid), dim3(CT), 0, s, dnext, P,
+                         zh, slot, B, T, F, C, pl, flat, af, sums, (float*)dz, bpart);
+  } else if (full && dz_dtype == ASR_DT_BF16) {
+    hipLaunchKernelGGL(post_bwd_full<uint16_t>, dim3(pgrid), dim3(CT), 0, s, dnext, P, zf, slot, B,
                        T, F, C, pl, flat, af, sums, (uint16_t*)dz, bpart);
   } else if (full) {
-    hipLaunchKernelGGL(post_bwd_full<float>, dim3(pgrid), dim3(CT), 0, s, dnext, P, z, slot, B, T,
+    hipLaunchKernelGGL(post_bwd_full<float>, dim3(pgrid), dim3(CT), 0, s, dnext, P, zf, slot, B, T,
                        F, C, pl, flat, af, sums, (float*)dz, bpart);
   } else if (dz_dtype == ASR_DT_BF16) {
     if (v4)
-      hipLaunchKernelGGL((post_bwd<uint16_t, 4>), dim3(pgrid), dim3(CT), 0, s, dnext, P, z, slot,
+      hipLaunchKernelGGL((post_bwd<uint16_t, 4>), dim3(pgrid), dim3(CT), 0, s, dnext, P, zf, slot,
                          B, T, F, C, pl, flat, af, sums, (uint16_t*)dz, bpart);
     else
-      hipLaunchKernelGGL((post_bwd<uint16_t, 1>), dim3(pgrid), dim3(CT), 0, s, dnext, P, z, slot,
+      hipLaunchKernelGGL((post_bwd<uint16_t, 1>), dim3(pgrid), dim3(CT), 0, s, dnext, P, zf, slot,
                          B, T, F, C, pl, flat, af, sums, (uint16_t*)dz, bpart);
   } else {
     if (v4)
-      hipLaunchKernelGGL((post_bwd<float, 4>), dim3(pgrid), dim3(CT), 0, s, dnext, P, z, slot, B,
+      hipLaunchKernelGGL((post_bwd<float, 4>), dim3(pgrid), dim3(CT), 0, s, dnext, P, zf, slot, B,
                          T, F, C, pl, flat, af, sums, (float*)dz, bpart);
     else
-      hipLaunchKernelGGL((post_bwd<float, 1>), dim3(pgrid), dim3(CT), 0, s, dnext, P, z, slot, B,
+      hipLaunchKernelGGL((post_bwd<float, 1>), dim3(pgrid), dim3(CT), 0, s, dnext, P, zf, slot, B,
                          T, F, C, pl, flat, af, sums, (float*)dz, bpart);
   }
   ASR_LAUNCH_CHECK();

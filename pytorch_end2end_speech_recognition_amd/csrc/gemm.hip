@@ -62,6 +62,7 @@ struct Problem {
   int M, N, K;
   float alpha, beta;
   int batch;
+  int c_bf16;   // C written as bf16 (beta 0, no split-K, store_acc kernels); fills padding
   long long sA, sB, sC;
   int ksplit;   // > 1: split-K into f32 slabs [ksplit][M][N], reduced by splitk_reduce
   int kchunk;   // K elements per split (multiple of BK)
@@ -287,7 +288,10 @@ __device__ __forceinline__ void store_acc(const Problem& pr, const f32x4 (&acc)[
         if (pr.bias2) v += pr.bias2[n];
         if (pr.beta != 0.f) v += pr.beta * crow[n];
         if (pr.drop_p > 0.f) v *= drop_scale(pr, off + n);
-        crow[n] = v;
+        if (pr.c_bf16)   // bf16 C (beta 0): element offsets of the same map, 2-B stores
+          ((uint16_t*)pr.c.base)[off + n] = f2bf(v);
+        else
+          crow[n] = v;
       }
     }
   }
@@ -307,7 +311,7 @@ __global__ void __launch_bounds__(NT) gemm_kernel(Params P) {
   if (zb > 0) {  // batched product: shift every base by its batch stride
     pr.a.map.base = (const char*)pr.a.map.base + zb * pr.sA * (pr.a.dtype == ASR_DT_F32 ? 4 : 2);
     pr.b.map.base = (const char*)pr.b.map.base + zb * pr.sB * (pr.b.dtype == ASR_DT_F32 ? 4 : 2);
-    pr.c.base = (const char*)pr.c.base + zb * pr.sC * 4;
+    pr.c.base = (const char*)pr.c.base + zb * pr.sC * (pr.c_bf16 ? 2 : 4);
   }
   const int gm = (pr.M + BM - 1) / BM, gn = (pr.N + BN - 1) / BN;
   const int nwg = gm * gn;
@@ -659,7 +663,7 @@ __global__ void __launch_bounds__(NT) gemm_bf16_fast(Params P) {
     pr.b.map.base = (const char*)pr.b.map.base + zb * pr.sB * 2;
     pr.a.bytes -= zb * pr.sA * 2;
     pr.b.bytes -= zb * pr.sB * 2;
-    pr.c.base = (const char*)pr.c.base + zb * pr.sC * 4;
+    pr.c.base = (const char*)pr.c.base + zb * pr.sC * (pr.c_bf16 ? 2 : 4);
   }
   const int gm = (pr.M + BM - 1) / BM, gn = (pr.N + BN - 1) / BN;
   const int nwg = gm * gn;
@@ -773,7 +777,7 @@ __global__ void __launch_bounds__(NT) gemm_bf16_n64(Params P) {
     pr.b.map.base = (const char*)pr.b.map.base + zb * pr.sB * 2;
     pr.a.bytes -= zb * pr.sA * 2;
     pr.b.bytes -= zb * pr.sB * 2;
-    pr.c.base = (const char*)pr.c.base + zb * pr.sC * 4;
+    pr.c.base = (const char*)pr.c.base + zb * pr.sC * (pr.c_bf16 ? 2 : 4);
   }
   const int gm = (pr.M + N64_BM - 1) / N64_BM;
   const int nsplit = pr.ksplit > 1 ? pr.ksplit : 1;
@@ -931,7 +935,7 @@ gemm_bf16_kk256(Params P) {
     pr.b.map.base = (const char*)pr.b.map.base + zb * pr.sB * 2;
     pr.a.bytes -= zb * pr.sA * 2;
     pr.b.bytes -= zb * pr.sB * 2;
-    pr.c.base = (const char*)pr.c.base + zb * pr.sC * 4;
+    pr.c.base = (const char*)pr.c.base + zb * pr.sC * (pr.c_bf16 ? 2 : 4);
   }
   const int gm = (pr.M + BT2 - 1) / BT2, gn = (pr.N + BT2 - 1) / BT2;
   const int nwg = gm * gn;
@@ -1297,7 +1301,7 @@ gemm_bf16_8w(Params P) {
     pr.b.map.base = (const char*)pr.b.map.base + zb * pr.sB * 2;
     pr.a.bytes -= zb * pr.sA * 2;
     pr.b.bytes -= zb * pr.sB * 2;
-    pr.c.base = (const char*)pr.c.base + zb * pr.sC * 4;
+    pr.c.base = (const char*)pr.c.base + zb * pr.sC * (pr.c_bf16 ? 2 : 4);
   }
   const int gm = (pr.M + T8 - 1) / T8, gn = (pr.N + T8 - 1) / T8;
   const int nwg = gm * gn;
@@ -1521,7 +1525,7 @@ gemm_bf16_8r(Params P) {
     pr.b.map.base = (const char*)pr.b.map.base + zb * pr.sB * 2;
     pr.a.bytes -= zb * pr.sA * 2;
     pr.b.bytes -= zb * pr.sB * 2;
-    pr.c.base = (const char*)pr.c.base + zb * pr.sC * 4;
+    pr.c.base = (const char*)pr.c.base + zb * pr.sC * (pr.c_bf16 ? 2 : 4);
   }
   const int gm = (pr.M + T8 - 1) / T8, gn = (pr.N + T8 - 1) / T8;
   const int nwg = gm * gn;
@@ -1802,7 +1806,8 @@ SplitPlan plan_split(const asr_gemm_t* g, int nprob) {
     // a few-tile dW next to a many-tile dX still gets its own K split
     const int tiles = ceil_div(g[i].M, BM) * ceil_div(g[i].N, BN);
     int ks = 1;
-    if (!nosplit && g[i].batch <= 1 && tiles > 0 && tiles < 512 && g[i].K >= 1024) {
+    if (!nosplit && g[i].c_dtype != ASR_DT_BF16 && g[i].batch <= 1 && tiles > 0 &&
+        tiles < 512 && g[i].K >= 1024) {
       // a few-tile, long-K product (the decoder / projection weight gradients,
       // K = B*S or B*T) is latency-bound per work-group: chunks >= 128
       ks = min(ceil_div(1024, tiles), g[i].K / 128);
@@ -1882,6 +1887,8 @@ int fast_modes(const asr_gemm_t* g, const Params& P) {
 // but the whole step did not move beyond noise, and the 4x320 / VGG configs
 // ran 0.2-0.5 ms/step slower with it (fewer work-groups per product).
 bool kk256_ok(const asr_gemm_t* g, int nprob) {
+  for (int i = 0; i < nprob; ++i)
+    if (g[i].c_dtype == ASR_DT_BF16) return false;   // its own f32 epilogue
   const char* e = getenv("ASR_GEMM_KK256");
   if (!(e && e[0] == '1')) return false;
   for (int i = 0; i < nprob; ++i)
@@ -1927,6 +1934,7 @@ bool big8_ok(const asr_gemm_t* g, int nprob) {
   if (e && e[0] == '0') return false;
   if (g_small_tiles) return false;
   for (int i = 0; i < nprob; ++i) {
+    if (g[i].c_dtype == ASR_DT_BF16) return false;   // its own f32 epilogue
     if (g[i].M < T8 || g[i].N < T8) return false;
     if (g[i].a.tap_group || g[i].b.tap_group) return false;     // taps: 128 x 128 kernel
     // K-mode operands advance their (utterance, frame) pair by 64 k-rows per tile
@@ -1967,6 +1975,11 @@ int gemm_launch_own(const asr_gemm_t* problems, int nprob, int compute_dtype, vo
     ASR_REQUIRE(g.drop_p == 0.f || g.batch <= 1, ASR_ERR_ARG, "gemm: dropout on a batched product");
     p.drop_p = g.drop_p;
     p.drop_seed = g.drop_seed;
+    ASR_REQUIRE(g.c_dtype == ASR_DT_F32 || g.c_dtype == ASR_DT_BF16, ASR_ERR_ARG,
+                "gemm: C dtype %d", g.c_dtype);
+    p.c_bf16 = g.c_dtype == ASR_DT_BF16;
+    ASR_REQUIRE(!p.c_bf16 || (g.beta == 0.f && compute_dtype == ASR_DT_BF16), ASR_ERR_ARG,
+                "gemm: bf16 C needs beta 0 and bf16 compute");
     p.batch = g.batch > 1 ? g.batch : 1;
     p.sA = g.batch_stride_a;
     p.sB = g.batch_stride_b;

@@ -97,12 +97,14 @@ def gemm_problem(a, b, c, c_map, M, N_, K, alpha=1.0, beta=0.0, bias=None, bias2
                  batch=1, batch_strides=(0, 0, 0), drop=None):
     """drop=(p, seed): the written values get asr_dropout's mask for their
     element offsets from c (dropout's backward fused into the product)."""
-    return N.Gemm(a, b, c.data_ptr() + 4 * c_offset, c_map,
+    c_bf16 = c.dtype == torch.bfloat16     # bf16 C: written as bf16 (beta 0, no split-K)
+    return N.Gemm(a, b, c.data_ptr() + c.element_size() * c_offset, c_map,
                   bias.data_ptr() if bias is not None else None,
                   bias2.data_ptr() if bias2 is not None else None, int(M), int(N_), int(K),
                   float(alpha), float(beta), int(batch), int(batch_strides[0]),
                   int(batch_strides[1]), int(batch_strides[2]),
-                  float(drop[0]) if drop else 0.0, int(drop[1]) if drop else 0)
+                  float(drop[0]) if drop else 0.0, int(drop[1]) if drop else 0,
+                  BF16 if c_bf16 else F32)
 
 
 def run_gemm(problems, device):
@@ -1578,7 +1580,15 @@ class VGGFn(torch.autograd.Function):
             w = sp['w']
             Co = w.shape[0]
             npad = B * (cT + 2) * (cF + 2)
-            z = torch.empty(npad, Co, **f32)
+            # bf16 mode: the GEMM / stencil layers write the conv output as bf16
+            # (read twice more: ReLU + pool, and the ReLU mask in the backward)
+            c1_xs = (use_gemm[l] and cC == 1 and Co % 4 == 0 and 256 % (Co // 4) == 0 and
+                     os.environ.get('ASR_VGG_C1_DIRECT', '1') != '0' and
+                     os.environ.get('ASR_VGG_C1_XS', '1') != '0')
+            z_bf = (cd == BF16 and Co % 4 == 0 and (c1_xs or not (cC == 1)) and use_gemm[l] and
+                    os.environ.get('ASR_VGG_Z_BF16', '1') != '0')
+            z = torch.empty(npad, Co, dtype=torch.bfloat16 if z_bf else torch.float32,
+                            device=dev)
             if not use_gemm[l]:
                 N.call('asr_conv_direct_forward', N.ptr(x_op), B, cT, cF, cC, Co, N.ptr(w),
                        N.ptr(sp['b']), N.ptr(z), N.stream_handle(dev))
@@ -1586,11 +1596,12 @@ class VGGFn(torch.autograd.Function):
                 # one input channel: a direct stencil from channel 0 of the padded
                 # operand (the GEMM would run K = 144 for 9 useful taps); the
                 # backward still takes the weight-gradient GEMM over this operand
-                if 256 % (Co // 4) == 0 and os.environ.get('ASR_VGG_C1_XS', '1') != '0':
+                if c1_xs:
                     # from the raw features (contiguous rows; rounded to bf16 as the
                     # staged operand is in bf16 mode)
                     N.call('asr_conv3x3_c1_forward_xs', N.ptr(xs), int(cd == BF16), B, cT, cF, Co,
-                           N.ptr(w), N.ptr(sp['b']), N.ptr(z), N.stream_handle(dev))
+                           N.ptr(w), N.ptr(sp['b']), N.ptr(z), BF16 if z_bf else F32,
+                           N.stream_handle(dev))
                 else:
                     N.call('asr_conv3x3_c1_forward', N.ptr(x_op), cd, cCp, B, cT, cF, Co,
                            N.ptr(w), N.ptr(sp['b']), N.ptr(z), N.stream_handle(dev))
@@ -1622,11 +1633,11 @@ class VGGFn(torch.autograd.Function):
                 out_dt, flat = (cd if use_gemm[l + 1] else F32), 0
             nb = N.query('asr_vgg_block_workspace_bytes', B, To, Fo, Co)
             ws = _ws(nb, dev)
-            N.call('asr_vgg_block_forward', N.ptr(z), B, cT, cF, Co, pt, pf, ceil, N.ptr(P),
-                   N.ptr(slot), N.ptr(sp['gamma']), N.ptr(sp['beta']), N.ptr(sp['run_mean']),
-                   N.ptr(sp['run_var']), int(bool(training)), float(sp['momentum']),
-                   float(sp['eps']), N.ptr(mean), N.ptr(rstd), drop, seed, N.ptr(out), out_dt,
-                   flat, N.ptr(ws), nb, N.stream_handle(dev))
+            N.call('asr_vgg_block_forward_z', N.ptr(z), BF16 if z_bf else F32, B, cT, cF, Co, pt,
+                   pf, ceil, N.ptr(P), N.ptr(slot), N.ptr(sp['gamma']), N.ptr(sp['beta']),
+                   N.ptr(sp['run_mean']), N.ptr(sp['run_var']), int(bool(training)),
+                   float(sp['momentum']), float(sp['eps']), N.ptr(mean), N.ptr(rstd), drop, seed,
+                   N.ptr(out), out_dt, flat, N.ptr(ws), nb, N.stream_handle(dev))
             saved += [x_op, z, P, slot, mean, rstd]
             layers.append((cT, cF, cC, cCp, Co, pt, pf, ceil, drop, seed, use_gemm[l]))
             x_op, cT, cF, cC, cCp = out, To, Fo, Co, Co
@@ -1664,7 +1675,8 @@ class VGGFn(torch.autograd.Function):
             nb = N.query('asr_vgg_block_workspace_bytes', B, To, Fo, Co)
             ws = _ws(nb, dev)
             bn = sp['gamma'] is not None
-            N.call('asr_vgg_block_backward_ex', N.ptr(dnext), flat, N.ptr(z), B, cT, cF, Co, pt,
+            N.call('asr_vgg_block_backward_z', N.ptr(dnext), flat, N.ptr(z),
+                   BF16 if z.dtype == torch.bfloat16 else F32, B, cT, cF, Co, pt,
                    pf, ceil, N.ptr(P), N.ptr(slot), N.ptr(sp['gamma']), N.ptr(mean), N.ptr(rstd),
                    N.ptr(grad_buffer(sp['gamma']) if bn else None),
                    N.ptr(grad_buffer(sp['beta']) if bn else None), drop, seed, N.ptr(dz),
