@@ -268,6 +268,10 @@ int asr_lstm_backward_dgbf_h(const float* dy, const void* whh_f, const void* whh
                              float* db_ih, float* db_hh, void* workspace, size_t ws_bytes,
                              void* stream);
 int asr_lstm_unpack_act_h(const uint16_t* act_h, int B, int T, int H, float* act, void* stream);
+/* Diagnostics only (tools/buckets_diag.py, ASR_DIAG_SPIN): nwg work-groups of
+ * 256 threads that fill 64 KB of LDS with a pattern and check it `iters`
+ * times; mismatches are added to *bad (device int). */
+int asr_diag_lds_spin(int nwg, int iters, int* bad, void* stream);
 
 /* ------------------------------------------------------------ GRU layer
  * Replaces the packed nn.GRU(bidirectional=True) of
