@@ -1419,7 +1419,14 @@ gemm_bf16_8w(Params P) {
 //   counted vmcnt + barrier (k-tile t + 1 landed) -> read its B, A rows 0-63
 //   | MFMA rows 64-127
 // R-mode image [256 rows][32 k]: 64-B rows, 16-B chunk c of row r at slot
-// c ^ ((r >> 2) & 3) (conflict-free ds_read_b128 over the 16-row fragment);
+// c ^ swz8r(r) with swz8r = 0, 0, 3, 3 for (r >> 2) & 3 = 0..3.  A 64-B row
+// covers 16 of the 64 banks, so rows r and r + 4 share banks; ds_read_b128
+// serves a wave in four fixed 16-lane groups (MI355X_MICROARCH.md §LDS), and
+// each group's (row % 4, slot) pairs must be distinct: the round-2 swizzle
+// (r >> 2) & 3 put two lanes of every group on the same banks (PMC: 46 % of
+// the fwd product's LDS cycles were conflict cycles); this one clears all four
+// groups.  K-mode image [32 k][256 rows] as the 256 x 256 kernel's.
+__device__ __forceinline__ int swz8r(int r) { return ((r >> 3) & 1) * 3; }
 // K-mode image [32 k][256 rows] as the 256 x 256 kernel's.
 // ---------------------------------------------------------------------------
 constexpr int BKR = 32, NSLOT = 5;
@@ -1439,7 +1446,7 @@ __device__ __forceinline__ void stager_init(const Operand& op, StageR& st, int t
     const int blk = wave * 2 + i;          // 1 KB of the 16-KB image
     if (MODE == 0) {
       const int r = blk * 16 + (lane >> 2);
-      const int c = (lane & 3) ^ ((r >> 2) & 3);
+      const int c = (lane & 3) ^ swz8r(r);
       const int row = tile0 + r;
       long long off = row < nrows ? row_off_np(op.map, row) : -1;
       st.base[i] = off >= 0 ? (unsigned)(off * 2) : 0u;
@@ -1495,7 +1502,7 @@ template <int MODE>
 __device__ __forceinline__ bf16x8 fragr(const char* lds_tile, int rb, int lane) {
   if (MODE == 0) {
     const int r = lane & 15;
-    const unsigned lo = (unsigned)(r * 64 + (((lane >> 4) ^ ((r >> 2) & 3)) * 16));
+    const unsigned lo = (unsigned)(r * 64 + (((lane >> 4) ^ swz8r(r)) * 16));
     return __builtin_bit_cast(bf16x8, *(const u32x4_t*)(lds_tile + rb * 64 + lo));
   }
   return frag_k256(lds_tile, rb, 0, lane);
