@@ -210,10 +210,6 @@ __device__ __forceinline__ void xg_place(int WPG, int allow_local, int* hdr, int
 // never match the first use (bit 1).  Error <= 1 bf16 ulp on one value in four
 // of the recurrent input; y / ybf keep the plain values.
 __device__ __forceinline__ unsigned tag_bit(int step) { return (((unsigned)step >> 1) & 1u) ^ 1u; }
-// Second tag bit (LSB of the second value) of the two-bit tag: with both bits
-// the steps s, s-2, s-4, s-6 that share a buffer all carry different codes, so
-// a granule left over from step s-4 can never pass for step s.
-__device__ __forceinline__ unsigned tag_bit_hi(int step) { return (((unsigned)step >> 2) & 1u) ^ 1u; }
 __device__ __forceinline__ unsigned bf_with_lsb(float h, unsigned bit) {
   const unsigned t = __float_as_uint(h) >> 16;
   return (t & 1u) == bit ? t : t + 1u;
@@ -784,13 +780,13 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
 // A fragments (VGPRs): A[m][k] = W_hh[gaterow(k)][m] for output unit m (M block
 // mb = mw + 4 i) and local gate row k in [0, 64): gate k >> 4, unit u0 + (k & 15).
 // ---------------------------------------------------------------------------
-template <int R, int MB>
+template <int R, int MB, bool AH>
 __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
     int B, int T, int H, const int32_t* __restrict__ lens, const float* __restrict__ whh_f,
     const float* __restrict__ whh_r, const float* __restrict__ dy, float* __restrict__ act_dg,
     const float* __restrict__ cst, unsigned long long* pg, int* hdr,
     uint16_t* __restrict__ dgbf, float* __restrict__ dbpart, unsigned epoch, int allow_local,
-    int dg_f32, int io_pos, int dg_st16, int tag2, const h16x4* __restrict__ acth, int acq) {
+    int dg_f32, int io_pos, int dg_st16, const h16x4* __restrict__ acth) {
   constexpr int NPG = 256 / (2 * R);   // producer subsets swept in parallel
   __shared__ float red[NPG][R][XU + 1];
   __shared__ __attribute__((aligned(16))) uint16_t dgt[16][4 * XU + 8];
@@ -802,7 +798,6 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
   if (threadIdx.x == 0) s_dead = 0;
   xg_place(WPG, allow_local, hdr, s_pl, epoch);  // epoch: the launch's sequence number
   if (!s_pl[3]) return;
-  if (acq) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // diagnostics (ASR_XG_ACQ)
   const int grp = s_pl[0], mem = s_pl[1];
   const bool local = s_pl[2] != 0;  // granules carry a 1-bit step tag (tag_bit)
   const int dir = grp & 1, rg = grp >> 1;
@@ -830,9 +825,6 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
       XG_TR(q, 0, __builtin_amdgcn_s_memrealtime());
       if (q > 0) {
         const unsigned ebit = tag_bit(q - 1);
-        const unsigned ebit2 = tag2 == 1 ? tag_bit_hi(q - 1) : 0u;
-        const unsigned hmask = tag2 == 1 ? 1u : 0u;   // second tag bit checked only with tag2
-        const unsigned dmask = tag2 == 2 ? 1u : 0u;   // tag2 == 2: the tag in both dwords
         const long long base = ((long long)((q - 1) & 1) * G + grp) * WPG;
         float sm[8];
         nap(ndelay);
@@ -849,8 +841,6 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
                 (unsigned)((((base + w) * R + srow) * (long long)hq + (u0 >> 2) + 2 * sq) * 8);
             const u32x4 v = ld_sc1(rs, off);
             ok &= (int)((((v[0] ^ ebit) | (v[2] ^ ebit)) & 1u) == 0u);
-            ok &= (int)(((((v[0] >> 16) ^ ebit2) | ((v[2] >> 16) ^ ebit2)) & hmask) == 0u);
-            ok &= (int)((((v[1] ^ ebit) | (v[3] ^ ebit)) & dmask) == 0u);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
               sm[2 * e] += bf2f((uint16_t)(v[e] & 0xffffu));
@@ -898,7 +888,7 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
       const int tp = dir == 0 ? t - 1 : t + 1;
       const long long gb = ((long long)b * T + t) * 8 * H + (long long)dir * H4 + j;
       const long long si = ((long long)b * T + t) * 2 * H + (long long)dir * H + j;
-      if (acth) {   // one 8-B load of the four fp16 gates, converted when used
+      if constexpr (AH) {   // one 8-B load of the four fp16 gates, converted when used
         avh = acth[(((long long)b * T + t) * 2 + dir) * H + j];
       } else {
 #pragma unroll
@@ -961,7 +951,7 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
 #pragma unroll
           for (int p = 0; p < NPG; ++p) dh += red[p][row][unit];
         }
-        if (acth) {
+        if constexpr (AH) {
 #pragma unroll
           for (int k = 0; k < 4; ++k) av[k] = (float)avh[k];
         }
@@ -1037,7 +1027,6 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
     const bf16x8 bf0 = *reinterpret_cast<const bf16x8*>(&dgt[ln][8 * kq]);
     const bf16x8 bf1 = *reinterpret_cast<const bf16x8*>(&dgt[ln][32 + 8 * kq]);
     const unsigned tb = tag_bit(q);
-    const unsigned tb2 = tag_bit_hi(q);
     const long long obase = (((long long)(q & 1) * G + grp) * WPG + mem) * R;
     // block by block: MFMA pair, convert, store.  All MFMAs first and then the
     // stores (every granule leaves in one burst) measured 0.7 ms / step slower
@@ -1052,10 +1041,8 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
         if (ln < R) {  // C[m][n]: n = ln (row), m = 16 mb + 4 kq + r
           // one granule: units 16 mb + 4 kq .. + 3, tag bit in the first value
           const unsigned off = (unsigned)(((obase + ln) * (long long)hq + 4 * mb + kq) * 8);
-          const unsigned p01 = bf_with_lsb(acc[0], tb) |
-                               ((tag2 == 1 ? bf_with_lsb(acc[1], tb2) : (unsigned)f2bf(acc[1])) << 16);
-          const unsigned p23 = (tag2 == 2 ? bf_with_lsb(acc[2], tb) : (unsigned)f2bf(acc[2])) |
-                               ((unsigned)f2bf(acc[3]) << 16);
+          const unsigned p01 = bf_with_lsb(acc[0], tb) | ((unsigned)f2bf(acc[1]) << 16);
+          const unsigned p23 = f2bf(acc[2]) | ((unsigned)f2bf(acc[3]) << 16);
           const u32x2 v0 = {p01, p23};
           if (local)  // plain: into this XCD's L2
             __builtin_amdgcn_raw_buffer_store_b64(v0, rs, off, 0, 0);
@@ -1232,22 +1219,23 @@ int lstm_bwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* wh
   const int io_pos = (li && atoi(li) == 1) ? 1 : 0;
   const char* s16 = getenv("ASR_XG_DG_ST16");   // A/B: bf16 dG by 16-B stores from LDS
   const int st16 = (s16 && s16[0] == '0') ? 0 : 1;
-  const char* t2e = getenv("ASR_XG_TAG2");      // two-bit step tags on the dh partials
-  const int tag2 = t2e ? atoi(t2e) : 0;
-  const char* acqe = getenv("ASR_XG_ACQ");
-  const int acq = (acqe && acqe[0] == '1') ? 1 : 0;
-#define ASR_XGB(RR, M)                                                                          \
+#define ASR_XGB2(RR, M, AHV)                                                                    \
   do {                                                                                          \
-    if (!xg_fits(lstm_bwd_xg<RR, M>, 512 + RR * XU, pin)) {                                     \
+    if (!xg_fits(lstm_bwd_xg<RR, M, AHV>, 512 + RR * XU, pin)) {                                \
       if (pin != XG_PIN_BWD) xg_warn_pin_unfit(pin);                                             \
       return 0;                                                                                 \
     }                                                                                           \
     if (dry) return 1;                                                                          \
     if (hipMemsetAsync(ws, 0, lstm_xg_bwd_bytes(B, H), s) != hipSuccess) return -1;             \
     xg_trace_setup(s);             \
-    hipLaunchKernelGGL((lstm_bwd_xg<RR, M>), dim3(grid), dim3(512 + RR * XU), pin, s, B, T, H,      \
-                       lens, whh_f, whh_r, dy, act_dg, cst, g, hdr, dgbf, dbpart, ep, al,        \
-                       (dg_f32 || !dgbf) ? 1 : 0, io_pos, st16, tag2, (const h16x4*)acth, acq);        \
+    hipLaunchKernelGGL((lstm_bwd_xg<RR, M, AHV>), dim3(grid), dim3(512 + RR * XU), pin, s, B, T, \
+                       H, lens, whh_f, whh_r, dy, act_dg, cst, g, hdr, dgbf, dbpart, ep, al,     \
+                       (dg_f32 || !dgbf) ? 1 : 0, io_pos, st16, (const h16x4*)acth);            \
+  } while (0)
+#define ASR_XGB(RR, M)                        \
+  do {                                        \
+    if (acth) ASR_XGB2(RR, M, true);          \
+    else ASR_XGB2(RR, M, false);              \
   } while (0)
 #define ASR_XGB_M(RR)                  \
   do {                                 \
@@ -1262,6 +1250,7 @@ int lstm_bwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* wh
   else ASR_XGB_M(16);
 #undef ASR_XGB_M
 #undef ASR_XGB
+#undef ASR_XGB2
   return hipGetLastError() == hipSuccess ? 1 : -1;
 }
 
