@@ -818,7 +818,7 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
     const int sl = tid & (2 * R - 1);
     const int srow = sl >> 1, sq = sl & 1;   // row, units 8 sq .. 8 sq + 7
     const int pgi = tid / (2 * R);
-    constexpr int MAXP = 64;  // WPG <= 64
+    constexpr int NLD = (4 * MB + NPG - 1) / NPG;   // producers per sweeper lane (WPG <= 4 MB)
     const int nsleep = __builtin_amdgcn_readfirstlane(g_xg_sleep);
     const int ndelay = __builtin_amdgcn_readfirstlane(g_xg_delay);
     for (int q = 0; q < T; ++q) {
@@ -833,14 +833,25 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
           int ok = 1;
 #pragma unroll
           for (int e = 0; e < 8; ++e) sm[e] = 0.f;
-#pragma unroll 8
-          for (int w = pgi; w < MAXP; w += NPG) {
-            if (w >= WPG) break;
+          // every load of the sweep is in flight before the first wait: slots
+          // past the group's last producer read beyond the buffer's extent, which
+          // a buffer load returns as zeros without a memory access (a guarded
+          // load per slot made the compiler wait for each one in turn: one L2
+          // round trip per slot instead of one per sweep)
+          u32x4 vv[NLD];
+#pragma unroll
+          for (int l = 0; l < NLD; ++l) {
+            const int w = pgi + l * NPG;
             // two granules = this block's units 8 sq .. 8 sq + 7 from producer w
             const unsigned off =
-                (unsigned)((((base + w) * R + srow) * (long long)hq + (u0 >> 2) + 2 * sq) * 8);
-            const u32x4 v = ld_sc1(rs, off);
-            ok &= (int)((((v[0] ^ ebit) | (v[2] ^ ebit)) & 1u) == 0u);
+                w < WPG ? (unsigned)((((base + w) * R + srow) * (long long)hq + (u0 >> 2) + 2 * sq) * 8)
+                        : 0x7ffffff0u;
+            vv[l] = ld_sc1(rs, off);
+          }
+#pragma unroll
+          for (int l = 0; l < NLD; ++l) {
+            const u32x4 v = vv[l];
+            ok &= (int)(pgi + l * NPG >= WPG) | (int)((((v[0] ^ ebit) | (v[2] ^ ebit)) & 1u) == 0u);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
               sm[2 * e] += bf2f((uint16_t)(v[e] & 0xffffu));
@@ -1028,29 +1039,46 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
     const bf16x8 bf1 = *reinterpret_cast<const bf16x8*>(&dgt[ln][32 + 8 * kq]);
     const unsigned tb = tag_bit(q);
     const long long obase = (((long long)(q & 1) * G + grp) * WPG + mem) * R;
-    // block by block: MFMA pair, convert, store.  All MFMAs first and then the
-    // stores (every granule leaves in one burst) measured 0.7 ms / step slower
-    // at 5x512 (interleaved A/B), although the MFMA wave's phase got shorter.
-#pragma unroll
-    for (int i = 0; i < MB; ++i) {
-      const int mb = mw + 4 * i;
-      if (mb < HB) {  // wave-uniform
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-        acc = mfma_bf16(wa[i][0], bf0, acc);
-        acc = mfma_bf16(wa[i][1], bf1, acc);
-        if (ln < R) {  // C[m][n]: n = ln (row), m = 16 mb + 4 kq + r
+    // block by block, one block of lag: the MFMA pair of block i is issued
+    // before block i - 1 is converted and stored, so the pair's latency hides
+    // behind the previous block's conversion (a block's MFMAs, convert and store
+    // back to back serialised the phase).  All MFMAs first and then the stores
+    // (every granule leaves in one burst) measured 0.7 ms / step slower at 5x512.
+    // Blocks past HB (wave-uniform) compute on a clamped fragment and store
+    // nothing.
+    f32x4 acc[MB];
+    auto mm = [&](int i) {
+      acc[i] = mfma_bf16(wa[i][0], bf0, f32x4{0.f, 0.f, 0.f, 0.f});
+      acc[i] = mfma_bf16(wa[i][1], bf1, acc[i]);
+    };
+    // granule of (row ln, block mb): units 16 mb + 4 kq .. + 3
+    const unsigned off0 = (unsigned)(((obase + ln) * (long long)hq + 4 * mw + kq) * 8);
+    auto publish = [&](auto aux) {
+      auto st = [&](int i) {
+        const int mb = mw + 4 * i;
+        if (ln < R && mb < HB) {  // C[m][n]: n = ln (row), m = 16 mb + 4 kq + r
           // one granule: units 16 mb + 4 kq .. + 3, tag bit in the first value
-          const unsigned off = (unsigned)(((obase + ln) * (long long)hq + 4 * mb + kq) * 8);
-          const unsigned p01 = bf_with_lsb(acc[0], tb) | ((unsigned)f2bf(acc[1]) << 16);
-          const unsigned p23 = f2bf(acc[2]) | ((unsigned)f2bf(acc[3]) << 16);
+          const unsigned off = off0 + 128u * i;
+          const unsigned p01 = bf_with_lsb(acc[i][0], tb) | ((unsigned)f2bf(acc[i][1]) << 16);
+          const unsigned p23 = f2bf(acc[i][2]) | ((unsigned)f2bf(acc[i][3]) << 16);
           const u32x2 v0 = {p01, p23};
-          if (local)  // plain: into this XCD's L2
-            __builtin_amdgcn_raw_buffer_store_b64(v0, rs, off, 0, 0);
-          else        // write-through
-            __builtin_amdgcn_raw_buffer_store_b64(v0, rs, off, 0, AUX_SC1);
+          __builtin_amdgcn_raw_buffer_store_b64(v0, rs, off, 0, decltype(aux)::value);
         }
+      };
+      mm(0);
+#pragma unroll
+      for (int i = 1; i < MB; ++i) {
+        mm(i);
+        __builtin_amdgcn_sched_barrier(0);
+        st(i - 1);
+        __builtin_amdgcn_sched_barrier(0);
       }
-    }
+      st(MB - 1);
+    };
+    if (local)  // plain: into this XCD's L2
+      publish(std::integral_constant<int, 0>());
+    else        // write-through
+      publish(std::integral_constant<int, (int)AUX_SC1>());
     if (mw == 0 && lane == 0 && tr && q < XG_TR_STEPS)
       tr[((long long)blockIdx.x * XG_TR_STEPS + q) * XG_TR_K + 4] = __builtin_amdgcn_s_memrealtime();
     __syncthreads();  // B3
