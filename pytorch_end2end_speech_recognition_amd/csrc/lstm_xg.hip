@@ -953,12 +953,14 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
     };
     for (int q = 0; q < T; ++q) {
       __syncthreads();  // B1
-      if (s_dead) return;
+      // the abort word is tested after the step's math, so its LDS read
+      // overlaps the partial-sum reads instead of preceding them
+      const int dead = s_dead;
       const int t = dir == 0 ? T - 1 - q : q;
       float d_i = 0.f, d_f = 0.f, d_g = 0.f, d_o = 0.f;
       if (own && t < len) {
         float dh = dyv;
-        if (q > 0) {
+        if (q > 0) {   // in order: a pairwise tree measured slower (same-box A/B)
 #pragma unroll
           for (int p = 0; p < NPG; ++p) dh += red[p][row][unit];
         }
@@ -981,6 +983,7 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
       } else {
         dc = 0.f;
       }
+      if (dead) return;
       const uint16_t bi = f2bf(d_i), bff = f2bf(d_f), bg = f2bf(d_g), bo = f2bf(d_o);
       dgt[row][unit] = bi;
       dgt[row][XU + unit] = bff;
@@ -1059,6 +1062,8 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
         if (ln < R && mb < HB) {  // C[m][n]: n = ln (row), m = 16 mb + 4 kq + r
           // one granule: units 16 mb + 4 kq .. + 3, tag bit in the first value
           const unsigned off = off0 + 128u * i;
+          // (packed v_cvt_pk_bf16_f32 conversions here, three VALU instead of
+          // about twelve, measured 35 us / launch SLOWER in a same-box A/B)
           const unsigned p01 = bf_with_lsb(acc[i][0], tb) | ((unsigned)f2bf(acc[i][1]) << 16);
           const unsigned p23 = f2bf(acc[i][2]) | ((unsigned)f2bf(acc[i][3]) << 16);
           const u32x2 v0 = {p01, p23};
