@@ -632,6 +632,30 @@ int asr_conv3x3_c1_forward(const void* x, int x_dtype, int cstride, int B, int T
 int asr_conv3x3_c1_forward_xs(const float* xs, int round_bf16, int B, int T, int F, int Co,
                               const float* w, const float* bias, void* z, int z_dtype,
                               void* stream);
+/* 3x3 convolution of a zero-haloed channels-last bf16 operand, tap-resident
+ * (csrc/conv.hip; replaces the tap-addressed asr_gemm product of the VGG
+ * convolutions, encoders/cnn.py:124-165 Conv2d 3x3 padding 1):
+ *   out[p][n] = bias[n] + sum_{tap < 9} sum_{c < Cin} in[p + s(tap)][c] * w[n][tap Cin + c],
+ *   s(tap) = sign * ((tap / 3 - 1) * Fp + (tap % 3 - 1)), rows outside [0, P) zero,
+ * for every padded pixel row p < P (Fp = F + 2: the grid's row pitch).  in bf16
+ * [P][Cin], w bf16 [Cout][9 Cin] (asr_conv_weight_pack_pad / _pack images),
+ * bias f32 [Cout] or NULL, out [P][Cout] f32 or bf16 (out_dtype).  sign = 1:
+ * the forward; sign = -1 with the mirrored weight image: the input gradient.
+ * The f32 sums are asr_gemm's (same k order).  Cin, Cout in {64, 128};
+ * ASR_ERR_UNSUPPORTED otherwise (asr_conv3x3_tr_supported says which). */
+int asr_conv3x3_tr_supported(int Cin, int Cout, int Fp);
+int asr_conv3x3_tr(const void* in, long long P, int Cin, int Fp, int sign, const void* w,
+                   int Cout, const float* bias, void* out, int out_dtype, void* stream);
+/* Weight-gradient image of the same convolution (csrc/conv.hip, replaces the
+ * dz^T X tap GEMM): packed[n][tap Cin + c] = sum_p dz[p][n] * x[p + s(tap)][c]
+ * (sign +1), overwritten, f32 [Cout][9 Cin] -- the image
+ * asr_conv_weight_unpack_acc_pad accumulates into the Conv2d weight gradient.
+ * x bf16 [P][Cin], dz bf16 [P][Cout]; per-chunk partials in the workspace
+ * (asr_conv3x3_tr_wgrad_workspace_bytes, 0 = shape not supported), summed in a
+ * fixed order (deterministic).  Cin, Cout in {64, 128}. */
+size_t asr_conv3x3_tr_wgrad_workspace_bytes(long long P, int Cin, int Cout, int Fp);
+int asr_conv3x3_tr_wgrad(const void* x, const void* dz, long long P, int Cin, int Fp, int Cout,
+                         float* packed, void* ws, size_t ws_bytes, void* stream);
 int asr_conv_direct_dgrad(const float* dz, int B, int T, int F, int Ci, int Co, const float* w,
                           float* dx, void* stream);
 size_t asr_conv_direct_wgrad_workspace_bytes(int B, int T, int F, int Ci, int Co);

@@ -53,6 +53,12 @@ SIGNATURES = {
                                       c_vp]),
     'asr_conv3x3_c1_forward_xs': (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp,
                                           c_vp, c_int, c_vp]),
+    'asr_conv3x3_tr_supported': (c_int, [c_int, c_int, c_int]),
+    'asr_conv3x3_tr': (c_int, [c_vp, c_ll, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_int,
+                               c_vp]),
+    'asr_conv3x3_tr_wgrad_workspace_bytes': (c_size, [c_ll, c_int, c_int, c_int]),
+    'asr_conv3x3_tr_wgrad': (c_int, [c_vp, c_vp, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_size,
+                                     c_vp]),
     'asr_conv3x3_c1_forward': (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp,
                                        c_vp, c_vp]),
     'asr_lstm_workspace_bytes': (c_size, [c_int, c_int, c_int, c_int]),

@@ -1545,6 +1545,37 @@ def _pool_dims(T, F, pt, pf, ceil):
     return To.value, Fo.value
 
 
+def _conv_tr_ok(cin, cout, fp):
+    """bf16 mode: the tap-resident convolution kernel (csrc/conv.hip) takes this
+    channel pair (ASR_VGG_TR=0 keeps the tap-addressed GEMM, for A/B)."""
+    return (compute_dtype() == BF16 and os.environ.get('ASR_VGG_TR', '1') != '0' and
+            N.query('asr_conv3x3_tr_supported', int(cin), int(cout), int(fp)) == 1)
+
+
+def conv3x3_tr(inp, P, cin, fp, sign, w, cout, bias, out):
+    """out[p][n] = bias[n] + sum_tap sum_c inp[p + sign*shift(tap)][c] w[n][tap cin + c]
+    on the tap-resident kernel (asr_conv3x3_tr); inp / w bf16, out f32 or bf16."""
+    N.require_device(inp, w, out)
+    od = BF16 if out.dtype == torch.bfloat16 else F32
+    N.call('asr_conv3x3_tr', N.ptr(inp), int(P), int(cin), int(fp), int(sign), N.ptr(w),
+           int(cout), N.ptr(bias), N.ptr(out), od, N.stream_handle(inp.device))
+
+
+def conv3x3_tr_wgrad(x, dz, P, cin, fp, cout, packed):
+    """packed[n][tap cin + c] = sum_p dz[p][n] x[p + shift(tap)][c] on the
+    tap-resident weight-gradient kernel; False when the shape does not take it."""
+    if compute_dtype() != BF16 or os.environ.get('ASR_VGG_TR', '1') == '0':
+        return False
+    nb = N.query('asr_conv3x3_tr_wgrad_workspace_bytes', int(P), int(cin), int(cout), int(fp))
+    if not nb:
+        return False
+    N.require_device(x, dz, packed)
+    ws = _ws(nb, x.device)
+    N.call('asr_conv3x3_tr_wgrad', N.ptr(x), N.ptr(dz), int(P), int(cin), int(fp), int(cout),
+           N.ptr(packed), N.ptr(ws), nb, N.stream_handle(x.device))
+    return True
+
+
 class VGGFn(torch.autograd.Function):
     """The whole conv stack as one op.  Layer l input: zero-haloed channels-last
     [B][T_l+2][F_l+2][C_in] (compute dtype for GEMM layers, f32 for direct
@@ -1610,10 +1641,14 @@ class VGGFn(torch.autograd.Function):
                                                                  device=dev)
                 N.call('asr_conv_weight_pack_pad', N.ptr(w), Co, cC, cCp, 0, cd, N.ptr(wg),
                        N.stream_handle(dev))
-                p = gemm_problem(_tap_operand(x_op, 0, cCp, cCp, cF + 2, 1),
-                                 operand(wg, 0, rowmap(9 * cCp)), z, rowmap(Co), npad, Co,
-                                 9 * cCp, bias=sp['b'])
-                run_gemm([p], dev)
+                if _conv_tr_ok(cCp, Co, cF + 2):
+                    # the input rows stay in an LDS ring across the nine taps
+                    conv3x3_tr(x_op, npad, cCp, cF + 2, 1, wg, Co, sp['b'], z)
+                else:
+                    p = gemm_problem(_tap_operand(x_op, 0, cCp, cCp, cF + 2, 1),
+                                     operand(wg, 0, rowmap(9 * cCp)), z, rowmap(Co), npad, Co,
+                                     9 * cCp, bias=sp['b'])
+                    run_gemm([p], dev)
             pt, pf, ceil = sp['pt'], sp['pf'], sp['ceil']
             To, Fo = _pool_dims(cT, cF, pt, pf, ceil) if pt else (cT, cF)
             P = torch.empty(B * To * Fo, Co, **f32)
@@ -1716,9 +1751,10 @@ class VGGFn(torch.autograd.Function):
             else:
                 # dW image [Co][9 Ci] = dz^T X (taps on the output index), K = padded pixels
                 packed = torch.empty(Co, 9 * cCp, **f32)
-                run_gemm([gemm_problem(operand(dz, 1, rowmap(Co)),
-                                       _tap_operand(x_op, 1, cCp, cCp, cF + 2, 1), packed,
-                                       rowmap(9 * cCp), Co, 9 * cCp, npad)], dev)
+                if not conv3x3_tr_wgrad(x_op, dz, npad, cCp, cF + 2, Co, packed):
+                    run_gemm([gemm_problem(operand(dz, 1, rowmap(Co)),
+                                           _tap_operand(x_op, 1, cCp, cCp, cF + 2, 1), packed,
+                                           rowmap(9 * cCp), Co, 9 * cCp, npad)], dev)
                 N.call('asr_conv_weight_unpack_acc_pad', N.ptr(packed), Co, cC, cCp,
                        N.ptr(grad_buffer(w)), N.stream_handle(dev))
             if l == 0:
@@ -1728,9 +1764,12 @@ class VGGFn(torch.autograd.Function):
             N.call('asr_conv_weight_pack', N.ptr(w), Co, cC, 1, cd, N.ptr(wt),
                    N.stream_handle(dev))
             dx = torch.empty(npad, cC, **f32)
-            run_gemm([gemm_problem(_tap_operand(dz, 0, Co, Co, cF + 2, -1),
-                                   operand(wt, 0, rowmap(9 * Co)), dx, rowmap(cC), npad, cC,
-                                   9 * Co)], dev)
+            if _conv_tr_ok(Co, cC, cF + 2):
+                conv3x3_tr(dz, npad, Co, cF + 2, -1, wt, cC, None, dx)
+            else:
+                run_gemm([gemm_problem(_tap_operand(dz, 0, Co, Co, cF + 2, -1),
+                                       operand(wt, 0, rowmap(9 * Co)), dx, rowmap(cC), npad, cC,
+                                       9 * Co)], dev)
             dnext, flat = dx, 0
         return (None, None, None, None) + (None,) * len(ctx.needs_input_grad[4:])
 
