@@ -180,12 +180,6 @@ __global__ void __launch_bounds__(TR_NT) conv3x3_tr(TrArgs a) {
   for (int j = 0; j < NW - 1; ++j)
     if (j < NKT) load_w(j % KT, j);
 
-  f32x4 acc[NI][NJ];
-#pragma unroll
-  for (int i = 0; i < NI; ++i)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  int bslot[NJ];   // ring slot of this lane's pixel row of fragment j (shift 0)
   // bias of this lane's channels, read before the loop (a global load inside it
   // would make the compiler drain the DMAs in flight before the epilogue)
   float bias4[NI][4];
@@ -193,83 +187,99 @@ __global__ void __launch_bounds__(TR_NT) conv3x3_tr(TrArgs a) {
   for (int i = 0; i < NI; ++i)
 #pragma unroll
     for (int r = 0; r < 4; ++r) bias4[i][r] = a.bias ? a.bias[16 * i + 4 * (lane >> 4) + r] : 0.f;
-
-  int m = t_beg, kq = 0;
-  for (int it = 0; it < NKT; ++it) {
-    if (kq == 0) {
-      const int pb = m * BM + w * WPX + (lane & 15);
+  // per-lane fragment addresses that never change: the weight rows (bytes
+  // within a slot) and the swizzle-free chunk part of the pixel-row reads
+  int woff[NI][2];
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) bslot[j] = (pb + 16 * j + a.RCB) % RC;
-    }
-    // wait for weight slice `it`: everything this wave issued after it may stay
-    // in flight -- later slices, the halo batch of the next tile (issued right
-    // after slice it - kq + NW - 1) and the previous tile's epilogue stores
-    {
-      int n = NBW * min(NW - 2, NKT - 1 - it);
-      if (kq >= 1 && kq <= NW - 1 && m + 1 < t_end) n += NH;
-      if (kq <= NW - 2 && m > t_beg) n += NST;
-      tr_wait(n);
-    }
-    __syncthreads();
-    if (it + NW - 1 < NKT) load_w((kq + NW - 1) % KT, (it + NW - 1) % NW);
-    if (kq == 0 && m + 1 < t_end) load_rows(hi_row(m), BM / 8);
-
-    const int tap = kq / NCB, cb = kq - tap * NCB;
-    const int sh = a.sign * ((tap / 3 - 1) * a.Fp + (tap % 3 - 1));
-    const char* hb = halo + (size_t)cb * RC * 128;
-    const char* wb = wring + (it % NW) * WSLOT;
-    int srow[NJ];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      int s = bslot[j] + sh;
-      s = s >= RC ? s - RC : s;
-      srow[j] = s < 0 ? s + RC : s;
-    }
+  for (int i = 0; i < NI; ++i)
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 fa[NI], fb[NJ];
+      const int r = 16 * i + (lane & 15);
+      woff[i][kk] = r * 128 + (((4 * kk + (lane >> 4)) ^ ((r >> 1) & 7)) << 4);
+    }
+  const int cpart0 = (lane >> 4) << 4, cpart1 = (4 + (lane >> 4)) << 4;
+  const int sh_t = a.Fp * a.sign, sh_f = a.sign;   // tap (kt, kf) shift = (kt-1) sh_t + (kf-1) sh_f
+
+  for (int m = t_beg; m < t_end; ++m) {
+    const bool more = m + 1 < t_end, prev = m > t_beg;
+    const int it0 = (m - t_beg) * KT;
+    const int pb = m * BM + w * WPX + (lane & 15);
+    int bslot[NJ];   // ring slot of this lane's pixel row of fragment j (shift 0)
 #pragma unroll
-      for (int i = 0; i < NI; ++i) fa[i] = tr_frag(wb, 16 * i + (lane & 15), kk, lane);
+    for (int j = 0; j < NJ; ++j) bslot[j] = (pb + 16 * j + a.RCB) % RC;
+    f32x4 acc[NI][NJ];
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) fb[j] = tr_frag(hb, srow[j], kk, lane);
+    for (int kq = 0; kq < KT; ++kq) {
+      const int it = it0 + kq;
+      // wait for weight slice `it`: everything this wave issued after it may stay
+      // in flight -- later slices, the halo batch of the next tile (issued right
+      // after slice it0 + NW - 1) and the previous tile's epilogue stores
+      {
+        int n = NBW * min(NW - 2, NKT - 1 - it);
+        if (kq >= 1 && kq <= NW - 1 && more) n += NH;
+        if (kq <= NW - 2 && prev) n += NST;
+        tr_wait(n);
+      }
+      __syncthreads();
+      if (it + NW - 1 < NKT) load_w((kq + NW - 1) % KT, (it + NW - 1) % NW);
+      if (kq == 0 && more) load_rows(hi_row(m), BM / 8);
+
+      const int tap = kq / NCB, cb = kq % NCB;
+      const int sh = (tap / 3 - 1) * sh_t + (tap % 3 - 1) * sh_f;
+      const char* hb = halo + (size_t)cb * RC * 128;
+      const char* wb = wring + (it % NW) * WSLOT;
+      int ra[NJ], sw[NJ];   // row byte address and swizzle (<< 4) of fragment j's rows
 #pragma unroll
-      for (int i = 0; i < NI; ++i)
+      for (int j = 0; j < NJ; ++j) {
+        int s = bslot[j] + sh;
+        s = s >= RC ? s - RC : s;
+        s = s < 0 ? s + RC : s;
+        ra[j] = s << 7;
+        sw[j] = (s << 3) & 0x70;
+      }
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma_bf16(fa[i], fb[j], acc[i][j]);
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 fa[NI], fb[NJ];
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+          fa[i] = __builtin_bit_cast(bf16x8, *(const tr_u32x4*)(wb + woff[i][kk]));
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          fb[j] = __builtin_bit_cast(
+              bf16x8, *(const tr_u32x4*)(hb + ra[j] + ((kk ? cpart1 : cpart0) ^ sw[j])));
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            acc[i][j] = mfma_bf16(fa[i], fb[j],
+                                  (kq == 0 && kk == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][j]);
+      }
     }
 
-    if (kq == KT - 1) {
-      // epilogue: lane = (pixel 16 j + lane & 15, channels 16 i + 4 (lane >> 4) .. + 3);
-      // every lane issues every store (out-of-range pixels at an out-of-range
-      // offset, dropped by the buffer) so the store count the waits assume holds
-      const int pb = m * BM + w * WPX + (lane & 15);
-      const int c4 = 4 * (lane >> 4);
+    // epilogue: lane = (pixel 16 j + lane & 15, channels 16 i + 4 (lane >> 4) .. + 3);
+    // every lane issues every store (out-of-range pixels at an out-of-range
+    // offset, dropped by the buffer) so the store count the waits assume holds
+    const int c4 = 4 * (lane >> 4);
 #pragma unroll
-      for (int i = 0; i < NI; ++i) {
-        const float* b4 = bias4[i];
+    for (int i = 0; i < NI; ++i) {
+      const float* b4 = bias4[i];
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const int p = pb + 16 * j;
-          const long long e = (long long)p * COUT + 16 * i + c4;
-          const f32x4 v = acc[i][j];
-          if constexpr (OUT_BF16) {
-            const unsigned voff = p < a.P ? (unsigned)(e * 2) : TR_OOB;
-            const tr_u32x2 pk = {(unsigned)f2bf(v[0] + b4[0]) | ((unsigned)f2bf(v[1] + b4[1]) << 16),
-                                 (unsigned)f2bf(v[2] + b4[2]) | ((unsigned)f2bf(v[3] + b4[3]) << 16)};
-            __builtin_amdgcn_raw_buffer_store_b64(pk, rout, voff, 0, 0);
-          } else {
-            const unsigned voff = p < a.P ? (unsigned)(e * 4) : TR_OOB;
-            const tr_u32x4 pk = {__float_as_uint(v[0] + b4[0]), __float_as_uint(v[1] + b4[1]),
-                                 __float_as_uint(v[2] + b4[2]), __float_as_uint(v[3] + b4[3])};
-            __builtin_amdgcn_raw_buffer_store_b128(pk, rout, voff, 0, 0);
-          }
-          acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < NJ; ++j) {
+        const int p = pb + 16 * j;
+        const long long e = (long long)p * COUT + 16 * i + c4;
+        const f32x4 v = acc[i][j];
+        if constexpr (OUT_BF16) {
+          const unsigned voff = p < a.P ? (unsigned)(e * 2) : TR_OOB;
+          const tr_u32x2 pk = {(unsigned)f2bf(v[0] + b4[0]) | ((unsigned)f2bf(v[1] + b4[1]) << 16),
+                               (unsigned)f2bf(v[2] + b4[2]) | ((unsigned)f2bf(v[3] + b4[3]) << 16)};
+          __builtin_amdgcn_raw_buffer_store_b64(pk, rout, voff, 0, 0);
+        } else {
+          const unsigned voff = p < a.P ? (unsigned)(e * 4) : TR_OOB;
+          const tr_u32x4 pk = {__float_as_uint(v[0] + b4[0]), __float_as_uint(v[1] + b4[1]),
+                               __float_as_uint(v[2] + b4[2]), __float_as_uint(v[3] + b4[3])};
+          __builtin_amdgcn_raw_buffer_store_b128(pk, rout, voff, 0, 0);
         }
       }
-      kq = 0;
-      ++m;
-    } else {
-      ++kq;
     }
   }
 }
@@ -387,12 +397,45 @@ __global__ void __launch_bounds__(CIN * 4) conv3x3_tr_wgrad(TrwArgs a) {
   for (int t = 1; t < TRW_D; ++t)
     if (t < nkt) load_tile(t);
 
+  // wave w owns channel tile w of x (16 channels: 64-channel half w >> 2,
+  // granule w & 3) for all nine taps: acc[i][tap] = rows 16 i .. of the block,
+  // columns tap CIN + 16 w ..
   f32x4 acc[4][9];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 9; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int kq = (lane >> 2) & 3, kg = lane >> 4;
+  const int kq = (lane >> 2) & 3, kg = lane >> 4, p8 = 8 * (lane & 3);
+  const int G = w & 3;
+  const char* xh = xr + (size_t)(w >> 2) * RC * 128;
+  // the swizzle of a row depends on its bits 1 and 3 only, which neither the
+  // 64-row advance per k-tile nor the ring wrap (RC % 16 == 0) changes: per tap
+  // the granule offsets of this lane's lo / hi rows are fixed for the kernel
+  int tzl[9], tzh[9];
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    const int r0 = cbeg + 8 * kg + kq + a.RCB + (tap / 3 - 1) * a.Fp + (tap % 3 - 1);
+    tzl[tap] = ((G ^ trh(r0)) << 5) + p8;
+    tzh[tap] = ((G ^ trh(r0 + 4)) << 5) + p8;
+  }
+  // dz fragment offsets within a slot (rows 32 kk + 8 kg + kq and + 4, granule i)
+  int zo[4][2][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int r = 32 * kk + 8 * kg + kq + 4 * h;
+        zo[i][kk][h] = r * 128 + ((i ^ trh(r)) << 5) + p8;
+      }
+  int xb = (cbeg + 8 * kg + kq + a.RCB) % RC;   // ring slot of this lane's row (shift 0)
+  auto rd = [&](const char* base, int off_lo, int off_hi) {
+    const tr_v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((tr_lds_v4s*)(base + off_lo));
+    const tr_v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((tr_lds_v4s*)(base + off_hi));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
+  auto up = [&](int v) { return v >= RC ? v - RC : v; };
 
   for (int t = 0; t < nkt; ++t) {
     // wait for tile t: tiles t + 1 .. t + D - 1 may stay in flight
@@ -404,29 +447,24 @@ __global__ void __launch_bounds__(CIN * 4) conv3x3_tr_wgrad(TrwArgs a) {
     }
     __syncthreads();
     if (t + TRW_D < nkt) load_tile(t + TRW_D);
-    const int p0 = cbeg + t * TRW_BK;
     const char* zs = zr + (t % NDZ) * DZSLOT;
-    const int xb = (p0 + 8 * kg + kq + a.RCB) % RC;   // ring slot of this lane's row, shift 0
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      const int zl = 32 * kk + 8 * kg + kq;
       bf16x8 fa[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = tr_tfrag(zs, zl, zl + 4, i, lane);
+      for (int i = 0; i < 4; ++i) fa[i] = rd(zs, zo[i][kk][0], zo[i][kk][1]);
 #pragma unroll
-      for (int jn = 0; jn < 9; ++jn) {
-        const int jt = 9 * w + jn;                 // 16-column tile of the 9 CIN columns
-        const int tap = (16 * jt) / CIN, c0 = (16 * jt) % CIN;
+      for (int tap = 0; tap < 9; ++tap) {
         const int sh = (tap / 3 - 1) * a.Fp + (tap % 3 - 1);
-        int s = xb + 32 * kk + sh;
-        s = s >= RC ? s - RC : (s < 0 ? s + RC : s);
-        int s4 = s + 4;
-        s4 = s4 >= RC ? s4 - RC : s4;
-        const bf16x8 fb = tr_tfrag(xr + (size_t)(c0 >> 6) * RC * 128, s, s4, (c0 & 63) >> 4, lane);
+        int s = xb + sh + 32 * kk;
+        s = s < 0 ? s + RC : up(s);
+        const int s4 = up(s + 4);
+        const bf16x8 fb = rd(xh, (s << 7) + tzl[tap], (s4 << 7) + tzh[tap]);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) acc[i][jn] = mfma_bf16(fa[i], fb, acc[i][jn]);
+        for (int i = 0; i < 4; ++i) acc[i][tap] = mfma_bf16(fa[i], fb, acc[i][tap]);
       }
     }
+    xb = up(xb + TRW_BK);
   }
   // partial image of this chunk: rows n = 16 i + 4 (l >> 4) + r, columns 16 jt + (l & 15)
   float* o = a.slab + ((size_t)split * NG + cob) * 64 * (9 * CIN);
@@ -436,7 +474,7 @@ __global__ void __launch_bounds__(CIN * 4) conv3x3_tr_wgrad(TrwArgs a) {
     for (int jn = 0; jn < 9; ++jn)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        o[(size_t)(16 * i + 4 * (lane >> 4) + r) * (9 * CIN) + 16 * (9 * w + jn) + (lane & 15)] =
+        o[(size_t)(16 * i + 4 * (lane >> 4) + r) * (9 * CIN) + jn * CIN + 16 * w + (lane & 15)] =
             acc[i][jn][r];
 }
 

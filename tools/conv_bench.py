@@ -11,6 +11,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from pytorch_end2end_speech_recognition_amd import native_ops as ops  # noqa: E402
 
 dev = torch.device('cuda:0')
+ONLY_TR = os.environ.get('CONV_BENCH_ONLY_TR') == '1'   # profiling: the tap-resident kernels only
 ops.set_compute_dtype('bf16')
 B = 32
 cases = [  # name, T, F, Cin, Cout, sign, out dtype
@@ -44,7 +45,7 @@ for name, T, F, ci, co, sign, odt in cases:
     out = torch.empty(P, co, dtype=odt, device=dev)
     fl = 2.0 * P * co * 9 * ci
     t_tr = timeit(lambda: ops.conv3x3_tr(x, P, ci, F + 2, sign, w, co, b, out))
-    t_g = timeit(lambda: ops.run_gemm([ops.gemm_problem(
+    t_g = 1e9 if ONLY_TR else timeit(lambda: ops.run_gemm([ops.gemm_problem(
         ops._tap_operand(x, 0, ci, ci, F + 2, sign), ops.operand(w, 0, ops.rowmap(9 * ci)), out,
         ops.rowmap(co), P, co, 9 * ci, bias=b)], dev))
     print('%s  P=%d  tr %8.1f us %6.0f TF/s | tap GEMM %8.1f us %6.0f TF/s' % (
@@ -59,7 +60,7 @@ for name, T, F, ci, co in [('L1 dW 64x64 F80', 1000, 80, 64, 64), ('L2 dW 64->12
     packed = torch.empty(co, 9 * ci, device=dev)
     fl = 2.0 * P * co * 9 * ci
     t_tr = timeit(lambda: ops.conv3x3_tr_wgrad(x, dz, P, ci, F + 2, co, packed))
-    t_g = timeit(lambda: ops.run_gemm([ops.gemm_problem(
+    t_g = 1e9 if ONLY_TR else timeit(lambda: ops.run_gemm([ops.gemm_problem(
         ops.operand(dz, 1, ops.rowmap(co)), ops._tap_operand(x, 1, ci, ci, F + 2, 1), packed,
         ops.rowmap(9 * ci), co, 9 * ci, P)], dev))
     print('%s  P=%d  tr %8.1f us %6.0f TF/s | tap GEMM %8.1f us %6.0f TF/s' % (
