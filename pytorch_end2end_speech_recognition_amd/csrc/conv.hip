@@ -113,7 +113,9 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* img, int row, int kk, int 
 }
 
 // CIN, COUT in {64, 128}; WPX pixels per wave (BM = 4 WPX per tile); NW
-// weight-ring slots (NW - 1 k-slices in flight).
+// weight-ring slots (NW - 1 k-slices in flight), or NW = 0: the whole weight
+// image resident in LDS (loaded once; one barrier per tile instead of one per
+// k-slice -- the 64 -> 64 layers, whose 72 KB image fits beside the ring).
 template <int CIN, int COUT, int WPX, int NW, bool OUT_BF16>
 __global__ void __launch_bounds__(TR_NT) conv3x3_tr(TrArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -173,12 +175,18 @@ __global__ void __launch_bounds__(TR_NT) conv3x3_tr(TrArgs a) {
   auto lo_row = [&](int m) { return ((m * BM - H1) >> 3) << 3; };          // floor to 8
   auto hi_row = [&](int m) { return ((m * BM + BM + H1 + 7) >> 3) << 3; };  // ceil to 8
 
-  // prologue: the first tile's rows, weight slices 0 .. NW - 2
+  // prologue: the first tile's rows, weight slices 0 .. NW - 2 (all of them
+  // when resident)
   load_rows(lo_row(t_beg), (hi_row(t_beg) - lo_row(t_beg)) >> 3);
   const int NKT = (t_end - t_beg) * KT;
+  if constexpr (NW == 0) {
 #pragma unroll
-  for (int j = 0; j < NW - 1; ++j)
-    if (j < NKT) load_w(j % KT, j);
+    for (int j = 0; j < KT; ++j) load_w(j, j);
+  } else {
+#pragma unroll
+    for (int j = 0; j < NW - 1; ++j)
+      if (j < NKT) load_w(j % KT, j);
+  }
 
   // bias of this lane's channels, read before the loop (a global load inside it
   // would make the compiler drain the DMAs in flight before the epilogue)
@@ -211,23 +219,35 @@ __global__ void __launch_bounds__(TR_NT) conv3x3_tr(TrArgs a) {
 #pragma unroll
     for (int kq = 0; kq < KT; ++kq) {
       const int it = it0 + kq;
-      // wait for weight slice `it`: everything this wave issued after it may stay
-      // in flight -- later slices, the halo batch of the next tile (issued right
-      // after slice it0 + NW - 1) and the previous tile's epilogue stores
-      {
-        int n = NBW * min(NW - 2, NKT - 1 - it);
-        if (kq >= 1 && kq <= NW - 1 && more) n += NH;
-        if (kq <= NW - 2 && prev) n += NST;
-        tr_wait(n);
+      if constexpr (NW == 0) {
+        // resident weights: per tile, wait for this tile's rows (the previous
+        // tile's epilogue stores may stay in flight), one barrier, then the
+        // next tile's rows go out
+        if (kq == 0) {
+          if (prev) tr_vmcnt<NST>();
+          else tr_vmcnt<0>();
+          __syncthreads();
+          if (more) load_rows(hi_row(m), BM / 8);
+        }
+      } else {
+        // wait for weight slice `it`: everything this wave issued after it may stay
+        // in flight -- later slices, the halo batch of the next tile (issued right
+        // after slice it0 + NW - 1) and the previous tile's epilogue stores
+        {
+          int n = NBW * min(NW - 2, NKT - 1 - it);
+          if (kq >= 1 && kq <= NW - 1 && more) n += NH;
+          if (kq <= NW - 2 && prev) n += NST;
+          tr_wait(n);
+        }
+        __syncthreads();
+        if (it + NW - 1 < NKT) load_w((kq + NW - 1) % KT, (it + NW - 1) % NW);
+        if (kq == 0 && more) load_rows(hi_row(m), BM / 8);
       }
-      __syncthreads();
-      if (it + NW - 1 < NKT) load_w((kq + NW - 1) % KT, (it + NW - 1) % NW);
-      if (kq == 0 && more) load_rows(hi_row(m), BM / 8);
 
       const int tap = kq / NCB, cb = kq % NCB;
       const int sh = (tap / 3 - 1) * sh_t + (tap % 3 - 1) * sh_f;
       const char* hb = halo + (size_t)cb * RC * 128;
-      const char* wb = wring + (it % NW) * WSLOT;
+      const char* wb = wring + (NW == 0 ? kq : it % (NW == 0 ? 1 : NW)) * WSLOT;
       int ra[NJ], sw[NJ];   // row byte address and swizzle (<< 4) of fragment j's rows
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
@@ -549,10 +569,12 @@ bool tr_plan(int Cin, int Cout, int Fp, TrPlan* pl) {
   const size_t halo = (size_t)(Cin / 64) * pl->RC * 128;
   const size_t wslot = (size_t)Cout * 128;
   const size_t cap = 160 * 1024;
-  if (halo + 4 * wslot <= cap) pl->nw = 4;
+  const char* wr = getenv("ASR_CONV_TR_WRES");   // A/B: 0 keeps the weight ring
+  if (Cin == 64 && Cout == 64 && halo + 9 * wslot <= cap && !(wr && wr[0] == '0')) pl->nw = 0;
+  else if (halo + 4 * wslot <= cap) pl->nw = 4;
   else if (halo + 3 * wslot <= cap) pl->nw = 3;
   else return false;
-  pl->lds = halo + pl->nw * wslot;
+  pl->lds = halo + (pl->nw ? pl->nw : 9 * (Cin / 64)) * wslot;
   return true;
 }
 
@@ -602,7 +624,8 @@ extern "C" int asr_conv3x3_tr(const void* in, long long P, int Cin, int Fp, int 
   int rc = ASR_ERR_UNSUPPORTED;
 #define TR_CASE(CI, CO, WPX, NW)                                                         \
   if (Cin == CI && Cout == CO && pl.wpx == WPX && pl.nw == NW) rc = tr_launch<CI, CO, WPX, NW>(a, bf, s, pl.lds)
-  TR_CASE(64, 64, 64, 4);
+  TR_CASE(64, 64, 64, 0);
+  else TR_CASE(64, 64, 64, 4);
   else TR_CASE(64, 128, 32, 4);
   else TR_CASE(128, 64, 32, 4);
   else TR_CASE(128, 128, 32, 4);

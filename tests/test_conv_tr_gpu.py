@@ -47,10 +47,14 @@ def _gemm_conv(inp, cin, fp, sign, wimg, cout, bias, out):
 
 
 @pytest.mark.parametrize('grid', ['3', '0'])
-@pytest.mark.parametrize('Ci,Co', [(64, 64), (64, 128), (128, 64), (128, 128)])
-def test_conv_tr_integer_exact(Ci, Co, grid, cuda_dev, monkeypatch):
+@pytest.mark.parametrize('Ci,Co,wres', [(64, 64, '1'), (64, 64, '0'), (64, 128, '1'),
+                                        (128, 64, '1'), (128, 128, '1')])
+def test_conv_tr_integer_exact(Ci, Co, wres, grid, cuda_dev, monkeypatch):
+    """wres '0': the 64 -> 64 layers on the weight ring instead of the resident
+    weight image."""
     if grid != '0':
         monkeypatch.setenv('ASR_CONV_TR_GRID', grid)
+    monkeypatch.setenv('ASR_CONV_TR_WRES', wres)
     ops.set_compute_dtype('bf16')
     try:
         assert N.query('asr_conv3x3_tr_supported', Ci, Co, 32) == 1
