@@ -1852,6 +1852,97 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
     PD_TR(51);
 
     // ================= E: d ctx_t, d aw_t, softmax chunk sums; conv features =================
+    // the previous step's (t + 1) conv transpose -> d aw_t carry and conv-kernel
+    // tiles, moved here from its G phase: they feed only this phase's d aw, so
+    // they run beside this phase's wait instead of on the dgates hand-off
+    // chain (G -> H).  The dF window goes to `un` after H is done with it; the
+    // aw_t window of step t + 1 is still in `awin` (reloaded below).
+    if (fact && has_r) {
+      {   // dF window rows [tt0 - half, tt0 + FCH + half) after 8 zero rows
+        for (int i = tid; i < (8 + KW) * C; i += PD_THREADS) {
+          const int row = i / C - 8, c = i % C, tt = tt0 - half + row;
+          L[G.un + i] = (row >= 0 && tt >= 0 && tt < d.T)
+                            ? pd_ld(rf, ((long long)be * d.T + tt) * d.C + c) : 0.f;
+        }
+      }
+      __syncthreads();
+      {
+        // d aw_{t-1}[j] = sum_c sum_k dF[j - k + half, c] cw[c, k] (dF window row
+        // j + K - 1 - k): (channel, 4 frames, K quarter) per item with a sliding
+        // 4-row register window -- two LDS loads per 4 products
+        const float* dFw = &L[G.un + 8 * C];   // row r of the window (rows -8..-1 are zero)
+        float* cp = &L[G.cmb];   // [4 quarters][FCH4][C]
+        const int NJG = (FCH + 3) / 4, FCH4 = NJG * 4, KQ4 = G.KQ4;
+        for (int it = tid; it < C * NJG * 4; it += PD_THREADS) {
+          const int kq = it & 3, rest = it >> 2, c = rest % C, jg = rest / C;
+          const int j0 = jg * 4, k0 = kq * KQ4;
+          float o0 = 0.f, o1 = 0.f, o2 = 0.f, o3 = 0.f;
+          if (j0 < nfr) {   // taps past K are zero in the padded kernel rows
+            int r = j0 + d.K - 1 - k0;
+            float w0 = dFw[r * C + c], w1 = dFw[(r + 1) * C + c], w2 = dFw[(r + 2) * C + c],
+                  w3 = dFw[(r + 3) * C + c];
+            const float* cwr = &L[G.cw + c * G.KP + k0];
+            for (int k = 0; k < KQ4; k += 4) {   // four taps' loads first, no branches
+              const float4 cv = *reinterpret_cast<const float4*>(cwr + k);
+              const float n0 = dFw[(r - 1) * C + c], n1 = dFw[(r - 2) * C + c],
+                          n2 = dFw[(r - 3) * C + c], n3 = dFw[(r - 4) * C + c];
+              o0 += w0 * cv.x; o1 += w1 * cv.x; o2 += w2 * cv.x; o3 += w3 * cv.x;
+              o0 += n0 * cv.y; o1 += w0 * cv.y; o2 += w1 * cv.y; o3 += w2 * cv.y;
+              o0 += n1 * cv.z; o1 += n0 * cv.z; o2 += w0 * cv.z; o3 += w1 * cv.z;
+              o0 += n2 * cv.w; o1 += n1 * cv.w; o2 += n0 * cv.w; o3 += w0 * cv.w;
+              w0 = n3;
+              w1 = n2;
+              w2 = n1;
+              w3 = n0;
+              r -= 4;
+            }
+          }
+          float* o = cp + (kq * FCH4 + j0) * C + c;
+          o[0] = o0;
+          o[C] = o1;
+          o[2 * C] = o2;
+          o[3 * C] = o3;
+        }
+        PD_TR(10);
+        // conv-kernel tiles: dcw[c][k] += sum_{own frames} dF[i][c] aw_{t-1}[i + k]
+  #pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          const int nt = wave + 8 * jj;
+          if (nt * 16 < d.K) {   // wave-uniform
+            const int crow = lane & 15, kk = lane >> 4, kcol = nt * 16 + (lane & 15);
+            const int nks = (FCH + 3) / 4;
+            f32x4 acc = dcwM[jj];
+            for (int st = 0; st < nks; st += 4) {
+              float a4[4], b4[4];
+  #pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                const int i = (st + j) * 4 + kk;
+                const bool ok = st + j < nks && i < nfr;
+                const int ic = min(i, FCH - 1);
+                const float av = dFw[(half + ic) * C + min(crow, C - 1)];
+                const float bv = L[G.awin + ic + min(kcol, d.K - 1)];
+                a4[j] = (ok && crow < C) ? av : 0.f;
+                b4[j] = (ok && kcol < d.K) ? bv : 0.f;
+              }
+  #pragma unroll
+              for (int j = 0; j < 4; ++j) acc = mfma_f32(a4[j], b4[j], acc);
+            }
+            dcwM[jj] = acc;
+          }
+        }
+      }
+      __syncthreads();
+      {
+        const int FCH4 = ((FCH + 3) / 4) * 4;
+        for (int i = tid; i < FCH; i += PD_THREADS) {
+          float s = 0.f;
+          for (int kq = 0; kq < 4; ++kq)
+            for (int c = 0; c < C; ++c) s += L[G.cmb + (kq * FCH4 + i) * C + c];
+          L[G.carry + i] = s;
+        }
+      }
+      __syncthreads();
+    }
     // before the wait (forward outputs, no hand-off): d_ctx_in, aw_t of the
     // chunk, the aw_{t-1} window, W_dec h_t, in one batch of loads; the conv
     // features of aw_{t-1}
@@ -2080,13 +2171,6 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
     }
     PB_WAIT();
     PD_TR(58);
-    if (fact && t > 0) {   // dF window rows [tt0 - half, tt0 + FCH + half) after 8 zero rows
-      for (int i = tid; i < (8 + KW) * C; i += PD_THREADS) {
-        const int row = i / C - 8, c = i % C, tt = tt0 - half + row;
-        L[G.un + i] = (row >= 0 && tt >= 0 && tt < d.T)
-                          ? pd_ld(rf, ((long long)be * d.T + tt) * d.C + c) : 0.f;
-      }
-    }
     for (int i = tid; i < PD_SLOTS * d.A; i += PD_THREADS) {   // dWd_t of the 4 utterances
       const int sl = i / d.A, a = i % d.A, bb = grp + PD_GROUPS * sl;
       float s = 0.f;
@@ -2103,71 +2187,6 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
     }
     __syncthreads();
     PD_TR(59);
-    if (fact && t > 0) {
-      // d aw_{t-1}[j] = sum_c sum_k dF[j - k + half, c] cw[c, k] (dF window row
-      // j + K - 1 - k): (channel, 4 frames, K quarter) per item with a sliding
-      // 4-row register window -- two LDS loads per 4 products
-      const float* dFw = &L[G.un + 8 * C];   // row r of the window (rows -8..-1 are zero)
-      float* cp = &L[G.cmb];   // [4 quarters][FCH4][C]
-      const int NJG = (FCH + 3) / 4, FCH4 = NJG * 4, KQ4 = G.KQ4;
-      for (int it = tid; it < C * NJG * 4; it += PD_THREADS) {
-        const int kq = it & 3, rest = it >> 2, c = rest % C, jg = rest / C;
-        const int j0 = jg * 4, k0 = kq * KQ4;
-        float o0 = 0.f, o1 = 0.f, o2 = 0.f, o3 = 0.f;
-        if (j0 < nfr) {   // taps past K are zero in the padded kernel rows
-          int r = j0 + d.K - 1 - k0;
-          float w0 = dFw[r * C + c], w1 = dFw[(r + 1) * C + c], w2 = dFw[(r + 2) * C + c],
-                w3 = dFw[(r + 3) * C + c];
-          const float* cwr = &L[G.cw + c * G.KP + k0];
-          for (int k = 0; k < KQ4; k += 4) {   // four taps' loads first, no branches
-            const float4 cv = *reinterpret_cast<const float4*>(cwr + k);
-            const float n0 = dFw[(r - 1) * C + c], n1 = dFw[(r - 2) * C + c],
-                        n2 = dFw[(r - 3) * C + c], n3 = dFw[(r - 4) * C + c];
-            o0 += w0 * cv.x; o1 += w1 * cv.x; o2 += w2 * cv.x; o3 += w3 * cv.x;
-            o0 += n0 * cv.y; o1 += w0 * cv.y; o2 += w1 * cv.y; o3 += w2 * cv.y;
-            o0 += n1 * cv.z; o1 += n0 * cv.z; o2 += w0 * cv.z; o3 += w1 * cv.z;
-            o0 += n2 * cv.w; o1 += n1 * cv.w; o2 += n0 * cv.w; o3 += w0 * cv.w;
-            w0 = n3;
-            w1 = n2;
-            w2 = n1;
-            w3 = n0;
-            r -= 4;
-          }
-        }
-        float* o = cp + (kq * FCH4 + j0) * C + c;
-        o[0] = o0;
-        o[C] = o1;
-        o[2 * C] = o2;
-        o[3 * C] = o3;
-      }
-      PD_TR(10);
-      // conv-kernel tiles: dcw[c][k] += sum_{own frames} dF[i][c] aw_{t-1}[i + k]
-#pragma unroll
-      for (int jj = 0; jj < 2; ++jj) {
-        const int nt = wave + 8 * jj;
-        if (nt * 16 < d.K) {   // wave-uniform
-          const int crow = lane & 15, kk = lane >> 4, kcol = nt * 16 + (lane & 15);
-          const int nks = (FCH + 3) / 4;
-          f32x4 acc = dcwM[jj];
-          for (int st = 0; st < nks; st += 4) {
-            float a4[4], b4[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const int i = (st + j) * 4 + kk;
-              const bool ok = st + j < nks && i < nfr;
-              const int ic = min(i, FCH - 1);
-              const float av = dFw[(half + ic) * C + min(crow, C - 1)];
-              const float bv = L[G.awin + ic + min(kcol, d.K - 1)];
-              a4[j] = (ok && crow < C) ? av : 0.f;
-              b4[j] = (ok && kcol < d.K) ? bv : 0.f;
-            }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc = mfma_f32(a4[j], b4[j], acc);
-          }
-          dcwM[jj] = acc;
-        }
-      }
-    }
     PD_TR(11);
     // d dec from the attention, W_dec^T dWd_t over this member's units:
     // (slot, unit, eighth of A) per thread, eighths summed in order
@@ -2215,15 +2234,6 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
     PD_TR(13);
     __syncthreads();
     PD_TR(14);
-    if (fact && t > 0) {
-      const int FCH4 = ((FCH + 3) / 4) * 4;
-      for (int i = tid; i < FCH; i += PD_THREADS) {
-        float s = 0.f;
-        for (int kq = 0; kq < 4; ++kq)
-          for (int c = 0; c < C; ++c) s += L[G.cmb + (kq * FCH4 + i) * C + c];
-        L[G.carry + i] = s;
-      }
-    }
     PD_TR(60);
     PB_PUBLISH();
     PD_TR(61);
