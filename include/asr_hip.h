@@ -653,6 +653,11 @@ int asr_conv3x3_tr(const void* in, long long P, int Cin, int Fp, int sign, const
  * x bf16 [P][Cin], dz bf16 [P][Cout]; per-chunk partials in the workspace
  * (asr_conv3x3_tr_wgrad_workspace_bytes, 0 = shape not supported), summed in a
  * fixed order (deterministic).  Cin, Cout in {64, 128}. */
+/* Zero the one-pixel halo (rows t = 0, T + 1 and columns f = 0, F + 1) of a
+ * channels-last padded grid [B][T+2][F+2][C] of dtype (ASR_DT_F32 / _BF16;
+ * C * size % 16 == 0): the producers of the VGG layer operands write only the
+ * interior, so the buffer need not be zero-filled whole. */
+int asr_vgg_zero_halo(void* buf, int dtype, int B, int T, int F, int C, void* stream);
 size_t asr_conv3x3_tr_wgrad_workspace_bytes(long long P, int Cin, int Cout, int Fp);
 int asr_conv3x3_tr_wgrad(const void* x, const void* dz, long long P, int Cin, int Fp, int Cout,
                          float* packed, void* ws, size_t ws_bytes, void* stream);

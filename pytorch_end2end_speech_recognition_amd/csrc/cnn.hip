@@ -718,9 +718,10 @@ __global__ void __launch_bounds__(CT) post_bwd_full(const float* __restrict__ dn
       const unsigned qp = ((unsigned)px.b * pl.To + to) * pl.Fo + fo;
       const long long ip = (long long)qp * C + c;
       VecF<V> g = dy_at<V>(dnext, qp, c, pl.To, pl.Fo, C, flat, af.drop, af.seed);
+      VecF<V> x;   // the pooled pre-BN value (read when BN or the pool needs it)
+      if (af.mean || pl.pt) x.load(P + ip);
       if (af.mean) {
-        VecF<V> x, m, r, gm, s1, s2;
-        x.load(P + ip);
+        VecF<V> m, r, gm, s1, s2;
         m.load(af.mean + c);
         r.load(af.rstd + c);
         gm.load(af.gamma + c);
@@ -732,8 +733,12 @@ __global__ void __launch_bounds__(CT) post_bwd_full(const float* __restrict__ dn
           g.v[j] = gm.v[j] * r.v[j] * (g.v[j] - s1.v[j] * inv_n - xh * s2.v[j] * inv_n);
         }
       }
+      // ReLU mask: z > 0 at the window's argmax pixel <=> the pooled value
+      // P = max(0, max z) > 0 there, so pooled layers read P (a quarter of the
+      // bytes, already loaded for BN) instead of the full-resolution z
       VecF<V> zv;
-      zv.load(z + p);
+      if (pl.pt) zv = x;
+      else zv.load(z + p);
       unsigned sl = 0u, me = 0u;
       if (pl.pt) {
         sl = *reinterpret_cast<const unsigned*>(slot + ip);   // four channels' argmax slots

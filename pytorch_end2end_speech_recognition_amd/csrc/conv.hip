@@ -498,19 +498,55 @@ __global__ void __launch_bounds__(CIN * 4) conv3x3_tr_wgrad(TrwArgs a) {
             acc[i][jn][r];
 }
 
-// packed[n][k] = sum over chunks s (in order) of slab[s][n / 64][n % 64][k]
-__global__ void tr_wgrad_reduce(const float* __restrict__ slab, int S, int NG, int K,
-                                float* __restrict__ packed) {
-  const long long i4 = (long long)blockIdx.x * blockDim.x + threadIdx.x;   // float4 index
+// packed[n][k] = sum over chunks s of slab[s][n / 64][n % 64][k], fixed order:
+// thread (column group cg = tid % 16, chunk lane q = tid / 16) of a 256-thread
+// block sums chunks q, q + 16, ... of its float4 column in order, the 16 lanes
+// are then summed in order q = 0 .. 15 (deterministic; every chunk row is read
+// by 16 x more threads than one sequential sum per column)
+__global__ void __launch_bounds__(256) tr_wgrad_reduce(const float* __restrict__ slab, int S,
+                                                       int NG, int K, float* __restrict__ packed) {
+  __shared__ float4 part[16][16];
+  const int cg = threadIdx.x & 15, q = threadIdx.x >> 4;
+  const long long i4 = (long long)blockIdx.x * 16 + cg;   // float4 column
   const long long n4 = (long long)NG * 64 * K / 4;
-  if (i4 >= n4) return;
-  const long long blk = (long long)NG * 64 * K;   // floats per chunk
-  float4 s = reinterpret_cast<const float4*>(slab)[i4];
-  for (int c = 1; c < S; ++c) {
-    const float4 v = reinterpret_cast<const float4*>(slab + c * blk)[i4];
-    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  const long long blk4 = n4;                              // float4s per chunk
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i4 < n4)
+    for (int c = q; c < S; c += 16) {
+      const float4 v = reinterpret_cast<const float4*>(slab)[c * blk4 + i4];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+  part[q][cg] = s;
+  __syncthreads();
+  if (q == 0 && i4 < n4) {
+    float4 t = part[0][cg];
+#pragma unroll
+    for (int j = 1; j < 16; ++j) {
+      const float4 v = part[j][cg];
+      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+    }
+    reinterpret_cast<float4*>(packed)[i4] = t;
   }
-  reinterpret_cast<float4*>(packed)[i4] = s;
+}
+
+// zero the one-pixel halo of a channels-last padded grid [B][T+2][F+2][C]
+// (the interior is written by the producing kernel): 16-B stores
+__global__ void zero_halo(char* __restrict__ buf, int B, int T, int F, int rowbytes) {
+  const int per_b = 2 * (F + 2) + 2 * T;   // border pixels of one utterance
+  const int chunks = rowbytes / 16;
+  const long long n = (long long)B * per_b * chunks;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int ch = (int)(e % chunks);
+    const long long k = e / chunks;
+    const int b = (int)(k / per_b), j = (int)(k % per_b);
+    int t, f;
+    if (j < F + 2) { t = 0; f = j; }
+    else if (j < 2 * (F + 2)) { t = T + 1; f = j - (F + 2); }
+    else { const int r = j - 2 * (F + 2); t = 1 + (r >> 1); f = (r & 1) ? F + 1 : 0; }
+    const long long pix = ((long long)b * (T + 2) + t) * (F + 2) + f;
+    *reinterpret_cast<uint4*>(buf + pix * rowbytes + ch * 16) = make_uint4(0u, 0u, 0u, 0u);
+  }
 }
 
 struct TrwPlan {
@@ -694,10 +730,22 @@ extern "C" int asr_conv3x3_tr_wgrad(const void* x, const void* dz, long long P, 
   else hipLaunchKernelGGL((conv3x3_tr_wgrad<128, 128>), grid, block, pl.lds, s, a);
   ASR_LAUNCH_CHECK();
   const long long n4 = (long long)NG * 64 * 9 * Cin / 4;
-  hipLaunchKernelGGL(tr_wgrad_reduce, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s,
+  hipLaunchKernelGGL(tr_wgrad_reduce, dim3((unsigned)((n4 + 15) / 16)), dim3(256), 0, s,
                      (const float*)ws, a.S, NG, 9 * Cin, packed);
   prof_end_launch(ASR_PROF_GEMM, slot, s);
   ASR_LAUNCH_CHECK();
   return ASR_OK;
 }
 
+extern "C" int asr_vgg_zero_halo(void* buf, int dtype, int B, int T, int F, int C, void* stream) {
+  ASR_REQUIRE(buf && B > 0 && T > 0 && F > 0 && C > 0, ASR_ERR_ARG, "vgg_zero_halo: bad args");
+  const int rowbytes = C * (dtype == ASR_DT_BF16 ? 2 : 4);
+  ASR_REQUIRE(rowbytes % 16 == 0 && ((uintptr_t)buf & 15) == 0, ASR_ERR_ARG,
+              "vgg_zero_halo: rows must be 16-B multiples");
+  const long long n = (long long)B * (2 * (F + 2) + 2 * T) * (rowbytes / 16);
+  const int grid = (int)std::min<long long>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(zero_halo, dim3(grid), dim3(256), 0, (hipStream_t)stream, (char*)buf, B, T, F,
+                     rowbytes);
+  ASR_LAUNCH_CHECK();
+  return ASR_OK;
+}

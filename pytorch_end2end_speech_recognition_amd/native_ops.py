@@ -1545,6 +1545,18 @@ def _pool_dims(T, F, pt, pf, ceil):
     return To.value, Fo.value
 
 
+def _halo_only(C, dtype):
+    """A padded VGG operand whose producer writes every interior pixel needs
+    only its halo zeroed (16-B rows; ASR_VGG_HALO_ONLY=0 zero-fills it whole)."""
+    size = 2 if dtype == torch.bfloat16 else 4
+    return C % 4 == 0 and (C * size) % 16 == 0 and os.environ.get('ASR_VGG_HALO_ONLY', '1') != '0'
+
+
+def _zero_halo(buf, B, T, F, C):
+    N.call('asr_vgg_zero_halo', N.ptr(buf), BF16 if buf.dtype == torch.bfloat16 else F32, int(B),
+           int(T), int(F), int(C), N.stream_handle(buf.device))
+
+
 def _conv_tr_ok(cin, cout, fp):
     """bf16 mode: the tap-resident convolution kernel (csrc/conv.hip) takes this
     channel pair (ASR_VGG_TR=0 keeps the tap-addressed GEMM, for A/B)."""
@@ -1664,7 +1676,12 @@ class VGGFn(torch.autograd.Function):
                 out_dt, flat = F32, 1
             else:
                 nxt_dt = opdt if use_gemm[l + 1] else torch.float32
-                out = torch.zeros(B * (To + 2) * (Fo + 2), Co, dtype=nxt_dt, device=dev)
+                if _halo_only(Co, nxt_dt):
+                    # the block kernel writes every interior pixel: zero only the halo
+                    out = torch.empty(B * (To + 2) * (Fo + 2), Co, dtype=nxt_dt, device=dev)
+                    _zero_halo(out, B, To, Fo, Co)
+                else:
+                    out = torch.zeros(B * (To + 2) * (Fo + 2), Co, dtype=nxt_dt, device=dev)
                 out_dt, flat = (cd if use_gemm[l + 1] else F32), 0
             nb = N.query('asr_vgg_block_workspace_bytes', B, To, Fo, Co)
             ws = _ws(nb, dev)
@@ -1703,8 +1720,14 @@ class VGGFn(torch.autograd.Function):
             # dz is the GEMM operand (compute dtype) of GEMM layers; their conv
             # bias gradient is summed from the f32 values inside the kernel
             dz_f32 = not gemm
-            dz = torch.zeros(npad, Co, **f32) if dz_f32 else torch.zeros(npad, Co, dtype=opdt,
-                                                                          device=dev)
+            if not dz_f32 and _halo_only(Co, opdt) and os.environ.get('ASR_VGG_POST_FULL',
+                                                                   '1') != '0':
+                # the full-resolution pass writes every interior pixel of dz
+                dz = torch.empty(npad, Co, dtype=opdt, device=dev)
+                _zero_halo(dz, B, cT, cF, Co)
+            else:
+                dz = torch.zeros(npad, Co, **f32) if dz_f32 else torch.zeros(npad, Co, dtype=opdt,
+                                                                              device=dev)
             fused_bias = gemm and sp['b'] is not None
             To, Fo = _pool_dims(cT, cF, pt, pf, ceil) if pt else (cT, cF)
             nb = N.query('asr_vgg_block_workspace_bytes', B, To, Fo, Co)
