@@ -166,10 +166,11 @@ __global__ void __launch_bounds__(256) ctc_emit_wide(const float* __restrict__ a
                                                      const int32_t* __restrict__ act_lens,
                                                      const int32_t* __restrict__ offs, int blank,
                                                      int Spad, float* __restrict__ lse_out,
-                                                     float* __restrict__ emit) {
+                                                     float* __restrict__ emit, int rev) {
   __shared__ float red_m[4], red_s[4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const long long row = blockIdx.x;
+  // rev: rows in descending order (see ctc_row_order)
+  const long long row = rev ? (long long)gridDim.x - 1 - blockIdx.x : blockIdx.x;
   const int b = (int)(row / T), t = (int)(row % T);
   if (t >= act_lens[b]) return;
   const float* x = acts + (long long)t * st + (long long)b * sb;
@@ -491,9 +492,9 @@ __global__ void __launch_bounds__(256) ctc_grad(
     const float* __restrict__ lse, const float* __restrict__ emit,
     const float* __restrict__ alpha, const float* __restrict__ beta,
     const float* __restrict__ logp, const float* __restrict__ grad_scale, float scale_mul,
-    float* __restrict__ grads, long long gst, long long gsb) {
+    float* __restrict__ grads, long long gst, long long gsb, int rev) {
   extern __shared__ __attribute__((aligned(16))) float occ[];  // [V] (kTable) or [Spad]
-  const long long row = blockIdx.x;
+  const long long row = rev ? (long long)gridDim.x - 1 - blockIdx.x : blockIdx.x;
   const int b = (int)(row / T), t = (int)(row % T);
   float* g = grads + (long long)t * gst + (long long)b * gsb;
   const float* x = acts + (long long)t * st + (long long)b * sb;
@@ -626,6 +627,20 @@ extern "C" size_t asr_ctc_workspace_bytes(int T, int B, int V, int max_label_len
   return ws_layout(T, B, max_label_len, nullptr, nullptr);
 }
 
+// Row order of the two passes that stream the activations (ASR_CTC_ORDER: bit
+// 0 the emission pass descending, bit 1 the gradient pass descending).  At
+// V = 10001 the [B][T][V] activations (320 MB) exceed the 256 MB Infinity
+// Cache by little: the gradient pass reading first the rows the emission pass
+// read last finds part of them still cached.
+static int ctc_row_order() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ASR_CTC_ORDER");
+    v = e ? (atoi(e) & 3) : 2;
+  }
+  return v;
+}
+
 extern "C" int asr_ctc_forward(const float* acts, long long stride_t, long long stride_b, int T,
                                int B, int V, const int32_t* labels_flat,
                                const int32_t* label_lens, const int32_t* act_lens,
@@ -650,7 +665,7 @@ extern "C" int asr_ctc_forward(const float* acts, long long stride_t, long long 
   if (V > 1024)
     hipLaunchKernelGGL(ctc_emit_wide, dim3((unsigned)rows), dim3(256), 0, s, acts, stride_t,
                        stride_b, T, V, labels_flat, label_lens, act_lens, ws.offs, blank, Spad,
-                       ws.lse, ws.emit);
+                       ws.lse, ws.emit, ctc_row_order() & 1);
   else
     hipLaunchKernelGGL(ctc_emit, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, acts, stride_t,
                        stride_b, T, B, V, labels_flat, label_lens, act_lens, ws.offs, blank, Spad,
@@ -701,12 +716,14 @@ extern "C" int asr_ctc_backward(const float* acts, long long stride_t, long long
     hipLaunchKernelGGL(ctc_grad<true>, dim3((unsigned)((long long)B * T)), dim3(threads),
                        V * sizeof(float), s, acts, stride_t, stride_b, T, V, labels_flat,
                        label_lens, act_lens, ws.offs, blank, Spad, ws.lse, ws.emit, ws.alpha,
-                       ws.beta, ws.logp, grad_scale, scale, grads, gstride_t, gstride_b);
+                       ws.beta, ws.logp, grad_scale, scale, grads, gstride_t, gstride_b,
+                       (ctc_row_order() >> 1) & 1);
   else
     hipLaunchKernelGGL(ctc_grad<false>, dim3((unsigned)((long long)B * T)), dim3(threads),
                        Spad * sizeof(float), s, acts, stride_t, stride_b, T, V, labels_flat,
                        label_lens, act_lens, ws.offs, blank, Spad, ws.lse, ws.emit, ws.alpha,
-                       ws.beta, ws.logp, grad_scale, scale, grads, gstride_t, gstride_b);
+                       ws.beta, ws.logp, grad_scale, scale, grads, gstride_t, gstride_b,
+                       (ctc_row_order() >> 1) & 1);
   ASR_LAUNCH_CHECK();
   prof_end_launch(ASR_PROF_CTC_GRAD, pslot, s);
   return ASR_OK;
