@@ -1627,7 +1627,7 @@ constexpr int PB_CM = PD_CM;
 struct PbGeom {
   int UPW, FCH, ECW, ED, G4, NPW, NKB, KQ, half, W, FS, AP, KQ4, KP;
   int encr, ea, cw, wc, v, dct, awin, f, daw, awt, de, carry, wd, un, dgs, part, dwdl, wdl,
-      cmb, red, total;   // LDS floats
+      cmb, cmbn, red, total;   // LDS floats
 };
 
 __host__ __device__ inline PbGeom pb_geom(const Dims& d) {
@@ -1675,7 +1675,9 @@ __host__ __device__ inline PbGeom pb_geom(const Dims& d) {
   g.part = o; o += 8 * PD_SLOTS * 16;
   g.dwdl = o; o += PD_SLOTS * d.A;
   g.wdl = o; o += d.A * g.UPW;
-  g.cmb = o; o += max(max(8 * d.A, PD_THREADS), 4 * ((g.FCH + 3) / 4) * 4 * d.C);
+  g.cmb = o;
+  g.cmbn = max(max(8 * d.A, PD_THREADS), 4 * ((g.FCH + 3) / 4) * 4 * d.C);
+  o += g.cmbn;
   g.red = o; o += 64;
   g.total = (o + 3) & ~3;
   return g;
@@ -1773,9 +1775,10 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
   // by the host, read-modify-written per step.
   const int NG = PD_THREADS / d.A, ta = tid % d.A, fg = tid / d.A;
   float accVr = 0.f;
-  f32x4 accWcM[NQ / 2], dcwM[2];
+  float accWc[CM];   // dW_conv row of this thread's attention unit (its frame group's part)
 #pragma unroll
-  for (int j = 0; j < NQ / 2; ++j) accWcM[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int c = 0; c < CM; ++c) accWc[c] = 0.f;
+  f32x4 dcwM[2];
   dcwM[0] = f32x4{0.f, 0.f, 0.f, 0.f};
   dcwM[1] = f32x4{0.f, 0.f, 0.f, 0.f};
   int nph = 0;
@@ -2045,12 +2048,15 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
       __syncthreads();
       PD_TR(1);
       // (frame, attention unit) pairs, thread (a = tid % A, frame group tid / A):
-      // tanh backward -> dp, d enc_a; dp tile [FCH][A] over the d enc_a rows
+      // tanh backward -> dp, d enc_a; dp tile [FCH][A] over the d enc_a rows.
+      // The thread also accumulates, for its (a, frames), the dW_conv row
+      // dp f (the pass's accumulators, registers) and the chunk's dWd sum.
       if (fg < NG) {
         float wcr[CM];
 #pragma unroll
         for (int c = 0; c < CM; ++c) wcr[c] = (CC || c < C) ? L[G.wc + ta * C + c] : 0.f;
         const float va = L[G.v + ta], wda = L[G.wd + ta];
+        float sdp = 0.f;
         for (int i = fg; i < FCH; i += NG) {
           const float de = L[G.de + i];   // 0 beyond nfr
           float dp = 0.f;
@@ -2073,19 +2079,28 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
             const float th = pd_tanh(p);
             dp = de * va * (1.f - th * th);
             accVr += de * th;
+#pragma unroll
+            for (int c = 0; c < CM; ++c) accWc[c] += dp * frv[c];
+            sdp += dp;
             d_enc_a[((long long)be * d.T + tt0 + i) * d.A + ta] = L[G.un + i * G.AP + ta] + dp;
           }
           L[G.un + i * G.AP + ta] = dp;
         }
+        L[G.part + fg * d.A + ta] = sdp;   // NG * A <= 512 = the part region
       }
       __syncthreads();
       PD_TR(2);
+      // dF [frames][C] = dp . W_conv: row tile rt, K half kh per wave (the
+      // halves summed below in order)
       const int MT = FCH <= 16 ? 1 : FCH <= 32 ? 2 : 4;
-      if (wave < MT) {   // dF [frames][C] = dp . W_conv, one row tile per wave
-        const int row = wave * 16 + (lane & 15), kk = lane >> 4, col = lane & 15;
-        const int nks = (d.A + 3) / 4;
+      const int nks = (d.A + 3) / 4;
+      const int KH = (2 * MT * 256 <= G.cmbn && 2 * MT <= PD_THREADS / 64) ? 2 : 1;
+      const int nh = KH == 2 ? ((nks + 7) / 8) * 4 : nks;
+      if (wave < KH * MT) {
+        const int rt = wave % MT, kh = wave / MT;
+        const int row = rt * 16 + (lane & 15), kk = lane >> 4, col = lane & 15;
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-        for (int st = 0; st < nks; st += 4) {
+        for (int st = kh * nh; st < (kh + 1 == KH ? nks : nh); st += 4) {
           float a4[4], b4[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
@@ -2101,51 +2116,24 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
           for (int j = 0; j < 4; ++j) acc = mfma_f32(a4[j], b4[j], acc);
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int i = wave * 16 + 4 * (lane >> 4) + r;
-          if (i < nfr && col < C) pd_st(rf, ((long long)be * d.T + tt0 + i) * d.C + col, acc[r]);
-        }
+        for (int r = 0; r < 4; ++r)
+          L[G.cmb + ((kh * MT + rt) * 16 + 4 * (lane >> 4) + r) * 16 + col] = acc[r];
       }
+      __syncthreads();
       PD_TR(3);
-      // dW_conv [A][C] += dp^T . f (the pass's accumulators)
-#pragma unroll
-      for (int j = 0; j < NQ / 2; ++j) {
-        const int mtile = wave + 8 * j;
-        if (mtile * 16 < d.A) {   // wave-uniform
-          const int arow = mtile * 16 + (lane & 15), kk = lane >> 4, col = lane & 15;
-          const int nks = (FCH + 3) / 4;
-          f32x4 acc = accWcM[j];
-          for (int st = 0; st < nks; st += 4) {
-            float a4[4], b4[4];
-#pragma unroll
-            for (int j2 = 0; j2 < 4; ++j2) {
-              const int i = (st + j2) * 4 + kk;
-              const bool ok = st + j2 < nks && i < FCH;
-              const int ic = min(i, FCH - 1);
-              const float av = L[G.un + ic * G.AP + min(arow, d.A - 1)];
-              const float bv = L[G.f + ic * G.FS + min(col, G.FS - 1)];
-              a4[j2] = (ok && arow < d.A) ? av : 0.f;
-              b4[j2] = (ok && col < C) ? bv : 0.f;
-            }
-#pragma unroll
-            for (int j2 = 0; j2 < 4; ++j2) acc = mfma_f32(a4[j2], b4[j2], acc);
-          }
-          accWcM[j] = acc;
-        }
+      for (int idx = tid; idx < MT * 256; idx += PD_THREADS) {
+        const int rt = idx >> 8, r16 = (idx >> 4) & 15, col = idx & 15;
+        const int i = rt * 16 + r16;
+        float v = L[G.cmb + idx];
+        if (KH == 2) v += L[G.cmb + MT * 256 + idx];
+        if (i < nfr && col < C) pd_st(rf, ((long long)be * d.T + tt0 + i) * d.C + col, v);
       }
       PD_TR(4);
-      // the chunk's d W_dec-input sum over its frames
+      // the chunk's d W_dec-input sum over its frames (frame-group partials in order)
       for (int a = tid; a < d.A; a += PD_THREADS) {
-        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-        int i = 0;
-        for (; i + 4 <= FCH; i += 4) {
-          s0 += L[G.un + i * G.AP + a];
-          s1 += L[G.un + (i + 1) * G.AP + a];
-          s2 += L[G.un + (i + 2) * G.AP + a];
-          s3 += L[G.un + (i + 3) * G.AP + a];
-        }
-        for (; i < FCH; ++i) s0 += L[G.un + i * G.AP + a];
-        pd_st(rw, ((long long)be * PD_CHUNKS + ch) * d.A + a, (s0 + s1) + (s2 + s3));
+        float sacc = 0.f;
+        for (int q = 0; q < NG; ++q) sacc += L[G.part + q * d.A + a];
+        pd_st(rw, ((long long)be * PD_CHUNKS + ch) * d.A + a, sacc);
       }
     }
     PD_TR(56);
@@ -2253,13 +2241,19 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
     for (int q = 0; q < NG; ++q) s += cV[q * d.A + a];
     dv_part[row * d.A + a] = s;
   }
+  // dW_conv: the frame groups' rows summed in order, one channel at a time
+  for (int c = 0; c < C; ++c) {
+    __syncthreads();
+    float v = 0.f;
 #pragma unroll
-  for (int j = 0; j < NQ / 2; ++j) {
-    const int mtile = wave + 8 * j;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int a = mtile * 16 + 4 * (lane >> 4) + r, c = lane & 15;
-      if (a < d.A && c < C) dwc_part[row * d.A * d.C + a * d.C + c] = accWcM[j][r];
+    for (int cc = 0; cc < CM; ++cc)
+      if (cc == c) v = accWc[cc];
+    if (fg < NG) cV[fg * d.A + ta] = v;
+    __syncthreads();
+    for (int a = tid; a < d.A; a += PD_THREADS) {
+      float sacc = 0.f;
+      for (int q = 0; q < NG; ++q) sacc += cV[q * d.A + a];
+      dwc_part[row * d.A * d.C + a * d.C + c] = sacc;
     }
   }
 #pragma unroll

@@ -8,9 +8,9 @@ tail -4 gpurun_out/att_ab_tests.log
 [ $rc -eq 0 ] || exit $rc
 for C in ${CONFIGS:-hybrid4x320}; do
   for i in 1 2; do
-    for nv in head=ab/libasr_hip_head.so new=pytorch_end2end_speech_recognition_amd/libasr_hip.so; do
+    for nv in head=ab/old new=.; do
       n=${nv%%=*}; p=${nv#*=}
-      ASR_LIB_PATH=$p timeout -k 10 200 python -u bench.py --config $C --steps 20 --warmup 5 --no-cpu-baseline --h2d-steps 0 > gpurun_out/attab_${C}_$n.json 2>/dev/null || exit 1
+      (cd $p && timeout -k 10 200 python -u bench.py --config $C --steps 20 --warmup 5 --no-cpu-baseline --h2d-steps 0) > gpurun_out/attab_${C}_$n.json 2>/dev/null || exit 1
       python -c "import json;d=json.load(open('gpurun_out/attab_${C}_$n.json'));o=d['roofline']['other_kernels'];print('$C $n', d['ms_per_step'], o.get('attdec_bwd_pass',{}).get('mean_launch_us'), o.get('attdec_fwd_pass',{}).get('mean_launch_us'))"
     done
   done
