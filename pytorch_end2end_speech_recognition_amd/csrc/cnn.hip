@@ -417,26 +417,38 @@ __global__ void __launch_bounds__(CT) col_moment(const float* __restrict__ X, lo
   }
 }
 
-// out[c] = scale * sum_q partial[q][c], fixed order: 4 interleaved phases per
-// column (64 columns per block), combined in LDS.
+// out[c] = scale * sum_q partial[q][c], fixed order: 16 columns per block, 16
+// interleaved phases per column (each summing every 16th partial into four
+// accumulators), phases combined in order through LDS.  (With 64 columns x 4
+// phases per block a 128-channel layer ran 2-4 blocks of 256-long dependent
+// chains: 35 us per call for a 0.5 MB read.)
+constexpr int SP_COLS = 16;
 __global__ void __launch_bounds__(CT) sum_partials(const float* __restrict__ partial, int nchunk,
                                                    int C, float scale, float* __restrict__ out) {
   __shared__ float red[CT];
   const int tid = threadIdx.x;
-  const int cl = tid & 63, q0 = tid >> 6;
-  const int c = blockIdx.x * 64 + cl;
-  float s0 = 0.f, s1 = 0.f;
+  const int cl = tid % SP_COLS, q0 = tid / SP_COLS;
+  constexpr int NPH = CT / SP_COLS;
+  const int c = blockIdx.x * SP_COLS + cl;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   if (c < C) {
     int q = q0;
-    for (; q + 4 < nchunk; q += 8) {
+    for (; q + 3 * NPH < nchunk; q += 4 * NPH) {
       s0 += partial[(long long)q * C + c];
-      s1 += partial[(long long)(q + 4) * C + c];
+      s1 += partial[(long long)(q + NPH) * C + c];
+      s2 += partial[(long long)(q + 2 * NPH) * C + c];
+      s3 += partial[(long long)(q + 3 * NPH) * C + c];
     }
-    for (; q < nchunk; q += 4) s0 += partial[(long long)q * C + c];
+    for (; q < nchunk; q += NPH) s0 += partial[(long long)q * C + c];
   }
-  red[tid] = s0 + s1;
+  red[tid] = (s0 + s1) + (s2 + s3);
   __syncthreads();
-  if (q0 == 0 && c < C) out[c] = (red[cl] + red[64 + cl] + red[128 + cl] + red[192 + cl]) * scale;
+  if (q0 == 0 && c < C) {
+    float t = 0.f;
+#pragma unroll
+    for (int j = 0; j < NPH; ++j) t += red[j * SP_COLS + cl];
+    out[c] = t * scale;
+  }
 }
 
 // mean -> (mean, rstd) from the centred second moment; running stats update
@@ -1039,7 +1051,7 @@ extern "C" int asr_conv_direct_wgrad(const float* x, const float* dz, int B, int
                      (int)per, part);
   ASR_LAUNCH_CHECK();
   // row 0 <- column totals (each column is read entirely before its thread writes it)
-  hipLaunchKernelGGL(sum_partials, dim3((nout + 63) / 64), dim3(CT), 0, s, part, nchunk, nout,
+  hipLaunchKernelGGL(sum_partials, dim3((nout + SP_COLS - 1) / SP_COLS), dim3(CT), 0, s, part, nchunk, nout,
                      1.f, part);
   ASR_LAUNCH_CHECK();
   return asr_vgg_accumulate(part, dw, Co * Ci * 9, dbias ? part + Co * Ci * 9 : nullptr, dbias,
@@ -1154,17 +1166,17 @@ extern "C" int asr_vgg_block_forward_z(const void* z, int z_dtype, int B, int T,
       float* part = (float*)workspace;
       float* m2 = part + (size_t)nchunk * C;
       if (fused_mean) {
-        hipLaunchKernelGGL(sum_partials, dim3((C + 63) / 64), dim3(CT), 0, s, mpart, fgrid, C,
+        hipLaunchKernelGGL(sum_partials, dim3((C + SP_COLS - 1) / SP_COLS), dim3(CT), 0, s, mpart, fgrid, C,
                            1.f / (float)nr, bn_mean);
       } else {
         hipLaunchKernelGGL(col_moment, dim3(nchunk), dim3(CT), 0, s, P, nr, C, per, nullptr, 0,
                            part);
-        hipLaunchKernelGGL(sum_partials, dim3((C + 63) / 64), dim3(CT), 0, s, part, nchunk, C,
+        hipLaunchKernelGGL(sum_partials, dim3((C + SP_COLS - 1) / SP_COLS), dim3(CT), 0, s, part, nchunk, C,
                            1.f / (float)nr, bn_mean);
       }
       hipLaunchKernelGGL(col_moment, dim3(nchunk), dim3(CT), 0, s, P, nr, C, per, bn_mean, 1,
                          part);
-      hipLaunchKernelGGL(sum_partials, dim3((C + 63) / 64), dim3(CT), 0, s, part, nchunk, C,
+      hipLaunchKernelGGL(sum_partials, dim3((C + SP_COLS - 1) / SP_COLS), dim3(CT), 0, s, part, nchunk, C,
                          1.f / (float)nr, m2);
       hipLaunchKernelGGL(bn_finalize, dim3((C + CT - 1) / CT), dim3(CT), 0, s, bn_mean, m2, C, nr,
                          eps, momentum, bn_rstd, run_mean, run_var);
@@ -1295,7 +1307,7 @@ extern "C" int asr_vgg_block_backward_z(const float* dnext, int flat, const void
     else
       hipLaunchKernelGGL(bn_bwd_moments<1>, dim3(nchunk), dim3(CT), 0, s, dnext, P, B, pl.To,
                          pl.Fo, C, flat, af, per, part);
-    hipLaunchKernelGGL(sum_partials, dim3((2 * C + 63) / 64), dim3(CT), 0, s, part, nchunk, 2 * C,
+    hipLaunchKernelGGL(sum_partials, dim3((2 * C + SP_COLS - 1) / SP_COLS), dim3(CT), 0, s, part, nchunk, 2 * C,
                        1.f, sums);
     hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + CT - 1) / CT), dim3(CT), 0, s, sums, C, dgamma,
                        dbeta);
@@ -1345,7 +1357,7 @@ extern "C" int asr_vgg_block_backward_z(const float* dnext, int flat, const void
   ASR_LAUNCH_CHECK();
   if (dbias) {   // total over the blocks in order, then dbias += total
     float* tot = bpart + (size_t)pgrid * C;
-    hipLaunchKernelGGL(sum_partials, dim3((C + 63) / 64), dim3(CT), 0, s, bpart, pgrid, C, 1.f,
+    hipLaunchKernelGGL(sum_partials, dim3((C + SP_COLS - 1) / SP_COLS), dim3(CT), 0, s, bpart, pgrid, C, 1.f,
                        tot);
     ASR_LAUNCH_CHECK();
     return asr_vgg_accumulate(tot, dbias, C, nullptr, nullptr, 0, stream);
