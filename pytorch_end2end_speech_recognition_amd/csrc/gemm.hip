@@ -1740,15 +1740,34 @@ __global__ void __launch_bounds__(256) colsum_partial(const float* __restrict__ 
   if (w == 0 && n < N)
     partial[(long long)chunk * N + n] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
-__global__ void colsum_final(const float* __restrict__ partial, int nchunk, int N, float alpha,
-                             float* __restrict__ out0, float* __restrict__ out1) {
-  const int n = blockIdx.x * 256 + threadIdx.x;
-  if (n >= N) return;
-  float s = 0.f;
-  for (int c = 0; c < nchunk; ++c) s += partial[(long long)c * N + n];
-  s *= alpha;
-  out0[n] += s;
-  if (out1) out1[n] += s;
+// 16 columns x 16 phases per 256-thread block (phase q sums chunks q, q + 16,
+// ... in order; phases combined in order): one thread per column walking all
+// chunks was a latency chain for the narrow bias vectors (~11 us per call)
+__global__ void __launch_bounds__(256) colsum_final(const float* __restrict__ partial, int nchunk,
+                                                    int N, float alpha, float* __restrict__ out0,
+                                                    float* __restrict__ out1) {
+  __shared__ float red[256];
+  const int cl = threadIdx.x & 15, q0 = threadIdx.x >> 4;
+  const int n = blockIdx.x * 16 + cl;
+  float s0 = 0.f, s1 = 0.f;
+  if (n < N) {
+    int c = q0;
+    for (; c + 16 < nchunk; c += 32) {
+      s0 += partial[(long long)c * N + n];
+      s1 += partial[(long long)(c + 16) * N + n];
+    }
+    for (; c < nchunk; c += 16) s0 += partial[(long long)c * N + n];
+  }
+  red[threadIdx.x] = s0 + s1;
+  __syncthreads();
+  if (q0 == 0 && n < N) {
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) s += red[j * 16 + cl];
+    s *= alpha;
+    out0[n] += s;
+    if (out1) out1[n] += s;
+  }
 }
 
 RowMap make_map(const asr_rowmap_t& m, const void* base) {
@@ -2359,7 +2378,7 @@ extern "C" int asr_colsum_accumulate(const float* g, long long ld, int M, int N,
   hipLaunchKernelGGL(colsum_partial, dim3(ceil_div(N, 64), nchunk), dim3(256), 0, s, g, ld, M, N,
                      rpc, (float*)workspace);
   ASR_LAUNCH_CHECK();
-  hipLaunchKernelGGL(colsum_final, dim3(ceil_div(N, 256)), dim3(256), 0, s,
+  hipLaunchKernelGGL(colsum_final, dim3(ceil_div(N, 16)), dim3(256), 0, s,
                      (const float*)workspace, nchunk, N, alpha, out0, out1);
   ASR_LAUNCH_CHECK();
   return ASR_OK;

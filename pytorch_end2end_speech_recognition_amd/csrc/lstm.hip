@@ -55,8 +55,17 @@ __global__ void bias_from_partials(const float* __restrict__ part, int B, int N,
                                    float* __restrict__ db_ih, float* __restrict__ db_hh) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;
-  float s = 0.f;
-  for (int b = 0; b < B; ++b) s += part[(long long)b * N + n];
+  // four independent partial sums (every load in flight; combined in a fixed order)
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int b = 0;
+  for (; b + 4 <= B; b += 4) {
+    s0 += part[(long long)b * N + n];
+    s1 += part[(long long)(b + 1) * N + n];
+    s2 += part[(long long)(b + 2) * N + n];
+    s3 += part[(long long)(b + 3) * N + n];
+  }
+  for (; b < B; ++b) s0 += part[(long long)b * N + n];
+  const float s = (s0 + s1) + (s2 + s3);
   db_ih[n] += s;
   if (db_hh) db_hh[n] += s;
 }
