@@ -21,7 +21,8 @@ from collections import defaultdict
 FAMILIES = [
     ('lstm_bwd_pass', ('lstm_bwd_xg', 'lstm_bwd_persist')),
     ('lstm_fwd_pass', ('lstm_fwd_xg', 'lstm_fwd_persist')),
-    ('gemm', ('gemm_bf16_fast', 'gemm_kernel', 'gemm_bf16_big')),
+    ('gemm', ('gemm_bf16_fast', 'gemm_kernel', 'gemm_bf16_big', 'gemm_bf16_8r', 'gemm_bf16_n64',
+              'conv3x3_tr')),
     ('ctc_lattice', ('ctc_lattice',)),
     ('ctc_grad', ('ctc_grad',)),
     ('optim_step', ('optim_step_kernel',)),
