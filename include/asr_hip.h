@@ -653,6 +653,16 @@ int asr_conv3x3_tr(const void* in, long long P, int Cin, int Fp, int sign, const
  * x bf16 [P][Cin], dz bf16 [P][Cout]; per-chunk partials in the workspace
  * (asr_conv3x3_tr_wgrad_workspace_bytes, 0 = shape not supported), summed in a
  * fixed order (deterministic).  Cin, Cout in {64, 128}. */
+/* Weight-gradient image of the first VGG layer (one input channel) straight
+ * from the raw features xs [B][T][F] f32 (rounded to bf16 when round_bf16):
+ * packed [Co][9 Cip] f32 (overwritten) = the tap GEMM's dz^T X image over the
+ * Cip-channel padded operand whose channel 0 holds xs (channels >= 1 zero);
+ * dz bf16 [B (T+2) (F+2)][Co].  Co = 64; workspace
+ * asr_conv3x3_c1_wgrad_workspace_bytes(Co). */
+size_t asr_conv3x3_c1_wgrad_workspace_bytes(int Co);
+int asr_conv3x3_c1_wgrad_xs(const float* xs, int round_bf16, int B, int T, int F, int Co,
+                            const void* dz, int Cip, float* packed, void* ws, size_t ws_bytes,
+                            void* stream);
 /* Zero the one-pixel halo (rows t = 0, T + 1 and columns f = 0, F + 1) of a
  * channels-last padded grid [B][T+2][F+2][C] of dtype (ASR_DT_F32 / _BF16;
  * C * size % 16 == 0): the producers of the VGG layer operands write only the

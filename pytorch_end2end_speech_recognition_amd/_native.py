@@ -57,6 +57,9 @@ SIGNATURES = {
     'asr_conv3x3_tr': (c_int, [c_vp, c_ll, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_int,
                                c_vp]),
     'asr_vgg_zero_halo': (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_vp]),
+    'asr_conv3x3_c1_wgrad_workspace_bytes': (c_size, [c_int]),
+    'asr_conv3x3_c1_wgrad_xs': (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_int, c_vp,
+                                        c_vp, c_size, c_vp]),
     'asr_conv3x3_tr_wgrad_workspace_bytes': (c_size, [c_ll, c_int, c_int, c_int]),
     'asr_conv3x3_tr_wgrad': (c_int, [c_vp, c_vp, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_size,
                                      c_vp]),

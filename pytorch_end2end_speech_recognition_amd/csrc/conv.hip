@@ -749,3 +749,124 @@ extern "C" int asr_vgg_zero_halo(void* buf, int dtype, int B, int T, int F, int 
   ASR_LAUNCH_CHECK();
   return ASR_OK;
 }
+
+// ---------------------------------------------------------------------------
+// Weight gradient of the first VGG layer (one input channel), direct from the
+// raw features: packed[n][tap Cip + c] = sum_p dz[p][n] * x[p + shift(tap)][c]
+// with x the padded operand the tap GEMM would read -- channel 0 = xs (bf16-
+// rounded when round_bf16), channels 1 .. Cip-1 zero -- so the image equals
+// the tap GEMM's (the padded 16-channel operand and its 48 GFLOP product at
+// vgg_hier are no longer needed: the work is 2 x 9 x Co MACs per pixel).
+// A work-group per contiguous pixel chunk, 256-pixel tiles: dz rows and the
+// tile's x window (+- Fp + 1 rows) in LDS, the next tile's dz prefetched into
+// registers; thread (n = tid % Co, kernel row kt = tid / Co < 3) accumulates
+// its three taps; per-chunk partials summed in a fixed order.
+// ---------------------------------------------------------------------------
+namespace asr {
+namespace {
+constexpr int C1W_TP = 256;   // pixels per tile
+
+template <int CO>
+__global__ void __launch_bounds__(256) c1_wgrad_xs(const float* __restrict__ xs, int round_bf16,
+                                                    int B, int T, int F,
+                                                    const uint16_t* __restrict__ dz, int P, int S,
+                                                    float* __restrict__ slab) {
+  constexpr int NV = C1W_TP * CO * 2 / 16 / 256;   // 16-B dz pieces per thread per tile
+  extern __shared__ __attribute__((aligned(16))) char sm[];
+  uint16_t* dzt = (uint16_t*)sm;                              // [TP][CO]
+  const int Fp = F + 2, H1 = Fp + 1;
+  float* xw = (float*)(sm + C1W_TP * CO * 2);                 // [TP + 2 H1]
+  const int tid = threadIdx.x;
+  const int beg = (int)((long long)P * blockIdx.x / S), end = (int)((long long)P * (blockIdx.x + 1) / S);
+  const int n = tid % CO, kt = tid / CO;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+  const int per_b = (T + 2) * Fp;
+  auto xval = [&](int q) {   // padded operand channel 0 at padded row q
+    if (q < 0 || q >= P) return 0.f;
+    const int b = q / per_b, r = q - b * per_b, tp = r / Fp, fp = r - tp * Fp;
+    if (tp < 1 || tp > T || fp < 1 || fp > F) return 0.f;
+    const float v = xs[((long long)b * T + tp - 1) * F + fp - 1];
+    return round_bf16 ? bf2f(f2bf(v)) : v;
+  };
+  uint4 pre[NV];
+  auto fetch = [&](int p0) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int e = (j * 256 + tid) * 8;        // bf16 element within the tile
+      const int p = p0 + e / CO;
+      pre[j] = p < end ? *reinterpret_cast<const uint4*>(dz + (long long)p0 * CO + e)
+                       : make_uint4(0u, 0u, 0u, 0u);
+    }
+  };
+  if (beg < end) fetch(beg);
+  for (int p0 = beg; p0 < end; p0 += C1W_TP) {
+    __syncthreads();   // the previous tile's reads are done
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+      *reinterpret_cast<uint4*>(dzt + (j * 256 + tid) * 8) = pre[j];
+    for (int i = tid; i < C1W_TP + 2 * H1; i += 256) xw[i] = xval(p0 - H1 + i);
+    __syncthreads();
+    if (p0 + C1W_TP < end) fetch(p0 + C1W_TP);   // in flight during this tile's sums
+    if (kt < 3) {
+      const int np = min(C1W_TP, end - p0);
+      const float* xr = xw + H1 + (kt - 1) * Fp - 1;   // tap (kt, kf): x[i + (kt-1) Fp + kf - 1]
+      for (int i = 0; i < np; ++i) {
+        const float d = bf2f(dzt[i * CO + n]);
+        a0 += d * xr[i];
+        a1 += d * xr[i + 1];
+        a2 += d * xr[i + 2];
+      }
+    }
+  }
+  if (kt < 3) {
+    float* o = slab + ((size_t)blockIdx.x * CO + n) * 9 + 3 * kt;
+    o[0] = a0;
+    o[1] = a1;
+    o[2] = a2;
+  }
+}
+
+// packed[n][tap Cip + c] = (c == 0) * sum_s slab[s][n][tap] (fixed order)
+__global__ void c1_wgrad_reduce(const float* __restrict__ slab, int S, int CO, int Cip,
+                                float* __restrict__ packed) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;   // over CO * 9 * Cip
+  if (i >= CO * 9 * Cip) return;
+  const int c = i % Cip, k = i / Cip, tap = k % 9, n = k / 9;
+  float s = 0.f;
+  if (c == 0)
+    for (int q = 0; q < S; ++q) s += slab[((size_t)q * CO + n) * 9 + tap];
+  packed[i] = s;
+}
+}  // namespace
+}  // namespace asr
+
+extern "C" size_t asr_conv3x3_c1_wgrad_workspace_bytes(int Co) {
+  return (size_t)256 * Co * 9 * sizeof(float);
+}
+
+extern "C" int asr_conv3x3_c1_wgrad_xs(const float* xs, int round_bf16, int B, int T, int F,
+                                       int Co, const void* dz, int Cip, float* packed, void* ws,
+                                       size_t ws_bytes, void* stream) {
+  ASR_REQUIRE(xs && dz && packed && ws && B > 0 && T > 0 && F > 0 && Cip >= 1, ASR_ERR_ARG,
+              "conv3x3_c1_wgrad_xs: bad args");
+  ASR_REQUIRE(Co == 64, ASR_ERR_UNSUPPORTED, "conv3x3_c1_wgrad_xs: Co %d (64 only)", Co);
+  ASR_REQUIRE(((uintptr_t)dz & 15) == 0, ASR_ERR_ARG, "conv3x3_c1_wgrad_xs: dz not 16-B aligned");
+  const long long P = (long long)B * (T + 2) * (F + 2);
+  ASR_REQUIRE(P * Co * 2 < (1LL << 31), ASR_ERR_UNSUPPORTED, "conv3x3_c1_wgrad_xs: too large");
+  const int S = (int)std::min<long long>(256, std::max<long long>(1, P / 1024));
+  ASR_REQUIRE(ws_bytes >= (size_t)S * Co * 9 * sizeof(float), ASR_ERR_WORKSPACE,
+              "conv3x3_c1_wgrad_xs: workspace");
+  const size_t lds = (size_t)C1W_TP * Co * 2 + (size_t)(C1W_TP + 2 * (F + 3)) * 4;
+  ASR_REQUIRE(lds <= 64 * 1024, ASR_ERR_UNSUPPORTED, "conv3x3_c1_wgrad_xs: F too large");
+  hipStream_t s = (hipStream_t)stream;
+  const int slot = prof_begin_launch(ASR_PROF_GEMM, s, 2.0 * P * Co * 9.0);
+  hipLaunchKernelGGL(c1_wgrad_xs<64>, dim3(S), dim3(256), lds, s, xs, round_bf16, B, T, F,
+                     (const uint16_t*)dz, (int)P, S, (float*)ws);
+  ASR_LAUNCH_CHECK();
+  const int n = Co * 9 * Cip;
+  hipLaunchKernelGGL(c1_wgrad_reduce, dim3((n + 255) / 256), dim3(256), 0, s, (const float*)ws, S,
+                     Co, Cip, packed);
+  prof_end_launch(ASR_PROF_GEMM, slot, s);
+  ASR_LAUNCH_CHECK();
+  return ASR_OK;
+}

@@ -1612,10 +1612,22 @@ class VGGFn(torch.autograd.Function):
                     for l, sp in enumerate(specs)]
         cC = 1
         cCp = 16 if use_gemm[0] else 1
-        x_op = torch.empty(B * (T + 2) * (F + 2), cCp, dtype=opdt if use_gemm[0] else
-                           torch.float32, device=dev)
-        N.call('asr_vgg_pad_input_ch', N.ptr(xs), B, T, F, cCp, cd if use_gemm[0] else F32,
-               N.ptr(x_op), N.stream_handle(dev))
+        # bf16, 64-channel first layer: its forward stencil and its weight gradient
+        # (asr_conv3x3_c1_wgrad_xs) both read the raw features, so the padded
+        # 16-channel operand is never built
+        co0 = specs[0]['w'].shape[0]
+        c1w = (cd == BF16 and use_gemm[0] and co0 == 64 and
+               os.environ.get('ASR_VGG_C1_DIRECT', '1') != '0' and
+               os.environ.get('ASR_VGG_C1_XS', '1') != '0' and
+               os.environ.get('ASR_VGG_C1_WGRAD', '1') != '0')
+        if c1w:
+            x_op = xs
+        else:
+            x_op = torch.empty(B * (T + 2) * (F + 2), cCp, dtype=opdt if use_gemm[0] else
+                               torch.float32, device=dev)
+            N.call('asr_vgg_pad_input_ch', N.ptr(xs), B, T, F, cCp, cd if use_gemm[0] else F32,
+                   N.ptr(x_op), N.stream_handle(dev))
+        ctx.c1w = c1w
         cT, cF = T, F
         saved, layers = [], []
         L = len(specs)
@@ -1774,7 +1786,12 @@ class VGGFn(torch.autograd.Function):
             else:
                 # dW image [Co][9 Ci] = dz^T X (taps on the output index), K = padded pixels
                 packed = torch.empty(Co, 9 * cCp, **f32)
-                if not conv3x3_tr_wgrad(x_op, dz, npad, cCp, cF + 2, Co, packed):
+                if l == 0 and ctx.c1w:   # x_op is the raw features xs
+                    nb = N.query('asr_conv3x3_c1_wgrad_workspace_bytes', Co)
+                    ws = _ws(nb, dev)
+                    N.call('asr_conv3x3_c1_wgrad_xs', N.ptr(x_op), 1, B, cT, cF, Co, N.ptr(dz), cCp,
+                           N.ptr(packed), N.ptr(ws), nb, N.stream_handle(dev))
+                elif not conv3x3_tr_wgrad(x_op, dz, npad, cCp, cF + 2, Co, packed):
                     run_gemm([gemm_problem(operand(dz, 1, rowmap(Co)),
                                            _tap_operand(x_op, 1, cCp, cCp, cF + 2, 1), packed,
                                            rowmap(9 * cCp), Co, 9 * cCp, npad)], dev)

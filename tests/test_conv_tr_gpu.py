@@ -178,3 +178,32 @@ def test_conv_tr_wgrad_random_vs_tap_gemm(Ci, Co, F, cuda_dev):
         assert rel < 1e-5, rel
     finally:
         ops.set_compute_dtype('fp32')
+
+
+@pytest.mark.parametrize('T,F', [(61, 30), (203, 80)])
+def test_conv_c1_wgrad_xs_integer_exact(T, F, cuda_dev):
+    """First-layer weight-gradient image straight from the raw features equals
+    the tap GEMM's image over the 16-channel padded operand, bit for bit on
+    small-integer values (channel 0 = xs, the others zero)."""
+    ops.set_compute_dtype('bf16')
+    try:
+        rng = np.random.RandomState(T + F)
+        B, Co, Cip = 3, 64, 16
+        xs = rng.randint(-3, 4, (B, T, F)).astype(np.float32)
+        g = rng.randint(-3, 4, (B, Co, F, T)).astype(np.float64)
+        xs_d = torch.from_numpy(xs).to(cuda_dev)
+        gb = _padded(g, T, F, cuda_dev).to(torch.bfloat16)
+        npad = gb.shape[0]
+        x_op = torch.empty(npad, Cip, dtype=torch.bfloat16, device=cuda_dev)
+        N.call('asr_vgg_pad_input_ch', N.ptr(xs_d), B, T, F, Cip, N.ASR_DT_BF16, N.ptr(x_op),
+               N.stream_handle(cuda_dev))
+        ref = _gemm_wgrad(x_op, gb, Cip, F + 2, Co)
+        packed = torch.full((Co, 9 * Cip), 7.0, device=cuda_dev)
+        nb = N.query('asr_conv3x3_c1_wgrad_workspace_bytes', Co)
+        ws = torch.empty(nb, dtype=torch.uint8, device=cuda_dev)
+        N.call('asr_conv3x3_c1_wgrad_xs', N.ptr(xs_d), 1, B, T, F, Co, N.ptr(gb), Cip,
+               N.ptr(packed), N.ptr(ws), nb, N.stream_handle(cuda_dev))
+        torch.cuda.synchronize()
+        assert torch.equal(packed, ref)
+    finally:
+        ops.set_compute_dtype('fp32')
