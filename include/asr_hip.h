@@ -717,6 +717,16 @@ int asr_vgg_block_backward_z(const float* dnext, int flat, const void* z, int z_
                              const float* bn_rstd, float* dgamma, float* dbeta, float drop,
                              unsigned long long seed, void* dz, int dz_dtype, float* dbias,
                              void* workspace, size_t ws_bytes, void* stream);
+/* asr_vgg_block_backward_z with the incoming gradient's dtype: dnext_dtype
+ * ASR_DT_BF16 (C % 4 == 0, bf16 z and dz, full-resolution pass) reads a bf16
+ * dnext (the input-gradient convolution of the layer above writes it so). */
+int asr_vgg_block_backward_zd(const void* dnext, int dnext_dtype, int flat, const void* z,
+                              int z_dtype, int B, int T, int F, int C, int pt, int pf,
+                              int ceil_mode, const float* P, const uint8_t* slot,
+                              const float* gamma, const float* bn_mean, const float* bn_rstd,
+                              float* dgamma, float* dbeta, float drop, unsigned long long seed,
+                              void* dz, int dz_dtype, float* dbias, void* workspace,
+                              size_t ws_bytes, void* stream);
 
 /* ----------------------------------------------------------- profiling
  * Sampled HIP-event timing of the recurrence step kernels on their own stream

@@ -532,8 +532,8 @@ __global__ void apply_fwd(const float* __restrict__ P, int B, int To, int Fo, in
 // dy (after the dropout mask) of the V elements at (pooled pixel q, channel c),
 // from the next layer's dX (padded rows, flat = 0) or the encoder's gradient
 // [B][T'][F'][C] (flat = 1).
-template <int V>
-__device__ __forceinline__ VecF<V> dy_at(const float* __restrict__ dnext, unsigned q, int c,
+template <int V, typename TD = float>
+__device__ __forceinline__ VecF<V> dy_at(const TD* __restrict__ dnext, unsigned q, int c,
                                          int To, int Fo, int C, int flat, float drop,
                                          unsigned long long seed) {
   const long long i = (long long)q * C + c;
@@ -554,8 +554,8 @@ __device__ __forceinline__ VecF<V> dy_at(const float* __restrict__ dnext, unsign
 // partial[chunk][c] = sum dy, partial[chunk][C + c] = sum dy * xhat over the
 // chunk's rows: thread (channel group, row phase), V channels per thread,
 // row phases combined in LDS in order
-template <int V>
-__global__ void __launch_bounds__(CT) bn_bwd_moments(const float* __restrict__ dnext,
+template <int V, typename TD = float>
+__global__ void __launch_bounds__(CT) bn_bwd_moments(const TD* __restrict__ dnext,
                                                      const float* __restrict__ P, int B, int To,
                                                      int Fo, int C, int flat, Affine af,
                                                      long long rows_per,
@@ -697,8 +697,8 @@ __global__ void __launch_bounds__(CT) post_bwd(const float* __restrict__ dnext,
 // time (554 us at the first pooled vgg_hier layer).  The window's gradient is
 // recomputed by each of its pixels (dnext / P / slot are a quarter of z's
 // size and come from the cache).  Bias partials as in post_bwd.
-template <typename TO, typename TZ = float>
-__global__ void __launch_bounds__(CT) post_bwd_full(const float* __restrict__ dnext,
+template <typename TO, typename TZ = float, typename TD = float>
+__global__ void __launch_bounds__(CT) post_bwd_full(const TD* __restrict__ dnext,
                                                     const float* __restrict__ P,
                                                     const TZ* __restrict__ z,
                                                     const uint8_t* __restrict__ slot, int B, int T,
@@ -1260,17 +1260,26 @@ extern "C" int asr_vgg_block_backward_ex(const float* dnext, int flat, const flo
                                   dz_dtype, dbias, workspace, ws_bytes, stream);
 }
 
-// z_dtype ASR_DT_BF16: the saved conv output z is bf16 (the ReLU mask read back)
-extern "C" int asr_vgg_block_backward_z(const float* dnext, int flat, const void* z,
-                                        int z_dtype, int B, int T, int F, int C, int pt, int pf,
-                                        int ceil_mode, const float* P, const uint8_t* slot,
-                                        const float* gamma, const float* bn_mean,
-                                        const float* bn_rstd, float* dgamma, float* dbeta,
-                                        float drop, unsigned long long seed, void* dz,
-                                        int dz_dtype, float* dbias, void* workspace,
-                                        size_t ws_bytes, void* stream) {
+// z_dtype ASR_DT_BF16: the saved conv output z is bf16 (the ReLU mask read back);
+// dnext_dtype ASR_DT_BF16 (full-resolution pass with C % 4 == 0 only): the
+// incoming gradient is bf16 (the input-gradient convolution writes it so)
+extern "C" int asr_vgg_block_backward_zd(const void* dnext_v, int dnext_dtype, int flat,
+                                         const void* z, int z_dtype, int B, int T, int F, int C,
+                                         int pt, int pf, int ceil_mode, const float* P,
+                                         const uint8_t* slot, const float* gamma,
+                                         const float* bn_mean, const float* bn_rstd,
+                                         float* dgamma, float* dbeta, float drop,
+                                         unsigned long long seed, void* dz, int dz_dtype,
+                                         float* dbias, void* workspace, size_t ws_bytes,
+                                         void* stream) {
+  const float* dnext = (const float*)dnext_v;
+  const uint16_t* dnh = (const uint16_t*)dnext_v;
+  const bool db16 = dnext_dtype == ASR_DT_BF16;
   ASR_REQUIRE(dnext && z && P && dz && B > 0 && T > 0 && F > 0 && C > 0, ASR_ERR_ARG,
               "vgg_block_backward: bad args");
+  ASR_REQUIRE(!db16 || (C % 4 == 0 && z_dtype == ASR_DT_BF16 && dz_dtype == ASR_DT_BF16 &&
+                        ((uintptr_t)dnh & 7) == 0),
+              ASR_ERR_UNSUPPORTED, "vgg_block_backward: bf16 dnext needs the bf16 full pass");
   const Pool pl = make_pool(T, F, pt, pf, ceil_mode);
   hipStream_t s = (hipStream_t)stream;
   const long long nr = (long long)B * pl.To * pl.Fo;
@@ -1301,7 +1310,10 @@ extern "C" int asr_vgg_block_backward_z(const float* dnext, int flat, const void
     const int nchunk = (int)((nr + per - 1) / per);
     float* part = (float*)workspace;
     sums = part + (size_t)nchunk * 2 * C;
-    if (v4)
+    if (db16)
+      hipLaunchKernelGGL((bn_bwd_moments<4, uint16_t>), dim3(nchunk), dim3(CT), 0, s, dnh, P, B,
+                         pl.To, pl.Fo, C, flat, af, per, part);
+    else if (v4)
       hipLaunchKernelGGL(bn_bwd_moments<4>, dim3(nchunk), dim3(CT), 0, s, dnext, P, B, pl.To,
                          pl.Fo, C, flat, af, per, part);
     else
@@ -1320,7 +1332,11 @@ extern "C" int asr_vgg_block_backward_z(const float* dnext, int flat, const void
   ASR_REQUIRE(!zb || v4, ASR_ERR_UNSUPPORTED, "vgg_block_backward: bf16 z needs C % 4 == 0");
   const float* zf = (const float*)z;
   const uint16_t* zh = (const uint16_t*)z;
-  if (zb) {
+  ASR_REQUIRE(!db16 || full, ASR_ERR_UNSUPPORTED, "vgg_block_backward: bf16 dnext needs the full pass");
+  if (db16) {
+    hipLaunchKernelGGL((post_bwd_full<uint16_t, uint16_t, uint16_t>), dim3(pgrid), dim3(CT), 0, s,
+                       dnh, P, zh, slot, B, T, F, C, pl, flat, af, sums, (uint16_t*)dz, bpart);
+  } else if (zb) {
     if (full && dz_dtype == ASR_DT_BF16)
       hipLaunchKernelGGL((post_bwd_full<uint16_t, uint16_t>), dim3(pgrid), dim3(CT), 0, s, dnext,
                          P, zh, slot, B, T, F, C, pl, flat, af, sums, (uint16_t*)dz, bpart);
@@ -1364,4 +1380,17 @@ extern "C" int asr_vgg_block_backward_z(const float* dnext, int flat, const void
   }
   ASR_LAUNCH_CHECK();
   return ASR_OK;
+}
+
+extern "C" int asr_vgg_block_backward_z(const float* dnext, int flat, const void* z,
+                                        int z_dtype, int B, int T, int F, int C, int pt, int pf,
+                                        int ceil_mode, const float* P, const uint8_t* slot,
+                                        const float* gamma, const float* bn_mean,
+                                        const float* bn_rstd, float* dgamma, float* dbeta,
+                                        float drop, unsigned long long seed, void* dz,
+                                        int dz_dtype, float* dbias, void* workspace,
+                                        size_t ws_bytes, void* stream) {
+  return asr_vgg_block_backward_zd(dnext, ASR_DT_F32, flat, z, z_dtype, B, T, F, C, pt, pf,
+                                   ceil_mode, P, slot, gamma, bn_mean, bn_rstd, dgamma, dbeta,
+                                   drop, seed, dz, dz_dtype, dbias, workspace, ws_bytes, stream);
 }

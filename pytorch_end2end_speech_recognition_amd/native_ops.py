@@ -1745,7 +1745,8 @@ class VGGFn(torch.autograd.Function):
             nb = N.query('asr_vgg_block_workspace_bytes', B, To, Fo, Co)
             ws = _ws(nb, dev)
             bn = sp['gamma'] is not None
-            N.call('asr_vgg_block_backward_z', N.ptr(dnext), flat, N.ptr(z),
+            N.call('asr_vgg_block_backward_zd', N.ptr(dnext),
+                   BF16 if dnext.dtype == torch.bfloat16 else F32, flat, N.ptr(z),
                    BF16 if z.dtype == torch.bfloat16 else F32, B, cT, cF, Co, pt,
                    pf, ceil, N.ptr(P), N.ptr(slot), N.ptr(sp['gamma']), N.ptr(mean), N.ptr(rstd),
                    N.ptr(grad_buffer(sp['gamma']) if bn else None),
@@ -1803,7 +1804,16 @@ class VGGFn(torch.autograd.Function):
             wt = torch.empty(cC, 9 * Co, dtype=opdt, device=dev)
             N.call('asr_conv_weight_pack', N.ptr(w), Co, cC, 1, cd, N.ptr(wt),
                    N.stream_handle(dev))
-            dx = torch.empty(npad, cC, **f32)
+            # bf16 mode: the input gradient goes to the layer below as bf16 when that
+            # layer's pool / ReLU / BN backward reads it on its bf16 full-resolution
+            # pass (half the bytes of the largest tensors of the VGG backward)
+            lo = layers[l - 1]
+            dx_bf = (cd == BF16 and lo[10] and cC % 4 == 0 and
+                     saved[6 * (l - 1) + 1].dtype == torch.bfloat16 and
+                     os.environ.get('ASR_VGG_POST_FULL', '1') != '0' and
+                     os.environ.get('ASR_VGG_DX_BF16', '1') != '0')
+            dx = torch.empty(npad, cC, dtype=torch.bfloat16 if dx_bf else torch.float32,
+                             device=dev)
             if _conv_tr_ok(Co, cC, cF + 2):
                 conv3x3_tr(dz, npad, Co, cF + 2, -1, wt, cC, None, dx)
             else:

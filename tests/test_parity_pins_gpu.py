@@ -131,6 +131,9 @@ def test_vgg_c1_direct_stencil_equals_tap_gemm(prec, cuda_dev, monkeypatch):
     asr_conv3x3_c1_wgrad_xs, sums the pixels in another order and has its own
     exact test in test_conv_tr_gpu.py.)"""
     monkeypatch.setenv('ASR_VGG_C1_WGRAD', '0')
+    # (and the layer-0 input gradient kept f32: with the tap GEMM layer 0's z is
+    # f32, which keeps its incoming gradient f32 too)
+    monkeypatch.setenv('ASR_VGG_DX_BF16', '0')
     kw = dict(VGG_PROD, input_size=40)
     model = _ctc(kw)
     rng = np.random.RandomState(3)
@@ -151,6 +154,8 @@ def test_vgg_c1_direct_stencil_equals_tap_gemm(prec, cuda_dev, monkeypatch):
 @pytest.mark.gpu
 @pytest.mark.parametrize('prec', ['bf16', 'fp32'])
 def test_vgg_post_bwd_full_equals_gather_form(prec, cuda_dev, monkeypatch):
+    # the gather form reads an f32 incoming gradient: keep the full pass's f32 too
+    monkeypatch.setenv('ASR_VGG_DX_BF16', '0')
     kw = dict(VGG_PROD, input_size=40)
     model = _ctc(kw)
     model.set_cuda()
