@@ -727,6 +727,24 @@ int asr_vgg_block_backward_zd(const void* dnext, int dnext_dtype, int flat, cons
                               float* dgamma, float* dbeta, float drop, unsigned long long seed,
                               void* dz, int dz_dtype, float* dbias, void* workspace,
                               size_t ws_bytes, void* stream);
+/* The two above with the pooled-value store P of dtype p_dtype: ASR_DT_BF16
+ * (bf16 z, C % 4 == 0, P 8-B aligned) stores P = max(0, max z) as bf16 --
+ * exact, since every candidate is a bf16 value -- halving P's write and its
+ * four reads (BN moments, BN apply, BN backward moments, ReLU mask). */
+int asr_vgg_block_forward_zp(const void* z, int z_dtype, int B, int T, int F, int C, int pt,
+                             int pf, int ceil_mode, void* P, int p_dtype, uint8_t* slot,
+                             const float* gamma, const float* beta, float* run_mean,
+                             float* run_var, int training, float momentum, float eps,
+                             float* bn_mean, float* bn_rstd, float drop, unsigned long long seed,
+                             void* out, int out_dtype, int flat, void* workspace,
+                             size_t ws_bytes, void* stream);
+int asr_vgg_block_backward_zdp(const void* dnext, int dnext_dtype, int flat, const void* z,
+                               int z_dtype, int B, int T, int F, int C, int pt, int pf,
+                               int ceil_mode, const void* P, int p_dtype, const uint8_t* slot,
+                               const float* gamma, const float* bn_mean, const float* bn_rstd,
+                               float* dgamma, float* dbeta, float drop, unsigned long long seed,
+                               void* dz, int dz_dtype, float* dbias, void* workspace,
+                               size_t ws_bytes, void* stream);
 
 /* ----------------------------------------------------------- profiling
  * Sampled HIP-event timing of the recurrence step kernels on their own stream

@@ -171,6 +171,14 @@ SIGNATURES = {
                                          c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                          c_vp, c_float, ctypes.c_ulonglong, c_vp, c_int, c_vp, c_vp,
                                          c_size, c_vp]),
+    'asr_vgg_block_forward_zp': (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                         c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
+                                         c_float, c_float, c_vp, c_vp, c_float, ctypes.c_ulonglong,
+                                         c_vp, c_int, c_int, c_vp, c_size, c_vp]),
+    'asr_vgg_block_backward_zdp': (c_int, [c_vp, c_int, c_int, c_vp, c_int, c_int, c_int, c_int,
+                                           c_int, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp,
+                                           c_vp, c_vp, c_vp, c_vp, c_float, ctypes.c_ulonglong,
+                                           c_vp, c_int, c_vp, c_vp, c_size, c_vp]),
     'asr_prof_begin': (c_int, [c_int]),
     'asr_prof_end': (c_int, [c_vp, c_vp, c_vp, c_int]),
     'asr_lstm_persist_status': (c_int, [c_vp, c_int, c_vp]),

@@ -284,6 +284,7 @@ struct VecF<1> {
   __device__ __forceinline__ void load(const float* p) { v[0] = *p; }
   __device__ __forceinline__ void load(const uint16_t* p) { v[0] = bf2f(*p); }
   __device__ __forceinline__ void store(float* p) const { *p = v[0]; }
+  __device__ __forceinline__ void store(uint16_t* p) const { *p = f2bf(v[0]); }
 };
 template <>
 struct VecF<4> {
@@ -300,14 +301,21 @@ struct VecF<4> {
   __device__ __forceinline__ void store(float* p) const {
     *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
   }
+  __device__ __forceinline__ void store(uint16_t* p) const {   // four bf16 (8-B aligned)
+    *reinterpret_cast<uint2*>(p) =
+        make_uint2(f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16), f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16));
+  }
 };
+__device__ __forceinline__ float ld1(const float* p) { return *p; }
+__device__ __forceinline__ float ld1(const uint16_t* p) { return bf2f(*p); }
 
 // P[b][t'][f'][c] = max over the window of relu(z); slot = argmax in torch's
 // scan order (freq outer, time inner; first maximum wins).  V channels per
 // thread (V = 4 when C % 4 == 0).
-template <int V, typename TZ = float>
+// TP = uint16_t (bf16 z only): P = max(0, max z) is a bf16 value, stored exactly.
+template <int V, typename TZ = float, typename TP = float>
 __global__ void __launch_bounds__(CT) post_fwd(const TZ* __restrict__ z, int B, int T, int F,
-                                               int C, Pool pl, float* __restrict__ P,
+                                               int C, Pool pl, TP* __restrict__ P,
                                                uint8_t* __restrict__ slot,
                                                float* __restrict__ mpart) {
   // mpart (nullable): per-block column sums of the P values written (the batch
@@ -380,7 +388,8 @@ __global__ void __launch_bounds__(CT) post_fwd(const TZ* __restrict__ z, int B, 
 // sum over the chunk's rows of (x - shift[c]) (shift = nullptr: 0) or of its
 // square.  The block's threads split the rows into CT / C interleaved phases
 // (C divides CT), four accumulators each; phases combine in LDS in order.
-__global__ void __launch_bounds__(CT) col_moment(const float* __restrict__ X, long long n, int C,
+template <typename TP = float>
+__global__ void __launch_bounds__(CT) col_moment(const TP* __restrict__ X, long long n, int C,
                                                  long long rows_per,
                                                  const float* __restrict__ shift, int square,
                                                  float* __restrict__ partial) {
@@ -395,15 +404,15 @@ __global__ void __launch_bounds__(CT) col_moment(const float* __restrict__ X, lo
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
     long long r = r0 + q;
     for (; r + 3 * ph < r1; r += 4 * ph) {
-      const float d0 = X[r * C + c] - m, d1 = X[(r + ph) * C + c] - m;
-      const float d2 = X[(r + 2 * ph) * C + c] - m, d3 = X[(r + 3 * ph) * C + c] - m;
+      const float d0 = ld1(X + r * C + c) - m, d1 = ld1(X + (r + ph) * C + c) - m;
+      const float d2 = ld1(X + (r + 2 * ph) * C + c) - m, d3 = ld1(X + (r + 3 * ph) * C + c) - m;
       s0 += square ? d0 * d0 : d0;
       s1 += square ? d1 * d1 : d1;
       s2 += square ? d2 * d2 : d2;
       s3 += square ? d3 * d3 : d3;
     }
     for (; r < r1; r += ph) {
-      const float d = X[r * C + c] - m;
+      const float d = ld1(X + r * C + c) - m;
       s0 += square ? d * d : d;
     }
     acc = (s0 + s1) + (s2 + s3);
@@ -487,8 +496,8 @@ struct Affine {
 
 // y = dropout(BN(P)); written to the next layer's padded input (bf16 / f32,
 // halo untouched: the caller zeroes it) or, out_flat, to [B][T'][F'][C].
-template <typename TO, int V>
-__global__ void apply_fwd(const float* __restrict__ P, int B, int To, int Fo, int C, Affine af,
+template <typename TO, int V, typename TP = float>
+__global__ void apply_fwd(const TP* __restrict__ P, int B, int To, int Fo, int C, Affine af,
                           TO* __restrict__ out, int flat) {
   const unsigned CV = (unsigned)(C / V);
   const unsigned n = (unsigned)B * To * Fo * CV;
@@ -554,9 +563,9 @@ __device__ __forceinline__ VecF<V> dy_at(const TD* __restrict__ dnext, unsigned 
 // partial[chunk][c] = sum dy, partial[chunk][C + c] = sum dy * xhat over the
 // chunk's rows: thread (channel group, row phase), V channels per thread,
 // row phases combined in LDS in order
-template <int V, typename TD = float>
+template <int V, typename TD = float, typename TP = float>
 __global__ void __launch_bounds__(CT) bn_bwd_moments(const TD* __restrict__ dnext,
-                                                     const float* __restrict__ P, int B, int To,
+                                                     const TP* __restrict__ P, int B, int To,
                                                      int Fo, int C, int flat, Affine af,
                                                      long long rows_per,
                                                      float* __restrict__ partial) {
@@ -619,9 +628,9 @@ __global__ void bn_bwd_finalize(const float* __restrict__ sums, int C, float* __
 // bias gradient before its fixed-order sum over blocks -- so dZ itself can be
 // a bf16 GEMM operand (C divides the block size: a thread's channels are the
 // same in every grid-stride iteration).
-template <typename TO, int V, typename TZ = float>
+template <typename TO, int V, typename TZ = float, typename TP = float>
 __global__ void __launch_bounds__(CT) post_bwd(const float* __restrict__ dnext,
-                                               const float* __restrict__ P,
+                                               const TP* __restrict__ P,
                                                const TZ* __restrict__ z,
                                                const uint8_t* __restrict__ slot, int B, int T,
                                                int F, int C, Pool pl, int flat, Affine af,
@@ -697,9 +706,9 @@ __global__ void __launch_bounds__(CT) post_bwd(const float* __restrict__ dnext,
 // time (554 us at the first pooled vgg_hier layer).  The window's gradient is
 // recomputed by each of its pixels (dnext / P / slot are a quarter of z's
 // size and come from the cache).  Bias partials as in post_bwd.
-template <typename TO, typename TZ = float, typename TD = float>
+template <typename TO, typename TZ = float, typename TD = float, typename TP = float>
 __global__ void __launch_bounds__(CT) post_bwd_full(const TD* __restrict__ dnext,
-                                                    const float* __restrict__ P,
+                                                    const TP* __restrict__ P,
                                                     const TZ* __restrict__ z,
                                                     const uint8_t* __restrict__ slot, int B, int T,
                                                     int F, int C, Pool pl, int flat, Affine af,
@@ -1108,13 +1117,14 @@ extern "C" int asr_vgg_block_forward(const float* z, int B, int T, int F, int C,
 }
 
 // z_dtype ASR_DT_BF16: the conv output z is bf16 (P and the statistics stay f32)
-extern "C" int asr_vgg_block_forward_z(const void* z, int z_dtype, int B, int T, int F, int C,
-                                       int pt, int pf, int ceil_mode, float* P, uint8_t* slot,
-                                       const float* gamma, const float* beta, float* run_mean,
-                                       float* run_var, int training, float momentum, float eps,
-                                       float* bn_mean, float* bn_rstd, float drop,
-                                       unsigned long long seed, void* out, int out_dtype, int flat,
-                                       void* workspace, size_t ws_bytes, void* stream) {
+// TP: the pooled-value store P (float, or bf16 when z is bf16 -- exact)
+template <typename TP>
+static int vgg_block_forward_impl(const void* z, int z_dtype, int B, int T, int F, int C, int pt,
+                                  int pf, int ceil_mode, TP* P, uint8_t* slot, const float* gamma,
+                                  const float* beta, float* run_mean, float* run_var, int training,
+                                  float momentum, float eps, float* bn_mean, float* bn_rstd,
+                                  float drop, unsigned long long seed, void* out, int out_dtype,
+                                  int flat, void* workspace, size_t ws_bytes, void* stream) {
   ASR_REQUIRE(z && P && out && B > 0 && T > 0 && F > 0 && C > 0, ASR_ERR_ARG,
               "vgg_block_forward: bad args");
   ASR_REQUIRE(!pt || slot, ASR_ERR_ARG, "vgg_block_forward: pooling needs slot");
@@ -1145,13 +1155,13 @@ extern "C" int asr_vgg_block_forward_z(const void* z, int z_dtype, int B, int T,
   ASR_REQUIRE(!zb || (v4 && ((uintptr_t)z & 7) == 0), ASR_ERR_UNSUPPORTED,
               "vgg_block_forward: bf16 z needs C % 4 == 0 and 8-B alignment");
   if (zb)
-    hipLaunchKernelGGL((post_fwd<4, uint16_t>), dim3(fgrid), dim3(CT), 0, s, (const uint16_t*)z, B,
+    hipLaunchKernelGGL((post_fwd<4, uint16_t, TP>), dim3(fgrid), dim3(CT), 0, s, (const uint16_t*)z, B,
                        T, F, C, pl, P, slot, mpart);
   else if (v4)
-    hipLaunchKernelGGL(post_fwd<4>, dim3(fgrid), dim3(CT), 0, s, (const float*)z, B, T, F, C, pl,
+    hipLaunchKernelGGL((post_fwd<4, float, TP>), dim3(fgrid), dim3(CT), 0, s, (const float*)z, B, T, F, C, pl,
                        P, slot, mpart);
   else
-    hipLaunchKernelGGL(post_fwd<1>, dim3(post_grid(nr, C)), dim3(CT), 0, s, (const float*)z, B, T,
+    hipLaunchKernelGGL((post_fwd<1, float, TP>), dim3(post_grid(nr, C)), dim3(CT), 0, s, (const float*)z, B, T,
                        F, C, pl, P, slot, (float*)nullptr);
   ASR_LAUNCH_CHECK();
   Affine af{nullptr, nullptr, nullptr, nullptr, drop, seed};
@@ -1169,12 +1179,12 @@ extern "C" int asr_vgg_block_forward_z(const void* z, int z_dtype, int B, int T,
         hipLaunchKernelGGL(sum_partials, dim3((C + SP_COLS - 1) / SP_COLS), dim3(CT), 0, s, mpart, fgrid, C,
                            1.f / (float)nr, bn_mean);
       } else {
-        hipLaunchKernelGGL(col_moment, dim3(nchunk), dim3(CT), 0, s, P, nr, C, per, nullptr, 0,
+        hipLaunchKernelGGL(col_moment<TP>, dim3(nchunk), dim3(CT), 0, s, P, nr, C, per, nullptr, 0,
                            part);
         hipLaunchKernelGGL(sum_partials, dim3((C + SP_COLS - 1) / SP_COLS), dim3(CT), 0, s, part, nchunk, C,
                            1.f / (float)nr, bn_mean);
       }
-      hipLaunchKernelGGL(col_moment, dim3(nchunk), dim3(CT), 0, s, P, nr, C, per, bn_mean, 1,
+      hipLaunchKernelGGL(col_moment<TP>, dim3(nchunk), dim3(CT), 0, s, P, nr, C, per, bn_mean, 1,
                          part);
       hipLaunchKernelGGL(sum_partials, dim3((C + SP_COLS - 1) / SP_COLS), dim3(CT), 0, s, part, nchunk, C,
                          1.f / (float)nr, m2);
@@ -1194,21 +1204,56 @@ extern "C" int asr_vgg_block_forward_z(const void* z, int z_dtype, int B, int T,
   const long long ng = v4 ? nr * C / 4 : nr * C;
   if (out_dtype == ASR_DT_BF16 && !flat) {
     if (v4)
-      hipLaunchKernelGGL((apply_fwd<uint16_t, 4>), dim3(grid_for(ng)), dim3(CT), 0, s, P, B,
+      hipLaunchKernelGGL((apply_fwd<uint16_t, 4, TP>), dim3(grid_for(ng)), dim3(CT), 0, s, P, B,
                          pl.To, pl.Fo, C, af, (uint16_t*)out, 0);
     else
-      hipLaunchKernelGGL((apply_fwd<uint16_t, 1>), dim3(grid_for(ng)), dim3(CT), 0, s, P, B,
+      hipLaunchKernelGGL((apply_fwd<uint16_t, 1, TP>), dim3(grid_for(ng)), dim3(CT), 0, s, P, B,
                          pl.To, pl.Fo, C, af, (uint16_t*)out, 0);
   } else {
     if (v4)
-      hipLaunchKernelGGL((apply_fwd<float, 4>), dim3(grid_for(ng)), dim3(CT), 0, s, P, B, pl.To,
+      hipLaunchKernelGGL((apply_fwd<float, 4, TP>), dim3(grid_for(ng)), dim3(CT), 0, s, P, B, pl.To,
                          pl.Fo, C, af, (float*)out, flat);
     else
-      hipLaunchKernelGGL((apply_fwd<float, 1>), dim3(grid_for(ng)), dim3(CT), 0, s, P, B, pl.To,
+      hipLaunchKernelGGL((apply_fwd<float, 1, TP>), dim3(grid_for(ng)), dim3(CT), 0, s, P, B, pl.To,
                          pl.Fo, C, af, (float*)out, flat);
   }
   ASR_LAUNCH_CHECK();
   return ASR_OK;
+}
+
+extern "C" int asr_vgg_block_forward_zp(const void* z, int z_dtype, int B, int T, int F, int C,
+                                        int pt, int pf, int ceil_mode, void* P, int p_dtype,
+                                        uint8_t* slot, const float* gamma, const float* beta,
+                                        float* run_mean, float* run_var, int training,
+                                        float momentum, float eps, float* bn_mean, float* bn_rstd,
+                                        float drop, unsigned long long seed, void* out,
+                                        int out_dtype, int flat, void* workspace, size_t ws_bytes,
+                                        void* stream) {
+  if (p_dtype == ASR_DT_BF16) {
+    ASR_REQUIRE(z_dtype == ASR_DT_BF16 && C % 4 == 0 && ((uintptr_t)P & 7) == 0,
+                ASR_ERR_UNSUPPORTED, "vgg_block_forward: bf16 P needs bf16 z and C %% 4 == 0");
+    return vgg_block_forward_impl(z, z_dtype, B, T, F, C, pt, pf, ceil_mode, (uint16_t*)P, slot,
+                                  gamma, beta, run_mean, run_var, training, momentum, eps,
+                                  bn_mean, bn_rstd, drop, seed, out, out_dtype, flat, workspace,
+                                  ws_bytes, stream);
+  }
+  ASR_REQUIRE(p_dtype == ASR_DT_F32, ASR_ERR_ARG, "vgg_block_forward: P dtype %d", p_dtype);
+  return vgg_block_forward_impl(z, z_dtype, B, T, F, C, pt, pf, ceil_mode, (float*)P, slot, gamma,
+                                beta, run_mean, run_var, training, momentum, eps, bn_mean, bn_rstd,
+                                drop, seed, out, out_dtype, flat, workspace, ws_bytes, stream);
+}
+
+extern "C" int asr_vgg_block_forward_z(const void* z, int z_dtype, int B, int T, int F, int C,
+                                       int pt, int pf, int ceil_mode, float* P, uint8_t* slot,
+                                       const float* gamma, const float* beta, float* run_mean,
+                                       float* run_var, int training, float momentum, float eps,
+                                       float* bn_mean, float* bn_rstd, float drop,
+                                       unsigned long long seed, void* out, int out_dtype, int flat,
+                                       void* workspace, size_t ws_bytes, void* stream) {
+  return asr_vgg_block_forward_zp(z, z_dtype, B, T, F, C, pt, pf, ceil_mode, P, ASR_DT_F32, slot,
+                                  gamma, beta, run_mean, run_var, training, momentum, eps, bn_mean,
+                                  bn_rstd, drop, seed, out, out_dtype, flat, workspace, ws_bytes,
+                                  stream);
 }
 
 // Backward of asr_vgg_block_forward (same geometry / saved tensors): dnext is
@@ -1263,15 +1308,14 @@ extern "C" int asr_vgg_block_backward_ex(const float* dnext, int flat, const flo
 // z_dtype ASR_DT_BF16: the saved conv output z is bf16 (the ReLU mask read back);
 // dnext_dtype ASR_DT_BF16 (full-resolution pass with C % 4 == 0 only): the
 // incoming gradient is bf16 (the input-gradient convolution writes it so)
-extern "C" int asr_vgg_block_backward_zd(const void* dnext_v, int dnext_dtype, int flat,
-                                         const void* z, int z_dtype, int B, int T, int F, int C,
-                                         int pt, int pf, int ceil_mode, const float* P,
-                                         const uint8_t* slot, const float* gamma,
-                                         const float* bn_mean, const float* bn_rstd,
-                                         float* dgamma, float* dbeta, float drop,
-                                         unsigned long long seed, void* dz, int dz_dtype,
-                                         float* dbias, void* workspace, size_t ws_bytes,
-                                         void* stream) {
+template <typename TP>
+static int vgg_block_backward_impl(const void* dnext_v, int dnext_dtype, int flat, const void* z,
+                                   int z_dtype, int B, int T, int F, int C, int pt, int pf,
+                                   int ceil_mode, const TP* P, const uint8_t* slot,
+                                   const float* gamma, const float* bn_mean, const float* bn_rstd,
+                                   float* dgamma, float* dbeta, float drop,
+                                   unsigned long long seed, void* dz, int dz_dtype, float* dbias,
+                                   void* workspace, size_t ws_bytes, void* stream) {
   const float* dnext = (const float*)dnext_v;
   const uint16_t* dnh = (const uint16_t*)dnext_v;
   const bool db16 = dnext_dtype == ASR_DT_BF16;
@@ -1311,13 +1355,13 @@ extern "C" int asr_vgg_block_backward_zd(const void* dnext_v, int dnext_dtype, i
     float* part = (float*)workspace;
     sums = part + (size_t)nchunk * 2 * C;
     if (db16)
-      hipLaunchKernelGGL((bn_bwd_moments<4, uint16_t>), dim3(nchunk), dim3(CT), 0, s, dnh, P, B,
+      hipLaunchKernelGGL((bn_bwd_moments<4, uint16_t, TP>), dim3(nchunk), dim3(CT), 0, s, dnh, P, B,
                          pl.To, pl.Fo, C, flat, af, per, part);
     else if (v4)
-      hipLaunchKernelGGL(bn_bwd_moments<4>, dim3(nchunk), dim3(CT), 0, s, dnext, P, B, pl.To,
+      hipLaunchKernelGGL((bn_bwd_moments<4, float, TP>), dim3(nchunk), dim3(CT), 0, s, dnext, P, B, pl.To,
                          pl.Fo, C, flat, af, per, part);
     else
-      hipLaunchKernelGGL(bn_bwd_moments<1>, dim3(nchunk), dim3(CT), 0, s, dnext, P, B, pl.To,
+      hipLaunchKernelGGL((bn_bwd_moments<1, float, TP>), dim3(nchunk), dim3(CT), 0, s, dnext, P, B, pl.To,
                          pl.Fo, C, flat, af, per, part);
     hipLaunchKernelGGL(sum_partials, dim3((2 * C + SP_COLS - 1) / SP_COLS), dim3(CT), 0, s, part, nchunk, 2 * C,
                        1.f, sums);
@@ -1334,40 +1378,40 @@ extern "C" int asr_vgg_block_backward_zd(const void* dnext_v, int dnext_dtype, i
   const uint16_t* zh = (const uint16_t*)z;
   ASR_REQUIRE(!db16 || full, ASR_ERR_UNSUPPORTED, "vgg_block_backward: bf16 dnext needs the full pass");
   if (db16) {
-    hipLaunchKernelGGL((post_bwd_full<uint16_t, uint16_t, uint16_t>), dim3(pgrid), dim3(CT), 0, s,
+    hipLaunchKernelGGL((post_bwd_full<uint16_t, uint16_t, uint16_t, TP>), dim3(pgrid), dim3(CT), 0, s,
                        dnh, P, zh, slot, B, T, F, C, pl, flat, af, sums, (uint16_t*)dz, bpart);
   } else if (zb) {
     if (full && dz_dtype == ASR_DT_BF16)
-      hipLaunchKernelGGL((post_bwd_full<uint16_t, uint16_t>), dim3(pgrid), dim3(CT), 0, s, dnext,
+      hipLaunchKernelGGL((post_bwd_full<uint16_t, uint16_t, float, TP>), dim3(pgrid), dim3(CT), 0, s, dnext,
                          P, zh, slot, B, T, F, C, pl, flat, af, sums, (uint16_t*)dz, bpart);
     else if (full)
-      hipLaunchKernelGGL((post_bwd_full<float, uint16_t>), dim3(pgrid), dim3(CT), 0, s, dnext, P,
+      hipLaunchKernelGGL((post_bwd_full<float, uint16_t, float, TP>), dim3(pgrid), dim3(CT), 0, s, dnext, P,
                          zh, slot, B, T, F, C, pl, flat, af, sums, (float*)dz, bpart);
     else if (dz_dtype == ASR_DT_BF16)
-      hipLaunchKernelGGL((post_bwd<uint16_t, 4, uint16_t>), dim3(pgrid), dim3(CT), 0, s, dnext, P,
+      hipLaunchKernelGGL((post_bwd<uint16_t, 4, uint16_t, TP>), dim3(pgrid), dim3(CT), 0, s, dnext, P,
                          zh, slot, B, T, F, C, pl, flat, af, sums, (uint16_t*)dz, bpart);
     else
-      hipLaunchKernelGGL((post_bwd<float, 4, uint16_t>), dim3(pgrid), dim3(CT), 0, s, dnext, P,
+      hipLaunchKernelGGL((post_bwd<float, 4, uint16_t, TP>), dim3(pgrid), dim3(CT), 0, s, dnext, P,
                          zh, slot, B, T, F, C, pl, flat, af, sums, (float*)dz, bpart);
   } else if (full && dz_dtype == ASR_DT_BF16) {
-    hipLaunchKernelGGL(post_bwd_full<uint16_t>, dim3(pgrid), dim3(CT), 0, s, dnext, P, zf, slot, B,
+    hipLaunchKernelGGL((post_bwd_full<uint16_t, float, float, TP>), dim3(pgrid), dim3(CT), 0, s, dnext, P, zf, slot, B,
                        T, F, C, pl, flat, af, sums, (uint16_t*)dz, bpart);
   } else if (full) {
-    hipLaunchKernelGGL(post_bwd_full<float>, dim3(pgrid), dim3(CT), 0, s, dnext, P, zf, slot, B, T,
+    hipLaunchKernelGGL((post_bwd_full<float, float, float, TP>), dim3(pgrid), dim3(CT), 0, s, dnext, P, zf, slot, B, T,
                        F, C, pl, flat, af, sums, (float*)dz, bpart);
   } else if (dz_dtype == ASR_DT_BF16) {
     if (v4)
-      hipLaunchKernelGGL((post_bwd<uint16_t, 4>), dim3(pgrid), dim3(CT), 0, s, dnext, P, zf, slot,
+      hipLaunchKernelGGL((post_bwd<uint16_t, 4, float, TP>), dim3(pgrid), dim3(CT), 0, s, dnext, P, zf, slot,
                          B, T, F, C, pl, flat, af, sums, (uint16_t*)dz, bpart);
     else
-      hipLaunchKernelGGL((post_bwd<uint16_t, 1>), dim3(pgrid), dim3(CT), 0, s, dnext, P, zf, slot,
+      hipLaunchKernelGGL((post_bwd<uint16_t, 1, float, TP>), dim3(pgrid), dim3(CT), 0, s, dnext, P, zf, slot,
                          B, T, F, C, pl, flat, af, sums, (uint16_t*)dz, bpart);
   } else {
     if (v4)
-      hipLaunchKernelGGL((post_bwd<float, 4>), dim3(pgrid), dim3(CT), 0, s, dnext, P, zf, slot, B,
+      hipLaunchKernelGGL((post_bwd<float, 4, float, TP>), dim3(pgrid), dim3(CT), 0, s, dnext, P, zf, slot, B,
                          T, F, C, pl, flat, af, sums, (float*)dz, bpart);
     else
-      hipLaunchKernelGGL((post_bwd<float, 1>), dim3(pgrid), dim3(CT), 0, s, dnext, P, zf, slot, B,
+      hipLaunchKernelGGL((post_bwd<float, 1, float, TP>), dim3(pgrid), dim3(CT), 0, s, dnext, P, zf, slot, B,
                          T, F, C, pl, flat, af, sums, (float*)dz, bpart);
   }
   ASR_LAUNCH_CHECK();
@@ -1380,6 +1424,46 @@ extern "C" int asr_vgg_block_backward_zd(const void* dnext_v, int dnext_dtype, i
   }
   ASR_LAUNCH_CHECK();
   return ASR_OK;
+}
+
+// p_dtype ASR_DT_BF16: P was stored bf16 by asr_vgg_block_forward_zp
+extern "C" int asr_vgg_block_backward_zdp(const void* dnext, int dnext_dtype, int flat,
+                                          const void* z, int z_dtype, int B, int T, int F, int C,
+                                          int pt, int pf, int ceil_mode, const void* P,
+                                          int p_dtype, const uint8_t* slot, const float* gamma,
+                                          const float* bn_mean, const float* bn_rstd,
+                                          float* dgamma, float* dbeta, float drop,
+                                          unsigned long long seed, void* dz, int dz_dtype,
+                                          float* dbias, void* workspace, size_t ws_bytes,
+                                          void* stream) {
+  if (p_dtype == ASR_DT_BF16) {
+    ASR_REQUIRE(z_dtype == ASR_DT_BF16 && C % 4 == 0 && ((uintptr_t)P & 7) == 0,
+                ASR_ERR_UNSUPPORTED, "vgg_block_backward: bf16 P needs bf16 z and C %% 4 == 0");
+    return vgg_block_backward_impl(dnext, dnext_dtype, flat, z, z_dtype, B, T, F, C, pt, pf,
+                                   ceil_mode, (const uint16_t*)P, slot, gamma, bn_mean, bn_rstd,
+                                   dgamma, dbeta, drop, seed, dz, dz_dtype, dbias, workspace,
+                                   ws_bytes, stream);
+  }
+  ASR_REQUIRE(p_dtype == ASR_DT_F32, ASR_ERR_ARG, "vgg_block_backward: P dtype %d", p_dtype);
+  return vgg_block_backward_impl(dnext, dnext_dtype, flat, z, z_dtype, B, T, F, C, pt, pf,
+                                 ceil_mode, (const float*)P, slot, gamma, bn_mean, bn_rstd, dgamma,
+                                 dbeta, drop, seed, dz, dz_dtype, dbias, workspace, ws_bytes,
+                                 stream);
+}
+
+extern "C" int asr_vgg_block_backward_zd(const void* dnext_v, int dnext_dtype, int flat,
+                                         const void* z, int z_dtype, int B, int T, int F, int C,
+                                         int pt, int pf, int ceil_mode, const float* P,
+                                         const uint8_t* slot, const float* gamma,
+                                         const float* bn_mean, const float* bn_rstd,
+                                         float* dgamma, float* dbeta, float drop,
+                                         unsigned long long seed, void* dz, int dz_dtype,
+                                         float* dbias, void* workspace, size_t ws_bytes,
+                                         void* stream) {
+  return asr_vgg_block_backward_zdp(dnext_v, dnext_dtype, flat, z, z_dtype, B, T, F, C, pt, pf,
+                                    ceil_mode, P, ASR_DT_F32, slot, gamma, bn_mean, bn_rstd,
+                                    dgamma, dbeta, drop, seed, dz, dz_dtype, dbias, workspace,
+                                    ws_bytes, stream);
 }
 
 extern "C" int asr_vgg_block_backward_z(const float* dnext, int flat, const void* z,

@@ -1675,7 +1675,11 @@ class VGGFn(torch.autograd.Function):
                     run_gemm([p], dev)
             pt, pf, ceil = sp['pt'], sp['pf'], sp['ceil']
             To, Fo = _pool_dims(cT, cF, pt, pf, ceil) if pt else (cT, cF)
-            P = torch.empty(B * To * Fo, Co, **f32)
+            # P = max(0, max z) of a bf16 z is itself a bf16 value: stored bf16 it
+            # is exact and halves P's write and four reads
+            p_bf = z_bf and os.environ.get('ASR_VGG_P_BF16', '1') != '0'
+            P = torch.empty(B * To * Fo, Co, dtype=torch.bfloat16 if p_bf else torch.float32,
+                            device=dev)
             slot = torch.empty(B * To * Fo * Co, dtype=torch.uint8, device=dev) if pt else None
             bn = sp['gamma'] is not None
             mean = torch.empty(Co, **f32) if bn else None
@@ -1697,8 +1701,8 @@ class VGGFn(torch.autograd.Function):
                 out_dt, flat = (cd if use_gemm[l + 1] else F32), 0
             nb = N.query('asr_vgg_block_workspace_bytes', B, To, Fo, Co)
             ws = _ws(nb, dev)
-            N.call('asr_vgg_block_forward_z', N.ptr(z), BF16 if z_bf else F32, B, cT, cF, Co, pt,
-                   pf, ceil, N.ptr(P), N.ptr(slot), N.ptr(sp['gamma']), N.ptr(sp['beta']),
+            N.call('asr_vgg_block_forward_zp', N.ptr(z), BF16 if z_bf else F32, B, cT, cF, Co, pt,
+                   pf, ceil, N.ptr(P), BF16 if p_bf else F32, N.ptr(slot), N.ptr(sp['gamma']), N.ptr(sp['beta']),
                    N.ptr(sp['run_mean']), N.ptr(sp['run_var']), int(bool(training)),
                    float(sp['momentum']), float(sp['eps']), N.ptr(mean), N.ptr(rstd), drop, seed,
                    N.ptr(out), out_dt, flat, N.ptr(ws), nb, N.stream_handle(dev))
@@ -1745,10 +1749,11 @@ class VGGFn(torch.autograd.Function):
             nb = N.query('asr_vgg_block_workspace_bytes', B, To, Fo, Co)
             ws = _ws(nb, dev)
             bn = sp['gamma'] is not None
-            N.call('asr_vgg_block_backward_zd', N.ptr(dnext),
+            N.call('asr_vgg_block_backward_zdp', N.ptr(dnext),
                    BF16 if dnext.dtype == torch.bfloat16 else F32, flat, N.ptr(z),
                    BF16 if z.dtype == torch.bfloat16 else F32, B, cT, cF, Co, pt,
-                   pf, ceil, N.ptr(P), N.ptr(slot), N.ptr(sp['gamma']), N.ptr(mean), N.ptr(rstd),
+                   pf, ceil, N.ptr(P), BF16 if P.dtype == torch.bfloat16 else F32, N.ptr(slot),
+                   N.ptr(sp['gamma']), N.ptr(mean), N.ptr(rstd),
                    N.ptr(grad_buffer(sp['gamma']) if bn else None),
                    N.ptr(grad_buffer(sp['beta']) if bn else None), drop, seed, N.ptr(dz),
                    F32 if dz_f32 else cd,

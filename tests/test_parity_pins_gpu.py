@@ -167,6 +167,22 @@ def test_vgg_post_bwd_full_equals_gather_form(prec, cuda_dev, monkeypatch):
         np.testing.assert_array_equal(g1[k], g0[k], err_msg=k)
 
 
+@pytest.mark.gpu
+def test_vgg_bf16_pool_store_is_exact(cuda_dev, monkeypatch):
+    # P = max(0, max z) of a bf16 z is a bf16 value: the bf16 P store must give
+    # bitwise the same loss and gradients as the f32 store (BN on, pooled and
+    # unpooled layers)
+    kw = dict(VGG_PROD, input_size=40)
+    model = _ctc(kw)
+    model.set_cuda()
+    batch = _vgg_batch(40, seed=9)
+    l1, g1 = _with_env(monkeypatch, 'ASR_VGG_P_BF16', '1', model, batch, 'bf16')
+    l0, g0 = _with_env(monkeypatch, 'ASR_VGG_P_BF16', '0', model, batch, 'bf16')
+    assert l1 == l0
+    for k in g0:
+        np.testing.assert_array_equal(g1[k], g0[k], err_msg=k)
+
+
 def _bf16_exact(t):
     """t rounded to the nearest bf16 value (kept as float32)."""
     return t.to(torch.bfloat16).to(t.dtype)
