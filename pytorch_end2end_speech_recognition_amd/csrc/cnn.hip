@@ -317,16 +317,27 @@ template <int V, typename TZ = float, typename TP = float>
 __global__ void __launch_bounds__(CT) post_fwd(const TZ* __restrict__ z, int B, int T, int F,
                                                int C, Pool pl, TP* __restrict__ P,
                                                uint8_t* __restrict__ slot,
-                                               float* __restrict__ mpart) {
+                                               float* __restrict__ mpart,
+                                               const float* __restrict__ shift,
+                                               float* __restrict__ qpart) {
   // mpart (nullable): per-block column sums of the P values written (the batch
   // norm's mean pass folded in: threads tid, tid + CV, ... hold the same
-  // channels; the block's phases are combined in a fixed order)
+  // channels; the block's phases are combined in a fixed order).  qpart
+  // (nullable, with mpart): the variance pass folded in as well -- mpart then
+  // sums P - shift[c] and qpart (P - shift[c])^2, shift being the running mean
+  // (a centre close to the batch mean, so E[d^2] - E[d]^2 does not cancel)
   __shared__ float red[CT * V];
   const unsigned CV = (unsigned)(C / V);
   const unsigned n = (unsigned)B * pl.To * pl.Fo * CV;
-  float macc[V];
+  float macc[V], qacc[V], sh[V];
+  {
+    const int c0 = (int)((blockIdx.x * blockDim.x + threadIdx.x) % CV) * V;
 #pragma unroll
-  for (int j = 0; j < V; ++j) macc[j] = 0.f;
+    for (int j = 0; j < V; ++j) {
+      macc[j] = qacc[j] = 0.f;
+      sh[j] = qpart ? shift[c0 + j] : 0.f;
+    }
+  }
   for (unsigned e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
     const unsigned q = e / CV;
     const int c = (int)(e - q * CV) * V;
@@ -338,7 +349,9 @@ __global__ void __launch_bounds__(CT) post_fwd(const TZ* __restrict__ z, int B, 
 #pragma unroll
       for (int j = 0; j < V; ++j) {
         best.v[j] = fmaxf(best.v[j], 0.f);
-        macc[j] += best.v[j];
+        const float d = best.v[j] - sh[j];
+        macc[j] += d;
+        qacc[j] += d * d;
       }
       best.store(P + i);
       continue;
@@ -365,7 +378,11 @@ __global__ void __launch_bounds__(CT) post_fwd(const TZ* __restrict__ z, int B, 
       }
     }
 #pragma unroll
-    for (int j = 0; j < V; ++j) macc[j] += best.v[j];
+    for (int j = 0; j < V; ++j) {
+      const float d = best.v[j] - sh[j];
+      macc[j] += d;
+      qacc[j] += d * d;
+    }
     best.store(P + i);
 #pragma unroll
     for (int j = 0; j < V; ++j) slot[i + j] = (uint8_t)bs[j];
@@ -380,6 +397,18 @@ __global__ void __launch_bounds__(CT) post_fwd(const TZ* __restrict__ z, int B, 
       float t = 0.f;
       for (int k = g2; k < CT; k += (int)CV) t += red[k * V + j];
       mpart[(long long)blockIdx.x * C + cc] = t;
+    }
+    if (qpart) {
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < V; ++j) red[tid * V + j] = qacc[j];
+      __syncthreads();
+      for (int cc = tid; cc < C; cc += CT) {
+        const int g2 = cc / V, j = cc % V;
+        float t = 0.f;
+        for (int k = g2; k < CT; k += (int)CV) t += red[k * V + j];
+        qpart[(long long)blockIdx.x * C + cc] = t;
+      }
     }
   }
 }
@@ -473,6 +502,27 @@ __global__ void bn_finalize(const float* __restrict__ mean, const float* __restr
   if (run_mean) {
     const float unb = n > 1 ? var * ((float)n / (float)(n - 1)) : var;
     run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean[c];
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * unb;
+  }
+}
+
+// the folded form: mean = shift + E[d], biased var = E[d^2] - E[d]^2 (d = x -
+// shift, both moments already / n); mean is written in place of E[d]
+__global__ void bn_finalize_shift(float* __restrict__ mean, const float* __restrict__ m2,
+                                  const float* shift, int C, long long n, float eps,
+                                  float momentum, float* __restrict__ rstd,
+                                  float* run_mean, float* __restrict__ run_var) {
+  // (shift is normally run_mean itself: each thread reads its entry first)
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float d = mean[c];
+  const float var = fmaxf(m2[c] - d * d, 0.f);
+  const float mu = shift[c] + d;
+  mean[c] = mu;
+  rstd[c] = rsqrtf(var + eps);
+  if (run_mean) {
+    const float unb = n > 1 ? var * ((float)n / (float)(n - 1)) : var;
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mu;
     run_var[c] = (1.f - momentum) * run_var[c] + momentum * unb;
   }
 }
@@ -756,9 +806,10 @@ __global__ void __launch_bounds__(CT) post_bwd_full(const TD* __restrict__ dnext
       }
       // ReLU mask: z > 0 at the window's argmax pixel <=> the pooled value
       // P = max(0, max z) > 0 there, so pooled layers read P (a quarter of the
-      // bytes, already loaded for BN) instead of the full-resolution z
+      // bytes, already loaded for BN) instead of the full-resolution z; an
+      // unpooled layer's P = max(0, z) is loaded for BN and gives the same mask
       VecF<V> zv;
-      if (pl.pt) zv = x;
+      if (pl.pt || af.mean) zv = x;
       else zv.load(z + p);
       unsigned sl = 0u, me = 0u;
       if (pl.pt) {
@@ -1151,18 +1202,27 @@ static int vgg_block_forward_impl(const void* z, int z_dtype, int B, int T, int 
   // fused: at most 1024 blocks, so the ordered partial sum (one thread per
   // column phase) stays short -- 8192 partials took 1 ms / step at vgg_hier
   const int fgrid = fused_mean ? std::min(post_grid(nr, C), 1024) : post_grid(nr, C);
+  // ... and the variance pass with it, centred on the running mean: the
+  // squared sums go to the BN partial region (fgrid <= its 1024 chunks)
+  const char* fv = getenv("ASR_VGG_FUSED_VAR");
+  const long long vchunks = (nr + rows_per_chunk(nr) - 1) / rows_per_chunk(nr);
+  const bool fused_var = fused_mean && run_mean && run_var && !(fv && fv[0] == '0') &&
+                         fgrid <= vchunks;
+  float* qpart = fused_var ? (float*)workspace : nullptr;
+  const float* vshift = fused_var ? run_mean : nullptr;
   const bool zb = z_dtype == ASR_DT_BF16;
   ASR_REQUIRE(!zb || (v4 && ((uintptr_t)z & 7) == 0), ASR_ERR_UNSUPPORTED,
               "vgg_block_forward: bf16 z needs C % 4 == 0 and 8-B alignment");
   if (zb)
     hipLaunchKernelGGL((post_fwd<4, uint16_t, TP>), dim3(fgrid), dim3(CT), 0, s, (const uint16_t*)z, B,
-                       T, F, C, pl, P, slot, mpart);
+                       T, F, C, pl, P, slot, mpart, vshift, qpart);
   else if (v4)
     hipLaunchKernelGGL((post_fwd<4, float, TP>), dim3(fgrid), dim3(CT), 0, s, (const float*)z, B, T, F, C, pl,
-                       P, slot, mpart);
+                       P, slot, mpart, vshift, qpart);
   else
     hipLaunchKernelGGL((post_fwd<1, float, TP>), dim3(post_grid(nr, C)), dim3(CT), 0, s, (const float*)z, B, T,
-                       F, C, pl, P, slot, (float*)nullptr);
+                       F, C, pl, P, slot, (float*)nullptr, (const float*)nullptr,
+                       (float*)nullptr);
   ASR_LAUNCH_CHECK();
   Affine af{nullptr, nullptr, nullptr, nullptr, drop, seed};
   if (gamma) {
@@ -1175,7 +1235,14 @@ static int vgg_block_forward_impl(const void* z, int z_dtype, int B, int T, int 
       const int nchunk = (int)((nr + per - 1) / per);
       float* part = (float*)workspace;
       float* m2 = part + (size_t)nchunk * C;
-      if (fused_mean) {
+      if (fused_var) {
+        hipLaunchKernelGGL(sum_partials, dim3((C + SP_COLS - 1) / SP_COLS), dim3(CT), 0, s, mpart,
+                           fgrid, C, 1.f / (float)nr, bn_mean);
+        hipLaunchKernelGGL(sum_partials, dim3((C + SP_COLS - 1) / SP_COLS), dim3(CT), 0, s, qpart,
+                           fgrid, C, 1.f / (float)nr, m2);
+        hipLaunchKernelGGL(bn_finalize_shift, dim3((C + CT - 1) / CT), dim3(CT), 0, s, bn_mean, m2,
+                           run_mean, C, nr, eps, momentum, bn_rstd, run_mean, run_var);
+      } else if (fused_mean) {
         hipLaunchKernelGGL(sum_partials, dim3((C + SP_COLS - 1) / SP_COLS), dim3(CT), 0, s, mpart, fgrid, C,
                            1.f / (float)nr, bn_mean);
       } else {
@@ -1184,12 +1251,14 @@ static int vgg_block_forward_impl(const void* z, int z_dtype, int B, int T, int 
         hipLaunchKernelGGL(sum_partials, dim3((C + SP_COLS - 1) / SP_COLS), dim3(CT), 0, s, part, nchunk, C,
                            1.f / (float)nr, bn_mean);
       }
-      hipLaunchKernelGGL(col_moment<TP>, dim3(nchunk), dim3(CT), 0, s, P, nr, C, per, bn_mean, 1,
-                         part);
-      hipLaunchKernelGGL(sum_partials, dim3((C + SP_COLS - 1) / SP_COLS), dim3(CT), 0, s, part, nchunk, C,
-                         1.f / (float)nr, m2);
-      hipLaunchKernelGGL(bn_finalize, dim3((C + CT - 1) / CT), dim3(CT), 0, s, bn_mean, m2, C, nr,
-                         eps, momentum, bn_rstd, run_mean, run_var);
+      if (!fused_var) {
+        hipLaunchKernelGGL(col_moment<TP>, dim3(nchunk), dim3(CT), 0, s, P, nr, C, per, bn_mean, 1,
+                           part);
+        hipLaunchKernelGGL(sum_partials, dim3((C + SP_COLS - 1) / SP_COLS), dim3(CT), 0, s, part,
+                           nchunk, C, 1.f / (float)nr, m2);
+        hipLaunchKernelGGL(bn_finalize, dim3((C + CT - 1) / CT), dim3(CT), 0, s, bn_mean, m2, C,
+                           nr, eps, momentum, bn_rstd, run_mean, run_var);
+      }
     } else {
       ASR_REQUIRE(run_mean && run_var, ASR_ERR_ARG, "vgg_block_forward: eval needs running stats");
       hipLaunchKernelGGL(bn_eval_stats, dim3((C + CT - 1) / CT), dim3(CT), 0, s, run_mean,

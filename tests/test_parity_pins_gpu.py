@@ -113,11 +113,18 @@ def test_vgg_prod_channels_fp32_vs_oracle(cuda_dev):
 
 
 def _with_env(monkeypatch, name, value, model, batch, prec):
+    # the running statistics are restored afterwards, so A/B calls start from the
+    # same state (the folded BN variance pass is centred on the running mean)
+    run = {k: v.clone() for k, v in model.state_dict().items() if 'running' in k}
     monkeypatch.setenv(name, value)
     try:
         return _gpu_grads(model, batch, prec)
     finally:
         monkeypatch.delenv(name)
+        with torch.no_grad():
+            sd = model.state_dict()
+            for k, v in run.items():
+                sd[k].copy_(v)
 
 
 @pytest.mark.gpu
@@ -181,6 +188,41 @@ def test_vgg_bf16_pool_store_is_exact(cuda_dev, monkeypatch):
     assert l1 == l0
     for k in g0:
         np.testing.assert_array_equal(g1[k], g0[k], err_msg=k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('prec', ['bf16', 'fp32'])
+def test_vgg_fused_bn_variance_matches_two_pass(prec, cuda_dev, monkeypatch):
+    # the pool pass sums (P - running mean) and its square (ASR_VGG_FUSED_VAR=1)
+    # instead of a second pass over P centred on the batch mean: same batch
+    # statistics to f32 rounding, so the same loss, gradients and running stats
+    kw = dict(VGG_PROD, input_size=40)
+    model = _ctc(kw)
+    model.set_cuda()
+    with torch.no_grad():   # a running mean away from 0, as after some steps
+        for k, v in model.state_dict().items():
+            if k.endswith('running_mean'):
+                v.uniform_(0.0, 0.5)
+    sd0 = {k: v.clone() for k, v in model.state_dict().items()}
+    batch = _vgg_batch(40, seed=12)
+    out = {}
+    for flag in ('1', '0'):
+        model.load_state_dict(sd0)
+        loss, g = _with_env(monkeypatch, 'ASR_VGG_FUSED_VAR', flag, model, batch, prec)
+        run = {k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items()
+               if 'running' in k}
+        out[flag] = (loss, g, run)
+    (l1, g1, r1), (l0, g0, r0) = out['1'], out['0']
+    np.testing.assert_allclose(l1, l0, rtol=1e-5)
+    if prec == 'fp32':
+        # (in bf16 a last-bit change of the statistics moves bf16 roundings of
+        # the activations, and the BN backward's cancellation amplifies that in
+        # the first layer's weight gradient: there the statistics themselves
+        # are compared, and the gradients against float64 below)
+        for k in g0:
+            assert _rel_l2(g1[k], g0[k]) <= 1e-4, (k, _rel_l2(g1[k], g0[k]))
+    for k in r0:
+        np.testing.assert_allclose(r1[k], r0[k], rtol=1e-5, atol=1e-6, err_msg=k)
 
 
 def _bf16_exact(t):
