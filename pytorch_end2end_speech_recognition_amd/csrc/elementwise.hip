@@ -3,6 +3,8 @@
 // gradient, tanh.  Vectorised 16 B per lane where the layout allows.
 #include "mfma.h"
 
+#include <algorithm>
+
 namespace asr {
 namespace {
 
@@ -151,6 +153,43 @@ __global__ void convert_rows_kernel(const float* __restrict__ src, asr_rowmap_t 
   }
 }
 
+// The same for rows whose width is not a multiple of 8 (e.g. the 10001-class
+// output layer's gradient, whose f32 rows are only 4-B aligned): lane-
+// consecutive columns, so every load and store instruction is coalesced (the
+// 8-columns-per-thread form above issued eight 32-B-strided scalar loads and
+// 2-B stores per thread: 300 us for an 8000 x 10001 gradient).  Block
+// (x, y): columns [x * 1024, +1024) of rows y, y + gridDim.y, ...
+template <bool DROP>
+__global__ void convert_rows_cols(const float* __restrict__ src, asr_rowmap_t m, int nrows,
+                                  int ncols, int ld, uint16_t* __restrict__ dst, float p,
+                                  unsigned long long seed) {
+  const float scale = DROP ? 1.f / (1.f - p) : 1.f;
+  const int rpb = m.rows_per_b > 0 ? m.rows_per_b : 0x7fffffff;
+  const int tmul = m.t_mul == 0 ? 1 : m.t_mul;
+  const int tlim = m.t_limit > 0 ? m.t_limit : 0x7fffffff;
+  for (int r = blockIdx.y; r < nrows; r += gridDim.y) {
+    const int b = r / rpb, t = r - b * rpb;
+    const int tp = t * tmul + m.t_add;
+    const bool ok = tp >= 0 && tp < tlim;
+    const long long so = ok ? (long long)(m.perm ? m.perm[b] : b) * m.stride_b +
+                                  (long long)tp * m.stride_t
+                            : 0;
+    uint16_t* d = dst + (long long)r * ld;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c = (blockIdx.x * 4 + k) * 256 + threadIdx.x;
+      if (c >= ld) break;
+      float x = 0.f;
+      if (ok && c < ncols) {
+        x = src[so + c];
+        if (DROP && u01(seed, (unsigned long long)(so + c)) < p) x = 0.f;
+        else if (DROP) x *= scale;
+      }
+      d[c] = f2bf(x);
+    }
+  }
+}
+
 // y = tanh(a + b): the attention bottleneck tanh(W_d(dec) + W_c(ctx)) when the
 // two LinearND outputs carry their own dropout (attention_seq2seq.py:788-790)
 __global__ void add_tanh_fwd(const float* __restrict__ a, const float* __restrict__ b,
@@ -268,8 +307,13 @@ extern "C" int asr_convert_rows_bf16_ld(const float* src, asr_rowmap_t map, int 
                 ASR_ERR_ARG, "convert_rows: vector path needs 16-B aligned rows");
   const long long n = (long long)nrows * ((ld + 7) / 8);
   if (n <= 0) return ASR_OK;
-  hipLaunchKernelGGL(convert_rows_kernel<false>, dim3(grid_for(n)), dim3(256), 0,
-                     (hipStream_t)stream, src, map, nrows, ncols, ld, dst, 0.f, 0ull);
+  if (!(ncols % 8 == 0 && ld % 8 == 0))
+    hipLaunchKernelGGL(convert_rows_cols<false>, dim3((ld + 1023) / 1024, std::min(nrows, 8192)),
+                       dim3(256), 0, (hipStream_t)stream, src, map, nrows, ncols, ld, dst, 0.f,
+                       0ull);
+  else
+    hipLaunchKernelGGL(convert_rows_kernel<false>, dim3(grid_for(n)), dim3(256), 0,
+                       (hipStream_t)stream, src, map, nrows, ncols, ld, dst, 0.f, 0ull);
   ASR_LAUNCH_CHECK();
   return ASR_OK;
 }
@@ -286,8 +330,13 @@ extern "C" int asr_convert_rows_bf16_dropout(const float* src, asr_rowmap_t map,
                 ASR_ERR_ARG, "convert_rows: vector path needs 16-B aligned rows");
   const long long n = (long long)nrows * ((ncols + 7) / 8);
   if (n <= 0) return ASR_OK;
-  hipLaunchKernelGGL(convert_rows_kernel<true>, dim3(grid_for(n)), dim3(256), 0,
-                     (hipStream_t)stream, src, map, nrows, ncols, ncols, dst, p, seed);
+  if (ncols % 8 != 0)
+    hipLaunchKernelGGL(convert_rows_cols<true>, dim3((ncols + 1023) / 1024, std::min(nrows, 8192)),
+                       dim3(256), 0, (hipStream_t)stream, src, map, nrows, ncols, ncols, dst, p,
+                       seed);
+  else
+    hipLaunchKernelGGL(convert_rows_kernel<true>, dim3(grid_for(n)), dim3(256), 0,
+                       (hipStream_t)stream, src, map, nrows, ncols, ncols, dst, p, seed);
   ASR_LAUNCH_CHECK();
   return ASR_OK;
 }

@@ -540,3 +540,38 @@ def test_padded_input_width_matches_fp32(B, T, H, Din, cuda_dev):
         assert err < 2e-2, (n, err)
     for b in range(B):      # padded frames stay exactly zero
         assert not outs['bf16'][0][b, lens[b]:].any()
+
+
+@pytest.mark.parametrize('cols,ld', [(10001, 10008), (123, 128), (37, 37)])
+def test_convert_rows_unaligned_width(cols, ld, cuda_dev):
+    """bf16 staging of rows whose width is not a multiple of 8 (the lane-
+    consecutive convert_rows_cols path): dst[r][c] = bf16(src[row(r)][c]), the
+    padding columns and the rows mapped outside [0, t_limit) zero; with the
+    fused dropout, the element mask of asr_dropout over src."""
+    ops = _ops()
+    N = ops.N
+    rng = np.random.RandomState(5)
+    B, T = 3, 7
+    src = torch.from_numpy(rng.randn(B, T, cols).astype(np.float32)).to(cuda_dev)
+    perm = torch.tensor([2, 0, 1], dtype=torch.int32, device=cuda_dev)
+    # rows (b, t) -> src[perm[b]][t - 1]: t = 0 maps outside and is zero
+    m = ops.rowmap(cols, stride_b=T * cols, rows_per_b=T, t_add=-1, t_limit=T, perm=perm)
+    out = torch.full((B * T, ld), 7.0, dtype=torch.bfloat16, device=cuda_dev)
+    N.call('asr_convert_rows_bf16_ld', N.ptr(src), m, B * T, cols, ld, N.ptr(out),
+           N.stream_handle(cuda_dev))
+    ref = torch.zeros(B, T, ld, dtype=torch.float32, device=cuda_dev)
+    ref[:, 1:, :cols] = src[perm.long()][:, :T - 1]
+    torch.testing.assert_close(out.float().view(B, T, ld), ref.to(torch.bfloat16).float(),
+                               rtol=0, atol=0)
+    if ld == cols:
+        p, seed = 0.3, 424242
+        outd = torch.empty(B * T, cols, dtype=torch.bfloat16, device=cuda_dev)
+        N.call('asr_convert_rows_bf16_dropout', N.ptr(src), m, B * T, cols, N.ptr(outd), p, seed,
+               N.stream_handle(cuda_dev))
+        dropped = torch.empty_like(src)
+        N.call('asr_dropout', N.ptr(src), N.ptr(dropped), src.numel(), p, seed,
+               N.stream_handle(cuda_dev))
+        refd = torch.zeros(B, T, cols, dtype=torch.float32, device=cuda_dev)
+        refd[:, 1:] = dropped[perm.long()][:, :T - 1]
+        torch.testing.assert_close(outd.float().view(B, T, cols),
+                                   refd.to(torch.bfloat16).float(), rtol=0, atol=0)
