@@ -764,7 +764,8 @@ extern "C" int asr_vgg_zero_halo(void* buf, int dtype, int B, int T, int F, int 
 // ---------------------------------------------------------------------------
 namespace asr {
 namespace {
-constexpr int C1W_TP = 256;   // pixels per tile
+constexpr int C1W_TP = 256;    // pixels per tile
+constexpr int C1W_MAXS = 1024; // work-groups (4 per CU: 34 KB of LDS each)
 
 template <int CO>
 __global__ void __launch_bounds__(256) c1_wgrad_xs(const float* __restrict__ xs, int round_bf16,
@@ -810,11 +811,18 @@ __global__ void __launch_bounds__(256) c1_wgrad_xs(const float* __restrict__ xs,
     if (kt < 3) {
       const int np = min(C1W_TP, end - p0);
       const float* xr = xw + H1 + (kt - 1) * Fp - 1;   // tap (kt, kf): x[i + (kt-1) Fp + kf - 1]
+      // the three taps' x values slide through registers: one LDS read of x
+      // and one of dz per three FMAs
+      float x0 = xr[0], x1 = xr[1];
+#pragma unroll 4
       for (int i = 0; i < np; ++i) {
+        const float x2 = xr[i + 2];
         const float d = bf2f(dzt[i * CO + n]);
-        a0 += d * xr[i];
-        a1 += d * xr[i + 1];
-        a2 += d * xr[i + 2];
+        a0 += d * x0;
+        a1 += d * x1;
+        a2 += d * x2;
+        x0 = x1;
+        x1 = x2;
       }
     }
   }
@@ -826,22 +834,47 @@ __global__ void __launch_bounds__(256) c1_wgrad_xs(const float* __restrict__ xs,
   }
 }
 
-// packed[n][tap Cip + c] = (c == 0) * sum_s slab[s][n][tap] (fixed order)
-__global__ void c1_wgrad_reduce(const float* __restrict__ slab, int S, int CO, int Cip,
-                                float* __restrict__ packed) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;   // over CO * 9 * Cip
-  if (i >= CO * 9 * Cip) return;
-  const int c = i % Cip, k = i / Cip, tap = k % 9, n = k / 9;
-  float s = 0.f;
-  if (c == 0)
-    for (int q = 0; q < S; ++q) s += slab[((size_t)q * CO + n) * 9 + tap];
-  packed[i] = s;
+// packed[n][tap Cip + c] = (c == 0) * sum_s slab[s][n][tap] (fixed order): a
+// block per 16 (n, tap) columns, 16 interleaved phases per column with four
+// accumulators each, combined in order through LDS (one thread per column
+// summing all S partials serially took 60 us)
+__global__ void __launch_bounds__(256) c1_wgrad_reduce(const float* __restrict__ slab, int S,
+                                                       int CO, int Cip,
+                                                       float* __restrict__ packed) {
+  __shared__ float red[256];
+  const int tid = threadIdx.x, cl = tid % 16, q0 = tid / 16;
+  const int k = blockIdx.x * 16 + cl;   // (n, tap) = (k / 9, k % 9)
+  const int K = CO * 9;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (k < K) {
+    int q = q0;
+    for (; q + 48 < S; q += 64) {
+      s0 += slab[(size_t)q * K + k];
+      s1 += slab[(size_t)(q + 16) * K + k];
+      s2 += slab[(size_t)(q + 32) * K + k];
+      s3 += slab[(size_t)(q + 48) * K + k];
+    }
+    for (; q < S; q += 16) s0 += slab[(size_t)q * K + k];
+  }
+  red[tid] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (q0 == 0 && k < K) {
+    float t = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) t += red[j * 16 + cl];
+    red[cl] = t;   // (own slot: read above by this thread only)
+  }
+  __syncthreads();
+  for (int e = tid; e < 16 * Cip; e += 256) {   // the block's 16 columns x Cip channels
+    const int kk = blockIdx.x * 16 + e / Cip, c = e % Cip;
+    if (kk < K) packed[(size_t)kk * Cip + c] = c == 0 ? red[kk - blockIdx.x * 16] : 0.f;
+  }
 }
 }  // namespace
 }  // namespace asr
 
 extern "C" size_t asr_conv3x3_c1_wgrad_workspace_bytes(int Co) {
-  return (size_t)256 * Co * 9 * sizeof(float);
+  return (size_t)C1W_MAXS * Co * 9 * sizeof(float);
 }
 
 extern "C" int asr_conv3x3_c1_wgrad_xs(const float* xs, int round_bf16, int B, int T, int F,
@@ -853,7 +886,7 @@ extern "C" int asr_conv3x3_c1_wgrad_xs(const float* xs, int round_bf16, int B, i
   ASR_REQUIRE(((uintptr_t)dz & 15) == 0, ASR_ERR_ARG, "conv3x3_c1_wgrad_xs: dz not 16-B aligned");
   const long long P = (long long)B * (T + 2) * (F + 2);
   ASR_REQUIRE(P * Co * 2 < (1LL << 31), ASR_ERR_UNSUPPORTED, "conv3x3_c1_wgrad_xs: too large");
-  const int S = (int)std::min<long long>(256, std::max<long long>(1, P / 1024));
+  const int S = (int)std::min<long long>(C1W_MAXS, std::max<long long>(1, P / 1024));
   ASR_REQUIRE(ws_bytes >= (size_t)S * Co * 9 * sizeof(float), ASR_ERR_WORKSPACE,
               "conv3x3_c1_wgrad_xs: workspace");
   const size_t lds = (size_t)C1W_TP * Co * 2 + (size_t)(C1W_TP + 2 * (F + 3)) * 4;
@@ -863,9 +896,8 @@ extern "C" int asr_conv3x3_c1_wgrad_xs(const float* xs, int round_bf16, int B, i
   hipLaunchKernelGGL(c1_wgrad_xs<64>, dim3(S), dim3(256), lds, s, xs, round_bf16, B, T, F,
                      (const uint16_t*)dz, (int)P, S, (float*)ws);
   ASR_LAUNCH_CHECK();
-  const int n = Co * 9 * Cip;
-  hipLaunchKernelGGL(c1_wgrad_reduce, dim3((n + 255) / 256), dim3(256), 0, s, (const float*)ws, S,
-                     Co, Cip, packed);
+  hipLaunchKernelGGL(c1_wgrad_reduce, dim3((Co * 9 + 15) / 16), dim3(256), 0, s, (const float*)ws,
+                     S, Co, Cip, packed);
   prof_end_launch(ASR_PROF_GEMM, slot, s);
   ASR_LAUNCH_CHECK();
   return ASR_OK;
