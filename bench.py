@@ -110,10 +110,58 @@ def synthetic_hier_batch(B, T, F, num_words, num_chars, seed):
     return batch
 
 
-def roofline_report(args, p, mean_us, launches, mean_work, workload):
-    """Roofline of the dominant kernel (largest mean launch time x launches over
-    the timed steps), from HIP-event timings taken on the kernels' own stream by
-    the library's prof hooks (asr_prof_*).  Algorithmic work per launch:
+KIND_NAMES = ['lstm_fwd_step', 'lstm_bwd_step', 'lstm_fwd_pass', 'lstm_bwd_pass', 'gemm',
+              'ctc_fwd', 'ctc_grad', 'attdec_fwd_pass', 'attdec_bwd_pass']
+# the rocprof kernel names behind each prof tag (csrc/prof.h ASR_PTAG_*)
+_GEMM_FAMILY = {1: 'gemm_bf16_8r<{a}, {b}>', 2: 'gemm_bf16_8w<{a}, {b}>', 3: 'gemm_bf16_kk256',
+                4: 'gemm_bf16_n64<{a}, {b}, *>', 5: 'gemm_bf16_fast<{a}, {b}, 2>',
+                6: 'gemm_bf16_fast<{a}, {b}, 4>', 7: 'gemm_kernel<true>', 8: 'gemm_kernel<false>',
+                9: 'conv3x3_tr<*>', 10: 'conv3x3_tr_wgrad<*> + tr_wgrad_reduce',
+                11: 'c1_wgrad_xs<64> + c1_wgrad_reduce'}
+_LSTM_PASS = {1: 'lstm_fwd_xg<*>', 2: 'lstm_fwd_xgx<*>', 3: 'lstm_bwd_xg<*>', 4: 'lstm_persist'}
+# MI355X_MICROARCH.md price list, handoff-1to1: one producer -> one consumer,
+# data-tagged granules, idle chip, 4 KB: 1.0 us (8 B: 0.8 us)
+HANDOFF_FLOOR_US = 1.0
+
+
+def kernel_name(kind, tag):
+    k = KIND_NAMES[kind]
+    if k == 'gemm':
+        fam = _GEMM_FAMILY.get(tag // 4, 'gemm?%d' % tag)
+        return fam.format(a=(tag % 4) >> 1, b=tag & 1)
+    if k.startswith('lstm_') and k.endswith('_pass'):
+        return _LSTM_PASS.get(tag, k)
+    if k == 'ctc_fwd':
+        return 'ctc_emit%s + ctc_lattice [V=%d]' % ('_wide' if tag > 1024 else '', tag)
+    if k == 'ctc_grad':
+        return 'ctc_grad [V=%d]' % tag
+    if k == 'attdec_fwd_pass':
+        return 'attdec_fwd_persist'
+    if k == 'attdec_bwd_pass':
+        return 'attdec_bwd_persist'
+    return k
+
+
+def prof_samples():
+    """Every timed sample of the run: {kind: [(tag, work, us), ...]}."""
+    import ctypes
+    out = {}
+    for kind in range(len(KIND_NAMES)):
+        n = N.lib().asr_prof_samples(kind, None, None, None, 0)
+        if n <= 0:
+            continue
+        tags = (ctypes.c_int * n)()
+        work = (ctypes.c_double * n)()
+        us = (ctypes.c_double * n)()
+        N.lib().asr_prof_samples(kind, tags, work, us, n)
+        out[kind] = list(zip(tags, work, us))
+    return out
+
+
+def roofline_report(args, p, samples, launches, workload):
+    """Roofline rows, one per kernel instantiation (kind x prof tag), from
+    HIP-event timings taken on the kernels' own stream by the library's prof
+    hooks (asr_prof_*).  Algorithmic work per launch:
       * lstm_{fwd,bwd}_pass (persistent, one launch = one layer pass, T steps x
         2 directions): HBM bytes that must move once -- gx / gate activations /
         y / c / dy read or written once per (b, t) cell plus W_hh once -- and
@@ -122,8 +170,14 @@ def roofline_report(args, p, mean_us, launches, mean_work, workload):
         projection's flops and reads the bf16 input rows instead of gx;
       * lstm_{fwd,bwd}_step (per-step kernels): the same per time step, W_hh
         re-streamed every step;
-      * gemm: 2*M*N*K summed over the launch's problems, reported by the library.
-    """
+      * GEMMs and convolutions: 2*M*N*K (2*P*Cout*9*Cin) per launch, reported
+        by the library with the launch;
+      * CTC: SURVEY §8(d)'s 8 * V bytes per output frame, split as 4 * V read
+        by the forward (emission + lattice) launch and 8 * V (read + write) by
+        the gradient launch; one extra 'ctc_op' row per V sums the two passes
+        of one call against 8 * V per frame (the whole-op figure);
+      * attention decoder passes: bytes recorded by the library, flops below.
+    The dominant kernel is the instantiation with the largest total time."""
     B, H = args.batch, p['encoder_num_units']
     # time steps of a layer pass, averaged over the layers (pyramidal drop
     # subsampling halves T after each flagged layer, rnn.py:413-439)
@@ -167,76 +221,111 @@ def roofline_report(args, p, mean_us, launches, mean_work, workload):
     # the LSTMCell [4D x (E + D)], W_dec h [A x D] and per frame the location
     # conv (C x K), W_conv f (A x C), V tanh (A) and the context (E); the
     # backward does twice the forward's multiply-adds
-    att_flops = [0.0, 0.0]
-    if p.get('attention_dim'):
+    def att_flops(i, nbytes):
+        if not p.get('attention_dim') or not nbytes:
+            return 0.0
         A, D = p['attention_dim'], p['decoder_num_units']
         E = 2 * H
         C, K = p['attention_conv_num_channels'], p['attention_conv_width']
         Tq = T_l[-1] // 2 if (p.get('subsample_list') or [False])[-1] else T_l[-1]
-        for i in (0, 1):
-            bs = mean_work[7 + i] / ((A + E + 2) * 4.0 * Tq) if mean_work[7 + i] else 0.0
-            mac = 4 * D * (E + D) + A * D + Tq * (A * C + C * K + A + E)
-            att_flops[i] = 2.0 * bs * mac * (1 if i == 0 else 2)
-    kinds = [
-        ('lstm_fwd_step', 'mfma', 2 * cell * fwd_cell + w_hh, flops_step),
-        ('lstm_bwd_step', 'mfma', 2 * cell * bwd_cell + w_hh, flops_step),
-        ('lstm_fwd_pass', 'mfma', fwd_pass_bytes, fwd_pass_flops),
-        ('lstm_bwd_pass', 'mfma', T * 2 * cell * bwd_cell + w_hh, T * flops_step),
-        ('gemm', 'mfma', 0, mean_work[4]),
-        ('ctc_fwd', 'hbm', mean_work[5], 0.0),
-        ('ctc_grad', 'hbm', mean_work[6], 0.0),
-        ('attdec_fwd_pass', 'hbm', mean_work[7], att_flops[0]),
-        ('attdec_bwd_pass', 'hbm', mean_work[8], att_flops[1]),
-    ]
+        bs = nbytes / ((A + E + 2) * 4.0 * Tq)
+        mac = 4 * D * (E + D) + A * D + Tq * (A * C + C * K + A + E)
+        return 2.0 * bs * mac * (1 if i == 0 else 2)
+
+    # (bound, bytes per launch, flops per launch) from the kind and the
+    # launch's recorded work
+    def model(kind, work):
+        k = KIND_NAMES[kind]
+        if k == 'lstm_fwd_step':
+            return 'mfma', 2 * cell * fwd_cell + w_hh, flops_step
+        if k == 'lstm_bwd_step':
+            return 'mfma', 2 * cell * bwd_cell + w_hh, flops_step
+        if k == 'lstm_fwd_pass':
+            return 'mfma', fwd_pass_bytes, fwd_pass_flops
+        if k == 'lstm_bwd_pass':
+            return 'mfma', T * 2 * cell * bwd_cell + w_hh, T * flops_step
+        if k == 'gemm':
+            return 'mfma', 0, work
+        if k in ('ctc_fwd', 'ctc_grad'):
+            return 'hbm', work, 0.0
+        return 'hbm', work, att_flops(0 if k == 'attdec_fwd_pass' else 1, work)
+
+    groups = {}
+    for kind, ss in samples.items():
+        for tag, work, us in ss:
+            groups.setdefault((kind, tag), []).append((work, us))
     rows = []
-    for i, (name, bound, nbytes, flops) in enumerate(kinds):
-        us = mean_us[i]
-        if us <= 0 or launches[i] == 0:
-            continue
-        gbs = nbytes / (us * 1e-6) / 1e9
-        tfs = flops / (us * 1e-6) / 1e12
-        rows.append(dict(name=name, bound=bound, us=us, n=int(launches[i]), bytes=nbytes,
-                         flops=flops, gbs=gbs, tfs=tfs, total=us * launches[i]))
+    for (kind, tag), ss in sorted(groups.items()):
+        n = len(ss)
+        us = sum(u for _, u in ss) / n
+        work = sum(w for w, _ in ss) / n
+        bound, nbytes, flops = model(kind, work)
+        # launches of this instantiation over the timed steps: every launch of
+        # the pass / GEMM / CTC kinds is timed; the per-step kinds are sampled
+        per = n if kind >= 2 else int(round(launches[kind] * n / max(1, len(samples[kind]))))
+        rows.append(dict(name=kernel_name(kind, tag), kind=KIND_NAMES[kind], tag=tag, bound=bound,
+                         us=us, n=per, bytes=nbytes, flops=flops,
+                         gbs=nbytes / (us * 1e-6) / 1e9, tfs=flops / (us * 1e-6) / 1e12,
+                         total=us * per))
     if not rows:
         return None
     dom = max(rows, key=lambda r: r['total'])
+    ktotal = sum(r['total'] for r in rows)
 
     def view(r):
         if r['bound'] == 'mfma':
-            return {'achieved': round(r['tfs'], 2), 'peak': BF16_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-                    'frac': round(r['tfs'] / BF16_PEAK_TFLOPS, 4)}
-        return {'achieved': round(r['gbs'], 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                'frac': round(r['gbs'] / HBM_PEAK_GBS, 4)}
+            v = {'achieved': round(r['tfs'], 2), 'peak': BF16_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+                 'frac': round(r['tfs'] / BF16_PEAK_TFLOPS, 4)}
+        else:
+            v = {'achieved': round(r['gbs'], 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                 'frac': round(r['gbs'] / HBM_PEAK_GBS, 4)}
+        if r['kind'].startswith('lstm') and r['kind'].endswith('_pass'):
+            # the recurrence is hand-off latency bound: T dependent steps per launch
+            v['hbm_achieved_gbs'] = round(r['gbs'], 1)
+            v['us_per_time_step'] = round(r['us'] / T, 3)
+            v['handoff_floor_us'] = HANDOFF_FLOOR_US
+            v['steps_per_launch'] = T
+        return v
 
     out = {'bound': dom['bound']}
     out.update(view(dom))
-    traffic, tsrc = pmc_traffic(dom['name'], workload)
-    out.update({'traffic': traffic, 'kernel': dom['name'], 'mean_launch_us': round(dom['us'], 3),
-                'launches_timed': dom['n'],
+    traffic, tsrc = pmc_traffic(dom['kind'], workload)
+    out.update({'traffic': traffic, 'kernel': dom['name'], 'kind': dom['kind'],
+                'mean_launch_us': round(dom['us'], 3), 'launches_timed': dom['n'],
                 'algorithmic_bytes_per_launch': int(dom['bytes']),
                 'algorithmic_flops_per_launch': float(dom['flops']),
-                'share_of_timed_kernel_time': round(dom['total'] / sum(r['total'] for r in rows),
-                                                    3)})
+                'share_of_timed_kernel_time': round(dom['total'] / ktotal, 3)})
     if tsrc:
         out['traffic_source'] = tsrc
-    if dom['name'].startswith('lstm'):
-        out['hbm_achieved_gbs'] = round(dom['gbs'], 1)
-        out['us_per_time_step'] = round(dom['us'] / T, 3)
     others = {}
     for r in rows:
         if r is dom:
             continue
-        v = {'bound': r['bound'], 'mean_launch_us': round(r['us'], 3), 'launches': r['n']}
+        v = {'bound': r['bound'], 'mean_launch_us': round(r['us'], 3), 'launches': r['n'],
+             'share_of_timed_kernel_time': round(r['total'] / ktotal, 3)}
         v.update(view(r))
         if r['bound'] == 'hbm' and r['flops']:
             v['mfma_tflops'] = round(r['tfs'], 2)
+        if r['bound'] == 'hbm':
             v['algorithmic_bytes_per_launch'] = int(r['bytes'])
-            v['algorithmic_flops_per_launch'] = float(r['flops'])
-        if r['name'].startswith('lstm'):
-            v['hbm_achieved_gbs'] = round(r['gbs'], 1)
-            if r['name'].endswith('_pass'):
-                v['us_per_time_step'] = round(r['us'] / T, 3)
         others[r['name']] = v
+    # whole-op CTC rows: emission + lattice launch and gradient launch of the
+    # same head (same V), against SURVEY §8(d)'s 8 * V bytes per output frame
+    for r in rows:
+        if r['kind'] != 'ctc_fwd':
+            continue
+        g = [q for q in rows if q['kind'] == 'ctc_grad' and q['tag'] == r['tag']]
+        if not g:
+            continue
+        us = r['us'] + g[0]['us']
+        nbytes = 2.0 * r['bytes']          # 4 V per frame (fwd) -> 8 V per frame
+        others['ctc_op [V=%d]' % r['tag']] = {
+            'bound': 'hbm', 'mean_call_us': round(us, 3), 'calls': min(r['n'], g[0]['n']),
+            'achieved': round(nbytes / (us * 1e-6) / 1e9, 1), 'peak': HBM_PEAK_GBS,
+            'unit': 'GB/s', 'frac': round(nbytes / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+            'algorithmic_bytes_per_call': int(nbytes),
+            'what': 'forward (emission + lattice) + gradient launches of one head, '
+                    '8 * V bytes per output frame'}
     out['other_kernels'] = others
     return out
 
@@ -646,12 +735,13 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     import ctypes
-    NK = 9
+    NK = len(KIND_NAMES)
     mean_us = (ctypes.c_double * NK)()
     launches = (ctypes.c_longlong * NK)()
     mean_work = (ctypes.c_double * NK)()
     N.call('asr_prof_end', ctypes.cast(mean_us, ctypes.c_void_p),
            ctypes.cast(launches, ctypes.c_void_p), ctypes.cast(mean_work, ctypes.c_void_p), NK)
+    samples = prof_samples()
     step_s = np.diff(np.asarray(marks))
     if world > 1:
         t = torch.tensor([elapsed] + list(step_s), dtype=torch.float64, device=dev)
@@ -671,7 +761,7 @@ def main():
         dist.destroy_process_group()
         return
 
-    roofline = roofline_report(args, p, mean_us, launches, mean_work, cfg['workload'])
+    roofline = roofline_report(args, p, samples, list(launches), cfg['workload'])
     # whole-job rate: the K timed steps between the two barrier + synchronize
     # brackets (max over ranks); per-step host marks only describe the spread
     med = elapsed / max(args.steps, 1)

@@ -84,6 +84,16 @@ int asr_ctc_backward(const float* acts, long long stride_t, long long stride_b, 
                      const int32_t* act_lens, int max_label_len, int blank,
                      const float* grad_scale, float scale, float* grads, long long gstride_t,
                      long long gstride_b, const void* workspace, size_t ws_bytes, void* stream);
+/* asr_ctc_backward writing the gradient as bf16 rows of gld columns (gld >= V,
+ * gld % 8 == 0, 16-B aligned rows, strides in elements), columns [V, gld)
+ * zero: the zero-padded dY operand of the output layer's staged bf16 GEMMs
+ * (the fused CTC head, native_ops.LinearCTCFn; no f32 gradient pass). */
+int asr_ctc_backward_bf16(const float* acts, long long stride_t, long long stride_b, int T, int B,
+                          int V, const int32_t* labels_flat, const int32_t* label_lens,
+                          const int32_t* act_lens, int max_label_len, int blank,
+                          const float* grad_scale, float scale, uint16_t* grads,
+                          long long gstride_t, long long gstride_b, int gld,
+                          const void* workspace, size_t ws_bytes, void* stream);
 /* warp-ctc drop-in: forward + backward with scale 1 in one call. */
 int asr_ctc_fwd_bwd(const float* acts, long long stride_t, long long stride_b, int T, int B,
                     int V, const int32_t* labels_flat, const int32_t* label_lens,
@@ -191,6 +201,10 @@ int asr_lstm_wgrad_gate(void* stream);
 size_t asr_colsum_workspace_bytes(int M, int N);
 int asr_colsum_accumulate(const float* g, long long ld, int M, int N, float alpha, float* out0,
                           float* out1, void* workspace, size_t ws_bytes, void* stream);
+/* asr_colsum_accumulate over a bf16 matrix (f32 sums). */
+int asr_colsum_accumulate_bf16(const uint16_t* g, long long ld, int M, int N, float alpha,
+                               float* out0, float* out1, void* workspace, size_t ws_bytes,
+                               void* stream);
 
 /* ---------------------------------------------------------- LSTM layer
  * Bidirectional recurrence of one encoder layer (nn.LSTM bidirectional with
@@ -760,6 +774,12 @@ int asr_vgg_block_backward_zdp(const void* dnext, int dnext_dtype, int flat, con
  */
 int asr_prof_begin(int stride);
 int asr_prof_end(double* mean_us, long long* launches, double* mean_work, int nkinds);
+/* Every timed sample of kind `kind` after asr_prof_end: per sample the tag
+ * naming the kernel instantiation (GEMM / convolution family x 4 + operand
+ * modes, the CTC vocabulary V, the persistent LSTM pass form; prof.h
+ * ASR_PTAG_*), its algorithmic work and its duration in microseconds, up to
+ * `max` samples.  Returns the sample count, -1 before asr_prof_end. */
+long long asr_prof_samples(int kind, int* tags, double* work, double* us, long long max);
 
 /* Status word of the persistent recurrence kernels: bit 0 set when a bounded
  * inter-work-group wait gave up (a co-residency failure; that pass's outputs
@@ -787,6 +807,11 @@ int asr_lstm_xg_mode(int* mode, int clear);
  * per-step phase timestamps of work-groups 0..3 (4 x 128 steps x 6 u64) to
  * `host` (may be NULL); returns the element count, 0 when tracing is off. */
 long long asr_xg_trace_read(unsigned long long* host);
+/* Diagnostics only (tools/cores_locate.py): backward recurrence launches
+ * enqueued on `stream` after this call record every dh_t their cell waves form
+ * into dh ([B][T][2][H] f32) and each step's sweep spin count into spins
+ * ([ceil(B/R)][T][2][H/16] u32); NULL pointers switch the recording off. */
+int asr_lstm_debug_dh(float* dh, unsigned* spins, void* stream);
 
 #ifdef __cplusplus
 }

@@ -40,6 +40,9 @@ SIGNATURES = {
                                 c_int, c_int, c_vp, c_vp, c_float, c_vp, c_size, c_vp]),
     'asr_ctc_backward': (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int,
                                  c_int, c_vp, c_float, c_vp, c_ll, c_ll, c_vp, c_size, c_vp]),
+    'asr_ctc_backward_bf16': (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp,
+                                      c_int, c_int, c_vp, c_float, c_vp, c_ll, c_ll, c_int, c_vp,
+                                      c_size, c_vp]),
     'asr_ctc_fwd_bwd': (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int,
                                 c_int, c_int, c_vp, c_vp, c_vp, c_size, c_vp]),
     'asr_gemm': (c_int, [c_vp, c_int, c_int, c_vp]),
@@ -51,6 +54,8 @@ SIGNATURES = {
     'asr_colsum_workspace_bytes': (c_size, [c_int, c_int]),
     'asr_colsum_accumulate': (c_int, [c_vp, c_ll, c_int, c_int, c_float, c_vp, c_vp, c_vp, c_size,
                                       c_vp]),
+    'asr_colsum_accumulate_bf16': (c_int, [c_vp, c_ll, c_int, c_int, c_float, c_vp, c_vp, c_vp,
+                                           c_size, c_vp]),
     'asr_conv3x3_c1_forward_xs': (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp,
                                           c_vp, c_int, c_vp]),
     'asr_conv3x3_tr_supported': (c_int, [c_int, c_int, c_int]),
@@ -181,6 +186,7 @@ SIGNATURES = {
                                            c_vp, c_int, c_vp, c_vp, c_size, c_vp]),
     'asr_prof_begin': (c_int, [c_int]),
     'asr_prof_end': (c_int, [c_vp, c_vp, c_vp, c_int]),
+    'asr_prof_samples': (c_ll, [c_int, c_vp, c_vp, c_vp, c_ll]),
     'asr_lstm_persist_status': (c_int, [c_vp, c_int, c_vp]),
     'asr_lstm_status_gather': (c_int, [c_vp, c_int, c_vp]),
     'asr_lstm_status_inject': (c_int, [c_int, c_vp]),
@@ -194,6 +200,7 @@ SIGNATURES = {
     'asr_att_step_backward': (c_int, [c_vp] + [c_vp] * 21 + [c_size, c_vp]),
     'asr_lstm_xg_mode': (c_int, [c_vp, c_int]),
     'asr_xg_trace_read': (c_ll, [c_vp]),
+    'asr_lstm_debug_dh': (c_int, [c_vp, c_vp, c_vp]),
 }
 
 

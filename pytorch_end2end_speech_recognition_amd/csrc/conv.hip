@@ -655,7 +655,8 @@ extern "C" int asr_conv3x3_tr(const void* in, long long P, int Cin, int Fp, int 
   a.w_bytes = (unsigned)((size_t)Cout * 9 * Cin * 2);
   a.out_bytes = (unsigned)(P * Cout * osz);
   hipStream_t s = (hipStream_t)stream;
-  const int slot = prof_begin_launch(ASR_PROF_GEMM, s, 2.0 * P * Cout * 9.0 * Cin);
+  const int slot = prof_begin_launch(ASR_PROF_GEMM, s, 2.0 * P * Cout * 9.0 * Cin,
+                                     4 * ASR_PTAG_CONV_TR);
   const int bf = out_dtype == ASR_DT_BF16;
   int rc = ASR_ERR_UNSUPPORTED;
 #define TR_CASE(CI, CO, WPX, NW)                                                         \
@@ -716,7 +717,8 @@ extern "C" int asr_conv3x3_tr_wgrad(const void* x, const void* dz, long long P, 
   a.x_bytes = (unsigned)(P * Cin * 2);
   a.dz_bytes = (unsigned)(P * Cout * 2);
   hipStream_t s = (hipStream_t)stream;
-  const int slot = prof_begin_launch(ASR_PROF_GEMM, s, 2.0 * P * Cout * 9.0 * Cin);
+  const int slot = prof_begin_launch(ASR_PROF_GEMM, s, 2.0 * P * Cout * 9.0 * Cin,
+                                     4 * ASR_PTAG_CONV_TR_WGRAD);
   const void* k = nullptr;
   if (Cin == 64 && Cout == 64) k = (const void*)conv3x3_tr_wgrad<64, 64>;
   else if (Cin == 64) k = (const void*)conv3x3_tr_wgrad<64, 128>;
@@ -892,7 +894,7 @@ extern "C" int asr_conv3x3_c1_wgrad_xs(const float* xs, int round_bf16, int B, i
   const size_t lds = (size_t)C1W_TP * Co * 2 + (size_t)(C1W_TP + 2 * (F + 3)) * 4;
   ASR_REQUIRE(lds <= 64 * 1024, ASR_ERR_UNSUPPORTED, "conv3x3_c1_wgrad_xs: F too large");
   hipStream_t s = (hipStream_t)stream;
-  const int slot = prof_begin_launch(ASR_PROF_GEMM, s, 2.0 * P * Co * 9.0);
+  const int slot = prof_begin_launch(ASR_PROF_GEMM, s, 2.0 * P * Co * 9.0, 4 * ASR_PTAG_CONV_C1_WGRAD);
   hipLaunchKernelGGL(c1_wgrad_xs<64>, dim3(S), dim3(256), lds, s, xs, round_bf16, B, T, F,
                      (const uint16_t*)dz, (int)P, S, (float*)ws);
   ASR_LAUNCH_CHECK();

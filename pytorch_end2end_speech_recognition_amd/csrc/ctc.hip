@@ -588,6 +588,106 @@ __global__ void __launch_bounds__(256) ctc_grad(
   }
 }
 
+// The same gradient written as the bf16 dY operand of the output layer's two
+// GEMMs (ctc_grad_bf16): rows (b, t) of `gld` columns (gld >= V, gld % 8 == 0,
+// 16-B aligned rows), columns [V, gld) zero -- the zero-padded pitch the
+// staged LinearND product reads (native_ops.LinearCTCFn), so the f32 gradient
+// is never written and never restaged.  Eight columns per thread, one 16-B
+// store; the class representatives then overwrite their own column.
+template <bool kTable>
+__global__ void __launch_bounds__(256) ctc_grad_bf16(
+    const float* __restrict__ acts, long long st, long long sb, int T, int V,
+    const int32_t* __restrict__ labels, const int32_t* __restrict__ label_lens,
+    const int32_t* __restrict__ act_lens, const int32_t* __restrict__ offs, int blank, int Spad,
+    const float* __restrict__ lse, const float* __restrict__ emit,
+    const float* __restrict__ alpha, const float* __restrict__ beta,
+    const float* __restrict__ logp, const float* __restrict__ grad_scale, float scale_mul,
+    uint16_t* __restrict__ grads, long long gst, long long gsb, int gld, int rev) {
+  extern __shared__ __attribute__((aligned(16))) float occ[];  // [V] (kTable) or [Spad]
+  const long long row = rev ? (long long)gridDim.x - 1 - blockIdx.x : blockIdx.x;
+  const int b = (int)(row / T), t = (int)(row % T);
+  uint16_t* g = grads + (long long)t * gst + (long long)b * gsb;
+  const float* x = acts + (long long)t * st + (long long)b * sb;
+  const int tid = threadIdx.x, nth = blockDim.x;
+  const int n8 = gld >> 3;
+  const int Tb = act_lens[b];
+  const float lp = logp[b];
+  if (t >= Tb || lp == neg_inf()) {
+    for (int i = tid; i < n8; i += nth) reinterpret_cast<uint4*>(g)[i] = make_uint4(0u, 0u, 0u, 0u);
+    return;
+  }
+  const float scale = (grad_scale ? grad_scale[0] : 1.0f) * scale_mul;
+  const float z = lse[row];
+  const int L = min(label_lens[b], (Spad - 1) / 2);
+  const int S = 2 * L + 1;
+  const int32_t* lab = labels + offs[b];
+  auto cls = [&](int s_) {
+    int c = (s_ & 1) ? lab[s_ >> 1] : blank;
+    return c < 0 ? 0 : (c >= V ? V - 1 : c);
+  };
+  const float* al = alpha + row * Spad;
+  const float* bt = beta + row * Spad;
+  const float* em = emit + row * Spad;
+  auto pack = [&](int c0, auto val) {   // 8 columns c0 .. c0 + 7 -> one 16-B store
+    unsigned w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = c0 + 2 * j;
+      const unsigned lo = c < V ? f2bf(val(c)) : 0u;
+      const unsigned hi = c + 1 < V ? f2bf(val(c + 1)) : 0u;
+      w[j] = lo | (hi << 16);
+    }
+    reinterpret_cast<uint4*>(g)[c0 >> 3] = make_uint4(w[0], w[1], w[2], w[3]);
+  };
+  if constexpr (kTable) {
+    for (int v = tid; v < V; v += nth) occ[v] = 0.f;
+    __syncthreads();
+    for (int s_ = tid; s_ < S; s_ += nth) atomicAdd(&occ[cls(s_)], ex2(al[s_] + bt[s_] - em[s_] - lp));
+    __syncthreads();
+    for (int i = tid; i < n8; i += nth)
+      pack(8 * i, [&](int c) { return (__expf(x[c] - z) - occ[c]) * scale; });
+    return;
+  } else {
+    for (int s_ = tid; s_ < S; s_ += nth) occ[s_] = ex2(al[s_] + bt[s_] - em[s_] - lp);
+    __syncthreads();
+    int rep_c[4];
+    float rep_v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      rep_c[r] = -1;
+      rep_v[r] = 0.f;
+      const int s_ = tid + r * nth;
+      if (s_ >= S) continue;
+      const int c = cls(s_);
+      bool first;
+      if ((s_ & 1) == 0) {
+        first = s_ == 0;
+      } else {
+        first = c != blank;
+        for (int q = 1; q < s_ && first; q += 2) first = cls(q) != c;
+      }
+      if (!first) continue;
+      float acc = 0.f;
+      for (int q = 0; q < S; ++q)
+        if (cls(q) == c) acc += occ[q];
+      rep_c[r] = c;
+      rep_v[r] = acc;
+    }
+    // stream the row: g = softmax * scale, two 8-column groups in flight per thread
+    int i = tid;
+    for (; i + nth < n8; i += 2 * nth) {
+      pack(8 * i, [&](int c) { return __expf(x[c] - z) * scale; });
+      pack(8 * (i + nth), [&](int c) { return __expf(x[c] - z) * scale; });
+    }
+    for (; i < n8; i += nth) pack(8 * i, [&](int c) { return __expf(x[c] - z) * scale; });
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (rep_c[r] >= 0) g[rep_c[r]] = f2bf((__expf(x[rep_c[r]] - z) - rep_v[r]) * scale);
+  }
+}
+
 __global__ void ctc_loss_reduce(const float* __restrict__ costs, int B, float scale,
                                 float* __restrict__ out) {
   __shared__ float red[256];
@@ -661,7 +761,7 @@ extern "C" int asr_ctc_forward(const float* acts, long long stride_t, long long 
   ASR_LAUNCH_CHECK();
   const long long rows = (long long)B * T;
   // algorithmic HBM bytes of the forward: the activations read once
-  const int pslot = prof_begin_launch(ASR_PROF_CTC_FWD, s, 4.0 * (double)V * (double)rows);
+  const int pslot = prof_begin_launch(ASR_PROF_CTC_FWD, s, 4.0 * (double)V * (double)rows, V);
   if (V > 1024)
     hipLaunchKernelGGL(ctc_emit_wide, dim3((unsigned)rows), dim3(256), 0, s, acts, stride_t,
                        stride_b, T, V, labels_flat, label_lens, act_lens, ws.offs, blank, Spad,
@@ -711,7 +811,7 @@ extern "C" int asr_ctc_backward(const float* acts, long long stride_t, long long
   const bool table = V <= 256;
   const int threads = table ? 64 : 256;  // compact mode: Spad <= 1024 = 4 * threads
   // algorithmic HBM bytes: activations read + gradient written
-  const int pslot = prof_begin_launch(ASR_PROF_CTC_GRAD, s, 8.0 * (double)V * B * T);
+  const int pslot = prof_begin_launch(ASR_PROF_CTC_GRAD, s, 8.0 * (double)V * B * T, V);
   if (table)
     hipLaunchKernelGGL(ctc_grad<true>, dim3((unsigned)((long long)B * T)), dim3(threads),
                        V * sizeof(float), s, acts, stride_t, stride_b, T, V, labels_flat,
@@ -724,6 +824,43 @@ extern "C" int asr_ctc_backward(const float* acts, long long stride_t, long long
                        label_lens, act_lens, ws.offs, blank, Spad, ws.lse, ws.emit, ws.alpha,
                        ws.beta, ws.logp, grad_scale, scale, grads, gstride_t, gstride_b,
                        (ctc_row_order() >> 1) & 1);
+  ASR_LAUNCH_CHECK();
+  prof_end_launch(ASR_PROF_CTC_GRAD, pslot, s);
+  return ASR_OK;
+}
+
+extern "C" int asr_ctc_backward_bf16(const float* acts, long long stride_t, long long stride_b,
+                                     int T, int B, int V, const int32_t* labels_flat,
+                                     const int32_t* label_lens, const int32_t* act_lens,
+                                     int max_label_len, int blank, const float* grad_scale,
+                                     float scale, uint16_t* grads, long long gstride_t,
+                                     long long gstride_b, int gld, const void* workspace,
+                                     size_t ws_bytes, void* stream) {
+  int rc = check_common(acts, T, B, V, labels_flat, label_lens, act_lens, max_label_len, blank,
+                        workspace, ws_bytes);
+  if (rc) return rc;
+  ASR_REQUIRE(grads, ASR_ERR_ARG, "ctc_bf16: grads is null");
+  ASR_REQUIRE(gld >= V && gld % 8 == 0 && gstride_t % 8 == 0 && gstride_b % 8 == 0 &&
+                  ((uintptr_t)grads & 15) == 0,
+              ASR_ERR_ARG, "ctc_bf16: gradient rows must be 16-B aligned with gld %d >= V %d", gld,
+              V);
+  hipStream_t s = (hipStream_t)stream;
+  CtcWs ws;
+  ws_layout(T, B, max_label_len, &ws, (char*)workspace);
+  const int Spad = 64 * pick_k(max_label_len);
+  const bool table = V <= 256;
+  const int threads = table ? 64 : 256;
+  // algorithmic HBM bytes: activations read (4 V) + bf16 gradient written (2 gld) per row
+  const int pslot = prof_begin_launch(ASR_PROF_CTC_GRAD, s, (4.0 * V + 2.0 * gld) * B * T, V);
+#define ASR_CTC_G16(TB)                                                                          \
+  hipLaunchKernelGGL(ctc_grad_bf16<TB>, dim3((unsigned)((long long)B * T)), dim3(threads),       \
+                     (TB ? V : Spad) * sizeof(float), s, acts, stride_t, stride_b, T, V,         \
+                     labels_flat, label_lens, act_lens, ws.offs, blank, Spad, ws.lse, ws.emit,   \
+                     ws.alpha, ws.beta, ws.logp, grad_scale, scale, grads, gstride_t, gstride_b, \
+                     gld, (ctc_row_order() >> 1) & 1)
+  if (table) ASR_CTC_G16(true);
+  else ASR_CTC_G16(false);
+#undef ASR_CTC_G16
   ASR_LAUNCH_CHECK();
   prof_end_launch(ASR_PROF_CTC_GRAD, pslot, s);
   return ASR_OK;

@@ -1712,7 +1712,11 @@ __global__ void splitk_reduce4(const float* __restrict__ slab, int ksplit, int M
 // One (64-column, row chunk) tile per work-group: 4 waves split the chunk's
 // rows (wave w takes rows w, w + 4, ...), each lane keeps eight rows' loads in
 // flight; the waves' sums are combined in LDS in wave order (deterministic).
-__global__ void __launch_bounds__(256) colsum_partial(const float* __restrict__ g, long long ld,
+__device__ __forceinline__ float colsum_ld(const float* g, long long i) { return g[i]; }
+__device__ __forceinline__ float colsum_ld(const uint16_t* g, long long i) { return bf2f(g[i]); }
+
+template <typename TG>
+__global__ void __launch_bounds__(256) colsum_partial(const TG* __restrict__ g, long long ld,
                                                       int M, int N, int rows_per_chunk,
                                                       float* __restrict__ partial) {
   __shared__ float red[4][64];
@@ -1726,14 +1730,14 @@ __global__ void __launch_bounds__(256) colsum_partial(const float* __restrict__ 
     for (; m + 28 < m1; m += 32) {
       float v[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = g[(long long)(m + 4 * j) * ld + n];
+      for (int j = 0; j < 8; ++j) v[j] = colsum_ld(g, (long long)(m + 4 * j) * ld + n);
 #pragma unroll
       for (int j = 0; j < 8; j += 2) {
         s0 += v[j];
         s1 += v[j + 1];
       }
     }
-    for (; m < m1; m += 4) s0 += g[(long long)m * ld + n];
+    for (; m < m1; m += 4) s0 += colsum_ld(g, (long long)m * ld + n);
   }
   red[w][lane] = s0 + s1;
   __syncthreads();
@@ -2063,6 +2067,7 @@ int gemm_launch_own(const asr_gemm_t* problems, int nprob, int compute_dtype, vo
     const dim3 g8(maxwg8, 1, nprob * maxb);
     const size_t lds8 = 4 * TILE8;
     const char* er = getenv("ASR_GEMM_8R");   // ring form by default (ASR_GEMM_8R=0: two buffers)
+    prof_set_tag(ASR_PROF_GEMM, slot, 4 * ((er && er[0] == '0') ? ASR_PTAG_GEMM_8W : ASR_PTAG_GEMM_8R) + fast);
     if (!(er && er[0] == '0')) {
       static bool attrr = false;
       const int ldsr = NSLOT * 2 * TILER;
@@ -2116,6 +2121,7 @@ int gemm_launch_own(const asr_gemm_t* problems, int nprob, int compute_dtype, vo
                   ASR_ERR_HIP, "gemm: cannot raise the LDS limit of the 256x256 kernel");
       attr = true;
     }
+    prof_set_tag(ASR_PROF_GEMM, slot, 4 * ASR_PTAG_GEMM_KK256 + fast);
     hipLaunchKernelGGL(gemm_bf16_kk256, dim3(maxwg2, 1, nprob * maxb), dim3(NT),
                        (size_t)NST2 * 2 * FTILE2, s, P);
   } else if (fast >= 0 && n64_ok(problems, nprob, fast & 1)) {
@@ -2139,6 +2145,7 @@ int gemm_launch_own(const asr_gemm_t* problems, int nprob, int compute_dtype, vo
     for (int i = 0; i < nprob; ++i)
       maxwg64 = max(maxwg64, ceil_div(P.p[i].M, N64_BM) * max(1, P.p[i].ksplit));
     const dim3 g64(maxwg64, 1, nprob * maxb);
+    prof_set_tag(ASR_PROF_GEMM, slot, 4 * ASR_PTAG_GEMM_N64 + fast);
 #define ASR_N64(A, B)                                                                          \
   do {                                                                                         \
     if (n64st == 3)                                                                            \
@@ -2156,6 +2163,8 @@ int gemm_launch_own(const asr_gemm_t* problems, int nprob, int compute_dtype, vo
   } else if (fast >= 0) {
     const int nst = g_small_tiles ? 2 : fast_stages();
     const size_t lds = (size_t)nst * 2 * FTILE;
+    prof_set_tag(ASR_PROF_GEMM, slot,
+                 4 * (nst == 4 ? ASR_PTAG_GEMM_FAST4 : ASR_PTAG_GEMM_FAST2) + fast);
     switch (fast) {
 #define ASR_FAST(A, B)                                                                   \
   do {                                                                                   \
@@ -2191,9 +2200,11 @@ int gemm_launch_own(const asr_gemm_t* problems, int nprob, int compute_dtype, vo
                 problems[i].a.tap_group, problems[i].a.map.perm != nullptr, problems[i].b.dtype,
                 problems[i].b.trans, problems[i].b.tap_group, problems[i].b.map.perm != nullptr);
     const size_t lds = 2 * BM * LDB16 * 2;
+    prof_set_tag(ASR_PROF_GEMM, slot, 4 * ASR_PTAG_GEMM_GEN_BF16);
     hipLaunchKernelGGL(gemm_kernel<true>, grid, dim3(NT), lds, s, P);
   } else {
     const size_t lds = 2 * BM * LDF32 * 4;
+    prof_set_tag(ASR_PROF_GEMM, slot, 4 * ASR_PTAG_GEMM_GEN_F32);
     hipLaunchKernelGGL(gemm_kernel<false>, grid, dim3(NT), lds, s, P);
   }
   ASR_LAUNCH_CHECK();
@@ -2365,9 +2376,10 @@ extern "C" size_t asr_colsum_workspace_bytes(int M, int N) {
   return (size_t)colsum_chunks(M, N) * N * sizeof(float);
 }
 
-extern "C" int asr_colsum_accumulate(const float* g, long long ld, int M, int N, float alpha,
-                                     float* out0, float* out1, void* workspace, size_t ws_bytes,
-                                     void* stream) {
+template <typename TG>
+static int colsum_accumulate_impl(const TG* g, long long ld, int M, int N, float alpha,
+                                  float* out0, float* out1, void* workspace, size_t ws_bytes,
+                                  void* stream) {
   ASR_REQUIRE(g && out0 && workspace, ASR_ERR_ARG, "colsum: null pointer");
   if (M <= 0 || N <= 0) return ASR_OK;
   const int nchunk = colsum_chunks(M, N);
@@ -2375,11 +2387,24 @@ extern "C" int asr_colsum_accumulate(const float* g, long long ld, int M, int N,
               "colsum: workspace too small");
   const int rpc = (M + nchunk - 1) / nchunk;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(colsum_partial, dim3(ceil_div(N, 64), nchunk), dim3(256), 0, s, g, ld, M, N,
-                     rpc, (float*)workspace);
+  hipLaunchKernelGGL(colsum_partial<TG>, dim3(ceil_div(N, 64), nchunk), dim3(256), 0, s, g, ld, M,
+                     N, rpc, (float*)workspace);
   ASR_LAUNCH_CHECK();
   hipLaunchKernelGGL(colsum_final, dim3(ceil_div(N, 16)), dim3(256), 0, s,
                      (const float*)workspace, nchunk, N, alpha, out0, out1);
   ASR_LAUNCH_CHECK();
   return ASR_OK;
+}
+
+extern "C" int asr_colsum_accumulate(const float* g, long long ld, int M, int N, float alpha,
+                                     float* out0, float* out1, void* workspace, size_t ws_bytes,
+                                     void* stream) {
+  return colsum_accumulate_impl(g, ld, M, N, alpha, out0, out1, workspace, ws_bytes, stream);
+}
+
+// The same over a bf16 matrix (the fused CTC head's dY operand), f32 sums.
+extern "C" int asr_colsum_accumulate_bf16(const uint16_t* g, long long ld, int M, int N,
+                                          float alpha, float* out0, float* out1, void* workspace,
+                                          size_t ws_bytes, void* stream) {
+  return colsum_accumulate_impl(g, ld, M, N, alpha, out0, out1, workspace, ws_bytes, stream);
 }

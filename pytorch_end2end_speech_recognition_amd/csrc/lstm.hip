@@ -561,7 +561,7 @@ extern "C" int asr_lstm_forward(float* gx_act, const void* whh_f, const void* wh
       lstm_fwd_xg_launch(B, T, H, lens, (const float*)whh_f, (const float*)whh_r, gx_act, y, cst,
                          workspace, ybf, s, true) == 1) {
     // one persistent launch, tagged-granule hand-off (lstm_xg.hip)
-    const int slot = prof_begin_launch(ASR_PROF_LSTM_FWD_SEQ, s);
+    const int slot = prof_begin_launch(ASR_PROF_LSTM_FWD_SEQ, s, 0.0, ASR_PTAG_LSTM_FWD_XG);
     const int rc = lstm_fwd_xg_launch(B, T, H, lens, (const float*)whh_f, (const float*)whh_r,
                                       gx_act, y, cst, workspace, ybf, s, false);
     ASR_REQUIRE(rc == 1, ASR_ERR_HIP, "lstm_forward: tagged-granule launch failed");
@@ -586,7 +586,7 @@ extern "C" int asr_lstm_forward(float* gx_act, const void* whh_f, const void* wh
                           true)) {
     // one persistent launch for the whole pass
     ASR_CHECK_HIP(hipMemsetAsync(ctr, 0, fwd_ctr_bytes(B), s));
-    const int slot = prof_begin_launch(ASR_PROF_LSTM_FWD_SEQ, s);
+    const int slot = prof_begin_launch(ASR_PROF_LSTM_FWD_SEQ, s, 0.0, ASR_PTAG_LSTM_PERSIST);
     const int rc = lstm_fwd_persistent(B, T, H, lens, wbf_f, gx_act, y, cst, (uint16_t*)hbuf,
                                        ctr, ybf, s, false);
     ASR_REQUIRE(rc == 1, ASR_ERR_HIP, "lstm_forward: persistent launch failed");
@@ -646,7 +646,7 @@ static int lstm_backward_impl(const float* dy, const void* whh_f, const void* wh
   if (bf && w_dtype == ASR_DT_F32 &&
       lstm_bwd_xg_launch(B, T, H, lens, (const float*)whh_f, (const float*)whh_r, dy, act_dg, cst,
                          workspace, dgbf, dbpart, s, true, dg_f32) == 1) {
-    const int slot = prof_begin_launch(ASR_PROF_LSTM_BWD_SEQ, s);
+    const int slot = prof_begin_launch(ASR_PROF_LSTM_BWD_SEQ, s, 0.0, ASR_PTAG_LSTM_BWD_XG);
     const int rc = lstm_bwd_xg_launch(B, T, H, lens, (const float*)whh_f, (const float*)whh_r, dy,
                                       act_dg, cst, workspace, dgbf, dbpart, s, false, dg_f32);
     ASR_REQUIRE(rc == 1, ASR_ERR_HIP, "lstm_backward: tagged-granule launch failed");
@@ -681,7 +681,7 @@ static int lstm_backward_impl(const float* dy, const void* whh_f, const void* wh
   }
   ASR_LAUNCH_CHECK();
   if (persist) {  // one persistent launch for the whole pass
-    const int slot = prof_begin_launch(ASR_PROF_LSTM_BWD_SEQ, s);
+    const int slot = prof_begin_launch(ASR_PROF_LSTM_BWD_SEQ, s, 0.0, ASR_PTAG_LSTM_PERSIST);
     const int rc = lstm_bwd_persistent(B, T, H, lens, (const uint16_t*)wt, dy, act_dg, cst,
                                        (uint16_t*)dg, ctr, dgbf, s, false);
     ASR_REQUIRE(rc == 1, ASR_ERR_HIP, "lstm_backward: persistent launch failed");
@@ -799,7 +799,7 @@ extern "C" int asr_lstm_backward_dgbf_h(const float* dy, const void* whh_f, cons
   if (lstm_bwd_xg_launch(B, T, H, lens, (const float*)whh_f, (const float*)whh_r, dy, nullptr, cst,
                          workspace, dgbf, part, s, true, false, act_h) != 1)
     return ASR_ERR_UNSUPPORTED;
-  const int slot = prof_begin_launch(ASR_PROF_LSTM_BWD_SEQ, s);
+  const int slot = prof_begin_launch(ASR_PROF_LSTM_BWD_SEQ, s, 0.0, ASR_PTAG_LSTM_BWD_XG);
   const int rc = lstm_bwd_xg_launch(B, T, H, lens, (const float*)whh_f, (const float*)whh_r, dy,
                                     nullptr, cst, workspace, dgbf, part, s, false, false, act_h);
   ASR_REQUIRE(rc == 1, ASR_ERR_HIP, "lstm_backward_dgbf_h: tagged-granule launch failed");

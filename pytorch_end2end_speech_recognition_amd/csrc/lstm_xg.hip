@@ -54,6 +54,11 @@ __device__ unsigned g_xg_resident;
 // Diagnostics only (ASR_XG_TRACE=1): per-step phase timestamps (100 MHz
 // s_memrealtime) of work-groups 0..XG_TR_WG-1, steps 0..XG_TR_STEPS-1.
 __device__ unsigned long long* g_xg_trace;
+// Diagnostics only (asr_lstm_debug_dh): when set, the backward's cell waves
+// record every dh_t they form, [B][T][2][H] f32 (the swept partial sums + dy),
+// and the spin count of the sweep that fed it, [B/R groups][T][2][H/16] u32.
+__device__ float* g_xg_dbg_dh;
+__device__ unsigned* g_xg_dbg_spins;
 #define XG_TR_WG 64
 #define XG_TR_STEPS 128
 #define XG_TR_K 8
@@ -238,6 +243,33 @@ __device__ __forceinline__ bf16x8 cvt_f32x8(const float* p) {
 
 __device__ __forceinline__ float fsig(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 __device__ __forceinline__ float ftanh(float x) { return 2.f * fsig(2.f * x) - 1.f; }
+
+// Packed fp16 gate activations (act_h) that keep precision near saturation.
+// The backward needs s and 1 - s of each sigmoid gate and g and 1 - g^2 of
+// the tanh gate; fp16's spacing just below 1.0 (4.9e-4) would make 1 - s of a
+// saturated gate coarse or zero.  A sigmoid gate is stored as s when s < 0.5
+// and as -(1 - s) otherwise (s > 0, so the sign bit is free); the tanh gate as
+// g when |g| <= 0.499 and as sign(g) * (1 - |g|) * 2^14 otherwise (magnitudes
+// >= 0.5 mark the complement form; 1 - |g| is clamped to >= 2^-15, so the
+// stored magnitude is >= 0.5 exactly, while direct values round to < 0.5).
+// Both forms carry fp16's relative precision for the small factor.
+__device__ __forceinline__ float enc_sig(float s) { return s < 0.5f ? s : s - 1.f; }
+__device__ __forceinline__ float enc_tanh(float g) {
+  const float a = fabsf(g);
+  return a <= 0.499f ? g : copysignf(fmaxf(1.f - a, 1.f / 32768.f) * 16384.f, g);
+}
+__device__ __forceinline__ void dec_sig(float e, float& s, float& om) {
+  const bool neg = (__float_as_uint(e) >> 31) != 0u;   // -0 (s == 1) included
+  s = neg ? 1.f + e : e;
+  om = neg ? -e : 1.f - e;
+}
+__device__ __forceinline__ void dec_tanh(float e, float& g, float& om2) {   // om2 = 1 - g^2
+  const float a = fabsf(e);
+  const float c = a * (1.f / 16384.f);
+  const bool cm = a >= 0.5f;
+  g = cm ? copysignf(1.f - c, e) : e;
+  om2 = cm ? c * (2.f - c) : 1.f - e * e;
+}
 
 // ---------------------------------------------------------------------------
 // forward.  grid = G * WPG (G = 2 * ceil(B / R) groups, WPG = H / 16).
@@ -694,8 +726,9 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
     const long long sidx = ((long long)b * T + tt) * 2 * H + (long long)dir * H + j;
     y[sidx] = v[0];
     cst[sidx] = v[1];
-    if (acth) {   // the four gates of (b, t, dir, j) as one 8-B fp16 store
-      const h16x4 hv = {(_Float16)v[2], (_Float16)v[3], (_Float16)v[4], (_Float16)v[5]};
+    if (acth) {   // the four gates of (b, t, dir, j) as one 8-B fp16 store (enc_sig / enc_tanh)
+      const h16x4 hv = {(_Float16)enc_sig(v[2]), (_Float16)enc_sig(v[3]), (_Float16)enc_tanh(v[4]),
+                        (_Float16)enc_sig(v[5])};
       acth[(((long long)b * T + tt) * 2 + dir) * H + j] = hv;
     } else {
       const long long gb = ((long long)b * T + tt) * H8 + gcol;
@@ -819,6 +852,7 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
     const int srow = sl >> 1, sq = sl & 1;   // row, units 8 sq .. 8 sq + 7
     const int pgi = tid / (2 * R);
     constexpr int NLD = (4 * MB + NPG - 1) / NPG;   // producers per sweeper lane (WPG <= 4 MB)
+    unsigned* dspin = g_xg_dbg_spins;
     const int nsleep = __builtin_amdgcn_readfirstlane(g_xg_sleep);
     const int ndelay = __builtin_amdgcn_readfirstlane(g_xg_delay);
     for (int q = 0; q < T; ++q) {
@@ -863,6 +897,8 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
             XG_TR(q, 5, spins);
             XG_TR(q, 6, t_iss);
             XG_TR(q, 7, (unsigned long long)(grp * 256 + mem));
+            if (dspin && tid == 0)
+              dspin[(((long long)rg * T + q) * 2 + dir) * WPG + mem] = spins + 1;
             break;
           }
           if (!keep_spinning(spins, abortw, nsleep)) {
@@ -892,6 +928,7 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
     const bool own = b < B;
     const int len = own ? lens[b] : 0;
     float dc = 0.f;
+    float* ddh = g_xg_dbg_dh;
     // c_t of step q is c_{tp} of step q - 1: with `carry` it is taken from there
     auto load_cell = [&](int q, float (&av)[4], h16x4& avh, float& cc, float& cp, float& dyv,
                          const float* carry) {
@@ -964,17 +1001,23 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
 #pragma unroll
           for (int p = 0; p < NPG; ++p) dh += red[p][row][unit];
         }
+        if (ddh) ddh[(((long long)b * T + t) * 2 + dir) * H + j] = dh;
+        float ig, fg, gg, og, omi, omf, omg2, omo;   // gates and 1 - s / 1 - g^2
         if constexpr (AH) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) av[k] = (float)avh[k];
+          dec_sig((float)avh[0], ig, omi);
+          dec_sig((float)avh[1], fg, omf);
+          dec_tanh((float)avh[2], gg, omg2);
+          dec_sig((float)avh[3], og, omo);
+        } else {
+          ig = av[0]; fg = av[1]; gg = av[2]; og = av[3];
+          omi = 1.f - ig; omf = 1.f - fg; omg2 = 1.f - gg * gg; omo = 1.f - og;
         }
-        const float ig = av[0], fg = av[1], gg = av[2], og = av[3];
         const float tc = ftanh(cc);
         const float dcell = dc + dh * og * (1.f - tc * tc);
-        d_i = dcell * gg * ig * (1.f - ig);
-        d_f = dcell * cp * fg * (1.f - fg);
-        d_g = dcell * ig * (1.f - gg * gg);
-        d_o = dh * tc * og * (1.f - og);
+        d_i = dcell * gg * ig * omi;
+        d_f = dcell * cp * fg * omf;
+        d_g = dcell * ig * omg2;
+        d_o = dh * tc * og * omo;
         dc = dcell * fg;
         sb_i += d_i;
         sb_f += d_f;
@@ -1406,6 +1449,19 @@ extern "C" long long asr_xg_trace_read(unsigned long long* host) {
   return (long long)n;
 }
 
+// Diagnostics: the backward recurrence's dh / spin-count recorders (NULL: off).
+// Stream-ordered: launches enqueued after this call on `stream` record into the
+// given buffers ([B][T][2][H] f32; [ceil(B/R)][T][2][H/16] u32).
+extern "C" int asr_lstm_debug_dh(float* dh, unsigned* spins, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemcpyToSymbolAsync(HIP_SYMBOL(asr::g_xg_dbg_dh), &dh, sizeof(dh), 0,
+                             hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyToSymbolAsync(HIP_SYMBOL(asr::g_xg_dbg_spins), &spins, sizeof(spins), 0,
+                             hipMemcpyHostToDevice, s) != hipSuccess)
+    return ASR_ERR_HIP;
+  return ASR_OK;
+}
+
 // Which hand-off protocols the tagged-granule recurrence used since the last
 // clear: bit 0 write-through (sc1, any placement), bit 1 XCD-local.
 extern "C" int asr_lstm_xg_mode(int* mode, int clear) {
@@ -1477,7 +1533,7 @@ extern "C" int asr_lstm_forward_x(const uint16_t* x, int Din, const uint16_t* wi
     return ASR_ERR_UNSUPPORTED;
   ASR_REQUIRE(ws_bytes >= asr::lstm_xg_fwd_bytes(B, H), ASR_ERR_WORKSPACE,
               "lstm_forward_x: workspace too small");
-  const int slot = asr::prof_begin_launch(ASR_PROF_LSTM_FWD_SEQ, s);
+  const int slot = asr::prof_begin_launch(ASR_PROF_LSTM_FWD_SEQ, s, 0.0, ASR_PTAG_LSTM_FWD_XGX);
   const int rc = asr::lstm_fwd_xgx_launch(B, T, H, lens, whh_f, whh_r, x, Din, wih, b_ih, b_hh,
                                           act, y, cst, workspace, ybf, s, false, nullptr);
   ASR_REQUIRE(rc == 1, ASR_ERR_HIP, "lstm_forward_x: launch failed");
@@ -1504,7 +1560,7 @@ extern "C" int asr_lstm_forward_xh(const uint16_t* x, int Din, const uint16_t* w
     return ASR_ERR_UNSUPPORTED;
   ASR_REQUIRE(ws_bytes >= asr::lstm_xg_fwd_bytes(B, H), ASR_ERR_WORKSPACE,
               "lstm_forward_xh: workspace too small");
-  const int slot = asr::prof_begin_launch(ASR_PROF_LSTM_FWD_SEQ, s);
+  const int slot = asr::prof_begin_launch(ASR_PROF_LSTM_FWD_SEQ, s, 0.0, ASR_PTAG_LSTM_FWD_XGX);
   const int rc = asr::lstm_fwd_xgx_launch(B, T, H, lens, whh_f, whh_r, x, Din, wih, b_ih, b_hh,
                                           nullptr, y, cst, workspace, ybf, s, false, act_h);
   ASR_REQUIRE(rc == 1, ASR_ERR_HIP, "lstm_forward_xh: launch failed");
@@ -1525,10 +1581,15 @@ __global__ void unpack_act_h(const h16x4* __restrict__ a, long long n, int H,
     const int r = (int)(i - bt * 2LL * H), dir = r / H, j = r - dir * H;
     const h16x4 v = a[i];
     float* o = act + bt * 8LL * H + (long long)dir * 4 * H + j;
-    o[0] = (float)v[0];
-    o[H] = (float)v[1];
-    o[2LL * H] = (float)v[2];
-    o[3LL * H] = (float)v[3];
+    float s, om;
+    dec_sig((float)v[0], s, om);
+    o[0] = s;
+    dec_sig((float)v[1], s, om);
+    o[H] = s;
+    dec_tanh((float)v[2], s, om);
+    o[2LL * H] = s;
+    dec_sig((float)v[3], s, om);
+    o[3LL * H] = s;
   }
 }
 }  // namespace

@@ -270,12 +270,17 @@ class AttentionSeq2seq(ModelBase):
 
     def compute_ctc_loss(self, enc_out, ys_ctc, x_lens, y_lens, task=0, scale=1.0):
         """:609-653 on the HIP CTC kernel; ys_ctc already +1 (blank 0)."""
-        logits = getattr(self, 'fc_ctc_%d' % task)(enc_out)
+        fc = getattr(self, 'fc_ctc_%d' % task)
         labels = self.np2var(_concatenate_labels_np(ys_ctc, y_lens))
         yl_d = self.np2var(y_lens.astype(np.int32))
         B = enc_out.shape[0]
         max_l = int(y_lens.max()) if len(y_lens) else 0
-        loss, _ = ops.ctc_loss(logits, labels, yl_d, x_lens, max_l, loss_scale=scale / B)
+        if not (self.training and fc.dropout_p > 0):
+            # LinearND + CTC as one op (native_ops.linear_ctc_loss)
+            loss, _ = ops.linear_ctc_loss(enc_out, fc.fc.weight, fc.fc.bias, labels, yl_d, x_lens,
+                                          max_l, loss_scale=scale / B)
+            return loss
+        loss, _ = ops.ctc_loss(fc(enc_out), labels, yl_d, x_lens, max_l, loss_scale=scale / B)
         return loss
 
     def _encode(self, xs, x_lens, is_multi_task=False):

@@ -24,6 +24,15 @@ from ..criterion import cross_entropy_label_smoothing
 from .decoders.greedy_decoder import GreedyDecoder
 
 
+class _Head(object):
+    """An output layer not applied yet: its input, the LinearND and the input
+    dropout handed over by the encoder (CTC._encode(defer_head=True))."""
+    __slots__ = ('x', 'fc', 'drop')
+
+    def __init__(self, x, fc, drop):
+        self.x, self.fc, self.drop = x, fc, drop
+
+
 def _concatenate_labels_np(ys, y_lens):
     """ctc.py:532-549 on the host, vectorised: [B, L] padded -> int32 [sum L]."""
     ys = np.asarray(ys)
@@ -110,7 +119,7 @@ class CTC(ModelBase):
                 self.inject_weight_noise(mean=0, std=self.weight_noise_std)
         B = len(xs)
         xs_d = self.np2var(xs, dtype='float')
-        logits, out_lens_d, perm_d = self._encode(xs_d, x_lens)
+        logits, out_lens_d, perm_d = self._encode(xs_d, x_lens, defer_head=True)
         if self.logits_temperature != 1:
             logits = logits * (1.0 / self.logits_temperature)
 
@@ -120,8 +129,16 @@ class CTC(ModelBase):
             return float(loss.item())
         return loss
 
-    def _encode(self, xs, x_lens, is_multi_task=False):
-        """ctc.py:344-396."""
+    def _head_fusable(self, fc):
+        """The output layer and the CTC loss can run as one op (LinearCTCFn):
+        nothing but the CTC term reads the logits."""
+        return (self.logits_temperature == 1 and self.ls_prob == 0 and
+                not (self.training and fc.dropout_p > 0))
+
+    def _encode(self, xs, x_lens, is_multi_task=False, defer_head=False):
+        """ctc.py:344-396.  defer_head: the output layer(s) whose only consumer
+        is the CTC loss are returned as _Head(x, fc, drop) for _ctc_term's
+        fused LinearND + CTC op instead of being applied here."""
         if is_multi_task:
             xs, x_lens, xs_sub, x_lens_sub, perm_idx = self.encoder(
                 xs, x_lens, volatile=not self.training)
@@ -134,11 +151,17 @@ class CTC(ModelBase):
         for i in range(len(self.fc_list)):
             xs = getattr(self, 'fc_' + str(i))(xs, input_drop=pd)
             pd = None
-        logits = self.fc_out(xs, input_drop=pd)
+        if defer_head and self._head_fusable(self.fc_out):
+            logits = _Head(xs, self.fc_out, pd)
+        else:
+            logits = self.fc_out(xs, input_drop=pd)
         if is_multi_task:
             for i in range(len(self.fc_list_sub)):
                 xs_sub = getattr(self, 'fc_sub_' + str(i))(xs_sub)
-            logits_sub = self.fc_out_sub(xs_sub)
+            if defer_head and self._head_fusable(self.fc_out_sub):
+                logits_sub = _Head(xs_sub, self.fc_out_sub, None)
+            else:
+                logits_sub = self.fc_out_sub(xs_sub)
             return logits, x_lens, logits_sub, x_lens_sub, perm_idx
         return logits, x_lens, perm_idx
 
@@ -149,6 +172,11 @@ class CTC(ModelBase):
         labels = self.np2var(_concatenate_labels_np(ys_s, yl_s))
         yl_d = self.np2var(yl_s)
         max_l = int(yl_s.max()) if len(yl_s) else 0
+        if isinstance(logits, _Head):     # LinearND + CTC as one op (no f32 d logits)
+            h = logits
+            loss, _ = ops.linear_ctc_loss(h.x, h.fc.fc.weight, h.fc.fc.bias, labels, yl_d, lens_d,
+                                          max_l, loss_scale=1.0 / B, drop=h.drop)
+            return loss
         loss, _ = ops.ctc_loss(logits, labels, yl_d, lens_d, max_l, loss_scale=1.0 / B)
         if self.ls_prob > 0:
             loss_ls = cross_entropy_label_smoothing(

@@ -106,7 +106,8 @@ class HierarchicalCTC(CTC):
         B = len(xs)
         xs_d = self.np2var(xs, dtype='float')
         logits, lens_d, logits_sub, lens_sub_d, _ = self._encode(xs_d, x_lens,
-                                                                 is_multi_task=True)
+                                                                 is_multi_task=True,
+                                                                 defer_head=True)
         if self.logits_temperature != 1:
             logits = logits * (1.0 / self.logits_temperature)
             logits_sub = logits_sub * (1.0 / self.logits_temperature)

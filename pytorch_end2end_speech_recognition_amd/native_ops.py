@@ -152,6 +152,82 @@ def _staged(t, rows, cols, ld=None):
     return out
 
 
+def _linear_stages(M, K, Nout):
+    """Whether LinearND's product is staged as bf16 operands (see _STAGE_FLOPS)."""
+    flops = 2.0 * M * Nout * K
+    return compute_dtype() == BF16 and (
+        flops >= _STAGE_FLOPS or (Nout % 8 != 0 and flops >= _STAGE_FLOPS_RAGGED))
+
+
+def _linear_forward(x, weight, bias, drop):
+    """y = dropout(x) W^T + b (f32 [..., Nout]); returns (y, xo, wo, stage):
+    the GEMM operands the backward reuses (bf16 staged copies when stage)."""
+    N.require_device(x, weight)
+    x = x.contiguous()
+    K = x.shape[-1]
+    Nout = weight.shape[0]
+    M = x.numel() // K
+    y = torch.empty(*x.shape[:-1], Nout, dtype=torch.float32, device=x.device)
+    stage = _linear_stages(M, K, Nout)
+    fused_drop = drop is not None and stage and K % 8 == 0
+    if drop is not None and not fused_drop:        # materialise dropout(x) first
+        xd = torch.empty_like(x)
+        N.call('asr_dropout', N.ptr(x), N.ptr(xd), x.numel(), float(drop[0]), int(drop[1]),
+               N.stream_handle(x.device))
+        x = xd
+    # staged copies: x [M][Kp], weight [Np][Kp] (rows Nout.. and columns K.. zero)
+    Kp, Np = ((K + 7) // 8 * 8, (Nout + 7) // 8 * 8) if stage else (K, Nout)
+    if stage:
+        # fused_drop: K % 8 == 0, so Kp == K and the dropped copy is the operand
+        xo = (convert_rows_bf16(x, rowmap(K), M, K, drop=drop) if fused_drop else
+              _staged(x, M, K, Kp))
+        wo = torch.empty(Np, Kp, dtype=torch.bfloat16, device=x.device)
+        N.call('asr_convert_rows_bf16_ld', N.ptr(weight), rowmap(K), Nout, K, Kp, N.ptr(wo),
+               N.stream_handle(x.device))
+        if Np > Nout:
+            N.call('asr_convert_rows_bf16_ld', N.ptr(weight), rowmap(0, t_limit=1,
+                   rows_per_b=Np - Nout, t_add=1), Np - Nout, Kp, Kp,
+                   ctypes.c_void_p(wo.data_ptr() + Nout * Kp * 2), N.stream_handle(x.device))
+    else:
+        xo, wo = x, weight
+    if M > 0:
+        p = gemm_problem(operand(xo, 0, rowmap(Kp)), operand(wo, 0, rowmap(Kp)), y,
+                         rowmap(Nout), M, Nout, Kp, bias=bias)
+        run_gemm([p], x.device)
+    return y, xo, wo, stage
+
+
+def _linear_backward(xo, wo, bias, stage, xshape, weight, drop, dyo, need_dx, dy_bias=None):
+    """dX and dW (+ db) of _linear_forward from dyo: the f32 dY, or with stage
+    its bf16 copy [M][Np] whose columns Nout.. are zero (they meet W's zero
+    rows).  dy_bias: the tensor the bias gradient is summed from (f32 [M,
+    Nout] or the bf16 dyo)."""
+    K = xshape[-1]
+    Nout = weight.shape[0]
+    M = int(np.prod(xshape[:-1]))
+    dev = dyo.device
+    Kp, Np = (xo.shape[-1], wo.shape[0]) if stage else (K, Nout)
+    dx = None
+    probs = []
+    if need_dx:
+        dx = torch.empty(xshape, dtype=torch.float32, device=dev)
+        probs.append(gemm_problem(operand(dyo, 0, rowmap(Np)), operand(wo, 1, rowmap(Kp)),
+                                  dx, rowmap(K), M, K, Np, drop=drop))
+    gw = grad_buffer(weight)
+    probs.append(gemm_problem(operand(dyo, 1, rowmap(Np)), operand(xo, 1, rowmap(Kp)), gw,
+                              rowmap(K), Nout, K, M, beta=1.0))
+    run_gemm(probs, dev)
+    if bias is not None:
+        if dy_bias.dtype == torch.bfloat16:
+            nb = N.query('asr_colsum_workspace_bytes', M, Nout)
+            ws = _ws(nb, dev)
+            N.call('asr_colsum_accumulate_bf16', N.ptr(dy_bias), dy_bias.shape[-1], M, Nout, 1.0,
+                   N.ptr(grad_buffer(bias)), None, N.ptr(ws), nb, N.stream_handle(dev))
+        else:
+            colsum_accumulate(dy_bias.view(M, Nout), grad_buffer(bias))
+    return dx
+
+
 class LinearFn(torch.autograd.Function):
     """y = dropout(x) W^T + b.  drop=(p, seed): dropout of the INPUT with
     asr_dropout's mask, folded into the bf16 staging of x (forward) and the dX
@@ -160,40 +236,7 @@ class LinearFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, drop=None):
-        N.require_device(x, weight)
-        x = x.contiguous()
-        K = x.shape[-1]
-        Nout = weight.shape[0]
-        M = x.numel() // K
-        y = torch.empty(*x.shape[:-1], Nout, dtype=torch.float32, device=x.device)
-        flops = 2.0 * M * Nout * K
-        stage = compute_dtype() == BF16 and (
-            flops >= _STAGE_FLOPS or (Nout % 8 != 0 and flops >= _STAGE_FLOPS_RAGGED))
-        fused_drop = drop is not None and stage and K % 8 == 0
-        if drop is not None and not fused_drop:        # materialise dropout(x) first
-            xd = torch.empty_like(x)
-            N.call('asr_dropout', N.ptr(x), N.ptr(xd), x.numel(), float(drop[0]), int(drop[1]),
-                   N.stream_handle(x.device))
-            x = xd
-        # staged copies: x [M][Kp], weight [Np][Kp] (rows Nout.. and columns K.. zero)
-        Kp, Np = ((K + 7) // 8 * 8, (Nout + 7) // 8 * 8) if stage else (K, Nout)
-        if stage:
-            # fused_drop: K % 8 == 0, so Kp == K and the dropped copy is the operand
-            xo = (convert_rows_bf16(x, rowmap(K), M, K, drop=drop) if fused_drop else
-                  _staged(x, M, K, Kp))
-            wo = torch.empty(Np, Kp, dtype=torch.bfloat16, device=x.device)
-            N.call('asr_convert_rows_bf16_ld', N.ptr(weight), rowmap(K), Nout, K, Kp, N.ptr(wo),
-                   N.stream_handle(x.device))
-            if Np > Nout:
-                N.call('asr_convert_rows_bf16_ld', N.ptr(weight), rowmap(0, t_limit=1,
-                       rows_per_b=Np - Nout, t_add=1), Np - Nout, Kp, Kp,
-                       ctypes.c_void_p(wo.data_ptr() + Nout * Kp * 2), N.stream_handle(x.device))
-        else:
-            xo, wo = x, weight
-        if M > 0:
-            p = gemm_problem(operand(xo, 0, rowmap(Kp)), operand(wo, 0, rowmap(Kp)), y,
-                             rowmap(Nout), M, Nout, Kp, bias=bias)
-            run_gemm([p], x.device)
+        y, xo, wo, stage = _linear_forward(x, weight, bias, drop)
         ctx.save_for_backward(xo, wo)
         ctx.meta = (bias, stage, tuple(x.shape), weight)
         ctx.drop = drop
@@ -203,28 +246,84 @@ class LinearFn(torch.autograd.Function):
     def backward(ctx, dy):
         xo, wo = ctx.saved_tensors
         bias, stage, xshape, weight = ctx.meta
-        drop = ctx.drop     # dropout's backward = its mask, applied by the dX epilogue
         dy = dy.contiguous()
-        K = xshape[-1]
         Nout = weight.shape[0]
         M = dy.numel() // Nout
-        dx = None
         if M == 0:
             return torch.zeros(xshape, dtype=torch.float32, device=dy.device), None, None, None
-        Kp, Np = (xo.shape[-1], wo.shape[0]) if stage else (K, Nout)
+        Np = wo.shape[0] if stage else Nout
         dyo = _staged(dy, M, Nout, Np) if stage else dy   # zero columns meet zero W rows
-        probs = []
-        if ctx.needs_input_grad[0]:
-            dx = torch.empty(xshape, dtype=torch.float32, device=dy.device)
-            probs.append(gemm_problem(operand(dyo, 0, rowmap(Np)), operand(wo, 1, rowmap(Kp)),
-                                      dx, rowmap(K), M, K, Np, drop=drop))
-        gw = grad_buffer(weight)
-        probs.append(gemm_problem(operand(dyo, 1, rowmap(Np)), operand(xo, 1, rowmap(Kp)), gw,
-                                  rowmap(K), Nout, K, M, beta=1.0))
-        run_gemm(probs, dy.device)
-        if bias is not None:
-            colsum_accumulate(dy.view(M, Nout), grad_buffer(bias))
+        # dropout's backward = its mask, applied by the dX epilogue
+        dx = _linear_backward(xo, wo, bias, stage, xshape, weight, ctx.drop, dyo,
+                              ctx.needs_input_grad[0], dy_bias=dy)
         return dx, None, None, None
+
+
+class LinearCTCFn(torch.autograd.Function):
+    """The CTC output layer and its loss as ONE op (LinearND + CTC: ctc.py:30-52
+    with linear.py:32-47), for heads whose product is staged in bf16.
+    Forward: the staged GEMM writes the f32 logits [B, T, V] (bias fused),
+    then the CTC forward (emissions + lattices) reads them.  Backward: the CTC
+    gradient is written straight into the bf16 dY operand of the two GEMMs --
+    rows of Np = V rounded up to 8 columns, the padding zero
+    (asr_ctc_backward_bf16) -- so the f32 d logits is never written and never
+    restaged (at the 10001-word head of configs[4]: 320 MB written + 480 MB
+    staging traffic per call saved), and the bias gradient is summed from the
+    same operand.  The loss and every gradient equal ctc_loss(linear(...))
+    up to the bf16 rounding of dY the staged product applies anyway."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, drop, labels_flat, label_lens, act_lens, max_label_len,
+                loss_scale, blank, zero_infinity):
+        N.require_device(labels_flat, label_lens, act_lens)
+        logits, xo, wo, stage = _linear_forward(x, weight, bias, drop)
+        assert stage, 'LinearCTCFn needs a staged (bf16) output layer'
+        B, T, V = logits.shape
+        nbytes = N.query('asr_ctc_workspace_bytes', T, B, V, max_label_len)
+        ws = _ws(nbytes, logits.device)
+        costs = torch.empty(B, dtype=torch.float32, device=logits.device)
+        loss = torch.empty(1, dtype=torch.float32, device=logits.device)
+        N.call('asr_ctc_forward', N.ptr(logits), V, T * V, T, B, V, N.ptr(labels_flat),
+               N.ptr(label_lens), N.ptr(act_lens), int(max_label_len), int(blank),
+               int(bool(zero_infinity)), N.ptr(costs), N.ptr(loss), float(loss_scale), N.ptr(ws),
+               nbytes, N.stream_handle(logits.device))
+        ctx.save_for_backward(xo, wo, logits, labels_flat, label_lens, act_lens, ws)
+        ctx.meta = (bias, tuple(x.shape), weight, int(max_label_len), int(blank),
+                    float(loss_scale), nbytes)
+        ctx.drop = drop
+        ctx.mark_non_differentiable(costs)
+        return loss, costs
+
+    @staticmethod
+    def backward(ctx, g_loss, g_costs):
+        xo, wo, logits, labels_flat, label_lens, act_lens, ws = ctx.saved_tensors
+        bias, xshape, weight, max_label_len, blank, loss_scale, nbytes = ctx.meta
+        B, T, V = logits.shape
+        Np = wo.shape[0]
+        dev = logits.device
+        dyo = torch.empty(B * T, Np, dtype=torch.bfloat16, device=dev)
+        g = g_loss.contiguous() if g_loss is not None else None
+        N.call('asr_ctc_backward_bf16', N.ptr(logits), V, T * V, T, B, V, N.ptr(labels_flat),
+               N.ptr(label_lens), N.ptr(act_lens), max_label_len, blank, N.ptr(g),
+               loss_scale if g is not None else 0.0, N.ptr(dyo), Np, T * Np, Np, N.ptr(ws),
+               nbytes, N.stream_handle(dev))
+        dx = _linear_backward(xo, wo, bias, True, xshape, weight, ctx.drop, dyo,
+                              ctx.needs_input_grad[0], dy_bias=dyo)
+        return (dx,) + (None,) * 10
+
+
+def linear_ctc_loss(x, weight, bias, labels_flat, label_lens, act_lens, max_label_len,
+                    loss_scale=1.0, drop=None, blank=0, zero_infinity=True):
+    """ctc_loss(linear(x, weight, bias, drop), ...) -> (loss [1], costs [B]);
+    one fused op (LinearCTCFn) when the output layer is staged in bf16
+    (ASR_CTC_HEAD_FUSED=0 keeps the two ops)."""
+    K = x.shape[-1]
+    if (x.dim() == 3 and _linear_stages(x.numel() // K, K, weight.shape[0]) and
+            os.environ.get('ASR_CTC_HEAD_FUSED', '1') != '0'):
+        return LinearCTCFn.apply(x, weight, bias, drop, labels_flat, label_lens, act_lens,
+                                 max_label_len, loss_scale, blank, zero_infinity)
+    return ctc_loss(linear(x, weight, bias, drop), labels_flat, label_lens, act_lens,
+                    max_label_len, loss_scale, blank, zero_infinity)
 
 
 def linear(x, weight, bias=None, drop=None):
@@ -902,16 +1001,9 @@ class BLSTMLayerFn(torch.autograd.Function):
                         # hold the GEMMs back until the previous layer's backward
                         # recurrence (launched next on the main stream) is resident
                         N.call('asr_lstm_wgrad_gate', N.stream_handle(dev))
-                    wbufs = gbufs
-                    if os.environ.get('ASR_DIAG_WGRAD_SCRATCH') == '1':   # diagnostics only
-                        wbufs = tuple(torch.zeros_like(g) for g in gbufs)
-                    if os.environ.get('ASR_DIAG_SPIN'):   # diagnostics: an LDS-only stand-in
-                        bad = torch.zeros(1, dtype=torch.int32, device=dev)
-                        N.call('asr_diag_lds_spin', 256, int(os.environ['ASR_DIAG_SPIN']),
-                               N.ptr(bad), N.stream_handle(dev))
-                        _diag_bad.append(bad)    # (weight gradients skipped)
-                    else:
-                        _blstm_wgrad(dg_op, act, x_op, x_map, y_op, T, wbufs, dev)
+                    # (tools/cores_locate.py replaces _blstm_wgrad with stand-in
+                    # side-stream workloads; nothing diagnostic runs here)
+                    _blstm_wgrad(dg_op, act, x_op, x_map, y_op, T, gbufs, dev)
             finally:
                 if small:
                     N.call('asr_gemm_set_small_tiles', 0)
@@ -1085,7 +1177,6 @@ def _blstm_wgrad(dg, dg_f32, x_op, x_map, y_op, T, gbufs, dev):
 
 
 _side_streams = {}
-_diag_bad = []         # ASR_DIAG_SPIN pattern-mismatch counters (diagnostics)
 _side_pending = []     # (side stream, gbufs, compute stream) of weight gradients not joined yet
 
 

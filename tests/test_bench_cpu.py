@@ -73,3 +73,35 @@ def test_repeat_batches_are_fresh_copies():
     assert x1['xs'] is not x2['xs'] and np.array_equal(x1['xs'], b['xs'])
     with pytest.raises(StopIteration):
         r.next()
+
+
+def test_roofline_rows_per_kernel_instantiation():
+    """The roofline is reported per kernel instantiation (kind x prof tag), the
+    dominant row names ONE kernel (not the GEMM family), and each CTC head
+    gets its own rows plus a whole-op row against 8 * V bytes per frame."""
+    bench = _bench()
+    import argparse
+    args = argparse.Namespace(batch=32, frames=1000, precision='bf16')
+    p = dict(bench.CONFIGS['vgg_hier']['params'])
+    V, rows = 10001, 32 * 250
+    samples = {
+        3: [(3, 0.0, 1000.0)] * 4,                                  # lstm_bwd_xg
+        4: ([(4 * 1 + 3, 2e11, 300.0)] * 10 +                       # gemm_bf16_8r<1, 1>
+            [(4 * 9, 5e10, 120.0)] * 6),                            # conv3x3_tr
+        5: [(V, 4.0 * V * rows, 100.0), (29, 4.0 * 29 * rows * 4, 50.0)],
+        6: [(V, 8.0 * V * rows, 120.0), (29, 8.0 * 29 * rows * 4, 20.0)],
+    }
+    launches = [0, 0, 0, 4, 16, 2, 2, 0, 0]
+    r = bench.roofline_report(args, p, samples, launches, 'x')
+    assert r['kernel'] == 'lstm_bwd_xg<*>' and r['launches_timed'] == 4
+    assert r['bound'] == 'mfma' and r['us_per_time_step'] > 0
+    o = r['other_kernels']
+    assert 'gemm_bf16_8r<1, 1>' in o and o['gemm_bf16_8r<1, 1>']['launches'] == 10
+    assert abs(o['gemm_bf16_8r<1, 1>']['achieved'] - 2e11 / 300e-6 / 1e12) < 0.01
+    assert 'conv3x3_tr<*>' in o
+    assert 'ctc_grad [V=10001]' in o and 'ctc_grad [V=29]' in o
+    op = o['ctc_op [V=10001]']
+    assert op['algorithmic_bytes_per_call'] == int(8.0 * V * rows)
+    assert abs(op['mean_call_us'] - 220.0) < 1e-9
+    assert abs(sum(v['share_of_timed_kernel_time'] for k, v in o.items() if 'ctc_op' not in k)
+               + r['share_of_timed_kernel_time'] - 1.0) < 0.01

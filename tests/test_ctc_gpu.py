@@ -115,3 +115,53 @@ def test_ctc_compact_grad_long_labels_k16(cuda_dev):
     # costs ~2600 nats: alpha + beta - log P reaches ~5e3 in magnitude, whose f32
     # spacing (4.9e-4) bounds the occupancy's relative accuracy at ~1e-3
     np.testing.assert_allclose(grads, g_ref, rtol=2e-3, atol=2e-4)
+
+
+@pytest.mark.parametrize('V,K', [(1001, 256), (29, 4096)])
+def test_fused_ctc_head_matches_separate_ops(V, K, cuda_dev, monkeypatch):
+    """linear_ctc_loss (LinearND + CTC as one op: the CTC gradient written
+    straight into the bf16, column-padded dY operand of the head's GEMMs) vs
+    linear() then ctc_loss() (f32 d logits, then a staging pass): the loss and
+    dX / dW are bitwise equal -- the same f32 values rounded to bf16 once
+    either way -- and the bias gradient (summed from the bf16 operand instead
+    of the f32 d logits) agrees to bf16 rounding.  V = 1001 exercises the
+    compact gradient (no V table), V = 29 the LDS class table."""
+    ops = _native()
+    rng = np.random.RandomState(11)
+    B, T = 8, 200
+    act_lens = np.sort(rng.randint(150, T + 1, B))[::-1].astype(np.int32)
+    act_lens[0] = T
+    label_lens = rng.randint(5, 40, B).astype(np.int32)
+    labels = np.concatenate([rng.randint(1, V, l) for l in label_lens]).astype(np.int32)
+    x0 = torch.from_numpy((rng.randn(B, T, K) * 0.5).astype(np.float32)).to(cuda_dev)
+    w0 = torch.from_numpy((rng.randn(V, K) * 0.05).astype(np.float32)).to(cuda_dev)
+    b0 = torch.from_numpy((rng.randn(V) * 0.1).astype(np.float32)).to(cuda_dev)
+    lab = torch.from_numpy(labels).to(cuda_dev)
+    ll = torch.from_numpy(label_lens).to(cuda_dev)
+    al = torch.from_numpy(act_lens).to(cuda_dev)
+    assert ops._linear_stages(B * T, K, V) is False     # fp32 mode: never staged
+    ops.set_compute_dtype('bf16')
+    try:
+        assert ops._linear_stages(B * T, K, V)
+        out = {}
+        for fused in ('1', '0'):
+            monkeypatch.setenv('ASR_CTC_HEAD_FUSED', fused)
+            x = x0.clone().requires_grad_(True)
+            w = w0.clone().requires_grad_(True)
+            b = b0.clone().requires_grad_(True)
+            w.grad = torch.zeros_like(w)
+            b.grad = torch.zeros_like(b)
+            loss, costs = ops.linear_ctc_loss(x, w, b, lab, ll, al, int(label_lens.max()),
+                                              loss_scale=1.0 / B)
+            (loss * 2.0).backward()
+            torch.cuda.synchronize()
+            out[fused] = [loss.detach().clone(), costs.clone(), x.grad.clone(), w.grad.clone(),
+                          b.grad.clone()]
+    finally:
+        ops.set_compute_dtype('fp32')
+    f, u = out['1'], out['0']
+    assert torch.equal(f[0], u[0]) and torch.equal(f[1], u[1])
+    assert torch.equal(f[2], u[2]), float((f[2] - u[2]).abs().max())
+    assert torch.equal(f[3], u[3]), float((f[3] - u[3]).abs().max())
+    rel = float((f[4] - u[4]).norm() / u[4].norm())
+    assert rel < 1e-2, rel

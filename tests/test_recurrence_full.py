@@ -142,3 +142,65 @@ def test_reference_init_early_steps_vs_float64(cuda_dev):
               for b in range(B))
     print('\nreference-init first %d steps: fwd %.2e, rev %.2e' % (W, fwd, rev))
     assert fwd <= 2e-2 and rev <= 2e-2, (fwd, rev)
+
+
+def _sat_case(seed=5, Bs=16, Ts=160, Hs=256, Ds=256):
+    """Saturated gates: every gate row's bias drawn +-U[3, 8] (random sign), so
+    sigmoid gates sit at 0.95-0.9997 or 3e-4-0.05 and the tanh gate near +-1,
+    where fp16 storage of s itself would make 1 - s coarse or zero."""
+    rng = np.random.RandomState(seed)
+    lens = np.sort(rng.randint(120, Ts + 1, Bs))[::-1].astype(np.int32)
+    lens[0] = Ts
+    x = (rng.randn(Bs, Ts, Ds) * 0.5).astype(np.float32)
+    for b in range(Bs):
+        x[b, lens[b]:] = 0
+    g = torch.Generator().manual_seed(seed + 1)
+    w_ih = torch.rand(8 * Hs, Ds, generator=g) * 0.2 - 0.1
+    w_hh = (torch.rand(8 * Hs, Hs, generator=g) * 2 - 1) * 0.03
+    mag = torch.rand(8 * Hs, generator=g) * 5 + 3
+    sign = torch.where(torch.rand(8 * Hs, generator=g) < 0.5, -1.0, 1.0)
+    b_ih = mag * sign
+    b_hh = torch.zeros(8 * Hs)
+    dy = torch.from_numpy(rng.randn(Bs, Ts, 2 * Hs).astype(np.float32))
+    for b in range(Bs):
+        dy[b, lens[b]:] = 0
+    return lens, torch.from_numpy(x), w_ih, w_hh, b_ih, b_hh, dy
+
+
+@pytest.mark.gpu
+def test_packed_gate_activations_saturated_vs_float64(cuda_dev, monkeypatch):
+    """The fused bf16 forward stores the gate activations packed as fp16
+    (ASR_XG_ACT_H=1, the default; enc_sig / enc_tanh in lstm_xg.hip keep 1 - s
+    and 1 - g^2 at fp16's relative precision).  With saturated gates, compare
+    it with the f32 activation layout (ASR_XG_ACT_H=0) and with float64: the
+    bias gradient of the saturated rows -- sums of d_gate = ... * s * (1 - s)
+    -- is where a plain fp16 s (spacing 4.9e-4 below 1.0) would lose 1 - s."""
+    global B, T, H
+    lens, x, w_ih, w_hh, b_ih, b_hh, dy = _sat_case()
+    Bs, Ts, Ds = x.shape
+    Hs = w_hh.shape[1]
+    saved = (B, T, H)
+    B, T, H = Bs, Ts, Hs
+    try:
+        ref = _oracle(lens, x, w_ih, w_hh, b_ih, b_hh, dy)
+        res = {}
+        for ah in ('1', '0'):
+            monkeypatch.setenv('ASR_XG_ACT_H', ah)
+            res[ah] = _gpu('bf16', lens, x, w_ih, w_hh, b_ih, b_hh, dy, cuda_dev)
+    finally:
+        B, T, H = saved
+    names = ['y', 'dx', 'dW_ih', 'dW_hh', 'db']
+    refs = list(ref[:4]) + [ref[4]]
+    out = {}
+    for ah, got in res.items():
+        got = got[:5]
+        errs = {n: float((g - r).norm() / r.norm()) for n, g, r in zip(names, got, refs)}
+        # every gate row's own relative error of db (the saturated rows' sums)
+        row = ((got[4] - refs[4]).abs() / refs[4].abs().clamp_min(1e-30))
+        errs['db_row_median'] = float(row.median())
+        out[ah] = errs
+    print('\nsaturated gates, rel. L2 vs float64: ACT_H=1 %s | ACT_H=0 %s' % (out['1'], out['0']))
+    for n in names:
+        assert out['1'][n] <= 2e-2, ('ACT_H=1', n, out['1'][n])
+        assert out['1'][n] <= 1.5 * out['0'][n] + 2e-3, (n, out['1'][n], out['0'][n])
+    assert out['1']['db_row_median'] <= 1.5 * out['0']['db_row_median'] + 2e-3

@@ -110,8 +110,6 @@ def layer_trace():
         return rec
 
     a, b = run(), run()
-    if no._diag_bad:
-        print('diag spin LDS pattern errors:', sum(int(t.item()) for t in no._diag_bad))
     if extras[0]:
         for i, (x, y) in enumerate(zip(extras[0], extras[1])):
             print('call %d after-run inputs maxdiff x_op %.3e act %.3e cst %.3e y_op %.3e dy %.3e' % (
