@@ -809,9 +809,11 @@ int asr_lstm_xg_mode(int* mode, int clear);
 long long asr_xg_trace_read(unsigned long long* host);
 /* Diagnostics only (tools/cores_locate.py): backward recurrence launches
  * enqueued on `stream` after this call record every dh_t their cell waves form
- * into dh ([B][T][2][H] f32) and each step's sweep spin count into spins
- * ([ceil(B/R)][T][2][H/16] u32); NULL pointers switch the recording off. */
-int asr_lstm_debug_dh(float* dh, unsigned* spins, void* stream);
+ * into dh ([B][T][2][H] f32), each step's sweep spin count into spins
+ * ([ceil(B/R)][T][2][H/16] u32) and, per cell and step, the four gate
+ * gradients computed, the four activations, c_t, c_{t-1}, dy and the incoming
+ * dc into cell ([B][T][2][H][12] f32); NULL pointers switch recording off. */
+int asr_lstm_debug_dh(float* dh, unsigned* spins, float* cell, void* stream);
 
 #ifdef __cplusplus
 }

@@ -115,11 +115,17 @@ def lstm_direction_bptt(x, lens, w_ih, w_hh, b_ih, b_hh, reverse, dy):
     return y, dx, dw_ih, dw_hh, db
 
 
-def vgg_front(p, prefix, cfg, xs, x_lens, masks=None, training=True):
+def vgg_front(p, prefix, cfg, xs, x_lens, masks=None, training=True, decisions=None):
     """CNNEncoder.forward (encoders/cnn.py:124-165) with relu, 3x3 / stride 1 /
     padding 1 convs, max-pool (first floor mode, later ceil mode), BatchNorm2d
     in training mode (batch statistics; running stats returned, not written)
     and optional replayed dropout masks (masks[l]: [B, T', F', C] scales).
+    decisions (test infrastructure: the bf16 pins): per layer (relu_mask
+    [B, C, F, T] bool, pool_index [B, C, F', T'] int64 flat index f * T + t of
+    each window's maximum, or None) -- the ReLU and max-pool choices of another
+    evaluation (the GPU's) replayed, so rounding-level differences of the
+    activations cannot move a max-pool argmax or a ReLU sign and route the
+    gradient to another pixel.
     Returns (out [B, T', F'*C], lens np.int64 via ConvOutSize's floor rule
     (cnn_utils.py:25-37), running-stat updates {name: tensor})."""
     Fn = torch.nn.functional
@@ -130,11 +136,15 @@ def vgg_front(p, prefix, cfg, xs, x_lens, masks=None, training=True):
         conv = '%sconv.layers.%d.' % (prefix, idx)
         x = Fn.conv2d(x, p[conv + 'weight'], p.get(conv + 'bias'), stride=1, padding=1)
         idx += 2                                              # conv, relu
-        x = torch.relu(x)
+        x = torch.relu(x) if decisions is None else x * decisions[l][0].to(x.dtype)
         pl = cfg['poolings'][l]
         if len(pl):
-            x = Fn.max_pool2d(x, kernel_size=tuple(pl), stride=tuple(pl),
-                              ceil_mode=not first_pool)
+            if decisions is None:
+                x = Fn.max_pool2d(x, kernel_size=tuple(pl), stride=tuple(pl),
+                                  ceil_mode=not first_pool)
+            else:
+                ind = decisions[l][1]
+                x = x.flatten(2).gather(2, ind.flatten(2)).view(ind.shape)
             lens = np.floor((lens - pl[1]) / pl[1] + 1).astype(np.int64)
             first_pool = False
             idx += 1
@@ -153,6 +163,36 @@ def vgg_front(p, prefix, cfg, xs, x_lens, masks=None, training=True):
     return x.transpose(1, 3).reshape(B, To, Fo * C), lens, stats
 
 
+def vgg_decisions(p, prefix, cfg, xs, training=True):
+    """The ReLU masks and max-pool argmax indices vgg_front's forward takes
+    (its `decisions` format; replaying them reproduces it exactly)."""
+    Fn = torch.nn.functional
+    x = xs.transpose(1, 2).unsqueeze(1)
+    idx, first_pool, out = 0, True, []
+    for l, C in enumerate(cfg['conv_channels']):
+        conv = '%sconv.layers.%d.' % (prefix, idx)
+        z = Fn.conv2d(x, p[conv + 'weight'], p.get(conv + 'bias'), stride=1, padding=1)
+        idx += 2
+        mask = z > 0
+        x = torch.relu(z)
+        pl = cfg['poolings'][l]
+        ind = None
+        if len(pl):
+            x, ind = Fn.max_pool2d(x, kernel_size=tuple(pl), stride=tuple(pl),
+                                   ceil_mode=not first_pool, return_indices=True)
+            first_pool = False
+            idx += 1
+        if cfg.get('batch_norm'):
+            bn = '%sconv.layers.%d.' % (prefix, idx)
+            x = Fn.batch_norm(x, p[bn + 'running_mean'].clone(), p[bn + 'running_var'].clone(),
+                              p[bn + 'weight'], p[bn + 'bias'], training=training,
+                              momentum=0.1, eps=1e-5)
+            idx += 1
+        idx += 1
+        out.append((mask, ind))
+    return out
+
+
 def blstm_encoder(p, prefix, cfg, xs, x_lens, capture_layer=0):
     """RNNEncoder.forward (rnn.py:284-487) for rnn_type 'lstm' or 'gru'
     (cfg['rnn_type']), bidirectional,
@@ -168,7 +208,8 @@ def blstm_encoder(p, prefix, cfg, xs, x_lens, capture_layer=0):
     x_lens = np.asarray(x_lens)
     if cfg.get('conv_channels'):
         xs, x_lens, _ = vgg_front(p, prefix, cfg, xs, x_lens,
-                                  training=cfg.get('bn_training', True))
+                                  training=cfg.get('bn_training', True),
+                                  decisions=cfg.get('vgg_decisions'))
     perm = np.argsort(-x_lens, kind='stable')                 # rnn.py:319-326
     xs = xs[torch.as_tensor(perm)]
     lens = x_lens[perm].astype(np.int64)

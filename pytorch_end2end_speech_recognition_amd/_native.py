@@ -200,7 +200,7 @@ SIGNATURES = {
     'asr_att_step_backward': (c_int, [c_vp] + [c_vp] * 21 + [c_size, c_vp]),
     'asr_lstm_xg_mode': (c_int, [c_vp, c_int]),
     'asr_xg_trace_read': (c_ll, [c_vp]),
-    'asr_lstm_debug_dh': (c_int, [c_vp, c_vp, c_vp]),
+    'asr_lstm_debug_dh': (c_int, [c_vp, c_vp, c_vp, c_vp]),
 }
 
 

@@ -59,6 +59,10 @@ __device__ unsigned long long* g_xg_trace;
 // and the spin count of the sweep that fed it, [B/R groups][T][2][H/16] u32.
 __device__ float* g_xg_dbg_dh;
 __device__ unsigned* g_xg_dbg_spins;
+// ... and per cell and step [B][T][2][H][12] f32: the four gate gradients it
+// computed, the four gate activations it used, c_t, c_{t-1}, dy and the
+// incoming dc carry.
+__device__ float* g_xg_dbg_cell;
 #define XG_TR_WG 64
 #define XG_TR_STEPS 128
 #define XG_TR_K 8
@@ -929,6 +933,7 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
     const int len = own ? lens[b] : 0;
     float dc = 0.f;
     float* ddh = g_xg_dbg_dh;
+    float* dcl = g_xg_dbg_cell;
     // c_t of step q is c_{tp} of step q - 1: with `carry` it is taken from there
     auto load_cell = [&](int q, float (&av)[4], h16x4& avh, float& cc, float& cp, float& dyv,
                          const float* carry) {
@@ -1018,6 +1023,12 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
         d_f = dcell * cp * fg * omf;
         d_g = dcell * ig * omg2;
         d_o = dh * tc * og * omo;
+        if (dcl) {
+          float* o = dcl + ((((long long)b * T + t) * 2 + dir) * H + j) * 12;
+          o[0] = d_i; o[1] = d_f; o[2] = d_g; o[3] = d_o;
+          o[4] = ig; o[5] = fg; o[6] = gg; o[7] = og;
+          o[8] = cc; o[9] = cp; o[10] = dyv; o[11] = dc;
+        }
         dc = dcell * fg;
         sb_i += d_i;
         sb_f += d_f;
@@ -1452,9 +1463,11 @@ extern "C" long long asr_xg_trace_read(unsigned long long* host) {
 // Diagnostics: the backward recurrence's dh / spin-count recorders (NULL: off).
 // Stream-ordered: launches enqueued after this call on `stream` record into the
 // given buffers ([B][T][2][H] f32; [ceil(B/R)][T][2][H/16] u32).
-extern "C" int asr_lstm_debug_dh(float* dh, unsigned* spins, void* stream) {
+extern "C" int asr_lstm_debug_dh(float* dh, unsigned* spins, float* cell, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (hipMemcpyToSymbolAsync(HIP_SYMBOL(asr::g_xg_dbg_dh), &dh, sizeof(dh), 0,
+                             hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyToSymbolAsync(HIP_SYMBOL(asr::g_xg_dbg_cell), &cell, sizeof(cell), 0,
                              hipMemcpyHostToDevice, s) != hipSuccess ||
       hipMemcpyToSymbolAsync(HIP_SYMBOL(asr::g_xg_dbg_spins), &spins, sizeof(spins), 0,
                              hipMemcpyHostToDevice, s) != hipSuccess)

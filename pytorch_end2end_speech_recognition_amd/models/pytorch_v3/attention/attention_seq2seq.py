@@ -23,7 +23,7 @@ import numpy as np
 import torch
 
 from .... import native_ops as ops
-from ..base import ModelBase, check_recurrences
+from ..base import ModelBase, check_recurrences, eval_retry
 from ..linear import LinearND, Embedding, Embedding_LS
 from ..encoders.load_encoder import load
 from .rnn_decoder import RNNDecoder
@@ -197,6 +197,7 @@ class AttentionSeq2seq(ModelBase):
         self.encoder.__dict__['_owner'] = self
 
     # ------------------------------------------------------------------
+    @eval_retry
     def forward(self, xs, ys, x_lens, y_lens, is_eval=False):
         """attention_seq2seq.py:422-562."""
         if is_eval:
@@ -472,6 +473,7 @@ class AttentionSeq2seq(ModelBase):
         logits = fc(z)
         return logits, aw
 
+    @eval_retry
     @torch.no_grad()
     def decode_ctc(self, xs, x_lens, beam_width=1, task_index=0):
         """:1239-1289 (greedy; HIP best path)."""
@@ -486,6 +488,7 @@ class AttentionSeq2seq(ModelBase):
         best = np.array([h - 1 for h in hyps] + [None], dtype=object)[:-1]
         return best, self.encoder.last_perm_np.copy()
 
+    @eval_retry
     @torch.no_grad()
     def decode(self, xs, x_lens, beam_width, max_decode_len, min_decode_len=0,
                length_penalty=0, coverage_penalty=0, task_index=0, resolving_unk=False):

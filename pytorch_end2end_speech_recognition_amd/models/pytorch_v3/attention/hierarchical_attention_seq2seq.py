@@ -24,7 +24,7 @@ the HIP CTC kernel.
 import numpy as np
 
 from .attention_seq2seq import AttentionSeq2seq
-from ..base import check_recurrences
+from ..base import check_recurrences, eval_retry
 from .attention_layer import AttentionMechanism
 from .rnn_decoder import RNNDecoder
 from ..encoders.load_encoder import load
@@ -169,6 +169,7 @@ class HierarchicalAttentionSeq2seq(AttentionSeq2seq):
         self.flatten_parameters_()
         self.encoder.__dict__['_owner'] = self
 
+    @eval_retry
     def forward(self, xs, ys, x_lens, y_lens, ys_sub, y_lens_sub, is_eval=False):
         """:382-567."""
         if is_eval:
@@ -222,6 +223,7 @@ class HierarchicalAttentionSeq2seq(AttentionSeq2seq):
             self._ss_prob = min(self.ss_prob, self.ss_prob / self.ss_max_step * self._step)
         return loss, loss_main, second
 
+    @eval_retry
     def decode(self, xs, x_lens, beam_width, max_decode_len, min_decode_len=0,
                length_penalty=0, coverage_penalty=0, task_index=0, **kwargs):
         """:569-648 (greedy or beam search; the joint word/char decodings

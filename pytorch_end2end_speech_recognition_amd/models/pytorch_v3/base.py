@@ -39,6 +39,28 @@ def resolve_pending_losses(model):
         pend.value()
 
 
+def eval_retry(fn):
+    """Eval / decode entry points (the is_eval forward the reference's training
+    scripts call for the dev loss every print_step, decode, posteriors): when a
+    persistent recurrence gives up its bounded wait during the pass
+    (check_recurrences raises RecurrenceGaveUp), the pass -- side-effect free:
+    BatchNorm on its running statistics, no dropout, no optimizer state -- runs
+    once more with a warning; a second give-up raises.  A training forward
+    never raises it (its give-ups are handled by the step's device guard), so
+    the wrapper changes nothing there."""
+    import functools
+
+    @functools.wraps(fn)
+    def wrapper(self, *args, **kwargs):
+        from ...native_ops import RecurrenceGaveUp
+        try:
+            return fn(self, *args, **kwargs)
+        except RecurrenceGaveUp as e:
+            logger.warning('%s: %s; running the pass once more', fn.__name__, e)
+        return fn(self, *args, **kwargs)
+    return wrapper
+
+
 def check_recurrences(model):
     """Eval / decode entry points: a persistent recurrence that gave up its
     bounded wait during this pass left invalid outputs -- raise instead of

@@ -17,7 +17,7 @@ import numpy as np
 import torch
 
 from .... import native_ops as ops
-from ..base import ModelBase, check_recurrences
+from ..base import ModelBase, check_recurrences, eval_retry
 from ..linear import LinearND
 from ..encoders.load_encoder import load
 from ..criterion import cross_entropy_label_smoothing
@@ -109,6 +109,7 @@ class CTC(ModelBase):
         self.encoder.__dict__['_owner'] = self
 
     # ------------------------------------------------------------------
+    @eval_retry
     def forward(self, xs, ys, x_lens, y_lens, is_eval=False):
         """ctc.py:272-342."""
         if is_eval:
@@ -190,6 +191,7 @@ class CTC(ModelBase):
         with torch.no_grad():
             self._flat_param.add_(torch.randn_like(self._flat_param) * std + mean)
 
+    @eval_retry
     @torch.no_grad()
     def decode(self, xs, x_lens, beam_width, max_decode_len=None, min_decode_len=0,
                length_penalty=0, coverage_penalty=0, task_index=0):
@@ -206,6 +208,7 @@ class CTC(ModelBase):
         best_hyps = np.array([h - 1 for h in best_hyps] + [None], dtype=object)[:-1]
         return best_hyps, None, self.encoder.last_perm_np.copy()
 
+    @eval_retry
     @torch.no_grad()
     def posteriors(self, xs, x_lens, temperature=1, blank_scale=None, task_idx=0):
         """ctc.py:455-502."""

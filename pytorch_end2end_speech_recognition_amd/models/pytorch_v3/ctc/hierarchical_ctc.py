@@ -15,7 +15,7 @@ returns (loss, loss_main, loss_sub) with
 import numpy as np
 
 from .ctc import CTC
-from ..base import check_recurrences
+from ..base import check_recurrences, eval_retry
 from ..linear import LinearND
 from ..encoders.load_encoder import load
 
@@ -95,6 +95,7 @@ class HierarchicalCTC(CTC):
         self.flatten_parameters_()
         self.encoder.__dict__['_owner'] = self
 
+    @eval_retry
     def forward(self, xs, ys, x_lens, y_lens, ys_sub, y_lens_sub, is_eval=False):
         """hierarchical_ctc.py:267-365."""
         if is_eval:

@@ -61,14 +61,19 @@ def recurrence_status(device):
     return st
 
 
+class RecurrenceGaveUp(N.NativeError):
+    """A persistent recurrence gave up a bounded wait: that pass's outputs are
+    invalid (the pass itself can be run again)."""
+
+
 def raise_if_recurrence_failed(device=None):
-    """Host check (synchronises): NativeError when a persistent recurrence
+    """Host check (synchronises): RecurrenceGaveUp when a persistent recurrence
     gave up since the last gather (its outputs are invalid)."""
     device = device or torch.device('cuda', torch.cuda.current_device())
     st = recurrence_status(device)
     if int(st.max().item()):
-        raise N.NativeError('persistent LSTM recurrence gave up a bounded wait (status %s): '
-                            'outputs of this pass are invalid' % st.tolist())
+        raise RecurrenceGaveUp('persistent LSTM recurrence gave up a bounded wait (status %s): '
+                               'outputs of this pass are invalid' % st.tolist())
 
 
 def grad_buffer(p):
@@ -1648,11 +1653,26 @@ def _zero_halo(buf, B, T, F, C):
            int(T), int(F), int(C), N.stream_handle(buf.device))
 
 
-def _conv_tr_ok(cin, cout, fp):
+_TWO_GIB = 1 << 31
+
+
+def _conv_tr_ok(cin, cout, fp, P, out_bytes):
     """bf16 mode: the tap-resident convolution kernel (csrc/conv.hip) takes this
-    channel pair (ASR_VGG_TR=0 keeps the tap-addressed GEMM, for A/B)."""
+    channel pair and operand sizes -- every operand below 2 GiB, the kernel's
+    buffer-resource limit (ASR_VGG_TR=0 keeps the tap-addressed GEMM, for A/B)."""
     return (compute_dtype() == BF16 and os.environ.get('ASR_VGG_TR', '1') != '0' and
+            P * cin * 2 < _TWO_GIB and P * cout * out_bytes < _TWO_GIB and
             N.query('asr_conv3x3_tr_supported', int(cin), int(cout), int(fp)) == 1)
+
+
+def _c1_wgrad_ok(B, T, F, co):
+    """The first layer's weight gradient from the raw features
+    (asr_conv3x3_c1_wgrad_xs) takes this shape: 64 output channels, the bf16 dz
+    operand below 2 GiB and the LDS tile of one frequency row (F) within 64 KB;
+    decided in the forward, which then skips the padded operand."""
+    P = B * (T + 2) * (F + 2)
+    lds = 256 * co * 2 + (256 + 2 * (F + 3)) * 4
+    return co == 64 and P * co * 2 < _TWO_GIB and lds <= 64 * 1024
 
 
 def conv3x3_tr(inp, P, cin, fp, sign, w, cout, bias, out):
@@ -1668,6 +1688,8 @@ def conv3x3_tr_wgrad(x, dz, P, cin, fp, cout, packed):
     """packed[n][tap cin + c] = sum_p dz[p][n] x[p + shift(tap)][c] on the
     tap-resident weight-gradient kernel; False when the shape does not take it."""
     if compute_dtype() != BF16 or os.environ.get('ASR_VGG_TR', '1') == '0':
+        return False
+    if P * cin * 2 >= _TWO_GIB or P * cout * 2 >= _TWO_GIB:   # the kernel's buffer limit
         return False
     nb = N.query('asr_conv3x3_tr_wgrad_workspace_bytes', int(P), int(cin), int(cout), int(fp))
     if not nb:
@@ -1707,7 +1729,7 @@ class VGGFn(torch.autograd.Function):
         # (asr_conv3x3_c1_wgrad_xs) both read the raw features, so the padded
         # 16-channel operand is never built
         co0 = specs[0]['w'].shape[0]
-        c1w = (cd == BF16 and use_gemm[0] and co0 == 64 and
+        c1w = (cd == BF16 and use_gemm[0] and _c1_wgrad_ok(B, T, F, co0) and
                os.environ.get('ASR_VGG_C1_DIRECT', '1') != '0' and
                os.environ.get('ASR_VGG_C1_XS', '1') != '0' and
                os.environ.get('ASR_VGG_C1_WGRAD', '1') != '0')
@@ -1756,7 +1778,7 @@ class VGGFn(torch.autograd.Function):
                                                                  device=dev)
                 N.call('asr_conv_weight_pack_pad', N.ptr(w), Co, cC, cCp, 0, cd, N.ptr(wg),
                        N.stream_handle(dev))
-                if _conv_tr_ok(cCp, Co, cF + 2):
+                if _conv_tr_ok(cCp, Co, cF + 2, npad, z.element_size()):
                     # the input rows stay in an LDS ring across the nine taps
                     conv3x3_tr(x_op, npad, cCp, cF + 2, 1, wg, Co, sp['b'], z)
                 else:
@@ -1910,7 +1932,7 @@ class VGGFn(torch.autograd.Function):
                      os.environ.get('ASR_VGG_DX_BF16', '1') != '0')
             dx = torch.empty(npad, cC, dtype=torch.bfloat16 if dx_bf else torch.float32,
                              device=dev)
-            if _conv_tr_ok(Co, cC, cF + 2):
+            if _conv_tr_ok(Co, cC, cF + 2, npad, dx.element_size()):
                 conv3x3_tr(dz, npad, Co, cF + 2, -1, wt, cC, None, dx)
             else:
                 run_gemm([gemm_problem(_tap_operand(dz, 0, Co, Co, cF + 2, -1),

@@ -230,7 +230,46 @@ def _bf16_exact(t):
     return t.to(torch.bfloat16).to(t.dtype)
 
 
-def _vgg_bf16_case(batch_norm, representable=False):
+def _vgg_node(t):
+    """The VGGFn node of t's autograd graph (its ctx: saved tensors, layers)."""
+    seen, todo = set(), [t.grad_fn]
+    while todo:
+        n = todo.pop()
+        if n is None or n in seen:
+            continue
+        seen.add(n)
+        if type(n).__name__.startswith('VGGFn'):
+            return n
+        todo.extend(f for f, _ in n.next_functions)
+    raise AssertionError('no VGGFn node in the graph')
+
+
+def _gpu_vgg_decisions(node):
+    """The GPU forward's ReLU masks (z > 0 of the stored conv output) and
+    max-pool argmax slots (csrc/cnn.hip post_fwd: slot = df * pt + dt) in the
+    oracle's NCHW layout (H = frequency, W = time): asr_ref.vgg_front's
+    `decisions` argument."""
+    saved = node.saved_tensors
+    out = []
+    B = node.B
+    for l, (cT, cF, cC, cCp, Co, pt, pf, ceil, drop, seed, gemm) in enumerate(node.layers):
+        z, slot = saved[6 * l + 1], saved[6 * l + 3]
+        zi = z.float().view(B, cT + 2, cF + 2, Co)[:, 1:-1, 1:-1, :]
+        mask = (zi > 0).permute(0, 3, 2, 1).cpu()                       # [B, C, F, T]
+        ind = None
+        if pt:
+            from pytorch_end2end_speech_recognition_amd.native_ops import _pool_dims
+            To, Fo = _pool_dims(cT, cF, pt, pf, ceil)
+            sl = slot.view(B, To, Fo, Co).long().cpu()
+            df, dt = sl // pt, sl % pt
+            f = torch.arange(Fo).view(1, 1, Fo, 1) * pf + df
+            t = torch.arange(To).view(1, To, 1, 1) * pt + dt
+            ind = (f * cT + t).permute(0, 3, 2, 1).contiguous()          # [B, C, F', T']
+        out.append((mask, ind))
+    return out
+
+
+def _vgg_bf16_case(batch_norm, representable=False, replay=False):
     kw = dict(VGG_PROD, input_size=40, batch_norm=batch_norm)
     model = _ctc(kw)
     if representable:
@@ -256,14 +295,28 @@ def _vgg_bf16_case(batch_norm, representable=False):
     for b in range(B):
         ys[b, :y_lens[b]] = rng.randint(0, 6, y_lens[b])
     batch = (xs, ys, x_lens, y_lens)
-    ref_loss, ref_g = _oracle(sd, _vgg_cfg(kw), batch, torch.float64)
     model.set_cuda()
-    loss, g = _gpu_grads(model, batch, 'bf16')
+    from pytorch_end2end_speech_recognition_amd import native_ops
+    native_ops.set_compute_dtype('bf16')
+    try:
+        model.zero_grad()
+        loss_t = model(*batch)
+        dec = _gpu_vgg_decisions(_vgg_node(loss_t)) if replay else None
+        loss_t.backward()
+        torch.cuda.synchronize()
+    finally:
+        native_ops.set_compute_dtype('fp32')
+    loss = float(loss_t.item())
+    g = {k: p.grad.detach().cpu().numpy().copy() for k, p in model.named_parameters()}
+    cfg = _vgg_cfg(kw)
+    if replay:
+        cfg['vgg_decisions'] = dec
+    ref_loss, ref_g = _oracle(sd, cfg, batch, torch.float64)
     errs = {k: _rel_l2(g[k], ga) for k, ga in ref_g.items()}
     worst = sorted(errs.items(), key=lambda kv: -kv[1])[:6]
     lerr = abs(loss - ref_loss) / abs(ref_loss)
-    print('\nbf16 VGG (batch_norm=%s) vs float64: loss %.2e, worst grads %s' % (
-        batch_norm, lerr, ', '.join('%s %.2e' % kv for kv in worst)))
+    print('\nbf16 VGG (batch_norm=%s, decisions replayed: %s) vs float64: loss %.2e, worst '
+          'grads %s' % (batch_norm, replay, lerr, ', '.join('%s %.2e' % kv for kv in worst)))
     return lerr, errs
 
 
@@ -282,21 +335,39 @@ def test_vgg_bf16_vs_float64(cuda_dev):
     test_vgg_bf16_bn_vs_float64) -- a property of bf16 operands, not of a
     kernel: the same kernels in fp32 mode meet 2e-3 with BN
     (test_vgg_prod_channels_fp32_vs_oracle)."""
-    lerr, errs = _vgg_bf16_case(False, representable=True)
+    lerr, errs = _vgg_bf16_case(False, representable=True, replay=True)
     assert lerr <= 1e-3
     for k, e in errs.items():
-        # the convolution weight / bias gradients are pixel sums of bf16 dZ
-        # (the GEMM operand) that cancel to a few % of their terms' scale at
-        # random init: measured 1-5 % there, <= 1e-2 everywhere else
-        assert e <= (0.1 if k.startswith('encoder.conv') else 1e-2), (k, e)
+        # with the ReLU / max-pool decisions replayed (test_vgg_bf16_bn_vs_float64)
+        assert e <= 2e-2, (k, e)
 
 
 @pytest.mark.gpu
 def test_vgg_bf16_bn_vs_float64(cuda_dev):
-    """The production config WITH training-mode BatchNorm in bf16: loss within
-    1e-3 of float64 and every gradient within 0.25 relative L2 (measured
-    0.08-0.13 on the BN-cancelled sums below the last BN layer; the
-    BLSTM / CTC head gradients stay near 1e-3)."""
+    """The production config WITH training-mode BatchNorm in bf16 (the vgg_hier
+    bench path), against float64 with the GPU forward's ReLU and max-pool
+    decisions replayed: loss within 1e-3 and EVERY gradient within 2e-2
+    relative L2.  Why the replay: a bf16 forward rounds the conv outputs by
+    2^-9, which flips the argmax of near-tied max-pool windows and the sign of
+    near-zero ReLU inputs; each flip routes that pixel's gradient elsewhere, and
+    below a training-mode BatchNorm (whose backward leaves a few-% residue of
+    the incoming gradient) those reroutings are 10-15 % of the conv / BN
+    gradients.  tools/vgg_bf16_emul.py measures it in float64 on the CPU: bf16
+    rounding at any single forward point moves the gradients by 4-17 %,
+    float32 rounding by 1e-7, and with the decisions held fixed the full bf16
+    path (forward operands, z, dz, dx, upstream dy) stays <= 1.2e-2 -- the
+    flips, not the kernels' arithmetic or the bf16 dZ storage.  The
+    un-replayed comparison is kept in test_vgg_bf16_bn_flips_vs_float64."""
+    lerr, errs = _vgg_bf16_case(True, replay=True)
+    assert lerr <= 1e-3
+    for k, e in errs.items():
+        assert e <= 2e-2, (k, e)
+
+
+@pytest.mark.gpu
+def test_vgg_bf16_bn_flips_vs_float64(cuda_dev):
+    """The same without the replay: every gradient within 0.25 relative L2
+    (the decision flips above; measured 0.08-0.15)."""
     lerr, errs = _vgg_bf16_case(True)
     assert lerr <= 1e-3
     for k, e in errs.items():

@@ -98,7 +98,11 @@ def test_failed_backward_with_pending_side_wgrads_then_clean_step(cuda_dev, monk
 
 
 @pytest.mark.gpu
-def test_eval_and_decode_raise_on_recurrence_give_up(cuda_dev):
+def test_eval_and_decode_retry_then_raise_on_recurrence_give_up(cuda_dev):
+    """The dev-loss eval (the reference's training scripts call
+    model(..., is_eval=True) every print_step) and decode: one give-up during
+    the pass re-runs it (same value as a healthy pass, a warning); a give-up on
+    the re-run too raises RecurrenceGaveUp (a NativeError)."""
     from pytorch_end2end_speech_recognition_amd import _native as N
     from pytorch_end2end_speech_recognition_amd import native_ops
     from pytorch_end2end_speech_recognition_amd.utils.training.training_loop import train_step
@@ -113,13 +117,28 @@ def test_eval_and_decode_raise_on_recurrence_give_up(cuda_dev):
         # healthy eval: no error
         v = m(batch['xs'], batch['ys'], batch['x_lens'], batch['y_lens'], is_eval=True)
         assert np.isfinite(v)
-        # a give-up during the eval pass (the status word a bounded spin sets)
+        h0 = m.decode(batch['xs'], batch['x_lens'], beam_width=1)[0]
+        # one give-up during the eval pass (the status word a bounded spin
+        # sets): retried, the same loss
         N.call('asr_lstm_status_inject', 1, N.stream_handle(cuda_dev))
-        with pytest.raises(N.NativeError):
-            m(batch['xs'], batch['ys'], batch['x_lens'], batch['y_lens'], is_eval=True)
+        assert m(batch['xs'], batch['ys'], batch['x_lens'], batch['y_lens'], is_eval=True) == v
         N.call('asr_lstm_status_inject', 1, N.stream_handle(cuda_dev))
-        with pytest.raises(N.NativeError):
-            m.decode(batch['xs'], batch['x_lens'], beam_width=1)
+        h1 = m.decode(batch['xs'], batch['x_lens'], beam_width=1)[0]
+        assert all(np.array_equal(a, b) for a, b in zip(h0, h1))
+        # a give-up in every pass: raises after the one retry
+        enc = m._encode
+
+        def failing(*a, **k):
+            N.call('asr_lstm_status_inject', 1, N.stream_handle(cuda_dev))
+            return enc(*a, **k)
+        m._encode = failing
+        try:
+            with pytest.raises(native_ops.RecurrenceGaveUp):
+                m(batch['xs'], batch['ys'], batch['x_lens'], batch['y_lens'], is_eval=True)
+            with pytest.raises(N.NativeError):
+                m.decode(batch['xs'], batch['x_lens'], beam_width=1)
+        finally:
+            del m._encode
         # the words were consumed: the next train_step trains
         m, lv = train_step(m, batch, clip_grad_norm=5.0)
         assert lv > 0 and m.optimizer._step == 1

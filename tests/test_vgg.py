@@ -221,3 +221,36 @@ def test_tap_gemm_conv_exact(fast, n64st, Ci, Co, cuda_dev, monkeypatch):
         np.testing.assert_array_equal(dw.cpu().double().numpy(), dw_ref.numpy())
     finally:
         ops.set_compute_dtype('fp32')
+
+
+def test_oracle_vgg_decision_replay_is_exact():
+    """asr_ref.vgg_front's `decisions` (the bf16 pins replay the GPU's ReLU /
+    max-pool choices): replaying the oracle's own choices reproduces its
+    output and gradients exactly (float64), ceil-mode windows included."""
+    import torch
+    from oracle import asr_ref
+    torch.manual_seed(3)
+    cfg = dict(conv_channels=[4, 6, 8], poolings=[[], [2, 2], [2, 2]], batch_norm=True)
+    p = {}
+    cin, idx = 1, 0
+    for l, C in enumerate(cfg['conv_channels']):
+        p['conv.layers.%d.weight' % idx] = torch.randn(C, cin, 3, 3, dtype=torch.float64) * 0.3
+        p['conv.layers.%d.bias' % idx] = torch.randn(C, dtype=torch.float64) * 0.1
+        idx += 2 + (1 if cfg['poolings'][l] else 0)
+        p['conv.layers.%d.weight' % idx] = 1 + 0.1 * torch.randn(C, dtype=torch.float64)
+        p['conv.layers.%d.bias' % idx] = 0.1 * torch.randn(C, dtype=torch.float64)
+        p['conv.layers.%d.running_mean' % idx] = torch.zeros(C, dtype=torch.float64)
+        p['conv.layers.%d.running_var' % idx] = torch.ones(C, dtype=torch.float64)
+        idx += 2
+        cin = C
+    xs = torch.randn(2, 13, 9, dtype=torch.float64)          # odd T, F: ceil windows
+    dec = asr_ref.vgg_decisions(p, '', cfg, xs)
+    outs = []
+    for d in (None, dec):
+        q = {k: v.clone().requires_grad_('running' not in k) for k, v in p.items()}
+        out, _, _ = asr_ref.vgg_front(q, '', cfg, xs, [13, 11], decisions=d)
+        (out * torch.linspace(-1, 1, out.numel(), dtype=torch.float64).view(out.shape)).sum().backward()
+        outs.append((out.detach(), {k: v.grad for k, v in q.items() if v.grad is not None}))
+    assert torch.equal(outs[0][0], outs[1][0])
+    for k in outs[0][1]:
+        assert torch.equal(outs[0][1][k], outs[1][1][k]), k

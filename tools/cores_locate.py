@@ -118,11 +118,15 @@ def run_once(sd, batch, env, side=None):
             Hh = dy.shape[2] // 2
             dh = torch.full((Bb, Tt, 2, Hh), float('nan'), device=dev)
             sp = torch.zeros(((Bb + 7) // 8, Tt, 2, Hh // 16), dtype=torch.int32, device=dev)
-            N.call('asr_lstm_debug_dh', N.ptr(dh), N.ptr(sp), N.stream_handle(dev))
-            dhs.append((dh, sp))
+            cl = (torch.full((Bb, Tt, 2, Hh, 12), float('nan'), device=dev)
+                  if os.environ.get('DIAG_CELL') == '1' else None)
+            N.call('asr_lstm_debug_dh', N.ptr(dh), N.ptr(sp), N.ptr(cl), N.stream_handle(dev))
+            saved = ctx.saved_tensors      # x_op, w_op, lens, w_hh, b_ih, b_hh, act, cst, y_op
+            dhs.append((dh, sp, cl, saved[6].detach().clone(), saved[7].detach().clone(),
+                        dy.detach().clone(), saved[2].detach().clone()))
         out = orig_bwd(ctx, dy)
         if DH:
-            N.call('asr_lstm_debug_dh', None, None, N.stream_handle(dev))
+            N.call('asr_lstm_debug_dh', None, None, None, N.stream_handle(dev))
         dxs.append(out[0].detach().clone() if out[0] is not None else None)
         return out
 
@@ -207,8 +211,133 @@ def first_diffs(ref, got, Tn, kind):
     return out, idx
 
 
+def report_cell(i, ref, got, dg_ref, dg_got, Tn):
+    """The first step where the cell's recorded values differ: its computed
+    gate gradients, the inputs it used, or only the stored bf16 dG."""
+    cr, cg = ref[2], got[2]
+    same = (cr == cg) | (torch.isnan(cr) & torch.isnan(cg))
+    names = ['d_i', 'd_f', 'd_g', 'd_o', 'ig', 'fg', 'gg', 'og', 'c', 'cp', 'dy', 'dc']
+    Bb = cr.shape[0]
+    dgr = dg_ref.float().view(Bb, Tn, 2, 4, H).permute(0, 1, 2, 4, 3)
+    dgg = dg_got.float().view(Bb, Tn, 2, 4, H).permute(0, 1, 2, 4, 3)
+    stored = (dgr != dgg).any(-1)                                   # [B, T, 2, H]
+    for dd in (0, 1):
+        qs = []
+        for what, m in (('cell record', ~same[:, :, dd].all(-1)), ('stored dG', stored[:, :, dd])):
+            idx = m.nonzero()
+            if idx.numel():
+                q = torch.where(torch.tensor(dd == 0), Tn - 1 - idx[:, 1], idx[:, 1])
+                qq = int(q.min())
+                sel = idx[q == qq]
+                qs.append('%s first at step %d (rows %s units %s)' % (
+                    what, qq, sorted(set(sel[:, 0].tolist()))[:4], sorted(set(sel[:, 2].tolist()))[:6]))
+                if what == 'cell record':
+                    b0, t0, j0 = [int(v) for v in sel[0]]
+                    fields = [names[k] for k in range(12)
+                              if not bool(same[b0, t0, dd, j0, k])]
+                    qs.append('   fields differing there: %s  ref %s  got %s' % (
+                        fields, [round(float(v), 7) for v in cr[b0, t0, dd, j0]],
+                        [round(float(v), 7) for v in cg[b0, t0, dd, j0]]))
+        print('   call %d dir%d: %s' % (i, dd, ' | '.join(qs) if qs else 'equal'), flush=True)
+
+
+def _dec_sig(e):
+    neg = torch.signbit(e)
+    return torch.where(neg, 1 + e, e), torch.where(neg, -e, 1 - e)
+
+
+def _dec_tanh(e):
+    a = e.abs()
+    c = a / 16384.0
+    cm = a >= 0.5
+    return torch.where(cm, torch.copysign(1 - c, e), e), torch.where(cm, c * (2 - c), 1 - e * e)
+
+
+def replay_cells(i, rec, dg_stored, Tn, tag):
+    """Recompute every cell's gate gradients from the recorded dh_t (what the
+    recurrence summed), the saved activations / c / dy and the dc carry, in
+    f32 on the device, and compare with the stored bf16 dG: where the kernel's
+    stored value departs from this recomputation while dh agrees, the cell
+    math or its inputs went wrong.  For the first such cell, test which
+    neighbouring inputs (other time steps / rows) explain the stored value."""
+    dh, _, _, act, cst, dy, lens = rec
+    Bb = dh.shape[0]
+    Hh = dh.shape[3]
+    a = act.float().view(Bb, Tn, 2, Hh, 4)
+    ig, omi = _dec_sig(a[..., 0])
+    fg, omf = _dec_sig(a[..., 1])
+    gg, omg = _dec_tanh(a[..., 2])
+    og, omo = _dec_sig(a[..., 3])
+    c = cst.view(Bb, Tn, 2, Hh)
+    dgs = dg_stored.float().view(Bb, Tn, 2, 4, Hh).permute(0, 1, 2, 4, 3)     # [B,T,2,H,4]
+    L = lens.long().view(Bb, 1)
+    worst = []
+    for dd in (0, 1):
+        dc = torch.zeros(Bb, Hh, device=dh.device)
+        for q in range(Tn):
+            t = Tn - 1 - q if dd == 0 else q
+            tp = t - 1 if dd == 0 else t + 1
+            act_m = (t < L).float()
+            h = dh[:, t, dd]
+            h = torch.nan_to_num(h)
+            cc = c[:, t, dd]
+            cp = c[:, tp, dd] if 0 <= tp < Tn else torch.zeros_like(cc)
+            tc = torch.tanh(cc)
+            dcell = dc + h * og[:, t, dd] * (1 - tc * tc)
+            d = torch.stack([dcell * gg[:, t, dd] * ig[:, t, dd] * omi[:, t, dd],
+                             dcell * cp * fg[:, t, dd] * omf[:, t, dd],
+                             dcell * ig[:, t, dd] * omg[:, t, dd],
+                             h * tc * og[:, t, dd] * omo[:, t, dd]], -1) * act_m.unsqueeze(-1)
+            dc = dcell * fg[:, t, dd] * act_m
+            st = dgs[:, t, dd]
+            err = (st - d).abs() / (d.abs() + 1e-3 * d.abs().max() + 1e-30)
+            m = float(err.max())
+            if m > 0.05:
+                k = int(err.argmax())
+                b0, j0, g0 = k // (Hh * 4), (k // 4) % Hh, k % 4
+                worst.append((q, dd, b0, j0, g0, m, float(st[b0, j0, g0]), float(d[b0, j0, g0])))
+                # which substituted input explains the stored value?  (dc and
+                # dh as recomputed / recorded; activations and c from another
+                # frame or row)
+                expl = []
+                hh = float(h[b0, j0])
+                dcv = float((dcell - h * og[:, t, dd] * (1 - tc * tc))[b0, j0])
+                for tb in range(max(0, t - 3), min(Tn, t + 4)):
+                    for bb in sorted(set([b0, b0 ^ 1, b0 ^ 2, b0 ^ 4, (b0 + 8) % Bb, (b0 - 8) % Bb])):
+                        for jj in sorted(set([j0, j0 ^ 1, j0 ^ 8])):
+                            for what in ('act', 'c', 'act+c'):
+                                A = (bb, tb, dd, jj) if 'act' in what else (b0, t, dd, j0)
+                                Cc = (bb, tb, dd, jj) if 'c' in what else (b0, t, dd, j0)
+                                if A == (b0, t, dd, j0) and Cc == (b0, t, dd, j0):
+                                    continue
+                                i_, f_, g_, o_ = ig[A], fg[A], gg[A], og[A]
+                                oi, of_, og2, oo = omi[A], omf[A], omg[A], omo[A]
+                                cc_ = c[Cc]
+                                tp_ = Cc[1] - 1 if dd == 0 else Cc[1] + 1
+                                cp_ = c[Cc[0], tp_, dd, Cc[3]] if 0 <= tp_ < Tn else 0.0
+                                tc_ = torch.tanh(cc_)
+                                dcl = dcv + hh * o_ * (1 - tc_ * tc_)
+                                dv = [dcl * g_ * i_ * oi, dcl * cp_ * f_ * of_, dcl * i_ * og2,
+                                      hh * tc_ * o_ * oo]
+                                e_ = max(abs(float(st[b0, j0, k_]) - float(dv[k_])) /
+                                         (abs(float(dv[k_])) + 1e-8) for k_ in range(4))
+                                if e_ < 1e-2:
+                                    expl.append('%s from (row %d, t %d, unit %d)' % (what, bb, tb, jj))
+                print('      stored %s recomputed %s dh %.6e dc %.6e; explained by: %s' % (
+                    [round(float(v), 8) for v in st[b0, j0]], [round(float(v), 8) for v in d[b0, j0]],
+                    hh, dcv, expl[:6] or 'nothing tried'), flush=True)
+                break
+    for w in worst:
+        print('   call %d %s: first cell whose stored dG departs from the recomputation: step %d dir%d '
+              'row %d unit %d gate %d rel %.2e stored %.6e recomputed %.6e' % ((i, tag) + w), flush=True)
+    if not worst:
+        print('   call %d %s: every stored dG matches the recomputation from the recorded dh' % (i, tag),
+              flush=True)
+
+
 def report_dh(i, ref, got, Tn):
-    (dref, sref), (dgot, sgot) = ref, got
+    dref, sref = ref[0], ref[1]
+    dgot, sgot = got[0], got[1]
     fd, _ = first_diffs(dref, dgot, Tn, 'dh')
     if not fd:
         print('   call %d dh: equal' % i, flush=True)
@@ -252,8 +381,13 @@ def main():
                 print('   call %d dG: %s' % (i, locate(r, g, B, T)), flush=True)
                 if DH and i < len(dhs):
                     report_dh(i, ref[3][i], dhs[i], T)
+                    if i == 1 and dhs[i][2] is not None:
+                        report_cell(i, ref[3][i], dhs[i], r, g, T)
+                    if i == 1:
+                        replay_cells(i, dhs[i], g, T, tag='got')
+                        replay_cells(i, ref[3][i], r, T, tag='ref')
                     fg, _ = first_diffs(r, g, T, 'dG')
-                    fh, _ = first_diffs(ref[3][i][0], dhs[i][0], T, 'dh')
+                    fh, _ = first_diffs(ref[3][i][0], dhs[i][0], T, 'dh')  # noqa
                     order = {k: ('dh first' if k in fh and fh[k][0] <= v[0] else 'dG first (dh equal so far)')
                              for k, v in fg.items()}
                     if order:
