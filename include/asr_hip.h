@@ -44,7 +44,8 @@ extern "C" {
 /* ---------------------------------------------------------------- info */
 const char* asr_version(void);
 const char* asr_last_error(void);
-/* Number of gfx950 code objects linked in (sanity check for loaders). */
+/* 1 when the current device is a gfx950 (the only code-object target of the
+ * library), 0 for another device, -1 when no device can be queried. */
 int asr_arch_is_gfx950(void);
 
 /* A HIP stream restricted to CUs [cu_begin, cu_begin + cu_count) of the
@@ -807,6 +808,11 @@ int asr_lstm_xg_mode(int* mode, int clear);
  * per-step phase timestamps of work-groups 0..3 (4 x 128 steps x 6 u64) to
  * `host` (may be NULL); returns the element count, 0 when tracing is off. */
 long long asr_xg_trace_read(unsigned long long* host);
+/* The persistent backward recurrence's dynamic-LDS pin (KB, in (80, 160]; 0 =
+ * ASR_XG_PIN_BWD_KB or the 140 KB default) for the launches that follow.  At
+ * the default no kernel with more than 9 KB of LDS -- every GEMM and
+ * convolution kernel -- can be co-resident with it. */
+int asr_lstm_set_bwd_pin_kb(int kb);
 /* Diagnostics only (tools/cores_locate.py): backward recurrence launches
  * enqueued on `stream` after this call record every dh_t their cell waves form
  * into dh ([B][T][2][H] f32), each step's sweep spin count into spins

@@ -201,6 +201,7 @@ SIGNATURES = {
     'asr_lstm_xg_mode': (c_int, [c_vp, c_int]),
     'asr_xg_trace_read': (c_ll, [c_vp]),
     'asr_lstm_debug_dh': (c_int, [c_vp, c_vp, c_vp, c_vp]),
+    'asr_lstm_set_bwd_pin_kb': (c_int, [c_int]),
 }
 
 
@@ -305,7 +306,17 @@ def stream_handle(device=None):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
+_arch_ok = []
+
+
 def require_device(*tensors):
     for t in tensors:
         if t is not None and not t.is_cuda:
             raise NativeError('HIP op called with a CPU tensor (no CPU fallback by design)')
+    if not _arch_ok:
+        # the code objects are gfx950 only: say so instead of failing to launch
+        a = lib().asr_arch_is_gfx950()
+        if a != 1:
+            raise NativeError('libasr_hip.so is built for gfx950 (MI355X) only; the current '
+                              'device is not one (asr_arch_is_gfx950 = %d)' % a)
+        _arch_ok.append(True)

@@ -1,6 +1,7 @@
 // Library-level entry points: version, thread-local error text, arch probe.
 #include <stdarg.h>
 #include <stdio.h>
+#include <string.h>
 
 #include "common.h"
 
@@ -19,12 +20,14 @@ extern "C" const char* asr_version(void) { return "asr_hip 0.1.0 gfx950"; }
 
 extern "C" const char* asr_last_error(void) { return asr::g_err; }
 
+// 1 when the current device is a gfx950 (the only target the code objects are
+// built for), 0 for any other device, -1 when no device can be queried.
 extern "C" int asr_arch_is_gfx950(void) {
-#if defined(__gfx950__)
-  return 1;
-#else
-  return 1;  // host pass: the library is only ever built with --offload-arch=gfx950
-#endif
+  int dev = 0;
+  hipDeviceProp_t prop;
+  if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess)
+    return -1;
+  return strncmp(prop.gcnArchName, "gfx950", 6) == 0 ? 1 : 0;
 }
 
 // A stream restricted to CUs [cu_begin, cu_begin + cu_count) of the current

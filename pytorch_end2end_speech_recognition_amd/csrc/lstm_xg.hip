@@ -83,7 +83,9 @@ constexpr size_t XG_PIN_BWD = 140 * 1024;
 // value above 80 KB still keeps one work-group per CU; 96 leaves 64 KB beside
 // it, room for one 128 x 128 GEMM work-group (the co-resident weight-gradient
 // mode of native_ops, ASR_OVERLAP_WGRAD=2).
+int g_pin_bwd_kb = 0;   // asr_lstm_set_bwd_pin_kb (0: ASR_XG_PIN_BWD_KB or the default)
 size_t xg_pin_bwd() {
+  if (g_pin_bwd_kb > 80 && g_pin_bwd_kb <= 160) return (size_t)g_pin_bwd_kb * 1024;
   const char* e = getenv("ASR_XG_PIN_BWD_KB");
   const int kb = e ? atoi(e) : 0;
   static bool warned = false;
@@ -114,6 +116,7 @@ typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
 typedef __attribute__((ext_vector_type(4))) _Float16 h16x4;
 typedef __attribute__((address_space(1))) int gint;
 typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) float gfloat;
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t xg_rsrc(void* p, unsigned bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(p, 0, (int)bytes, 0x00020000);
@@ -129,6 +132,7 @@ __device__ __forceinline__ int tags_ok(const u32x4& v, unsigned tag) {
 
 // Called by a whole wave after a failed sweep; false = give up (abort word set
 // by someone, or this wave's spin budget is spent).
+__device__ int g_xg_cell_sc1;  // backward cell inputs by sc1 (L2) loads (ASR_XG_CELL_SC1)
 __device__ int g_xg_sleep;   // s_sleep(1) units between polls (ASR_XG_SLEEP, default 1)
 __device__ int g_xg_delay;   // s_sleep(1) units before a step's first poll (ASR_XG_DELAY)
 
@@ -935,6 +939,11 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
     float* ddh = g_xg_dbg_dh;
     float* dcl = g_xg_dbg_cell;
     // c_t of step q is c_{tp} of step q - 1: with `carry` it is taken from there
+    const int lsc1 = __builtin_amdgcn_readfirstlane(g_xg_cell_sc1);
+    auto ldf = [&](const float* p) {
+      return lsc1 ? __hip_atomic_load((const gfloat*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                  : *p;
+    };
     auto load_cell = [&](int q, float (&av)[4], h16x4& avh, float& cc, float& cp, float& dyv,
                          const float* carry) {
       const int t = dir == 0 ? T - 1 - q : q;
@@ -942,14 +951,19 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
       const long long gb = ((long long)b * T + t) * 8 * H + (long long)dir * H4 + j;
       const long long si = ((long long)b * T + t) * 2 * H + (long long)dir * H + j;
       if constexpr (AH) {   // one 8-B load of the four fp16 gates, converted when used
-        avh = acth[(((long long)b * T + t) * 2 + dir) * H + j];
+        const h16x4* pa = acth + (((long long)b * T + t) * 2 + dir) * H + j;
+        if (lsc1)
+          avh = __builtin_bit_cast(h16x4, __hip_atomic_load((const gu64*)pa, __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT));
+        else
+          avh = *pa;
       } else {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) av[k] = act_dg[gb + (long long)k * H];
+        for (int k = 0; k < 4; ++k) av[k] = ldf(act_dg + gb + (long long)k * H);
       }
-      cc = carry ? *carry : cst[si];
-      cp = (tp >= 0 && tp < T) ? cst[si + (long long)(tp - t) * 2 * H] : 0.f;
-      dyv = dy ? dy[si] : 0.f;
+      cc = carry ? *carry : ldf(cst + si);
+      cp = (tp >= 0 && tp < T) ? ldf(cst + si + (long long)(tp - t) * 2 * H) : 0.f;
+      dyv = dy ? ldf(dy + si) : 0.f;
     };
     // inputs of step q (av, cc, cp, dyv) and q + 1 (n*): loaded two steps ahead
     float av[4] = {0.f, 0.f, 0.f, 0.f}, cc = 0.f, cp = 0.f, dyv = 0.f;
@@ -1415,6 +1429,16 @@ void xg_tuning_setup(hipStream_t s) {
 
 void xg_trace_setup(hipStream_t s) {
   xg_tuning_setup(s);
+  {  // read per launch (A/B within one process)
+    static int last = -1;
+    const char* c1 = getenv("ASR_XG_CELL_SC1");
+    const int sc1 = c1 ? atoi(c1) : 0;
+    if (sc1 != last) {
+      last = sc1;
+      (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_xg_cell_sc1), &sc1, sizeof(int), 0,
+                                   hipMemcpyHostToDevice, s);
+    }
+  }
   static unsigned long long* buf = nullptr;
   if (!getenv("ASR_XG_TRACE") || buf) return;
   const size_t n = (size_t)XG_TR_WG * XG_TR_STEPS * XG_TR_K;
@@ -1458,6 +1482,18 @@ extern "C" long long asr_xg_trace_read(unsigned long long* host) {
   const size_t n = (size_t)XG_TR_WG * XG_TR_STEPS * XG_TR_K;
   if (host && hipMemcpy(host, buf, n * 8, hipMemcpyDeviceToHost) != hipSuccess) return -1;
   return (long long)n;
+}
+
+// The backward recurrence's dynamic-LDS pin for the launches that follow
+// (kb in (80, 160]; 0 = ASR_XG_PIN_BWD_KB or the 140 KB default).  native_ops
+// sets 84 while weight-gradient GEMMs are meant to co-reside (opt-in
+// ASR_OVERLAP_WGRAD=2) and 0 otherwise: at 140 KB (+ 11 KB static) no kernel
+// with more than 9 KB of LDS -- every GEMM / convolution kernel -- can share a
+// CU with the recurrence.
+extern "C" int asr_lstm_set_bwd_pin_kb(int kb) {
+  ASR_REQUIRE(kb == 0 || (kb > 80 && kb <= 160), ASR_ERR_ARG, "lstm pin: %d KB", kb);
+  asr::g_pin_bwd_kb = kb;
+  return ASR_OK;
 }
 
 // Diagnostics: the backward recurrence's dh / spin-count recorders (NULL: off).

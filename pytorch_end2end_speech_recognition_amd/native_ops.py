@@ -937,6 +937,9 @@ class BLSTMLayerFn(torch.autograd.Function):
         # persistent recurrence starts (a kernel co-resident with the
         # recurrence perturbs it)
         notify_grad_event('pre_recurrence')
+        # the recurrence's LDS pin: co-resident GEMM work-groups only in the
+        # opt-in mode 2 (84 KB); otherwise 140 KB excludes every GEMM kernel
+        N.call('asr_lstm_set_bwd_pin_kb', 84 if _overlap_mode(dev, B, H) == '2' else 0)
         if act.dtype == torch.float16:
             # packed fp16 activations of asr_lstm_forward_xh: the tagged-granule
             # backward reads them directly; otherwise they are unpacked to f32
@@ -995,14 +998,14 @@ class BLSTMLayerFn(torch.autograd.Function):
             # weight gradients on a side stream, overlapping this layer's dX
             # GEMM and the previous layer's backward recurrence; joined back
             # into the main stream at the end of the backward pass
-            side, small = side_ent
+            side, small, gated = side_ent
             main = torch.cuda.current_stream(dev)
             side.wait_stream(main)
             if small:
                 N.call('asr_gemm_set_small_tiles', 1)
             try:
                 with torch.cuda.stream(side):
-                    if small and ctx.next_rec:
+                    if gated and ctx.next_rec:
                         # hold the GEMMs back until the previous layer's backward
                         # recurrence (launched next on the main stream) is resident
                         N.call('asr_lstm_wgrad_gate', N.stream_handle(dev))
@@ -1235,37 +1238,44 @@ def _xg_grid(B, H, ncu):
     return 1 << 30
 
 
-def _wgrad_side_stream(dev, B, H):
-    """Where the weight-gradient GEMMs of a BLSTM layer's backward run:
-    (stream, small_tiles) or None (main stream, default).
-
-    ASR_OVERLAP_WGRAD=1: a CU-masked side stream (upper half of the CUs), only
-    when the persistent backward recurrence fits in the other half.
-    ASR_OVERLAP_WGRAD=2: a plain side stream whose GEMMs use the 128 x 128
-    kernel only (64 KB of LDS, asr_gemm_set_small_tiles) while the backward
-    recurrence pins just under 96 KB (ASR_XG_PIN_BWD_KB), so one GEMM
-    work-group fits beside the recurrence's one work-group on every CU and the
-    weight gradients of layer l run during the recurrence of layer l - 1.
-    Default (auto): 2 when the recurrence leaves CUs free, else 0.
-    Both need bf16 mode and the persistent recurrence."""
+def _overlap_mode(dev, B, H):
+    """The resolved ASR_OVERLAP_WGRAD mode for a BLSTM layer's backward:
+      '0'  weight gradients on the compute stream;
+      '1'  a CU-masked side stream (upper half of the CUs), only when the
+           persistent backward recurrence fits in the other half;
+      '2'  (opt-in, timing experiments only) a plain side stream whose GEMMs
+           use the 128 x 128 kernel (64 KB of LDS) while the recurrence pins
+           84 KB, so GEMM work-groups are co-resident with the recurrence's on
+           every CU -- that changes the recurrence's results (DESIGN.md §5);
+      '3'  a plain side stream with the recurrence at its default 140 KB pin,
+           so no GEMM work-group can share a CU with it: the weight-gradient
+           GEMMs run on the CUs the recurrence leaves free.
+    auto = '3' when the recurrence leaves at least 32 CUs free (the H = 320
+    configs: 160 of 256 CUs), else '0'.  All need bf16 and the persistent
+    recurrence."""
     mode = os.environ.get('ASR_OVERLAP_WGRAD', 'auto')
     if compute_dtype() != BF16 or os.environ.get('ASR_LSTM_PERSIST', '1') == '0' or H % 32:
-        return None
+        return '0'
+    ncu = _num_cus(dev)
     if mode == 'auto':
-        # Round 3: OFF.  With GEMM work-groups co-resident on the recurrence's
-        # CUs the backward recurrence's results change from run to run by up to
-        # 2 % relative even with contracting weights (tools/buckets_diag.py
-        # trace; DESIGN.md §5) -- wrong gradients, not rounding.  An LDS-only
-        # co-resident stand-in leaves them bitwise stable; GEMMs writing to
-        # scratch outputs do not.  Until that is understood, the weight
-        # gradients stay on the compute stream (mode 1, CU-disjoint, remains
-        # available where the recurrence fits in half the chip).
-        mode = '0'
+        mode = '3' if _xg_grid(B, H, ncu) + 32 <= ncu else '0'
     elif mode == '2':
         _warn_once('ASR_OVERLAP_WGRAD=2: weight-gradient GEMMs co-resident with the backward '
                    'recurrence give run-to-run different (wrong) recurrence results on '
                    'gfx950 (DESIGN.md §5); use for timing experiments only')
-    if mode not in ('1', '2'):
+    if mode == '1' and _xg_grid(B, H, 2 * (ncu - ncu // 2)) > ncu // 2:
+        mode = '0'
+    return mode if mode in ('1', '2', '3') else '0'
+
+
+def _wgrad_side_stream(dev, B, H):
+    """Where the weight-gradient GEMMs of a BLSTM layer's backward run:
+    (stream, small_tiles, gated) or None (the compute stream); see
+    _overlap_mode.  gated: the GEMMs wait for the next recurrence to be
+    resident (asr_lstm_wgrad_gate) so they take the CUs it leaves free rather
+    than CUs it needs."""
+    mode = _overlap_mode(dev, B, H)
+    if mode == '0':
         return None
     key = (dev.index, mode)
     ent = _side_streams.get(key)
@@ -1275,18 +1285,11 @@ def _wgrad_side_stream(dev, B, H):
             h = ctypes.c_void_p()
             with torch.cuda.device(dev):
                 N.call('asr_stream_create_cu_masked', ncu // 2, ncu - ncu // 2, ctypes.byref(h))
-            ent = (torch.cuda.ExternalStream(h.value, device=dev), ncu // 2)
+            ent = torch.cuda.ExternalStream(h.value, device=dev)
         else:
-            # dynamic pin + the kernel's ~11 KB of static LDS stays <= 96 KB
-            os.environ.setdefault('ASR_XG_PIN_BWD_KB', '84')
-            ent = (torch.cuda.Stream(device=dev), ncu)
+            ent = torch.cuda.Stream(device=dev)
         _side_streams[key] = ent
-    stream, free_cus = ent
-    if mode == '2':
-        return stream, True
-    # the persistent backward recurrence (lstm_xg.hip) pins one work-group per
-    # CU: 2 directions x ceil(B / 8) utterance groups x H / 16 unit slices
-    return (stream, False) if _xg_grid(B, H, 2 * free_cus) <= free_cus else None
+    return ent, mode == '2', mode != '1'
 
 
 def blstm_layer(x_src, lens, T, w_ih, w_hh, b_ih, b_hh, perm=None, t_mul=1, t_add=0, gbufs=None,

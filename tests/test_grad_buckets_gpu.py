@@ -51,15 +51,15 @@ def _batch(B=32, T=240, seed=0):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('overlap,H,L', [('auto', 512, 5), ('auto', 320, 4), ('2', 256, 3)])
+@pytest.mark.parametrize('overlap,H,L', [('auto', 512, 5), ('auto', 320, 4), ('3', 256, 3),
+                                         ('0', 320, 4)])
 def test_buckets_on_real_model(overlap, H, L, cuda_dev, monkeypatch):
-    """ctc5x512's encoder and the 4x320 encoder of configs[2]-[4] (auto: weight
-    gradients on the compute stream), and a 3x256 encoder with its weight
-    gradients on the side stream beside the next recurrence (opt-in mode 2,
-    which joins them into the compute stream before their bucket is issued).
-    Mode 2's co-resident GEMMs perturb the recurrence itself,
-    so there the update is compared with the plain step within 5 % instead of
-    bitwise; the bucket checks are exact in every mode."""
+    """ctc5x512's encoder (auto: weight gradients on the compute stream), the
+    4x320 encoder of configs[2]-[4] (auto: on the side stream, mode 3, on the
+    CUs the next backward recurrence leaves free -- joined into the compute
+    stream before their bucket is issued), a 3x256 encoder in mode 3 and the
+    4x320 one on the compute stream (mode 0).  Every mode updates the weights
+    bitwise like the plain single-process step; the bucket checks are exact."""
     from pytorch_end2end_speech_recognition_amd import native_ops
     from pytorch_end2end_speech_recognition_amd.utils.training import training_loop as TL
     monkeypatch.setenv('ASR_OVERLAP_WGRAD', overlap)
@@ -118,10 +118,6 @@ def test_buckets_on_real_model(overlap, H, L, cuda_dev, monkeypatch):
             assert torch.equal(snap, flat[a:b]), (a, b, float((snap - flat[a:b]).abs().max()))
         assert guards and all(op == dist.ReduceOp.MAX for op, _ in guards)
         assert lv == lv_ref
-        if overlap == '2':
-            g0, g1 = ref._flat_grad.double(), m._flat_grad.double()
-            assert float((g1 - g0).norm() / g0.norm()) < 5e-2
-        else:
-            assert torch.equal(m._flat_param, ref._flat_param)
+        assert torch.equal(m._flat_param, ref._flat_param)
     finally:
         native_ops.set_compute_dtype('fp32')

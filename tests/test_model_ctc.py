@@ -270,28 +270,42 @@ def test_deferred_loss_readback_matches_synchronous_steps(cuda_dev):
         native_ops.set_compute_dtype('fp32')
 
 
-def test_wgrad_overlap_off_by_default(monkeypatch):
-    """auto keeps every weight-gradient GEMM on the compute stream: co-resident
-    GEMMs perturb the backward recurrence."""
+def test_wgrad_overlap_auto_mode(monkeypatch):
+    """auto: the weight-gradient GEMMs go to a side stream (mode 3, the
+    recurrence at its 140 KB LDS pin so no GEMM work-group can share its CUs)
+    when the persistent backward recurrence leaves >= 32 of the 256 CUs free
+    (the H = 320 configs), else they stay on the compute stream; co-resident
+    GEMMs (mode 2) are never chosen automatically."""
     from pytorch_end2end_speech_recognition_amd import native_ops
     monkeypatch.delenv('ASR_OVERLAP_WGRAD', raising=False)
+    monkeypatch.setattr(native_ops, '_num_cus', lambda dev: 256)
     prev = native_ops.compute_dtype()
     native_ops.set_compute_dtype('bf16')
     try:
-        for B, H in ((32, 512), (32, 320), (16, 256)):
-            assert native_ops._wgrad_side_stream(torch.device('cpu'), B, H) is None
+        cpu = torch.device('cpu')
+        assert native_ops._overlap_mode(cpu, 32, 512) == '0'     # 256 work-groups
+        assert native_ops._overlap_mode(cpu, 32, 320) == '3'     # 160
+        assert native_ops._overlap_mode(cpu, 16, 256) == '3'     # 64
+        assert native_ops._overlap_mode(cpu, 32, 500) == '0'     # no persistent recurrence
+        monkeypatch.setenv('ASR_OVERLAP_WGRAD', '1')
+        assert native_ops._overlap_mode(cpu, 32, 320) == '0'     # 160 > 128: no half fits
+        assert native_ops._overlap_mode(cpu, 16, 256) == '1'
+        native_ops.set_compute_dtype('fp32')
+        monkeypatch.setenv('ASR_OVERLAP_WGRAD', '3')
+        assert native_ops._overlap_mode(cpu, 16, 256) == '0'     # fp32 parity mode
     finally:
         native_ops.set_compute_dtype('bf16' if prev == native_ops.BF16 else 'fp32')
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('mode', ['1'])
+@pytest.mark.parametrize('mode', ['1', '3'])
 def test_wgrad_side_stream_matches_main_stream(mode, cuda_dev, monkeypatch):
     """Weight gradients computed on the side stream (ASR_OVERLAP_WGRAD=1: CU-masked
-    half of the chip; 2: small-tile GEMMs co-resident with the next layer's
-    persistent backward recurrence) equal the main-stream ones up to the GEMM
-    kernels' summation order, at a shape that takes the persistent recurrence
-    (B = 16, H = 256, three layers, T = 160), and the recurrence did not give up."""
+    half of the chip; 3: the CUs the next layer's persistent backward
+    recurrence leaves free) equal the main-stream ones -- bitwise: the same GEMM
+    kernels on the same operands -- at a shape that takes the persistent
+    recurrence (B = 16, H = 256, three layers, T = 160), and the recurrence did
+    not give up."""
     from pytorch_end2end_speech_recognition_amd import native_ops
     kw = dict(input_size=40, encoder_type='lstm', encoder_bidirectional=True,
               encoder_num_units=256, encoder_num_proj=0, encoder_num_layers=3, fc_list=[],
@@ -338,9 +352,7 @@ def test_wgrad_side_stream_matches_main_stream(mode, cuda_dev, monkeypatch):
     assert events['0'] == ['recurrence', 'grads'] * 3
     assert events[mode][:5] == ['recurrence', 'grads', 'recurrence', 'grads', 'recurrence']
     for k, g0 in grads['0'].items():
-        g1 = grads[mode][k]
-        scale = np.abs(g0).max() + 1e-12
-        assert np.abs(g1 - g0).max() / scale < 1e-4, (k, np.abs(g1 - g0).max(), scale)
+        np.testing.assert_array_equal(grads[mode][k], g0, err_msg=k)
 
 
 @pytest.mark.gpu

@@ -87,6 +87,8 @@ VARIANTS = {
     'copy': dict(env={'ASR_OVERLAP_WGRAD': '2'}, side='copy'),
     'tiny': dict(env={'ASR_OVERLAP_WGRAD': '2'}, side='tiny'),
     'lds': dict(env={'ASR_OVERLAP_WGRAD': '2'}, side='lds'),
+    'mode2_sc1': dict(env={'ASR_OVERLAP_WGRAD': '2', 'ASR_XG_CELL_SC1': '1'}),
+    'mode3': dict(env={'ASR_OVERLAP_WGRAD': '3'}),
 }
 
 
@@ -107,7 +109,7 @@ def run_once(sd, batch, env, side=None):
     def wgrad(dg, *a):
         dgs.append(dg.detach().clone())          # stream-ordered after the recurrence
         cur = torch.cuda.current_stream()
-        if work is not None and any(cur == e[0] for e in no._side_streams.values()):
+        if work is not None and any(cur == e for e in no._side_streams.values()):
             work(dg, *a)                          # side stream: the stand-in workload
         else:
             _orig_wgrad(dg, *a)
@@ -121,9 +123,14 @@ def run_once(sd, batch, env, side=None):
             cl = (torch.full((Bb, Tt, 2, Hh, 12), float('nan'), device=dev)
                   if os.environ.get('DIAG_CELL') == '1' else None)
             N.call('asr_lstm_debug_dh', N.ptr(dh), N.ptr(sp), N.ptr(cl), N.stream_handle(dev))
-            saved = ctx.saved_tensors      # x_op, w_op, lens, w_hh, b_ih, b_hh, act, cst, y_op
-            dhs.append((dh, sp, cl, saved[6].detach().clone(), saved[7].detach().clone(),
-                        dy.detach().clone(), saved[2].detach().clone()))
+            if os.environ.get('DIAG_REPLAY', '0') == '1':
+                # (the clones before the recurrence launch change its timing:
+                # the perturbation then did not reproduce)
+                saved = ctx.saved_tensors  # x_op, w_op, lens, w_hh, b_ih, b_hh, act, cst, y_op
+                dhs.append((dh, sp, cl, saved[6].detach().clone(), saved[7].detach().clone(),
+                            dy.detach().clone(), saved[2].detach().clone()))
+            else:
+                dhs.append((dh, sp, cl, None, None, None, None))
         out = orig_bwd(ctx, dy)
         if DH:
             N.call('asr_lstm_debug_dh', None, None, None, N.stream_handle(dev))
@@ -383,7 +390,7 @@ def main():
                     report_dh(i, ref[3][i], dhs[i], T)
                     if i == 1 and dhs[i][2] is not None:
                         report_cell(i, ref[3][i], dhs[i], r, g, T)
-                    if i == 1:
+                    if i == 1 and dhs[i][3] is not None:
                         replay_cells(i, dhs[i], g, T, tag='got')
                         replay_cells(i, ref[3][i], r, T, tag='ref')
                     fg, _ = first_diffs(r, g, T, 'dG')
