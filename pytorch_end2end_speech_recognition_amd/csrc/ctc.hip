@@ -588,6 +588,13 @@ __global__ void __launch_bounds__(256) ctc_grad(
   }
 }
 
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+template <int A>
+__device__ __forceinline__ void take8(const float (&v)[12], float (&o)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = v[A + j];
+}
+
 // The same gradient written as the bf16 dY operand of the output layer's two
 // GEMMs (ctc_grad_bf16): rows (b, t) of `gld` columns (gld >= V, gld % 8 == 0,
 // 16-B aligned rows), columns [V, gld) zero -- the zero-padded pitch the
@@ -602,7 +609,8 @@ __global__ void __launch_bounds__(256) ctc_grad_bf16(
     const float* __restrict__ lse, const float* __restrict__ emit,
     const float* __restrict__ alpha, const float* __restrict__ beta,
     const float* __restrict__ logp, const float* __restrict__ grad_scale, float scale_mul,
-    uint16_t* __restrict__ grads, long long gst, long long gsb, int gld, int rev) {
+    uint16_t* __restrict__ grads, long long gst, long long gsb, int gld, int rev,
+    int acts_bytes) {
   extern __shared__ __attribute__((aligned(16))) float occ[];  // [V] (kTable) or [Spad]
   const long long row = rev ? (long long)gridDim.x - 1 - blockIdx.x : blockIdx.x;
   const int b = (int)(row / T), t = (int)(row % T);
@@ -673,13 +681,50 @@ __global__ void __launch_bounds__(256) ctc_grad_bf16(
       rep_c[r] = c;
       rep_v[r] = acc;
     }
-    // stream the row: g = softmax * scale, two 8-column groups in flight per thread
-    int i = tid;
-    for (; i + nth < n8; i += 2 * nth) {
-      pack(8 * i, [&](int c) { return __expf(x[c] - z) * scale; });
-      pack(8 * (i + nth), [&](int c) { return __expf(x[c] - z) * scale; });
+    // stream the row: g = softmax * scale.  The f32 row starts at any 4-B
+    // alignment, a (row-uniform) elements past a 16-B boundary; each thread
+    // takes 8 columns at a time with three aligned 16-B buffer loads (past the
+    // activations' end they read zeros) and keeps elements a .. a + 7
+    if (acts_bytes) {
+      const long long xo = (long long)t * st + (long long)b * sb;   // row start (elements)
+      const int a = (int)(xo & 3);
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc((void*)acts, 0, acts_bytes, 0x00020000);
+      const unsigned base = (unsigned)((xo - a) * 4);
+      auto chunk = [&](int k) {
+        float v[12];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          const f32x4 w = __builtin_bit_cast(
+              f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, base + (unsigned)(32 * k + 16 * q), 0, 0));
+          v[4 * q] = w[0]; v[4 * q + 1] = w[1]; v[4 * q + 2] = w[2]; v[4 * q + 3] = w[3];
+        }
+        float o[8];
+        switch (a) {   // row-uniform
+          case 0: take8<0>(v, o); break;
+          case 1: take8<1>(v, o); break;
+          case 2: take8<2>(v, o); break;
+          default: take8<3>(v, o); break;
+        }
+        const int c0 = 8 * k;
+        unsigned w4[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const unsigned lo = c0 + 2 * j < V ? f2bf(__expf(o[2 * j] - z) * scale) : 0u;
+          const unsigned hi = c0 + 2 * j + 1 < V ? f2bf(__expf(o[2 * j + 1] - z) * scale) : 0u;
+          w4[j] = lo | (hi << 16);
+        }
+        reinterpret_cast<uint4*>(g)[k] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+      };
+      int i = tid;
+      for (; i + nth < n8; i += 2 * nth) {
+        chunk(i);
+        chunk(i + nth);
+      }
+      for (; i < n8; i += nth) chunk(i);
+    } else {
+      for (int i = tid; i < n8; i += nth) pack(8 * i, [&](int c) { return __expf(x[c] - z) * scale; });
     }
-    for (; i < n8; i += nth) pack(8 * i, [&](int c) { return __expf(x[c] - z) * scale; });
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
 #pragma unroll
@@ -850,6 +895,13 @@ extern "C" int asr_ctc_backward_bf16(const float* acts, long long stride_t, long
   const int Spad = 64 * pick_k(max_label_len);
   const bool table = V <= 256;
   const int threads = table ? 64 : 256;
+  // aligned 16-B buffer loads of the activation rows (compact form) when the
+  // activations are one dense [B][T][V] or [T][B][V] block below 2 GiB
+  const long long nb = 4LL * B * T * V;
+  const bool dense = (stride_t == V && stride_b == (long long)T * V) ||
+                     (stride_b == V && stride_t == (long long)B * V);
+  const int abytes = (!table && dense && nb < 0x7fffff00LL && ((uintptr_t)acts & 15) == 0)
+                         ? (int)nb : 0;
   // algorithmic HBM bytes: activations read (4 V) + bf16 gradient written (2 gld) per row
   const int pslot = prof_begin_launch(ASR_PROF_CTC_GRAD, s, (4.0 * V + 2.0 * gld) * B * T, V);
 #define ASR_CTC_G16(TB)                                                                          \
@@ -857,7 +909,7 @@ extern "C" int asr_ctc_backward_bf16(const float* acts, long long stride_t, long
                      (TB ? V : Spad) * sizeof(float), s, acts, stride_t, stride_b, T, V,         \
                      labels_flat, label_lens, act_lens, ws.offs, blank, Spad, ws.lse, ws.emit,   \
                      ws.alpha, ws.beta, ws.logp, grad_scale, scale, grads, gstride_t, gstride_b, \
-                     gld, (ctc_row_order() >> 1) & 1)
+                     gld, (ctc_row_order() >> 1) & 1, abytes)
   if (table) ASR_CTC_G16(true);
   else ASR_CTC_G16(false);
 #undef ASR_CTC_G16

@@ -261,7 +261,10 @@ __device__ __forceinline__ float ftanh(float x) { return 2.f * fsig(2.f * x) - 1
 // >= 0.5 mark the complement form; 1 - |g| is clamped to >= 2^-15, so the
 // stored magnitude is >= 0.5 exactly, while direct values round to < 0.5).
 // Both forms carry fp16's relative precision for the small factor.
-__device__ __forceinline__ float enc_sig(float s) { return s < 0.5f ? s : s - 1.f; }
+// (-(1 - s), not s - 1: a saturated s == 1 must store -0, whose sign bit marks
+// the complement form; s - 1 would give +0 and decode as s = 0)
+#ifndef ASR_ACTH_PLAIN
+__device__ __forceinline__ float enc_sig(float s) { return s < 0.5f ? s : -(1.f - s); }
 __device__ __forceinline__ float enc_tanh(float g) {
   const float a = fabsf(g);
   return a <= 0.499f ? g : copysignf(fmaxf(1.f - a, 1.f / 32768.f) * 16384.f, g);
@@ -278,6 +281,12 @@ __device__ __forceinline__ void dec_tanh(float e, float& g, float& om2) {   // o
   g = cm ? copysignf(1.f - c, e) : e;
   om2 = cm ? c * (2.f - c) : 1.f - e * e;
 }
+#else   // A/B builds only: the gates stored as plain fp16 (round 3)
+__device__ __forceinline__ float enc_sig(float s) { return s; }
+__device__ __forceinline__ float enc_tanh(float g) { return g; }
+__device__ __forceinline__ void dec_sig(float e, float& s, float& om) { s = e; om = 1.f - e; }
+__device__ __forceinline__ void dec_tanh(float e, float& g, float& om2) { g = e; om2 = 1.f - e * e; }
+#endif
 
 // ---------------------------------------------------------------------------
 // forward.  grid = G * WPG (G = 2 * ceil(B / R) groups, WPG = H / 16).

@@ -147,7 +147,8 @@ def test_reference_init_early_steps_vs_float64(cuda_dev):
 def _sat_case(seed=5, Bs=16, Ts=160, Hs=256, Ds=256):
     """Saturated gates: every gate row's bias drawn +-U[3, 8] (random sign), so
     sigmoid gates sit at 0.95-0.9997 or 3e-4-0.05 and the tanh gate near +-1,
-    where fp16 storage of s itself would make 1 - s coarse or zero."""
+    where fp16 storage of s itself would make 1 - s coarse or zero; every 16th
+    row +-25, where the f32 gate is exactly 1 / 0 / +-1."""
     rng = np.random.RandomState(seed)
     lens = np.sort(rng.randint(120, Ts + 1, Bs))[::-1].astype(np.int32)
     lens[0] = Ts
@@ -158,6 +159,7 @@ def _sat_case(seed=5, Bs=16, Ts=160, Hs=256, Ds=256):
     w_ih = torch.rand(8 * Hs, Ds, generator=g) * 0.2 - 0.1
     w_hh = (torch.rand(8 * Hs, Hs, generator=g) * 2 - 1) * 0.03
     mag = torch.rand(8 * Hs, generator=g) * 5 + 3
+    mag[::16] = 25.0          # sigmoid == 1 / tanh == +-1 exactly in f32 (the -0 encoding)
     sign = torch.where(torch.rand(8 * Hs, generator=g) < 0.5, -1.0, 1.0)
     b_ih = mag * sign
     b_hh = torch.zeros(8 * Hs)
