@@ -813,6 +813,16 @@ long long asr_xg_trace_read(unsigned long long* host);
  * the default no kernel with more than 9 KB of LDS -- every GEMM and
  * convolution kernel -- can be co-resident with it. */
 int asr_lstm_set_bwd_pin_kb(int kb);
+/* Hidden units per work-group of the tagged-granule backward recurrence for the
+ * launches that follow: 0 (ASR_XG_BWD_XU, else 16), 16, or 32 -- half the
+ * work-groups, so a layer of 2 x 8 rows x 512 units takes 128 of 256 CUs and
+ * the weight-gradient GEMMs of the layer above run beside it (native_ops'
+ * ASR_OVERLAP_WGRAD mode 3).  32 applies only where H % 32 == 0, H <= 512 and
+ * 8 rows per group fit; elsewhere 16 is used. */
+int asr_lstm_set_bwd_units(int xu);
+/* Work-groups that backward recurrence launches for [B, *, H] with xu units per
+ * work-group (0: the current setting); 0 if the shape cannot take that path. */
+int asr_lstm_backward_grid(int B, int H, int xu);
 /* Diagnostics only (tools/cores_locate.py): backward recurrence launches
  * enqueued on `stream` after this call record every dh_t their cell waves form
  * into dh ([B][T][2][H] f32), each step's sweep spin count into spins

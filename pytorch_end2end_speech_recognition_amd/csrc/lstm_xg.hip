@@ -97,6 +97,20 @@ size_t xg_pin_bwd() {
   return (kb > 80 && kb <= 160) ? (size_t)kb * 1024 : XG_PIN_BWD;
 }
 
+// Units per backward work-group (lstm_bwd_xg's XB): asr_lstm_set_bwd_units, else
+// ASR_XG_BWD_XU, else 16.  32 only where it is supported: H % 32 == 0, R = 8 and
+// at most 32 A fragments per MFMA lane (H <= 512).
+int g_bwd_xu = 0;
+int xg_bwd_xu(int R, int H) {
+  int xu = g_bwd_xu;
+  if (!xu) {
+    const char* e = getenv("ASR_XG_BWD_XU");
+    xu = e ? atoi(e) : 16;
+  }
+  if (xu == 32 && R == 8 && H % 32 == 0 && (H / 16 + 3) / 4 <= 8) return 32;
+  return 16;
+}
+
 // The backward's pin leaves no room for the kernel's static LDS: the layer
 // would silently take the slower counter-form recurrence -- say so once.
 static void xg_warn_pin_unfit(size_t pin) {
@@ -814,36 +828,43 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
 }
 
 // ---------------------------------------------------------------------------
-// backward.  grid = G * WPG.  Processing step q handles the forward direction
-// at t = T-1-q and the reverse direction at t = q.
+// backward.  grid = G * WPG, WPG = H / XB work-groups per group, each owning
+// XB units (16, or 32 to leave half of a 256-CU chip to the weight-gradient
+// GEMMs at 5x512: the group's fan-in halves and the MFMA phase doubles).
+// Processing step q handles the forward direction at t = T-1-q and the reverse
+// direction at t = q.
 // Granules: pg[par][grp][producer][row][H/4] u64 = four bf16 partials of dh
 // (units 4p .. 4p+3), the first one's LSB the step tag bit -- the partials are
 // sums of bf16 dg x bf16 W_hh products accumulated in f32 and rounded once for
 // transport; the consumer sums the WPG partials in f32.
 // Wave roles, two barriers per step (B1: partials summed; B2: dg in LDS):
-//   waves 0..3 (sweepers): poll the partials of dh for this block's 16 units
+//   waves 0..3 (sweepers): poll the partials of dh for this block's XB units
 //     from every producer of the group, sum per producer subset -> LDS, B1, B2.
-//   R/4 cell waves: B1, dh = dy + sum, cell backward -> dg (bf16 -> LDS), B2,
-//     then the f32 / bf16 dg stores and the next step's prefetch.
-//   4 MFMA waves: B1, B2, partial dh_{t-1}[rows][all units] = dg x (this
-//     block's 64 rows of W_hh) -> write-through granules.
+//   R XB / 64 cell waves: B1, dh = dy + sum, cell backward -> dg (bf16 -> LDS),
+//     B2, then the f32 / bf16 dg stores and the next step's prefetch.
+//   XB / 4 MFMA waves: B1, B2, partial dh_{t-1}[rows][all units] = dg x (this
+//     block's 4 XB rows of W_hh) -> write-through granules.
 // A fragments (VGPRs): A[m][k] = W_hh[gaterow(k)][m] for output unit m (M block
-// mb = mw + 4 i) and local gate row k in [0, 64): gate k >> 4, unit u0 + (k & 15).
+// mb = mw + (XB / 4) i) and local gate row k in [0, 4 XB): gate k / XB, unit u0 + k % XB.
 // ---------------------------------------------------------------------------
-template <int R, int MB, bool AH>
-__global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
+template <int R, int MB, bool AH, int XB>
+__global__ void __launch_bounds__(256 + R * XB + 16 * XB) lstm_bwd_xg(
     int B, int T, int H, const int32_t* __restrict__ lens, const float* __restrict__ whh_f,
     const float* __restrict__ whh_r, const float* __restrict__ dy, float* __restrict__ act_dg,
     const float* __restrict__ cst, unsigned long long* pg, int* hdr,
     uint16_t* __restrict__ dgbf, float* __restrict__ dbpart, unsigned epoch, int allow_local,
     int dg_f32, int io_pos, int dg_st16, const h16x4* __restrict__ acth) {
-  constexpr int NPG = 256 / (2 * R);   // producer subsets swept in parallel
-  __shared__ float red[NPG][R][XU + 1];
-  __shared__ __attribute__((aligned(16))) uint16_t dgt[16][4 * XU + 8];
+  constexpr int SQ = XB / 8;           // 16-B loads (8 units) per row of a producer's slice
+  constexpr int LPS = R * SQ;          // sweeper lanes per producer subset
+  constexpr int NPG = 256 / LPS;       // producer subsets swept in parallel
+  constexpr int NKS = XB / 8;          // MFMA k-steps: 4 gates x XB units / 32
+  constexpr int NMW = XB / 4;          // MFMA waves (8 at XB = 32: 64 fragment VGPRs each)
+  __shared__ float red[NPG][R][XB + 1];
+  __shared__ __attribute__((aligned(16))) uint16_t dgt[16][4 * XB + 8];
   __shared__ int s_dead;
   __shared__ int s_pl[4];
   int* abortw = hdr;
-  const int WPG = H / XU;
+  const int WPG = H / XB;
   const int G = gridDim.x / WPG;
   if (threadIdx.x == 0) s_dead = 0;
   xg_place(WPG, allow_local, hdr, s_pl, epoch);  // epoch: the launch's sequence number
@@ -851,24 +872,25 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
   const int grp = s_pl[0], mem = s_pl[1];
   const bool local = s_pl[2] != 0;  // granules carry a 1-bit step tag (tag_bit)
   const int dir = grp & 1, rg = grp >> 1;
-  const int u0 = mem * XU, b0 = rg * R;
+  const int u0 = mem * XB, b0 = rg * R;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int HB = H / XU;                 // output M blocks
+  const int HB = H / 16;                 // output M blocks
   const int H4 = 4 * H;
   const int hq = H / 4;                  // granules per producer row
   const unsigned pg_bytes = (unsigned)(2ull * G * WPG * R * hq * 8);
   const __amdgpu_buffer_rsrc_t rs = xg_rsrc(pg, pg_bytes);
   unsigned long long* tr = blockIdx.x < XG_TR_WG ? g_xg_trace : nullptr;
-  for (int e = tid; e < 16 * (4 * XU + 8); e += blockDim.x) (&dgt[0][0])[e] = 0;
-  const int NCW = R / 4;                 // cell waves: 4 .. 4 + NCW - 1; MFMA waves after
+  for (int e = tid; e < 16 * (4 * XB + 8); e += blockDim.x) (&dgt[0][0])[e] = 0;
+  const int NCW = R * XB / 64;                // cell waves: 4 .. 4 + NCW - 1; MFMA waves after
 
   if (wave < 4) {
     // ------------------------------ sweeper -------------------------------
-    const int sl = tid & (2 * R - 1);
-    const int srow = sl >> 1, sq = sl & 1;   // row, units 8 sq .. 8 sq + 7
-    const int pgi = tid / (2 * R);
-    constexpr int NLD = (4 * MB + NPG - 1) / NPG;   // producers per sweeper lane (WPG <= 4 MB)
+    const int sl = tid & (LPS - 1);
+    const int srow = sl / SQ, sq = sl % SQ;   // row, units 8 sq .. 8 sq + 7
+    const int pgi = tid / LPS;
+    // producers per sweeper lane (WPG = H / XB <= 16 NMW MB / XB = 4 MB)
+    constexpr int NLD = (4 * MB + NPG - 1) / NPG;
     unsigned* dspin = g_xg_dbg_spins;
     const int nsleep = __builtin_amdgcn_readfirstlane(g_xg_sleep);
     const int ndelay = __builtin_amdgcn_readfirstlane(g_xg_delay);
@@ -940,7 +962,7 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
     // -------------------------------- cell --------------------------------
     __builtin_amdgcn_s_setprio(2);
     const int ct = tid - 256;
-    const int row = ct >> 4, unit = ct & 15;
+    const int row = ct / XB, unit = ct % XB;
     const int b = b0 + row, j = u0 + unit;
     const bool own = b < B;
     const int len = own ? lens[b] : 0;
@@ -990,8 +1012,8 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
     // as ONE 16-B store per lane of the first R / 8 cell waves -- R rows x 4
     // gates x 2 halves of 8 units -- instead of four 2-B stores per (row, unit)
     // lane on every cell wave (dg_st16; ASR_XG_DG_ST16=0: the per-lane stores).
-    const int srow = ct >> 3, sg = (ct >> 1) & 3, sh = ct & 1;
-    const bool st16 = dg_st16 && dgbf && ct < 8 * R && b0 + srow < B;
+    const int srow = ct / (4 * SQ), sg = (ct / SQ) & 3, sh = ct % SQ;
+    const bool st16 = dg_st16 && dgbf && ct < 4 * SQ * R && b0 + srow < B;
     auto step_io = [&](int q, int t, float d_i, float d_f, float d_g, float d_o, uint16_t bi,
                        uint16_t bff, uint16_t bg, uint16_t bo) {
       if (own) {
@@ -1010,7 +1032,7 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
         }
       }
       if (st16) {
-        const uint4 v = *reinterpret_cast<const uint4*>(&dgt[srow][sg * XU + 8 * sh]);
+        const uint4 v = *reinterpret_cast<const uint4*>(&dgt[srow][sg * XB + 8 * sh]);
         *reinterpret_cast<uint4*>(dgbf + ((long long)(b0 + srow) * T + t) * 8 * H +
                                   (long long)dir * H4 + (long long)sg * H + u0 + 8 * sh) = v;
       }
@@ -1063,9 +1085,9 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
       if (dead) return;
       const uint16_t bi = f2bf(d_i), bff = f2bf(d_f), bg = f2bf(d_g), bo = f2bf(d_o);
       dgt[row][unit] = bi;
-      dgt[row][XU + unit] = bff;
-      dgt[row][2 * XU + unit] = bg;
-      dgt[row][3 * XU + unit] = bo;
+      dgt[row][XB + unit] = bff;
+      dgt[row][2 * XB + unit] = bg;
+      dgt[row][3 * XB + unit] = bo;
       // step q + 1's inputs (loaded two steps ahead)
 #pragma unroll
       for (int k = 0; k < 4; ++k) av[k] = nav[k];
@@ -1090,22 +1112,22 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
 
   // --------------------------------- MFMA -----------------------------------
   __builtin_amdgcn_s_setprio(2);
-  const int mw = wave - 4 - NCW;         // 0..3
+  const int mw = wave - 4 - NCW;         // 0 .. NMW - 1
   const int kq = lane >> 4, ln = lane & 15;
-  bf16x8 wa[MB][2];
+  bf16x8 wa[MB][NKS];
   {
     const float* W = dir ? whh_r : whh_f;
 #pragma unroll
     for (int i = 0; i < MB; ++i) {
-      const int mb = min(mw + 4 * i, HB - 1);
+      const int mb = min(mw + NMW * i, HB - 1);
       const int m = 16 * mb + ln;
 #pragma unroll
-      for (int kst = 0; kst < 2; ++kst) {
+      for (int kst = 0; kst < NKS; ++kst) {
         u16x8 r;
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj) {
           const int k = 32 * kst + 8 * kq + jj;
-          r[jj] = f2bf(W[(long long)((k >> 4) * H + u0 + (k & 15)) * H + m]);
+          r[jj] = f2bf(W[(long long)((k / XB) * H + u0 + (k % XB)) * H + m]);
         }
         wa[i][kst] = as_bf16x8(r);
       }
@@ -1115,8 +1137,10 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
     __syncthreads();  // B1
     if (s_dead) return;
     __syncthreads();  // B2
-    const bf16x8 bf0 = *reinterpret_cast<const bf16x8*>(&dgt[ln][8 * kq]);
-    const bf16x8 bf1 = *reinterpret_cast<const bf16x8*>(&dgt[ln][32 + 8 * kq]);
+    bf16x8 bfk[NKS];
+#pragma unroll
+    for (int kst = 0; kst < NKS; ++kst)
+      bfk[kst] = *reinterpret_cast<const bf16x8*>(&dgt[ln][32 * kst + 8 * kq]);
     const unsigned tb = tag_bit(q);
     const long long obase = (((long long)(q & 1) * G + grp) * WPG + mem) * R;
     // block by block, one block of lag: the MFMA pair of block i is issued
@@ -1128,17 +1152,18 @@ __global__ void __launch_bounds__(512 + R * XU) lstm_bwd_xg(
     // nothing.
     f32x4 acc[MB];
     auto mm = [&](int i) {
-      acc[i] = mfma_bf16(wa[i][0], bf0, f32x4{0.f, 0.f, 0.f, 0.f});
-      acc[i] = mfma_bf16(wa[i][1], bf1, acc[i]);
+      acc[i] = mfma_bf16(wa[i][0], bfk[0], f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+      for (int kst = 1; kst < NKS; ++kst) acc[i] = mfma_bf16(wa[i][kst], bfk[kst], acc[i]);
     };
     // granule of (row ln, block mb): units 16 mb + 4 kq .. + 3
     const unsigned off0 = (unsigned)(((obase + ln) * (long long)hq + 4 * mw + kq) * 8);
     auto publish = [&](auto aux) {
       auto st = [&](int i) {
-        const int mb = mw + 4 * i;
+        const int mb = mw + NMW * i;
         if (ln < R && mb < HB) {  // C[m][n]: n = ln (row), m = 16 mb + 4 kq + r
           // one granule: units 16 mb + 4 kq .. + 3, tag bit in the first value
-          const unsigned off = off0 + 128u * i;
+          const unsigned off = off0 + 32u * NMW * i;
           // (packed v_cvt_pk_bf16_f32 conversions here, three VALU instead of
           // about twelve, measured 35 us / launch SLOWER in a same-box A/B)
           const unsigned p01 = bf_with_lsb(acc[i][0], tb) | ((unsigned)f2bf(acc[i][1]) << 16);
@@ -1317,9 +1342,10 @@ int lstm_bwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* wh
   if (!xg_enabled()) return 0;
   const int R = xg_rows(B, H);
   if (!R) return 0;
-  const int mb = (H / XU + 3) / 4;
+  const int xb = xg_bwd_xu(R, H);
+  const int mb = (H / 16 + xb / 4 - 1) / (xb / 4);   // M blocks per MFMA wave
   if (mb > 16) return 0;
-  const int grid = 2 * ((B + R - 1) / R) * (H / XU);
+  const int grid = 2 * ((B + R - 1) / R) * (H / xb);
   int* hdr = (int*)ws;
   unsigned long long* g = (unsigned long long*)((char*)ws + XG_HDR);
   const unsigned ep = xg_bwd_seq(true);
@@ -1329,18 +1355,30 @@ int lstm_bwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* wh
   const int io_pos = (li && atoi(li) == 1) ? 1 : 0;
   const char* s16 = getenv("ASR_XG_DG_ST16");   // A/B: bf16 dG by 16-B stores from LDS
   const int st16 = (s16 && s16[0] == '0') ? 0 : 1;
-#define ASR_XGB2(RR, M, AHV)                                                                    \
+#define ASR_XGB3(RR, M, AHV, XBV)                                                               \
   do {                                                                                          \
-    if (!xg_fits(lstm_bwd_xg<RR, M, AHV>, 512 + RR * XU, pin)) {                                \
+    if (!xg_fits(lstm_bwd_xg<RR, M, AHV, XBV>, 256 + (RR + 16) * XBV, pin)) {                   \
       if (pin != XG_PIN_BWD) xg_warn_pin_unfit(pin);                                             \
       return 0;                                                                                 \
     }                                                                                           \
     if (dry) return 1;                                                                          \
     if (hipMemsetAsync(ws, 0, lstm_xg_bwd_bytes(B, H), s) != hipSuccess) return -1;             \
-    xg_trace_setup(s);             \
-    hipLaunchKernelGGL((lstm_bwd_xg<RR, M, AHV>), dim3(grid), dim3(512 + RR * XU), pin, s, B, T, \
-                       H, lens, whh_f, whh_r, dy, act_dg, cst, g, hdr, dgbf, dbpart, ep, al,     \
-                       (dg_f32 || !dgbf) ? 1 : 0, io_pos, st16, (const h16x4*)acth);            \
+    xg_trace_setup(s);                                                                          \
+    hipLaunchKernelGGL((lstm_bwd_xg<RR, M, AHV, XBV>), dim3(grid), dim3(256 + (RR + 16) * XBV),   \
+                       pin, s,                                                                  \
+                       B, T, H, lens, whh_f, whh_r, dy, act_dg, cst, g, hdr, dgbf, dbpart, ep,   \
+                       al, (dg_f32 || !dgbf) ? 1 : 0, io_pos, st16, (const h16x4*)acth);        \
+  } while (0)
+#define ASR_XGB2(RR, M, AHV)                                  \
+  do {                                                        \
+    bool done32 = false;                                      \
+    if constexpr (RR == 8 && M <= 4) {                        \
+      if (xb == 32) {                                         \
+        ASR_XGB3(RR, M, AHV, 32);                             \
+        done32 = true;                                        \
+      }                                                       \
+    }                                                         \
+    if (!done32) ASR_XGB3(RR, M, AHV, 16);                    \
   } while (0)
 #define ASR_XGB(RR, M)                        \
   do {                                        \
@@ -1361,6 +1399,7 @@ int lstm_bwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* wh
 #undef ASR_XGB_M
 #undef ASR_XGB
 #undef ASR_XGB2
+#undef ASR_XGB3
   return hipGetLastError() == hipSuccess ? 1 : -1;
 }
 
@@ -1503,6 +1542,27 @@ extern "C" int asr_lstm_set_bwd_pin_kb(int kb) {
   ASR_REQUIRE(kb == 0 || (kb > 80 && kb <= 160), ASR_ERR_ARG, "lstm pin: %d KB", kb);
   asr::g_pin_bwd_kb = kb;
   return ASR_OK;
+}
+
+// Units per work-group of the backward recurrence for the launches that follow
+// (0: ASR_XG_BWD_XU or 16; 16; 32 -- half the work-groups, see lstm_bwd_xg).
+extern "C" int asr_lstm_set_bwd_units(int xu) {
+  ASR_REQUIRE(xu == 0 || xu == 16 || xu == 32, ASR_ERR_ARG, "lstm units: %d", xu);
+  asr::g_bwd_xu = xu;
+  return ASR_OK;
+}
+
+// Work-groups of the tagged-granule backward recurrence for [B, *, H] with xu
+// units per work-group (0: the current setting), 0 if the shape cannot take it.
+extern "C" int asr_lstm_backward_grid(int B, int H, int xu) {
+  const int R = asr::xg_rows(B, H);
+  if (!R) return 0;
+  int xb = 16;
+  if (xu == 0) xb = asr::xg_bwd_xu(R, H);
+  else if (xu == 32) xb = (R == 8 && H % 32 == 0 && (H / 16 + 3) / 4 <= 8) ? 32 : 0;
+  else if (xu != 16) return 0;
+  if (!xb) return 0;
+  return 2 * ((B + R - 1) / R) * (H / xb);
 }
 
 // Diagnostics: the backward recurrence's dh / spin-count recorders (NULL: off).

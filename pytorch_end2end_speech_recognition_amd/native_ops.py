@@ -938,8 +938,11 @@ class BLSTMLayerFn(torch.autograd.Function):
         # recurrence perturbs it)
         notify_grad_event('pre_recurrence')
         # the recurrence's LDS pin: co-resident GEMM work-groups only in the
-        # opt-in mode 2 (84 KB); otherwise 140 KB excludes every GEMM kernel
-        N.call('asr_lstm_set_bwd_pin_kb', 84 if _overlap_mode(dev, B, H) == '2' else 0)
+        # opt-in mode 2 (84 KB); otherwise 140 KB excludes every GEMM kernel.
+        # Units per work-group: 32 where that frees the CUs for mode 3.
+        mode, xu = _overlap_plan(dev, B, H)
+        N.call('asr_lstm_set_bwd_pin_kb', 84 if mode == '2' else 0)
+        N.call('asr_lstm_set_bwd_units', xu)
         if act.dtype == torch.float16:
             # packed fp16 activations of asr_lstm_forward_xh: the tagged-granule
             # backward reads them directly; otherwise they are unpacked to f32
@@ -974,6 +977,7 @@ class BLSTMLayerFn(torch.autograd.Function):
                    N.ptr(lens), B, T, H, cd, N.ptr(act), N.ptr(cst), N.ptr(dg_bf), N.ptr(ws), nb,
                    N.stream_handle(dev))
             colsum_accumulate(act.view(B * T, 8 * H), gbufs[2], gbufs[3])
+        N.call('asr_lstm_set_bwd_units', 0)     # direct API callers: the default again
         # weight gradients of the layer above, if they went to a side stream: join
         # them here (they run beside the recurrence just enqueued) so the
         # gradient-ready bucket sees them on the compute stream
@@ -1226,20 +1230,25 @@ def _num_cus(dev):
     return torch.cuda.get_device_properties(dev).multi_processor_count
 
 
-def _xg_grid(B, H, ncu):
+def _xg_grid(B, H, ncu, xu=16):
     """Work-groups of the persistent recurrence (lstm_xg.hip xg_rows): groups of
-    R = 8 utterances (16 when 8 would not fit) x direction x H / 16 slices."""
+    R = 8 utterances (16 when 8 would not fit) x direction x H / xu slices --
+    the backward's xu = 32 (asr_lstm_backward_grid) only with R = 8, H <= 512."""
     if H % 32 or H // 16 > 64 or os.environ.get('ASR_LSTM_XG', '1') == '0':
         return 1 << 30        # not the tagged-granule recurrence
     for R in (8, 16):
         g = 2 * ((B + R - 1) // R) * (H // 16)
         if g <= ncu:
+            if xu == 32:
+                return g // 2 if R == 8 and H <= 512 else 1 << 30
             return g
     return 1 << 30
 
 
-def _overlap_mode(dev, B, H):
-    """The resolved ASR_OVERLAP_WGRAD mode for a BLSTM layer's backward:
+def _overlap_plan(dev, B, H):
+    """(mode, units): the resolved ASR_OVERLAP_WGRAD mode for a BLSTM layer's
+    backward and the hidden units per work-group of its backward recurrence.
+    Modes:
       '0'  weight gradients on the compute stream;
       '1'  a CU-masked side stream (upper half of the CUs), only when the
            persistent backward recurrence fits in the other half;
@@ -1250,22 +1259,37 @@ def _overlap_mode(dev, B, H):
       '3'  a plain side stream with the recurrence at its default 140 KB pin,
            so no GEMM work-group can share a CU with it: the weight-gradient
            GEMMs run on the CUs the recurrence leaves free.
-    auto = '3' when the recurrence leaves at least 32 CUs free (the H = 320
-    configs: 160 of 256 CUs), else '0'.  All need bf16 and the persistent
-    recurrence."""
+    auto = '3' when the recurrence leaves at least 32 CUs free -- with 16 units
+    per work-group (the H = 320 configs: 160 of 256 CUs) or else with 32
+    (ctc5x512: 128 of 256 CUs; ASR_XG_BWD_XU=16 keeps 16 and mode '0') --
+    otherwise '0'.  Units: ASR_XG_BWD_XU=16|32 forces them; auto takes 32 only
+    for mode 3 when 16 would leave fewer than 32 CUs.  All modes need bf16 and
+    the persistent recurrence."""
     mode = os.environ.get('ASR_OVERLAP_WGRAD', 'auto')
+    xu_env = os.environ.get('ASR_XG_BWD_XU', 'auto')
+    forced = 32 if xu_env == '32' else 16
     if compute_dtype() != BF16 or os.environ.get('ASR_LSTM_PERSIST', '1') == '0' or H % 32:
-        return '0'
+        return '0', forced
     ncu = _num_cus(dev)
+    roomy16 = _xg_grid(B, H, ncu) + 32 <= ncu
+    roomy32 = _xg_grid(B, H, ncu, 32) + 32 <= ncu
     if mode == 'auto':
-        mode = '3' if _xg_grid(B, H, ncu) + 32 <= ncu else '0'
+        mode = '3' if roomy16 or (xu_env != '16' and roomy32) else '0'
     elif mode == '2':
         _warn_once('ASR_OVERLAP_WGRAD=2: weight-gradient GEMMs co-resident with the backward '
                    'recurrence give run-to-run different (wrong) recurrence results on '
                    'gfx950 (DESIGN.md §5); use for timing experiments only')
     if mode == '1' and _xg_grid(B, H, 2 * (ncu - ncu // 2)) > ncu // 2:
         mode = '0'
-    return mode if mode in ('1', '2', '3') else '0'
+    mode = mode if mode in ('1', '2', '3') else '0'
+    if xu_env in ('16', '32'):
+        return mode, forced
+    return mode, (32 if mode == '3' and not roomy16 and roomy32 else 16)
+
+
+def _overlap_mode(dev, B, H):
+    """The resolved ASR_OVERLAP_WGRAD mode (see _overlap_plan)."""
+    return _overlap_plan(dev, B, H)[0]
 
 
 def _wgrad_side_stream(dev, B, H):

@@ -274,7 +274,8 @@ def test_wgrad_overlap_auto_mode(monkeypatch):
     """auto: the weight-gradient GEMMs go to a side stream (mode 3, the
     recurrence at its 140 KB LDS pin so no GEMM work-group can share its CUs)
     when the persistent backward recurrence leaves >= 32 of the 256 CUs free
-    (the H = 320 configs), else they stay on the compute stream; co-resident
+    (the H = 320 configs; ctc5x512 with 32 units per backward work-group),
+    else they stay on the compute stream; co-resident
     GEMMs (mode 2) are never chosen automatically."""
     from pytorch_end2end_speech_recognition_amd import native_ops
     monkeypatch.delenv('ASR_OVERLAP_WGRAD', raising=False)
@@ -283,7 +284,13 @@ def test_wgrad_overlap_auto_mode(monkeypatch):
     native_ops.set_compute_dtype('bf16')
     try:
         cpu = torch.device('cpu')
-        assert native_ops._overlap_mode(cpu, 32, 512) == '0'     # 256 work-groups
+        # 5x512: 256 work-groups at 16 units each, 128 at 32 -> mode 3 with 32
+        assert native_ops._overlap_plan(cpu, 32, 512) == ('3', 32)
+        assert native_ops._overlap_plan(cpu, 32, 320) == ('3', 16)
+        assert native_ops._overlap_plan(cpu, 64, 512) == ('0', 16)   # 256 even at 32
+        monkeypatch.setenv('ASR_XG_BWD_XU', '16')
+        assert native_ops._overlap_mode(cpu, 32, 512) == '0'
+        monkeypatch.delenv('ASR_XG_BWD_XU')
         assert native_ops._overlap_mode(cpu, 32, 320) == '3'     # 160
         assert native_ops._overlap_mode(cpu, 16, 256) == '3'     # 64
         assert native_ops._overlap_mode(cpu, 32, 500) == '0'     # no persistent recurrence

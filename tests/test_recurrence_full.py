@@ -110,9 +110,13 @@ def _rel(a, ref):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('prec,bound', [('bf16', 2e-2), ('fp32', 1e-4)])
-def test_full_shape_layer_vs_float64_oracle(prec, bound, cuda_dev):
+@pytest.mark.parametrize('prec,bound,xu', [('bf16', 2e-2, '16'), ('bf16', 2e-2, '32'),
+                                           ('fp32', 1e-4, '16')])
+def test_full_shape_layer_vs_float64_oracle(prec, bound, xu, cuda_dev, monkeypatch):
+    """xu: hidden units per work-group of the backward recurrence (32: half the
+    work-groups, the default of the ctc5x512 layer's mode-3 overlap)."""
     from test_encoder_gpu import _xg_mode
+    monkeypatch.setenv('ASR_XG_BWD_XU', xu)
     case = _case(0.03)
     ref = _oracle(*case)
     _xg_mode()                                   # clear
@@ -122,8 +126,8 @@ def test_full_shape_layer_vs_float64_oracle(prec, bound, cuda_dev):
     names = ['y', 'dx', 'dW_ih', 'dW_hh', 'db_ih', 'db_hh']
     refs = list(ref[:4]) + [ref[4], ref[4]]
     errs = {n: _rel(g, r) for n, g, r in zip(names, got, refs)}
-    print('\n%s full-shape max error / max|ref|: %s' % (
-        prec, ', '.join('%s %.2e' % kv for kv in errs.items())))
+    print('\n%s xu=%s full-shape max error / max|ref|: %s' % (
+        prec, xu, ', '.join('%s %.2e' % kv for kv in errs.items())))
     for n, e in errs.items():
         assert e <= bound, (prec, n, e, bound)
 
@@ -206,3 +210,52 @@ def test_packed_gate_activations_saturated_vs_float64(cuda_dev, monkeypatch):
         assert out['1'][n] <= 2e-2, ('ACT_H=1', n, out['1'][n])
         assert out['1'][n] <= 1.5 * out['0'][n] + 2e-3, (n, out['1'][n], out['0'][n])
     assert out['1']['db_row_median'] <= 1.5 * out['0']['db_row_median'] + 2e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('Bs,Ts,Hs,Ds', [(20, 96, 384, 128), (9, 64, 512, 64), (8, 40, 64, 32)])
+def test_backward_units_per_workgroup_vs_float64(Bs, Ts, Hs, Ds, cuda_dev, monkeypatch):
+    """The backward recurrence with 32 hidden units per work-group (lstm_bwd_xg
+    XB = 32: 16-B sweeps of four 8-unit quarters, 8 MFMA waves over 128 gate
+    rows) against float64 and against 16 units per work-group: ragged batches
+    that do not fill the last 8-row group, H = 384 (M blocks past the last in
+    the clamped MFMA waves), H = 512 and H = 64 (two producers per group)."""
+    from test_encoder_gpu import _xg_mode
+    global B, T, H
+    rng = np.random.RandomState(Bs + Hs)
+    lens = np.sort(rng.randint(Ts // 2, Ts + 1, Bs))[::-1].astype(np.int32)
+    lens[0] = Ts
+    x = (rng.randn(Bs, Ts, Ds) * 0.5).astype(np.float32)
+    for b in range(Bs):
+        x[b, lens[b]:] = 0
+    g = torch.Generator().manual_seed(Hs)
+    w_ih = torch.rand(8 * Hs, Ds, generator=g) * 0.2 - 0.1
+    w_hh = (torch.rand(8 * Hs, Hs, generator=g) * 2 - 1) * 0.03
+    b_ih = torch.rand(8 * Hs, generator=g) * 0.2 - 0.1
+    b_hh = torch.rand(8 * Hs, generator=g) * 0.2 - 0.1
+    dy = torch.from_numpy(rng.randn(Bs, Ts, 2 * Hs).astype(np.float32))
+    for b in range(Bs):
+        dy[b, lens[b]:] = 0
+    case = (lens, torch.from_numpy(x), w_ih, w_hh, b_ih, b_hh, dy)
+    saved = (B, T, H)
+    B, T, H = Bs, Ts, Hs
+    try:
+        ref = _oracle(*case)
+        res = {}
+        for xu in ('16', '32'):
+            monkeypatch.setenv('ASR_XG_BWD_XU', xu)
+            _xg_mode()
+            res[xu] = _gpu('bf16', *case, cuda_dev)
+            assert _xg_mode() != 0, 'the persistent tagged-granule recurrence did not run'
+    finally:
+        B, T, H = saved
+    names = ['y', 'dx', 'dW_ih', 'dW_hh', 'db']
+    refs = list(ref[:4]) + [ref[4]]
+    out = {xu: {n: float((gg - r).norm() / r.norm()) for n, gg, r in zip(names, got[:5], refs)}
+           for xu, got in res.items()}
+    print('\nunits per work-group, rel. L2 vs float64: 16 %s | 32 %s' % (out['16'], out['32']))
+    # the forward is the same kernel either way
+    assert torch.equal(res['16'][0], res['32'][0])
+    for n in names:
+        assert out['32'][n] <= 2e-2, (n, out['32'][n])
+        assert out['32'][n] <= 1.5 * out['16'][n] + 2e-3, (n, out['32'][n], out['16'][n])
