@@ -275,6 +275,19 @@ int asr_lstm_forward_xh(const uint16_t* x, int Din, const uint16_t* wih, const f
                         const int32_t* lens, int B, int T, int H, uint16_t* act_h, float* y,
                         float* cst, uint16_t* ybf, void* workspace, size_t ws_bytes,
                         void* stream);
+/* asr_lstm_forward_xh for a layer whose output feeds only the next BLSTM
+ * layer's staged bf16 input (the stacked nn.LSTM layers of
+ * models/pytorch_v3/encoders/rnn.py:343-390 with dropout between them,
+ * rnn.py:398): y may be NULL (the f32 output is then not written); ydrop,
+ * when non-NULL, receives bf16(dropout(y)) [B][T][2H] with asr_dropout's mask
+ * for (drop_p, drop_seed) -- what asr_convert_rows_bf16_dropout would stage
+ * from y; ybf (bf16 y) is required. */
+int asr_lstm_forward_xh_drop(const uint16_t* x, int Din, const uint16_t* wih, const float* b_ih,
+                             const float* b_hh, const float* whh_f, const float* whh_r,
+                             const int32_t* lens, int B, int T, int H, uint16_t* act_h,
+                             float* y, float* cst, uint16_t* ybf, uint16_t* ydrop, float drop_p,
+                             unsigned long long drop_seed, void* workspace, size_t ws_bytes,
+                             void* stream);
 /* asr_lstm_backward_dgbf reading act_h of asr_lstm_forward_xh (tagged-granule
  * recurrence only; ASR_ERR_UNSUPPORTED otherwise).  Same workspace. */
 int asr_lstm_backward_dgbf_h(const float* dy, const void* whh_f, const void* whh_r, int w_dtype,

@@ -84,6 +84,9 @@ SIGNATURES = {
     'asr_lstm_forward_x_ok': (c_int, [c_int, c_int, c_int]),
     'asr_lstm_forward_xh': (c_int, [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int,
                                     c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
+    'asr_lstm_forward_xh_drop': (c_int, [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
+                                         c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_float,
+                                         ctypes.c_ulonglong, c_vp, c_size, c_vp]),
     'asr_lstm_backward_dgbf_h': (c_int, [c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int,
                                          c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
     'asr_diag_lds_spin': (c_int, [c_int, c_int, c_vp, c_vp]),

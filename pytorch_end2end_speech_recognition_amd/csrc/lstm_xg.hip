@@ -536,7 +536,8 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
     const uint16_t* __restrict__ wih, const float* __restrict__ b_ih,
     const float* __restrict__ b_hh, float* __restrict__ act, float* __restrict__ y,
     float* __restrict__ cst, unsigned long long* xg, int* hdr, uint16_t* __restrict__ ybf,
-    int allow_local, int late_load, int defer_st, h16x4* __restrict__ acth) {
+    int allow_local, int late_load, int defer_st, h16x4* __restrict__ acth,
+    uint16_t* __restrict__ ydrop, float drop_p, unsigned long long drop_seed) {
   (void)late_load;   // input rows now staged by LDS DMA three steps ahead
   __shared__ float part[2][NSW][R][4 * XU + 4];
   __shared__ float xpart[2][NPW][R][4 * XU + 4];
@@ -751,11 +752,14 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
   // (ahead of step s+1's cell math) instead of right after Bp(s), where they
   // share the CU's vector-memory path with the sweepers' polls for step s+1
   float pv[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  unsigned pval = 0u;
+  unsigned pval = 0u, pdval = 0u;
   int pt = -1;
-  auto store_step = [&](int tt, const float* v, unsigned bv) {
+  // ydrop: bf16 dropout(y) with asr_dropout's mask over [B][T][2H] -- the next
+  // layer's staged input, written here instead of from an f32 y (y may be null)
+  const float dscale = 1.f / (1.f - drop_p);
+  auto store_step = [&](int tt, const float* v, unsigned bv, unsigned dv) {
     const long long sidx = ((long long)b * T + tt) * 2 * H + (long long)dir * H + j;
-    y[sidx] = v[0];
+    if (y) y[sidx] = v[0];
     cst[sidx] = v[1];
     if (acth) {   // the four gates of (b, t, dir, j) as one 8-B fp16 store (enc_sig / enc_tanh)
       const h16x4 hv = {(_Float16)enc_sig(v[2]), (_Float16)enc_sig(v[3]), (_Float16)enc_tanh(v[4]),
@@ -770,12 +774,14 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
     }
     if (ybf && (unit & 1) == 0)
       *reinterpret_cast<uint32_t*>(ybf + ((long long)b * T + tt) * 2 * H + dir * H + j) = bv;
+    if (ydrop && (unit & 1) == 0)
+      *reinterpret_cast<uint32_t*>(ydrop + ((long long)b * T + tt) * 2 * H + dir * H + j) = dv;
   };
   for (int s = 0; s < T; ++s) {
     const int t = dir ? T - 1 - s : s;
     __syncthreads();  // B(s)
     if (s_dead) return;
-    if (defer_st && own && pt >= 0) store_step(pt, pv, pval);
+    if (defer_st && own && pt >= 0) store_step(pt, pv, pval, pdval);
     float h = 0.f, cn = 0.f, ig = 0.f, fg = 0.f, gg = 0.f, og = 0.f;
     const bool active = own && t < len;
     if (active) {
@@ -814,7 +820,12 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
     pv[0] = h; pv[1] = cn; pv[2] = ig; pv[3] = fg; pv[4] = gg; pv[5] = og;
     pval = val;
     pt = t;
-    if (own && (!defer_st || s + 1 == T)) store_step(t, pv, pval);
+    if (ydrop) {   // off the hand-off chain: the sweepers are polling for step s + 1
+      const long long sidx = ((long long)b * T + t) * 2 * H + (long long)dir * H + j;
+      const unsigned db = f2bf(u01(drop_seed, (unsigned long long)sidx) >= drop_p ? h * dscale : 0.f);
+      pdval = db | (row_from_upper<1>(db) << 16);
+    }
+    if (own && (!defer_st || s + 1 == T)) store_step(t, pv, pval, pdval);
     if (s + 1 < T) {  // the producers wrote pre(s+1) before B(s)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -1411,7 +1422,9 @@ constexpr int XGX_NPW = 6;   // 12 waves: 3 per SIMD, 170 registers per wave (8:
 int lstm_fwd_xgx_launch(int B, int T, int H, const int32_t* lens, const float* whh_f,
                         const float* whh_r, const uint16_t* x, int Din, const uint16_t* wih,
                         const float* b_ih, const float* b_hh, float* act, float* y, float* cst,
-                        void* ws, uint16_t* ybf, hipStream_t s, bool dry, uint16_t* acth) {
+                        void* ws, uint16_t* ybf, hipStream_t s, bool dry, uint16_t* acth,
+                        uint16_t* ydrop = nullptr, float drop_p = 0.f,
+                        unsigned long long drop_seed = 0) {
   if (!xg_enabled()) return 0;
   const char* e = getenv("ASR_FUSE_XPROJ");
   if (e && e[0] == '0') return 0;
@@ -1446,7 +1459,7 @@ int lstm_fwd_xgx_launch(int B, int T, int H, const int32_t* lens, const float* w
     xg_trace_setup(s);                                                                          \
     hipLaunchKernelGGL(kfn, dim3(grid), dim3(threads), pin, s, B, T, H, lens, whh_f, whh_r, x,  \
                        Din, wih, b_ih, b_hh, act, y, cst, g, hdr, ybf, al, late, defer,          \
-                       (h16x4*)acth);                                                            \
+                       (h16x4*)acth, ydrop, drop_p, drop_seed);                                  \
   } while (0)
 #define ASR_XGX_P(KS)                    \
   do {                                   \
@@ -1682,6 +1695,41 @@ extern "C" int asr_lstm_forward_xh(const uint16_t* x, int Din, const uint16_t* w
   const int rc = asr::lstm_fwd_xgx_launch(B, T, H, lens, whh_f, whh_r, x, Din, wih, b_ih, b_hh,
                                           nullptr, y, cst, workspace, ybf, s, false, act_h);
   ASR_REQUIRE(rc == 1, ASR_ERR_HIP, "lstm_forward_xh: launch failed");
+  asr::prof_end_launch(ASR_PROF_LSTM_FWD_SEQ, slot, s);
+  return ASR_OK;
+}
+
+// asr_lstm_forward_xh for a layer whose consumer is the next BLSTM layer's
+// staged bf16 input: y (the f32 output) may be NULL -- not written -- and ydrop
+// (non-NULL) receives bf16(dropout(y)) with asr_dropout's mask for (drop_p,
+// drop_seed) over the [B][T][2H] output, i.e. exactly what
+// asr_convert_rows_bf16_dropout would stage from y.  ybf (bf16 y, the dW_hh
+// operand) is required.
+extern "C" int asr_lstm_forward_xh_drop(const uint16_t* x, int Din, const uint16_t* wih,
+                                        const float* b_ih, const float* b_hh, const float* whh_f,
+                                        const float* whh_r, const int32_t* lens, int B, int T,
+                                        int H, uint16_t* act_h, float* y, float* cst,
+                                        uint16_t* ybf, uint16_t* ydrop, float drop_p,
+                                        unsigned long long drop_seed, void* workspace,
+                                        size_t ws_bytes, void* stream) {
+  ASR_REQUIRE(x && wih && b_ih && b_hh && whh_f && whh_r && lens && act_h && cst && ybf &&
+              workspace, ASR_ERR_ARG, "lstm_forward_xh_drop: null pointer");
+  ASR_REQUIRE(B > 0 && T > 0 && H > 0 && Din > 0, ASR_ERR_ARG, "lstm_forward_xh_drop: bad shape");
+  ASR_REQUIRE(drop_p >= 0.f && drop_p < 1.f, ASR_ERR_ARG, "lstm_forward_xh_drop: p=%f",
+              (double)drop_p);
+  ASR_REQUIRE(((uintptr_t)act_h & 7) == 0 && ((uintptr_t)ybf & 3) == 0 &&
+              ((uintptr_t)ydrop & 3) == 0, ASR_ERR_ARG, "lstm_forward_xh_drop: misaligned");
+  hipStream_t s = (hipStream_t)stream;
+  if (asr::lstm_fwd_xgx_launch(B, T, H, lens, whh_f, whh_r, x, Din, wih, b_ih, b_hh, nullptr, y,
+                               cst, workspace, ybf, s, true, act_h) != 1)
+    return ASR_ERR_UNSUPPORTED;
+  ASR_REQUIRE(ws_bytes >= asr::lstm_xg_fwd_bytes(B, H), ASR_ERR_WORKSPACE,
+              "lstm_forward_xh_drop: workspace too small");
+  const int slot = asr::prof_begin_launch(ASR_PROF_LSTM_FWD_SEQ, s, 0.0, ASR_PTAG_LSTM_FWD_XGX);
+  const int rc = asr::lstm_fwd_xgx_launch(B, T, H, lens, whh_f, whh_r, x, Din, wih, b_ih, b_hh,
+                                          nullptr, y, cst, workspace, ybf, s, false, act_h, ydrop,
+                                          drop_p, drop_seed);
+  ASR_REQUIRE(rc == 1, ASR_ERR_HIP, "lstm_forward_xh_drop: launch failed");
   asr::prof_end_launch(ASR_PROF_LSTM_FWD_SEQ, slot, s);
   return ASR_OK;
 }

@@ -190,15 +190,30 @@ class RNNEncoder(nn.Module):
                 h = ops.bgru_layer(h, lens_d, T, w_ih, w_hh, b_ih, b_hh, perm=pm, t_mul=t_mul,
                                    t_add=t_add, gbufs=tuple(gbufs), graph_params=graph,
                                    concat=concat)
-            else:
+            # this layer's output feeds only the next BLSTM layer, through an
+            # identity row map: bf16 mode hands it over as that layer's staged
+            # bf16 input (dropout applied) instead of an f32 tensor
+            handoff = (self.rnn_type != 'gru' and ops.fuse_dropout_ok() and
+                       l < self.num_layers - 1 and
+                       not (self.num_layers_sub >= 1 and l == self.num_layers_sub - 1) and
+                       not (self.residual or self.dense_residual or self.num_proj > 0) and
+                       not self.subsample_list[l])
+            drop_out = self.training and self.dropout_hidden_p > 0
+            # same seed stream either way (one seed per layer, drawn in order)
+            seed = ops.next_seed() if drop_out and handoff else None
+            if self.rnn_type != 'gru':
                 h = ops.blstm_layer(h, lens_d, T, w_ih, w_hh, b_ih, b_hh, perm=pm, t_mul=t_mul,
                                     t_add=t_add, gbufs=tuple(gbufs), graph_params=graph,
-                                    concat=concat, drop=pending, next_rec=l > 0)
+                                    concat=concat, drop=pending, next_rec=l > 0,
+                                    bf16_handoff=handoff,
+                                    out_drop=(self.dropout_hidden_p, seed) if seed is not None
+                                    else None)
             pending = None
-            if self.training and self.dropout_hidden_p > 0:
-                # same seed stream either way; fused when the next consumer is the
-                # next layer's input staging and nothing else reads the dropped h
-                seed = ops.next_seed()
+            if drop_out:
+                # fused when the next consumer is the next layer's input staging
+                # and nothing else reads the dropped h
+                if seed is None:
+                    seed = ops.next_seed()
                 if (ops.fuse_dropout_ok() and l < self.num_layers - 1 and
                         not (self.num_layers_sub >= 1 and l == self.num_layers_sub - 1) and
                         not (self.residual or self.dense_residual or self.num_proj > 0) and

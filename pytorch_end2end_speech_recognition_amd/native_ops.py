@@ -833,9 +833,11 @@ class BLSTMLayerFn(torch.autograd.Function):
     directly (exact-f32 MFMA, parity mode)."""
 
     @staticmethod
-    def forward(ctx, x_src, lens, T, perm, t_mul, t_add, gbufs, concat, drop, next_rec, w_ih, w_hh,
-                b_ih, b_hh, *graph_params):
+    def forward(ctx, x_src, lens, T, perm, t_mul, t_add, gbufs, concat, drop, next_rec, out_spec,
+                w_ih, w_hh, b_ih, b_hh, *graph_params):
         N.require_device(x_src, lens, w_ih, w_hh, b_ih, b_hh)
+        # the layer below handed its output over as staged bf16 (bf16_handoff)
+        twin = _handoff_input(x_src, perm, t_mul, t_add, T, concat, drop, w_ih.shape[1])
         x_src = x_src.contiguous()
         fused_drop = drop is not None and compute_dtype() == BF16 and not concat
         if drop is not None and not fused_drop:   # materialise dropout(x_src) first
@@ -856,7 +858,11 @@ class BLSTMLayerFn(torch.autograd.Function):
         fuse_x = False
         gx = None       # f32 gate pre-activations -> activations [B, T, 8H], or
         Dp = Din        # packed fp16 activations [B, T, 2, H, 4] (fused bf16 path)
-        if cd == BF16:
+        if twin is not None:
+            x_op = twin.view(B * T, Din)
+            w_op = convert_rows_bf16(w_ih, rowmap(Din), 8 * H, Din)   # [8H, Din]
+            y_bf = torch.empty(B, T, 2 * H, dtype=torch.bfloat16, device=dev)
+        elif cd == BF16:
             if Din % 8 and not fused_drop:
                 # an input width that is not a multiple of 8 (TIMIT's 123) is
                 # staged with zero-padded rows of Dp columns, so the fused
@@ -879,21 +885,37 @@ class BLSTMLayerFn(torch.autograd.Function):
         nb = N.query('asr_lstm_workspace_bytes', B, H, cd, 0)
         ws = _ws(nb, dev)
         whh_r = w_hh.data_ptr() + 4 * H * H * 4
+        y_f32, out_drop = out_spec
+        handoff = None     # (bf16 tensor the next layer stages from, its dropout)
         if cd == BF16 and _fuse_xproj_on():
             # the input projection inside the persistent recurrence (no gx GEMM);
             # ASR_ERR_UNSUPPORTED when this shape / configuration does not take it.
             # The gate activations are kept as packed fp16 (8 B per cell instead
             # of 16; ASR_XG_ACT_H=0 keeps the f32 layout)
-            if _act_h_on():
+            args = (N.ptr(x_op), Dp, N.ptr(w_op), N.ptr(b_ih), N.ptr(b_hh), N.ptr(w_hh),
+                    ctypes.c_void_p(whh_r), N.ptr(lens), B, T, H)
+            if _act_h_on() and not y_f32:
+                # the next BLSTM layer stages its input from bf16 written here (its
+                # dropout applied): no f32 y, no conversion pass
                 gx = torch.empty(B, T, 2, H, 4, dtype=torch.float16, device=dev)
-                fn = 'asr_lstm_forward_xh'
+                fn = 'asr_lstm_forward_xh_drop'
+                y_d = (torch.empty(B, T, 2 * H, dtype=torch.bfloat16, device=dev)
+                       if out_drop is not None else None)
+                p, seed = out_drop if out_drop is not None else (0.0, 0)
+                rc = N.query(fn, *args, N.ptr(gx), None, N.ptr(cst), N.ptr(y_bf),
+                             N.ptr(y_d) if y_d is not None else None, ctypes.c_float(p),
+                             ctypes.c_ulonglong(seed), N.ptr(ws), nb, N.stream_handle(dev))
+                if rc == 0:
+                    handoff = (y_d if y_d is not None else y_bf, out_drop)
             else:
-                gx = torch.empty(B, T, 8 * H, dtype=torch.float32, device=dev)
-                fn = 'asr_lstm_forward_x'
-            rc = N.query(fn, N.ptr(x_op), Dp, N.ptr(w_op), N.ptr(b_ih),
-                         N.ptr(b_hh), N.ptr(w_hh), ctypes.c_void_p(whh_r), N.ptr(lens), B, T, H,
-                         N.ptr(gx), N.ptr(y), N.ptr(cst), N.ptr(y_bf), N.ptr(ws), nb,
-                         N.stream_handle(dev))
+                if _act_h_on():
+                    gx = torch.empty(B, T, 2, H, 4, dtype=torch.float16, device=dev)
+                    fn = 'asr_lstm_forward_xh'
+                else:
+                    gx = torch.empty(B, T, 8 * H, dtype=torch.float32, device=dev)
+                    fn = 'asr_lstm_forward_x'
+                rc = N.query(fn, *args, N.ptr(gx), N.ptr(y), N.ptr(cst), N.ptr(y_bf), N.ptr(ws),
+                             nb, N.stream_handle(dev))
             if rc not in (0, N.ASR_ERR_UNSUPPORTED):
                 raise N.NativeError('%s failed (rc=%d): %s' % (
                     fn, rc, N.lib().asr_last_error().decode(errors='replace')))
@@ -917,6 +939,10 @@ class BLSTMLayerFn(torch.autograd.Function):
         ctx.drop = drop
         ctx.next_rec = bool(next_rec)
         ctx.n_graph = len(graph_params)
+        if handoff is not None:
+            # y was not written: only the next BLSTM layer may consume it, through
+            # the bf16 tensor (_handoff_input raises for any other use it sees)
+            y._asr_handoff = handoff
         return y
 
     @staticmethod
@@ -1040,7 +1066,7 @@ class BLSTMLayerFn(torch.autograd.Function):
             p = gemm_problem(operand(dg_op, 0, rowmap(8 * H)), operand(w_op, 1, rowmap(Dp)), dx,
                              c_map, BT, Din, 8 * H, drop=ctx.drop)
             run_gemm([p], dev)
-        return (dx,) + (None,) * (13 + ctx.n_graph)
+        return (dx,) + (None,) * (14 + ctx.n_graph)
 
 
 class BGRULayerFn(torch.autograd.Function):
@@ -1317,7 +1343,8 @@ def _wgrad_side_stream(dev, B, H):
 
 
 def blstm_layer(x_src, lens, T, w_ih, w_hh, b_ih, b_hh, perm=None, t_mul=1, t_add=0, gbufs=None,
-                graph_params=(), concat=False, drop=None, next_rec=False):
+                graph_params=(), concat=False, drop=None, next_rec=False, bf16_handoff=False,
+                out_drop=None):
     """gbufs: optional (g_w_ih, g_w_hh, g_b_ih, g_b_hh) gradient views to accumulate
     into; default: the tensors' own .grad.  graph_params: the nn.Parameters the
     combined [fwd; rev] views alias -- passed only so autograd records that the
@@ -1328,9 +1355,42 @@ def blstm_layer(x_src, lens, T, w_ih, w_hh, b_ih, b_hh, perm=None, t_mul=1, t_ad
     fused into the bf16 input staging; its input gradient gets the same mask.
     next_rec: another BLSTM layer's backward recurrence follows this layer's in
     the backward pass (the layer below), so ASR_OVERLAP_WGRAD=2 can run this
-    layer's weight gradients beside it."""
+    layer's weight gradients beside it.
+    bf16_handoff: the output's only consumer is the next BLSTM layer, reading
+    it through an identity row map with drop=out_drop (its fused dropout, or
+    None): in bf16 mode the fused forward then writes that layer's staged
+    bf16 input (dropout applied) instead of the f32 output, whose tensor is
+    returned unwritten (for autograd; reading it otherwise raises in the next
+    layer, and no other consumer may read it)."""
+    spec = (not (bf16_handoff and compute_dtype() == BF16 and handoff_on()),
+            out_drop if bf16_handoff else None)
     return BLSTMLayerFn.apply(x_src, lens, T, perm, t_mul, t_add, gbufs, bool(concat), drop,
-                              bool(next_rec), w_ih, w_hh, b_ih, b_hh, *graph_params)
+                              bool(next_rec), spec, w_ih, w_hh, b_ih, b_hh, *graph_params)
+
+
+def handoff_on():
+    """ASR_BF16_HANDOFF=0: every BLSTM layer writes its f32 output and the next
+    layer stages it (A/B)."""
+    return os.environ.get('ASR_BF16_HANDOFF', '1') != '0'
+
+
+def _handoff_input(x_src, perm, t_mul, t_add, T, concat, drop, din):
+    """The bf16 tensor a BLSTM layer's input was handed over as (see
+    blstm_layer's bf16_handoff), or None for an ordinary f32 input.  Raises if
+    the input was handed over but this layer cannot read it that way (its f32
+    values were never written)."""
+    h = getattr(x_src, '_asr_handoff', None)
+    if h is None:
+        return None
+    t, hdrop = h
+    B = x_src.shape[0]
+    ok = (compute_dtype() == BF16 and perm is None and t_mul == 1 and t_add == 0 and
+          not concat and x_src.shape[1] == T and x_src.shape[2] == din and din % 8 == 0 and
+          drop == hdrop and t.shape == (B, T, din))
+    if not ok:
+        raise N.NativeError('BLSTM layer input was handed over as bf16 (its f32 values were '
+                            'not written) but this layer cannot stage it that way')
+    return t
 
 
 # ---------------------------------------------------------------------------

@@ -453,6 +453,88 @@ def test_output_dropout_folded_into_head_bitwise(cuda_dev, monkeypatch):
     assert g1.abs().sum().item() > 0
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize('training', [True, False])
+def test_bf16_handoff_between_layers_bitwise(training, cuda_dev, monkeypatch):
+    """bf16 mode: a BLSTM layer whose output feeds only the next one writes that
+    layer's staged bf16 input itself (dropout applied with the same mask,
+    asr_lstm_forward_xh_drop) and no f32 output -- the same loss and gradients,
+    bit for bit, as writing the f32 output and staging it in a separate pass
+    (ASR_BF16_HANDOFF=0), in training (encoder dropout 0.2) and in eval."""
+    from pytorch_end2end_speech_recognition_amd import native_ops
+    kw = dict(input_size=40, encoder_type='lstm', encoder_bidirectional=True,
+              encoder_num_units=256, encoder_num_proj=0, encoder_num_layers=3, fc_list=[],
+              dropout_input=0, dropout_encoder=0.2, num_classes=29, parameter_init=0.1,
+              subsample_list=[], subsample_type='drop')
+    rng = np.random.RandomState(12)
+    B, T = 16, 120
+    x_lens = np.sort(rng.randint(80, T + 1, B)).astype(np.int32)[::-1].copy()
+    x_lens[0] = T
+    y_lens = rng.randint(10, 30, B).astype(np.int32)
+    xs = rng.randn(B, T, 40).astype(np.float32)
+    for b in range(B):
+        xs[b, x_lens[b]:] = 0
+    ys = np.full((B, 30), -1, np.int32)
+    for b in range(B):
+        ys[b, :y_lens[b]] = rng.randint(0, 28, y_lens[b])
+    used = []
+    orig = native_ops._handoff_input
+
+    def spy(*a):
+        t = orig(*a)
+        used.append(t is not None)
+        return t
+
+    monkeypatch.setattr(native_ops, '_handoff_input', spy)
+    outs = {}
+    native_ops.set_compute_dtype('bf16')
+    try:
+        for on in ('1', '0'):
+            monkeypatch.setenv('ASR_BF16_HANDOFF', on)
+            native_ops.manual_seed(99)
+            del used[:]
+            model = _build(kw)
+            model.set_cuda()
+            model.train(training)
+            model.zero_grad()
+            loss = model(xs, ys, x_lens, y_lens)
+            loss.backward()
+            torch.cuda.synchronize()
+            outs[on] = (loss.item(), model._flat_grad.clone(), list(used))
+    finally:
+        native_ops.set_compute_dtype('fp32')
+    assert outs['1'][2] == [False, True, True], outs['1'][2]    # layers 1 and 2 took it
+    assert outs['0'][2] == [False, False, False]
+    assert outs['1'][0] == outs['0'][0], (outs['1'][0], outs['0'][0])
+    assert torch.equal(outs['1'][1], outs['0'][1])
+    assert outs['1'][1].abs().sum().item() > 0
+
+
+def test_handoff_input_refuses_other_reads(monkeypatch):
+    """A handed-over layer output (its f32 values never written) is readable
+    only as the next layer's identity-mapped input with the same dropout:
+    anything else raises instead of reading the unwritten tensor."""
+    from pytorch_end2end_speech_recognition_amd import native_ops
+    prev = native_ops.compute_dtype()
+    native_ops.set_compute_dtype('bf16')
+    try:
+        y = torch.empty(2, 5, 16)
+        tw = torch.zeros(2, 5, 16, dtype=torch.bfloat16)
+        y._asr_handoff = (tw, (0.2, 7))
+        assert native_ops._handoff_input(y, None, 1, 0, 5, False, (0.2, 7), 16) is tw
+        assert native_ops._handoff_input(torch.empty(2, 5, 16), None, 1, 0, 5, False, None,
+                                         16) is None
+        for args in [(torch.zeros(2, dtype=torch.int32), 1, 0, 5, False, (0.2, 7), 16),
+                     (None, 2, 1, 2, False, (0.2, 7), 16),
+                     (None, 1, 0, 5, True, (0.2, 7), 32),
+                     (None, 1, 0, 5, False, None, 16),
+                     (None, 1, 0, 5, False, (0.2, 8), 16)]:
+            with pytest.raises(native_ops.N.NativeError):
+                native_ops._handoff_input(y, *args)
+    finally:
+        native_ops.set_compute_dtype('bf16' if prev == native_ops.BF16 else 'fp32')
+
+
 def test_eval_retry_policy_cpu():
     """models/pytorch_v3/base.eval_retry: a RecurrenceGaveUp re-runs the pass
     once; a second one propagates; other errors propagate at once."""
