@@ -818,7 +818,7 @@ int asr_lstm_status_inject(int bits, void* stream);
 int asr_lstm_xg_mode(int* mode, int clear);
 
 /* Diagnostics (ASR_XG_TRACE=1 at the first recurrence launch): copies the
- * per-step phase timestamps of work-groups 0..3 (4 x 128 steps x 6 u64) to
+ * per-step phase timestamps of work-groups 0..63 (64 x 128 steps x 12 u64) to
  * `host` (may be NULL); returns the element count, 0 when tracing is off. */
 long long asr_xg_trace_read(unsigned long long* host);
 /* The persistent backward recurrence's dynamic-LDS pin (KB, in (80, 160]; 0 =
@@ -836,6 +836,16 @@ int asr_lstm_set_bwd_units(int xu);
 /* Work-groups that backward recurrence launches for [B, *, H] with xu units per
  * work-group (0: the current setting); 0 if the shape cannot take that path. */
 int asr_lstm_backward_grid(int B, int H, int xu);
+/* Pipelined input gradients (the layer above's dX GEMMs overlapping this
+ * layer's backward recurrence, rnn.py:343-390's stacked layers): dy of the
+ * asr_lstm_backward_dgbf_h launches that follow is written concurrently, in
+ * chunks of processing steps q in [c0 k, c0 (k + 1)) -- rows t = q and
+ * t = T - 1 - q -- complete once flags[k] == epoch (chunks up to the middle
+ * step (T + 1) / 2 - 1).  The recurrence
+ * waits for each chunk's flag before reading its dy rows.  flags NULL: off. */
+int asr_lstm_set_dy_flags(const int* flags, int c0, int epoch);
+/* Stream-ordered: flags[k] = epoch after the work enqueued before it. */
+int asr_lstm_dy_signal(int* flags, int k, int epoch, void* stream);
 /* Diagnostics only (tools/cores_locate.py): backward recurrence launches
  * enqueued on `stream` after this call record every dh_t their cell waves form
  * into dh ([B][T][2][H] f32), each step's sweep spin count into spins

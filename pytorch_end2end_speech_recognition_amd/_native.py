@@ -206,6 +206,8 @@ SIGNATURES = {
     'asr_lstm_debug_dh': (c_int, [c_vp, c_vp, c_vp, c_vp]),
     'asr_lstm_set_bwd_pin_kb': (c_int, [c_int]),
     'asr_lstm_set_bwd_units': (c_int, [c_int]),
+    'asr_lstm_set_dy_flags': (c_int, [c_vp, c_int, c_int]),
+    'asr_lstm_dy_signal': (c_int, [c_vp, c_int, c_int, c_vp]),
     'asr_lstm_backward_grid': (c_int, [c_int, c_int, c_int]),
 }
 

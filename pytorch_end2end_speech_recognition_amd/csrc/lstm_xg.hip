@@ -65,7 +65,12 @@ __device__ unsigned* g_xg_dbg_spins;
 __device__ float* g_xg_dbg_cell;
 #define XG_TR_WG 64
 #define XG_TR_STEPS 128
-#define XG_TR_K 8
+#define XG_TR_K 12
+#define XG_TR_AT(step, k, val)                                                           \
+  do {                                                                                  \
+    if (tr && (step) < XG_TR_STEPS)                                                    \
+      tr[((long long)blockIdx.x * XG_TR_STEPS + (step)) * XG_TR_K + (k)] = (val);      \
+  } while (0)
 #define XG_TR(step, k, val)                                                              \
   do {                                                                                  \
     if (tr && (step) < XG_TR_STEPS && lane == 0 && wave == 0)                          \
@@ -110,6 +115,12 @@ int xg_bwd_xu(int R, int H) {
   if (xu == 32 && R == 8 && H % 32 == 0 && (H / 16 + 3) / 4 <= 8) return 32;
   return 16;
 }
+
+// asr_lstm_set_dy_flags: dy of the next packed-activation backward launch
+// arrives chunk by chunk (see lstm_bwd_xg's sweepers); NULL = off.
+const int* g_dyflag = nullptr;
+int g_dyc0 = 16;
+unsigned g_dyepoch = 0;
 
 // The backward's pin leaves no room for the kernel's static LDS: the layer
 // would silently take the slower counter-form recurrence -- say so once.
@@ -539,8 +550,15 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
     int allow_local, int late_load, int defer_st, h16x4* __restrict__ acth,
     uint16_t* __restrict__ ydrop, float drop_p, unsigned long long drop_seed) {
   (void)late_load;   // input rows now staged by LDS DMA three steps ahead
-  __shared__ float part[2][NSW][R][4 * XU + 4];
-  __shared__ float xpart[2][NPW][R][4 * XU + 4];
+  // partial gate inputs, row r of a step at prow(r).  (A bank-conflict-free
+  // pitch -- rows 80 floats apart, rows 4..7 a further 16 on -- measured
+  // 1457 vs 1450 us per 5x512 launch against this 68-float pitch: the cell's
+  // partial-sum reads are not what bounds the step.)
+  constexpr int PROW = 4 * XU + 4;
+  constexpr int PSZ = R * PROW;
+  auto prow = [](int r) { return r * PROW; };
+  __shared__ float part[2][NSW][PSZ];
+  __shared__ float xpart[2][NPW][PSZ];
   // input rows of steps s+1 .. s+3: [3 slots][R rows][XGX_DMAX] bf16, filled by
   // buffer -> LDS DMA three steps ahead (16-B chunks XOR-swizzled by row when
   // Din % 64 == 0, so a fragment read of 8 rows hits distinct banks)
@@ -562,6 +580,11 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
   const int nks = H >> 5;
   const unsigned quarter = (unsigned)(H / 4);
   constexpr int NCW = R * XU / 64;
+#ifdef ASR_XG_TRACE_FWD   // phase stamps (tools/xg_trace.py); they cost ~5 % of the step
+  unsigned long long* tr = blockIdx.x < XG_TR_WG ? g_xg_trace : nullptr;
+#else
+  constexpr unsigned long long* tr = nullptr;
+#endif
 
   if (wave < NSW) {
     // ------------------------------ sweeper (as lstm_fwd_xg) ------------------
@@ -585,6 +608,7 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
     __syncthreads();  // B_pre: the first three steps' input rows are in LDS
     __syncthreads();  // B_init: the producers' pre(0) is in LDS
     for (int s = 0; s < T; ++s) {
+      XG_TR(s, 0, __builtin_amdgcn_s_memrealtime());
       f32x4 acc[4];
 #pragma unroll
       for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -595,6 +619,7 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
         u32x4 v[KSW];
         nap(ndelay);
         for (unsigned spins = 0;; ++spins) {
+          const unsigned long long t_iss = tr ? __builtin_amdgcn_s_memrealtime() : 0;
           int ok = 1;
           if (sweeper) {
 #pragma unroll
@@ -604,7 +629,13 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
             for (int i = 0; i < KSW; ++i)
               ok &= (int)((((v[i][0] ^ ebit) | (v[i][2] ^ ebit)) & 1u) == 0u);
           }
-          if (__all(ok)) break;
+          if (__all(ok)) {
+            XG_TR(s, 1, __builtin_amdgcn_s_memrealtime());
+            XG_TR(s, 5, spins);
+            XG_TR(s, 6, t_iss);
+            XG_TR(s, 7, (unsigned long long)(grp * 256 + mem));
+            break;
+          }
           if (!keep_spinning(spins, abortw, nsleep)) {
             s_dead = 1;
             break;
@@ -620,13 +651,19 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
           }
         }
       }
+      if (tr && wave == 0 && lane == 0) {
+        asm volatile("" ::"v"(acc[0][0]), "v"(acc[1][0]), "v"(acc[2][0]), "v"(acc[3][0]));
+        XG_TR_AT(s, 11, __builtin_amdgcn_s_memrealtime());
+      }
       if (4 * kq < R) {
 #pragma unroll
         for (int g = 0; g < 4; ++g)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) part[s & 1][wave][4 * kq + r][g * XU + ln] = acc[g][r];
+          for (int r = 0; r < 4; ++r) part[s & 1][wave][prow(4 * kq + r) + g * XU + ln] = acc[g][r];
       }
+      XG_TR(s, 4, __builtin_amdgcn_s_memrealtime());
       __syncthreads();  // B(s)
+      XG_TR(s, 2, __builtin_amdgcn_s_memrealtime());
       if (s_dead) return;
       __syncthreads();  // Bp(s)
     }
@@ -687,6 +724,9 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
       for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int i = 0; i < KPW; ++i) {
+#ifdef ASR_XGX_HALF_TEST   // timing experiment only: half the projection (wrong results)
+        if ((i & 1) && st > 0) continue;
+#endif
         if (pw + NPW * i < nkx) {  // wave-uniform
           const int k = 32 * (pw + NPW * i) + 8 * kq;
           bf16x8 a = as_bf16x8(z8);
@@ -702,7 +742,7 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
 #pragma unroll
         for (int g = 0; g < 4; ++g)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) xpart[st & 1][pw][4 * kq + r][g * XU + ln] = acc[g][r];
+          for (int r = 0; r < 4; ++r) xpart[st & 1][pw][prow(4 * kq + r) + g * XU + ln] = acc[g][r];
       }
     };
     for (int st = 0; st < 3 && st < T; ++st) stage_x(st);
@@ -715,6 +755,7 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
     // then publishes every wave's rows of step s+2 for produce(s+2).
     for (int s = 0; s < T; ++s) {
       if (s + 1 < T) produce(s + 1);
+      if (pw == 0 && lane == 0) XG_TR_AT(s, 8, __builtin_amdgcn_s_memrealtime());
       __syncthreads();  // B(s)
       if (s_dead) return;
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -744,7 +785,7 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
   for (int q = 0; q < 4; ++q) {
     float v = bsum[q];
 #pragma unroll
-    for (int p = 0; p < NPW; ++p) v += xpart[0][p][row][q * XU + unit];
+    for (int p = 0; p < NPW; ++p) v += xpart[0][p][prow(row) + q * XU + unit];
     gxv[q] = v;
   }
   __builtin_amdgcn_s_setprio(2);  // the cell update + publish is the critical path
@@ -780,7 +821,9 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
   for (int s = 0; s < T; ++s) {
     const int t = dir ? T - 1 - s : s;
     __syncthreads();  // B(s)
-    if (s_dead) return;
+    // the abort word is tested after the step's math: its LDS read overlaps
+    // the partial-sum reads instead of preceding them
+    const int dead = s_dead;
     if (defer_st && own && pt >= 0) store_step(pt, pv, pval, pdval);
     float h = 0.f, cn = 0.f, ig = 0.f, fg = 0.f, gg = 0.f, og = 0.f;
     const bool active = own && t < len;
@@ -789,10 +832,14 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int col = q * XU + unit;
-        float a = part[s & 1][0][row][col];
+        float a = part[s & 1][0][prow(row) + col];
 #pragma unroll
-        for (int w = 1; w < NSW; ++w) a += part[s & 1][w][row][col];
+        for (int w = 1; w < NSW; ++w) a += part[s & 1][w][prow(row) + col];
         pre[q] = a + gxv[q];
+      }
+      if (ct == 0 && tr) {   // (trace) the partial sums are in registers
+        asm volatile("" ::"v"(pre[0]), "v"(pre[1]), "v"(pre[2]), "v"(pre[3]));
+        XG_TR_AT(s, 9, __builtin_amdgcn_s_memrealtime());
       }
       ig = fsig(pre[0]);
       fg = fsig(pre[1]);
@@ -800,8 +847,13 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
       og = fsig(pre[3]);
       cn = fg * c + ig * gg;
       h = og * ftanh(cn);
+      if (ct == 0 && tr) {
+        asm volatile("" ::"v"(h));
+        XG_TR_AT(s, 10, __builtin_amdgcn_s_memrealtime());
+      }
     }
     c = cn;
+    if (dead) return;
     const unsigned hb = f2bf(h);
     const unsigned h1 = row_from_upper<1>(hb);
     const unsigned val = hb | (h1 << 16);
@@ -816,6 +868,8 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
       else
         __hip_atomic_store(p, gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (ct == 0 && tr && s < XG_TR_STEPS)
+      tr[((long long)blockIdx.x * XG_TR_STEPS + s) * XG_TR_K + 3] = __builtin_amdgcn_s_memrealtime();
     __syncthreads();  // Bp(s)
     pv[0] = h; pv[1] = cn; pv[2] = ig; pv[3] = fg; pv[4] = gg; pv[5] = og;
     pval = val;
@@ -831,7 +885,7 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
       for (int q = 0; q < 4; ++q) {
         float v = bsum[q];
 #pragma unroll
-        for (int p = 0; p < NPW; ++p) v += xpart[(s + 1) & 1][p][row][q * XU + unit];
+        for (int p = 0; p < NPW; ++p) v += xpart[(s + 1) & 1][p][prow(row) + q * XU + unit];
         gxv[q] = v;
       }
     }
@@ -864,7 +918,8 @@ __global__ void __launch_bounds__(256 + R * XB + 16 * XB) lstm_bwd_xg(
     const float* __restrict__ whh_r, const float* __restrict__ dy, float* __restrict__ act_dg,
     const float* __restrict__ cst, unsigned long long* pg, int* hdr,
     uint16_t* __restrict__ dgbf, float* __restrict__ dbpart, unsigned epoch, int allow_local,
-    int dg_f32, int io_pos, int dg_st16, const h16x4* __restrict__ acth) {
+    int dg_f32, int io_pos, int dg_st16, const h16x4* __restrict__ acth,
+    const int* __restrict__ dyflag, int dyc0, int dyepoch) {
   constexpr int SQ = XB / 8;           // 16-B loads (8 units) per row of a producer's slice
   constexpr int LPS = R * SQ;          // sweeper lanes per producer subset
   constexpr int NPG = 256 / LPS;       // producer subsets swept in parallel
@@ -905,8 +960,30 @@ __global__ void __launch_bounds__(256 + R * XB + 16 * XB) lstm_bwd_xg(
     unsigned* dspin = g_xg_dbg_spins;
     const int nsleep = __builtin_amdgcn_readfirstlane(g_xg_sleep);
     const int ndelay = __builtin_amdgcn_readfirstlane(g_xg_delay);
+    // dyflag (non-null): dy is being written while this kernel runs -- by the
+    // layer above's input-gradient GEMMs, chunk by chunk from both ends of the
+    // sequence (chunk k = processing steps [c0 k, c0 (k + 1)), signalled in
+    // order up to the middle step).  The cell waves load step
+    // q + 2's dy after B2 of step q, so the sweepers make sure of chunk
+    // (q + 2) -- clamped to the middle step, whose chunk covers the rows of
+    // every later step -- before B1 of step q; the flag's load is issued
+    // before the step's poll and checked after it.
+    const int qmid = (T + 1) / 2 - 1;
+    int dyk = -1, dynext = 0, dyv = 0;
+    auto dy_need = [&](int q) { return min(q, qmid) >= dynext; };
+    if (dyflag && dy_need(min(1, T - 1))) {   // steps 0 and 1 (loaded before the loop)
+      for (unsigned spins = 0;; ++spins) {
+        if (__hip_atomic_load(dyflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == dyepoch) break;
+        if (!keep_spinning(spins, abortw, nsleep)) { s_dead = 1; break; }
+      }
+      dyk = 0;
+      dynext = dyc0;
+    }
+    __syncthreads();  // B0: the cell waves load steps 0 and 1 after it
     for (int q = 0; q < T; ++q) {
       XG_TR(q, 0, __builtin_amdgcn_s_memrealtime());
+      const bool dyw = dyflag && q + 2 < T && dy_need(q + 2);
+      if (dyw) dyv = __hip_atomic_load(dyflag + dyk + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (q > 0) {
         const unsigned ebit = tag_bit(q - 1);
         const long long base = ((long long)((q - 1) & 1) * G + grp) * WPG;
@@ -959,6 +1036,14 @@ __global__ void __launch_bounds__(256 + R * XB + 16 * XB) lstm_bwd_xg(
 #pragma unroll
         for (int e = 0; e < 8; ++e) red[pgi][srow][8 * sq + e] = sm[e];
       }
+      if (dyw) {   // chunk dyk + 1 (one step may cross at most one boundary)
+        for (unsigned spins = 0; dyv != dyepoch; ++spins) {
+          if (!keep_spinning(spins, abortw, nsleep)) { s_dead = 1; break; }
+          dyv = __hip_atomic_load(dyflag + dyk + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        ++dyk;
+        dynext = dyc0 * (dyk + 1);
+      }
       __syncthreads();  // B1
       XG_TR(q, 2, __builtin_amdgcn_s_memrealtime());
       if (s_dead) return;
@@ -981,9 +1066,11 @@ __global__ void __launch_bounds__(256 + R * XB + 16 * XB) lstm_bwd_xg(
     float* ddh = g_xg_dbg_dh;
     float* dcl = g_xg_dbg_cell;
     // c_t of step q is c_{tp} of step q - 1: with `carry` it is taken from there
-    const int lsc1 = __builtin_amdgcn_readfirstlane(g_xg_cell_sc1);
+    // bit 0: every cell input by agent-scope loads (ASR_XG_CELL_SC1); bit 1: dy
+    // only -- it is written by another stream's GEMMs while this launch runs
+    const int lsc1 = __builtin_amdgcn_readfirstlane(g_xg_cell_sc1) | (dyflag ? 2 : 0);
     auto ldf = [&](const float* p) {
-      return lsc1 ? __hip_atomic_load((const gfloat*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+      return (lsc1 & 1) ? __hip_atomic_load((const gfloat*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                   : *p;
     };
     auto load_cell = [&](int q, float (&av)[4], h16x4& avh, float& cc, float& cp, float& dyv,
@@ -1005,7 +1092,12 @@ __global__ void __launch_bounds__(256 + R * XB + 16 * XB) lstm_bwd_xg(
       }
       cc = carry ? *carry : ldf(cst + si);
       cp = (tp >= 0 && tp < T) ? ldf(cst + si + (long long)(tp - t) * 2 * H) : 0.f;
-      dyv = dy ? ldf(dy + si) : 0.f;
+      if (!dy)
+        dyv = 0.f;
+      else if (lsc1)   // bit 1: dy written by another stream's GEMMs during the launch
+        dyv = __hip_atomic_load((const gfloat*)(dy + si), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else
+        dyv = *(dy + si);
     };
     // inputs of step q (av, cc, cp, dyv) and q + 1 (n*): loaded two steps ahead
     float av[4] = {0.f, 0.f, 0.f, 0.f}, cc = 0.f, cp = 0.f, dyv = 0.f;
@@ -1013,6 +1105,7 @@ __global__ void __launch_bounds__(256 + R * XB + 16 * XB) lstm_bwd_xg(
     h16x4 avh = {0, 0, 0, 0}, navh = {0, 0, 0, 0};
     // bias gradient: sum over t of this (utterance, unit)'s four gate gradients
     float sb_i = 0.f, sb_f = 0.f, sb_g = 0.f, sb_o = 0.f;
+    __syncthreads();  // B0 (the sweepers have seen dy's first chunk)
     if (own) load_cell(0, av, avh, cc, cp, dyv, nullptr);
     if (own && T > 1) load_cell(1, nav, navh, ncc, ncp, ndyv, nullptr);
     // io_pos: where the cell waves issue a step's dG stores and the loads of
@@ -1144,6 +1237,7 @@ __global__ void __launch_bounds__(256 + R * XB + 16 * XB) lstm_bwd_xg(
       }
     }
   }
+  __syncthreads();  // B0
   for (int q = 0; q < T; ++q) {
     __syncthreads();  // B1
     if (s_dead) return;
@@ -1378,7 +1472,8 @@ int lstm_bwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* wh
     hipLaunchKernelGGL((lstm_bwd_xg<RR, M, AHV, XBV>), dim3(grid), dim3(256 + (RR + 16) * XBV),   \
                        pin, s,                                                                  \
                        B, T, H, lens, whh_f, whh_r, dy, act_dg, cst, g, hdr, dgbf, dbpart, ep,   \
-                       al, (dg_f32 || !dgbf) ? 1 : 0, io_pos, st16, (const h16x4*)acth);        \
+                       al, (dg_f32 || !dgbf) ? 1 : 0, io_pos, st16, (const h16x4*)acth,         \
+                       acth ? g_dyflag : nullptr, g_dyc0, (int)g_dyepoch);                       \
   } while (0)
 #define ASR_XGB2(RR, M, AHV)                                  \
   do {                                                        \
@@ -1555,6 +1650,37 @@ extern "C" int asr_lstm_set_bwd_pin_kb(int kb) {
   ASR_REQUIRE(kb == 0 || (kb > 80 && kb <= 160), ASR_ERR_ARG, "lstm pin: %d KB", kb);
   asr::g_pin_bwd_kb = kb;
   return ASR_OK;
+}
+
+// dy of the backward recurrence launches that follow (asr_lstm_backward_dgbf_h
+// only) is written concurrently by input-gradient GEMMs on another stream:
+// processing steps [c0 k, c0 (k + 1)) -- dy rows t = q and t = T - 1 - q for
+// those steps q -- are complete once flags[k] == epoch
+// (set by asr_lstm_dy_signal after the chunk's GEMMs).  flags NULL: off.
+extern "C" int asr_lstm_set_dy_flags(const int* flags, int c0, int epoch) {
+  ASR_REQUIRE(!flags || (c0 > 0 && epoch != 0), ASR_ERR_ARG, "dy flags: c0 %d epoch %d", c0,
+              epoch);
+  asr::g_dyflag = flags;
+  asr::g_dyc0 = c0;
+  asr::g_dyepoch = (unsigned)epoch;
+  return ASR_OK;
+}
+
+namespace asr {
+namespace {
+__global__ void dy_signal(int* flags, int k, int epoch) {
+  if (threadIdx.x == 0)
+    __hip_atomic_store(flags + k, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+}  // namespace
+}  // namespace asr
+
+// Stream-ordered: flags[k] = epoch once the work enqueued before it on
+// `stream` is complete (one thread; the chunk's dy rows are then visible).
+extern "C" int asr_lstm_dy_signal(int* flags, int k, int epoch, void* stream) {
+  ASR_REQUIRE(flags && k >= 0 && epoch != 0, ASR_ERR_ARG, "dy signal");
+  hipLaunchKernelGGL(asr::dy_signal, dim3(1), dim3(64), 0, (hipStream_t)stream, flags, k, epoch);
+  return hipGetLastError() == hipSuccess ? ASR_OK : ASR_ERR_HIP;
 }
 
 // Units per work-group of the backward recurrence for the launches that follow

@@ -939,6 +939,7 @@ class BLSTMLayerFn(torch.autograd.Function):
         ctx.drop = drop
         ctx.next_rec = bool(next_rec)
         ctx.n_graph = len(graph_params)
+        ctx.handoff_in = twin is not None
         if handoff is not None:
             # y was not written: only the next BLSTM layer may consume it, through
             # the bf16 tensor (_handoff_input raises for any other use it sees)
@@ -952,6 +953,13 @@ class BLSTMLayerFn(torch.autograd.Function):
         H = w_hh.shape[1]
         dev = act.device
         dy = dy.contiguous()
+        # dy still being written by the layer above's input-gradient GEMMs
+        # (_dx_pipelined): only the packed-activation tagged-granule backward
+        # reads it that way; anything else waits for them first
+        pipe = getattr(dy, '_asr_dy_pipe', None)
+        if pipe is not None and act.dtype != torch.float16:
+            torch.cuda.current_stream(dev).wait_event(pipe[3])
+            pipe = None
         if gbufs is None:
             gbufs = tuple(grad_buffer(p) for p in (w_ih, w_hh, b_ih, b_hh))
         fused_db = os.environ.get('ASR_BIAS_FUSED', '1') != '0'
@@ -974,9 +982,19 @@ class BLSTMLayerFn(torch.autograd.Function):
             # backward reads them directly; otherwise they are unpacked to f32
             nb = N.query('asr_lstm_workspace_bytes', B, H, cd, 2)
             ws = _ws(nb, dev)
-            rc = N.query('asr_lstm_backward_dgbf_h', N.ptr(dy), N.ptr(w_hh), ctypes.c_void_p(whh_r),
-                         F32, N.ptr(lens), B, T, H, cd, N.ptr(act), N.ptr(cst), N.ptr(dg_bf),
-                         N.ptr(gbufs[2]), N.ptr(gbufs[3]), N.ptr(ws), nb, N.stream_handle(dev))
+            if pipe is not None:
+                N.call('asr_lstm_set_dy_flags', N.ptr(pipe[0]), pipe[1], pipe[2])
+            try:
+                rc = N.query('asr_lstm_backward_dgbf_h', N.ptr(dy), N.ptr(w_hh),
+                             ctypes.c_void_p(whh_r), F32, N.ptr(lens), B, T, H, cd, N.ptr(act),
+                             N.ptr(cst), N.ptr(dg_bf), N.ptr(gbufs[2]), N.ptr(gbufs[3]),
+                             N.ptr(ws), nb, N.stream_handle(dev))
+            finally:
+                if pipe is not None:
+                    N.call('asr_lstm_set_dy_flags', None, 16, 0)
+                    # (after the launch: later compute-stream work sees all of dy)
+                    torch.cuda.current_stream(dev).wait_event(pipe[3])
+                    pipe = None
             if rc not in (0, N.ASR_ERR_UNSUPPORTED):
                 raise N.NativeError('asr_lstm_backward_dgbf_h failed (rc=%d): %s' % (
                     rc, N.lib().asr_last_error().decode(errors='replace')))
@@ -1021,6 +1039,16 @@ class BLSTMLayerFn(torch.autograd.Function):
         # the co-resident small tiles the 4x320 layer-0 dW_ih ran at 29 TF/s)
         last_main = not ctx.next_rec and os.environ.get('ASR_WGRAD_LAST_MAIN', '1') != '0'
         side_ent = None if last_main else _wgrad_side_stream(dev, B, H)
+        # pipelined input gradient (_dx_pipelined): enqueued first, and the
+        # side-stream weight gradients start after it, so the CUs the next
+        # recurrence leaves free serve dX -- which that recurrence waits for --
+        # before the weight gradients, which only the optimizer needs
+        BT = B * T
+        dx = dx_done = None
+        pipelined = ctx.needs_input_grad[0] and _dx_pipeline_ok(ctx, B, T, Din, dev)
+        if pipelined:
+            dx = torch.empty(B, T_src, Dsrc, dtype=torch.float32, device=dev)
+            dx_done = _dx_pipelined(dx, dg_op, w_op, B, T, H, Din, Dp, ctx.drop, dev)
         if side_ent is None:
             _blstm_wgrad(dg_op, act, x_op, x_map, y_op, T, gbufs, dev)
             notify_grad_event('grads', gbufs)      # final on the compute stream
@@ -1035,7 +1063,9 @@ class BLSTMLayerFn(torch.autograd.Function):
                 N.call('asr_gemm_set_small_tiles', 1)
             try:
                 with torch.cuda.stream(side):
-                    if gated and ctx.next_rec:
+                    if dx_done is not None:
+                        side.wait_event(dx_done)
+                    elif gated and ctx.next_rec:
                         # hold the GEMMs back until the previous layer's backward
                         # recurrence (launched next on the main stream) is resident
                         N.call('asr_lstm_wgrad_gate', N.stream_handle(dev))
@@ -1051,9 +1081,7 @@ class BLSTMLayerFn(torch.autograd.Function):
                 torch.autograd.Variable._execution_engine.queue_callback(
                     lambda: _join_side_wgrads(dev, notify=False))
             _side_pending.append((side, gbufs, main))
-        BT = B * T
-        dx = None
-        if ctx.needs_input_grad[0]:
+        if ctx.needs_input_grad[0] and not pipelined:
             # dX [BT, Din] = dG [BT, 8H] W_ih [8H, Din], scattered back through the input map
             if perm is None and t_mul == 1 and t_add == 0 and T == T_src and Din == Dsrc:
                 dx = torch.empty(B, T_src, Dsrc, dtype=torch.float32, device=dev)
@@ -1340,6 +1368,76 @@ def _wgrad_side_stream(dev, B, H):
             ent = torch.cuda.Stream(device=dev)
         _side_streams[key] = ent
     return ent, mode == '2', mode != '1'
+
+
+DX_CHUNK = int(os.environ.get('ASR_DX_CHUNK', '64'))   # processing steps per pipelined dX chunk
+_dx_state = {}
+
+
+def _dx_pipeline_ok(ctx, B, T, Din, dev):
+    """The input gradient of this layer feeds only the backward recurrence of
+    the BLSTM layer below (its input was handed over as bf16), that recurrence
+    is the packed-activation tagged-granule kernel and it leaves >= 32 CUs
+    free: dX may then be computed beside it.  Opt-in (ASR_DX_PIPE=1): at 5x512
+    the free half of the chip runs these GEMMs and the weight gradients too
+    slowly to stay ahead of the recurrence."""
+    if not getattr(ctx, 'handoff_in', False) or os.environ.get('ASR_DX_PIPE', '0') != '1':
+        return False
+    if Din % 2 or not _act_h_on() or compute_dtype() != BF16 or (T + 1) // 2 > 4096 * DX_CHUNK:
+        return False
+    # the GEMMs need CUs beside that recurrence (140 KB LDS pin: none on its CUs)
+    _, xu = _overlap_plan(dev, B, Din // 2)
+    grid = N.query('asr_lstm_backward_grid', B, Din // 2, xu)
+    return grid > 0 and grid + 32 <= _num_cus(dev)
+
+
+def _dx_pipelined(dx, dg_op, w_op, B, T, H, Din, Dp, drop, dev):
+    """dX [B, T, Din] = dG W_ih on a high-priority side stream, in chunks of
+    time steps from both ends of the sequence inwards -- the order in which the
+    layer below's backward recurrence reads them (steps q: rows t = q and
+    T - 1 - q) -- each chunk signalled by a flag (asr_lstm_dy_signal) the
+    recurrence polls before reading its dy rows.  The GEMMs first wait for that
+    recurrence to be resident (asr_lstm_wgrad_gate), so they take the CUs it
+    leaves free.  dx carries (flags, c0, epoch, done-event) as _asr_dy_pipe."""
+    st = _dx_state.get(dev.index)
+    if st is None:
+        st = {'flags': torch.zeros(4096, dtype=torch.int32, device=dev),
+              'stream': torch.cuda.Stream(device=dev, priority=-1), 'epoch': 0}
+        _dx_state[dev.index] = st
+    st['epoch'] = st['epoch'] % 0x7ffffff0 + 1
+    epoch, flags, side = st['epoch'], st['flags'], st['stream']
+    main = torch.cuda.current_stream(dev)
+    side.wait_stream(main)
+    half = (T + 1) // 2
+    small = os.environ.get('ASR_DX_SMALL', '1') != '0'   # 128 x 128 tiles: more work-groups
+    with torch.cuda.stream(side):
+        N.call('asr_lstm_wgrad_gate', N.stream_handle(dev))
+        if small:
+            N.call('asr_gemm_set_small_tiles', 1)
+        try:
+            for k in range((half + DX_CHUNK - 1) // DX_CHUNK):
+                s0, s1 = k * DX_CHUNK, (k + 1) * DX_CHUNK
+                probs = []
+                for t0, t1 in ((s0, min(s1, half)), (max(T - s1, half), T - s0)):
+                    if t1 <= t0:
+                        continue
+                    n = t1 - t0
+                    a = operand(dg_op, 0, rowmap(8 * H, stride_b=T * 8 * H, rows_per_b=n,
+                                                 t_add=t0))
+                    c_map = rowmap(Din, stride_b=T * Din, rows_per_b=n, t_add=t0)
+                    probs.append(gemm_problem(a, operand(w_op, 1, rowmap(Dp)), dx, c_map, B * n,
+                                              Din, 8 * H, drop=drop))
+                run_gemm(probs, dev)
+                N.call('asr_lstm_dy_signal', N.ptr(flags), k, epoch, N.stream_handle(dev))
+        finally:
+            if small:
+                N.call('asr_gemm_set_small_tiles', 0)
+        done = torch.cuda.Event()
+        done.record(side)
+    for t in (dx, dg_op, w_op, flags):
+        t.record_stream(side)
+    dx._asr_dy_pipe = (flags, DX_CHUNK, epoch, done)
+    return done
 
 
 def blstm_layer(x_src, lens, T, w_ih, w_hh, b_ih, b_hh, perm=None, t_mul=1, t_add=0, gbufs=None,

@@ -13,7 +13,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from pytorch_end2end_speech_recognition_amd import _native as N  # noqa: E402
 from pytorch_end2end_speech_recognition_amd import native_ops as ops  # noqa: E402
 
-WG, STEPS, K = 64, 128, 8
+WG, STEPS, K = 64, 128, 12
 
 
 def read():
@@ -76,6 +76,10 @@ def main():
     hop('backward', bwd, 4)
     report('forward (us): sweep = start->sweep ok, comb = sweep->barrier, cell = barrier->publish',
            fwd, [(0, 1, 'sweep'), (1, 4, 'mfma'), (4, 2, 'bar'), (2, 3, 'cell')])
+    report('forward detail (us): prod = step start -> projection done; mm = sweep ok -> MFMA '
+           'results; rd = barrier -> partial sums read; act = -> h; pub = -> published',
+           fwd, [(0, 8, 'prod'), (1, 11, 'mm'), (11, 4, 'lds'), (2, 9, 'rd'), (9, 10, 'act'),
+                 (10, 3, 'pub')])
     report('backward (us)', bwd, [(0, 1, 'sweep'), (1, 2, 'b1'), (2, 3, 'cell+b2'),
                                   (3, 4, 'mfma+pub')])
 
