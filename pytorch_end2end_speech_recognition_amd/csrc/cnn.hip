@@ -846,6 +846,314 @@ __global__ void __launch_bounds__(CT) post_bwd_full(const TD* __restrict__ dnext
   }
 }
 
+// ---------------------------------------------------------------------------
+// Row-blocked forms of the bf16 element-wise passes (z / P / dz bf16, C % 8 ==
+// 0 and C / 8 dividing 256, no pooling or 2 x 2 pooling).  A block owns
+// consecutive image rows (b, t) of the pass's grid; within a row the pixels x C
+// channels are contiguous in every operand -- flat rows and the interior of
+// padded rows alike -- so lane l covers 8 channels (one 16-B access) of pixel
+// g / (C / 8) for g = l, l + 256, ...: no per-element index division (the
+// grid-stride forms above spent two to three 32-bit divisions per 8-B access
+// and ran the 64-channel vgg_hier layer at 2.4-3.6 TB/s), and a lane's
+// channels are the same in every row (256 is a multiple of C / 8), so the
+// per-channel parameters and partial sums live in its registers.  Partial sums
+// are combined per block in a fixed order (lanes of a channel group in lane
+// order) and across blocks by sum_partials: run-to-run deterministic.
+// ---------------------------------------------------------------------------
+constexpr int RW_NT = 256;
+
+struct Bf8 {
+  float v[8];
+  __device__ __forceinline__ void load(const uint16_t* p) {
+    const uint4 x = *reinterpret_cast<const uint4*>(p);
+    const unsigned w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[2 * k] = bf2f((uint16_t)(w[k] & 0xffffu));
+      v[2 * k + 1] = bf2f((uint16_t)(w[k] >> 16));
+    }
+  }
+  __device__ __forceinline__ void load(const float* p) {
+    const float4 a = *reinterpret_cast<const float4*>(p);
+    const float4 b = *reinterpret_cast<const float4*>(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+  __device__ __forceinline__ void store(uint16_t* p) const {
+    uint4 x;
+    x.x = f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
+    x.y = f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+    x.z = f2bf(v[4]) | ((unsigned)f2bf(v[5]) << 16);
+    x.w = f2bf(v[6]) | ((unsigned)f2bf(v[7]) << 16);
+    *reinterpret_cast<uint4*>(p) = x;
+  }
+  __device__ __forceinline__ void store(float* p) const {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+};
+
+// element offset of pixel (b, t, 0) of a [B][T][F] grid: flat rows, or the
+// first interior pixel of padded rows [B][T+2][F+2]
+__device__ __forceinline__ long long row_base(int b, int t, int T, int F, int C, int flat) {
+  return flat ? ((long long)b * T + t) * F * C
+              : (((long long)b * (T + 2) + t + 1) * (F + 2) + 1) * C;
+}
+
+// lanes with the same channel group (tid % cg8) hold partial sums of the same
+// 8 channels: out[c] = their sum in lane order (c < C)
+__device__ __forceinline__ void rw_reduce(const float (&acc)[8], int cg8, int C, float* red,
+                                          float* __restrict__ out) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[tid * 8 + j] = acc[j];
+  __syncthreads();
+  for (int cc = tid; cc < C; cc += RW_NT) {
+    const int g = cc >> 3, j = cc & 7;
+    float t = 0.f;
+    for (int k = g; k < RW_NT; k += cg8) t += red[k * 8 + j];
+    out[cc] = t;
+  }
+  __syncthreads();
+}
+
+// y = dropout(BN(P)) row by row into the next layer's padded input (bf16) or
+// the flat f32 encoder input; the same arithmetic as apply_fwd.
+template <typename TO>
+__global__ void __launch_bounds__(RW_NT) rw_apply(const uint16_t* __restrict__ P, int B, int To,
+                                                  int Fo, int C, Affine af, TO* __restrict__ out,
+                                                  int flat, int rpb) {
+  const int tid = threadIdx.x, cg8 = C >> 3;
+  const int c = (tid & (cg8 - 1)) * 8;
+  float m[8], r[8], g[8], bt[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    m[j] = af.mean ? af.mean[c + j] : 0.f;
+    r[j] = af.mean ? af.rstd[c + j] : 0.f;
+    g[j] = af.mean ? af.gamma[c + j] : 0.f;
+    bt[j] = af.mean ? af.beta[c + j] : 0.f;
+  }
+  const int rows = B * To, ng = Fo * cg8;
+  const int r0 = blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
+  for (int rr = r0; rr < r1; ++rr) {
+    const int b = rr / To, t = rr - b * To;
+    const long long pb = (long long)rr * Fo * C;
+    const long long ob = row_base(b, t, To, Fo, C, flat);
+    for (int gg = tid; gg < ng; gg += RW_NT) {
+      const long long e = (long long)gg * 8;
+      Bf8 y;
+      y.load(P + pb + e);
+      if (af.mean) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y.v[j] = (y.v[j] - m[j]) * r[j] * g[j] + bt[j];
+      }
+      if (af.drop > 0.f) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          y.v[j] *= drop_scale(af.drop, af.seed, (unsigned long long)(pb + e + j));
+      }
+      y.store(out + ob + e);
+    }
+  }
+}
+
+// ReLU (+ 2 x 2 max pool, PL = 2) of bf16 z rows into bf16 P (+ slot), with the
+// batch-norm moment partials of P - shift (mpart, qpart: [block][C]; qpart
+// nullable).  The same window scan as post_fwd (freq outer, time inner, first
+// maximum wins).
+template <int PL>
+__global__ void __launch_bounds__(RW_NT) rw_post_fwd(const uint16_t* __restrict__ z, int B, int T,
+                                                     int F, int C, Pool pl,
+                                                     uint16_t* __restrict__ P,
+                                                     uint8_t* __restrict__ slot,
+                                                     float* __restrict__ mpart,
+                                                     const float* __restrict__ shift,
+                                                     float* __restrict__ qpart, int rpb) {
+  __shared__ float red[RW_NT * 8];
+  const int tid = threadIdx.x, cg8 = C >> 3, sh3 = __builtin_ctz(cg8);
+  const int c = (tid & (cg8 - 1)) * 8;
+  float sh[8], macc[8], qacc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sh[j] = qpart ? shift[c + j] : 0.f;
+    macc[j] = qacc[j] = 0.f;
+  }
+  const int rows = B * pl.To, ng = pl.Fo * cg8;
+  const int r0 = blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
+  for (int rr = r0; rr < r1; ++rr) {
+    const int b = rr / pl.To, to = rr - b * pl.To;
+    const long long pb = (long long)rr * pl.Fo * C;
+    for (int gg = tid; gg < ng; gg += RW_NT) {
+      const int fo = gg >> sh3;
+      const long long e = (long long)gg * 8;
+      Bf8 best;
+      if constexpr (PL == 0) {
+        best.load(z + row_base(b, to, T, F, C, 0) + e);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) best.v[j] = fmaxf(best.v[j], 0.f);
+      } else {
+        unsigned bs[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          best.v[j] = -__builtin_huge_valf();
+          bs[j] = 0u;
+        }
+#pragma unroll
+        for (int df = 0; df < 2; ++df) {
+          const int f = fo * 2 + df;
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt) {
+            const int t = to * 2 + dt;
+            if (f < F && t < T) {
+              Bf8 x;
+              x.load(z + row_base(b, t, T, F, C, 0) + (long long)f * C + c);
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                const float v = fmaxf(x.v[j], 0.f);
+                if (v > best.v[j]) { best.v[j] = v; bs[j] = (unsigned)(df * 2 + dt); }
+              }
+            }
+          }
+        }
+        uint2 sl;
+        sl.x = bs[0] | (bs[1] << 8) | (bs[2] << 16) | (bs[3] << 24);
+        sl.y = bs[4] | (bs[5] << 8) | (bs[6] << 16) | (bs[7] << 24);
+        *reinterpret_cast<uint2*>(slot + pb + e) = sl;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = best.v[j] - sh[j];
+        macc[j] += d;
+        qacc[j] += d * d;
+      }
+      best.store(P + pb + e);
+    }
+  }
+  if (mpart) {
+    rw_reduce(macc, cg8, C, red, mpart + (long long)blockIdx.x * C);
+    if (qpart) rw_reduce(qacc, cg8, C, red, qpart + (long long)blockIdx.x * C);
+  }
+}
+
+// partial[block][c] = sum dy, partial[block][C + c] = sum dy * xhat (as
+// bn_bwd_moments) over the block's rows of the pooled grid
+template <typename TD>
+__global__ void __launch_bounds__(RW_NT) rw_bn_moments(const TD* __restrict__ dnext,
+                                                       const uint16_t* __restrict__ P, int B,
+                                                       int To, int Fo, int C, int flat,
+                                                       Affine af, float* __restrict__ partial,
+                                                       int rpb) {
+  __shared__ float red[RW_NT * 8];
+  const int tid = threadIdx.x, cg8 = C >> 3;
+  const int c = (tid & (cg8 - 1)) * 8;
+  float m[8], rs[8], s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    m[j] = af.mean[c + j];
+    rs[j] = af.rstd[c + j];
+    s1[j] = s2[j] = 0.f;
+  }
+  const int rows = B * To, ng = Fo * cg8;
+  const int r0 = blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
+  for (int rr = r0; rr < r1; ++rr) {
+    const int b = rr / To, t = rr - b * To;
+    const long long pb = (long long)rr * Fo * C;
+    const long long db = row_base(b, t, To, Fo, C, flat);
+    for (int gg = tid; gg < ng; gg += RW_NT) {
+      const long long e = (long long)gg * 8;
+      Bf8 gv, x;
+      gv.load(dnext + db + e);
+      x.load(P + pb + e);
+      if (af.drop > 0.f) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          gv.v[j] *= drop_scale(af.drop, af.seed, (unsigned long long)(pb + e + j));
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s1[j] += gv.v[j];
+        s2[j] += gv.v[j] * (x.v[j] - m[j]) * rs[j];
+      }
+    }
+  }
+  rw_reduce(s1, cg8, C, red, partial + (long long)blockIdx.x * 2 * C);
+  rw_reduce(s2, cg8, C, red, partial + ((long long)blockIdx.x * 2 + 1) * C);
+}
+
+// dz over full-resolution rows (as post_bwd_full, BN present): each pixel takes
+// its window's gradient where it was the argmax (PL = 2) and the pooled /
+// unpooled value P > 0 (the ReLU mask); bf16 dz at every interior pixel, the
+// conv-bias partials of the f32 values per block (bias_part nullable).
+template <int PL, typename TD>
+__global__ void __launch_bounds__(RW_NT) rw_post_bwd(const TD* __restrict__ dnext,
+                                                     const uint16_t* __restrict__ P,
+                                                     const uint8_t* __restrict__ slot, int B, int T,
+                                                     int F, int C, Pool pl, int flat, Affine af,
+                                                     const float* __restrict__ sums,
+                                                     uint16_t* __restrict__ dz,
+                                                     float* __restrict__ bias_part, int rpb) {
+  __shared__ float red[RW_NT * 8];
+  const int tid = threadIdx.x, cg8 = C >> 3, sh3 = __builtin_ctz(cg8);
+  const int c = (tid & (cg8 - 1)) * 8;
+  const float inv_n = 1.f / (float)((unsigned)B * pl.To * pl.Fo);
+  float m[8], r[8], gm[8], a1[8], a2[8], bacc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    m[j] = af.mean[c + j];
+    r[j] = af.rstd[c + j];
+    gm[j] = af.gamma[c + j];
+    a1[j] = sums[c + j];
+    a2[j] = sums[C + c + j];
+    bacc[j] = 0.f;
+  }
+  const int rows = B * T, ng = F * cg8;
+  const int r0 = blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
+  for (int rr = r0; rr < r1; ++rr) {
+    const int b = rr / T, t = rr - b * T;
+    const int to = PL ? t >> 1 : t;
+    const bool trow = to < pl.To;
+    const long long zb = row_base(b, t, T, F, C, 0);
+    const long long pb = ((long long)b * pl.To + to) * pl.Fo * C;
+    const long long db = row_base(b, to, pl.To, pl.Fo, C, flat);
+    for (int gg = tid; gg < ng; gg += RW_NT) {
+      const int f = gg >> sh3;
+      const int fo = PL ? f >> 1 : f;
+      Bf8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v.v[j] = 0.f;
+      if (trow && fo < pl.Fo) {
+        const long long ip = (long long)fo * C + c;
+        Bf8 g, x;
+        g.load(dnext + db + ip);
+        x.load(P + pb + ip);
+        if (af.drop > 0.f) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            g.v[j] *= drop_scale(af.drop, af.seed, (unsigned long long)(pb + ip + j));
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xh = (x.v[j] - m[j]) * r[j];
+          g.v[j] = gm[j] * r[j] * (g.v[j] - a1[j] * inv_n - xh * a2[j] * inv_n);
+        }
+        unsigned long long sl = 0ull, me = 0ull;
+        if constexpr (PL != 0) {
+          sl = *reinterpret_cast<const unsigned long long*>(slot + pb + ip);
+          me = (unsigned long long)((f - fo * 2) * 2 + (t - to * 2));
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const bool hit = PL == 0 || ((sl >> (8 * j)) & 0xffull) == me;
+          v.v[j] = (hit && x.v[j] > 0.f) ? g.v[j] : 0.f;
+          bacc[j] += v.v[j];
+        }
+      }
+      v.store(dz + zb + (long long)gg * 8);
+    }
+  }
+  if (bias_part) rw_reduce(bacc, cg8, C, red, bias_part + (long long)blockIdx.x * C);
+}
+
 // GEMM weight images of a torch Conv2d weight W [Co][Ci][3(f)][3(t)], tap
 // j = kw*3 + kh (the row shift (kw-1)(F+2) + (kh-1) of gemm.hip tap addressing):
 //   mode 0 (forward):  out[co][j*Ci + ci] = W[co][ci][kh][kw]
@@ -1131,6 +1439,16 @@ inline int post_grid(long long nr, int C) {
   return grid_for(C % 4 == 0 ? nr * C / 4 : nr * C);
 }
 
+// the row-blocked passes apply: bf16 P, C % 8 == 0 with C / 8 dividing 256, no
+// pooling or 2 x 2 pooling; ASR_VGG_ROWS=0 keeps the grid-stride passes (A/B)
+template <typename TP>
+bool rw_ok(int C, int pt, int pf) {
+  const char* e = getenv("ASR_VGG_ROWS");
+  if (e && e[0] == '0') return false;
+  if (sizeof(TP) != 2 || C % 8 || 256 % (C / 8)) return false;
+  return pt == 0 || (pt == 2 && pf == 2);
+}
+
 extern "C" size_t asr_vgg_block_workspace_bytes(int B, int To, int Fo, int C) {
   const long long n = (long long)B * To * Fo;
   const long long per = rows_per_chunk(n);
@@ -1213,7 +1531,24 @@ static int vgg_block_forward_impl(const void* z, int z_dtype, int B, int T, int 
   const bool zb = z_dtype == ASR_DT_BF16;
   ASR_REQUIRE(!zb || (v4 && ((uintptr_t)z & 7) == 0), ASR_ERR_UNSUPPORTED,
               "vgg_block_forward: bf16 z needs C % 4 == 0 and 8-B alignment");
-  if (zb)
+  // row-blocked passes (rw_*): bf16 z and P, 16-B aligned operands
+  const bool rows_ok = rw_ok<TP>(C, pt, pf) && ((uintptr_t)z & 15) == 0 &&
+                       ((uintptr_t)P & 15) == 0 && (!slot || ((uintptr_t)slot & 7) == 0) &&
+                       (!gamma || !training || fused_mean);
+  const int nrow = B * pl.To;
+  int rgrid = fgrid, rrpb = 1;
+  if (rows_ok) {   // blocks <= the partial regions' capacity (fgrid, the BN chunks)
+    rrpb = (nrow + fgrid - 1) / fgrid;
+    rgrid = (nrow + rrpb - 1) / rrpb;
+  }
+  if (rows_ok) {
+    if (pt)
+      hipLaunchKernelGGL((rw_post_fwd<2>), dim3(rgrid), dim3(RW_NT), 0, s, (const uint16_t*)z, B,
+                         T, F, C, pl, (uint16_t*)P, slot, mpart, vshift, qpart, rrpb);
+    else
+      hipLaunchKernelGGL((rw_post_fwd<0>), dim3(rgrid), dim3(RW_NT), 0, s, (const uint16_t*)z, B,
+                         T, F, C, pl, (uint16_t*)P, slot, mpart, vshift, qpart, rrpb);
+  } else if (zb)
     hipLaunchKernelGGL((post_fwd<4, uint16_t, TP>), dim3(fgrid), dim3(CT), 0, s, (const uint16_t*)z, B,
                        T, F, C, pl, P, slot, mpart, vshift, qpart);
   else if (v4)
@@ -1237,13 +1572,13 @@ static int vgg_block_forward_impl(const void* z, int z_dtype, int B, int T, int 
       float* m2 = part + (size_t)nchunk * C;
       if (fused_var) {
         hipLaunchKernelGGL(sum_partials, dim3((C + SP_COLS - 1) / SP_COLS), dim3(CT), 0, s, mpart,
-                           fgrid, C, 1.f / (float)nr, bn_mean);
+                           rgrid, C, 1.f / (float)nr, bn_mean);
         hipLaunchKernelGGL(sum_partials, dim3((C + SP_COLS - 1) / SP_COLS), dim3(CT), 0, s, qpart,
-                           fgrid, C, 1.f / (float)nr, m2);
+                           rgrid, C, 1.f / (float)nr, m2);
         hipLaunchKernelGGL(bn_finalize_shift, dim3((C + CT - 1) / CT), dim3(CT), 0, s, bn_mean, m2,
                            run_mean, C, nr, eps, momentum, bn_rstd, run_mean, run_var);
       } else if (fused_mean) {
-        hipLaunchKernelGGL(sum_partials, dim3((C + SP_COLS - 1) / SP_COLS), dim3(CT), 0, s, mpart, fgrid, C,
+        hipLaunchKernelGGL(sum_partials, dim3((C + SP_COLS - 1) / SP_COLS), dim3(CT), 0, s, mpart, rgrid, C,
                            1.f / (float)nr, bn_mean);
       } else {
         hipLaunchKernelGGL(col_moment<TP>, dim3(nchunk), dim3(CT), 0, s, P, nr, C, per, nullptr, 0,
@@ -1271,7 +1606,16 @@ static int vgg_block_forward_impl(const void* z, int z_dtype, int B, int T, int 
     af.beta = beta;
   }
   const long long ng = v4 ? nr * C / 4 : nr * C;
-  if (out_dtype == ASR_DT_BF16 && !flat) {
+  const bool out16 = ((uintptr_t)out & 15) == 0;
+  if (rows_ok && out16 && (out_dtype == ASR_DT_F32 || !flat)) {
+    const int agrid = std::min(nrow, 4096), arpb = (nrow + agrid - 1) / agrid;
+    if (out_dtype == ASR_DT_BF16)
+      hipLaunchKernelGGL((rw_apply<uint16_t>), dim3((nrow + arpb - 1) / arpb), dim3(RW_NT), 0, s,
+                         (const uint16_t*)P, B, pl.To, pl.Fo, C, af, (uint16_t*)out, flat, arpb);
+    else
+      hipLaunchKernelGGL((rw_apply<float>), dim3((nrow + arpb - 1) / arpb), dim3(RW_NT), 0, s,
+                         (const uint16_t*)P, B, pl.To, pl.Fo, C, af, (float*)out, flat, arpb);
+  } else if (out_dtype == ASR_DT_BF16 && !flat) {
     if (v4)
       hipLaunchKernelGGL((apply_fwd<uint16_t, 4, TP>), dim3(grid_for(ng)), dim3(CT), 0, s, P, B,
                          pl.To, pl.Fo, C, af, (uint16_t*)out, 0);
@@ -1405,6 +1749,11 @@ static int vgg_block_backward_impl(const void* dnext_v, int dnext_dtype, int fla
   float* sums = nullptr;
   float* bpart = nullptr;
   const int pgrid = post_grid(nr, C);
+  // row-blocked passes (rw_*): bf16 z / P / dz with batch norm, 16-B aligned
+  const bool rows_b = rw_ok<TP>(C, pt, pf) && gamma && z_dtype == ASR_DT_BF16 &&
+                      dz_dtype == ASR_DT_BF16 && ((uintptr_t)P & 15) == 0 &&
+                      ((uintptr_t)dz & 15) == 0 && ((uintptr_t)dnext_v & 15) == 0 &&
+                      (!slot || ((uintptr_t)slot & 7) == 0);
   if (dbias) {
     ASR_REQUIRE(workspace && ws_bytes >= asr_vgg_block_workspace_bytes(B, pl.To, pl.Fo, C),
                 ASR_ERR_WORKSPACE, "vgg_block_backward: bias needs the workspace");
@@ -1423,7 +1772,17 @@ static int vgg_block_backward_impl(const void* dnext_v, int dnext_dtype, int fla
     const int nchunk = (int)((nr + per - 1) / per);
     float* part = (float*)workspace;
     sums = part + (size_t)nchunk * 2 * C;
-    if (db16)
+    int mchunk = nchunk;
+    if (rows_b) {   // row-blocked moments: at most nchunk blocks
+      const int nrow = B * pl.To, rpb = (nrow + nchunk - 1) / nchunk;
+      mchunk = (nrow + rpb - 1) / rpb;
+      if (db16)
+        hipLaunchKernelGGL((rw_bn_moments<uint16_t>), dim3(mchunk), dim3(RW_NT), 0, s, dnh,
+                           (const uint16_t*)P, B, pl.To, pl.Fo, C, flat, af, part, rpb);
+      else
+        hipLaunchKernelGGL((rw_bn_moments<float>), dim3(mchunk), dim3(RW_NT), 0, s, dnext,
+                           (const uint16_t*)P, B, pl.To, pl.Fo, C, flat, af, part, rpb);
+    } else if (db16)
       hipLaunchKernelGGL((bn_bwd_moments<4, uint16_t, TP>), dim3(nchunk), dim3(CT), 0, s, dnh, P, B,
                          pl.To, pl.Fo, C, flat, af, per, part);
     else if (v4)
@@ -1432,7 +1791,7 @@ static int vgg_block_backward_impl(const void* dnext_v, int dnext_dtype, int fla
     else
       hipLaunchKernelGGL((bn_bwd_moments<1, float, TP>), dim3(nchunk), dim3(CT), 0, s, dnext, P, B, pl.To,
                          pl.Fo, C, flat, af, per, part);
-    hipLaunchKernelGGL(sum_partials, dim3((2 * C + SP_COLS - 1) / SP_COLS), dim3(CT), 0, s, part, nchunk, 2 * C,
+    hipLaunchKernelGGL(sum_partials, dim3((2 * C + SP_COLS - 1) / SP_COLS), dim3(CT), 0, s, part, mchunk, 2 * C,
                        1.f, sums);
     hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + CT - 1) / CT), dim3(CT), 0, s, sums, C, dgamma,
                        dbeta);
@@ -1446,7 +1805,30 @@ static int vgg_block_backward_impl(const void* dnext_v, int dnext_dtype, int fla
   const float* zf = (const float*)z;
   const uint16_t* zh = (const uint16_t*)z;
   ASR_REQUIRE(!db16 || full, ASR_ERR_UNSUPPORTED, "vgg_block_backward: bf16 dnext needs the full pass");
-  if (db16) {
+  int bgrid = pgrid;
+  if (rows_b) {   // at most pgrid blocks (the bias-partial region)
+    const int nrow = B * T, rpb = (nrow + pgrid - 1) / pgrid;
+    bgrid = (nrow + rpb - 1) / rpb;
+    if (db16) {
+      if (pt)
+        hipLaunchKernelGGL((rw_post_bwd<2, uint16_t>), dim3(bgrid), dim3(RW_NT), 0, s, dnh,
+                           (const uint16_t*)P, slot, B, T, F, C, pl, flat, af, sums, (uint16_t*)dz,
+                           bpart, rpb);
+      else
+        hipLaunchKernelGGL((rw_post_bwd<0, uint16_t>), dim3(bgrid), dim3(RW_NT), 0, s, dnh,
+                           (const uint16_t*)P, slot, B, T, F, C, pl, flat, af, sums, (uint16_t*)dz,
+                           bpart, rpb);
+    } else {
+      if (pt)
+        hipLaunchKernelGGL((rw_post_bwd<2, float>), dim3(bgrid), dim3(RW_NT), 0, s, dnext,
+                           (const uint16_t*)P, slot, B, T, F, C, pl, flat, af, sums, (uint16_t*)dz,
+                           bpart, rpb);
+      else
+        hipLaunchKernelGGL((rw_post_bwd<0, float>), dim3(bgrid), dim3(RW_NT), 0, s, dnext,
+                           (const uint16_t*)P, slot, B, T, F, C, pl, flat, af, sums, (uint16_t*)dz,
+                           bpart, rpb);
+    }
+  } else if (db16) {
     hipLaunchKernelGGL((post_bwd_full<uint16_t, uint16_t, uint16_t, TP>), dim3(pgrid), dim3(CT), 0, s,
                        dnh, P, zh, slot, B, T, F, C, pl, flat, af, sums, (uint16_t*)dz, bpart);
   } else if (zb) {
@@ -1486,7 +1868,7 @@ static int vgg_block_backward_impl(const void* dnext_v, int dnext_dtype, int fla
   ASR_LAUNCH_CHECK();
   if (dbias) {   // total over the blocks in order, then dbias += total
     float* tot = bpart + (size_t)pgrid * C;
-    hipLaunchKernelGGL(sum_partials, dim3((C + SP_COLS - 1) / SP_COLS), dim3(CT), 0, s, bpart, pgrid, C, 1.f,
+    hipLaunchKernelGGL(sum_partials, dim3((C + SP_COLS - 1) / SP_COLS), dim3(CT), 0, s, bpart, bgrid, C, 1.f,
                        tot);
     ASR_LAUNCH_CHECK();
     return asr_vgg_accumulate(tot, dbias, C, nullptr, nullptr, 0, stream);

@@ -138,6 +138,9 @@ def test_vgg_c1_direct_stencil_equals_tap_gemm(prec, cuda_dev, monkeypatch):
     asr_conv3x3_c1_wgrad_xs, sums the pixels in another order and has its own
     exact test in test_conv_tr_gpu.py.)"""
     monkeypatch.setenv('ASR_VGG_C1_WGRAD', '0')
+    # the element-wise passes in one form for both (the tap GEMM's f32 z keeps
+    # layer 0 off the bf16 row-blocked passes, whose BN sums run in another order)
+    monkeypatch.setenv('ASR_VGG_ROWS', '0')
     # (and the layer-0 input gradient kept f32: with the tap GEMM layer 0's z is
     # f32, which keeps its incoming gradient f32 too)
     monkeypatch.setenv('ASR_VGG_DX_BF16', '0')
@@ -163,6 +166,7 @@ def test_vgg_c1_direct_stencil_equals_tap_gemm(prec, cuda_dev, monkeypatch):
 def test_vgg_post_bwd_full_equals_gather_form(prec, cuda_dev, monkeypatch):
     # the gather form reads an f32 incoming gradient: keep the full pass's f32 too
     monkeypatch.setenv('ASR_VGG_DX_BF16', '0')
+    monkeypatch.setenv('ASR_VGG_ROWS', '0')   # (the row-blocked passes replace both)
     kw = dict(VGG_PROD, input_size=40)
     model = _ctc(kw)
     model.set_cuda()
@@ -179,6 +183,7 @@ def test_vgg_bf16_pool_store_is_exact(cuda_dev, monkeypatch):
     # P = max(0, max z) of a bf16 z is a bf16 value: the bf16 P store must give
     # bitwise the same loss and gradients as the f32 store (BN on, pooled and
     # unpooled layers)
+    monkeypatch.setenv('ASR_VGG_ROWS', '0')   # the f32 store is grid-stride only: same form
     kw = dict(VGG_PROD, input_size=40)
     model = _ctc(kw)
     model.set_cuda()
@@ -213,7 +218,9 @@ def test_vgg_fused_bn_variance_matches_two_pass(prec, cuda_dev, monkeypatch):
                if 'running' in k}
         out[flag] = (loss, g, run)
     (l1, g1, r1), (l0, g0, r0) = out['1'], out['0']
-    np.testing.assert_allclose(l1, l0, rtol=1e-5)
+    # (bf16: last-bit changes of the statistics move bf16 roundings of the
+    # activations; measured 1.8e-5 on the loss with the row-blocked passes)
+    np.testing.assert_allclose(l1, l0, rtol=1e-5 if prec == 'fp32' else 5e-5)
     if prec == 'fp32':
         # (in bf16 a last-bit change of the statistics moves bf16 roundings of
         # the activations, and the BN backward's cancellation amplifies that in
