@@ -900,6 +900,33 @@ __device__ __forceinline__ long long row_base(int b, int t, int T, int F, int C,
               : (((long long)b * (T + 2) + t + 1) * (F + 2) + 1) * C;
 }
 
+// A block's rows [r0, r1) of a grid with Tr rows per utterance, walked as one
+// flat sequence of 8-channel groups: lane l takes group l, then every 256th --
+// across row ends (rows of a 2 x 2-pooled 128-channel layer hold 320 groups:
+// per-row loops left most lanes idle in each row's tail).  ng % (C / 8) == 0
+// and 256 % (C / 8) == 0 keep a lane's channels fixed.
+struct RowWalk {
+  int r, b, t, g;
+  __device__ __forceinline__ RowWalk(int r0, int r1, int Tr, int ng) {
+    r = r0;
+    b = r0 / Tr;
+    t = r0 - b * Tr;
+    g = threadIdx.x;
+    settle(r1, Tr, ng);
+  }
+  __device__ __forceinline__ void settle(int r1, int Tr, int ng) {
+    while (g >= ng && r < r1) {
+      g -= ng;
+      ++r;
+      if (++t == Tr) { t = 0; ++b; }
+    }
+  }
+  __device__ __forceinline__ void next(int r1, int Tr, int ng) {
+    g += RW_NT;
+    settle(r1, Tr, ng);
+  }
+};
+
 // lanes with the same channel group (tid % cg8) hold partial sums of the same
 // 8 channels: out[c] = their sum in lane order (c < C)
 __device__ __forceinline__ void rw_reduce(const float (&acc)[8], int cg8, int C, float* red,
@@ -935,25 +962,22 @@ __global__ void __launch_bounds__(RW_NT) rw_apply(const uint16_t* __restrict__ P
   }
   const int rows = B * To, ng = Fo * cg8;
   const int r0 = blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
-  for (int rr = r0; rr < r1; ++rr) {
-    const int b = rr / To, t = rr - b * To;
-    const long long pb = (long long)rr * Fo * C;
-    const long long ob = row_base(b, t, To, Fo, C, flat);
-    for (int gg = tid; gg < ng; gg += RW_NT) {
-      const long long e = (long long)gg * 8;
-      Bf8 y;
-      y.load(P + pb + e);
-      if (af.mean) {
+  for (RowWalk it(r0, r1, To, ng); it.r < r1; it.next(r1, To, ng)) {
+    const long long pb = (long long)it.r * Fo * C;
+    const long long ob = row_base(it.b, it.t, To, Fo, C, flat);
+    const long long e = (long long)it.g * 8;
+    Bf8 y;
+    y.load(P + pb + e);
+    if (af.mean) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) y.v[j] = (y.v[j] - m[j]) * r[j] * g[j] + bt[j];
-      }
-      if (af.drop > 0.f) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          y.v[j] *= drop_scale(af.drop, af.seed, (unsigned long long)(pb + e + j));
-      }
-      y.store(out + ob + e);
+      for (int j = 0; j < 8; ++j) y.v[j] = (y.v[j] - m[j]) * r[j] * g[j] + bt[j];
     }
+    if (af.drop > 0.f) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        y.v[j] *= drop_scale(af.drop, af.seed, (unsigned long long)(pb + e + j));
+    }
+    y.store(out + ob + e);
   }
 }
 
@@ -980,10 +1004,10 @@ __global__ void __launch_bounds__(RW_NT) rw_post_fwd(const uint16_t* __restrict_
   }
   const int rows = B * pl.To, ng = pl.Fo * cg8;
   const int r0 = blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
-  for (int rr = r0; rr < r1; ++rr) {
-    const int b = rr / pl.To, to = rr - b * pl.To;
-    const long long pb = (long long)rr * pl.Fo * C;
-    for (int gg = tid; gg < ng; gg += RW_NT) {
+  for (RowWalk it(r0, r1, pl.To, ng); it.r < r1; it.next(r1, pl.To, ng)) {
+    const int b = it.b, to = it.t, gg = it.g;
+    const long long pb = (long long)it.r * pl.Fo * C;
+    {
       const int fo = gg >> sh3;
       const long long e = (long long)gg * 8;
       Bf8 best;
@@ -1055,12 +1079,11 @@ __global__ void __launch_bounds__(RW_NT) rw_bn_moments(const TD* __restrict__ dn
   }
   const int rows = B * To, ng = Fo * cg8;
   const int r0 = blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
-  for (int rr = r0; rr < r1; ++rr) {
-    const int b = rr / To, t = rr - b * To;
-    const long long pb = (long long)rr * Fo * C;
-    const long long db = row_base(b, t, To, Fo, C, flat);
-    for (int gg = tid; gg < ng; gg += RW_NT) {
-      const long long e = (long long)gg * 8;
+  for (RowWalk it(r0, r1, To, ng); it.r < r1; it.next(r1, To, ng)) {
+    const long long pb = (long long)it.r * Fo * C;
+    const long long db = row_base(it.b, it.t, To, Fo, C, flat);
+    {
+      const long long e = (long long)it.g * 8;
       Bf8 gv, x;
       gv.load(dnext + db + e);
       x.load(P + pb + e);
@@ -1108,14 +1131,14 @@ __global__ void __launch_bounds__(RW_NT) rw_post_bwd(const TD* __restrict__ dnex
   }
   const int rows = B * T, ng = F * cg8;
   const int r0 = blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
-  for (int rr = r0; rr < r1; ++rr) {
-    const int b = rr / T, t = rr - b * T;
+  for (RowWalk it(r0, r1, T, ng); it.r < r1; it.next(r1, T, ng)) {
+    const int b = it.b, t = it.t, gg = it.g;
     const int to = PL ? t >> 1 : t;
     const bool trow = to < pl.To;
     const long long zb = row_base(b, t, T, F, C, 0);
     const long long pb = ((long long)b * pl.To + to) * pl.Fo * C;
     const long long db = row_base(b, to, pl.To, pl.Fo, C, flat);
-    for (int gg = tid; gg < ng; gg += RW_NT) {
+    {
       const int f = gg >> sh3;
       const int fo = PL ? f >> 1 : f;
       Bf8 v;
