@@ -773,6 +773,27 @@ int asr_vgg_block_backward_zdp(const void* dnext, int dnext_dtype, int flat, con
                                float* dgamma, float* dbeta, float drop, unsigned long long seed,
                                void* dz, int dz_dtype, float* dbias, void* workspace,
                                size_t ws_bytes, void* stream);
+/* The first VGG layer (one input channel, stencil from the raw features as
+ * asr_conv3x3_c1_forward_xs) when it is unpooled and followed by batch norm:
+ * writes P = max(0, bf16(z)) [B][T][F][Co] bf16 directly -- the value the
+ * ReLU pass would store -- and, with mpart / qpart, per-block partial sums of
+ * P - shift and its square ([asr_vgg_c1_relu_p_blocks(B, T)][Co] each; shift =
+ * the running mean), so no conv output z is written or read back
+ * (cnn.py:124-165's Conv2d -> ReLU -> BatchNorm2d of layer 0). */
+int asr_vgg_c1_relu_p_blocks(int B, int T);
+int asr_vgg_c1_forward_relu_p(const float* xs, int round_bf16, int B, int T, int F, int Co,
+                              const float* w, const float* bias, uint16_t* P, const float* shift,
+                              float* mpart, float* qpart, void* stream);
+/* asr_vgg_block_forward_zp from that P and its partials: batch statistics
+ * (training) or running statistics, the running-stat update, and the next
+ * layer's input (bf16 padded rows, or flat f32).  workspace >= C floats. */
+int asr_vgg_block_forward_given_p(const uint16_t* P, int B, int T, int F, int C,
+                                  const float* gamma, const float* beta, float* run_mean,
+                                  float* run_var, int training, float momentum, float eps,
+                                  float* bn_mean, float* bn_rstd, float drop,
+                                  unsigned long long seed, void* out, int out_dtype, int flat,
+                                  const float* mpart, const float* qpart, int nblk,
+                                  void* workspace, size_t ws_bytes, void* stream);
 
 /* ----------------------------------------------------------- profiling
  * Sampled HIP-event timing of the recurrence step kernels on their own stream

@@ -179,6 +179,13 @@ SIGNATURES = {
                                          c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                          c_vp, c_float, ctypes.c_ulonglong, c_vp, c_int, c_vp, c_vp,
                                          c_size, c_vp]),
+    'asr_vgg_c1_relu_p_blocks': (c_int, [c_int, c_int]),
+    'asr_vgg_c1_forward_relu_p': (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp,
+                                          c_vp, c_vp, c_vp, c_vp, c_vp]),
+    'asr_vgg_block_forward_given_p': (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp,
+                                              c_vp, c_int, c_float, c_float, c_vp, c_vp, c_float,
+                                              ctypes.c_ulonglong, c_vp, c_int, c_int, c_vp, c_vp,
+                                              c_int, c_vp, c_size, c_vp]),
     'asr_vgg_block_forward_zp': (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                          c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
                                          c_float, c_float, c_vp, c_vp, c_float, ctypes.c_ulonglong,

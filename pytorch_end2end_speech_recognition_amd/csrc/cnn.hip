@@ -203,6 +203,100 @@ __global__ void __launch_bounds__(CT) conv3x3_c1_fwd_xs(const float* __restrict_
   }
 }
 
+// The same stencil with the next element-wise pass folded in, for an unpooled
+// layer followed by batch norm (vgg_hier's first layer): P = max(0, bf16(z))
+// written bf16 to the flat [B][T][F][Co] layout -- the value post_fwd would
+// store from the bf16 z -- and, with mpart / qpart, the batch-norm moment
+// partials of P - shift per block ([block][Co], a lane's four channels summed
+// in registers, the block's lanes combined in lane order).  z is never
+// written or read back.  ft time rows per block (so the partial count stays
+// near 1024).
+__global__ void __launch_bounds__(CT) conv3x3_c1_fwd_relu_p(
+    const float* __restrict__ xs, int T, int F, int Co, int round_bf16, int ft,
+    const float* __restrict__ w, const float* __restrict__ bias, uint16_t* __restrict__ P,
+    const float* __restrict__ shift, float* __restrict__ mpart, float* __restrict__ qpart) {
+  extern __shared__ float sm[];
+  __shared__ float red[CT * 4];
+  float* xr = sm;                    // [ft + 2][F + 2], zero halo
+  const int ntile = (T + ft - 1) / ft;
+  const int b = blockIdx.x / ntile, t0 = (blockIdx.x - b * ntile) * ft;
+  const int W = F + 2;
+  for (int i = threadIdx.x; i < (ft + 2) * W; i += CT) {
+    const int r = i / W, fp = i - r * W;
+    const int t = t0 - 1 + r, f = fp - 1;
+    float v = 0.f;
+    if (t >= 0 && t < T && f >= 0 && f < F) {
+      v = xs[((long long)b * T + t) * F + f];
+      if (round_bf16) v = bf2f(f2bf(v));
+    }
+    xr[i] = v;
+  }
+  const int ng = Co >> 2;
+  const int c4 = 4 * (threadIdx.x % ng);
+  float4 wr[9];
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    wr[tap].x = w[(c4 + 0) * 9 + tap];
+    wr[tap].y = w[(c4 + 1) * 9 + tap];
+    wr[tap].z = w[(c4 + 2) * 9 + tap];
+    wr[tap].w = w[(c4 + 3) * 9 + tap];
+  }
+  const float4 b4 = bias ? *reinterpret_cast<const float4*>(bias + c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+  float sh[4] = {0.f, 0.f, 0.f, 0.f}, macc[4] = {0.f, 0.f, 0.f, 0.f}, qacc[4] = {0.f, 0.f, 0.f, 0.f};
+  if (mpart && shift) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sh[j] = shift[c4 + j];
+  }
+  __syncthreads();
+  const int nt = min(ft, T - t0);
+  const int ppi = CT / ng;
+  for (int q = threadIdx.x / ng; q < nt * F; q += ppi) {
+    const int r = q / F, f = q - r * F;
+    float4 acc = b4;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const float xv = xr[(r + kw) * W + f + kh];
+        const float4 wv = wr[kh * 3 + kw];
+        acc.x += wv.x * xv;
+        acc.y += wv.y * xv;
+        acc.z += wv.z * xv;
+        acc.w += wv.w * xv;
+      }
+    const uint16_t h[4] = {f2bf(acc.x), f2bf(acc.y), f2bf(acc.z), f2bf(acc.w)};
+    float pv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      pv[j] = fmaxf(bf2f(h[j]), 0.f);   // exact: a bf16 value or 0
+      const float d = pv[j] - sh[j];
+      macc[j] += d;
+      qacc[j] += d * d;
+    }
+    uint2 o;
+    o.x = (unsigned)f2bf(pv[0]) | ((unsigned)f2bf(pv[1]) << 16);
+    o.y = (unsigned)f2bf(pv[2]) | ((unsigned)f2bf(pv[3]) << 16);
+    *reinterpret_cast<uint2*>(P + (((long long)b * T + t0 + r) * F + f) * Co + c4) = o;
+  }
+  if (mpart) {   // lanes tid, tid + ng, ... hold the same four channels
+    auto reduce = [&](const float (&acc)[4], float* out) {
+      const int tid = threadIdx.x;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) red[tid * 4 + j] = acc[j];
+      __syncthreads();
+      for (int cc = tid; cc < Co; cc += CT) {
+        const int g2 = cc >> 2, j = cc & 3;
+        float t = 0.f;
+        for (int k = g2; k < CT; k += ng) t += red[k * 4 + j];
+        out[cc] = t;
+      }
+      __syncthreads();
+    };
+    reduce(macc, mpart + (long long)blockIdx.x * Co);
+    if (qpart) reduce(qacc, qpart + (long long)blockIdx.x * Co);
+  }
+}
+
 // dx[p][ci] = sum_{co,kh,kw} dz[p - shift][co] w[co][ci][kh][kw] (dz halo rows zero)
 __global__ void conv_direct_dgrad(const float* __restrict__ dz, int B, int T, int F, int Ci,
                                   int Co, const float* __restrict__ w, float* __restrict__ dx) {
@@ -907,11 +1001,15 @@ __device__ __forceinline__ long long row_base(int b, int t, int T, int F, int C,
 // and 256 % (C / 8) == 0 keep a lane's channels fixed.
 struct RowWalk {
   int r, b, t, g;
-  __device__ __forceinline__ RowWalk(int r0, int r1, int Tr, int ng) {
+  __device__ __forceinline__ RowWalk() {}
+  // goff: this walker's first group beyond the lane's (U walkers per lane keep
+  // U 16-B loads in flight: with one, a lane's load -> use -> store chain left
+  // the passes at ~3.3 TB/s)
+  __device__ __forceinline__ RowWalk(int r0, int r1, int Tr, int ng, int goff = 0) {
     r = r0;
     b = r0 / Tr;
     t = r0 - b * Tr;
-    g = threadIdx.x;
+    g = threadIdx.x + goff;
     settle(r1, Tr, ng);
   }
   __device__ __forceinline__ void settle(int r1, int Tr, int ng) {
@@ -921,11 +1019,12 @@ struct RowWalk {
       if (++t == Tr) { t = 0; ++b; }
     }
   }
-  __device__ __forceinline__ void next(int r1, int Tr, int ng) {
-    g += RW_NT;
+  __device__ __forceinline__ void next(int r1, int Tr, int ng, int stride = RW_NT) {
+    g += stride;
     settle(r1, Tr, ng);
   }
 };
+constexpr int RW_U = 4;   // walkers per lane
 
 // lanes with the same channel group (tid % cg8) hold partial sums of the same
 // 8 channels: out[c] = their sum in lane order (c < C)
@@ -962,22 +1061,32 @@ __global__ void __launch_bounds__(RW_NT) rw_apply(const uint16_t* __restrict__ P
   }
   const int rows = B * To, ng = Fo * cg8;
   const int r0 = blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
-  for (RowWalk it(r0, r1, To, ng); it.r < r1; it.next(r1, To, ng)) {
-    const long long pb = (long long)it.r * Fo * C;
-    const long long ob = row_base(it.b, it.t, To, Fo, C, flat);
-    const long long e = (long long)it.g * 8;
-    Bf8 y;
-    y.load(P + pb + e);
-    if (af.mean) {
+  RowWalk it[RW_U];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) y.v[j] = (y.v[j] - m[j]) * r[j] * g[j] + bt[j];
-    }
-    if (af.drop > 0.f) {
+  for (int u = 0; u < RW_U; ++u) it[u] = RowWalk(r0, r1, To, ng, u * RW_NT);
+  while (it[0].r < r1) {   // walker 0 trails the others
+    Bf8 y[RW_U];
+    long long pe[RW_U];
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        y.v[j] *= drop_scale(af.drop, af.seed, (unsigned long long)(pb + e + j));
+    for (int u = 0; u < RW_U; ++u) {
+      pe[u] = (long long)it[u].r * Fo * C + (long long)it[u].g * 8;
+      if (it[u].r < r1) y[u].load(P + pe[u]);
     }
-    y.store(out + ob + e);
+#pragma unroll
+    for (int u = 0; u < RW_U; ++u) {
+      if (it[u].r >= r1) continue;
+      if (af.mean) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[u].v[j] = (y[u].v[j] - m[j]) * r[j] * g[j] + bt[j];
+      }
+      if (af.drop > 0.f) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          y[u].v[j] *= drop_scale(af.drop, af.seed, (unsigned long long)(pe[u] + j));
+      }
+      y[u].store(out + row_base(it[u].b, it[u].t, To, Fo, C, flat) + (long long)it[u].g * 8);
+      it[u].next(r1, To, ng, RW_U * RW_NT);
+    }
   }
 }
 
@@ -1004,53 +1113,70 @@ __global__ void __launch_bounds__(RW_NT) rw_post_fwd(const uint16_t* __restrict_
   }
   const int rows = B * pl.To, ng = pl.Fo * cg8;
   const int r0 = blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
-  for (RowWalk it(r0, r1, pl.To, ng); it.r < r1; it.next(r1, pl.To, ng)) {
-    const int b = it.b, to = it.t, gg = it.g;
-    const long long pb = (long long)it.r * pl.Fo * C;
-    {
-      const int fo = gg >> sh3;
-      const long long e = (long long)gg * 8;
-      Bf8 best;
+  constexpr int U = PL ? 2 : RW_U;   // walkers per lane (a pooled walker loads four pixels)
+  RowWalk it[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) it[u] = RowWalk(r0, r1, pl.To, ng, u * RW_NT);
+  while (it[0].r < r1) {
+    Bf8 best[U];
+    unsigned bs[U][8];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (it[u].r >= r1) continue;
+      const int b = it[u].b, to = it[u].t;
+      const int fo = it[u].g >> sh3;
       if constexpr (PL == 0) {
-        best.load(z + row_base(b, to, T, F, C, 0) + e);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) best.v[j] = fmaxf(best.v[j], 0.f);
+        best[u].load(z + row_base(b, to, T, F, C, 0) + (long long)it[u].g * 8);
       } else {
-        unsigned bs[8];
+        Bf8 x[4];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          best.v[j] = -__builtin_huge_valf();
-          bs[j] = 0u;
-        }
-#pragma unroll
-        for (int df = 0; df < 2; ++df) {
-          const int f = fo * 2 + df;
+        for (int df = 0; df < 2; ++df)
 #pragma unroll
           for (int dt = 0; dt < 2; ++dt) {
-            const int t = to * 2 + dt;
+            const int f = fo * 2 + df, t = to * 2 + dt;
+            if (f < F && t < T) x[df * 2 + dt].load(z + row_base(b, t, T, F, C, 0) + (long long)f * C + c);
+          }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          best[u].v[j] = -__builtin_huge_valf();
+          bs[u][j] = 0u;
+        }
+#pragma unroll
+        for (int df = 0; df < 2; ++df)
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt) {
+            const int f = fo * 2 + df, t = to * 2 + dt;
             if (f < F && t < T) {
-              Bf8 x;
-              x.load(z + row_base(b, t, T, F, C, 0) + (long long)f * C + c);
 #pragma unroll
               for (int j = 0; j < 8; ++j) {
-                const float v = fmaxf(x.v[j], 0.f);
-                if (v > best.v[j]) { best.v[j] = v; bs[j] = (unsigned)(df * 2 + dt); }
+                const float v = fmaxf(x[df * 2 + dt].v[j], 0.f);
+                if (v > best[u].v[j]) { best[u].v[j] = v; bs[u][j] = (unsigned)(df * 2 + dt); }
               }
             }
           }
-        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {   // in walker order: the moment sums' order is fixed
+      if (it[u].r >= r1) continue;
+      const long long pe = (long long)it[u].r * pl.Fo * C + (long long)it[u].g * 8;
+      if constexpr (PL == 0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) best[u].v[j] = fmaxf(best[u].v[j], 0.f);
+      } else {
         uint2 sl;
-        sl.x = bs[0] | (bs[1] << 8) | (bs[2] << 16) | (bs[3] << 24);
-        sl.y = bs[4] | (bs[5] << 8) | (bs[6] << 16) | (bs[7] << 24);
-        *reinterpret_cast<uint2*>(slot + pb + e) = sl;
+        sl.x = bs[u][0] | (bs[u][1] << 8) | (bs[u][2] << 16) | (bs[u][3] << 24);
+        sl.y = bs[u][4] | (bs[u][5] << 8) | (bs[u][6] << 16) | (bs[u][7] << 24);
+        *reinterpret_cast<uint2*>(slot + pe) = sl;
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float d = best.v[j] - sh[j];
+        const float d = best[u].v[j] - sh[j];
         macc[j] += d;
         qacc[j] += d * d;
       }
-      best.store(P + pb + e);
+      best[u].store(P + pe);
+      it[u].next(r1, pl.To, ng, U * RW_NT);
     }
   }
   if (mpart) {
@@ -1079,24 +1205,35 @@ __global__ void __launch_bounds__(RW_NT) rw_bn_moments(const TD* __restrict__ dn
   }
   const int rows = B * To, ng = Fo * cg8;
   const int r0 = blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
-  for (RowWalk it(r0, r1, To, ng); it.r < r1; it.next(r1, To, ng)) {
-    const long long pb = (long long)it.r * Fo * C;
-    const long long db = row_base(it.b, it.t, To, Fo, C, flat);
-    {
-      const long long e = (long long)it.g * 8;
-      Bf8 gv, x;
-      gv.load(dnext + db + e);
-      x.load(P + pb + e);
+  RowWalk it[RW_U];
+#pragma unroll
+  for (int u = 0; u < RW_U; ++u) it[u] = RowWalk(r0, r1, To, ng, u * RW_NT);
+  while (it[0].r < r1) {
+    Bf8 gv[RW_U], x[RW_U];
+    long long pe[RW_U];
+#pragma unroll
+    for (int u = 0; u < RW_U; ++u) {
+      const long long e = (long long)it[u].g * 8;
+      pe[u] = (long long)it[u].r * Fo * C + e;
+      if (it[u].r < r1) {
+        gv[u].load(dnext + row_base(it[u].b, it[u].t, To, Fo, C, flat) + e);
+        x[u].load(P + pe[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < RW_U; ++u) {   // in walker order: the sums' order is fixed
+      if (it[u].r >= r1) continue;
       if (af.drop > 0.f) {
 #pragma unroll
         for (int j = 0; j < 8; ++j)
-          gv.v[j] *= drop_scale(af.drop, af.seed, (unsigned long long)(pb + e + j));
+          gv[u].v[j] *= drop_scale(af.drop, af.seed, (unsigned long long)(pe[u] + j));
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        s1[j] += gv.v[j];
-        s2[j] += gv.v[j] * (x.v[j] - m[j]) * rs[j];
+        s1[j] += gv[u].v[j];
+        s2[j] += gv[u].v[j] * (x[u].v[j] - m[j]) * rs[j];
       }
+      it[u].next(r1, To, ng, RW_U * RW_NT);
     }
   }
   rw_reduce(s1, cg8, C, red, partial + (long long)blockIdx.x * 2 * C);
@@ -1131,47 +1268,56 @@ __global__ void __launch_bounds__(RW_NT) rw_post_bwd(const TD* __restrict__ dnex
   }
   const int rows = B * T, ng = F * cg8;
   const int r0 = blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
-  for (RowWalk it(r0, r1, T, ng); it.r < r1; it.next(r1, T, ng)) {
-    const int b = it.b, t = it.t, gg = it.g;
-    const int to = PL ? t >> 1 : t;
-    const bool trow = to < pl.To;
-    const long long zb = row_base(b, t, T, F, C, 0);
-    const long long pb = ((long long)b * pl.To + to) * pl.Fo * C;
-    const long long db = row_base(b, to, pl.To, pl.Fo, C, flat);
-    {
-      const int f = gg >> sh3;
-      const int fo = PL ? f >> 1 : f;
+  constexpr int U = 2;   // walkers per lane (three loads each)
+  RowWalk it[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) it[u] = RowWalk(r0, r1, T, ng, u * RW_NT);
+  while (it[0].r < r1) {
+    Bf8 g[U], x[U];
+    unsigned long long sl[U];
+    bool in[U];
+    long long pbi[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int t = it[u].t, to = PL ? t >> 1 : t;
+      const int f = it[u].g >> sh3, fo = PL ? f >> 1 : f;
+      in[u] = it[u].r < r1 && to < pl.To && fo < pl.Fo;
+      const long long ip = (long long)fo * C + c;
+      pbi[u] = ((long long)it[u].b * pl.To + to) * pl.Fo * C + ip;
+      sl[u] = 0ull;
+      if (in[u]) {
+        g[u].load(dnext + row_base(it[u].b, to, pl.To, pl.Fo, C, flat) + ip);
+        x[u].load(P + pbi[u]);
+        if constexpr (PL != 0) sl[u] = *reinterpret_cast<const unsigned long long*>(slot + pbi[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {   // in walker order: the bias sums' order is fixed
+      if (it[u].r >= r1) continue;
+      const int t = it[u].t, to = PL ? t >> 1 : t;
+      const int f = it[u].g >> sh3, fo = PL ? f >> 1 : f;
       Bf8 v;
 #pragma unroll
       for (int j = 0; j < 8; ++j) v.v[j] = 0.f;
-      if (trow && fo < pl.Fo) {
-        const long long ip = (long long)fo * C + c;
-        Bf8 g, x;
-        g.load(dnext + db + ip);
-        x.load(P + pb + ip);
+      if (in[u]) {
         if (af.drop > 0.f) {
 #pragma unroll
           for (int j = 0; j < 8; ++j)
-            g.v[j] *= drop_scale(af.drop, af.seed, (unsigned long long)(pb + ip + j));
+            g[u].v[j] *= drop_scale(af.drop, af.seed, (unsigned long long)(pbi[u] + j));
         }
+        const unsigned long long me =
+            PL ? (unsigned long long)((f - fo * 2) * 2 + (t - to * 2)) : 0ull;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float xh = (x.v[j] - m[j]) * r[j];
-          g.v[j] = gm[j] * r[j] * (g.v[j] - a1[j] * inv_n - xh * a2[j] * inv_n);
-        }
-        unsigned long long sl = 0ull, me = 0ull;
-        if constexpr (PL != 0) {
-          sl = *reinterpret_cast<const unsigned long long*>(slot + pb + ip);
-          me = (unsigned long long)((f - fo * 2) * 2 + (t - to * 2));
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const bool hit = PL == 0 || ((sl >> (8 * j)) & 0xffull) == me;
-          v.v[j] = (hit && x.v[j] > 0.f) ? g.v[j] : 0.f;
+          const float xh = (x[u].v[j] - m[j]) * r[j];
+          const float gj = gm[j] * r[j] * (g[u].v[j] - a1[j] * inv_n - xh * a2[j] * inv_n);
+          const bool hit = PL == 0 || ((sl[u] >> (8 * j)) & 0xffull) == me;
+          v.v[j] = (hit && x[u].v[j] > 0.f) ? gj : 0.f;
           bacc[j] += v.v[j];
         }
       }
-      v.store(dz + zb + (long long)gg * 8);
+      v.store(dz + row_base(it[u].b, t, T, F, C, 0) + (long long)it[u].g * 8);
+      it[u].next(r1, T, ng, U * RW_NT);
     }
   }
   if (bias_part) rw_reduce(bacc, cg8, C, red, bias_part + (long long)blockIdx.x * C);
@@ -1386,6 +1532,38 @@ extern "C" int asr_conv3x3_c1_forward_xs(const float* xs, int round_bf16, int B,
   else
     hipLaunchKernelGGL(conv3x3_c1_fwd_xs<float>, dim3((unsigned)nwg), dim3(CT), lds,
                        (hipStream_t)stream, xs, T, F, Co, round_bf16, w, bias, (float*)z);
+  ASR_LAUNCH_CHECK();
+  return ASR_OK;
+}
+
+// Rows per block of asr_vgg_c1_forward_relu_p (its partial count = the return
+// value of asr_vgg_c1_relu_p_blocks).
+static int c1p_rows(int B, int T) {
+  const long long want = 1024;
+  int ft = (int)(((long long)B * T + want - 1) / want);
+  return std::max(4, std::min(ft, 64));
+}
+extern "C" int asr_vgg_c1_relu_p_blocks(int B, int T) {
+  const int ft = c1p_rows(B, T);
+  return B * ((T + ft - 1) / ft);
+}
+
+extern "C" int asr_vgg_c1_forward_relu_p(const float* xs, int round_bf16, int B, int T, int F,
+                                         int Co, const float* w, const float* bias,
+                                         uint16_t* P, const float* shift, float* mpart,
+                                         float* qpart, void* stream) {
+  ASR_REQUIRE(xs && w && P && B > 0 && T > 0 && F > 0, ASR_ERR_ARG, "c1_forward_relu_p: bad args");
+  ASR_REQUIRE(Co > 0 && Co % 4 == 0 && CT % (Co / 4) == 0, ASR_ERR_UNSUPPORTED,
+              "c1_forward_relu_p: Co / 4 must divide %d", CT);
+  ASR_REQUIRE(((uintptr_t)P & 7) == 0 && (!bias || ((uintptr_t)bias & 15) == 0), ASR_ERR_ARG,
+              "c1_forward_relu_p: P / bias alignment");
+  ASR_REQUIRE(!qpart || (mpart && shift), ASR_ERR_ARG, "c1_forward_relu_p: qpart needs mpart, shift");
+  const int ft = c1p_rows(B, T);
+  const size_t lds = (size_t)(ft + 2) * (F + 2) * 4;
+  ASR_REQUIRE(lds <= 48 * 1024, ASR_ERR_UNSUPPORTED, "c1_forward_relu_p: F too large");
+  const int nwg = asr_vgg_c1_relu_p_blocks(B, T);
+  hipLaunchKernelGGL(conv3x3_c1_fwd_relu_p, dim3((unsigned)nwg), dim3(CT), lds, (hipStream_t)stream,
+                     xs, T, F, Co, round_bf16, ft, w, bias, P, shift, mpart, qpart);
   ASR_LAUNCH_CHECK();
   return ASR_OK;
 }
@@ -1692,6 +1870,62 @@ extern "C" int asr_vgg_block_forward_z(const void* z, int z_dtype, int B, int T,
                                   stream);
 }
 
+// asr_vgg_block_forward_zp for an unpooled layer whose P (bf16, flat) and
+// batch-norm moment partials were produced by its convolution
+// (asr_vgg_c1_forward_relu_p; mpart / qpart [nblk][C] of P - run_mean and its
+// square): the statistics, the running-stat update and the next layer's
+// input, without the ReLU pass.  workspace >= C floats.
+extern "C" int asr_vgg_block_forward_given_p(const uint16_t* P, int B, int T, int F, int C,
+                                             const float* gamma, const float* beta,
+                                             float* run_mean, float* run_var, int training,
+                                             float momentum, float eps, float* bn_mean,
+                                             float* bn_rstd, float drop, unsigned long long seed,
+                                             void* out, int out_dtype, int flat,
+                                             const float* mpart, const float* qpart, int nblk,
+                                             void* workspace, size_t ws_bytes, void* stream) {
+  ASR_REQUIRE(P && out && B > 0 && T > 0 && F > 0, ASR_ERR_ARG, "vgg_block_forward_given_p: bad args");
+  ASR_REQUIRE(rw_ok<uint16_t>(C, 0, 0) && ((uintptr_t)P & 15) == 0 && ((uintptr_t)out & 15) == 0 &&
+              (out_dtype == ASR_DT_F32 || !flat), ASR_ERR_UNSUPPORTED,
+              "vgg_block_forward_given_p: row-blocked apply only");
+  hipStream_t s = (hipStream_t)stream;
+  const long long nr = (long long)B * T * F;
+  Affine af{nullptr, nullptr, nullptr, nullptr, drop, seed};
+  if (gamma) {
+    ASR_REQUIRE(beta && bn_mean && bn_rstd, ASR_ERR_ARG, "vgg_block_forward_given_p: BN args");
+    if (training) {
+      ASR_REQUIRE(mpart && qpart && nblk > 0 && run_mean && run_var && workspace &&
+                  ws_bytes >= (size_t)C * sizeof(float), ASR_ERR_ARG,
+                  "vgg_block_forward_given_p: training needs the partials and running stats");
+      float* m2 = (float*)workspace;
+      hipLaunchKernelGGL(sum_partials, dim3((C + SP_COLS - 1) / SP_COLS), dim3(CT), 0, s, mpart,
+                         nblk, C, 1.f / (float)nr, bn_mean);
+      hipLaunchKernelGGL(sum_partials, dim3((C + SP_COLS - 1) / SP_COLS), dim3(CT), 0, s, qpart,
+                         nblk, C, 1.f / (float)nr, m2);
+      hipLaunchKernelGGL(bn_finalize_shift, dim3((C + CT - 1) / CT), dim3(CT), 0, s, bn_mean, m2,
+                         run_mean, C, nr, eps, momentum, bn_rstd, run_mean, run_var);
+    } else {
+      ASR_REQUIRE(run_mean && run_var, ASR_ERR_ARG, "vgg_block_forward_given_p: eval needs running stats");
+      hipLaunchKernelGGL(bn_eval_stats, dim3((C + CT - 1) / CT), dim3(CT), 0, s, run_mean, run_var,
+                         C, eps, bn_mean, bn_rstd);
+    }
+    ASR_LAUNCH_CHECK();
+    af.mean = bn_mean;
+    af.rstd = bn_rstd;
+    af.gamma = gamma;
+    af.beta = beta;
+  }
+  const int nrow = B * T;
+  const int agrid = std::min(nrow, 4096), arpb = (nrow + agrid - 1) / agrid;
+  if (out_dtype == ASR_DT_BF16)
+    hipLaunchKernelGGL((rw_apply<uint16_t>), dim3((nrow + arpb - 1) / arpb), dim3(RW_NT), 0, s, P, B,
+                       T, F, C, af, (uint16_t*)out, flat, arpb);
+  else
+    hipLaunchKernelGGL((rw_apply<float>), dim3((nrow + arpb - 1) / arpb), dim3(RW_NT), 0, s, P, B, T,
+                       F, C, af, (float*)out, flat, arpb);
+  ASR_LAUNCH_CHECK();
+  return ASR_OK;
+}
+
 // Backward of asr_vgg_block_forward (same geometry / saved tensors): dnext is
 // the gradient of `out` (padded rows f32 or flat); dz [padded pixels][C] of
 // dz_dtype receives d(conv output) (the caller zeroes it: halo and
@@ -1773,6 +2007,9 @@ static int vgg_block_backward_impl(const void* dnext_v, int dnext_dtype, int fla
   float* bpart = nullptr;
   const int pgrid = post_grid(nr, C);
   // row-blocked passes (rw_*): bf16 z / P / dz with batch norm, 16-B aligned
+  // z == P (the convolution wrote only P, asr_vgg_c1_forward_relu_p): the ReLU
+  // mask must come from P -- the row-blocked pass or the full pass with BN
+  const bool z_is_p = (const void*)z == (const void*)P;
   const bool rows_b = rw_ok<TP>(C, pt, pf) && gamma && z_dtype == ASR_DT_BF16 &&
                       dz_dtype == ASR_DT_BF16 && ((uintptr_t)P & 15) == 0 &&
                       ((uintptr_t)dz & 15) == 0 && ((uintptr_t)dnext_v & 15) == 0 &&
@@ -1828,6 +2065,8 @@ static int vgg_block_backward_impl(const void* dnext_v, int dnext_dtype, int fla
   const float* zf = (const float*)z;
   const uint16_t* zh = (const uint16_t*)z;
   ASR_REQUIRE(!db16 || full, ASR_ERR_UNSUPPORTED, "vgg_block_backward: bf16 dnext needs the full pass");
+  ASR_REQUIRE(!z_is_p || rows_b || (full && gamma && pt == 0), ASR_ERR_UNSUPPORTED,
+              "vgg_block_backward: z aliased to P needs a pass that masks from P");
   int bgrid = pgrid;
   if (rows_b) {   // at most pgrid blocks (the bias-partial region)
     const int nrow = B * T, rpb = (nrow + pgrid - 1) / pgrid;

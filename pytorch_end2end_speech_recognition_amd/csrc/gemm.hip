@@ -1466,9 +1466,21 @@ __device__ __forceinline__ void stager_init(const Operand& op, StageR& st, int t
   }
 }
 
+// a K-mode operand whose k-rows are consecutive rows of one group (no time
+// offset / stride / limit): row k sits at k * stride_t -- one 32-bit multiply-add
+// per DMA instead of the (b, t) walk with 64-bit products (the weight-gradient
+// operands dG and X; the shifted h_{t-1} rows of dW_hh keep the walk)
+__device__ __forceinline__ bool kmode_dense(const RowMap& m) {
+  return m.t_mul == 1 && m.t_add == 0 && !m.perm &&
+         (m.rows_per_b >= 0x40000000 || m.stride_b == (long long)m.rows_per_b * m.stride_t) &&
+         m.t_limit >= m.rows_per_b;
+}
+
 template <int MODE>
 __device__ __forceinline__ void stager(const Operand& op, __amdgpu_buffer_rsrc_t rs, StageR& st,
                                        char* lds_tile, int k0, int kend, int wave) {
+  const bool dense = MODE == 1 && kmode_dense(op.map);
+  const unsigned kst = (unsigned)(op.map.stride_t * 2);
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int blk = wave * 2 + i;
@@ -1476,6 +1488,8 @@ __device__ __forceinline__ void stager(const Operand& op, __amdgpu_buffer_rsrc_t
     const int k = k0 + st.kr[i];
     if (MODE == 0) {
       if (((st.valid >> i) & 1) && k < kend) voff = st.base[i] + (unsigned)(k * 2);
+    } else if (dense) {
+      if (k < kend) voff = (unsigned)k * kst + st.base[i];
     } else {
       const int tp = st.t[i] * op.map.t_mul + op.map.t_add;
       if (k < kend && tp >= 0 && tp < op.map.t_limit)
@@ -1598,9 +1612,12 @@ gemm_bf16_8r(Params P) {
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __builtin_amdgcn_s_barrier();
-  bf16x8 b0[4], a0[4], a1[4];
+  bf16x8 b0[4], b1[4], a0[4], a1[4];
   fragsr<AMODE, BMODE>(smem, wr, wc, lane, true, a0, b0);
-  for (int kt = 0; kt < nk; ++kt) {
+  // one k-tile; bc: its B fragments, bn: receives the next tile's (the loop
+  // runs two tiles per trip with the roles swapped, so the B fragments are
+  // never copied -- 16 v_mov per k-tile and wave otherwise)
+  auto ktile = [&](int kt, bf16x8 (&bc)[4], bf16x8 (&bn)[4]) {
     const char* cur = smem + (kt % NSLOT) * SLOT;
     // slot (kt - 1) % NSLOT was last read before iteration kt - 1's barrier
     // the DMA of k-tile kt + 4 is spread over the two MFMA phases (A before the
@@ -1610,10 +1627,9 @@ gemm_bf16_8r(Params P) {
     char* fre = smem + ((kt + NSLOT - 1) % NSLOT) * SLOT;
     const int kd = kbeg + (kt + NSLOT - 1) * BKR;
     if (dma) stager<AMODE>(pr.a, ra, sa, fre, kd, kend, w);
-    fragsr<AMODE, BMODE>(cur, wr + 64, wc, lane, false, a1, b0);
-    mma8(a0, b0, acc, 0);
+    fragsr<AMODE, BMODE>(cur, wr + 64, wc, lane, false, a1, bc);
+    mma8(a0, bc, acc, 0);
     if (dma) stager<BMODE>(pr.b, rb, sb, fre + TILER, kd, kend, w);
-    bf16x8 b1[4];
     if (kt + 1 < nk) {
       const int after = min(NSLOT - 2, nk - 2 - kt);    // k-tiles issued after tile kt + 1
       if (after >= 3) asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory");
@@ -1623,11 +1639,13 @@ gemm_bf16_8r(Params P) {
       // k-tile kt + 1 landed for all waves; every wave's reads of slot kt done
       __builtin_amdgcn_s_barrier();
       const char* nxt = smem + ((kt + 1) % NSLOT) * SLOT;
-      fragsr<AMODE, BMODE>(nxt, wr, wc, lane, true, a0, b1);
+      fragsr<AMODE, BMODE>(nxt, wr, wc, lane, true, a0, bn);
     }
-    mma8(a1, b0, acc, 1);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) b0[j] = b1[j];
+    mma8(a1, bc, acc, 1);
+  };
+  for (int kt = 0; kt < nk; kt += 2) {
+    ktile(kt, b0, b1);
+    if (kt + 1 < nk) ktile(kt + 1, b1, b0);
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 

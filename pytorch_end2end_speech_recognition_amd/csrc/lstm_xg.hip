@@ -557,7 +557,18 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
   constexpr int PROW = 4 * XU + 4;
   constexpr int PSZ = R * PROW;
   auto prow = [](int r) { return r * PROW; };
+  // the sweepers' partials column-major: a lane's four rows of one gate column
+  // (its MFMA accumulator) are one 16-B store -- four per lane instead of
+  // sixteen 4-B stores between the MFMAs and barrier B(s); a 12-float column
+  // pitch keeps the cells' reads (4 rows x 16 units per wave) conflict-free.
+  // (-DASR_XGX_PART_ROWS builds keep the row-major form, for A/B runs.)
+#ifndef ASR_XGX_PART_ROWS
+  constexpr int PCOL = R + 4;
+  static_assert(R == 8, "column pitch chosen for 8 rows");
+  __shared__ __attribute__((aligned(16))) float part[2][NSW][4 * XU * PCOL];
+#else
   __shared__ float part[2][NSW][PSZ];
+#endif
   __shared__ float xpart[2][NPW][PSZ];
   // input rows of steps s+1 .. s+3: [3 slots][R rows][XGX_DMAX] bf16, filled by
   // buffer -> LDS DMA three steps ahead (16-B chunks XOR-swizzled by row when
@@ -658,8 +669,12 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
       if (4 * kq < R) {
 #pragma unroll
         for (int g = 0; g < 4; ++g)
+#ifndef ASR_XGX_PART_ROWS
+          *reinterpret_cast<f32x4*>(&part[s & 1][wave][(g * XU + ln) * PCOL + 4 * kq]) = acc[g];
+#else
 #pragma unroll
           for (int r = 0; r < 4; ++r) part[s & 1][wave][prow(4 * kq + r) + g * XU + ln] = acc[g][r];
+#endif
       }
       XG_TR(s, 4, __builtin_amdgcn_s_memrealtime());
       __syncthreads();  // B(s)
@@ -832,9 +847,14 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int col = q * XU + unit;
-        float a = part[s & 1][0][prow(row) + col];
+#ifndef ASR_XGX_PART_ROWS
+        const int pi = col * PCOL + row;
+#else
+        const int pi = prow(row) + col;
+#endif
+        float a = part[s & 1][0][pi];
 #pragma unroll
-        for (int w = 1; w < NSW; ++w) a += part[s & 1][w][prow(row) + col];
+        for (int w = 1; w < NSW; ++w) a += part[s & 1][w][pi];
         pre[q] = a + gxv[q];
       }
       if (ct == 0 && tr) {   // (trace) the partial sums are in registers
@@ -925,7 +945,8 @@ __global__ void __launch_bounds__(256 + R * XB + 16 * XB) lstm_bwd_xg(
   constexpr int NPG = 256 / LPS;       // producer subsets swept in parallel
   constexpr int NKS = XB / 8;          // MFMA k-steps: 4 gates x XB units / 32
   constexpr int NMW = XB / 4;          // MFMA waves (8 at XB = 32: 64 fragment VGPRs each)
-  __shared__ float red[NPG][R][XB + 1];
+  // row pitch XB + 4: a sweeper lane's 8 partial sums are two 16-B stores
+  __shared__ __attribute__((aligned(16))) float red[NPG][R][XB + 4];
   __shared__ __attribute__((aligned(16))) uint16_t dgt[16][4 * XB + 8];
   __shared__ int s_dead;
   __shared__ int s_pl[4];
@@ -1034,7 +1055,9 @@ __global__ void __launch_bounds__(256 + R * XB + 16 * XB) lstm_bwd_xg(
           }
         }
 #pragma unroll
-        for (int e = 0; e < 8; ++e) red[pgi][srow][8 * sq + e] = sm[e];
+        for (int e = 0; e < 8; e += 4)
+          *reinterpret_cast<f32x4*>(&red[pgi][srow][8 * sq + e]) =
+              f32x4{sm[e], sm[e + 1], sm[e + 2], sm[e + 3]};
       }
       if (dyw) {   // chunk dyk + 1 (one step may cross at most one boundary)
         for (unsigned spins = 0; dyv != dyepoch; ++spins) {

@@ -1940,9 +1940,26 @@ class VGGFn(torch.autograd.Function):
                      os.environ.get('ASR_VGG_C1_XS', '1') != '0')
             z_bf = (cd == BF16 and Co % 4 == 0 and (c1_xs or not (cC == 1)) and use_gemm[l] and
                     os.environ.get('ASR_VGG_Z_BF16', '1') != '0')
-            z = torch.empty(npad, Co, dtype=torch.bfloat16 if z_bf else torch.float32,
-                            device=dev)
-            if not use_gemm[l]:
+            pt, pf, ceil = sp['pt'], sp['pf'], sp['ceil']
+            # unpooled stencil layer followed by batch norm: the stencil writes P and
+            # the BN moment partials itself (asr_vgg_c1_forward_relu_p), no z
+            c1p = (c1_xs and z_bf and not pt and sp['gamma'] is not None and Co % 8 == 0 and
+                   (not training or sp['run_mean'] is not None) and
+                   os.environ.get('ASR_VGG_P_BF16', '1') != '0' and
+                   os.environ.get('ASR_VGG_ROWS', '1') != '0' and
+                   os.environ.get('ASR_VGG_C1_RELU_P', '1') != '0')
+            z = (None if c1p else
+                 torch.empty(npad, Co, dtype=torch.bfloat16 if z_bf else torch.float32, device=dev))
+            if c1p:
+                P = torch.empty(B * cT * cF, Co, dtype=torch.bfloat16, device=dev)
+                nblk = N.query('asr_vgg_c1_relu_p_blocks', B, cT)
+                mqp = torch.empty(2, nblk, Co, **f32) if training else None
+                N.call('asr_vgg_c1_forward_relu_p', N.ptr(xs), int(cd == BF16), B, cT, cF, Co,
+                       N.ptr(w), N.ptr(sp['b']), N.ptr(P),
+                       N.ptr(sp['run_mean']) if training else None,
+                       N.ptr(mqp[0]) if training else None, N.ptr(mqp[1]) if training else None,
+                       N.stream_handle(dev))
+            elif not use_gemm[l]:
                 N.call('asr_conv_direct_forward', N.ptr(x_op), B, cT, cF, cC, Co, N.ptr(w),
                        N.ptr(sp['b']), N.ptr(z), N.stream_handle(dev))
             elif cC == 1 and Co % 4 == 0 and os.environ.get('ASR_VGG_C1_DIRECT', '1') != '0':
@@ -1971,13 +1988,13 @@ class VGGFn(torch.autograd.Function):
                                      operand(wg, 0, rowmap(9 * cCp)), z, rowmap(Co), npad, Co,
                                      9 * cCp, bias=sp['b'])
                     run_gemm([p], dev)
-            pt, pf, ceil = sp['pt'], sp['pf'], sp['ceil']
             To, Fo = _pool_dims(cT, cF, pt, pf, ceil) if pt else (cT, cF)
             # P = max(0, max z) of a bf16 z is itself a bf16 value: stored bf16 it
             # is exact and halves P's write and four reads
             p_bf = z_bf and os.environ.get('ASR_VGG_P_BF16', '1') != '0'
-            P = torch.empty(B * To * Fo, Co, dtype=torch.bfloat16 if p_bf else torch.float32,
-                            device=dev)
+            if not c1p:
+                P = torch.empty(B * To * Fo, Co, dtype=torch.bfloat16 if p_bf else torch.float32,
+                                device=dev)
             slot = torch.empty(B * To * Fo * Co, dtype=torch.uint8, device=dev) if pt else None
             bn = sp['gamma'] is not None
             mean = torch.empty(Co, **f32) if bn else None
@@ -1999,11 +2016,22 @@ class VGGFn(torch.autograd.Function):
                 out_dt, flat = (cd if use_gemm[l + 1] else F32), 0
             nb = N.query('asr_vgg_block_workspace_bytes', B, To, Fo, Co)
             ws = _ws(nb, dev)
-            N.call('asr_vgg_block_forward_zp', N.ptr(z), BF16 if z_bf else F32, B, cT, cF, Co, pt,
-                   pf, ceil, N.ptr(P), BF16 if p_bf else F32, N.ptr(slot), N.ptr(sp['gamma']), N.ptr(sp['beta']),
-                   N.ptr(sp['run_mean']), N.ptr(sp['run_var']), int(bool(training)),
-                   float(sp['momentum']), float(sp['eps']), N.ptr(mean), N.ptr(rstd), drop, seed,
-                   N.ptr(out), out_dt, flat, N.ptr(ws), nb, N.stream_handle(dev))
+            if c1p:
+                N.call('asr_vgg_block_forward_given_p', N.ptr(P), B, cT, cF, Co,
+                       N.ptr(sp['gamma']), N.ptr(sp['beta']), N.ptr(sp['run_mean']),
+                       N.ptr(sp['run_var']), int(bool(training)), float(sp['momentum']),
+                       float(sp['eps']), N.ptr(mean), N.ptr(rstd), drop, seed, N.ptr(out),
+                       out_dt, flat, N.ptr(mqp[0]) if training else None,
+                       N.ptr(mqp[1]) if training else None, nblk if training else 0, N.ptr(ws),
+                       nb, N.stream_handle(dev))
+                z = P     # the backward masks from P (asr_vgg_block_backward_zdp: z == P)
+            else:
+                N.call('asr_vgg_block_forward_zp', N.ptr(z), BF16 if z_bf else F32, B, cT, cF,
+                       Co, pt, pf, ceil, N.ptr(P), BF16 if p_bf else F32, N.ptr(slot),
+                       N.ptr(sp['gamma']), N.ptr(sp['beta']), N.ptr(sp['run_mean']),
+                       N.ptr(sp['run_var']), int(bool(training)), float(sp['momentum']),
+                       float(sp['eps']), N.ptr(mean), N.ptr(rstd), drop, seed, N.ptr(out),
+                       out_dt, flat, N.ptr(ws), nb, N.stream_handle(dev))
             saved += [x_op, z, P, slot, mean, rstd]
             layers.append((cT, cF, cC, cCp, Co, pt, pf, ceil, drop, seed, use_gemm[l]))
             x_op, cT, cF, cC, cCp = out, To, Fo, Co, Co

@@ -128,3 +128,40 @@ def test_row_passes_match_grid_stride(B, T, F, C, pt, flat, cuda_dev, monkeypatc
         assert _rel(d1, d0) <= 2e-3, (dnb, _rel(d1, d0))
         assert float((d1 - d0).abs().max()) <= 8e-3 * float(d0.abs().max()), dnb
         assert float(d0.abs().sum()) > 0
+
+
+@pytest.mark.gpu
+def test_first_layer_relu_p_matches_separate_pass(cuda_dev, monkeypatch):
+    """The first VGG layer's stencil writing P = max(0, bf16 z) and the batch-norm
+    moment partials itself (asr_vgg_c1_forward_relu_p, no z) against the stencil
+    + ReLU pass (ASR_VGG_C1_RELU_P=0), production channel plan, bf16: eval-mode
+    losses (running statistics: elementwise arithmetic only) bitwise equal; in
+    training the moments are summed in another fixed order, so the loss agrees
+    to f32 rounding moved through bf16 roundings and the gradients to the
+    bf16-flip level of the batch-norm backward."""
+    from test_parity_pins_gpu import VGG_PROD, _ctc, _vgg_batch, _with_env
+    from pytorch_end2end_speech_recognition_amd import native_ops
+    kw = dict(VGG_PROD, input_size=40)
+    model = _ctc(kw)
+    model.set_cuda()
+    batch = _vgg_batch(40, seed=21)
+    xs, ys, x_lens, y_lens = batch
+    native_ops.set_compute_dtype('bf16')
+    try:
+        ev = {}
+        for v in ('1', '0'):
+            monkeypatch.setenv('ASR_VGG_C1_RELU_P', v)
+            model.eval()
+            with torch.no_grad():
+                ev[v] = float(model(xs, ys, x_lens, y_lens, is_eval=True))
+        model.train()
+    finally:
+        monkeypatch.delenv('ASR_VGG_C1_RELU_P', raising=False)
+        native_ops.set_compute_dtype('fp32')
+    assert ev['1'] == ev['0'], ev
+    l1, g1 = _with_env(monkeypatch, 'ASR_VGG_C1_RELU_P', '1', model, batch, 'bf16')
+    l0, g0 = _with_env(monkeypatch, 'ASR_VGG_C1_RELU_P', '0', model, batch, 'bf16')
+    np.testing.assert_allclose(l1, l0, rtol=5e-5)
+    for k in g0:
+        d = float(np.linalg.norm(g1[k] - g0[k]) / max(np.linalg.norm(g0[k]), 1e-30))
+        assert d <= 5e-2, (k, d)

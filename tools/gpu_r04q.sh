@@ -1,0 +1,22 @@
+#!/bin/bash
+# round 4: GEMM loop (unroll, dense K staging) + VGG walkers vs ablib/head
+set -o pipefail
+mkdir -p gpurun_out
+R=$(pwd)
+timeout -k 10 400 python -u -m pytest -x -q --timeout 240 --timeout-method thread -m gpu \
+  tests/test_vgg_rows_gpu.py tests/test_gemm_gpu.py tests/test_parity_pins_gpu.py tests/test_recurrence_full.py tests/test_encoder_gpu.py tests/test_model_ctc.py > gpurun_out/r04q_tests.log 2>&1
+rc=$?; echo "tests rc=$rc"; tail -2 gpurun_out/r04q_tests.log
+[ $rc = 0 ] || exit 1
+for v in head cur; do
+  if [ $v = head ]; then L=$R/ablib/head/libasr_hip.so; else L=$R/pytorch_end2end_speech_recognition_amd/libasr_hip.so; fi
+  echo "== $v"; ASR_LIB_PATH=$L timeout -k 10 200 python -u tools/gemm_bench.py 2>&1 | grep -v amdgpu.ids | grep TF || exit 1
+done
+for i in 1 2; do
+  for c in vgg_hier ctc5x512; do
+    for v in head cur; do
+      if [ $v = head ]; then L=$R/ablib/head/libasr_hip.so; else L=$R/pytorch_end2end_speech_recognition_amd/libasr_hip.so; fi
+      ASR_LIB_PATH=$L timeout -k 10 200 python -u bench.py --config $c --steps 12 --warmup 3 --no-cpu-baseline --h2d-steps 0 > gpurun_out/q_${c}_${v}_$i.json 2> gpurun_out/q_${c}_${v}_$i.err || { tail gpurun_out/q_${c}_${v}_$i.err; exit 1; }
+      python3 -c "import json;d=json.load(open('gpurun_out/q_${c}_${v}_$i.json'));r=d['roofline'];o=r['other_kernels'];print('$c $v', d['ms_per_step'], r['kernel'], r['mean_launch_us'], {k:v.get('mean_launch_us') for k,v in o.items() if 'lstm' in k})"
+    done
+  done
+done

@@ -24,6 +24,8 @@ FAMILIES = [
     ('gemm', ('gemm_bf16_fast', 'gemm_kernel', 'gemm_bf16_big', 'gemm_bf16_8r', 'gemm_bf16_n64',
               'conv3x3_tr')),
     ('ctc_lattice', ('ctc_lattice',)),
+    ('ctc_emit', ('ctc_emit',)),
+    ('vgg_rows', ('rw_apply', 'rw_post_fwd', 'rw_bn_moments', 'rw_post_bwd')),
     ('ctc_grad', ('ctc_grad',)),
     ('optim_step', ('optim_step_kernel',)),
 ]
