@@ -165,3 +165,32 @@ def test_fused_ctc_head_matches_separate_ops(V, K, cuda_dev, monkeypatch):
     assert torch.equal(f[3], u[3]), float((f[3] - u[3]).abs().max())
     rel = float((f[4] - u[4]).norm() / u[4].norm())
     assert rel < 1e-2, rel
+
+
+@pytest.mark.parametrize('K,Ls', [(1, [0, 5, 31]), (2, [32, 40, 63]), (4, [64, 95, 127, 70]),
+                                  (8, [128, 200, 255]), (16, [256, 400, 511])])
+def test_multiwave_lattice_bitwise(K, Ls, cuda_dev, monkeypatch):
+    """ctc_lattice_mw (states spread over min(K, 4) skewed lattice waves) against
+    the single-wave ctc_lattice (ASR_CTC_LATTICE_MW=0): costs and gradients
+    bitwise equal, and both against the float64 oracle.  Label lengths put the
+    last states on either side of a wave boundary (S = 2L + 1 = 65, 129, 191,
+    ...); an empty label, a one-frame utterance and repeated labels included."""
+    rng = np.random.RandomState(100 + K)
+    V = 40
+    B = len(Ls) + 1
+    label_lens = np.array(list(Ls) + [0])             # the one-frame utterance: empty label
+    T = int(max(2 * max(Ls) + 8, 48))
+    act_lens = np.array([T] + [int(rng.randint(2 * l + 2, T + 1)) for l in label_lens[1:-1]] + [1])
+    labels = np.concatenate([rng.randint(1, V, l) for l in label_lens]).astype(np.int32)
+    if len(labels) > 4:
+        labels[1] = labels[2]                         # a repeat (no skip transition)
+    acts = (rng.randn(B, T, V) * 2).astype(np.float32)
+    out = {}
+    for mw in ('1', '0'):
+        monkeypatch.setenv('ASR_CTC_LATTICE_MW', mw)
+        out[mw] = _run(acts, labels, label_lens, act_lens, cuda_dev)
+    np.testing.assert_array_equal(out['1'][1], out['0'][1])
+    np.testing.assert_array_equal(out['1'][2], out['0'][2])
+    c_ref, g_ref = ctc_ref.ctc_batch(acts, labels, label_lens, act_lens, time_major=False)
+    np.testing.assert_allclose(out['1'][1], c_ref, rtol=1e-4)
+    np.testing.assert_allclose(out['1'][2], g_ref, rtol=2e-3, atol=2e-4)

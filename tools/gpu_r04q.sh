@@ -4,13 +4,15 @@ set -o pipefail
 mkdir -p gpurun_out
 R=$(pwd)
 timeout -k 10 400 python -u -m pytest -x -q --timeout 240 --timeout-method thread -m gpu \
-  tests/test_vgg_rows_gpu.py tests/test_gemm_gpu.py tests/test_parity_pins_gpu.py tests/test_recurrence_full.py tests/test_encoder_gpu.py tests/test_model_ctc.py > gpurun_out/r04q_tests.log 2>&1
+  tests/test_ctc_gpu.py tests/test_vgg_rows_gpu.py tests/test_gemm_gpu.py tests/test_parity_pins_gpu.py tests/test_recurrence_full.py tests/test_encoder_gpu.py tests/test_model_ctc.py > gpurun_out/r04q_tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; tail -2 gpurun_out/r04q_tests.log
 [ $rc = 0 ] || exit 1
 for v in head cur; do
   if [ $v = head ]; then L=$R/ablib/head/libasr_hip.so; else L=$R/pytorch_end2end_speech_recognition_amd/libasr_hip.so; fi
   echo "== $v"; ASR_LIB_PATH=$L timeout -k 10 200 python -u tools/gemm_bench.py 2>&1 | grep -v amdgpu.ids | grep TF || exit 1
 done
+for m in 0 1; do echo "== lattice_mw=$m"; ASR_CTC_LATTICE_MW=$m timeout -k 10 120 python -u tools/ctc_bench.py 2>&1 | grep -v amdgpu.ids || exit 1; done
+timeout -k 10 120 python -u tools/blas_probe.py 2>&1 | grep TF || exit 1
 for i in 1 2; do
   for c in vgg_hier ctc5x512; do
     for v in head cur; do
