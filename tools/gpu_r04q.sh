@@ -3,10 +3,11 @@
 set -o pipefail
 mkdir -p gpurun_out
 R=$(pwd)
-timeout -k 10 400 python -u -m pytest -x -q --timeout 240 --timeout-method thread -m gpu \
-  tests/test_ctc_gpu.py tests/test_vgg_rows_gpu.py tests/test_gemm_gpu.py tests/test_parity_pins_gpu.py tests/test_recurrence_full.py tests/test_encoder_gpu.py tests/test_model_ctc.py > gpurun_out/r04q_tests.log 2>&1
-rc=$?; echo "tests rc=$rc"; tail -2 gpurun_out/r04q_tests.log
+timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 240 --timeout-method thread > gpurun_out/r04q_tests.log 2>&1
+rc=$?; echo "tests rc=$rc"; grep -E "passed|failed|FAILED|Error" gpurun_out/r04q_tests.log | tail -5
 [ $rc = 0 ] || exit 1
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/r04q_smoke.log 2>&1 || { tail -5 gpurun_out/r04q_smoke.log; exit 1; }
+tail -2 gpurun_out/r04q_smoke.log
 for v in head cur; do
   if [ $v = head ]; then L=$R/ablib/head/libasr_hip.so; else L=$R/pytorch_end2end_speech_recognition_amd/libasr_hip.so; fi
   echo "== $v"; ASR_LIB_PATH=$L timeout -k 10 200 python -u tools/gemm_bench.py 2>&1 | grep -v amdgpu.ids | grep TF || exit 1
