@@ -53,7 +53,7 @@ def ctc_single(acts, labels, blank=0):
     for t in range(1, T):
         a = alpha[t - 1]
         a1 = np.concatenate([[NEG], a[:-1]])
-        a2 = np.concatenate([[NEG, NEG], a[:-2]])
+        a2 = np.concatenate([[NEG, NEG], a[:-2]])[:S]     # [:S]: S = 1 (empty label)
         a2 = np.where(skip, a2, NEG)
         alpha[t] = _lse(a, a1, a2) + emit[t]
 
@@ -66,7 +66,7 @@ def ctc_single(acts, labels, blank=0):
     for t in range(T - 2, -1, -1):
         b = beta[t + 1]
         b1 = np.concatenate([b[1:], [NEG]])
-        b2 = np.concatenate([b[2:], [NEG, NEG]])
+        b2 = np.concatenate([b[2:], [NEG, NEG]])[:S]
         b2 = np.where(skip_fwd, b2, NEG)
         beta[t] = _lse(b, b1, b2) + emit[t]
 

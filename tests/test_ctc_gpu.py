@@ -184,7 +184,7 @@ def test_multiwave_lattice_bitwise(K, Ls, cuda_dev, monkeypatch):
     labels = np.concatenate([rng.randint(1, V, l) for l in label_lens]).astype(np.int32)
     if len(labels) > 4:
         labels[1] = labels[2]                         # a repeat (no skip transition)
-    acts = (rng.randn(B, T, V) * 2).astype(np.float32)
+    acts = (rng.randn(B, T, V) * (2 if K <= 4 else 1)).astype(np.float32)
     out = {}
     for mw in ('1', '0'):
         monkeypatch.setenv('ASR_CTC_LATTICE_MW', mw)
@@ -193,4 +193,7 @@ def test_multiwave_lattice_bitwise(K, Ls, cuda_dev, monkeypatch):
     np.testing.assert_array_equal(out['1'][2], out['0'][2])
     c_ref, g_ref = ctc_ref.ctc_batch(acts, labels, label_lens, act_lens, time_major=False)
     np.testing.assert_allclose(out['1'][1], c_ref, rtol=1e-4)
-    np.testing.assert_allclose(out['1'][2], g_ref, rtol=2e-3, atol=2e-4)
+    # costs of 1e3-3e3 nats at K >= 8: alpha + beta - log P near 5e3, whose f32
+    # spacing bounds the occupancies at ~1e-3 absolute (the single-wave lattice
+    # has the same bits)
+    np.testing.assert_allclose(out['1'][2], g_ref, rtol=2e-3, atol=2e-4 if K <= 4 else 2e-3)

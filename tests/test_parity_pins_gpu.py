@@ -261,7 +261,12 @@ def _gpu_vgg_decisions(node):
     B = node.B
     for l, (cT, cF, cC, cCp, Co, pt, pf, ceil, drop, seed, gemm) in enumerate(node.layers):
         z, slot = saved[6 * l + 1], saved[6 * l + 3]
-        zi = z.float().view(B, cT + 2, cF + 2, Co)[:, 1:-1, 1:-1, :]
+        if z.numel() == B * cT * cF * Co:
+            # an unpooled layer whose stencil stored only P = max(0, bf16 z) (flat
+            # rows, asr_vgg_c1_forward_relu_p): P > 0 is the same mask
+            zi = z.float().view(B, cT, cF, Co)
+        else:
+            zi = z.float().view(B, cT + 2, cF + 2, Co)[:, 1:-1, 1:-1, :]
         mask = (zi > 0).permute(0, 3, 2, 1).cpu()                       # [B, C, F, T]
         ind = None
         if pt:
