@@ -284,7 +284,10 @@ def lib():
             h = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
         except OSError as e:
             raise NativeError('failed to load %s: %s' % (LIB_PATH, e))
+        ab = bool(os.environ.get('ASR_LIB_PATH'))
         for name, (res, args) in SIGNATURES.items():
+            if ab and not hasattr(h, name):
+                continue   # an older A/B build without this entry point
             fn = getattr(h, name)
             fn.restype = res
             fn.argtypes = args
