@@ -89,6 +89,14 @@ __global__ void ctc_prep(const int32_t* __restrict__ label_lens, const int32_t* 
   }
 }
 
+// A work-group barrier that orders LDS only, for the lattices' per-chunk
+// barriers: __syncthreads also drains vmcnt, i.e. waits for the lattice rows'
+// global stores and the loader's prefetch loads issued just before it -- one
+// memory round trip per chunk on the sequential chain.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // The lattice runs in base 2 (emissions scaled by log2 e in ctc_emit; alpha,
 // beta and log P in log2 units; the cost converted back with ln 2), so every
 // transcendental is a bare v_exp_f32 / v_log_f32.
@@ -350,7 +358,7 @@ __global__ void __launch_bounds__(128) ctc_lattice(int T, const int32_t* __restr
             load_k<K>(r[j], E + (size_t)row_of((c + 2) * C + j) * Spad);
         }
       }
-      __syncthreads();
+      lds_barrier();
     }
     return;
   }
@@ -382,12 +390,16 @@ __global__ void __launch_bounds__(128) ctc_lattice(int T, const int32_t* __restr
     }
     __syncthreads();
     for (int c = 0; c < nch; ++c) {
+      // the chunk's emissions into registers first: one LDS wait per chunk
+      // instead of one on every step's dependency chain
+      float ec[C][K];
+#pragma unroll
+      for (int j = 0; j < C; ++j) load_k<K>(ec[j], &ring[c & 1][j][lane * K]);
 #pragma unroll
       for (int j = 0; j < C; ++j) {
         const int n = c * C + j;
         if (n < N) {
-          float e[K];
-          load_k<K>(e, &ring[c & 1][j][lane * K]);
+          const float (&e)[K] = ec[j];
           float p1 = from_lower_lane(a[K - 1]);
           float p2 = (K >= 2) ? from_lower_lane(a[K >= 2 ? K - 2 : 0]) : from_lower_lane(p1);
           if (lane == 0) { p1 = NEG; p2 = NEG; }
@@ -408,7 +420,7 @@ __global__ void __launch_bounds__(128) ctc_lattice(int T, const int32_t* __restr
           store_k<K>(A + (size_t)(1 + n) * Spad, a);
         }
       }
-      __syncthreads();
+      lds_barrier();
     }
 
     // log P from the last two states at t = Tb-1
@@ -450,12 +462,14 @@ __global__ void __launch_bounds__(128) ctc_lattice(int T, const int32_t* __restr
   }
   __syncthreads();
   for (int c = 0; c < nch; ++c) {
+    float ec[C][K];
+#pragma unroll
+    for (int j = 0; j < C; ++j) load_k<K>(ec[j], &ring[c & 1][j][lane * K]);
 #pragma unroll
     for (int j = 0; j < C; ++j) {
       const int n = c * C + j;
       if (n < N) {
-        float e[K];
-        load_k<K>(e, &ring[c & 1][j][lane * K]);
+        const float (&e)[K] = ec[j];
         float n1 = from_upper_lane(be[0]);
         float n2 = (K >= 2) ? from_upper_lane(be[K >= 2 ? 1 : 0]) : from_upper_lane(n1);
         if (lane == 63) { n1 = NEG; n2 = NEG; }
@@ -475,7 +489,7 @@ __global__ void __launch_bounds__(128) ctc_lattice(int T, const int32_t* __restr
         store_k<K>(Bt + (size_t)(Tb - 2 - n) * Spad, be);
       }
     }
-    __syncthreads();
+    lds_barrier();
   }
 }
 
@@ -563,7 +577,7 @@ __global__ void __launch_bounds__(64 * ((K < 4 ? K : 4) + 1))
         }
       }
       slot = slot + 1 == NSLOT ? 0 : slot + 1;
-      __syncthreads();
+      lds_barrier();
     }
     __syncthreads();   // the log P exchange (alpha) / end (beta)
     return;
@@ -610,13 +624,21 @@ __global__ void __launch_bounds__(64 * ((K < 4 ? K : 4) + 1))
       const int cw = c - wave;
       if (cw >= 0 && cw < nch) {
         const int sl = cw % NSLOT;
+        // the chunk's emissions and boundary states into registers first: one
+        // LDS wait per chunk instead of one on every step's dependency chain
+        float ec[C][KW];
+        float2 bc[C];
+#pragma unroll
+        for (int j = 0; j < C; ++j) {
+          load_k<KW>(ec[j], &ring[sl][j][64 * KW * wave + lane * KW]);
+          bc[j] = wave > 0 ? bnd[wave - 1][(cw * C + j) & (BR - 1)] : make_float2(NEG, NEG);
+        }
 #pragma unroll
         for (int j = 0; j < C; ++j) {
           const int n = cw * C + j;
           if (n < N) {
-            float e[KW];
-            load_k<KW>(e, &ring[sl][j][64 * KW * wave + lane * KW]);
-            const float2 bp = wave > 0 ? bnd[wave - 1][n & (BR - 1)] : make_float2(NEG, NEG);
+            const float (&e)[KW] = ec[j];
+            const float2 bp = bc[j];
             float p1 = from_lower_lane(a[KW - 1]);
             if (lane == 0) p1 = bp.x;
             float p2;
@@ -643,7 +665,7 @@ __global__ void __launch_bounds__(64 * ((K < 4 ? K : 4) + 1))
           }
         }
       }
-      __syncthreads();
+      lds_barrier();
     }
     // log P = lse2 of the last two states at t = Tb - 1
 #pragma unroll
@@ -698,13 +720,19 @@ __global__ void __launch_bounds__(64 * ((K < 4 ? K : 4) + 1))
     const int cw = c - (NW - 1 - wave);
     if (cw >= 0 && cw < nch) {
       const int sl = cw % NSLOT;
+      float ec[C][KW];
+      float2 bc[C];
+#pragma unroll
+      for (int j = 0; j < C; ++j) {
+        load_k<KW>(ec[j], &ring[sl][j][64 * KW * wave + lane * KW]);
+        bc[j] = wave + 1 < NW ? bnd[wave + 1][(cw * C + j) & (BR - 1)] : make_float2(NEG, NEG);
+      }
 #pragma unroll
       for (int j = 0; j < C; ++j) {
         const int n = cw * C + j;
         if (n < N) {
-          float e[KW];
-          load_k<KW>(e, &ring[sl][j][64 * KW * wave + lane * KW]);
-          const float2 bq = wave + 1 < NW ? bnd[wave + 1][n & (BR - 1)] : make_float2(NEG, NEG);
+          const float (&e)[KW] = ec[j];
+          const float2 bq = bc[j];
           float n1 = from_upper_lane(be[0]);
           if (lane == 63) n1 = bq.x;
           float n2;
@@ -731,7 +759,7 @@ __global__ void __launch_bounds__(64 * ((K < 4 ? K : 4) + 1))
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
   }
   __syncthreads();   // as many barriers as the alpha waves and the loader
 }

@@ -561,14 +561,12 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
   // (its MFMA accumulator) are one 16-B store -- four per lane instead of
   // sixteen 4-B stores between the MFMAs and barrier B(s); a 12-float column
   // pitch keeps the cells' reads (4 rows x 16 units per wave) conflict-free.
-  // (-DASR_XGX_PART_ROWS builds keep the row-major form, for A/B runs.)
-#ifndef ASR_XGX_PART_ROWS
+  // Measured (same-box A/B): 303 -> 289 us per launch at H = 320 (KSW = 3),
+  // 1442 -> 1450 at H = 512 (KSW = 4), so H = 512 keeps the row-major form.
+  constexpr bool PCM = KSW < 4;
   constexpr int PCOL = R + 4;
-  static_assert(R == 8, "column pitch chosen for 8 rows");
-  __shared__ __attribute__((aligned(16))) float part[2][NSW][4 * XU * PCOL];
-#else
-  __shared__ float part[2][NSW][PSZ];
-#endif
+  static_assert(!PCM || R == 8, "column pitch chosen for 8 rows");
+  __shared__ __attribute__((aligned(16))) float part[2][NSW][PCM ? 4 * XU * PCOL : PSZ];
   __shared__ float xpart[2][NPW][PSZ];
   // input rows of steps s+1 .. s+3: [3 slots][R rows][XGX_DMAX] bf16, filled by
   // buffer -> LDS DMA three steps ahead (16-B chunks XOR-swizzled by row when
@@ -669,12 +667,12 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
       if (4 * kq < R) {
 #pragma unroll
         for (int g = 0; g < 4; ++g)
-#ifndef ASR_XGX_PART_ROWS
-          *reinterpret_cast<f32x4*>(&part[s & 1][wave][(g * XU + ln) * PCOL + 4 * kq]) = acc[g];
-#else
+          if constexpr (PCM) {
+            *reinterpret_cast<f32x4*>(&part[s & 1][wave][(g * XU + ln) * PCOL + 4 * kq]) = acc[g];
+          } else {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) part[s & 1][wave][prow(4 * kq + r) + g * XU + ln] = acc[g][r];
-#endif
+            for (int r = 0; r < 4; ++r) part[s & 1][wave][prow(4 * kq + r) + g * XU + ln] = acc[g][r];
+          }
       }
       XG_TR(s, 4, __builtin_amdgcn_s_memrealtime());
       __syncthreads();  // B(s)
@@ -847,11 +845,7 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int col = q * XU + unit;
-#ifndef ASR_XGX_PART_ROWS
-        const int pi = col * PCOL + row;
-#else
-        const int pi = prow(row) + col;
-#endif
+        const int pi = PCM ? col * PCOL + row : prow(row) + col;
         float a = part[s & 1][0][pi];
 #pragma unroll
         for (int w = 1; w < NSW; ++w) a += part[s & 1][w][pi];
