@@ -553,31 +553,36 @@ __global__ void __launch_bounds__(64 * ((K < 4 ? K : 4) + 1))
 
   if (wave == NW) {
     // ---------------- loader (whole rows, lane l: elements l K .. l K + K - 1) ----------------
+    // Two chunks in flight in registers (ra, rb alternate): a round of the
+    // multi-wave lattice (~1 us) is shorter than the emission rows' load
+    // latency, so the chunk stored in round c was loaded in round c - 2.
     const float* El = E + lane * K;
-    float r[C][K];
+    float ra[C][K], rb[C][K];
+    auto load_chunk = [&](float (&r)[C][K], int ck) {
+#pragma unroll
+      for (int j = 0; j < C; ++j) load_k<K>(r[j], El + (size_t)row_of(ck * C + j) * Spad);
+    };
     if (nch > 0) {
+      load_chunk(ra, 0);
 #pragma unroll
-      for (int j = 0; j < C; ++j) load_k<K>(r[j], El + (size_t)row_of(j) * Spad);
-#pragma unroll
-      for (int j = 0; j < C; ++j) store_k<K>(&ring[0][j][lane * K], r[j]);
-      if (nch > 1) {
-#pragma unroll
-        for (int j = 0; j < C; ++j) load_k<K>(r[j], El + (size_t)row_of(C + j) * Spad);
-      }
+      for (int j = 0; j < C; ++j) store_k<K>(&ring[0][j][lane * K], ra[j]);
+      if (nch > 1) load_chunk(ra, 1);
+      if (nch > 2) load_chunk(rb, 2);
     }
     __syncthreads();
     int slot = 1;   // (c + 1) % NSLOT
-    for (int c = 0; c < rounds; ++c) {
+    auto round = [&](int c, float (&r)[C][K]) {
       if (c + 1 < nch) {
 #pragma unroll
         for (int j = 0; j < C; ++j) store_k<K>(&ring[slot][j][lane * K], r[j]);
-        if (c + 2 < nch) {
-#pragma unroll
-          for (int j = 0; j < C; ++j) load_k<K>(r[j], El + (size_t)row_of((c + 2) * C + j) * Spad);
-        }
+        if (c + 3 < nch) load_chunk(r, c + 3);
       }
       slot = slot + 1 == NSLOT ? 0 : slot + 1;
       lds_barrier();
+    };
+    for (int c = 0; c < rounds; c += 2) {
+      round(c, ra);
+      if (c + 1 < rounds) round(c + 1, rb);
     }
     __syncthreads();   // the log P exchange (alpha) / end (beta)
     return;
