@@ -17,9 +17,6 @@
 //               A loader wave streams the emission rows into an LDS ring so
 //               the lattice wave never waits on a global load.  The sequential
 //               depth is T steps, not the 2T of an alpha-then-beta pass.
-//               ctc_lattice_mw (default) spreads the states over up to four
-//               lattice waves, skewed by one chunk so they exchange neighbour
-//               states through LDS without per-step synchronisation.
 //   ctc_grad    one row per block: occupancy exp(alpha+beta-e-logP) of the
 //               row's S states, summed per class through LDS (repeated
 //               labels), grad = (softmax - occupancy) * scale written once.
@@ -493,282 +490,6 @@ __global__ void __launch_bounds__(128) ctc_lattice(int T, const int32_t* __restr
   }
 }
 
-// The same lattice on NW = min(K, 4) lattice waves, each owning KW = K / NW
-// consecutive states per lane (wave w: states 64 KW w .. 64 KW (w + 1) - 1),
-// so each wave issues 1/NW of the per-step transcendentals (one wave holding
-// all 4 states of a lane was issue-bound at ~0.18 us per step at T = 1000).
-// The waves run skewed by one chunk of C steps: in round c wave w advances
-// chunk c - w (alpha; beta: c - (NW - 1 - w)), so the two neighbour states it
-// needs from the wave below (above) at each step were written to LDS in an
-// earlier round, on the far side of a round barrier -- no per-step
-// synchronisation between waves.  The loader wave keeps NW + 1 chunks of
-// emission rows in the LDS ring (the NW chunks being read, the one being
-// written).  Per state the arithmetic is ctc_lattice's -- a blank state with
-// KW odd goes through lse3 with a -inf third term, which is bitwise lse2 --
-// and log P combines the last two states as lse2, which is what the single
-// wave's lane-then-wave reduction computes; so alpha, beta, log P and the
-// costs are bitwise those of ctc_lattice.
-template <int K>
-__global__ void __launch_bounds__(64 * ((K < 4 ? K : 4) + 1))
-    ctc_lattice_mw(int T, const int32_t* __restrict__ labels,
-                   const int32_t* __restrict__ label_lens, const int32_t* __restrict__ act_lens,
-                   const int32_t* __restrict__ offs, int blank, int zero_infinity,
-                   const float* __restrict__ emit, float* __restrict__ alpha,
-                   float* __restrict__ beta, float* __restrict__ logp_out,
-                   float* __restrict__ costs) {
-  constexpr int NW = K < 4 ? K : 4;
-  constexpr int KW = K / NW;
-  constexpr int Spad = 64 * K;
-  constexpr int C = K <= 4 ? 16 : (K == 8 ? 8 : 4);  // rows per chunk
-  constexpr int NSLOT = NW + 1;                      // ring: (NW + 1) C Spad floats <= 80 KB
-  constexpr int BR = 4 * C;                          // boundary rows kept (> 2 C + 1)
-  __shared__ __attribute__((aligned(16))) float ring[NSLOT][C][Spad];
-  __shared__ float2 bnd[NW][BR];
-  __shared__ float fin[2];
-  const int b = blockIdx.x;
-  const bool is_beta = blockIdx.y == 1;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int Tb = min(act_lens[b], T);
-  const int L = min(label_lens[b], (Spad - 1) / 2);
-  const int S = 2 * L + 1;
-  const int32_t* lab = labels + offs[b];
-  const float NEG = neg_inf();
-
-  if (Tb <= 0) {
-    if (threadIdx.x == 0 && !is_beta) {
-      bool feas = (L == 0);
-      logp_out[b] = feas ? 0.f : NEG;
-      costs[b] = feas ? 0.f : (zero_infinity ? 0.f : __builtin_huge_valf());
-    }
-    return;
-  }
-  const int N = Tb - 1;
-  const int nch = (N + C - 1) / C;
-  const int rounds = nch + NW - 1;
-  auto row_of = [&](int n) {
-    n = min(n, N - 1);
-    return is_beta ? Tb - 2 - n : 1 + n;
-  };
-  const float* E = emit + (size_t)b * T * Spad;
-
-  if (wave == NW) {
-    // ---------------- loader (whole rows, lane l: elements l K .. l K + K - 1) ----------------
-    // Two chunks in flight in registers (ra, rb alternate): a round of the
-    // multi-wave lattice (~1 us) is shorter than the emission rows' load
-    // latency, so the chunk stored in round c was loaded in round c - 2.
-    const float* El = E + lane * K;
-    float ra[C][K], rb[C][K];
-    auto load_chunk = [&](float (&r)[C][K], int ck) {
-#pragma unroll
-      for (int j = 0; j < C; ++j) load_k<K>(r[j], El + (size_t)row_of(ck * C + j) * Spad);
-    };
-    if (nch > 0) {
-      load_chunk(ra, 0);
-#pragma unroll
-      for (int j = 0; j < C; ++j) store_k<K>(&ring[0][j][lane * K], ra[j]);
-      if (nch > 1) load_chunk(ra, 1);
-      if (nch > 2) load_chunk(rb, 2);
-    }
-    __syncthreads();
-    int slot = 1;   // (c + 1) % NSLOT
-    auto round = [&](int c, float (&r)[C][K]) {
-      if (c + 1 < nch) {
-#pragma unroll
-        for (int j = 0; j < C; ++j) store_k<K>(&ring[slot][j][lane * K], r[j]);
-        if (c + 3 < nch) load_chunk(r, c + 3);
-      }
-      slot = slot + 1 == NSLOT ? 0 : slot + 1;
-      lds_barrier();
-    };
-    for (int c = 0; c < rounds; c += 2) {
-      round(c, ra);
-      if (c + 1 < rounds) round(c + 1, rb);
-    }
-    __syncthreads();   // the log P exchange (alpha) / end (beta)
-    return;
-  }
-
-  const int s0 = 64 * KW * wave + lane * KW;   // this lane's first state
-  bool valid[KW];
-#pragma unroll
-  for (int k = 0; k < KW; ++k) valid[k] = s0 + k < S;
-
-  if (!is_beta) {
-    // ---------------- alpha ----------------
-    bool skip[KW];
-#pragma unroll
-    for (int k = 0; k < KW; ++k) {
-      const int s = s0 + k;
-      skip[k] = (s & 1) && s >= 3 && s < S && lab[s >> 1] != lab[(s >> 1) - 1];
-    }
-    float* A = alpha + (size_t)b * T * Spad + s0;
-    float a[KW];
-    {
-      float e0[KW];
-      load_k<KW>(e0, E + s0);
-#pragma unroll
-      for (int k = 0; k < KW; ++k) a[k] = (s0 + k < 2 && valid[k]) ? e0[k] : NEG;
-      store_k<KW>(A, a);
-    }
-    // boundary row v (alpha row v of visit order) for the wave above: its lane 0
-    // needs this wave's states 64 KW (w + 1) - 1 and - 2
-    auto put_bnd = [&](int v) {
-      if (wave + 1 < NW) {
-        if constexpr (KW >= 2) {
-          if (lane == 63) bnd[wave][v & (BR - 1)] = make_float2(a[KW - 1], a[KW - 2]);
-        } else {
-          if (lane == 63) bnd[wave][v & (BR - 1)].x = a[0];
-          if (lane == 62) bnd[wave][v & (BR - 1)].y = a[0];
-        }
-      }
-    };
-    put_bnd(0);
-    if (threadIdx.x == 0) { fin[0] = NEG; fin[1] = NEG; }
-    __syncthreads();
-    for (int c = 0; c < rounds; ++c) {
-      const int cw = c - wave;
-      if (cw >= 0 && cw < nch) {
-        const int sl = cw % NSLOT;
-        // the chunk's emissions and boundary states into registers first: one
-        // LDS wait per chunk instead of one on every step's dependency chain
-        float ec[C][KW];
-        float2 bc[C];
-#pragma unroll
-        for (int j = 0; j < C; ++j) {
-          load_k<KW>(ec[j], &ring[sl][j][64 * KW * wave + lane * KW]);
-          bc[j] = wave > 0 ? bnd[wave - 1][(cw * C + j) & (BR - 1)] : make_float2(NEG, NEG);
-        }
-#pragma unroll
-        for (int j = 0; j < C; ++j) {
-          const int n = cw * C + j;
-          if (n < N) {
-            const float (&e)[KW] = ec[j];
-            const float2 bp = bc[j];
-            float p1 = from_lower_lane(a[KW - 1]);
-            if (lane == 0) p1 = bp.x;
-            float p2;
-            if constexpr (KW >= 2) {
-              p2 = from_lower_lane(a[KW >= 2 ? KW - 2 : 0]);
-            } else {
-              p2 = from_lower_lane(p1);
-            }
-            if (lane == 0) p2 = bp.y;
-            float nx[KW];
-#pragma unroll
-            for (int k = 0; k < KW; ++k) {
-              const float a1 = (k >= 1) ? a[k >= 1 ? k - 1 : 0] : p1;
-              const float a2 = (k >= 2) ? a[k >= 2 ? k - 2 : 0] : ((k == 1) ? p1 : p2);
-              const float v = ((KW % 2 == 0) && (k % 2 == 0) ? lse2_b2(a[k], a1)
-                                                             : lse3_b2(a[k], a1, skip[k] ? a2 : NEG)) +
-                              e[k];
-              nx[k] = valid[k] ? v : NEG;
-            }
-#pragma unroll
-            for (int k = 0; k < KW; ++k) a[k] = nx[k];
-            store_k<KW>(A + (size_t)(1 + n) * Spad, a);
-            put_bnd(n + 1);
-          }
-        }
-      }
-      lds_barrier();
-    }
-    // log P = lse2 of the last two states at t = Tb - 1
-#pragma unroll
-    for (int k = 0; k < KW; ++k) {
-      const int s = s0 + k;
-      if (s == S - 2) fin[0] = a[k];
-      if (s == S - 1) fin[1] = a[k];
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const float logP = lse2_b2(fin[0], fin[1]);   // log2 units
-      logp_out[b] = logP;
-      costs[b] = (logP == NEG) ? (zero_infinity ? 0.f : __builtin_huge_valf()) : -logP * kLn2;
-    }
-    return;
-  }
-
-  // ---------------- beta ----------------
-  bool skipf[KW];
-#pragma unroll
-  for (int k = 0; k < KW; ++k) {
-    const int s = s0 + k;
-    skipf[k] = (s & 1) && s + 2 < S && lab[s >> 1] != lab[(s >> 1) + 1];
-  }
-  float* Bt = beta + (size_t)b * T * Spad + s0;
-  float be[KW];
-  {
-    float et[KW];
-    load_k<KW>(et, E + (size_t)(Tb - 1) * Spad + s0);
-#pragma unroll
-    for (int k = 0; k < KW; ++k) {
-      const int s = s0 + k;
-      be[k] = (valid[k] && (s == S - 1 || s == S - 2)) ? et[k] : NEG;
-    }
-    store_k<KW>(Bt + (size_t)(Tb - 1) * Spad, be);
-  }
-  // boundary row v for the wave below: its lane 63 needs this wave's states
-  // 64 KW w and 64 KW w + 1
-  auto put_bnd = [&](int v) {
-    if (wave > 0) {
-      if constexpr (KW >= 2) {
-        if (lane == 0) bnd[wave][v & (BR - 1)] = make_float2(be[0], be[1]);
-      } else {
-        if (lane == 0) bnd[wave][v & (BR - 1)].x = be[0];
-        if (lane == 1) bnd[wave][v & (BR - 1)].y = be[0];
-      }
-    }
-  };
-  put_bnd(0);
-  __syncthreads();
-  for (int c = 0; c < rounds; ++c) {
-    const int cw = c - (NW - 1 - wave);
-    if (cw >= 0 && cw < nch) {
-      const int sl = cw % NSLOT;
-      float ec[C][KW];
-      float2 bc[C];
-#pragma unroll
-      for (int j = 0; j < C; ++j) {
-        load_k<KW>(ec[j], &ring[sl][j][64 * KW * wave + lane * KW]);
-        bc[j] = wave + 1 < NW ? bnd[wave + 1][(cw * C + j) & (BR - 1)] : make_float2(NEG, NEG);
-      }
-#pragma unroll
-      for (int j = 0; j < C; ++j) {
-        const int n = cw * C + j;
-        if (n < N) {
-          const float (&e)[KW] = ec[j];
-          const float2 bq = bc[j];
-          float n1 = from_upper_lane(be[0]);
-          if (lane == 63) n1 = bq.x;
-          float n2;
-          if constexpr (KW >= 2) {
-            n2 = from_upper_lane(be[KW >= 2 ? 1 : 0]);
-          } else {
-            n2 = from_upper_lane(n1);
-          }
-          if (lane == 63) n2 = bq.y;
-          float nx[KW];
-#pragma unroll
-          for (int k = 0; k < KW; ++k) {
-            const float b1 = (k < KW - 1) ? be[k < KW - 1 ? k + 1 : 0] : n1;
-            const float b2 = (k < KW - 2) ? be[k < KW - 2 ? k + 2 : 0] : ((k == KW - 2) ? n1 : n2);
-            const float v = ((KW % 2 == 0) && (k % 2 == 0) ? lse2_b2(be[k], b1)
-                                                           : lse3_b2(be[k], b1, skipf[k] ? b2 : NEG)) +
-                            e[k];
-            nx[k] = valid[k] ? v : NEG;
-          }
-#pragma unroll
-          for (int k = 0; k < KW; ++k) be[k] = nx[k];
-          store_k<KW>(Bt + (size_t)(Tb - 2 - n) * Spad, be);
-          put_bnd(n + 1);
-        }
-      }
-    }
-    lds_barrier();
-  }
-  __syncthreads();   // as many barriers as the alpha waves and the loader
-}
-
 // grad = (softmax - occupancy) * scale, one row (b,t) per block.
 //   kTable (V <= 256): occupancies summed per class in a V-entry LDS table.
 //   otherwise, no V-sized table: (1) the S state occupancies go to LDS; (2) the
@@ -1109,18 +830,10 @@ extern "C" int asr_ctc_forward(const float* acts, long long stride_t, long long 
                        stride_b, T, B, V, labels_flat, label_lens, act_lens, ws.offs, blank, Spad,
                        ws.lse, ws.emit);
   ASR_LAUNCH_CHECK();
-  // ASR_CTC_LATTICE_MW=0: the single-wave lattice (A/B runs; bitwise the same)
-  const char* mwe = getenv("ASR_CTC_LATTICE_MW");
-  const bool mw = !(mwe && mwe[0] == '0');
-#define ASR_CTC_LAT(KK)                                                                          \
-  if (mw)                                                                                        \
-    hipLaunchKernelGGL(ctc_lattice_mw<KK>, dim3(B, 2), dim3(64 * ((KK < 4 ? KK : 4) + 1)), 0, s, \
-                       T, labels_flat, label_lens, act_lens, ws.offs, blank, zero_infinity,      \
-                       ws.emit, ws.alpha, ws.beta, ws.logp, costs);                              \
-  else                                                                                           \
-    hipLaunchKernelGGL(ctc_lattice<KK>, dim3(B, 2), dim3(128), 0, s, T, labels_flat, label_lens, \
-                       act_lens, ws.offs, blank, zero_infinity, ws.emit, ws.alpha, ws.beta,      \
-                       ws.logp, costs)
+#define ASR_CTC_LAT(KK)                                                                        \
+  hipLaunchKernelGGL(ctc_lattice<KK>, dim3(B, 2), dim3(128), 0, s, T, labels_flat, label_lens,  \
+                     act_lens, ws.offs, blank, zero_infinity, ws.emit, ws.alpha, ws.beta,      \
+                     ws.logp, costs)
   switch (K) {
     case 1: ASR_CTC_LAT(1); break;
     case 2: ASR_CTC_LAT(2); break;
