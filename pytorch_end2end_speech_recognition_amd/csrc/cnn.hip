@@ -1024,7 +1024,11 @@ struct RowWalk {
     settle(r1, Tr, ng);
   }
 };
-constexpr int RW_U = 4;   // walkers per lane
+// walkers per lane: 1.  Four (2 for the pooled forward and the backward)
+// measured slower at vgg_hier (kernel trace, same build otherwise: rw_apply
+// 116 -> 145 us, rw_bn_moments 116 -> 137, rw_post_bwd<0> 158 -> 185) and no
+// faster elsewhere, so the walker arrays stay at one element.
+constexpr int RW_U = 1;
 
 // lanes with the same channel group (tid % cg8) hold partial sums of the same
 // 8 channels: out[c] = their sum in lane order (c < C)
@@ -1113,7 +1117,7 @@ __global__ void __launch_bounds__(RW_NT) rw_post_fwd(const uint16_t* __restrict_
   }
   const int rows = B * pl.To, ng = pl.Fo * cg8;
   const int r0 = blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
-  constexpr int U = PL ? 2 : RW_U;   // walkers per lane (a pooled walker loads four pixels)
+  constexpr int U = RW_U;   // walkers per lane
   RowWalk it[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) it[u] = RowWalk(r0, r1, pl.To, ng, u * RW_NT);
@@ -1268,7 +1272,7 @@ __global__ void __launch_bounds__(RW_NT) rw_post_bwd(const TD* __restrict__ dnex
   }
   const int rows = B * T, ng = F * cg8;
   const int r0 = blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
-  constexpr int U = 2;   // walkers per lane (three loads each)
+  constexpr int U = RW_U;   // walkers per lane
   RowWalk it[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) it[u] = RowWalk(r0, r1, T, ng, u * RW_NT);
