@@ -1084,9 +1084,7 @@ __global__ void __launch_bounds__(RW_NT) rw_apply(const uint16_t* __restrict__ P
         for (int j = 0; j < 8; ++j) y[u].v[j] = (y[u].v[j] - m[j]) * r[j] * g[j] + bt[j];
       }
       if (af.drop > 0.f) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          y[u].v[j] *= drop_scale(af.drop, af.seed, (unsigned long long)(pe[u] + j));
+        drop_n_aligned<8>(y[u].v, af.drop, af.seed, (unsigned long long)pe[u]);
       }
       y[u].store(out + row_base(it[u].b, it[u].t, To, Fo, C, flat) + (long long)it[u].g * 8);
       it[u].next(r1, To, ng, RW_U * RW_NT);
@@ -1228,9 +1226,7 @@ __global__ void __launch_bounds__(RW_NT) rw_bn_moments(const TD* __restrict__ dn
     for (int u = 0; u < RW_U; ++u) {   // in walker order: the sums' order is fixed
       if (it[u].r >= r1) continue;
       if (af.drop > 0.f) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          gv[u].v[j] *= drop_scale(af.drop, af.seed, (unsigned long long)(pe[u] + j));
+        drop_n_aligned<8>(gv[u].v, af.drop, af.seed, (unsigned long long)pe[u]);
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -1305,9 +1301,7 @@ __global__ void __launch_bounds__(RW_NT) rw_post_bwd(const TD* __restrict__ dnex
       for (int j = 0; j < 8; ++j) v.v[j] = 0.f;
       if (in[u]) {
         if (af.drop > 0.f) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j)
-            g[u].v[j] *= drop_scale(af.drop, af.seed, (unsigned long long)(pbi[u] + j));
+          drop_n_aligned<8>(g[u].v, af.drop, af.seed, (unsigned long long)pbi[u]);
         }
         const unsigned long long me =
             PL ? (unsigned long long)((f - fo * 2) * 2 + (t - to * 2)) : 0ull;

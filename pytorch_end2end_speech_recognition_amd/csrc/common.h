@@ -89,20 +89,77 @@ __device__ __forceinline__ float wave_max(float v) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
-// Dropout RNG shared by every kernel that applies or regenerates a mask:
-// 64-bit counter hash -> uniform [0,1) (splitmix64 finaliser).  Element i of a
-// tensor dropped with `seed` is kept iff u01(seed, i) >= p.
-__device__ __forceinline__ float u01(unsigned long long seed, unsigned long long i) {
-  unsigned long long z = seed + 0x9E3779B97F4A7C15ull * (i + 1);
+// Dropout RNG shared by every kernel that applies or regenerates a mask.
+// Element i of a tensor dropped with `seed` is kept iff u01(seed, i) >= p,
+// where u01 is 16-bit field i % 4 of the splitmix64 finaliser of
+// seed + golden * (i / 4 + 1): four consecutive elements share one 64-bit
+// hash (resolution 2^-16: p = 0.2 drops with probability 0.200012).  The
+// element-wise passes take whole 4-element groups through u01x4 / drop8 --
+// one hash per 4 elements instead of one per element, which had made the
+// dropout-applying VGG passes VALU-bound (~30 VALU instructions per hash).
+__device__ __forceinline__ unsigned long long drop_hash(unsigned long long seed,
+                                                        unsigned long long q) {
+  unsigned long long z = seed + 0x9E3779B97F4A7C15ull * (q + 1);
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= z >> 31;
-  return (float)(z >> 40) * (1.0f / 16777216.0f);
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ float u16_u01(unsigned v) {
+  return (float)(v & 0xffffu) * (1.0f / 65536.0f);
+}
+__device__ __forceinline__ float u01(unsigned long long seed, unsigned long long i) {
+  return u16_u01((unsigned)(drop_hash(seed, i >> 2) >> (16u * (unsigned)(i & 3))));
+}
+// u[e] = u01(seed, i + e), e < 4, for i % 4 == 0 (one hash)
+__device__ __forceinline__ void u01x4(unsigned long long seed, unsigned long long i, float (&u)[4]) {
+  const unsigned long long z = drop_hash(seed, i >> 2);
+  u[0] = u16_u01((unsigned)z);
+  u[1] = u16_u01((unsigned)(z >> 16));
+  u[2] = u16_u01((unsigned)(z >> 32));
+  u[3] = u16_u01((unsigned)(z >> 48));
 }
 
 __device__ __forceinline__ float drop_scale(float p, unsigned long long seed,
                                             unsigned long long i) {
   return u01(seed, i) >= p ? 1.f / (1.f - p) : 0.f;
+}
+
+// v[e] *= drop_scale(p, seed, i + e), e < N, for i % 4 == 0 (callers whose
+// offsets are multiples of 4 by construction: no fallback path, whose
+// registers cost the memory-bound passes occupancy)
+template <int N>
+__device__ __forceinline__ void drop_n_aligned(float* v, float p, unsigned long long seed,
+                                               unsigned long long i) {
+  static_assert(N % 4 == 0, "groups of 4");
+  const float sc = 1.f / (1.f - p);
+#pragma unroll
+  for (int g = 0; g < N; g += 4) {
+    float u[4];
+    u01x4(seed, i + g, u);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[g + e] *= u[e] >= p ? sc : 0.f;
+  }
+}
+
+// v[e] *= drop_scale(p, seed, i + e) for N (a multiple of 4) consecutive
+// elements: one hash per 4 when i % 4 == 0 (the same values either way)
+template <int N>
+__device__ __forceinline__ void drop_n(float* v, float p, unsigned long long seed,
+                                       unsigned long long i) {
+  static_assert(N % 4 == 0, "groups of 4");
+  const float sc = 1.f / (1.f - p);
+  if ((i & 3) == 0) {
+#pragma unroll
+    for (int g = 0; g < N; g += 4) {
+      float u[4];
+      u01x4(seed, i + g, u);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[g + e] *= u[e] >= p ? sc : 0.f;
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < N; ++e) v[e] *= drop_scale(p, seed, i + e);
+  }
 }
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }

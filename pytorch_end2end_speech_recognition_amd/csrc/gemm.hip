@@ -1270,10 +1270,7 @@ __device__ __forceinline__ void epi8(const Problem& pr, const RowMap& cm, bool r
           const float4 c = *reinterpret_cast<const float4*>(cp);
           o[0] += pr.beta * c.x; o[1] += pr.beta * c.y; o[2] += pr.beta * c.z; o[3] += pr.beta * c.w;
         }
-        if (!raw && pr.drop_p > 0.f) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] *= drop_scale(pr, off + n + e);
-        }
+        if (!raw && pr.drop_p > 0.f) drop_n<4>(o, pr.drop_p, pr.drop_seed, (unsigned long long)(off + n));
         *reinterpret_cast<float4*>(cp) = make_float4(o[0], o[1], o[2], o[3]);
       } else {
 #pragma unroll
@@ -1717,12 +1714,7 @@ __global__ void splitk_reduce4(const float* __restrict__ slab, int ksplit, int M
     const float4 o = *reinterpret_cast<const float4*>(crow);
     v[0] += beta * o.x; v[1] += beta * o.y; v[2] += beta * o.z; v[3] += beta * o.w;
   }
-  if (drop_p > 0.f) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      v[q] *= u01(drop_seed, (unsigned long long)(off + n + q)) >= drop_p ? 1.f / (1.f - drop_p)
-                                                                         : 0.f;
-  }
+  if (drop_p > 0.f) drop_n<4>(v, drop_p, drop_seed, (unsigned long long)(off + n));
   *reinterpret_cast<float4*>(crow) = make_float4(v[0], v[1], v[2], v[3]);
 }
 

@@ -131,7 +131,9 @@ def test_persistent_forward_gradients_match(shape, cuda_dev):
     print(shape, 'bwd only', {k: '%.2e' % v for k, v in errs.items()})
     # (bf16 rounding flips of dgates in r = dgates Wcat and of the GEMM operands
     # downstream: 1.5e-4 .. 5.6e-4 measured at the production shape; the ragged
-    # shape, whose steps carry no flips, agrees to ~3e-7 -- every code path
-    # but the 10-channel instantiation's constants is exercised there)
+    # shape carries at most a flip or two: ~3e-7 with the round-3 dropout
+    # masks, 1.6e-5 on d_w_dec with the round-4 masks (one hash per four
+    # elements) -- every code path but the 10-channel instantiation's constants
+    # is exercised there)
     for name in names:
-        assert errs[name] < (2e-3 if shape != 'ragged' else 1e-5), (name, errs[name])
+        assert errs[name] < (2e-3 if shape != 'ragged' else 1e-4), (name, errs[name])
