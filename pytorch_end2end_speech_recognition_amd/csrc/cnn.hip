@@ -1097,7 +1097,7 @@ __global__ void __launch_bounds__(RW_NT) rw_apply(const uint16_t* __restrict__ P
 // nullable).  The same window scan as post_fwd (freq outer, time inner, first
 // maximum wins).
 template <int PL>
-__global__ void __launch_bounds__(RW_NT) rw_post_fwd(const uint16_t* __restrict__ z, int B, int T,
+__global__ void __launch_bounds__(RW_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) rw_post_fwd(const uint16_t* __restrict__ z, int B, int T,
                                                      int F, int C, Pool pl,
                                                      uint16_t* __restrict__ P,
                                                      uint8_t* __restrict__ slot,
@@ -1130,13 +1130,18 @@ __global__ void __launch_bounds__(RW_NT) rw_post_fwd(const uint16_t* __restrict_
       if constexpr (PL == 0) {
         best[u].load(z + row_base(b, to, T, F, C, 0) + (long long)it[u].g * 8);
       } else {
-        Bf8 x[4];
+        // the window's four pixels kept packed (16 B each) until compared:
+        // unpacked on load they held 32 VGPRs and the pass ran at 5 waves / SIMD
+        uint4 x[4];
 #pragma unroll
         for (int df = 0; df < 2; ++df)
 #pragma unroll
           for (int dt = 0; dt < 2; ++dt) {
             const int f = fo * 2 + df, t = to * 2 + dt;
-            if (f < F && t < T) x[df * 2 + dt].load(z + row_base(b, t, T, F, C, 0) + (long long)f * C + c);
+            x[df * 2 + dt] = uint4{0u, 0u, 0u, 0u};
+            if (f < F && t < T)
+              x[df * 2 + dt] = *reinterpret_cast<const uint4*>(z + row_base(b, t, T, F, C, 0) +
+                                                               (long long)f * C + c);
           }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -1149,9 +1154,12 @@ __global__ void __launch_bounds__(RW_NT) rw_post_fwd(const uint16_t* __restrict_
           for (int dt = 0; dt < 2; ++dt) {
             const int f = fo * 2 + df, t = to * 2 + dt;
             if (f < F && t < T) {
+              const uint4 w4 = x[df * 2 + dt];
+              const unsigned w[4] = {w4.x, w4.y, w4.z, w4.w};
 #pragma unroll
               for (int j = 0; j < 8; ++j) {
-                const float v = fmaxf(x[df * 2 + dt].v[j], 0.f);
+                const uint16_t hb = (uint16_t)((j & 1) ? (w[j >> 1] >> 16) : (w[j >> 1] & 0xffffu));
+                const float v = fmaxf(bf2f(hb), 0.f);
                 if (v > best[u].v[j]) { best[u].v[j] = v; bs[u][j] = (unsigned)(df * 2 + dt); }
               }
             }
@@ -1245,7 +1253,7 @@ __global__ void __launch_bounds__(RW_NT) rw_bn_moments(const TD* __restrict__ dn
 // unpooled value P > 0 (the ReLU mask); bf16 dz at every interior pixel, the
 // conv-bias partials of the f32 values per block (bias_part nullable).
 template <int PL, typename TD>
-__global__ void __launch_bounds__(RW_NT) rw_post_bwd(const TD* __restrict__ dnext,
+__global__ void __launch_bounds__(RW_NT) __attribute__((amdgpu_waves_per_eu(8, 8))) rw_post_bwd(const TD* __restrict__ dnext,
                                                      const uint16_t* __restrict__ P,
                                                      const uint8_t* __restrict__ slot, int B, int T,
                                                      int F, int C, Pool pl, int flat, Affine af,
@@ -1253,19 +1261,28 @@ __global__ void __launch_bounds__(RW_NT) rw_post_bwd(const TD* __restrict__ dnex
                                                      uint16_t* __restrict__ dz,
                                                      float* __restrict__ bias_part, int rpb) {
   __shared__ float red[RW_NT * 8];
+  // the per-channel batch-norm parameters [5][C] (mean, rstd, gamma, the two
+  // BN-backward sums) in LDS, read per group: held in registers they took the
+  // kernel to 90 VGPRs, 5 waves per SIMD, for a pass bound by loads in flight
+  extern __shared__ __attribute__((aligned(16))) float prm[];
   const int tid = threadIdx.x, cg8 = C >> 3, sh3 = __builtin_ctz(cg8);
   const int c = (tid & (cg8 - 1)) * 8;
   const float inv_n = 1.f / (float)((unsigned)B * pl.To * pl.Fo);
-  float m[8], r[8], gm[8], a1[8], a2[8], bacc[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    m[j] = af.mean[c + j];
-    r[j] = af.rstd[c + j];
-    gm[j] = af.gamma[c + j];
-    a1[j] = sums[c + j];
-    a2[j] = sums[C + c + j];
-    bacc[j] = 0.f;
+  for (int i = tid; i < C; i += RW_NT) {
+    prm[i] = af.mean[i];
+    prm[C + i] = af.rstd[i];
+    prm[2 * C + i] = af.gamma[i];
+    prm[3 * C + i] = sums[i];
+    prm[4 * C + i] = sums[C + i];
   }
+  float bacc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bacc[j] = 0.f;
+  __syncthreads();
+  auto ld4 = [&](int k, int h, float (&o)[4]) {
+    const float4 a = *reinterpret_cast<const float4*>(&prm[k * C + c + h]);
+    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w;
+  };
   const int rows = B * T, ng = F * cg8;
   const int r0 = blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
   constexpr int U = RW_U;   // walkers per lane
@@ -1306,12 +1323,18 @@ __global__ void __launch_bounds__(RW_NT) rw_post_bwd(const TD* __restrict__ dnex
         const unsigned long long me =
             PL ? (unsigned long long)((f - fo * 2) * 2 + (t - to * 2)) : 0ull;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float xh = (x[u].v[j] - m[j]) * r[j];
-          const float gj = gm[j] * r[j] * (g[u].v[j] - a1[j] * inv_n - xh * a2[j] * inv_n);
-          const bool hit = PL == 0 || ((sl[u] >> (8 * j)) & 0xffull) == me;
-          v.v[j] = (hit && x[u].v[j] > 0.f) ? gj : 0.f;
-          bacc[j] += v.v[j];
+        for (int h = 0; h < 8; h += 4) {   // four channels' parameters live at a time
+          float m[4], r[4], gm[4], a1[4], a2[4];
+          ld4(0, h, m); ld4(1, h, r); ld4(2, h, gm); ld4(3, h, a1); ld4(4, h, a2);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int j = h + e;
+            const float xh = (x[u].v[j] - m[e]) * r[e];
+            const float gj = gm[e] * r[e] * (g[u].v[j] - a1[e] * inv_n - xh * a2[e] * inv_n);
+            const bool hit = PL == 0 || ((sl[u] >> (8 * j)) & 0xffull) == me;
+            v.v[j] = (hit && x[u].v[j] > 0.f) ? gj : 0.f;
+            bacc[j] += v.v[j];
+          }
         }
       }
       v.store(dz + row_base(it[u].b, t, T, F, C, 0) + (long long)it[u].g * 8);
@@ -2071,20 +2094,20 @@ static int vgg_block_backward_impl(const void* dnext_v, int dnext_dtype, int fla
     bgrid = (nrow + rpb - 1) / rpb;
     if (db16) {
       if (pt)
-        hipLaunchKernelGGL((rw_post_bwd<2, uint16_t>), dim3(bgrid), dim3(RW_NT), 0, s, dnh,
+        hipLaunchKernelGGL((rw_post_bwd<2, uint16_t>), dim3(bgrid), dim3(RW_NT), 5 * C * sizeof(float), s, dnh,
                            (const uint16_t*)P, slot, B, T, F, C, pl, flat, af, sums, (uint16_t*)dz,
                            bpart, rpb);
       else
-        hipLaunchKernelGGL((rw_post_bwd<0, uint16_t>), dim3(bgrid), dim3(RW_NT), 0, s, dnh,
+        hipLaunchKernelGGL((rw_post_bwd<0, uint16_t>), dim3(bgrid), dim3(RW_NT), 5 * C * sizeof(float), s, dnh,
                            (const uint16_t*)P, slot, B, T, F, C, pl, flat, af, sums, (uint16_t*)dz,
                            bpart, rpb);
     } else {
       if (pt)
-        hipLaunchKernelGGL((rw_post_bwd<2, float>), dim3(bgrid), dim3(RW_NT), 0, s, dnext,
+        hipLaunchKernelGGL((rw_post_bwd<2, float>), dim3(bgrid), dim3(RW_NT), 5 * C * sizeof(float), s, dnext,
                            (const uint16_t*)P, slot, B, T, F, C, pl, flat, af, sums, (uint16_t*)dz,
                            bpart, rpb);
       else
-        hipLaunchKernelGGL((rw_post_bwd<0, float>), dim3(bgrid), dim3(RW_NT), 0, s, dnext,
+        hipLaunchKernelGGL((rw_post_bwd<0, float>), dim3(bgrid), dim3(RW_NT), 5 * C * sizeof(float), s, dnext,
                            (const uint16_t*)P, slot, B, T, F, C, pl, flat, af, sums, (uint16_t*)dz,
                            bpart, rpb);
     }
