@@ -1381,7 +1381,7 @@ def _dx_pipeline_ok(ctx, B, T, Din, dev):
     free: dX may then be computed beside it.  Opt-in (ASR_DX_PIPE=1): at 5x512
     the free half of the chip runs these GEMMs and the weight gradients too
     slowly to stay ahead of the recurrence."""
-    if not getattr(ctx, 'handoff_in', False) or os.environ.get('ASR_DX_PIPE', '0') != '1':
+    if not getattr(ctx, 'handoff_in', False) or os.environ.get('ASR_DX_PIPE', '0') not in ('1', '2'):
         return False
     if Din % 2 or not _act_h_on() or compute_dtype() != BF16 or (T + 1) // 2 > 4096 * DX_CHUNK:
         return False
@@ -1392,13 +1392,17 @@ def _dx_pipeline_ok(ctx, B, T, Din, dev):
 
 
 def _dx_pipelined(dx, dg_op, w_op, B, T, H, Din, Dp, drop, dev):
-    """dX [B, T, Din] = dG W_ih on a high-priority side stream, in chunks of
-    time steps from both ends of the sequence inwards -- the order in which the
-    layer below's backward recurrence reads them (steps q: rows t = q and
-    T - 1 - q) -- each chunk signalled by a flag (asr_lstm_dy_signal) the
-    recurrence polls before reading its dy rows.  The GEMMs first wait for that
-    recurrence to be resident (asr_lstm_wgrad_gate), so they take the CUs it
-    leaves free.  dx carries (flags, c0, epoch, done-event) as _asr_dy_pipe."""
+    """dX [B, T, Din] = dG W_ih in chunks of time steps from both ends of the
+    sequence inwards -- the order in which the layer below's backward
+    recurrence reads them (steps q: rows t = q and T - 1 - q) -- each chunk
+    signalled by a flag (asr_lstm_dy_signal) the recurrence polls before
+    reading its dy rows.  ASR_DX_PIPE=1: every chunk (ASR_DX_CHUNK steps) on a
+    high-priority side stream that first waits for that recurrence to be
+    resident (asr_lstm_wgrad_gate), so the GEMMs take the CUs it leaves free.
+    ASR_DX_PIPE=2: two chunks of about T / 4 steps -- the outer rows on the
+    main stream with the whole chip before the recurrence is launched, the
+    middle rows beside it, where the recurrence reaches them ~T/4 steps later.
+    dx carries (flags, c0, epoch, done-event) as _asr_dy_pipe."""
     st = _dx_state.get(dev.index)
     if st is None:
         st = {'flags': torch.zeros(4096, dtype=torch.int32, device=dev),
@@ -1407,28 +1411,41 @@ def _dx_pipelined(dx, dg_op, w_op, B, T, H, Din, Dp, drop, dev):
     st['epoch'] = st['epoch'] % 0x7ffffff0 + 1
     epoch, flags, side = st['epoch'], st['flags'], st['stream']
     main = torch.cuda.current_stream(dev)
-    side.wait_stream(main)
     half = (T + 1) // 2
+    head_main = os.environ.get('ASR_DX_PIPE', '0') == '2'
+    c0 = DX_CHUNK
+    if head_main and 'ASR_DX_CHUNK' not in os.environ:
+        c0 = (half + 1) // 2
+
+    def chunk(k):
+        s0, s1 = k * c0, (k + 1) * c0
+        probs = []
+        for t0, t1 in ((s0, min(s1, half)), (max(T - s1, half), T - s0)):
+            if t1 <= t0:
+                continue
+            n = t1 - t0
+            a = operand(dg_op, 0, rowmap(8 * H, stride_b=T * 8 * H, rows_per_b=n, t_add=t0))
+            c_map = rowmap(Din, stride_b=T * Din, rows_per_b=n, t_add=t0)
+            probs.append(gemm_problem(a, operand(w_op, 1, rowmap(Dp)), dx, c_map, B * n,
+                                      Din, 8 * H, drop=drop))
+        run_gemm(probs, dev)
+        N.call('asr_lstm_dy_signal', N.ptr(flags), k, epoch, N.stream_handle(dev))
+
+    nch = (half + c0 - 1) // c0
+    k0 = 0
+    if head_main:   # the first chunk with the whole chip, before the recurrence
+        chunk(0)
+        k0 = 1
+    side.wait_stream(main)
     small = os.environ.get('ASR_DX_SMALL', '1') != '0'   # 128 x 128 tiles: more work-groups
     with torch.cuda.stream(side):
-        N.call('asr_lstm_wgrad_gate', N.stream_handle(dev))
+        if k0 < nch:
+            N.call('asr_lstm_wgrad_gate', N.stream_handle(dev))
         if small:
             N.call('asr_gemm_set_small_tiles', 1)
         try:
-            for k in range((half + DX_CHUNK - 1) // DX_CHUNK):
-                s0, s1 = k * DX_CHUNK, (k + 1) * DX_CHUNK
-                probs = []
-                for t0, t1 in ((s0, min(s1, half)), (max(T - s1, half), T - s0)):
-                    if t1 <= t0:
-                        continue
-                    n = t1 - t0
-                    a = operand(dg_op, 0, rowmap(8 * H, stride_b=T * 8 * H, rows_per_b=n,
-                                                 t_add=t0))
-                    c_map = rowmap(Din, stride_b=T * Din, rows_per_b=n, t_add=t0)
-                    probs.append(gemm_problem(a, operand(w_op, 1, rowmap(Dp)), dx, c_map, B * n,
-                                              Din, 8 * H, drop=drop))
-                run_gemm(probs, dev)
-                N.call('asr_lstm_dy_signal', N.ptr(flags), k, epoch, N.stream_handle(dev))
+            for k in range(k0, nch):
+                chunk(k)
         finally:
             if small:
                 N.call('asr_gemm_set_small_tiles', 0)
@@ -1436,7 +1453,7 @@ def _dx_pipelined(dx, dg_op, w_op, B, T, H, Din, Dp, drop, dev):
         done.record(side)
     for t in (dx, dg_op, w_op, flags):
         t.record_stream(side)
-    dx._asr_dy_pipe = (flags, DX_CHUNK, epoch, done)
+    dx._asr_dy_pipe = (flags, c0, epoch, done)
     return done
 
 

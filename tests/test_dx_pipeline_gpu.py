@@ -72,12 +72,15 @@ def _run(case, dev, drop, monkeypatch, pipe):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('mode', ['1', '2'])
 @pytest.mark.parametrize('B,T,H,D0,drop', [(32, 1000, 512, 80, None), (32, 1000, 512, 80, 0.2),
                                            (20, 101, 256, 40, 0.3), (9, 37, 64, 16, None)])
-def test_pipelined_dx_matches_serial(B, T, H, D0, drop, cuda_dev, monkeypatch):
+def test_pipelined_dx_matches_serial(B, T, H, D0, drop, mode, cuda_dev, monkeypatch):
+    """mode 1: every chunk beside the recurrence; mode 2: the outer quarter
+    of the rows on the compute stream before it, the middle beside it."""
     case = _stack_case(B, T, H, D0)
     d = (drop, 12345) if drop else None
-    got, n_pipe = _run(case, cuda_dev, d, monkeypatch, '1')
+    got, n_pipe = _run(case, cuda_dev, d, monkeypatch, mode)
     ref, n_ser = _run(case, cuda_dev, d, monkeypatch, '0')
     assert n_pipe == 1 and n_ser == 0, (n_pipe, n_ser)
     names = ['y', 'dx'] + ['%s%d' % (n, l) for l in range(2)
@@ -90,12 +93,13 @@ def test_pipelined_dx_matches_serial(B, T, H, D0, drop, cuda_dev, monkeypatch):
 
 
 @pytest.mark.gpu
-def test_pipelined_stack_vs_float64(cuda_dev, monkeypatch):
+@pytest.mark.parametrize('mode', ['1', '2'])
+def test_pipelined_stack_vs_float64(mode, cuda_dev, monkeypatch):
     """The two-layer stack with the pipelined dX against float64 (no dropout):
     every gradient within the bf16 bound of tests/test_recurrence_full."""
     B, T, H, D0 = 16, 300, 256, 64
     lens, x, layers, dy = case = _stack_case(B, T, H, D0, seed=3)
-    got, n_pipe = _run(case, cuda_dev, None, monkeypatch, '1')
+    got, n_pipe = _run(case, cuda_dev, None, monkeypatch, mode)
     assert n_pipe == 1
     torch.set_num_threads(8)
     d = torch.float64
