@@ -2,24 +2,28 @@
 mask stream of the HIP kernels restated in numpy, so the oracle can replay the
 exact masks a GPU run drew.  Element i of a tensor dropped with `seed` is kept
 iff u01(seed, i) >= p; kept elements are scaled by 1 / (1 - p)
-(csrc/common.h u01 / drop_scale: 16-bit field i % 4 of the splitmix64
-finaliser of seed + golden * (i // 4 + 1))."""
+(csrc/common.h u01 / drop_scale: 16-bit field i % 2 of a 32-bit lowbias32
+hash of the seed's 32-bit key + (i // 2) * 0x9E3779B9)."""
 import numpy as np
 
 _M = np.uint64(0xFFFFFFFFFFFFFFFF)
 
 
 def u01(seed, n):
-    """u01(seed, i) for i < n: 16-bit field i % 4 of the finaliser of
-    seed + golden * (i // 4 + 1) (four elements per 64-bit hash)."""
-    with np.errstate(over='ignore'):
-        i = np.arange(n, dtype=np.uint64)
-        q = (i >> np.uint64(2)) + np.uint64(1)
-        z = np.uint64(seed) + np.uint64(0x9E3779B97F4A7C15) * q
-        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
-        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
-        z = z ^ (z >> np.uint64(31))
-        f = (z >> (np.uint64(16) * (i & np.uint64(3)))) & np.uint64(0xFFFF)
+    """u01(seed, i) for i < n: 16-bit field i % 2 of lowbias32(key + (i // 2)
+    * 0x9E3779B9) in 32-bit arithmetic, key = low 32 bits of seed xor high 32
+    bits * 0x85EBCA6B, divided by 65536 (two elements per hash)."""
+    M32 = np.uint64(0xFFFFFFFF)
+    seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    key = np.uint64(((seed & 0xFFFFFFFF) ^ (((seed >> 32) * 0x85EBCA6B) & 0xFFFFFFFF)))
+    i = np.arange(n, dtype=np.uint64)
+    x = (key + (i >> np.uint64(1)) * np.uint64(0x9E3779B9)) & M32
+    x ^= x >> np.uint64(16)
+    x = (x * np.uint64(0x7FEB352D)) & M32
+    x ^= x >> np.uint64(15)
+    x = (x * np.uint64(0x846CA68B)) & M32
+    x ^= x >> np.uint64(16)
+    f = (x >> (np.uint64(16) * (i & np.uint64(1)))) & np.uint64(0xFFFF)
     return f.astype(np.float32) * np.float32(1.0 / 65536.0)
 
 

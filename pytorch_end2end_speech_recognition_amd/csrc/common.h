@@ -91,32 +91,38 @@ __device__ __forceinline__ float wave_max(float v) {
 
 // Dropout RNG shared by every kernel that applies or regenerates a mask.
 // Element i of a tensor dropped with `seed` is kept iff u01(seed, i) >= p,
-// where u01 is 16-bit field i % 4 of the splitmix64 finaliser of
-// seed + golden * (i / 4 + 1): four consecutive elements share one 64-bit
-// hash (resolution 2^-16: p = 0.2 drops with probability 0.200012).  The
-// element-wise passes take whole 4-element groups through u01x4 / drop8 --
-// one hash per 4 elements instead of one per element, which had made the
-// dropout-applying VGG passes VALU-bound (~30 VALU instructions per hash).
-__device__ __forceinline__ unsigned long long drop_hash(unsigned long long seed,
-                                                        unsigned long long q) {
-  unsigned long long z = seed + 0x9E3779B97F4A7C15ull * (q + 1);
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
+// where u01 is 16-bit field i % 2 of lowbias32(key + (i / 2) * 0x9E3779B9)
+// (32-bit arithmetic, key = the seed folded to 32 bits), divided by 65536:
+// two elements per hash of 7 VALU instructions.  (Round 4 first used one
+// 64-bit splitmix64 finaliser per 4 elements, ~30 instructions; the
+// dropout-applying VGG passes were then ~50 % VALU-busy, 157 instructions per
+// 16-B group.)  Resolution 2^-16: p = 0.2 drops with probability 0.200012.
+__device__ __forceinline__ unsigned drop_key(unsigned long long seed) {
+  return (unsigned)seed ^ ((unsigned)(seed >> 32) * 0x85EBCA6Bu);
+}
+__device__ __forceinline__ unsigned drop_hash(unsigned key, unsigned q) {
+  unsigned x = key + q * 0x9E3779B9u;
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
 }
 __device__ __forceinline__ float u16_u01(unsigned v) {
   return (float)(v & 0xffffu) * (1.0f / 65536.0f);
 }
 __device__ __forceinline__ float u01(unsigned long long seed, unsigned long long i) {
-  return u16_u01((unsigned)(drop_hash(seed, i >> 2) >> (16u * (unsigned)(i & 3))));
+  return u16_u01(drop_hash(drop_key(seed), (unsigned)(i >> 1)) >> (16u * (unsigned)(i & 1)));
 }
-// u[e] = u01(seed, i + e), e < 4, for i % 4 == 0 (one hash)
+// u[e] = u01(seed, i + e), e < 4, for i % 2 == 0
 __device__ __forceinline__ void u01x4(unsigned long long seed, unsigned long long i, float (&u)[4]) {
-  const unsigned long long z = drop_hash(seed, i >> 2);
-  u[0] = u16_u01((unsigned)z);
-  u[1] = u16_u01((unsigned)(z >> 16));
-  u[2] = u16_u01((unsigned)(z >> 32));
-  u[3] = u16_u01((unsigned)(z >> 48));
+  const unsigned k = drop_key(seed), q = (unsigned)(i >> 1);
+  const unsigned z0 = drop_hash(k, q), z1 = drop_hash(k, q + 1);
+  u[0] = u16_u01(z0);
+  u[1] = u16_u01(z0 >> 16);
+  u[2] = u16_u01(z1);
+  u[3] = u16_u01(z1 >> 16);
 }
 
 __device__ __forceinline__ float drop_scale(float p, unsigned long long seed,
@@ -124,31 +130,33 @@ __device__ __forceinline__ float drop_scale(float p, unsigned long long seed,
   return u01(seed, i) >= p ? 1.f / (1.f - p) : 0.f;
 }
 
-// v[e] *= drop_scale(p, seed, i + e), e < N, for i % 4 == 0 (callers whose
-// offsets are multiples of 4 by construction: no fallback path, whose
-// registers cost the memory-bound passes occupancy)
+// v[e] *= drop_scale(p, seed, i + e), e < N, for i % 2 == 0 (callers whose
+// offsets are even by construction: no fallback path, whose registers cost
+// the memory-bound passes occupancy).  The 16-bit fields are compared as
+// integers with ceil(65536 p): u = f / 65536 exactly, so the same mask.
 template <int N>
 __device__ __forceinline__ void drop_n_aligned(float* v, float p, unsigned long long seed,
                                                unsigned long long i) {
-  static_assert(N % 4 == 0, "groups of 4");
+  static_assert(N % 2 == 0, "pairs");
   const float sc = 1.f / (1.f - p);
+  const unsigned thr = (unsigned)__builtin_ceilf(p * 65536.f);
+  const unsigned k = drop_key(seed), q = (unsigned)(i >> 1);
 #pragma unroll
-  for (int g = 0; g < N; g += 4) {
-    float u[4];
-    u01x4(seed, i + g, u);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[g + e] *= u[e] >= p ? sc : 0.f;
+  for (int g = 0; g < N; g += 2) {
+    const unsigned z = drop_hash(k, q + (unsigned)(g >> 1));
+    v[g] = (z & 0xffffu) >= thr ? v[g] * sc : 0.f;
+    v[g + 1] = (z >> 16) >= thr ? v[g + 1] * sc : 0.f;
   }
 }
 
 // v[e] *= drop_scale(p, seed, i + e) for N (a multiple of 4) consecutive
-// elements: one hash per 4 when i % 4 == 0 (the same values either way)
+// elements: one hash per 2 when i is even (the same values either way)
 template <int N>
 __device__ __forceinline__ void drop_n(float* v, float p, unsigned long long seed,
                                        unsigned long long i) {
   static_assert(N % 4 == 0, "groups of 4");
   const float sc = 1.f / (1.f - p);
-  if ((i & 3) == 0) {
+  if ((i & 1) == 0) {
 #pragma unroll
     for (int g = 0; g < N; g += 4) {
       float u[4];
