@@ -362,9 +362,9 @@ int asr_optim_step(int kind, float* params, const float* grads, float* m, float*
 /* ------------------------------------------------------- elementwise
  * asr_dropout: y = x * (u(seed, i) >= p) / (1 - p), u a counter hash (the
  *   mask is recomputed from (seed, i) in backward: call again on dy).  u(seed,
- *   i) is 16-bit field i % 4 of the splitmix64 finaliser of
- *   seed + 0x9E3779B97F4A7C15 * (i / 4 + 1), divided by 65536 (round 4: four
- *   elements per hash; oracle/rng.py restates it).
+ *   i) is 16-bit field i % 2 of lowbias32(key + (i / 2) * 0x9E3779B9), key =
+ *   (uint32)seed ^ (uint32)(seed >> 32) * 0x85EBCA6B, divided by 65536
+ *   (round 4: two elements per 32-bit hash; oracle/rng.py restates it).
  *   Replaces nn.Dropout on the encoder / decoder activations.
  * asr_embedding_*: nn.Embedding(padding_idx) lookup / gradient (linear.py:50-77;
  *   trans=1: weight stored [E][V], the one-hot @ W^T of Embedding_LS,
