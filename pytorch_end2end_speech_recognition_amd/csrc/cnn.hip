@@ -1344,6 +1344,84 @@ __global__ void __launch_bounds__(RW_NT) __attribute__((amdgpu_waves_per_eu(8, 8
   if (bias_part) rw_reduce(bacc, cg8, C, red, bias_part + (long long)blockIdx.x * C);
 }
 
+// The pooled layers' backward on the POOLED grid (every input pixel inside a
+// window: ceil mode or even extents): each group's ReLU / batch-norm backward
+// is computed once and scattered to its 2 x 2 window -- the argmax pixel gets
+// it, the other three 0 -- where rw_post_bwd<2> walks the input pixels and
+// recomputes it (and reloads dnext, P and the slots) for each of the four.
+// Same arithmetic per element; the conv-bias sums add the same values in
+// another fixed order.
+template <typename TD>
+__global__ void __launch_bounds__(RW_NT)
+    rw_post_bwd_pool(const TD* __restrict__ dnext, const uint16_t* __restrict__ P,
+                     const uint8_t* __restrict__ slot, int B, int T, int F, int C, Pool pl,
+                     int flat, Affine af, const float* __restrict__ sums,
+                     uint16_t* __restrict__ dz, float* __restrict__ bias_part, int rpb) {
+  __shared__ float red[RW_NT * 8];
+  extern __shared__ __attribute__((aligned(16))) float prm[];   // [5][C], as rw_post_bwd
+  const int tid = threadIdx.x, cg8 = C >> 3, sh3 = __builtin_ctz(cg8);
+  const int c = (tid & (cg8 - 1)) * 8;
+  const float inv_n = 1.f / (float)((unsigned)B * pl.To * pl.Fo);
+  for (int i = tid; i < C; i += RW_NT) {
+    prm[i] = af.mean[i];
+    prm[C + i] = af.rstd[i];
+    prm[2 * C + i] = af.gamma[i];
+    prm[3 * C + i] = sums[i];
+    prm[4 * C + i] = sums[C + i];
+  }
+  float bacc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bacc[j] = 0.f;
+  __syncthreads();
+  auto ld4 = [&](int k, int h, float (&o)[4]) {
+    const float4 a = *reinterpret_cast<const float4*>(&prm[k * C + c + h]);
+    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w;
+  };
+  const int rows = B * pl.To, ng = pl.Fo * cg8;
+  const int r0 = blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
+  for (RowWalk it(r0, r1, pl.To, ng); it.r < r1; it.next(r1, pl.To, ng)) {
+    const int b = it.b, to = it.t, fo = it.g >> sh3;
+    const long long ip = (long long)fo * C + c;
+    const long long pbi = ((long long)b * pl.To + to) * pl.Fo * C + ip;
+    Bf8 g, x;
+    g.load(dnext + row_base(b, to, pl.To, pl.Fo, C, flat) + ip);
+    x.load(P + pbi);
+    const unsigned long long sl = *reinterpret_cast<const unsigned long long*>(slot + pbi);
+    if (af.drop > 0.f) drop_n_aligned<8>(g.v, af.drop, af.seed, (unsigned long long)pbi);
+    float gj[8];
+#pragma unroll
+    for (int h = 0; h < 8; h += 4) {
+      float m[4], r[4], gm[4], a1[4], a2[4];
+      ld4(0, h, m); ld4(1, h, r); ld4(2, h, gm); ld4(3, h, a1); ld4(4, h, a2);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int j = h + e;
+        const float xh = (x.v[j] - m[e]) * r[e];
+        const float v = gm[e] * r[e] * (g.v[j] - a1[e] * inv_n - xh * a2[e] * inv_n);
+        gj[j] = x.v[j] > 0.f ? v : 0.f;
+      }
+    }
+    // one window pixel at a time (unrolled, the four pixels' values were all
+    // live at once: 102 VGPRs, 4 waves per SIMD)
+#pragma unroll 1
+    for (int w = 0; w < 4; ++w) {
+        const int df = w >> 1, dt = w & 1;
+        const int f = fo * 2 + df, t = to * 2 + dt;
+        if (f < F && t < T) {
+          const unsigned long long me = (unsigned long long)w;
+          Bf8 v;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            v.v[j] = ((sl >> (8 * j)) & 0xffull) == me ? gj[j] : 0.f;
+            bacc[j] += v.v[j];
+          }
+          v.store(dz + row_base(b, t, T, F, C, 0) + (long long)f * C + c);
+        }
+      }
+  }
+  if (bias_part) rw_reduce(bacc, cg8, C, red, bias_part + (long long)blockIdx.x * C);
+}
+
 // GEMM weight images of a torch Conv2d weight W [Co][Ci][3(f)][3(t)], tap
 // j = kw*3 + kh (the row shift (kw-1)(F+2) + (kh-1) of gemm.hip tap addressing):
 //   mode 0 (forward):  out[co][j*Ci + ci] = W[co][ci][kh][kw]
@@ -2089,10 +2167,27 @@ static int vgg_block_backward_impl(const void* dnext_v, int dnext_dtype, int fla
   ASR_REQUIRE(!z_is_p || rows_b || (full && gamma && pt == 0), ASR_ERR_UNSUPPORTED,
               "vgg_block_backward: z aliased to P needs a pass that masks from P");
   int bgrid = pgrid;
-  if (rows_b) {   // at most pgrid blocks (the bias-partial region)
+  // pooled layers whose windows cover every input pixel: the pooled-grid walk
+  // (ASR_VGG_POOL_WALK=0: the input-pixel walk)
+  const char* pwe = getenv("ASR_VGG_POOL_WALK");
+  const bool pool_walk = rows_b && pt && !(pwe && pwe[0] == '0') && 2 * pl.To >= T &&
+                         2 * pl.Fo >= F;
+  if (pool_walk) {
+    const int nrow = B * pl.To, rpb = (nrow + pgrid - 1) / pgrid;
+    bgrid = (nrow + rpb - 1) / rpb;
+    if (db16)
+      hipLaunchKernelGGL((rw_post_bwd_pool<uint16_t>), dim3(bgrid), dim3(RW_NT), 5 * C * sizeof(float),
+                         s, dnh, (const uint16_t*)P, slot, B, T, F, C, pl, flat, af, sums,
+                         (uint16_t*)dz, bpart, rpb);
+    else
+      hipLaunchKernelGGL((rw_post_bwd_pool<float>), dim3(bgrid), dim3(RW_NT), 5 * C * sizeof(float),
+                         s, dnext, (const uint16_t*)P, slot, B, T, F, C, pl, flat, af, sums,
+                         (uint16_t*)dz, bpart, rpb);
+  } else if (rows_b) {   // at most pgrid blocks (the bias-partial region)
     const int nrow = B * T, rpb = (nrow + pgrid - 1) / pgrid;
     bgrid = (nrow + rpb - 1) / rpb;
     if (db16) {
+
       if (pt)
         hipLaunchKernelGGL((rw_post_bwd<2, uint16_t>), dim3(bgrid), dim3(RW_NT), 5 * C * sizeof(float), s, dnh,
                            (const uint16_t*)P, slot, B, T, F, C, pl, flat, af, sums, (uint16_t*)dz,
