@@ -202,11 +202,12 @@ def _linear_forward(x, weight, bias, drop):
     return y, xo, wo, stage
 
 
-def _linear_backward(xo, wo, bias, stage, xshape, weight, drop, dyo, need_dx, dy_bias=None):
+def _linear_backward(xo, wo, bias, stage, xshape, weight, drop, dyo, need_dx, dy_bias=None,
+                     wgrad=True):
     """dX and dW (+ db) of _linear_forward from dyo: the f32 dY, or with stage
     its bf16 copy [M][Np] whose columns Nout.. are zero (they meet W's zero
     rows).  dy_bias: the tensor the bias gradient is summed from (f32 [M,
-    Nout] or the bf16 dyo)."""
+    Nout] or the bf16 dyo).  wgrad=False: dX only (_linear_wgrad elsewhere)."""
     K = xshape[-1]
     Nout = weight.shape[0]
     M = int(np.prod(xshape[:-1]))
@@ -218,10 +219,31 @@ def _linear_backward(xo, wo, bias, stage, xshape, weight, drop, dyo, need_dx, dy
         dx = torch.empty(xshape, dtype=torch.float32, device=dev)
         probs.append(gemm_problem(operand(dyo, 0, rowmap(Np)), operand(wo, 1, rowmap(Kp)),
                                   dx, rowmap(K), M, K, Np, drop=drop))
+    if not wgrad:
+        if probs:
+            run_gemm(probs, dev)
+        return dx
     gw = grad_buffer(weight)
     probs.append(gemm_problem(operand(dyo, 1, rowmap(Np)), operand(xo, 1, rowmap(Kp)), gw,
                               rowmap(K), Nout, K, M, beta=1.0))
     run_gemm(probs, dev)
+    _linear_bias_grad(bias, dy_bias, M, Nout, dev)
+    return dx
+
+
+def _linear_wgrad(xo, wo, bias, stage, xshape, weight, dyo, dy_bias=None):
+    """dW (+ db) of _linear_backward alone."""
+    K = xshape[-1]
+    Nout = weight.shape[0]
+    M = int(np.prod(xshape[:-1]))
+    dev = dyo.device
+    Kp, Np = (xo.shape[-1], wo.shape[0]) if stage else (K, Nout)
+    run_gemm([gemm_problem(operand(dyo, 1, rowmap(Np)), operand(xo, 1, rowmap(Kp)),
+                           grad_buffer(weight), rowmap(K), Nout, K, M, beta=1.0)], dev)
+    _linear_bias_grad(bias, dy_bias, M, Nout, dev)
+
+
+def _linear_bias_grad(bias, dy_bias, M, Nout, dev):
     if bias is not None:
         if dy_bias.dtype == torch.bfloat16:
             nb = N.query('asr_colsum_workspace_bytes', M, Nout)
@@ -230,7 +252,6 @@ def _linear_backward(xo, wo, bias, stage, xshape, weight, drop, dyo, need_dx, dy
                    N.ptr(grad_buffer(bias)), None, N.ptr(ws), nb, N.stream_handle(dev))
         else:
             colsum_accumulate(dy_bias.view(M, Nout), grad_buffer(bias))
-    return dx
 
 
 class LinearFn(torch.autograd.Function):
@@ -295,6 +316,9 @@ class LinearCTCFn(torch.autograd.Function):
         ctx.save_for_backward(xo, wo, logits, labels_flat, label_lens, act_lens, ws)
         ctx.meta = (bias, tuple(x.shape), weight, int(max_label_len), int(blank),
                     float(loss_scale), nbytes)
+        # produced by a BLSTM layer: its backward recurrence is the next one
+        ctx.from_blstm = type(x.grad_fn).__name__.startswith('BLSTMLayerFn') \
+            if x.grad_fn is not None else False
         ctx.drop = drop
         ctx.mark_non_differentiable(costs)
         return loss, costs
@@ -312,8 +336,39 @@ class LinearCTCFn(torch.autograd.Function):
                N.ptr(label_lens), N.ptr(act_lens), max_label_len, blank, N.ptr(g),
                loss_scale if g is not None else 0.0, N.ptr(dyo), Np, T * Np, Np, N.ptr(ws),
                nbytes, N.stream_handle(dev))
+        side_ent = None
+        if ctx.from_blstm and len(xshape) == 3 and xshape[-1] % 2 == 0 and \
+                os.environ.get('ASR_HEAD_WGRAD_SIDE', '1') != '0':
+            side_ent = _wgrad_side_stream(dev, xshape[0], xshape[-1] // 2)
+        if side_ent is None:
+            dx = _linear_backward(xo, wo, bias, True, xshape, weight, ctx.drop, dyo,
+                                  ctx.needs_input_grad[0], dy_bias=dyo)
+            return (dx,) + (None,) * 10
+        # the head's weight gradient (only the optimizer needs it) beside the
+        # top BLSTM layer's backward recurrence, as that layer's own weight
+        # gradients run beside the next one: dX alone stays on the compute stream
         dx = _linear_backward(xo, wo, bias, True, xshape, weight, ctx.drop, dyo,
-                              ctx.needs_input_grad[0], dy_bias=dyo)
+                              ctx.needs_input_grad[0], dy_bias=dyo, wgrad=False)
+        side, small, gated = side_ent
+        main = torch.cuda.current_stream(dev)
+        side.wait_stream(main)
+        if small:
+            N.call('asr_gemm_set_small_tiles', 1)
+        try:
+            with torch.cuda.stream(side):
+                if gated:
+                    N.call('asr_lstm_wgrad_gate', N.stream_handle(dev))
+                _linear_wgrad(xo, wo, bias, True, xshape, weight, dyo, dy_bias=dyo)
+        finally:
+            if small:
+                N.call('asr_gemm_set_small_tiles', 0)
+        for t in (xo, wo, dyo):
+            t.record_stream(side)
+        if not _side_pending:
+            torch.autograd.Variable._execution_engine.queue_callback(
+                lambda: _join_side_wgrads(dev, notify=False))
+        gbufs = (grad_buffer(weight),) + ((grad_buffer(bias),) if bias is not None else ())
+        _side_pending.append((side, gbufs, main))
         return (dx,) + (None,) * 10
 
 

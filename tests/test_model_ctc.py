@@ -562,3 +562,56 @@ def test_eval_retry_policy_cpu():
     with pytest.raises(ValueError):
         m.forward(1)
     assert m.calls == 1
+
+
+@pytest.mark.gpu
+def test_ctc_head_weight_gradient_beside_recurrence_bitwise(cuda_dev, monkeypatch):
+    """bf16 mode: the fused CTC head's weight / bias gradient enqueued on the
+    weight-gradient side stream, gated on the top BLSTM layer's backward
+    recurrence (LinearCTCFn.backward) -- the same loss and flat gradient, bit
+    for bit, as computing it on the compute stream (ASR_HEAD_WGRAD_SIDE=0)."""
+    from pytorch_end2end_speech_recognition_amd import native_ops
+    kw = dict(input_size=40, encoder_type='lstm', encoder_bidirectional=True,
+              encoder_num_units=256, encoder_num_proj=0, encoder_num_layers=2, fc_list=[],
+              dropout_input=0, dropout_encoder=0.2, num_classes=29, parameter_init=0.1,
+              subsample_list=[], subsample_type='drop')
+    rng = np.random.RandomState(13)
+    B, T = 32, 100
+    x_lens = np.sort(rng.randint(70, T + 1, B)).astype(np.int32)[::-1].copy()
+    x_lens[0] = T
+    y_lens = rng.randint(10, 25, B).astype(np.int32)
+    xs = rng.randn(B, T, 40).astype(np.float32)
+    for b in range(B):
+        xs[b, x_lens[b]:] = 0
+    ys = np.full((B, 25), -1, np.int32)
+    for b in range(B):
+        ys[b, :y_lens[b]] = rng.randint(0, 28, y_lens[b])
+    calls = []
+    orig = native_ops._linear_wgrad
+
+    def spy(*a, **k):
+        calls.append(torch.cuda.current_stream().cuda_stream)
+        return orig(*a, **k)
+
+    monkeypatch.setattr(native_ops, '_linear_wgrad', spy)
+    outs = {}
+    native_ops.set_compute_dtype('bf16')
+    try:
+        for on in ('1', '0'):
+            monkeypatch.setenv('ASR_HEAD_WGRAD_SIDE', on)
+            native_ops.manual_seed(7)
+            del calls[:]
+            model = _build(kw)
+            model.set_cuda()
+            model.train()
+            model.zero_grad()
+            loss = model(xs, ys, x_lens, y_lens)
+            loss.backward()
+            torch.cuda.synchronize()
+            outs[on] = (loss.item(), model._flat_grad.clone(), len(calls))
+    finally:
+        native_ops.set_compute_dtype('fp32')
+    assert outs['1'][2] == 1 and outs['0'][2] == 0, (outs['1'][2], outs['0'][2])
+    assert outs['1'][0] == outs['0'][0]
+    assert torch.equal(outs['1'][1], outs['0'][1])
+    assert outs['1'][1].abs().sum().item() > 0
