@@ -316,9 +316,9 @@ class LinearCTCFn(torch.autograd.Function):
         ctx.save_for_backward(xo, wo, logits, labels_flat, label_lens, act_lens, ws)
         ctx.meta = (bias, tuple(x.shape), weight, int(max_label_len), int(blank),
                     float(loss_scale), nbytes)
-        # produced by a BLSTM layer: its backward recurrence is the next one
-        ctx.from_blstm = type(x.grad_fn).__name__.startswith('BLSTMLayerFn') \
-            if x.grad_fn is not None else False
+        # produced by a BLSTM layer (through at most a few views / permutes):
+        # its backward recurrence is the next one the gate can wait for
+        ctx.from_blstm = _produced_by_blstm(x)
         ctx.drop = drop
         ctx.mark_non_differentiable(costs)
         return loss, costs
@@ -370,6 +370,21 @@ class LinearCTCFn(torch.autograd.Function):
         gbufs = (grad_buffer(weight),) + ((grad_buffer(bias),) if bias is not None else ())
         _side_pending.append((side, gbufs, main))
         return (dx,) + (None,) * 10
+
+
+def _produced_by_blstm(t, depth=4):
+    """t's autograd graph reaches a BLSTMLayerFn within `depth` hops."""
+    frontier = [t.grad_fn] if t.grad_fn is not None else []
+    for _ in range(depth):
+        nxt = []
+        for fn in frontier:
+            if fn is None:
+                continue
+            if type(fn).__name__.startswith('BLSTMLayerFn'):
+                return True
+            nxt.extend(f for f, _ in getattr(fn, 'next_functions', ()))
+        frontier = nxt
+    return False
 
 
 def linear_ctc_loss(x, weight, bias, labels_flat, label_lens, act_lens, max_label_len,

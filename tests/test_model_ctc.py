@@ -594,6 +594,23 @@ def test_ctc_head_weight_gradient_beside_recurrence_bitwise(cuda_dev, monkeypatc
         return orig(*a, **k)
 
     monkeypatch.setattr(native_ops, '_linear_wgrad', spy)
+    # the fused head (LinearCTCFn) at this small shape: stage the 29-class product
+    monkeypatch.setattr(native_ops, '_STAGE_FLOPS_RAGGED', 1e6)
+    seen = []
+    orig_p, orig_s = native_ops._produced_by_blstm, native_ops._wgrad_side_stream
+
+    def spy_p(t, *a):
+        r = orig_p(t, *a)
+        seen.append(('from_blstm', r, type(t.grad_fn).__name__))
+        return r
+
+    def spy_s(*a):
+        r = orig_s(*a)
+        seen.append(('side', a[1:], r is not None))
+        return r
+
+    monkeypatch.setattr(native_ops, '_produced_by_blstm', spy_p)
+    monkeypatch.setattr(native_ops, '_wgrad_side_stream', spy_s)
     outs = {}
     native_ops.set_compute_dtype('bf16')
     try:
@@ -611,7 +628,7 @@ def test_ctc_head_weight_gradient_beside_recurrence_bitwise(cuda_dev, monkeypatc
             outs[on] = (loss.item(), model._flat_grad.clone(), len(calls))
     finally:
         native_ops.set_compute_dtype('fp32')
-    assert outs['1'][2] == 1 and outs['0'][2] == 0, (outs['1'][2], outs['0'][2])
+    assert outs['1'][2] == 1 and outs['0'][2] == 0, (outs['1'][2], outs['0'][2], seen)
     assert outs['1'][0] == outs['0'][0]
     assert torch.equal(outs['1'][1], outs['0'][1])
     assert outs['1'][1].abs().sum().item() > 0
