@@ -2203,19 +2203,34 @@ class VGGFn(torch.autograd.Function):
                 N.call('asr_conv_weight_unpack_acc_pad_t', N.ptr(packed_t), Co, cC, cCp,
                        N.ptr(grad_buffer(w)), N.stream_handle(dev))
             else:
-                # dW image [Co][9 Ci] = dz^T X (taps on the output index), K = padded pixels
-                packed = torch.empty(Co, 9 * cCp, **f32)
-                if l == 0 and ctx.c1w:   # x_op is the raw features xs
-                    nb = N.query('asr_conv3x3_c1_wgrad_workspace_bytes', Co)
-                    ws = _ws(nb, dev)
-                    N.call('asr_conv3x3_c1_wgrad_xs', N.ptr(x_op), 1, B, cT, cF, Co, N.ptr(dz), cCp,
-                           N.ptr(packed), N.ptr(ws), nb, N.stream_handle(dev))
-                elif not conv3x3_tr_wgrad(x_op, dz, npad, cCp, cF + 2, Co, packed):
-                    run_gemm([gemm_problem(operand(dz, 1, rowmap(Co)),
-                                           _tap_operand(x_op, 1, cCp, cCp, cF + 2, 1), packed,
-                                           rowmap(9 * cCp), Co, 9 * cCp, npad)], dev)
-                N.call('asr_conv_weight_unpack_acc_pad', N.ptr(packed), Co, cC, cCp,
-                       N.ptr(grad_buffer(w)), N.stream_handle(dev))
+                # dW image [Co][9 Ci] = dz^T X (taps on the output index), K = padded pixels.
+                # On a side stream (ASR_VGG_WGRAD_SIDE, default on): only the
+                # optimizer reads it, so it runs beside this layer's input-gradient
+                # convolution and the layer below's element-wise passes
+                side = _vgg_wgrad_stream(dev)
+                if side is not None:
+                    main = torch.cuda.current_stream(dev)
+                    side.wait_stream(main)
+                with torch.cuda.stream(side) if side is not None else _nullctx():
+                    packed = torch.empty(Co, 9 * cCp, **f32)
+                    if l == 0 and ctx.c1w:   # x_op is the raw features xs
+                        nb = N.query('asr_conv3x3_c1_wgrad_workspace_bytes', Co)
+                        ws = _ws(nb, dev)
+                        N.call('asr_conv3x3_c1_wgrad_xs', N.ptr(x_op), 1, B, cT, cF, Co, N.ptr(dz),
+                               cCp, N.ptr(packed), N.ptr(ws), nb, N.stream_handle(dev))
+                    elif not conv3x3_tr_wgrad(x_op, dz, npad, cCp, cF + 2, Co, packed):
+                        run_gemm([gemm_problem(operand(dz, 1, rowmap(Co)),
+                                               _tap_operand(x_op, 1, cCp, cCp, cF + 2, 1), packed,
+                                               rowmap(9 * cCp), Co, 9 * cCp, npad)], dev)
+                    N.call('asr_conv_weight_unpack_acc_pad', N.ptr(packed), Co, cC, cCp,
+                           N.ptr(grad_buffer(w)), N.stream_handle(dev))
+                if side is not None:
+                    for t in (x_op, dz):
+                        t.record_stream(side)
+                    if not _side_pending:
+                        torch.autograd.Variable._execution_engine.queue_callback(
+                            lambda: _join_side_wgrads(dev, notify=False))
+                    _side_pending.append((side, (grad_buffer(w),), main))
             if l == 0:
                 break
             # d input (padded rows of layer l's input) = dz (taps, mirrored) x W^T image
@@ -2240,6 +2255,28 @@ class VGGFn(torch.autograd.Function):
                                        9 * Co)], dev)
             dnext, flat = dx, 0
         return (None, None, None, None) + (None,) * len(ctx.needs_input_grad[4:])
+
+
+_vgg_side = {}
+
+
+def _vgg_wgrad_stream(dev):
+    """The stream the VGG convolutions' weight gradients run on, or None (the
+    compute stream; ASR_VGG_WGRAD_SIDE=0)."""
+    if os.environ.get('ASR_VGG_WGRAD_SIDE', '1') == '0':
+        return None
+    st = _vgg_side.get(dev.index)
+    if st is None:
+        st = _vgg_side[dev.index] = torch.cuda.Stream(device=dev)
+    return st
+
+
+class _nullctx(object):
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
 
 
 def vgg_front(xs, specs, training, p_drop):

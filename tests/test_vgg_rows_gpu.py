@@ -165,3 +165,21 @@ def test_first_layer_relu_p_matches_separate_pass(cuda_dev, monkeypatch):
     for k in g0:
         d = float(np.linalg.norm(g1[k] - g0[k]) / max(np.linalg.norm(g0[k]), 1e-30))
         assert d <= 5e-2, (k, d)
+
+
+@pytest.mark.gpu
+def test_conv_weight_gradients_on_side_stream_bitwise(cuda_dev, monkeypatch):
+    """The VGG convolutions' weight gradients on a side stream beside the input
+    gradient and the layer below's passes (ASR_VGG_WGRAD_SIDE, default on)
+    against the same kernels on the compute stream: loss and every gradient
+    bit for bit (production channel plan, bf16, training-mode BN)."""
+    from test_parity_pins_gpu import VGG_PROD, _ctc, _vgg_batch, _with_env
+    kw = dict(VGG_PROD, input_size=40)
+    model = _ctc(kw)
+    model.set_cuda()
+    batch = _vgg_batch(40, seed=5)
+    l1, g1 = _with_env(monkeypatch, 'ASR_VGG_WGRAD_SIDE', '1', model, batch, 'bf16')
+    l0, g0 = _with_env(monkeypatch, 'ASR_VGG_WGRAD_SIDE', '0', model, batch, 'bf16')
+    assert l1 == l0, (l1, l0)
+    for k in g0:
+        np.testing.assert_array_equal(g1[k], g0[k], err_msg=k)
