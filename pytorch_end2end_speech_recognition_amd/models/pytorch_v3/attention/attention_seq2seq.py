@@ -423,7 +423,17 @@ class AttentionSeq2seq(ModelBase):
         fused loop, dropout on the W_d / W_c bottleneck outputs (LinearND,
         linear.py:44-45), embedding dropout, and scheduled sampling -- sampled
         steps take embed(argmax logits_{t-1}) computed inside the loop from the
-        same dropped bottleneck the loss sees (shared dropout seeds)."""
+        same dropped bottleneck the loss sees (shared dropout seeds).
+
+        With a BLSTM encoder, the decoder-side linear layers' weight gradients
+        run beside that encoder's top backward recurrence
+        (native_ops.wgrad_beside_encoder; ASR_DEC_WGRAD_SIDE=0: before it)."""
+        if enc_out.dim() == 3 and enc_out.shape[-1] % 2 == 0 and ops._produced_by_blstm(enc_out):
+            with ops.wgrad_beside_encoder(enc_out.shape[0], enc_out.shape[-1] // 2):
+                return self._decode_train_fused_body(enc_out, x_lens, ys, task, dir)
+        return self._decode_train_fused_body(enc_out, x_lens, ys, task, dir)
+
+    def _decode_train_fused_body(self, enc_out, x_lens, ys, task=0, dir='fwd'):
         att = getattr(self, 'attend_%d_%s' % (task, dir))
         cell = getattr(self, 'decoder_%d_%s' % (task, dir)).lstm_l0
         W_d, W_c = getattr(self, 'W_d_%d_%s' % (task, dir)), getattr(self, 'W_c_%d_%s' % (task, dir))

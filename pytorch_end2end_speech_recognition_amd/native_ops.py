@@ -254,6 +254,58 @@ def _linear_bias_grad(bias, dy_bias, M, Nout, dev):
             colsum_accumulate(dy_bias.view(M, Nout), grad_buffer(bias))
 
 
+def _wgrad_beside(dev, plan, fn, keep, gbufs):
+    """Enqueue the weight-gradient work fn() on the weight-gradient side stream
+    of the recurrence shape plan = (B, H), gated on the next backward
+    recurrence (as a BLSTM layer's own weight gradients); keep: tensors the
+    side stream reads.  False when that shape runs weight gradients on the
+    compute stream (the caller then runs fn itself)."""
+    side_ent = _wgrad_side_stream(dev, *plan)
+    if side_ent is None:
+        return False
+    side, small, gated = side_ent
+    main = torch.cuda.current_stream(dev)
+    side.wait_stream(main)
+    if small:
+        N.call('asr_gemm_set_small_tiles', 1)
+    try:
+        with torch.cuda.stream(side):
+            if gated:
+                N.call('asr_lstm_wgrad_gate', N.stream_handle(dev))
+            fn()
+    finally:
+        if small:
+            N.call('asr_gemm_set_small_tiles', 0)
+    for t in keep:
+        t.record_stream(side)
+    if not _side_pending:
+        torch.autograd.Variable._execution_engine.queue_callback(
+            lambda: _join_side_wgrads(dev, notify=False))
+    _side_pending.append((side, gbufs, main))
+    return True
+
+
+# (B, H) of the encoder recurrence whose backward follows, while the decoder-side
+# linear layers of an attention model are built (wgrad_beside_encoder): their
+# weight gradients then run beside that recurrence instead of before it
+_beside_plan = [None]
+
+
+class wgrad_beside_encoder(object):
+    def __init__(self, B, H):
+        self.plan = (int(B), int(H))
+
+    def __enter__(self):
+        self.prev = _beside_plan[0]
+        if os.environ.get('ASR_DEC_WGRAD_SIDE', '1') != '0':
+            _beside_plan[0] = self.plan
+        return self
+
+    def __exit__(self, *a):
+        _beside_plan[0] = self.prev
+        return False
+
+
 class LinearFn(torch.autograd.Function):
     """y = dropout(x) W^T + b.  drop=(p, seed): dropout of the INPUT with
     asr_dropout's mask, folded into the bf16 staging of x (forward) and the dX
@@ -266,6 +318,7 @@ class LinearFn(torch.autograd.Function):
         ctx.save_for_backward(xo, wo)
         ctx.meta = (bias, stage, tuple(x.shape), weight)
         ctx.drop = drop
+        ctx.beside = _beside_plan[0]
         return y
 
     @staticmethod
@@ -280,6 +333,16 @@ class LinearFn(torch.autograd.Function):
         Np = wo.shape[0] if stage else Nout
         dyo = _staged(dy, M, Nout, Np) if stage else dy   # zero columns meet zero W rows
         # dropout's backward = its mask, applied by the dX epilogue
+        if ctx.beside is not None:
+            dx = _linear_backward(xo, wo, bias, stage, xshape, weight, ctx.drop, dyo,
+                                  ctx.needs_input_grad[0], dy_bias=dy, wgrad=False)
+            gb = (grad_buffer(weight),) + ((grad_buffer(bias),) if bias is not None else ())
+            if not _wgrad_beside(dy.device, ctx.beside,
+                                 lambda: _linear_wgrad(xo, wo, bias, stage, xshape, weight, dyo,
+                                                       dy_bias=dy),
+                                 (xo, wo, dyo, dy), gb):
+                _linear_wgrad(xo, wo, bias, stage, xshape, weight, dyo, dy_bias=dy)
+            return dx, None, None, None
         dx = _linear_backward(xo, wo, bias, stage, xshape, weight, ctx.drop, dyo,
                               ctx.needs_input_grad[0], dy_bias=dy)
         return dx, None, None, None
@@ -336,39 +399,22 @@ class LinearCTCFn(torch.autograd.Function):
                N.ptr(label_lens), N.ptr(act_lens), max_label_len, blank, N.ptr(g),
                loss_scale if g is not None else 0.0, N.ptr(dyo), Np, T * Np, Np, N.ptr(ws),
                nbytes, N.stream_handle(dev))
-        side_ent = None
         if ctx.from_blstm and len(xshape) == 3 and xshape[-1] % 2 == 0 and \
                 os.environ.get('ASR_HEAD_WGRAD_SIDE', '1') != '0':
-            side_ent = _wgrad_side_stream(dev, xshape[0], xshape[-1] // 2)
-        if side_ent is None:
+            # the head's weight gradient (only the optimizer needs it) beside the
+            # top BLSTM layer's backward recurrence, as that layer's own weight
+            # gradients run beside the next one: dX alone on the compute stream
             dx = _linear_backward(xo, wo, bias, True, xshape, weight, ctx.drop, dyo,
-                                  ctx.needs_input_grad[0], dy_bias=dyo)
-            return (dx,) + (None,) * 10
-        # the head's weight gradient (only the optimizer needs it) beside the
-        # top BLSTM layer's backward recurrence, as that layer's own weight
-        # gradients run beside the next one: dX alone stays on the compute stream
-        dx = _linear_backward(xo, wo, bias, True, xshape, weight, ctx.drop, dyo,
-                              ctx.needs_input_grad[0], dy_bias=dyo, wgrad=False)
-        side, small, gated = side_ent
-        main = torch.cuda.current_stream(dev)
-        side.wait_stream(main)
-        if small:
-            N.call('asr_gemm_set_small_tiles', 1)
-        try:
-            with torch.cuda.stream(side):
-                if gated:
-                    N.call('asr_lstm_wgrad_gate', N.stream_handle(dev))
+                                  ctx.needs_input_grad[0], dy_bias=dyo, wgrad=False)
+            gb = (grad_buffer(weight),) + ((grad_buffer(bias),) if bias is not None else ())
+            if not _wgrad_beside(dev, (xshape[0], xshape[-1] // 2),
+                                 lambda: _linear_wgrad(xo, wo, bias, True, xshape, weight, dyo,
+                                                       dy_bias=dyo),
+                                 (xo, wo, dyo), gb):
                 _linear_wgrad(xo, wo, bias, True, xshape, weight, dyo, dy_bias=dyo)
-        finally:
-            if small:
-                N.call('asr_gemm_set_small_tiles', 0)
-        for t in (xo, wo, dyo):
-            t.record_stream(side)
-        if not _side_pending:
-            torch.autograd.Variable._execution_engine.queue_callback(
-                lambda: _join_side_wgrads(dev, notify=False))
-        gbufs = (grad_buffer(weight),) + ((grad_buffer(bias),) if bias is not None else ())
-        _side_pending.append((side, gbufs, main))
+            return (dx,) + (None,) * 10
+        dx = _linear_backward(xo, wo, bias, True, xshape, weight, ctx.drop, dyo,
+                              ctx.needs_input_grad[0], dy_bias=dyo)
         return (dx,) + (None,) * 10
 
 

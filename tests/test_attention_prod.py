@@ -150,3 +150,32 @@ def test_prod_attention_bf16_within_tolerance(name, cuda_dev):
     np.testing.assert_allclose(loss, float(d['loss'][0]), rtol=1e-2)
     for k, e in errs.items():
         assert e <= 0.3, (k, e)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name', NAMES)
+def test_decoder_weight_gradients_beside_encoder_bitwise(name, cuda_dev, monkeypatch):
+    """The decoder-side linear layers' weight gradients enqueued on the
+    weight-gradient side stream, gated on the encoder's top backward recurrence
+    (native_ops.wgrad_beside_encoder) -- loss and every gradient bit for bit as
+    on the compute stream (ASR_DEC_WGRAD_SIDE=0), bf16 mode."""
+    from pytorch_end2end_speech_recognition_amd import native_ops
+    used = []
+    orig = native_ops._wgrad_beside
+
+    def spy(*a, **k):
+        r = orig(*a, **k)
+        used.append(r)
+        return r
+
+    monkeypatch.setattr(native_ops, '_wgrad_beside', spy)
+    out = {}
+    for on in ('1', '0'):
+        monkeypatch.setenv('ASR_DEC_WGRAD_SIDE', on)
+        del used[:]
+        _, loss, grads, _ = _gpu_run(name, 'bf16', cuda_dev)
+        out[on] = (loss, grads, sum(1 for u in used if u))
+    assert out['1'][2] > 0, out['1'][2]
+    assert out['1'][0] == out['0'][0], (out['1'][0], out['0'][0])
+    for k in out['0'][1]:
+        np.testing.assert_array_equal(out['1'][1][k], out['0'][1][k], err_msg=k)
