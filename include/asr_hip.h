@@ -95,6 +95,20 @@ int asr_ctc_backward_bf16(const float* acts, long long stride_t, long long strid
                           const float* grad_scale, float scale, uint16_t* grads,
                           long long gstride_t, long long gstride_b, int gld,
                           const void* workspace, size_t ws_bytes, void* stream);
+/* asr_ctc_backward_bf16 that also ADDS the f32 column sums of the gradient,
+ * formed before the bf16 rounding, into dbias [V] (the output layer's bias
+ * gradient of the fused CTC head: the reference's LinearND bias gradient,
+ * linear.py:32-47, summed from dY = ctc.py:30-52's gradient).  Deterministic
+ * (fixed-order per-block partials); bias_ws holds
+ * asr_ctc_bias_workspace_bytes(T, B, V, gld) bytes.  V <= 16384. */
+size_t asr_ctc_bias_workspace_bytes(int T, int B, int V, int gld);
+int asr_ctc_backward_bf16_db(const float* acts, long long stride_t, long long stride_b, int T,
+                             int B, int V, const int32_t* labels_flat, const int32_t* label_lens,
+                             const int32_t* act_lens, int max_label_len, int blank,
+                             const float* grad_scale, float scale, uint16_t* grads,
+                             long long gstride_t, long long gstride_b, int gld,
+                             const void* workspace, size_t ws_bytes, float* dbias, void* bias_ws,
+                             size_t bias_ws_bytes, void* stream);
 /* warp-ctc drop-in: forward + backward with scale 1 in one call. */
 int asr_ctc_fwd_bwd(const float* acts, long long stride_t, long long stride_b, int T, int B,
                     int V, const int32_t* labels_flat, const int32_t* label_lens,
@@ -362,9 +376,10 @@ int asr_optim_step(int kind, float* params, const float* grads, float* m, float*
 /* ------------------------------------------------------- elementwise
  * asr_dropout: y = x * (u(seed, i) >= p) / (1 - p), u a counter hash (the
  *   mask is recomputed from (seed, i) in backward: call again on dy).  u(seed,
- *   i) is 16-bit field i % 2 of lowbias32(key + (i / 2) * 0x9E3779B9), key =
- *   (uint32)seed ^ (uint32)(seed >> 32) * 0x85EBCA6B, divided by 65536
- *   (round 4: two elements per 32-bit hash; oracle/rng.py restates it).
+ *   i) is 16-bit field i % 2 of lowbias32(((i / 2) * 0x9E3779B9) ^ key), key =
+ *   lowbias32((uint32)seed ^ (uint32)(seed >> 32) * 0x85EBCA6B), divided by
+ *   65536 (two elements per 32-bit hash; one stream covers 2^33 elements;
+ *   oracle/rng.py restates it).
  *   Replaces nn.Dropout on the encoder / decoder activations.
  * asr_embedding_*: nn.Embedding(padding_idx) lookup / gradient (linear.py:50-77;
  *   trans=1: weight stored [E][V], the one-hot @ W^T of Embedding_LS,

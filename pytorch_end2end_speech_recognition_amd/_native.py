@@ -43,6 +43,10 @@ SIGNATURES = {
     'asr_ctc_backward_bf16': (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp,
                                       c_int, c_int, c_vp, c_float, c_vp, c_ll, c_ll, c_int, c_vp,
                                       c_size, c_vp]),
+    'asr_ctc_bias_workspace_bytes': (c_size, [c_int, c_int, c_int, c_int]),
+    'asr_ctc_backward_bf16_db': (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp,
+                                         c_int, c_int, c_vp, c_float, c_vp, c_ll, c_ll, c_int, c_vp,
+                                         c_size, c_vp, c_vp, c_size, c_vp]),
     'asr_ctc_fwd_bwd': (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int,
                                 c_int, c_int, c_vp, c_vp, c_vp, c_size, c_vp]),
     'asr_gemm': (c_int, [c_vp, c_int, c_int, c_vp]),

@@ -91,23 +91,30 @@ __device__ __forceinline__ float wave_max(float v) {
 
 // Dropout RNG shared by every kernel that applies or regenerates a mask.
 // Element i of a tensor dropped with `seed` is kept iff u01(seed, i) >= p,
-// where u01 is 16-bit field i % 2 of lowbias32(key + (i / 2) * 0x9E3779B9)
-// (32-bit arithmetic, key = the seed folded to 32 bits), divided by 65536:
-// two elements per hash of 7 VALU instructions.  (Round 4 first used one
-// 64-bit splitmix64 finaliser per 4 elements, ~30 instructions; the
-// dropout-applying VGG passes were then ~50 % VALU-busy, 157 instructions per
-// 16-B group.)  Resolution 2^-16: p = 0.2 drops with probability 0.200012.
-__device__ __forceinline__ unsigned drop_key(unsigned long long seed) {
-  return (unsigned)seed ^ ((unsigned)(seed >> 32) * 0x85EBCA6Bu);
-}
-__device__ __forceinline__ unsigned drop_hash(unsigned key, unsigned q) {
-  unsigned x = key + q * 0x9E3779B9u;
+// where u01 is 16-bit field i % 2 of lowbias32(((i / 2) * 0x9E3779B9) ^ key)
+// (32-bit arithmetic), divided by 65536: two elements per hash of 7 VALU
+// instructions.  key = lowbias32 of the seed folded to 32 bits: mixed in by
+// XOR after a pre-hash, two seeds' streams are not shifted copies of one
+// another (round 4 added an unhashed key to the counter: every seed read the
+// same sequence from a different start).  One stream covers 2^33
+// elements (the counter i / 2 is 32 bits); the largest dropped tensor here is
+// B x T x 2H = 3.3e7 at the bench shapes.  (Round 4 first used one 64-bit
+// splitmix64 finaliser per 4 elements, ~30 instructions; the dropout-applying
+// VGG passes were then ~50 % VALU-busy.)  Resolution 2^-16: p = 0.2 drops
+// with probability 0.200012.
+__device__ __forceinline__ unsigned lowbias32(unsigned x) {
   x ^= x >> 16;
   x *= 0x7FEB352Du;
   x ^= x >> 15;
   x *= 0x846CA68Bu;
   x ^= x >> 16;
   return x;
+}
+__device__ __forceinline__ unsigned drop_key(unsigned long long seed) {
+  return lowbias32((unsigned)seed ^ ((unsigned)(seed >> 32) * 0x85EBCA6Bu));
+}
+__device__ __forceinline__ unsigned drop_hash(unsigned key, unsigned q) {
+  return lowbias32((q * 0x9E3779B9u) ^ key);
 }
 __device__ __forceinline__ float u16_u01(unsigned v) {
   return (float)(v & 0xffffu) * (1.0f / 65536.0f);

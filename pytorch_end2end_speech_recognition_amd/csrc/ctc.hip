@@ -615,7 +615,14 @@ __device__ __forceinline__ void take8(const float (&v)[12], float (&o)[8]) {
 // staged LinearND product reads (native_ops.LinearCTCFn), so the f32 gradient
 // is never written and never restaged.  Eight columns per thread, one 16-B
 // store; the class representatives then overwrite their own column.
-template <bool kTable>
+// NCH > 0: the block also sums its `rpb` consecutive rows' f32 gradient per
+// column BEFORE the bf16 rounding (the output layer's bias gradient; column
+// sums of the rounded operand lose the cancellation of softmax - occupancy),
+// into colpart[block][gld]: thread-owned chunks k = tid + j * nth (j < NCH)
+// accumulate in registers; the occupancy terms of the class representatives
+// go to an LDS table [V] -- one representative per class and row, rows
+// separated by barriers, so every sum has a fixed order (deterministic).
+template <bool kTable, int NCH>
 __global__ void __launch_bounds__(256) ctc_grad_bf16(
     const float* __restrict__ acts, long long st, long long sb, int T, int V,
     const int32_t* __restrict__ labels, const int32_t* __restrict__ label_lens,
@@ -624,126 +631,192 @@ __global__ void __launch_bounds__(256) ctc_grad_bf16(
     const float* __restrict__ alpha, const float* __restrict__ beta,
     const float* __restrict__ logp, const float* __restrict__ grad_scale, float scale_mul,
     uint16_t* __restrict__ grads, long long gst, long long gsb, int gld, int rev,
-    int acts_bytes) {
-  extern __shared__ __attribute__((aligned(16))) float occ[];  // [V] (kTable) or [Spad]
-  const long long row = rev ? (long long)gridDim.x - 1 - blockIdx.x : blockIdx.x;
-  const int b = (int)(row / T), t = (int)(row % T);
-  uint16_t* g = grads + (long long)t * gst + (long long)b * gsb;
-  const float* x = acts + (long long)t * st + (long long)b * sb;
+    int acts_bytes, float* __restrict__ colpart, int rpb, long long nrows) {
+  // kTable: occ [V]; else occ [Spad] (+ the representatives' table [V] when NCH > 0)
+  extern __shared__ __attribute__((aligned(16))) float occ[];
+  float* rtab = occ + Spad;
   const int tid = threadIdx.x, nth = blockDim.x;
   const int n8 = gld >> 3;
-  const int Tb = act_lens[b];
-  const float lp = logp[b];
-  if (t >= Tb || lp == neg_inf()) {
-    for (int i = tid; i < n8; i += nth) reinterpret_cast<uint4*>(g)[i] = make_uint4(0u, 0u, 0u, 0u);
-    return;
-  }
   const float scale = (grad_scale ? grad_scale[0] : 1.0f) * scale_mul;
-  const float z = lse[row];
-  const int L = min(label_lens[b], (Spad - 1) / 2);
-  const int S = 2 * L + 1;
-  const int32_t* lab = labels + offs[b];
-  auto cls = [&](int s_) {
-    int c = (s_ & 1) ? lab[s_ >> 1] : blank;
-    return c < 0 ? 0 : (c >= V ? V - 1 : c);
-  };
-  const float* al = alpha + row * Spad;
-  const float* bt = beta + row * Spad;
-  const float* em = emit + row * Spad;
-  auto pack = [&](int c0, auto val) {   // 8 columns c0 .. c0 + 7 -> one 16-B store
-    unsigned w[4];
+  float acc[NCH > 0 ? NCH : 1][8];
+  if constexpr (NCH > 0) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = c0 + 2 * j;
-      const unsigned lo = c < V ? f2bf(val(c)) : 0u;
-      const unsigned hi = c + 1 < V ? f2bf(val(c + 1)) : 0u;
-      w[j] = lo | (hi << 16);
+    for (int j = 0; j < NCH; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[j][e] = 0.f;
+    if constexpr (!kTable) {
+      for (int v = tid; v < V; v += nth) rtab[v] = 0.f;
     }
-    reinterpret_cast<uint4*>(g)[c0 >> 3] = make_uint4(w[0], w[1], w[2], w[3]);
-  };
-  if constexpr (kTable) {
-    for (int v = tid; v < V; v += nth) occ[v] = 0.f;
-    __syncthreads();
-    for (int s_ = tid; s_ < S; s_ += nth) atomicAdd(&occ[cls(s_)], ex2(al[s_] + bt[s_] - em[s_] - lp));
-    __syncthreads();
-    for (int i = tid; i < n8; i += nth)
-      pack(8 * i, [&](int c) { return (__expf(x[c] - z) - occ[c]) * scale; });
-    return;
-  } else {
-    for (int s_ = tid; s_ < S; s_ += nth) occ[s_] = ex2(al[s_] + bt[s_] - em[s_] - lp);
-    __syncthreads();
-    int rep_c[4];
-    float rep_v[4];
+  }
+  for (int r = 0; r < rpb; ++r) {
+    const long long lin = (long long)blockIdx.x * rpb + r;
+    if (lin >= nrows) break;                       // block-uniform
+    const long long row = rev ? nrows - 1 - lin : lin;
+    const int b = (int)(row / T), t = (int)(row % T);
+    uint16_t* g = grads + (long long)t * gst + (long long)b * gsb;
+    const float* x = acts + (long long)t * st + (long long)b * sb;
+    const int Tb = act_lens[b];
+    const float lp = logp[b];
+    if (t >= Tb || lp == neg_inf()) {               // row-uniform
+      for (int i = tid; i < n8; i += nth) reinterpret_cast<uint4*>(g)[i] = make_uint4(0u, 0u, 0u, 0u);
+      continue;
+    }
+    const float z = lse[row];
+    const int L = min(label_lens[b], (Spad - 1) / 2);
+    const int S = 2 * L + 1;
+    const int32_t* lab = labels + offs[b];
+    auto cls = [&](int s_) {
+      int c = (s_ & 1) ? lab[s_ >> 1] : blank;
+      return c < 0 ? 0 : (c >= V ? V - 1 : c);
+    };
+    const float* al = alpha + row * Spad;
+    const float* bt = beta + row * Spad;
+    const float* em = emit + row * Spad;
+    // 8 columns c0 .. c0 + 7 -> one 16-B store (+ their f32 values into a[])
+    auto pack = [&](int c0, auto val, float* a) {
+      unsigned w[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      rep_c[r] = -1;
-      rep_v[r] = 0.f;
-      const int s_ = tid + r * nth;
-      if (s_ >= S) continue;
-      const int c = cls(s_);
-      bool first;
-      if ((s_ & 1) == 0) {
-        first = s_ == 0;
+      for (int j = 0; j < 4; ++j) {
+        const int c = c0 + 2 * j;
+        const float lo = c < V ? val(c) : 0.f;
+        const float hi = c + 1 < V ? val(c + 1) : 0.f;
+        if (a) { a[2 * j] += lo; a[2 * j + 1] += hi; }
+        w[j] = (c < V ? (unsigned)f2bf(lo) : 0u) | ((c + 1 < V ? (unsigned)f2bf(hi) : 0u) << 16);
+      }
+      reinterpret_cast<uint4*>(g)[c0 >> 3] = make_uint4(w[0], w[1], w[2], w[3]);
+    };
+    if constexpr (kTable) {
+      for (int v = tid; v < V; v += nth) occ[v] = 0.f;
+      __syncthreads();
+      for (int s_ = tid; s_ < S; s_ += nth) atomicAdd(&occ[cls(s_)], ex2(al[s_] + bt[s_] - em[s_] - lp));
+      __syncthreads();
+      auto val = [&](int c) { return (__expf(x[c] - z) - occ[c]) * scale; };
+      if constexpr (NCH > 0) {
+#pragma unroll
+        for (int j = 0; j < NCH; ++j) {
+          const int k = tid + j * nth;
+          if (k < n8) pack(8 * k, val, acc[j]);
+        }
       } else {
-        first = c != blank;
-        for (int q = 1; q < s_ && first; q += 2) first = cls(q) != c;
+        for (int i = tid; i < n8; i += nth) pack(8 * i, val, (float*)nullptr);
       }
-      if (!first) continue;
-      float acc = 0.f;
-      for (int q = 0; q < S; ++q)
-        if (cls(q) == c) acc += occ[q];
-      rep_c[r] = c;
-      rep_v[r] = acc;
-    }
-    // stream the row: g = softmax * scale.  The f32 row starts at any 4-B
-    // alignment, a (row-uniform) elements past a 16-B boundary; each thread
-    // takes 8 columns at a time with three aligned 16-B buffer loads (past the
-    // activations' end they read zeros) and keeps elements a .. a + 7
-    if (acts_bytes) {
-      const long long xo = (long long)t * st + (long long)b * sb;   // row start (elements)
-      const int a = (int)(xo & 3);
-      const __amdgpu_buffer_rsrc_t rs =
-          __builtin_amdgcn_make_buffer_rsrc((void*)acts, 0, acts_bytes, 0x00020000);
-      const unsigned base = (unsigned)((xo - a) * 4);
-      auto chunk = [&](int k) {
-        float v[12];
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-          const f32x4 w = __builtin_bit_cast(
-              f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, base + (unsigned)(32 * k + 16 * q), 0, 0));
-          v[4 * q] = w[0]; v[4 * q + 1] = w[1]; v[4 * q + 2] = w[2]; v[4 * q + 3] = w[3];
-        }
-        float o[8];
-        switch (a) {   // row-uniform
-          case 0: take8<0>(v, o); break;
-          case 1: take8<1>(v, o); break;
-          case 2: take8<2>(v, o); break;
-          default: take8<3>(v, o); break;
-        }
-        const int c0 = 8 * k;
-        unsigned w4[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const unsigned lo = c0 + 2 * j < V ? f2bf(__expf(o[2 * j] - z) * scale) : 0u;
-          const unsigned hi = c0 + 2 * j + 1 < V ? f2bf(__expf(o[2 * j + 1] - z) * scale) : 0u;
-          w4[j] = lo | (hi << 16);
-        }
-        reinterpret_cast<uint4*>(g)[k] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
-      };
-      int i = tid;
-      for (; i + nth < n8; i += 2 * nth) {
-        chunk(i);
-        chunk(i + nth);
-      }
-      for (; i < n8; i += nth) chunk(i);
+      __syncthreads();   // occ is rewritten by the next row
     } else {
-      for (int i = tid; i < n8; i += nth) pack(8 * i, [&](int c) { return __expf(x[c] - z) * scale; });
-    }
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
+      for (int s_ = tid; s_ < S; s_ += nth) occ[s_] = ex2(al[s_] + bt[s_] - em[s_] - lp);
+      __syncthreads();
+      int rep_c[4];
+      float rep_v[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (rep_c[r] >= 0) g[rep_c[r]] = f2bf((__expf(x[rep_c[r]] - z) - rep_v[r]) * scale);
+      for (int q4 = 0; q4 < 4; ++q4) {
+        rep_c[q4] = -1;
+        rep_v[q4] = 0.f;
+        const int s_ = tid + q4 * nth;
+        if (s_ >= S) continue;
+        const int c = cls(s_);
+        bool first;
+        if ((s_ & 1) == 0) {
+          first = s_ == 0;
+        } else {
+          first = c != blank;
+          for (int q = 1; q < s_ && first; q += 2) first = cls(q) != c;
+        }
+        if (!first) continue;
+        float sum = 0.f;
+        for (int q = 0; q < S; ++q)
+          if (cls(q) == c) sum += occ[q];
+        rep_c[q4] = c;
+        rep_v[q4] = sum;
+      }
+      // stream the row: g = softmax * scale.  The f32 row starts at any 4-B
+      // alignment, a (row-uniform) elements past a 16-B boundary; each thread
+      // takes 8 columns at a time with three aligned 16-B buffer loads (past the
+      // activations' end they read zeros) and keeps elements a .. a + 7
+      if (acts_bytes) {
+        const long long xo = (long long)t * st + (long long)b * sb;   // row start (elements)
+        const int a = (int)(xo & 3);
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc((void*)acts, 0, acts_bytes, 0x00020000);
+        const unsigned base = (unsigned)((xo - a) * 4);
+        auto chunk = [&](int k, float* ac) {
+          float v[12];
+#pragma unroll
+          for (int q = 0; q < 3; ++q) {
+            const f32x4 w = __builtin_bit_cast(
+                f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, base + (unsigned)(32 * k + 16 * q), 0, 0));
+            v[4 * q] = w[0]; v[4 * q + 1] = w[1]; v[4 * q + 2] = w[2]; v[4 * q + 3] = w[3];
+          }
+          float o[8];
+          switch (a) {   // row-uniform
+            case 0: take8<0>(v, o); break;
+            case 1: take8<1>(v, o); break;
+            case 2: take8<2>(v, o); break;
+            default: take8<3>(v, o); break;
+          }
+          const int c0 = 8 * k;
+          unsigned w4[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float lo = c0 + 2 * j < V ? __expf(o[2 * j] - z) * scale : 0.f;
+            const float hi = c0 + 2 * j + 1 < V ? __expf(o[2 * j + 1] - z) * scale : 0.f;
+            if (ac) { ac[2 * j] += lo; ac[2 * j + 1] += hi; }
+            w4[j] = (c0 + 2 * j < V ? (unsigned)f2bf(lo) : 0u) |
+                    ((c0 + 2 * j + 1 < V ? (unsigned)f2bf(hi) : 0u) << 16);
+          }
+          reinterpret_cast<uint4*>(g)[k] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+        };
+        if constexpr (NCH > 0) {
+#pragma unroll
+          for (int j = 0; j < NCH; ++j) {
+            const int k = tid + j * nth;
+            if (k < n8) chunk(k, acc[j]);
+          }
+        } else {
+          int i = tid;
+          for (; i + nth < n8; i += 2 * nth) {
+            chunk(i, nullptr);
+            chunk(i + nth, nullptr);
+          }
+          for (; i < n8; i += nth) chunk(i, nullptr);
+        }
+      } else {
+        auto val = [&](int c) { return __expf(x[c] - z) * scale; };
+        if constexpr (NCH > 0) {
+#pragma unroll
+          for (int j = 0; j < NCH; ++j) {
+            const int k = tid + j * nth;
+            if (k < n8) pack(8 * k, val, acc[j]);
+          }
+        } else {
+          for (int i = tid; i < n8; i += nth) pack(8 * i, val, (float*)nullptr);
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4)
+        if (rep_c[q4] >= 0) {
+          g[rep_c[q4]] = f2bf((__expf(x[rep_c[q4]] - z) - rep_v[q4]) * scale);
+          if constexpr (NCH > 0) atomicAdd(&rtab[rep_c[q4]], rep_v[q4] * scale);
+        }
+    }
+  }
+  if constexpr (NCH > 0) {
+    __syncthreads();   // the representatives' table is complete
+    float* o = colpart + (long long)blockIdx.x * gld;
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      const int k = tid + j * nth;
+      if (k >= n8) continue;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = 8 * k + e;
+        v[e] = acc[j][e];
+        if constexpr (!kTable) v[e] -= c < V ? rtab[c] : 0.f;
+      }
+      *reinterpret_cast<f32x4*>(o + 8 * k) = f32x4{v[0], v[1], v[2], v[3]};
+      *reinterpret_cast<f32x4*>(o + 8 * k + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    }
   }
 }
 
@@ -888,13 +961,34 @@ extern "C" int asr_ctc_backward(const float* acts, long long stride_t, long long
   return ASR_OK;
 }
 
-extern "C" int asr_ctc_backward_bf16(const float* acts, long long stride_t, long long stride_b,
-                                     int T, int B, int V, const int32_t* labels_flat,
-                                     const int32_t* label_lens, const int32_t* act_lens,
-                                     int max_label_len, int blank, const float* grad_scale,
-                                     float scale, uint16_t* grads, long long gstride_t,
-                                     long long gstride_b, int gld, const void* workspace,
-                                     size_t ws_bytes, void* stream) {
+// Output-layer bias gradient of the fused head (asr_ctc_backward_bf16_db):
+// rows per block and blocks of the column-partial pass.
+static void ctc_bias_grid(int T, int B, int V, int* rpb, int* nblk) {
+  const long long rows = (long long)B * T;
+  const long long target = V <= 1024 ? 1024 : 512;   // partial rows: nblk x gld f32
+  long long r = rows / target;
+  if (r < 1) r = 1;
+  if (r > 64) r = 64;
+  *rpb = (int)r;
+  *nblk = (int)((rows + r - 1) / r);
+}
+
+extern "C" size_t asr_ctc_bias_workspace_bytes(int T, int B, int V, int gld) {
+  if (T <= 0 || B <= 0 || V <= 1 || gld < V) return 0;
+  int rpb, nblk;
+  ctc_bias_grid(T, B, V, &rpb, &nblk);
+  const size_t part = ((size_t)nblk * gld * sizeof(float) + 255) & ~(size_t)255;
+  return part + asr_colsum_workspace_bytes(nblk, V);
+}
+
+static int ctc_backward_bf16_impl(const float* acts, long long stride_t, long long stride_b, int T,
+                                  int B, int V, const int32_t* labels_flat,
+                                  const int32_t* label_lens, const int32_t* act_lens,
+                                  int max_label_len, int blank, const float* grad_scale,
+                                  float scale, uint16_t* grads, long long gstride_t,
+                                  long long gstride_b, int gld, const void* workspace,
+                                  size_t ws_bytes, float* dbias, void* bws, size_t bws_bytes,
+                                  void* stream) {
   int rc = check_common(acts, T, B, V, labels_flat, label_lens, act_lens, max_label_len, blank,
                         workspace, ws_bytes);
   if (rc) return rc;
@@ -916,20 +1010,80 @@ extern "C" int asr_ctc_backward_bf16(const float* acts, long long stride_t, long
                      (stride_b == V && stride_t == (long long)B * V);
   const int abytes = (!table && dense && nb < 0x7fffff00LL && ((uintptr_t)acts & 15) == 0)
                          ? (int)nb : 0;
+  const long long rows = (long long)B * T;
+  const int rev = (ctc_row_order() >> 1) & 1;
+  int rpb = 1, nblk = (int)rows, nch = 0;
+  float* colpart = nullptr;
+  if (dbias) {
+    ASR_REQUIRE(bws && bws_bytes >= asr_ctc_bias_workspace_bytes(T, B, V, gld), ASR_ERR_WORKSPACE,
+                "ctc_bf16_db: bias workspace %zu < %zu", bws_bytes,
+                asr_ctc_bias_workspace_bytes(T, B, V, gld));
+    const int n8 = gld >> 3;
+    nch = (n8 + threads - 1) / threads;
+    nch = nch <= 1 ? 1 : nch <= 2 ? 2 : nch <= 4 ? 4 : nch <= 8 ? 8 : 0;
+    ASR_REQUIRE(nch > 0 && (table || (size_t)(Spad + V) * 4 <= 64 * 1024), ASR_ERR_UNSUPPORTED,
+                "ctc_bf16_db: V %d too wide for the in-kernel bias sums", V);
+    ctc_bias_grid(T, B, V, &rpb, &nblk);
+    colpart = (float*)bws;
+  }
   // algorithmic HBM bytes: activations read (4 V) + bf16 gradient written (2 gld) per row
   const int pslot = prof_begin_launch(ASR_PROF_CTC_GRAD, s, (4.0 * V + 2.0 * gld) * B * T, V);
-#define ASR_CTC_G16(TB)                                                                          \
-  hipLaunchKernelGGL(ctc_grad_bf16<TB>, dim3((unsigned)((long long)B * T)), dim3(threads),       \
-                     (TB ? V : Spad) * sizeof(float), s, acts, stride_t, stride_b, T, V,         \
-                     labels_flat, label_lens, act_lens, ws.offs, blank, Spad, ws.lse, ws.emit,   \
-                     ws.alpha, ws.beta, ws.logp, grad_scale, scale, grads, gstride_t, gstride_b, \
-                     gld, (ctc_row_order() >> 1) & 1, abytes)
-  if (table) ASR_CTC_G16(true);
-  else ASR_CTC_G16(false);
+  const size_t lds = (table ? V : Spad + (dbias ? V : 0)) * sizeof(float);
+#define ASR_CTC_G16(TB, NC)                                                                      \
+  hipLaunchKernelGGL((ctc_grad_bf16<TB, NC>), dim3((unsigned)nblk), dim3(threads), lds, s, acts,  \
+                     stride_t, stride_b, T, V, labels_flat, label_lens, act_lens, ws.offs, blank, \
+                     Spad, ws.lse, ws.emit, ws.alpha, ws.beta, ws.logp, grad_scale, scale, grads, \
+                     gstride_t, gstride_b, gld, rev, abytes, colpart, rpb, rows)
+  if (table) {
+    if (nch) ASR_CTC_G16(true, 1);
+    else ASR_CTC_G16(true, 0);
+  } else {
+    switch (nch) {
+      case 0: ASR_CTC_G16(false, 0); break;
+      case 1: ASR_CTC_G16(false, 1); break;
+      case 2: ASR_CTC_G16(false, 2); break;
+      case 4: ASR_CTC_G16(false, 4); break;
+      default: ASR_CTC_G16(false, 8); break;
+    }
+  }
 #undef ASR_CTC_G16
   ASR_LAUNCH_CHECK();
   prof_end_launch(ASR_PROF_CTC_GRAD, pslot, s);
+  if (dbias) {   // fixed-order column sums of the per-block partials, added into dbias
+    const size_t part = ((size_t)nblk * gld * sizeof(float) + 255) & ~(size_t)255;
+    rc = asr_colsum_accumulate(colpart, gld, nblk, V, 1.0f, dbias, nullptr, (char*)bws + part,
+                               bws_bytes - part, stream);
+    if (rc) return rc;
+  }
   return ASR_OK;
+}
+
+extern "C" int asr_ctc_backward_bf16(const float* acts, long long stride_t, long long stride_b,
+                                     int T, int B, int V, const int32_t* labels_flat,
+                                     const int32_t* label_lens, const int32_t* act_lens,
+                                     int max_label_len, int blank, const float* grad_scale,
+                                     float scale, uint16_t* grads, long long gstride_t,
+                                     long long gstride_b, int gld, const void* workspace,
+                                     size_t ws_bytes, void* stream) {
+  return ctc_backward_bf16_impl(acts, stride_t, stride_b, T, B, V, labels_flat, label_lens,
+                                act_lens, max_label_len, blank, grad_scale, scale, grads,
+                                gstride_t, gstride_b, gld, workspace, ws_bytes, nullptr, nullptr, 0,
+                                stream);
+}
+
+extern "C" int asr_ctc_backward_bf16_db(const float* acts, long long stride_t, long long stride_b,
+                                        int T, int B, int V, const int32_t* labels_flat,
+                                        const int32_t* label_lens, const int32_t* act_lens,
+                                        int max_label_len, int blank, const float* grad_scale,
+                                        float scale, uint16_t* grads, long long gstride_t,
+                                        long long gstride_b, int gld, const void* workspace,
+                                        size_t ws_bytes, float* dbias, void* bias_ws,
+                                        size_t bias_ws_bytes, void* stream) {
+  ASR_REQUIRE(dbias, ASR_ERR_ARG, "ctc_bf16_db: dbias is null");
+  return ctc_backward_bf16_impl(acts, stride_t, stride_b, T, B, V, labels_flat, label_lens,
+                                act_lens, max_label_len, blank, grad_scale, scale, grads,
+                                gstride_t, gstride_b, gld, workspace, ws_bytes, dbias, bias_ws,
+                                bias_ws_bytes, stream);
 }
 
 extern "C" int asr_ctc_fwd_bwd(const float* acts, long long stride_t, long long stride_b, int T,

@@ -428,8 +428,9 @@ class AttentionSeq2seq(ModelBase):
         With a BLSTM encoder, the decoder-side linear layers' weight gradients
         run beside that encoder's top backward recurrence
         (native_ops.wgrad_beside_encoder; ASR_DEC_WGRAD_SIDE=0: before it)."""
-        if enc_out.dim() == 3 and enc_out.shape[-1] % 2 == 0 and ops._produced_by_blstm(enc_out):
-            with ops.wgrad_beside_encoder(enc_out.shape[0], enc_out.shape[-1] // 2):
+        bh = ops._produced_by_blstm(enc_out) if enc_out.dim() == 3 else None
+        if bh is not None:
+            with ops.wgrad_beside_encoder(*bh):
                 return self._decode_train_fused_body(enc_out, x_lens, ys, task, dir)
         return self._decode_train_fused_body(enc_out, x_lens, ys, task, dir)
 

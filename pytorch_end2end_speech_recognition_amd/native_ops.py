@@ -357,9 +357,12 @@ class LinearCTCFn(torch.autograd.Function):
     rows of Np = V rounded up to 8 columns, the padding zero
     (asr_ctc_backward_bf16) -- so the f32 d logits is never written and never
     restaged (at the 10001-word head of configs[4]: 320 MB written + 480 MB
-    staging traffic per call saved), and the bias gradient is summed from the
-    same operand.  The loss and every gradient equal ctc_loss(linear(...))
-    up to the bf16 rounding of dY the staged product applies anyway."""
+    staging traffic per call saved).  The bias gradient is summed in f32 by
+    the same pass before the rounding (asr_ctc_backward_bf16_db: per-block
+    column partials, then a fixed-order sum).  dX and dW equal
+    ctc_loss(linear(...))'s up to the bf16 rounding of dY the staged product
+    applies anyway; the bias gradient equals the f32 column sum up to
+    summation order."""
 
     @staticmethod
     def forward(ctx, x, weight, bias, drop, labels_flat, label_lens, act_lens, max_label_len,
@@ -395,31 +398,43 @@ class LinearCTCFn(torch.autograd.Function):
         dev = logits.device
         dyo = torch.empty(B * T, Np, dtype=torch.bfloat16, device=dev)
         g = g_loss.contiguous() if g_loss is not None else None
-        N.call('asr_ctc_backward_bf16', N.ptr(logits), V, T * V, T, B, V, N.ptr(labels_flat),
-               N.ptr(label_lens), N.ptr(act_lens), max_label_len, blank, N.ptr(g),
-               loss_scale if g is not None else 0.0, N.ptr(dyo), Np, T * Np, Np, N.ptr(ws),
-               nbytes, N.stream_handle(dev))
-        if ctx.from_blstm and len(xshape) == 3 and xshape[-1] % 2 == 0 and \
-                os.environ.get('ASR_HEAD_WGRAD_SIDE', '1') != '0':
+        args = (N.ptr(logits), V, T * V, T, B, V, N.ptr(labels_flat), N.ptr(label_lens),
+                N.ptr(act_lens), max_label_len, blank, N.ptr(g),
+                loss_scale if g is not None else 0.0, N.ptr(dyo), Np, T * Np, Np, N.ptr(ws), nbytes)
+        # the bias gradient: f32 column sums formed inside the gradient pass before
+        # the bf16 rounding (ASR_CTC_HEAD_DB=0: column sums of the rounded dY)
+        bws = None
+        if bias is not None and V <= 16384 and os.environ.get('ASR_CTC_HEAD_DB', '1') != '0':
+            bnb = N.query('asr_ctc_bias_workspace_bytes', T, B, V, Np)
+            bws = _ws(bnb, dev)
+            N.call('asr_ctc_backward_bf16_db', *args, N.ptr(grad_buffer(bias)), N.ptr(bws), bnb,
+                   N.stream_handle(dev))
+        else:
+            N.call('asr_ctc_backward_bf16', *args, N.stream_handle(dev))
+        bias_w = None if bws is not None else bias   # bias gradient still to be summed from dY
+        if ctx.from_blstm is not None and os.environ.get('ASR_HEAD_WGRAD_SIDE', '1') != '0':
             # the head's weight gradient (only the optimizer needs it) beside the
             # top BLSTM layer's backward recurrence, as that layer's own weight
             # gradients run beside the next one: dX alone on the compute stream
-            dx = _linear_backward(xo, wo, bias, True, xshape, weight, ctx.drop, dyo,
+            dx = _linear_backward(xo, wo, bias_w, True, xshape, weight, ctx.drop, dyo,
                                   ctx.needs_input_grad[0], dy_bias=dyo, wgrad=False)
             gb = (grad_buffer(weight),) + ((grad_buffer(bias),) if bias is not None else ())
-            if not _wgrad_beside(dev, (xshape[0], xshape[-1] // 2),
-                                 lambda: _linear_wgrad(xo, wo, bias, True, xshape, weight, dyo,
+            if not _wgrad_beside(dev, ctx.from_blstm,
+                                 lambda: _linear_wgrad(xo, wo, bias_w, True, xshape, weight, dyo,
                                                        dy_bias=dyo),
                                  (xo, wo, dyo), gb):
-                _linear_wgrad(xo, wo, bias, True, xshape, weight, dyo, dy_bias=dyo)
+                _linear_wgrad(xo, wo, bias_w, True, xshape, weight, dyo, dy_bias=dyo)
             return (dx,) + (None,) * 10
-        dx = _linear_backward(xo, wo, bias, True, xshape, weight, ctx.drop, dyo,
+        dx = _linear_backward(xo, wo, bias_w, True, xshape, weight, ctx.drop, dyo,
                               ctx.needs_input_grad[0], dy_bias=dyo)
         return (dx,) + (None,) * 10
 
 
 def _produced_by_blstm(t, depth=4):
-    """t's autograd graph reaches a BLSTMLayerFn within `depth` hops."""
+    """(B, H) of the BLSTMLayerFn whose output t derives from within `depth`
+    autograd hops (views, permutes, fc layers), else None: its backward
+    recurrence is the one a gated side stream waits for, so the overlap plan
+    is built from ITS shape, not from t's width."""
     frontier = [t.grad_fn] if t.grad_fn is not None else []
     for _ in range(depth):
         nxt = []
@@ -427,10 +442,10 @@ def _produced_by_blstm(t, depth=4):
             if fn is None:
                 continue
             if type(fn).__name__.startswith('BLSTMLayerFn'):
-                return True
+                return getattr(fn, 'bh', None)
             nxt.extend(f for f, _ in getattr(fn, 'next_functions', ()))
         frontier = nxt
-    return False
+    return None
 
 
 def linear_ctc_loss(x, weight, bias, labels_flat, label_lens, act_lens, max_label_len,
@@ -1052,6 +1067,7 @@ class BLSTMLayerFn(torch.autograd.Function):
         ctx.save_for_backward(x_op, w_op, lens, w_hh, b_ih, b_hh, gx, cst,
                               y_bf if y_bf is not None else y)
         ctx.meta = (T, perm, t_mul, t_add, gbufs, cd, (B, T_src, Dsrc, Din, Dp), w_ih)
+        ctx.bh = (B, H)     # the recurrence shape a gated side stream waits on
         ctx.drop = drop
         ctx.next_rec = bool(next_rec)
         ctx.n_graph = len(graph_params)
@@ -1093,51 +1109,53 @@ class BLSTMLayerFn(torch.autograd.Function):
         mode, xu = _overlap_plan(dev, B, H)
         N.call('asr_lstm_set_bwd_pin_kb', 84 if mode == '2' else 0)
         N.call('asr_lstm_set_bwd_units', xu)
-        if act.dtype == torch.float16:
-            # packed fp16 activations of asr_lstm_forward_xh: the tagged-granule
-            # backward reads them directly; otherwise they are unpacked to f32
-            nb = N.query('asr_lstm_workspace_bytes', B, H, cd, 2)
-            ws = _ws(nb, dev)
-            if pipe is not None:
-                N.call('asr_lstm_set_dy_flags', N.ptr(pipe[0]), pipe[1], pipe[2])
-            try:
-                rc = N.query('asr_lstm_backward_dgbf_h', N.ptr(dy), N.ptr(w_hh),
-                             ctypes.c_void_p(whh_r), F32, N.ptr(lens), B, T, H, cd, N.ptr(act),
-                             N.ptr(cst), N.ptr(dg_bf), N.ptr(gbufs[2]), N.ptr(gbufs[3]),
-                             N.ptr(ws), nb, N.stream_handle(dev))
-            finally:
+        try:
+            if act.dtype == torch.float16:
+                # packed fp16 activations of asr_lstm_forward_xh: the tagged-granule
+                # backward reads them directly; otherwise they are unpacked to f32
+                nb = N.query('asr_lstm_workspace_bytes', B, H, cd, 2)
+                ws = _ws(nb, dev)
                 if pipe is not None:
-                    N.call('asr_lstm_set_dy_flags', None, 16, 0)
-                    # (after the launch: later compute-stream work sees all of dy)
-                    torch.cuda.current_stream(dev).wait_event(pipe[3])
-                    pipe = None
-            if rc not in (0, N.ASR_ERR_UNSUPPORTED):
-                raise N.NativeError('asr_lstm_backward_dgbf_h failed (rc=%d): %s' % (
-                    rc, N.lib().asr_last_error().decode(errors='replace')))
-            done = rc == 0
-            if not done:
-                a32 = torch.empty(B, T, 8 * H, dtype=torch.float32, device=dev)
-                N.call('asr_lstm_unpack_act_h', N.ptr(act), B, T, H, N.ptr(a32),
+                    N.call('asr_lstm_set_dy_flags', N.ptr(pipe[0]), pipe[1], pipe[2])
+                try:
+                    rc = N.query('asr_lstm_backward_dgbf_h', N.ptr(dy), N.ptr(w_hh),
+                                 ctypes.c_void_p(whh_r), F32, N.ptr(lens), B, T, H, cd, N.ptr(act),
+                                 N.ptr(cst), N.ptr(dg_bf), N.ptr(gbufs[2]), N.ptr(gbufs[3]),
+                                 N.ptr(ws), nb, N.stream_handle(dev))
+                finally:
+                    if pipe is not None:
+                        N.call('asr_lstm_set_dy_flags', None, 16, 0)
+                        # (after the launch: later compute-stream work sees all of dy)
+                        torch.cuda.current_stream(dev).wait_event(pipe[3])
+                        pipe = None
+                if rc not in (0, N.ASR_ERR_UNSUPPORTED):
+                    raise N.NativeError('asr_lstm_backward_dgbf_h failed (rc=%d): %s' % (
+                        rc, N.lib().asr_last_error().decode(errors='replace')))
+                done = rc == 0
+                if not done:
+                    a32 = torch.empty(B, T, 8 * H, dtype=torch.float32, device=dev)
+                    N.call('asr_lstm_unpack_act_h', N.ptr(act), B, T, H, N.ptr(a32),
+                           N.stream_handle(dev))
+                    act = a32
+            nb = N.query('asr_lstm_workspace_bytes', B, H, cd, 2 if fused_db else 1)
+            ws = _ws(nb, dev)
+            # the saved activations become the gate gradients dG in place; the bias
+            # gradients (sum of dG over b, t) are accumulated by the same call
+            if done:
+                pass
+            elif fused_db:
+                # bf16 mode: only the bf16 dG feeds the GEMMs, so the f32 dG is not stored
+                fn = 'asr_lstm_backward_dgbf' if dg_bf is not None else 'asr_lstm_backward_db'
+                N.call(fn, N.ptr(dy), N.ptr(w_hh), ctypes.c_void_p(whh_r), F32,
+                       N.ptr(lens), B, T, H, cd, N.ptr(act), N.ptr(cst), N.ptr(dg_bf),
+                       N.ptr(gbufs[2]), N.ptr(gbufs[3]), N.ptr(ws), nb, N.stream_handle(dev))
+            else:   # A/B: separate column-sum pass over dG
+                N.call('asr_lstm_backward', N.ptr(dy), N.ptr(w_hh), ctypes.c_void_p(whh_r), F32,
+                       N.ptr(lens), B, T, H, cd, N.ptr(act), N.ptr(cst), N.ptr(dg_bf), N.ptr(ws), nb,
                        N.stream_handle(dev))
-                act = a32
-        nb = N.query('asr_lstm_workspace_bytes', B, H, cd, 2 if fused_db else 1)
-        ws = _ws(nb, dev)
-        # the saved activations become the gate gradients dG in place; the bias
-        # gradients (sum of dG over b, t) are accumulated by the same call
-        if done:
-            pass
-        elif fused_db:
-            # bf16 mode: only the bf16 dG feeds the GEMMs, so the f32 dG is not stored
-            fn = 'asr_lstm_backward_dgbf' if dg_bf is not None else 'asr_lstm_backward_db'
-            N.call(fn, N.ptr(dy), N.ptr(w_hh), ctypes.c_void_p(whh_r), F32,
-                   N.ptr(lens), B, T, H, cd, N.ptr(act), N.ptr(cst), N.ptr(dg_bf),
-                   N.ptr(gbufs[2]), N.ptr(gbufs[3]), N.ptr(ws), nb, N.stream_handle(dev))
-        else:   # A/B: separate column-sum pass over dG
-            N.call('asr_lstm_backward', N.ptr(dy), N.ptr(w_hh), ctypes.c_void_p(whh_r), F32,
-                   N.ptr(lens), B, T, H, cd, N.ptr(act), N.ptr(cst), N.ptr(dg_bf), N.ptr(ws), nb,
-                   N.stream_handle(dev))
-            colsum_accumulate(act.view(B * T, 8 * H), gbufs[2], gbufs[3])
-        N.call('asr_lstm_set_bwd_units', 0)     # direct API callers: the default again
+                colsum_accumulate(act.view(B * T, 8 * H), gbufs[2], gbufs[3])
+        finally:
+            N.call('asr_lstm_set_bwd_units', 0)   # direct API callers: the default again
         # weight gradients of the layer above, if they went to a side stream: join
         # them here (they run beside the recurrence just enqueued) so the
         # gradient-ready bucket sees them on the compute stream
@@ -1422,10 +1440,11 @@ def _overlap_plan(dev, B, H):
       '0'  weight gradients on the compute stream;
       '1'  a CU-masked side stream (upper half of the CUs), only when the
            persistent backward recurrence fits in the other half;
-      '2'  (opt-in, timing experiments only) a plain side stream whose GEMMs
-           use the 128 x 128 kernel (64 KB of LDS) while the recurrence pins
-           84 KB, so GEMM work-groups are co-resident with the recurrence's on
-           every CU -- that changes the recurrence's results (DESIGN.md §5);
+      '2'  (opt-in) a plain side stream whose GEMMs use the 128 x 128 kernel
+           (64 KB of LDS) while the recurrence pins 84 KB, so GEMM work-groups
+           are co-resident with the recurrence's on every CU (rounds 3-4: wrong
+           values, a gfx950 packed-FP32 hazard the library no longer contains,
+           DESIGN.md §5; bitwise mode 0 since, tests/test_coresidency_gpu.py);
       '3'  a plain side stream with the recurrence at its default 140 KB pin,
            so no GEMM work-group can share a CU with it: the weight-gradient
            GEMMs run on the CUs the recurrence leaves free.
@@ -1445,10 +1464,6 @@ def _overlap_plan(dev, B, H):
     roomy32 = _xg_grid(B, H, ncu, 32) + 32 <= ncu
     if mode == 'auto':
         mode = '3' if roomy16 or (xu_env != '16' and roomy32) else '0'
-    elif mode == '2':
-        _warn_once('ASR_OVERLAP_WGRAD=2: weight-gradient GEMMs co-resident with the backward '
-                   'recurrence give run-to-run different (wrong) recurrence results on '
-                   'gfx950 (DESIGN.md §5); use for timing experiments only')
     if mode == '1' and _xg_grid(B, H, 2 * (ncu - ncu // 2)) > ncu // 2:
         mode = '0'
     mode = mode if mode in ('1', '2', '3') else '0'

@@ -6,16 +6,19 @@ natural bucket: its gradients are final once its weight-gradient GEMMs are
 enqueued (native_ops.BLSTMLayerFn.backward notifies 'grads').  The bucket's
 collective is issued right after the NEXT layer's backward recurrence has been
 enqueued (notification 'recurrence'), so on the device it starts when that
-persistent recurrence has finished and runs beside the GEMMs that follow it,
-and the compute stream waits for it before the recurrence after those GEMMs is
-enqueued (notification 'pre_recurrence'):
+persistent recurrence has finished and runs beside the GEMMs and the
+recurrences that follow it.  The stream semantics are RCCL's own:
+ProcessGroupNCCL makes its stream wait for the current (compute) stream at
+issue time, and ``wait()`` makes the compute stream wait for the collective.
 
-  * it never competes with a persistent recurrence for co-residency at launch
-    (the recurrence pins one work-group per CU; a collective kernel that is
-    already resident when the next recurrence launches finishes on its own);
-  * the stream semantics are RCCL's own: ProcessGroupNCCL makes its stream wait
-    for the current (compute) stream at issue time, and ``wait()`` makes the
-    compute stream wait for the collective.
+Rounds 3-4 also made the compute stream wait for every issued collective
+before each backward recurrence ('pre_recurrence'), because co-resident
+kernels changed the recurrence's results.  Round 5 found the cause -- a gfx950
+packed-FP32 operand-selection hazard the library no longer contains
+(tools/isa_check.py) -- and collectives now run beside the
+recurrences (tests/test_coresidency_gpu.py runs memory traffic beside the
+5x512 recurrence bitwise against none).  ASR_DP_SERIALIZE=1 restores the
+wait.
 
 Every rank issues the same buckets in the same canonical order (top layer
 first, then the remainder of the buffer), whatever happens during its backward:
@@ -27,6 +30,8 @@ Each bucket is scaled by grad_scale (local_B / global_B) on the compute stream
 before its SUM, so the reduced gradient equals the 1-GPU gradient of the
 global batch for any shard sizes.
 """
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -89,11 +94,12 @@ class GradBuckets(object):
 
     def _on_event(self, event, arg=None):
         if event == 'pre_recurrence':
-            # the compute stream waits for every collective issued so far, so
-            # no RCCL kernel is co-resident with the persistent recurrence
-            # about to be enqueued (co-resident kernels perturb its results,
-            # DESIGN.md §5); the collectives ran beside the GEMMs that follow
-            # the previous recurrence, so the wait is normally already met
+            # opt-in (ASR_DP_SERIALIZE=1): the compute stream waits for every
+            # collective issued so far, so none is co-resident with the
+            # persistent recurrence about to be enqueued (rounds 3-4; the
+            # co-residency fault's cause is gone)
+            if os.environ.get('ASR_DP_SERIALIZE', '0') != '1':
+                return
             for w in self.works[self.waited:]:
                 w.wait()
             self.waited = len(self.works)

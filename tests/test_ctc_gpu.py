@@ -117,19 +117,22 @@ def test_ctc_compact_grad_long_labels_k16(cuda_dev):
     np.testing.assert_allclose(grads, g_ref, rtol=2e-3, atol=2e-4)
 
 
-@pytest.mark.parametrize('V,K', [(1001, 256), (29, 4096)])
-def test_fused_ctc_head_matches_separate_ops(V, K, cuda_dev, monkeypatch):
+@pytest.mark.parametrize('V,K,B,T', [(1001, 256, 8, 200), (29, 4096, 8, 200), (29, 512, 32, 400),
+                                     (10001, 256, 8, 200)])
+def test_fused_ctc_head_matches_separate_ops(V, K, B, T, cuda_dev, monkeypatch):
     """linear_ctc_loss (LinearND + CTC as one op: the CTC gradient written
     straight into the bf16, column-padded dY operand of the head's GEMMs) vs
     linear() then ctc_loss() (f32 d logits, then a staging pass): the loss and
     dX / dW are bitwise equal -- the same f32 values rounded to bf16 once
-    either way -- and the bias gradient (summed from the bf16 operand instead
-    of the f32 d logits) agrees to bf16 rounding.  V = 1001 exercises the
-    compact gradient (no V table), V = 29 the LDS class table."""
+    either way -- and the bias gradient, summed in f32 inside the gradient
+    pass before the rounding (asr_ctc_backward_bf16_db), equals the unfused
+    path's f32 column sum up to summation order (summed from the
+    bf16 operand it was only within 1e-2).  V = 1001 / 10001 exercise the
+    compact gradient (one and eight 8-column chunks per thread), V = 29 the
+    LDS class table; B 32 x T 400 puts 12 rows in each bias-partial block."""
     ops = _native()
     rng = np.random.RandomState(11)
-    B, T = 8, 200
-    act_lens = np.sort(rng.randint(150, T + 1, B))[::-1].astype(np.int32)
+    act_lens = np.sort(rng.randint(int(T * 0.75), T + 1, B))[::-1].astype(np.int32)
     act_lens[0] = T
     label_lens = rng.randint(5, 40, B).astype(np.int32)
     labels = np.concatenate([rng.randint(1, V, l) for l in label_lens]).astype(np.int32)
@@ -144,27 +147,33 @@ def test_fused_ctc_head_matches_separate_ops(V, K, cuda_dev, monkeypatch):
     try:
         assert ops._linear_stages(B * T, K, V)
         out = {}
-        for fused in ('1', '0'):
+        for fused, db in (('1', '1'), ('0', '1'), ('1', '0'), ('1', '1')):
             monkeypatch.setenv('ASR_CTC_HEAD_FUSED', fused)
+            monkeypatch.setenv('ASR_CTC_HEAD_DB', db)
             x = x0.clone().requires_grad_(True)
             w = w0.clone().requires_grad_(True)
             b = b0.clone().requires_grad_(True)
             w.grad = torch.zeros_like(w)
-            b.grad = torch.zeros_like(b)
+            b.grad = torch.full_like(b, 0.25)          # the bias sums accumulate
             loss, costs = ops.linear_ctc_loss(x, w, b, lab, ll, al, int(label_lens.max()),
                                               loss_scale=1.0 / B)
             (loss * 2.0).backward()
             torch.cuda.synchronize()
-            out[fused] = [loss.detach().clone(), costs.clone(), x.grad.clone(), w.grad.clone(),
-                          b.grad.clone()]
+            r = [loss.detach().clone(), costs.clone(), x.grad.clone(), w.grad.clone(),
+                 b.grad.clone() - 0.25]
+            if (fused, db) in out:
+                assert all(torch.equal(p, q) for p, q in zip(out[(fused, db)], r))  # deterministic
+            out[(fused, db)] = r
     finally:
         ops.set_compute_dtype('fp32')
-    f, u = out['1'], out['0']
+    f, u, old = out[('1', '1')], out[('0', '1')], out[('1', '0')]
     assert torch.equal(f[0], u[0]) and torch.equal(f[1], u[1])
     assert torch.equal(f[2], u[2]), float((f[2] - u[2]).abs().max())
     assert torch.equal(f[3], u[3]), float((f[3] - u[3]).abs().max())
     rel = float((f[4] - u[4]).norm() / u[4].norm())
-    assert rel < 1e-2, rel
+    assert rel < 2e-5, rel
+    rel_old = float((old[4] - u[4]).norm() / u[4].norm())
+    assert rel_old < 1e-2, rel_old
 
 
 @pytest.mark.parametrize('K,Ls', [(1, [0, 5, 31]), (2, [32, 40, 63]), (4, [64, 95, 127, 70]),

@@ -54,12 +54,15 @@ def _batch(B=32, T=240, seed=0):
 @pytest.mark.parametrize('overlap,H,L', [('auto', 512, 5), ('auto', 320, 4), ('3', 256, 3),
                                          ('0', 320, 4)])
 def test_buckets_on_real_model(overlap, H, L, cuda_dev, monkeypatch):
-    """ctc5x512's encoder (auto: weight gradients on the compute stream), the
-    4x320 encoder of configs[2]-[4] (auto: on the side stream, mode 3, on the
-    CUs the next backward recurrence leaves free -- joined into the compute
-    stream before their bucket is issued), a 3x256 encoder in mode 3 and the
-    4x320 one on the compute stream (mode 0).  Every mode updates the weights
-    bitwise like the plain single-process step; the bucket checks are exact."""
+    """ctc5x512's encoder (auto: mode 3 with 32-unit backward work-groups, the
+    weight gradients on the side stream beside the next recurrence), the 4x320
+    encoder of configs[2]-[4] (auto: mode 3 with 16 units), a 3x256 encoder in
+    mode 3 and the 4x320 one on the compute stream (mode 0); the side-stream
+    gradients are joined into the compute stream before their bucket is
+    issued.  Within each parametrisation the bucketed step updates the weights
+    bitwise like the plain single-process step in the SAME overlap mode (run
+    to run, not across modes: tests/test_coresidency_gpu.py compares modes 2
+    and 3 with mode 0 bitwise); the bucket checks are exact."""
     from pytorch_end2end_speech_recognition_amd import native_ops
     from pytorch_end2end_speech_recognition_amd.utils.training import training_loop as TL
     monkeypatch.setenv('ASR_OVERLAP_WGRAD', overlap)
