@@ -172,10 +172,12 @@ def roofline_report(args, p, samples, launches, workload):
         re-streamed every step;
       * GEMMs and convolutions: 2*M*N*K (2*P*Cout*9*Cin) per launch, reported
         by the library with the launch;
-      * CTC: SURVEY §8(d)'s 8 * V bytes per output frame, split as 4 * V read
-        by the forward (emission + lattice) launch and 8 * V (read + write) by
-        the gradient launch; one extra 'ctc_op' row per V sums the two passes
-        of one call against 8 * V per frame (the whole-op figure);
+      * CTC: 4 * V bytes per output frame read by the forward (emission +
+        lattice) launch; the gradient launch reads 4 * V and writes the
+        gradient (4 * V f32, or the fused head's bf16 dY: 2 bytes x V rounded
+        up to 8 columns); one extra 'ctc_op' row per V times both passes of one
+        call against the bytes the op must move once (activations read, gradient
+        written: 8 * V per frame f32, ~6 * V bf16);
       * attention decoder passes: bytes recorded by the library, flops below.
     The dominant kernel is the instantiation with the largest total time."""
     B, H = args.batch, p['encoder_num_units']
@@ -318,14 +320,20 @@ def roofline_report(args, p, samples, launches, workload):
         if not g:
             continue
         us = r['us'] + g[0]['us']
-        nbytes = 2.0 * r['bytes']          # 4 V per frame (fwd) -> 8 V per frame
+        # the op's algorithmic bytes are the ones it must move once: the
+        # activations read (4 V per frame) and the gradient written -- f32 (4 V,
+        # 8 V in all) or, for the fused head, the bf16 dY operand (2 V rounded up
+        # to 8 columns, ~6 V in all): the gradient launch's own recorded bytes
+        # (round 4 counted 8 V for both)
+        nbytes = g[0]['bytes']
         others['ctc_op [V=%d]' % r['tag']] = {
             'bound': 'hbm', 'mean_call_us': round(us, 3), 'calls': min(r['n'], g[0]['n']),
             'achieved': round(nbytes / (us * 1e-6) / 1e9, 1), 'peak': HBM_PEAK_GBS,
             'unit': 'GB/s', 'frac': round(nbytes / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
             'algorithmic_bytes_per_call': int(nbytes),
-            'what': 'forward (emission + lattice) + gradient launches of one head, '
-                    '8 * V bytes per output frame'}
+            'bytes_per_frame_over_V': round(nbytes / max(1.0, r['bytes'] / 4.0), 3),
+            'what': 'forward (emission + lattice) + gradient launches of one head; bytes: '
+                    'activations read once + gradient written once'}
     out['other_kernels'] = others
     return out
 

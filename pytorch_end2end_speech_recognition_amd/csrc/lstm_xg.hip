@@ -1170,39 +1170,64 @@ __global__ void __launch_bounds__(256 + R * XB + 16 * XB) lstm_bwd_xg(
 #endif
     };
     for (int q = 0; q < T; ++q) {
+      const int t = dir == 0 ? T - 1 - q : q;
+      const bool act = own && t < len;
+      float ig, fg, gg, og, omi, omf, omg2, omo;   // gates and 1 - s / 1 - g^2
+      if constexpr (AH) {
+        dec_sig((float)avh[0], ig, omi);
+        dec_sig((float)avh[1], fg, omf);
+        dec_tanh((float)avh[2], gg, omg2);
+        dec_sig((float)avh[3], og, omo);
+      } else {
+        ig = av[0]; fg = av[1]; gg = av[2]; og = av[3];
+        omi = 1.f - ig; omf = 1.f - fg; omg2 = 1.f - gg * gg; omo = 1.f - og;
+      }
+#ifndef ASR_XG_BWD_NOPRE
+      // everything that does not depend on dh_t, formed while this wave waits
+      // at B1 for the sweepers (the step's inputs are in registers since the
+      // previous step): after B1 only dcell = dc + dh k_d and four products
+      // remain on the step's critical path
+      const float tc = ftanh(cc);
+      float k_d = og * (1.f - tc * tc);
+      float k_i = gg * ig * omi, k_f = cp * fg * omf, k_g = ig * omg2;
+      float k_o = tc * og * omo;
+      // pinned here: the compiler would otherwise sink them past B1 into the
+      // active-cell branch, back onto the critical path
+      asm volatile("" : "+v"(k_d), "+v"(k_i), "+v"(k_f), "+v"(k_g), "+v"(k_o), "+v"(fg));
+#endif
+      if (ct == 0) XG_TR_AT(q, 8, __builtin_amdgcn_s_memrealtime());
       __syncthreads();  // B1
+      if (ct == 0) XG_TR_AT(q, 9, __builtin_amdgcn_s_memrealtime());
       // the abort word is tested after the step's math, so its LDS read
       // overlaps the partial-sum reads instead of preceding them
       const int dead = s_dead;
-      const int t = dir == 0 ? T - 1 - q : q;
       float d_i = 0.f, d_f = 0.f, d_g = 0.f, d_o = 0.f;
-      if (own && t < len) {
+      if (act) {
         float dh = dyv;
         if (q > 0) {   // in order: a pairwise tree measured slower (same-box A/B)
 #pragma unroll
           for (int p = 0; p < NPG; ++p) dh += red[p][row][unit];
         }
         if (ddh) ddh[(((long long)b * T + t) * 2 + dir) * H + j] = dh;
-        float ig, fg, gg, og, omi, omf, omg2, omo;   // gates and 1 - s / 1 - g^2
-        if constexpr (AH) {
-          dec_sig((float)avh[0], ig, omi);
-          dec_sig((float)avh[1], fg, omf);
-          dec_tanh((float)avh[2], gg, omg2);
-          dec_sig((float)avh[3], og, omo);
-        } else {
-          ig = av[0]; fg = av[1]; gg = av[2]; og = av[3];
-          omi = 1.f - ig; omf = 1.f - fg; omg2 = 1.f - gg * gg; omo = 1.f - og;
-        }
+#ifndef ASR_XG_BWD_NOPRE
+        float dcell = __builtin_fmaf(dh, k_d, dc);
+        // dcell as an opaque value, so the vectoriser cannot splat it out of
+        // the HIGH half of a packed pair (op_sel:[x,1] -- the gfx950
+        // co-residency hazard, tools/isa_check.py)
+        asm volatile("" : "+v"(dcell));
+        d_i = dcell * k_i;
+        d_f = dcell * k_f;
+        d_g = dcell * k_g;
+        d_o = dh * k_o;
+#else
         const float tc = ftanh(cc);
         float dcell = dc + dh * og * (1.f - tc * tc);
-        // f32 activations: dcell as an opaque value, so the vectoriser cannot
-        // splat it out of the HIGH half of a packed pair (op_sel:[x,1] -- the
-        // gfx950 co-residency hazard, tools/isa_check.py)
         if constexpr (!AH) asm volatile("" : "+v"(dcell));
         d_i = dcell * gg * ig * omi;
         d_f = dcell * cp * fg * omf;
         d_g = dcell * ig * omg2;
         d_o = dh * tc * og * omo;
+#endif
         if (dcl) {
           float* o = dcl + ((((long long)b * T + t) * 2 + dir) * H + j) * 12;
           o[0] = d_i; o[1] = d_f; o[2] = d_g; o[3] = d_o;
@@ -1232,6 +1257,7 @@ __global__ void __launch_bounds__(256 + R * XB + 16 * XB) lstm_bwd_xg(
       cp = ncp;
       dyv = ndyv;
 #endif
+      if (ct == 0) XG_TR_AT(q, 10, __builtin_amdgcn_s_memrealtime());
       __syncthreads();  // B2
       if (io_pos == 0) step_io(q, t, d_i, d_f, d_g, d_o, bi, bff, bg, bo);
       __syncthreads();  // B3
@@ -1275,6 +1301,7 @@ __global__ void __launch_bounds__(256 + R * XB + 16 * XB) lstm_bwd_xg(
     __syncthreads();  // B1
     if (s_dead) return;
     __syncthreads();  // B2
+    if (mw == 0 && lane == 0) XG_TR_AT(q, 11, __builtin_amdgcn_s_memrealtime());
     bf16x8 bfk[NKS];
 #pragma unroll
     for (int kst = 0; kst < NKS; ++kst)

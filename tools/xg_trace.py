@@ -82,6 +82,11 @@ def main():
                  (10, 3, 'pub')])
     report('backward (us)', bwd, [(0, 1, 'sweep'), (1, 2, 'b1'), (2, 3, 'cell+b2'),
                                   (3, 4, 'mfma+pub')])
+    report('backward detail (us): cell wave 0: pre = step start -> at B1, b1w = waits at B1, '
+           'cell = B1 -> dg in LDS, b2w = -> past B2; mfma wave 0: b2m = B2 -> MFMA start, '
+           'mp = -> published', bwd,
+           [(0, 8, 'pre'), (8, 9, 'b1w'), (9, 10, 'cell'), (10, 3, 'b2w'), (3, 11, 'b2m'),
+            (11, 4, 'mp')])
 
 
 if __name__ == '__main__':
