@@ -47,6 +47,15 @@ int lstm_bwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* wh
                        const float* whh_r, const float* dy, float* act_dg, const float* cst,
                        void* ws, uint16_t* dgbf, float* dbpart, hipStream_t s, bool dry,
                        bool dg_f32, const uint16_t* acth = nullptr);
+// the same hand-off at reference precision (f32 granules, f32 MFMA)
+size_t lstm_xg32_fwd_bytes(int B, int H);
+size_t lstm_xg32_bwd_bytes(int B, int H);
+int lstm_fwd_xg32_launch(int B, int T, int H, const int32_t* lens, const float* whh_f,
+                         const float* whh_r, float* gx_act, float* y, float* cst, void* ws,
+                         hipStream_t s, bool dry);
+int lstm_bwd_xg32_launch(int B, int T, int H, const int32_t* lens, const float* whh_f,
+                         const float* whh_r, const float* dy, float* act_dg, const float* cst,
+                         void* ws, float* dbpart, hipStream_t s, bool dry);
 
 namespace {
 
@@ -496,7 +505,7 @@ size_t fwd_state_bytes(int B, int H, int cdt) {
 
 size_t fwd_ws(int B, int H, int cdt) {
   size_t w = cdt == ASR_DT_BF16 ? (size_t)2 * 4 * H * H * 2 : 0;  // bf16 copy of W_hh
-  const size_t xg = cdt == ASR_DT_BF16 ? lstm_xg_fwd_bytes(B, H) : 0;
+  const size_t xg = cdt == ASR_DT_BF16 ? lstm_xg_fwd_bytes(B, H) : lstm_xg32_fwd_bytes(B, H);
   return std::max(fwd_state_bytes(B, H, cdt) + w, xg);
 }
 
@@ -515,7 +524,7 @@ BwdLayout bwd_layout(int B, int H, int cdt) {
   return l;
 }
 size_t bwd_ws(int B, int H, int cdt) {
-  const size_t xg = cdt == ASR_DT_BF16 ? lstm_xg_bwd_bytes(B, H) : 0;
+  const size_t xg = cdt == ASR_DT_BF16 ? lstm_xg_bwd_bytes(B, H) : lstm_xg32_bwd_bytes(B, H);
   return std::max(bwd_layout(B, H, cdt).total, xg);
 }
 // Bias-gradient scratch behind the backward workspace: [max(B, 64)][8H] f32
@@ -566,6 +575,22 @@ extern "C" int asr_lstm_forward(float* gx_act, const void* whh_f, const void* wh
                                       gx_act, y, cst, workspace, ybf, s, false);
     ASR_REQUIRE(rc == 1, ASR_ERR_HIP, "lstm_forward: tagged-granule launch failed");
     prof_end_launch(ASR_PROF_LSTM_FWD_SEQ, slot, s);
+    return ASR_OK;
+  }
+  if (!bf && lstm_fwd_xg32_launch(B, T, H, lens, (const float*)whh_f, (const float*)whh_r, gx_act,
+                                  y, cst, workspace, s, true) == 1) {
+    // reference precision: the same persistent hand-off with f32 granules
+    const int slot = prof_begin_launch(ASR_PROF_LSTM_FWD_SEQ, s, 0.0, ASR_PTAG_LSTM_FWD_XG);
+    const int rc = lstm_fwd_xg32_launch(B, T, H, lens, (const float*)whh_f, (const float*)whh_r,
+                                        gx_act, y, cst, workspace, s, false);
+    ASR_REQUIRE(rc == 1, ASR_ERR_HIP, "lstm_forward: f32 tagged-granule launch failed");
+    prof_end_launch(ASR_PROF_LSTM_FWD_SEQ, slot, s);
+    if (ybf) {
+      const long long n = (long long)B * T * 2 * H;
+      hipLaunchKernelGGL(to_bf16, dim3((unsigned)min(4096LL, (n + 255) / 256)), dim3(256), 0, s, y,
+                         ybf, n);
+      ASR_LAUNCH_CHECK();
+    }
     return ASR_OK;
   }
   // bf16 mode with f32 weights: one conversion pass so the T step launches
@@ -652,6 +677,23 @@ static int lstm_backward_impl(const float* dy, const void* whh_f, const void* wh
     ASR_REQUIRE(rc == 1, ASR_ERR_HIP, "lstm_backward: tagged-granule launch failed");
     prof_end_launch(ASR_PROF_LSTM_BWD_SEQ, slot, s);
     *fused_bias = dbpart != nullptr;
+    return ASR_OK;
+  }
+  if (!bf && w_dtype == ASR_DT_F32 && dg_f32 &&
+      lstm_bwd_xg32_launch(B, T, H, lens, (const float*)whh_f, (const float*)whh_r, dy, act_dg, cst,
+                           workspace, dbpart, s, true) == 1) {
+    const int slot = prof_begin_launch(ASR_PROF_LSTM_BWD_SEQ, s, 0.0, ASR_PTAG_LSTM_BWD_XG);
+    const int rc = lstm_bwd_xg32_launch(B, T, H, lens, (const float*)whh_f, (const float*)whh_r, dy,
+                                        act_dg, cst, workspace, dbpart, s, false);
+    ASR_REQUIRE(rc == 1, ASR_ERR_HIP, "lstm_backward: f32 tagged-granule launch failed");
+    prof_end_launch(ASR_PROF_LSTM_BWD_SEQ, slot, s);
+    *fused_bias = dbpart != nullptr;
+    if (dgbf) {
+      const long long n = (long long)B * T * 8 * H;
+      hipLaunchKernelGGL(to_bf16, dim3((unsigned)min(4096LL, (n + 255) / 256)), dim3(256), 0, s,
+                         act_dg, dgbf, n);
+      ASR_LAUNCH_CHECK();
+    }
     return ASR_OK;
   }
   const BwdLayout L = bwd_layout(B, H, compute_dtype);

@@ -326,8 +326,18 @@ __device__ __forceinline__ void dec_tanh(float e, float& g, float& om2) { g = e;
 //     granules FIRST, then the y / c / activation / bf16-y stores and the next
 //     step's input-projection prefetch.
 // One __syncthreads per step; `part` is double-buffered by step parity.
+//
+// F32 (the reference-precision configs): h_{t-1} travels as f32 and the
+// sweepers multiply it by f32 W_hh on v_mfma_f32_16x16x4_f32.  Granules:
+// xg[par][grp][row][H/2] u64 = {h(2p) with its LSB the step tag, h(2p+1)}
+// (<= 1 f32 ulp on every other value of the recurrent input; y keeps the plain
+// values).  The K range is split into 16 contiguous slices of H / 16 units, one
+// per (sweeper wave, lane group): lane group kq of wave w covers units
+// [(4 w + kq) H / 16, ...), so each 16-B poll of four consecutive units feeds
+// four successive k-steps and the W_hh fragments are loaded in that same k
+// order.  KSW is then the number of 16-B polls per lane (H = 64 KSW, NSW = 4).
 // ---------------------------------------------------------------------------
-template <int R, int KSW, int NSW>
+template <int R, int KSW, int NSW, bool F32 = false>
 __global__ void __launch_bounds__(64 * NSW + R * XU) lstm_fwd_xg(
     int B, int T, int H, const int32_t* __restrict__ lens, const float* __restrict__ whh_f,
     const float* __restrict__ whh_r, float* __restrict__ gx_act, float* __restrict__ y,
@@ -353,7 +363,85 @@ __global__ void __launch_bounds__(64 * NSW + R * XU) lstm_fwd_xg(
   const unsigned quarter = (unsigned)(H / 4);   // granules per row
   unsigned long long* tr = blockIdx.x < XG_TR_WG ? g_xg_trace : nullptr;
 
-  if (wave < NSW) {
+  if constexpr (F32) {
+    if (wave < NSW) {
+      // --------------------------- f32 sweeper ----------------------------
+      static_assert(NSW == 4, "f32 sweepers: 16 K slices = 4 waves x 4 lane groups");
+      const int kq = lane >> 4, ln = lane & 15;
+      const bool sweeper = ln < R;
+      const int kb = (4 * wave + kq) * 4 * KSW;   // this lane group's first unit of K
+      // B fragments: B[k][n] = W_hh[g*H + u0 + n][kb + k-step], n = ln
+      float wf[4 * KSW][4];
+      {
+        const float* W = dir ? whh_r : whh_f;
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int i = 0; i < KSW; ++i) {
+            const float4 w4 = *reinterpret_cast<const float4*>(
+                W + (long long)(g * H + u0 + ln) * H + kb + 4 * i);
+            wf[4 * i][g] = w4.x;
+            wf[4 * i + 1][g] = w4.y;
+            wf[4 * i + 2][g] = w4.z;
+            wf[4 * i + 3][g] = w4.w;
+          }
+      }
+      const __amdgpu_buffer_rsrc_t rs = xg_rsrc(xg, (unsigned)(2ull * G * R * H * 4));
+      const int nsleep = __builtin_amdgcn_readfirstlane(g_xg_sleep);
+      const int ndelay = __builtin_amdgcn_readfirstlane(g_xg_delay);
+      for (int s = 0; s < T; ++s) {
+        XG_TR(s, 0, __builtin_amdgcn_s_memrealtime());
+        f32x4 acc[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (s > 0) {
+          const unsigned ebit = tag_bit(s - 1);
+          const unsigned rowoff =
+              (unsigned)(((((s - 1) & 1) * G + grp) * R + (sweeper ? ln : 0)) * (long long)H * 4);
+          u32x4 v[KSW];
+          nap(ndelay);
+          for (unsigned spins = 0;; ++spins) {
+            int ok = 1;
+            if (sweeper) {
+#pragma unroll
+              for (int i = 0; i < KSW; ++i) v[i] = ld_sc1(rs, rowoff + (unsigned)((kb + 4 * i) * 4));
+#pragma unroll
+              for (int i = 0; i < KSW; ++i)
+                ok &= (int)((((v[i][0] ^ ebit) | (v[i][2] ^ ebit)) & 1u) == 0u);
+            }
+            if (__all(ok)) {
+              XG_TR(s, 1, __builtin_amdgcn_s_memrealtime());
+              XG_TR(s, 5, spins);
+              break;
+            }
+            if (!keep_spinning(spins, abortw, nsleep)) {
+              s_dead = 1;
+              break;
+            }
+          }
+          // whole-wave MFMAs; rows >= R (lanes that did not sweep) multiply zeros
+#pragma unroll
+          for (int i = 0; i < KSW; ++i)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float a = sweeper ? __uint_as_float(v[i][e]) : 0.f;
+#pragma unroll
+              for (int g = 0; g < 4; ++g) acc[g] = mfma_f32(a, wf[4 * i + e][g], acc[g]);
+            }
+        }
+        if (4 * kq < R) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) part[s & 1][wave][4 * kq + r][g * XU + ln] = acc[g][r];
+        }
+        __syncthreads();  // B(s)
+        if (s_dead) return;
+        __syncthreads();  // Bp(s)
+      }
+      return;
+    }
+  } else if (wave < NSW) {
     // ------------------------------ sweeper -------------------------------
     const int kq = lane >> 4, ln = lane & 15;
     const bool sweeper = ln < R;
@@ -485,6 +573,20 @@ __global__ void __launch_bounds__(64 * NSW + R * XU) lstm_fwd_xg(
     const unsigned hb = f2bf(h);
     const unsigned h1 = row_from_upper<1>(hb);
     const unsigned val = hb | (h1 << 16);                 // bf16 pair for ybf
+    if constexpr (F32) {
+      // {h(j) with the tag in its LSB, h(j + 1)}: one 8-B granule per unit pair
+      const unsigned fb = __float_as_uint(h);
+      const unsigned f1 = row_from_upper<1>(fb);
+      if ((unit & 1) == 0) {
+        const unsigned long long gr =
+            ((unsigned long long)f1 << 32) | ((fb & ~1u) | tag_bit(s));
+        gu64* p = xgg + ((((long long)(s & 1) * G + grp) * R + row) * (H >> 1) + (j >> 1));
+        if (local)
+          __hip_atomic_store(p, gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        else
+          __hip_atomic_store(p, gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    } else {
     const unsigned h2 = row_from_upper<2>(hb), h3 = row_from_upper<3>(hb);
     const unsigned h0t = bf_with_lsb(h, tag_bit(s));
     if ((unit & 3) == 0) {
@@ -495,6 +597,7 @@ __global__ void __launch_bounds__(64 * NSW + R * XU) lstm_fwd_xg(
         __hip_atomic_store(p, gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       else        // write-through (sc1) 8-B store
         __hip_atomic_store(p, gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     }
     if (cw == 0 && lane == 0 && tr && s < XG_TR_STEPS)
       tr[((long long)blockIdx.x * XG_TR_STEPS + s) * XG_TR_K + 3] = __builtin_amdgcn_s_memrealtime();
@@ -925,8 +1028,16 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
 //     block's 4 XB rows of W_hh) -> write-through granules.
 // A fragments (VGPRs): A[m][k] = W_hh[gaterow(k)][m] for output unit m (M block
 // mb = mw + (XB / 4) i) and local gate row k in [0, 4 XB): gate k / XB, unit u0 + k % XB.
+//
+// F32 (reference-precision configs; XB = 16, f32 activations, f32 dG): the
+// partials of dh travel as f32 pairs (pg[par][grp][producer][row][H/2] u64 =
+// {partial(2p) with the tag in its LSB, partial(2p + 1)}), dG sits in LDS as
+// f32 and the MFMA waves run v_mfma_f32_16x16x4_f32 over 16 k-steps; lane
+// group kq takes gate kq's 16 units in order (k = 16 kq + k-step), so its B
+// operand is four 16-B LDS reads of one dG row and its A fragments are
+// W_hh[kq H + u0 + k-step][m].
 // ---------------------------------------------------------------------------
-template <int R, int MB, bool AH, int XB>
+template <int R, int MB, bool AH, int XB, bool F32 = false>
 __global__ void __launch_bounds__(256 + R * XB + 16 * XB) lstm_bwd_xg(
     int B, int T, int H, const int32_t* __restrict__ lens, const float* __restrict__ whh_f,
     const float* __restrict__ whh_r, const float* __restrict__ dy, float* __restrict__ act_dg,
@@ -934,14 +1045,17 @@ __global__ void __launch_bounds__(256 + R * XB + 16 * XB) lstm_bwd_xg(
     uint16_t* __restrict__ dgbf, float* __restrict__ dbpart, unsigned epoch, int allow_local,
     int dg_f32, int io_pos, int dg_st16, const h16x4* __restrict__ acth,
     const int* __restrict__ dyflag, int dyc0, int dyepoch) {
-  constexpr int SQ = XB / 8;           // 16-B loads (8 units) per row of a producer's slice
+  static_assert(!F32 || (XB == 16 && !AH), "f32 backward: 16 units, f32 activations");
+  constexpr int UPL = F32 ? 4 : 8;     // units per 16-B load
+  constexpr int SQ = XB / UPL;         // 16-B loads per row of a producer's slice
   constexpr int LPS = R * SQ;          // sweeper lanes per producer subset
   constexpr int NPG = 256 / LPS;       // producer subsets swept in parallel
-  constexpr int NKS = XB / 8;          // MFMA k-steps: 4 gates x XB units / 32
+  constexpr int NKS = F32 ? 16 : XB / 8;   // MFMA k-steps: 4 gates x XB units / (4 or 32)
   constexpr int NMW = XB / 4;          // MFMA waves (8 at XB = 32: 64 fragment VGPRs each)
+  typedef typename std::conditional<F32, float, uint16_t>::type dgt_t;
   // row pitch XB + 4: a sweeper lane's 8 partial sums are two 16-B stores
   __shared__ __attribute__((aligned(16))) float red[NPG][R][XB + 4];
-  __shared__ __attribute__((aligned(16))) uint16_t dgt[16][4 * XB + 8];
+  __shared__ __attribute__((aligned(16))) dgt_t dgt[16][4 * XB + (F32 ? 4 : 8)];
   __shared__ int s_dead;
   __shared__ int s_pl[4];
   int* abortw = hdr;
@@ -958,17 +1072,17 @@ __global__ void __launch_bounds__(256 + R * XB + 16 * XB) lstm_bwd_xg(
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int HB = H / 16;                 // output M blocks
   const int H4 = 4 * H;
-  const int hq = H / 4;                  // granules per producer row
+  const int hq = F32 ? H / 2 : H / 4;    // granules per producer row
   const unsigned pg_bytes = (unsigned)(2ull * G * WPG * R * hq * 8);
   const __amdgpu_buffer_rsrc_t rs = xg_rsrc(pg, pg_bytes);
   unsigned long long* tr = blockIdx.x < XG_TR_WG ? g_xg_trace : nullptr;
-  for (int e = tid; e < 16 * (4 * XB + 8); e += blockDim.x) (&dgt[0][0])[e] = 0;
+  for (int e = tid; e < (int)(sizeof(dgt) / sizeof(dgt_t)); e += blockDim.x) (&dgt[0][0])[e] = 0;
   const int NCW = R * XB / 64;                // cell waves: 4 .. 4 + NCW - 1; MFMA waves after
 
   if (wave < 4) {
     // ------------------------------ sweeper -------------------------------
     const int sl = tid & (LPS - 1);
-    const int srow = sl / SQ, sq = sl % SQ;   // row, units 8 sq .. 8 sq + 7
+    const int srow = sl / SQ, sq = sl % SQ;   // row, units UPL sq .. UPL (sq + 1) - 1
     const int pgi = tid / LPS;
     // producers per sweeper lane (WPG = H / XB <= 16 NMW MB / XB = 4 MB)
     constexpr int NLD = (4 * MB + NPG - 1) / NPG;
@@ -1020,7 +1134,7 @@ __global__ void __launch_bounds__(256 + R * XB + 16 * XB) lstm_bwd_xg(
             const int w = pgi + l * NPG;
             // two granules = this block's units 8 sq .. 8 sq + 7 from producer w
             const unsigned off =
-                w < WPG ? (unsigned)((((base + w) * R + srow) * (long long)hq + (u0 >> 2) + 2 * sq) * 8)
+                w < WPG ? (unsigned)((((base + w) * R + srow) * (long long)hq + u0 / (UPL / 2) + 2 * sq) * 8)
                         : 0x7ffffff0u;
             vv[l] = ld_sc1(rs, off);
           }
@@ -1030,8 +1144,12 @@ __global__ void __launch_bounds__(256 + R * XB + 16 * XB) lstm_bwd_xg(
             ok &= (int)(pgi + l * NPG >= WPG) | (int)((((v[0] ^ ebit) | (v[2] ^ ebit)) & 1u) == 0u);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              sm[2 * e] += bf2f((uint16_t)(v[e] & 0xffffu));
-              sm[2 * e + 1] += bf2f((uint16_t)(v[e] >> 16));
+              if constexpr (F32) {
+                sm[e] += __uint_as_float(v[e]);
+              } else {
+                sm[2 * e] += bf2f((uint16_t)(v[e] & 0xffffu));
+                sm[2 * e + 1] += bf2f((uint16_t)(v[e] >> 16));
+              }
             }
           }
           if (__all(ok)) {
@@ -1049,8 +1167,8 @@ __global__ void __launch_bounds__(256 + R * XB + 16 * XB) lstm_bwd_xg(
           }
         }
 #pragma unroll
-        for (int e = 0; e < 8; e += 4)
-          *reinterpret_cast<f32x4*>(&red[pgi][srow][8 * sq + e]) =
+        for (int e = 0; e < UPL; e += 4)
+          *reinterpret_cast<f32x4*>(&red[pgi][srow][UPL * sq + e]) =
               f32x4{sm[e], sm[e + 1], sm[e + 2], sm[e + 3]};
       }
       if (dyw) {   // chunk dyk + 1 (one step may cross at most one boundary)
@@ -1140,7 +1258,7 @@ __global__ void __launch_bounds__(256 + R * XB + 16 * XB) lstm_bwd_xg(
     // gates x 2 halves of 8 units -- instead of four 2-B stores per (row, unit)
     // lane on every cell wave (dg_st16; ASR_XG_DG_ST16=0: the per-lane stores).
     const int srow = ct / (4 * SQ), sg = (ct / SQ) & 3, sh = ct % SQ;
-    const bool st16 = dg_st16 && dgbf && ct < 4 * SQ * R && b0 + srow < B;
+    const bool st16 = !F32 && dg_st16 && dgbf && ct < 4 * SQ * R && b0 + srow < B;
     auto step_io = [&](int q, int t, float d_i, float d_f, float d_g, float d_o, uint16_t bi,
                        uint16_t bff, uint16_t bg, uint16_t bo) {
       if (own) {
@@ -1158,10 +1276,12 @@ __global__ void __launch_bounds__(256 + R * XB + 16 * XB) lstm_bwd_xg(
           dgbf[gb + 3 * H] = bo;
         }
       }
-      if (st16) {
-        const uint4 v = *reinterpret_cast<const uint4*>(&dgt[srow][sg * XB + 8 * sh]);
-        *reinterpret_cast<uint4*>(dgbf + ((long long)(b0 + srow) * T + t) * 8 * H +
-                                  (long long)dir * H4 + (long long)sg * H + u0 + 8 * sh) = v;
+      if constexpr (!F32) {
+        if (st16) {
+          const uint4 v = *reinterpret_cast<const uint4*>(&dgt[srow][sg * XB + 8 * sh]);
+          *reinterpret_cast<uint4*>(dgbf + ((long long)(b0 + srow) * T + t) * 8 * H +
+                                    (long long)dir * H4 + (long long)sg * H + u0 + 8 * sh) = v;
+        }
       }
 #ifdef ASR_XG_DIAG_PREF1   // diagnostics build: inputs one step ahead, straight into place
       if (own && q + 1 < T) load_cell(q + 1, av, avh, cc, cp, dyv, &cp);
@@ -1244,10 +1364,17 @@ __global__ void __launch_bounds__(256 + R * XB + 16 * XB) lstm_bwd_xg(
       }
       if (dead) return;
       const uint16_t bi = f2bf(d_i), bff = f2bf(d_f), bg = f2bf(d_g), bo = f2bf(d_o);
-      dgt[row][unit] = bi;
-      dgt[row][XB + unit] = bff;
-      dgt[row][2 * XB + unit] = bg;
-      dgt[row][3 * XB + unit] = bo;
+      if constexpr (F32) {
+        dgt[row][unit] = d_i;
+        dgt[row][XB + unit] = d_f;
+        dgt[row][2 * XB + unit] = d_g;
+        dgt[row][3 * XB + unit] = d_o;
+      } else {
+        dgt[row][unit] = bi;
+        dgt[row][XB + unit] = bff;
+        dgt[row][2 * XB + unit] = bg;
+        dgt[row][3 * XB + unit] = bo;
+      }
 #ifndef ASR_XG_DIAG_PREF1
       // step q + 1's inputs (loaded two steps ahead)
 #pragma unroll
@@ -1277,6 +1404,71 @@ __global__ void __launch_bounds__(256 + R * XB + 16 * XB) lstm_bwd_xg(
   __builtin_amdgcn_s_setprio(2);
   const int mw = wave - 4 - NCW;         // 0 .. NMW - 1
   const int kq = lane >> 4, ln = lane & 15;
+  if constexpr (F32) {
+    // A[m][k] = W_hh[kq H + u0 + k-step][16 mb + ln]: lane group kq = gate kq
+    float wa[MB][NKS];
+    {
+      const float* W = dir ? whh_r : whh_f;
+#pragma unroll
+      for (int i = 0; i < MB; ++i) {
+        const int mb = min(mw + NMW * i, HB - 1);
+#pragma unroll
+        for (int kst = 0; kst < NKS; ++kst)
+          wa[i][kst] = W[(long long)(kq * H + u0 + kst) * H + 16 * mb + ln];
+      }
+    }
+    __syncthreads();  // B0
+    for (int q = 0; q < T; ++q) {
+      __syncthreads();  // B1
+      if (s_dead) return;
+      __syncthreads();  // B2
+      float bfk[NKS];   // B[k][n] = dG[row n][gate kq, unit k-step]
+#pragma unroll
+      for (int c = 0; c < NKS; c += 4) {
+        const f32x4 d = *reinterpret_cast<const f32x4*>(&dgt[ln][16 * kq + c]);
+        bfk[c] = d[0];
+        bfk[c + 1] = d[1];
+        bfk[c + 2] = d[2];
+        bfk[c + 3] = d[3];
+      }
+      const unsigned tb = tag_bit(q);
+      const long long obase = (((long long)(q & 1) * G + grp) * WPG + mem) * R;
+      f32x4 acc[MB];
+      auto mm = [&](int i) {
+        acc[i] = mfma_f32(wa[i][0], bfk[0], f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+        for (int kst = 1; kst < NKS; ++kst) acc[i] = mfma_f32(wa[i][kst], bfk[kst], acc[i]);
+      };
+      // two granules of (row ln, block mb): units 16 mb + 4 kq .. + 3
+      const unsigned off0 = (unsigned)(((obase + ln) * (long long)H + 16 * mw + 4 * kq) * 4);
+      auto publish = [&](auto aux) {
+        auto st = [&](int i) {
+          const int mb = mw + NMW * i;
+          if (ln < R && mb < HB) {
+            const u32x4 v = {(__float_as_uint(acc[i][0]) & ~1u) | tb, __float_as_uint(acc[i][1]),
+                             (__float_as_uint(acc[i][2]) & ~1u) | tb, __float_as_uint(acc[i][3])};
+            __builtin_amdgcn_raw_buffer_store_b128(v, rs, off0 + 64u * NMW * i, 0,
+                                                   decltype(aux)::value);
+          }
+        };
+        mm(0);
+#pragma unroll
+        for (int i = 1; i < MB; ++i) {
+          mm(i);
+          __builtin_amdgcn_sched_barrier(0);
+          st(i - 1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        st(MB - 1);
+      };
+      if (local)
+        publish(std::integral_constant<int, 0>());
+      else
+        publish(std::integral_constant<int, (int)AUX_SC1>());
+      __syncthreads();  // B3
+    }
+    return;
+  }
   bf16x8 wa[MB][NKS];
   {
     const float* W = dir ? whh_r : whh_f;
@@ -1446,6 +1638,109 @@ size_t lstm_xg_bwd_bytes(int B, int H) {
   if (!R) return 0;
   const long long rows = 2LL * ((B + R - 1) / R) * R;
   return XG_HDR + (size_t)2 * rows * (H / XU) * (H / 4) * 8;
+}
+
+// f32 granules: two values per 8 B (twice the bf16 footprint)
+size_t lstm_xg32_fwd_bytes(int B, int H) {
+  const size_t b = lstm_xg_fwd_bytes(B, H);
+  return b ? XG_HDR + 2 * (b - XG_HDR) : 0;
+}
+size_t lstm_xg32_bwd_bytes(int B, int H) {
+  const size_t b = lstm_xg_bwd_bytes(B, H);
+  return b ? XG_HDR + 2 * (b - XG_HDR) : 0;
+}
+
+// f32 shapes: H a multiple of 64 (16 K slices of whole 16-B polls) up to 512
+// forward, up to 384 backward (MB <= 6 M blocks per MFMA wave: 16 f32 A
+// fragments per block must stay in registers beside the other roles' waves).
+bool xg32_shape_ok(int H, bool backward) { return H % 64 == 0 && H <= (backward ? 384 : 512); }
+
+// Reference-precision (f32) forward: 1 launched / eligible (dry), 0 not, -1 error.
+int lstm_fwd_xg32_launch(int B, int T, int H, const int32_t* lens, const float* whh_f,
+                         const float* whh_r, float* gx_act, float* y, float* cst, void* ws,
+                         hipStream_t s, bool dry) {
+  if (!xg_enabled()) return 0;
+  const char* e = getenv("ASR_LSTM_XG32");
+  if (e && e[0] == '0') return 0;
+  const int R = xg_rows(B, H);
+  if (!R || !xg32_shape_ok(H, false)) return 0;
+  const int nl = H / 64;
+  const int grid = 2 * ((B + R - 1) / R) * (H / XU);
+  int* hdr = (int*)ws;
+  unsigned long long* g = (unsigned long long*)((char*)ws + XG_HDR);
+  const int al = xg_allow_local();
+#define ASR_XGF32(RR, NL)                                                                        \
+  do {                                                                                           \
+    if (!xg_fits(lstm_fwd_xg<RR, NL, 4, true>, 256 + RR * XU, XG_PIN_FWD)) return 0;              \
+    if (dry) return 1;                                                                           \
+    if (hipMemsetAsync(ws, 0, lstm_xg32_fwd_bytes(B, H), s) != hipSuccess) return -1;            \
+    xg_trace_setup(s);                                                                           \
+    hipLaunchKernelGGL((lstm_fwd_xg<RR, NL, 4, true>), dim3(grid), dim3(256 + RR * XU),          \
+                       XG_PIN_FWD, s, B, T, H, lens, whh_f, whh_r, gx_act, y, cst, g, hdr,       \
+                       (uint16_t*)nullptr, 0u, al);                                              \
+  } while (0)
+#define ASR_XGF32_N(RR)                   \
+  do {                                    \
+    switch (nl) {                         \
+      case 1: ASR_XGF32(RR, 1); break;    \
+      case 2: ASR_XGF32(RR, 2); break;    \
+      case 3: ASR_XGF32(RR, 3); break;    \
+      case 4: ASR_XGF32(RR, 4); break;    \
+      case 5: ASR_XGF32(RR, 5); break;    \
+      case 6: ASR_XGF32(RR, 6); break;    \
+      case 7: ASR_XGF32(RR, 7); break;    \
+      default: ASR_XGF32(RR, 8); break;   \
+    }                                     \
+  } while (0)
+  if (R == 8) ASR_XGF32_N(8);
+  else ASR_XGF32_N(16);
+#undef ASR_XGF32_N
+#undef ASR_XGF32
+  return hipGetLastError() == hipSuccess ? 1 : -1;
+}
+
+// Reference-precision (f32) backward: f32 dG in place of the activations,
+// per-utterance bias partials into dbpart (if given).
+int lstm_bwd_xg32_launch(int B, int T, int H, const int32_t* lens, const float* whh_f,
+                         const float* whh_r, const float* dy, float* act_dg, const float* cst,
+                         void* ws, float* dbpart, hipStream_t s, bool dry) {
+  if (!xg_enabled()) return 0;
+  const char* e = getenv("ASR_LSTM_XG32");
+  if (e && e[0] == '0') return 0;
+  const int R = xg_rows(B, H);
+  if (!R || !xg32_shape_ok(H, true)) return 0;
+  const int mb = (H / 16 + 3) / 4;
+  const int grid = 2 * ((B + R - 1) / R) * (H / 16);
+  int* hdr = (int*)ws;
+  unsigned long long* g = (unsigned long long*)((char*)ws + XG_HDR);
+  const unsigned ep = xg_bwd_seq(true);
+  const int al = xg_allow_local();
+  const size_t pin = XG_PIN_BWD;
+#define ASR_XGB32(RR, M)                                                                         \
+  do {                                                                                           \
+    if (!xg_fits(lstm_bwd_xg<RR, M, false, 16, true>, 256 + (RR + 16) * 16, pin)) return 0;      \
+    if (dry) return 1;                                                                           \
+    if (hipMemsetAsync(ws, 0, lstm_xg32_bwd_bytes(B, H), s) != hipSuccess) return -1;            \
+    xg_trace_setup(s);                                                                           \
+    hipLaunchKernelGGL((lstm_bwd_xg<RR, M, false, 16, true>), dim3(grid),                        \
+                       dim3(256 + (RR + 16) * 16), pin, s, B, T, H, lens, whh_f, whh_r, dy,     \
+                       act_dg, cst, g, hdr, (uint16_t*)nullptr, dbpart, ep, al, 1, 0, 0,        \
+                       (const h16x4*)nullptr, (const int*)nullptr, 0, 0);                        \
+  } while (0)
+#define ASR_XGB32_M(RR)                 \
+  do {                                  \
+    if (mb <= 1) ASR_XGB32(RR, 1);      \
+    else if (mb <= 2) ASR_XGB32(RR, 2); \
+    else if (mb <= 3) ASR_XGB32(RR, 3); \
+    else if (mb <= 4) ASR_XGB32(RR, 4); \
+    else if (mb <= 5) ASR_XGB32(RR, 5); \
+    else ASR_XGB32(RR, 6);              \
+  } while (0)
+  if (R == 8) ASR_XGB32_M(8);
+  else ASR_XGB32_M(16);
+#undef ASR_XGB32_M
+#undef ASR_XGB32
+  return hipGetLastError() == hipSuccess ? 1 : -1;
 }
 
 // Returns 1 if launched (or, with dry, if this shape/device can take the

@@ -271,6 +271,63 @@ def test_xg_local_and_write_through_agree_bitwise(B, H, cuda_dev, monkeypatch):
     ops.set_compute_dtype('fp32')
 
 
+@pytest.mark.parametrize('B,T,H', [(20, 37, 64), (7, 15, 320), (32, 120, 320), (28, 50, 256),
+                                   (64, 40, 320), (32, 60, 384), (16, 30, 512)])
+def test_f32_persistent_recurrence(B, T, H, cuda_dev, monkeypatch):
+    """fp32 mode: the tagged-granule recurrence at reference precision (f32
+    granules, f32 MFMA; lstm_fwd_xg / lstm_bwd_xg <F32>) against the per-step
+    f32 kernels (ASR_LSTM_XG32=0) and the fp32 torch-CPU oracle: outputs, input
+    grads and every weight grad within 1e-4 of the largest magnitude (the tag
+    bit perturbs one f32 ulp of every other hand-off value), padded frames
+    exactly zero; XCD-local and write-through hand-offs bitwise equal.  Ragged
+    lengths, B not a multiple of the row group, B = 64 (16-row groups), H = 512
+    (persistent forward, per-step backward)."""
+    ops = _ops()
+    ops.set_compute_dtype('fp32')
+    rng = np.random.RandomState(B * 1000 + H + 7)
+    Din = 40
+    lens = np.sort(rng.randint(1, T + 1, B))[::-1].astype(np.int32)
+    lens[0] = T
+    x = torch.from_numpy(rng.randn(B, T, Din).astype(np.float32))
+    ws = [torch.from_numpy(rng.uniform(-0.1, 0.1, s).astype(np.float32))
+          for s in ((8 * H, Din), (8 * H, H), (8 * H,), (8 * H,))]
+    R = torch.from_numpy(rng.randn(B, T, 2 * H).astype(np.float32)).to(cuda_dev)
+    res, modes = {}, {}
+    _persist_status()
+    for name, env in (('xg32', {}), ('xg32_sc1', {'ASR_XG_LOCAL': '0'}),
+                      ('step', {'ASR_LSTM_XG32': '0'})):
+        for k in ('ASR_LSTM_XG32', 'ASR_XG_LOCAL'):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        _xg_mode()
+        xd = x.to(cuda_dev).requires_grad_(True)
+        wd = [w.to(cuda_dev).requires_grad_(True) for w in ws]
+        y = ops.blstm_layer(xd, torch.from_numpy(lens).to(cuda_dev), T, *wd)
+        (y * R).sum().backward()
+        torch.cuda.synchronize()
+        modes[name] = _xg_mode()
+        res[name] = [y.detach().cpu().numpy(), xd.grad.cpu().numpy()] + \
+            [w.grad.cpu().numpy() for w in wd]
+        assert _persist_status() == 0, name
+    assert modes['step'] == 0 and modes['xg32'] != 0 and modes['xg32_sc1'] == 1, modes
+    H4 = 4 * H
+    ref_y = torch.cat([asr_ref.lstm_direction(x, lens, ws[0][:H4], ws[1][:H4], ws[2][:H4],
+                                              ws[3][:H4], False),
+                       asr_ref.lstm_direction(x, lens, ws[0][H4:], ws[1][H4:], ws[2][H4:],
+                                              ws[3][H4:], True)], dim=2).numpy()
+    err = np.abs(res['xg32'][0] - ref_y).max() / (np.abs(ref_y).max() + 1e-6)
+    assert err < 1e-4, ('y vs oracle', err)
+    names = ['y', 'dx', 'dW_ih', 'dW_hh', 'db_ih', 'db_hh']
+    for n, a, b in zip(names, res['xg32'], res['step']):
+        scale = np.abs(b).max() + 1e-6
+        assert np.abs(a - b).max() / scale < 1e-4, (n, np.abs(a - b).max(), scale)
+    for n, a, b in zip(names, res['xg32'], res['xg32_sc1']):
+        np.testing.assert_array_equal(a, b, err_msg=n)
+    for b in range(B):
+        assert not res['xg32'][0][b, lens[b]:].any()
+
+
 def _logical(store, trans, nrows, K, stride_t, stride_b=0, rows_per_b=0, t_add=0, t_limit=0):
     """Materialise the logical [nrows, K] operand of asr_gemm from its flat
     storage and row map (include/asr_hip.h): trans=0 -> element (i, k) at
