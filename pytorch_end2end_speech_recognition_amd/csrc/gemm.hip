@@ -750,6 +750,285 @@ __global__ void __launch_bounds__(NT) gemm_bf16_fast(Params P) {
   store_acc(pr, acc, tm, tn, wr, wc, lane, split, nsplit);
 }
 
+// ---------------------------------------------------------------------------
+// f32 fast path (reference precision): gemm_bf16_fast's structure -- LDS-DMA
+// staging (buffer_load ... lds, 16 B per lane), division-free per-slot row
+// state (taps included), double-buffered k-tiles -- with f32 elements (32-k
+// tiles) and v_mfma_f32_16x16x4_f32 (exact f32 products, f32 accumulate).
+// The generic register-staged kernel ran these products at 45-90 TF/s (157
+// peak).  Work-group tile (64 TMW) x (64 TNW), TMW TNW = 4 waves of 64 x 64:
+// 128 x 128, or 256 x 64 for N <= 64 (the 64-channel convolutions) and
+// 64 x 256 for M <= 64 (their weight gradients), so no tile is half empty.
+//   R mode (k contiguous): LDS [ROWS][32 k], 128-B rows; 16-B chunk c of row r
+//     at chunk c ^ ((r >> 1) & 7) (the bf16 image's swizzle).  A k extent that
+//     is not a multiple of 4 is allowed: the one 16-B chunk straddling the end
+//     of k (inside the row: rows are 16-B aligned and at least k long) has its
+//     elements past the end zeroed in LDS by the lane that loaded it, after
+//     its wait and before the barrier.
+//   K mode (rows contiguous): LDS [32 k-rows][ROWS], ROWS 4-B k-rows; 16-B
+//     chunk c of k-row k at chunk c ^ (4 ((k >> 3) & 3)).
+// k order inside a k-tile: at MFMA s (0..7) lane group g = lane >> 4 supplies
+// k = 8 g + s, so an R-mode fragment is two ds_read_b128 of one row and a
+// K-mode fragment eight ds_read_b32 down one column (the swizzle puts the four
+// lane groups' k-rows in different bank quarters).  Summation order differs
+// from gemm_kernel<false>; every product is still one f32 FMA into an f32 sum.
+// ---------------------------------------------------------------------------
+constexpr int FBK32 = 32;
+
+__device__ __forceinline__ int swz32(int k) { return ((k >> 3) & 3) << 2; }
+
+template <int NB>
+struct StageF32 {
+  int x[NB], y[NB], z[NB];
+  unsigned base[NB];
+  int valid;
+  int tmask, tn;   // R mode: slots whose chunk straddles the end of k, valid elements
+};
+
+template <int MODE, int ROWS>
+__device__ __forceinline__ void stagef32_init(const Operand& op, StageF32<ROWS / 32>& st,
+                                              int tile0, int nrows, int kbeg, int wave, int lane) {
+  constexpr int NB = ROWS / 32, KPD = 256 / ROWS, LPK = ROWS / 4;
+  st.valid = 0;
+  st.tmask = 0;
+  st.tn = 4;
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int blk = wave * NB + i;
+    if (MODE == 0) {
+      const int r = blk * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      const int row = tile0 + r, k = kbeg + 4 * c;
+      if (row < nrows) st.valid |= 1 << i;
+      if (op.tap_g) {
+        st.y[i] = k / op.tap_g;
+        st.x[i] = k - st.y[i] * op.tap_g;
+        st.z[i] = row;
+        st.base[i] = 0u;
+      } else {
+        const long long off = row < nrows ? row_off_np(op.map, row) : -1;
+        if (off < 0) st.valid &= ~(1 << i);
+        st.base[i] = off >= 0 ? (unsigned)(off * 4) : 0u;
+        st.x[i] = 4 * c;
+        st.y[i] = st.z[i] = 0;
+      }
+    } else {
+      const int kr = blk * KPD + lane / LPK;
+      const int c = (lane % LPK) ^ swz32(kr);
+      int col = tile0 + 4 * c, shift = 0;
+      if (op.tap_g) {
+        const int tap = col / op.tap_g;
+        col -= tap * op.tap_g;
+        shift = tap_shift(op, tap);
+      }
+      st.base[i] = (unsigned)(col * 4);
+      const int k = kbeg + kr;
+      if (op.plain) {
+        st.x[i] = k + shift;
+        st.y[i] = st.z[i] = 0;
+      } else {
+        st.z[i] = k / op.map.rows_per_b;
+        st.y[i] = k - st.z[i] * op.map.rows_per_b;
+        st.x[i] = 0;
+      }
+    }
+  }
+}
+
+template <int MODE, int ROWS>
+__device__ __forceinline__ void stagef32(const Operand& op, __amdgpu_buffer_rsrc_t rs,
+                                         StageF32<ROWS / 32>& st, char* lds_tile, int k0, int kend,
+                                         int wave, int lane) {
+  constexpr int NB = ROWS / 32, KPD = 256 / ROWS, LPK = ROWS / 4;
+  st.tmask = 0;
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int blk = wave * NB + i;
+    unsigned voff = OOB_OFF;
+    if (MODE == 0) {
+      const int r = blk * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      const int k = k0 + 4 * c;
+      bool on = false;
+      if (op.tap_g) {
+        const int rr = st.z[i] + tap_shift(op, st.y[i]);
+        on = ((st.valid >> i) & 1) && k < kend && rr >= 0 && rr < op.map.t_limit;
+        if (on) voff = (unsigned)(((long long)rr * op.map.stride_t + st.x[i]) * 4);
+        st.x[i] += FBK32;
+        while (st.x[i] >= op.tap_g) {
+          st.x[i] -= op.tap_g;
+          ++st.y[i];
+        }
+      } else if (((st.valid >> i) & 1) && k < kend) {
+        on = true;
+        voff = st.base[i] + (unsigned)(k * 4);
+      }
+      if (on && k + 4 > kend) {
+        st.tmask |= 1 << i;
+        st.tn = kend - k;
+      }
+    } else {
+      const int kr = blk * KPD + lane / LPK;
+      const int k = k0 + kr;
+      if (op.plain) {
+        const int rr = st.x[i];
+        if (k < kend && rr >= 0 && rr < op.map.t_limit)
+          voff = (unsigned)((long long)rr * op.map.stride_t * 4) + st.base[i];
+        st.x[i] += FBK32;
+      } else {
+        const int tp = st.y[i] * op.map.t_mul + op.map.t_add;
+        if (k < kend && tp >= 0 && tp < op.map.t_limit)
+          voff = (unsigned)(((long long)st.z[i] * op.map.stride_b +
+                             (long long)tp * op.map.stride_t) * 4) + st.base[i];
+        st.y[i] += FBK32;
+        while (st.y[i] >= op.map.rows_per_b) {
+          st.y[i] -= op.map.rows_per_b;
+          ++st.z[i];
+        }
+      }
+    }
+    const unsigned lds_addr = (unsigned)(uintptr_t)(lds_void_t*)(lds_tile + blk * 1024);
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(rs), "s"(lds_addr)
+        : "memory");
+  }
+}
+
+// After the wait for a tile's DMAs, before its barrier: zero the elements past
+// the end of k in this lane's straddling R-mode chunks (see above).
+template <int ROWS>
+__device__ __forceinline__ void tailfix32(const StageF32<ROWS / 32>& st, char* lds_tile, int wave,
+                                          int lane) {
+  constexpr int NB = ROWS / 32;
+  if (!st.tmask) return;
+#pragma unroll
+  for (int i = 0; i < NB; ++i)
+    if ((st.tmask >> i) & 1) {
+      float* p = (float*)(lds_tile + (wave * NB + i) * 1024 + lane * 16);
+      for (int e = st.tn; e < 4; ++e) p[e] = 0.f;
+    }
+}
+
+// The four k values 8 g + 4 h .. + 3 (g = lane >> 4) of tile row / column
+// rb + (lane & 15); ROWS: the tile's extent along the operand's outer dim.
+template <int MODE, int ROWS>
+__device__ __forceinline__ f32x4 frag_f32(const char* lds_tile, int rb, int h, int lane) {
+  const int g = lane >> 4;
+  if (MODE == 0) {
+    const int r = rb + (lane & 15);
+    const int c = (2 * g + h) ^ ((r >> 1) & 7);
+    return *(const f32x4*)(lds_tile + r * 128 + c * 16);
+  } else {
+    const int j = rb + (lane & 15);
+    const int cb = (((j >> 2) ^ (g << 2)) << 4) + 4 * (j & 3);
+    f32x4 v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      v[e] = *(const float*)(lds_tile + (8 * g + 4 * h + e) * (ROWS * 4) + cb);
+    return v;
+  }
+}
+
+template <int AMODE, int BMODE, int TMW>
+__global__ void __launch_bounds__(NT) gemm_f32_fast(Params P) {
+  constexpr int TNW = 4 / TMW, TM = 64 * TMW, TN = 64 * TNW;
+  constexpr int ATILE = TM * FBK32 * 4, STAGE = (TM + TN) * FBK32 * 4;
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // 2 stages x (A, B) tiles
+  const int zb = blockIdx.z / P.nprob, zp = blockIdx.z % P.nprob;
+  Problem pr = P.p[zp];
+  if (zb >= pr.batch) return;
+  if (zb > 0) {
+    pr.a.map.base = (const char*)pr.a.map.base + zb * pr.sA * 4;
+    pr.b.map.base = (const char*)pr.b.map.base + zb * pr.sB * 4;
+    pr.a.bytes -= zb * pr.sA * 4;
+    pr.b.bytes -= zb * pr.sB * 4;
+    pr.c.base = (const char*)pr.c.base + zb * pr.sC * 4;
+  }
+  const int gm = (pr.M + TM - 1) / TM, gn = (pr.N + TN - 1) / TN;
+  const int nwg = gm * gn;
+  const int nsplit = pr.ksplit > 1 ? pr.ksplit : 1;
+  const int ntot = nwg * nsplit;
+  int id = blockIdx.x;
+  if (id >= ntot) return;
+  {
+    const int q = ntot / 8, r = ntot % 8, x = id % 8;
+    id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + id / 8;
+  }
+  const int split = id / nwg;
+  id -= split * nwg;
+  int tm, tn;
+  {   // tile_coords with this kernel's tile extents
+    const int per = GM * gn;
+    const int g = id / per, r = id - g * per;
+    const int m0 = g * GM;
+    const int gs = min(GM, gm - m0);
+    tm = (m0 + r % gs) * TM;
+    tn = (r / gs) * TN;
+  }
+  const int kbeg = nsplit > 1 ? split * pr.kchunk : 0;
+  const int kend = nsplit > 1 ? min(pr.K, kbeg + pr.kchunk) : pr.K;
+
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = (w / TNW) * 64, wc = (w % TNW) * 64;
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc((void*)pr.a.map.base, 0, (int)pr.a.bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)pr.b.map.base, 0, (int)pr.b.bytes, 0x00020000);
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (kend - kbeg + FBK32 - 1) / FBK32;
+  StageF32<TM / 32> sa;
+  StageF32<TN / 32> sb;
+  stagef32_init<AMODE, TM>(pr.a, sa, tm, pr.M, kbeg, w, lane);
+  stagef32_init<BMODE, TN>(pr.b, sb, tn, pr.N, kbeg, w, lane);
+  stagef32<AMODE, TM>(pr.a, ra, sa, smem, kbeg, kend, w, lane);
+  stagef32<BMODE, TN>(pr.b, rb, sb, smem + ATILE, kbeg, kend, w, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (AMODE == 0) tailfix32<TM>(sa, smem, w, lane);
+  if (BMODE == 0) tailfix32<TN>(sb, smem + ATILE, w, lane);
+  __builtin_amdgcn_s_barrier();
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* cur = smem + (kt & 1) * STAGE;
+    char* nxt = smem + ((kt + 1) & 1) * STAGE;
+    if (kt + 1 < nk) {
+      const int k0 = kbeg + (kt + 1) * FBK32;
+      stagef32<AMODE, TM>(pr.a, ra, sa, nxt, k0, kend, w, lane);
+      stagef32<BMODE, TN>(pr.b, rb, sb, nxt + ATILE, k0, kend, w, lane);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      f32x4 fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = frag_f32<AMODE, TM>(cur, wr + 16 * i, h, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = frag_f32<BMODE, TN>(cur + ATILE, wc + 16 * j, h, lane);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma_f32(fa[i][e], fb[j][e], acc[i][j]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (kt + 1 < nk) {
+      if (AMODE == 0) tailfix32<TM>(sa, nxt, w, lane);
+      if (BMODE == 0) tailfix32<TN>(sb, nxt + ATILE, w, lane);
+    }
+    __builtin_amdgcn_s_barrier();
+  }
+  store_acc(pr, acc, tm, tn, wr, wc, lane, split, nsplit);
+}
+
 // 256 x 64 tiles for products with N <= 64 and B in R mode (B stored [N][K]:
 // the 3x3 convolutions of the 64-channel VGG layers, forward and input
 // gradient).  The 128 x 128 kernel computed those with half of every B tile
@@ -1906,6 +2185,36 @@ int fast_stages() {
   return n;
 }
 
+// The f32 fast path's operand mode pair, or -1 (gemm_kernel<false>).  Every
+// operand f32 with a known extent < 2 GiB, 16-B aligned rows, no batch
+// permutation and the division-free staging (taps only on a plain map).
+// ASR_GEMM_F32FAST=0 keeps the generic kernel.
+bool fast32_operand_ok(const asr_operand_t& o, const Operand& op, long long batch_stride,
+                       int batch, int kdim) {
+  if (o.dtype != ASR_DT_F32 || o.bytes <= 0 || o.bytes > 0x7fff0000LL) return false;
+  if (o.map.perm || !op.sf) return false;
+  if (!aligned16(o.ptr) || o.map.stride_t % 4 || o.map.stride_b % 4) return false;
+  if (batch > 1 && batch_stride % 4) return false;
+  (void)kdim;   // R mode: a k extent that is not a multiple of 4 is zero-filled in LDS
+  return true;
+}
+
+int fast32_modes(const asr_gemm_t* g, const Params& P) {
+  const char* e = getenv("ASR_GEMM_F32FAST");
+  if (e && e[0] == '0') return -1;
+  int modes = -1;
+  for (int i = 0; i < P.nprob; ++i) {
+    const Problem& p = P.p[i];
+    if (!fast32_operand_ok(g[i].a, p.a, p.sA, p.batch, p.K) ||
+        !fast32_operand_ok(g[i].b, p.b, p.sB, p.batch, p.K))
+      return -1;
+    const int m = 2 * (g[i].a.trans ? 1 : 0) + (g[i].b.trans ? 1 : 0);
+    if (modes >= 0 && m != modes) return -1;
+    modes = m;
+  }
+  return modes;
+}
+
 int fast_modes(const asr_gemm_t* g, const Params& P) {
   if (getenv("ASR_GEMM_FAST") && getenv("ASR_GEMM_FAST")[0] == '0') return -1;
   int modes = -1;
@@ -2212,6 +2521,34 @@ int gemm_launch_own(const asr_gemm_t* problems, int nprob, int compute_dtype, vo
     const size_t lds = 2 * BM * LDB16 * 2;
     prof_set_tag(ASR_PROF_GEMM, slot, 4 * ASR_PTAG_GEMM_GEN_BF16);
     hipLaunchKernelGGL(gemm_kernel<true>, grid, dim3(NT), lds, s, P);
+  } else if (const int f32m = fast32_modes(problems, P); f32m >= 0) {
+    // tile shape: 256 x 64 when every N <= 64, 64 x 256 when every M <= 64
+    bool n64 = true, m64 = true;
+    for (int i = 0; i < nprob; ++i) {
+      n64 &= problems[i].N <= 64;
+      m64 &= problems[i].M <= 64;
+    }
+    const int tmw = n64 ? 4 : m64 ? 1 : 2;
+    const int tmr = 64 * tmw, tnr = 256 / tmw;
+    int wg32 = 0;
+    for (int i = 0; i < nprob; ++i)
+      wg32 = max(wg32, ceil_div(P.p[i].M, tmr) * ceil_div(P.p[i].N, tnr) * max(1, P.p[i].ksplit));
+    const dim3 g32(wg32, 1, nprob * maxb);
+    const size_t lds = 2 * (size_t)(tmr + tnr) * FBK32 * 4;
+    prof_set_tag(ASR_PROF_GEMM, slot, 4 * ASR_PTAG_GEMM_F32F + f32m);
+#define ASR_F32F(A, B)                                                                           \
+  do {                                                                                           \
+    if (tmw == 4) hipLaunchKernelGGL((gemm_f32_fast<A, B, 4>), g32, dim3(NT), lds, s, P);         \
+    else if (tmw == 1) hipLaunchKernelGGL((gemm_f32_fast<A, B, 1>), g32, dim3(NT), lds, s, P);    \
+    else hipLaunchKernelGGL((gemm_f32_fast<A, B, 2>), g32, dim3(NT), lds, s, P);                  \
+  } while (0)
+    switch (f32m) {
+      case 0: ASR_F32F(0, 0); break;
+      case 1: ASR_F32F(0, 1); break;
+      case 2: ASR_F32F(1, 0); break;
+      default: ASR_F32F(1, 1); break;
+    }
+#undef ASR_F32F
   } else {
     const size_t lds = 2 * BM * LDF32 * 4;
     prof_set_tag(ASR_PROF_GEMM, slot, 4 * ASR_PTAG_GEMM_GEN_F32);

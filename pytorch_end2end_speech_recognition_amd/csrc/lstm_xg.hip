@@ -337,17 +337,17 @@ __device__ __forceinline__ void dec_tanh(float e, float& g, float& om2) { g = e;
 // four successive k-steps and the W_hh fragments are loaded in that same k
 // order.  KSW is then the number of 16-B polls per lane (H = 64 KSW, NSW = 4).
 // ---------------------------------------------------------------------------
-template <int R, int KSW, int NSW, bool F32 = false>
-__global__ void __launch_bounds__(64 * NSW + R * XU) lstm_fwd_xg(
+template <int R, int KSW, int NSW, bool F32 = false, int XUF = XU>
+__global__ void __launch_bounds__(64 * NSW + R * XUF) lstm_fwd_xg(
     int B, int T, int H, const int32_t* __restrict__ lens, const float* __restrict__ whh_f,
     const float* __restrict__ whh_r, float* __restrict__ gx_act, float* __restrict__ y,
     float* __restrict__ cst, unsigned long long* xg, int* hdr, uint16_t* __restrict__ ybf,
     unsigned epoch, int allow_local) {
-  __shared__ float part[2][NSW][R][4 * XU + 4];
+  __shared__ float part[2][NSW][R][4 * XUF + 4];
   __shared__ int s_dead;  // a sweeper gave up: every wave exits after the next barrier
   __shared__ int s_pl[4];
   int* abortw = hdr;
-  const int WPG = H / XU;
+  const int WPG = H / XUF;
   const int G = gridDim.x / WPG;
   if (threadIdx.x == 0) s_dead = 0;
   xg_place(WPG, allow_local, hdr, s_pl);
@@ -356,7 +356,7 @@ __global__ void __launch_bounds__(64 * NSW + R * XU) lstm_fwd_xg(
   const bool local = s_pl[2] != 0;
   (void)epoch;  // forward granules carry a 1-bit step tag (tag_bit) instead
   const int dir = grp & 1, rg = grp >> 1;
-  const int u0 = mem * XU, b0 = rg * R;
+  const int u0 = mem * XUF, b0 = rg * R;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nks = H >> 5;
@@ -370,16 +370,20 @@ __global__ void __launch_bounds__(64 * NSW + R * XU) lstm_fwd_xg(
       const int kq = lane >> 4, ln = lane & 15;
       const bool sweeper = ln < R;
       const int kb = (4 * wave + kq) * 4 * KSW;   // this lane group's first unit of K
-      // B fragments: B[k][n] = W_hh[g*H + u0 + n][kb + k-step], n = ln
-      float wf[4 * KSW][4];
+      // NBK blocks of 16 gate columns: column c = 16 blk + ln is gate c / XUF,
+      // unit u0 + c % XUF (XUF = 16: one gate per block; 8: two)
+      constexpr int NBK = XUF / 4;
+      // B fragments: B[k][n] = W_hh[gate row of column 16 blk + n][kb + k-step]
+      float wf[4 * KSW][NBK];
       {
         const float* W = dir ? whh_r : whh_f;
 #pragma unroll
-        for (int g = 0; g < 4; ++g)
+        for (int g = 0; g < NBK; ++g)
 #pragma unroll
           for (int i = 0; i < KSW; ++i) {
+            const int c = 16 * g + ln;
             const float4 w4 = *reinterpret_cast<const float4*>(
-                W + (long long)(g * H + u0 + ln) * H + kb + 4 * i);
+                W + (long long)((c / XUF) * H + u0 + c % XUF) * H + kb + 4 * i);
             wf[4 * i][g] = w4.x;
             wf[4 * i + 1][g] = w4.y;
             wf[4 * i + 2][g] = w4.z;
@@ -391,9 +395,9 @@ __global__ void __launch_bounds__(64 * NSW + R * XU) lstm_fwd_xg(
       const int ndelay = __builtin_amdgcn_readfirstlane(g_xg_delay);
       for (int s = 0; s < T; ++s) {
         XG_TR(s, 0, __builtin_amdgcn_s_memrealtime());
-        f32x4 acc[4];
+        f32x4 acc[NBK];
 #pragma unroll
-        for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int g = 0; g < NBK; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
         if (s > 0) {
           const unsigned ebit = tag_bit(s - 1);
           const unsigned rowoff =
@@ -426,14 +430,14 @@ __global__ void __launch_bounds__(64 * NSW + R * XU) lstm_fwd_xg(
             for (int e = 0; e < 4; ++e) {
               const float a = sweeper ? __uint_as_float(v[i][e]) : 0.f;
 #pragma unroll
-              for (int g = 0; g < 4; ++g) acc[g] = mfma_f32(a, wf[4 * i + e][g], acc[g]);
+              for (int g = 0; g < NBK; ++g) acc[g] = mfma_f32(a, wf[4 * i + e][g], acc[g]);
             }
         }
         if (4 * kq < R) {
 #pragma unroll
-          for (int g = 0; g < 4; ++g)
+          for (int g = 0; g < NBK; ++g)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) part[s & 1][wave][4 * kq + r][g * XU + ln] = acc[g][r];
+            for (int r = 0; r < 4; ++r) part[s & 1][wave][4 * kq + r][16 * g + ln] = acc[g][r];
         }
         __syncthreads();  // B(s)
         if (s_dead) return;
@@ -514,7 +518,7 @@ __global__ void __launch_bounds__(64 * NSW + R * XU) lstm_fwd_xg(
 #pragma unroll
         for (int g = 0; g < 4; ++g)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) part[s & 1][wave][4 * kq + r][g * XU + ln] = acc[g][r];
+          for (int r = 0; r < 4; ++r) part[s & 1][wave][4 * kq + r][g * XUF + ln] = acc[g][r];
       }
       XG_TR(s, 4, __builtin_amdgcn_s_memrealtime());
       __syncthreads();  // B(s): partial sums in LDS
@@ -530,7 +534,8 @@ __global__ void __launch_bounds__(64 * NSW + R * XU) lstm_fwd_xg(
 
   // -------------------------------- cell ----------------------------------
   const int ct = tid - 64 * NSW;
-  const int row = ct >> 4, unit = ct & 15;
+  static_assert(XUF == 16 || XUF == 8, "units per work-group");
+  const int row = ct >> (XUF == 16 ? 4 : 3), unit = ct & (XUF - 1);
   const int b = b0 + row, j = u0 + unit;
   const bool own = b < B;
   const int len = own ? lens[b] : 0;
@@ -556,7 +561,7 @@ __global__ void __launch_bounds__(64 * NSW + R * XU) lstm_fwd_xg(
       float pre[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int col = q * XU + unit;
+        const int col = q * XUF + unit;
         float a = part[s & 1][0][row][col];
 #pragma unroll
         for (int w = 1; w < NSW; ++w) a += part[s & 1][w][row][col];
@@ -1038,20 +1043,23 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
 // W_hh[kq H + u0 + k-step][m].
 // ---------------------------------------------------------------------------
 template <int R, int MB, bool AH, int XB, bool F32 = false>
-__global__ void __launch_bounds__(256 + R * XB + 16 * XB) lstm_bwd_xg(
+__global__ void __launch_bounds__(256 + R * XB + 64 * (F32 ? 4 : XB / 4)) lstm_bwd_xg(
     int B, int T, int H, const int32_t* __restrict__ lens, const float* __restrict__ whh_f,
     const float* __restrict__ whh_r, const float* __restrict__ dy, float* __restrict__ act_dg,
     const float* __restrict__ cst, unsigned long long* pg, int* hdr,
     uint16_t* __restrict__ dgbf, float* __restrict__ dbpart, unsigned epoch, int allow_local,
     int dg_f32, int io_pos, int dg_st16, const h16x4* __restrict__ acth,
     const int* __restrict__ dyflag, int dyc0, int dyepoch) {
-  static_assert(!F32 || (XB == 16 && !AH), "f32 backward: 16 units, f32 activations");
+  static_assert(!F32 || ((XB == 16 || XB == 8) && !AH), "f32 backward: 8 or 16 units, f32 activations");
   constexpr int UPL = F32 ? 4 : 8;     // units per 16-B load
   constexpr int SQ = XB / UPL;         // 16-B loads per row of a producer's slice
   constexpr int LPS = R * SQ;          // sweeper lanes per producer subset
   constexpr int NPG = 256 / LPS;       // producer subsets swept in parallel
-  constexpr int NKS = F32 ? 16 : XB / 8;   // MFMA k-steps: 4 gates x XB units / (4 or 32)
-  constexpr int NMW = XB / 4;          // MFMA waves (8 at XB = 32: 64 fragment VGPRs each)
+  constexpr int NKS = F32 ? XB : XB / 8;   // MFMA k-steps: 4 gates x XB units / (4 or 32)
+  // MFMA waves (bf16: XB / 4, 8 at XB = 32 with 64 fragment VGPRs each; f32: 4,
+  // one per SIMD, whatever XB)
+  constexpr int NMW = F32 ? 4 : XB / 4;
+  constexpr int WPGMAX = 16 * NMW * MB / XB;   // producers: H / XB <= 16 NMW MB / XB
   typedef typename std::conditional<F32, float, uint16_t>::type dgt_t;
   // row pitch XB + 4: a sweeper lane's 8 partial sums are two 16-B stores
   __shared__ __attribute__((aligned(16))) float red[NPG][R][XB + 4];
@@ -1084,8 +1092,8 @@ __global__ void __launch_bounds__(256 + R * XB + 16 * XB) lstm_bwd_xg(
     const int sl = tid & (LPS - 1);
     const int srow = sl / SQ, sq = sl % SQ;   // row, units UPL sq .. UPL (sq + 1) - 1
     const int pgi = tid / LPS;
-    // producers per sweeper lane (WPG = H / XB <= 16 NMW MB / XB = 4 MB)
-    constexpr int NLD = (4 * MB + NPG - 1) / NPG;
+    // producers per sweeper lane
+    constexpr int NLD = (WPGMAX + NPG - 1) / NPG;
     unsigned* dspin = g_xg_dbg_spins;
     const int nsleep = __builtin_amdgcn_readfirstlane(g_xg_sleep);
     const int ndelay = __builtin_amdgcn_readfirstlane(g_xg_delay);
@@ -1425,7 +1433,7 @@ __global__ void __launch_bounds__(256 + R * XB + 16 * XB) lstm_bwd_xg(
       float bfk[NKS];   // B[k][n] = dG[row n][gate kq, unit k-step]
 #pragma unroll
       for (int c = 0; c < NKS; c += 4) {
-        const f32x4 d = *reinterpret_cast<const f32x4*>(&dgt[ln][16 * kq + c]);
+        const f32x4 d = *reinterpret_cast<const f32x4*>(&dgt[ln][XB * kq + c]);
         bfk[c] = d[0];
         bfk[c + 1] = d[1];
         bfk[c + 2] = d[2];
@@ -1640,14 +1648,30 @@ size_t lstm_xg_bwd_bytes(int B, int H) {
   return XG_HDR + (size_t)2 * rows * (H / XU) * (H / 4) * 8;
 }
 
-// f32 granules: two values per 8 B (twice the bf16 footprint)
+// f32 layouts.  With 16-row groups the f32 MFMA's 16 columns are all real
+// rows (8-row groups multiply 8 zero rows), so where the chip holds the grid
+// at 8 units per work-group (twice the work-groups of 16 units, half the
+// groups of 8 rows) the f32 kernels take 16 rows x 8 units: half the MFMAs
+// per work-group per step on as many CUs.  ASR_XG32_XU=16 keeps 16 units.
+int xg32_units(int B, int H) {
+  const char* e = getenv("ASR_XG32_XU");
+  if (e && atoi(e) == 16) return 16;
+  if (H % 64 != 0 || H / 8 > 64) return 16;
+  const int G = 2 * ((B + 15) / 16);
+  return G * (H / 8) <= xg_num_cus() ? 8 : 16;
+}
+int xg32_rows(int B, int H) { return xg32_units(B, H) == 8 ? 16 : xg_rows(B, H); }
+
+// f32 granules: two values per 8 B; rows rounded up to 16 covers every layout
 size_t lstm_xg32_fwd_bytes(int B, int H) {
-  const size_t b = lstm_xg_fwd_bytes(B, H);
-  return b ? XG_HDR + 2 * (b - XG_HDR) : 0;
+  if (!xg_rows(B, H)) return 0;
+  const long long rows = 2LL * ((B + 15) / 16) * 16;
+  return XG_HDR + (size_t)2 * rows * H * 4;
 }
 size_t lstm_xg32_bwd_bytes(int B, int H) {
-  const size_t b = lstm_xg_bwd_bytes(B, H);
-  return b ? XG_HDR + 2 * (b - XG_HDR) : 0;
+  if (!xg_rows(B, H)) return 0;
+  const long long rows = 2LL * ((B + 15) / 16) * 16;
+  return XG_HDR + (size_t)2 * rows * (H / 8) * H * 4;
 }
 
 // f32 shapes: H a multiple of 64 (16 K slices of whole 16-B polls) up to 512
@@ -1662,38 +1686,40 @@ int lstm_fwd_xg32_launch(int B, int T, int H, const int32_t* lens, const float* 
   if (!xg_enabled()) return 0;
   const char* e = getenv("ASR_LSTM_XG32");
   if (e && e[0] == '0') return 0;
-  const int R = xg_rows(B, H);
-  if (!R || !xg32_shape_ok(H, false)) return 0;
+  if (!xg_rows(B, H) || !xg32_shape_ok(H, false)) return 0;
+  const int xu = xg32_units(B, H);
+  const int R = xg32_rows(B, H);
   const int nl = H / 64;
-  const int grid = 2 * ((B + R - 1) / R) * (H / XU);
+  const int grid = 2 * ((B + R - 1) / R) * (H / xu);
   int* hdr = (int*)ws;
   unsigned long long* g = (unsigned long long*)((char*)ws + XG_HDR);
   const int al = xg_allow_local();
-#define ASR_XGF32(RR, NL)                                                                        \
+#define ASR_XGF32(RR, NL, XV)                                                                    \
   do {                                                                                           \
-    if (!xg_fits(lstm_fwd_xg<RR, NL, 4, true>, 256 + RR * XU, XG_PIN_FWD)) return 0;              \
+    if (!xg_fits(lstm_fwd_xg<RR, NL, 4, true, XV>, 256 + RR * XV, XG_PIN_FWD)) return 0;          \
     if (dry) return 1;                                                                           \
     if (hipMemsetAsync(ws, 0, lstm_xg32_fwd_bytes(B, H), s) != hipSuccess) return -1;            \
     xg_trace_setup(s);                                                                           \
-    hipLaunchKernelGGL((lstm_fwd_xg<RR, NL, 4, true>), dim3(grid), dim3(256 + RR * XU),          \
+    hipLaunchKernelGGL((lstm_fwd_xg<RR, NL, 4, true, XV>), dim3(grid), dim3(256 + RR * XV),      \
                        XG_PIN_FWD, s, B, T, H, lens, whh_f, whh_r, gx_act, y, cst, g, hdr,       \
                        (uint16_t*)nullptr, 0u, al);                                              \
   } while (0)
-#define ASR_XGF32_N(RR)                   \
-  do {                                    \
-    switch (nl) {                         \
-      case 1: ASR_XGF32(RR, 1); break;    \
-      case 2: ASR_XGF32(RR, 2); break;    \
-      case 3: ASR_XGF32(RR, 3); break;    \
-      case 4: ASR_XGF32(RR, 4); break;    \
-      case 5: ASR_XGF32(RR, 5); break;    \
-      case 6: ASR_XGF32(RR, 6); break;    \
-      case 7: ASR_XGF32(RR, 7); break;    \
-      default: ASR_XGF32(RR, 8); break;   \
-    }                                     \
+#define ASR_XGF32_N(RR, XV)                   \
+  do {                                        \
+    switch (nl) {                             \
+      case 1: ASR_XGF32(RR, 1, XV); break;    \
+      case 2: ASR_XGF32(RR, 2, XV); break;    \
+      case 3: ASR_XGF32(RR, 3, XV); break;    \
+      case 4: ASR_XGF32(RR, 4, XV); break;    \
+      case 5: ASR_XGF32(RR, 5, XV); break;    \
+      case 6: ASR_XGF32(RR, 6, XV); break;    \
+      case 7: ASR_XGF32(RR, 7, XV); break;    \
+      default: ASR_XGF32(RR, 8, XV); break;   \
+    }                                         \
   } while (0)
-  if (R == 8) ASR_XGF32_N(8);
-  else ASR_XGF32_N(16);
+  if (xu == 8) ASR_XGF32_N(16, 8);
+  else if (R == 8) ASR_XGF32_N(8, 16);
+  else ASR_XGF32_N(16, 16);
 #undef ASR_XGF32_N
 #undef ASR_XGF32
   return hipGetLastError() == hipSuccess ? 1 : -1;
@@ -1707,41 +1733,44 @@ int lstm_bwd_xg32_launch(int B, int T, int H, const int32_t* lens, const float* 
   if (!xg_enabled()) return 0;
   const char* e = getenv("ASR_LSTM_XG32");
   if (e && e[0] == '0') return 0;
-  const int R = xg_rows(B, H);
-  if (!R || !xg32_shape_ok(H, true)) return 0;
+  if (!xg_rows(B, H) || !xg32_shape_ok(H, true)) return 0;
+  const int xb = xg32_units(B, H);
+  const int R = xg32_rows(B, H);
   const int mb = (H / 16 + 3) / 4;
-  const int grid = 2 * ((B + R - 1) / R) * (H / 16);
+  const int grid = 2 * ((B + R - 1) / R) * (H / xb);
   int* hdr = (int*)ws;
   unsigned long long* g = (unsigned long long*)((char*)ws + XG_HDR);
   const unsigned ep = xg_bwd_seq(true);
   const int al = xg_allow_local();
   const size_t pin = XG_PIN_BWD;
-#define ASR_XGB32(RR, M)                                                                         \
+#define ASR_XGB32(RR, M, XV)                                                                     \
   do {                                                                                           \
-    if (!xg_fits(lstm_bwd_xg<RR, M, false, 16, true>, 256 + (RR + 16) * 16, pin)) return 0;      \
+    if (!xg_fits(lstm_bwd_xg<RR, M, false, XV, true>, 256 + RR * XV + 256, pin)) return 0;       \
     if (dry) return 1;                                                                           \
     if (hipMemsetAsync(ws, 0, lstm_xg32_bwd_bytes(B, H), s) != hipSuccess) return -1;            \
     xg_trace_setup(s);                                                                           \
-    hipLaunchKernelGGL((lstm_bwd_xg<RR, M, false, 16, true>), dim3(grid),                        \
-                       dim3(256 + (RR + 16) * 16), pin, s, B, T, H, lens, whh_f, whh_r, dy,     \
+    hipLaunchKernelGGL((lstm_bwd_xg<RR, M, false, XV, true>), dim3(grid),                        \
+                       dim3(256 + RR * XV + 256), pin, s, B, T, H, lens, whh_f, whh_r, dy,      \
                        act_dg, cst, g, hdr, (uint16_t*)nullptr, dbpart, ep, al, 1, 0, 0,        \
                        (const h16x4*)nullptr, (const int*)nullptr, 0, 0);                        \
   } while (0)
-#define ASR_XGB32_M(RR)                 \
-  do {                                  \
-    if (mb <= 1) ASR_XGB32(RR, 1);      \
-    else if (mb <= 2) ASR_XGB32(RR, 2); \
-    else if (mb <= 3) ASR_XGB32(RR, 3); \
-    else if (mb <= 4) ASR_XGB32(RR, 4); \
-    else if (mb <= 5) ASR_XGB32(RR, 5); \
-    else ASR_XGB32(RR, 6);              \
+#define ASR_XGB32_M(RR, XV)                 \
+  do {                                      \
+    if (mb <= 1) ASR_XGB32(RR, 1, XV);      \
+    else if (mb <= 2) ASR_XGB32(RR, 2, XV); \
+    else if (mb <= 3) ASR_XGB32(RR, 3, XV); \
+    else if (mb <= 4) ASR_XGB32(RR, 4, XV); \
+    else if (mb <= 5) ASR_XGB32(RR, 5, XV); \
+    else ASR_XGB32(RR, 6, XV);              \
   } while (0)
-  if (R == 8) ASR_XGB32_M(8);
-  else ASR_XGB32_M(16);
+  if (xb == 8) ASR_XGB32_M(16, 8);
+  else if (R == 8) ASR_XGB32_M(8, 16);
+  else ASR_XGB32_M(16, 16);
 #undef ASR_XGB32_M
 #undef ASR_XGB32
   return hipGetLastError() == hipSuccess ? 1 : -1;
 }
+
 
 // Returns 1 if launched (or, with dry, if this shape/device can take the
 // path), 0 if not eligible, -1 on a launch error.  ws must hold

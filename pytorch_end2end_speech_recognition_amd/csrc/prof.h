@@ -28,6 +28,7 @@
 #define ASR_PTAG_CONV_TR 9        /* modes: 0 */
 #define ASR_PTAG_CONV_TR_WGRAD 10
 #define ASR_PTAG_CONV_C1_WGRAD 11
+#define ASR_PTAG_GEMM_F32F 12      /* gemm_f32_fast<a, b> */
 #define ASR_PTAG_LSTM_FWD_XG 1
 #define ASR_PTAG_LSTM_FWD_XGX 2
 #define ASR_PTAG_LSTM_BWD_XG 3

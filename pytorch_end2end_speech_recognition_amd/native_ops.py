@@ -430,6 +430,83 @@ class LinearCTCFn(torch.autograd.Function):
         return (dx,) + (None,) * 10
 
 
+class LinearCTC32Fn(torch.autograd.Function):
+    """The CTC output layer and its loss as one op at reference precision (fp32
+    mode; LinearND + CTC, ctc.py:30-52 with linear.py:32-47): the logits are
+    written with a row pitch of V rounded up to 4 columns, and the CTC
+    gradient with the same pitch, so the three products (logits, dX, dW) get
+    16-B aligned rows and run on the f32 fast kernel (gemm_f32_fast) instead of
+    the generic one (an unpadded 10001-column row is not 16-B aligned; the
+    fast kernel zero-fills the k tail of the dX product in LDS).  Values equal
+    ctc_loss(linear(...))'s up to the summation order of the products."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, drop, labels_flat, label_lens, act_lens, max_label_len,
+                loss_scale, blank, zero_infinity):
+        N.require_device(x, weight, labels_flat, label_lens, act_lens)
+        x = x.contiguous()
+        B, T, K = x.shape
+        V = weight.shape[0]
+        Vp = (V + 3) // 4 * 4
+        dev = x.device
+        if drop is not None:   # materialise dropout(x); the dX epilogue applies the mask
+            xd = torch.empty_like(x)
+            N.call('asr_dropout', N.ptr(x), N.ptr(xd), x.numel(), float(drop[0]), int(drop[1]),
+                   N.stream_handle(dev))
+            x = xd
+        logits = torch.empty(B * T, Vp, dtype=torch.float32, device=dev)
+        if B * T > 0:
+            run_gemm([gemm_problem(operand(x, 0, rowmap(K)), operand(weight, 0, rowmap(K)),
+                                   logits, rowmap(Vp), B * T, V, K, bias=bias)], dev)
+        nbytes = N.query('asr_ctc_workspace_bytes', T, B, V, max_label_len)
+        ws = _ws(nbytes, dev)
+        costs = torch.empty(B, dtype=torch.float32, device=dev)
+        loss = torch.empty(1, dtype=torch.float32, device=dev)
+        N.call('asr_ctc_forward', N.ptr(logits), Vp, T * Vp, T, B, V, N.ptr(labels_flat),
+               N.ptr(label_lens), N.ptr(act_lens), int(max_label_len), int(blank),
+               int(bool(zero_infinity)), N.ptr(costs), N.ptr(loss), float(loss_scale), N.ptr(ws),
+               nbytes, N.stream_handle(dev))
+        ctx.save_for_backward(x, logits, labels_flat, label_lens, act_lens, ws)
+        ctx.meta = (bias, weight, B, T, V, Vp, int(max_label_len), int(blank), float(loss_scale),
+                    nbytes)
+        ctx.from_blstm = _produced_by_blstm(x)
+        ctx.drop = drop
+        ctx.mark_non_differentiable(costs)
+        return loss, costs
+
+    @staticmethod
+    def backward(ctx, g_loss, g_costs):
+        x, logits, labels_flat, label_lens, act_lens, ws = ctx.saved_tensors
+        bias, weight, B, T, V, Vp, max_label_len, blank, loss_scale, nbytes = ctx.meta
+        dev = logits.device
+        K = x.shape[-1]
+        M = B * T
+        dl = torch.empty(M, Vp, dtype=torch.float32, device=dev)
+        g = g_loss.contiguous() if g_loss is not None else None
+        N.call('asr_ctc_backward', N.ptr(logits), Vp, T * Vp, T, B, V, N.ptr(labels_flat),
+               N.ptr(label_lens), N.ptr(act_lens), max_label_len, blank, N.ptr(g),
+               loss_scale if g is not None else 0.0, N.ptr(dl), Vp, T * Vp, N.ptr(ws), nbytes,
+               N.stream_handle(dev))
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty(B, T, K, dtype=torch.float32, device=dev)
+            if M > 0:
+                run_gemm([gemm_problem(operand(dl, 0, rowmap(Vp)), operand(weight, 1, rowmap(K)),
+                                       dx, rowmap(K), M, K, V, drop=ctx.drop)], dev)
+
+        def wgrad():
+            if M > 0:
+                run_gemm([gemm_problem(operand(dl, 1, rowmap(Vp)), operand(x, 1, rowmap(K)),
+                                       grad_buffer(weight), rowmap(K), V, K, M, beta=1.0)], dev)
+            if bias is not None:
+                colsum_accumulate(dl[:, :V], grad_buffer(bias))
+        gb = (grad_buffer(weight),) + ((grad_buffer(bias),) if bias is not None else ())
+        if not (ctx.from_blstm is not None and os.environ.get('ASR_HEAD_WGRAD_SIDE', '1') != '0'
+                and _wgrad_beside(dev, ctx.from_blstm, wgrad, (x, dl), gb)):
+            wgrad()
+        return (dx,) + (None,) * 10
+
+
 def _produced_by_blstm(t, depth=4):
     """(B, H) of the BLSTMLayerFn whose output t derives from within `depth`
     autograd hops (views, permutes, fc layers), else None: its backward
@@ -451,13 +528,16 @@ def _produced_by_blstm(t, depth=4):
 def linear_ctc_loss(x, weight, bias, labels_flat, label_lens, act_lens, max_label_len,
                     loss_scale=1.0, drop=None, blank=0, zero_infinity=True):
     """ctc_loss(linear(x, weight, bias, drop), ...) -> (loss [1], costs [B]);
-    one fused op (LinearCTCFn) when the output layer is staged in bf16
-    (ASR_CTC_HEAD_FUSED=0 keeps the two ops)."""
+    one fused op: LinearCTCFn when the output layer is staged in bf16,
+    LinearCTC32Fn in fp32 mode (ASR_CTC_HEAD_FUSED=0 keeps the two ops)."""
     K = x.shape[-1]
-    if (x.dim() == 3 and _linear_stages(x.numel() // K, K, weight.shape[0]) and
-            os.environ.get('ASR_CTC_HEAD_FUSED', '1') != '0'):
+    fused = os.environ.get('ASR_CTC_HEAD_FUSED', '1') != '0'
+    if x.dim() == 3 and _linear_stages(x.numel() // K, K, weight.shape[0]) and fused:
         return LinearCTCFn.apply(x, weight, bias, drop, labels_flat, label_lens, act_lens,
                                  max_label_len, loss_scale, blank, zero_infinity)
+    if x.dim() == 3 and compute_dtype() == F32 and fused:
+        return LinearCTC32Fn.apply(x, weight, bias, drop, labels_flat, label_lens, act_lens,
+                                   max_label_len, loss_scale, blank, zero_infinity)
     return ctc_loss(linear(x, weight, bias, drop), labels_flat, label_lens, act_lens,
                     max_label_len, loss_scale, blank, zero_infinity)
 

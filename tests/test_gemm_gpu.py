@@ -383,3 +383,129 @@ def test_n64_kernel_exact(M, N, K, atrans, btrans, cuda_dev, monkeypatch):
         np.testing.assert_array_equal(outs[0], outs[1])
     finally:
         ops.set_compute_dtype('fp32')
+
+
+def _f32_run(ops, dev, probs_fn, fast, monkeypatch):
+    monkeypatch.setenv('ASR_GEMM_F32FAST', fast)
+    probs, outs = probs_fn()
+    ops.run_gemm(probs, dev)
+    torch.cuda.synchronize()
+    return [o.cpu().numpy() for o in outs]
+
+
+@pytest.mark.parametrize('at,bt', [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize('M,N,K', [(600, 389, 1032), (128, 128, 32), (300, 260, 203),
+                                    (192, 160, 32768), (1030, 777, 1001), (5000, 64, 576),
+                                    (4391, 40, 198), (64, 576, 20000), (37, 300, 401)])
+def test_f32_fast_kernel_exact(at, bt, M, N, K, cuda_dev, monkeypatch):
+    """gemm_f32_fast (fp32 mode: LDS-DMA staging, v_mfma_f32_16x16x4_f32) in
+    every operand layout and all three tile shapes (128 x 128; 256 x 64 for
+    N <= 64; 64 x 256 for M <= 64): ragged M / N, K not a multiple of the
+    32-deep k-tile and not of 4 (the straddling chunk zero-filled in LDS), a
+    single k-tile, split-K (few tiles, long K), padded leading dimensions
+    (16-B aligned rows), alpha / beta / bias pair.  Small integers: exact, so
+    equal to float64 bit for bit (and to gemm_kernel<false>,
+    ASR_GEMM_F32FAST=0)."""
+    ops = _ops()
+    ops.set_compute_dtype('fp32')
+    rng = np.random.RandomState(M * 5 + N * 3 + K + 17 * at + 19 * bt)
+
+    def ld(cols, pad):
+        return (cols + 3) // 4 * 4 + pad
+    sa = _store(rng, K if at else M, M if at else K, ld(M if at else K, 4))
+    sb = _store(rng, K if bt else N, N if bt else K, ld(N if bt else K, 12))
+    # garbage past each row's end (inside the padding): must not reach C
+    sa[:, (M if at else K):] = 1e30
+    sb[:, (N if bt else K):] = -1e30
+    A = (sa[:, :M].T if at else sa[:, :K]).astype(np.float64)
+    Bm = (sb[:, :N].T if bt else sb[:, :K]).astype(np.float64)
+    c0 = rng.randint(-4, 5, (M, N)).astype(np.float32)
+    b1 = rng.randint(-8, 9, N).astype(np.float32)
+    b2 = rng.randint(-8, 9, N).astype(np.float32)
+    ad, bd = torch.from_numpy(sa).to(cuda_dev), torch.from_numpy(sb).to(cuda_dev)
+    bias, bias2 = torch.from_numpy(b1).to(cuda_dev), torch.from_numpy(b2).to(cuda_dev)
+
+    def probs():
+        C = torch.from_numpy(c0).to(cuda_dev)
+        return [ops.gemm_problem(ops.operand(ad, at, ops.rowmap(sa.shape[1])),
+                                 ops.operand(bd, bt, ops.rowmap(sb.shape[1])), C, ops.rowmap(N),
+                                 M, N, K, alpha=2.0, beta=1.0, bias=bias, bias2=bias2)], [C]
+    got = _f32_run(ops, cuda_dev, probs, '1', monkeypatch)[0]
+    ref = 2.0 * (A @ Bm.T) + c0 + b1 + b2
+    np.testing.assert_array_equal(got, ref)
+    np.testing.assert_array_equal(got, _f32_run(ops, cuda_dev, probs, '0', monkeypatch)[0])
+
+
+def test_f32_fast_kernel_mapped_rows_exact(cuda_dev, monkeypatch):
+    """gemm_f32_fast with row-mapped operands (utterance groups, frame stride
+    2, offset 1, frame limit) in K mode (weight-gradient shape) and R mode, and
+    two problems in one launch: exact against float64."""
+    ops = _ops()
+    ops.set_compute_dtype('fp32')
+    rng = np.random.RandomState(71)
+    M, Nn = 320, 200
+    rpb, T, t_mul, t_add, t_limit = 37, 80, 2, 1, 60
+    nb = 9
+    K = nb * rpb
+    lda, ldb = M + 4, Nn + 4
+    sa = _store(rng, nb * T, M, lda)
+    sb = _store(rng, nb * T, Nn, ldb)
+    A = _mapped_rows(sa, rpb, T * lda, lda, t_mul, t_add, t_limit, K, M)
+    Bm = _mapped_rows(sb, rpb, T * ldb, ldb, t_mul, t_add, t_limit, K, Nn)
+    ad, bd = torch.from_numpy(sa).to(cuda_dev), torch.from_numpy(sb).to(cuda_dev)
+    Mr = nb * rpb
+    A2 = _mapped_rows(sa, rpb, T * lda, lda, t_mul, t_add, t_limit, Mr, 64)
+    sb2 = _store(rng, Nn, 64, 64)
+    bd2 = torch.from_numpy(sb2).to(cuda_dev)
+
+    def probs():
+        C = torch.zeros(M, Nn, device=cuda_dev)
+        C2 = torch.zeros(Mr, Nn, device=cuda_dev)
+        return [ops.gemm_problem(
+            ops.operand(ad, 1, ops.rowmap(lda, T * lda, rpb, t_mul, t_add, t_limit)),
+            ops.operand(bd, 1, ops.rowmap(ldb, T * ldb, rpb, t_mul, t_add, t_limit)),
+            C, ops.rowmap(Nn), M, Nn, K),
+            ops.gemm_problem(
+            ops.operand(ad, 0, ops.rowmap(lda, T * lda, rpb, t_mul, t_add, t_limit)),
+            ops.operand(bd2, 0, ops.rowmap(64)), C2, ops.rowmap(Nn), Mr, Nn, 64)], [C, C2]
+    # one launch per layout pair (the fast kernel takes one pair per launch)
+    p, o = probs()
+    monkeypatch.setenv('ASR_GEMM_F32FAST', '1')
+    ops.run_gemm(p[:1], cuda_dev)
+    ops.run_gemm(p[1:], cuda_dev)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(o[0].cpu().numpy(), A.T @ Bm)
+    np.testing.assert_array_equal(o[1].cpu().numpy(), A2 @ sb2.astype(np.float64).T)
+
+
+@pytest.mark.parametrize('ci,co,F,sign', [(64, 64, 20, 1), (64, 128, 12, -1), (16, 32, 9, 1)])
+def test_f32_fast_kernel_taps_match_generic(ci, co, F, sign, cuda_dev, monkeypatch):
+    """3x3 convolutions as tap-addressed products in fp32 mode (forward /
+    input-gradient geometry: taps on A's k; weight gradient: taps on B's
+    columns in K mode): gemm_f32_fast bitwise equal to gemm_kernel<false>
+    (small integers: both exact)."""
+    ops = _ops()
+    ops.set_compute_dtype('fp32')
+    rng = np.random.RandomState(ci + co + F)
+    B, T = 3, 11
+    P = B * (T + 2) * (F + 2)
+    x = torch.from_numpy(rng.randint(-3, 4, (P, ci)).astype(np.float32)).to(cuda_dev)
+    w = torch.from_numpy(rng.randint(-3, 4, (co, 9 * ci)).astype(np.float32)).to(cuda_dev)
+    dz = torch.from_numpy(rng.randint(-3, 4, (P, co)).astype(np.float32)).to(cuda_dev)
+
+    def fwd():
+        out = torch.zeros(P, co, device=cuda_dev)
+        return [ops.gemm_problem(ops._tap_operand(x, 0, ci, ci, F + 2, sign),
+                                 ops.operand(w, 0, ops.rowmap(9 * ci)), out, ops.rowmap(co),
+                                 P, co, 9 * ci)], [out]
+
+    def wgrad():
+        packed = torch.zeros(co, 9 * ci, device=cuda_dev)
+        return [ops.gemm_problem(ops.operand(dz, 1, ops.rowmap(co)),
+                                 ops._tap_operand(x, 1, ci, ci, F + 2, 1), packed,
+                                 ops.rowmap(9 * ci), co, 9 * ci, P)], [packed]
+    for fn in (fwd, wgrad):
+        a = _f32_run(ops, cuda_dev, fn, '1', monkeypatch)[0]
+        b = _f32_run(ops, cuda_dev, fn, '0', monkeypatch)[0]
+        assert np.abs(b).max() > 0
+        np.testing.assert_array_equal(a, b)

@@ -48,15 +48,16 @@ cases += [
                        beta=1.0)]),
 ]
 Mh, V = 8000, 10001
-xh, wh, lg = f(Mh, D), f(V, D, scale=0.05), torch.empty(Mh, V, device=dev)
-dlg, dxh, dwh = f(Mh, V), torch.empty(Mh, D, device=dev), torch.zeros(V, D, device=dev)
+Vp = (V + 3) // 4 * 4   # the fp32 CTC head's logits pitch (native_ops.LinearCTC32Fn)
+xh, wh, lg = f(Mh, D), f(V, D, scale=0.05), torch.empty(Mh, Vp, device=dev)
+dlg, dxh, dwh = f(Mh, Vp), torch.empty(Mh, D, device=dev), torch.zeros(V, D, device=dev)
 cases += [
     ('head fwd M=8000 N=10001 K=640 (RR)', 2.0 * Mh * V * D,
-     [ops.gemm_problem(ops.operand(xh, 0, R(D)), ops.operand(wh, 0, R(D)), lg, R(V), Mh, V, D)]),
+     [ops.gemm_problem(ops.operand(xh, 0, R(D)), ops.operand(wh, 0, R(D)), lg, R(Vp), Mh, V, D)]),
     ('head dX  M=8000 N=640 K=10001 (RK)', 2.0 * Mh * V * D,
-     [ops.gemm_problem(ops.operand(dlg, 0, R(V)), ops.operand(wh, 1, R(D)), dxh, R(D), Mh, D, V)]),
+     [ops.gemm_problem(ops.operand(dlg, 0, R(Vp)), ops.operand(wh, 1, R(D)), dxh, R(D), Mh, D, V)]),
     ('head dW  M=10001 N=640 K=8000 (KK)', 2.0 * Mh * V * D,
-     [ops.gemm_problem(ops.operand(dlg, 1, R(V)), ops.operand(xh, 1, R(D)), dwh, R(D), V, D, Mh,
+     [ops.gemm_problem(ops.operand(dlg, 1, R(Vp)), ops.operand(xh, 1, R(D)), dwh, R(D), V, D, Mh,
                        beta=1.0)]),
 ]
 B = 32
