@@ -80,6 +80,17 @@ int asr_ctc_forward(const float* acts, long long stride_t, long long stride_b, i
                     const int32_t* act_lens, int max_label_len, int blank, int zero_infinity,
                     float* costs, float* loss_out, float loss_scale, void* workspace,
                     size_t ws_bytes, void* stream);
+/* asr_ctc_forward with the per-frame log-sum-exp already formed by the output
+ * layer's GEMM (asr_gemm_lse_ws): lse_part holds, for every frame row b*T + t
+ * and 64-class slab q < nslab = ceil(V / 64), the pair (max, sum exp(x - max))
+ * at lse_part[2 (q B T + b T + t)].  The activations are then read only at
+ * the label columns; costs, loss and the workspace state for asr_ctc_backward
+ * are those of asr_ctc_forward. */
+int asr_ctc_forward_lse(const float* acts, long long stride_t, long long stride_b, int T, int B,
+                        int V, const float* lse_part, int nslab, const int32_t* labels_flat,
+                        const int32_t* label_lens, const int32_t* act_lens, int max_label_len,
+                        int blank, int zero_infinity, float* costs, float* loss_out,
+                        float loss_scale, void* workspace, size_t ws_bytes, void* stream);
 int asr_ctc_backward(const float* acts, long long stride_t, long long stride_b, int T, int B,
                      int V, const int32_t* labels_flat, const int32_t* label_lens,
                      const int32_t* act_lens, int max_label_len, int blank,
@@ -195,6 +206,13 @@ int asr_gemm(const asr_gemm_t* problems, int nprob, int compute_dtype, void* str
 size_t asr_gemm_workspace_bytes(const asr_gemm_t* problems, int nprob);
 int asr_gemm_ws(const asr_gemm_t* problems, int nprob, int compute_dtype, void* workspace,
                 size_t ws_bytes, void* stream);
+/* asr_gemm_ws of ONE product (beta 0, no dropout, f32 C, batch 1) whose
+ * epilogue also writes, for every row m < M and 64-column slab q < ceil(N/64),
+ * the online log-sum-exp pair of the values written to C: lse[2 (q M + m)] =
+ * max, lse[2 (q M + m) + 1] = sum exp(c - max) (the CTC normaliser of an
+ * output layer, formed where the logits are produced; asr_ctc_forward_lse). */
+int asr_gemm_lse_ws(const asr_gemm_t* problem, int compute_dtype, float* lse, void* workspace,
+                    size_t ws_bytes, void* stream);
 
 /* on != 0: later asr_gemm / asr_gemm_ws calls FROM THIS HOST THREAD use only the
  * 128 x 128 kernel (64 KB of LDS per work-group) until reset with 0, so that

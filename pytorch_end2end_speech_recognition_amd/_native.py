@@ -38,6 +38,9 @@ SIGNATURES = {
     'asr_ctc_workspace_bytes': (c_size, [c_int, c_int, c_int, c_int]),
     'asr_ctc_forward': (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int,
                                 c_int, c_int, c_vp, c_vp, c_float, c_vp, c_size, c_vp]),
+    'asr_ctc_forward_lse': (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_int, c_vp, c_int, c_vp,
+                                    c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_float, c_vp,
+                                    c_size, c_vp]),
     'asr_ctc_backward': (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int,
                                  c_int, c_vp, c_float, c_vp, c_ll, c_ll, c_vp, c_size, c_vp]),
     'asr_ctc_backward_bf16': (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp,
@@ -52,6 +55,7 @@ SIGNATURES = {
     'asr_gemm': (c_int, [c_vp, c_int, c_int, c_vp]),
     'asr_gemm_workspace_bytes': (c_size, [c_vp, c_int]),
     'asr_gemm_ws': (c_int, [c_vp, c_int, c_int, c_vp, c_size, c_vp]),
+    'asr_gemm_lse_ws': (c_int, [c_vp, c_int, c_vp, c_vp, c_size, c_vp]),
     'asr_gemm_set_small_tiles': (c_int, [c_int]),
     'asr_gemm_set_n64_kmode': (c_int, [c_int]),
     'asr_lstm_wgrad_gate': (c_int, [c_vp]),

@@ -230,6 +230,64 @@ __global__ void __launch_bounds__(256) ctc_emit_wide(const float* __restrict__ a
   }
 }
 
+// The head GEMM's epilogue already formed each row's log-sum-exp in 64-column
+// slabs (asr_gemm_lse_ws: (max, sum exp) pairs, part[2 (q M + row)]): one
+// thread per row folds its nslab pairs (consecutive rows: coalesced 8-B
+// reads) -- the activations are not read for the normaliser at all.
+__global__ void __launch_bounds__(256) ctc_lse_from_parts(const float* __restrict__ part,
+                                                          int nslab, long long M, int T,
+                                                          const int32_t* __restrict__ act_lens,
+                                                          int rev, float* __restrict__ lse_out) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= M) return;
+  const long long row = rev ? M - 1 - i : i;
+  const int b = (int)(row / T), t = (int)(row % T);
+  if (t >= act_lens[b]) return;
+  float m = neg_inf(), sm = 0.f;
+  for (int q = 0; q < nslab; ++q) {
+    const float2 pq = *reinterpret_cast<const float2*>(part + 2 * ((long long)q * M + row));
+    if (pq.x > m) {
+      sm = sm * __expf(m - pq.x) + pq.y;   // m = -inf on the first slab: 0 * 0
+      m = pq.x;
+    } else {
+      sm += pq.y * __expf(pq.x - m);
+    }
+  }
+  lse_out[row] = m + __logf(sm);
+}
+
+// The S emissions of a row from its log-sum-exp (ctc_emit's tail): one wave
+// per row, four rows per work-group.
+__global__ void __launch_bounds__(256) ctc_emit_gather(const float* __restrict__ acts, long long st,
+                                                       long long sb, int T, int B, int V,
+                                                       const int32_t* __restrict__ labels,
+                                                       const int32_t* __restrict__ label_lens,
+                                                       const int32_t* __restrict__ act_lens,
+                                                       const int32_t* __restrict__ offs, int blank,
+                                                       int Spad, const float* __restrict__ lse_in,
+                                                       float* __restrict__ emit) {
+  const int lane = threadIdx.x & 63;
+  const long long row = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= (long long)B * T) return;
+  const int b = (int)(row / T), t = (int)(row % T);
+  if (t >= act_lens[b]) return;
+  const float* x = acts + (long long)t * st + (long long)b * sb;
+  const float lse = lse_in[row];
+  const int L = min(label_lens[b], (Spad - 1) / 2);
+  const int S = 2 * L + 1;
+  const int32_t* lab = labels + offs[b];
+  float* e = emit + row * Spad;
+  for (int st_ = lane; st_ < Spad; st_ += 64) {
+    float v = neg_inf();
+    if (st_ < S) {
+      int c = (st_ & 1) ? lab[st_ >> 1] : blank;
+      c = c < 0 ? 0 : (c >= V ? V - 1 : c);
+      v = (x[c] - lse) * kLog2e;
+    }
+    e[st_] = v;
+  }
+}
+
 template <int K>
 __device__ __forceinline__ void load_k(float (&r)[K], const float* p) {
   if constexpr (K % 4 == 0) {
@@ -873,16 +931,18 @@ static int ctc_row_order() {
   return v;
 }
 
-extern "C" int asr_ctc_forward(const float* acts, long long stride_t, long long stride_b, int T,
-                               int B, int V, const int32_t* labels_flat,
-                               const int32_t* label_lens, const int32_t* act_lens,
-                               int max_label_len, int blank, int zero_infinity, float* costs,
-                               float* loss_out, float loss_scale, void* workspace,
-                               size_t ws_bytes, void* stream) {
+static int ctc_forward_impl(const float* acts, long long stride_t, long long stride_b, int T,
+                            int B, int V, const float* lse_part, int nslab,
+                            const int32_t* labels_flat, const int32_t* label_lens,
+                            const int32_t* act_lens, int max_label_len, int blank,
+                            int zero_infinity, float* costs, float* loss_out, float loss_scale,
+                            void* workspace, size_t ws_bytes, void* stream) {
   int rc = check_common(acts, T, B, V, labels_flat, label_lens, act_lens, max_label_len, blank,
                         workspace, ws_bytes);
   if (rc) return rc;
   ASR_REQUIRE(costs, ASR_ERR_ARG, "ctc: costs is null");
+  ASR_REQUIRE(!lse_part || nslab == (V + 63) / 64, ASR_ERR_ARG,
+              "ctc: %d log-sum-exp slabs for V=%d (need %d)", nslab, V, (V + 63) / 64);
   hipStream_t s = (hipStream_t)stream;
   CtcWs ws;
   ws_layout(T, B, max_label_len, &ws, (char*)workspace);
@@ -892,9 +952,18 @@ extern "C" int asr_ctc_forward(const float* acts, long long stride_t, long long 
                      max_label_len, ws.offs, ws.status);
   ASR_LAUNCH_CHECK();
   const long long rows = (long long)B * T;
-  // algorithmic HBM bytes of the forward: the activations read once
-  const int pslot = prof_begin_launch(ASR_PROF_CTC_FWD, s, 4.0 * (double)V * (double)rows, V);
-  if (V > 1024)
+  // algorithmic HBM bytes of the forward: the activations read once,
+  // or with the GEMM's partials, those (8 B per slab per row)
+  const int pslot = prof_begin_launch(
+      ASR_PROF_CTC_FWD, s, (lse_part ? 8.0 * nslab : 4.0 * (double)V) * (double)rows, V);
+  if (lse_part) {
+    hipLaunchKernelGGL(ctc_lse_from_parts, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s,
+                       lse_part, nslab, rows, T, act_lens, 0, ws.lse);
+    ASR_LAUNCH_CHECK();
+    hipLaunchKernelGGL(ctc_emit_gather, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, acts,
+                       stride_t, stride_b, T, B, V, labels_flat, label_lens, act_lens, ws.offs,
+                       blank, Spad, ws.lse, ws.emit);
+  } else if (V > 1024)
     hipLaunchKernelGGL(ctc_emit_wide, dim3((unsigned)rows), dim3(256), 0, s, acts, stride_t,
                        stride_b, T, V, labels_flat, label_lens, act_lens, ws.offs, blank, Spad,
                        ws.lse, ws.emit, ctc_row_order() & 1);
@@ -923,6 +992,30 @@ extern "C" int asr_ctc_forward(const float* acts, long long stride_t, long long 
     ASR_LAUNCH_CHECK();
   }
   return ASR_OK;
+}
+
+extern "C" int asr_ctc_forward(const float* acts, long long stride_t, long long stride_b, int T,
+                               int B, int V, const int32_t* labels_flat,
+                               const int32_t* label_lens, const int32_t* act_lens,
+                               int max_label_len, int blank, int zero_infinity, float* costs,
+                               float* loss_out, float loss_scale, void* workspace,
+                               size_t ws_bytes, void* stream) {
+  return ctc_forward_impl(acts, stride_t, stride_b, T, B, V, nullptr, 0, labels_flat, label_lens,
+                          act_lens, max_label_len, blank, zero_infinity, costs, loss_out,
+                          loss_scale, workspace, ws_bytes, stream);
+}
+
+extern "C" int asr_ctc_forward_lse(const float* acts, long long stride_t, long long stride_b,
+                                   int T, int B, int V, const float* lse_part, int nslab,
+                                   const int32_t* labels_flat, const int32_t* label_lens,
+                                   const int32_t* act_lens, int max_label_len, int blank,
+                                   int zero_infinity, float* costs, float* loss_out,
+                                   float loss_scale, void* workspace, size_t ws_bytes,
+                                   void* stream) {
+  ASR_REQUIRE(lse_part, ASR_ERR_ARG, "ctc: lse_part is null");
+  return ctc_forward_impl(acts, stride_t, stride_b, T, B, V, lse_part, nslab, labels_flat,
+                          label_lens, act_lens, max_label_len, blank, zero_infinity, costs,
+                          loss_out, loss_scale, workspace, ws_bytes, stream);
 }
 
 extern "C" int asr_ctc_backward(const float* acts, long long stride_t, long long stride_b, int T,

@@ -69,6 +69,10 @@ struct Problem {
   float* slab;
   float drop_p;                  // > 0: C element at offset i from C's base is kept iff
   unsigned long long drop_seed;  // u01(drop_seed, i) >= drop_p, scaled by 1 / (1 - p)
+  // non-null (asr_gemm_lse_ws): per row m and 64-column slab q of C, the online
+  // log-sum-exp pair (max, sum exp(c - max)) of the written values ->
+  // lse[2 (q M + m)], lse[2 (q M + m) + 1] (beta 0, no dropout, f32 C, no split)
+  float* lse;
 };
 
 // Dropout mask of the epilogue (asr_dropout's mask over C's flat offsets).
@@ -250,6 +254,27 @@ __device__ __forceinline__ void store_tile(const Operand& op, void* lds, const f
   }
 }
 
+// One row's (max, sum exp) over a 64-column slab held by the 16 lanes of a
+// lane group (4 values each, -inf where the column is past N): reduce across
+// the group, lane 0 of it stores.  Every lane of the wave calls it (shuffles).
+__device__ __forceinline__ void lse_pair_store(const Problem& pr, int q, int m, const float (&v)[4],
+                                               float mx, int lane) {
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  float sm = 0.f;
+  if (mx != neg_inf()) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) sm += __expf(v[e] - mx);
+  }
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) sm += __shfl_xor(sm, o);
+  if ((lane & 15) == 0 && m < pr.M && mx != neg_inf()) {
+    float* p = pr.lse + 2 * ((long long)q * pr.M + m);
+    p[0] = mx;
+    p[1] = sm;
+  }
+}
+
 // Epilogue shared by the GEMM kernels.  C/D layout: col = lane&15, row = 4*(lane>>4) + r.
 __device__ __forceinline__ void store_acc(const Problem& pr, const f32x4 (&acc)[4][4], int tm,
                                           int tn, int wr, int wc, int lane, int split,
@@ -269,6 +294,28 @@ __device__ __forceinline__ void store_acc(const Problem& pr, const f32x4 (&acc)[
         }
       }
     return;
+  }
+  if (pr.lse) {   // row log-sum-exp partials of this wave's 64-column slab
+    const int q = (tn + wc) >> 6;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v[4];
+        float mx = neg_inf();
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = tn + wc + j * 16 + (lane & 15);
+          v[j] = neg_inf();
+          if (n < pr.N) {
+            v[j] = pr.alpha * acc[i][j][r];
+            if (pr.bias) v[j] += pr.bias[n];
+            if (pr.bias2) v[j] += pr.bias2[n];
+          }
+          mx = fmaxf(mx, v[j]);
+        }
+        lse_pair_store(pr, q, tm + wr + i * 16 + 4 * (lane >> 4) + r, v, mx, lane);
+      }
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -933,10 +980,20 @@ __device__ __forceinline__ f32x4 frag_f32(const char* lds_tile, int rb, int h, i
   }
 }
 
-template <int AMODE, int BMODE, int TMW>
+// s_waitcnt vmcnt(n) with expcnt / lgkmcnt left at their maxima (gfx9 encoding)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+// NSTAGE = 2: double buffer, two work-groups per CU; 3: a ring with two
+// k-tiles in flight (one work-group per CU), counted waits.
+template <int AMODE, int BMODE, int TMW, int NSTAGE = 2>
 __global__ void __launch_bounds__(NT) gemm_f32_fast(Params P) {
   constexpr int TNW = 4 / TMW, TM = 64 * TMW, TN = 64 * TNW;
   constexpr int ATILE = TM * FBK32 * 4, STAGE = (TM + TN) * FBK32 * 4;
+  constexpr int DPT = (TM + TN) / 32;   // DMAs per wave per k-tile
   extern __shared__ __attribute__((aligned(16))) char smem[];  // 2 stages x (A, B) tiles
   const int zb = blockIdx.z / P.nprob, zp = blockIdx.z % P.nprob;
   Problem pr = P.p[zp];
@@ -991,20 +1048,7 @@ __global__ void __launch_bounds__(NT) gemm_f32_fast(Params P) {
   StageF32<TN / 32> sb;
   stagef32_init<AMODE, TM>(pr.a, sa, tm, pr.M, kbeg, w, lane);
   stagef32_init<BMODE, TN>(pr.b, sb, tn, pr.N, kbeg, w, lane);
-  stagef32<AMODE, TM>(pr.a, ra, sa, smem, kbeg, kend, w, lane);
-  stagef32<BMODE, TN>(pr.b, rb, sb, smem + ATILE, kbeg, kend, w, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (AMODE == 0) tailfix32<TM>(sa, smem, w, lane);
-  if (BMODE == 0) tailfix32<TN>(sb, smem + ATILE, w, lane);
-  __builtin_amdgcn_s_barrier();
-  for (int kt = 0; kt < nk; ++kt) {
-    const char* cur = smem + (kt & 1) * STAGE;
-    char* nxt = smem + ((kt + 1) & 1) * STAGE;
-    if (kt + 1 < nk) {
-      const int k0 = kbeg + (kt + 1) * FBK32;
-      stagef32<AMODE, TM>(pr.a, ra, sa, nxt, k0, kend, w, lane);
-      stagef32<BMODE, TN>(pr.b, rb, sb, nxt + ATILE, k0, kend, w, lane);
-    }
+  auto mma = [&](const char* cur) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       f32x4 fa[4], fb[4];
@@ -1019,12 +1063,46 @@ __global__ void __launch_bounds__(NT) gemm_f32_fast(Params P) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) acc[i][j] = mfma_f32(fa[i][e], fb[j][e], acc[i][j]);
     }
+  };
+  auto stage = [&](char* st, int k0) {
+    stagef32<AMODE, TM>(pr.a, ra, sa, st, k0, kend, w, lane);
+    stagef32<BMODE, TN>(pr.b, rb, sb, st + ATILE, k0, kend, w, lane);
+  };
+  // the last k-tile's straddling R-mode chunks (the only ones), once landed
+  auto tail = [&](char* st) {
+    if (AMODE == 0) tailfix32<TM>(sa, st, w, lane);
+    if (BMODE == 0) tailfix32<TN>(sb, st + ATILE, w, lane);
+  };
+  if constexpr (NSTAGE == 2) {
+    stage(smem, kbeg);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (kt + 1 < nk) {
-      if (AMODE == 0) tailfix32<TM>(sa, nxt, w, lane);
-      if (BMODE == 0) tailfix32<TN>(sb, nxt + ATILE, w, lane);
-    }
+    tail(smem);
     __builtin_amdgcn_s_barrier();
+    for (int kt = 0; kt < nk; ++kt) {
+      const char* cur = smem + (kt & 1) * STAGE;
+      char* nxt = smem + ((kt + 1) & 1) * STAGE;
+      if (kt + 1 < nk) stage(nxt, kbeg + (kt + 1) * FBK32);
+      mma(cur);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (kt + 1 < nk) tail(nxt);
+      __builtin_amdgcn_s_barrier();
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < NSTAGE - 1; ++j)
+      if (j < nk) stage(smem + j * STAGE, kbeg + j * FBK32);
+    for (int kt = 0; kt < nk; ++kt) {
+      const int after = min(NSTAGE - 2, nk - 1 - kt);   // tiles issued after tile kt
+      if (after >= 1) wait_vmcnt<DPT>();
+      else wait_vmcnt<0>();
+      asm volatile("" ::: "memory");
+      char* cur = smem + (kt % NSTAGE) * STAGE;
+      if (kt == nk - 1) tail(cur);
+      __builtin_amdgcn_s_barrier();
+      if (kt + NSTAGE - 1 < nk)
+        stage(smem + ((kt + NSTAGE - 1) % NSTAGE) * STAGE, kbeg + (kt + NSTAGE - 1) * FBK32);
+      mma(cur);
+    }
   }
   store_acc(pr, acc, tm, tn, wr, wc, lane, split, nsplit);
 }
@@ -1510,6 +1588,27 @@ __device__ __forceinline__ void epi8(const Problem& pr, const RowMap& cm, bool r
         for (int r = 0; r < 4; ++r)
           tile[(16 * i + 4 * (lane >> 4) + r) * EP8 + 16 * j + (lane & 15)] = acc[2 * h + i][j][r];
     __syncthreads();
+    if (!raw && pr.lse) {   // row log-sum-exp partials of this wave's 64-column slab
+      for (int it = 0; it < 8; ++it) {
+        const int row = it * 4 + (lane >> 4), ch = lane & 15;
+        const int n = tn + wc + 4 * ch;
+        const float4 t4 = *reinterpret_cast<const float4*>(tile + row * EP8 + 4 * ch);
+        const float tv[4] = {t4.x, t4.y, t4.z, t4.w};
+        float v[4];
+        float mx = neg_inf();
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = neg_inf();
+          if (n + e < pr.N) {
+            v[e] = tv[e] * pr.alpha;
+            if (pr.bias) v[e] += pr.bias[n + e];
+            if (pr.bias2) v[e] += pr.bias2[n + e];
+          }
+          mx = fmaxf(mx, v[e]);
+        }
+        lse_pair_store(pr, (tn + wc) >> 6, tm + wr + 32 * h + row, v, mx, lane);
+      }
+    }
 #pragma unroll 4
     for (int it = 0; it < 8; ++it) {
       const int row = it * 4 + (lane >> 4), ch = lane & 15;
@@ -2261,6 +2360,7 @@ int split_target() {
 // run co-resident with the persistent backward recurrence (native_ops,
 // ASR_OVERLAP_WGRAD=2) must fit beside its work-group on every CU.
 thread_local int g_small_tiles = 0;
+thread_local float* g_row_lse = nullptr;   // asr_gemm_lse_ws: the product's row-LSE partials
 thread_local int g_n64_kmode = 0;
 
 // Products with N <= 64 and many rows take the 256 x 64 kernel (B in R mode;
@@ -2324,6 +2424,7 @@ int gemm_launch_own(const asr_gemm_t* problems, int nprob, int compute_dtype, vo
     ASR_REQUIRE(g.drop_p == 0.f || g.batch <= 1, ASR_ERR_ARG, "gemm: dropout on a batched product");
     p.drop_p = g.drop_p;
     p.drop_seed = g.drop_seed;
+    p.lse = nullptr;
     ASR_REQUIRE(g.c_dtype == ASR_DT_F32 || g.c_dtype == ASR_DT_BF16, ASR_ERR_ARG,
                 "gemm: C dtype %d", g.c_dtype);
     p.c_bf16 = g.c_dtype == ASR_DT_BF16;
@@ -2341,6 +2442,13 @@ int gemm_launch_own(const asr_gemm_t* problems, int nprob, int compute_dtype, vo
     p.slab = p.ksplit > 1 ? (float*)((char*)workspace + sp.slab_off[i]) : nullptr;
     maxwg = max(maxwg, ceil_div(g.M, BM) * ceil_div(g.N, BN) * p.ksplit);
     maxb = max(maxb, p.batch);
+  }
+  if (g_row_lse) {   // asr_gemm_lse_ws: one product, whole-K tiles (no split slabs)
+    P.p[0].lse = g_row_lse;
+    P.p[0].ksplit = 1;
+    P.p[0].kchunk = P.p[0].K;
+    P.p[0].slab = nullptr;
+    maxwg = ceil_div(problems[0].M, BM) * ceil_div(problems[0].N, BN);
   }
   if (nprob == 1) { P.p[1] = P.p[0]; P.p[1].batch = 0; }
   if (maxwg == 0) return ASR_OK;
@@ -2415,7 +2523,7 @@ int gemm_launch_own(const asr_gemm_t* problems, int nprob, int compute_dtype, vo
       case 2: hipLaunchKernelGGL((gemm_bf16_8w<1, 0>), g8, dim3(NT8), lds8, s, P); break;
       default: hipLaunchKernelGGL((gemm_bf16_8w<1, 1>), g8, dim3(NT8), lds8, s, P); break;
     }
-  } else if (fast == 3 && kk256_ok(problems, nprob)) {
+  } else if (fast == 3 && !g_row_lse && kk256_ok(problems, nprob)) {
     // 256 x 256 tiles; the split never exceeds the workspace plan's (128 x 128) split
     int maxwg2 = 0;
     for (int i = 0; i < nprob; ++i) {
@@ -2536,9 +2644,30 @@ int gemm_launch_own(const asr_gemm_t* problems, int nprob, int compute_dtype, vo
     const dim3 g32(wg32, 1, nprob * maxb);
     const size_t lds = 2 * (size_t)(tmr + tnr) * FBK32 * 4;
     prof_set_tag(ASR_PROF_GEMM, slot, 4 * ASR_PTAG_GEMM_F32F + f32m);
+    const char* fst = getenv("ASR_GEMM_F32_STAGES");   // 3: the ring (A/B; read per launch)
+    const bool ring = fst && fst[0] == '3';
+    if (ring) {
+      static bool attr = false;
+      if (!attr) {
+        attr = true;
+#define ASR_F32R_ATTR(A, B, TW)                                                                  \
+  (void)hipFuncSetAttribute((const void*)gemm_f32_fast<A, B, TW, 3>,                             \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 3 * 320 * FBK32 * 4)
+        ASR_F32R_ATTR(0, 0, 1); ASR_F32R_ATTR(0, 0, 2); ASR_F32R_ATTR(0, 0, 4);
+        ASR_F32R_ATTR(0, 1, 1); ASR_F32R_ATTR(0, 1, 2); ASR_F32R_ATTR(0, 1, 4);
+        ASR_F32R_ATTR(1, 0, 1); ASR_F32R_ATTR(1, 0, 2); ASR_F32R_ATTR(1, 0, 4);
+        ASR_F32R_ATTR(1, 1, 1); ASR_F32R_ATTR(1, 1, 2); ASR_F32R_ATTR(1, 1, 4);
+#undef ASR_F32R_ATTR
+      }
+    }
+    const size_t ldsr = ring ? lds / 2 * 3 : lds;
 #define ASR_F32F(A, B)                                                                           \
   do {                                                                                           \
-    if (tmw == 4) hipLaunchKernelGGL((gemm_f32_fast<A, B, 4>), g32, dim3(NT), lds, s, P);         \
+    if (ring) {                                                                                  \
+      if (tmw == 4) hipLaunchKernelGGL((gemm_f32_fast<A, B, 4, 3>), g32, dim3(NT), ldsr, s, P);   \
+      else if (tmw == 1) hipLaunchKernelGGL((gemm_f32_fast<A, B, 1, 3>), g32, dim3(NT), ldsr, s, P); \
+      else hipLaunchKernelGGL((gemm_f32_fast<A, B, 2, 3>), g32, dim3(NT), ldsr, s, P);            \
+    } else if (tmw == 4) hipLaunchKernelGGL((gemm_f32_fast<A, B, 4>), g32, dim3(NT), lds, s, P);  \
     else if (tmw == 1) hipLaunchKernelGGL((gemm_f32_fast<A, B, 1>), g32, dim3(NT), lds, s, P);    \
     else hipLaunchKernelGGL((gemm_f32_fast<A, B, 2>), g32, dim3(NT), lds, s, P);                  \
   } while (0)
@@ -2550,6 +2679,16 @@ int gemm_launch_own(const asr_gemm_t* problems, int nprob, int compute_dtype, vo
     }
 #undef ASR_F32F
   } else {
+    if (getenv("ASR_GEMM_DEBUG"))   // which fp32-mode products miss the f32 fast kernel
+      for (int i = 0; i < nprob; ++i)
+        fprintf(stderr, "[asr_gemm generic f32] M=%d N=%d K=%d batch=%d a(dt=%d tr=%d tap=%d "
+                "perm=%d ld=%lld al=%d) b(dt=%d tr=%d tap=%d perm=%d ld=%lld al=%d)\n",
+                problems[i].M, problems[i].N, problems[i].K, problems[i].batch,
+                problems[i].a.dtype, problems[i].a.trans, problems[i].a.tap_group,
+                problems[i].a.map.perm != nullptr, problems[i].a.map.stride_t,
+                (int)aligned16(problems[i].a.ptr), problems[i].b.dtype, problems[i].b.trans,
+                problems[i].b.tap_group, problems[i].b.map.perm != nullptr,
+                problems[i].b.map.stride_t, (int)aligned16(problems[i].b.ptr));
     const size_t lds = 2 * BM * LDF32 * 4;
     prof_set_tag(ASR_PROF_GEMM, slot, 4 * ASR_PTAG_GEMM_GEN_F32);
     hipLaunchKernelGGL(gemm_kernel<false>, grid, dim3(NT), lds, s, P);
@@ -2701,6 +2840,18 @@ extern "C" size_t asr_gemm_workspace_bytes(const asr_gemm_t* problems, int nprob
   const size_t base = split_bytes_aligned(problems, nprob);
   const size_t stage = plan_stage(problems, nprob, base).bytes;
   return stage ? base + stage : plan_split(problems, nprob).bytes;
+}
+
+extern "C" int asr_gemm_lse_ws(const asr_gemm_t* problem, int compute_dtype, float* lse,
+                               void* workspace, size_t ws_bytes, void* stream) {
+  ASR_REQUIRE(problem && lse, ASR_ERR_ARG, "gemm_lse: null pointer");
+  ASR_REQUIRE(problem->beta == 0.f && problem->drop_p == 0.f && problem->c_dtype == ASR_DT_F32 &&
+                  problem->batch <= 1,
+              ASR_ERR_ARG, "gemm_lse: needs beta 0, no dropout, f32 C, one batch");
+  g_row_lse = lse;
+  const int rc = gemm_launch(problem, 1, compute_dtype, workspace, ws_bytes, stream);
+  g_row_lse = nullptr;
+  return rc;
 }
 
 extern "C" int asr_gemm_ws(const asr_gemm_t* problems, int nprob, int compute_dtype,

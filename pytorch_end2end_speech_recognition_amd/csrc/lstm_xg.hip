@@ -1648,14 +1648,16 @@ size_t lstm_xg_bwd_bytes(int B, int H) {
   return XG_HDR + (size_t)2 * rows * (H / XU) * (H / 4) * 8;
 }
 
-// f32 layouts.  With 16-row groups the f32 MFMA's 16 columns are all real
-// rows (8-row groups multiply 8 zero rows), so where the chip holds the grid
-// at 8 units per work-group (twice the work-groups of 16 units, half the
-// groups of 8 rows) the f32 kernels take 16 rows x 8 units: half the MFMAs
-// per work-group per step on as many CUs.  ASR_XG32_XU=16 keeps 16 units.
+// f32 layouts.  16 units per work-group with the row groups of the bf16 path
+// (xg_rows), or, with ASR_XG32_XU=8, 16-row groups of 8 units where the chip
+// holds that grid: every column of the f32 MFMA is then a real row and each
+// work-group does half the MFMAs per step -- but the hand-offs carry twice the
+// rows per poll and the backward sweep twice the producers, and the step
+// measured SLOWER (att4x320 fp32: forward 1.90 -> 2.56 ms, backward 1.72 ->
+// 2.90 ms per launch): the f32 recurrence is hand-off bound, not MFMA bound.
 int xg32_units(int B, int H) {
   const char* e = getenv("ASR_XG32_XU");
-  if (e && atoi(e) == 16) return 16;
+  if (!(e && atoi(e) == 8)) return 16;
   if (H % 64 != 0 || H / 8 > 64) return 16;
   const int G = 2 * ((B + 15) / 16);
   return G * (H / 8) <= xg_num_cus() ? 8 : 16;

@@ -112,15 +112,29 @@ def gemm_problem(a, b, c, c_map, M, N_, K, alpha=1.0, beta=0.0, bias=None, bias2
                   BF16 if c_bf16 else F32)
 
 
-def run_gemm(problems, device):
+def run_gemm(problems, device, lse=None):
     """One launch of up to two products; long-K / few-tile products (weight
-    gradients) get a split-K workspace from torch's caching allocator."""
+    gradients) get a split-K workspace from torch's caching allocator.
+    lse (one product): f32 [ceil(N / 64), M, 2] tensor receiving the row
+    log-sum-exp partials of the written C (asr_gemm_lse_ws)."""
     arr = (N.Gemm * len(problems))(*problems)
     parr = ctypes.cast(arr, ctypes.c_void_p)
     nb = N.query('asr_gemm_workspace_bytes', parr, len(problems))
     ws = _ws(nb, device) if nb else None
+    if lse is not None:
+        assert len(problems) == 1
+        N.call('asr_gemm_lse_ws', parr, compute_dtype(), N.ptr(lse), N.ptr(ws), nb,
+               N.stream_handle(device))
+        return
     N.call('asr_gemm_ws', parr, len(problems), compute_dtype(), N.ptr(ws), nb,
            N.stream_handle(device))
+
+
+def _ctc_lse_epilogue(V):
+    """The CTC normaliser of a wide output layer (V > 1024) is formed in the
+    head GEMM's epilogue (ASR_CTC_LSE_EPI=0: by the CTC forward's own pass
+    over the logits)."""
+    return V > 1024 and os.environ.get('ASR_CTC_LSE_EPI', '1') != '0'
 
 
 def colsum_accumulate(g2d, out0, out1=None, alpha=1.0):
@@ -164,9 +178,10 @@ def _linear_stages(M, K, Nout):
         flops >= _STAGE_FLOPS or (Nout % 8 != 0 and flops >= _STAGE_FLOPS_RAGGED))
 
 
-def _linear_forward(x, weight, bias, drop):
+def _linear_forward(x, weight, bias, drop, lse=None):
     """y = dropout(x) W^T + b (f32 [..., Nout]); returns (y, xo, wo, stage):
-    the GEMM operands the backward reuses (bf16 staged copies when stage)."""
+    the GEMM operands the backward reuses (bf16 staged copies when stage).
+    lse: row log-sum-exp partials of y (run_gemm)."""
     N.require_device(x, weight)
     x = x.contiguous()
     K = x.shape[-1]
@@ -198,7 +213,7 @@ def _linear_forward(x, weight, bias, drop):
     if M > 0:
         p = gemm_problem(operand(xo, 0, rowmap(Kp)), operand(wo, 0, rowmap(Kp)), y,
                          rowmap(Nout), M, Nout, Kp, bias=bias)
-        run_gemm([p], x.device)
+        run_gemm([p], x.device, lse=lse)
     return y, xo, wo, stage
 
 
@@ -348,6 +363,19 @@ class LinearFn(torch.autograd.Function):
         return dx, None, None, None
 
 
+def _ctc_forward(logits, st, sb, T, B, V, lse, labels_flat, label_lens, act_lens, max_label_len,
+                 blank, zero_infinity, costs, loss, loss_scale, ws, nbytes):
+    """asr_ctc_forward, or asr_ctc_forward_lse from the head GEMM's partials."""
+    common = (N.ptr(labels_flat), N.ptr(label_lens), N.ptr(act_lens), int(max_label_len),
+              int(blank), int(bool(zero_infinity)), N.ptr(costs), N.ptr(loss), float(loss_scale),
+              N.ptr(ws), nbytes, N.stream_handle(logits.device))
+    if lse is not None:
+        N.call('asr_ctc_forward_lse', N.ptr(logits), st, sb, T, B, V, N.ptr(lse), lse.shape[0],
+               *common)
+    else:
+        N.call('asr_ctc_forward', N.ptr(logits), st, sb, T, B, V, *common)
+
+
 class LinearCTCFn(torch.autograd.Function):
     """The CTC output layer and its loss as ONE op (LinearND + CTC: ctc.py:30-52
     with linear.py:32-47), for heads whose product is staged in bf16.
@@ -368,17 +396,19 @@ class LinearCTCFn(torch.autograd.Function):
     def forward(ctx, x, weight, bias, drop, labels_flat, label_lens, act_lens, max_label_len,
                 loss_scale, blank, zero_infinity):
         N.require_device(labels_flat, label_lens, act_lens)
-        logits, xo, wo, stage = _linear_forward(x, weight, bias, drop)
+        V = weight.shape[0]
+        M = x.numel() // x.shape[-1]
+        lse = (torch.empty((V + 63) // 64, M, 2, dtype=torch.float32, device=x.device)
+               if _ctc_lse_epilogue(V) and M > 0 else None)
+        logits, xo, wo, stage = _linear_forward(x, weight, bias, drop, lse=lse)
         assert stage, 'LinearCTCFn needs a staged (bf16) output layer'
         B, T, V = logits.shape
         nbytes = N.query('asr_ctc_workspace_bytes', T, B, V, max_label_len)
         ws = _ws(nbytes, logits.device)
         costs = torch.empty(B, dtype=torch.float32, device=logits.device)
         loss = torch.empty(1, dtype=torch.float32, device=logits.device)
-        N.call('asr_ctc_forward', N.ptr(logits), V, T * V, T, B, V, N.ptr(labels_flat),
-               N.ptr(label_lens), N.ptr(act_lens), int(max_label_len), int(blank),
-               int(bool(zero_infinity)), N.ptr(costs), N.ptr(loss), float(loss_scale), N.ptr(ws),
-               nbytes, N.stream_handle(logits.device))
+        _ctc_forward(logits, V, T * V, T, B, V, lse, labels_flat, label_lens, act_lens,
+                     max_label_len, blank, zero_infinity, costs, loss, loss_scale, ws, nbytes)
         ctx.save_for_backward(xo, wo, logits, labels_flat, label_lens, act_lens, ws)
         ctx.meta = (bias, tuple(x.shape), weight, int(max_label_len), int(blank),
                     float(loss_scale), nbytes)
@@ -455,17 +485,17 @@ class LinearCTC32Fn(torch.autograd.Function):
                    N.stream_handle(dev))
             x = xd
         logits = torch.empty(B * T, Vp, dtype=torch.float32, device=dev)
+        lse = (torch.empty((V + 63) // 64, B * T, 2, dtype=torch.float32, device=dev)
+               if _ctc_lse_epilogue(V) and B * T > 0 else None)
         if B * T > 0:
             run_gemm([gemm_problem(operand(x, 0, rowmap(K)), operand(weight, 0, rowmap(K)),
-                                   logits, rowmap(Vp), B * T, V, K, bias=bias)], dev)
+                                   logits, rowmap(Vp), B * T, V, K, bias=bias)], dev, lse=lse)
         nbytes = N.query('asr_ctc_workspace_bytes', T, B, V, max_label_len)
         ws = _ws(nbytes, dev)
         costs = torch.empty(B, dtype=torch.float32, device=dev)
         loss = torch.empty(1, dtype=torch.float32, device=dev)
-        N.call('asr_ctc_forward', N.ptr(logits), Vp, T * Vp, T, B, V, N.ptr(labels_flat),
-               N.ptr(label_lens), N.ptr(act_lens), int(max_label_len), int(blank),
-               int(bool(zero_infinity)), N.ptr(costs), N.ptr(loss), float(loss_scale), N.ptr(ws),
-               nbytes, N.stream_handle(dev))
+        _ctc_forward(logits, Vp, T * Vp, T, B, V, lse, labels_flat, label_lens, act_lens,
+                     max_label_len, blank, zero_infinity, costs, loss, loss_scale, ws, nbytes)
         ctx.save_for_backward(x, logits, labels_flat, label_lens, act_lens, ws)
         ctx.meta = (bias, weight, B, T, V, Vp, int(max_label_len), int(blank), float(loss_scale),
                     nbytes)

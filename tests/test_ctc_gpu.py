@@ -122,14 +122,18 @@ def test_ctc_compact_grad_long_labels_k16(cuda_dev):
 def test_fused_ctc_head_matches_separate_ops(V, K, B, T, cuda_dev, monkeypatch):
     """linear_ctc_loss (LinearND + CTC as one op: the CTC gradient written
     straight into the bf16, column-padded dY operand of the head's GEMMs) vs
-    linear() then ctc_loss() (f32 d logits, then a staging pass): the loss and
-    dX / dW are bitwise equal -- the same f32 values rounded to bf16 once
-    either way -- and the bias gradient, summed in f32 inside the gradient
+    linear() then ctc_loss() (f32 d logits, then a staging pass): with the
+    normaliser formed by the CTC forward's own pass (ASR_CTC_LSE_EPI=0) the
+    loss and dX / dW are bitwise equal -- the same f32 values rounded to bf16
+    once either way -- and the bias gradient, summed in f32 inside the gradient
     pass before the rounding (asr_ctc_backward_bf16_db), equals the unfused
     path's f32 column sum up to summation order (summed from the
-    bf16 operand it was only within 1e-2).  V = 1001 / 10001 exercise the
-    compact gradient (one and eight 8-column chunks per thread), V = 29 the
-    LDS class table; B 32 x T 400 puts 12 rows in each bias-partial block."""
+    bf16 operand it was only within 1e-2).  V = 10001: the default forms the
+    per-frame log-sum-exp in the head GEMM's epilogue (asr_gemm_lse_ws +
+    asr_ctc_forward_lse): the loss within 1e-6, dX / dW within the bf16
+    rounding of dY.  V = 1001 / 10001 exercise the compact gradient (one and
+    eight 8-column chunks per thread), V = 29 the LDS class table; B 32 x T 400
+    puts 12 rows in each bias-partial block."""
     ops = _native()
     rng = np.random.RandomState(11)
     act_lens = np.sort(rng.randint(int(T * 0.75), T + 1, B))[::-1].astype(np.int32)
@@ -147,9 +151,11 @@ def test_fused_ctc_head_matches_separate_ops(V, K, B, T, cuda_dev, monkeypatch):
     try:
         assert ops._linear_stages(B * T, K, V)
         out = {}
-        for fused, db in (('1', '1'), ('0', '1'), ('1', '0'), ('1', '1')):
+        for fused, db, epi in (('1', '1', '1'), ('0', '1', '1'), ('1', '0', '0'), ('1', '1', '0'),
+                               ('1', '1', '1')):
             monkeypatch.setenv('ASR_CTC_HEAD_FUSED', fused)
             monkeypatch.setenv('ASR_CTC_HEAD_DB', db)
+            monkeypatch.setenv('ASR_CTC_LSE_EPI', epi)
             x = x0.clone().requires_grad_(True)
             w = w0.clone().requires_grad_(True)
             b = b0.clone().requires_grad_(True)
@@ -161,12 +167,12 @@ def test_fused_ctc_head_matches_separate_ops(V, K, B, T, cuda_dev, monkeypatch):
             torch.cuda.synchronize()
             r = [loss.detach().clone(), costs.clone(), x.grad.clone(), w.grad.clone(),
                  b.grad.clone() - 0.25]
-            if (fused, db) in out:
-                assert all(torch.equal(p, q) for p, q in zip(out[(fused, db)], r))  # deterministic
-            out[(fused, db)] = r
+            if (fused, db, epi) in out:
+                assert all(torch.equal(p, q) for p, q in zip(out[(fused, db, epi)], r))  # deterministic
+            out[(fused, db, epi)] = r
     finally:
         ops.set_compute_dtype('fp32')
-    f, u, old = out[('1', '1')], out[('0', '1')], out[('1', '0')]
+    f, u, old = out[('1', '1', '0')], out[('0', '1', '1')], out[('1', '0', '0')]
     assert torch.equal(f[0], u[0]) and torch.equal(f[1], u[1])
     assert torch.equal(f[2], u[2]), float((f[2] - u[2]).abs().max())
     assert torch.equal(f[3], u[3]), float((f[3] - u[3]).abs().max())
@@ -174,6 +180,60 @@ def test_fused_ctc_head_matches_separate_ops(V, K, B, T, cuda_dev, monkeypatch):
     assert rel < 2e-5, rel
     rel_old = float((old[4] - u[4]).norm() / u[4].norm())
     assert rel_old < 1e-2, rel_old
+    e = out[('1', '1', '1')]
+    if V <= 1024:
+        assert all(torch.equal(p, q) for p, q in zip(e, f))
+    else:
+        assert abs(float(e[0]) - float(f[0])) <= 1e-6 * abs(float(f[0]))
+        assert float((e[1] - f[1]).abs().max()) <= 1e-6 * float(f[1].abs().max())
+        for i in (2, 3, 4):
+            d = float((e[i] - f[i]).norm() / f[i].norm())
+            assert d < 5e-3, (i, d)
+
+
+@pytest.mark.parametrize('V', [29, 1001, 10001])
+def test_fused_ctc_head_fp32_matches_separate_ops(V, cuda_dev, monkeypatch):
+    """fp32 mode: linear_ctc_loss as one op (LinearCTC32Fn: logits and the CTC
+    gradient with a 4-column-padded pitch so the three products run on the f32
+    fast kernel; at V = 10001 the normaliser from the head GEMM's epilogue) vs
+    linear() then ctc_loss(): loss and costs within 1e-6, dX / dW / db within
+    1e-4 in norm (the two paths' logits differ in the summation order of the
+    product, and the occupancies amplify that: alpha + beta - log P reaches
+    thousands of nats, see above)."""
+    ops = _native()
+    rng = np.random.RandomState(V)
+    B, T, K = 8, 150, 320
+    act_lens = np.sort(rng.randint(int(T * 0.75), T + 1, B))[::-1].astype(np.int32)
+    act_lens[0] = T
+    label_lens = rng.randint(5, 40, B).astype(np.int32)
+    labels = np.concatenate([rng.randint(1, V, l) for l in label_lens]).astype(np.int32)
+    x0 = torch.from_numpy((rng.randn(B, T, K) * 0.5).astype(np.float32)).to(cuda_dev)
+    w0 = torch.from_numpy((rng.randn(V, K) * 0.05).astype(np.float32)).to(cuda_dev)
+    b0 = torch.from_numpy((rng.randn(V) * 0.1).astype(np.float32)).to(cuda_dev)
+    lab = torch.from_numpy(labels).to(cuda_dev)
+    ll = torch.from_numpy(label_lens).to(cuda_dev)
+    al = torch.from_numpy(act_lens).to(cuda_dev)
+    ops.set_compute_dtype('fp32')
+    out = {}
+    for fused in ('1', '0'):
+        monkeypatch.setenv('ASR_CTC_HEAD_FUSED', fused)
+        x = x0.clone().requires_grad_(True)
+        w = w0.clone().requires_grad_(True)
+        b = b0.clone().requires_grad_(True)
+        w.grad = torch.zeros_like(w)
+        b.grad = torch.zeros_like(b)
+        loss, costs = ops.linear_ctc_loss(x, w, b, lab, ll, al, int(label_lens.max()),
+                                          loss_scale=1.0 / B)
+        (loss * 2.0).backward()
+        torch.cuda.synchronize()
+        out[fused] = [loss.detach().clone(), costs.clone(), x.grad.clone(), w.grad.clone(),
+                      b.grad.clone()]
+    f, u = out['1'], out['0']
+    assert abs(float(f[0]) - float(u[0])) <= 1e-6 * abs(float(u[0]))
+    assert float((f[1] - u[1]).abs().max()) <= 1e-6 * float(u[1].abs().max())
+    for i in (2, 3, 4):
+        d = float((f[i] - u[i]).norm() / u[i].norm())
+        assert d < 1e-4, (i, d)
 
 
 @pytest.mark.parametrize('K,Ls', [(1, [0, 5, 31]), (2, [32, 40, 63]), (4, [64, 95, 127, 70]),

@@ -397,7 +397,8 @@ def _f32_run(ops, dev, probs_fn, fast, monkeypatch):
 @pytest.mark.parametrize('M,N,K', [(600, 389, 1032), (128, 128, 32), (300, 260, 203),
                                     (192, 160, 32768), (1030, 777, 1001), (5000, 64, 576),
                                     (4391, 40, 198), (64, 576, 20000), (37, 300, 401)])
-def test_f32_fast_kernel_exact(at, bt, M, N, K, cuda_dev, monkeypatch):
+@pytest.mark.parametrize('stages', ['2', '3'])
+def test_f32_fast_kernel_exact(at, bt, M, N, K, stages, cuda_dev, monkeypatch):
     """gemm_f32_fast (fp32 mode: LDS-DMA staging, v_mfma_f32_16x16x4_f32) in
     every operand layout and all three tile shapes (128 x 128; 256 x 64 for
     N <= 64; 64 x 256 for M <= 64): ragged M / N, K not a multiple of the
@@ -405,7 +406,8 @@ def test_f32_fast_kernel_exact(at, bt, M, N, K, cuda_dev, monkeypatch):
     single k-tile, split-K (few tiles, long K), padded leading dimensions
     (16-B aligned rows), alpha / beta / bias pair.  Small integers: exact, so
     equal to float64 bit for bit (and to gemm_kernel<false>,
-    ASR_GEMM_F32FAST=0)."""
+    ASR_GEMM_F32FAST=0).  stages: the double buffer and the three-stage ring."""
+    monkeypatch.setenv('ASR_GEMM_F32_STAGES', stages)
     ops = _ops()
     ops.set_compute_dtype('fp32')
     rng = np.random.RandomState(M * 5 + N * 3 + K + 17 * at + 19 * bt)
@@ -509,3 +511,41 @@ def test_f32_fast_kernel_taps_match_generic(ci, co, F, sign, cuda_dev, monkeypat
         b = _f32_run(ops, cuda_dev, fn, '0', monkeypatch)[0]
         assert np.abs(b).max() > 0
         np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize('precision,M,N', [('bf16', 700, 10001), ('bf16', 300, 200),
+                                           ('fp32', 700, 10001), ('fp32', 50, 1000),
+                                           ('fp32', 4000, 60)])
+def test_gemm_row_lse_partials(precision, M, N, cuda_dev):
+    """asr_gemm_lse_ws: the epilogue's per-row (max, sum exp) over every
+    64-column slab of the written C (with the bias) -- the 8-wave / 128 x 128
+    bf16 kernels and the f32 fast kernel's three tile shapes: each pair equals
+    the slab's max and sum of exp(C - max) computed from the returned C, and
+    their fold equals logsumexp of the row (1e-6)."""
+    ops = _ops()
+    ops.set_compute_dtype(precision)
+    try:
+        rng = np.random.RandomState(M + N)
+        K = 256
+        x = torch.from_numpy(rng.randn(M, K).astype(np.float32)).to(cuda_dev)
+        w = torch.from_numpy((rng.randn(N, K) * 0.2).astype(np.float32)).to(cuda_dev)
+        b = torch.from_numpy(rng.randn(N).astype(np.float32)).to(cuda_dev)
+        nq = (N + 63) // 64
+        lse = torch.full((nq, M, 2), float('nan'), device=cuda_dev)
+        y, _, _, _ = ops._linear_forward(x, w, b, None, lse=lse)
+        torch.cuda.synchronize()
+        c = y.double().cpu().numpy()
+        part = lse.double().cpu().numpy()
+        pad = np.full((M, nq * 64), -np.inf)
+        pad[:, :N] = c
+        slabs = pad.reshape(M, nq, 64)
+        mx = slabs.max(axis=2).T
+        np.testing.assert_allclose(part[:, :, 0], mx, rtol=1e-6, atol=1e-6)
+        sm = np.exp(slabs - mx.T[:, :, None]).sum(axis=2).T
+        np.testing.assert_allclose(part[:, :, 1], sm, rtol=2e-6)
+        m = part[:, :, 0].max(axis=0)
+        tot = (part[:, :, 1] * np.exp(part[:, :, 0] - m)).sum(axis=0)
+        ref = np.log(np.exp(c - c.max(axis=1, keepdims=True)).sum(axis=1)) + c.max(axis=1)
+        np.testing.assert_allclose(m + np.log(tot), ref, rtol=1e-6)
+    finally:
+        ops.set_compute_dtype('fp32')
