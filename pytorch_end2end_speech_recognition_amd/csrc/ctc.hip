@@ -243,15 +243,25 @@ __global__ void __launch_bounds__(256) ctc_lse_from_parts(const float* __restric
   const long long row = rev ? M - 1 - i : i;
   const int b = (int)(row / T), t = (int)(row % T);
   if (t >= act_lens[b]) return;
+  // 16 slabs' loads in flight per round, then their fold (a load-use chain
+  // per slab ran the pass at one memory latency per slab)
+  constexpr int QB = 16;
   float m = neg_inf(), sm = 0.f;
-  for (int q = 0; q < nslab; ++q) {
-    const float2 pq = *reinterpret_cast<const float2*>(part + 2 * ((long long)q * M + row));
-    if (pq.x > m) {
-      sm = sm * __expf(m - pq.x) + pq.y;   // m = -inf on the first slab: 0 * 0
-      m = pq.x;
-    } else {
-      sm += pq.y * __expf(pq.x - m);
-    }
+  for (int q0 = 0; q0 < nslab; q0 += QB) {
+    float2 pq[QB];
+#pragma unroll
+    for (int k = 0; k < QB; ++k)
+      pq[k] = q0 + k < nslab
+                  ? *reinterpret_cast<const float2*>(part + 2 * ((long long)(q0 + k) * M + row))
+                  : make_float2(neg_inf(), 0.f);
+    float mq = m;
+#pragma unroll
+    for (int k = 0; k < QB; ++k) mq = fmaxf(mq, pq[k].x);
+    sm = m == neg_inf() ? 0.f : sm * __expf(m - mq);
+#pragma unroll
+    for (int k = 0; k < QB; ++k)
+      if (pq[k].x != neg_inf()) sm += pq[k].y * __expf(pq[k].x - mq);
+    m = mq;
   }
   lse_out[row] = m + __logf(sm);
 }
@@ -598,7 +608,11 @@ __global__ void __launch_bounds__(256) ctc_grad(
     for (int v = tid; v < V; v += nth) g[v] = (__expf(x[v] - z) - occ[v]) * scale;
     return;
   } else {
-    for (int s_ = tid; s_ < S; s_ += nth) occ[s_] = ex2(al[s_] + bt[s_] - em[s_] - lp);
+    int* clsT = (int*)(occ + Spad);   // the row's state classes (LDS, see ctc_grad_bf16)
+    for (int s_ = tid; s_ < S; s_ += nth) {
+      occ[s_] = ex2(al[s_] + bt[s_] - em[s_] - lp);
+      clsT[s_] = cls(s_);
+    }
     __syncthreads();
     // representatives (at most 4 states per thread: the host keeps Spad <= 4 * nth)
     int rep_c[4];
@@ -609,18 +623,18 @@ __global__ void __launch_bounds__(256) ctc_grad(
       rep_v[r] = 0.f;
       const int s_ = tid + r * nth;
       if (s_ >= S) continue;
-      const int c = cls(s_);
+      const int c = clsT[s_];
       bool first;
       if ((s_ & 1) == 0) {
         first = s_ == 0;
       } else {
         first = c != blank;
-        for (int q = 1; q < s_ && first; q += 2) first = cls(q) != c;
+        for (int q = 1; q < s_ && first; q += 2) first = clsT[q] != c;
       }
       if (!first) continue;
       float acc = 0.f;
       for (int q = 0; q < S; ++q)
-        if (cls(q) == c) acc += occ[q];
+        if (clsT[q] == c) acc += occ[q];
       rep_c[r] = c;
       rep_v[r] = acc;
     }
@@ -691,8 +705,12 @@ __global__ void __launch_bounds__(256) ctc_grad_bf16(
     uint16_t* __restrict__ grads, long long gst, long long gsb, int gld, int rev,
     int acts_bytes, float* __restrict__ colpart, int rpb, long long nrows) {
   // kTable: occ [V]; else occ [Spad] (+ the representatives' table [V] when NCH > 0)
+  // + the row's state classes [Spad] (the representative search reads them
+  // from LDS: from the label array it was a chain of dependent global loads,
+  // ~S of them per row, on the critical path of every one of a block's rows)
   extern __shared__ __attribute__((aligned(16))) float occ[];
   float* rtab = occ + Spad;
+  int* clsT = (int*)(occ + Spad + (NCH > 0 ? V : 0));
   const int tid = threadIdx.x, nth = blockDim.x;
   const int n8 = gld >> 3;
   const float scale = (grad_scale ? grad_scale[0] : 1.0f) * scale_mul;
@@ -760,7 +778,10 @@ __global__ void __launch_bounds__(256) ctc_grad_bf16(
       }
       __syncthreads();   // occ is rewritten by the next row
     } else {
-      for (int s_ = tid; s_ < S; s_ += nth) occ[s_] = ex2(al[s_] + bt[s_] - em[s_] - lp);
+      for (int s_ = tid; s_ < S; s_ += nth) {
+        occ[s_] = ex2(al[s_] + bt[s_] - em[s_] - lp);
+        clsT[s_] = cls(s_);
+      }
       __syncthreads();
       int rep_c[4];
       float rep_v[4];
@@ -770,18 +791,18 @@ __global__ void __launch_bounds__(256) ctc_grad_bf16(
         rep_v[q4] = 0.f;
         const int s_ = tid + q4 * nth;
         if (s_ >= S) continue;
-        const int c = cls(s_);
+        const int c = clsT[s_];
         bool first;
         if ((s_ & 1) == 0) {
           first = s_ == 0;
         } else {
           first = c != blank;
-          for (int q = 1; q < s_ && first; q += 2) first = cls(q) != c;
+          for (int q = 1; q < s_ && first; q += 2) first = clsT[q] != c;
         }
         if (!first) continue;
         float sum = 0.f;
         for (int q = 0; q < S; ++q)
-          if (cls(q) == c) sum += occ[q];
+          if (clsT[q] == c) sum += occ[q];
         rep_c[q4] = c;
         rep_v[q4] = sum;
       }
@@ -1045,7 +1066,7 @@ extern "C" int asr_ctc_backward(const float* acts, long long stride_t, long long
                        (ctc_row_order() >> 1) & 1);
   else
     hipLaunchKernelGGL(ctc_grad<false>, dim3((unsigned)((long long)B * T)), dim3(threads),
-                       Spad * sizeof(float), s, acts, stride_t, stride_b, T, V, labels_flat,
+                       2 * Spad * sizeof(float), s, acts, stride_t, stride_b, T, V, labels_flat,
                        label_lens, act_lens, ws.offs, blank, Spad, ws.lse, ws.emit, ws.alpha,
                        ws.beta, ws.logp, grad_scale, scale, grads, gstride_t, gstride_b,
                        (ctc_row_order() >> 1) & 1);
@@ -1114,14 +1135,14 @@ static int ctc_backward_bf16_impl(const float* acts, long long stride_t, long lo
     const int n8 = gld >> 3;
     nch = (n8 + threads - 1) / threads;
     nch = nch <= 1 ? 1 : nch <= 2 ? 2 : nch <= 4 ? 4 : nch <= 8 ? 8 : 0;
-    ASR_REQUIRE(nch > 0 && (table || (size_t)(Spad + V) * 4 <= 64 * 1024), ASR_ERR_UNSUPPORTED,
+    ASR_REQUIRE(nch > 0 && (table || (size_t)(2 * Spad + V) * 4 <= 64 * 1024), ASR_ERR_UNSUPPORTED,
                 "ctc_bf16_db: V %d too wide for the in-kernel bias sums", V);
     ctc_bias_grid(T, B, V, &rpb, &nblk);
     colpart = (float*)bws;
   }
   // algorithmic HBM bytes: activations read (4 V) + bf16 gradient written (2 gld) per row
   const int pslot = prof_begin_launch(ASR_PROF_CTC_GRAD, s, (4.0 * V + 2.0 * gld) * B * T, V);
-  const size_t lds = (table ? V : Spad + (dbias ? V : 0)) * sizeof(float);
+  const size_t lds = (table ? V : 2 * Spad + (dbias ? V : 0)) * sizeof(float);
 #define ASR_CTC_G16(TB, NC)                                                                      \
   hipLaunchKernelGGL((ctc_grad_bf16<TB, NC>), dim3((unsigned)nblk), dim3(threads), lds, s, acts,  \
                      stride_t, stride_b, T, V, labels_flat, label_lens, act_lens, ws.offs, blank, \

@@ -257,17 +257,35 @@ __device__ __forceinline__ void store_tile(const Operand& op, void* lds, const f
 // One row's (max, sum exp) over a 64-column slab held by the 16 lanes of a
 // lane group (4 values each, -inf where the column is past N): reduce across
 // the group, lane 0 of it stores.  Every lane of the wave calls it (shuffles).
+// All-reduce over a 16-lane DPP row: lane ^ 1, lane ^ 2 (quad_perm), then the
+// row rotated by 4 and by 8 -- VALU only (ds_bpermute shuffles made the
+// 8-wave kernel's epilogue 66 us slower per 8000 x 10001 product).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float row16_max(float x) {
+  x = fmaxf(x, dpp_f<0xB1>(x));    // quad_perm [1,0,3,2]
+  x = fmaxf(x, dpp_f<0x4E>(x));    // quad_perm [2,3,0,1]
+  x = fmaxf(x, dpp_f<0x124>(x));   // row_ror:4
+  return fmaxf(x, dpp_f<0x128>(x));   // row_ror:8
+}
+__device__ __forceinline__ float row16_sum(float x) {
+  x += dpp_f<0xB1>(x);
+  x += dpp_f<0x4E>(x);
+  x += dpp_f<0x124>(x);
+  return x + dpp_f<0x128>(x);
+}
+
 __device__ __forceinline__ void lse_pair_store(const Problem& pr, int q, int m, const float (&v)[4],
                                                float mx, int lane) {
-#pragma unroll
-  for (int o = 1; o < 16; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  mx = row16_max(mx);
   float sm = 0.f;
   if (mx != neg_inf()) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) sm += __expf(v[e] - mx);
   }
-#pragma unroll
-  for (int o = 1; o < 16; o <<= 1) sm += __shfl_xor(sm, o);
+  sm = row16_sum(sm);
   if ((lane & 15) == 0 && m < pr.M && mx != neg_inf()) {
     float* p = pr.lse + 2 * ((long long)q * pr.M + m);
     p[0] = mx;
@@ -297,6 +315,16 @@ __device__ __forceinline__ void store_acc(const Problem& pr, const f32x4 (&acc)[
   }
   if (pr.lse) {   // row log-sum-exp partials of this wave's 64-column slab
     const int q = (tn + wc) >> 6;
+    float bj[4];    // this lane's four columns' bias, loaded once
+    bool inj[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = tn + wc + j * 16 + (lane & 15);
+      inj[j] = n < pr.N;
+      bj[j] = 0.f;
+      if (inj[j] && pr.bias) bj[j] += pr.bias[n];
+      if (inj[j] && pr.bias2) bj[j] += pr.bias2[n];
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -305,13 +333,7 @@ __device__ __forceinline__ void store_acc(const Problem& pr, const f32x4 (&acc)[
         float mx = neg_inf();
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int n = tn + wc + j * 16 + (lane & 15);
-          v[j] = neg_inf();
-          if (n < pr.N) {
-            v[j] = pr.alpha * acc[i][j][r];
-            if (pr.bias) v[j] += pr.bias[n];
-            if (pr.bias2) v[j] += pr.bias2[n];
-          }
+          v[j] = inj[j] ? pr.alpha * acc[i][j][r] + bj[j] : neg_inf();
           mx = fmaxf(mx, v[j]);
         }
         lse_pair_store(pr, q, tm + wr + i * 16 + 4 * (lane >> 4) + r, v, mx, lane);
@@ -827,6 +849,7 @@ __device__ __forceinline__ int swz32(int k) { return ((k >> 3) & 3) << 2; }
 template <int NB>
 struct StageF32 {
   int x[NB], y[NB], z[NB];
+  int zp[NB];      // K mode, general map: perm[z] (the batch permutation), or z
   unsigned base[NB];
   int valid;
   int tmask, tn;   // R mode: slots whose chunk straddles the end of k, valid elements
@@ -834,7 +857,8 @@ struct StageF32 {
 
 template <int MODE, int ROWS>
 __device__ __forceinline__ void stagef32_init(const Operand& op, StageF32<ROWS / 32>& st,
-                                              int tile0, int nrows, int kbeg, int wave, int lane) {
+                                              int tile0, int nrows, int kbeg, int kend0, int wave,
+                                              int lane) {
   constexpr int NB = ROWS / 32, KPD = 256 / ROWS, LPK = ROWS / 4;
   st.valid = 0;
   st.tmask = 0;
@@ -853,7 +877,8 @@ __device__ __forceinline__ void stagef32_init(const Operand& op, StageF32<ROWS /
         st.z[i] = row;
         st.base[i] = 0u;
       } else {
-        const long long off = row < nrows ? row_off_np(op.map, row) : -1;
+        // rows are fixed in R mode: the batch permutation is applied once here
+        const long long off = row < nrows ? row_off(op.map, row) : -1;
         if (off < 0) st.valid &= ~(1 << i);
         st.base[i] = off >= 0 ? (unsigned)(off * 4) : 0u;
         st.x[i] = 4 * c;
@@ -877,6 +902,7 @@ __device__ __forceinline__ void stagef32_init(const Operand& op, StageF32<ROWS /
         st.z[i] = k / op.map.rows_per_b;
         st.y[i] = k - st.z[i] * op.map.rows_per_b;
         st.x[i] = 0;
+        st.zp[i] = (op.map.perm && k < kend0) ? op.map.perm[st.z[i]] : st.z[i];
       }
     }
   }
@@ -925,13 +951,18 @@ __device__ __forceinline__ void stagef32(const Operand& op, __amdgpu_buffer_rsrc
       } else {
         const int tp = st.y[i] * op.map.t_mul + op.map.t_add;
         if (k < kend && tp >= 0 && tp < op.map.t_limit)
-          voff = (unsigned)(((long long)st.z[i] * op.map.stride_b +
+          voff = (unsigned)(((long long)st.zp[i] * op.map.stride_b +
                              (long long)tp * op.map.stride_t) * 4) + st.base[i];
         st.y[i] += FBK32;
+        bool moved = false;
         while (st.y[i] >= op.map.rows_per_b) {
           st.y[i] -= op.map.rows_per_b;
           ++st.z[i];
+          moved = true;
         }
+        // the permuted utterance of this slot's next k-row, read only when it
+        // changes and exists (k-tiles cross an utterance every rows_per_b / 32)
+        if (moved) st.zp[i] = (op.map.perm && k + FBK32 < kend) ? op.map.perm[st.z[i]] : st.z[i];
       }
     }
     const unsigned lds_addr = (unsigned)(uintptr_t)(lds_void_t*)(lds_tile + blk * 1024);
@@ -1046,8 +1077,8 @@ __global__ void __launch_bounds__(NT) gemm_f32_fast(Params P) {
   const int nk = (kend - kbeg + FBK32 - 1) / FBK32;
   StageF32<TM / 32> sa;
   StageF32<TN / 32> sb;
-  stagef32_init<AMODE, TM>(pr.a, sa, tm, pr.M, kbeg, w, lane);
-  stagef32_init<BMODE, TN>(pr.b, sb, tn, pr.N, kbeg, w, lane);
+  stagef32_init<AMODE, TM>(pr.a, sa, tm, pr.M, kbeg, kend, w, lane);
+  stagef32_init<BMODE, TN>(pr.b, sb, tn, pr.N, kbeg, kend, w, lane);
   auto mma = [&](const char* cur) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -1577,6 +1608,19 @@ __device__ __forceinline__ void epi8(const Problem& pr, const RowMap& cm, bool r
   const bool plain = cm.rows_per_b == 0x7fffffff && cm.t_mul == 1 && cm.t_add == 0 &&
                      cm.t_limit == 0x7fffffff && !cm.perm;
   const bool bias_vec = ((uintptr_t)pr.bias & 15) == 0 && ((uintptr_t)pr.bias2 & 15) == 0;
+  // the row-LSE pass: this lane's four columns (fixed over the quarters) and
+  // their bias, loaded once
+  float lb[4] = {0.f, 0.f, 0.f, 0.f};
+  bool lin[4] = {false, false, false, false};
+  if (!raw && pr.lse) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int n = tn + wc + 4 * (lane & 15) + e;
+      lin[e] = n < pr.N;
+      if (lin[e] && pr.bias) lb[e] += pr.bias[n];
+      if (lin[e] && pr.bias2) lb[e] += pr.bias2[n];
+    }
+  }
 #pragma unroll
   for (int h = 0; h < 4; ++h) {
     __syncthreads();   // LDS free (k-loop done / previous quarter read back)
@@ -1591,19 +1635,13 @@ __device__ __forceinline__ void epi8(const Problem& pr, const RowMap& cm, bool r
     if (!raw && pr.lse) {   // row log-sum-exp partials of this wave's 64-column slab
       for (int it = 0; it < 8; ++it) {
         const int row = it * 4 + (lane >> 4), ch = lane & 15;
-        const int n = tn + wc + 4 * ch;
         const float4 t4 = *reinterpret_cast<const float4*>(tile + row * EP8 + 4 * ch);
         const float tv[4] = {t4.x, t4.y, t4.z, t4.w};
         float v[4];
         float mx = neg_inf();
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          v[e] = neg_inf();
-          if (n + e < pr.N) {
-            v[e] = tv[e] * pr.alpha;
-            if (pr.bias) v[e] += pr.bias[n + e];
-            if (pr.bias2) v[e] += pr.bias2[n + e];
-          }
+          v[e] = lin[e] ? tv[e] * pr.alpha + lb[e] : neg_inf();
           mx = fmaxf(mx, v[e]);
         }
         lse_pair_store(pr, (tn + wc) >> 6, tm + wr + 32 * h + row, v, mx, lane);
@@ -2285,13 +2323,15 @@ int fast_stages() {
 }
 
 // The f32 fast path's operand mode pair, or -1 (gemm_kernel<false>).  Every
-// operand f32 with a known extent < 2 GiB, 16-B aligned rows, no batch
-// permutation and the division-free staging (taps only on a plain map).
-// ASR_GEMM_F32FAST=0 keeps the generic kernel.
+// operand f32 with a known extent < 2 GiB and 16-B aligned rows; a batch
+// permutation is allowed, taps need a plain map.  ASR_GEMM_F32FAST=0 keeps
+// the generic kernel.
 bool fast32_operand_ok(const asr_operand_t& o, const Operand& op, long long batch_stride,
                        int batch, int kdim) {
   if (o.dtype != ASR_DT_F32 || o.bytes <= 0 || o.bytes > 0x7fff0000LL) return false;
-  if (o.map.perm || !op.sf) return false;
+  // the division-free staging (taps only on a plain map); a batch permutation
+  // is applied once per R-mode row and once per utterance crossing in K mode
+  if (o.tap_group && !op.plain) return false;
   if (!aligned16(o.ptr) || o.map.stride_t % 4 || o.map.stride_b % 4) return false;
   if (batch > 1 && batch_stride % 4) return false;
   (void)kdim;   // R mode: a k extent that is not a multiple of 4 is zero-filled in LDS

@@ -549,3 +549,36 @@ def test_gemm_row_lse_partials(precision, M, N, cuda_dev):
         np.testing.assert_allclose(m + np.log(tot), ref, rtol=1e-6)
     finally:
         ops.set_compute_dtype('fp32')
+
+
+def test_f32_fast_kernel_batch_permutation_matches_generic(cuda_dev, monkeypatch):
+    """gemm_f32_fast with the encoder's batch permutation in the row map (the
+    first BLSTM layer of a length-sorted batch): an R-mode operand (rows
+    permuted once per slot) and a K-mode operand (the permuted utterance
+    re-read at every utterance crossing, frame stride 2 / offset 1 / limit),
+    bitwise equal to gemm_kernel<false> on small integers."""
+    ops = _ops()
+    ops.set_compute_dtype('fp32')
+    rng = np.random.RandomState(5)
+    nb, T, rpb, D, Nn = 7, 90, 45, 132, 200
+    perm = torch.from_numpy(rng.permutation(nb).astype(np.int32)).to(cuda_dev)
+    x = torch.from_numpy(rng.randint(-3, 4, (nb * T, D)).astype(np.float32)).to(cuda_dev)
+    w = torch.from_numpy(rng.randint(-3, 4, (Nn, D)).astype(np.float32)).to(cuda_dev)
+    g = torch.from_numpy(rng.randint(-3, 4, (nb * rpb, Nn)).astype(np.float32)).to(cuda_dev)
+    M = nb * rpb
+
+    def fwd():
+        c = torch.zeros(M, Nn, device=cuda_dev)
+        return [ops.gemm_problem(ops.operand(x, 0, ops.rowmap(D, T * D, rpb, 2, 1, T, perm=perm)),
+                                 ops.operand(w, 0, ops.rowmap(D)), c, ops.rowmap(Nn), M, Nn, D)], [c]
+
+    def wgrad():
+        c = torch.zeros(Nn, D, device=cuda_dev)
+        return [ops.gemm_problem(ops.operand(g, 1, ops.rowmap(Nn)),
+                                 ops.operand(x, 1, ops.rowmap(D, T * D, rpb, 2, 1, T, perm=perm)),
+                                 c, ops.rowmap(D), Nn, D, M)], [c]
+    for fn in (fwd, wgrad):
+        a = _f32_run(ops, cuda_dev, fn, '1', monkeypatch)[0]
+        b = _f32_run(ops, cuda_dev, fn, '0', monkeypatch)[0]
+        assert np.abs(b).max() > 0
+        np.testing.assert_array_equal(a, b)
