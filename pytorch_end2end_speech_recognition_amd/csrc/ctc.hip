@@ -694,7 +694,7 @@ __device__ __forceinline__ void take8(const float (&v)[12], float (&o)[8]) {
 // accumulate in registers; the occupancy terms of the class representatives
 // go to an LDS table [V] -- one representative per class and row, rows
 // separated by barriers, so every sum has a fixed order (deterministic).
-template <bool kTable, int NCH>
+template <bool kTable, int NCH, bool AL = false>
 __global__ void __launch_bounds__(256) ctc_grad_bf16(
     const float* __restrict__ acts, long long st, long long sb, int T, int V,
     const int32_t* __restrict__ labels, const int32_t* __restrict__ label_lens,
@@ -812,24 +812,34 @@ __global__ void __launch_bounds__(256) ctc_grad_bf16(
       // activations' end they read zeros) and keeps elements a .. a + 7
       if (acts_bytes) {
         const long long xo = (long long)t * st + (long long)b * sb;   // row start (elements)
-        const int a = (int)(xo & 3);
+        const int a = AL ? 0 : (int)(xo & 3);
         const __amdgpu_buffer_rsrc_t rs =
             __builtin_amdgcn_make_buffer_rsrc((void*)acts, 0, acts_bytes, 0x00020000);
         const unsigned base = (unsigned)((xo - a) * 4);
-        auto chunk = [&](int k, float* ac) {
-          float v[12];
+        // AL (16-B aligned rows: the fused head's padded logits pitch): two 16-B
+        // loads per 8 columns and no window shift -- the shift over a runtime a
+        // is folded by the compiler into a dynamically indexed array, i.e.
+        // scratch memory per lane (48 B per chunk in flight)
+        auto load12 = [&](int k, float (&v)[12]) {
 #pragma unroll
-          for (int q = 0; q < 3; ++q) {
+          for (int q = 0; q < (AL ? 2 : 3); ++q) {
             const f32x4 w = __builtin_bit_cast(
                 f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, base + (unsigned)(32 * k + 16 * q), 0, 0));
             v[4 * q] = w[0]; v[4 * q + 1] = w[1]; v[4 * q + 2] = w[2]; v[4 * q + 3] = w[3];
           }
+        };
+        auto chunk_v = [&](int k, const float (&v)[12], float* ac) {
           float o[8];
-          switch (a) {   // row-uniform
-            case 0: take8<0>(v, o); break;
-            case 1: take8<1>(v, o); break;
-            case 2: take8<2>(v, o); break;
-            default: take8<3>(v, o); break;
+          if constexpr (AL) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] = v[j];
+          } else {
+            switch (a) {   // row-uniform
+              case 0: take8<0>(v, o); break;
+              case 1: take8<1>(v, o); break;
+              case 2: take8<2>(v, o); break;
+              default: take8<3>(v, o); break;
+            }
           }
           const int c0 = 8 * k;
           unsigned w4[4];
@@ -843,11 +853,24 @@ __global__ void __launch_bounds__(256) ctc_grad_bf16(
           }
           reinterpret_cast<uint4*>(g)[k] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
         };
+        auto chunk = [&](int k, float* ac) {
+          float v[12];
+          load12(k, v);
+          chunk_v(k, v, ac);
+        };
         if constexpr (NCH > 0) {
+          // every chunk's loads in flight before the first use (the buffer loads
+          // may alias the gradient stores as far as the compiler knows)
+          float vv[NCH][12];
 #pragma unroll
           for (int j = 0; j < NCH; ++j) {
             const int k = tid + j * nth;
-            if (k < n8) chunk(k, acc[j]);
+            if (k < n8) load12(k, vv[j]);
+          }
+#pragma unroll
+          for (int j = 0; j < NCH; ++j) {
+            const int k = tid + j * nth;
+            if (k < n8) chunk_v(k, vv[j], acc[j]);
           }
         } else {
           int i = tid;
@@ -1079,7 +1102,13 @@ extern "C" int asr_ctc_backward(const float* acts, long long stride_t, long long
 // rows per block and blocks of the column-partial pass.
 static void ctc_bias_grid(int T, int B, int V, int* rpb, int* nblk) {
   const long long rows = (long long)B * T;
-  const long long target = V <= 1024 ? 1024 : 512;   // partial rows: nblk x gld f32
+  // partial rows: nblk x gld f32.  A block's rows run one after another, so
+  // fewer rows per block hide more latency at the price of partial traffic:
+  // at V = 10001, 534 / 1067 / 2134 blocks measured 265 + 13 / 202 + 20 /
+  // 185 + 33 us (gradient + column sums).  ASR_CTC_BIAS_BLOCKS: the target (A/B)
+  static const long long env_target =
+      getenv("ASR_CTC_BIAS_BLOCKS") ? atoll(getenv("ASR_CTC_BIAS_BLOCKS")) : 0;
+  const long long target = env_target > 0 ? env_target : 1024;
   long long r = rows / target;
   if (r < 1) r = 1;
   if (r > 64) r = 64;
@@ -1119,11 +1148,18 @@ static int ctc_backward_bf16_impl(const float* acts, long long stride_t, long lo
   const int threads = table ? 64 : 256;
   // aligned 16-B buffer loads of the activation rows (compact form) when the
   // activations are one dense [B][T][V] or [T][B][V] block below 2 GiB
-  const long long nb = 4LL * B * T * V;
+  // (or [B][T] rows of a padded pitch >= V: the fused heads' logits); the
+  // buffer's extent ends with the last row.  al: every row 16-B aligned
+  const long long nb =
+      stride_t >= 0 && stride_b >= 0
+          ? 4LL * ((long long)(B - 1) * stride_b + (long long)(T - 1) * stride_t + V)
+          : 0;
   const bool dense = (stride_t == V && stride_b == (long long)T * V) ||
-                     (stride_b == V && stride_t == (long long)B * V);
-  const int abytes = (!table && dense && nb < 0x7fffff00LL && ((uintptr_t)acts & 15) == 0)
+                     (stride_b == V && stride_t == (long long)B * V) ||
+                     (stride_t >= V && stride_b == (long long)T * stride_t);
+  const int abytes = (!table && dense && nb > 0 && nb < 0x7fffff00LL && ((uintptr_t)acts & 15) == 0)
                          ? (int)nb : 0;
+  const bool al = abytes && stride_t % 4 == 0 && stride_b % 4 == 0;
   const long long rows = (long long)B * T;
   const int rev = (ctc_row_order() >> 1) & 1;
   int rpb = 1, nblk = (int)rows, nch = 0;
@@ -1134,7 +1170,7 @@ static int ctc_backward_bf16_impl(const float* acts, long long stride_t, long lo
                 asr_ctc_bias_workspace_bytes(T, B, V, gld));
     const int n8 = gld >> 3;
     nch = (n8 + threads - 1) / threads;
-    nch = nch <= 1 ? 1 : nch <= 2 ? 2 : nch <= 4 ? 4 : nch <= 8 ? 8 : 0;
+    nch = nch <= 1 ? 1 : nch <= 2 ? 2 : nch <= 4 ? 4 : nch <= 5 ? 5 : nch <= 8 ? 8 : 0;
     ASR_REQUIRE(nch > 0 && (table || (size_t)(2 * Spad + V) * 4 <= 64 * 1024), ASR_ERR_UNSUPPORTED,
                 "ctc_bf16_db: V %d too wide for the in-kernel bias sums", V);
     ctc_bias_grid(T, B, V, &rpb, &nblk);
@@ -1143,23 +1179,30 @@ static int ctc_backward_bf16_impl(const float* acts, long long stride_t, long lo
   // algorithmic HBM bytes: activations read (4 V) + bf16 gradient written (2 gld) per row
   const int pslot = prof_begin_launch(ASR_PROF_CTC_GRAD, s, (4.0 * V + 2.0 * gld) * B * T, V);
   const size_t lds = (table ? V : 2 * Spad + (dbias ? V : 0)) * sizeof(float);
-#define ASR_CTC_G16(TB, NC)                                                                      \
-  hipLaunchKernelGGL((ctc_grad_bf16<TB, NC>), dim3((unsigned)nblk), dim3(threads), lds, s, acts,  \
-                     stride_t, stride_b, T, V, labels_flat, label_lens, act_lens, ws.offs, blank, \
-                     Spad, ws.lse, ws.emit, ws.alpha, ws.beta, ws.logp, grad_scale, scale, grads, \
-                     gstride_t, gstride_b, gld, rev, abytes, colpart, rpb, rows)
+#define ASR_CTC_G16A(TB, NC, A)                                                                  \
+  hipLaunchKernelGGL((ctc_grad_bf16<TB, NC, A>), dim3((unsigned)nblk), dim3(threads), lds, s,     \
+                     acts, stride_t, stride_b, T, V, labels_flat, label_lens, act_lens, ws.offs,  \
+                     blank, Spad, ws.lse, ws.emit, ws.alpha, ws.beta, ws.logp, grad_scale, scale, \
+                     grads, gstride_t, gstride_b, gld, rev, abytes, colpart, rpb, rows)
+#define ASR_CTC_G16(TB, NC)                  \
+  do {                                       \
+    if (al) ASR_CTC_G16A(TB, NC, true);      \
+    else ASR_CTC_G16A(TB, NC, false);        \
+  } while (0)
   if (table) {
-    if (nch) ASR_CTC_G16(true, 1);
-    else ASR_CTC_G16(true, 0);
+    if (nch) ASR_CTC_G16A(true, 1, false);
+    else ASR_CTC_G16A(true, 0, false);
   } else {
     switch (nch) {
       case 0: ASR_CTC_G16(false, 0); break;
       case 1: ASR_CTC_G16(false, 1); break;
       case 2: ASR_CTC_G16(false, 2); break;
       case 4: ASR_CTC_G16(false, 4); break;
+      case 5: ASR_CTC_G16(false, 5); break;
       default: ASR_CTC_G16(false, 8); break;
     }
   }
+#undef ASR_CTC_G16A
 #undef ASR_CTC_G16
   ASR_LAUNCH_CHECK();
   prof_end_launch(ASR_PROF_CTC_GRAD, pslot, s);

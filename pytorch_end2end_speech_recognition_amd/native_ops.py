@@ -178,16 +178,24 @@ def _linear_stages(M, K, Nout):
         flops >= _STAGE_FLOPS or (Nout % 8 != 0 and flops >= _STAGE_FLOPS_RAGGED))
 
 
-def _linear_forward(x, weight, bias, drop, lse=None):
+def _linear_forward(x, weight, bias, drop, lse=None, ld=None):
     """y = dropout(x) W^T + b (f32 [..., Nout]); returns (y, xo, wo, stage):
     the GEMM operands the backward reuses (bf16 staged copies when stage).
-    lse: row log-sum-exp partials of y (run_gemm)."""
+    lse: row log-sum-exp partials of y (run_gemm).  ld: y's row pitch (>=
+    Nout; y is then a strided view of [M, ld] storage)."""
     N.require_device(x, weight)
     x = x.contiguous()
     K = x.shape[-1]
     Nout = weight.shape[0]
     M = x.numel() // K
-    y = torch.empty(*x.shape[:-1], Nout, dtype=torch.float32, device=x.device)
+    ld = Nout if ld is None else int(ld)
+    if ld == Nout:
+        y = torch.empty(*x.shape[:-1], Nout, dtype=torch.float32, device=x.device)
+    else:
+        ybuf = torch.empty(M * ld, dtype=torch.float32, device=x.device)
+        lead = tuple(x.shape[:-1])
+        strides = tuple(int(np.prod(lead[i + 1:])) * ld for i in range(len(lead))) + (1,)
+        y = torch.as_strided(ybuf, lead + (Nout,), strides)
     stage = _linear_stages(M, K, Nout)
     fused_drop = drop is not None and stage and K % 8 == 0
     if drop is not None and not fused_drop:        # materialise dropout(x) first
@@ -212,7 +220,7 @@ def _linear_forward(x, weight, bias, drop, lse=None):
         xo, wo = x, weight
     if M > 0:
         p = gemm_problem(operand(xo, 0, rowmap(Kp)), operand(wo, 0, rowmap(Kp)), y,
-                         rowmap(Nout), M, Nout, Kp, bias=bias)
+                         rowmap(ld), M, Nout, Kp, bias=bias)
         run_gemm([p], x.device, lse=lse)
     return y, xo, wo, stage
 
@@ -400,15 +408,21 @@ class LinearCTCFn(torch.autograd.Function):
         M = x.numel() // x.shape[-1]
         lse = (torch.empty((V + 63) // 64, M, 2, dtype=torch.float32, device=x.device)
                if _ctc_lse_epilogue(V) and M > 0 else None)
-        logits, xo, wo, stage = _linear_forward(x, weight, bias, drop, lse=lse)
+        # wide heads: logits pitch V rounded up to 4 columns, so the gradient
+        # pass reads 16-B aligned rows (ctc_grad_bf16's aligned form; a narrow
+        # head keeps the dense layout, whose values the unfused ops reproduce
+        # bit for bit)
+        logits, xo, wo, stage = _linear_forward(x, weight, bias, drop, lse=lse,
+                                                ld=(V + 3) // 4 * 4 if V > 1024 else V)
         assert stage, 'LinearCTCFn needs a staged (bf16) output layer'
         B, T, V = logits.shape
         nbytes = N.query('asr_ctc_workspace_bytes', T, B, V, max_label_len)
         ws = _ws(nbytes, logits.device)
         costs = torch.empty(B, dtype=torch.float32, device=logits.device)
         loss = torch.empty(1, dtype=torch.float32, device=logits.device)
-        _ctc_forward(logits, V, T * V, T, B, V, lse, labels_flat, label_lens, act_lens,
-                     max_label_len, blank, zero_infinity, costs, loss, loss_scale, ws, nbytes)
+        _ctc_forward(logits, logits.stride(1), logits.stride(0), T, B, V, lse, labels_flat,
+                     label_lens, act_lens, max_label_len, blank, zero_infinity, costs, loss,
+                     loss_scale, ws, nbytes)
         ctx.save_for_backward(xo, wo, logits, labels_flat, label_lens, act_lens, ws)
         ctx.meta = (bias, tuple(x.shape), weight, int(max_label_len), int(blank),
                     float(loss_scale), nbytes)
@@ -428,7 +442,8 @@ class LinearCTCFn(torch.autograd.Function):
         dev = logits.device
         dyo = torch.empty(B * T, Np, dtype=torch.bfloat16, device=dev)
         g = g_loss.contiguous() if g_loss is not None else None
-        args = (N.ptr(logits), V, T * V, T, B, V, N.ptr(labels_flat), N.ptr(label_lens),
+        args = (N.ptr(logits), logits.stride(1), logits.stride(0), T, B, V, N.ptr(labels_flat),
+                N.ptr(label_lens),
                 N.ptr(act_lens), max_label_len, blank, N.ptr(g),
                 loss_scale if g is not None else 0.0, N.ptr(dyo), Np, T * Np, Np, N.ptr(ws), nbytes)
         # the bias gradient: f32 column sums formed inside the gradient pass before
