@@ -1276,9 +1276,12 @@ __device__ __forceinline__ void pd_publish(int* ctr) {
 // NQ: 64-lane groups of the attention dim (A <= 64 NQ).  SA, SE, SD, SK: the
 // attention / encoder / decoder dims and the conv width fixed at compile time
 // (0 = from Dims): the production instantiation folds its whole geometry.
-template <int CC, int NQ, int SA, int SE, int SD, int SK>
+// F32 (fp32 mode): Wcat and x_t in f32, the cell product on
+// v_mfma_f32_16x16x4_f32 (each of the six cell waves holds its tile's K half as
+// 8 PD_KMAX f32 fragments: k-step s of the half is k = 4 (kh + 2 s) + lane / 16).
+template <int CC, int NQ, int SA, int SE, int SD, int SK, bool F32 = false>
 __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
-    Dims dd, const uint16_t* __restrict__ wcat, const float* __restrict__ pre_emb,
+    Dims dd, const void* __restrict__ wcat_v, const float* __restrict__ pre_emb,
     const float* __restrict__ h0, const float* __restrict__ enc, const float* __restrict__ enc_a,
     const int32_t* __restrict__ lens, const float* __restrict__ w_dec,
     const float* __restrict__ w_conv, const float* __restrict__ conv_w,
@@ -1317,17 +1320,28 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
   const int C = CC ? CC : d.C;
 
   // ---- once per pass: weights and the utterance's constant rows
-  bf16x8 wf[PD_KMAX];
+  constexpr int KM32 = F32 ? 8 * PD_KMAX : 1;
+  bf16x8 wf[F32 ? 1 : PD_KMAX];
+  float wf32[KM32];
   {
     const int tile = wave >> 1, kh = wave & 1;
     const int gr = tile * 16 + (lane & 15), q = gr / UPW, u = gr % UPW;
     const bool ok = wave < 6 && q < 4 && u < nu;
-    const uint16_t* wr = wcat + (long long)(ok ? q * d.D + u0 + u : 0) * ED;
+    if constexpr (F32) {
+      const float* wr = (const float*)wcat_v + (long long)(ok ? q * d.D + u0 + u : 0) * ED;
 #pragma unroll
-    for (int i = 0; i < PD_KMAX; ++i) {
-      const int k = (kh + 2 * i) * 32 + 8 * (lane >> 4);
-      wf[i] = (ok && kh + 2 * i < NKB && k < ED) ? load_bf16x8(wr + k)
-                                                  : as_bf16x8(u16x8{0, 0, 0, 0, 0, 0, 0, 0});
+      for (int i = 0; i < KM32; ++i) {
+        const int k = 4 * (kh + 2 * i) + (lane >> 4);
+        wf32[i] = (ok && k < ED) ? wr[k] : 0.f;
+      }
+    } else {
+      const uint16_t* wr = (const uint16_t*)wcat_v + (long long)(ok ? q * d.D + u0 + u : 0) * ED;
+#pragma unroll
+      for (int i = 0; i < PD_KMAX; ++i) {
+        const int k = (kh + 2 * i) * 32 + 8 * (lane >> 4);
+        wf[i] = (ok && kh + 2 * i < NKB && k < ED) ? load_bf16x8(wr + k)
+                                                    : as_bf16x8(u16x8{0, 0, 0, 0, 0, 0, 0, 0});
+      }
     }
   }
   float ea[PD_FPW][NQ];
@@ -1376,7 +1390,8 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
       __syncthreads();
       if (!s_ok) return;
       PD_TR(33);
-      // x_t rows of the 4 utterances, rounded to bf16 once (the MFMA A operand)
+      // x_t rows of the 4 utterances, rounded to bf16 once (the MFMA A operand;
+      // f32 as they are with F32)
       uint16_t* xsb = reinterpret_cast<uint16_t*>(&L[G.xs]);
       const int nv = ED / 4;
       for (int i = tid; i < PD_SLOTS * nv; i += PD_THREADS) {
@@ -1385,13 +1400,35 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
         if (bb < d.B)
           v = __builtin_amdgcn_raw_buffer_load_b128(
               rx, (unsigned)((((long long)bb * d.S + t) * ED + 4 * k4) * 4), 0, 16);
-        const unsigned lo = f2bf(__uint_as_float(v[0])) | ((unsigned)f2bf(__uint_as_float(v[1])) << 16);
-        const unsigned hi = f2bf(__uint_as_float(v[2])) | ((unsigned)f2bf(__uint_as_float(v[3])) << 16);
-        *reinterpret_cast<uint2*>(xsb + sl * ED + 4 * k4) = make_uint2(lo, hi);
+        if constexpr (F32) {
+          *reinterpret_cast<pd_u32x4*>(&L[G.xs + sl * ED + 4 * k4]) = v;
+        } else {
+          const unsigned lo = f2bf(__uint_as_float(v[0])) | ((unsigned)f2bf(__uint_as_float(v[1])) << 16);
+          const unsigned hi = f2bf(__uint_as_float(v[2])) | ((unsigned)f2bf(__uint_as_float(v[3])) << 16);
+          *reinterpret_cast<uint2*>(xsb + sl * ED + 4 * k4) = make_uint2(lo, hi);
+        }
       }
       __syncthreads();
       PD_TR(34);
-      if (wave < 6) {
+      if constexpr (F32) {
+        if (wave < 6) {
+          const int kh = wave & 1, mm = lane & 15;
+          f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int i = 0; i < KM32; ++i) {
+            if (4 * (kh + 2 * i) < ED) {   // wave-uniform
+              const int k = 4 * (kh + 2 * i) + (lane >> 4);
+              const float a = (mm < PD_SLOTS && k < ED) ? L[G.xs + mm * ED + k] : 0.f;
+              if (i & 1) acc1 = mfma_f32(a, wf32[i], acc1);
+              else acc0 = mfma_f32(a, wf32[i], acc0);
+            }
+          }
+          if (lane < 16) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) L[G.part + (wave * PD_SLOTS + r) * 16 + lane] = acc0[r] + acc1[r];
+          }
+        }
+      } else if (wave < 6) {
         const int kh = wave & 1, mm = lane & 15;
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -1630,7 +1667,7 @@ struct PbGeom {
       cmb, cmbn, red, total;   // LDS floats
 };
 
-__host__ __device__ inline PbGeom pb_geom(const Dims& d) {
+__host__ __device__ inline PbGeom pb_geom(const Dims& d, bool f32 = false) {
   PbGeom g;
   g.UPW = (d.D + PD_MEMBERS - 1) / PD_MEMBERS;
   g.FCH = (d.T + PD_CHUNKS - 1) / PD_CHUNKS;
@@ -1662,9 +1699,9 @@ __host__ __device__ inline PbGeom pb_geom(const Dims& d) {
   g.carry = o; o += g.FCH;
   g.wd = o; o += d.A;
   o = (o + 3) & ~3;
-  {  // one region, used by phase H (bf16 dgates rows [4][G4]), F (the chunk's
-     // d enc_a rows) and G (dF window [W][C] + the W_dec^T dWd partials)
-    int un = PD_SLOTS * g.G4 / 2 + 4;
+  {  // one region, used by phase H (bf16 dgates rows [4][G4], f32 with f32), F
+     // (the chunk's d enc_a rows) and G (dF window [W][C] + the W_dec^T dWd partials)
+    int un = f32 ? PD_SLOTS * g.G4 + 4 : PD_SLOTS * g.G4 / 2 + 4;
     g.AP = d.A + 1;   // the [frames][A] tiles' row stride (odd: no bank conflicts down a column)
     un = max(un, g.FCH * g.AP);
     un = max(un, (8 + g.W) * d.C + PD_SLOTS * g.UPW * 8);   // dF window after 8 zero rows
@@ -1683,9 +1720,12 @@ __host__ __device__ inline PbGeom pb_geom(const Dims& d) {
   return g;
 }
 
-template <int CC, int NQ, int SA, int SE, int SD, int SK>
+// F32 (fp32 mode): Wcat^T and dgates in f32, r on v_mfma_f32_16x16x4_f32 (each
+// wave holds its column tile's K quarter as f32 fragments: k-step s of the
+// quarter is k = 4 (kq KQ32 + s) + lane / 16).
+template <int CC, int NQ, int SA, int SE, int SD, int SK, bool F32 = false>
 __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
-    Dims dd, const uint16_t* __restrict__ wcatT, const float* __restrict__ enc,
+    Dims dd, const void* __restrict__ wcatT_v, const float* __restrict__ enc,
     const float* __restrict__ enc_a, const int32_t* __restrict__ lens,
     const float* __restrict__ w_dec, const float* __restrict__ w_conv,
     const float* __restrict__ conv_w, const float* __restrict__ vw,
@@ -1705,7 +1745,7 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
   if (SK) d.K = SK;
   __shared__ int s_ok;
   __shared__ float s_sdot;
-  const PbGeom G = pb_geom(d);
+  const PbGeom G = pb_geom(d, F32);
   const int UPW = G.UPW, FCH = G.FCH, ECW = G.ECW, ED = G.ED, G4 = G.G4, NPW = G.NPW;
   const int half = G.half, KW = G.W;
   const int grp = blockIdx.x % PD_GROUPS, m = blockIdx.x / PD_GROUPS;
@@ -1735,18 +1775,30 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
   float dc_reg = 0.f;
 
   // ---- once per pass
-  bf16x8 wf[PB_KQ];
+  constexpr int KB32 = F32 ? 8 * PB_KQ : 1;
+  const int KQ32 = ((G4 + 3) / 4 + 3) / 4;   // f32 k-steps per K quarter
+  bf16x8 wf[F32 ? 1 : PB_KQ];
+  float wf32[KB32];
   {
     const int tile = wave & 1, kq = wave >> 1;
     const int c16 = tile * 16 + (lane & 15);
     const bool ok = c16 < nn;
-    const uint16_t* wr = wcatT + (long long)(ok ? n0 + c16 : 0) * G4;
+    if constexpr (F32) {
+      const float* wr = (const float*)wcatT_v + (long long)(ok ? n0 + c16 : 0) * G4;
 #pragma unroll
-    for (int i = 0; i < PB_KQ; ++i) {
-      const int kb = kq * G.KQ + i;
-      const int k = kb * 32 + 8 * (lane >> 4);
-      wf[i] = (ok && i < G.KQ && kb < G.NKB && k < G4)
-                  ? load_bf16x8(wr + k) : as_bf16x8(u16x8{0, 0, 0, 0, 0, 0, 0, 0});
+      for (int i = 0; i < KB32; ++i) {
+        const int k = 4 * (kq * KQ32 + i) + (lane >> 4);
+        wf32[i] = (ok && i < KQ32 && k < G4) ? wr[k] : 0.f;
+      }
+    } else {
+      const uint16_t* wr = (const uint16_t*)wcatT_v + (long long)(ok ? n0 + c16 : 0) * G4;
+#pragma unroll
+      for (int i = 0; i < PB_KQ; ++i) {
+        const int kb = kq * G.KQ + i;
+        const int k = kb * 32 + 8 * (lane >> 4);
+        wf[i] = (ok && i < G.KQ && kb < G.NKB && k < G4)
+                    ? load_bf16x8(wr + k) : as_bf16x8(u16x8{0, 0, 0, 0, 0, 0, 0, 0});
+      }
     }
   }
   for (int i = tid; i < FCH * d.E; i += PD_THREADS) {
@@ -1813,14 +1865,35 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
         if (bb < d.B)
           v = __builtin_amdgcn_raw_buffer_load_b128(
               rg, (unsigned)((((long long)bb * d.S + t + 1) * G4 + 4 * k4) * 4), 0, 16);
-        uint16_t* o = dgs + sl * G4 + 4 * k4;
-        o[0] = f2bf(__uint_as_float(v[0]));
-        o[1] = f2bf(__uint_as_float(v[1]));
-        o[2] = f2bf(__uint_as_float(v[2]));
-        o[3] = f2bf(__uint_as_float(v[3]));
+        if constexpr (F32) {
+          *reinterpret_cast<pd_u32x4*>(&L[G.dgs + sl * G4 + 4 * k4]) = v;
+        } else {
+          uint16_t* o = dgs + sl * G4 + 4 * k4;
+          o[0] = f2bf(__uint_as_float(v[0]));
+          o[1] = f2bf(__uint_as_float(v[1]));
+          o[2] = f2bf(__uint_as_float(v[2]));
+          o[3] = f2bf(__uint_as_float(v[3]));
+        }
       }
       __syncthreads();
-      {
+      if constexpr (F32) {
+        const int kq = wave >> 1, mm = lane & 15;
+        f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < KB32; ++i) {
+          const int k = 4 * (kq * KQ32 + i) + (lane >> 4);
+          if (i < KQ32 && 4 * (kq * KQ32 + i) < G4) {   // wave-uniform
+            const float a = (mm < PD_SLOTS && k < G4) ? L[G.dgs + mm * G4 + k] : 0.f;
+            if (i & 1) acc1 = mfma_f32(a, wf32[i], acc1);
+            else acc0 = mfma_f32(a, wf32[i], acc0);
+          }
+        }
+        if (lane < 16) {
+#pragma unroll
+          for (int rr4 = 0; rr4 < 4; ++rr4)
+            L[G.part + (wave * PD_SLOTS + rr4) * 16 + lane] = acc0[rr4] + acc1[rr4];
+        }
+      } else {
         const int kq = wave >> 1, mm = lane & 15;
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -2294,13 +2367,19 @@ int pd_kind(const Dims& d) {
   return d.C == 10 && d.A <= 128 ? 1 : 0;
 }
 bool pd_ten(const Dims& d) { return pd_kind(d) > 0; }
-#define PD_SEL(K, KIND)                                                                    \
-  ((KIND) == 2 ? (const void*)K<10, 2, 128, 640, 320, 201>                                 \
-               : (KIND) == 1 ? (const void*)K<10, 2, 0, 0, 0, 0> : (const void*)K<0, 4, 0, 0, 0, 0>)
+#define PD_SEL(K, KIND, F)                                                                   \
+  ((KIND) == 2 ? (const void*)K<10, 2, 128, 640, 320, 201, F>                                \
+               : (KIND) == 1 ? (const void*)K<10, 2, 0, 0, 0, 0, F>                          \
+                             : (const void*)K<0, 4, 0, 0, 0, 0, F>)
 
-bool pd_eligible(const Dims& d) {
+// f32: fp32 mode (the f32-MFMA cell / r products).  ASR_ATT_PERSIST32=0 keeps
+// fp32 mode on the per-step kernels.
+bool pd_eligible(const Dims& d, bool f32) {
   const char* e = getenv("ASR_ATT_PERSIST");
   if (e && e[0] == '0') return false;
+  const char* e32 = getenv("ASR_ATT_PERSIST32");
+  if (f32 && e32 && e32[0] == '0') return false;
+  if (f32 && (d.E + d.D) % 4 != 0) return false;   // 16-B x rows
   const PdGeom G = pd_geom(d);
   const size_t lds = (size_t)G.total * 4;
   if (d.B > PD_GROUPS * PD_SLOTS || G.UPW > PD_UMAX || G.ED % 8 != 0 || G.NKB > 2 * PD_KMAX ||
@@ -2309,7 +2388,8 @@ bool pd_eligible(const Dims& d) {
       (size_t)d.B * d.S * G.ED * 4 >= (1ull << 31) || (size_t)d.B * d.T * 4 >= (1ull << 31))
     return false;
   if (device_cus() < PD_GROUPS * PD_MEMBERS) return false;
-  const void* k = PD_SEL(attdec_fwd_persist, pd_kind(d));
+  const void* k = f32 ? PD_SEL(attdec_fwd_persist, pd_kind(d), true)
+                      : PD_SEL(attdec_fwd_persist, pd_kind(d), false);
   if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return false;
   int per_cu = 0;
@@ -2318,12 +2398,15 @@ bool pd_eligible(const Dims& d) {
   return per_cu >= 1;
 }
 
-bool pb_eligible(const Dims& d) {
+bool pb_eligible(const Dims& d, bool f32) {
   const char* e = getenv("ASR_ATT_PERSIST");
   if (e && e[0] == '0') return false;
   const char* eb = getenv("ASR_ATT_PERSIST_BWD");
   if (eb && eb[0] == '0') return false;
-  const PbGeom G = pb_geom(d);
+  const char* e32 = getenv("ASR_ATT_PERSIST32");
+  if (f32 && e32 && e32[0] == '0') return false;
+  if (f32 && ((4 * d.D + 3) / 4 + 3) / 4 > 8 * PB_KQ) return false;
+  const PbGeom G = pb_geom(d, f32);
   const size_t lds = (size_t)G.total * 4;
   if (d.B > PD_GROUPS * PD_SLOTS || G.UPW > PD_UMAX || G.NPW > 32 || G.G4 % 8 != 0 ||
       G.KQ > PB_KQ || G.FCH > 8 * PD_FPW || d.A > 256 || (!pd_ten(d) && d.C > PB_CM) ||
@@ -2332,7 +2415,8 @@ bool pb_eligible(const Dims& d) {
       (size_t)d.B * d.T * d.C * 4 >= (1ull << 31))
     return false;
   if (device_cus() < PD_GROUPS * PD_MEMBERS) return false;
-  const void* k = PD_SEL(attdec_bwd_persist, pd_kind(d));
+  const void* k = f32 ? PD_SEL(attdec_bwd_persist, pd_kind(d), true)
+                      : PD_SEL(attdec_bwd_persist, pd_kind(d), false);
   if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return false;
   int per_cu = 0;
@@ -2455,7 +2539,7 @@ extern "C" int asr_attdec_forward_ex(const asr_attdec_dims_t* dims, const asr_at
   g_att_last[0] = (d.C == 10 || d.C == 3) ? d.C : 0;
   g_att_last[1] = (int)eg.x;
   g_att_persist_last[0] = 0;
-  if (bf && !ss && pd_eligible(d)) {
+  if (!ss && pd_eligible(d, !bf)) {
     const PdGeom G = pd_geom(d);
     int* ctr = (int*)((char*)workspace + W.ctr);
     float* pbuf = (float*)((char*)workspace + W.pbuf);
@@ -2464,15 +2548,21 @@ extern "C" int asr_attdec_forward_ex(const asr_attdec_dims_t* dims, const asr_at
     const dim3 grid(PD_GROUPS * PD_MEMBERS);
     // (A + E + 2) * 4 * T' algorithmic bytes per decoder step and utterance
     const int pslot = prof_begin_launch(ASR_PROF_ATT_FWD, s, att_pass_bytes(d));
-#define ASR_PD(CC, NQ, SA, SE, SD, SK)                                                                            \
-  hipLaunchKernelGGL((attdec_fwd_persist<CC, NQ, SA, SE, SD, SK>), grid, dim3(PD_THREADS), lds, s, d,                 \
-                     (const uint16_t*)workspace, pre_emb, h0, enc, enc_a, lens, w_dec, w_conv,   \
+#define ASR_PD2(CC, NQ, SA, SE, SD, SK, F)                                                         \
+  hipLaunchKernelGGL((attdec_fwd_persist<CC, NQ, SA, SE, SD, SK, F>), grid, dim3(PD_THREADS), lds,  \
+                     s, d, (const void*)workspace, pre_emb, h0, enc, enc_a, lens, w_dec, w_conv,  \
                      conv_w, v, dec, c_all, gates, x, ctx_all, aw_all, pbuf, ebuf, ctr,          \
                      lstm_persist_status_word(), drop_h, seed_h)
+#define ASR_PD(CC, NQ, SA, SE, SD, SK)                  \
+  do {                                                  \
+    if (bf) ASR_PD2(CC, NQ, SA, SE, SD, SK, false);     \
+    else ASR_PD2(CC, NQ, SA, SE, SD, SK, true);         \
+  } while (0)
     if (pd_kind(d) == 2) ASR_PD(10, 2, 128, 640, 320, 201);
     else if (pd_kind(d) == 1) ASR_PD(10, 2, 0, 0, 0, 0);
     else ASR_PD(0, 4, 0, 0, 0, 0);
 #undef ASR_PD
+#undef ASR_PD2
     ASR_LAUNCH_CHECK();
     prof_end_launch(ASR_PROF_ATT_FWD, pslot, s);
     g_att_last[0] = pd_ten(d) ? 10 : 0;
@@ -2621,8 +2711,8 @@ extern "C" int asr_attdec_backward_ex(const asr_attdec_dims_t* dims, const asr_a
     ASR_CHECK_HIP(hipMemsetAsync(dcw_part, 0, prow * d.C * d.K * 4, s));
   }
   g_att_persist_last[1] = 0;
-  if (bf && pb_eligible(d)) {
-    const PbGeom PG = pb_geom(d);
+  if (pb_eligible(d, !bf)) {
+    const PbGeom PG = pb_geom(d, !bf);
     int* ctr = (int*)(p + W.ctr);
     float* sbuf = (float*)(p + W.sbuf);
     ASR_CHECK_HIP(hipMemsetAsync(ctr, 0, (size_t)(1 + PD_GROUPS) * PD_CTR * 4, s));
@@ -2630,16 +2720,22 @@ extern "C" int asr_attdec_backward_ex(const asr_attdec_dims_t* dims, const asr_a
     const size_t lds = (size_t)PG.total * 4;
     const dim3 grid(PD_GROUPS * PD_MEMBERS);
     const int pslot = prof_begin_launch(ASR_PROF_ATT_BWD, s, att_pass_bytes(d));
-#define ASR_PB(CC, NQ, SA, SE, SD, SK)                                                                            \
-  hipLaunchKernelGGL((attdec_bwd_persist<CC, NQ, SA, SE, SD, SK>), grid, dim3(PD_THREADS), lds, s, d,                 \
-                     (const uint16_t*)wcatT, enc, enc_a, lens, w_dec, w_conv, conv_w, v, c_all,  \
+#define ASR_PB2(CC, NQ, SA, SE, SD, SK, F)                                                         \
+  hipLaunchKernelGGL((attdec_bwd_persist<CC, NQ, SA, SE, SD, SK, F>), grid, dim3(PD_THREADS), lds,  \
+                     s, d, (const void*)wcatT, enc, enc_a, lens, w_dec, w_conv, conv_w, v, c_all, \
                      aw_all, wd_all, d_dec_in, d_ctx_in, gates_dg, dctx_tot, d_enc_a, d_h0,      \
                      dwd_all, dv_part, dwc_part, dcw_part, r, sbuf, dwd_chunk, dFbuf, ctr,       \
                      lstm_persist_status_word(), drop_h, seed_h)
+#define ASR_PB(CC, NQ, SA, SE, SD, SK)                  \
+  do {                                                  \
+    if (bf) ASR_PB2(CC, NQ, SA, SE, SD, SK, false);     \
+    else ASR_PB2(CC, NQ, SA, SE, SD, SK, true);         \
+  } while (0)
     if (pd_kind(d) == 2) ASR_PB(10, 2, 128, 640, 320, 201);
     else if (pd_kind(d) == 1) ASR_PB(10, 2, 0, 0, 0, 0);
     else ASR_PB(0, 4, 0, 0, 0, 0);
 #undef ASR_PB
+#undef ASR_PB2
     ASR_LAUNCH_CHECK();
     prof_end_launch(ASR_PROF_ATT_BWD, pslot, s);
     g_att_last[2] = pd_ten(d) ? 10 : 0;

@@ -1,6 +1,7 @@
 """The persistent decoder passes (decoder.hip attdec_fwd_persist /
 attdec_bwd_persist: all S steps of the LSTMCell + location attention, forward
-or backward, in one launch each, bf16 mode) against the per-step kernels they
+or backward, in one launch each; bf16 mode, and fp32 mode through the F32
+instantiations) against the per-step kernels they
 replace (ASR_ATT_PERSIST=0), on the same inputs:
 every saved tensor the backward reads (dec, c, gates, x, ctx, aw) and the
 gradients of the whole decoder pass.  The two differ only in f32 summation
@@ -87,31 +88,46 @@ def _rel(a, b):
     return float((a - b).norm() / max(float(b.norm()), 1e-30))
 
 
+@pytest.mark.parametrize('precision', ['bf16', 'fp32'])
 @pytest.mark.parametrize('shape', sorted(SHAPES))
-def test_persistent_forward_matches_per_step(shape, cuda_dev):
+def test_persistent_forward_matches_per_step(shape, precision, cuda_dev):
+    """fp32: the F32 instantiations (f32 Wcat, f32-MFMA cell product) -- f32
+    summation order and the energies' one-exp tanh only: 2e-5."""
     from pytorch_end2end_speech_recognition_amd import native_ops
-    native_ops.set_compute_dtype('bf16')
+    native_ops.set_compute_dtype(precision)
     p = SHAPES[shape]
     t = _inputs(p, cuda_dev)
-    ref, f0 = _run(p, t, False, False)
-    got, f1 = _run(p, t, True, False)
+    try:
+        ref, f0 = _run(p, t, False, False)
+        got, f1 = _run(p, t, True, False)
+    finally:
+        native_ops.set_compute_dtype('fp32')
     assert f0 == 0 and f1 == 1, 'persistent forward did not run'
+    tol = 1e-3 if precision == 'bf16' else 2e-5
     for name, a, b in zip(('dec', 'c', 'gates', 'x', 'ctx', 'aw'), got, ref):
         assert torch.isfinite(a).all(), name
-        assert _rel(a, b) < 1e-3, (name, _rel(a, b))
+        assert _rel(a, b) < tol, (name, _rel(a, b))
     # softmax rows (the multiplicative mask leaves padded frames at energy 0,
     # as the reference does, so they keep a weight)
     np.testing.assert_allclose(got[5].sum(-1).cpu().numpy(), 1.0, rtol=1e-5)
 
 
+@pytest.mark.parametrize('precision', ['bf16', 'fp32'])
 @pytest.mark.parametrize('shape', sorted(SHAPES))
-def test_persistent_forward_gradients_match(shape, cuda_dev):
+def test_persistent_forward_gradients_match(shape, precision, cuda_dev):
+    """fp32: both passes' F32 instantiations against the per-step kernels,
+    1e-4 on every output and gradient (f32 summation order only)."""
     from pytorch_end2end_speech_recognition_amd import native_ops
-    native_ops.set_compute_dtype('bf16')
+    native_ops.set_compute_dtype(precision)
     p = SHAPES[shape]
     t = _inputs(p, cuda_dev, seed=1)
-    ref, f0 = _run(p, t, False, True)
-    got, f1 = _run(p, t, True, True)
+    try:
+        ref, f0 = _run(p, t, False, True)
+        got, f1 = _run(p, t, True, True)
+        if precision == 'bf16':
+            mid, fm = _run(p, t, True, True, persist_bwd=False)
+    finally:
+        native_ops.set_compute_dtype('fp32')
     assert f0 == (0, 0) and f1 == (1, 1), (f0, f1)
     names = ('dec', 'ctx', 'aw', 'd_enc', 'd_enc_a', 'd_pre_emb', 'd_h0', 'd_w_ih', 'd_w_hh',
              'd_w_dec', 'd_w_conv', 'd_conv_w', 'd_v')
@@ -119,13 +135,16 @@ def test_persistent_forward_gradients_match(shape, cuda_dev):
     print(shape, {k: '%.2e' % v for k, v in errs.items()})
     for name, a in zip(names, got):
         assert torch.isfinite(a).all(), name
+    if precision == 'fp32':
+        for name in names:
+            assert errs[name] < 1e-4, (name, errs[name])
+        return
     # outputs as the forward test; gradients: the backward's bf16 GEMM operands
     # (aw, dctx, dgates, x rounded to bf16) turn the forward's f32-order
     # differences into bf16 rounding flips (2^-8 relative each), hence 5e-3
     for name in names:
         assert errs[name] < (1e-3 if name in ('dec', 'ctx', 'aw') else 5e-3), (name, errs[name])
     # the backward pass alone: persistent forward under both backward forms
-    mid, fm = _run(p, t, True, True, persist_bwd=False)
     assert fm == (1, 0), fm
     errs = {name: _rel(a, b) for name, a, b in zip(names, got, mid)}
     print(shape, 'bwd only', {k: '%.2e' % v for k, v in errs.items()})
