@@ -154,10 +154,12 @@ def colsum_accumulate(g2d, out0, out1=None, alpha=1.0):
 # head, 8000 x 640 x 10001, ran at ~140 TF/s that way).  The padded pitches
 # also put backward products whose K is the output width (the 29-class CTC
 # head's dX, K = 29) on the fast kernels, so such layers are staged from
-# 250 MFLOP (the 5x512 CTC head, 32000 x 1024 x 29: -0.1 ms/step); staging a
-# layer whose width is already a multiple of 8 below 2 GFLOP measured slower.
+# 32 MFLOP (round 4: 250 MFLOP, the 5x512 CTC head, 32000 x 1024 x 29: -0.1
+# ms/step; round 5 also the attention decoder's 29-class output layer, 4032 x
+# 320 x 29, whose dX had stayed on the generic kernel); staging a layer whose
+# width is already a multiple of 8 below 2 GFLOP measured slower.
 _STAGE_FLOPS = 2e9
-_STAGE_FLOPS_RAGGED = float(os.environ.get("ASR_LINEAR_STAGE_FLOPS", "2.5e8"))
+_STAGE_FLOPS_RAGGED = float(os.environ.get("ASR_LINEAR_STAGE_FLOPS", "3.2e7"))
 
 
 def _staged(t, rows, cols, ld=None):
