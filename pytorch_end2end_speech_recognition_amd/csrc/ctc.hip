@@ -922,6 +922,183 @@ __global__ void __launch_bounds__(256) ctc_grad_bf16(
   }
 }
 
+// The wide fused head's gradient pass (V > 256, 16-B aligned rows; the
+// class-table-free form of ctc_grad_bf16) with a block's rows software-
+// pipelined.  A block streams rpb consecutive rows one after another (the
+// bias sums stay in registers, in row order), so its time is rpb times a row's
+// chain of memory round trips; here that chain is one: while row r streams,
+// the next row's header (length, log P, log-sum-exp) and state values (alpha,
+// beta, emission) are already in flight, its label classes are re-read only
+// when the utterance changes, and the class representatives' occupancy sums
+// go to an LDS correction table BEFORE the row is streamed -- every column is
+// written once as (softmax - corr) * scale, with no store-completion wait,
+// barrier and read-modify-write of the representatives' columns after it.
+// Values: bitwise those of ctc_grad_bf16's dY; the bias sums differ only in
+// f32 summation order (sum of differences instead of difference of sums).
+template <int NCH>
+__global__ void __launch_bounds__(256) ctc_grad_bf16_pipe(
+    const float* __restrict__ acts, long long st, long long sb, int T, int V,
+    const int32_t* __restrict__ labels, const int32_t* __restrict__ label_lens,
+    const int32_t* __restrict__ act_lens, const int32_t* __restrict__ offs, int blank, int Spad,
+    const float* __restrict__ lse, const float* __restrict__ emit,
+    const float* __restrict__ alpha, const float* __restrict__ beta,
+    const float* __restrict__ logp, const float* __restrict__ grad_scale, float scale_mul,
+    uint16_t* __restrict__ grads, long long gst, long long gsb, int gld, int rev,
+    int acts_bytes, float* __restrict__ colpart, int rpb, long long nrows) {
+  // occ [Spad] | corr [V] | clsT [Spad]
+  extern __shared__ __attribute__((aligned(16))) float occ[];
+  float* corr = occ + Spad;
+  int* clsT = (int*)(occ + Spad + V);
+  __shared__ int s_b;   // utterance whose classes clsT holds
+  const int tid = threadIdx.x, nth = blockDim.x;
+  const int n8 = gld >> 3;
+  const float scale = (grad_scale ? grad_scale[0] : 1.0f) * scale_mul;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)acts, 0, acts_bytes, 0x00020000);
+  float acc[NCH > 0 ? NCH : 1][8];
+#pragma unroll
+  for (int j = 0; j < (NCH > 0 ? NCH : 1); ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[j][e] = 0.f;
+  for (int v = tid; v < V; v += nth) corr[v] = 0.f;
+  if (tid == 0) s_b = -1;
+  // a row's header and this thread's four state values (s = tid + 256 q)
+  struct Row { long long row; int b, t, Tb, L; float lp, z; float sv[4]; };
+  auto fetch = [&](int r, Row& h) {
+    const long long lin = (long long)blockIdx.x * rpb + r;
+    h.row = rev ? nrows - 1 - lin : lin;
+    h.b = (int)(h.row / T);
+    h.t = (int)(h.row % T);
+    h.Tb = act_lens[h.b];
+    h.lp = logp[h.b];
+    h.z = lse[h.row];
+    h.L = label_lens[h.b];
+    const long long so = h.row * Spad;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int s_ = tid + q * nth;   // < 4 nth = Spad bound (host: Spad <= 1024)
+      h.sv[q] = s_ < Spad ? alpha[so + s_] + beta[so + s_] - emit[so + s_] : 0.f;
+    }
+  };
+  const int nr = (int)min((long long)rpb, nrows - (long long)blockIdx.x * rpb);
+  Row cur;
+  if (nr > 0) fetch(0, cur);
+  for (int r = 0; r < nr; ++r) {
+    const int b = cur.b, t = cur.t;
+    uint16_t* g = grads + (long long)t * gst + (long long)b * gsb;
+    const bool live = t < cur.Tb && cur.lp != neg_inf();   // row-uniform
+    const int L = min(cur.L, (Spad - 1) / 2);
+    const int S = 2 * L + 1;
+    // the utterance's state classes (consecutive rows share it)
+    __syncthreads();   // previous row's reads of clsT / occ / corr done
+    if (live && s_b != b) {
+      const int32_t* lab = labels + offs[b];
+      for (int s_ = tid; s_ < S; s_ += nth) {
+        int c = (s_ & 1) ? lab[s_ >> 1] : blank;
+        clsT[s_] = c < 0 ? 0 : (c >= V ? V - 1 : c);
+      }
+    }
+    if (live) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int s_ = tid + q * nth;
+        if (s_ < S) occ[s_] = ex2(cur.sv[q] - cur.lp);
+      }
+    }
+    __syncthreads();   // occ, clsT
+    if (tid == 0 && live) s_b = b;
+    int rep_c[4] = {-1, -1, -1, -1};
+    if (live) {
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) {
+        const int s_ = tid + q4 * nth;
+        if (s_ >= S) continue;
+        const int c = clsT[s_];
+        bool first;
+        if ((s_ & 1) == 0) {
+          first = s_ == 0;
+        } else {
+          first = c != blank;
+          for (int q = 1; q < s_ && first; q += 2) first = clsT[q] != c;
+        }
+        if (!first) continue;
+        float sum = 0.f;
+        for (int q = 0; q < S; ++q)
+          if (clsT[q] == c) sum += occ[q];
+        rep_c[q4] = c;
+        corr[c] = sum;
+      }
+    }
+    __syncthreads();   // corr complete
+    // this row's stream loads, then the next row's header / states
+    const float z = cur.z;
+    const long long xo = (long long)t * st + (long long)b * sb;
+    const unsigned base = (unsigned)(xo * 4);
+    float vv[NCH > 0 ? NCH : 1][8];
+    if (live) {
+#pragma unroll
+      for (int j = 0; j < NCH; ++j) {
+        const int k = tid + j * nth;
+        if (k < n8) {
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const f32x4 w = __builtin_bit_cast(
+                f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, base + (unsigned)(32 * k + 16 * q), 0, 0));
+            vv[j][4 * q] = w[0]; vv[j][4 * q + 1] = w[1]; vv[j][4 * q + 2] = w[2]; vv[j][4 * q + 3] = w[3];
+          }
+        }
+      }
+    }
+    Row nxt;
+    if (r + 1 < nr) fetch(r + 1, nxt);
+    if (live) {
+#pragma unroll
+      for (int j = 0; j < NCH; ++j) {
+        const int k = tid + j * nth;
+        if (k >= n8) continue;
+        const int c0 = 8 * k;
+        float cr[8];
+        if (c0 + 8 <= V) {
+          const f32x4 c_lo = *reinterpret_cast<const f32x4*>(corr + c0);
+          const f32x4 c_hi = *reinterpret_cast<const f32x4*>(corr + c0 + 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { cr[e] = c_lo[e]; cr[4 + e] = c_hi[e]; }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) cr[e] = c0 + e < V ? corr[c0 + e] : 0.f;
+        }
+        unsigned w4[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int c = c0 + 2 * jj;
+          const float lo = c < V ? (__expf(vv[j][2 * jj] - z) - cr[2 * jj]) * scale : 0.f;
+          const float hi = c + 1 < V ? (__expf(vv[j][2 * jj + 1] - z) - cr[2 * jj + 1]) * scale : 0.f;
+          if (NCH > 0) { acc[j][2 * jj] += lo; acc[j][2 * jj + 1] += hi; }
+          w4[jj] = (c < V ? (unsigned)f2bf(lo) : 0u) | ((c + 1 < V ? (unsigned)f2bf(hi) : 0u) << 16);
+        }
+        reinterpret_cast<uint4*>(g)[k] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+      }
+    } else {
+      for (int i = tid; i < n8; i += nth) reinterpret_cast<uint4*>(g)[i] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    __syncthreads();   // every read of corr for this row done
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4)
+      if (rep_c[q4] >= 0) corr[rep_c[q4]] = 0.f;
+    if (r + 1 < nr) cur = nxt;
+  }
+  if (NCH > 0 && colpart) {
+    float* o = colpart + (long long)blockIdx.x * gld;
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      const int k = tid + j * nth;
+      if (k >= n8) continue;
+      *reinterpret_cast<f32x4*>(o + 8 * k) = f32x4{acc[j][0], acc[j][1], acc[j][2], acc[j][3]};
+      *reinterpret_cast<f32x4*>(o + 8 * k + 4) = f32x4{acc[j][4], acc[j][5], acc[j][6], acc[j][7]};
+    }
+  }
+}
+
 __global__ void ctc_loss_reduce(const float* __restrict__ costs, int B, float scale,
                                 float* __restrict__ out) {
   __shared__ float red[256];
@@ -1189,7 +1366,22 @@ static int ctc_backward_bf16_impl(const float* acts, long long stride_t, long lo
     if (al) ASR_CTC_G16A(TB, NC, true);      \
     else ASR_CTC_G16A(TB, NC, false);        \
   } while (0)
-  if (table) {
+  const char* ep = getenv("ASR_CTC_GRAD_PIPE");   // 0: the unpipelined pass (A/B)
+  const bool pipe = al && !table && nch > 0 && !(ep && ep[0] == '0');
+#define ASR_CTC_GP(NC)                                                                           \
+  hipLaunchKernelGGL((ctc_grad_bf16_pipe<NC>), dim3((unsigned)nblk), dim3(threads), lds, s, acts, \
+                     stride_t, stride_b, T, V, labels_flat, label_lens, act_lens, ws.offs, blank, \
+                     Spad, ws.lse, ws.emit, ws.alpha, ws.beta, ws.logp, grad_scale, scale, grads, \
+                     gstride_t, gstride_b, gld, rev, abytes, colpart, rpb, rows)
+  if (pipe) {
+    switch (nch) {
+      case 1: ASR_CTC_GP(1); break;
+      case 2: ASR_CTC_GP(2); break;
+      case 4: ASR_CTC_GP(4); break;
+      case 5: ASR_CTC_GP(5); break;
+      default: ASR_CTC_GP(8); break;
+    }
+  } else if (table) {
     if (nch) ASR_CTC_G16A(true, 1, false);
     else ASR_CTC_G16A(true, 0, false);
   } else {
@@ -1203,6 +1395,7 @@ static int ctc_backward_bf16_impl(const float* acts, long long stride_t, long lo
     }
   }
 #undef ASR_CTC_G16A
+#undef ASR_CTC_GP
 #undef ASR_CTC_G16
   ASR_LAUNCH_CHECK();
   prof_end_launch(ASR_PROF_CTC_GRAD, pslot, s);

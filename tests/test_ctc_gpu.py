@@ -270,3 +270,48 @@ def test_lattice_edge_cases_vs_oracle(K, Ls, cuda_dev):
     again = _run(acts, labels, label_lens, act_lens, cuda_dev)
     np.testing.assert_array_equal(costs, again[1])
     np.testing.assert_array_equal(grads, again[2])
+
+
+@pytest.mark.parametrize('rows_per_block', ['0', '1500'])
+def test_wide_head_gradient_pipeline_matches_unpipelined(rows_per_block, cuda_dev, monkeypatch):
+    """The wide fused head's gradient pass with a block's rows pipelined
+    (ctc_grad_bf16_pipe: next row's header / states in flight, the
+    representatives folded in through an LDS correction table) against the
+    unpipelined pass (ASR_CTC_GRAD_PIPE=0) at V = 10001 with ragged lengths
+    (dead rows inside blocks): dX / dW bitwise (the same bf16 dY), the bias
+    gradient within 1e-6 (f32 summation order).  '1500': few blocks, so each
+    runs long chains of rows across utterance boundaries."""
+    ops = _native()
+    if rows_per_block != '0':
+        monkeypatch.setenv('ASR_CTC_BIAS_BLOCKS', rows_per_block)
+    rng = np.random.RandomState(23)
+    B, T, K, V = 6, 90, 128, 10001
+    act_lens = np.sort(rng.randint(40, T + 1, B))[::-1].astype(np.int32)
+    act_lens[0] = T
+    label_lens = rng.randint(5, 19, B).astype(np.int32)
+    labels = np.concatenate([rng.randint(1, V, l) for l in label_lens]).astype(np.int32)
+    labels[:3] = labels[0]   # a repeated label (one representative for three states)
+    x0 = torch.from_numpy((rng.randn(B, T, K) * 0.5).astype(np.float32)).to(cuda_dev)
+    w0 = torch.from_numpy((rng.randn(V, K) * 0.05).astype(np.float32)).to(cuda_dev)
+    b0 = torch.from_numpy((rng.randn(V) * 0.1).astype(np.float32)).to(cuda_dev)
+    lab = torch.from_numpy(labels).to(cuda_dev)
+    ll = torch.from_numpy(label_lens).to(cuda_dev)
+    al = torch.from_numpy(act_lens).to(cuda_dev)
+    ops.set_compute_dtype('bf16')
+    out = {}
+    try:
+        for pipe in ('1', '0'):
+            monkeypatch.setenv('ASR_CTC_GRAD_PIPE', pipe)
+            x = x0.clone().requires_grad_(True)
+            w = w0.clone().requires_grad_(True)
+            b = b0.clone().requires_grad_(True)
+            loss, _ = ops.linear_ctc_loss(x, w, b, lab, ll, al, int(label_lens.max()), 1.0 / B)
+            loss.backward()
+            torch.cuda.synchronize()
+            out[pipe] = [x.grad.clone(), w.grad.clone(), b.grad.clone()]
+    finally:
+        ops.set_compute_dtype('fp32')
+    p, u = out['1'], out['0']
+    assert torch.equal(p[0], u[0]), float((p[0] - u[0]).abs().max())
+    assert torch.equal(p[1], u[1]), float((p[1] - u[1]).abs().max())
+    assert float((p[2] - u[2]).abs().max()) <= 1e-6 * float(u[2].abs().max()) + 1e-9
