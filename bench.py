@@ -192,6 +192,7 @@ def roofline_report(args, p, samples, launches, workload):
         T_l.append(t)
         t = t // 2 if flag else t
     T = sum(T_l) / len(T_l)
+    frames_ctc = B * t                        # output frames of the CTC head(s)
     esz = 2 if args.precision == 'bf16' else 4
     cell = B * H                              # (utterance, unit) cells per direction
     w_hh = 2 * 4 * H * H * esz                # both directions
@@ -331,9 +332,10 @@ def roofline_report(args, p, samples, launches, workload):
             'achieved': round(nbytes / (us * 1e-6) / 1e9, 1), 'peak': HBM_PEAK_GBS,
             'unit': 'GB/s', 'frac': round(nbytes / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
             'algorithmic_bytes_per_call': int(nbytes),
-            'bytes_per_frame_over_V': round(nbytes / max(1.0, r['bytes'] / 4.0), 3),
-            'what': 'forward (emission + lattice) + gradient launches of one head; bytes: '
-                    'activations read once + gradient written once'}
+            'bytes_per_frame_over_V': round(nbytes / max(1.0, float(frames_ctc) * r['tag']), 3),
+            'what': 'forward (emission or log-sum-exp fold + lattice) + gradient launches of one '
+                    'head; bytes: activations read once + gradient written once (with the head '
+                    'GEMM\'s log-sum-exp partials the forward reads no activation row)'}
     out['other_kernels'] = others
     return out
 
