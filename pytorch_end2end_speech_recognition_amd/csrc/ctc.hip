@@ -1099,6 +1099,243 @@ __global__ void __launch_bounds__(256) ctc_grad_bf16_pipe(
   }
 }
 
+// The wide fused head's gradient pass, streamed (V > 256, 16-B aligned
+// activation rows of a padded pitch; ASR_CTC_GRAD_STREAM=0 selects
+// ctc_grad_bf16_pipe).  512 threads, two work-groups per CU (grid = 2 x CUs,
+// each a contiguous run of rows), and the rows software-pipelined two deep:
+// while row r is turned into dY, row r+1's activations (3 x 32 B per thread at
+// V = 10001) and row r+2's header / state sums are in flight, so the HBM
+// stream never waits on a row's occupancy work.  The per-row class work is
+// O(multiplicity), not O(S): per utterance (when the block's rows cross one)
+// each label state learns whether it is its class's first occurrence and the
+// next state of its class (nxt); per row a class representative sums its chain
+// of occupancies, the blank class's sum is a block reduction, and the
+// representative is pushed onto its 8-column chunk's list (head[k] ->
+// link[]), so a chunk reads one LDS word and, in the rare chunk holding a
+// label class, walks a one- or two-entry list -- no V-sized correction table
+// (LDS per work-group ~20 KB, not 40 KB).  dY values: bitwise those of
+// ctc_grad_bf16 (each column subtracts its single class sum); bias sums in f32
+// over the block's rows in row order.
+template <int NCH>
+__global__ void __launch_bounds__(512, 4) ctc_grad_bf16_stream(
+    const float* __restrict__ acts, long long st, long long sb, int T, int V,
+    const int32_t* __restrict__ labels, const int32_t* __restrict__ label_lens,
+    const int32_t* __restrict__ act_lens, const int32_t* __restrict__ offs, int blank, int Spad,
+    const float* __restrict__ lse, const float* __restrict__ emit,
+    const float* __restrict__ alpha, const float* __restrict__ beta,
+    const float* __restrict__ logp, const float* __restrict__ grad_scale, float scale_mul,
+    uint16_t* __restrict__ grads, long long gst, long long gsb, int gld, int rev,
+    int acts_bytes, float* __restrict__ colpart, int rpb, long long nrows) {
+  constexpr int NT = 512, NW = NT / 64;
+  // occ [Spad] f32 | repv [Spad] f32 | clsT [Spad] | nxt [Spad] | link [Spad] | head [n8] | red [NW]
+  extern __shared__ __attribute__((aligned(16))) float occ[];
+  float* repv = occ + Spad;
+  int* clsT = (int*)(repv + Spad);
+  int* nxt = clsT + Spad;
+  int* link = nxt + Spad;
+  int* head = link + Spad;
+  const int n8 = gld >> 3;
+  float* red = (float*)(head + n8);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const float scale = (grad_scale ? grad_scale[0] : 1.0f) * scale_mul;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)acts, 0, acts_bytes, 0x00020000);
+  for (int k = tid; k < n8; k += NT) head[k] = 0;
+  float acc[NCH][8];
+#pragma unroll
+  for (int j = 0; j < NCH; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[j][e] = 0.f;
+
+  struct Row { int b, t, Tb, L; float lp, z; float sv[2]; bool live; };
+  const long long r0 = (long long)blockIdx.x * rpb;
+  const int nr = (int)max(0LL, min((long long)rpb, nrows - r0));
+  auto fetch = [&](int r, Row& h) {
+    const long long lin = r0 + r;
+    const long long row = rev ? nrows - 1 - lin : lin;
+    h.b = (int)(row / T);
+    h.t = (int)(row % T);
+    h.Tb = act_lens[h.b];
+    h.lp = logp[h.b];
+    h.z = lse[row];
+    h.L = min(label_lens[h.b], (Spad - 1) / 2);
+    h.live = h.t < h.Tb && h.lp != neg_inf();
+    const long long so = row * Spad;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int s_ = tid + q * NT;
+      h.sv[q] = s_ < 2 * h.L + 1 ? alpha[so + s_] + beta[so + s_] - emit[so + s_] : 0.f;
+    }
+  };
+  auto load_row = [&](const Row& h, float (&v)[NCH][8]) {
+    if (!h.live) return;
+    const unsigned base = (unsigned)(((long long)h.t * st + (long long)h.b * sb) * 4);
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      const int k = tid + j * NT;
+      if (8 * k < V) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const f32x4 w = __builtin_bit_cast(
+              f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, base + (unsigned)(32 * k + 16 * q), 0, 0));
+          v[j][4 * q] = w[0]; v[j][4 * q + 1] = w[1]; v[j][4 * q + 2] = w[2]; v[j][4 * q + 3] = w[3];
+        }
+      }
+    }
+  };
+  // per-utterance state classes: rep[q] (first state of a label class), isb[q] (blank class)
+  int ub = -1;
+  bool rep[2] = {false, false}, isb[2] = {false, false};
+  auto setup_utt = [&](const Row& h) {
+    const int S = 2 * h.L + 1;
+    const int32_t* lab = labels + offs[h.b];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int s_ = tid + q * NT;
+      if (s_ < S) {
+        int c = (s_ & 1) ? lab[s_ >> 1] : blank;
+        clsT[s_] = c < 0 ? 0 : (c >= V ? V - 1 : c);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int s_ = tid + q * NT;
+      rep[q] = false;
+      isb[q] = false;
+      if (s_ >= S) continue;
+      const int c = clsT[s_];
+      isb[q] = c == blank;
+      if (c == blank) continue;   // only odd states reach here
+      bool first = true;
+      for (int p = s_ - 2; p >= 1 && first; p -= 2) first = clsT[p] != c;
+      int nx = -1;
+      for (int p = s_ + 2; p < S && nx < 0; p += 2)
+        if (clsT[p] == c) nx = p;
+      rep[q] = first;
+      nxt[s_] = nx;
+    }
+    // the blank class's representative: state 0
+    if (tid == 0) rep[0] = true;
+    ub = h.b;
+  };
+  auto step = [&](int r, const Row& cur, Row& n1, Row& n2, float (&vc)[NCH][8], float (&vn)[NCH][8]) {
+    // in flight: row r+1's activations, row r+2's header
+    if (r + 1 < nr) load_row(n1, vn);
+    if (r + 2 < nr) fetch(r + 2, n2);
+    const int S = 2 * cur.L + 1;
+    if (cur.live && cur.b != ub) setup_utt(cur);   // block-uniform
+    float bl = 0.f;
+    if (cur.live) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int s_ = tid + q * NT;
+        if (s_ < S) {
+          const float o = ex2(cur.sv[q] - cur.lp);
+          occ[s_] = o;
+          if (isb[q]) bl += o;
+        }
+      }
+      bl = wave_sum(bl);
+      if (lane == 0) red[wave] = bl;
+    }
+    __syncthreads();   // occ, red
+    if (cur.live) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int s_ = tid + q * NT;
+        if (!rep[q] || s_ >= S) continue;
+        float sum;
+        int c;
+        if (s_ == 0) {
+          sum = 0.f;
+#pragma unroll
+          for (int w = 0; w < NW; ++w) sum += red[w];
+          c = blank;
+        } else {
+          sum = occ[s_];
+          for (int p = nxt[s_]; p >= 0; p = nxt[p]) sum += occ[p];
+          c = clsT[s_];
+        }
+        repv[s_] = sum;
+        link[s_] = atomicExch(&head[c >> 3], s_ + 1);
+      }
+    }
+    __syncthreads();   // head / link / repv
+    uint16_t* g = grads + (long long)cur.t * gst + (long long)cur.b * gsb;
+    const float z = cur.z;
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      const int k = tid + j * NT;
+      if (k >= n8) continue;
+      const int c0 = 8 * k;
+      float e[8];
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj)
+        e[jj] = (cur.live && c0 + jj < V) ? __expf(vc[j][jj] - z) : 0.f;
+      if (cur.live) {
+        for (int h = head[k]; h != 0; h = link[h - 1]) {
+          const int sr = h - 1;
+          const int off = clsT[sr] - c0;   // clsT[0] = blank
+          const float rv = repv[sr];
+#pragma unroll
+          for (int jj = 0; jj < 8; ++jj) e[jj] -= off == jj ? rv : 0.f;
+        }
+      }
+      unsigned w4[4];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const float lo = e[2 * jj] * scale, hi = e[2 * jj + 1] * scale;
+        acc[j][2 * jj] += lo;
+        acc[j][2 * jj + 1] += hi;
+        w4[jj] = (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
+      }
+      reinterpret_cast<uint4*>(g)[k] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+    }
+    __syncthreads();   // every read of head / link / repv / clsT for this row done
+    if (cur.live) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int s_ = tid + q * NT;
+        if (rep[q] && s_ < S) head[clsT[s_] >> 3] = 0;
+      }
+    }
+  };
+  Row ra, rb, rc;
+  float va[NCH][8], vb[NCH][8];
+  if (nr > 0) {
+    fetch(0, ra);
+    if (nr > 1) fetch(1, rb);
+    load_row(ra, va);
+  }
+  __syncthreads();   // head cleared
+  // three headers (rows r, r+1, r+2) and two activation buffers (rows r,
+  // r+1) rotate with period 6: a six-way unroll keeps every one in registers
+  // without a copy (copying a register with a load in flight waits for it)
+  for (int r = 0; r < nr; r += 6) {
+#define ASR_GS(I, C, N1, N2, VC, VN) \
+  if (r + I >= nr) break;            \
+  step(r + I, C, N1, N2, VC, VN);
+    ASR_GS(0, ra, rb, rc, va, vb)
+    ASR_GS(1, rb, rc, ra, vb, va)
+    ASR_GS(2, rc, ra, rb, va, vb)
+    ASR_GS(3, ra, rb, rc, vb, va)
+    ASR_GS(4, rb, rc, ra, va, vb)
+    ASR_GS(5, rc, ra, rb, vb, va)
+#undef ASR_GS
+  }
+  if (colpart) {
+    float* o = colpart + (long long)blockIdx.x * gld;
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      const int k = tid + j * NT;
+      if (k >= n8) continue;
+      *reinterpret_cast<f32x4*>(o + 8 * k) = f32x4{acc[j][0], acc[j][1], acc[j][2], acc[j][3]};
+      *reinterpret_cast<f32x4*>(o + 8 * k + 4) = f32x4{acc[j][4], acc[j][5], acc[j][6], acc[j][7]};
+    }
+  }
+}
+
 __global__ void ctc_loss_reduce(const float* __restrict__ costs, int B, float scale,
                                 float* __restrict__ out) {
   __shared__ float red[256];
@@ -1283,8 +1520,8 @@ static void ctc_bias_grid(int T, int B, int V, int* rpb, int* nblk) {
   // fewer rows per block hide more latency at the price of partial traffic:
   // at V = 10001, 534 / 1067 / 2134 blocks measured 265 + 13 / 202 + 20 /
   // 185 + 33 us (gradient + column sums).  ASR_CTC_BIAS_BLOCKS: the target (A/B)
-  static const long long env_target =
-      getenv("ASR_CTC_BIAS_BLOCKS") ? atoll(getenv("ASR_CTC_BIAS_BLOCKS")) : 0;
+  const char* bb_env = getenv("ASR_CTC_BIAS_BLOCKS");   // per call: the tests switch it
+  const long long env_target = bb_env ? atoll(bb_env) : 0;
   const long long target = env_target > 0 ? env_target : 1024;
   long long r = rows / target;
   if (r < 1) r = 1;
@@ -1368,6 +1605,37 @@ static int ctc_backward_bf16_impl(const float* acts, long long stride_t, long lo
   } while (0)
   const char* ep = getenv("ASR_CTC_GRAD_PIPE");   // 0: the unpipelined pass (A/B)
   const bool pipe = al && !table && nch > 0 && !(ep && ep[0] == '0');
+  // the streamed pass (512 threads, 2 work-groups per CU): ASR_CTC_GRAD_STREAM=0 (A/B)
+  const char* es = getenv("ASR_CTC_GRAD_STREAM");
+  const int n8s = gld >> 3;
+  const int nchs = (n8s + 511) / 512;
+  if (al && !table && nchs <= 3 && !(es && es[0] == '0')) {   // NCH 4 spills at 128 VGPRs
+    static int cus = 0;
+    if (cus == 0) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+          cus <= 0)
+        cus = 256;
+    }
+    long long nb2 = std::min<long long>(rows, 2LL * cus);
+    if (dbias) nb2 = std::min<long long>(nb2, nblk);   // the bias workspace holds nblk partials
+    const long long rp2 = (rows + nb2 - 1) / nb2;
+    rpb = (int)rp2;
+    nblk = (int)((rows + rp2 - 1) / rp2);
+    const size_t lds2 = (size_t)(5 * Spad + n8s + 8) * sizeof(float);
+#define ASR_CTC_GS(NC)                                                                           \
+  hipLaunchKernelGGL((ctc_grad_bf16_stream<NC>), dim3((unsigned)nblk), dim3(512), lds2, s, acts, \
+                     stride_t, stride_b, T, V, labels_flat, label_lens, act_lens, ws.offs, blank, \
+                     Spad, ws.lse, ws.emit, ws.alpha, ws.beta, ws.logp, grad_scale, scale, grads, \
+                     gstride_t, gstride_b, gld, rev, abytes, colpart, rpb, rows)
+    switch (nchs) {
+      case 1: ASR_CTC_GS(1); break;
+      case 2: ASR_CTC_GS(2); break;
+      default: ASR_CTC_GS(3); break;
+    }
+#undef ASR_CTC_GS
+  } else
 #define ASR_CTC_GP(NC)                                                                           \
   hipLaunchKernelGGL((ctc_grad_bf16_pipe<NC>), dim3((unsigned)nblk), dim3(threads), lds, s, acts, \
                      stride_t, stride_b, T, V, labels_flat, label_lens, act_lens, ws.offs, blank, \

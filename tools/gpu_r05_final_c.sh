@@ -9,3 +9,6 @@ done
 bash tools/gpu_pmc.sh r05 > /dev/null || exit 1
 cat gpurun_out/r05_pmc_traffic.json | head -40
 CONFIG=vgg_hier WORKLOAD=vgg_hier bash tools/gpu_pmc.sh r05_vgg > /dev/null || exit 1
+timeout -k 10 300 python -u tools/gemm_bench.py > gpurun_out/r05_gemm_bench_bf16.txt 2>&1 || exit 1
+timeout -k 10 300 python -u tools/gemm_f32_bench.py > gpurun_out/r05_gemm_bench_f32.txt 2>&1 || exit 1
+cat gpurun_out/r05_gemm_bench_bf16.txt gpurun_out/r05_gemm_bench_f32.txt | grep -v amdgpu.ids

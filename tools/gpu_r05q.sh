@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -k 10 600 python -u -m pytest tests/test_ctc_gpu.py -x -q --timeout 150 --timeout-method thread -m gpu > gpurun_out/q_tests.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_ctc_gpu.py tests/test_model_ctc.py -x -q --timeout 150 --timeout-method thread -m gpu > gpurun_out/q_tests.log 2>&1
 rc=$?; tail -2 gpurun_out/q_tests.log; [ $rc -eq 0 ] || exit $rc
 rm -rf gpurun_out/q_prof
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/q_prof -- python3 tools/ctc_head_bench.py > gpurun_out/q_head.log 2>&1
