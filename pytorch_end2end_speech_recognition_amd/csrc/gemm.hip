@@ -2341,16 +2341,24 @@ bool fast32_operand_ok(const asr_operand_t& o, const Operand& op, long long batc
 int fast32_modes(const asr_gemm_t* g, const Params& P) {
   const char* e = getenv("ASR_GEMM_F32FAST");
   if (e && e[0] == '0') return -1;
+  // diagnostics: ASR_GEMM_F32FAST_MASK (bit m: layout mode m may take the
+  // kernel), ASR_GEMM_F32FAST_NOTAP=1 (no tap-addressed operand)
+  const char* em = getenv("ASR_GEMM_F32FAST_MASK");
+  const int mask = em ? atoi(em) : 15;
+  const char* et = getenv("ASR_GEMM_F32FAST_NOTAP");
+  const bool notap = et && et[0] == '1';
   int modes = -1;
   for (int i = 0; i < P.nprob; ++i) {
     const Problem& p = P.p[i];
     if (!fast32_operand_ok(g[i].a, p.a, p.sA, p.batch, p.K) ||
         !fast32_operand_ok(g[i].b, p.b, p.sB, p.batch, p.K))
       return -1;
+    if (notap && (g[i].a.tap_group || g[i].b.tap_group)) return -1;
     const int m = 2 * (g[i].a.trans ? 1 : 0) + (g[i].b.trans ? 1 : 0);
     if (modes >= 0 && m != modes) return -1;
     modes = m;
   }
+  if (modes >= 0 && !((mask >> modes) & 1)) return -1;
   return modes;
 }
 
