@@ -33,6 +33,7 @@ baseline timed on this host.
 import argparse
 import json
 import os
+import random
 import sys
 import time
 
@@ -697,6 +698,10 @@ def main():
     p = dict(cfg['params'])
     torch.manual_seed(1623)
     native_ops.manual_seed(1623 + rank)
+    # the scheduled-sampling draws (attention configs: random.random() per
+    # decoder step, as the reference) seeded too, so a run's count of steps
+    # that sample -- and take the per-step decoder -- is reproducible
+    random.seed(1623 + rank)
     model = load(cfg['model_type'], p, 'pytorch')
     model.set_cuda()
     if world > 1:   # identical initial weights on every rank

@@ -275,6 +275,10 @@ __device__ __forceinline__ bf16x8 cvt_f32x8(const float* p) {
 }
 
 __device__ __forceinline__ float fsig(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+// ftanh's error is absolute (~1e-7 near 0, where tanh(x) ~ x): fine for the
+// bf16 paths, not for reference precision -- the F32 kernels take tanhf (an
+// LSTM with tiny inputs and forget-gate bias 1 carries h ~ 1e-6 for many steps,
+// where ftanh's error was 5 % per step)
 __device__ __forceinline__ float ftanh(float x) { return 2.f * fsig(2.f * x) - 1.f; }
 
 // Packed fp16 gate activations (act_h) that keep precision near saturation.
@@ -569,10 +573,10 @@ __global__ void __launch_bounds__(64 * NSW + R * XUF) lstm_fwd_xg(
       }
       ig = fsig(pre[0]);
       fg = fsig(pre[1]);
-      gg = ftanh(pre[2]);
+      gg = F32 ? tanhf(pre[2]) : ftanh(pre[2]);
       og = fsig(pre[3]);
       cn = fg * c + ig * gg;
-      h = og * ftanh(cn);
+      h = og * (F32 ? tanhf(cn) : ftanh(cn));
     }
     c = cn;
     const unsigned hb = f2bf(h);
@@ -1315,7 +1319,7 @@ __global__ void __launch_bounds__(256 + R * XB + 64 * (F32 ? 4 : XB / 4)) lstm_b
       // at B1 for the sweepers (the step's inputs are in registers since the
       // previous step): after B1 only dcell = dc + dh k_d and four products
       // remain on the step's critical path
-      const float tc = ftanh(cc);
+      const float tc = F32 ? tanhf(cc) : ftanh(cc);
       float k_d = og * (1.f - tc * tc);
       float k_i = gg * ig * omi, k_f = cp * fg * omf, k_g = ig * omg2;
       float k_o = tc * og * omo;
@@ -1348,7 +1352,7 @@ __global__ void __launch_bounds__(256 + R * XB + 64 * (F32 ? 4 : XB / 4)) lstm_b
         d_g = dcell * k_g;
         d_o = dh * k_o;
 #else
-        const float tc = ftanh(cc);
+        const float tc = F32 ? tanhf(cc) : ftanh(cc);
         float dcell = dc + dh * og * (1.f - tc * tc);
         if constexpr (!AH) asm volatile("" : "+v"(dcell));
         d_i = dcell * gg * ig * omi;
