@@ -922,6 +922,117 @@ __global__ void __launch_bounds__(256) ctc_grad_bf16(
   }
 }
 
+// The narrow head's gradient pass (V <= 256: the char / phone CTC heads):
+// ctc_grad_bf16<true>'s per-row work with each of a work-group's four waves on
+// rows of its own (a wave-private class table in LDS, no block barrier per
+// row).  ctc_grad_bf16<true> ran one 64-thread work-group per row or a
+// block's rows one after another: ~1000 single-wave work-groups, each a chain
+// of 31 rows at 32000 rows (ctc5x512: 106 us for 3.7 MB).  Here the rows of a
+// work-group are dealt to its waves round-robin (one row per wave by default,
+// the row's activation loads issued before its occupancy work), so the rows
+// run in parallel instead of as one wave's chain; the bias partials of the four
+// waves are summed in wave order into the block's colpart row (deterministic).
+// dY values: bitwise ctc_grad_bf16<true>'s (same per-row arithmetic and
+// atomic order within a wave).
+template <int NCH>
+__global__ void __launch_bounds__(256) ctc_grad_bf16_narrow(
+    const float* __restrict__ acts, long long st, long long sb, int T, int V,
+    const int32_t* __restrict__ labels, const int32_t* __restrict__ label_lens,
+    const int32_t* __restrict__ act_lens, const int32_t* __restrict__ offs, int blank, int Spad,
+    const float* __restrict__ lse, const float* __restrict__ emit,
+    const float* __restrict__ alpha, const float* __restrict__ beta,
+    const float* __restrict__ logp, const float* __restrict__ grad_scale, float scale_mul,
+    uint16_t* __restrict__ grads, long long gst, long long gsb, int gld, int rev,
+    float* __restrict__ colpart, int rpb, long long nrows) {
+  constexpr int NW = 4;
+  // occ [NW][V] | wave partials [NW][gld] (colpart only)
+  extern __shared__ __attribute__((aligned(16))) float lds_n[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float* occ = lds_n + wave * V;
+  const int n8 = gld >> 3;
+  const float scale = (grad_scale ? grad_scale[0] : 1.0f) * scale_mul;
+  float acc[NCH][8];
+#pragma unroll
+  for (int j = 0; j < NCH; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[j][e] = 0.f;
+  for (int r = wave; r < rpb; r += NW) {
+    const long long lin = (long long)blockIdx.x * rpb + r;
+    if (lin >= nrows) break;                       // wave-uniform
+    const long long row = rev ? nrows - 1 - lin : lin;
+    const int b = (int)(row / T), t = (int)(row % T);
+    uint16_t* g = grads + (long long)t * gst + (long long)b * gsb;
+    const float* x = acts + (long long)t * st + (long long)b * sb;
+    const int Tb = act_lens[b];
+    const float lp = logp[b];
+    if (t >= Tb || lp == neg_inf()) {               // row-uniform
+      for (int i = lane; i < n8; i += 64) reinterpret_cast<uint4*>(g)[i] = make_uint4(0u, 0u, 0u, 0u);
+      continue;
+    }
+    // the row's activations first: their loads overlap the occupancy work
+    float xv[NCH][8];
+#pragma unroll
+    for (int j = 0; j < NCH; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = 8 * (lane + 64 * j) + e;
+        xv[j][e] = c < V ? x[c] : 0.f;
+      }
+    const float z = lse[row];
+    const int L = min(label_lens[b], (Spad - 1) / 2);
+    const int S = 2 * L + 1;
+    const int32_t* lab = labels + offs[b];
+    const float* al = alpha + row * Spad;
+    const float* bt = beta + row * Spad;
+    const float* em = emit + row * Spad;
+    for (int v = lane; v < V; v += 64) occ[v] = 0.f;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    for (int s_ = lane; s_ < S; s_ += 64) {
+      int c = (s_ & 1) ? lab[s_ >> 1] : blank;
+      c = c < 0 ? 0 : (c >= V ? V - 1 : c);
+      atomicAdd(&occ[c], ex2(al[s_] + bt[s_] - em[s_] - lp));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      const int k = lane + 64 * j;
+      if (k >= n8) continue;
+      unsigned w[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c = 8 * k + 2 * q;
+        const float lo = c < V ? (__expf(xv[j][2 * q] - z) - occ[c]) * scale : 0.f;
+        const float hi = c + 1 < V ? (__expf(xv[j][2 * q + 1] - z) - occ[c + 1]) * scale : 0.f;
+        acc[j][2 * q] += lo;
+        acc[j][2 * q + 1] += hi;
+        w[q] = (c < V ? (unsigned)f2bf(lo) : 0u) | ((c + 1 < V ? (unsigned)f2bf(hi) : 0u) << 16);
+      }
+      reinterpret_cast<uint4*>(g)[k] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();   // occ is rewritten by this wave's next row
+  }
+  if (!colpart) return;
+  float* wp = lds_n + NW * V;   // [NW][gld]
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) {
+    const int k = lane + 64 * j;
+    if (k >= n8) continue;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) wp[wave * gld + 8 * k + e] = acc[j][e];
+  }
+  __syncthreads();
+  float* o = colpart + (long long)blockIdx.x * gld;
+  for (int c = threadIdx.x; c < gld; c += 64 * NW) {
+    float v = wp[c];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) v += wp[w * gld + c];
+    o[c] = v;
+  }
+}
+
 // The wide fused head's gradient pass (V > 256, 16-B aligned rows; the
 // class-table-free form of ctc_grad_bf16) with a block's rows software-
 // pipelined.  A block streams rpb consecutive rows one after another (the
@@ -1522,7 +1633,11 @@ static void ctc_bias_grid(int T, int B, int V, int* rpb, int* nblk) {
   // 185 + 33 us (gradient + column sums).  ASR_CTC_BIAS_BLOCKS: the target (A/B)
   const char* bb_env = getenv("ASR_CTC_BIAS_BLOCKS");   // per call: the tests switch it
   const long long env_target = bb_env ? atoll(bb_env) : 0;
-  const long long target = env_target > 0 ? env_target : 1024;
+  // narrow heads (V <= 256, ctc_grad_bf16_narrow): 4 rows per work-group, one
+  // per wave (the partials are gld <= 256 columns; a row is a chain of ~3
+  // dependent memory round trips, so rows in parallel, not in sequence: 16
+  // rows per work-group measured 54 us at 32000 rows)
+  const long long target = env_target > 0 ? env_target : V <= 256 ? (rows + 3) / 4 : 1024;
   long long r = rows / target;
   if (r < 1) r = 1;
   if (r > 64) r = 64;
@@ -1603,6 +1718,29 @@ static int ctc_backward_bf16_impl(const float* acts, long long stride_t, long lo
     if (al) ASR_CTC_G16A(TB, NC, true);      \
     else ASR_CTC_G16A(TB, NC, false);        \
   } while (0)
+  // narrow heads: four waves per work-group on rows of their own
+  // (ASR_CTC_GRAD_NARROW=0: ctc_grad_bf16<true>, one wave per work-group)
+  const char* en = getenv("ASR_CTC_GRAD_NARROW");
+  if (table && !(en && en[0] == '0')) {
+    if (!dbias) {
+      rpb = 4;
+      nblk = (int)((rows + 3) / 4);
+    }
+    const size_t ldsn = (size_t)(4 * V + (dbias ? 4 * gld : 0)) * sizeof(float);
+    hipLaunchKernelGGL((ctc_grad_bf16_narrow<1>), dim3((unsigned)nblk), dim3(256), ldsn, s, acts,
+                       stride_t, stride_b, T, V, labels_flat, label_lens, act_lens, ws.offs, blank,
+                       Spad, ws.lse, ws.emit, ws.alpha, ws.beta, ws.logp, grad_scale, scale, grads,
+                       gstride_t, gstride_b, gld, rev, colpart, rpb, rows);
+    ASR_LAUNCH_CHECK();
+    prof_end_launch(ASR_PROF_CTC_GRAD, pslot, s);
+    if (dbias) {
+      const size_t part = ((size_t)nblk * gld * sizeof(float) + 255) & ~(size_t)255;
+      rc = asr_colsum_accumulate(colpart, gld, nblk, V, 1.0f, dbias, nullptr, (char*)bws + part,
+                                 bws_bytes - part, stream);
+      if (rc) return rc;
+    }
+    return ASR_OK;
+  }
   const char* ep = getenv("ASR_CTC_GRAD_PIPE");   // 0: the unpipelined pass (A/B)
   const bool pipe = al && !table && nch > 0 && !(ep && ep[0] == '0');
   // the streamed pass (512 threads, 2 work-groups per CU): ASR_CTC_GRAD_STREAM=0 (A/B)

@@ -325,3 +325,43 @@ def test_wide_head_gradient_passes_agree(bias_blocks, cuda_dev, monkeypatch):
         d = float((st[i] - u[i]).norm() / u[i].norm())
         assert d < 2e-3, (i, d)
     assert float((st[2] - u[2]).abs().max()) <= 1e-5 * float(u[2].abs().max()) + 1e-9
+
+
+def test_narrow_head_gradient_waves_match_single_wave(cuda_dev, monkeypatch):
+    """The narrow head's gradient pass (V <= 256) with four waves per
+    work-group on rows of their own (ctc_grad_bf16_narrow, the default)
+    against one wave per work-group (ASR_CTC_GRAD_NARROW=0): dX / dW bitwise
+    (the same bf16 dY: per-row arithmetic and atomic order unchanged), bias
+    within 1e-6 (the per-wave partials add in another order).  Ragged lengths
+    and a row count that is not a multiple of the 16 rows per work-group."""
+    ops = _native()
+    rng = np.random.RandomState(31)
+    B, T, K, V = 7, 83, 96, 29
+    act_lens = np.sort(rng.randint(30, T + 1, B))[::-1].astype(np.int32)
+    act_lens[0] = T
+    label_lens = rng.randint(3, 30, B).astype(np.int32)
+    labels = np.concatenate([rng.randint(1, V, l) for l in label_lens]).astype(np.int32)
+    x0 = torch.from_numpy((rng.randn(B, T, K) * 0.5).astype(np.float32)).to(cuda_dev)
+    w0 = torch.from_numpy((rng.randn(V, K) * 0.1).astype(np.float32)).to(cuda_dev)
+    b0 = torch.from_numpy((rng.randn(V) * 0.1).astype(np.float32)).to(cuda_dev)
+    lab = torch.from_numpy(labels).to(cuda_dev)
+    ll = torch.from_numpy(label_lens).to(cuda_dev)
+    al = torch.from_numpy(act_lens).to(cuda_dev)
+    ops.set_compute_dtype('bf16')
+    out = {}
+    try:
+        for narrow in ('1', '0'):
+            monkeypatch.setenv('ASR_CTC_GRAD_NARROW', narrow)
+            x = x0.clone().requires_grad_(True)
+            w = w0.clone().requires_grad_(True)
+            b = b0.clone().requires_grad_(True)
+            loss, _ = ops.linear_ctc_loss(x, w, b, lab, ll, al, int(label_lens.max()), 1.0 / B)
+            loss.backward()
+            torch.cuda.synchronize()
+            out[narrow] = [x.grad.clone(), w.grad.clone(), b.grad.clone()]
+    finally:
+        ops.set_compute_dtype('fp32')
+    n, o = out['1'], out['0']
+    assert torch.equal(n[0], o[0]), float((n[0] - o[0]).abs().max())
+    assert torch.equal(n[1], o[1]), float((n[1] - o[1]).abs().max())
+    assert float((n[2] - o[2]).abs().max()) <= 1e-6 * float(o[2].abs().max()) + 1e-9
