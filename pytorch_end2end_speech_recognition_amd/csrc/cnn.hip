@@ -1248,6 +1248,78 @@ __global__ void __launch_bounds__(RW_NT) rw_bn_moments(const TD* __restrict__ dn
   rw_reduce(s2, cg8, C, red, partial + ((long long)blockIdx.x * 2 + 1) * C);
 }
 
+// rw_bn_moments with NT threads per work-group and U rows-walkers per lane
+// (U 16-B load pairs in flight per lane): the pass reads 1.1 GB per vgg_hier
+// step at ~2 TB/s with NT = 256, U = 1 -- its grid is capped by the 1024
+// partial rows, so the loads in flight per CU are what it can raise.  Sums in
+// walker order, then lane order (deterministic; another association than
+// U = 1).  ASR_VGG_BNM=<NT>x<U> selects it (A/B).
+template <int NT>
+__device__ __forceinline__ void rw_reduce_nt(const float (&acc)[8], int cg8, int C, float* red,
+                                             float* __restrict__ out) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[tid * 8 + j] = acc[j];
+  __syncthreads();
+  for (int cc = tid; cc < C; cc += NT) {
+    const int g = cc >> 3, j = cc & 7;
+    float t = 0.f;
+    for (int k = g; k < NT; k += cg8) t += red[k * 8 + j];
+    out[cc] = t;
+  }
+  __syncthreads();
+}
+template <typename TD, int NT, int U>
+__global__ void __launch_bounds__(NT) rw_bn_moments_nu(const TD* __restrict__ dnext,
+                                                       const uint16_t* __restrict__ P, int B,
+                                                       int To, int Fo, int C, int flat,
+                                                       Affine af, float* __restrict__ partial,
+                                                       int rpb) {
+  extern __shared__ __attribute__((aligned(16))) float red_nu[];   // [NT * 8]
+  const int tid = threadIdx.x, cg8 = C >> 3;
+  const int c = (tid & (cg8 - 1)) * 8;
+  float m[8], rs[8], s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    m[j] = af.mean[c + j];
+    rs[j] = af.rstd[c + j];
+    s1[j] = s2[j] = 0.f;
+  }
+  const int rows = B * To, ng = Fo * cg8;
+  const int r0 = blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
+  RowWalk it[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) it[u] = RowWalk(r0, r1, To, ng, u * NT);
+  while (it[0].r < r1) {
+    Bf8 gv[U], x[U];
+    long long pe[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long e = (long long)it[u].g * 8;
+      pe[u] = (long long)it[u].r * Fo * C + e;
+      if (it[u].r < r1) {
+        gv[u].load(dnext + row_base(it[u].b, it[u].t, To, Fo, C, flat) + e);
+        x[u].load(P + pe[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (it[u].r >= r1) continue;
+      if (af.drop > 0.f) {
+        drop_n_aligned<8>(gv[u].v, af.drop, af.seed, (unsigned long long)pe[u]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s1[j] += gv[u].v[j];
+        s2[j] += gv[u].v[j] * (x[u].v[j] - m[j]) * rs[j];
+      }
+      it[u].next(r1, To, ng, U * NT);
+    }
+  }
+  rw_reduce_nt<NT>(s1, cg8, C, red_nu, partial + (long long)blockIdx.x * 2 * C);
+  rw_reduce_nt<NT>(s2, cg8, C, red_nu, partial + ((long long)blockIdx.x * 2 + 1) * C);
+}
+
 // dz over full-resolution rows (as post_bwd_full, BN present): each pixel takes
 // its window's gradient where it was the argmax (PL = 2) and the pooled /
 // unpooled value P > 0 (the ReLU mask); bf16 dz at every interior pixel, the
@@ -2135,7 +2207,21 @@ static int vgg_block_backward_impl(const void* dnext_v, int dnext_dtype, int fla
     if (rows_b) {   // row-blocked moments: at most nchunk blocks
       const int nrow = B * pl.To, rpb = (nrow + nchunk - 1) / nchunk;
       mchunk = (nrow + rpb - 1) / rpb;
-      if (db16)
+      const char* bnm = getenv("ASR_VGG_BNM");   // "<NT>x<U>" (A/B; read per call)
+      int bnt = 256, bu = 1;
+      if (bnm) sscanf(bnm, "%dx%d", &bnt, &bu);
+      const size_t lnu = (size_t)bnt * 8 * sizeof(float);
+#define ASR_BNM(NT, U)                                                                           \
+  hipLaunchKernelGGL((rw_bn_moments_nu<uint16_t, NT, U>), dim3(mchunk), dim3(NT), lnu, s, dnh,   \
+                     (const uint16_t*)P, B, pl.To, pl.Fo, C, flat, af, part, rpb)
+      if (db16 && bnt == 256 && bu == 2) ASR_BNM(256, 2);
+      else if (db16 && bnt == 256 && bu == 4) ASR_BNM(256, 4);
+      else if (db16 && bnt == 512 && bu == 1) ASR_BNM(512, 1);
+      else if (db16 && bnt == 512 && bu == 2) ASR_BNM(512, 2);
+      else if (db16 && bnt == 1024 && bu == 1) ASR_BNM(1024, 1);
+      else if (db16 && bnt == 1024 && bu == 2) ASR_BNM(1024, 2);
+#undef ASR_BNM
+      else if (db16)
         hipLaunchKernelGGL((rw_bn_moments<uint16_t>), dim3(mchunk), dim3(RW_NT), 0, s, dnh,
                            (const uint16_t*)P, B, pl.To, pl.Fo, C, flat, af, part, rpb);
       else
