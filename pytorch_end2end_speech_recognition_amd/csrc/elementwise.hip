@@ -212,7 +212,73 @@ inline int grid_for(long long n) {
   return (int)(b < 4096 ? (b > 0 ? b : 1) : 4096);
 }
 
+// Up to four row-map conversions (the vector form of convert_rows_kernel<false>:
+// ncols % 8 == 0, ld % 8 == 0, 16-B aligned rows) in one launch: job k owns
+// blocks [blk0[k], blk0[k + 1]).  The GEMM's operand staging converted each
+// f32 operand in a launch of its own, ~5 us apiece however small.
+struct ConvJob {
+  const float* src;
+  asr_rowmap_t m;
+  int nrows, ld;
+  uint16_t* dst;
+  int blk0;
+};
+struct ConvJobs {
+  ConvJob j[4];
+  int n;
+};
+__global__ void __launch_bounds__(256) convert_rows_multi(ConvJobs J) {
+  int k = 0;
+  while (k + 1 < J.n && (int)blockIdx.x >= J.j[k + 1].blk0) ++k;
+  const ConvJob& jb = J.j[k];
+  const int nb = (k + 1 < J.n ? J.j[k + 1].blk0 : (int)gridDim.x) - jb.blk0;
+  const asr_rowmap_t& m = jb.m;
+  const int cpr = jb.ld >> 3;
+  const long long nchunks = (long long)jb.nrows * cpr;
+  const int rpb = m.rows_per_b > 0 ? m.rows_per_b : 0x7fffffff;
+  const int tmul = m.t_mul == 0 ? 1 : m.t_mul;
+  const int tlim = m.t_limit > 0 ? m.t_limit : 0x7fffffff;
+  for (long long e = (long long)(blockIdx.x - jb.blk0) * blockDim.x + threadIdx.x; e < nchunks;
+       e += (long long)nb * blockDim.x) {
+    const int r = (int)(e / cpr), c0 = (int)(e - (long long)r * cpr) * 8;
+    const int b = r / rpb, t = r - b * rpb;
+    const int tp = t * tmul + m.t_add;
+    const bool ok = tp >= 0 && tp < tlim;
+    u16x8 v = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (ok) {
+      const float* s = jb.src + (long long)(m.perm ? m.perm[b] : b) * m.stride_b +
+                       (long long)tp * m.stride_t + c0;
+      const float4 x0 = *reinterpret_cast<const float4*>(s);
+      const float4 x1 = *reinterpret_cast<const float4*>(s + 4);
+      v = u16x8{f2bf(x0.x), f2bf(x0.y), f2bf(x0.z), f2bf(x0.w),
+                f2bf(x1.x), f2bf(x1.y), f2bf(x1.z), f2bf(x1.w)};
+    }
+    *reinterpret_cast<u16x8*>(jb.dst + (long long)r * jb.ld + c0) = v;
+  }
+}
+
 }  // namespace
+
+// n <= 4 conversions with ncols == ld (multiples of 8) and 16-B aligned rows,
+// one launch (the GEMM operand staging); false when a job does not qualify
+// (the caller converts one by one)
+int convert_rows_bf16_multi(const float* const* src, const asr_rowmap_t* maps, const int* nrows,
+                            const int* ncols, uint16_t* const* dst, int n, void* stream) {
+  if (n < 1 || n > 4) return 0;
+  ConvJobs J{};
+  int blk = 0;
+  for (int k = 0; k < n; ++k) {
+    if (ncols[k] % 8 || nrows[k] <= 0 || ((uintptr_t)src[k] & 15) || ((uintptr_t)dst[k] & 15) ||
+        maps[k].stride_t % 4 || maps[k].stride_b % 4)
+      return 0;
+    J.j[k] = ConvJob{src[k], maps[k], nrows[k], ncols[k], dst[k], blk};
+    blk += grid_for((long long)nrows[k] * (ncols[k] / 8));
+  }
+  J.n = n;
+  hipLaunchKernelGGL(convert_rows_multi, dim3(blk), dim3(256), 0, (hipStream_t)stream, J);
+  return hipGetLastError() == hipSuccess ? 1 : -1;
+}
+
 }  // namespace asr
 
 using namespace asr;

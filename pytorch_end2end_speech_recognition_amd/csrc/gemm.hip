@@ -2772,6 +2772,11 @@ int gemm_launch_own(const asr_gemm_t* problems, int nprob, int compute_dtype, vo
 // 8-wave kernels; the arithmetic is unchanged (bf16 operands, f32 accumulate).
 // ASR_GEMM_STAGE=0 keeps the generic kernel (A/B).
 constexpr double STAGE_FLOPS = 3.2e7;
+}  // namespace
+// elementwise.hip: up to four conversions in one launch (1), or 0 (not eligible)
+int convert_rows_bf16_multi(const float* const* src, const asr_rowmap_t* maps, const int* nrows,
+                            const int* ncols, uint16_t* const* dst, int n, void* stream);
+namespace {
 
 struct StagePlan {
   bool on[2][2];
@@ -2838,6 +2843,30 @@ int gemm_launch(const asr_gemm_t* problems, int nprob, int compute_dtype, void* 
     const size_t base = split_bytes_aligned(problems, nprob);
     const StagePlan st = plan_stage(problems, nprob, base);
     if (st.bytes > 0 && ws_bytes >= base + st.bytes) {
+      // every staged operand in one launch when all take the vector form
+      // (ASR_GEMM_STAGE_MULTI=0: one launch per operand)
+      const float* msrc[4];
+      asr_rowmap_t mmap[4];
+      int mrows[4], mcols[4], nm = 0;
+      uint16_t* mdst[4];
+      bool multi = !(getenv("ASR_GEMM_STAGE_MULTI") && getenv("ASR_GEMM_STAGE_MULTI")[0] == '0');
+      for (int i = 0; i < nprob && multi; ++i)
+        for (int j = 0; j < 2; ++j) {
+          if (!st.on[i][j]) continue;
+          const asr_operand_t& op = j ? problems[i].b : problems[i].a;
+          if (st.cols[i][j] != st.ld[i][j]) multi = false;
+          msrc[nm] = (const float*)op.ptr;
+          mmap[nm] = op.map;
+          mrows[nm] = st.rows[i][j];
+          mcols[nm] = st.cols[i][j];
+          mdst[nm] = (uint16_t*)((char*)workspace + st.off[i][j]);
+          ++nm;
+        }
+      int done = 0;
+      if (multi && nm > 1) {
+        done = convert_rows_bf16_multi(msrc, mmap, mrows, mcols, mdst, nm, stream);
+        ASR_REQUIRE(done >= 0, ASR_ERR_HIP, "gemm: operand staging launch failed");
+      }
       asr_gemm_t g2[2];
       for (int i = 0; i < nprob; ++i) {
         g2[i] = problems[i];
@@ -2845,8 +2874,10 @@ int gemm_launch(const asr_gemm_t* problems, int nprob, int compute_dtype, void* 
           if (!st.on[i][j]) continue;
           asr_operand_t& op = j ? g2[i].b : g2[i].a;
           uint16_t* dst = (uint16_t*)((char*)workspace + st.off[i][j]);
-          const int rc = asr_convert_rows_bf16_ld((const float*)op.ptr, op.map, st.rows[i][j],
-                                                  st.cols[i][j], st.ld[i][j], dst, stream);
+          const int rc = done ? 0
+                              : asr_convert_rows_bf16_ld((const float*)op.ptr, op.map,
+                                                         st.rows[i][j], st.cols[i][j],
+                                                         st.ld[i][j], dst, stream);
           if (rc) return rc;
           op.ptr = dst;
           op.dtype = ASR_DT_BF16;
