@@ -2685,9 +2685,11 @@ extern "C" int asr_attdec_backward_ex(const asr_attdec_dims_t* dims, const asr_a
     g.a.ptr = dec;
     g.a.dtype = ASR_DT_F32;
     g.a.map.stride_t = d.D;
+    g.a.bytes = 4LL * d.B * d.S * d.D;   // the extents: the f32 fast kernel's buffer bounds
     g.b.ptr = w_dec;
     g.b.dtype = ASR_DT_F32;
     g.b.map.stride_t = d.D;
+    g.b.bytes = 4LL * d.A * d.D;
     g.c = wd_all;
     g.c_map.stride_t = d.A;
     g.M = d.B * d.S; g.N = d.A; g.K = d.D;
@@ -2960,9 +2962,11 @@ extern "C" int asr_att_step_backward(const asr_attdec_dims_t* dims, const float*
     g.a.ptr = dec2;
     g.a.dtype = ASR_DT_F32;
     g.a.map.stride_t = d.D;
+    g.a.bytes = 4LL * d.B * 2 * d.D;
     g.b.ptr = w_dec;
     g.b.dtype = ASR_DT_F32;
     g.b.map.stride_t = d.D;
+    g.b.bytes = 4LL * d.A * d.D;
     g.c = wd2;
     g.c_map.stride_t = d.A;
     g.M = d.B * 2; g.N = d.A; g.K = d.D;
