@@ -2791,11 +2791,20 @@ StagePlan plan_stage(const asr_gemm_t* g, int nprob, size_t base) {
   if (e && e[0] == '0') return sp;
   bool any = false;
   for (int i = 0; i < nprob; ++i) {
-    if (g[i].batch > 1 || g[i].K % 8 || 2.0 * g[i].M * g[i].N * g[i].K < STAGE_FLOPS) return sp;
+    // batched products (the attention context's per-utterance products): each
+    // operand staged as [batch][rows][ld] through a row map whose utterance
+    // stride is the operand's batch stride; a K that is not a multiple of 8
+    // only when both operands are K-major (the fast kernels' R-mode rows need it)
+    const int nb = g[i].batch > 1 ? g[i].batch : 1;
+    const bool kk = g[i].a.trans && g[i].b.trans;
+    if ((g[i].K % 8 && !kk) || 2.0 * g[i].M * g[i].N * g[i].K * nb < STAGE_FLOPS) return sp;
     for (int j = 0; j < 2; ++j) {
       const asr_operand_t& op = j ? g[i].b : g[i].a;
       if (op.dtype != ASR_DT_F32) continue;
       if (op.tap_group) return sp;
+      if (nb > 1 && (op.map.rows_per_b > 0 || op.map.perm || (op.map.t_mul != 0 && op.map.t_mul != 1) ||
+                     (j ? g[i].batch_stride_b : g[i].batch_stride_a) % 4))
+        return sp;
       const int outer = j ? g[i].N : g[i].M;
       const int cols = op.trans ? outer : g[i].K;
       if (cols % 8 == 0 && (!aligned16(op.ptr) || op.map.stride_t % 4 || op.map.stride_b % 4))
@@ -2815,10 +2824,23 @@ StagePlan plan_stage(const asr_gemm_t* g, int nprob, size_t base) {
       sp.cols[i][j] = op.trans ? outer : g[i].K;
       sp.ld[i][j] = (sp.cols[i][j] + 7) / 8 * 8;
       sp.off[i][j] = o;
-      o += ((size_t)sp.rows[i][j] * sp.ld[i][j] * 2 + 255) & ~(size_t)255;
+      const int nb = g[i].batch > 1 ? g[i].batch : 1;
+      o += ((size_t)nb * sp.rows[i][j] * sp.ld[i][j] * 2 + 255) & ~(size_t)255;
     }
   sp.bytes = o - base;
   return sp;
+}
+
+// the conversion's row map of operand j of g: the operand's own map, and for a
+// batched product its utterances as blocks of `rows` rows at the batch stride
+asr_rowmap_t stage_map(const asr_gemm_t& g, int j, int rows) {
+  const asr_operand_t& op = j ? g.b : g.a;
+  asr_rowmap_t m = op.map;
+  if (g.batch > 1) {
+    m.rows_per_b = rows;
+    m.stride_b = j ? g.batch_stride_b : g.batch_stride_a;
+  }
+  return m;
 }
 
 size_t split_bytes_aligned(const asr_gemm_t* g, int nprob) {
@@ -2856,8 +2878,8 @@ int gemm_launch(const asr_gemm_t* problems, int nprob, int compute_dtype, void* 
           const asr_operand_t& op = j ? problems[i].b : problems[i].a;
           if (st.cols[i][j] != st.ld[i][j]) multi = false;
           msrc[nm] = (const float*)op.ptr;
-          mmap[nm] = op.map;
-          mrows[nm] = st.rows[i][j];
+          mmap[nm] = stage_map(problems[i], j, st.rows[i][j]);
+          mrows[nm] = st.rows[i][j] * (problems[i].batch > 1 ? problems[i].batch : 1);
           mcols[nm] = st.cols[i][j];
           mdst[nm] = (uint16_t*)((char*)workspace + st.off[i][j]);
           ++nm;
@@ -2874,16 +2896,20 @@ int gemm_launch(const asr_gemm_t* problems, int nprob, int compute_dtype, void* 
           if (!st.on[i][j]) continue;
           asr_operand_t& op = j ? g2[i].b : g2[i].a;
           uint16_t* dst = (uint16_t*)((char*)workspace + st.off[i][j]);
+          const int nbt = problems[i].batch > 1 ? problems[i].batch : 1;
           const int rc = done ? 0
-                              : asr_convert_rows_bf16_ld((const float*)op.ptr, op.map,
-                                                         st.rows[i][j], st.cols[i][j],
+                              : asr_convert_rows_bf16_ld((const float*)op.ptr,
+                                                         stage_map(problems[i], j, st.rows[i][j]),
+                                                         st.rows[i][j] * nbt, st.cols[i][j],
                                                          st.ld[i][j], dst, stream);
           if (rc) return rc;
           op.ptr = dst;
           op.dtype = ASR_DT_BF16;
           memset(&op.map, 0, sizeof(op.map));
           op.map.stride_t = st.ld[i][j];
-          op.bytes = (long long)st.rows[i][j] * st.ld[i][j] * 2;
+          op.bytes = (long long)nbt * st.rows[i][j] * st.ld[i][j] * 2;
+          if (nbt > 1) (j ? g2[i].batch_stride_b : g2[i].batch_stride_a) =
+              (long long)st.rows[i][j] * st.ld[i][j];
         }
       }
       return gemm_launch_own(g2, nprob, compute_dtype, workspace, ws_bytes, stream);
