@@ -126,6 +126,12 @@ int asr_ctc_fwd_bwd(const float* acts, long long stride_t, long long stride_b, i
                     const int32_t* act_lens, int max_label_len, int blank, int zero_infinity,
                     float* costs, float* grads, void* workspace, size_t ws_bytes, void* stream);
 
+/* Which kernels the last CTC forward / gradient ran (host-side record), out2 =
+ * {normaliser: 0 the emission pass over the logits, 1 the head GEMM
+ * epilogue's partials; gradient: 0 f32 ctc_grad, 1 ctc_grad_bf16, 2 narrow
+ * (V <= 256), 3 pipelined, 4 streamed}. */
+int asr_ctc_last_path(int* out2);
+
 /* ---------------------------------------------------------------- GEMM
  * C(m,n) = alpha * sum_k A(m,k) B(n,k) + beta * C(m,n) + bias[n] + bias2[n]  (f32 C)
  * Replaces every nn.Linear / LinearND GEMM (linear.py:15-47) and the LSTM
@@ -332,6 +338,11 @@ int asr_lstm_unpack_act_h(const uint16_t* act_h, int B, int T, int H, float* act
  * 256 threads that fill 64 KB of LDS with a pattern and check it `iters`
  * times; mismatches are added to *bad (device int). */
 int asr_diag_lds_spin(int nwg, int iters, int* bad, void* stream);
+
+/* Diagnostics only (tests/test_coresidency_gpu.py): nwg work-groups of 256
+ * threads holding lds_bytes of LDS each stay resident for usec microseconds
+ * (a long-lived kernel beside the next persistent recurrence launch). */
+int asr_diag_hold_cus(int nwg, int lds_bytes, int usec, void* stream);
 
 /* ------------------------------------------------------------ GRU layer
  * Replaces the packed nn.GRU(bidirectional=True) of
@@ -873,6 +884,13 @@ int asr_lstm_status_inject(int bits, void* stream);
  * XCD-local (every group's work-groups registered on one XCD).  Synchronises
  * the device. */
 int asr_lstm_xg_mode(int* mode, int clear);
+
+/* Which recurrence implementation the last BLSTM layer pass ran (host-side
+ * record), out2 = {forward pass, backward pass}: 0 per-step kernels, 1
+ * tagged-granule bf16, 2 tagged-granule f32 (reference precision), 3
+ * tagged-granule bf16 with the fused input projection, 4 counter-form
+ * persistent. */
+int asr_lstm_last_path(int* out2);
 
 /* Diagnostics (ASR_XG_TRACE=1 at the first recurrence launch): copies the
  * per-step phase timestamps of work-groups 0..63 (64 x 128 steps x 12 u64) to

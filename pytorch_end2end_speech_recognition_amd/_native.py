@@ -98,6 +98,7 @@ SIGNATURES = {
     'asr_lstm_backward_dgbf_h': (c_int, [c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int,
                                          c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
     'asr_diag_lds_spin': (c_int, [c_int, c_int, c_vp, c_vp]),
+    'asr_diag_hold_cus': (c_int, [c_int, c_int, c_int, c_vp]),
     'asr_lstm_unpack_act_h': (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp]),
     'asr_gru_workspace_bytes': (c_size, [c_int, c_int]),
     'asr_gru_forward': (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp]),
@@ -217,6 +218,8 @@ SIGNATURES = {
     'asr_att_step_forward': (c_int, [c_vp] + [c_vp] * 12 + [c_size, c_vp]),
     'asr_att_step_backward': (c_int, [c_vp] + [c_vp] * 21 + [c_size, c_vp]),
     'asr_lstm_xg_mode': (c_int, [c_vp, c_int]),
+    'asr_lstm_last_path': (c_int, [c_vp]),
+    'asr_ctc_last_path': (c_int, [c_vp]),
     'asr_xg_trace_read': (c_ll, [c_vp]),
     'asr_lstm_debug_dh': (c_int, [c_vp, c_vp, c_vp, c_vp]),
     'asr_lstm_set_bwd_pin_kb': (c_int, [c_int]),

@@ -257,10 +257,11 @@ __global__ void __launch_bounds__(256) ctc_lse_from_parts(const float* __restric
     float mq = m;
 #pragma unroll
     for (int k = 0; k < QB; ++k) mq = fmaxf(mq, pq[k].x);
-    sm = m == neg_inf() ? 0.f : sm * __expf(m - mq);
+    // (with m still -inf, sm holds only empty slabs' sums: 0, or a NaN to keep)
+    sm = m == neg_inf() ? sm : sm * __expf(m - mq);
 #pragma unroll
-    for (int k = 0; k < QB; ++k)
-      if (pq[k].x != neg_inf()) sm += pq[k].y * __expf(pq[k].x - mq);
+    for (int k = 0; k < QB; ++k)   // an empty slab's sum is 0, or NaN from a NaN logit
+      sm += pq[k].x != neg_inf() ? pq[k].y * __expf(pq[k].x - mq) : pq[k].y;
     m = mq;
   }
   lse_out[row] = m + __logf(sm);
@@ -1500,6 +1501,20 @@ static int ctc_row_order() {
   return v;
 }
 
+// Which kernels the last CTC forward / gradient ran (host-side record;
+// asr_ctc_last_path): {normaliser: 0 the emission pass over the logits, 1 the
+// head GEMM epilogue's (max, sum exp) partials; gradient: 0 f32 ctc_grad,
+// 1 ctc_grad_bf16, 2 ctc_grad_bf16_narrow, 3 ctc_grad_bf16_pipe,
+// 4 ctc_grad_bf16_stream}.
+static int g_ctc_last_path[2];
+
+extern "C" int asr_ctc_last_path(int* out2) {
+  ASR_REQUIRE(out2, ASR_ERR_ARG, "ctc_last_path: null pointer");
+  out2[0] = g_ctc_last_path[0];
+  out2[1] = g_ctc_last_path[1];
+  return ASR_OK;
+}
+
 static int ctc_forward_impl(const float* acts, long long stride_t, long long stride_b, int T,
                             int B, int V, const float* lse_part, int nslab,
                             const int32_t* labels_flat, const int32_t* label_lens,
@@ -1525,6 +1540,7 @@ static int ctc_forward_impl(const float* acts, long long stride_t, long long str
   // or with the GEMM's partials, those (8 B per slab per row)
   const int pslot = prof_begin_launch(
       ASR_PROF_CTC_FWD, s, (lse_part ? 8.0 * nslab : 4.0 * (double)V) * (double)rows, V);
+  g_ctc_last_path[0] = lse_part ? 1 : 0;
   if (lse_part) {
     hipLaunchKernelGGL(ctc_lse_from_parts, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s,
                        lse_part, nslab, rows, T, act_lens, 0, ws.lse);
@@ -1606,6 +1622,7 @@ extern "C" int asr_ctc_backward(const float* acts, long long stride_t, long long
   const int threads = table ? 64 : 256;  // compact mode: Spad <= 1024 = 4 * threads
   // algorithmic HBM bytes: activations read + gradient written
   const int pslot = prof_begin_launch(ASR_PROF_CTC_GRAD, s, 8.0 * (double)V * B * T, V);
+  g_ctc_last_path[1] = 0;
   if (table)
     hipLaunchKernelGGL(ctc_grad<true>, dim3((unsigned)((long long)B * T)), dim3(threads),
                        V * sizeof(float), s, acts, stride_t, stride_b, T, V, labels_flat,
@@ -1727,6 +1744,7 @@ static int ctc_backward_bf16_impl(const float* acts, long long stride_t, long lo
       nblk = (int)((rows + 3) / 4);
     }
     const size_t ldsn = (size_t)(4 * V + (dbias ? 4 * gld : 0)) * sizeof(float);
+    g_ctc_last_path[1] = 2;
     hipLaunchKernelGGL((ctc_grad_bf16_narrow<1>), dim3((unsigned)nblk), dim3(256), ldsn, s, acts,
                        stride_t, stride_b, T, V, labels_flat, label_lens, act_lens, ws.offs, blank,
                        Spad, ws.lse, ws.emit, ws.alpha, ws.beta, ws.logp, grad_scale, scale, grads,
@@ -1762,6 +1780,7 @@ static int ctc_backward_bf16_impl(const float* acts, long long stride_t, long lo
     rpb = (int)rp2;
     nblk = (int)((rows + rp2 - 1) / rp2);
     const size_t lds2 = (size_t)(5 * Spad + n8s + 8) * sizeof(float);
+    g_ctc_last_path[1] = 4;
 #define ASR_CTC_GS(NC)                                                                           \
   hipLaunchKernelGGL((ctc_grad_bf16_stream<NC>), dim3((unsigned)nblk), dim3(512), lds2, s, acts, \
                      stride_t, stride_b, T, V, labels_flat, label_lens, act_lens, ws.offs, blank, \
@@ -1780,6 +1799,7 @@ static int ctc_backward_bf16_impl(const float* acts, long long stride_t, long lo
                      Spad, ws.lse, ws.emit, ws.alpha, ws.beta, ws.logp, grad_scale, scale, grads, \
                      gstride_t, gstride_b, gld, rev, abytes, colpart, rpb, rows)
   if (pipe) {
+    g_ctc_last_path[1] = 3;
     switch (nch) {
       case 1: ASR_CTC_GP(1); break;
       case 2: ASR_CTC_GP(2); break;
@@ -1788,9 +1808,11 @@ static int ctc_backward_bf16_impl(const float* acts, long long stride_t, long lo
       default: ASR_CTC_GP(8); break;
     }
   } else if (table) {
+    g_ctc_last_path[1] = 1;
     if (nch) ASR_CTC_G16A(true, 1, false);
     else ASR_CTC_G16A(true, 0, false);
   } else {
+    g_ctc_last_path[1] = 1;
     switch (nch) {
       case 0: ASR_CTC_G16(false, 0); break;
       case 1: ASR_CTC_G16(false, 1); break;

@@ -280,13 +280,18 @@ __device__ __forceinline__ float row16_sum(float x) {
 __device__ __forceinline__ void lse_pair_store(const Problem& pr, int q, int m, const float (&v)[4],
                                                float mx, int lane) {
   mx = row16_max(mx);
+  // fmaxf drops NaN, so a NaN logit is carried by the sum instead: with the
+  // slab's max -inf (every column -inf, past N, or NaN) the exponentials are
+  // taken against 0, which gives 0 for -inf and NaN for NaN.  Every slab of
+  // the row's extent stores its pair (a skipped store left the
+  // partials uninitialised, so a diverged forward could fold a finite loss);
+  // the fold (ctc_lse_from_parts) adds an empty slab's sum as is.
+  const float base = mx == neg_inf() ? 0.f : mx;
   float sm = 0.f;
-  if (mx != neg_inf()) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) sm += __expf(v[e] - mx);
-  }
+  for (int e = 0; e < 4; ++e) sm += __expf(v[e] - base);
   sm = row16_sum(sm);
-  if ((lane & 15) == 0 && m < pr.M && mx != neg_inf()) {
+  if ((lane & 15) == 0 && m < pr.M && 64 * q < pr.N) {
     float* p = pr.lse + 2 * ((long long)q * pr.M + m);
     p[0] = mx;
     p[1] = sm;

@@ -544,6 +544,21 @@ extern "C" int asr_colsum_accumulate(const float* g, long long ld, int M, int N,
                                      float* out0, float* out1, void* workspace, size_t ws_bytes,
                                      void* stream);
 
+namespace asr {
+// Which recurrence implementation the last layer pass ran, per direction of
+// the pass {forward, backward} (host-side record; asr_lstm_last_path):
+// 0 per-step kernels, 1 tagged-granule bf16 (lstm_xg.hip), 2 tagged-granule
+// f32, 3 tagged-granule bf16 with the fused input projection, 4 counter form.
+int g_lstm_last_path[2];
+}  // namespace asr
+
+extern "C" int asr_lstm_last_path(int* out2) {
+  ASR_REQUIRE(out2, ASR_ERR_ARG, "lstm_last_path: null pointer");
+  out2[0] = asr::g_lstm_last_path[0];
+  out2[1] = asr::g_lstm_last_path[1];
+  return ASR_OK;
+}
+
 // backward: 0 forward, 1 backward, 2 backward with bias gradients (asr_lstm_backward_db)
 extern "C" size_t asr_lstm_workspace_bytes(int B, int H, int compute_dtype, int backward) {
   if (backward == 2) return bwd_ws_bias(B, H, compute_dtype);
@@ -575,6 +590,7 @@ extern "C" int asr_lstm_forward(float* gx_act, const void* whh_f, const void* wh
                                       gx_act, y, cst, workspace, ybf, s, false);
     ASR_REQUIRE(rc == 1, ASR_ERR_HIP, "lstm_forward: tagged-granule launch failed");
     prof_end_launch(ASR_PROF_LSTM_FWD_SEQ, slot, s);
+    g_lstm_last_path[0] = 1;
     return ASR_OK;
   }
   if (!bf && lstm_fwd_xg32_launch(B, T, H, lens, (const float*)whh_f, (const float*)whh_r, gx_act,
@@ -585,6 +601,7 @@ extern "C" int asr_lstm_forward(float* gx_act, const void* whh_f, const void* wh
                                         gx_act, y, cst, workspace, s, false);
     ASR_REQUIRE(rc == 1, ASR_ERR_HIP, "lstm_forward: f32 tagged-granule launch failed");
     prof_end_launch(ASR_PROF_LSTM_FWD_SEQ, slot, s);
+    g_lstm_last_path[0] = 2;
     if (ybf) {
       const long long n = (long long)B * T * 2 * H;
       hipLaunchKernelGGL(to_bf16, dim3((unsigned)min(4096LL, (n + 255) / 256)), dim3(256), 0, s, y,
@@ -616,8 +633,10 @@ extern "C" int asr_lstm_forward(float* gx_act, const void* whh_f, const void* wh
                                        ctr, ybf, s, false);
     ASR_REQUIRE(rc == 1, ASR_ERR_HIP, "lstm_forward: persistent launch failed");
     prof_end_launch(ASR_PROF_LSTM_FWD_SEQ, slot, s);
+    g_lstm_last_path[0] = 4;
     return ASR_OK;
   }
+  g_lstm_last_path[0] = 0;
   ASR_CHECK_HIP(hipMemsetAsync(workspace, 0, fwd_state_bytes(B, H, compute_dtype), s));
   const int nks = H / 32;
   const int fast_ks = (bf && H % 32 == 0) ? (nks <= 4 ? 1 : nks <= 8 ? 2 : nks <= 16 ? 4 :
@@ -677,6 +696,7 @@ static int lstm_backward_impl(const float* dy, const void* whh_f, const void* wh
     ASR_REQUIRE(rc == 1, ASR_ERR_HIP, "lstm_backward: tagged-granule launch failed");
     prof_end_launch(ASR_PROF_LSTM_BWD_SEQ, slot, s);
     *fused_bias = dbpart != nullptr;
+    g_lstm_last_path[1] = 1;
     return ASR_OK;
   }
   if (!bf && w_dtype == ASR_DT_F32 && dg_f32 &&
@@ -688,6 +708,7 @@ static int lstm_backward_impl(const float* dy, const void* whh_f, const void* wh
     ASR_REQUIRE(rc == 1, ASR_ERR_HIP, "lstm_backward: f32 tagged-granule launch failed");
     prof_end_launch(ASR_PROF_LSTM_BWD_SEQ, slot, s);
     *fused_bias = dbpart != nullptr;
+    g_lstm_last_path[1] = 2;
     if (dgbf) {
       const long long n = (long long)B * T * 8 * H;
       hipLaunchKernelGGL(to_bf16, dim3((unsigned)min(4096LL, (n + 255) / 256)), dim3(256), 0, s,
@@ -728,8 +749,10 @@ static int lstm_backward_impl(const float* dy, const void* whh_f, const void* wh
                                        (uint16_t*)dg, ctr, dgbf, s, false);
     ASR_REQUIRE(rc == 1, ASR_ERR_HIP, "lstm_backward: persistent launch failed");
     prof_end_launch(ASR_PROF_LSTM_BWD_SEQ, slot, s);
+    g_lstm_last_path[1] = 4;
     return ASR_OK;
   }
+  g_lstm_last_path[1] = 0;
   const int vec = (H % 8 == 0) ? 1 : 0;
   dim3 grid(ceil_div(H, BU), 2, ceil_div(B, MB));
   const int nks = 4 * H / 32;
@@ -846,6 +869,7 @@ extern "C" int asr_lstm_backward_dgbf_h(const float* dy, const void* whh_f, cons
                                     nullptr, cst, workspace, dgbf, part, s, false, false, act_h);
   ASR_REQUIRE(rc == 1, ASR_ERR_HIP, "lstm_backward_dgbf_h: tagged-granule launch failed");
   prof_end_launch(ASR_PROF_LSTM_BWD_SEQ, slot, s);
+  g_lstm_last_path[1] = 1;
   hipLaunchKernelGGL(bias_from_partials, dim3(ceil_div(8 * H, 256)), dim3(256), 0, s, part, B,
                      8 * H, db_ih, db_hh);
   ASR_LAUNCH_CHECK();

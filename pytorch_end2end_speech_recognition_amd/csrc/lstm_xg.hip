@@ -46,6 +46,7 @@
 
 namespace asr {
 
+extern int g_lstm_last_path[2];   // lstm.hip: {forward, backward} implementation of the last pass
 __device__ int g_xg_status;  // bit 0: a bounded spin gave up (results invalid)
 __device__ int g_xg_mode;    // bit 0: a launch ran write-through (sc1); bit 1: XCD-local
 // Sequence number of the last backward launch whose work-groups were all
@@ -2152,6 +2153,29 @@ extern "C" int asr_diag_lds_spin(int nwg, int iters, int* bad, void* stream) {
   return hipGetLastError() == hipSuccess ? ASR_OK : ASR_ERR_HIP;
 }
 
+// Diagnostics only (tests/test_coresidency_gpu.py): nwg work-groups of 256
+// threads, each holding `lds_bytes` of dynamic LDS, that stay resident for
+// `usec` microseconds (s_memrealtime, 100 MHz) and exit -- a stand-in for a
+// long-lived kernel (an RCCL collective spinning on its peer) occupying CUs
+// when a persistent recurrence is launched.  Bounded by its own clock.
+namespace asr {
+__global__ void diag_hold(unsigned long long ticks) {
+  extern __shared__ unsigned hl[];
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) hl[0] = 0u;
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(32);
+}
+}  // namespace asr
+
+extern "C" int asr_diag_hold_cus(int nwg, int lds_bytes, int usec, void* stream) {
+  ASR_REQUIRE(nwg > 0 && nwg <= 4096 && lds_bytes >= 4 && lds_bytes <= 160 * 1024 && usec >= 0 &&
+                  usec <= 10000000, ASR_ERR_ARG, "diag_hold_cus: nwg %d lds %d usec %d", nwg,
+              lds_bytes, usec);
+  hipLaunchKernelGGL(asr::diag_hold, dim3(nwg), dim3(256), (size_t)lds_bytes, (hipStream_t)stream,
+                     (unsigned long long)usec * 100ull);
+  return hipGetLastError() == hipSuccess ? ASR_OK : ASR_ERR_HIP;
+}
+
 extern "C" int asr_lstm_wgrad_gate(void* stream) {
   const unsigned want = asr::xg_bwd_seq(false) + 1;
   hipLaunchKernelGGL(asr::xg_wgrad_gate, dim3(1), dim3(64), 0, (hipStream_t)stream,
@@ -2185,6 +2209,7 @@ extern "C" int asr_lstm_forward_x(const uint16_t* x, int Din, const uint16_t* wi
                                           act, y, cst, workspace, ybf, s, false, nullptr);
   ASR_REQUIRE(rc == 1, ASR_ERR_HIP, "lstm_forward_x: launch failed");
   asr::prof_end_launch(ASR_PROF_LSTM_FWD_SEQ, slot, s);
+  asr::g_lstm_last_path[0] = 3;
   return ASR_OK;
 }
 
@@ -2212,6 +2237,7 @@ extern "C" int asr_lstm_forward_xh(const uint16_t* x, int Din, const uint16_t* w
                                           nullptr, y, cst, workspace, ybf, s, false, act_h);
   ASR_REQUIRE(rc == 1, ASR_ERR_HIP, "lstm_forward_xh: launch failed");
   asr::prof_end_launch(ASR_PROF_LSTM_FWD_SEQ, slot, s);
+  asr::g_lstm_last_path[0] = 3;
   return ASR_OK;
 }
 
@@ -2247,6 +2273,7 @@ extern "C" int asr_lstm_forward_xh_drop(const uint16_t* x, int Din, const uint16
                                           drop_p, drop_seed);
   ASR_REQUIRE(rc == 1, ASR_ERR_HIP, "lstm_forward_xh_drop: launch failed");
   asr::prof_end_launch(ASR_PROF_LSTM_FWD_SEQ, slot, s);
+  asr::g_lstm_last_path[0] = 3;
   return ASR_OK;
 }
 

@@ -491,6 +491,9 @@ class LinearCTC32Fn(torch.autograd.Function):
     def forward(ctx, x, weight, bias, drop, labels_flat, label_lens, act_lens, max_label_len,
                 loss_scale, blank, zero_infinity):
         N.require_device(x, weight, labels_flat, label_lens, act_lens)
+        # the producing BLSTM layer is found from the ORIGINAL input: the
+        # contiguous copy and the materialised dropout below carry no grad_fn
+        ctx.from_blstm = _produced_by_blstm(x)
         x = x.contiguous()
         B, T, K = x.shape
         V = weight.shape[0]
@@ -516,7 +519,6 @@ class LinearCTC32Fn(torch.autograd.Function):
         ctx.save_for_backward(x, logits, labels_flat, label_lens, act_lens, ws)
         ctx.meta = (bias, weight, B, T, V, Vp, int(max_label_len), int(blank), float(loss_scale),
                     nbytes)
-        ctx.from_blstm = _produced_by_blstm(x)
         ctx.drop = drop
         ctx.mark_non_differentiable(costs)
         return loss, costs

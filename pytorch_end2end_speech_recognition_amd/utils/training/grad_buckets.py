@@ -11,14 +11,23 @@ recurrences that follow it.  The stream semantics are RCCL's own:
 ProcessGroupNCCL makes its stream wait for the current (compute) stream at
 issue time, and ``wait()`` makes the compute stream wait for the collective.
 
-Rounds 3-4 also made the compute stream wait for every issued collective
-before each backward recurrence ('pre_recurrence'), because co-resident
-kernels changed the recurrence's results.  Round 5 found the cause -- a gfx950
-packed-FP32 operand-selection hazard the library no longer contains
-(tools/isa_check.py) -- and collectives now run beside the
-recurrences (tests/test_coresidency_gpu.py runs memory traffic beside the
-5x512 recurrence bitwise against none).  ASR_DP_SERIALIZE=1 restores the
-wait.
+Before each backward recurrence ('pre_recurrence') the compute stream waits
+for every collective issued so far (the default; ASR_DP_SERIALIZE=0 lets them
+run beside the recurrences).  Rounds 3-4 introduced the wait because
+co-resident kernels changed the recurrence's results; round 5 found that
+cause -- a gfx950 packed-FP32 operand-selection hazard the library no longer
+contains (tools/isa_check.py).  The wait stays the default for
+the second reason: the persistent recurrence needs every one of
+its work-groups resident at once, and an RCCL kernel spinning on its peer can
+hold CUs while the next recurrence registers.  What a timeout does then: the
+registered work-groups give up their bounded wait, the recurrence's status
+word is set and the step is skipped on EVERY rank (the status word is folded
+into the MAX-reduced device guard the fused optimizer reads; train_step counts
+it in STEP_STATS['recurrence_give_ups'] / ['skipped'] and logs it) -- never a
+silently wrong update.  tests/test_coresidency_gpu.py holds CUs beside a
+5x512 backward recurrence for shorter and longer than that wait and checks
+both outcomes.  Without RCCL on more than one GPU here, the overlapped form is
+measured only with memory traffic and held CUs in its place.
 
 Every rank issues the same buckets in the same canonical order (top layer
 first, then the remainder of the buffer), whatever happens during its backward:
@@ -94,11 +103,11 @@ class GradBuckets(object):
 
     def _on_event(self, event, arg=None):
         if event == 'pre_recurrence':
-            # opt-in (ASR_DP_SERIALIZE=1): the compute stream waits for every
-            # collective issued so far, so none is co-resident with the
-            # persistent recurrence about to be enqueued (rounds 3-4; the
-            # co-residency fault's cause is gone)
-            if os.environ.get('ASR_DP_SERIALIZE', '0') != '1':
+            # default (ASR_DP_SERIALIZE=0 turns it off): the compute stream
+            # waits for every collective issued so far, so none holds CUs when
+            # the persistent recurrence about to be enqueued registers its
+            # work-groups (module docstring)
+            if os.environ.get('ASR_DP_SERIALIZE', '1') == '0':
                 return
             for w in self.works[self.waited:]:
                 w.wait()

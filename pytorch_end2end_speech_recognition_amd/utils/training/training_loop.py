@@ -25,6 +25,19 @@ from .grad_buckets import GradBuckets
 logger = logging.getLogger('training')
 INF = float('inf')
 
+# Per-process counters of the training steps this module ran (VERDICT r05 #7:
+# a skipped step is never silent): 'skipped' counts every step whose update
+# was dropped -- a RuntimeError on some rank, or a persistent recurrence that
+# gave up a bounded wait (its status word folded into the device guard) --
+# and 'recurrence_give_ups' the subset whose guard carried a recurrence status
+# word rather than an exception on this rank.  bench.py reports both.
+STEP_STATS = {'steps': 0, 'skipped': 0, 'recurrence_give_ups': 0}
+
+
+def reset_step_stats():
+    for k in STEP_STATS:
+        STEP_STATS[k] = 0
+
 
 def _world():
     return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
@@ -116,6 +129,8 @@ def _finish(model, host, n_losses, n_guard, has_losses, zero=True):
     training_loop.py:69-83)."""
     vals = host[:n_losses] if has_losses else [0.] * n_losses
     if n_guard and max(host[-n_guard:]) > 0:
+        if has_losses:    # no exception on this rank: the guard is a status word
+            STEP_STATS['recurrence_give_ups'] += 1
         # the fused step left the weights untouched; undo its step count
         if hasattr(model.optimizer, 'undo_step_count'):
             model.optimizer.undo_step_count()
@@ -139,6 +154,7 @@ def _step(model, forward, clip_grad_norm, n_losses, grad_scale, sync=True):
     host sync before the optimizer; the host reads the guard with the loss."""
     ok = 1
     world = _world()
+    STEP_STATS['steps'] += 1
     if model.device.type == 'cuda':
         from ... import native_ops
         # weight gradients a failed backward outside train_step left pending
@@ -182,6 +198,7 @@ def _step(model, forward, clip_grad_norm, n_losses, grad_scale, sync=True):
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         ok = int(flag.item())
     if not ok and (guard is None or world == 1):
+        STEP_STATS['skipped'] += 1
         model.zero_grad()
         return [0.] * n_losses
     prev = getattr(model, '_pending_losses', None)
@@ -191,6 +208,8 @@ def _step(model, forward, clip_grad_norm, n_losses, grad_scale, sync=True):
         model.optimizer.clip_and_step(clip_grad_norm if clip_grad_norm > 0 else 0.0, guard=guard)
     else:
         if guard is not None and int(guard.max().item()):
+            if ok:
+                STEP_STATS['recurrence_give_ups'] += 1
             return _skipped(model, n_losses, 'persistent recurrence gave up')
         if clip_grad_norm > 0:
             torch.nn.utils.clip_grad_norm_(model.parameters(), clip_grad_norm)
@@ -228,6 +247,7 @@ class _Resolved(object):
 
 
 def _skipped(model, n_losses, why, zero=True):
+    STEP_STATS['skipped'] += 1
     logger.warning('!!!Skip mini-batch!!! %s' % why)
     if zero:
         model.zero_grad()

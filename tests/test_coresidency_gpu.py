@@ -22,6 +22,7 @@ and compare every gradient BITWISE with the same backward run alone:
     data-parallel all-reduce puts beside the recurrence now that the compute
     stream no longer waits for collectives before it) against none.
 """
+import ctypes
 import os
 
 import numpy as np
@@ -147,5 +148,76 @@ def test_side_stream_memory_traffic_beside_recurrence_bitwise(cuda_dev):
         ref = _grads(sd, batch, 512, 5, {'ASR_OVERLAP_WGRAD': 'auto'})
         got = _grads(sd, batch, 512, 5, {'ASR_OVERLAP_WGRAD': 'auto'}, side=traffic)
         _equal(ref, got, 'side traffic')
+    finally:
+        native_ops.set_compute_dtype('fp32')
+
+
+def _held_step(sd, batch, hold_us, nwg=200):
+    """One train_step of the 5x512 CTC model (bf16, the default overlap mode);
+    with hold_us > 0, right before the FIRST backward recurrence is enqueued a
+    side stream launches nwg work-groups that hold 96 KB of LDS each (one per
+    CU) for hold_us microseconds -- a long-lived kernel (an RCCL collective
+    spinning on its peer) occupying CUs while the recurrence registers its
+    work-groups.  Returns (loss value, weights before and after the step,
+    step stats)."""
+    from pytorch_end2end_speech_recognition_amd import _native as N
+    from pytorch_end2end_speech_recognition_amd import native_ops
+    from pytorch_end2end_speech_recognition_amd.utils.training import training_loop as TL
+    dev = torch.device('cuda', 0)
+    m = _build(_kw(512, 5))
+    m.load_state_dict(sd)
+    m.set_cuda()
+    m.set_optimizer('adam', 1e-3, weight_decay=1e-6)
+    side = torch.cuda.Stream(device=dev)
+    fired = []
+    before = m._flat_param.clone()
+
+    def hook(ev, arg=None):
+        if ev == 'pre_recurrence' and hold_us > 0 and not fired:
+            fired.append(1)
+            # not joined into the compute stream: it runs beside what follows
+            N.call('asr_diag_hold_cus', nwg, 96 * 1024, int(hold_us),
+                   ctypes.c_void_p(side.cuda_stream))
+    TL.reset_step_stats()
+    native_ops.recurrence_status(dev)
+    native_ops.set_grad_ready_hook(hook)
+    try:
+        m, lv = TL.train_step(m, batch, clip_grad_norm=5.0)
+    finally:
+        native_ops.set_grad_ready_hook(None)
+    torch.cuda.synchronize()
+    side.synchronize()
+    assert fired or hold_us == 0
+    return float(lv), before, m._flat_param.clone(), dict(TL.STEP_STATS)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('hold_ms', [20, 4000])
+def test_held_cus_beside_recurrence_bitwise_or_visible_skip(hold_ms, cuda_dev):
+    """VERDICT r05 #7 / ADVICE r05: 200 CUs held by a resident kernel when the
+    backward recurrence (5 x 512, B 32, T 240) registers -- 20 ms (within the
+    recurrence's bounded wait: it waits, then runs) and 4 s (beyond it: its
+    registered work-groups give up).  The training step either updates the
+    weights BITWISE as the step without the held CUs, or is skipped in a way
+    the caller sees: loss 0, weights untouched, counted in
+    STEP_STATS['recurrence_give_ups'] and ['skipped'].  Never a silent
+    wrong update."""
+    from pytorch_end2end_speech_recognition_amd import native_ops
+    sd, batch = _setup(512, 5, 240)
+    try:
+        lv0, _, w0, st0 = _held_step(sd, batch, 0)
+        assert st0['skipped'] == 0 and lv0 > 0
+        lv1, before, w1, st1 = _held_step(sd, batch, hold_ms * 1000)
+        if st1['skipped']:
+            print('\nheld %d ms: the recurrence gave up; step skipped visibly %s' % (hold_ms, st1))
+            assert st1['recurrence_give_ups'] == 1 and lv1 == 0.0, st1
+            assert torch.equal(w1, before)
+        else:
+            print('\nheld %d ms: the recurrence waited; update bitwise equal' % hold_ms)
+            assert lv1 == lv0
+            assert torch.equal(w1, w0)
+        if hold_ms <= 20:
+            assert not st1['skipped'], st1
+        assert int(native_ops.recurrence_status(cuda_dev).max()) == 0
     finally:
         native_ops.set_compute_dtype('fp32')

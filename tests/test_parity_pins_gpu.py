@@ -112,13 +112,29 @@ def test_vgg_prod_channels_fp32_vs_oracle(cuda_dev):
         assert err <= 2e-3, (k, err)
 
 
-def _with_env(monkeypatch, name, value, model, batch, prec):
+def _gpu_grads_dec(model, batch, prec):
+    """_gpu_grads plus the forward's ReLU / max-pool decisions per VGG layer."""
+    from pytorch_end2end_speech_recognition_amd import native_ops
+    native_ops.set_compute_dtype(prec)
+    try:
+        model.zero_grad()
+        loss = model(*batch)
+        dec = _gpu_vgg_decisions(_vgg_node(loss))
+        loss.backward()
+        torch.cuda.synchronize()
+    finally:
+        native_ops.set_compute_dtype('fp32')
+    return float(loss.item()), {k: p.grad.detach().cpu().numpy().copy()
+                                for k, p in model.named_parameters()}, dec
+
+
+def _with_env(monkeypatch, name, value, model, batch, prec, fn=None):
     # the running statistics are restored afterwards, so A/B calls start from the
     # same state (the folded BN variance pass is centred on the running mean)
     run = {k: v.clone() for k, v in model.state_dict().items() if 'running' in k}
     monkeypatch.setenv(name, value)
     try:
-        return _gpu_grads(model, batch, prec)
+        return (fn or _gpu_grads)(model, batch, prec)
     finally:
         monkeypatch.delenv(name)
         with torch.no_grad():
@@ -213,11 +229,12 @@ def test_vgg_fused_bn_variance_matches_two_pass(prec, cuda_dev, monkeypatch):
     out = {}
     for flag in ('1', '0'):
         model.load_state_dict(sd0)
-        loss, g = _with_env(monkeypatch, 'ASR_VGG_FUSED_VAR', flag, model, batch, prec)
+        loss, g, dec = _with_env(monkeypatch, 'ASR_VGG_FUSED_VAR', flag, model, batch, prec,
+                                 fn=_gpu_grads_dec)
         run = {k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items()
                if 'running' in k}
-        out[flag] = (loss, g, run)
-    (l1, g1, r1), (l0, g0, r0) = out['1'], out['0']
+        out[flag] = (loss, g, run, dec)
+    (l1, g1, r1, d1), (l0, g0, r0, d0) = out['1'], out['0']
     # (bf16: last-bit changes of the statistics move bf16 roundings of the
     # activations; measured 1.8e-5 on the loss with the row-blocked passes)
     np.testing.assert_allclose(l1, l0, rtol=1e-5 if prec == 'fp32' else 5e-5)
@@ -226,16 +243,32 @@ def test_vgg_fused_bn_variance_matches_two_pass(prec, cuda_dev, monkeypatch):
         # the activations, and the BN backward's cancellation amplifies that in
         # the first layer's weight gradient: there the statistics themselves
         # are compared, and the gradients against float64 below).  fp32: a
-        # last-bit change of z can also flip a ReLU / max-pool decision of a
+        # last-bit change of z can flip a ReLU / max-pool decision of a
         # near-zero or near-tied pre-activation, which moves that pixel's whole
-        # gradient.  With the f32 MFMA convolutions' summation order this seed
-        # moves the gradients of conv3 and every layer under it by 2.4e-3
-        # (relative L2; 1e-5 with the generic kernel) while every GEMM of the
-        # step equals the generic kernel's to 1e-7 (tools/diag_gemm_f32.py) and
-        # the layers above conv3 agree to 6e-6 -- the signature of one such
-        # flip.  Bound: 5e-3; the loss and the running statistics stay at 1e-5.
+        # gradient in its layer and every layer under it (round 5 measured
+        # 2.4e-3 relative L2 at conv3 and below for this seed, 6e-6 above).
+        # The flips are counted here from both runs' recorded decisions: every
+        # parameter ABOVE the highest flipped layer keeps the 1e-4 bound; only
+        # the layers at or below a counted flip get 5e-3.
+        flipped = []
+        for l, ((m1, i1), (m0, i0)) in enumerate(zip(d1, d0)):
+            n = int((m1 != m0).sum()) + (int((i1 != i0).sum()) if i0 is not None else 0)
+            if n:
+                flipped.append(l)
+        top = max(flipped) if flipped else -1
+        convs = [i for i, mod in enumerate(model.encoder.conv.layers)
+                 if isinstance(mod, torch.nn.Conv2d)]
+
+        def vgg_layer(k):   # VGG layer of encoder.conv.layers.<i>.*, else None
+            if not k.startswith('encoder.conv.layers.'):
+                return None
+            i = int(k.split('.')[3])
+            return max(l for l, c in enumerate(convs) if c <= i)
+        print('\nfp32 fused BN variance: decisions flipped in VGG layers %s' % flipped)
         for k in g0:
-            assert _rel_l2(g1[k], g0[k]) <= 5e-3, (k, _rel_l2(g1[k], g0[k]))
+            l = vgg_layer(k)
+            bound = 5e-3 if (l is not None and l <= top) else 1e-4
+            assert _rel_l2(g1[k], g0[k]) <= bound, (k, _rel_l2(g1[k], g0[k]), bound, flipped)
     for k in r0:
         np.testing.assert_allclose(r1[k], r0[k], rtol=1e-5, atol=1e-6, err_msg=k)
 

@@ -3,8 +3,11 @@ T = 1000, ragged lengths U[800, 1000], Din = 1024 as in layers 1-4 of
 ctc5x512) against the float64 oracle, for every output and gradient: y, dx,
 dW_ih, dW_hh, db.  In bf16 mode this is the persistent tagged-granule
 recurrence (lstm_xg.hip: lstm_fwd_xg / lstm_bwd_xg, one launch per pass, the
-one-bit step tag in the LSB of one bf16 in four) plus the bf16 GEMMs; in fp32
-mode the exact-f32 per-step kernels.
+one-bit step tag in the LSB of one bf16 in four) plus the bf16 GEMMs.  In fp32
+mode the forward is the f32 tagged-granule recurrence (lstm_fwd_xg<..., F32>,
+f32 granules, H <= 512) and the backward the exact-f32 per-step kernels (the
+f32 persistent backward takes H <= 384); asr_lstm_last_path records which ran,
+and the test asserts it.
 
 Why two weight regimes.  With the reference's initialisation (uniform +-0.1,
 H = 512) the recurrence is chaotic: a 1e-7 perturbation grows ~x65 per 100
@@ -105,6 +108,14 @@ def _gpu(prec, lens, x, w_ih, w_hh, b_ih, b_hh, dy, dev):
         ops.set_compute_dtype('fp32')
 
 
+def _last_path():
+    import ctypes
+    from pytorch_end2end_speech_recognition_amd import _native as N
+    out = (ctypes.c_int * 2)()
+    N.call('asr_lstm_last_path', ctypes.cast(out, ctypes.c_void_p))
+    return list(out)
+
+
 def _rel(a, ref):
     return float((a - ref).abs().max() / ref.abs().max())
 
@@ -121,8 +132,15 @@ def test_full_shape_layer_vs_float64_oracle(prec, bound, xu, cuda_dev, monkeypat
     ref = _oracle(*case)
     _xg_mode()                                   # clear
     got = _gpu(prec, *case, cuda_dev)
+    path = _last_path()
     if prec == 'bf16':
         assert _xg_mode() != 0, 'the persistent tagged-granule recurrence did not run'
+        # tagged-granule bf16 both passes (the forward with or without the fused
+        # input projection)
+        assert path[0] in (1, 3) and path[1] == 1, path
+    else:
+        # f32 tagged-granule forward; per-step exact-f32 backward (H = 512 > 384)
+        assert path == [2, 0], path
     names = ['y', 'dx', 'dW_ih', 'dW_hh', 'db_ih', 'db_hh']
     refs = list(ref[:4]) + [ref[4], ref[4]]
     errs = {n: _rel(g, r) for n, g, r in zip(names, got, refs)}

@@ -13,7 +13,8 @@ form such instructions (csrc/Makefile), and this script proves it on the built
 code objects: every packed-FP32 instruction is counted and any high-dword
 selection on src1 / src2 is an error.
 
-usage: python tools/isa_check.py [lib.so]   (exit 1 on a finding)
+usage: python tools/isa_check.py [lib.so]   (exit 1 on a finding, or when no code
+object / no packed-FP32 instruction was found: the check would be vacuous)
 """
 import os
 import re
@@ -56,10 +57,13 @@ def crossing(operands):
     return any(sel[i] == 1 for i in (1, 2) if i < len(sel))
 
 
-def scan(path=LIB):
+def scan(path=LIB, counts=None):
     findings, total = [], 0
+    cos = code_objects(path)
+    if counts is not None:
+        counts['code_objects'] = len(cos)
     with tempfile.TemporaryDirectory() as d:
-        for k, co in enumerate(code_objects(path)):
+        for k, co in enumerate(cos):
             f = os.path.join(d, 'co%d.o' % k)
             open(f, 'wb').write(co)
             txt = subprocess.run([OBJDUMP, '-d', '--no-show-raw-insn', f], capture_output=True,
@@ -79,11 +83,19 @@ def scan(path=LIB):
 
 def main():
     path = sys.argv[1] if len(sys.argv) > 1 else LIB
-    findings, total = scan(path)
-    print('%s: %d packed-FP32 instructions, %d selecting a src1 / src2 high dword'
-          % (os.path.basename(path), total, len(findings)))
+    counts = {}
+    findings, total = scan(path, counts)
+    print('%s: %d gfx950 code objects, %d packed-FP32 instructions, %d selecting a src1 / '
+          'src2 high dword' % (os.path.basename(path), counts['code_objects'], total,
+                               len(findings)))
     for kern, line in findings[:40]:
         print('  %s: %s' % (kern[:90], line))
+    if not counts['code_objects'] or not total:
+        # nothing scanned (a changed bundle format or triple, or a build without
+        # the recurrence's packed math): the gate would be vacuous -- fail it
+        print('isa_check: no gfx950 code object or no packed-FP32 instruction found; '
+              'the hazard check did not run (ADVICE r05)')
+        return 1
     return 1 if findings else 0
 
 
