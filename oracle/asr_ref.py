@@ -399,7 +399,9 @@ def attention_xe(p, cfg, enc_out, enc_lens, ys, y_lens, perm, task=0, train=None
     'd' / 'c' [B,S,Dz] scales on the W_d / W_c LinearND outputs (linear.py:45),
     'emb' [B,S,Y] scales on the teacher embeddings, and scheduled sampling
     (attention_seq2seq.py:744-748): 'ss' [S] flags, 'emb_ss' [B,S,Y] scales on
-    the sampled embedding embed(argmax logits_{t-1}) (detached)."""
+    the sampled embedding embed(argmax logits_{t-1}) (detached).  Test hooks:
+    'tok' [B,S] replays given sampled tokens instead of this oracle's argmax,
+    '_log' (a list) receives (t, argmax, top-2 gap) of every sampled step."""
     train = train or {}
     B, T, E = enc_out.shape
     ncls = cfg['num_classes'] if task == 0 else cfg['num_classes_sub']
@@ -435,7 +437,8 @@ def attention_xe(p, cfg, enc_out, enc_lens, ys, y_lens, perm, task=0, train=None
     else:                                                    # Embedding, padding_idx=-1
         emb_w = p['embed_%d.embed.weight' % task]
     ys_emb = emb_w[torch.as_tensor(ys_in)]                   # [B, L+1, emb]
-    mk = {k: torch.from_numpy(np.asarray(v, np.float32)) for k, v in train.items() if k != 'ss'}
+    mk = {k: torch.from_numpy(np.asarray(v, np.float32)) for k, v in train.items()
+          if k not in ('ss', 'tok', '_log')}
     if 'emb' in mk:
         ys_emb = ys_emb * mk['emb']
     ss = train.get('ss')
@@ -444,6 +447,11 @@ def attention_xe(p, cfg, enc_out, enc_lens, ys, y_lens, perm, task=0, train=None
         if t > 0:
             if ss is not None and ss[t]:                     # scheduled sampling :744-748
                 tok = torch.argmax(logits[-1], dim=-1)
+                if '_log' in train:   # test hook: this oracle's argmax and its top-2 gap
+                    top2 = torch.topk(logits[-1].detach(), 2, dim=-1).values
+                    train['_log'].append((t, tok.clone(), (top2[:, 0] - top2[:, 1]).clone()))
+                if 'tok' in train:    # test hook: replay given tokens [B, S]
+                    tok = torch.as_tensor(np.asarray(train['tok'])[:, t], dtype=torch.long)
                 y = emb_w[tok].detach()
                 if 'emb_ss' in mk:
                     y = y * mk['emb_ss'][:, t]

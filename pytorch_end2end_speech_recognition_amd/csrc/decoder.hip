@@ -141,6 +141,23 @@ __global__ void build_wcat(Dims d, const float* __restrict__ w_ih_ctx, long long
   }
 }
 
+// Zcat[z][0:E] = W_c[z][:], Zcat[z][E:] = W_d[z][:] (z < Dz): the bottleneck rows
+// of a sampled step's z = W_c ctx + W_d h, in Wcat's column layout
+template <typename TO>
+__global__ void build_zcat(Dims d, int Dz, const float* __restrict__ w_c,
+                           const float* __restrict__ w_d, TO* __restrict__ out) {
+  const int ED = d.E + d.D;
+  const long long n = (long long)Dz * ED;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long z = i / ED;
+    const int k = (int)(i % ED);
+    const float v = k < d.E ? w_c[z * d.E + k] : w_d[z * d.D + (k - d.E)];
+    if constexpr (sizeof(TO) == 2) out[i] = f2bf(v);
+    else out[i] = v;
+  }
+}
+
 // Wcat^T[n][g] (n < E + D): the backward's per-step r = dgates @ Wcat reads rows
 template <typename TO>
 __global__ void build_wcat_t(Dims d, const float* __restrict__ w_ih_ctx, long long ld_ih,
@@ -1075,7 +1092,8 @@ size_t al256(size_t n) { return (n + 255) & ~size_t(255); }
 // Workspace: [Wcat (fwd) or Wcat^T (bwd)][energies / d aw [B][T]] and, backward
 // only, [r][carry][ddec_att][dc][flags][dF [B][T][C]][dWd chunk partials].
 struct AttWs {
-  size_t wcat, ebuf, r, carry, ddec, dc, flags, dF, dwdc, wd, pbuf, ctr, sbuf, total;
+  size_t wcat, ebuf, r, carry, ddec, dc, flags, dF, dwdc, wd, pbuf, ctr, sbuf, lbuf, ssd, zcat,
+      total;
 };
 AttWs att_ws(const Dims& d, int cdt, bool bwd) {
   AttWs w;
@@ -1095,7 +1113,15 @@ AttWs att_ws(const Dims& d, int cdt, bool bwd) {
     w.ctr = o; o += al256((size_t)(1 + 8) * 64 * 4);
   } else {   // the persistent forward's W_dec h partials and group counters
     w.pbuf = o; o += al256((size_t)8 * 32 * 4 * d.A * 4);
-    w.ctr = o; o += al256((size_t)(1 + 8) * 64 * 4);
+    // (1 + 8) counters of the three per-step hand-offs + 8 of the sampled-step
+    // logits hand-off, then the partial logits of the sampled steps
+    // [8 groups][32 members][4 slots][PD_VMAX = 128] and the step flags [S]
+    w.ctr = o; o += al256((size_t)(1 + 2 * 8) * 64 * 4);
+    w.lbuf = o; o += al256((size_t)8 * 32 * 4 * 128 * 4);
+    w.flags = o; o += al256((size_t)d.S * 4);
+    w.ssd = o; o += 512;   // the sampled steps' operand record (PdSs)
+    // [W_c | W_d] rows of the sampled steps (Dz <= 512), f32 or bf16
+    w.zcat = o; o += al256((size_t)512 * (d.E + d.D) * (cdt == ASR_DT_BF16 ? 2 : 4));
   }
   w.total = o;
   return w;
@@ -1142,6 +1168,50 @@ constexpr int PD_FPW = 8;        // frames per wave: FCH <= 64
 constexpr int PD_CTR = 64;       // ints per counter (own 256-B line)
 constexpr int PD_CM = 4;         // conv channels of the generic instantiations (C <= 4)
 constexpr unsigned PD_SPIN_LIMIT = 1u << 20;
+constexpr int PD_VMAX = 128;     // sampled steps in the pass: classes <= PD_THREADS / PD_SLOTS
+constexpr int PD_YMAX = 64;      // ... embedding dim
+constexpr int PD_ZMAX = 16;      // ... bottleneck units per member (Dz <= 512: one MFMA tile)
+
+// Scheduled sampling inside the persistent forward (attention_seq2seq.py:742-748,
+// asr_attdec_opts_t): flags == nullptr when no step of the pass samples.
+struct PdSs {
+  const int32_t* flags;          // [S] (device), t >= 1
+  const float *w_d, *b_d, *w_c, *b_c, *w_fc, *b_fc, *emb_w, *w_ih_emb, *b_ih, *b_hh;
+  float drop_d, drop_c, drop_emb;
+  unsigned long long seed_d, seed_c, seed_emb;
+  int Y, Dz, V, emb_trans;
+  long long ld_ih;
+  float *pre_ss, *emb_ss;
+  long long* tok_ss;
+  float* lbuf;                   // [PD_GROUPS][PD_MEMBERS][PD_SLOTS][PD_VMAX] partial logits
+  const void* zcat;              // [Dz][E + D] = [W_c | W_d] in the pass's Wcat dtype
+};
+static_assert(sizeof(PdSs) <= 512, "AttWs::ssd holds one PdSs");
+
+// Host staging of the PdSs records: a ring of pinned slots, each reused only
+// after the copy that read it has completed (its event).
+int pd_ss_upload(const PdSs& v, void* dst, hipStream_t s) {
+  constexpr int NSLOT = 64;
+  static PdSs* ring = nullptr;
+  static hipEvent_t ev[NSLOT];
+  static int next = 0;
+  if (!ring) {
+    if (hipHostMalloc((void**)&ring, NSLOT * sizeof(PdSs), hipHostMallocDefault) != hipSuccess) {
+      ring = nullptr;
+      return ASR_ERR_HIP;
+    }
+    for (int i = 0; i < NSLOT; ++i)
+      if (hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess) return ASR_ERR_HIP;
+  }
+  const int k = next;
+  next = (next + 1) % NSLOT;
+  if (hipEventSynchronize(ev[k]) != hipSuccess) return ASR_ERR_HIP;   // never recorded: returns
+  ring[k] = v;
+  if (hipMemcpyAsync(dst, &ring[k], sizeof(PdSs), hipMemcpyHostToDevice, s) != hipSuccess)
+    return ASR_ERR_HIP;
+  if (hipEventRecord(ev[k], s) != hipSuccess) return ASR_ERR_HIP;
+  return ASR_OK;
+}
 
 typedef __attribute__((address_space(1))) int pd_gint;
 typedef __attribute__((ext_vector_type(4))) unsigned int pd_u32x4;
@@ -1177,6 +1247,27 @@ __host__ __device__ inline PdGeom pd_geom(const Dims& d) {
   g.cpart = o; o += PD_THREADS;
   g.mp = o; o += 2048;
   g.encs = o; o += d.T * g.ECW;
+  g.total = (o + 3) & ~3;
+  return g;
+}
+
+// LDS regions of the sampled steps (floats), after the base geometry (base =
+// pd_geom(d).total): only a pass with sampled steps allocates them.
+struct PdSsGeom {
+  int zp, zz, lg, tk, ev, wie, bs, wfc, ssf, total;
+};
+__host__ __device__ inline PdSsGeom pd_ss_geom(const Dims& d, int base, int UPW, int Y, int ZPW) {
+  PdSsGeom g;
+  int o = base;
+  g.ssf = o; o += (d.S + 3) & ~3;           // the step flags (int bits); first: at base
+  g.zp = o; o += 2 * 2 * PD_SLOTS * 16;     // z MFMA partials [wave 6/7][ctx/h][slot][unit]
+  g.zz = o; o += PD_SLOTS * 16;             // z = tanh(...) of this member's units
+  g.lg = o; o += PD_SLOTS * PD_VMAX;        // the group's logits of the previous step
+  g.tk = o; o += 8;                         // sampled token per slot (int bits)
+  g.ev = o; o += PD_SLOTS * Y;              // the sampled embeddings (dropout applied)
+  g.wie = o; o += 4 * UPW * Y;              // W_ih[:, :Y] rows of this member's gate rows
+  g.bs = o; o += 4 * UPW;                   // their b_ih + b_hh
+  g.wfc = o; o += ZPW * PD_VMAX;            // fc columns of this member's bottleneck units
   g.total = (o + 3) & ~3;
   return g;
 }
@@ -1288,7 +1379,7 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
     const float* __restrict__ vw, float* __restrict__ dec, float* __restrict__ c_all,
     float* __restrict__ gates, float* x, float* __restrict__ ctx_all,
     float* __restrict__ aw_all, float* pbuf, float* ebuf, int* ctr, int* status, float drop_h,
-    unsigned long long seed_h) {
+    unsigned long long seed_h, const PdSs* __restrict__ ssp) {
   extern __shared__ __attribute__((aligned(16))) float L[];
   Dims d = dd;
   if (CC) d.C = CC;
@@ -1297,6 +1388,9 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
   if (SD) d.D = SD;
   if (SK) d.K = SK;
   __shared__ int s_ok;
+  // sampled steps (ssp: the operands, in device memory -- read where used, so
+  // they never hold scalar registers across the pass)
+  const bool ss_on = ssp != nullptr;     // kernel-uniform
   const PdGeom G = pd_geom(d);
   const int UPW = G.UPW, FCH = G.FCH, ECW = G.ECW, ED = G.ED, NKB = G.NKB, half = G.half;
   const int grp = blockIdx.x % PD_GROUPS, m = blockIdx.x / PD_GROUPS;
@@ -1305,6 +1399,7 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
   const int u0 = m * UPW, nu = max(0, min(UPW, d.D - u0));
   const int G4 = 4 * d.D;
   int* my_ctr = ctr + (1 + grp) * PD_CTR;
+  int* ss_ctr = ctr + (1 + PD_GROUPS + grp) * PD_CTR;   // sampled steps' logits hand-off
   const __amdgpu_buffer_rsrc_t rx = pd_rsrc(x, (unsigned)((size_t)d.B * d.S * ED * 4));
   const __amdgpu_buffer_rsrc_t rp =
       pd_rsrc(pbuf, (unsigned)((size_t)PD_GROUPS * PD_MEMBERS * PD_SLOTS * d.A * 4));
@@ -1323,23 +1418,34 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
   constexpr int KM32 = F32 ? 8 * PD_KMAX : 1;
   bf16x8 wf[F32 ? 1 : PD_KMAX];
   float wf32[KM32];
+  // sampled steps: member m's bottleneck units [zu0, zu0 + nz) of Dz
   {
     const int tile = wave >> 1, kh = wave & 1;
     const int gr = tile * 16 + (lane & 15), q = gr / UPW, u = gr % UPW;
     const bool ok = wave < 6 && q < 4 && u < nu;
+    // waves 6, 7 (idle in the cell product): row tile 3 = [W_c | W_d] rows of
+    // this member's bottleneck units, so a sampled step's z = W_c ctx + W_d h
+    // runs beside the gate product on the same x rows (ctx and h parts kept
+    // apart: their dropout masks differ)
+    const int zdz = ss_on ? ssp->Dz : 0, zpw = (zdz + PD_MEMBERS - 1) / PD_MEMBERS;
+    const int zr = m * zpw + (lane & 15);
+    const bool zok = ss_on && wave >= 6 && (lane & 15) < zpw && zr < zdz;
+    const void* wsrc = zok ? ssp->zcat : wcat_v;
+    const long long wrow = ok ? q * d.D + u0 + u : zok ? zr : 0;
+    const bool wl = ok || zok;
     if constexpr (F32) {
-      const float* wr = (const float*)wcat_v + (long long)(ok ? q * d.D + u0 + u : 0) * ED;
+      const float* wr = (const float*)wsrc + wrow * ED;
 #pragma unroll
       for (int i = 0; i < KM32; ++i) {
         const int k = 4 * (kh + 2 * i) + (lane >> 4);
-        wf32[i] = (ok && k < ED) ? wr[k] : 0.f;
+        wf32[i] = (wl && k < ED) ? wr[k] : 0.f;
       }
     } else {
-      const uint16_t* wr = (const uint16_t*)wcat_v + (long long)(ok ? q * d.D + u0 + u : 0) * ED;
+      const uint16_t* wr = (const uint16_t*)wsrc + wrow * ED;
 #pragma unroll
       for (int i = 0; i < PD_KMAX; ++i) {
         const int k = (kh + 2 * i) * 32 + 8 * (lane >> 4);
-        wf[i] = (ok && kh + 2 * i < NKB && k < ED) ? load_bf16x8(wr + k)
+        wf[i] = (wl && kh + 2 * i < NKB && k < ED) ? load_bf16x8(wr + k)
                                                     : as_bf16x8(u16x8{0, 0, 0, 0, 0, 0, 0, 0});
       }
     }
@@ -1380,11 +1486,39 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
   const int cb = grp + PD_GROUPS * csl, cj = u0 + cu;
   const bool cown = tid < PD_SLOTS * UPW && cu < nu && cb < d.B;
   float c_reg = 0.f;
+  // sampled steps: the step flags, this member's W_ih[:, :Y] gate rows, the
+  // cell threads' bias sums, the (slot, class) threads' fc columns of this
+  // member's bottleneck units
+  // (in LDS, not registers: the pass is at its VGPR budget)
+  if (ss_on) {
+    const PdSs& ss = *ssp;
+    const int Y = ss.Y, ZPW = (ss.Dz + PD_MEMBERS - 1) / PD_MEMBERS, zu0 = m * ZPW;
+    const int nz = max(0, min(ZPW, ss.Dz - zu0));
+    const PdSsGeom Z = pd_ss_geom(d, G.total, UPW, Y, ZPW);
+    int* fl = reinterpret_cast<int*>(&L[Z.ssf]);
+    for (int i = tid; i < d.S; i += PD_THREADS) fl[i] = ss.flags[i];
+    for (int i = tid; i < 4 * UPW * Y; i += PD_THREADS) {
+      const int q = i / (UPW * Y), u = (i / Y) % UPW, y = i % Y;
+      L[Z.wie + i] = u < nu ? ss.w_ih_emb[(long long)(q * d.D + u0 + u) * ss.ld_ih + y] : 0.f;
+    }
+    for (int i = tid; i < 4 * UPW; i += PD_THREADS) {
+      const int q = i / UPW, u = i % UPW, r = q * d.D + u0 + u;
+      L[Z.bs + i] = u < nu ? ss.b_ih[r] + ss.b_hh[r] : 0.f;
+    }
+    for (int i = tid; i < ZPW * PD_VMAX; i += PD_THREADS) {
+      const int z = i / PD_VMAX, v = i % PD_VMAX;
+      L[Z.wfc + i] = (z < nz && v < ss.V) ? ss.w_fc[(long long)v * ss.Dz + zu0 + z] : 0.f;
+    }
+  }
+  int nss = 0;   // sampled steps so far (the logits hand-off's counter target)
   __syncthreads();
 
   for (int t = 0; t < d.S; ++t) {
     // ================= C: cell step t (t = 0: the initial state h0) =================
     PD_TR(32);
+    // step t feeds embed(argmax logits_{t-1}) instead of the teacher token
+    // (work-group and group uniform: every member reads the same flags)
+    const int smp = (ss_on && t > 0) ? reinterpret_cast<const int*>(&L[G.total])[t] : 0;
     if (t > 0) {
       if (tid == 0) s_ok = pd_wait(my_ctr, PD_MEMBERS * 3 * t, ctr, status);
       __syncthreads();
@@ -1427,8 +1561,54 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
 #pragma unroll
             for (int r = 0; r < 4; ++r) L[G.part + (wave * PD_SLOTS + r) * 16 + lane] = acc0[r] + acc1[r];
           }
+        } else if (smp) {   // waves 6, 7: z partials of a sampled step (ctx / h apart)
+          const int kh = wave & 1, mm = lane & 15;
+          f32x4 ac = {0.f, 0.f, 0.f, 0.f}, ad = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int i = 0; i < KM32; ++i) {
+            if (4 * (kh + 2 * i) < ED) {   // wave-uniform
+              const int k = 4 * (kh + 2 * i) + (lane >> 4);
+              const float a = (mm < PD_SLOTS && k < ED) ? L[G.xs + mm * ED + k] : 0.f;
+              // k-step kh + 2 i is a ctx column iff i < E / 8 (E % 8 == 0: pd_ss_ok)
+              if (i < d.E / 8) ac = mfma_f32(a, wf32[i], ac);
+              else ad = mfma_f32(a, wf32[i], ad);
+            }
+          }
+          if (lane < 16) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int zp = G.total + ((d.S + 3) & ~3);   // pd_ss_geom's zp
+              L[zp + (((wave - 6) * 2 + 0) * PD_SLOTS + r) * 16 + lane] = ac[r];
+              L[zp + (((wave - 6) * 2 + 1) * PD_SLOTS + r) * 16 + lane] = ad[r];
+            }
+          }
         }
-      } else if (wave < 6) {
+      } else if (wave >= 6) {
+        if (smp) {   // waves 6, 7: z partials of a sampled step (ctx / h apart)
+          const int kh = wave & 1, mm = lane & 15;
+          f32x4 ac = {0.f, 0.f, 0.f, 0.f}, ad = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int i = 0; i < PD_KMAX; ++i) {
+            const int kb = kh + 2 * i;
+            if (kb < NKB) {   // wave-uniform
+              const int k = kb * 32 + 8 * (lane >> 4);
+              const bf16x8 a = (mm < PD_SLOTS && k < ED) ? load_bf16x8(xsb + mm * ED + k)
+                                                        : as_bf16x8(u16x8{0, 0, 0, 0, 0, 0, 0, 0});
+              // block kh + 2 i is a ctx block iff i < E / 64 (E % 64 == 0: pd_ss_ok)
+              if (i < d.E / 64) ac = mfma_bf16(a, wf[i], ac);
+              else ad = mfma_bf16(a, wf[i], ad);
+            }
+          }
+          if (lane < 16) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int zp = G.total + ((d.S + 3) & ~3);   // pd_ss_geom's zp
+              L[zp + (((wave - 6) * 2 + 0) * PD_SLOTS + r) * 16 + lane] = ac[r];
+              L[zp + (((wave - 6) * 2 + 1) * PD_SLOTS + r) * 16 + lane] = ad[r];
+            }
+          }
+        }
+      } else {
         const int kh = wave & 1, mm = lane & 15;
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -1448,6 +1628,99 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
       }
       __syncthreads();
       PD_TR(35);
+      float pss[4] = {0.f, 0.f, 0.f, 0.f};
+      if (smp) {
+        // ---- sampled step (ss_step's arithmetic, split over the group):
+        // z = tanh(drop_d(W_d h_{t-1} + b_d) + drop_c(W_c ctx_{t-1} + b_c)) of
+        // this member's units -> partial logits over them -> one group hand-off
+        // -> logits_{t-1} (fixed member order) -> first argmax -> the sampled
+        // embedding (dropout) -> pre = W_ih[:, :Y] e + b_ih + b_hh
+        ++nss;
+        const PdSs& ss = *ssp;
+        const int ZPW = (ss.Dz + PD_MEMBERS - 1) / PD_MEMBERS, zu0 = m * ZPW;
+        const int nz = max(0, min(ZPW, ss.Dz - zu0));
+        const PdSsGeom Z = pd_ss_geom(d, G.total, UPW, ss.Y, ZPW);
+        if (tid < PD_SLOTS * 16) {
+          const int sl = tid >> 4, zu = tid & 15, bb = grp + PD_GROUPS * sl;
+          float zv = 0.f;
+          if (zu < nz && bb < d.B) {
+            const int zr = zu0 + zu;
+            float a = L[Z.zp + ((0 * 2 + 1) * PD_SLOTS + sl) * 16 + zu] +
+                      L[Z.zp + ((1 * 2 + 1) * PD_SLOTS + sl) * 16 + zu] + (ss.b_d ? ss.b_d[zr] : 0.f);
+            float c = L[Z.zp + ((0 * 2 + 0) * PD_SLOTS + sl) * 16 + zu] +
+                      L[Z.zp + ((1 * 2 + 0) * PD_SLOTS + sl) * 16 + zu] + (ss.b_c ? ss.b_c[zr] : 0.f);
+            const unsigned idx = ((unsigned)bb * d.S + (t - 1)) * (unsigned)ss.Dz + zr;
+            if (ss.drop_d > 0.f) a *= drop_scale(ss.drop_d, ss.seed_d, idx);
+            if (ss.drop_c > 0.f) c *= drop_scale(ss.drop_c, ss.seed_c, idx);
+            zv = tanhf(a + c);
+          }
+          L[Z.zz + tid] = zv;
+        }
+        __syncthreads();
+        const int lsl = tid / ss.V, lv = tid % ss.V;
+        const bool lown = tid < PD_SLOTS * ss.V;
+        if (lown) {
+          float pl = 0.f;
+          for (int z = 0; z < nz; ++z) pl += L[Z.wfc + z * PD_VMAX + lv] * L[Z.zz + lsl * 16 + z];
+          pd_st(pd_rsrc(ss.lbuf, (unsigned)((size_t)PD_GROUPS * PD_MEMBERS * PD_SLOTS * PD_VMAX * 4)),
+                (((long long)grp * PD_MEMBERS + m) * PD_SLOTS + lsl) * PD_VMAX + lv, pl);
+        }
+        pd_publish(ss_ctr);
+        if (tid == 0) s_ok = pd_wait(ss_ctr, PD_MEMBERS * nss, ctr, status);
+        __syncthreads();
+        if (!s_ok) return;
+        if (lown) {
+          const __amdgpu_buffer_rsrc_t rl =
+              pd_rsrc(ss.lbuf, (unsigned)((size_t)PD_GROUPS * PD_MEMBERS * PD_SLOTS * PD_VMAX * 4));
+          float lsum = 0.f;
+          const int lb = (grp * PD_MEMBERS * PD_SLOTS + lsl) * PD_VMAX + lv;
+#pragma unroll 1
+          for (int j0 = 0; j0 < PD_MEMBERS; j0 += 4) {
+            float pv[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) pv[j] = pd_ld(rl, lb + (j0 + j) * PD_SLOTS * PD_VMAX);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) lsum += pv[j];
+          }
+          L[Z.lg + lsl * PD_VMAX + lv] = lsum + (ss.b_fc ? ss.b_fc[lv] : 0.f);
+        }
+        __syncthreads();
+        int* tk = reinterpret_cast<int*>(&L[Z.tk]);
+        if (tid < PD_SLOTS) {   // strict: the first maximum wins (torch.max)
+          float best = -__builtin_huge_valf();
+          int bi = 0;
+          for (int v = 0; v < ss.V; ++v) {
+            const float l = L[Z.lg + tid * PD_VMAX + v];
+            if (l > best) { best = l; bi = v; }
+          }
+          tk[tid] = bi;
+          const int bb = grp + PD_GROUPS * tid;
+          if (m == 0 && bb < d.B && ss.tok_ss) ss.tok_ss[(long long)bb * d.S + t] = bi;
+        }
+        __syncthreads();
+        for (int i = tid; i < PD_SLOTS * ss.Y; i += PD_THREADS) {
+          const int sl = i / ss.Y, y = i % ss.Y, bb = grp + PD_GROUPS * sl, tok = tk[sl];
+          float ev = ss.emb_trans ? ss.emb_w[(long long)y * ss.V + tok]
+                                  : ss.emb_w[(long long)tok * ss.Y + y];
+          const unsigned ei = ((unsigned)bb * d.S + t) * (unsigned)ss.Y + y;
+          if (ss.drop_emb > 0.f) ev *= drop_scale(ss.drop_emb, ss.seed_emb, ei);
+          L[Z.ev + i] = ev;
+          if (m == 0 && bb < d.B) ss.emb_ss[ei] = ev;
+        }
+        __syncthreads();
+        if (cown) {
+          const long long gb = ((long long)cb * d.S + t) * G4 + cj;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            float sv = L[Z.bs + q * UPW + cu];
+            const float* wr = &L[Z.wie + (q * UPW + cu) * ss.Y];
+            const float* ev = &L[Z.ev + csl * ss.Y];
+            for (int y = 0; y < ss.Y; ++y) sv += wr[y] * ev[y];
+            pss[q] = sv;
+            ss.pre_ss[gb + (long long)q * d.D] = sv;
+          }
+        }
+      }
       if (cown) {
         const long long gb = ((long long)cb * d.S + t) * G4 + cj;
         float pre[4];
@@ -1456,7 +1729,7 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
           const int gr = q * UPW + cu, tile = gr >> 4, col = gr & 15;
           pre[q] = L[G.part + ((2 * tile) * PD_SLOTS + csl) * 16 + col] +
                    L[G.part + ((2 * tile + 1) * PD_SLOTS + csl) * 16 + col] +
-                   pre_emb[gb + (long long)q * d.D];
+                   (smp ? pss[q] : pre_emb[gb + (long long)q * d.D]);
         }
         const float ig = sigmoidf_(pre[0]), fg = sigmoidf_(pre[1]);
         const float gg = tanhf_(pre[2]), og = sigmoidf_(pre[3]);
@@ -2374,14 +2647,16 @@ bool pd_ten(const Dims& d) { return pd_kind(d) > 0; }
 
 // f32: fp32 mode (the f32-MFMA cell / r products).  ASR_ATT_PERSIST32=0 keeps
 // fp32 mode on the per-step kernels.
-bool pd_eligible(const Dims& d, bool f32) {
+bool pd_eligible(const Dims& d, bool f32, int ssY = 0, int ssDz = 0) {
   const char* e = getenv("ASR_ATT_PERSIST");
   if (e && e[0] == '0') return false;
   const char* e32 = getenv("ASR_ATT_PERSIST32");
   if (f32 && e32 && e32[0] == '0') return false;
   if (f32 && (d.E + d.D) % 4 != 0) return false;   // 16-B x rows
   const PdGeom G = pd_geom(d);
-  const size_t lds = (size_t)G.total * 4;
+  const size_t lds = (size_t)(ssY ? pd_ss_geom(d, G.total, G.UPW, ssY,
+                                               (ssDz + PD_MEMBERS - 1) / PD_MEMBERS).total
+                                  : G.total) * 4;
   if (d.B > PD_GROUPS * PD_SLOTS || G.UPW > PD_UMAX || G.ED % 8 != 0 || G.NKB > 2 * PD_KMAX ||
       G.FCH > 8 * PD_FPW || d.A > 256 || (!pd_ten(d) && d.C > PD_CM) || G.ECW > PD_THREADS ||
       lds > 160 * 1024 ||
@@ -2396,6 +2671,19 @@ bool pd_eligible(const Dims& d, bool f32) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, PD_THREADS, lds) != hipSuccess)
     return false;
   return per_cu >= 1;
+}
+
+// Scheduled sampling inside the persistent forward (the sampled steps' phase of
+// attdec_fwd_persist): classes, embedding and bottleneck within the in-pass
+// limits, the ctx / h boundary of x where each K half's interleaved blocks
+// split by index alone (E % 64 == 0), every operand given.
+// ASR_ATT_PERSIST_SS=0: a pass with sampled steps takes the per-step kernels.
+bool pd_ss_ok(const Dims& d, const asr_attdec_opts_t& o) {
+  const char* e = getenv("ASR_ATT_PERSIST_SS");
+  if (e && e[0] == '0') return false;
+  return o.V > 0 && o.V <= PD_VMAX && o.Y > 0 && o.Y <= PD_YMAX && o.Dz > 0 &&
+         (o.Dz + PD_MEMBERS - 1) / PD_MEMBERS <= PD_ZMAX && d.E % 64 == 0 && o.w_d && o.w_c &&
+         o.w_fc && o.emb_w && o.w_ih_emb && o.b_ih && o.b_hh && o.pre_ss && o.emb_ss;
 }
 
 bool pb_eligible(const Dims& d, bool f32) {
@@ -2539,12 +2827,52 @@ extern "C" int asr_attdec_forward_ex(const asr_attdec_dims_t* dims, const asr_at
   g_att_last[0] = (d.C == 10 || d.C == 3) ? d.C : 0;
   g_att_last[1] = (int)eg.x;
   g_att_persist_last[0] = 0;
-  if (!ss && pd_eligible(d, !bf)) {
+  // sampled steps run inside the persistent pass when their operands fit its
+  // limits (pd_ss_ok); otherwise such a pass takes the per-step kernels
+  const bool ssin = ss && pd_ss_ok(d, *opts);
+  const int ssY = ssin ? opts->Y : 0, ssDz = ssin ? opts->Dz : 0;
+  if ((!ss || ssin) && pd_eligible(d, !bf, ssY, ssDz)) {
     const PdGeom G = pd_geom(d);
     int* ctr = (int*)((char*)workspace + W.ctr);
     float* pbuf = (float*)((char*)workspace + W.pbuf);
-    ASR_CHECK_HIP(hipMemsetAsync(ctr, 0, (size_t)(1 + PD_GROUPS) * PD_CTR * 4, s));
-    const size_t lds = (size_t)G.total * 4;
+    ASR_CHECK_HIP(hipMemsetAsync(ctr, 0, (size_t)(1 + 2 * PD_GROUPS) * PD_CTR * 4, s));
+    PdSs pss;
+    memset(&pss, 0, sizeof(pss));
+    PdSs* ssdev = nullptr;
+    if (ssin) {
+      int32_t* fl = (int32_t*)((char*)workspace + W.flags);
+      ASR_CHECK_HIP(hipMemcpyAsync(fl, opts->ss_steps_host, (size_t)d.S * 4,
+                                   hipMemcpyHostToDevice, s));
+      pss.flags = fl;
+      pss.w_d = opts->w_d; pss.b_d = opts->b_d; pss.w_c = opts->w_c; pss.b_c = opts->b_c;
+      pss.w_fc = opts->w_fc; pss.b_fc = opts->b_fc; pss.emb_w = opts->emb_w;
+      pss.w_ih_emb = opts->w_ih_emb; pss.b_ih = opts->b_ih; pss.b_hh = opts->b_hh;
+      pss.drop_d = opts->drop_d; pss.drop_c = opts->drop_c; pss.drop_emb = opts->drop_emb;
+      pss.seed_d = opts->seed_d; pss.seed_c = opts->seed_c; pss.seed_emb = opts->seed_emb;
+      pss.Y = opts->Y; pss.Dz = opts->Dz; pss.V = opts->V; pss.emb_trans = opts->emb_trans;
+      pss.ld_ih = opts->ld_ih;
+      pss.pre_ss = opts->pre_ss; pss.emb_ss = opts->emb_ss; pss.tok_ss = opts->tok_ss;
+      pss.lbuf = (float*)((char*)workspace + W.lbuf);
+      void* zc = (char*)workspace + W.zcat;
+      pss.zcat = zc;
+      {
+        const long long nz = (long long)opts->Dz * (d.E + d.D);
+        const int gz = (int)((nz + 255) / 256 < 4096 ? (nz + 255) / 256 : 4096);
+        if (bf)
+          hipLaunchKernelGGL((build_zcat<uint16_t>), dim3(gz), dim3(256), 0, s, d, opts->Dz,
+                             opts->w_c, opts->w_d, (uint16_t*)zc);
+        else
+          hipLaunchKernelGGL((build_zcat<float>), dim3(gz), dim3(256), 0, s, d, opts->Dz,
+                             opts->w_c, opts->w_d, (float*)zc);
+        ASR_LAUNCH_CHECK();
+      }
+      ssdev = (PdSs*)((char*)workspace + W.ssd);
+      rc = pd_ss_upload(pss, ssdev, s);
+      if (rc) return rc;
+    }
+    const size_t lds = (size_t)(ssin ? pd_ss_geom(d, G.total, G.UPW, ssY,
+                                                  (ssDz + PD_MEMBERS - 1) / PD_MEMBERS).total
+                                     : G.total) * 4;
     const dim3 grid(PD_GROUPS * PD_MEMBERS);
     // (A + E + 2) * 4 * T' algorithmic bytes per decoder step and utterance
     const int pslot = prof_begin_launch(ASR_PROF_ATT_FWD, s, att_pass_bytes(d));
@@ -2552,7 +2880,7 @@ extern "C" int asr_attdec_forward_ex(const asr_attdec_dims_t* dims, const asr_at
   hipLaunchKernelGGL((attdec_fwd_persist<CC, NQ, SA, SE, SD, SK, F>), grid, dim3(PD_THREADS), lds,  \
                      s, d, (const void*)workspace, pre_emb, h0, enc, enc_a, lens, w_dec, w_conv,  \
                      conv_w, v, dec, c_all, gates, x, ctx_all, aw_all, pbuf, ebuf, ctr,          \
-                     lstm_persist_status_word(), drop_h, seed_h)
+                     lstm_persist_status_word(), drop_h, seed_h, ssdev)
 #define ASR_PD(CC, NQ, SA, SE, SD, SK)                  \
   do {                                                  \
     if (bf) ASR_PD2(CC, NQ, SA, SE, SD, SK, false);     \

@@ -798,6 +798,16 @@ def att_decode_greedy(enc, enc_a, lens, h0, emb_dim, sharpen, sigmoid, w_ih, w_h
     return keep['tok_ss'][:, 1:], outs[5][:, :S - 1]
 
 
+_last_sampled = {'tok': None}
+
+
+def last_sampled_tokens():
+    """The sampled tokens [B, S] (int64, device; -1 at teacher-forced steps)
+    of the last fused decoder forward that had sampled steps, else None (the
+    decoder pass's tok_ss output; tests read it)."""
+    return _last_sampled['tok']
+
+
 class AttDecoderFn(torch.autograd.Function):
     """Returns (dec_out [B,S,D], ctx [B,S,E], aw [B,S,T]).  Weights:
     w_ih [4D, emb+E] (LSTMCell; only the context columns are used here, the
@@ -813,6 +823,7 @@ class AttDecoderFn(torch.autograd.Function):
             conv_w, v, train_opts)
         ctx.save_for_backward(enc, enc_a, lens, w_ih, w_hh, w_dec, w_conv, conv_w, v, dec, cst,
                               gates, x, aw)
+        _last_sampled['tok'] = keep.get('tok_ss')
         ctx.meta = (dims, emb_dim, h0 is not None)
         ctx.opts = (opts, keep, train_opts)
         ctx.mark_non_differentiable(aw)
