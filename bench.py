@@ -63,9 +63,10 @@ def _cfg(workload, model_type, params, **kw):
 CONFIGS = {
     'timit2x320': _cfg('timit_phone61_ctc_blstm2x320_f123', 'ctc', recipes.timit2x320()),
     # cpu_utts: the timed CPU step's sample, sized to ~10-30 s on 16 host
-    # threads (the 5x512 CPU step costs ~16 s per utterance at T = 1000)
+    # threads (round 5 measured 4.4 s for a 2-utterance step of 5x512 at
+    # T = 1000: a quarter of the B = 32 batch, 8 utterances, is ~18 s)
     'ctc5x512': _cfg('librispeech100h_char_ctc_blstm5x512', 'ctc', recipes.ctc5x512(),
-                     cpu_utts=2),
+                     cpu_utts=8),
     'att4x320': _cfg('librispeech100h_char_location_attention_blstm4x320', 'attention',
                      recipes.attention4x320(0.0)),
     'hybrid4x320': _cfg('librispeech_char_hybrid_ctc0.3_attention_blstm4x320', 'attention',
@@ -673,6 +674,15 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-parity', action='store_true')
     ap.add_argument('--prof-stride', type=int, default=8)
+    ap.add_argument('--prof-steps', type=int, default=-1,
+                    help='steps of the separate profiled pass the roofline samples come from '
+                         '(-1: = --steps, 0: none); the headline loop runs unprofiled')
+    ap.add_argument('--ss', default='steady', choices=['steady', 'early', 'off'],
+                    help='attention configs: scheduled sampling at the recipe\'s steady state '
+                         '(_ss_prob = scheduled_sampling_prob, reached after '
+                         'scheduled_sampling_max_step steps), at the first training steps '
+                         '(_step from 0: _ss_prob ~ 0), or off; the other two are timed as '
+                         'legs beside the headline')
     ap.add_argument('--sync-each-step', action='store_true',
                     help='read every step\'s loss back before the next step starts (the '
                          'reference loop\'s loss.item()); default: one step late '
@@ -740,46 +750,100 @@ def main():
     batch = dict(batch)
     batch['xs'] = torch.from_numpy(np.ascontiguousarray(host_batch['xs'])).to(dev)
 
+    ss_cfg = cfg['model_type'] == 'attention' and p.get('scheduled_sampling_prob', 0) > 0
+
+    def set_ss(mode):
+        # the reference's schedule (attention_seq2seq.py:555-561): _ss_prob grows
+        # linearly to scheduled_sampling_prob over scheduled_sampling_max_step
+        # training steps; 'steady' = past that ramp, 'early' = the first steps
+        if not ss_cfg:
+            return
+        if mode == 'steady':
+            model._step = int(p['scheduled_sampling_max_step'])
+            model._ss_prob = float(p['scheduled_sampling_prob'])
+        elif mode == 'early':
+            model._step = 1
+            model._ss_prob = p['scheduled_sampling_prob'] / p['scheduled_sampling_max_step']
+        else:
+            model._ss_prob = 0.0
+
+    def timed(nsteps, profile=False):
+        """nsteps training steps between barrier + synchronize brackets;
+        (elapsed s, per-step host marks, losses).  profile: the library's
+        per-launch HIP-event samples (asr_prof_*) are taken in this pass."""
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        if profile:
+            N.call('asr_prof_begin', args.prof_stride)
+        t0 = time.perf_counter()
+        lv_all, mk = [], [t0]
+        m = model
+        for _ in range(nsteps):
+            # sync_each_step: reads the loss back, the step has drained; otherwise the
+            # previous step's loss is read back when this step reaches its optimizer
+            m, lv = step(m, batch)
+            lv_all.append(lv)
+            mk.append(time.perf_counter())
+        lv_all = [float(v) for v in lv_all]
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        st = np.diff(np.asarray(mk))
+        if world > 1:
+            t = torch.tensor([el] + list(st), dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el, st = float(t[0].item()), t[1:].cpu().numpy()
+        return el, st, lv_all
+
+    set_ss(args.ss)
     for _ in range(args.warmup):
         model, lv = step(model, batch)
     float(lv) if args.warmup else None
-    torch.cuda.synchronize()
+    from pytorch_end2end_speech_recognition_amd.utils.training import training_loop as TL
+    TL.reset_step_stats()
+    # the headline: unprofiled
+    elapsed, step_s, losses = timed(args.steps)
+    step_stats = dict(TL.STEP_STATS)
     if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    N.call('asr_prof_begin', args.prof_stride)
-    t0 = time.perf_counter()
-    losses, marks = [], [t0]
-    for _ in range(args.steps):
-        # sync_each_step: reads the loss back, the step has drained; otherwise the
-        # previous step's loss is read back when this step reaches its optimizer
-        model, lv = step(model, batch)
-        losses.append(lv)
-        marks.append(time.perf_counter())
-    losses = [float(lv) for lv in losses]
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    import ctypes
-    NK = len(KIND_NAMES)
-    mean_us = (ctypes.c_double * NK)()
-    launches = (ctypes.c_longlong * NK)()
-    mean_work = (ctypes.c_double * NK)()
-    N.call('asr_prof_end', ctypes.cast(mean_us, ctypes.c_void_p),
-           ctypes.cast(launches, ctypes.c_void_p), ctypes.cast(mean_work, ctypes.c_void_p), NK)
-    samples = prof_samples()
-    step_s = np.diff(np.asarray(marks))
-    if world > 1:
-        t = torch.tensor([elapsed] + list(step_s), dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, step_s = float(t[0].item()), t[1:].cpu().numpy()
         fr = torch.tensor([frames_per_step], dtype=torch.float64, device=dev)
         dist.all_reduce(fr, op=dist.ReduceOp.SUM)
         total_frames_per_step = float(fr.item())
     else:
         total_frames_per_step = frames_per_step
+    # the roofline samples: a separate profiled pass of the same step
+    import ctypes
+    NK = len(KIND_NAMES)
+    mean_us = (ctypes.c_double * NK)()
+    launches = (ctypes.c_longlong * NK)()
+    mean_work = (ctypes.c_double * NK)()
+    prof_steps = args.steps if args.prof_steps < 0 else args.prof_steps
+    prof_elapsed = None
+    samples = {}
+    if prof_steps > 0:
+        prof_elapsed, _, _ = timed(prof_steps, profile=True)
+        N.call('asr_prof_end', ctypes.cast(mean_us, ctypes.c_void_p),
+               ctypes.cast(launches, ctypes.c_void_p), ctypes.cast(mean_work, ctypes.c_void_p),
+               NK)
+        samples = prof_samples()
+    # scheduled-sampling legs: the same step at the other sampling regimes
+    ss_legs = None
+    if ss_cfg and args.steps > 0:
+        ss_legs = {}
+        for mode in ('steady', 'early', 'off'):
+            if mode == args.ss:
+                continue
+            set_ss(mode)
+            for _ in range(2):
+                model, lv = step(model, batch)
+            float(lv)
+            el, _, _ = timed(args.steps)
+            ss_legs[mode] = {'ms_per_step': round(1000.0 * el / args.steps, 3),
+                             'ss_prob': round(float(model._ss_prob), 6)}
+        set_ss(args.ss)
 
     h2d_steps = args.steps if args.h2d_steps < 0 else args.h2d_steps
     h2d = h2d_loop(model, step, host_batch, dev, args.warmup, h2d_steps, world,
@@ -820,8 +884,23 @@ def main():
                    'ms_per_step_median_host_marks':
                    round(1000.0 * float(np.median(step_s)), 3),
                    'ms_per_step_min': round(1000.0 * float(np.min(step_s)), 3),
-                   'ms_per_step_max': round(1000.0 * float(np.max(step_s)), 3)},
+                   'ms_per_step_max': round(1000.0 * float(np.max(step_s)), 3),
+                   'profiling': ('none in the headline loop; the roofline samples come from '
+                                 'a separate pass of %d profiled steps (%s ms/step)'
+                                 % (prof_steps, round(1000.0 * prof_elapsed / prof_steps, 3)
+                                    if prof_elapsed else None))},
+        'steps_stats': {'skipped': step_stats['skipped'],
+                        'recurrence_give_ups': step_stats['recurrence_give_ups'],
+                        'steps': step_stats['steps'],
+                        'what': 'headline-loop training steps whose update was dropped '
+                                '(utils/training/training_loop.STEP_STATS)'},
         'h2d': h2d,
+        'scheduled_sampling': ({'headline': args.ss, 'ss_prob': round(float(model._ss_prob), 6),
+                                'legs': ss_legs,
+                                'what': 'per decoder step, random.random() < _ss_prob feeds '
+                                        'embed(argmax logits_{t-1}) (attention_seq2seq.py:'
+                                        '742-748), inside the persistent decoder pass'}
+                               if ss_cfg else None),
         'loss_last': losses[-1] if losses else None,
         'roofline': roofline,
         'cpu_baseline': cpu,

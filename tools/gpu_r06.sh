@@ -7,7 +7,7 @@ set -o pipefail
 mkdir -p gpurun_out
 T=${TAG:-x}
 if [ -n "$TESTS" ]; then
-  timeout -k 10 900 python -u -m pytest $TESTS -x -v -s --timeout 300 --timeout-method thread \
+  timeout -k 10 900 python -u -m pytest $TESTS -m gpu -x -v -s --timeout 300 --timeout-method thread \
     > gpurun_out/t_$T.log 2>&1
   rc=$?; grep -E "passed|failed|error" gpurun_out/t_$T.log | tail -3; [ $rc -eq 0 ] || { tail -40 gpurun_out/t_$T.log; exit $rc; }
 fi
