@@ -3069,6 +3069,7 @@ extern "C" int asr_attdec_backward_ex(const asr_attdec_dims_t* dims, const asr_a
     ASR_LAUNCH_CHECK();
     prof_end_launch(ASR_PROF_ATT_BWD, pslot, s);
     g_att_last[2] = pd_ten(d) ? 10 : 0;
+    g_att_last[3] = att_chunks(d);   // (the frame split the per-step kernels would use)
     g_att_persist_last[1] = 1;
   } else {
   ASR_CHECK_HIP(hipMemsetAsync(carry, 0, (size_t)d.B * d.T * 4, s));

@@ -153,6 +153,7 @@ def test_prod_attention_bf16_within_tolerance(name, cuda_dev):
     (tests/test_recurrence_full.py)."""
     d, loss, grads, launch = _gpu_run(name, 'bf16', cuda_dev)
     assert launch[0] == 10 and launch[1] >= 4 and launch[2] == 10 and launch[3] >= 4, launch
+    assert launch[4:6] == [1, 1], launch                        # both passes persistent
     errs = _norm_errors(d, grads)
     worst = sorted(errs.items(), key=lambda kv: -kv[1])[:6]
     print('\nbf16 loss rel err %.2e; worst gradient rel-L2 errors: %s' % (
