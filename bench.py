@@ -758,6 +758,7 @@ def main():
         # training steps; 'steady' = past that ramp, 'early' = the first steps
         if not ss_cfg:
             return
+        model.ss_prob = 0.0 if mode == 'off' else float(p['scheduled_sampling_prob'])
         if mode == 'steady':
             model._step = int(p['scheduled_sampling_max_step'])
             model._ss_prob = float(p['scheduled_sampling_prob'])

@@ -465,19 +465,34 @@ extern "C" int asr_lstm_persist_status(int* status, int clear, void* stream) {
 // device after the recurrences that precede it on the stream; clear = 1 then
 // zeroes both words (also stream-ordered).  dst feeds asr_optim_step_guarded
 // (directly, or after a MAX all-reduce over the data-parallel ranks).
+namespace asr {
+namespace {
+// both status words copied (and cleared) by one thread: one launch where two
+// copies and two fills were four (each a dispatch on the step's stream)
+__global__ void status_gather_k(int* dst, int* pp, int* xg, int clear) {
+  if (threadIdx.x == 0) {
+    const int a = __hip_atomic_load(pp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int b = __hip_atomic_load(xg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    dst[0] = a;
+    dst[1] = b;
+    if (clear) {
+      __hip_atomic_store(pp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(xg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+}  // namespace
+}  // namespace asr
+
 extern "C" int asr_lstm_status_gather(int* dst, int clear, void* stream) {
   ASR_REQUIRE(dst, ASR_ERR_ARG, "status_gather: null pointer");
   hipStream_t s = (hipStream_t)stream;
   int* xg = lstm_xg_status_word();
-  void* pp = nullptr;
+  static void* pp = nullptr;
   ASR_REQUIRE(xg, ASR_ERR_HIP, "status_gather: no tagged-granule status word");
-  ASR_CHECK_HIP(hipGetSymbolAddress(&pp, HIP_SYMBOL(g_persist_status)));
-  ASR_CHECK_HIP(hipMemcpyAsync(dst, pp, sizeof(int), hipMemcpyDeviceToDevice, s));
-  ASR_CHECK_HIP(hipMemcpyAsync(dst + 1, xg, sizeof(int), hipMemcpyDeviceToDevice, s));
-  if (clear) {
-    ASR_CHECK_HIP(hipMemsetAsync(pp, 0, sizeof(int), s));
-    ASR_CHECK_HIP(hipMemsetAsync(xg, 0, sizeof(int), s));
-  }
+  if (!pp) ASR_CHECK_HIP(hipGetSymbolAddress(&pp, HIP_SYMBOL(g_persist_status)));
+  hipLaunchKernelGGL(asr::status_gather_k, dim3(1), dim3(64), 0, s, dst, (int*)pp, xg, clear);
+  ASR_LAUNCH_CHECK();
   return ASR_OK;
 }
 

@@ -2081,8 +2081,8 @@ int lstm_xg_status(int* status, int clear, hipStream_t s) {
 
 // Device address of g_xg_status (stream-ordered gathers and clears, no host sync).
 int* lstm_xg_status_word() {
-  void* p = nullptr;
-  if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_xg_status)) != hipSuccess) return nullptr;
+  static void* p = nullptr;
+  if (!p && hipGetSymbolAddress(&p, HIP_SYMBOL(g_xg_status)) != hipSuccess) p = nullptr;
   return (int*)p;
 }
 
