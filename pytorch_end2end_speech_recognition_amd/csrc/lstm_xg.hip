@@ -160,10 +160,6 @@ __device__ __forceinline__ int tags_ok(const u32x4& v, unsigned tag) {
 // by someone, or this wave's spin budget is spent).
 __device__ int g_xg_cell_sc1;  // backward cell inputs by sc1 (L2) loads (ASR_XG_CELL_SC1)
 __device__ int g_xg_sleep;   // s_sleep(1) units between polls (ASR_XG_SLEEP, default 1)
-// ASR_XG_POLL2: the sweepers keep two polls in flight (the next one issued before
-// the previous one is checked), so a granule that lands just after a poll has
-// read L2 is seen half a round trip sooner on average
-__device__ int g_xg_poll2;
 __device__ int g_xg_delay;   // s_sleep(1) units before a step's first poll (ASR_XG_DELAY)
 
 __device__ __forceinline__ void nap(int n) {
@@ -731,7 +727,6 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
     const __amdgpu_buffer_rsrc_t rs = xg_rsrc(xg, xg_bytes);
     const int nsleep = __builtin_amdgcn_readfirstlane(g_xg_sleep);
     const int ndelay = __builtin_amdgcn_readfirstlane(g_xg_delay);
-    const int poll2 = __builtin_amdgcn_readfirstlane(g_xg_poll2);
     __syncthreads();  // B_pre: the first three steps' input rows are in LDS
     __syncthreads();  // B_init: the producers' pre(0) is in LDS
     for (int s = 0; s < T; ++s) {
@@ -745,39 +740,6 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
                                             (long long)quarter) * 8);
         u32x4 v[KSW];
         nap(ndelay);
-        if (poll2) {   // two polls in flight (see lstm_bwd_xg)
-          auto issue = [&](u32x4 (&vv)[KSW]) {
-            if (sweeper) {
-#pragma unroll
-              for (int i = 0; i < KSW; ++i)
-                vv[i] = ld_sc1(rs, rowoff + (unsigned)((8 * min(wave + NSW * i, nks - 1) + 2 * kq) * 8));
-            }
-          };
-          auto check = [&](const u32x4 (&vv)[KSW]) {
-            int ok = 1;
-            if (sweeper) {
-#pragma unroll
-              for (int i = 0; i < KSW; ++i)
-                ok &= (int)((((vv[i][0] ^ ebit) | (vv[i][2] ^ ebit)) & 1u) == 0u);
-            }
-            return __all(ok);
-          };
-          u32x4 vb[KSW];
-          issue(v);
-          for (unsigned spins = 0;; spins += 2) {
-            issue(vb);
-            if (check(v)) break;
-            if (!keep_spinning(spins, abortw, nsleep)) { s_dead = 1; break; }
-            issue(v);
-            if (check(vb)) {
-#pragma unroll
-              for (int i = 0; i < KSW; ++i) v[i] = vb[i];
-              break;
-            }
-            if (!keep_spinning(spins + 1, abortw, nsleep)) { s_dead = 1; break; }
-          }
-          XG_TR(s, 1, __builtin_amdgcn_s_memrealtime());
-        } else
         for (unsigned spins = 0;; ++spins) {
           const unsigned long long t_iss = tr ? __builtin_amdgcn_s_memrealtime() : 0;
           int ok = 1;
@@ -1149,7 +1111,6 @@ __global__ void __launch_bounds__(256 + R * XB + 64 * (F32 ? 4 : XB / 4)) lstm_b
     // every later step -- before B1 of step q; the flag's load is issued
     // before the step's poll and checked after it.
     const int qmid = (T + 1) / 2 - 1;
-    const int poll2 = __builtin_amdgcn_readfirstlane(g_xg_poll2);
     int dyk = -1, dynext = 0, dyv = 0;
     auto dy_need = [&](int q) { return min(q, qmid) >= dynext; };
     if (dyflag && dy_need(min(1, T - 1))) {   // steps 0 and 1 (loaded before the loop)
@@ -1206,19 +1167,6 @@ __global__ void __launch_bounds__(256 + R * XB + 64 * (F32 ? 4 : XB / 4)) lstm_b
           }
           return __all(ok);
         };
-        if (poll2) {   // two polls in flight: issue the next before checking the older
-          u32x4 va[NLD], vb[NLD];
-          issue(va);
-          for (unsigned spins = 0;; spins += 2) {
-            issue(vb);
-            if (check(va)) break;
-            if (!keep_spinning(spins, abortw, nsleep)) { s_dead = 1; break; }
-            issue(va);
-            if (check(vb)) break;
-            if (!keep_spinning(spins + 1, abortw, nsleep)) { s_dead = 1; break; }
-          }
-          XG_TR(q, 1, __builtin_amdgcn_s_memrealtime());
-        } else
         for (unsigned spins = 0;; ++spins) {
           const unsigned long long t_iss = tr ? __builtin_amdgcn_s_memrealtime() : 0;
           u32x4 vv[NLD];
@@ -2034,16 +1982,6 @@ void xg_tuning_setup(hipStream_t s) {
 
 void xg_trace_setup(hipStream_t s) {
   xg_tuning_setup(s);
-  {  // read per launch (A/B within one process)
-    static int lastp = -1;
-    const char* p2 = getenv("ASR_XG_POLL2");
-    const int poll2 = p2 ? atoi(p2) : 0;
-    if (poll2 != lastp) {
-      lastp = poll2;
-      (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_xg_poll2), &poll2, sizeof(int), 0,
-                                   hipMemcpyHostToDevice, s);
-    }
-  }
   {  // read per launch (A/B within one process)
     static int last = -1;
     const char* c1 = getenv("ASR_XG_CELL_SC1");

@@ -5,7 +5,7 @@ set -e
 NAME=$1; SRC=$2; FLAGS=$3
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 C=$ROOT/pytorch_end2end_speech_recognition_amd/csrc
-OUT=$ROOT/ablib/$NAME
+OUT=${VAR_DIR:-$ROOT/varlib}/$NAME   # varlib/ travels to the GPU box (git-ignored only)
 mkdir -p $OUT/obj
 BASE=$(basename $SRC .hip)
 SLP=-fno-slp-vectorize   # as csrc/Makefile: SLP only in lstm_xg.hip

@@ -65,10 +65,17 @@ def main():
     ws = [torch.from_numpy(rng.uniform(-0.1, 0.1, s).astype(np.float32)).to(dev).requires_grad_(True)
           for s in ((8 * H, Din), (8 * H, H), (8 * H,), (8 * H,))]
     lens = torch.full((B,), T, dtype=torch.int32, device=dev)
+    bwd = None
     for _ in range(2):
         y = ops.blstm_layer(x, lens, T, *ws)
         torch.cuda.synchronize()
         fwd = read()
+        if bwd is not None and np.array_equal(fwd, bwd):
+            # the fused forward (lstm_fwd_xgx) stamps only in a -DASR_XG_TRACE_FWD
+            # build: what was read is the previous backward's trace
+            print('WARNING: the forward pass wrote no stamps (build lstm_xg.hip with '
+                  '-DASR_XG_TRACE_FWD, tools/build_variant.sh); its rows below repeat the '
+                  'backward', flush=True)
         y.backward(torch.randn_like(y))
         torch.cuda.synchronize()
         bwd = read()
