@@ -225,6 +225,10 @@ int asr_gemm_lse_ws(const asr_gemm_t* problem, int compute_dtype, float* lse, vo
  * their work-groups fit beside a persistent recurrence work-group on every CU
  * (weight gradients co-resident with the backward recurrence). */
 int asr_gemm_set_small_tiles(int on);
+/* on != 0: later asr_gemm calls FROM THIS HOST THREAD take no split-K slabs
+ * (rows of one product computed by several launches then sum every output
+ * element in the order one launch would: bitwise the same dX either way). */
+int asr_gemm_set_nosplit(int on);
 /* asr_gemm_set_n64_kmode(1): products with N <= 64 (M >= 4096) whose B is
  * K-major also take the 256 x 64 kernel (launches from this host thread). */
 int asr_gemm_set_n64_kmode(int on);
@@ -919,6 +923,19 @@ int asr_lstm_backward_grid(int B, int H, int xu);
  * step (T + 1) / 2 - 1).  The recurrence
  * waits for each chunk's flag before reading its dy rows.  flags NULL: off. */
 int asr_lstm_set_dy_flags(const int* flags, int c0, int epoch);
+
+/* Split input gradient (round 6): the next asr_lstm_backward_dgbf_h launch
+ * adds 1 to *counter per cell wave once the gate gradients of processing steps
+ * <= q are stored and released at agent scope (NULL: off; applies to launches
+ * from the calling host thread until reset).  asr_lstm_bwd_progress_arrivals:
+ * what one launch of [B, *, H] adds.  asr_lstm_progress_gate enqueues a wait
+ * on another stream until *counter >= target (bounded; a timeout sets the
+ * recurrence status word, so the step is skipped).  Processing step q covers
+ * t = T-1-q (forward direction) and t = q (reverse): rows t in [T-1-q, q] of
+ * dG are final once q >= T/2. */
+int asr_lstm_set_bwd_progress(unsigned long long* counter, int q);
+long long asr_lstm_bwd_progress_arrivals(int B, int H);
+int asr_lstm_progress_gate(const unsigned long long* counter, long long target, void* stream);
 /* Stream-ordered: flags[k] = epoch after the work enqueued before it. */
 int asr_lstm_dy_signal(int* flags, int k, int epoch, void* stream);
 /* Diagnostics only (tools/cores_locate.py): backward recurrence launches

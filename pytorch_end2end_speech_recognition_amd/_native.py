@@ -57,6 +57,7 @@ SIGNATURES = {
     'asr_gemm_ws': (c_int, [c_vp, c_int, c_int, c_vp, c_size, c_vp]),
     'asr_gemm_lse_ws': (c_int, [c_vp, c_int, c_vp, c_vp, c_size, c_vp]),
     'asr_gemm_set_small_tiles': (c_int, [c_int]),
+    'asr_gemm_set_nosplit': (c_int, [c_int]),
     'asr_gemm_set_n64_kmode': (c_int, [c_int]),
     'asr_lstm_wgrad_gate': (c_int, [c_vp]),
     'asr_colsum_workspace_bytes': (c_size, [c_int, c_int]),
@@ -220,6 +221,9 @@ SIGNATURES = {
     'asr_lstm_xg_mode': (c_int, [c_vp, c_int]),
     'asr_lstm_last_path': (c_int, [c_vp]),
     'asr_ctc_last_path': (c_int, [c_vp]),
+    'asr_lstm_set_bwd_progress': (c_int, [c_vp, c_int]),
+    'asr_lstm_bwd_progress_arrivals': (c_ll, [c_int, c_int]),
+    'asr_lstm_progress_gate': (c_int, [c_vp, c_ll, c_vp]),
     'asr_xg_trace_read': (c_ll, [c_vp]),
     'asr_lstm_debug_dh': (c_int, [c_vp, c_vp, c_vp, c_vp]),
     'asr_lstm_set_bwd_pin_kb': (c_int, [c_int]),

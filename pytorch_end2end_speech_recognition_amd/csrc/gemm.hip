@@ -2258,10 +2258,15 @@ struct SplitPlan {
   size_t bytes;
 };
 
+// asr_gemm_set_nosplit(1): launches from this host thread take no split-K
+// slabs until reset (products whose rows are computed in several launches
+// that must sum each output element in the same order as one launch would)
+thread_local int g_nosplit = 0;
+
 SplitPlan plan_split(const asr_gemm_t* g, int nprob) {
   SplitPlan sp{};
   const char* ns = getenv("ASR_GEMM_NOSPLIT");   // diagnostics: no split-K slabs
-  const bool nosplit = ns && ns[0] == '1';
+  const bool nosplit = (ns && ns[0] == '1') || g_nosplit;
   for (int i = 0; i < nprob; ++i) {
     // per problem: the problems of one launch run side by side (blockIdx.z), so
     // a few-tile dW next to a many-tile dX still gets its own K split
@@ -2927,6 +2932,11 @@ int gemm_launch(const asr_gemm_t* problems, int nprob, int compute_dtype, void* 
 }  // namespace asr
 
 using namespace asr;
+
+extern "C" int asr_gemm_set_nosplit(int on) {
+  g_nosplit = on ? 1 : 0;
+  return ASR_OK;
+}
 
 extern "C" int asr_gemm_set_small_tiles(int on) {
   g_small_tiles = on ? 1 : 0;

@@ -120,6 +120,12 @@ int xg_bwd_xu(int R, int H) {
 // asr_lstm_set_dy_flags: dy of the next packed-activation backward launch
 // arrives chunk by chunk (see lstm_bwd_xg's sweepers); NULL = off.
 const int* g_dyflag = nullptr;
+// asr_lstm_set_bwd_progress: the next packed-activation backward launch reports
+// when the gate gradients of processing steps <= g_prog_q are stored (every
+// cell wave adds 1 to *g_prog_ctr after a release), so the input-gradient GEMM
+// of the rows complete by then can start beside the rest of the pass.
+unsigned long long* g_prog_ctr = nullptr;
+int g_prog_q = -1;
 int g_dyc0 = 16;
 unsigned g_dyepoch = 0;
 
@@ -1054,7 +1060,8 @@ __global__ void __launch_bounds__(256 + R * XB + 64 * (F32 ? 4 : XB / 4)) lstm_b
     const float* __restrict__ cst, unsigned long long* pg, int* hdr,
     uint16_t* __restrict__ dgbf, float* __restrict__ dbpart, unsigned epoch, int allow_local,
     int dg_f32, int io_pos, int dg_st16, const h16x4* __restrict__ acth,
-    const int* __restrict__ dyflag, int dyc0, int dyepoch) {
+    const int* __restrict__ dyflag, int dyc0, int dyepoch, unsigned long long* prog,
+    int prog_q) {
   static_assert(!F32 || ((XB == 16 || XB == 8) && !AH), "f32 backward: 8 or 16 units, f32 activations");
   constexpr int UPL = F32 ? 4 : 8;     // units per 16-B load
   constexpr int SQ = XB / UPL;         // 16-B loads per row of a producer's slice
@@ -1408,6 +1415,15 @@ __global__ void __launch_bounds__(256 + R * XB + 64 * (F32 ? 4 : XB / 4)) lstm_b
       if (io_pos == 0) step_io(q, t, d_i, d_f, d_g, d_o, bi, bff, bg, bo);
       __syncthreads();  // B3
       if (io_pos == 1) step_io(q, t, d_i, d_f, d_g, d_o, bi, bff, bg, bo);
+      if (prog && q == prog_q) {
+        // every dG store of steps <= q by this wave is complete and released
+        // at agent scope (written back from this XCD's L2), then counted: a
+        // reader on another stream that sees all arrivals reads final rows
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if (lane == 0)
+          __hip_atomic_fetch_add((gu64*)prog, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
     if (own && dbpart) {  // per-utterance bias-gradient partials [B][8H]
       float* o = dbpart + (long long)b * 8 * H + (long long)dir * H4 + j;
@@ -1765,7 +1781,7 @@ int lstm_bwd_xg32_launch(int B, int T, int H, const int32_t* lens, const float* 
     hipLaunchKernelGGL((lstm_bwd_xg<RR, M, false, XV, true>), dim3(grid),                        \
                        dim3(256 + RR * XV + 256), pin, s, B, T, H, lens, whh_f, whh_r, dy,      \
                        act_dg, cst, g, hdr, (uint16_t*)nullptr, dbpart, ep, al, 1, 0, 0,        \
-                       (const h16x4*)nullptr, (const int*)nullptr, 0, 0);                        \
+                       (const h16x4*)nullptr, (const int*)nullptr, 0, 0, nullptr, -1);           \
   } while (0)
 #define ASR_XGB32_M(RR, XV)                 \
   do {                                      \
@@ -1870,7 +1886,8 @@ int lstm_bwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* wh
                        pin, s,                                                                  \
                        B, T, H, lens, whh_f, whh_r, dy, act_dg, cst, g, hdr, dgbf, dbpart, ep,   \
                        al, (dg_f32 || !dgbf) ? 1 : 0, io_pos, st16, (const h16x4*)acth,         \
-                       acth ? g_dyflag : nullptr, g_dyc0, (int)g_dyepoch);                       \
+                       acth ? g_dyflag : nullptr, g_dyc0, (int)g_dyepoch,                        \
+                       acth ? g_prog_ctr : nullptr, g_prog_q);                                   \
   } while (0)
 #define ASR_XGB2(RR, M, AHV)                                  \
   do {                                                        \
@@ -2077,6 +2094,58 @@ __global__ void dy_signal(int* flags, int k, int epoch) {
 extern "C" int asr_lstm_dy_signal(int* flags, int k, int epoch, void* stream) {
   ASR_REQUIRE(flags && k >= 0 && epoch != 0, ASR_ERR_ARG, "dy signal");
   hipLaunchKernelGGL(asr::dy_signal, dim3(1), dim3(64), 0, (hipStream_t)stream, flags, k, epoch);
+  return hipGetLastError() == hipSuccess ? ASR_OK : ASR_ERR_HIP;
+}
+
+// The next packed-activation backward launch (asr_lstm_backward_dgbf_h) adds 1
+// to *counter per cell wave once the gate gradients of processing steps <= q
+// are stored and released; counter NULL: off.  Stream-ordered launches only
+// ever add, so a reader waits for the running total (asr_lstm_progress_gate).
+extern "C" int asr_lstm_set_bwd_progress(unsigned long long* counter, int q) {
+  ASR_REQUIRE(!counter || q >= 0, ASR_ERR_ARG, "bwd progress: q %d", q);
+  asr::g_prog_ctr = counter;
+  asr::g_prog_q = counter ? q : -1;
+  return ASR_OK;
+}
+
+// Arrivals one backward launch of this shape adds to the progress counter
+// (cell waves x work-groups), 0 if the shape does not take the tagged-granule
+// backward with the current units setting.
+extern "C" long long asr_lstm_bwd_progress_arrivals(int B, int H) {
+  const int R = asr::xg_rows(B, H);
+  if (!R) return 0;
+  const int xb = asr::xg_bwd_xu(R, H);
+  return (long long)(2 * ((B + R - 1) / R) * (H / xb)) * (R * xb / 64);
+}
+
+namespace asr {
+namespace {
+// one lane waits (acquire, agent scope) until *ctr >= target; bounded by
+// `ticks` of the 100 MHz clock: a timeout marks the recurrence as given up
+// (g_xg_status: the training step that needed these rows is skipped, never
+// computed from incomplete rows)
+__global__ void progress_gate(const unsigned long long* ctr, unsigned long long target,
+                              unsigned long long ticks) {
+  if (threadIdx.x != 0) return;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__hip_atomic_load((const gu64*)ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+      atomicOr(&g_xg_status, 2);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(8);
+  }
+}
+}  // namespace
+}  // namespace asr
+
+// Enqueue on `stream`: return once the progress counter reaches `target`
+// (bounded at ~2 s; a timeout sets the recurrence status word).
+extern "C" int asr_lstm_progress_gate(const unsigned long long* counter, long long target,
+                                      void* stream) {
+  ASR_REQUIRE(counter && target > 0, ASR_ERR_ARG, "progress gate: args");
+  hipLaunchKernelGGL(asr::progress_gate, dim3(1), dim3(64), 0, (hipStream_t)stream, counter,
+                     (unsigned long long)target, 200000000ull);
   return hipGetLastError() == hipSuccess ? ASR_OK : ASR_ERR_HIP;
 }
 

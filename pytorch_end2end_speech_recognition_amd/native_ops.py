@@ -1249,6 +1249,18 @@ class BLSTMLayerFn(torch.autograd.Function):
         mode, xu = _overlap_plan(dev, B, H)
         N.call('asr_lstm_set_bwd_pin_kb', 84 if mode == '2' else 0)
         N.call('asr_lstm_set_bwd_units', xu)
+        split = None
+        if (act.dtype == torch.float16 and pipe is None and _dx_split_ok(ctx, B, T, dev, mode)
+                and not _dx_pipeline_ok(ctx, B, T, Din, dev)):
+            N.call('asr_lstm_set_bwd_units', xu)     # (arrivals follow the units setting)
+            arrivals = N.query('asr_lstm_bwd_progress_arrivals', B, H)
+            if arrivals > 0:
+                split = (T // 4, _progress_counter(dev), int(arrivals))
+                # dX before the recurrence: its zero fill (non-identity maps) precedes
+                # the side stream's writes
+                ident = perm is None and t_mul == 1 and t_add == 0 and T == T_src and Din == Dsrc
+                dx_split = (torch.empty if ident else torch.zeros)(B, T_src, Dsrc,
+                                                                   dtype=torch.float32, device=dev)
         try:
             if act.dtype == torch.float16:
                 # packed fp16 activations of asr_lstm_forward_xh: the tagged-granule
@@ -1257,12 +1269,20 @@ class BLSTMLayerFn(torch.autograd.Function):
                 ws = _ws(nb, dev)
                 if pipe is not None:
                     N.call('asr_lstm_set_dy_flags', N.ptr(pipe[0]), pipe[1], pipe[2])
+                if split is not None:
+                    N.call('asr_lstm_set_bwd_progress', N.ptr(split[1][0]), T - 1 - split[0])
+                    # everything the side stream's share of dX reads that is not
+                    # written by the recurrence is enqueued by now (dx's fill included)
+                    split_pre = torch.cuda.Event()
+                    split_pre.record(torch.cuda.current_stream(dev))
                 try:
                     rc = N.query('asr_lstm_backward_dgbf_h', N.ptr(dy), N.ptr(w_hh),
                                  ctypes.c_void_p(whh_r), F32, N.ptr(lens), B, T, H, cd, N.ptr(act),
                                  N.ptr(cst), N.ptr(dg_bf), N.ptr(gbufs[2]), N.ptr(gbufs[3]),
                                  N.ptr(ws), nb, N.stream_handle(dev))
                 finally:
+                    if split is not None:
+                        N.call('asr_lstm_set_bwd_progress', None, 0)
                     if pipe is not None:
                         N.call('asr_lstm_set_dy_flags', None, 16, 0)
                         # (after the launch: later compute-stream work sees all of dy)
@@ -1272,6 +1292,11 @@ class BLSTMLayerFn(torch.autograd.Function):
                     raise N.NativeError('asr_lstm_backward_dgbf_h failed (rc=%d): %s' % (
                         rc, N.lib().asr_last_error().decode(errors='replace')))
                 done = rc == 0
+                if done and split is not None:
+                    split[1][1] += split[2]          # the arrivals this launch adds
+                    split = split + (split[1][1], split_pre)
+                else:
+                    split = None
                 if not done:
                     a32 = torch.empty(B, T, 8 * H, dtype=torch.float32, device=dev)
                     N.call('asr_lstm_unpack_act_h', N.ptr(act), B, T, H, N.ptr(a32),
@@ -1302,6 +1327,23 @@ class BLSTMLayerFn(torch.autograd.Function):
         _join_side_wgrads(dev)
         notify_grad_event('recurrence')
         dg_op = dg_bf if dg_bf is not None else act
+        split_done = None
+        if split is not None:
+            t0, (ctr, _), _, target, pre = split
+            side = _wgrad_side_stream(dev, B, H)[0]
+            side.wait_event(pre)         # not the recurrence itself: the gate waits on its progress
+            with torch.cuda.stream(side):
+                N.call('asr_lstm_progress_gate', N.ptr(ctr), target, N.stream_handle(dev))
+                N.call('asr_gemm_set_nosplit', 1)     # per output element: one launch's sum
+                try:
+                    run_gemm([_dx_rows_problem(dg_op, w_op, dx_split, ctx, B, T, T_src, H, Din,
+                                               Dp, Dsrc, perm, t_mul, t_add, t0, T - t0)], dev)
+                finally:
+                    N.call('asr_gemm_set_nosplit', 0)
+                split_done = torch.cuda.Event()
+                split_done.record(side)
+            for tt in (dg_op, w_op, dx_split, ctr) + ((perm,) if perm is not None else ()):
+                tt.record_stream(side)
         # X as the dW_ih operand: the bf16 copy is already gathered (identity map)
         if cd == BF16:
             x_map = rowmap(Dp)
@@ -1355,7 +1397,21 @@ class BLSTMLayerFn(torch.autograd.Function):
                 torch.autograd.Variable._execution_engine.queue_callback(
                     lambda: _join_side_wgrads(dev, notify=False))
             _side_pending.append((side, gbufs, main))
-        if ctx.needs_input_grad[0] and not pipelined:
+        if split_done is not None:
+            # the outer rows t in [0, T/4) and [3T/4, T) on the compute stream, then
+            # the side stream's middle rows joined
+            t0 = split[0]
+            N.call('asr_gemm_set_nosplit', 1)
+            try:
+                run_gemm([_dx_rows_problem(dg_op, w_op, dx_split, ctx, B, T, T_src, H, Din, Dp,
+                                           Dsrc, perm, t_mul, t_add, 0, t0),
+                          _dx_rows_problem(dg_op, w_op, dx_split, ctx, B, T, T_src, H, Din, Dp,
+                                           Dsrc, perm, t_mul, t_add, T - t0, T)], dev)
+            finally:
+                N.call('asr_gemm_set_nosplit', 0)
+            torch.cuda.current_stream(dev).wait_event(split_done)
+            dx = dx_split
+        elif ctx.needs_input_grad[0] and not pipelined:
             # dX [BT, Din] = dG [BT, 8H] W_ih [8H, Din], scattered back through the input map
             if perm is None and t_mul == 1 and t_add == 0 and T == T_src and Din == Dsrc:
                 dx = torch.empty(B, T_src, Dsrc, dtype=torch.float32, device=dev)
@@ -1369,6 +1425,19 @@ class BLSTMLayerFn(torch.autograd.Function):
                              c_map, BT, Din, 8 * H, drop=ctx.drop)
             run_gemm([p], dev)
         return (dx,) + (None,) * (14 + ctx.n_graph)
+
+
+def _dx_rows_problem(dg_op, w_op, dx, ctx, B, T, T_src, H, Din, Dp, Dsrc, perm, t_mul, t_add,
+                     ta, tb):
+    """dX rows (b, t) for t in [ta, tb) of every utterance: dG [B, T, 8H] W_ih
+    [8H, Din], written through the layer's input map (the dropout mask by dX's
+    element offsets, as the whole-product form)."""
+    n = tb - ta
+    a_map = rowmap(8 * H, stride_b=T * 8 * H, rows_per_b=n, t_add=ta)
+    c_map = rowmap(Dsrc, stride_b=T_src * Dsrc, rows_per_b=n, t_mul=t_mul, t_add=t_add + ta * t_mul,
+                   t_limit=T_src, perm=perm)
+    return gemm_problem(operand(dg_op, 0, a_map), operand(w_op, 1, rowmap(Dp)), dx, c_map,
+                        B * n, Din, 8 * H, drop=ctx.drop)
 
 
 class BGRULayerFn(torch.autograd.Function):
@@ -1639,6 +1708,28 @@ def _wgrad_side_stream(dev, B, H):
             ent = torch.cuda.Stream(device=dev)
         _side_streams[key] = ent
     return ent, mode == '2', mode != '1'
+
+
+_progress = {}   # device index -> [uint64 counter (device), running total of arrivals]
+
+
+def _progress_counter(dev):
+    ent = _progress.get(dev.index)
+    if ent is None:
+        ent = _progress[dev.index] = [torch.zeros(1, dtype=torch.int64, device=dev), 0]
+    return ent
+
+
+def _dx_split_ok(ctx, B, T, dev, mode):
+    """Split input gradient (round 6, ASR_DX_SPLIT=0 turns it off): the
+    backward recurrence reports when the gate gradients of the middle rows t in
+    [T/4, 3T/4) are final (processing step 3T/4 - 1 of both directions), and
+    their share of dX = dG W_ih runs on the weight-gradient side stream beside
+    the last quarter of that recurrence, on the CUs it leaves free (mode 3);
+    the outer rows follow on the compute stream.  Needs the packed-activation
+    tagged-granule backward (the one that reports progress)."""
+    return (os.environ.get('ASR_DX_SPLIT', '1') != '0' and mode == '3' and T >= 64
+            and compute_dtype() == BF16 and ctx.needs_input_grad[0])
 
 
 DX_CHUNK = int(os.environ.get('ASR_DX_CHUNK', '64'))   # processing steps per pipelined dX chunk

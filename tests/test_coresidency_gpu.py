@@ -221,3 +221,47 @@ def test_held_cus_beside_recurrence_bitwise_or_visible_skip(hold_ms, cuda_dev):
         assert int(native_ops.recurrence_status(cuda_dev).max()) == 0
     finally:
         native_ops.set_compute_dtype('fp32')
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('H,L,T,sub,drop', [(512, 5, 240, [], 0.0),
+                                            (320, 4, 400, [False, True, True, False], 0.2)])
+def test_split_input_gradient_bitwise_equals_whole(H, L, T, sub, drop, cuda_dev):
+    """The split input gradient (round 6, native_ops._dx_split_ok): the middle
+    rows t in [T/4, 3T/4) of dX = dG W_ih computed on the side stream beside
+    the last quarter of the backward recurrence (gated on the progress the
+    recurrence publishes at processing step 3T/4 - 1), the outer rows after it
+    -- every gradient bitwise equal to the whole product (ASR_DX_SPLIT=0),
+    at the 5x512 shape and at a 4x320 encoder with pyramidal subsampling and
+    encoder dropout (the input maps and the dX epilogue's dropout mask), and
+    the split path actually ran (its progress counter advanced)."""
+    from pytorch_end2end_speech_recognition_amd import native_ops
+    native_ops.set_compute_dtype('bf16')
+    try:
+        kw = dict(_kw(H, L), subsample_list=sub, dropout_encoder=drop)
+        torch.manual_seed(1623)
+        sd = {k: v.clone() for k, v in _build(kw).state_dict().items()}
+        batch = _batch(T=T)
+        out = {}
+        for flag in ('0', '1'):
+            before = native_ops._progress_counter(cuda_dev)[1]
+            os.environ['ASR_DX_SPLIT'] = flag
+            try:
+                m = _build(kw)
+                m.load_state_dict(sd)
+                m.set_cuda()
+                m.zero_grad()
+                native_ops.manual_seed(7)
+                native_ops.recurrence_status(cuda_dev)
+                loss = m(batch['xs'], batch['ys'], batch['x_lens'], batch['y_lens'])
+                loss.backward()
+                torch.cuda.synchronize()
+                assert int(native_ops.recurrence_status(cuda_dev).max()) == 0
+                out[flag] = (loss.item(), m._flat_grad.clone())
+            finally:
+                os.environ.pop('ASR_DX_SPLIT', None)
+            ran = native_ops._progress_counter(cuda_dev)[1] - before
+            assert (ran > 0) == (flag == '1'), (flag, ran)
+        _equal(out['0'], out['1'], 'split dX')
+    finally:
+        native_ops.set_compute_dtype('fp32')
