@@ -936,6 +936,12 @@ int asr_lstm_set_dy_flags(const int* flags, int c0, int epoch);
 int asr_lstm_set_bwd_progress(unsigned long long* counter, int q);
 long long asr_lstm_bwd_progress_arrivals(int B, int H);
 int asr_lstm_progress_gate(const unsigned long long* counter, long long target, void* stream);
+/* Per-step workspace arena (round 6): the workspace handed to the next
+ * tagged-granule launch from this host thread is already zero (on = 1), so
+ * the launch skips its own memset.  Consumed by that launch; reset it after
+ * the call.  Replaces asr_lstm_workspace_bytes' "zeroed before every launch"
+ * with one fill per training step (native_ops.rec_arena_begin). */
+int asr_lstm_ws_prezeroed(int on);
 /* Stream-ordered: flags[k] = epoch after the work enqueued before it. */
 int asr_lstm_dy_signal(int* flags, int k, int epoch, void* stream);
 /* Diagnostics only (tools/cores_locate.py): backward recurrence launches

@@ -716,6 +716,9 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
 
   if (wave < NSW) {
     // ------------------------------ sweeper (as lstm_fwd_xg) ------------------
+#ifdef ASR_XG_SWEEP_PRIO   // A/B build: the sweepers' MFMAs ahead of the producers'
+    __builtin_amdgcn_s_setprio(ASR_XG_SWEEP_PRIO);
+#endif
     const int kq = lane >> 4, ln = lane & 15;
     const bool sweeper = ln < R;
     bf16x8 wf[KSW][4];
@@ -1626,6 +1629,19 @@ void xg_trace_setup(hipStream_t s);
 
 constexpr size_t XG_HDR = 256;  // abort word + placement registry, zeroed with the granules
 
+// The caller's workspace is already zero (a per-step arena cleared by one fill
+// for every layer pass, native_ops.rec_arena_begin): the next launch skips its
+// own memset.  Thread-local like the other per-call settings.
+thread_local int g_ws_zeroed = 0;
+
+hipError_t xg_ws_clear(void* ws, size_t n, hipStream_t s) {
+  if (g_ws_zeroed) {
+    g_ws_zeroed = 0;
+    return hipSuccess;
+  }
+  return hipMemsetAsync(ws, 0, n, s);
+}
+
 unsigned xg_next_epoch() {
   static unsigned e = 0;
   e = (e + 1) & 0xFFFu;
@@ -1727,7 +1743,7 @@ int lstm_fwd_xg32_launch(int B, int T, int H, const int32_t* lens, const float* 
   do {                                                                                           \
     if (!xg_fits(lstm_fwd_xg<RR, NL, 4, true, XV>, 256 + RR * XV, XG_PIN_FWD)) return 0;          \
     if (dry) return 1;                                                                           \
-    if (hipMemsetAsync(ws, 0, lstm_xg32_fwd_bytes(B, H), s) != hipSuccess) return -1;            \
+    if (xg_ws_clear(ws, lstm_xg32_fwd_bytes(B, H), s) != hipSuccess) return -1;                  \
     xg_trace_setup(s);                                                                           \
     hipLaunchKernelGGL((lstm_fwd_xg<RR, NL, 4, true, XV>), dim3(grid), dim3(256 + RR * XV),      \
                        XG_PIN_FWD, s, B, T, H, lens, whh_f, whh_r, gx_act, y, cst, g, hdr,       \
@@ -1776,7 +1792,7 @@ int lstm_bwd_xg32_launch(int B, int T, int H, const int32_t* lens, const float* 
   do {                                                                                           \
     if (!xg_fits(lstm_bwd_xg<RR, M, false, XV, true>, 256 + RR * XV + 256, pin)) return 0;       \
     if (dry) return 1;                                                                           \
-    if (hipMemsetAsync(ws, 0, lstm_xg32_bwd_bytes(B, H), s) != hipSuccess) return -1;            \
+    if (xg_ws_clear(ws, lstm_xg32_bwd_bytes(B, H), s) != hipSuccess) return -1;                  \
     xg_trace_setup(s);                                                                           \
     hipLaunchKernelGGL((lstm_bwd_xg<RR, M, false, XV, true>), dim3(grid),                        \
                        dim3(256 + RR * XV + 256), pin, s, B, T, H, lens, whh_f, whh_r, dy,      \
@@ -1826,7 +1842,7 @@ int lstm_fwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* wh
   do {                                                                                          \
     if (!xg_fits(lstm_fwd_xg<RR, KS, NS>, 64 * NS + RR * XU, PIN)) return 0;                     \
     if (dry) return 1;                                                                          \
-    if (hipMemsetAsync(ws, 0, lstm_xg_fwd_bytes(B, H), s) != hipSuccess) return -1;             \
+    if (xg_ws_clear(ws, lstm_xg_fwd_bytes(B, H), s) != hipSuccess) return -1;                   \
     xg_trace_setup(s);                                                                          \
     hipLaunchKernelGGL((lstm_fwd_xg<RR, KS, NS>), dim3(grid), dim3(64 * NS + RR * XU), PIN, s,   \
                        B, T, H, lens, whh_f, whh_r, gx_act, y, cst, g, hdr, ybf, ep, al);        \
@@ -1880,7 +1896,7 @@ int lstm_bwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* wh
       return 0;                                                                                 \
     }                                                                                           \
     if (dry) return 1;                                                                          \
-    if (hipMemsetAsync(ws, 0, lstm_xg_bwd_bytes(B, H), s) != hipSuccess) return -1;             \
+    if (xg_ws_clear(ws, lstm_xg_bwd_bytes(B, H), s) != hipSuccess) return -1;                   \
     xg_trace_setup(s);                                                                          \
     hipLaunchKernelGGL((lstm_bwd_xg<RR, M, AHV, XBV>), dim3(grid), dim3(256 + (RR + 16) * XBV),   \
                        pin, s,                                                                  \
@@ -1964,7 +1980,7 @@ int lstm_fwd_xgx_launch(int B, int T, int H, const int32_t* lens, const float* w
     const size_t pin = fa.sharedSizeBytes >= 84 * 1024 ? 0 : 84 * 1024 - fa.sharedSizeBytes;   \
     if (!xg_fits(kfn, threads, pin)) return 0;                                                  \
     if (dry) return 1;                                                                          \
-    if (hipMemsetAsync(ws, 0, lstm_xg_fwd_bytes(B, H), s) != hipSuccess) return -1;             \
+    if (xg_ws_clear(ws, lstm_xg_fwd_bytes(B, H), s) != hipSuccess) return -1;                   \
     xg_trace_setup(s);                                                                          \
     hipLaunchKernelGGL(kfn, dim3(grid), dim3(threads), pin, s, B, T, H, lens, whh_f, whh_r, x,  \
                        Din, wih, b_ih, b_hh, act, y, cst, g, hdr, ybf, al, late, defer,          \
@@ -2101,6 +2117,14 @@ extern "C" int asr_lstm_dy_signal(int* flags, int k, int epoch, void* stream) {
 // to *counter per cell wave once the gate gradients of processing steps <= q
 // are stored and released; counter NULL: off.  Stream-ordered launches only
 // ever add, so a reader waits for the running total (asr_lstm_progress_gate).
+// The workspace of the next tagged-granule launch on this thread is already
+// zero (on: 1): it skips its memset.  Consumed by that launch; callers reset
+// it after the call (a call that took another path leaves it set).
+extern "C" int asr_lstm_ws_prezeroed(int on) {
+  asr::g_ws_zeroed = on ? 1 : 0;
+  return ASR_OK;
+}
+
 extern "C" int asr_lstm_set_bwd_progress(unsigned long long* counter, int q) {
   ASR_REQUIRE(!counter || q >= 0, ASR_ERR_ARG, "bwd progress: q %d", q);
   asr::g_prog_ctr = counter;

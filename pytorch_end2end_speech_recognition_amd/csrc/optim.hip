@@ -71,9 +71,16 @@ __global__ void optim_step_kernel(float* __restrict__ p, const float* __restrict
                                   uint16_t* __restrict__ shadow, const int* __restrict__ guard) {
   // guard: the step's recurrence status words (asr_lstm_status_gather); a
   // bounded spin that gave up invalidated the gradients -> no update at all
-  if (guard && (guard[0] | guard[1])) return;
-  const float coef = clip_coef(sqnorm, a.max_norm);
+  // (the bf16 shadow is still rewritten from the unchanged parameters, so it
+  // matches them after every step, skipped or not)
   const long long stride = (long long)gridDim.x * blockDim.x;
+  if (guard && (guard[0] | guard[1])) {
+    if (shadow)
+      for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        shadow[i] = f2bf(p[i]);
+    return;
+  }
+  const float coef = clip_coef(sqnorm, a.max_norm);
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     float w = p[i];
     float gr = g[i] * coef + a.weight_decay * w;

@@ -22,6 +22,7 @@ import torch
 import torch.nn as nn
 
 from ... import _native as N
+from ... import native_ops as ops
 
 logger = logging.getLogger('training')
 
@@ -397,10 +398,16 @@ class FlatOptimizer(torch.optim.Optimizer):
         sq = self.grad_norm_sq() if max_norm and max_norm > 0 else None
         N.require_device(p)
         b1, b2 = g['betas']
+        # bf16 mode: the kernel also writes the bf16 shadow the next forward's
+        # BLSTM layers stage W_ih from (native_ops.param_shadow)
+        sh = ops.param_shadow(p)
         N.call('asr_optim_step_guarded', OPTIMIZER_KINDS[self.kind], N.ptr(p), N.ptr(gr),
                N.ptr(self.m), N.ptr(self.v), p.numel(), float(g['lr']), float(b1), float(b2),
                float(g['eps']), float(g['weight_decay']), self._step, float(g['momentum']), 0.0,
-               N.ptr(sq), float(max_norm or 0.0), None, N.ptr(guard), N.stream_handle(p.device))
+               N.ptr(sq), float(max_norm or 0.0), N.ptr(sh.buf) if sh is not None else None,
+               N.ptr(guard), N.stream_handle(p.device))
+        if sh is not None:
+            ops.param_shadow_written(sh, p, self.model.parameters())
         return loss
 
     def clip_and_step(self, max_norm, guard=None):

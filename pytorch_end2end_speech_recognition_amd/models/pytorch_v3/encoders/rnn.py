@@ -180,9 +180,18 @@ class RNNEncoder(nn.Module):
         res_outputs = []
         pending = None   # (p, seed): this layer's dropout, fused into the next layer's staging
         self.pending_output_drop = None
+        lens_d, lens_key = None, None
+        if self.rnn_type != 'gru':
+            # one fill for the recurrence workspaces of every layer's forward and
+            # backward pass (instead of a memset launch before each)
+            ops.rec_arena_begin(dev, int(h.shape[0]), self.num_units, 2 * self.num_layers)
         for l in range(self.num_layers):
             (w_ih, w_hh, b_ih, b_hh), gbufs = self._layer_tensors(l)
-            lens_d = torch.from_numpy(lens.astype(np.int32)).to(dev, non_blocking=True)
+            # one H2D copy per distinct length vector (they change only where a
+            # layer subsamples), not one per layer on the compute stream
+            if lens_key is None or not np.array_equal(lens_key, lens):
+                lens_key = lens.copy()
+                lens_d = torch.from_numpy(lens.astype(np.int32)).to(dev, non_blocking=True)
             graph = tuple(p for pair in self._layer_params(l) for p in pair)
             if self.rnn_type == 'gru':
                 if pending is not None:

@@ -10,6 +10,7 @@ the Functions therefore return ``None`` for weights.
 """
 import ctypes
 import os
+import weakref
 
 import numpy as np
 import torch
@@ -35,6 +36,70 @@ def compute_dtype():
 
 def _ws(nbytes, device):
     return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
+
+
+# ---------------------------------------------------------------------------
+# Per-step recurrence workspace arena.  Every tagged-granule launch needs its
+# granule workspace zero (lstm_xg.hip); instead of one memset launch before
+# each of the 2 x L layer passes of a step, the encoder forward clears one
+# arena with a slot per pass (rec_arena_begin), each BLSTM forward takes a
+# slot for itself and reserves one for its backward, and those launches skip
+# their memset (asr_lstm_ws_prezeroed).  A slot is handed out once per
+# generation; a backward whose reservation is from an older generation (the
+# arena was cleared again by another forward since) takes a private workspace
+# and the launch's own memset.
+# ---------------------------------------------------------------------------
+_arena = {'buf': None, 'gen': 0, 'off': 0, 'slot': 0}
+
+
+def rec_arena_begin(dev, B, H, passes):
+    """Clear the arena for `passes` recurrence launches of [B, *, H] (one fill
+    on the current stream); ASR_REC_ARENA=0: off."""
+    if os.environ.get('ASR_REC_ARENA', '1') == '0':
+        _arena['slot'] = 0
+        return
+    cd = compute_dtype()
+    nb = max(N.query('asr_lstm_workspace_bytes', B, H, cd, k) for k in (0, 1, 2))
+    slot = (int(nb) + 255) // 256 * 256
+    need = slot * int(passes)
+    buf = _arena['buf']
+    if buf is None or buf.device != dev or buf.numel() < need:
+        buf = torch.empty(need, dtype=torch.uint8, device=dev)
+    buf[:need].zero_()
+    _arena.update(buf=buf, gen=_arena['gen'] + 1, off=0, slot=slot)
+
+
+def _arena_take(nbytes, dev):
+    """(zeroed slot tensor, generation) from the current arena, or None."""
+    a = _arena
+    if not a['slot'] or a['buf'] is None or a['buf'].device != dev or nbytes > a['slot']:
+        return None
+    if a['off'] + a['slot'] > a['buf'].numel():
+        return None
+    t = a['buf'][a['off']:a['off'] + a['slot']]
+    a['off'] += a['slot']
+    return t, a['gen']
+
+
+def _arena_valid(res):
+    return res is not None and res[1] == _arena['gen']
+
+
+class _prezeroed:
+    """Tell the recurrence launch inside the block that its workspace is
+    already zero (asr_lstm_ws_prezeroed), and clear the setting after it."""
+
+    def __init__(self, on):
+        self.on = bool(on)
+
+    def __enter__(self):
+        if self.on:
+            N.call('asr_lstm_ws_prezeroed', 1)
+
+    def __exit__(self, *exc):
+        if self.on:
+            N.call('asr_lstm_ws_prezeroed', 0)
+        return False
 
 
 # Gradient-ready notifications for the data-parallel bucketed all-reduce
@@ -171,6 +236,82 @@ def _staged(t, rows, cols, ld=None):
     N.call('asr_convert_rows_bf16_ld', N.ptr(t), rowmap(cols), int(rows), int(cols), int(ld),
            N.ptr(out), N.stream_handle(t.device))
     return out
+
+
+# ---------------------------------------------------------------------------
+# bf16 parameter shadow.  The fused optimizer step (optim.hip) rounds every
+# updated parameter to bf16 beside its f32 write, into one shadow of the flat
+# parameter buffer, so the next forward's BLSTM layers read their staged W_ih
+# from it instead of converting it again (one pass over 8H x Din f32 per
+# layer).  The shadow is trusted only while nothing else wrote the parameters
+# since: the flat buffer's version (writes through flat views) and every
+# parameter's own version (torch.optim, load_state_dict, in-place init) must be
+# the ones recorded at the optimizer step.  ASR_PARAM_SHADOW=0 turns it off.
+# ---------------------------------------------------------------------------
+_shadows = {}   # id(flat param tensor) -> _ParamShadow (tensors compare elementwise)
+SHADOW_STATS = {'hits': 0}               # BLSTM layer forwards that read the shadow
+
+
+class _ParamShadow:
+    __slots__ = ('flat', 'buf', 'flat_version', 'param_versions')
+
+    def __init__(self, flat, buf):
+        self.flat = weakref.ref(flat)
+        self.buf = buf
+        self.flat_version = None
+        self.param_versions = None
+
+
+def param_shadow(flat):
+    """The bf16 shadow the optimizer step over `flat` should write, or None
+    (fp32 mode, or switched off)."""
+    if compute_dtype() != BF16 or os.environ.get('ASR_PARAM_SHADOW', '1') == '0':
+        return None
+    sh = _shadows.get(id(flat))
+    if sh is None or sh.flat() is not flat or sh.buf.device != flat.device:
+        for k in [k for k, v in _shadows.items() if v.flat() is None]:
+            del _shadows[k]
+        sh = _ParamShadow(flat, torch.empty(flat.numel(), dtype=torch.bfloat16,
+                                            device=flat.device))
+        _shadows[id(flat)] = sh
+    return sh
+
+
+def param_shadow_written(sh, flat, params):
+    """Record the versions the shadow matches (call right after enqueueing the
+    optimizer step that writes it; later writes are ordered after it and bump
+    a version)."""
+    sh.flat_version = flat._version
+    sh.param_versions = {id(p): p._version for p in params}
+
+
+def _shadow_rows(w, params):
+    """bf16 view of the shadow's copy of `w` (a dense view of a flat parameter
+    buffer, spanning `params`), or None when there is no current shadow."""
+    flat = w._base
+    if flat is None or w.dtype != torch.float32 or not w.is_contiguous():
+        return None
+    sh = _shadows.get(id(flat))
+    if (sh is None or sh.flat() is not flat or sh.param_versions is None or
+            flat._version != sh.flat_version):
+        return None
+    pv = sh.param_versions
+    if not params or any(pv.get(id(p)) != p._version for p in params):
+        return None
+    off = w.storage_offset() - flat.storage_offset()
+    if off < 0 or off + w.numel() > flat.numel():
+        return None
+    return sh.buf[off:off + w.numel()].view(w.shape)
+
+
+def _wih_bf16(w_ih, params, H, Din):
+    """Staged bf16 W_ih [8H, Din] of a BLSTM layer: the optimizer's shadow
+    when current, else one conversion pass."""
+    w = _shadow_rows(w_ih, params)
+    if w is None:
+        return convert_rows_bf16(w_ih, rowmap(Din), 8 * H, Din)
+    SHADOW_STATS['hits'] += 1
+    return w
 
 
 def _linear_stages(M, K, Nout):
@@ -1131,7 +1272,7 @@ class BLSTMLayerFn(torch.autograd.Function):
         Dp = Din        # packed fp16 activations [B, T, 2, H, 4] (fused bf16 path)
         if twin is not None:
             x_op = twin.view(B * T, Din)
-            w_op = convert_rows_bf16(w_ih, rowmap(Din), 8 * H, Din)   # [8H, Din]
+            w_op = _wih_bf16(w_ih, graph_params, H, Din)           # [8H, Din]
             y_bf = torch.empty(B, T, 2 * H, dtype=torch.bfloat16, device=dev)
         elif cd == BF16:
             if Din % 8 and not fused_drop:
@@ -1147,14 +1288,18 @@ class BLSTMLayerFn(torch.autograd.Function):
             else:
                 x_op = convert_rows_bf16(x_src, a_map, B * T, Din,    # [B*T, Din]
                                          drop=drop if fused_drop else None)
-                w_op = convert_rows_bf16(w_ih, rowmap(Din), 8 * H, Din)   # [8H, Din]
+                w_op = _wih_bf16(w_ih, graph_params, H, Din)           # [8H, Din]
             y_bf = torch.empty(B, T, 2 * H, dtype=torch.bfloat16, device=dev)
         else:
             x_op, w_op, y_bf = x_src, w_ih, None
         y = torch.empty(B, T, 2 * H, dtype=torch.float32, device=dev)
         cst = torch.empty(B, T, 2 * H, dtype=torch.float32, device=dev)
         nb = N.query('asr_lstm_workspace_bytes', B, H, cd, 0)
-        ws = _ws(nb, dev)
+        slot = _arena_take(nb, dev)         # zeroed by rec_arena_begin
+        ws = slot[0] if slot is not None else _ws(nb, dev)
+        pz = slot is not None
+        # the backward's slot, reserved now so the arena's one fill covers it
+        ctx.bws = _arena_take(N.query('asr_lstm_workspace_bytes', B, H, cd, 2), dev) if pz else None
         whh_r = w_hh.data_ptr() + 4 * H * H * 4
         y_f32, out_drop = out_spec
         handoff = None     # (bf16 tensor the next layer stages from, its dropout)
@@ -1173,9 +1318,10 @@ class BLSTMLayerFn(torch.autograd.Function):
                 y_d = (torch.empty(B, T, 2 * H, dtype=torch.bfloat16, device=dev)
                        if out_drop is not None else None)
                 p, seed = out_drop if out_drop is not None else (0.0, 0)
-                rc = N.query(fn, *args, N.ptr(gx), None, N.ptr(cst), N.ptr(y_bf),
-                             N.ptr(y_d) if y_d is not None else None, ctypes.c_float(p),
-                             ctypes.c_ulonglong(seed), N.ptr(ws), nb, N.stream_handle(dev))
+                with _prezeroed(pz):
+                    rc = N.query(fn, *args, N.ptr(gx), None, N.ptr(cst), N.ptr(y_bf),
+                                 N.ptr(y_d) if y_d is not None else None, ctypes.c_float(p),
+                                 ctypes.c_ulonglong(seed), N.ptr(ws), nb, N.stream_handle(dev))
                 if rc == 0:
                     handoff = (y_d if y_d is not None else y_bf, out_drop)
             else:
@@ -1185,8 +1331,9 @@ class BLSTMLayerFn(torch.autograd.Function):
                 else:
                     gx = torch.empty(B, T, 8 * H, dtype=torch.float32, device=dev)
                     fn = 'asr_lstm_forward_x'
-                rc = N.query(fn, *args, N.ptr(gx), N.ptr(y), N.ptr(cst), N.ptr(y_bf), N.ptr(ws),
-                             nb, N.stream_handle(dev))
+                with _prezeroed(pz):
+                    rc = N.query(fn, *args, N.ptr(gx), N.ptr(y), N.ptr(cst), N.ptr(y_bf),
+                                 N.ptr(ws), nb, N.stream_handle(dev))
             if rc not in (0, N.ASR_ERR_UNSUPPORTED):
                 raise N.NativeError('%s failed (rc=%d): %s' % (
                     fn, rc, N.lib().asr_last_error().decode(errors='replace')))
@@ -1201,9 +1348,10 @@ class BLSTMLayerFn(torch.autograd.Function):
                 run_gemm([gemm_problem(operand(x_src, 0, a_map), operand(w_ih, 0, rowmap(Din)), gx,
                                        rowmap(8 * H), B * T, 8 * H, Din, bias=b_ih, bias2=b_hh)],
                          dev)
-            N.call('asr_lstm_forward', N.ptr(gx), N.ptr(w_hh), ctypes.c_void_p(whh_r), F32,
-                   N.ptr(lens), B, T, H, cd, N.ptr(y), N.ptr(cst), N.ptr(y_bf), N.ptr(ws), nb,
-                   N.stream_handle(dev))
+            with _prezeroed(pz):
+                N.call('asr_lstm_forward', N.ptr(gx), N.ptr(w_hh), ctypes.c_void_p(whh_r), F32,
+                       N.ptr(lens), B, T, H, cd, N.ptr(y), N.ptr(cst), N.ptr(y_bf), N.ptr(ws),
+                       nb, N.stream_handle(dev))
         ctx.save_for_backward(x_op, w_op, lens, w_hh, b_ih, b_hh, gx, cst,
                               y_bf if y_bf is not None else y)
         ctx.meta = (T, perm, t_mul, t_add, gbufs, cd, (B, T_src, Dsrc, Din, Dp), w_ih)
@@ -1266,7 +1414,9 @@ class BLSTMLayerFn(torch.autograd.Function):
                 # packed fp16 activations of asr_lstm_forward_xh: the tagged-granule
                 # backward reads them directly; otherwise they are unpacked to f32
                 nb = N.query('asr_lstm_workspace_bytes', B, H, cd, 2)
-                ws = _ws(nb, dev)
+                res, ctx.bws = ctx.bws, None      # a reserved slot serves one backward
+                pz = _arena_valid(res) and nb <= res[0].numel()
+                ws = res[0] if pz else _ws(nb, dev)
                 if pipe is not None:
                     N.call('asr_lstm_set_dy_flags', N.ptr(pipe[0]), pipe[1], pipe[2])
                 if split is not None:
@@ -1276,10 +1426,11 @@ class BLSTMLayerFn(torch.autograd.Function):
                     split_pre = torch.cuda.Event()
                     split_pre.record(torch.cuda.current_stream(dev))
                 try:
-                    rc = N.query('asr_lstm_backward_dgbf_h', N.ptr(dy), N.ptr(w_hh),
-                                 ctypes.c_void_p(whh_r), F32, N.ptr(lens), B, T, H, cd, N.ptr(act),
-                                 N.ptr(cst), N.ptr(dg_bf), N.ptr(gbufs[2]), N.ptr(gbufs[3]),
-                                 N.ptr(ws), nb, N.stream_handle(dev))
+                    with _prezeroed(pz):
+                        rc = N.query('asr_lstm_backward_dgbf_h', N.ptr(dy), N.ptr(w_hh),
+                                     ctypes.c_void_p(whh_r), F32, N.ptr(lens), B, T, H, cd,
+                                     N.ptr(act), N.ptr(cst), N.ptr(dg_bf), N.ptr(gbufs[2]),
+                                     N.ptr(gbufs[3]), N.ptr(ws), nb, N.stream_handle(dev))
                 finally:
                     if split is not None:
                         N.call('asr_lstm_set_bwd_progress', None, 0)
