@@ -942,6 +942,9 @@ int asr_lstm_progress_gate(const unsigned long long* counter, long long target, 
  * the call.  Replaces asr_lstm_workspace_bytes' "zeroed before every launch"
  * with one fill per training step (native_ops.rec_arena_begin). */
 int asr_lstm_ws_prezeroed(int on);
+/* Leading bytes of such a workspace a tagged-granule launch of [B, *, H]
+ * zeroes (the arena clears only these). */
+size_t asr_lstm_ws_zero_bytes(int B, int H);
 /* Stream-ordered: flags[k] = epoch after the work enqueued before it. */
 int asr_lstm_dy_signal(int* flags, int k, int epoch, void* stream);
 /* Diagnostics only (tools/cores_locate.py): backward recurrence launches

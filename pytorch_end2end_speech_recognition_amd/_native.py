@@ -223,6 +223,7 @@ SIGNATURES = {
     'asr_ctc_last_path': (c_int, [c_vp]),
     'asr_lstm_set_bwd_progress': (c_int, [c_vp, c_int]),
     'asr_lstm_ws_prezeroed': (c_int, [c_int]),
+    'asr_lstm_ws_zero_bytes': (c_size, [c_int, c_int]),
     'asr_lstm_bwd_progress_arrivals': (c_ll, [c_int, c_int]),
     'asr_lstm_progress_gate': (c_int, [c_vp, c_ll, c_vp]),
     'asr_xg_trace_read': (c_ll, [c_vp]),

@@ -2125,6 +2125,15 @@ extern "C" int asr_lstm_ws_prezeroed(int on) {
   return ASR_OK;
 }
 
+// Leading bytes of a recurrence workspace that a tagged-granule launch of
+// [B, *, H] zeroes (header + granules; the rest of asr_lstm_workspace_bytes
+// belongs to the per-step kernels, which clear their own).
+extern "C" size_t asr_lstm_ws_zero_bytes(int B, int H) {
+  if (B <= 0 || H <= 0) return 0;
+  return std::max(std::max(asr::lstm_xg_fwd_bytes(B, H), asr::lstm_xg_bwd_bytes(B, H)),
+                  std::max(asr::lstm_xg32_fwd_bytes(B, H), asr::lstm_xg32_bwd_bytes(B, H)));
+}
+
 extern "C" int asr_lstm_set_bwd_progress(unsigned long long* counter, int q) {
   ASR_REQUIRE(!counter || q >= 0, ASR_ERR_ARG, "bwd progress: q %d", q);
   asr::g_prog_ctr = counter;

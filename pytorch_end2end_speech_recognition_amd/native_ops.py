@@ -65,7 +65,9 @@ def rec_arena_begin(dev, B, H, passes):
     buf = _arena['buf']
     if buf is None or buf.device != dev or buf.numel() < need:
         buf = torch.empty(need, dtype=torch.uint8, device=dev)
-    buf[:need].zero_()
+    # only each slot's leading bytes must be zero (one strided fill)
+    zb = min(int(N.query('asr_lstm_ws_zero_bytes', B, H)), slot)
+    buf[:need].view(int(passes), slot)[:, :zb].zero_()
     _arena.update(buf=buf, gen=_arena['gen'] + 1, off=0, slot=slot)
 
 
