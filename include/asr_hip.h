@@ -131,6 +131,9 @@ int asr_ctc_fwd_bwd(const float* acts, long long stride_t, long long stride_b, i
  * epilogue's partials; gradient: 0 f32 ctc_grad, 1 ctc_grad_bf16, 2 narrow
  * (V <= 256), 3 pipelined, 4 streamed}. */
 int asr_ctc_last_path(int* out2);
+/* Waves per direction of the last CTC forward's lattice (round 6): 1 = the
+ * one-wave ctc_lattice, 2 / 4 = ctc_lattice_w (ASR_CTC_LATTICE_W=1 forces 1). */
+int asr_ctc_last_lattice_waves(void);
 
 /* ---------------------------------------------------------------- GEMM
  * C(m,n) = alpha * sum_k A(m,k) B(n,k) + beta * C(m,n) + bias[n] + bias2[n]  (f32 C)

@@ -328,6 +328,8 @@ __device__ __forceinline__ void store_k(float* p, const float (&r)[K]) {
   }
 }
 
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
 // DPP wave shifts (GFX9 wave_shr:1 / wave_shl:1): lane i receives lane i-1 /
 // i+1; the lane without a source receives 0 (callers overwrite it).
 __device__ __forceinline__ float from_lower_lane(float x) {
@@ -559,6 +561,263 @@ __global__ void __launch_bounds__(128) ctc_lattice(int T, const int32_t* __restr
   }
 }
 
+// The lattice split over W waves (round 6): wave w owns states [w 64 KW,
+// (w+1) 64 KW), KW = K / W per lane, so a step costs each wave a W-th of the
+// transcendental and VALU work of the one-wave form -- which bounds it (one
+// wave issuing ~10 v_exp / v_log per lane per step at K = 4).  The recursion
+// only looks DOWN the state axis for alpha (s-1, s-2) and UP for beta (s+1,
+// s+2), so the waves form a one-way pipeline: after each step a wave posts its
+// two edge states (with the step number as a tag, one 16-B LDS record) and its
+// neighbour on the dependent side spins on that record before the same step --
+// no work-group barrier per step, the downstream waves simply run a step or two
+// behind.  The records live in a ring of 2 C steps; the per-chunk barrier of
+// the emission ring bounds any wave's lead to one chunk, so a record is never
+// overwritten before it is read.  Every alpha / beta value is computed by
+// the same arithmetic as in ctc_lattice (bitwise equal); log P sums the two
+// final states across lanes / waves in another grouping (last-bit changes).
+template <int K, int W>
+__global__ void __launch_bounds__(64 * (W + 1)) ctc_lattice_w(
+    int T, const int32_t* __restrict__ labels, const int32_t* __restrict__ label_lens,
+    const int32_t* __restrict__ act_lens, const int32_t* __restrict__ offs, int blank,
+    int zero_infinity, const float* __restrict__ emit, float* __restrict__ alpha,
+    float* __restrict__ beta, float* __restrict__ logp_out, float* __restrict__ costs) {
+  static_assert(K % W == 0, "states per lane split evenly over the waves");
+  constexpr int KW = K / W;
+  constexpr int Spad = 64 * K;
+  constexpr int C = K <= 4 ? 32 : (K == 8 ? 16 : 8);   // rows per chunk (ring 2 C Spad 4 B <= 64 KB)
+  constexpr int RB = 2 * C;                            // edge-record ring (steps)
+  __shared__ __attribute__((aligned(16))) float ring[2][C][Spad];
+  __shared__ __attribute__((aligned(16))) f32x4 edge[W][RB];   // {v1, v2, tag, -}
+  __shared__ float lpart[W];
+  const int b = blockIdx.x;
+  const bool is_beta = blockIdx.y == 1;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int Tb = min(act_lens[b], T);
+  const int L = min(label_lens[b], (Spad - 1) / 2);
+  const int S = 2 * L + 1;
+  const int32_t* lab = labels + offs[b];
+  const float NEG = neg_inf();
+
+  if (Tb <= 0) {
+    if (threadIdx.x == 0 && !is_beta) {
+      bool feas = (L == 0);
+      logp_out[b] = feas ? 0.f : NEG;
+      costs[b] = feas ? 0.f : (zero_infinity ? 0.f : __builtin_huge_valf());
+    }
+    return;
+  }
+  const int N = Tb - 1;
+  const int nch = (N + C - 1) / C;
+  auto row_of = [&](int n) {
+    n = min(n, N - 1);
+    return is_beta ? Tb - 2 - n : 1 + n;
+  };
+  for (int e = threadIdx.x; e < W * RB; e += blockDim.x)
+    (&edge[0][0])[e] = f32x4{0.f, 0.f, __int_as_float(-1), 0.f};
+  __syncthreads();   // no record is posted before every tag reads -1
+
+  if (wave == W) {
+    // ---------------- loader (whole rows, as ctc_lattice) ----------------
+    const float* E = emit + (size_t)b * T * Spad + lane * K;
+    float r[C][K];
+    if (nch > 0) {
+#pragma unroll
+      for (int j = 0; j < C; ++j) load_k<K>(r[j], E + (size_t)row_of(j) * Spad);
+#pragma unroll
+      for (int j = 0; j < C; ++j) store_k<K>(&ring[0][j][lane * K], r[j]);
+      if (nch > 1) {
+#pragma unroll
+        for (int j = 0; j < C; ++j) load_k<K>(r[j], E + (size_t)row_of(C + j) * Spad);
+      }
+    }
+    __syncthreads();
+    for (int c = 0; c < nch; ++c) {
+      if (c + 1 < nch) {
+#pragma unroll
+        for (int j = 0; j < C; ++j) store_k<K>(&ring[(c + 1) & 1][j][lane * K], r[j]);
+        if (c + 2 < nch) {
+#pragma unroll
+          for (int j = 0; j < C; ++j)
+            load_k<K>(r[j], E + (size_t)row_of((c + 2) * C + j) * Spad);
+        }
+      }
+      lds_barrier();
+    }
+    lds_barrier();   // the lattice waves' log P reduction
+    return;
+  }
+
+  const int sb = wave * 64 * KW + lane * KW;   // this lane's first state
+  const float* E = emit + (size_t)b * T * Spad + sb;
+  bool valid[KW];
+#pragma unroll
+  for (int k = 0; k < KW; ++k) valid[k] = sb + k < S;
+  // the edge record of step n posted by wave v; spins until it is there
+  auto wait_edge = [&](int v, int n) {
+    const f32x4* p = &edge[v][n & (RB - 1)];
+    f32x4 rec;
+    for (unsigned spins = 0;; ++spins) {
+      rec = *reinterpret_cast<const volatile f32x4*>(p);
+      if (__float_as_int(rec[2]) == n || spins > (1u << 20)) break;   // (bounded: never hangs)
+      __builtin_amdgcn_s_sleep(0);
+    }
+    return rec;
+  };
+  auto post_edge = [&](int n, float v1, float v2, bool poster) {
+    if (poster) edge[wave][n & (RB - 1)] = f32x4{v1, v2, __int_as_float(n), 0.f};
+  };
+
+  if (!is_beta) {
+    // ---------------- alpha: wave w waits on wave w-1 ----------------
+    bool skip[KW];
+#pragma unroll
+    for (int k = 0; k < KW; ++k) {
+      const int s = sb + k;
+      skip[k] = (s & 1) && s >= 3 && s < S && lab[s >> 1] != lab[(s >> 1) - 1];
+    }
+    float* A = alpha + (size_t)b * T * Spad + sb;
+    float a[KW];
+    {
+      float e0[KW];
+      load_k<KW>(e0, E);
+#pragma unroll
+      for (int k = 0; k < KW; ++k) {
+        const int s = sb + k;
+        a[k] = (s < 2 && valid[k]) ? e0[k] : NEG;
+      }
+      store_k<KW>(A, a);
+    }
+    // edge: the two top states (lane 63; with KW = 1 the second from lane 62)
+    auto post_top = [&](int n) {
+      const float lo = KW >= 2 ? a[KW >= 2 ? KW - 2 : 0] : from_lower_lane(a[0]);
+      if (wave + 1 < W) post_edge(n, a[KW - 1], lo, lane == 63);
+    };
+    post_top(0);
+    __syncthreads();
+    for (int c = 0; c < nch; ++c) {
+      float ec[C][KW];
+#pragma unroll
+      for (int j = 0; j < C; ++j) load_k<KW>(ec[j], &ring[c & 1][j][sb]);
+#pragma unroll
+      for (int j = 0; j < C; ++j) {
+        const int n = c * C + j;
+        if (n < N) {
+          const float (&e)[KW] = ec[j];
+          float p1 = from_lower_lane(a[KW - 1]);
+          float p2 = (KW >= 2) ? from_lower_lane(a[KW >= 2 ? KW - 2 : 0]) : from_lower_lane(p1);
+          float e1 = NEG, e2 = NEG;   // states sb_wave - 1, - 2 at step n (row n)
+          if (wave > 0) {
+            const f32x4 r = wait_edge(wave - 1, n);
+            e1 = r[0];
+            e2 = r[1];
+          }
+          if (lane == 0) { p1 = e1; p2 = e2; }
+          if (KW == 1 && lane == 1) p2 = e1;
+          float nx[KW];
+#pragma unroll
+          for (int k = 0; k < KW; ++k) {
+            const float a1 = (k >= 1) ? a[k >= 1 ? k - 1 : 0] : p1;
+            const float a2 = (k >= 2) ? a[k >= 2 ? k - 2 : 0] : ((k == 1) ? p1 : p2);
+            const float v = ((KW % 2 == 0) && (k % 2 == 0) ? lse2_b2(a[k], a1)
+                                                            : lse3_b2(a[k], a1, skip[k] ? a2 : NEG)) +
+                            e[k];
+            nx[k] = valid[k] ? v : NEG;
+          }
+#pragma unroll
+          for (int k = 0; k < KW; ++k) a[k] = nx[k];
+          post_top(n + 1);
+          store_k<KW>(A + (size_t)(1 + n) * Spad, a);
+        }
+      }
+      lds_barrier();
+    }
+    float part = NEG;
+#pragma unroll
+    for (int k = 0; k < KW; ++k) {
+      const int s = sb + k;
+      if (s == S - 1 || s == S - 2) part = lse2_b2(part, a[k]);
+    }
+    float mx = wave_max(part);
+    float sm = (mx == NEG) ? 0.f : wave_sum(ex2(part - mx));
+    if (lane == 0) lpart[wave] = (mx == NEG) ? NEG : mx + lg2(sm);
+    lds_barrier();
+    if (wave == 0 && lane == 0) {
+      // the two final states lie in one wave or straddle two: combine in order
+      float logP = NEG;
+#pragma unroll
+      for (int v = 0; v < W; ++v) logP = lse2_b2(logP, lpart[v]);
+      logp_out[b] = logP;
+      costs[b] = (logP == NEG) ? (zero_infinity ? 0.f : __builtin_huge_valf()) : -logP * kLn2;
+    }
+    return;
+  }
+
+  // ---------------- beta: wave w waits on wave w+1 ----------------
+  bool skipf[KW];
+#pragma unroll
+  for (int k = 0; k < KW; ++k) {
+    const int s = sb + k;
+    skipf[k] = (s & 1) && s + 2 < S && lab[s >> 1] != lab[(s >> 1) + 1];
+  }
+  float* Bt = beta + (size_t)b * T * Spad + sb;
+  float be[KW];
+  {
+    float et[KW];
+    load_k<KW>(et, E + (size_t)(Tb - 1) * Spad);
+#pragma unroll
+    for (int k = 0; k < KW; ++k) {
+      const int s = sb + k;
+      be[k] = (valid[k] && (s == S - 1 || s == S - 2)) ? et[k] : NEG;
+    }
+    store_k<KW>(Bt + (size_t)(Tb - 1) * Spad, be);
+  }
+  // edge: the two bottom states (lane 0; with KW = 1 the second from lane 1)
+  auto post_bottom = [&](int n) {
+    const float hi = KW >= 2 ? be[KW >= 2 ? 1 : 0] : from_upper_lane(be[0]);
+    if (wave > 0) post_edge(n, be[0], hi, lane == 0);
+  };
+  post_bottom(0);
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
+    float ec[C][KW];
+#pragma unroll
+    for (int j = 0; j < C; ++j) load_k<KW>(ec[j], &ring[c & 1][j][sb]);
+#pragma unroll
+    for (int j = 0; j < C; ++j) {
+      const int n = c * C + j;
+      if (n < N) {
+        const float (&e)[KW] = ec[j];
+        float n1 = from_upper_lane(be[0]);
+        float n2 = (KW >= 2) ? from_upper_lane(be[KW >= 2 ? 1 : 0]) : from_upper_lane(n1);
+        float e1 = NEG, e2 = NEG;   // states sb_wave + 64 KW, + 1 at step n
+        if (wave + 1 < W) {
+          const f32x4 r = wait_edge(wave + 1, n);
+          e1 = r[0];
+          e2 = r[1];
+        }
+        if (lane == 63) { n1 = e1; n2 = e2; }
+        if (KW == 1 && lane == 62) n2 = e1;
+        float nx[KW];
+#pragma unroll
+        for (int k = 0; k < KW; ++k) {
+          const float b1 = (k < KW - 1) ? be[k < KW - 1 ? k + 1 : 0] : n1;
+          const float b2 = (k < KW - 2) ? be[k < KW - 2 ? k + 2 : 0] : ((k == KW - 2) ? n1 : n2);
+          const float v = ((KW % 2 == 0) && (k % 2 == 0) ? lse2_b2(be[k], b1)
+                                                          : lse3_b2(be[k], b1, skipf[k] ? b2 : NEG)) +
+                          e[k];
+          nx[k] = valid[k] ? v : NEG;
+        }
+#pragma unroll
+        for (int k = 0; k < KW; ++k) be[k] = nx[k];
+        post_bottom(n + 1);
+        store_k<KW>(Bt + (size_t)(Tb - 2 - n) * Spad, be);
+      }
+    }
+    lds_barrier();
+  }
+  lds_barrier();   // (pairs with the alpha side's log P barrier; the loader's last)
+}
+
 // grad = (softmax - occupancy) * scale, one row (b,t) per block.
 //   kTable (V <= 256): occupancies summed per class in a V-entry LDS table.
 //   otherwise, no V-sized table: (1) the S state occupancies go to LDS; (2) the
@@ -675,7 +934,6 @@ __global__ void __launch_bounds__(256) ctc_grad(
   }
 }
 
-typedef __attribute__((ext_vector_type(4))) float f32x4;
 template <int A>
 __device__ __forceinline__ void take8(const float (&v)[12], float (&o)[8]) {
 #pragma unroll
@@ -1505,8 +1763,9 @@ static int ctc_row_order() {
 // asr_ctc_last_path): {normaliser: 0 the emission pass over the logits, 1 the
 // head GEMM epilogue's (max, sum exp) partials; gradient: 0 f32 ctc_grad,
 // 1 ctc_grad_bf16, 2 ctc_grad_bf16_narrow, 3 ctc_grad_bf16_pipe,
-// 4 ctc_grad_bf16_stream}.
-static int g_ctc_last_path[2];
+// 4 ctc_grad_bf16_stream}; [2] (round 6, asr_ctc_last_lattice_waves): the
+// waves of the last forward's lattice (1: ctc_lattice, else ctc_lattice_w).
+static int g_ctc_last_path[3];
 
 extern "C" int asr_ctc_last_path(int* out2) {
   ASR_REQUIRE(out2, ASR_ERR_ARG, "ctc_last_path: null pointer");
@@ -1514,6 +1773,8 @@ extern "C" int asr_ctc_last_path(int* out2) {
   out2[1] = g_ctc_last_path[1];
   return ASR_OK;
 }
+
+extern "C" int asr_ctc_last_lattice_waves(void) { return g_ctc_last_path[2]; }
 
 static int ctc_forward_impl(const float* acts, long long stride_t, long long stride_b, int T,
                             int B, int V, const float* lse_part, int nslab,
@@ -1561,14 +1822,24 @@ static int ctc_forward_impl(const float* acts, long long stride_t, long long str
   hipLaunchKernelGGL(ctc_lattice<KK>, dim3(B, 2), dim3(128), 0, s, T, labels_flat, label_lens,  \
                      act_lens, ws.offs, blank, zero_infinity, ws.emit, ws.alpha, ws.beta,      \
                      ws.logp, costs)
+#define ASR_CTC_LATW(KK, WW)                                                                   \
+  hipLaunchKernelGGL((ctc_lattice_w<KK, WW>), dim3(B, 2), dim3(64 * (WW + 1)), 0, s, T,         \
+                     labels_flat, label_lens, act_lens, ws.offs, blank, zero_infinity, ws.emit,  \
+                     ws.alpha, ws.beta, ws.logp, costs)
+  // the lattice over several waves (ctc_lattice_w) from K = 2; ASR_CTC_LATTICE_W=1
+  // keeps the one-wave kernel (A/B)
+  const char* lw = getenv("ASR_CTC_LATTICE_W");
+  const bool multi = !(lw && atoi(lw) == 1);
+  g_ctc_last_path[2] = multi && K >= 2 ? (K >= 4 ? 4 : 2) : 1;
   switch (K) {
     case 1: ASR_CTC_LAT(1); break;
-    case 2: ASR_CTC_LAT(2); break;
-    case 4: ASR_CTC_LAT(4); break;
-    case 8: ASR_CTC_LAT(8); break;
-    case 16: ASR_CTC_LAT(16); break;
+    case 2: if (multi) ASR_CTC_LATW(2, 2); else ASR_CTC_LAT(2); break;
+    case 4: if (multi) ASR_CTC_LATW(4, 4); else ASR_CTC_LAT(4); break;
+    case 8: if (multi) ASR_CTC_LATW(8, 4); else ASR_CTC_LAT(8); break;
+    case 16: if (multi) ASR_CTC_LATW(16, 4); else ASR_CTC_LAT(16); break;
     default: set_error("ctc: unsupported K=%d", K); return ASR_ERR_UNSUPPORTED;
   }
+#undef ASR_CTC_LATW
 #undef ASR_CTC_LAT
   ASR_LAUNCH_CHECK();
   prof_end_launch(ASR_PROF_CTC_FWD, pslot, s);

@@ -272,6 +272,45 @@ def test_lattice_edge_cases_vs_oracle(K, Ls, cuda_dev):
     np.testing.assert_array_equal(grads, again[2])
 
 
+@pytest.mark.parametrize('K,Ls,W', [(2, [32, 40, 63], 2), (4, [64, 95, 127, 70], 4),
+                                    (4, [66, 125, 100, 60, 125, 93], 4),
+                                    (8, [128, 200, 255], 4), (16, [256, 400, 511], 4)])
+def test_lattice_waves_match_single_wave(K, Ls, W, cuda_dev, monkeypatch):
+    """The lattice split over W waves (ctc_lattice_w: per-step edge records
+    between the waves instead of one wave doing every state) against the
+    one-wave kernel (ASR_CTC_LATTICE_W=1): alpha / beta are the same
+    arithmetic, so the gradients (built from alpha + beta - log P) agree to
+    the last bit wherever log P does, and log P -- the two final states summed
+    in another lane / wave grouping -- within one f32 ulp.  Label lengths put
+    the final states inside one wave and across a wave boundary (64 KW
+    states per wave), with repeats, an empty label and a one-frame
+    utterance."""
+    from pytorch_end2end_speech_recognition_amd import _native as N
+    rng = np.random.RandomState(300 + K + len(Ls))
+    V = 40
+    B = len(Ls) + 1
+    label_lens = np.array(list(Ls) + [0])
+    T = int(max(2 * max(Ls) + 8, 48))
+    act_lens = np.array([T] + [int(rng.randint(2 * l + 2, T + 1)) for l in label_lens[1:-1]] + [1])
+    labels = np.concatenate([rng.randint(1, V, l) for l in label_lens]).astype(np.int32)
+    labels[1] = labels[2]
+    acts = (rng.randn(B, T, V) * 2).astype(np.float32)
+    monkeypatch.setenv('ASR_CTC_LATTICE_W', '1')
+    one = _run(acts, labels, label_lens, act_lens, cuda_dev)
+    assert N.lib().asr_ctc_last_lattice_waves() == 1
+    monkeypatch.delenv('ASR_CTC_LATTICE_W')
+    multi = _run(acts, labels, label_lens, act_lens, cuda_dev)
+    assert N.lib().asr_ctc_last_lattice_waves() == W
+    np.testing.assert_allclose(multi[1], one[1], rtol=3e-7, atol=0)
+    same_lp = multi[1] == one[1]
+    assert same_lp.sum() >= len(Ls) // 2, (multi[1], one[1])
+    for b in np.nonzero(same_lp)[0]:
+        np.testing.assert_array_equal(multi[2][b], one[2][b])
+    np.testing.assert_allclose(multi[2], one[2], rtol=1e-5, atol=1e-6)
+    c_ref, _ = ctc_ref.ctc_batch(acts, labels, label_lens, act_lens, time_major=False)
+    np.testing.assert_allclose(multi[1], c_ref, rtol=1e-4)
+
+
 @pytest.mark.parametrize('bias_blocks', ['0', '8'])
 def test_wide_head_gradient_passes_agree(bias_blocks, cuda_dev, monkeypatch):
     """The wide fused head's three gradient passes at V = 10001 with ragged
