@@ -1485,6 +1485,10 @@ class BLSTMLayerFn(torch.autograd.Function):
             t0, (ctr, _), _, target, pre = split
             side = _wgrad_side_stream(dev, B, H)[0]
             side.wait_event(pre)         # not the recurrence itself: the gate waits on its progress
+            if os.environ.get('ASR_DX_SPLIT_SYNC') == '1':   # diagnostics: after the whole recurrence
+                rec_done = torch.cuda.Event()
+                rec_done.record(torch.cuda.current_stream(dev))
+                side.wait_event(rec_done)
             with torch.cuda.stream(side):
                 N.call('asr_lstm_progress_gate', N.ptr(ctr), target, N.stream_handle(dev))
                 N.call('asr_gemm_set_nosplit', 1)     # per output element: one launch's sum
@@ -1874,14 +1878,14 @@ def _progress_counter(dev):
 
 
 def _dx_split_ok(ctx, B, T, dev, mode):
-    """Split input gradient (round 6, ASR_DX_SPLIT=0 turns it off): the
+    """Split input gradient (round 6, opt-in ASR_DX_SPLIT=1): the
     backward recurrence reports when the gate gradients of the middle rows t in
     [T/4, 3T/4) are final (processing step 3T/4 - 1 of both directions), and
     their share of dX = dG W_ih runs on the weight-gradient side stream beside
     the last quarter of that recurrence, on the CUs it leaves free (mode 3);
     the outer rows follow on the compute stream.  Needs the packed-activation
     tagged-granule backward (the one that reports progress)."""
-    return (os.environ.get('ASR_DX_SPLIT', '1') != '0' and mode == '3' and T >= 64
+    return (os.environ.get('ASR_DX_SPLIT', '0') == '1' and mode == '3' and T >= 64
             and compute_dtype() == BF16 and ctx.needs_input_grad[0])
 
 

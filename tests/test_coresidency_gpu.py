@@ -224,9 +224,11 @@ def test_held_cus_beside_recurrence_bitwise_or_visible_skip(hold_ms, cuda_dev):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('sync', ['1', '0'])
 @pytest.mark.parametrize('H,L,T,sub,drop', [(512, 5, 240, [], 0.0),
                                             (320, 4, 400, [False, True, True, False], 0.2)])
-def test_split_input_gradient_bitwise_equals_whole(H, L, T, sub, drop, cuda_dev):
+def test_split_input_gradient_bitwise_equals_whole(H, L, T, sub, drop, sync, cuda_dev,
+                                                   monkeypatch):
     """The split input gradient (round 6, native_ops._dx_split_ok): the middle
     rows t in [T/4, 3T/4) of dX = dG W_ih computed on the side stream beside
     the last quarter of the backward recurrence (gated on the progress the
@@ -234,8 +236,12 @@ def test_split_input_gradient_bitwise_equals_whole(H, L, T, sub, drop, cuda_dev)
     -- every gradient bitwise equal to the whole product (ASR_DX_SPLIT=0),
     at the 5x512 shape and at a 4x320 encoder with pyramidal subsampling and
     encoder dropout (the input maps and the dX epilogue's dropout mask), and
-    the split path actually ran (its progress counter advanced)."""
+    the split path actually ran (its progress counter advanced).  sync=1:
+    the side stream's share also waits for the whole recurrence
+    (ASR_DX_SPLIT_SYNC, diagnostics: separates the row products from the
+    progress hand-off)."""
     from pytorch_end2end_speech_recognition_amd import native_ops
+    monkeypatch.setenv('ASR_DX_SPLIT_SYNC', sync)
     native_ops.set_compute_dtype('bf16')
     try:
         kw = dict(_kw(H, L), subsample_list=sub, dropout_encoder=drop)
@@ -265,3 +271,43 @@ def test_split_input_gradient_bitwise_equals_whole(H, L, T, sub, drop, cuda_dev)
         _equal(out['0'], out['1'], 'split dX')
     finally:
         native_ops.set_compute_dtype('fp32')
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('B,T,T_src,H,Dsrc,t_mul,t_add,permute', [
+    (32, 240, 240, 512, 1024, 1, 0, False), (8, 100, 200, 320, 640, 2, 1, True)])
+def test_split_row_problems_equal_whole_product(B, T, T_src, H, Dsrc, t_mul, t_add, permute,
+                                                cuda_dev):
+    """The split input gradient's three row-range products (native_ops.
+    _dx_rows_problem: t in [0, T/4), [T/4, 3T/4), [3T/4, T), each with its own
+    A / C row maps, K unsplit) against the whole dX = dG W_ih product on the
+    same bf16 operands: bitwise, with and without the batch permutation and
+    the pyramidal input map.  GEMMs only (no recurrence, no progress gate)."""
+    from types import SimpleNamespace
+    from pytorch_end2end_speech_recognition_amd import native_ops as ops
+    from pytorch_end2end_speech_recognition_amd import _native as N
+    ops.set_compute_dtype('bf16')
+    g = torch.Generator(device='cpu').manual_seed(5)
+    dg = torch.randn(B, T, 8 * H, generator=g).to(torch.bfloat16).to(cuda_dev)
+    w = (torch.randn(8 * H, Dsrc, generator=g) * 0.05).to(torch.bfloat16).to(cuda_dev)
+    perm = (torch.randperm(B, generator=g).to(torch.int32).to(cuda_dev) if permute else None)
+    ctx = SimpleNamespace(drop=None)
+    whole = torch.zeros(B, T_src, Dsrc, device=cuda_dev)
+    c_map = ops.rowmap(Dsrc, stride_b=T_src * Dsrc, rows_per_b=T, t_mul=t_mul, t_add=t_add,
+                       t_limit=T_src, perm=perm)
+    N.call('asr_gemm_set_nosplit', 1)
+    try:
+        ops.run_gemm([ops.gemm_problem(ops.operand(dg, 0, ops.rowmap(8 * H)),
+                                       ops.operand(w, 1, ops.rowmap(Dsrc)), whole, c_map,
+                                       B * T, Dsrc, 8 * H)], cuda_dev)
+        parts = torch.zeros_like(whole)
+        t0 = T // 4
+        for ta, tb in ((t0, T - t0), (0, t0), (T - t0, T)):
+            ops.run_gemm([ops._dx_rows_problem(dg, w, parts, ctx, B, T, T_src, H, Dsrc, Dsrc, Dsrc,
+                                               perm, t_mul, t_add, ta, tb)], cuda_dev)
+    finally:
+        N.call('asr_gemm_set_nosplit', 0)
+    torch.cuda.synchronize()
+    d = (whole != parts).nonzero()
+    assert d.numel() == 0, (d[:5].tolist(), float((whole - parts).abs().max()))
+    assert float(whole.abs().sum()) > 0
