@@ -233,7 +233,8 @@ def test_split_input_gradient_bitwise_equals_whole(H, L, T, sub, drop, sync, cud
     rows t in [T/4, 3T/4) of dX = dG W_ih computed on the side stream beside
     the last quarter of the backward recurrence (gated on the progress the
     recurrence publishes at processing step 3T/4 - 1), the outer rows after it
-    -- every gradient bitwise equal to the whole product (ASR_DX_SPLIT=0),
+    -- every gradient bitwise equal to the whole product (ASR_DX_SPLIT=0, both
+    without split-K slabs),
     at the 5x512 shape and at a 4x320 encoder with pyramidal subsampling and
     encoder dropout (the input maps and the dX epilogue's dropout mask), and
     the split path actually ran (its progress counter advanced).  sync=1:
@@ -242,6 +243,10 @@ def test_split_input_gradient_bitwise_equals_whole(H, L, T, sub, drop, sync, cud
     progress hand-off)."""
     from pytorch_end2end_speech_recognition_amd import native_ops
     monkeypatch.setenv('ASR_DX_SPLIT_SYNC', sync)
+    # the split's row products take no split-K (one launch's sum per element);
+    # the whole product would take it at these test sizes (T 240 / 400), so
+    # both runs go without it: the comparison is then of the same arithmetic
+    monkeypatch.setenv('ASR_GEMM_NOSPLIT', '1')
     native_ops.set_compute_dtype('bf16')
     try:
         kw = dict(_kw(H, L), subsample_list=sub, dropout_encoder=drop)

@@ -44,11 +44,14 @@ def test_shadow_training_bitwise_equals_conversion(poke, cuda_dev, monkeypatch):
     from pytorch_end2end_speech_recognition_amd import native_ops
     H, L, steps = 256, 3, 3
     native_ops.set_compute_dtype('bf16')
-    torch.manual_seed(1623)
-    sd = {k: v.clone() for k, v in _build(_kw(H, L)).state_dict().items()}
-    batch = _batch(T=160)
-    l0, p0, h0 = _train(sd, batch, H, L, steps, poke, monkeypatch, shadow=False)
-    l1, p1, h1 = _train(sd, batch, H, L, steps, poke, monkeypatch, shadow=True)
+    try:
+        torch.manual_seed(1623)
+        sd = {k: v.clone() for k, v in _build(_kw(H, L)).state_dict().items()}
+        batch = _batch(T=160)
+        l0, p0, h0 = _train(sd, batch, H, L, steps, poke, monkeypatch, shadow=False)
+        l1, p1, h1 = _train(sd, batch, H, L, steps, poke, monkeypatch, shadow=True)
+    finally:
+        native_ops.set_compute_dtype('fp32')
     assert h0 == 0
     # every layer of every forward after the first step reads the shadow,
     # except the poked layer's forward right after the poke

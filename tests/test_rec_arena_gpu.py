@@ -22,11 +22,18 @@ def _loss_grad(m, batch):
     return loss.item(), m._flat_grad.clone()
 
 
+@pytest.fixture
+def bf16_mode():
+    from pytorch_end2end_speech_recognition_amd import native_ops
+    native_ops.set_compute_dtype('bf16')
+    yield
+    native_ops.set_compute_dtype('fp32')
+
+
 @pytest.mark.gpu
-def test_arena_bitwise_equals_per_launch_memset(cuda_dev, monkeypatch):
+def test_arena_bitwise_equals_per_launch_memset(cuda_dev, monkeypatch, bf16_mode):
     from pytorch_end2end_speech_recognition_amd import native_ops
     H, L = 256, 3
-    native_ops.set_compute_dtype('bf16')
     torch.manual_seed(1623)
     sd = {k: v.clone() for k, v in _build(_kw(H, L)).state_dict().items()}
     b1, b2 = _batch(T=160, seed=1), _batch(T=200, seed=2)
