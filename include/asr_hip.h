@@ -937,6 +937,9 @@ int asr_lstm_set_dy_flags(const int* flags, int c0, int epoch);
  * t = T-1-q (forward direction) and t = q (reverse): rows t in [T-1-q, q] of
  * dG are final once q >= T/2. */
 int asr_lstm_set_bwd_progress(unsigned long long* counter, int q);
+/* Two reporting steps q1 < q2 (round 6, the two-chunk split): one launch's
+ * arrivals are added at each. */
+int asr_lstm_set_bwd_progress2(unsigned long long* counter, int q1, int q2);
 long long asr_lstm_bwd_progress_arrivals(int B, int H);
 int asr_lstm_progress_gate(const unsigned long long* counter, long long target, void* stream);
 /* Per-step workspace arena (round 6): the workspace handed to the next

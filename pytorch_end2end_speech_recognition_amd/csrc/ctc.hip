@@ -652,14 +652,16 @@ __global__ void __launch_bounds__(64 * (W + 1)) ctc_lattice_w(
   bool valid[KW];
 #pragma unroll
   for (int k = 0; k < KW; ++k) valid[k] = sb + k < S;
-  // the edge record of step n posted by wave v; spins until it is there
-  auto wait_edge = [&](int v, int n) {
-    const f32x4* p = &edge[v][n & (RB - 1)];
-    f32x4 rec;
-    for (unsigned spins = 0;; ++spins) {
-      rec = *reinterpret_cast<const volatile f32x4*>(p);
-      if (__float_as_int(rec[2]) == n || spins > (1u << 20)) break;   // (bounded: never hangs)
-      __builtin_amdgcn_s_sleep(0);
+  // the edge record of step n posted by wave v: read once ahead (issued after
+  // the previous step, so its LDS latency overlaps that step's row store),
+  // then re-read until its tag says step n
+  auto read_edge = [&](int v, int n) {
+    return *reinterpret_cast<const volatile f32x4*>(&edge[v][n & (RB - 1)]);
+  };
+  auto wait_edge = [&](int v, int n, f32x4 rec) {
+    for (unsigned spins = 0; __float_as_int(rec[2]) != n && spins <= (1u << 20); ++spins) {
+      __builtin_amdgcn_s_sleep(0);   // (bounded: never hangs)
+      rec = read_edge(v, n);
     }
     return rec;
   };
@@ -694,6 +696,7 @@ __global__ void __launch_bounds__(64 * (W + 1)) ctc_lattice_w(
     };
     post_top(0);
     __syncthreads();
+    f32x4 ahead = read_edge(wave > 0 ? wave - 1 : 0, 0);
     for (int c = 0; c < nch; ++c) {
       float ec[C][KW];
 #pragma unroll
@@ -707,7 +710,7 @@ __global__ void __launch_bounds__(64 * (W + 1)) ctc_lattice_w(
           float p2 = (KW >= 2) ? from_lower_lane(a[KW >= 2 ? KW - 2 : 0]) : from_lower_lane(p1);
           float e1 = NEG, e2 = NEG;   // states sb_wave - 1, - 2 at step n (row n)
           if (wave > 0) {
-            const f32x4 r = wait_edge(wave - 1, n);
+            const f32x4 r = wait_edge(wave - 1, n, ahead);
             e1 = r[0];
             e2 = r[1];
           }
@@ -726,6 +729,7 @@ __global__ void __launch_bounds__(64 * (W + 1)) ctc_lattice_w(
 #pragma unroll
           for (int k = 0; k < KW; ++k) a[k] = nx[k];
           post_top(n + 1);
+          if (wave > 0) ahead = read_edge(wave - 1, n + 1);
           store_k<KW>(A + (size_t)(1 + n) * Spad, a);
         }
       }
@@ -778,6 +782,7 @@ __global__ void __launch_bounds__(64 * (W + 1)) ctc_lattice_w(
   };
   post_bottom(0);
   __syncthreads();
+  f32x4 ahead = read_edge(wave + 1 < W ? wave + 1 : 0, 0);
   for (int c = 0; c < nch; ++c) {
     float ec[C][KW];
 #pragma unroll
@@ -791,7 +796,7 @@ __global__ void __launch_bounds__(64 * (W + 1)) ctc_lattice_w(
         float n2 = (KW >= 2) ? from_upper_lane(be[KW >= 2 ? 1 : 0]) : from_upper_lane(n1);
         float e1 = NEG, e2 = NEG;   // states sb_wave + 64 KW, + 1 at step n
         if (wave + 1 < W) {
-          const f32x4 r = wait_edge(wave + 1, n);
+          const f32x4 r = wait_edge(wave + 1, n, ahead);
           e1 = r[0];
           e2 = r[1];
         }
@@ -810,6 +815,7 @@ __global__ void __launch_bounds__(64 * (W + 1)) ctc_lattice_w(
 #pragma unroll
         for (int k = 0; k < KW; ++k) be[k] = nx[k];
         post_bottom(n + 1);
+        if (wave + 1 < W) ahead = read_edge(wave + 1, n + 1);
         store_k<KW>(Bt + (size_t)(Tb - 2 - n) * Spad, be);
       }
     }
@@ -1828,15 +1834,17 @@ static int ctc_forward_impl(const float* acts, long long stride_t, long long str
                      ws.alpha, ws.beta, ws.logp, costs)
   // the lattice over several waves (ctc_lattice_w) from K = 2; ASR_CTC_LATTICE_W=1
   // keeps the one-wave kernel (A/B)
+  // (ASR_CTC_LATTICE_W=2: at most two waves, two states per lane from K = 4)
   const char* lw = getenv("ASR_CTC_LATTICE_W");
-  const bool multi = !(lw && atoi(lw) == 1);
-  g_ctc_last_path[2] = multi && K >= 2 ? (K >= 4 ? 4 : 2) : 1;
+  const int wmax = lw ? atoi(lw) : 4;
+  const int W = K < 2 || wmax <= 1 ? 1 : (wmax == 2 || K == 2 ? 2 : 4);
+  g_ctc_last_path[2] = W;
   switch (K) {
     case 1: ASR_CTC_LAT(1); break;
-    case 2: if (multi) ASR_CTC_LATW(2, 2); else ASR_CTC_LAT(2); break;
-    case 4: if (multi) ASR_CTC_LATW(4, 4); else ASR_CTC_LAT(4); break;
-    case 8: if (multi) ASR_CTC_LATW(8, 4); else ASR_CTC_LAT(8); break;
-    case 16: if (multi) ASR_CTC_LATW(16, 4); else ASR_CTC_LAT(16); break;
+    case 2: if (W > 1) ASR_CTC_LATW(2, 2); else ASR_CTC_LAT(2); break;
+    case 4: if (W == 4) ASR_CTC_LATW(4, 4); else if (W == 2) ASR_CTC_LATW(4, 2); else ASR_CTC_LAT(4); break;
+    case 8: if (W == 4) ASR_CTC_LATW(8, 4); else if (W == 2) ASR_CTC_LATW(8, 2); else ASR_CTC_LAT(8); break;
+    case 16: if (W == 4) ASR_CTC_LATW(16, 4); else if (W == 2) ASR_CTC_LATW(16, 2); else ASR_CTC_LAT(16); break;
     default: set_error("ctc: unsupported K=%d", K); return ASR_ERR_UNSUPPORTED;
   }
 #undef ASR_CTC_LATW

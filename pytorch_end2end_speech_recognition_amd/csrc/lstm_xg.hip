@@ -126,6 +126,7 @@ const int* g_dyflag = nullptr;
 // of the rows complete by then can start beside the rest of the pass.
 unsigned long long* g_prog_ctr = nullptr;
 int g_prog_q = -1;
+int g_prog_q2 = -1;   // a second reporting step (asr_lstm_set_bwd_progress2), -1: none
 int g_dyc0 = 16;
 unsigned g_dyepoch = 0;
 
@@ -716,9 +717,6 @@ __global__ void __launch_bounds__(64 * NSW + R * XU + 64 * NPW) lstm_fwd_xgx(
 
   if (wave < NSW) {
     // ------------------------------ sweeper (as lstm_fwd_xg) ------------------
-#ifdef ASR_XG_SWEEP_PRIO   // A/B build: the sweepers' MFMAs ahead of the producers'
-    __builtin_amdgcn_s_setprio(ASR_XG_SWEEP_PRIO);
-#endif
     const int kq = lane >> 4, ln = lane & 15;
     const bool sweeper = ln < R;
     bf16x8 wf[KSW][4];
@@ -1064,7 +1062,7 @@ __global__ void __launch_bounds__(256 + R * XB + 64 * (F32 ? 4 : XB / 4)) lstm_b
     uint16_t* __restrict__ dgbf, float* __restrict__ dbpart, unsigned epoch, int allow_local,
     int dg_f32, int io_pos, int dg_st16, const h16x4* __restrict__ acth,
     const int* __restrict__ dyflag, int dyc0, int dyepoch, unsigned long long* prog,
-    int prog_q) {
+    int prog_q, int prog_q2) {
   static_assert(!F32 || ((XB == 16 || XB == 8) && !AH), "f32 backward: 8 or 16 units, f32 activations");
   constexpr int UPL = F32 ? 4 : 8;     // units per 16-B load
   constexpr int SQ = XB / UPL;         // 16-B loads per row of a producer's slice
@@ -1418,7 +1416,7 @@ __global__ void __launch_bounds__(256 + R * XB + 64 * (F32 ? 4 : XB / 4)) lstm_b
       if (io_pos == 0) step_io(q, t, d_i, d_f, d_g, d_o, bi, bff, bg, bo);
       __syncthreads();  // B3
       if (io_pos == 1) step_io(q, t, d_i, d_f, d_g, d_o, bi, bff, bg, bo);
-      if (prog && q == prog_q) {
+      if (prog && (q == prog_q || q == prog_q2)) {
         // every dG store of steps <= q by this wave is complete and released
         // at agent scope (written back from this XCD's L2), then counted: a
         // reader on another stream that sees all arrivals reads final rows
@@ -1797,7 +1795,7 @@ int lstm_bwd_xg32_launch(int B, int T, int H, const int32_t* lens, const float* 
     hipLaunchKernelGGL((lstm_bwd_xg<RR, M, false, XV, true>), dim3(grid),                        \
                        dim3(256 + RR * XV + 256), pin, s, B, T, H, lens, whh_f, whh_r, dy,      \
                        act_dg, cst, g, hdr, (uint16_t*)nullptr, dbpart, ep, al, 1, 0, 0,        \
-                       (const h16x4*)nullptr, (const int*)nullptr, 0, 0, nullptr, -1);           \
+                       (const h16x4*)nullptr, (const int*)nullptr, 0, 0, nullptr, -1, -1);       \
   } while (0)
 #define ASR_XGB32_M(RR, XV)                 \
   do {                                      \
@@ -1903,7 +1901,7 @@ int lstm_bwd_xg_launch(int B, int T, int H, const int32_t* lens, const float* wh
                        B, T, H, lens, whh_f, whh_r, dy, act_dg, cst, g, hdr, dgbf, dbpart, ep,   \
                        al, (dg_f32 || !dgbf) ? 1 : 0, io_pos, st16, (const h16x4*)acth,         \
                        acth ? g_dyflag : nullptr, g_dyc0, (int)g_dyepoch,                        \
-                       acth ? g_prog_ctr : nullptr, g_prog_q);                                   \
+                       acth ? g_prog_ctr : nullptr, g_prog_q, g_prog_q2);                        \
   } while (0)
 #define ASR_XGB2(RR, M, AHV)                                  \
   do {                                                        \
@@ -2138,6 +2136,16 @@ extern "C" int asr_lstm_set_bwd_progress(unsigned long long* counter, int q) {
   ASR_REQUIRE(!counter || q >= 0, ASR_ERR_ARG, "bwd progress: q %d", q);
   asr::g_prog_ctr = counter;
   asr::g_prog_q = counter ? q : -1;
+  asr::g_prog_q2 = -1;
+  return ASR_OK;
+}
+
+// Two reporting steps q1 < q2: the counter gains one launch's arrivals at each.
+extern "C" int asr_lstm_set_bwd_progress2(unsigned long long* counter, int q1, int q2) {
+  ASR_REQUIRE(!counter || (q1 >= 0 && q2 > q1), ASR_ERR_ARG, "bwd progress: q %d, %d", q1, q2);
+  asr::g_prog_ctr = counter;
+  asr::g_prog_q = counter ? q1 : -1;
+  asr::g_prog_q2 = counter ? q2 : -1;
   return ASR_OK;
 }
 

@@ -1405,7 +1405,11 @@ class BLSTMLayerFn(torch.autograd.Function):
             N.call('asr_lstm_set_bwd_units', xu)     # (arrivals follow the units setting)
             arrivals = N.query('asr_lstm_bwd_progress_arrivals', B, H)
             if arrivals > 0:
-                split = (T // 4, _progress_counter(dev), int(arrivals))
+                # row bands by when their gate gradients are final: [T/4, 3T/4) at
+                # processing step 3T/4 - 1, with two chunks also [T/8, T/4) and
+                # [3T/4, 7T/8) at 7T/8 - 1; the rest after the recurrence
+                two = _dx_split_chunks() == 2 and T >= 128
+                split = (T // 4, _progress_counter(dev), int(arrivals), T // 8 if two else None)
                 # dX before the recurrence: its zero fill (non-identity maps) precedes
                 # the side stream's writes
                 ident = perm is None and t_mul == 1 and t_add == 0 and T == T_src and Din == Dsrc
@@ -1422,7 +1426,11 @@ class BLSTMLayerFn(torch.autograd.Function):
                 if pipe is not None:
                     N.call('asr_lstm_set_dy_flags', N.ptr(pipe[0]), pipe[1], pipe[2])
                 if split is not None:
-                    N.call('asr_lstm_set_bwd_progress', N.ptr(split[1][0]), T - 1 - split[0])
+                    if split[3] is not None:
+                        N.call('asr_lstm_set_bwd_progress2', N.ptr(split[1][0]), T - 1 - split[0],
+                               T - 1 - split[3])
+                    else:
+                        N.call('asr_lstm_set_bwd_progress', N.ptr(split[1][0]), T - 1 - split[0])
                     # everything the side stream's share of dX reads that is not
                     # written by the recurrence is enqueued by now (dx's fill included)
                     split_pre = torch.cuda.Event()
@@ -1446,8 +1454,9 @@ class BLSTMLayerFn(torch.autograd.Function):
                         rc, N.lib().asr_last_error().decode(errors='replace')))
                 done = rc == 0
                 if done and split is not None:
-                    split[1][1] += split[2]          # the arrivals this launch adds
-                    split = split + (split[1][1], split_pre)
+                    first = split[1][1] + split[2]   # the arrivals this launch adds per step
+                    split[1][1] += split[2] * (2 if split[3] is not None else 1)
+                    split = split + ((first, split[1][1]), split_pre)
                 else:
                     split = None
                 if not done:
@@ -1482,19 +1491,24 @@ class BLSTMLayerFn(torch.autograd.Function):
         dg_op = dg_bf if dg_bf is not None else act
         split_done = None
         if split is not None:
-            t0, (ctr, _), _, target, pre = split
+            t0, (ctr, _), _, t1, targets, pre = split
             side = _wgrad_side_stream(dev, B, H)[0]
             side.wait_event(pre)         # not the recurrence itself: the gate waits on its progress
             if os.environ.get('ASR_DX_SPLIT_SYNC') == '1':   # diagnostics: after the whole recurrence
                 rec_done = torch.cuda.Event()
                 rec_done.record(torch.cuda.current_stream(dev))
                 side.wait_event(rec_done)
+            rows = lambda ta, tb: _dx_rows_problem(dg_op, w_op, dx_split, ctx, B, T, T_src, H,  # noqa: E731
+                                                   Din, Dp, Dsrc, perm, t_mul, t_add, ta, tb)
             with torch.cuda.stream(side):
-                N.call('asr_lstm_progress_gate', N.ptr(ctr), target, N.stream_handle(dev))
                 N.call('asr_gemm_set_nosplit', 1)     # per output element: one launch's sum
                 try:
-                    run_gemm([_dx_rows_problem(dg_op, w_op, dx_split, ctx, B, T, T_src, H, Din,
-                                               Dp, Dsrc, perm, t_mul, t_add, t0, T - t0)], dev)
+                    N.call('asr_lstm_progress_gate', N.ptr(ctr), targets[0], N.stream_handle(dev))
+                    run_gemm([rows(t0, T - t0)], dev)
+                    if t1 is not None:
+                        N.call('asr_lstm_progress_gate', N.ptr(ctr), targets[1],
+                               N.stream_handle(dev))
+                        run_gemm([rows(t1, t0), rows(T - t0, T - t1)], dev)
                 finally:
                     N.call('asr_gemm_set_nosplit', 0)
                 split_done = torch.cuda.Event()
@@ -1555,9 +1569,9 @@ class BLSTMLayerFn(torch.autograd.Function):
                     lambda: _join_side_wgrads(dev, notify=False))
             _side_pending.append((side, gbufs, main))
         if split_done is not None:
-            # the outer rows t in [0, T/4) and [3T/4, T) on the compute stream, then
-            # the side stream's middle rows joined
-            t0 = split[0]
+            # the outer rows t in [0, T/4) and [3T/4, T) (two chunks: [0, T/8) and
+            # [7T/8, T)) on the compute stream, then the side stream's rows joined
+            t0 = split[3] if split[3] is not None else split[0]
             N.call('asr_gemm_set_nosplit', 1)
             try:
                 run_gemm([_dx_rows_problem(dg_op, w_op, dx_split, ctx, B, T, T_src, H, Din, Dp,
@@ -1877,15 +1891,21 @@ def _progress_counter(dev):
     return ent
 
 
+def _dx_split_chunks():
+    """Row chunks the split input gradient computes beside the recurrence:
+    ASR_DX_SPLIT=1 one ([T/4, 3T/4)), 2 two (and [T/8, T/4) + [3T/4, 7T/8))."""
+    return 2 if os.environ.get('ASR_DX_SPLIT', '1') == '2' else 1
+
+
 def _dx_split_ok(ctx, B, T, dev, mode):
-    """Split input gradient (round 6, opt-in ASR_DX_SPLIT=1): the
+    """Split input gradient (round 6, ASR_DX_SPLIT=0 turns it off): the
     backward recurrence reports when the gate gradients of the middle rows t in
     [T/4, 3T/4) are final (processing step 3T/4 - 1 of both directions), and
     their share of dX = dG W_ih runs on the weight-gradient side stream beside
     the last quarter of that recurrence, on the CUs it leaves free (mode 3);
     the outer rows follow on the compute stream.  Needs the packed-activation
     tagged-granule backward (the one that reports progress)."""
-    return (os.environ.get('ASR_DX_SPLIT', '0') == '1' and mode == '3' and T >= 64
+    return (os.environ.get('ASR_DX_SPLIT', '1') != '0' and mode == '3' and T >= 64
             and compute_dtype() == BF16 and ctx.needs_input_grad[0])
 
 

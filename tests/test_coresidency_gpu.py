@@ -237,7 +237,9 @@ def test_split_input_gradient_bitwise_equals_whole(H, L, T, sub, drop, sync, cud
     without split-K slabs),
     at the 5x512 shape and at a 4x320 encoder with pyramidal subsampling and
     encoder dropout (the input maps and the dX epilogue's dropout mask), and
-    the split path actually ran (its progress counter advanced).  sync=1:
+    the split path actually ran (its progress counter advanced); also the
+    two-chunk form (ASR_DX_SPLIT=2: [T/8, T/4) and [3T/4, 7T/8) at processing
+    step 7T/8 - 1 as a second side-stream product).  sync=1:
     the side stream's share also waits for the whole recurrence
     (ASR_DX_SPLIT_SYNC, diagnostics: separates the row products from the
     progress hand-off)."""
@@ -254,7 +256,7 @@ def test_split_input_gradient_bitwise_equals_whole(H, L, T, sub, drop, sync, cud
         sd = {k: v.clone() for k, v in _build(kw).state_dict().items()}
         batch = _batch(T=T)
         out = {}
-        for flag in ('0', '1'):
+        for flag in ('0', '1', '2'):
             before = native_ops._progress_counter(cuda_dev)[1]
             os.environ['ASR_DX_SPLIT'] = flag
             try:
@@ -272,8 +274,9 @@ def test_split_input_gradient_bitwise_equals_whole(H, L, T, sub, drop, sync, cud
             finally:
                 os.environ.pop('ASR_DX_SPLIT', None)
             ran = native_ops._progress_counter(cuda_dev)[1] - before
-            assert (ran > 0) == (flag == '1'), (flag, ran)
+            assert (ran > 0) == (flag != '0'), (flag, ran)
         _equal(out['0'], out['1'], 'split dX')
+        _equal(out['0'], out['2'], 'split dX, two chunks')
     finally:
         native_ops.set_compute_dtype('fp32')
 
