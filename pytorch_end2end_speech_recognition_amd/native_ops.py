@@ -1400,6 +1400,9 @@ class BLSTMLayerFn(torch.autograd.Function):
         N.call('asr_lstm_set_bwd_pin_kb', 84 if mode == '2' else 0)
         N.call('asr_lstm_set_bwd_units', xu)
         split = None
+        last_main = not ctx.next_rec and os.environ.get('ASR_WGRAD_LAST_MAIN', '1') != '0'
+        wsplit = last_main and _wgrad_split_ok(ctx, T, mode)
+        wprog = None      # (counter, target, event) of the bottom layer's banded dW overlap
         if (act.dtype == torch.float16 and pipe is None and _dx_split_ok(ctx, B, T, dev, mode)
                 and not _dx_pipeline_ok(ctx, B, T, Din, dev)):
             N.call('asr_lstm_set_bwd_units', xu)     # (arrivals follow the units setting)
@@ -1425,6 +1428,13 @@ class BLSTMLayerFn(torch.autograd.Function):
                 ws = res[0] if pz else _ws(nb, dev)
                 if pipe is not None:
                     N.call('asr_lstm_set_dy_flags', N.ptr(pipe[0]), pipe[1], pipe[2])
+                if split is None and wsplit and mode == '3':
+                    arrivals = N.query('asr_lstm_bwd_progress_arrivals', B, H)
+                    if arrivals > 0:
+                        wprog = (_progress_counter(dev), int(arrivals))
+                        N.call('asr_lstm_set_bwd_progress', N.ptr(wprog[0][0]), T - 1 - T // 4)
+                        wprog_pre = torch.cuda.Event()
+                        wprog_pre.record(torch.cuda.current_stream(dev))
                 if split is not None:
                     if split[3] is not None:
                         N.call('asr_lstm_set_bwd_progress2', N.ptr(split[1][0]), T - 1 - split[0],
@@ -1442,7 +1452,7 @@ class BLSTMLayerFn(torch.autograd.Function):
                                      N.ptr(act), N.ptr(cst), N.ptr(dg_bf), N.ptr(gbufs[2]),
                                      N.ptr(gbufs[3]), N.ptr(ws), nb, N.stream_handle(dev))
                 finally:
-                    if split is not None:
+                    if split is not None or wprog is not None:
                         N.call('asr_lstm_set_bwd_progress', None, 0)
                     if pipe is not None:
                         N.call('asr_lstm_set_dy_flags', None, 16, 0)
@@ -1453,6 +1463,11 @@ class BLSTMLayerFn(torch.autograd.Function):
                     raise N.NativeError('asr_lstm_backward_dgbf_h failed (rc=%d): %s' % (
                         rc, N.lib().asr_last_error().decode(errors='replace')))
                 done = rc == 0
+                if done and wprog is not None:
+                    wprog[0][1] += wprog[1]
+                    wprog = (wprog[0][0], wprog[0][1], wprog_pre)
+                else:
+                    wprog = None
                 if done and split is not None:
                     first = split[1][1] + split[2]   # the arrivals this launch adds per step
                     split[1][1] += split[2] * (2 if split[3] is not None else 1)
@@ -1524,7 +1539,6 @@ class BLSTMLayerFn(torch.autograd.Function):
         # the bottom layer's weight gradients have no recurrence left to run
         # beside: they take the main stream and the full-size GEMM kernels (on
         # the co-resident small tiles the 4x320 layer-0 dW_ih ran at 29 TF/s)
-        last_main = not ctx.next_rec and os.environ.get('ASR_WGRAD_LAST_MAIN', '1') != '0'
         side_ent = None if last_main else _wgrad_side_stream(dev, B, H)
         # pipelined input gradient (_dx_pipelined): enqueued first, and the
         # side-stream weight gradients start after it, so the CUs the next
@@ -1536,7 +1550,29 @@ class BLSTMLayerFn(torch.autograd.Function):
         if pipelined:
             dx = torch.empty(B, T_src, Dsrc, dtype=torch.float32, device=dev)
             dx_done = _dx_pipelined(dx, dg_op, w_op, B, T, H, Din, Dp, ctx.drop, dev)
-        if side_ent is None:
+        if side_ent is None and wsplit:
+            # time bands: the middle one first (beside the recurrence's last
+            # quarter when it reported progress), then the outer two
+            tq = T // 4
+            Dx = x_op.shape[-1]
+            if wprog is not None:
+                ctr, target, pre = wprog
+                side = _wgrad_side_stream(dev, B, H)[0]
+                side.wait_event(pre)
+                with torch.cuda.stream(side):
+                    N.call('asr_lstm_progress_gate', N.ptr(ctr), target, N.stream_handle(dev))
+                    _blstm_wgrad_rows(dg_op, x_op, Dx, y_op, T, gbufs, dev, tq, T - tq)
+                    mid_done = torch.cuda.Event()
+                    mid_done.record(side)
+                for tt in (dg_op, x_op, y_op, ctr):
+                    tt.record_stream(side)
+                torch.cuda.current_stream(dev).wait_event(mid_done)
+            else:
+                _blstm_wgrad_rows(dg_op, x_op, Dx, y_op, T, gbufs, dev, tq, T - tq)
+            _blstm_wgrad_rows(dg_op, x_op, Dx, y_op, T, gbufs, dev, 0, tq)
+            _blstm_wgrad_rows(dg_op, x_op, Dx, y_op, T, gbufs, dev, T - tq, T)
+            notify_grad_event('grads', gbufs)      # final on the compute stream
+        elif side_ent is None:
             _blstm_wgrad(dg_op, act, x_op, x_map, y_op, T, gbufs, dev)
             notify_grad_event('grads', gbufs)      # final on the compute stream
         else:
@@ -1754,6 +1790,42 @@ def _blstm_wgrad(dg, dg_f32, x_op, x_map, y_op, T, gbufs, dev):
                      operand(y_op, 1, hp_r, offset=H), g_hh, rowmap(H), 4 * H, H, BT, beta=1.0,
                      c_offset=4 * H * H),
     ], dev)
+
+
+def _blstm_wgrad_rows(dg, x_op, Dx, y_op, T, gbufs, dev, ta, tb):
+    """_blstm_wgrad over the rows (b, t), t in [ta, tb), of every utterance
+    (bf16 mode: dg and x_op dense [B*T, width] rows): the weight gradients
+    accumulated (beta = 1) from that band of time steps only."""
+    B = dg.shape[0]
+    H = y_op.shape[2] // 2
+    n = tb - ta
+    if n <= 0:
+        return
+    g_ih, g_hh, g_bih, g_bhh = gbufs
+    Din = g_ih.shape[-1]
+    band = lambda ld, add=0: rowmap(ld, stride_b=T * ld, rows_per_b=n, t_add=ta + add,  # noqa: E731
+                                    t_limit=T)
+    run_gemm([gemm_problem(operand(dg, 1, band(8 * H)), operand(x_op, 1, band(Dx)), g_ih,
+                           rowmap(Din), 8 * H, Din, B * n, beta=1.0)], dev)
+    run_gemm([
+        gemm_problem(operand(dg, 1, band(8 * H)), operand(y_op, 1, band(2 * H, -1)), g_hh,
+                     rowmap(H), 4 * H, H, B * n, beta=1.0),
+        gemm_problem(operand(dg, 1, band(8 * H), offset=4 * H),
+                     operand(y_op, 1, band(2 * H, 1), offset=H), g_hh, rowmap(H), 4 * H, H,
+                     B * n, beta=1.0, c_offset=4 * H * H),
+    ], dev)
+
+
+def _wgrad_split_ok(ctx, T, mode):
+    """The bottom BLSTM layer's weight gradients in three time bands (round 6,
+    ASR_WGRAD_SPLIT=0 turns it off): the middle band [T/4, 3T/4) on the side
+    stream beside the last quarter of the layer's own backward recurrence
+    (gated on its progress report, mode 3), then [0, T/4) and [3T/4, T) on
+    the compute stream -- in that order in every mode, so the sums are the
+    same arithmetic with or without the overlap.  bf16 mode (dense staged
+    operands), a layer with no recurrence left below it."""
+    return (os.environ.get('ASR_WGRAD_SPLIT', '1') != '0' and not ctx.next_rec and T >= 64
+            and compute_dtype() == BF16)
 
 
 _side_streams = {}

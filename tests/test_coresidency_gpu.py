@@ -319,3 +319,53 @@ def test_split_row_problems_equal_whole_product(B, T, T_src, H, Dsrc, t_mul, t_a
     d = (whole != parts).nonzero()
     assert d.numel() == 0, (d[:5].tolist(), float((whole - parts).abs().max()))
     assert float(whole.abs().sum()) > 0
+
+
+@pytest.mark.gpu
+def test_bottom_layer_banded_wgrad(cuda_dev, monkeypatch):
+    """The bottom BLSTM layer's weight gradients in three time bands (round 6,
+    native_ops._wgrad_split_ok): the middle band beside the last quarter of
+    its own backward recurrence (mode 3 at 5x512), the outer bands after it.
+    Against the single product (ASR_WGRAD_SPLIT=0): every other gradient
+    bitwise, the bottom layer's W_ih / W_hh within f32 re-association of the
+    three band sums; the overlap actually ran (its progress counter moved)."""
+    from pytorch_end2end_speech_recognition_amd import native_ops
+    native_ops.set_compute_dtype('bf16')
+    try:
+        H, L, T = 512, 5, 240
+        torch.manual_seed(1623)
+        sd = {k: v.clone() for k, v in _build(_kw(H, L)).state_dict().items()}
+        batch = _batch(T=T)
+        out = {}
+        for flag in ('0', '1'):
+            monkeypatch.setenv('ASR_WGRAD_SPLIT', flag)
+            before = native_ops._progress_counter(cuda_dev)[1]
+            m = _build(_kw(H, L))
+            m.load_state_dict(sd)
+            m.set_cuda()
+            m.zero_grad()
+            native_ops.recurrence_status(cuda_dev)
+            loss = m(batch['xs'], batch['ys'], batch['x_lens'], batch['y_lens'])
+            loss.backward()
+            torch.cuda.synchronize()
+            assert int(native_ops.recurrence_status(cuda_dev).max()) == 0
+            ran = native_ops._progress_counter(cuda_dev)[1] - before
+            bottom = [p for n, p in m.named_parameters() if 'weight' in n and '_l0' in n]
+            out[flag] = (loss.item(), m._flat_grad.clone(), ran,
+                         [p.grad.clone() for p in bottom],
+                         {p.grad.data_ptr() for p in bottom})
+        assert out['0'][0] == out['1'][0]
+        assert out['1'][2] > out['0'][2], (out['0'][2], out['1'][2])   # + the bottom layer's report
+        for a, b in zip(out['0'][3], out['1'][3]):
+            assert torch.allclose(a, b, rtol=1e-5, atol=1e-6 * float(a.abs().max())), (
+                float((a - b).abs().max()), float(a.abs().max()))
+        # everything but the bottom layer's weight gradients: bitwise
+        g0, g1 = out['0'][1].clone(), out['1'][1].clone()
+        flat = m._flat_grad
+        for p in [p for n, p in m.named_parameters() if 'weight' in n and '_l0' in n]:
+            o = (p.grad.data_ptr() - flat.data_ptr()) // 4
+            g0[o:o + p.numel()] = 0
+            g1[o:o + p.numel()] = 0
+        assert torch.equal(g0, g1), int((g0 != g1).sum())
+    finally:
+        native_ops.set_compute_dtype('fp32')
