@@ -1832,11 +1832,12 @@ static int ctc_forward_impl(const float* acts, long long stride_t, long long str
   hipLaunchKernelGGL((ctc_lattice_w<KK, WW>), dim3(B, 2), dim3(64 * (WW + 1)), 0, s, T,         \
                      labels_flat, label_lens, act_lens, ws.offs, blank, zero_infinity, ws.emit,  \
                      ws.alpha, ws.beta, ws.logp, costs)
-  // the lattice over several waves (ctc_lattice_w) from K = 2; ASR_CTC_LATTICE_W=1
-  // keeps the one-wave kernel (A/B)
-  // (ASR_CTC_LATTICE_W=2: at most two waves, two states per lane from K = 4)
+  // the one-wave kernel by default; ASR_CTC_LATTICE_W=2 / 4: the lattice over
+  // at most two / four waves (ctc_lattice_w) -- measured SLOWER at ctc5x512
+  // (B 32 x T 1000, K 4: forward 195 us one wave, 265 two, 262 four;
+  // tools/ctc_lattice_bench.py), kept as a tested alternative
   const char* lw = getenv("ASR_CTC_LATTICE_W");
-  const int wmax = lw ? atoi(lw) : 4;
+  const int wmax = lw ? atoi(lw) : 1;
   const int W = K < 2 || wmax <= 1 ? 1 : (wmax == 2 || K == 2 ? 2 : 4);
   g_ctc_last_path[2] = W;
   switch (K) {

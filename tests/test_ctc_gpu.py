@@ -278,9 +278,10 @@ def test_lattice_edge_cases_vs_oracle(K, Ls, cuda_dev):
                                     (8, [128, 200, 255], 4), (8, [128, 200, 255], 2),
                                     (16, [256, 400, 511], 4)])
 def test_lattice_waves_match_single_wave(K, Ls, W, cuda_dev, monkeypatch):
-    """The lattice split over W waves (ctc_lattice_w: per-step edge records
-    between the waves instead of one wave doing every state) against the
-    one-wave kernel (ASR_CTC_LATTICE_W=1): alpha / beta are the same
+    """The lattice split over W waves (ctc_lattice_w, ASR_CTC_LATTICE_W=W:
+    per-step edge records between the waves instead of one wave doing every
+    state; opt-in, measured slower) against the one-wave kernel (the
+    default): alpha / beta are the same
     arithmetic, so the gradients (built from alpha + beta - log P) agree to
     the last bit wherever log P does, and log P -- the two final states summed
     in another lane / wave grouping -- within one f32 ulp.  Label lengths put
@@ -300,9 +301,7 @@ def test_lattice_waves_match_single_wave(K, Ls, W, cuda_dev, monkeypatch):
     monkeypatch.setenv('ASR_CTC_LATTICE_W', '1')
     one = _run(acts, labels, label_lens, act_lens, cuda_dev)
     assert N.lib().asr_ctc_last_lattice_waves() == 1
-    monkeypatch.delenv('ASR_CTC_LATTICE_W')
-    if W == 2 and K > 2:
-        monkeypatch.setenv('ASR_CTC_LATTICE_W', '2')   # two waves, two states per lane
+    monkeypatch.setenv('ASR_CTC_LATTICE_W', str(W))   # (the one-wave kernel is the default)
     multi = _run(acts, labels, label_lens, act_lens, cuda_dev)
     assert N.lib().asr_ctc_last_lattice_waves() == W
     np.testing.assert_allclose(multi[1], one[1], rtol=3e-7, atol=0)
