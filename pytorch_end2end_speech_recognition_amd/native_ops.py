@@ -1818,13 +1818,15 @@ def _blstm_wgrad_rows(dg, x_op, Dx, y_op, T, gbufs, dev, ta, tb):
 
 def _wgrad_split_ok(ctx, T, mode):
     """The bottom BLSTM layer's weight gradients in three time bands (round 6,
-    ASR_WGRAD_SPLIT=0 turns it off): the middle band [T/4, 3T/4) on the side
+    opt-in ASR_WGRAD_SPLIT=1; measured slower at ctc5x512, 17.48 vs 17.42
+    ms/step: the band beside the recurrence costs it more than the 120 us it
+    takes off the tail): the middle band [T/4, 3T/4) on the side
     stream beside the last quarter of the layer's own backward recurrence
     (gated on its progress report, mode 3), then [0, T/4) and [3T/4, T) on
     the compute stream -- in that order in every mode, so the sums are the
     same arithmetic with or without the overlap.  bf16 mode (dense staged
     operands), a layer with no recurrence left below it."""
-    return (os.environ.get('ASR_WGRAD_SPLIT', '1') != '0' and not ctx.next_rec and T >= 64
+    return (os.environ.get('ASR_WGRAD_SPLIT', '0') == '1' and not ctx.next_rec and T >= 64
             and compute_dtype() == BF16)
 
 
