@@ -1400,24 +1400,30 @@ class BLSTMLayerFn(torch.autograd.Function):
         N.call('asr_lstm_set_bwd_pin_kb', 84 if mode == '2' else 0)
         N.call('asr_lstm_set_bwd_units', xu)
         split = None
+        band_seq = None   # (t0, t1): the same row bands, computed after the recurrence
+        dx_split = None
         last_main = not ctx.next_rec and os.environ.get('ASR_WGRAD_LAST_MAIN', '1') != '0'
         wsplit = last_main and _wgrad_split_ok(ctx, T, mode)
         wprog = None      # (counter, target, event) of the bottom layer's banded dW overlap
         if (act.dtype == torch.float16 and pipe is None and _dx_split_ok(ctx, B, T, dev, mode)
                 and not _dx_pipeline_ok(ctx, B, T, Din, dev)):
             N.call('asr_lstm_set_bwd_units', xu)     # (arrivals follow the units setting)
-            arrivals = N.query('asr_lstm_bwd_progress_arrivals', B, H)
+            # row bands by when their gate gradients are final: [T/4, 3T/4) at
+            # processing step 3T/4 - 1, with two chunks also [T/8, T/4) and
+            # [3T/4, 7T/8) at 7T/8 - 1; the rest after the recurrence.  Beside the
+            # recurrence in mode 3; in the other modes the same bands after it, so
+            # every mode computes dX by the same products
+            two = _dx_split_chunks() == 2 and T >= 128
+            arrivals = N.query('asr_lstm_bwd_progress_arrivals', B, H) if mode == '3' else 0
+            # dX before the recurrence: its zero fill (non-identity maps) precedes
+            # the side stream's writes
+            ident = perm is None and t_mul == 1 and t_add == 0 and T == T_src and Din == Dsrc
+            dx_split = (torch.empty if ident else torch.zeros)(B, T_src, Dsrc,
+                                                               dtype=torch.float32, device=dev)
             if arrivals > 0:
-                # row bands by when their gate gradients are final: [T/4, 3T/4) at
-                # processing step 3T/4 - 1, with two chunks also [T/8, T/4) and
-                # [3T/4, 7T/8) at 7T/8 - 1; the rest after the recurrence
-                two = _dx_split_chunks() == 2 and T >= 128
                 split = (T // 4, _progress_counter(dev), int(arrivals), T // 8 if two else None)
-                # dX before the recurrence: its zero fill (non-identity maps) precedes
-                # the side stream's writes
-                ident = perm is None and t_mul == 1 and t_add == 0 and T == T_src and Din == Dsrc
-                dx_split = (torch.empty if ident else torch.zeros)(B, T_src, Dsrc,
-                                                                   dtype=torch.float32, device=dev)
+            else:
+                band_seq = (T // 4, T // 8 if two else None)
         try:
             if act.dtype == torch.float16:
                 # packed fp16 activations of asr_lstm_forward_xh: the tagged-granule
@@ -1472,7 +1478,8 @@ class BLSTMLayerFn(torch.autograd.Function):
                     first = split[1][1] + split[2]   # the arrivals this launch adds per step
                     split[1][1] += split[2] * (2 if split[3] is not None else 1)
                     split = split + ((first, split[1][1]), split_pre)
-                else:
+                elif split is not None:            # no report: the same bands after it
+                    band_seq = (split[0], split[3])
                     split = None
                 if not done:
                     a32 = torch.empty(B, T, 8 * H, dtype=torch.float32, device=dev)
@@ -1617,6 +1624,21 @@ class BLSTMLayerFn(torch.autograd.Function):
             finally:
                 N.call('asr_gemm_set_nosplit', 0)
             torch.cuda.current_stream(dev).wait_event(split_done)
+            dx = dx_split
+        elif band_seq is not None:
+            # the split's row bands in its order, on the compute stream
+            t0, t1 = band_seq
+            rows = lambda ta, tb: _dx_rows_problem(dg_op, w_op, dx_split, ctx, B, T, T_src, H,  # noqa: E731
+                                                   Din, Dp, Dsrc, perm, t_mul, t_add, ta, tb)
+            N.call('asr_gemm_set_nosplit', 1)
+            try:
+                run_gemm([rows(T // 4, T - T // 4)], dev)
+                if t1 is not None:
+                    run_gemm([rows(t1, t0), rows(T - t0, T - t1)], dev)
+                te = t1 if t1 is not None else t0
+                run_gemm([rows(0, te), rows(T - te, T)], dev)
+            finally:
+                N.call('asr_gemm_set_nosplit', 0)
             dx = dx_split
         elif ctx.needs_input_grad[0] and not pipelined:
             # dX [BT, Din] = dG [BT, 8H] W_ih [8H, Din], scattered back through the input map
@@ -1978,8 +2000,10 @@ def _dx_split_ok(ctx, B, T, dev, mode):
     their share of dX = dG W_ih runs on the weight-gradient side stream beside
     the last quarter of that recurrence, on the CUs it leaves free (mode 3);
     the outer rows follow on the compute stream.  Needs the packed-activation
-    tagged-granule backward (the one that reports progress)."""
-    return (os.environ.get('ASR_DX_SPLIT', '1') != '0' and mode == '3' and T >= 64
+    tagged-granule backward (the one that reports progress).  In the other
+    overlap modes the same row bands run after the recurrence, so dX is the
+    same arithmetic in every mode."""
+    return (os.environ.get('ASR_DX_SPLIT', '1') != '0' and T >= 64
             and compute_dtype() == BF16 and ctx.needs_input_grad[0])
 
 
