@@ -251,7 +251,7 @@ def _staged(t, rows, cols, ld=None):
 # the ones recorded at the optimizer step.  ASR_PARAM_SHADOW=0 turns it off.
 # ---------------------------------------------------------------------------
 _shadows = {}   # id(flat param tensor) -> _ParamShadow (tensors compare elementwise)
-SHADOW_STATS = {'hits': 0}               # BLSTM layer forwards that read the shadow
+SHADOW_STATS = {'hits': 0, 'linear_hits': 0}   # BLSTM / linear forwards that read the shadow
 
 
 class _ParamShadow:
@@ -290,9 +290,18 @@ def param_shadow_written(sh, flat, params):
 def _shadow_rows(w, params):
     """bf16 view of the shadow's copy of `w` (a dense view of a flat parameter
     buffer, spanning `params`), or None when there is no current shadow."""
-    flat = w._base
-    if flat is None or w.dtype != torch.float32 or not w.is_contiguous():
+    if w.dtype != torch.float32 or not w.is_contiguous():
         return None
+    flat = w._base
+    if flat is None:
+        # a module's nn.Parameter (its .data a slice of the flat buffer): the
+        # flat buffer by storage
+        sp = w.untyped_storage().data_ptr()
+        flat = next((sh.flat() for sh in _shadows.values()
+                     if sh.flat() is not None and sh.flat().untyped_storage().data_ptr() == sp),
+                    None)
+        if flat is None:
+            return None
     sh = _shadows.get(id(flat))
     if (sh is None or sh.flat() is not flat or sh.param_versions is None or
             flat._version != sh.flat_version):
@@ -354,9 +363,14 @@ def _linear_forward(x, weight, bias, drop, lse=None, ld=None):
         # fused_drop: K % 8 == 0, so Kp == K and the dropped copy is the operand
         xo = (convert_rows_bf16(x, rowmap(K), M, K, drop=drop) if fused_drop else
               _staged(x, M, K, Kp))
-        wo = torch.empty(Np, Kp, dtype=torch.bfloat16, device=x.device)
-        N.call('asr_convert_rows_bf16_ld', N.ptr(weight), rowmap(K), Nout, K, Kp, N.ptr(wo),
-               N.stream_handle(x.device))
+        # a dense weight (no padding) from the optimizer's bf16 shadow when current
+        wo = _shadow_rows(weight, (weight,)) if (Np == Nout and Kp == K) else None
+        if wo is not None:
+            SHADOW_STATS['linear_hits'] += 1
+        else:
+            wo = torch.empty(Np, Kp, dtype=torch.bfloat16, device=x.device)
+            N.call('asr_convert_rows_bf16_ld', N.ptr(weight), rowmap(K), Nout, K, Kp, N.ptr(wo),
+                   N.stream_handle(x.device))
         if Np > Nout:
             N.call('asr_convert_rows_bf16_ld', N.ptr(weight), rowmap(0, t_limit=1,
                    rows_per_b=Np - Nout, t_add=1), Np - Nout, Kp, Kp,
