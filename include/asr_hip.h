@@ -134,6 +134,9 @@ int asr_ctc_last_path(int* out2);
 /* Waves per direction of the last CTC forward's lattice (round 6): 1 = the
  * one-wave ctc_lattice, 2 / 4 = ctc_lattice_w (ASR_CTC_LATTICE_W=1 forces 1). */
 int asr_ctc_last_lattice_waves(void);
+/* Tag of the last GEMM launch (4 x kernel family + operand mode, the
+ * ASR_PTAG_GEMM_* families of csrc/prof.h): diagnostics, tools/gemm_log.py. */
+int asr_gemm_last_family(void);
 
 /* ---------------------------------------------------------------- GEMM
  * C(m,n) = alpha * sum_k A(m,k) B(n,k) + beta * C(m,n) + bias[n] + bias2[n]  (f32 C)

@@ -56,7 +56,10 @@ int prof_begin_launch(int kind, hipStream_t s, double work, int tag) {
   return slot;
 }
 
+int g_last_tag[ASR_PROF_NKINDS];   // the last launch's tag per kind, sampled or not
+
 void prof_set_tag(int kind, int slot, int tag) {
+  g_last_tag[kind] = tag;
   if (slot < 0) return;
   prof().k[kind].tag[slot] = tag;
 }
@@ -66,6 +69,10 @@ void prof_end_launch(int kind, int slot, hipStream_t s) {
   (void)hipEventRecord(prof().k[kind].ev[2 * slot + 1], s);
 }
 }  // namespace asr
+
+// Tag of the last GEMM launch from any host thread (4 x kernel family + mode,
+// csrc/prof.h ASR_PTAG_GEMM_*): diagnostics (tools/gemm_log.py).
+extern "C" int asr_gemm_last_family(void) { return asr::g_last_tag[ASR_PROF_GEMM]; }
 
 using namespace asr;
 
