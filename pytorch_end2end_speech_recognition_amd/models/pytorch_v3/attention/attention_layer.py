@@ -81,7 +81,7 @@ class AttentionMechanism(nn.Module):
         if torch.is_tensor(x_lens):
             lens = x_lens.reshape(-1).to(device=dev, dtype=torch.int32)
         else:
-            lens = torch.from_numpy(np.asarray(x_lens, np.int32).reshape(-1)).to(dev)
+            lens = ops.h2d(np.asarray(x_lens, np.int32).reshape(-1), dev)
         w_conv, conv_w = self.conv_weights()
         ctx, aw = ops.att_step(enc_out, enc_out_a.reshape(B, T, -1), lens,
                                dec_out.reshape(B, -1), aw_step.reshape(B, T),

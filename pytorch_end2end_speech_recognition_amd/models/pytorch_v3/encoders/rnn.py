@@ -173,7 +173,7 @@ class RNNEncoder(nn.Module):
 
         perm = np.argsort(-x_lens, kind='stable')                   # rnn.py:319-326
         lens = x_lens[perm]
-        perm_d = torch.from_numpy(perm.astype(np.int32)).to(dev, non_blocking=True)
+        perm_d = ops.h2d(perm.astype(np.int32), dev)
         T = int(lens.max())                                          # pad_packed length
         h, pm, t_mul, t_add, concat = xs.contiguous(), perm_d, 1, 0, False
         h_sub = lens_sub = None
@@ -191,7 +191,7 @@ class RNNEncoder(nn.Module):
             # layer subsamples), not one per layer on the compute stream
             if lens_key is None or not np.array_equal(lens_key, lens):
                 lens_key = lens.copy()
-                lens_d = torch.from_numpy(lens.astype(np.int32)).to(dev, non_blocking=True)
+                lens_d = ops.h2d(lens.astype(np.int32), dev)
             graph = tuple(p for pair in self._layer_params(l) for p in pair)
             if self.rnn_type == 'gru':
                 if pending is not None:
@@ -259,10 +259,10 @@ class RNNEncoder(nn.Module):
         assert t_mul == 1
         self.last_lens_np = lens.astype(np.int32)
         self.last_perm_np = perm.astype(np.int64)
-        out_lens = torch.from_numpy(self.last_lens_np).to(dev, non_blocking=True)
-        perm_idx = torch.from_numpy(self.last_perm_np).to(dev, non_blocking=True)
+        out_lens = ops.h2d(self.last_lens_np, dev)
+        perm_idx = ops.h2d(self.last_perm_np, dev)
         if self.num_layers_sub >= 1:                              # rnn.py:479-487
             self.last_lens_sub_np = lens_sub
-            lens_sub_d = torch.from_numpy(lens_sub).to(dev, non_blocking=True)
+            lens_sub_d = ops.h2d(lens_sub, dev)
             return h, out_lens, h_sub, lens_sub_d, perm_idx
         return h, out_lens, perm_idx

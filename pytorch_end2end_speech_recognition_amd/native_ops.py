@@ -38,6 +38,21 @@ def _ws(nbytes, device):
     return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
 
 
+def h2d(a, device):
+    """Host array -> device tensor without blocking the host: staged through
+    pinned memory (torch's caching host allocator keeps the block until the
+    copy has run).  A copy from pageable memory waits for the stream to reach
+    it, i.e. for the work already queued -- the host then falls behind the
+    GPU and the next kernels launch into an idle queue."""
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if _H2D_PINNED:
+        t = t.pin_memory()
+    return t.to(device, non_blocking=True)
+
+
+_H2D_PINNED = os.environ.get('ASR_H2D_PINNED', '1') != '0'   # (A/B: 0 = pageable copies)
+
+
 # ---------------------------------------------------------------------------
 # Per-step recurrence workspace arena.  Every tagged-granule launch needs its
 # granule workspace zero (lstm_xg.hip); instead of one memset launch before
@@ -2347,8 +2362,8 @@ class EmbeddingFn(torch.autograd.Function):
             starts = np.zeros(V + 1, np.int32)
             np.cumsum(np.bincount(flat, minlength=V), out=starts[1:])
             dev = idx.device
-            order_d = torch.from_numpy(order).to(dev, non_blocking=True)
-            starts_d = torch.from_numpy(starts).to(dev, non_blocking=True)
+            order_d = h2d(order, dev)
+            starts_d = h2d(starts, dev)
             N.call('asr_embedding_backward_csr', N.ptr(order_d), N.ptr(starts_d), N.ptr(dout), V,
                    E, int(trans), pad, N.ptr(grad_buffer(weight)), N.stream_handle(dev))
         else:
