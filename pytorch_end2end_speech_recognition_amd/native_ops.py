@@ -798,6 +798,7 @@ class LinearExFn(torch.autograd.Function):
         run_gemm([p], x.device)
         ctx.save_for_backward(x, weight)
         ctx.meta = (bias, bias2, c0, K, t_index, M, amap, a_off)
+        ctx.beside = _beside_plan[0]
         return y
 
     @staticmethod
@@ -813,6 +814,24 @@ class LinearExFn(torch.autograd.Function):
             probs.append(gemm_problem(operand(dy, 0, rowmap(Nout)),
                                       operand(weight, 1, rowmap(ldw), offset=c0), dx, amap, M, K,
                                       Nout, c_offset=a_off))
+
+        def wgrad():
+            run_gemm([gemm_problem(operand(dy, 1, rowmap(Nout)), operand(x, 1, amap, offset=a_off),
+                                   grad_buffer(weight), rowmap(ldw), Nout, K, M, beta=1.0,
+                                   c_offset=c0)], x.device)
+            if bias is not None:
+                colsum_accumulate(dy.view(M, Nout), grad_buffer(bias),
+                                  grad_buffer(bias2) if bias2 is not None else None)
+
+        if ctx.beside is not None:
+            # the weight / bias gradients beside the encoder's top backward
+            # recurrence (as LinearFn's), only dX on the compute stream
+            if probs:
+                run_gemm(probs, x.device)
+            gb = tuple(grad_buffer(t) for t in (weight, bias, bias2) if t is not None)
+            if not _wgrad_beside(dy.device, ctx.beside, wgrad, (x, dy), gb):
+                wgrad()
+            return dx, None, None, None, None, None, None
         probs.append(gemm_problem(operand(dy, 1, rowmap(Nout)), operand(x, 1, amap, offset=a_off),
                                   grad_buffer(weight), rowmap(ldw), Nout, K, M, beta=1.0,
                                   c_offset=c0))
@@ -2348,6 +2367,7 @@ class EmbeddingFn(torch.autograd.Function):
                N.ptr(out), N.stream_handle(idx.device))
         ctx.save_for_backward(idx, weight)
         ctx.meta = (trans, padding_idx, V, E, idx_host)
+        ctx.beside = _beside_plan[0]
         return out
 
     @staticmethod
@@ -2356,19 +2376,30 @@ class EmbeddingFn(torch.autograd.Function):
         trans, padding_idx, V, E, idx_host = ctx.meta
         dout = dout.contiguous()
         pad = -1 if padding_idx is None else int(padding_idx)
+        dev = idx.device
         if idx_host is not None:
             flat = np.clip(np.asarray(idx_host, np.int64).reshape(-1), 0, V - 1)
             order = np.argsort(flat, kind='stable').astype(np.int32)
             starts = np.zeros(V + 1, np.int32)
             np.cumsum(np.bincount(flat, minlength=V), out=starts[1:])
-            dev = idx.device
             order_d = h2d(order, dev)
             starts_d = h2d(starts, dev)
-            N.call('asr_embedding_backward_csr', N.ptr(order_d), N.ptr(starts_d), N.ptr(dout), V,
-                   E, int(trans), pad, N.ptr(grad_buffer(weight)), N.stream_handle(dev))
+
+            def wgrad():
+                N.call('asr_embedding_backward_csr', N.ptr(order_d), N.ptr(starts_d), N.ptr(dout),
+                       V, E, int(trans), pad, N.ptr(grad_buffer(weight)), N.stream_handle(dev))
+            keep = (order_d, starts_d, dout)
         else:
-            N.call('asr_embedding_backward', N.ptr(idx), N.ptr(dout), idx.numel(), V, E,
-                   int(trans), pad, N.ptr(grad_buffer(weight)), N.stream_handle(idx.device))
+            def wgrad():
+                N.call('asr_embedding_backward', N.ptr(idx), N.ptr(dout), idx.numel(), V, E,
+                       int(trans), pad, N.ptr(grad_buffer(weight)), N.stream_handle(dev))
+            keep = (idx, dout)
+        # the embedding gradient has no consumer but the optimizer: beside the
+        # encoder's top backward recurrence when the decoder is built under
+        # wgrad_beside_encoder
+        if ctx.beside is None or not _wgrad_beside(dev, ctx.beside, wgrad, keep,
+                                                   (grad_buffer(weight),)):
+            wgrad()
         return None, None, None, None, None
 
 
