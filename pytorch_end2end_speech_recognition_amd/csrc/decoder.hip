@@ -2215,6 +2215,7 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
         }
       }
       __syncthreads();
+      PD_TR(18);
       {
         // d aw_{t-1}[j] = sum_c sum_k dF[j - k + half, c] cw[c, k] (dF window row
         // j + K - 1 - k): (channel, 4 frames, K quarter) per item with a sliding
@@ -2281,6 +2282,7 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
         }
       }
       __syncthreads();
+      PD_TR(19);
       {
         const int FCH4 = ((FCH + 3) / 4) * 4;
         for (int i = tid; i < FCH; i += PD_THREADS) {
@@ -2291,6 +2293,7 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
         }
       }
       __syncthreads();
+      PD_TR(27);
     }
     // before the wait (forward outputs, no hand-off): d_ctx_in, aw_t of the
     // chunk, the aw_{t-1} window, W_dec h_t, in one batch of loads; the conv
@@ -2326,9 +2329,11 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
         }
       }
       __syncthreads();
+      PD_TR(28);
       if (t > 0) pd_conv_feat(&L[G.cw], &L[G.awin], C, d.K, FCH, &L[G.un], &L[G.f], G.FS, G.KP);
       else
         for (int i = tid; i < FCH * G.FS; i += PD_THREADS) L[G.f + i] = 0.f;
+      PD_TR(29);
     }
     PB_WAIT();
     PD_TR(52);

@@ -50,3 +50,4 @@ ph('persist_bwd G', [57, 58, 59, 60, 61])
 ph('persist_bwd step', [48, 51, 54, 57, 61])
 ph('persist_bwd F in', [55, 0, 1, 2, 3, 4, 56])
 ph('persist_bwd G in', [59, 10, 11, 12, 13, 14, 60])
+ph('persist_bwd E in', [51, 18, 10, 19, 27, 28, 29, 52])
