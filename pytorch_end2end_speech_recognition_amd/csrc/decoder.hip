@@ -2127,8 +2127,26 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
     const bool has_r = t + 1 < d.S;
     PD_TR(48);
     // ================= H: r = dgates_{t+1} Wcat (this member's columns) =================
+    // the dF window phase E reads (written by the previous step's F phase,
+    // complete once H's wait has passed): loaded right after that wait, so
+    // its latency passes behind H
+    constexpr int PB_DFR = 5;   // registers per thread (8 + KW) C <= 5 x 512 (production 2400)
+    // (the bf16 production geometry only: the f32 and runtime-geometry
+    // instantiations have no registers to spare)
+    constexpr bool PB_PREF = !F32 && SE != 0;
+    const bool dfpre = PB_PREF && fact && has_r && (8 + KW) * C <= PB_DFR * PD_THREADS;
+    float dfv[PB_DFR];
     if (has_r) {
       PB_WAIT();
+      if (dfpre) {
+#pragma unroll
+        for (int j = 0; j < PB_DFR; ++j) {
+          const int i = tid + j * PD_THREADS;
+          const int row = i / C - 8, c = i % C, tt = tt0 - half + row;
+          dfv[j] = (i < (8 + KW) * C && row >= 0 && tt >= 0 && tt < d.T)
+                       ? pd_ld(rf, ((long long)be * d.T + tt) * d.C + c) : 0.f;
+        }
+      }
       PD_TR(49);
       uint16_t* dgs = reinterpret_cast<uint16_t*>(&L[G.dgs]);
       const int nv = G4 / 4;
@@ -2201,6 +2219,32 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
     PD_TR(51);
 
     // ================= E: d ctx_t, d aw_t, softmax chunk sums; conv features =================
+    // this step's forward outputs (no hand-off: d_ctx_in, aw_t of the chunk, the
+    // aw_{t-1} window, W_dec h_t) are loaded first, so their latency passes
+    // behind the conv transpose below; they go to LDS after it (its aw window
+    // of step t + 1 is still in use until then)
+    const int pn1 = d.E, pn2 = pn1 + FCH, pn3 = pn2 + KW, ptotal = pn3 + d.A;
+    const long long pst = (long long)be * d.S + t;
+    auto pre_load = [&](int base, float (&v)[4]) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int i = base + j * PD_THREADS + tid;
+        float x = 0.f;
+        if (i < pn1) {
+          x = d_ctx_in[pst * d.E + i];
+        } else if (i < pn2) {
+          if (i - pn1 < nfr) x = aw_all[pst * d.T + tt0 + (i - pn1)];
+        } else if (i < pn3) {
+          const int tt = tt0 - half + (i - pn2);
+          if (t > 0 && tt >= 0 && tt < d.T) x = aw_all[(pst - 1) * d.T + tt];
+        } else if (i < ptotal) {
+          x = wd_all[pst * d.A + (i - pn3)];
+        }
+        v[j] = x;
+      }
+    };
+    float pv0[4] = {0.f, 0.f, 0.f, 0.f};
+    if (PB_PREF && fact) pre_load(0, pv0);
     // the previous step's (t + 1) conv transpose -> d aw_t carry and conv-kernel
     // tiles, moved here from its G phase: they feed only this phase's d aw, so
     // they run beside this phase's wait instead of on the dgates hand-off
@@ -2208,10 +2252,18 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
     // aw_t window of step t + 1 is still in `awin` (reloaded below).
     if (fact && has_r) {
       {   // dF window rows [tt0 - half, tt0 + FCH + half) after 8 zero rows
-        for (int i = tid; i < (8 + KW) * C; i += PD_THREADS) {
-          const int row = i / C - 8, c = i % C, tt = tt0 - half + row;
-          L[G.un + i] = (row >= 0 && tt >= 0 && tt < d.T)
-                            ? pd_ld(rf, ((long long)be * d.T + tt) * d.C + c) : 0.f;
+        if (dfpre) {
+#pragma unroll
+          for (int j = 0; j < PB_DFR; ++j) {
+            const int i = tid + j * PD_THREADS;
+            if (i < (8 + KW) * C) L[G.un + i] = dfv[j];
+          }
+        } else {
+          for (int i = tid; i < (8 + KW) * C; i += PD_THREADS) {
+            const int row = i / C - 8, c = i % C, tt = tt0 - half + row;
+            L[G.un + i] = (row >= 0 && tt >= 0 && tt < d.T)
+                              ? pd_ld(rf, ((long long)be * d.T + tt) * d.C + c) : 0.f;
+          }
         }
       }
       __syncthreads();
@@ -2299,33 +2351,21 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
     // chunk, the aw_{t-1} window, W_dec h_t, in one batch of loads; the conv
     // features of aw_{t-1}
     if (fact) {
-      const int n1 = d.E, n2 = n1 + FCH, n3 = n2 + KW, total = n3 + d.A;
-      const long long st = (long long)be * d.S + t;
-      for (int base = 0; base < total; base += 4 * PD_THREADS) {
+      for (int base = 0; base < ptotal; base += 4 * PD_THREADS) {
         float v[4];
+        if (PB_PREF && base == 0) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int i = base + j * PD_THREADS + tid;
-          float x = 0.f;
-          if (i < n1) {
-            x = d_ctx_in[st * d.E + i];
-          } else if (i < n2) {
-            if (i - n1 < nfr) x = aw_all[st * d.T + tt0 + (i - n1)];
-          } else if (i < n3) {
-            const int tt = tt0 - half + (i - n2);
-            if (t > 0 && tt >= 0 && tt < d.T) x = aw_all[(st - 1) * d.T + tt];
-          } else if (i < total) {
-            x = wd_all[st * d.A + (i - n3)];
-          }
-          v[j] = x;
+          for (int j = 0; j < 4; ++j) v[j] = pv0[j];
+        } else {
+          pre_load(base, v);
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int i = base + j * PD_THREADS + tid;
-          if (i < n1) L[G.dct + i] = v[j];
-          else if (i < n2) L[G.awt + i - n1] = v[j];
-          else if (i < n3) L[G.awin + i - n2] = v[j];
-          else if (i < total) L[G.wd + i - n3] = v[j];
+          if (i < pn1) L[G.dct + i] = v[j];
+          else if (i < pn2) L[G.awt + i - pn1] = v[j];
+          else if (i < pn3) L[G.awin + i - pn2] = v[j];
+          else if (i < ptotal) L[G.wd + i - pn3] = v[j];
         }
       }
       __syncthreads();
