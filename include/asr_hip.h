@@ -651,6 +651,14 @@ int asr_attdec_last_launch(int* out4);
  * persistent launch (bf16, B <= 32, no scheduled sampling; ASR_ATT_PERSIST=0
  * disables it). */
 int asr_attdec_persist_last(int* out2);
+/* Round 6: the conv features of every decoder step kept by the next
+ * persistent forward pass from this host thread and read back by the next
+ * persistent backward pass (instead of recomputing them from aw); buf holds
+ * asr_attdec_conv_feat_bytes(dims) bytes, NULL turns it off.  The caller sets
+ * it before each pass and resets it after; a backward may only be given the
+ * buffer of a forward that ran persistent (asr_attdec_persist_last). */
+int asr_attdec_set_conv_feat(float* buf);
+size_t asr_attdec_conv_feat_bytes(const asr_attdec_dims_t* dims);
 int asr_attdec_backward_ex(const asr_attdec_dims_t* dims, const asr_attdec_opts_t* opts,
                            int compute_dtype, const float* enc, const float* enc_a,
                            const int32_t* lens, const float* w_ih_ctx, long long ld_ih,

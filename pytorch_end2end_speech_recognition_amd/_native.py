@@ -223,6 +223,8 @@ SIGNATURES = {
     'asr_ctc_last_path': (c_int, [c_vp]),
     'asr_ctc_last_lattice_waves': (c_int, []),
     'asr_gemm_last_family': (c_int, []),
+    'asr_attdec_set_conv_feat': (c_int, [c_vp]),
+    'asr_attdec_conv_feat_bytes': (c_size, [c_vp]),
     'asr_lstm_set_bwd_progress': (c_int, [c_vp, c_int]),
     'asr_lstm_set_bwd_progress2': (c_int, [c_vp, c_int, c_int]),
     'asr_lstm_ws_prezeroed': (c_int, [c_int]),

@@ -1188,6 +1188,11 @@ struct PdSs {
 };
 static_assert(sizeof(PdSs) <= 512, "AttWs::ssd holds one PdSs");
 
+// asr_attdec_set_conv_feat: the next persistent decoder pass from this host
+// thread writes (forward) / reads (backward) the conv features of every step
+// here ([B][S][8 chunks][FCH][FS] f32), NULL: recomputed in the backward.
+thread_local float* g_pd_fsave = nullptr;
+
 // Host staging of the PdSs records: a ring of pinned slots, each reused only
 // after the copy that read it has completed (its event).
 int pd_ss_upload(const PdSs& v, void* dst, hipStream_t s) {
@@ -1280,7 +1285,8 @@ __host__ __device__ inline PdSsGeom pd_ss_geom(const Dims& d, int base, int UPW,
 // window load and one kernel load per lane per 4 taps, against two LDS loads
 // per tap of a dot-product loop.
 __device__ __forceinline__ void pd_conv_feat(const float* cw, const float* win, int C, int K,
-                                             int FCH, float* part, float* f, int fs, int ks) {
+                                             int FCH, float* part, float* f, int fs, int ks,
+                                             float* gout = nullptr) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int MT = FCH <= 16 ? 1 : FCH <= 32 ? 2 : 4;
   const int KP = 8 / MT;
@@ -1313,6 +1319,7 @@ __device__ __forceinline__ void pd_conv_feat(const float* cw, const float* win, 
     if (c < C)
       for (int q = 0; q < KP; ++q) v += part[((q * MT + tl) * 16 + rr) * 16 + c];
     f[i] = v;
+    if (gout) gout[i] = v;   // (the forward keeps them for the backward pass)
   }
 }
 
@@ -1379,7 +1386,7 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
     const float* __restrict__ vw, float* __restrict__ dec, float* __restrict__ c_all,
     float* __restrict__ gates, float* x, float* __restrict__ ctx_all,
     float* __restrict__ aw_all, float* pbuf, float* ebuf, int* ctr, int* status, float drop_h,
-    unsigned long long seed_h, const PdSs* __restrict__ ssp) {
+    unsigned long long seed_h, const PdSs* __restrict__ ssp, float* __restrict__ fsave) {
   extern __shared__ __attribute__((aligned(16))) float L[];
   Dims d = dd;
   if (CC) d.C = CC;
@@ -1767,7 +1774,9 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_fwd_persist(
     PD_TR(37);
     // conv features of aw_{t-1} for this chunk (local data: before the wait)
     if (fact && t > 0)
-      pd_conv_feat(&L[G.cw], &L[G.awp + tt0], C, d.K, FCH, &L[G.mp], &L[G.f], G.FS, d.K);
+      pd_conv_feat(&L[G.cw], &L[G.awp + tt0], C, d.K, FCH, &L[G.mp], &L[G.f], G.FS, d.K,
+                   fsave ? fsave + (((long long)be * d.S + t) * PD_CHUNKS + ch) * FCH * G.FS
+                         : nullptr);
 
     // ================= E: energies of this work-group's frame chunk =================
     if (tid == 0) s_ok = pd_wait(my_ctr, PD_MEMBERS * (3 * t + 1), ctr, status);
@@ -2008,7 +2017,7 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
     float* __restrict__ d_enc_a, float* __restrict__ d_h0, float* __restrict__ dwd_all,
     float* __restrict__ dv_part, float* __restrict__ dwc_part, float* __restrict__ dcw_part,
     float* rbuf, float* sbuf, float* dwdc, float* dFbuf, int* ctr, int* status, float drop_h,
-    unsigned long long seed_h) {
+    unsigned long long seed_h, const float* __restrict__ fsave) {
   extern __shared__ __attribute__((aligned(16))) float L[];
   Dims d = dd;
   if (CC) d.C = CC;
@@ -2245,6 +2254,12 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
     };
     float pv0[4] = {0.f, 0.f, 0.f, 0.f};
     if (PB_PREF && fact) pre_load(0, pv0);
+    // the conv features of aw_{t-1}: kept by the forward pass (fsave) instead
+    // of recomputed (the same pd_conv_feat on the same aw values: bitwise)
+    const float* fsv = fsave ? fsave + (((long long)be * d.S + t) * PD_CHUNKS + ch) * FCH * G.FS
+                             : nullptr;
+    const bool fpre = PB_PREF && fsv && fact && t > 0 && FCH * G.FS <= PD_THREADS;
+    const float fv0 = (fpre && tid < FCH * G.FS) ? fsv[tid] : 0.f;
     // the previous step's (t + 1) conv transpose -> d aw_t carry and conv-kernel
     // tiles, moved here from its G phase: they feed only this phase's d aw, so
     // they run beside this phase's wait instead of on the dgates hand-off
@@ -2370,9 +2385,15 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
       }
       __syncthreads();
       PD_TR(28);
-      if (t > 0) pd_conv_feat(&L[G.cw], &L[G.awin], C, d.K, FCH, &L[G.un], &L[G.f], G.FS, G.KP);
-      else
+      if (t > 0 && fpre) {
+        if (tid < FCH * G.FS) L[G.f + tid] = fv0;
+      } else if (t > 0 && fsv) {
+        for (int i = tid; i < FCH * G.FS; i += PD_THREADS) L[G.f + i] = fsv[i];
+      } else if (t > 0) {
+        pd_conv_feat(&L[G.cw], &L[G.awin], C, d.K, FCH, &L[G.un], &L[G.f], G.FS, G.KP);
+      } else {
         for (int i = tid; i < FCH * G.FS; i += PD_THREADS) L[G.f + i] = 0.f;
+      }
       PD_TR(29);
     }
     PB_WAIT();
@@ -2925,7 +2946,7 @@ extern "C" int asr_attdec_forward_ex(const asr_attdec_dims_t* dims, const asr_at
   hipLaunchKernelGGL((attdec_fwd_persist<CC, NQ, SA, SE, SD, SK, F>), grid, dim3(PD_THREADS), lds,  \
                      s, d, (const void*)workspace, pre_emb, h0, enc, enc_a, lens, w_dec, w_conv,  \
                      conv_w, v, dec, c_all, gates, x, ctx_all, aw_all, pbuf, ebuf, ctr,          \
-                     lstm_persist_status_word(), drop_h, seed_h, ssdev)
+                     lstm_persist_status_word(), drop_h, seed_h, ssdev, g_pd_fsave)
 #define ASR_PD(CC, NQ, SA, SE, SD, SK)                  \
   do {                                                  \
     if (bf) ASR_PD2(CC, NQ, SA, SE, SD, SK, false);     \
@@ -2985,6 +3006,20 @@ extern "C" int asr_attdec_persist_last(int* out2) {
   out2[0] = g_att_persist_last[0];
   out2[1] = g_att_persist_last[1];
   return ASR_OK;
+}
+
+// The conv-feature buffer of the next persistent decoder pass from this host
+// thread (NULL: none); asr_attdec_conv_feat_bytes: its size for dims.
+extern "C" int asr_attdec_set_conv_feat(float* buf) {
+  g_pd_fsave = buf;
+  return ASR_OK;
+}
+
+extern "C" size_t asr_attdec_conv_feat_bytes(const asr_attdec_dims_t* dims) {
+  if (!dims || dims->B <= 0 || dims->S <= 0 || dims->T <= 0) return 0;
+  const size_t fch = (size_t)(dims->T + PD_CHUNKS - 1) / PD_CHUNKS;
+  const size_t fs = (size_t)((dims->C + 3) & ~3);
+  return (size_t)dims->B * dims->S * PD_CHUNKS * fch * fs * sizeof(float);
 }
 
 extern "C" int asr_attdec_last_launch(int* out4) {
@@ -3100,7 +3135,7 @@ extern "C" int asr_attdec_backward_ex(const asr_attdec_dims_t* dims, const asr_a
                      s, d, (const void*)wcatT, enc, enc_a, lens, w_dec, w_conv, conv_w, v, c_all, \
                      aw_all, wd_all, d_dec_in, d_ctx_in, gates_dg, dctx_tot, d_enc_a, d_h0,      \
                      dwd_all, dv_part, dwc_part, dcw_part, r, sbuf, dwd_chunk, dFbuf, ctr,       \
-                     lstm_persist_status_word(), drop_h, seed_h)
+                     lstm_persist_status_word(), drop_h, seed_h, (const float*)g_pd_fsave)
 #define ASR_PB(CC, NQ, SA, SE, SD, SK)                  \
   do {                                                  \
     if (bf) ASR_PB2(CC, NQ, SA, SE, SD, SK, false);     \

@@ -932,7 +932,7 @@ def linear2(x1, w1, b1, x2, w2, b2):
 # Teacher-forced location-attention decoder loop (attention_seq2seq.py:704-799)
 # ---------------------------------------------------------------------------
 def _attdec_forward(enc, enc_a, lens, pre_emb, h0, emb_dim, sharpen, sigmoid, w_ih, w_hh, w_dec,
-                    w_conv, conv_w, v, train_opts):
+                    w_conv, conv_w, v, train_opts, keep_feat=False):
     """One asr_attdec_forward_ex call over S = pre_emb.shape[1] steps.  Returns
     (dims, (dec, cst, gates, x, ctx, aw), opts, buffers kept alive)."""
     N.require_device(enc, enc_a, lens, pre_emb, w_ih)
@@ -956,12 +956,28 @@ def _attdec_forward(enc, enc_a, lens, pre_emb, h0, emb_dim, sharpen, sigmoid, w_
     ld_ih = w_ih.shape[1]
     w_ih_ctx = ctypes.c_void_p(w_ih.data_ptr() + 4 * emb_dim)
     opts, keep = _attdec_opts(train_opts, B, S, D, emb_dim, w_ih, dev)
-    N.call('asr_attdec_forward_ex', ctypes.byref(dims), N.ptr_struct(opts), cd, N.ptr(enc),
-           N.ptr(enc_a), N.ptr(lens), w_ih_ctx, ld_ih, N.ptr(w_hh), N.ptr(w_dec),
-           N.ptr(w_conv), N.ptr(conv_w), N.ptr(v), N.ptr(pre_emb),
-           N.ptr(h0.contiguous() if h0 is not None else None), N.ptr(dec), N.ptr(cst),
-           N.ptr(gates), N.ptr(x), N.ptr(ctxv), N.ptr(aw), N.ptr(ws), nb,
-           N.stream_handle(dev))
+    # a backward will follow: the persistent pass keeps every step's conv
+    # features for it (asr_attdec_set_conv_feat; ASR_ATT_CONV_FEAT=0: recomputed)
+    feat = None
+    if keep_feat and os.environ.get('ASR_ATT_CONV_FEAT', '1') != '0':
+        fb = N.query('asr_attdec_conv_feat_bytes', ctypes.byref(dims))
+        feat = torch.empty(max(int(fb) // 4, 1), dtype=torch.float32, device=dev)
+        N.call('asr_attdec_set_conv_feat', N.ptr(feat))
+    try:
+        N.call('asr_attdec_forward_ex', ctypes.byref(dims), N.ptr_struct(opts), cd, N.ptr(enc),
+               N.ptr(enc_a), N.ptr(lens), w_ih_ctx, ld_ih, N.ptr(w_hh), N.ptr(w_dec),
+               N.ptr(w_conv), N.ptr(conv_w), N.ptr(v), N.ptr(pre_emb),
+               N.ptr(h0.contiguous() if h0 is not None else None), N.ptr(dec), N.ptr(cst),
+               N.ptr(gates), N.ptr(x), N.ptr(ctxv), N.ptr(aw), N.ptr(ws), nb,
+               N.stream_handle(dev))
+    finally:
+        if feat is not None:
+            N.call('asr_attdec_set_conv_feat', None)
+    if feat is not None:
+        ran = (ctypes.c_int * 2)()
+        N.call("asr_attdec_persist_last", ctypes.cast(ran, ctypes.c_void_p))
+        if ran[0] == 1:          # written only by the persistent forward pass
+            keep['conv_feat'] = feat
     return dims, (dec, cst, gates, x, ctxv, aw), opts, keep
 
 
@@ -1011,7 +1027,7 @@ class AttDecoderFn(torch.autograd.Function):
         enc, enc_a, pre_emb = enc.contiguous(), enc_a.contiguous(), pre_emb.contiguous()
         dims, (dec, cst, gates, x, ctxv, aw), opts, keep = _attdec_forward(
             enc, enc_a, lens, pre_emb, h0, emb_dim, sharpen, sigmoid, w_ih, w_hh, w_dec, w_conv,
-            conv_w, v, train_opts)
+            conv_w, v, train_opts, keep_feat=any(ctx.needs_input_grad))
         ctx.save_for_backward(enc, enc_a, lens, w_ih, w_hh, w_dec, w_conv, conv_w, v, dec, cst,
                               gates, x, aw)
         _last_sampled['tok'] = keep.get('tok_ss')
@@ -1049,12 +1065,19 @@ class AttDecoderFn(torch.autograd.Function):
             d_pre = torch.empty(B, S, 4 * D, **f32)
             dg_ss = torch.empty(B, S, 4 * D, **f32)
             opts.d_pre, opts.dg_ss = d_pre.data_ptr(), dg_ss.data_ptr()
-        N.call('asr_attdec_backward_ex', ctypes.byref(dims), N.ptr_struct(opts), cd, N.ptr(enc),
-               N.ptr(enc_a), N.ptr(lens), w_ih_ctx, ld_ih, N.ptr(w_hh), N.ptr(w_dec),
-               N.ptr(w_conv), N.ptr(conv_w), N.ptr(v), N.ptr(dec), N.ptr(cst), N.ptr(aw),
-               N.ptr(d_dec), N.ptr(d_ctx), N.ptr(gates), N.ptr(dctx_tot), N.ptr(d_enc_a),
-               N.ptr(d_h0), N.ptr(dwd), N.ptr(dv_part), N.ptr(dwc_part), N.ptr(dcw_part),
-               N.ptr(ws), nb, N.stream_handle(dev))
+        feat = keep.get('conv_feat')
+        if feat is not None:
+            N.call('asr_attdec_set_conv_feat', N.ptr(feat))
+        try:
+            N.call('asr_attdec_backward_ex', ctypes.byref(dims), N.ptr_struct(opts), cd,
+                   N.ptr(enc), N.ptr(enc_a), N.ptr(lens), w_ih_ctx, ld_ih, N.ptr(w_hh),
+                   N.ptr(w_dec), N.ptr(w_conv), N.ptr(conv_w), N.ptr(v), N.ptr(dec), N.ptr(cst),
+                   N.ptr(aw), N.ptr(d_dec), N.ptr(d_ctx), N.ptr(gates), N.ptr(dctx_tot),
+                   N.ptr(d_enc_a), N.ptr(d_h0), N.ptr(dwd), N.ptr(dv_part), N.ptr(dwc_part),
+                   N.ptr(dcw_part), N.ptr(ws), nb, N.stream_handle(dev))
+        finally:
+            if feat is not None:
+                N.call('asr_attdec_set_conv_feat', None)
         dg = gates                          # dgates (row t = 0 is zero)
         d_pre_out = dg
         if sampled:

@@ -194,6 +194,25 @@ def test_decoder_weight_gradients_beside_encoder_bitwise(name, cuda_dev, monkeyp
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('prec', ['bf16', 'fp32'])
+def test_saved_conv_features_bitwise(prec, cuda_dev, monkeypatch):
+    """Round 6: the persistent forward keeps every step's conv features and
+    the persistent backward reads them (asr_attdec_set_conv_feat) instead of
+    recomputing them from aw -- the same pd_conv_feat on the same values, so
+    the loss and every gradient are bitwise those of the recomputing pass
+    (ASR_ATT_CONV_FEAT=0), at the production hybrid shape."""
+    out = {}
+    for on in ('1', '0'):
+        monkeypatch.setenv('ASR_ATT_CONV_FEAT', on)
+        _, loss, grads, launch = _gpu_run('model_att_prod_hybrid', prec, cuda_dev)
+        assert launch[4:] == [1, 1], launch
+        out[on] = (loss, grads)
+    assert out['1'][0] == out['0'][0]
+    for k in out['0'][1]:
+        np.testing.assert_array_equal(out['1'][1][k], out['0'][1][k], err_msg=k)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize('ss_prob', [0.5, 1.0])
 def test_prod_scheduled_sampling_persistent_fp32_vs_oracle(ss_prob, cuda_dev):
     """scheduled sampling (attention_seq2seq.py:742-748) INSIDE
