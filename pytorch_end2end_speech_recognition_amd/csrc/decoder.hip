@@ -2005,7 +2005,7 @@ __host__ __device__ inline PbGeom pb_geom(const Dims& d, bool f32 = false) {
 // F32 (fp32 mode): Wcat^T and dgates in f32, r on v_mfma_f32_16x16x4_f32 (each
 // wave holds its column tile's K quarter as f32 fragments: k-step s of the
 // quarter is k = 4 (kq KQ32 + s) + lane / 16).
-template <int CC, int NQ, int SA, int SE, int SD, int SK, bool F32 = false>
+template <int CC, int NQ, int SA, int SE, int SD, int SK, bool F32 = false, bool FS = false>
 __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
     Dims dd, const void* __restrict__ wcatT_v, const float* __restrict__ enc,
     const float* __restrict__ enc_a, const int32_t* __restrict__ lens,
@@ -2256,9 +2256,11 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
     if (PB_PREF && fact) pre_load(0, pv0);
     // the conv features of aw_{t-1}: kept by the forward pass (fsave) instead
     // of recomputed (the same pd_conv_feat on the same aw values: bitwise)
-    const float* fsv = fsave ? fsave + (((long long)be * d.S + t) * PD_CHUNKS + ch) * FCH * G.FS
-                             : nullptr;
-    const bool fpre = PB_PREF && fsv && fact && t > 0 && FCH * G.FS <= PD_THREADS;
+    // (FS: a separate instantiation -- the load and the recompute paths in one
+    // kernel cost the production bf16 kernel a 12-B spill, +4.6 ms / att step)
+    const float* fsv = FS ? fsave + (((long long)be * d.S + t) * PD_CHUNKS + ch) * FCH * G.FS
+                          : nullptr;
+    const bool fpre = PB_PREF && FS && fact && t > 0 && FCH * G.FS <= PD_THREADS;
     const float fv0 = (fpre && tid < FCH * G.FS) ? fsv[tid] : 0.f;
     // the previous step's (t + 1) conv transpose -> d aw_t carry and conv-kernel
     // tiles, moved here from its G phase: they feed only this phase's d aw, so
@@ -2387,9 +2389,9 @@ __global__ void __launch_bounds__(PD_THREADS) attdec_bwd_persist(
       PD_TR(28);
       if (t > 0 && fpre) {
         if (tid < FCH * G.FS) L[G.f + tid] = fv0;
-      } else if (t > 0 && fsv) {
+      } else if (FS && t > 0) {
         for (int i = tid; i < FCH * G.FS; i += PD_THREADS) L[G.f + i] = fsv[i];
-      } else if (t > 0) {
+      } else if (!FS && t > 0) {
         pd_conv_feat(&L[G.cw], &L[G.awin], C, d.K, FCH, &L[G.un], &L[G.f], G.FS, G.KP);
       } else {
         for (int i = tid; i < FCH * G.FS; i += PD_THREADS) L[G.f + i] = 0.f;
@@ -3130,12 +3132,18 @@ extern "C" int asr_attdec_backward_ex(const asr_attdec_dims_t* dims, const asr_a
     const size_t lds = (size_t)PG.total * 4;
     const dim3 grid(PD_GROUPS * PD_MEMBERS);
     const int pslot = prof_begin_launch(ASR_PROF_ATT_BWD, s, att_pass_bytes(d));
-#define ASR_PB2(CC, NQ, SA, SE, SD, SK, F)                                                         \
-  hipLaunchKernelGGL((attdec_bwd_persist<CC, NQ, SA, SE, SD, SK, F>), grid, dim3(PD_THREADS), lds,  \
+#define ASR_PB3(CC, NQ, SA, SE, SD, SK, F, FS)                                                     \
+  hipLaunchKernelGGL((attdec_bwd_persist<CC, NQ, SA, SE, SD, SK, F, FS>), grid, dim3(PD_THREADS),   \
+                     lds,                                                                        \
                      s, d, (const void*)wcatT, enc, enc_a, lens, w_dec, w_conv, conv_w, v, c_all, \
                      aw_all, wd_all, d_dec_in, d_ctx_in, gates_dg, dctx_tot, d_enc_a, d_h0,      \
                      dwd_all, dv_part, dwc_part, dcw_part, r, sbuf, dwd_chunk, dFbuf, ctr,       \
                      lstm_persist_status_word(), drop_h, seed_h, (const float*)g_pd_fsave)
+#define ASR_PB2(CC, NQ, SA, SE, SD, SK, F)                                       \
+  do {                                                                          \
+    if (g_pd_fsave) ASR_PB3(CC, NQ, SA, SE, SD, SK, F, true);                   \
+    else ASR_PB3(CC, NQ, SA, SE, SD, SK, F, false);                             \
+  } while (0)
 #define ASR_PB(CC, NQ, SA, SE, SD, SK)                  \
   do {                                                  \
     if (bf) ASR_PB2(CC, NQ, SA, SE, SD, SK, false);     \
@@ -3146,6 +3154,7 @@ extern "C" int asr_attdec_backward_ex(const asr_attdec_dims_t* dims, const asr_a
     else ASR_PB(0, 4, 0, 0, 0, 0);
 #undef ASR_PB
 #undef ASR_PB2
+#undef ASR_PB3
     ASR_LAUNCH_CHECK();
     prof_end_launch(ASR_PROF_ATT_BWD, pslot, s);
     g_att_last[2] = pd_ten(d) ? 10 : 0;
