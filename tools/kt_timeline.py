@@ -12,9 +12,10 @@ import sys
 
 
 def short(name):
-    n = name.split('(')[0]
+    n = name
     for pre in ('void ', 'asr::', '(anonymous namespace)::'):
         n = n.replace(pre, '')
+    n = n.split('(')[0]
     return n[:60]
 
 
