@@ -467,6 +467,14 @@ int asr_convert_rows_bf16(const float* src, asr_rowmap_t map, int nrows, int nco
  * bf16 operand whose leading dimension is padded to a multiple of 8). */
 int asr_convert_rows_bf16_ld(const float* src, asr_rowmap_t map, int nrows, int ncols, int ld,
                              uint16_t* dst, void* stream);
+/* Up to four asr_convert_rows_bf16 conversions in one launch (round 6: a
+ * staged linear layer's input, weight and zero pad rows).  Each needs ncols % 8
+ * == 0, 16-B aligned rows (src, dst, map strides); returns 1 when launched, 0
+ * when a job does not qualify (nothing launched: convert one by one), < 0 on
+ * a launch error.  The same bits as the one-by-one conversions. */
+int asr_convert_rows_bf16_multi(int n, const float* const* src, const asr_rowmap_t* maps,
+                                const int* nrows, const int* ncols, uint16_t* const* dst,
+                                void* stream);
 /* asr_convert_rows_bf16 of dropout(src): element at linear offset i of src is
  * kept iff u(seed, i) >= p and scaled by 1/(1-p) -- the mask asr_dropout(src,
  * ., n, p, seed) applies -- so a layer's dropped output is staged as the next

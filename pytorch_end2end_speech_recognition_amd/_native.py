@@ -249,6 +249,7 @@ class RowMap(ctypes.Structure):
 
 SIGNATURES['asr_convert_rows_bf16'] = (c_int, [c_vp, RowMap, c_int, c_int, c_vp, c_vp])
 SIGNATURES['asr_convert_rows_bf16_ld'] = (c_int, [c_vp, RowMap, c_int, c_int, c_int, c_vp, c_vp])
+SIGNATURES['asr_convert_rows_bf16_multi'] = (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp])
 SIGNATURES['asr_convert_rows_bf16_dropout'] = (c_int, [c_vp, RowMap, c_int, c_int, c_vp, c_float,
                                                         ctypes.c_ulonglong, c_vp])
 

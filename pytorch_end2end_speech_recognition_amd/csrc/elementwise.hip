@@ -384,6 +384,15 @@ extern "C" int asr_convert_rows_bf16_ld(const float* src, asr_rowmap_t map, int 
   return ASR_OK;
 }
 
+extern "C" int asr_convert_rows_bf16_multi(int n, const float* const* src,
+                                           const asr_rowmap_t* maps, const int* nrows,
+                                           const int* ncols, uint16_t* const* dst, void* stream) {
+  if (!src || !maps || !nrows || !ncols || !dst || n < 1 || n > 4) return 0;
+  for (int k = 0; k < n; ++k)
+    if (!src[k] || !dst[k]) return 0;
+  return convert_rows_bf16_multi(src, maps, nrows, ncols, dst, n, stream);
+}
+
 extern "C" int asr_convert_rows_bf16_dropout(const float* src, asr_rowmap_t map, int nrows,
                                              int ncols, uint16_t* dst, float p,
                                              unsigned long long seed, void* stream) {

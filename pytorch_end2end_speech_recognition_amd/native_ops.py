@@ -375,28 +375,58 @@ def _linear_forward(x, weight, bias, drop, lse=None, ld=None):
     # staged copies: x [M][Kp], weight [Np][Kp] (rows Nout.. and columns K.. zero)
     Kp, Np = ((K + 7) // 8 * 8, (Nout + 7) // 8 * 8) if stage else (K, Nout)
     if stage:
-        # fused_drop: K % 8 == 0, so Kp == K and the dropped copy is the operand
-        xo = (convert_rows_bf16(x, rowmap(K), M, K, drop=drop) if fused_drop else
-              _staged(x, M, K, Kp))
         # a dense weight (no padding) from the optimizer's bf16 shadow when current
         wo = _shadow_rows(weight, (weight,)) if (Np == Nout and Kp == K) else None
         if wo is not None:
             SHADOW_STATS['linear_hits'] += 1
-        else:
+        elif not fused_drop and K % 8 == 0 and os.environ.get('ASR_LINEAR_MULTI', '1') != '0':
+            # input, weight and zero pad rows staged in one launch (the same bits)
+            xo = torch.empty(M, Kp, dtype=torch.bfloat16, device=x.device)
+            wo = torch.empty(Np, Kp, dtype=torch.bfloat16, device=x.device)
+            jobs = [(x, rowmap(K), M, K, xo.data_ptr()), (weight, rowmap(K), Nout, K, wo.data_ptr())]
+            if Np > Nout:
+                jobs.append((weight, rowmap(0, t_limit=1, rows_per_b=Np - Nout, t_add=1),
+                             Np - Nout, Kp, wo.data_ptr() + Nout * Kp * 2))
+            if M > 0 and _convert_multi(jobs, x.device):
+                return _linear_gemm(xo, wo, y, ld, M, Nout, Kp, bias, lse, x.device) + (stage,)
+        # fused_drop: K % 8 == 0, so Kp == K and the dropped copy is the operand
+        xo = (convert_rows_bf16(x, rowmap(K), M, K, drop=drop) if fused_drop else
+              _staged(x, M, K, Kp))
+        if wo is None:
             wo = torch.empty(Np, Kp, dtype=torch.bfloat16, device=x.device)
             N.call('asr_convert_rows_bf16_ld', N.ptr(weight), rowmap(K), Nout, K, Kp, N.ptr(wo),
                    N.stream_handle(x.device))
-        if Np > Nout:
-            N.call('asr_convert_rows_bf16_ld', N.ptr(weight), rowmap(0, t_limit=1,
-                   rows_per_b=Np - Nout, t_add=1), Np - Nout, Kp, Kp,
-                   ctypes.c_void_p(wo.data_ptr() + Nout * Kp * 2), N.stream_handle(x.device))
+            if Np > Nout:
+                N.call('asr_convert_rows_bf16_ld', N.ptr(weight), rowmap(0, t_limit=1,
+                       rows_per_b=Np - Nout, t_add=1), Np - Nout, Kp, Kp,
+                       ctypes.c_void_p(wo.data_ptr() + Nout * Kp * 2), N.stream_handle(x.device))
     else:
         xo, wo = x, weight
+    return _linear_gemm(xo, wo, y, ld, M, Nout, Kp, bias, lse, x.device) + (stage,)
+
+
+def _linear_gemm(xo, wo, y, ld, M, Nout, Kp, bias, lse, dev):
     if M > 0:
         p = gemm_problem(operand(xo, 0, rowmap(Kp)), operand(wo, 0, rowmap(Kp)), y,
                          rowmap(ld), M, Nout, Kp, bias=bias)
-        run_gemm([p], x.device, lse=lse)
-    return y, xo, wo, stage
+        run_gemm([p], dev, lse=lse)
+    return y, xo, wo
+
+
+def _convert_multi(jobs, dev):
+    """jobs: (src tensor, RowMap, rows, cols, dst address) -- asr_convert_rows_bf16
+    of each in one launch; False when a job does not qualify (nothing launched)."""
+    n = len(jobs)
+    src = (ctypes.c_void_p * n)(*[j[0].data_ptr() for j in jobs])
+    maps = (N.RowMap * n)(*[j[1] for j in jobs])
+    rows = (ctypes.c_int * n)(*[int(j[2]) for j in jobs])
+    cols = (ctypes.c_int * n)(*[int(j[3]) for j in jobs])
+    dst = (ctypes.c_void_p * n)(*[j[4] for j in jobs])
+    rc = N.lib().asr_convert_rows_bf16_multi(n, src, maps, rows, cols, dst,
+                                              N.stream_handle(dev))
+    if rc < 0:
+        raise N.NativeError('asr_convert_rows_bf16_multi: launch failed')
+    return rc == 1
 
 
 def _linear_backward(xo, wo, bias, stage, xshape, weight, drop, dyo, need_dx, dy_bias=None,

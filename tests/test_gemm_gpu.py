@@ -133,6 +133,36 @@ def test_linear_bf16_staged_padded(cuda_dev):
         ops.set_compute_dtype('fp32')
 
 
+@pytest.mark.parametrize('M,K,Nout', [(2048, 640, 1001), (4160, 320, 320), (999, 960, 33)])
+def test_linear_staging_one_launch_bitwise(M, K, Nout, cuda_dev, monkeypatch):
+    """A staged bf16 linear layer converts its input, weight and zero pad rows
+    in one launch (asr_convert_rows_bf16_multi): y, dx, dW, db equal the
+    one-conversion-per-launch path (ASR_LINEAR_MULTI=0) bit for bit, padded
+    (Nout % 8 != 0) and dense output widths."""
+    ops = _ops()
+    ops.set_compute_dtype('bf16')
+    try:
+        rng = np.random.RandomState(M + K + Nout)
+        x = rng.randn(M, K).astype(np.float32)
+        w = (rng.randn(Nout, K) * 0.05).astype(np.float32)
+        b = rng.randn(Nout).astype(np.float32)
+        dy = rng.randn(M, Nout).astype(np.float32)
+        outs = {}
+        for multi in ('0', '1'):
+            monkeypatch.setenv('ASR_LINEAR_MULTI', multi)
+            xd = torch.from_numpy(x).to(cuda_dev).requires_grad_(True)
+            wd = torch.from_numpy(w).to(cuda_dev).requires_grad_(True)
+            bd = torch.from_numpy(b).to(cuda_dev).requires_grad_(True)
+            y = ops.linear(xd, wd, bd)
+            y.backward(torch.from_numpy(dy).to(cuda_dev))
+            torch.cuda.synchronize()
+            outs[multi] = [t.detach().cpu() for t in (y, xd.grad, wd.grad, bd.grad)]
+        for name, a1, a0 in zip(('y', 'dx', 'dW', 'db'), outs['1'], outs['0']):
+            assert torch.equal(a1, a0), name
+    finally:
+        ops.set_compute_dtype('fp32')
+
+
 @pytest.mark.parametrize('M,N,K', [(529, 389, 3000), (256, 256, 64), (300, 260, 200),
                                     (1024, 512, 8000)])
 def test_kmajor_256_tiles_exact(M, N, K, cuda_dev, monkeypatch):
